@@ -1,0 +1,171 @@
+"""Event-trace and capture formats shared by the reference harness (oracle/ref_harness.cpp),
+the CPU restatement (oracle/relay_model.cpp) and the GPU engine's replay driver.
+
+A *trace* is what a reflector sees: push sessions (one SDP each), then a time-ordered event
+list.  It mirrors the reference's entry points:
+
+* ``PKT``  -> ``ReflectorStream::PushPacket`` for an RTSP-interleaved push
+  (QTSSReflectorModule.cpp:604-678: track = channel/2, RTCP = channel & 1);
+* ``JOIN`` -> SETUP+PLAY of one subscriber on every track of a session
+  (QTSSReflectorModule.cpp:1610-1622, 1942-1946);
+* ``TICK`` -> ``ReflectorSender::ReflectPackets`` on every sender
+  (ReflectorStream.cpp:1709-1714).
+
+Every event carries the virtual clock value (ms) that ``OS::Milliseconds`` returns while it
+is applied.  The GPU engine's batch boundary is the TICK: all PKTs since the previous TICK
+form one ingest batch (a UDP read event is the same natural boundary in the reference,
+ReflectorStream.cpp:1676-1714).
+
+Binary layout (little endian)::
+
+    trace   := "EDTR" u32 version=1 u32 n_sessions { u32 sdp_len sdp_bytes }* event* u8 0
+    event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
+             | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
+             | u8 3 i64 t                                                    (TICK)
+    capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
+                             u64 n_packets u64 n_bytes bytes[n_bytes] }*
+
+``kind`` is 0 for the RTP sub-stream, 1 for RTCP.  The capture bytes are the sub-stream's
+*wire image*: UDP = ``BE16(len) + datagram`` per packet; TCP = the exact interleaved byte
+stream ``'$' ch BE16(len) + packet`` (RTSPSessionInterface.cpp:329-344).
+"""
+from __future__ import annotations
+
+import hashlib
+import struct
+from dataclasses import dataclass, field
+
+PKT, JOIN, TICK = 1, 2, 3
+UDP, TCP = 0, 1
+
+
+@dataclass
+class Trace:
+    sdps: list[str] = field(default_factory=list)
+    events: list[tuple] = field(default_factory=list)   # (type, t, ...) in file order
+
+    def add_session(self, sdp: str) -> int:
+        self.sdps.append(sdp)
+        return len(self.sdps) - 1
+
+    def pkt(self, t: int, session: int, channel: int, data: bytes):
+        self.events.append((PKT, int(t), session, channel, bytes(data)))
+
+    def join(self, t: int, session: int, sub_id: int, transport: int = UDP, ua_flags: int = 0):
+        self.events.append((JOIN, int(t), session, sub_id, transport, ua_flags))
+
+    def tick(self, t: int):
+        self.events.append((TICK, int(t)))
+
+    # -- serialisation ------------------------------------------------------------------
+    def to_bytes(self) -> bytes:
+        out = [b"EDTR", struct.pack("<II", 1, len(self.sdps))]
+        for s in self.sdps:
+            b = s.encode()
+            out.append(struct.pack("<I", len(b)))
+            out.append(b)
+        for ev in self.events:
+            if ev[0] == PKT:
+                _, t, s, ch, data = ev
+                out.append(struct.pack("<BqIBI", PKT, t, s, ch, len(data)))
+                out.append(data)
+            elif ev[0] == JOIN:
+                _, t, s, sub, tr, ua = ev
+                out.append(struct.pack("<BqIIBB", JOIN, t, s, sub, tr, ua))
+            else:
+                out.append(struct.pack("<Bq", TICK, ev[1]))
+        out.append(b"\x00")
+        return b"".join(out)
+
+    def write(self, path: str):
+        with open(path, "wb") as f:
+            f.write(self.to_bytes())
+
+    @staticmethod
+    def from_bytes(buf: bytes) -> "Trace":
+        assert buf[:4] == b"EDTR"
+        ver, n = struct.unpack_from("<II", buf, 4)
+        assert ver == 1
+        p = 12
+        tr = Trace()
+        for _ in range(n):
+            (ln,) = struct.unpack_from("<I", buf, p)
+            p += 4
+            tr.sdps.append(buf[p:p + ln].decode())
+            p += ln
+        while p < len(buf):
+            typ = buf[p]
+            if typ == 0:
+                break
+            if typ == PKT:
+                _, t, s, ch, ln = struct.unpack_from("<BqIBI", buf, p)
+                p += 18
+                tr.events.append((PKT, t, s, ch, bytes(buf[p:p + ln])))
+                p += ln
+            elif typ == JOIN:
+                _, t, s, sub, trn, ua = struct.unpack_from("<BqIIBB", buf, p)
+                p += 19
+                tr.events.append((JOIN, t, s, sub, trn, ua))
+            elif typ == TICK:
+                _, t = struct.unpack_from("<Bq", buf, p)
+                p += 9
+                tr.events.append((TICK, t))
+            else:
+                raise ValueError(f"bad event {typ} at {p}")
+        return tr
+
+
+@dataclass
+class SubStream:
+    sub: int
+    session: int
+    track: int
+    kind: int          # 0 RTP, 1 RTCP
+    tcp: int
+    n_packets: int
+    data: bytes
+
+    @property
+    def key(self):
+        return (self.sub, self.track, self.kind)
+
+    def digest(self) -> str:
+        return hashlib.sha256(self.data).hexdigest()
+
+
+def read_capture(path_or_bytes) -> dict:
+    buf = path_or_bytes
+    if isinstance(path_or_bytes, str):
+        with open(path_or_bytes, "rb") as f:
+            buf = f.read()
+    assert buf[:4] == b"EDCP", "bad capture magic"
+    (n,) = struct.unpack_from("<I", buf, 4)
+    p = 8
+    out = {}
+    for _ in range(n):
+        sub, sess, track, kind, tcp, npk, nb = struct.unpack_from("<IIHBBQQ", buf, p)
+        p += 28
+        data = bytes(buf[p:p + nb])
+        p += nb
+        ss = SubStream(sub, sess, track, kind, tcp, npk, data)
+        out[ss.key] = ss
+    return out
+
+
+def capture_summary(cap: dict) -> dict:
+    """Digest form used by the committed golden fixtures."""
+    return {f"{k[0]}/{k[1]}/{k[2]}": [v.n_packets, len(v.data), v.digest()]
+            for k, v in sorted(cap.items())}
+
+
+def split_wire_image(data: bytes, tcp: int) -> list[bytes]:
+    """Wire image -> list of packets (inverse of the framing described above)."""
+    out, p = [], 0
+    hdr = 4 if tcp else 2
+    while p < len(data):
+        if tcp:
+            assert data[p] == 0x24
+        ln = (data[p + hdr - 2] << 8) | data[p + hdr - 1]
+        out.append(data[p + hdr:p + hdr + ln])
+        p += hdr + ln
+    return out

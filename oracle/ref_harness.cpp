@@ -1,0 +1,348 @@
+// oracle/ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as
+// the product).  Drives the REAL EasyDarwin reflector hot path, compiled from the
+// read-only reference sources by oracle/_ref/Makefile, with a fake QTSS server:
+//
+//   * a callback table (QTSS_Private.h:52-127) whose dictionary calls are served by a
+//     tiny in-memory attribute store, whose QTSS_Write (index 10) captures the bytes
+//     per subscriber sub-stream, and whose Milliseconds is a virtual clock;
+//   * OS::Milliseconds is link-wrapped (-Wl,--wrap) onto the same virtual clock;
+//   * push sessions are built exactly as FindOrCreateSession does for an RTSP-TCP
+//     (interleaved, EasyPusher-default) push (QTSSReflectorModule.cpp:1379-1460):
+//     SDPSourceInfo -> ReflectorSession -> SetupReflectorSession(kMarkSetup|kIsPushSession,
+//     one SSRC per stream = true, 30 s);
+//   * subscribers are built as DoSetup/DoPlay do (QTSSReflectorModule.cpp:1610-1622,
+//     1766-1786, 1942-1946): RTPSessionOutput + ReflectorSession::AddOutput, one RTP
+//     stream object per track carrying the ReflectorStream cookie, then InitializeStreams
+//     and state = playing;
+//   * PKT events call ReflectorStream::PushPacket (as ProcessRTPData does,
+//     QTSSReflectorModule.cpp:604-678: track = channel/2, RTCP = channel&1);
+//   * TICK events call ReflectPackets on every sender (RTP then RTCP, track order), as
+//     ReflectorSocket::Run does (ReflectorStream.cpp:1709-1714).
+//
+// Usage: ref_harness <trace.edtr> <capture.edcp>
+// Trace / capture formats: see easydarwin_amd/trace.py (shared with the port oracle and
+// the GPU engine's replay driver).
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+#include <memory>
+#include <algorithm>
+
+#include "QTSS.h"
+#include "QTSS_Private.h"
+#include "OS.h"
+#include "OSQueue.h"
+#include "MyAssert.h"
+#include "SDPSourceInfo.h"
+#include "ReflectorSession.h"
+#include "ReflectorStream.h"
+#include "RTPSessionOutput.h"
+#include "QTSServerInterface.h"
+
+// ---------------------------------------------------------------------------------------
+// The two server-side module tables ReflectorSession::SetSessionName reads
+// (QTSServerInterface.h:356-357).  The harness *is* the server, with zero modules
+// registered in any role.
+QTSSModule** QTSServerInterface::sModuleArray[QTSSModule::kNumRoles];
+UInt32       QTSServerInterface::sNumModulesInRole[QTSSModule::kNumRoles];
+
+// ---------------------------------------------------------------------------------------
+// Virtual clock.
+static SInt64 g_now = 0;
+extern "C" SInt64 __wrap__ZN2OS12MillisecondsEv() { return g_now; }
+
+// ---------------------------------------------------------------------------------------
+// Attribute store.  Values have stable storage because RTPSessionOutput writes through
+// pointers returned by QTSS_GetValuePtr (RTPSessionOutput.cpp:647-651).
+struct Value { std::vector<char> buf; UInt32 len = 0; };
+struct FakeObj {
+    std::map<UInt32, std::vector<std::unique_ptr<Value>>> attrs;
+    // capture side (RTP stream objects only)
+    bool is_stream = false;
+    UInt32 sub_id = 0, session = 0, track = 0, transport = 0;
+    UInt32 rtp_channel = 0, rtcp_channel = 1;
+    std::string cap[2];          // [0] RTP writes, [1] RTCP writes (wire image)
+    UInt64 npk[2] = {0, 0};
+};
+static std::vector<std::unique_ptr<FakeObj>> g_objs;
+static FakeObj* new_obj() { g_objs.emplace_back(new FakeObj()); return g_objs.back().get(); }
+
+static void set_value(FakeObj* o, UInt32 id, UInt32 idx, const void* p, UInt32 len) {
+    auto& vec = o->attrs[id];
+    if (vec.size() <= idx) vec.resize(idx + 1);
+    if (!vec[idx]) vec[idx].reset(new Value());
+    Value& v = *vec[idx];
+    if (v.buf.size() < len) v.buf.resize(std::max<size_t>(len, 16));
+    if (len) memcpy(v.buf.data(), p, len);
+    v.len = len;
+}
+static Value* get_value(FakeObj* o, UInt32 id, UInt32 idx) {
+    auto it = o->attrs.find(id);
+    if (it == o->attrs.end() || idx >= it->second.size() || !it->second[idx]) return nullptr;
+    return it->second[idx].get();
+}
+
+static std::map<std::string, UInt32> g_attr_ids;
+static UInt32 g_cookie_attr = 0;
+
+// ---------------------------------------------------------------------------------------
+// Callbacks (all reached through QTSS_Private.cpp's varargs stubs).
+static QTSS_Error cb_fail(...) { return QTSS_RequestFailed; }
+static QTSS_Error cb_ok(...) { return QTSS_NoErr; }
+static QTSS_Error cb_milliseconds(SInt64* out, ...) { *out = g_now; return QTSS_NoErr; }
+static QTSS_Error cb_id_for_tag(UInt32 type, const char* tag, QTSS_AttributeID* out, ...) {
+    std::string key = std::to_string(type) + ":" + tag;
+    auto it = g_attr_ids.find(key);
+    if (it == g_attr_ids.end()) {
+        UInt32 id = 0x40000000u + (UInt32)g_attr_ids.size();
+        it = g_attr_ids.emplace(key, id).first;
+    }
+    *out = it->second;
+    return QTSS_NoErr;
+}
+// A real QTSSDictionary refuses qtssIllegalAttrID (QTSS.h:342) with QTSS_AttrDoesntExist;
+// QTSSModuleUtils::CreateAttribute relies on that when a pref is missing.
+static QTSS_Error cb_get_value_ptr(void* obj, UInt32 id, UInt32 idx, void** out, UInt32* len, ...) {
+    if (!obj) return QTSS_BadArgument;
+    if (id == (UInt32)qtssIllegalAttrID) return QTSS_AttrDoesntExist;
+    Value* v = get_value((FakeObj*)obj, id, idx);
+    if (!v) { if (len) *len = 0; return QTSS_ValueNotFound; }
+    *out = v->buf.data();
+    if (len) *len = v->len;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_get_value(void* obj, UInt32 id, UInt32 idx, void* buf, UInt32* len, ...) {
+    if (!obj) return QTSS_BadArgument;
+    if (id == (UInt32)qtssIllegalAttrID) return QTSS_AttrDoesntExist;
+    Value* v = get_value((FakeObj*)obj, id, idx);
+    if (!v) return QTSS_ValueNotFound;
+    if (*len < v->len) { *len = v->len; return QTSS_NotEnoughSpace; }
+    memcpy(buf, v->buf.data(), v->len);
+    *len = v->len;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf, UInt32 len, ...) {
+    if (!obj) return QTSS_BadArgument;
+    if (id == (UInt32)qtssIllegalAttrID) return QTSS_AttrDoesntExist;
+    set_value((FakeObj*)obj, id, idx, buf, len);
+    return QTSS_NoErr;
+}
+// QTSS_Write(stream, QTSS_PacketStruct*, len, outLen, flags): RTPStream::Write's framing
+// (RTPStream.cpp:1098-1145) -- UDP datagram, or '$' ch BE16(len) + packet on the RTP or
+// RTCP channel (RTSPSessionInterface.cpp:329-344).  Sinks never block (Q20).
+static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* outLen, UInt32 flags, ...) {
+    FakeObj* s = (FakeObj*)stream;
+    const QTSS_PacketStruct* pkt = (const QTSS_PacketStruct*)buf;
+    int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
+    if (len == 0) return QTSS_NoErr;
+    std::string& c = s->cap[k];
+    if (s->transport == qtssRTPTransportTypeTCP) {
+        c.push_back('$');
+        c.push_back((char)(k ? s->rtcp_channel : s->rtp_channel));
+    }
+    c.push_back((char)(len >> 8));
+    c.push_back((char)(len & 0xff));
+    c.append((const char*)pkt->packetData, len);
+    s->npk[k]++;
+    if (outLen) *outLen = len;
+    return QTSS_NoErr;
+}
+
+struct NoopAssert : public AssertLogger {
+    unsigned long count = 0;
+    void LogAssert(char* m) override { if (getenv("EDTR_SHOW_ASSERTS")) fprintf(stderr, "assert: %s\n", m); ++count; }
+};
+
+// ---------------------------------------------------------------------------------------
+// Trace reader (format: easydarwin_amd/trace.py).
+struct Reader {
+    std::vector<unsigned char> d; size_t p = 0;
+    template <class T> T get() { T v; memcpy(&v, &d[p], sizeof(T)); p += sizeof(T); return v; }
+    bool done() const { return p >= d.size(); }
+};
+
+struct Sub {
+    UInt32 id, session;
+    FakeObj* client;
+    std::vector<FakeObj*> streams;
+    RTPSessionOutput* output;
+};
+
+int main(int argc, char** argv) {
+    if (argc != 3) { fprintf(stderr, "usage: %s trace.edtr capture.edcp\n", argv[0]); return 2; }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) { perror(argv[1]); return 2; }
+    Reader r;
+    fseek(f, 0, SEEK_END); r.d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
+    if (fread(r.d.data(), 1, r.d.size(), f) != r.d.size()) { perror("read"); return 2; }
+    fclose(f);
+    if (memcmp(&r.d[0], "EDTR", 4) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
+    r.p = 4;
+    UInt32 version = r.get<UInt32>();
+    if (version != 1) { fprintf(stderr, "bad version\n"); return 2; }
+
+    static NoopAssert logger;
+    SetAssertLogger(&logger);
+
+    static QTSS_Callbacks cbs;
+    for (int i = 0; i < kLastCallback; i++) cbs.addr[i] = (QTSS_CallbackProcPtr)cb_fail;
+    cbs.addr[kMillisecondsCallback]        = (QTSS_CallbackProcPtr)cb_milliseconds;
+    cbs.addr[kAddStaticAttributeCallback]  = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kIDForTagCallback]            = (QTSS_CallbackProcPtr)cb_id_for_tag;
+    cbs.addr[kGetAttributePtrByIDCallback] = (QTSS_CallbackProcPtr)cb_get_value_ptr;
+    cbs.addr[kGetAttributeByIDCallback]    = (QTSS_CallbackProcPtr)cb_get_value;
+    cbs.addr[kSetAttributeByIDCallback]    = (QTSS_CallbackProcPtr)cb_set_value;
+    cbs.addr[kWriteCallback]               = (QTSS_CallbackProcPtr)cb_write;
+    cbs.addr[kRefreshTimeOutCallback]      = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kLockObjectCallback]          = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kUnlockObjectCallback]        = (QTSS_CallbackProcPtr)cb_ok;
+    QTSS_PrivateArgs args;
+    memset(&args, 0, sizeof(args));
+    args.inServerAPIVersion = QTSS_API_VERSION;
+    args.inCallbacks = &cbs;
+    extern QTSS_Error _stublibrary_main(void*, QTSS_DispatchFuncPtr);
+    _stublibrary_main(&args, NULL);
+
+    // Register role work the module does (QTSSReflectorModule.cpp:265-365 subset).
+    ReflectorStream::Register();
+    RTPSessionOutput::Register();
+    (void)QTSS_IDForAttr(qtssRTPStreamObjectType, "qtssReflectorModuleStreamCookie", &g_cookie_attr);
+    FakeObj* prefs = new_obj();
+    ReflectorStream::Initialize((QTSS_ModulePrefsObject)prefs);   // every pref -> its default
+    if (ReflectorStream::sOverBufferInMsec != 1000) {      // pinned prefs: SURVEY.md §5 defaults
+        fprintf(stderr, "unexpected reflector prefs (overbuffer %u ms)\n", (unsigned)ReflectorStream::sOverBufferInMsec);
+        return 3;
+    }
+
+    // Sessions.
+    UInt32 nsess = r.get<UInt32>();
+    std::vector<ReflectorSession*> sessions(nsess, nullptr);
+    for (UInt32 s = 0; s < nsess; s++) {
+        UInt32 sdplen = r.get<UInt32>();
+        std::string sdp((const char*)&r.d[r.p], sdplen);
+        r.p += sdplen;
+        char* sdpbuf = new char[sdplen + 1];
+        memcpy(sdpbuf, sdp.data(), sdplen); sdpbuf[sdplen] = 0;
+        SDPSourceInfo* info = new SDPSourceInfo(sdpbuf, sdplen);
+        char name[64];
+        snprintf(name, sizeof(name), "live/stream%u.sdp", s);
+        StrPtrLen nm(name);
+        ReflectorSession* sess = new ReflectorSession(&nm, 1, NULL);
+        sess->SetHasBufferedStreams(true);
+        FakeObj* req = new_obj();
+        UInt32 tcp = qtssRTPTransportTypeTCP;
+        set_value(req, qtssRTSPReqTransportType, 0, &tcp, sizeof(tcp));
+        FakeObj* bcast = new_obj();
+        QTSS_StandardRTSP_Params params;
+        memset(&params, 0, sizeof(params));
+        params.inRTSPRequest = (QTSS_RTSPRequestObject)req;
+        params.inClientSession = (QTSS_ClientSessionObject)bcast;
+        QTSS_Error err = sess->SetupReflectorSession(info, &params,
+            ReflectorSession::kMarkSetup | ReflectorSession::kIsPushSession, true, 30);
+        if (err != QTSS_NoErr) { fprintf(stderr, "setup failed %d\n", (int)err); return 3; }
+        sessions[s] = sess;
+    }
+
+    std::vector<Sub> subs;
+    std::vector<char> pktbuf(70000);
+    while (!r.done()) {
+        UInt8 type = r.get<UInt8>();
+        if (type == 0) break;
+        SInt64 t = r.get<SInt64>();
+        if (t > g_now) g_now = t;
+        if (type == 1) {            // PKT
+            UInt32 s = r.get<UInt32>();
+            UInt8 ch = r.get<UInt8>();
+            UInt32 len = r.get<UInt32>();
+            memcpy(pktbuf.data(), &r.d[r.p], len);
+            r.p += len;
+            ReflectorSession* sess = sessions[s];
+            UInt32 idx = ch / 2;
+            if (idx < sess->GetNumStreams())
+                sess->GetStreamByIndex(idx)->PushPacket(pktbuf.data(), len, (ch & 1) != 0);
+        } else if (type == 2) {     // JOIN
+            UInt32 s = r.get<UInt32>();
+            UInt32 sub_id = r.get<UInt32>();
+            UInt8 transport = r.get<UInt8>();
+            UInt8 uaflags = r.get<UInt8>();
+            (void)uaflags;
+            ReflectorSession* sess = sessions[s];
+            Sub sb;
+            sb.id = sub_id; sb.session = s;
+            sb.client = new_obj();
+            UInt32 nstreams = sess->GetNumStreams();
+            for (UInt32 x = 0; x < nstreams; x++) {
+                FakeObj* st = new_obj();
+                st->is_stream = true;
+                st->sub_id = sub_id; st->session = s; st->track = x;
+                st->transport = transport ? qtssRTPTransportTypeTCP : qtssRTPTransportTypeUDP;
+                st->rtp_channel = 2 * x; st->rtcp_channel = 2 * x + 1;   // RTPStream.cpp:472-473
+                void* cookie = sess->GetStreamByIndex(x)->GetStreamCookie();
+                set_value(st, g_cookie_attr, 0, &cookie, sizeof(cookie));
+                set_value(st, qtssRTPStrTransportType, 0, &st->transport, sizeof(UInt32));
+                UInt16 firstSeq = 0;
+                set_value(st, qtssRTPStrFirstSeqNumber, 0, &firstSeq, sizeof(firstSeq));
+                QTSS_RTPStreamObject so = (QTSS_RTPStreamObject)st;
+                set_value(sb.client, qtssCliSesStreamObjects, x, &so, sizeof(so));
+                sb.streams.push_back(st);
+            }
+            sb.output = new RTPSessionOutput((QTSS_ClientSessionObject)sb.client, sess, NULL, g_cookie_attr);
+            sess->AddOutput(sb.output, true);
+            sb.output->InitializeStreams();
+            QTSS_RTPSessionState playing = qtssPlayingState;
+            set_value(sb.client, qtssCliSesState, 0, &playing, sizeof(playing));
+            subs.push_back(sb);
+        } else if (type == 3) {     // TICK
+            for (UInt32 s = 0; s < nsess; s++) {
+                ReflectorSession* sess = sessions[s];
+                for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+                    ReflectorStream* st = sess->GetStreamByIndex(x);
+                    OSQueue* freeA = NULL;
+                    // The socket's free queue is private; ReflectPackets only EnQueues
+                    // freed packets onto it, so a harness-owned queue is equivalent.
+                    static OSQueue sFree;
+                    freeA = &sFree;
+                    SInt64 wake = 0;
+                    st->GetRTPSender()->ReflectPackets(&wake, freeA);
+                    wake = 0;
+                    st->GetRTCPSender()->ReflectPackets(&wake, freeA);
+                }
+            }
+        } else {
+            fprintf(stderr, "bad event type %u at %zu\n", type, r.p);
+            return 3;
+        }
+    }
+
+    // Capture: one record per (subscriber, track, kind), sorted by (sub, track, kind).
+    FILE* o = fopen(argv[2], "wb");
+    if (!o) { perror(argv[2]); return 2; }
+    fwrite("EDCP", 1, 4, o);
+    UInt32 nrec = 0;
+    for (auto& sb : subs) nrec += (UInt32)sb.streams.size() * 2;
+    fwrite(&nrec, 4, 1, o);
+    std::sort(subs.begin(), subs.end(), [](const Sub& a, const Sub& b) { return a.id < b.id; });
+    for (auto& sb : subs) {
+        for (FakeObj* st : sb.streams) {
+            for (int k = 0; k < 2; k++) {
+                UInt32 u32; UInt16 u16; UInt8 u8; UInt64 u64;
+                u32 = st->sub_id; fwrite(&u32, 4, 1, o);
+                u32 = st->session; fwrite(&u32, 4, 1, o);
+                u16 = (UInt16)st->track; fwrite(&u16, 2, 1, o);
+                u8 = (UInt8)k; fwrite(&u8, 1, 1, o);
+                u8 = (UInt8)(st->transport == qtssRTPTransportTypeTCP); fwrite(&u8, 1, 1, o);
+                u64 = st->npk[k]; fwrite(&u64, 8, 1, o);
+                u64 = st->cap[k].size(); fwrite(&u64, 8, 1, o);
+                fwrite(st->cap[k].data(), 1, st->cap[k].size(), o);
+            }
+        }
+    }
+    fclose(o);
+    fprintf(stderr, "ref_harness: %zu subs, %lu asserts logged\n", subs.size(), logger.count);
+    return 0;
+}

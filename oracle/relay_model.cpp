@@ -1,0 +1,482 @@
+// oracle/relay_model.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Clean-room CPU restatement of EasyDarwin's reflector hot path (QTSSReflectorModule),
+// written from a reading of the reference, not copied from it.  Used (a) as the checker the
+// GPU engine is compared against, bit for bit, in tests/ and smoke(); (b) as bench.py's
+// `cpu_baseline` leg (kind "port").  It is pinned against the reference itself: every
+// golden trace in tests/golden/ is replayed through oracle/_ref/ref_harness (the real
+// reference sources) and through this model, and the captures must be identical.
+//
+// Semantics restated (file:line into /root/reference/EasyDarwin/APIModules/QTSSReflectorModule
+// unless noted; Q-tags are SURVEY.md §8.a's parity quirks):
+//   ingest    ReflectorStream::PushPacket          ReflectorStream.cpp:529-576
+//             ReflectorSocket::ProcessPacket       ReflectorStream.cpp:1769-2010
+//             ReflectorSocket::FilterInvalidSSRCs  ReflectorStream.cpp:1732-1767 (Q13)
+//             ReflectorPacket::SetPacketData clamp ReflectorStream.h:104-114 (Q11)
+//             RTCPPacket::ParsePacket + SR gate    RTCPUtilitiesLib/RTCPPacket.cpp:40-63 (Q14)
+//   keyframe  ReflectorSender::IsKeyFrameFirstPacket ReflectorStream.cpp:1403-1513 (Q4)
+//             index update / audio anchor           ReflectorStream.cpp:1876-1934 (Q3,Q5,Q6)
+//   fan-out   ReflectorSender::ReflectPackets       ReflectorStream.cpp:1024-1136 (Q7)
+//             SendPacketsToOutput                   ReflectorStream.cpp:1138-1198
+//             GetClientBufferStartPacketOffset      ReflectorStream.cpp:1201-1231
+//             RemoveOldPackets                      ReflectorStream.cpp:1233-1289 (Q16)
+//             NeedRelocateBookMark                  ReflectorStream.cpp:1293-1353 (Q9)
+//             ReflectorOutput bookmarks             ReflectorOutput.h:137-194 (Q8)
+//             RTPSessionOutput::WritePacket         RTPSessionOutput.cpp:564-662 (Q1,Q10)
+//   egress    RTPStream::Write / InterleavedWrite   Server.tproj/RTPStream.cpp:1084-1147,
+//                                                   RTSPSessionInterface.cpp:270-344 (Q2)
+//   SDP       SDPSourceInfo::Parse m= / a=rtpmap    APICommonCode/SDPSourceInfo.cpp:259-353
+//
+// Out of parity scope (documented in DESIGN.md): bytes read past the packet length by the
+// key detector when 12+4*CC >= len (the reference reads stale buffer memory there; this model
+// reads 0), Q17 (recycled bookmarks after >10 s lag), Q20 (TCP audio thinning), blocking sinks.
+//
+// Usage:  relay_model <trace.edtr> <capture.edcp>
+//         relay_model --bench <trace.edtr> <threads>   (memcpy sinks, prints JSON)
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <list>
+#include <map>
+#include <memory>
+#include <algorithm>
+#include <chrono>
+#include <thread>
+#include <atomic>
+#include <array>
+
+namespace relay {
+
+enum { kMaxPacket = 2060 };                      // ReflectorStream.h:126
+enum PayloadType { kUnknown = 0, kVideo = 1, kAudio = 2 };
+
+struct Prefs {                                   // ReflectorStream::Initialize defaults
+    int64_t over_buffer_ms = 1000;               // reflector_buffer_size_sec = 1
+    int64_t max_packet_age_ms = 10000;           // 10 x over buffer
+    int64_t relocate_age_ms = 2000;              // rtp_reflector_threshold_msec
+    uint32_t ssrc_timeout_s = 30;                // timeout_stream_SSRC_secs
+    bool filter_ssrcs = true;                    // use_one_SSRC_per_stream
+};
+
+struct TrackInfo { PayloadType type = kUnknown; std::string name; };
+
+// SDP: m=<media> ... opens a track; the first "a=rtpmap:<pt> <name>" of a track names it
+// (everything after the first space up to end of line).  a= lines before any m= are ignored.
+static std::vector<TrackInfo> parse_sdp(const std::string& sdp) {
+    std::vector<TrackInfo> tracks;
+    size_t p = 0;
+    while (p < sdp.size()) {
+        size_t e = sdp.find_first_of("\r\n", p);
+        if (e == std::string::npos) e = sdp.size();
+        std::string line = sdp.substr(p, e - p);
+        p = e;
+        while (p < sdp.size() && (sdp[p] == '\r' || sdp[p] == '\n')) p++;
+        if (line.size() < 2 || line[1] != '=') continue;
+        if (line[0] == 'm') {
+            TrackInfo t;
+            size_t sp = line.find(' ', 2);
+            std::string media = line.substr(2, sp == std::string::npos ? std::string::npos : sp - 2);
+            t.type = media == "video" ? kVideo : media == "audio" ? kAudio : kUnknown;
+            tracks.push_back(t);
+        } else if (line[0] == 'a' && !tracks.empty()) {
+            if (line.compare(2, 7, "rtpmap:") == 0 && tracks.back().name.empty()) {
+                size_t sp = line.find(' ', 2);
+                if (sp != std::string::npos) tracks.back().name = line.substr(sp + 1);
+            }
+        }
+    }
+    return tracks;
+}
+
+static inline uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+static inline uint16_t be16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
+
+// H.264 "first packet of a key frame" (Q4).  Bytes at or past `len` read as 0 here.
+static bool key_frame_first_packet(const uint8_t* p, uint32_t len) {
+    if (len < 20) return false;
+    auto at = [&](uint32_t i) -> uint8_t { return i < len ? p[i] : 0; };
+    uint32_t h = 12 + 4u * (p[0] & 0x0F);
+    uint8_t t = at(h) & 0x1F;
+    switch (t) {
+        case 24: if (len > h + 3) t = at(h + 3) & 0x1F; break;   // STAP-A
+        case 25: if (len > h + 5) t = at(h + 5) & 0x1F; break;   // STAP-B
+        case 26: if (len > h + 8) t = at(h + 8) & 0x1F; break;   // MTAP16
+        case 27: if (len > h + 9) t = at(h + 9) & 0x1F; break;   // MTAP24
+        case 28: case 29:                                         // FU-A / FU-B: start bit only
+            if (len > h + 1 && (at(h + 1) & 0x80)) t = at(h + 1) & 0x1F;
+            break;
+        default: break;
+    }
+    return t == 5 || t == 7 || t == 8;
+}
+
+struct Packet {
+    std::vector<uint8_t> data;      // clamped bytes
+    uint32_t len = 0;               // 0 after the SSRC filter rejects it
+    uint64_t id = 0;                // per-stream arrival counter shared by RTP+RTCP
+    int64_t arrival = 0;
+    bool needed = false;            // pinned (bookmark, key pointer)
+};
+using PacketRef = std::list<Packet>::iterator;
+
+struct Sender {
+    bool rtcp_flag = false;         // written with IsRTCP (the stream's second sender)
+    bool rtcp_port = false;         // RTCP by local-port parity (UDP push); false for TCP push (Q12)
+    std::list<Packet> q;            // oldest -> newest, with holes after RemoveOldPackets
+    bool has_key = false;
+    PacketRef key;
+    // per-socket SSRC filter state
+    uint32_t valid_ssrc = 0;
+    int64_t last_valid_s = 0;
+};
+
+struct Stream {
+    TrackInfo info;
+    uint64_t packet_count = 0;
+    Sender snd[2];                  // [0] RTP (socket A), [1] RTCP (socket B)
+};
+
+struct SubStreamState {             // one client RTP stream object (per track)
+    bool has_last[2] = {false, false};
+    uint64_t last_id[2] = {0, 0};   // qtssReflectorStreamLastRTPPacketID / ...RTCPPacketID
+    uint32_t packet_count = 0;      // qtssReflectorStreamPacketCount
+    uint16_t first_seq = 0;         // qtssRTPStrFirstSeqNumber (0 unless RTP-Info)
+    std::string cap[2];             // wire images
+    uint64_t npk[2] = {0, 0};
+};
+
+struct Output {
+    uint32_t sub_id = 0;
+    bool tcp = false;
+    // one bookmark per sender (stream x, kind)
+    std::vector<std::array<bool, 2>> has_bm;
+    std::vector<std::array<PacketRef, 2>> bm;
+    std::vector<SubStreamState> ss;   // per track
+    bool capture = true;              // false: bench sink (count bytes only)
+    std::vector<uint8_t>* sink = nullptr;
+    uint64_t sink_bytes = 0, sink_pkts = 0;
+};
+
+struct Session {
+    std::vector<Stream> streams;
+    bool video_key_flag = false;      // ReflectorSession::fHasVideoKeyFrameUpdate
+    std::vector<std::unique_ptr<Output>> outputs;   // bucket order == join order here
+    bool udp_push = false;
+};
+
+struct Model {
+    Prefs prefs;
+    std::vector<std::unique_ptr<Session>> sessions;
+    int64_t now = 0;
+
+    int add_session(const std::string& sdp, bool udp_push = false) {
+        auto s = std::make_unique<Session>();
+        s->udp_push = udp_push;
+        for (auto& ti : parse_sdp(sdp)) {
+            Stream st;
+            st.info = ti;
+            st.snd[0].rtcp_flag = false;
+            st.snd[1].rtcp_flag = true;
+            st.snd[1].rtcp_port = udp_push;     // socket B is the odd port only when bound (UDP push)
+            s->streams.push_back(std::move(st));
+        }
+        sessions.push_back(std::move(s));
+        return (int)sessions.size() - 1;
+    }
+
+    // ---- ingest -------------------------------------------------------------------------
+    static uint32_t get_ssrc(const Packet& p, bool rtcp) {
+        if (p.len < 8) return 0;
+        if (rtcp) return be32(&p.data[4]);
+        if (p.len < 12) return 0;
+        return be32(&p.data[8]);
+    }
+
+    void filter_ssrc(Sender& s, Packet& p) {
+        if (p.len == 0) return;
+        int64_t now_s = now / 1000;
+        if (s.valid_ssrc == 0) { s.valid_ssrc = get_ssrc(p, s.rtcp_port); s.last_valid_s = now_s; return; }
+        uint32_t ssrc = get_ssrc(p, s.rtcp_port);
+        if (ssrc != 0) {
+            if (ssrc == s.valid_ssrc) { s.last_valid_s = now_s; return; }
+            p.len = 0;
+        }
+        if (s.last_valid_s + (int64_t)prefs.ssrc_timeout_s < now_s) s.valid_ssrc = 0;
+    }
+
+    static bool is_rtcp_sr(const Packet& p) {
+        if (p.len < 8) return false;
+        uint32_t words = be16(&p.data[2]);
+        if (p.len < words * 4 + 4) return false;
+        if ((p.data[0] >> 6) != 2) return false;
+        return p.data[1] == 200;
+    }
+
+    void push(int session, int track, bool rtcp_socket, const uint8_t* data, uint32_t len) {
+        Session& se = *sessions[session];
+        if (track < 0 || track >= (int)se.streams.size() || len == 0) return;
+        Stream& st = se.streams[track];
+        Sender& snd = st.snd[rtcp_socket ? 1 : 0];
+        Packet p;
+        uint32_t n = std::min<uint32_t>(len, kMaxPacket);
+        p.data.assign(data, data + n);
+        p.len = n;
+        if (snd.rtcp_port && !is_rtcp_sr(p)) return;          // UDP RTCP: SR-first only (Q14)
+        if (prefs.filter_ssrcs) filter_ssrc(snd, p);
+        p.id = ++st.packet_count;
+        p.arrival = now;
+        snd.q.push_back(std::move(p));
+        PacketRef it = std::prev(snd.q.end());
+        const bool rtp_by_port = !snd.rtcp_port;
+        if (rtp_by_port && st.info.type == kVideo && st.info.name == "H264/90000" &&
+            key_frame_first_packet(it->data.data(), it->len)) {
+            if (snd.has_key) snd.key->needed = false;
+            it->needed = true;
+            snd.key = it; snd.has_key = true;
+            se.video_key_flag = true;
+        }
+        if (rtp_by_port && st.info.type == kAudio && se.video_key_flag) {
+            if (snd.has_key) snd.key->needed = false;
+            it->needed = true;
+            snd.key = it; snd.has_key = true;
+            se.video_key_flag = false;
+        }
+    }
+
+    // ---- join ---------------------------------------------------------------------------
+    void join(int session, uint32_t sub_id, bool tcp, std::vector<uint8_t>* sink = nullptr) {
+        Session& se = *sessions[session];
+        auto o = std::make_unique<Output>();
+        o->sub_id = sub_id;
+        o->tcp = tcp;
+        o->has_bm.assign(se.streams.size(), {false, false});
+        o->bm.resize(se.streams.size());
+        o->ss.resize(se.streams.size());
+        if (sink) { o->capture = false; o->sink = sink; }
+        se.outputs.push_back(std::move(o));
+    }
+
+    // ---- fan-out ------------------------------------------------------------------------
+    void write_packet(Output& o, int track, int kind, const Packet& p) {
+        if (p.len == 0) return;                                   // SSRC-rejected survivor
+        SubStreamState& s = o.ss[track];
+        if (kind == 0 && s.packet_count == 0) {                   // FilterPacket (Q10)
+            uint16_t seq = p.len >= 4 ? be16(&p.data[2]) : 0;
+            if (seq < s.first_seq) return;
+        }
+        if (s.has_last[kind] && p.id <= s.last_id[kind]) return;  // PacketAlreadySent (Q8)
+        if (o.capture) {
+            std::string& c = s.cap[kind];
+            if (o.tcp) { c.push_back('$'); c.push_back((char)(2 * track + kind)); }
+            c.push_back((char)(p.len >> 8));
+            c.push_back((char)(p.len & 0xFF));
+            c.append((const char*)p.data.data(), p.len);
+        } else {
+            uint8_t hdr[4] = {'$', (uint8_t)(2 * track + kind), (uint8_t)(p.len >> 8), (uint8_t)p.len};
+            size_t h = o.tcp ? 4 : 0;
+            size_t off = o.sink->size();
+            o.sink->resize(off + h + p.len);
+            if (h) memcpy(o.sink->data() + off, hdr, 4);
+            memcpy(o.sink->data() + off + h, p.data.data(), p.len);
+            o.sink_bytes += h + p.len;
+            o.sink_pkts++;
+        }
+        s.npk[kind]++;
+        s.has_last[kind] = true;
+        s.last_id[kind] = p.id;
+        s.packet_count++;
+    }
+
+    PacketRef buffer_start(Sender& snd, bool& found) {
+        for (auto it = snd.q.begin(); it != snd.q.end(); ++it)
+            if (now - it->arrival <= prefs.over_buffer_ms) { found = true; return it; }
+        found = false;
+        return snd.q.end();
+    }
+
+    void reflect(Session& se, int track, int kind) {
+        Sender& snd = se.streams[track].snd[kind];
+        bool have_new_start = false;
+        PacketRef new_start;
+        if (snd.has_key) { new_start = snd.key; have_new_start = true; }
+        else new_start = buffer_start(snd, have_new_start);
+        for (auto& op : se.outputs) {
+            Output& o = *op;
+            bool have = false;
+            PacketRef start;
+            if (o.has_bm[track][kind]) {
+                o.has_bm[track][kind] = false;               // GetBookMarkedPacket frees the slot
+                // The bookmark is live as long as the packet was never freed; packets only
+                // leave through RemoveOldPackets, which never frees a pinned bookmark here.
+                start = o.bm[track][kind]; have = true;
+            }
+            if (!have) { start = new_start; have = have_new_start; }
+            if (!have) continue;                             // NULL start sends nothing (Q7)
+            PacketRef last = start;
+            for (PacketRef it = start; it != snd.q.end(); ++it) {
+                last = it;
+                write_packet(o, track, kind, *it);
+            }
+            // NeedRelocateBookMark (Q9): only fires for a lagging bookmark.
+            if (now - last->arrival > prefs.relocate_age_ms && snd.has_key &&
+                snd.key->arrival > last->arrival) {
+                last = snd.key;
+                se.video_key_flag = true;
+            }
+            last->needed = true;
+            o.bm[track][kind] = last;
+            o.has_bm[track][kind] = true;
+        }
+        remove_old(snd);
+    }
+
+    void remove_old(Sender& snd) {
+        for (auto it = snd.q.begin(); it != snd.q.end();) {
+            int64_t age = now - it->arrival;
+            if (!it->needed && age > prefs.max_packet_age_ms) {
+                it = snd.q.erase(it);
+                continue;
+            }
+            if (snd.has_key && it == snd.key) break;
+            it->needed = false;
+            if (age <= prefs.max_packet_age_ms) break;
+            ++it;
+        }
+    }
+
+    void tick() {
+        for (auto& se : sessions)
+            for (auto& o : se->outputs)
+                if (!o->capture) o->sink->clear();      // bench: sinks are recycled per tick
+        for (auto& se : sessions)
+            for (int x = 0; x < (int)se->streams.size(); x++) {
+                reflect(*se, x, 0);
+                reflect(*se, x, 1);
+            }
+    }
+};
+
+}  // namespace relay
+
+// -------------------------------------------------------------------------------------------
+struct Reader {
+    std::vector<uint8_t> d; size_t p = 0;
+    template <class T> T get() { T v; memcpy(&v, &d[p], sizeof(T)); p += sizeof(T); return v; }
+};
+
+static bool load(const char* path, Reader& r) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { perror(path); return false; }
+    fseek(f, 0, SEEK_END); r.d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
+    bool ok = fread(r.d.data(), 1, r.d.size(), f) == r.d.size();
+    fclose(f);
+    if (!ok || r.d.size() < 12 || memcmp(r.d.data(), "EDTR", 4) != 0) { fprintf(stderr, "bad trace\n"); return false; }
+    r.p = 4;
+    return r.get<uint32_t>() == 1;
+}
+
+// Replays a trace into `m`.  `sink_for` (bench mode) routes output bytes to memcpy sinks.
+template <class OnJoin>
+static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 0, uint32_t nshards = 1) {
+    uint32_t nsess = r.get<uint32_t>();
+    for (uint32_t s = 0; s < nsess; s++) {
+        uint32_t n = r.get<uint32_t>();
+        m.add_session(std::string((const char*)&r.d[r.p], n));
+        r.p += n;
+    }
+    while (r.p < r.d.size()) {
+        uint8_t type = r.get<uint8_t>();
+        if (type == 0) break;
+        int64_t t = r.get<int64_t>();
+        if (t > m.now) m.now = t;
+        if (type == 1) {
+            uint32_t s = r.get<uint32_t>();
+            uint8_t ch = r.get<uint8_t>();
+            uint32_t len = r.get<uint32_t>();
+            if (s % nshards == shard) m.push(s, ch / 2, ch & 1, &r.d[r.p], len);
+            r.p += len;
+        } else if (type == 2) {
+            uint32_t s = r.get<uint32_t>();
+            uint32_t sub = r.get<uint32_t>();
+            uint8_t tr = r.get<uint8_t>();
+            (void)r.get<uint8_t>();
+            if (s % nshards == shard) on_join(s, sub, tr != 0);
+        } else if (type == 3) {
+            m.tick();
+        } else {
+            fprintf(stderr, "bad event %u\n", type);
+            exit(3);
+        }
+    }
+}
+
+static int run_capture(const char* in, const char* out) {
+    Reader r;
+    if (!load(in, r)) return 2;
+    relay::Model m;
+    replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp) { m.join(s, sub, tcp); });
+    struct Rec { uint32_t sub, sess; uint16_t track; relay::Output* o; };
+    std::vector<Rec> recs;
+    for (uint32_t s = 0; s < m.sessions.size(); s++)
+        for (auto& o : m.sessions[s]->outputs)
+            for (uint16_t x = 0; x < m.sessions[s]->streams.size(); x++) recs.push_back({o->sub_id, s, x, o.get()});
+    std::stable_sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) {
+        return a.sub != b.sub ? a.sub < b.sub : a.track < b.track; });
+    FILE* f = fopen(out, "wb");
+    if (!f) { perror(out); return 2; }
+    fwrite("EDCP", 1, 4, f);
+    uint32_t n = (uint32_t)recs.size() * 2;
+    fwrite(&n, 4, 1, f);
+    for (auto& rc : recs)
+        for (int k = 0; k < 2; k++) {
+            auto& ss = rc.o->ss[rc.track];
+            uint8_t kind = (uint8_t)k, tcp = rc.o->tcp;
+            uint64_t npk = ss.npk[k], nb = ss.cap[k].size();
+            fwrite(&rc.sub, 4, 1, f); fwrite(&rc.sess, 4, 1, f); fwrite(&rc.track, 2, 1, f);
+            fwrite(&kind, 1, 1, f); fwrite(&tcp, 1, 1, f); fwrite(&npk, 8, 1, f); fwrite(&nb, 8, 1, f);
+            fwrite(ss.cap[k].data(), 1, nb, f);
+        }
+    fclose(f);
+    return 0;
+}
+
+// Bench: sessions sharded over threads (session % T), each thread replays the whole trace
+// but only applies its own sessions; sinks are memcpy into per-subscriber buffers that are
+// recycled every tick.  Reports relayed packets/s of the replay (ingest + fan-out).
+static int run_bench(const char* in, int threads) {
+    Reader r0;
+    if (!load(in, r0)) return 2;
+    std::atomic<uint64_t> pkts{0}, bytes{0};
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++)
+        th.emplace_back([&, t]() {
+            Reader r = r0;   // private copy of the cursor (shares nothing mutable)
+            relay::Model m;
+            std::vector<std::unique_ptr<std::vector<uint8_t>>> sinks;
+            replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp) {
+                sinks.emplace_back(new std::vector<uint8_t>());
+                sinks.back()->reserve(1 << 20);
+                m.join(s, sub, tcp, sinks.back().get());
+            }, (uint32_t)t, (uint32_t)threads);
+            uint64_t p = 0, b = 0;
+            for (auto& se : m.sessions) for (auto& o : se->outputs) { p += o->sink_pkts; b += o->sink_bytes; }
+            pkts += p; bytes += b;
+        });
+    for (auto& x : th) x.join();
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"threads\": %d, "
+           "\"packets_per_s\": %.1f}\n", (unsigned long long)pkts.load(), (unsigned long long)bytes.load(),
+           s, threads, pkts.load() / s);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc == 4 && std::string(argv[1]) == "--bench") return run_bench(argv[2], atoi(argv[3]));
+    if (argc != 3) { fprintf(stderr, "usage: %s trace capture | --bench trace threads\n", argv[0]); return 2; }
+    return run_capture(argv[1], argv[2]);
+}

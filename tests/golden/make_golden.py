@@ -1,0 +1,77 @@
+"""Regenerates the golden parity fixtures in tests/golden/ from the REAL reference.
+
+For every scenario in tests/scenarios.py:
+  1. write the trace;
+  2. replay it through oracle/_ref/ref_harness (EasyDarwin's reflector compiled from the
+     read-only reference sources, oracle/_ref/Makefile) -> capture;
+  3. replay it through oracle/relay_model (the clean-room restatement) -> capture, and
+     require byte equality with (2);
+  4. commit <name>.json = {trace sha256, per sub-stream [packets, bytes, sha256]} and, for the
+     small scenarios, the trace and the reference capture themselves (<name>.edtr/.edcp).
+
+Run here (needs /root/reference):  python tests/golden/make_golden.py
+The fixtures are data only (inputs + expected outputs); nothing here is reference source.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from easydarwin_amd.trace import capture_summary, read_capture  # noqa: E402
+from scenarios import SCENARIOS  # noqa: E402
+
+FULL = {"tiny", "nal", "clamp", "ssrc"}          # small enough to commit byte for byte
+
+
+def main():
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    port = os.path.join(ROOT, "oracle", "relay_model")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    index = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, fn in SCENARIOS.items():
+            trace = fn().to_bytes()
+            tpath = os.path.join(td, name + ".edtr")
+            with open(tpath, "wb") as f:
+                f.write(trace)
+            rc, pc = tpath + ".ref", tpath + ".port"
+            subprocess.run([ref, tpath, rc], check=True, stderr=subprocess.DEVNULL)
+            subprocess.run([port, tpath, pc], check=True)
+            rb, pb = open(rc, "rb").read(), open(pc, "rb").read()
+            if rb != pb:
+                raise SystemExit(f"{name}: port oracle disagrees with the reference")
+            cap = read_capture(rb)
+            fix = {
+                "scenario": name,
+                "trace_sha256": hashlib.sha256(trace).hexdigest(),
+                "trace_bytes": len(trace),
+                "capture_sha256": hashlib.sha256(rb).hexdigest(),
+                "generator": "tests/scenarios.py:%s (numpy PCG64, seed base 0xEA5D)" % name,
+                "source": "oracle/_ref/ref_harness (EasyDarwin reference reflector)",
+                "substreams": capture_summary(cap),
+            }
+            with open(os.path.join(HERE, name + ".json"), "w") as f:
+                json.dump(fix, f, indent=1, sort_keys=True)
+            if name in FULL:
+                with open(os.path.join(HERE, name + ".edtr"), "wb") as f:
+                    f.write(trace)
+                with open(os.path.join(HERE, name + ".edcp"), "wb") as f:
+                    f.write(rb)
+            index[name] = {"relayed_packets": sum(v.n_packets for v in cap.values()),
+                           "substreams": len(cap)}
+            print(f"{name:8s} ok  {index[name]}")
+    with open(os.path.join(HERE, "index.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,233 @@
+"""Deterministic trace scenarios used for parity (golden fixtures, oracle pinning, GPU tests).
+
+Each scenario function returns a :class:`easydarwin_amd.trace.Trace`.  Seeds derive from
+``0xEA5D``.  The scenarios cover every row of SURVEY.md §8.a that has a
+parity consequence:
+
+* ``c1``            configs[0]: 1 H.264 720p30 push (2 s GOP) -> 4 UDP subscribers, two of
+                    them joining mid-GOP at 3.3 s (Q3/Q4/Q5/Q7 key-pointer start, SPS/PPS not
+                    replayed).
+* ``mixed``         C5-style: H.264 / MP4V-ES / JPEG video with AAC / PCMA / PCMU audio,
+                    jittered packet sizes, UDP and TCP-interleaved subscribers (Q2), pusher
+                    RTCP SRs carried on the odd channel of a TCP push (Q12), staggered joins.
+* ``clamp``         packets above the 2060-byte ReflectorPacket limit (Q11).
+* ``ssrc``          SSRC switch mid-stream, zero-length survivors and the 30 s reset (Q13).
+* ``nal``           crafted H.264 payloads: STAP-A/B, MTAP16/24, FU-A/FU-B with and without
+                    the start bit, the 19/20-byte length boundary, CSRC counts (Q4).
+* ``nokey``         a stream with no key frames: new subscribers start at the 1 s buffer
+                    window, and a join while the pusher is stalled gets a NULL start (Q7).
+* ``stall``         a 12 s pusher stall with subscribers attached (Q16 retention, bookmarks).
+* ``anchor``        video + two audio tracks: the session-wide audio anchor flag (Q6).
+* ``tiny``          a 1-session, 2-subscriber smoke case (used by ``smoke()``).
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+from easydarwin_amd.synth import (SEED_BASE, TrackSpec, make_sdp, rtp_header, rtcp_sr,
+                                  session_packets)
+from easydarwin_amd.trace import TCP, UDP, Trace
+
+
+def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
+              joins: list[tuple], tick_times=None):
+    """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
+    and ticks.  Within one tick interval the order is: packets (time order, session order),
+    then joins, then the TICK at the interval end."""
+    pkts = []
+    for s, lst in enumerate(per_session):
+        for k, (t, ch, data) in enumerate(lst):
+            pkts.append((t, s, k, ch, data))
+    pkts.sort(key=lambda x: (x[0], x[1], x[2]))
+    joins = sorted(joins)
+    ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
+    i = j = 0
+    for tt in ticks:
+        while i < len(pkts) and pkts[i][0] <= tt:
+            t, s, _, ch, data = pkts[i]
+            tr.pkt(t, s, ch, data)
+            i += 1
+        while j < len(joins) and joins[j][0] <= tt:
+            t, s, sub, transport = joins[j]
+            tr.join(t, s, sub, transport)
+            j += 1
+        tr.tick(tt)
+    return tr
+
+
+def c1(duration_ms: int = 10_000) -> Trace:
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=2_000_000, gop=60, idr_bytes=40_000)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    pk = session_packets(tracks, duration_ms, SEED_BASE + 0)
+    joins = [(0, 0, 1, UDP), (0, 0, 2, UDP), (3300, 0, 3, UDP), (3300, 0, 4, UDP)]
+    return _assemble(tr, [pk], 100, duration_ms, joins)
+
+
+def mixed(duration_ms: int = 4_000) -> Trace:
+    vids = [("H264/90000", True), ("MP4V-ES/90000", False), ("JPEG/90000", False)]
+    auds = ["MPEG4-GENERIC/48000/2", "PCMA/8000", "PCMU/8000"]
+    tr = Trace()
+    per, joins = [], []
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 4))
+    sub = 100
+    for s in range(6):
+        vname, _ = vids[s % 3]
+        tracks = [TrackSpec("video", vname, 96, bitrate=600_000, gop=30, idr_bytes=9_000,
+                            jitter_sizes=(s % 2 == 1), rtcp_every_ms=(700 if s in (0, 3) else 0)),
+                  TrackSpec("audio", auds[(s // 2) % 3], 97 if s % 3 == 0 else (8 if s % 3 == 1 else 0),
+                            jitter_sizes=(s == 5))]
+        tr.add_session(make_sdp(tracks))
+        per.append(session_packets(tracks, duration_ms, SEED_BASE + 40 + s))
+        for k in range(4):
+            t = int(rng.integers(0, duration_ms - 500)) if k else 0
+            joins.append((t, s, sub, TCP if (sub % 2) else UDP))
+            sub += 1
+    return _assemble(tr, per, 100, duration_ms, joins)
+
+
+def clamp() -> Trace:
+    tracks = [TrackSpec("video", "MP4V-ES/90000", 96)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 7))
+    ssrc = 0x1234ABCD
+    pk = []
+    for i, n in enumerate([100, 2059, 2060, 2061, 3000, 8000, 65535, 12, 20, 1400]):
+        pay = rng.integers(0, 256, size=max(n - 12, 0), dtype=np.uint8).tobytes()
+        pk.append((50 * i, 0, (rtp_header(1000 + i, 3000 * i, ssrc, 96, True) + pay)[:n]))
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (220, 0, 3, TCP)]
+    return _assemble(tr, [pk], 100, 600, joins)
+
+
+def ssrc() -> Trace:
+    tracks = [TrackSpec("video", "H264/90000", 96)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 8))
+    pk, seq = [], 0
+
+    def pkt(t, ssrc_v, nal=0x41, n=200):
+        nonlocal seq
+        seq += 1
+        pay = bytes([nal]) + rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        pk.append((t, 0, rtp_header(seq, t * 90, ssrc_v, 96, True) + pay))
+
+    pkt(0, 0xAAAA0001, 0x65)
+    for t in range(200, 2000, 200):
+        pkt(t, 0xAAAA0001)
+    pkt(2100, 0)                       # SSRC 0 survives the filter
+    pkt(2150, 0xAAAA0001)
+    for t in range(2200, 40_000, 1000):  # new pusher SSRC: zero-length until the 30 s reset
+        pkt(t, 0xBBBB0002, 0x65 if t % 5000 == 200 else 0x41)
+    pkt(40_100, 0xAAAA0001)
+    joins = [(0, 0, 1, UDP), (1000, 0, 2, TCP), (20_000, 0, 3, UDP), (35_000, 0, 4, TCP)]
+    return _assemble(tr, [pk], 500, 41_000, joins)
+
+
+def _h264_pkt(seq, t, payload: bytes, cc: int = 0, ssrc=0x51515151):
+    csrc = b"".join(struct.pack(">I", 0x1000 + k) for k in range(cc))
+    return rtp_header(seq, t * 90, ssrc, 96, False, cc=cc) + csrc + payload
+
+
+def nal() -> Trace:
+    """Crafted payloads through IsKeyFrameFirstPacket; a join after every candidate shows
+    which packet became the key pointer (the new subscriber's first packet)."""
+    tracks = [TrackSpec("video", "H264/90000", 96)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 9))
+
+    def rnd(n):
+        return rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+
+    cases = [
+        bytes([0x41]) + rnd(30),                       # non-IDR slice
+        bytes([0x65]) + rnd(30),                       # IDR            -> key
+        bytes([0x67]) + rnd(7),                        # SPS, 20-B pkt  -> key (boundary)
+        bytes([0x68]) + rnd(6),                        # PPS, 19-B pkt  -> not key (len < 20)
+        bytes([0x78, 0, 4, 0x67]) + rnd(30),           # STAP-A(SPS)    -> key
+        bytes([0x78, 0, 4, 0x41]) + rnd(30),           # STAP-A(slice)
+        bytes([0x79, 0, 0, 0, 4, 0x65]) + rnd(30),     # STAP-B(IDR)    -> key
+        bytes([0x7A, 0, 0, 0, 0, 0, 0, 0, 0x68]) + rnd(30),       # MTAP16(PPS) -> key
+        bytes([0x7B, 0, 0, 0, 0, 0, 0, 0, 0, 0x65]) + rnd(30),    # MTAP24(IDR) -> key
+        bytes([0x7B, 0, 0, 0, 0, 0, 0, 0, 0, 0x41]) + rnd(30),    # MTAP24(slice)
+        bytes([0x7C, 0x85]) + rnd(30),                 # FU-A start IDR -> key
+        bytes([0x7C, 0x05]) + rnd(30),                 # FU-A cont. IDR -> not key
+        bytes([0x7C, 0x45]) + rnd(30),                 # FU-A end IDR   -> not key
+        bytes([0x7D, 0x87]) + rnd(30),                 # FU-B start SPS -> key
+        bytes([0x7C, 0x81]) + rnd(30),                 # FU-A start slice
+        bytes([0x66]) + rnd(30),                       # SEI (type 6)
+        bytes([0x78, 0, 4]),                           # STAP-A, too short to peek (len 15 < 20)
+        bytes([0x78]) + rnd(6),                        # STAP-A, len 19
+        bytes([0x78, 0, 4]) + rnd(5),                  # STAP-A, len 20, peek byte random
+    ]
+    pk = []
+    t = 0
+    seq = 7
+    for i, pay in enumerate(cases):
+        pk.append((t, 0, _h264_pkt(seq, t, pay)))
+        seq += 1
+        t += 100
+    for cc in (1, 2):                                  # CSRC-shifted headers (h = 12 + 4cc < len)
+        pk.append((t, 0, _h264_pkt(seq, t, bytes([0x65]) + rnd(40), cc=cc))); seq += 1; t += 100
+        pk.append((t, 0, _h264_pkt(seq, t, bytes([0x41]) + rnd(40), cc=cc))); seq += 1; t += 100
+    end = t + 200
+    joins = [(tt, 0, 10 + k, UDP if k % 2 else TCP) for k, tt in enumerate(range(50, end, 100))]
+    return _assemble(tr, [pk], 50, end, joins)
+
+
+def nokey() -> Trace:
+    tracks = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=300_000),
+              TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    pk = session_packets(tracks, 3000, SEED_BASE + 10)
+    pk += [(t + 6000, ch, d) for (t, ch, d) in session_packets(tracks, 1500, SEED_BASE + 11)]
+    joins = [(0, 0, 1, UDP), (1500, 0, 2, TCP), (4500, 0, 3, UDP), (6500, 0, 4, TCP)]
+    return _assemble(tr, [pk], 100, 7600, joins)
+
+
+def stall() -> Trace:
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=15, idr_bytes=4000),
+              TrackSpec("audio", "PCMA/8000", 8)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    pk = session_packets(tracks, 2000, SEED_BASE + 12)
+    pk += [(t + 14_000, ch, d) for (t, ch, d) in session_packets(tracks, 1500, SEED_BASE + 13)]
+    joins = [(0, 0, 1, TCP), (5000, 0, 2, UDP), (13_000, 0, 3, TCP), (14_500, 0, 4, UDP)]
+    return _assemble(tr, [pk], 250, 16_000, joins)
+
+
+def anchor() -> Trace:
+    tracks = [TrackSpec("audio", "PCMA/8000", 8),
+              TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=20, idr_bytes=5000),
+              TrackSpec("audio", "MPEG4-GENERIC/48000/2", 97)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    tracks2 = [TrackSpec("audio", "PCMU/8000", 0)]           # audio-only session: no anchor
+    tr.add_session(make_sdp(tracks2))
+    pk0 = session_packets(tracks, 3000, SEED_BASE + 14)
+    pk1 = session_packets(tracks2, 3000, SEED_BASE + 15)
+    joins = [(0, 0, 1, UDP), (750, 0, 2, TCP), (1400, 0, 3, UDP), (2100, 0, 4, TCP),
+             (0, 1, 5, UDP), (1500, 1, 6, TCP)]
+    ticks = sorted(set(list(range(0, 3001, 150)) + [333, 1001, 1777]))
+    return _assemble(tr, [pk0, pk1], 150, 3000, joins, tick_times=ticks)
+
+
+def tiny() -> Trace:
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=15, idr_bytes=6000),
+              TrackSpec("audio", "PCMA/8000", 8)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    pk = session_packets(tracks, 1200, SEED_BASE + 16)
+    joins = [(0, 0, 1, UDP), (600, 0, 2, TCP)]
+    return _assemble(tr, [pk], 100, 1200, joins)
+
+
+SCENARIOS = {
+    "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
+    "nokey": nokey, "stall": stall, "anchor": anchor,
+}
