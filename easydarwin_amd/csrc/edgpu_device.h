@@ -1,0 +1,134 @@
+// edgpu_device.h -- device-resident tables of the relay engine (shared by host and kernels).
+//
+// HBM layout (one context = one GPU):
+//   * per sender (track x {RTP socket, RTCP socket}, the reference's ReflectorSender,
+//     ReflectorStream.h:274-351) two rings:
+//       - a packet-metadata ring of PktMeta (32 B), power-of-two entries, indexed by the
+//         sender's monotonically increasing packet index (its queue position);
+//       - a byte ring of 16-B "slots": each packet occupies roundup16(4 + len) bytes,
+//         [4-B RTSP-interleaved header '$' 0 BE16(len)][packet bytes][pad].  Slot offsets are
+//         kept in a *virtual* byte space (vbyte, monotonic u64); the ring position is
+//         vbyte mod ring_bytes, so a 16-B word never straddles the ring end.
+//     The slot layout is also the fan-out output layout, so relaying a range of packets to a
+//     subscriber is one contiguous, 16-B-aligned copy (UDP datagram at slot+4; TCP frame at
+//     slot+0 with the channel byte patched).
+//   * SenderDev / StreamDev / SessionDev / SubDev tables (AoS, small).
+#pragma once
+#include <stdint.h>
+
+namespace edgpu {
+
+enum : uint32_t {
+    kMaxPacket = 2060,              // ReflectorPacket::kMaxReflectorPacketSize (ReflectorStream.h:126)
+    kChunkPackets = 32,             // fan-out work item = 32 consecutive packets of one sender
+    kChunkWords = 32 * 129,         // 32 * roundup16(4 + 2060) / 16
+    kFanoutThreads = 256,
+    kFanoutRegWords = (kChunkWords + kFanoutThreads - 1) / kFanoutThreads,   // 17
+    kIngestThreads = 256,
+    kMaxTracks = 16,                // per session
+    kMaxSendersPerSession = 2 * kMaxTracks,
+};
+
+// SenderDev.flags
+enum : uint32_t {
+    kSndRtcpPort = 1u << 0,         // RTCP by local-port parity (bound UDP push socket B)
+    kSndRtcpKind = 1u << 1,         // written with qtssWriteFlagsIsRTCP (second sender of a stream)
+    kSndVideo    = 1u << 2,         // stream payload type video
+    kSndH264     = 1u << 3,         // payload name exactly "H264/90000"
+    kSndAudio    = 1u << 4,         // stream payload type audio
+};
+
+struct PktMeta {                    // 32 B
+    uint64_t vbyte;                 // virtual offset of the packet's slot
+    uint64_t id;                    // fStreamCountID
+    int64_t  arrival;               // fTimeArrived
+    uint32_t len;                   // fPacketPtr.Len (0 = rejected by the SSRC filter)
+    uint32_t vcount;                // number of non-empty packets before this one (mod 2^32)
+};
+
+struct SenderDev {
+    // static
+    uint64_t meta;                  // device pointer to PktMeta[ring_packets]
+    uint64_t ring;                  // device pointer to the byte ring
+    uint32_t pk_mask;               // ring_packets - 1
+    uint32_t word_mask;             // ring_bytes / 16 - 1
+    uint32_t flags;
+    uint32_t session;
+    uint32_t stream;                // global stream (track) index
+    uint32_t track;
+    uint32_t _pad0, _pad1;
+    // dynamic (ingest)
+    uint64_t head;                  // packets ever enqueued
+    uint64_t vbyte_end;             // virtual bytes ever enqueued
+    uint32_t vcount_end;            // non-empty packets ever enqueued (mod 2^32)
+    uint32_t valid_ssrc;            // FilterInvalidSSRCs state
+    int64_t  last_valid_s;
+    int64_t  key;                   // fKeyFrameStartPacketElementPointer as an index, -1 = NULL
+    int64_t  last_nonzero;          // index of the newest non-empty packet, -1 = none
+    // per tick
+    int64_t  new_start;             // fFirstPacketInQueueForNewOutput, -1 = NULL
+    uint64_t tail;                  // oldest index still intact in both rings
+    uint64_t umin;                  // min range start over this sender's sub-streams
+    uint32_t chunk_base, nchunks;   // fan-out work items
+};
+
+struct StreamDev {
+    uint64_t packet_count;          // ReflectorStream::fPacketCount (shared by both senders)
+};
+
+struct SessionDev {
+    uint32_t first_sender;          // senders of track t: first_sender + 2t (+1 for RTCP)
+    uint32_t ntracks;
+    uint32_t video_key_flag;        // ReflectorSession::fHasVideoKeyFrameUpdate
+    uint32_t first_stream;
+};
+
+struct SubDev {                     // one sub-stream: subscriber x sender
+    uint32_t handle;                // subscriber handle
+    uint32_t sender;
+    uint16_t track;
+    uint8_t  kind;                  // 0 RTP, 1 RTCP
+    uint8_t  transport;             // 0 UDP, 1 TCP
+    uint8_t  channel;               // interleaved channel 2*track + kind (RTPStream.cpp:472-473)
+    uint8_t  active;
+    uint8_t  has_last;
+    uint8_t  _pad0;
+    int64_t  bookmark;              // ReflectorOutput bookmark index, -1 = none
+    uint64_t last_id;               // qtssReflectorStreamLast{RTP,RTCP}PacketID
+    // per tick
+    uint64_t a;                     // first packet index of this tick's range
+    uint64_t vstart;                // vbyte of `a`
+    uint32_t vcstart;               // vcount of `a`
+    uint32_t count;                 // packets to send (non-empty)
+    uint64_t bytes;                 // slot bytes spanned
+    uint64_t out_base;
+    uint32_t desc_base;
+    uint32_t nonempty;              // range [a, head) is non-empty
+};
+
+struct WorkItem {
+    uint32_t sender;
+    uint32_t chunk;
+};
+
+struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
+    unsigned long long relayed_packets;
+    unsigned long long relayed_bytes;
+    unsigned long long arena_bytes;
+    unsigned long long ingested_packets;
+    unsigned long long ingested_bytes;
+    int status;
+    unsigned int nwork;
+};
+
+struct TickParams {
+    int64_t  now;
+    int64_t  over_buffer_ms;
+    uint64_t arena_bytes;
+    uint32_t max_desc;
+    uint32_t nsenders;
+    uint32_t nsubs;
+    uint32_t nsub_blocks;
+};
+
+}  // namespace edgpu

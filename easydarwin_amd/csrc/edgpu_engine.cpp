@@ -1,0 +1,551 @@
+// edgpu_engine.cpp -- host side of the relay engine behind the C ABI (include/edgpu.h).
+//
+// Owns the per-GPU context: HIP stream and events, the device tables of edgpu_device.h, the
+// per-sender HBM rings, ingest staging, the fan-out arena, and the session / subscriber
+// bookkeeping the reflector keeps on the CPU (ReflectorSession / ReflectorStream /
+// ReflectorOutput membership).  Every packet-rate decision runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "edgpu.h"
+#include "edgpu_device.h"
+
+#include "edgpu_params.h"
+
+namespace edgpu {
+hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_plan(const PlanParams& p, hipStream_t st);
+hipError_t launch_fanout(const FanoutParams& p, uint32_t grid, hipStream_t st);
+int fanout_occupancy();
+}  // namespace edgpu
+
+using namespace edgpu;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) { g_err = msg; return code; }
+#define HIP_CHECK(expr)                                                                   \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(EDGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+// Growable device array of POD T.
+template <typename T>
+struct DevVec {
+    T* ptr = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n, hipStream_t st) {
+        if (n <= cap) return hipSuccess;
+        size_t nc = std::max<size_t>(n, cap ? cap * 2 : 64);
+        T* np = nullptr;
+        hipError_t e = hipMalloc(&np, nc * sizeof(T));
+        if (e != hipSuccess) return e;
+        if (ptr) {
+            e = hipMemcpyAsync(np, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            (void)hipFree(ptr);
+            if (e != hipSuccess) { (void)hipFree(np); return e; }
+        }
+        ptr = np;
+        cap = nc;
+        return hipSuccess;
+    }
+    void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; cap = 0; }
+};
+
+struct TrackHost { uint32_t type = 0; std::string name; };   // 1 video, 2 audio
+
+struct SessionHost {
+    uint32_t first_sender, ntracks, first_stream;
+    bool udp_push;
+};
+
+struct SubscriberHost {
+    uint32_t session;
+    uint32_t first_sub;         // first SubDev index
+    uint32_t nsub;
+    bool active;
+};
+
+struct edgpu_ctx {
+    edgpu_config cfg;
+    int device = 0;
+    int num_cus = 256;
+    int fanout_blocks = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    bool timed_fanout = false, timed_ingest = false, timed_keyframe = false;
+
+    std::vector<SessionHost> sessions;
+    std::vector<SubscriberHost> subscribers;
+    std::vector<uint32_t> sub_sender;   // host mirror: SubDev index -> sender
+    std::vector<uint8_t> sub_active;
+    uint32_t nsenders = 0, nstreams = 0;
+    std::vector<void*> ring_allocs;
+    uint64_t work_cap_needed = 0;
+
+    DevVec<SessionDev> d_sessions;
+    DevVec<SenderDev> d_senders;
+    DevVec<StreamDev> d_streams;
+    DevVec<SubDev> d_subs;
+    DevVec<uint32_t> d_sub_index;
+    DevVec<uint32_t> d_sub_range;
+    DevVec<edgpu_substream_out> d_sub_out;
+    DevVec<WorkItem> d_work;
+    DevVec<uint64_t> d_blk_bytes, d_blk_bytes_base;
+    DevVec<uint32_t> d_blk_count, d_blk_count_base;
+    bool index_dirty = true;
+
+    // ingest staging
+    edgpu_pkt_desc* d_desc = nullptr;
+    uint32_t* d_seg = nullptr;
+    uint32_t* d_seg_sess = nullptr;
+    uint8_t* d_blob = nullptr;
+    uint32_t* d_pflags = nullptr;
+    uint64_t* d_pidx = nullptr;
+    // pending batch for keyframe_index
+    const uint32_t* pend_seg = nullptr;
+    const uint32_t* pend_seg_sess = nullptr;
+    uint32_t pend_nseg = 0;
+    bool pending = false;
+
+    uint8_t* d_arena = nullptr;
+    edgpu_out_desc* d_out_desc = nullptr;
+    TickTotals* d_totals = nullptr;
+};
+
+extern "C" {
+
+const char* edgpu_version(void) { return "edgpu 0.1 (gfx950)"; }
+const char* edgpu_last_error(void) { return g_err.c_str(); }
+
+void edgpu_config_default(edgpu_config* c) {
+    memset(c, 0, sizeof(*c));
+}
+
+static void fill_defaults(edgpu_config& c) {
+    if (!c.reflector_buffer_size_sec) c.reflector_buffer_size_sec = 1;
+    if (!c.rtp_reflector_threshold_msec) c.rtp_reflector_threshold_msec = 2000;
+    if (c.rtp_reflector_threshold_msec < 1000) c.rtp_reflector_threshold_msec = 1000;
+    if (!c.timeout_stream_SSRC_secs) c.timeout_stream_SSRC_secs = 30;
+    c.use_one_SSRC_per_stream = (c.use_one_SSRC_per_stream == EDGPU_FALSE) ? 0 : 1;
+    if (!c.video_ring_packets) c.video_ring_packets = 8192;
+    if (!c.video_ring_bytes) c.video_ring_bytes = 8ull << 20;
+    if (!c.other_ring_packets) c.other_ring_packets = 2048;
+    if (!c.other_ring_bytes) c.other_ring_bytes = 1ull << 20;
+    if (!c.out_arena_bytes) c.out_arena_bytes = 256ull << 20;
+    if (!c.max_out_packets) c.max_out_packets = 1u << 20;
+    if (!c.max_batch_packets) c.max_batch_packets = 1u << 20;
+    if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;
+}
+
+static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
+    if (!out) return fail(EDGPU_BAD_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    edgpu_config c;
+    if (cfg_in) c = *cfg_in; else edgpu_config_default(&c);
+    fill_defaults(c);
+    if (!pow2(c.video_ring_packets) || !pow2(c.other_ring_packets) || !pow2(c.video_ring_bytes) ||
+        !pow2(c.other_ring_bytes) || c.video_ring_bytes < 4096 || c.other_ring_bytes < 4096)
+        return fail(EDGPU_BAD_ARGUMENT, "ring capacities must be powers of two (bytes >= 4096)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(EDGPU_NO_DEVICE, "no HIP device visible (libedgpu needs an MI355X / gfx950)");
+    if (c.device < 0 || c.device >= ndev) return fail(EDGPU_BAD_ARGUMENT, "bad device ordinal");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c.device) != hipSuccess)
+        return fail(EDGPU_NO_DEVICE, "hipGetDeviceProperties failed");
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(EDGPU_NO_DEVICE, std::string("libedgpu is built for gfx950, device is ") + prop.gcnArchName);
+    edgpu_ctx* x = new edgpu_ctx();
+    x->cfg = c;
+    x->device = c.device;
+    x->num_cus = prop.multiProcessorCount;
+    if (hipSetDevice(c.device) != hipSuccess) { delete x; return fail(EDGPU_NO_DEVICE, "hipSetDevice failed"); }
+    auto bad = [&](const char* what) { edgpu_ctx_destroy(x); return fail(EDGPU_OUT_OF_MEMORY, what); };
+    if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return bad("stream");
+    for (auto& e : x->ev) if (hipEventCreate(&e) != hipSuccess) return bad("event");
+    if (hipMalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
+    if (hipMalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
+    if (hipMalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
+    if (hipMalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
+    if (hipMalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
+    if (hipMalloc(&x->d_blob, c.max_batch_bytes) != hipSuccess) return bad("blob staging");
+    if (hipMalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
+    if (hipMalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
+    if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    x->fanout_blocks = x->num_cus * fanout_occupancy();
+    *out = x;
+    return EDGPU_OK;
+}
+
+int edgpu_ctx_destroy(edgpu_ctx* x) {
+    if (!x) return EDGPU_OK;
+    (void)hipSetDevice(x->device);
+    if (x->stream) (void)hipStreamSynchronize(x->stream);
+    for (void* p : x->ring_allocs) (void)hipFree(p);
+    x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
+    x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_out.release(); x->d_work.release();
+    x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
+    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx,
+                    (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals})
+        if (p) (void)hipFree(p);
+    for (auto& e : x->ev) if (e) (void)hipEventDestroy(e);
+    if (x->stream) (void)hipStreamDestroy(x->stream);
+    delete x;
+    return EDGPU_OK;
+}
+
+int edgpu_sync(edgpu_ctx* x) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    return EDGPU_OK;
+}
+
+// SDP restatement: a track per m= line (media word -> payload type), named by the rest of
+// its first a=rtpmap line after the first space (SDPSourceInfo.cpp:259-353).
+static std::vector<TrackHost> parse_sdp(const char* sdp, uint32_t n) {
+    std::vector<TrackHost> t;
+    std::string s(sdp, n);
+    size_t p = 0;
+    while (p < s.size()) {
+        size_t e = s.find_first_of("\r\n", p);
+        if (e == std::string::npos) e = s.size();
+        std::string line = s.substr(p, e - p);
+        p = e;
+        while (p < s.size() && (s[p] == '\r' || s[p] == '\n')) p++;
+        if (line.size() < 2 || line[1] != '=') continue;
+        if (line[0] == 'm') {
+            size_t sp = line.find(' ', 2);
+            std::string media = line.substr(2, sp == std::string::npos ? std::string::npos : sp - 2);
+            TrackHost th;
+            th.type = media == "video" ? 1 : media == "audio" ? 2 : 0;
+            t.push_back(th);
+        } else if (line[0] == 'a' && !t.empty() && line.compare(2, 7, "rtpmap:") == 0 && t.back().name.empty()) {
+            size_t sp = line.find(' ', 2);
+            if (sp != std::string::npos) t.back().name = line.substr(sp + 1);
+        }
+    }
+    return t;
+}
+
+int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_push, uint32_t* out_session) {
+    if (!x || !sdp) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    std::vector<TrackHost> tracks = parse_sdp(sdp, sdp_len);
+    if (tracks.empty() || tracks.size() > kMaxTracks)
+        return fail(EDGPU_BAD_ARGUMENT, "SDP must describe 1..16 tracks");
+    const uint32_t sid = (uint32_t)x->sessions.size();
+    SessionHost sh{x->nsenders, (uint32_t)tracks.size(), x->nstreams, udp_push != 0};
+    const uint32_t nsnd = 2 * sh.ntracks;
+    HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
+    HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));
+    HIP_CHECK(x->d_streams.reserve(x->nstreams + sh.ntracks, x->stream));
+    HIP_CHECK(x->d_sub_range.reserve(2 * (x->nsenders + nsnd), x->stream));
+    std::vector<SenderDev> snd(nsnd);
+    std::vector<StreamDev> str(sh.ntracks);
+    for (uint32_t t = 0; t < sh.ntracks; t++) {
+        uint32_t base = 0;
+        if (tracks[t].type == 1) base |= kSndVideo;
+        if (tracks[t].type == 2) base |= kSndAudio;
+        if (tracks[t].name == "H264/90000") base |= kSndH264;    // exact, case-sensitive (Q3)
+        for (uint32_t k = 0; k < 2; k++) {
+            SenderDev& D = snd[2 * t + k];
+            memset(&D, 0, sizeof(D));
+            const bool big = (k == 0 && tracks[t].type == 1);
+            const uint64_t pk = big ? x->cfg.video_ring_packets : x->cfg.other_ring_packets;
+            const uint64_t by = big ? x->cfg.video_ring_bytes : x->cfg.other_ring_bytes;
+            void* meta = nullptr; void* ring = nullptr;
+            if (hipMalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring");
+            x->ring_allocs.push_back(meta);
+            if (hipMalloc(&ring, by) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring");
+            x->ring_allocs.push_back(ring);
+            D.meta = (uint64_t)(uintptr_t)meta;
+            D.ring = (uint64_t)(uintptr_t)ring;
+            D.pk_mask = (uint32_t)(pk - 1);
+            D.word_mask = (uint32_t)(by / 16 - 1);
+            D.flags = base | (k ? kSndRtcpKind : 0u) | ((k && sh.udp_push) ? kSndRtcpPort : 0u);
+            D.session = sid;
+            D.stream = x->nstreams + t;
+            D.track = t;
+            D.key = -1;
+            D.last_nonzero = -1;
+            D.new_start = -1;
+            x->work_cap_needed += pk / kChunkPackets + 1;
+        }
+        str[t].packet_count = 0;
+    }
+    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream};
+    HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + x->nsenders, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + x->nstreams, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + sid, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    x->sessions.push_back(sh);
+    x->nsenders += nsnd;
+    x->nstreams += sh.ntracks;
+    x->index_dirty = true;
+    if (out_session) *out_session = sid;
+    return EDGPU_OK;
+}
+
+int edgpu_session_tracks(edgpu_ctx* x, uint32_t session, uint32_t* out_tracks) {
+    if (!x || session >= x->sessions.size() || !out_tracks) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    *out_tracks = x->sessions[session].ntracks;
+    return EDGPU_OK;
+}
+
+int edgpu_subscriber_add(edgpu_ctx* x, uint32_t session, int transport, uint32_t* out_handle) {
+    if (!x || session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (transport != EDGPU_TRANSPORT_UDP && transport != EDGPU_TRANSPORT_TCP)
+        return fail(EDGPU_BAD_ARGUMENT, "bad transport");
+    HIP_CHECK(hipSetDevice(x->device));
+    const SessionHost& sh = x->sessions[session];
+    const uint32_t handle = (uint32_t)x->subscribers.size();
+    const uint32_t first = (uint32_t)x->sub_sender.size();
+    const uint32_t n = 2 * sh.ntracks;
+    HIP_CHECK(x->d_subs.reserve(first + n, x->stream));
+    std::vector<SubDev> v(n);
+    for (uint32_t t = 0; t < sh.ntracks; t++)
+        for (uint32_t k = 0; k < 2; k++) {
+            SubDev& Q = v[2 * t + k];
+            memset(&Q, 0, sizeof(Q));
+            Q.handle = handle;
+            Q.sender = sh.first_sender + 2 * t + k;
+            Q.track = (uint16_t)t;
+            Q.kind = (uint8_t)k;
+            Q.transport = (uint8_t)transport;
+            Q.channel = (uint8_t)(2 * t + k);        // GetTwoChannelNumbers in SETUP order
+            Q.active = 1;
+            Q.bookmark = -1;
+            x->sub_sender.push_back(Q.sender);
+            x->sub_active.push_back(1);
+        }
+    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), n * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    x->subscribers.push_back(SubscriberHost{session, first, n, true});
+    x->index_dirty = true;
+    if (out_handle) *out_handle = handle;
+    return EDGPU_OK;
+}
+
+int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
+    if (!x || handle >= x->subscribers.size() || !x->subscribers[handle].active)
+        return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
+    HIP_CHECK(hipSetDevice(x->device));
+    SubscriberHost& s = x->subscribers[handle];
+    const uint8_t zero = 0;
+    for (uint32_t i = 0; i < s.nsub; i++) {
+        x->sub_active[s.first_sub + i] = 0;
+        HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(x->d_subs.ptr + s.first_sub + i) + offsetof(SubDev, active),
+                                 &zero, 1, hipMemcpyHostToDevice, x->stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    s.active = false;
+    x->index_dirty = true;
+    return EDGPU_OK;
+}
+
+static int rebuild_index(edgpu_ctx* x) {
+    const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    std::vector<uint32_t> idx;
+    idx.reserve(nsub);
+    for (uint32_t i = 0; i < nsub; i++) if (x->sub_active[i]) idx.push_back(i);
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return x->sub_sender[a] < x->sub_sender[b]; });
+    std::vector<uint32_t> range(2 * (size_t)x->nsenders, 0);
+    for (uint32_t k = 0; k < idx.size();) {
+        uint32_t s = x->sub_sender[idx[k]], e = k;
+        while (e < idx.size() && x->sub_sender[idx[e]] == s) e++;
+        range[2 * s] = k; range[2 * s + 1] = e;
+        k = e;
+    }
+    HIP_CHECK(x->d_sub_index.reserve(std::max<size_t>(idx.size(), 1), x->stream));
+    HIP_CHECK(x->d_sub_range.reserve(std::max<size_t>(range.size(), 2), x->stream));
+    if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_index.ptr, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, x->stream));
+    if (!range.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_range.ptr, range.data(), range.size() * 4, hipMemcpyHostToDevice, x->stream));
+    const uint32_t nblk = (nsub + 255) / 256;
+    HIP_CHECK(x->d_sub_out.reserve(std::max<uint32_t>(nsub, 1), x->stream));
+    HIP_CHECK(x->d_blk_bytes.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_blk_bytes_base.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_blk_count.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_blk_count_base.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_work.reserve(std::max<uint64_t>(x->work_cap_needed, 1), x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    x->index_dirty = false;
+    return EDGPU_OK;
+}
+
+int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
+                 const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets || blob_bytes > x->cfg.max_batch_bytes)
+        return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
+    if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
+    HIP_CHECK(hipSetDevice(x->device));
+    const edgpu_pkt_desc* dd = desc;
+    const uint32_t* ds = seg_off;
+    const uint32_t* dss = seg_sess;
+    const uint8_t* db = blob;
+    if (where == EDGPU_PTR_HOST) {
+        // validate on the host (segment bounds, session ids, slot bounds) before any launch
+        if (nseg && seg_off[nseg] != n) return fail(EDGPU_BAD_ARGUMENT, "seg_offsets[n_segments] != n_packets");
+        for (uint32_t s = 0; s < nseg; s++) {
+            if (seg_off[s] > seg_off[s + 1]) return fail(EDGPU_BAD_ARGUMENT, "segments not monotone");
+            if (seg_sess[s] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in batch");
+        }
+        for (uint32_t i = 0; i < n; i++)
+            if ((uint64_t)desc[i].slot * 16 + 4 + std::min<uint32_t>(desc[i].len, kMaxPacket) + 15 > blob_bytes + 15 ||
+                (uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
+                return fail(EDGPU_BAD_ARGUMENT, "packet slot outside blob");
+        HIP_CHECK(hipMemcpyAsync(x->d_desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipMemcpyAsync(x->d_seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipMemcpyAsync(x->d_seg_sess, seg_sess, (size_t)nseg * 4, hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipMemcpyAsync(x->d_blob, blob, blob_bytes, hipMemcpyHostToDevice, x->stream));
+        dd = x->d_desc; ds = x->d_seg; dss = x->d_seg_sess; db = x->d_blob;
+    } else if (where != EDGPU_PTR_DEVICE) {
+        return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
+    }
+    IngestParams p;
+    p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
+    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
+    p.pflags = x->d_pflags; p.pidx = x->d_pidx;
+    p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
+    p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
+    p.totals = x->d_totals;
+    HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
+    HIP_CHECK(launch_ingest(p, nseg, x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
+    x->timed_ingest = true;
+    x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
+    return EDGPU_OK;
+}
+
+int edgpu_keyframe_index(edgpu_ctx* x) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (!x->pending) return fail(EDGPU_ERR, "no ingested batch pending a keyframe index");
+    HIP_CHECK(hipSetDevice(x->device));
+    KeyframeParams p;
+    p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
+    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
+    HIP_CHECK(hipEventRecord(x->ev[6], x->stream));
+    HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[7], x->stream));
+    x->timed_keyframe = true;
+    x->pending = false;
+    return EDGPU_OK;
+}
+
+int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    HIP_CHECK(hipSetDevice(x->device));
+    if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
+    const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    PlanParams p;
+    p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
+    p.sub_out = x->d_sub_out.ptr; p.work = x->d_work.ptr;
+    p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
+    p.blk_bytes_base = x->d_blk_bytes_base.ptr; p.blk_count_base = x->d_blk_count_base.ptr;
+    p.totals = x->d_totals;
+    p.T.now = now_ms;
+    p.T.over_buffer_ms = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
+    p.T.arena_bytes = x->cfg.out_arena_bytes;
+    p.T.max_desc = x->cfg.max_out_packets;
+    p.T.nsenders = x->nsenders;
+    p.T.nsubs = nsub;
+    p.T.nsub_blocks = (nsub + 255) / 256;
+    // reset per-tick totals (relayed_*, arena, status, nwork); keep the ingest counters
+    HIP_CHECK(hipMemsetAsync(x->d_totals, 0, 3 * sizeof(unsigned long long), x->stream));
+    HIP_CHECK(hipMemsetAsync(&x->d_totals->status, 0, 2 * sizeof(int), x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[0], x->stream));
+    HIP_CHECK(launch_plan(p, x->stream));
+    FanoutParams f;
+    f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
+    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
+    f.totals = x->d_totals;
+    HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
+    HIP_CHECK(launch_fanout(f, (uint32_t)x->fanout_blocks, x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[2], x->stream));
+    x->timed_fanout = true;
+    if (out) {
+        out->arena = x->d_arena;
+        out->desc = x->d_out_desc;
+        out->substreams = x->d_sub_out.ptr;
+        out->n_substreams = nsub;
+    }
+    return EDGPU_OK;
+}
+
+int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
+    if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    TickTotals t;
+    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    out->relayed_packets = t.relayed_packets;
+    out->relayed_bytes = t.relayed_bytes;
+    out->arena_bytes = t.arena_bytes;
+    out->ingested_packets = t.ingested_packets;
+    out->ingested_bytes = t.ingested_bytes;
+    out->status = t.status;
+    out->_pad = t.nwork;
+    return EDGPU_OK;
+}
+
+int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes) {
+    if (!x || (!dst && bytes) || (!src && bytes)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!bytes) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    return EDGPU_OK;
+}
+
+int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
+    if (!x || !out_ms) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    out_ms[0] = out_ms[1] = out_ms[2] = out_ms[3] = 0.f;
+    if (x->timed_fanout) {
+        HIP_CHECK(hipEventElapsedTime(&out_ms[0], x->ev[1], x->ev[2]));
+        HIP_CHECK(hipEventElapsedTime(&out_ms[1], x->ev[0], x->ev[2]));
+    }
+    if (x->timed_ingest) HIP_CHECK(hipEventElapsedTime(&out_ms[2], x->ev[4], x->ev[5]));
+    if (x->timed_keyframe) HIP_CHECK(hipEventElapsedTime(&out_ms[3], x->ev[6], x->ev[7]));
+    return EDGPU_OK;
+}
+
+int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out_packets, uint64_t* out_bytes) {
+    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks)
+        return fail(EDGPU_BAD_ARGUMENT, "bad session/track");
+    HIP_CHECK(hipSetDevice(x->device));
+    SenderDev D;
+    HIP_CHECK(hipMemcpyAsync(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D),
+                             hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    uint64_t pk = 0, by = 0;
+    if (D.key >= 0) {
+        PktMeta m;
+        HIP_CHECK(hipMemcpyAsync(&m, reinterpret_cast<PktMeta*>(D.meta) + ((uint64_t)D.key & D.pk_mask), sizeof(m),
+                                 hipMemcpyDeviceToHost, x->stream));
+        HIP_CHECK(hipStreamSynchronize(x->stream));
+        pk = D.head - (uint64_t)D.key;
+        by = D.vbyte_end - m.vbyte;
+    }
+    if (out_packets) *out_packets = pk;
+    if (out_bytes) *out_bytes = by;
+    return EDGPU_OK;
+}
+
+}  // extern "C"

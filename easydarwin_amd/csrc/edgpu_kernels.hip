@@ -1,0 +1,669 @@
+// edgpu_kernels.hip -- CDNA4 (gfx950) kernels of the relay engine.
+//
+//   k_ingest        ReflectorStream::PushPacket + ReflectorSocket::ProcessPacket
+//                   (ReflectorStream.cpp:529-576, 1769-2010): clamp (Q11), UDP-RTCP SR gate
+//                   (Q14), SSRC latch filter (Q13, ReflectorStream.cpp:1732-1767), per-stream
+//                   packet ids, enqueue into the sender's HBM rings, key-frame candidate parse
+//                   (IsKeyFrameFirstPacket, ReflectorStream.cpp:1403-1513).
+//                   One 256-thread workgroup per session segment, one packet per lane.
+//   k_keyframe      key pointer update and session-wide audio anchor (ReflectorStream.cpp:
+//                   1876-1934): one wave per session, 64 packets per step, ballot +
+//                   last-set-bit instead of the reference's per-packet branch chain.
+//   k_plan_*        ReflectPackets' per-tick decisions (ReflectorStream.cpp:1024-1136):
+//                   new-output start (key pointer, else GetClientBufferStartPacketOffset),
+//                   per-sub-stream range, bookmark and last-id commit, output offsets.
+//   k_fanout        SendPacketsToOutput -> WritePacket -> RTPStream::Write framing for every
+//                   (sub-stream, packet): each workgroup owns 32 consecutive packets of one
+//                   sender, loads their slots from HBM once into registers and writes them
+//                   to every sub-stream of that sender (16-B stores), patching the
+//                   interleaved channel byte for TCP subscribers, plus one 16-B descriptor
+//                   per output packet.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "edgpu.h"
+#include "edgpu_device.h"
+#include "edgpu_params.h"
+
+namespace edgpu {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t be16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+    return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+// RTSP-interleaved header dword stored at the start of every slot: '$', channel 0, BE16(len)
+// (RTSPSessionInterface.cpp:329-336), as a little-endian u32.
+__device__ __forceinline__ uint32_t slot_header(uint32_t len) {
+    return 0x24u | ((len >> 8) & 0xFF) << 16 | (len & 0xFF) << 24;
+}
+
+// H.264 "first packet of a key frame" rule (Q4): length >= 20, header size 12 + 4*CC
+// (the X bit and padding are ignored), aggregation units peek at their first NAL, FU-A/B
+// only on the start fragment; key iff NAL type 5, 7 or 8.  Bytes at or past `len` read 0.
+__device__ bool key_frame_first_packet(const uint8_t* p, uint32_t len) {
+    if (len < 20) return false;
+    const uint32_t h = 12 + 4u * (p[0] & 0x0F);
+    auto at = [&](uint32_t i) -> uint32_t { return i < len ? p[i] : 0u; };
+    uint32_t t = at(h) & 0x1F;
+    if (t == 24) { if (len > h + 3) t = at(h + 3) & 0x1F; }
+    else if (t == 25) { if (len > h + 5) t = at(h + 5) & 0x1F; }
+    else if (t == 26) { if (len > h + 8) t = at(h + 8) & 0x1F; }
+    else if (t == 27) { if (len > h + 9) t = at(h + 9) & 0x1F; }
+    else if (t == 28 || t == 29) { if (len > h + 1 && (at(h + 1) & 0x80)) t = at(h + 1) & 0x1F; }
+    return t == 5 || t == 7 || t == 8;
+}
+
+// ReflectorPacket::GetSSRC (ReflectorStream.h:145-158)
+__device__ __forceinline__ uint32_t packet_ssrc(const uint8_t* p, uint32_t len, bool rtcp) {
+    if (len < 8) return 0;
+    if (rtcp) return be32(p + 4);
+    if (len < 12) return 0;
+    return be32(p + 8);
+}
+
+// 256-thread exclusive scan (4 waves of 64).  `scratch` holds 4 entries.
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        T t = scratch[w];
+        if (w < wid) base += t;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + x - v;
+}
+
+// =========================================================================================
+// Ingest
+// =========================================================================================
+
+__global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
+    const uint32_t seg = blockIdx.x;
+    const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
+    const SessionDev S = P.sessions[P.seg_sess[seg]];
+    const uint32_t nsnd = 2 * S.ntracks;
+    const int tid = threadIdx.x;
+
+    __shared__ uint64_t s_head[kMaxSendersPerSession], s_vbyte[kMaxSendersPerSession];
+    __shared__ uint32_t s_vcount[kMaxSendersPerSession], s_valid[kMaxSendersPerSession];
+    __shared__ int64_t s_lastv[kMaxSendersPerSession], s_lastnz[kMaxSendersPerSession];
+    __shared__ uint32_t s_flags[kMaxSendersPerSession], s_pkmask[kMaxSendersPerSession], s_wmask[kMaxSendersPerSession];
+    __shared__ uint64_t s_meta[kMaxSendersPerSession], s_ring[kMaxSendersPerSession];
+    __shared__ uint64_t s_count[kMaxTracks];
+    __shared__ uint64_t c_tot[kMaxSendersPerSession];
+    __shared__ uint32_t c_ttot[kMaxTracks];
+    // per packet of the current chunk
+    __shared__ uint8_t p_snd[kIngestThreads];
+    __shared__ uint8_t p_acc[kIngestThreads];
+    __shared__ uint16_t p_len[kIngestThreads];
+    __shared__ uint32_t p_ssrc[kIngestThreads];
+    __shared__ int64_t p_ts[kIngestThreads];
+    __shared__ uint32_t p_src[kIngestThreads];
+    __shared__ uint32_t p_slotb[kIngestThreads];
+    __shared__ uint64_t p_vb[kIngestThreads];
+    __shared__ uint64_t scan64[4];
+    __shared__ uint32_t scan32[4];
+
+    if (tid < (int)nsnd) {
+        const SenderDev& D = P.senders[S.first_sender + tid];
+        s_head[tid] = D.head; s_vbyte[tid] = D.vbyte_end; s_vcount[tid] = D.vcount_end;
+        s_valid[tid] = D.valid_ssrc; s_lastv[tid] = D.last_valid_s; s_lastnz[tid] = D.last_nonzero;
+        s_flags[tid] = D.flags; s_pkmask[tid] = D.pk_mask; s_wmask[tid] = D.word_mask;
+        s_meta[tid] = D.meta; s_ring[tid] = D.ring;
+    }
+    if (tid < (int)S.ntracks) s_count[tid] = P.streams[S.first_stream + tid].packet_count;
+    __syncthreads();
+
+    uint64_t in_pk = 0, in_bytes = 0;
+    for (uint32_t base = b; base < e; base += kIngestThreads) {
+        const uint32_t n = min((uint32_t)kIngestThreads, e - base);
+        const uint32_t i = base + tid;
+        const bool valid = (uint32_t)tid < n;
+        uint32_t len = 0, track = 0, ls = 0, fl = 0, slot = 0;
+        int64_t arrival = 0;
+        bool acc = false;
+        const uint8_t* pk = nullptr;
+        if (valid) {
+            const edgpu_pkt_desc d = P.desc[i];
+            len = min((uint32_t)d.len, (uint32_t)kMaxPacket);
+            track = d.channel >> 1;
+            ls = 2 * track + (d.channel & 1);
+            arrival = d.arrival_ms;
+            slot = d.slot;
+            acc = track < S.ntracks && len > 0;       // ProcessRTPData: inIndex < numStreams
+            pk = P.blob + (uint64_t)slot * 16 + 4;
+            if (acc) fl = s_flags[ls];
+            // UDP push: socket B is the odd port, so only SRs survive (Q14)
+            if (acc && (fl & kSndRtcpPort))
+                acc = len >= 8 && len >= 4 * be16(pk + 2) + 4 && (pk[0] >> 6) == 2 && pk[1] == 200;
+            in_pk += 1;
+            in_bytes += len;
+        }
+        p_snd[tid] = (uint8_t)ls;
+        p_acc[tid] = acc;
+        p_len[tid] = (uint16_t)len;
+        p_src[tid] = slot;
+        p_ssrc[tid] = acc ? packet_ssrc(pk, len, (fl & kSndRtcpPort) != 0) : 0;
+        p_ts[tid] = arrival / 1000;          // OS::Milliseconds() / 1000, truncating
+        // ---- SSRC latch filter (sequential per socket; fast path when nothing changes) ----
+        if (P.filter_ssrc) {
+            const bool ok = !acc || (s_valid[ls] != 0 && p_ssrc[tid] == s_valid[ls]);
+            const int allok = __syncthreads_and(ok ? 1 : 0);
+            if (allok) {
+                if (tid < (int)nsnd) {                     // newest accepted packet per socket
+                    for (int p = (int)n - 1; p >= 0; p--)
+                        if (p_acc[p] && p_snd[p] == tid) { s_lastv[tid] = p_ts[p]; break; }
+                }
+            } else if (tid == 0) {
+                for (uint32_t p = 0; p < n; p++) {
+                    if (!p_acc[p]) continue;
+                    const uint32_t s = p_snd[p];
+                    const uint32_t ssrc = p_ssrc[p];
+                    const int64_t now_s = p_ts[p];
+                    if (s_valid[s] == 0) { s_valid[s] = ssrc; s_lastv[s] = now_s; continue; }
+                    if (ssrc != 0) {
+                        if (ssrc == s_valid[s]) { s_lastv[s] = now_s; continue; }
+                        p_len[p] = 0;                      // wrong SSRC: stays queued, length 0
+                    }
+                    if (s_lastv[s] + (int64_t)P.ssrc_timeout_s < now_s) s_valid[s] = 0;
+                }
+            }
+            __syncthreads();
+            len = p_len[tid];
+        }
+        const bool nz = acc && len > 0;
+        const uint32_t slotb = nz ? ((len + 4 + 15) & ~15u) : 0;
+        // ---- per-sender queue index / slot offset / non-empty count ----
+        uint32_t my_rank = 0, my_nzpre = 0;
+        uint64_t my_slotpre = 0;
+        for (uint32_t s = 0; s < nsnd; s++) {
+            const bool mine = acc && ls == s;
+            const uint64_t x = mine ? (1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20) : 0ull;
+            uint64_t tot;
+            const uint64_t pre = block_exclusive_scan<uint64_t>(x, scan64, tot);
+            if (mine) { my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20; }
+            if (tid == 0) c_tot[s] = tot;
+        }
+        uint32_t my_trank = 0;
+        for (uint32_t t = 0; t < S.ntracks; t++) {
+            const bool mine = acc && track == t;
+            uint32_t tot;
+            const uint32_t pre = block_exclusive_scan<uint32_t>(mine ? 1u : 0u, scan32, tot);
+            if (mine) my_trank = pre;
+            if (tid == 0) c_ttot[t] = tot;
+        }
+        uint64_t idx = 0, vb = 0;
+        if (acc) {
+            idx = s_head[ls] + my_rank;
+            vb = s_vbyte[ls] + my_slotpre;
+            PktMeta m;
+            m.vbyte = vb;
+            m.id = s_count[track] + my_trank + 1;        // fStreamCountID = ++fPacketCount
+            m.arrival = arrival;
+            m.len = len;
+            m.vcount = s_vcount[ls] + my_nzpre;
+            reinterpret_cast<PktMeta*>(s_meta[ls])[idx & s_pkmask[ls]] = m;
+            const bool by_port_rtp = !(fl & kSndRtcpPort);
+            const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len >= 20 &&
+                             key_frame_first_packet(pk, len);
+            const bool aud = by_port_rtp && (fl & kSndAudio);
+            P.pflags[i] = 1u | (key ? 2u : 0u) | (aud ? 4u : 0u) | ls << 8;
+            P.pidx[i] = idx;
+        } else if (valid) {
+            P.pflags[i] = 0;
+            P.pidx[i] = 0;
+        }
+        p_slotb[tid] = slotb;
+        p_vb[tid] = vb;
+        __syncthreads();
+        // ---- copy packet bytes into the byte rings: one wave per packet, 16 B per lane ----
+        {
+            const int lane = tid & 63, wid = tid >> 6;
+            for (uint32_t p = wid; p < n; p += kIngestThreads / 64) {
+                const uint32_t sb = p_slotb[p];
+                if (sb == 0) continue;
+                const uint32_t s = p_snd[p];
+                const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16);
+                u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
+                const uint64_t w0 = p_vb[p] >> 4;
+                const uint32_t wm = s_wmask[s];
+                for (uint32_t w = lane; w < sb / 16; w += 64) {
+                    u32x4 v = src[w];
+                    if (w == 0) v.x = slot_header(p_len[p]);
+                    ring[(w0 + w) & wm] = v;
+                }
+            }
+        }
+        // ---- advance per-sender / per-stream state ----
+        if (tid < (int)nsnd) {
+            const uint64_t t = c_tot[tid];
+            const uint32_t cnt = t & 1023;
+            if (cnt) {
+                for (int p = (int)n - 1; p >= 0; p--)
+                    if (p_snd[p] == tid && p_slotb[p] != 0) {
+                        // queue index of packet p = head + (#accepted of this sender before p)
+                        uint32_t r = 0;
+                        for (int q = 0; q < p; q++) r += (p_acc[q] && p_snd[q] == tid);
+                        s_lastnz[tid] = (int64_t)(s_head[tid] + r);
+                        break;
+                    }
+            }
+            s_head[tid] += cnt;
+            s_vcount[tid] += (uint32_t)((t >> 10) & 1023);
+            s_vbyte[tid] += t >> 20;
+        }
+        if (tid < (int)S.ntracks) s_count[tid] += c_ttot[tid];
+        __syncthreads();
+    }
+
+    if (tid < (int)nsnd) {
+        SenderDev& D = P.senders[S.first_sender + tid];
+        D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
+        D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
+    }
+    if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];
+    // block totals
+    uint64_t t1, t2;
+    const uint64_t a1 = block_exclusive_scan<uint64_t>(in_pk, scan64, t1);
+    const uint64_t a2 = block_exclusive_scan<uint64_t>(in_bytes, scan64, t2);
+    (void)a1; (void)a2;
+    if (tid == 0) {
+        atomicAdd(&P.totals->ingested_packets, (unsigned long long)t1);
+        atomicAdd(&P.totals->ingested_bytes, (unsigned long long)t2);
+    }
+}
+
+// =========================================================================================
+// Keyframe index + audio anchor: one wave per session segment.
+// =========================================================================================
+
+__global__ __launch_bounds__(64) void k_keyframe(KeyframeParams P) {
+    const uint32_t seg = blockIdx.x;
+    const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
+    const uint32_t sess = P.seg_sess[seg];
+    const SessionDev S = P.sessions[sess];
+    const int lane = threadIdx.x;
+    bool flag = S.video_key_flag != 0;
+    __shared__ int64_t s_key[kMaxSendersPerSession];
+    const uint32_t nsnd = 2 * S.ntracks;
+    if (lane < (int)nsnd) s_key[lane] = P.senders[S.first_sender + lane].key;
+    __syncthreads();
+    for (uint32_t base = b; base < e; base += 64) {
+        const uint32_t i = base + lane;
+        const uint32_t f = i < e ? P.pflags[i] : 0u;
+        const uint64_t idx = i < e ? P.pidx[i] : 0ull;
+        const uint64_t K = __ballot((f & 2u) != 0);
+        const uint64_t A = __ballot((f & 4u) != 0);
+        const uint64_t E = K | A;
+        const uint64_t below = (lane == 0) ? 0ull : (E & ((1ull << lane) - 1));
+        bool anchor = false;
+        if (f & 4u) {
+            if (below) {
+                const int j = 63 - __clzll((long long)below);
+                anchor = (K >> j) & 1ull;
+            } else {
+                anchor = flag;
+            }
+        }
+        uint64_t C = __ballot((f & 2u) != 0 || anchor);
+        // apply in arrival order: the latest match wins (Q5)
+        while (C) {
+            const int j = __ffsll((unsigned long long)C) - 1;
+            C &= C - 1;
+            const uint32_t fj = __shfl(f, j, 64);
+            const uint64_t ij = __shfl(idx, j, 64);
+            if (lane == 0) s_key[(fj >> 8) & 0xFF] = (int64_t)ij;
+        }
+        if (E) {
+            const int top = 63 - __clzll((long long)E);
+            flag = (K >> top) & 1ull;
+        }
+        __syncthreads();
+    }
+    if (lane < (int)nsnd) P.senders[S.first_sender + lane].key = s_key[lane];
+    if (lane == 0) P.sessions[sess].video_key_flag = flag ? 1u : 0u;
+}
+
+// =========================================================================================
+// Fan-out planning
+// =========================================================================================
+
+// First index in [lo, hi) whose meta satisfies pred (monotone false..true), hi if none.
+template <typename Pred>
+__device__ uint64_t lower_bound_meta(const PktMeta* meta, uint32_t mask, uint64_t lo, uint64_t hi, Pred pred) {
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (pred(meta[mid & mask])) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+// K1: per sender -- ring tail, fFirstPacketInQueueForNewOutput (ReflectorStream.cpp:1058-1069).
+__global__ void k_plan_senders(PlanParams P) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.T.nsenders) return;
+    SenderDev& D = P.senders[s];
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint64_t head = D.head;
+    const uint64_t pk_cap = (uint64_t)D.pk_mask + 1;
+    const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16;
+    uint64_t lo = head > pk_cap ? head - pk_cap : 0;
+    const uint64_t vend = D.vbyte_end;
+    // oldest packet whose slot is still intact in the byte ring
+    uint64_t tail = lower_bound_meta(meta, D.pk_mask, lo, head,
+                                     [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
+    D.tail = tail;
+    int64_t ns = -1;
+    if (D.key >= 0) {
+        ns = D.key;
+        if ((uint64_t)ns < tail) ns = -2;                      // key packet overwritten
+    } else if (head > tail) {
+        const int64_t cutoff = P.T.now - P.T.over_buffer_ms;  // now - arrival <= over buffer
+        const uint64_t f = lower_bound_meta(meta, D.pk_mask, tail, head,
+                                            [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        if (f < head) ns = (f == tail && tail > 0) ? -2 : (int64_t)f;   // -2: window exceeds ring
+    }
+    D.new_start = ns;
+    D.umin = head;
+    D.nchunks = 0;
+}
+
+// K2: per sub-stream -- this tick's range and the bookmark / last-id commit
+// (ReflectorStream.cpp:1092-1116; RTPSessionOutput.cpp:283-315, 624-639).
+__global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t bytes = 0;
+    uint32_t count = 0;
+    if (q < P.T.nsubs) {
+        SubDev& Q = P.subs[q];
+        Q.nonempty = 0; Q.count = 0; Q.bytes = 0;
+        if (Q.active) {
+            SenderDev& D = P.senders[Q.sender];
+            const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+            const uint64_t head = D.head;
+            bool have = false;
+            uint64_t a = 0;
+            if (Q.bookmark >= 0) {                     // GetBookMarkedPacket: resume after it
+                a = (uint64_t)Q.bookmark + 1;
+                have = true;
+                if (a < D.tail && a < head) { atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW); a = D.tail; }
+            } else if (D.new_start >= 0) {             // new output: key pointer / buffer start
+                a = (uint64_t)D.new_start;
+                have = true;
+                if (Q.has_last)                        // PacketAlreadySent for a re-joined output
+                    a = lower_bound_meta(meta, D.pk_mask, a, head,
+                                         [&](const PktMeta& m) { return m.id > Q.last_id; });
+            } else if (D.new_start == -2) {
+                atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW);
+            }
+            if (have) {
+                if (a < head) {
+                    const PktMeta m = meta[a & D.pk_mask];
+                    Q.a = a;
+                    Q.vstart = m.vbyte;
+                    Q.vcstart = m.vcount;
+                    bytes = D.vbyte_end - m.vbyte;
+                    count = D.vcount_end - m.vcount;
+                    Q.bytes = bytes;
+                    Q.count = count;
+                    Q.nonempty = 1;
+                    atomicMin((unsigned long long*)&D.umin, (unsigned long long)a);
+                }
+                // SendPacketsToOutput returns the newest visited packet; with sinks that never
+                // block NeedRelocateBookMark (Q9) cannot fire: the bookmark is the newest packet.
+                if (head > 0) Q.bookmark = (int64_t)(head - 1);
+                if (count > 0) {
+                    Q.last_id = meta[(uint64_t)D.last_nonzero & D.pk_mask].id;
+                    Q.has_last = 1;
+                }
+            }
+        }
+    }
+    // block partials for the output-offset scan
+    __shared__ uint64_t sb[4];
+    __shared__ uint32_t sc[4];
+    uint64_t tb; uint32_t tc;
+    (void)block_exclusive_scan<uint64_t>(bytes, sb, tb);
+    (void)block_exclusive_scan<uint32_t>(count, sc, tc);
+    if (threadIdx.x == 0) { P.blk_bytes[blockIdx.x] = tb; P.blk_count[blockIdx.x] = tc; }
+}
+
+// K3: single workgroup -- scans over K2 block partials and over senders' chunk counts.
+__global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
+    const int tid = threadIdx.x;
+    const int nt = blockDim.x;
+    __shared__ uint64_t sh64[1024];
+    __shared__ uint32_t sh32[1024];
+    // (a) block partial scan
+    {
+        const uint32_t n = P.T.nsub_blocks;
+        const uint32_t per = (n + nt - 1) / nt;
+        const uint32_t b0 = tid * per, b1 = min(n, b0 + per);
+        uint64_t sbytes = 0; uint32_t scount = 0;
+        for (uint32_t i = b0; i < b1; i++) { sbytes += P.blk_bytes[i]; scount += P.blk_count[i]; }
+        sh64[tid] = sbytes; sh32[tid] = scount;
+        __syncthreads();
+        for (int o = 1; o < nt; o <<= 1) {
+            uint64_t y = tid >= o ? sh64[tid - o] : 0; uint32_t z = tid >= o ? sh32[tid - o] : 0;
+            __syncthreads();
+            sh64[tid] += y; sh32[tid] += z;
+            __syncthreads();
+        }
+        uint64_t rb = sh64[tid] - sbytes; uint32_t rc = sh32[tid] - scount;
+        for (uint32_t i = b0; i < b1; i++) {
+            P.blk_bytes_base[i] = rb; P.blk_count_base[i] = rc;
+            rb += P.blk_bytes[i]; rc += P.blk_count[i];
+        }
+        if (tid == nt - 1) {
+            P.totals->arena_bytes = sh64[tid];
+            P.totals->relayed_packets = sh32[tid];
+            if (sh64[tid] > P.T.arena_bytes || sh32[tid] > P.T.max_desc)
+                atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
+        }
+        __syncthreads();
+    }
+    // (b) sender chunk scan
+    {
+        const uint32_t n = P.T.nsenders;
+        const uint32_t per = (n + nt - 1) / nt;
+        const uint32_t s0 = tid * per, s1 = min(n, s0 + per);
+        uint32_t sum = 0;
+        for (uint32_t s = s0; s < s1; s++) {
+            const SenderDev& D = P.senders[s];
+            const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
+            sum += (uint32_t)((span + kChunkPackets - 1) / kChunkPackets);
+        }
+        sh32[tid] = sum;
+        __syncthreads();
+        for (int o = 1; o < nt; o <<= 1) {
+            uint32_t z = tid >= o ? sh32[tid - o] : 0;
+            __syncthreads();
+            sh32[tid] += z;
+            __syncthreads();
+        }
+        uint32_t r = sh32[tid] - sum;
+        for (uint32_t s = s0; s < s1; s++) {
+            SenderDev& D = P.senders[s];
+            const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
+            const uint32_t k = (uint32_t)((span + kChunkPackets - 1) / kChunkPackets);
+            D.chunk_base = r; D.nchunks = k;
+            r += k;
+        }
+        if (tid == nt - 1) P.totals->nwork = sh32[tid];
+    }
+}
+
+// K3b: per sub-stream -- final arena / descriptor offsets and the public sub-stream table;
+// per sender -- work items.
+__global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t bytes = 0; uint32_t count = 0;
+    if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
+    __shared__ uint64_t sb[4];
+    __shared__ uint32_t sc[4];
+    uint64_t tb; uint32_t tc;
+    const uint64_t pb = block_exclusive_scan<uint64_t>(bytes, sb, tb);
+    const uint32_t pc = block_exclusive_scan<uint32_t>(count, sc, tc);
+    if (q < P.T.nsubs) {
+        SubDev& Q = P.subs[q];
+        Q.out_base = P.blk_bytes_base[blockIdx.x] + pb;
+        Q.desc_base = P.blk_count_base[blockIdx.x] + pc;
+        edgpu_substream_out o;
+        o.subscriber = Q.handle;
+        o.track = Q.track;
+        o.kind = Q.kind;
+        o.transport = Q.transport;
+        o.desc_base = Q.desc_base;
+        o.desc_count = Q.count;
+        o.out_base = Q.out_base;
+        o.out_bytes = Q.bytes;
+        P.sub_out[q] = o;
+    }
+    // work items: thread q doubles as sender q
+    if (q < P.T.nsenders) {
+        const SenderDev& D = P.senders[q];
+        for (uint32_t k = 0; k < D.nchunks; k++) P.work[D.chunk_base + k] = WorkItem{q, k};
+    }
+}
+
+// =========================================================================================
+// Fan-out: register-staged, write-many copy
+// =========================================================================================
+
+__global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
+    const uint32_t nwork = P.totals->nwork;
+    if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    __shared__ uint64_t m_vb[kChunkPackets + 1];
+    __shared__ uint64_t m_id[kChunkPackets];
+    __shared__ uint32_t m_len[kChunkPackets];
+    __shared__ uint32_t m_vc[kChunkPackets];
+    __shared__ uint32_t startmap[(kChunkWords + 31) / 32];
+    __shared__ unsigned long long s_wire[4];
+    unsigned long long wire = 0;
+
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const WorkItem it = P.work[w];
+        const SenderDev& D = P.senders[it.sender];
+        const uint64_t lo = D.umin + (uint64_t)it.chunk * kChunkPackets;
+        const uint64_t head = D.head;
+        const uint32_t np = (uint32_t)min((uint64_t)kChunkPackets, head - lo);
+        const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        if (tid < (int)np) {
+            const PktMeta m = meta[(lo + tid) & D.pk_mask];
+            m_vb[tid] = m.vbyte; m_id[tid] = m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
+        }
+        if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
+        for (int k = tid; k < (int)((kChunkWords + 31) / 32); k += kFanoutThreads) startmap[k] = 0;
+        __syncthreads();
+        const uint64_t vb0 = m_vb[0];
+        const uint32_t nwords = (uint32_t)((m_vb[np] - vb0) >> 4);
+        if (tid < (int)np && m_len[tid] != 0) {
+            const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
+            atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
+        }
+        __syncthreads();
+        // load the chunk once (HBM -> VGPRs)
+        const u32x4* ring = reinterpret_cast<const u32x4*>(D.ring);
+        const uint64_t rw0 = vb0 >> 4;
+        u32x4 r[kFanoutRegWords];
+        uint32_t smask = 0;
+#pragma unroll
+        for (int j = 0; j < (int)kFanoutRegWords; j++) {
+            const uint32_t wi = tid + j * kFanoutThreads;
+            if (wi < nwords) {
+                r[j] = ring[(rw0 + wi) & D.word_mask];
+                smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
+            }
+        }
+        // write it to every sub-stream of the sender
+        const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
+        for (uint32_t qi = qb; qi < qe; qi++) {
+            const SubDev& Q = P.subs[P.sub_index[qi]];
+            if (!Q.nonempty || Q.a >= lo + np) continue;
+            const uint64_t first = Q.a > lo ? Q.a : lo;
+            const uint32_t fw = (uint32_t)((m_vb[first - lo] - vb0) >> 4);
+            // arena word of chunk word 0 (may precede the sub-stream's region; only words
+            // >= fw are written)
+            const int64_t dw0 = (int64_t)(Q.out_base >> 4) + ((int64_t)(vb0 - Q.vstart) >> 4);
+            u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+            const uint32_t chbits = Q.transport ? ((uint32_t)Q.channel << 8) : 0u;
+#pragma unroll
+            for (int j = 0; j < (int)kFanoutRegWords; j++) {
+                const uint32_t wi = tid + j * kFanoutThreads;
+                if (wi >= fw && wi < nwords) {
+                    u32x4 v = r[j];
+                    if ((smask >> j) & 1u) v.x |= chbits;
+                    __builtin_nontemporal_store(v, &out[dw0 + wi]);
+                }
+            }
+            // descriptors for this sub-stream's packets in the chunk
+            const uint32_t p0 = (uint32_t)(first - lo);
+            if (tid >= (int)p0 && tid < (int)np && m_len[tid] != 0) {
+                const uint32_t len = m_len[tid];
+                const uint64_t off = Q.out_base + (m_vb[tid] - Q.vstart) + (Q.transport ? 0 : 4);
+                const uint32_t wlen = len + (Q.transport ? 4 : 0);
+                const uint32_t di = Q.desc_base + (m_vc[tid] - Q.vcstart);
+                u32x4 dv;
+                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = (uint32_t)m_id[tid];
+                __builtin_nontemporal_store(dv, reinterpret_cast<u32x4*>(P.desc) + di);
+                wire += wlen;
+            }
+        }
+        __syncthreads();
+    }
+    unsigned long long tot;
+    (void)block_exclusive_scan<unsigned long long>(wire, s_wire, tot);
+    if (tid == 0 && tot) atomicAdd(&P.totals->relayed_bytes, tot);
+}
+
+}  // namespace edgpu
+
+// ---------------------------------------------------------------------------------------
+// Launch wrappers (internal C++ API used by edgpu_engine.cpp)
+namespace edgpu {
+
+hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ingest, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    return hipGetLastError();
+}
+hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_keyframe, dim3(nseg), dim3(64), 0, st, p);
+    return hipGetLastError();
+}
+hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
+    const uint32_t nsb = p.T.nsenders ? (p.T.nsenders + 255) / 256 : 0;
+    if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3(nsb), dim3(256), 0, st, p);
+    if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, p);
+    const uint32_t nfb = max(p.T.nsub_blocks, nsb);
+    if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+hipError_t launch_fanout(const FanoutParams& p, uint32_t grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_fanout, dim3(grid), dim3(kFanoutThreads), 0, st, p);
+    return hipGetLastError();
+}
+int fanout_occupancy() {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_fanout, kFanoutThreads, 0) != hipSuccess) return 4;
+    return blocks > 0 ? blocks : 1;
+}
+
+}  // namespace edgpu

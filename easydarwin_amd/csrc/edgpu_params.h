@@ -1,0 +1,58 @@
+// edgpu_params.h -- kernel argument blocks (shared by edgpu_kernels.hip and edgpu_engine.cpp).
+#pragma once
+#include <stdint.h>
+#include "edgpu.h"
+#include "edgpu_device.h"
+
+namespace edgpu {
+
+struct IngestParams {
+    const edgpu_pkt_desc* desc;
+    const uint32_t* seg_off;
+    const uint32_t* seg_sess;
+    const uint8_t* blob;
+    SessionDev* sessions;
+    SenderDev* senders;
+    StreamDev* streams;
+    uint32_t* pflags;       // per desc: bit0 enqueued, bit1 video key, bit2 audio event, bits 8-15 local sender
+    uint64_t* pidx;         // per desc: sender queue index
+    uint32_t filter_ssrc;
+    uint32_t ssrc_timeout_s;
+    TickTotals* totals;
+};
+
+struct KeyframeParams {
+    const uint32_t* seg_off;
+    const uint32_t* seg_sess;
+    const uint32_t* pflags;
+    const uint64_t* pidx;
+    SessionDev* sessions;
+    SenderDev* senders;
+};
+
+struct PlanParams {
+    SenderDev* senders;
+    SubDev* subs;
+    const uint32_t* sub_index;
+    edgpu_substream_out* sub_out;
+    WorkItem* work;
+    uint64_t* blk_bytes;        // per K2 block partials
+    uint32_t* blk_count;
+    uint64_t* blk_bytes_base;
+    uint32_t* blk_count_base;
+    TickTotals* totals;
+    TickParams T;
+};
+
+struct FanoutParams {
+    const SenderDev* senders;
+    const uint32_t* sub_range;  // per sender [begin, end) into sub_index
+    const SubDev* subs;
+    const uint32_t* sub_index;
+    const WorkItem* work;
+    uint8_t* arena;
+    edgpu_out_desc* desc;
+    TickTotals* totals;
+};
+
+}  // namespace edgpu

@@ -1,0 +1,272 @@
+"""ctypes binding of libedgpu.so (include/edgpu.h) -- the host-side mirror of the reflector's
+module interface for this path.
+
+There is no CPU fallback: if the HIP extension is missing or no gfx950 device is visible the
+calls raise.  ``EdgpuError`` carries the QTSS_Error-compatible status code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libedgpu.so")
+
+OK, ERR, BAD_ARGUMENT, WOULD_BLOCK = 0, -1, -10, -14
+NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW = -101, -102, -103, -104
+TRANSPORT_UDP, TRANSPORT_TCP = 0, 1
+PTR_HOST, PTR_DEVICE = 0, 1
+FALSE = 0xFFFFFFFF
+
+EXPORTED = [
+    "edgpu_version", "edgpu_last_error", "edgpu_config_default", "edgpu_ctx_create",
+    "edgpu_ctx_destroy", "edgpu_sync", "edgpu_session_add", "edgpu_session_tracks",
+    "edgpu_subscriber_add", "edgpu_subscriber_remove", "edgpu_ingest", "edgpu_keyframe_index",
+    "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
+    "edgpu_gop_span",
+]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("reflector_buffer_size_sec", C.c_uint32),
+        ("rtp_reflector_threshold_msec", C.c_uint32),
+        ("timeout_stream_SSRC_secs", C.c_uint32),
+        ("use_one_SSRC_per_stream", C.c_uint32),
+        ("video_ring_packets", C.c_uint32),
+        ("video_ring_bytes", C.c_uint64),
+        ("other_ring_packets", C.c_uint32),
+        ("other_ring_bytes", C.c_uint64),
+        ("out_arena_bytes", C.c_uint64),
+        ("max_out_packets", C.c_uint32),
+        ("max_batch_packets", C.c_uint32),
+        ("max_batch_bytes", C.c_uint64),
+    ]
+
+
+class PktDesc(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("len", C.c_uint16), ("channel", C.c_uint8),
+                ("flags", C.c_uint8), ("arrival_ms", C.c_int64)]
+
+
+class OutDesc(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("len", C.c_uint32), ("packet_id", C.c_uint32)]
+
+
+class SubstreamOut(C.Structure):
+    _fields_ = [("subscriber", C.c_uint32), ("track", C.c_uint16), ("kind", C.c_uint8),
+                ("transport", C.c_uint8), ("desc_base", C.c_uint32), ("desc_count", C.c_uint32),
+                ("out_base", C.c_uint64), ("out_bytes", C.c_uint64)]
+
+
+class FanoutResult(C.Structure):
+    _fields_ = [("arena", C.c_void_p), ("desc", C.c_void_p), ("substreams", C.c_void_p),
+                ("n_substreams", C.c_uint32)]
+
+
+class TickStats(C.Structure):
+    _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
+                ("arena_bytes", C.c_uint64), ("ingested_packets", C.c_uint64),
+                ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32)]
+
+
+# numpy mirrors (same layout as the C structs)
+PKT_DTYPE = np.dtype([("slot", "<u4"), ("len", "<u2"), ("channel", "u1"), ("flags", "u1"),
+                      ("arrival_ms", "<i8")])
+OUT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("packet_id", "<u4")])
+SUB_DTYPE = np.dtype([("subscriber", "<u4"), ("track", "<u2"), ("kind", "u1"), ("transport", "u1"),
+                      ("desc_base", "<u4"), ("desc_count", "<u4"), ("out_base", "<u8"),
+                      ("out_bytes", "<u8")])
+assert PKT_DTYPE.itemsize == C.sizeof(PktDesc) == 16
+assert OUT_DTYPE.itemsize == C.sizeof(OutDesc) == 16
+assert SUB_DTYPE.itemsize == C.sizeof(SubstreamOut) == 32
+
+
+class EdgpuError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"edgpu error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libedgpu.so.  Raises (loudly) when the extension has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} missing: build it with `make -C easydarwin_amd/csrc` "
+                                "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(path)
+    P, U32, U64, I32, I64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_int64
+    sig = {
+        "edgpu_version": (C.c_char_p, []),
+        "edgpu_last_error": (C.c_char_p, []),
+        "edgpu_config_default": (None, [C.POINTER(Config)]),
+        "edgpu_ctx_create": (I32, [C.POINTER(Config), C.POINTER(P)]),
+        "edgpu_ctx_destroy": (I32, [P]),
+        "edgpu_sync": (I32, [P]),
+        "edgpu_session_add": (I32, [P, C.c_char_p, U32, I32, C.POINTER(U32)]),
+        "edgpu_session_tracks": (I32, [P, U32, C.POINTER(U32)]),
+        "edgpu_subscriber_add": (I32, [P, U32, I32, C.POINTER(U32)]),
+        "edgpu_subscriber_remove": (I32, [P, U32]),
+        "edgpu_ingest": (I32, [P, P, U32, P, P, U32, P, U64, I32]),
+        "edgpu_keyframe_index": (I32, [P]),
+        "edgpu_fanout": (I32, [P, I64, C.POINTER(FanoutResult)]),
+        "edgpu_tick_stats_get": (I32, [P, C.POINTER(TickStats)]),
+        "edgpu_copy_to_host": (I32, [P, P, P, U64]),
+        "edgpu_last_timings": (I32, [P, C.POINTER(C.c_float)]),
+        "edgpu_gop_span": (I32, [P, U32, U32, C.POINTER(U64), C.POINTER(U64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != OK:
+        raise EdgpuError(rc, _lib.edgpu_last_error().decode(errors="replace"))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One engine context (one GPU).  Mirrors the module-side calls of the reflector."""
+
+    def __init__(self, device: int = 0, **cfg):
+        lib = load()
+        c = Config()
+        lib.edgpu_config_default(C.byref(c))
+        c.device = device
+        for k, v in cfg.items():
+            setattr(c, k, v)
+        h = C.c_void_p()
+        _check(lib.edgpu_ctx_create(C.byref(c), C.byref(h)))
+        self.h = h
+        self.lib = lib
+
+    def close(self):
+        if self.h:
+            _check(self.lib.edgpu_ctx_destroy(self.h))
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def session_add(self, sdp: str, udp_push: bool = False) -> int:
+        b = sdp.encode()
+        out = C.c_uint32()
+        _check(self.lib.edgpu_session_add(self.h, b, len(b), int(udp_push), C.byref(out)))
+        return out.value
+
+    def session_tracks(self, session: int) -> int:
+        out = C.c_uint32()
+        _check(self.lib.edgpu_session_tracks(self.h, session, C.byref(out)))
+        return out.value
+
+    def subscriber_add(self, session: int, transport: int = TRANSPORT_UDP) -> int:
+        out = C.c_uint32()
+        _check(self.lib.edgpu_subscriber_add(self.h, session, transport, C.byref(out)))
+        return out.value
+
+    def subscriber_remove(self, handle: int):
+        _check(self.lib.edgpu_subscriber_remove(self.h, handle))
+
+    def ingest_host(self, desc: np.ndarray, seg_off: np.ndarray, seg_sess: np.ndarray, blob: np.ndarray):
+        desc = np.ascontiguousarray(desc, dtype=PKT_DTYPE)
+        seg_off = np.ascontiguousarray(seg_off, dtype=np.uint32)
+        seg_sess = np.ascontiguousarray(seg_sess, dtype=np.uint32)
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        _check(self.lib.edgpu_ingest(self.h, _ptr(desc), len(desc), _ptr(seg_off), _ptr(seg_sess),
+                                     len(seg_sess), _ptr(blob), blob.nbytes, PTR_HOST))
+
+    def ingest_device(self, desc_ptr: int, n: int, seg_ptr: int, seg_sess_ptr: int, nseg: int,
+                      blob_ptr: int, blob_bytes: int):
+        _check(self.lib.edgpu_ingest(self.h, C.c_void_p(desc_ptr), n, C.c_void_p(seg_ptr),
+                                     C.c_void_p(seg_sess_ptr), nseg, C.c_void_p(blob_ptr),
+                                     blob_bytes, PTR_DEVICE))
+
+    def keyframe_index(self):
+        _check(self.lib.edgpu_keyframe_index(self.h))
+
+    def fanout(self, now_ms: int) -> FanoutResult:
+        r = FanoutResult()
+        _check(self.lib.edgpu_fanout(self.h, int(now_ms), C.byref(r)))
+        return r
+
+    def stats(self) -> TickStats:
+        s = TickStats()
+        _check(self.lib.edgpu_tick_stats_get(self.h, C.byref(s)))
+        return s
+
+    def sync(self):
+        _check(self.lib.edgpu_sync(self.h))
+
+    def timings(self):
+        a = (C.c_float * 4)()
+        _check(self.lib.edgpu_last_timings(self.h, a))
+        return {"fanout_ms": a[0], "tick_ms": a[1], "ingest_ms": a[2], "keyframe_ms": a[3]}
+
+    def gop_span(self, session: int, track: int):
+        p, b = C.c_uint64(), C.c_uint64()
+        _check(self.lib.edgpu_gop_span(self.h, session, track, C.byref(p), C.byref(b)))
+        return p.value, b.value
+
+    def copy_to_host(self, dev_ptr, nbytes: int) -> np.ndarray:
+        out = np.empty(int(nbytes), dtype=np.uint8)
+        if nbytes:
+            _check(self.lib.edgpu_copy_to_host(self.h, _ptr(out), C.c_void_p(dev_ptr), int(nbytes)))
+        return out
+
+    def read_tick(self, r: FanoutResult):
+        """(stats, substream table, descriptors, arena) of the last fan-out, on the host."""
+        st = self.stats()
+        if st.status != OK:
+            raise EdgpuError(st.status, "device-side status after fan-out")
+        subs = self.copy_to_host(r.substreams, r.n_substreams * SUB_DTYPE.itemsize).view(SUB_DTYPE)
+        desc = self.copy_to_host(r.desc, st.relayed_packets * OUT_DTYPE.itemsize).view(OUT_DTYPE)
+        arena = self.copy_to_host(r.arena, st.arena_bytes)
+        return st, subs, desc, arena
+
+
+def build_batch(pkts):
+    """Host-side batch builder: ``pkts`` is a list of (session, channel, arrival_ms, bytes) in
+    arrival order.  Groups them by session (stable) into the edgpu_ingest layout: 16-B
+    slots with the packet 4 bytes in, a descriptor per packet, per-session segments."""
+    order = sorted(range(len(pkts)), key=lambda i: (pkts[i][0], i))
+    n = len(pkts)
+    desc = np.zeros(n, dtype=PKT_DTYPE)
+    sizes = [((min(len(pkts[i][3]), 65535) + 4 + 15) // 16) * 16 for i in order]
+    total = int(sum(sizes))
+    blob = np.zeros(max(total, 16), dtype=np.uint8)
+    seg_off, seg_sess = [0], []
+    off = 0
+    last = None
+    for k, i in enumerate(order):
+        s, ch, t, data = pkts[i]
+        data = data[:65535]
+        if s != last:
+            if last is not None:
+                seg_off.append(k)
+            seg_sess.append(s)
+            last = s
+        desc[k] = (off // 16, len(data), ch, 0, t)
+        blob[off + 4:off + 4 + len(data)] = np.frombuffer(data, dtype=np.uint8)
+        off += sizes[k]
+    seg_off.append(n)
+    if n == 0:
+        seg_off = [0]
+    return desc, np.array(seg_off, dtype=np.uint32), np.array(seg_sess, dtype=np.uint32), blob

@@ -1,0 +1,87 @@
+"""Replays an event trace (easydarwin_amd/trace.py) through the GPU engine and returns the
+capture in the same format the reference harness and the CPU restatement write, so parity
+is a byte comparison.
+
+Batch semantics: all PKT events since the previous TICK form one ``edgpu_ingest`` batch
+(grouped by session, arrival order kept), followed by ``edgpu_keyframe_index``; JOINs since
+the previous TICK become ``edgpu_subscriber_add``; the TICK itself is ``edgpu_fanout(now)``.
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+from . import edgpu
+from .trace import JOIN, PKT, TICK, Trace
+
+
+def _wire_images(subs, desc, arena, images):
+    for s in subs:
+        n = int(s["desc_count"])
+        if n == 0:
+            continue
+        key = (int(s["subscriber"]), int(s["track"]), int(s["kind"]))
+        d = desc[int(s["desc_base"]):int(s["desc_base"]) + n]
+        tcp = int(s["transport"]) == edgpu.TRANSPORT_TCP
+        parts = images[key]
+        for off, ln in zip(d["offset"].tolist(), d["len"].tolist()):
+            if tcp:
+                parts.append(arena[off:off + ln].tobytes())
+            else:
+                parts.append(struct.pack(">H", ln) + arena[off:off + ln].tobytes())
+
+
+def replay(trace: Trace, ctx: edgpu.Context | None = None, **cfg):
+    """Returns (capture_bytes, per-tick stats list)."""
+    own = ctx is None
+    if own:
+        ctx = edgpu.Context(**cfg)
+    try:
+        sess_tracks = []
+        for sdp in trace.sdps:
+            sid = ctx.session_add(sdp)
+            assert sid == len(sess_tracks)
+            sess_tracks.append(ctx.session_tracks(sid))
+        subs_meta = {}          # handle -> (sub_id, session, tcp)
+        images = {}
+        pending, joins, stats = [], [], []
+        for ev in trace.events:
+            if ev[0] == PKT:
+                _, t, s, ch, data = ev
+                pending.append((s, ch, t, data))
+            elif ev[0] == JOIN:
+                joins.append(ev)
+            elif ev[0] == TICK:
+                t = ev[1]
+                if pending:
+                    desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
+                    ctx.ingest_host(desc, seg_off, seg_sess, blob)
+                    ctx.keyframe_index()
+                    pending = []
+                for (_, jt, s, sub_id, transport, _ua) in joins:
+                    h = ctx.subscriber_add(s, edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP)
+                    subs_meta[h] = (sub_id, s, transport)
+                    for tr in range(sess_tracks[s]):
+                        for k in (0, 1):
+                            images[(h, tr, k)] = []
+                joins = []
+                r = ctx.fanout(t)
+                st, subs, desc, arena = ctx.read_tick(r)
+                stats.append((t, st.relayed_packets, st.relayed_bytes))
+                _wire_images(subs, desc, arena, images)
+        # capture: one record per (subscriber, track, kind), sorted by subscriber id
+        recs = []
+        for (h, tr, k), parts in images.items():
+            sub_id, s, transport = subs_meta[h]
+            recs.append((sub_id, s, tr, k, transport, parts))
+        recs.sort(key=lambda r: (r[0], r[2], r[3]))
+        out = [b"EDCP", struct.pack("<I", len(recs))]
+        for sub_id, s, tr, k, transport, parts in recs:
+            data = b"".join(parts)
+            out.append(struct.pack("<IIHBBQQ", sub_id, s, tr, k, transport, len(parts), len(data)))
+            out.append(data)
+        return b"".join(out), stats
+    finally:
+        if own:
+            ctx.close()

@@ -1,0 +1,193 @@
+/*
+ * edgpu.h -- C ABI of the MI355X-native batched RTP relay engine (libedgpu.so).
+ *
+ * The engine replaces EasyDarwin's reflector hot path behind the QTSSReflectorModule
+ * plugin boundary.  Each entry point names the reference interface it stands in for
+ * (paths relative to the EasyDarwin reference tree):
+ *
+ *   edgpu_session_add      ReflectorSession::SetupReflectorSession
+ *                          (APIModules/QTSSReflectorModule/ReflectorSession.cpp:140-188) with the
+ *                          SDP parse of SDPSourceInfo (APICommonCode/SDPSourceInfo.cpp:259-353)
+ *   edgpu_subscriber_add   RTPSessionOutput ctor + ReflectorSession::AddOutput
+ *                          (RTPSessionOutput.cpp:73-88, ReflectorSession.cpp:209-253),
+ *                          i.e. QTSSReflectorModule DoSetup/DoPlay for a player
+ *                          (QTSSReflectorModule.cpp:1610-1622, 1942-1946)
+ *   edgpu_subscriber_remove ReflectorSession::RemoveOutput (ReflectorSession.cpp:255-279)
+ *   edgpu_ingest           ReflectorStream::PushPacket + ReflectorSocket::ProcessPacket
+ *                          (ReflectorStream.cpp:529-576, 1769-2010), called per packet by
+ *                          ProcessRTPData (QTSSReflectorModule.cpp:604-678)
+ *   edgpu_keyframe_index   the keyframe index update + audio anchor inside ProcessPacket
+ *                          (ReflectorStream.cpp:1876-1934, IsKeyFrameFirstPacket :1403-1513)
+ *   edgpu_fanout           ReflectorSender::ReflectPackets / SendPacketsToOutput /
+ *                          RTPSessionOutput::WritePacket and the egress framing of
+ *                          RTPStream::Write (ReflectorStream.cpp:1024-1198,
+ *                          RTPSessionOutput.cpp:564-662, Server.tproj/RTPStream.cpp:1084-1147,
+ *                          RTSPSessionInterface.cpp:329-344), for every sender at once
+ *
+ * Conventions
+ *   - Every function returns an int status using QTSS_Error values (QTSS.h:61-76):
+ *     EDGPU_OK = QTSS_NoErr, EDGPU_ERR = QTSS_RequestFailed, EDGPU_BAD_ARGUMENT =
+ *     QTSS_BadArgument, EDGPU_WOULD_BLOCK = QTSS_WouldBlock, plus engine-specific codes
+ *     below -100 (capacity / device errors).  edgpu_last_error() gives a message.
+ *   - One context per GPU.  Calls on a context are externally serialised (the reference's
+ *     per-stream fBucketMutex); contexts on different GPUs run concurrently.
+ *   - All device work runs on the context's HIP stream and is asynchronous unless stated.
+ *     Pointers flagged EDGPU_PTR_DEVICE must stay valid until edgpu_sync() returns.
+ *   - No torch or HIP types in the ABI: plain pointers and sizes.
+ */
+#ifndef EDGPU_H
+#define EDGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (QTSS_Error-compatible where a reference counterpart exists) */
+#define EDGPU_OK                 0
+#define EDGPU_ERR               -1     /* QTSS_RequestFailed  */
+#define EDGPU_BAD_ARGUMENT     -10     /* QTSS_BadArgument    */
+#define EDGPU_WOULD_BLOCK      -14     /* QTSS_WouldBlock     */
+#define EDGPU_NOT_CONNECTED    -15     /* QTSS_NotConnected   */
+#define EDGPU_NO_DEVICE       -101     /* no usable gfx950 device / HIP failure */
+#define EDGPU_OUT_OF_MEMORY   -102
+#define EDGPU_RING_OVERFLOW   -103     /* a needed packet fell out of a sender ring */
+#define EDGPU_OUT_OVERFLOW    -104     /* fan-out arena too small for this tick */
+
+/* transport of a subscriber (qtssRTPTransportType, QTSS.h:219-221) */
+#define EDGPU_TRANSPORT_UDP      0
+#define EDGPU_TRANSPORT_TCP      1     /* RTSP-interleaved '$' framing */
+
+/* pointer-location flags for edgpu_ingest */
+#define EDGPU_PTR_HOST           0     /* engine stages through pinned memory */
+#define EDGPU_PTR_DEVICE         1     /* already resident in HBM on the ctx device */
+
+/* Engine configuration.  Reflector prefs keep the reference's XML key names
+ * (WinNTSupport/easydarwin.xml:131-163, read at ReflectorStream.cpp:87-117 and
+ * QTSSReflectorModule.cpp:450-586); 0 selects the reference default. */
+typedef struct edgpu_config {
+    int32_t  device;                        /* HIP device ordinal */
+    uint32_t reflector_buffer_size_sec;     /* default 1  -> 1000 ms new-client window */
+    uint32_t rtp_reflector_threshold_msec;  /* default 2000, floor 1000 (relocation)   */
+    uint32_t timeout_stream_SSRC_secs;      /* default 30                               */
+    uint32_t use_one_SSRC_per_stream;       /* default 1 (0 = keep every SSRC) -- pass
+                                               EDGPU_FALSE to disable                   */
+    /* capacities (0 = default) */
+    uint32_t video_ring_packets;            /* per video RTP sender, power of two (8192)  */
+    uint64_t video_ring_bytes;              /* per video RTP sender, power of two (8 MiB) */
+    uint32_t other_ring_packets;            /* audio/RTCP/other senders (2048)           */
+    uint64_t other_ring_bytes;              /* (1 MiB)                                   */
+    uint64_t out_arena_bytes;               /* fan-out output arena per tick (256 MiB)   */
+    uint32_t max_out_packets;               /* descriptor capacity per tick (1 Mi)       */
+    uint32_t max_batch_packets;             /* ingest batch capacity (1 Mi)              */
+    uint64_t max_batch_bytes;               /* ingest blob capacity (1 GiB)              */
+} edgpu_config;
+#define EDGPU_FALSE 0xFFFFFFFFu
+
+/* One ingested packet.  The batch blob is a sequence of 16-byte-aligned slots; a packet's
+ * bytes start 4 bytes into its slot (the 4 bytes before it are the RTSP-interleaved header
+ * slot the engine rewrites), so `slot` is the slot's offset / 16.  Packets of one session
+ * must be contiguous and in arrival order (a pusher's TCP connection delivers exactly that);
+ * `seg_offsets` (n_segments + 1 entries) splits the descriptor array into per-session
+ * segments and `seg_session` names each segment's session.  A session appears in at most
+ * one segment per batch. */
+typedef struct edgpu_pkt_desc {
+    uint32_t slot;          /* blob byte offset / 16 */
+    uint16_t len;           /* packet length as received (clamped to 2060 at ingest, Q11) */
+    uint8_t  channel;       /* interleaved channel: 2*track + is_rtcp */
+    uint8_t  flags;         /* reserved, 0 */
+    int64_t  arrival_ms;    /* OS::Milliseconds() when the packet was pushed */
+} edgpu_pkt_desc;
+
+/* One send-ready output packet (16 bytes).  `offset` is the byte offset in the output
+ * arena of the bytes to put on the wire: the UDP datagram, or the '$' ch BE16(len) frame
+ * for an RTSP-interleaved subscriber. */
+typedef struct edgpu_out_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint32_t packet_id;     /* low 32 bits of fStreamCountID */
+} edgpu_out_desc;
+
+/* One sub-stream (subscriber x track x RTP|RTCP) of a fan-out tick, in subscriber-handle,
+ * track, kind order.  Its packets are desc[desc_base .. desc_base + desc_count). */
+typedef struct edgpu_substream_out {
+    uint32_t subscriber;    /* handle from edgpu_subscriber_add */
+    uint16_t track;
+    uint8_t  kind;          /* 0 RTP, 1 RTCP */
+    uint8_t  transport;     /* EDGPU_TRANSPORT_* */
+    uint32_t desc_base;
+    uint32_t desc_count;
+    uint64_t out_base;      /* arena offset of the first slot */
+    uint64_t out_bytes;     /* arena bytes spanned (slot-padded) */
+} edgpu_substream_out;
+
+/* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout. */
+typedef struct edgpu_fanout_result {
+    const uint8_t*              arena;          /* device */
+    const edgpu_out_desc*       desc;           /* device */
+    const edgpu_substream_out*  substreams;     /* device */
+    uint32_t                    n_substreams;
+} edgpu_fanout_result;
+
+/* Per-tick totals, read back by edgpu_tick_stats_get (which syncs). */
+typedef struct edgpu_tick_stats {
+    uint64_t relayed_packets;   /* IncrementTotalPackets semantics (RTPStream.cpp:1213-1216) */
+    uint64_t relayed_bytes;     /* wire bytes incl. '$' framing */
+    uint64_t arena_bytes;
+    uint64_t ingested_packets;  /* last ingest batch */
+    uint64_t ingested_bytes;
+    int32_t  status;            /* sticky device-side error (EDGPU_RING_OVERFLOW, ...) */
+    uint32_t _pad;
+} edgpu_tick_stats;
+
+typedef struct edgpu_ctx edgpu_ctx;
+
+const char* edgpu_version(void);
+const char* edgpu_last_error(void);
+void        edgpu_config_default(edgpu_config* cfg);
+
+int  edgpu_ctx_create(const edgpu_config* cfg, edgpu_ctx** out);
+int  edgpu_ctx_destroy(edgpu_ctx* ctx);
+int  edgpu_sync(edgpu_ctx* ctx);
+
+/* Push sessions.  `udp_push` = 0 for an RTSP-interleaved (TCP) push, 1 for UDP push
+ * (then the RTCP socket is bound on an odd port and only SRs are accepted, Q12/Q14). */
+int  edgpu_session_add(edgpu_ctx* ctx, const char* sdp, uint32_t sdp_len, int udp_push,
+                       uint32_t* out_session);
+int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks);
+
+/* Subscribers: a join takes effect at the next edgpu_fanout, like a new output being
+ * picked up by the next ReflectPackets. */
+int  edgpu_subscriber_add(edgpu_ctx* ctx, uint32_t session, int transport,
+                          uint32_t* out_handle);
+int  edgpu_subscriber_remove(edgpu_ctx* ctx, uint32_t handle);
+
+int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets,
+                  const uint32_t* seg_offsets, const uint32_t* seg_session,
+                  uint32_t n_segments, const uint8_t* blob, uint64_t blob_bytes,
+                  int ptr_location);
+int  edgpu_keyframe_index(edgpu_ctx* ctx);
+int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
+
+int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
+
+/* Copies device memory of this context to the host (synchronous).  Convenience for hosts
+ * and tests that read fan-out results. */
+int  edgpu_copy_to_host(edgpu_ctx* ctx, void* dst, const void* device_src, uint64_t bytes);
+
+/* Device-side timing of the last edgpu_fanout's kernels (HIP events on the ctx stream),
+ * in milliseconds: [0] fan-out copy kernel, [1] whole fan-out (plan + copy),
+ * [2] ingest, [3] keyframe index. */
+int  edgpu_last_timings(edgpu_ctx* ctx, float out_ms[4]);
+
+/* Keyframe fast start: bytes a joining subscriber of `session`/`track` would receive now
+ * (key pointer -> newest), cf. CKeyFrameCache (CommonUtilitiesLib/keyframecache.h:14-72). */
+int  edgpu_gop_span(edgpu_ctx* ctx, uint32_t session, uint32_t track,
+                    uint64_t* out_packets, uint64_t* out_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDGPU_H */

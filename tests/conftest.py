@@ -1,0 +1,23 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and libedgpu.so")
+
+
+@pytest.fixture(scope="session")
+def oracle_bins():
+    """Builds (here) or reuses (GPU box) the oracle binaries."""
+    port = os.path.join(ROOT, "oracle", "relay_model")
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(port) or os.path.exists("/root/reference/EasyDarwin"):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return {"port": port, "ref": ref if os.path.exists(ref) else None}
