@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Relay benchmark: relayed RTP packets/s (whole node) + achieved HBM GB/s, 1080p H.264 fan-out.
+
+One *step* = one pass of the hot path over one batch (one 1-s tick of synthetic input):
+``edgpu_ingest`` + ``edgpu_keyframe_index`` + ``edgpu_fanout`` for every session of this
+rank.  At N=1 the workload is BASELINE.json configs[1] (C2: 1024 H.264 1080p30 4 Mb/s
+streams x 16 UDP subscribers on one MI355X).  With N ranks the global session set is
+N x 1024 streams sharded by FNV-1a(stream ID) with no collective on the data path (weak
+scaling); ``--subs 64`` gives the C3 per-GPU shape.
+
+All W+K input batches are generated and made resident in HBM before timing.  Launch::
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from easydarwin_amd import edgpu  # noqa: E402
+from easydarwin_amd.workload import H264Fleet, shard_sessions  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_batch_on_device(b: dict, dev: torch.device, gen: torch.Generator):
+    """Materialise one batch in HBM: random payload bytes + the synthetic RTP/FU headers."""
+    n = b["n"]
+    slot_bytes = b["slot_bytes"]
+    slot_off = np.concatenate([[0], np.cumsum(slot_bytes)[:-1]])
+    total = int(slot_bytes.sum())
+    blob = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)
+    words = blob.view(-1, 16)
+    widx = torch.from_numpy(slot_off // 16).to(dev)
+    words[widx] = torch.from_numpy(b["hdr"]).to(dev)
+    # bytes 16..17 of the slot: packet bytes 12..13 (FU indicator/header or NAL bytes)
+    fu_pos = torch.from_numpy(slot_off + 16).to(dev)
+    blob[fu_pos] = torch.from_numpy(np.ascontiguousarray(b["fu"][:, 0])).to(dev)
+    blob[fu_pos + 1] = torch.from_numpy(np.ascontiguousarray(b["fu"][:, 1])).to(dev)
+    desc = np.zeros(n, dtype=edgpu.PKT_DTYPE)
+    desc["slot"] = slot_off // 16
+    desc["len"] = b["len"]
+    desc["channel"] = b["channel"]
+    desc["arrival_ms"] = b["arrival"]
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_seg = torch.from_numpy(b["seg_off"].astype(np.uint32).view(np.int32)).to(dev)
+    nseg = len(b["seg_off"]) - 1
+    d_sess = torch.arange(nseg, dtype=torch.int32, device=dev)
+    return {"desc": d_desc, "seg": d_seg, "sess": d_sess, "blob": blob, "n": n, "nseg": nseg,
+            "bytes": total, "t": b["t_end"], "in_bytes": int(b["len"].astype(np.int64).sum())}
+
+
+def run_step(ctx: edgpu.Context, bt: dict):
+    ctx.ingest_device(bt["desc"].data_ptr(), bt["n"], bt["seg"].data_ptr(), bt["sess"].data_ptr(),
+                      bt["nseg"], bt["blob"].data_ptr(), bt["bytes"])
+    ctx.keyframe_index()
+    ctx.fanout(bt["t"])
+
+
+def cpu_baseline(args) -> dict | None:
+    """The CPU restatement (oracle/relay_model, memcpy sinks, sessions sharded over threads)
+    on a bounded sample of the same workload: 64 sessions x subs x 3 s at 100-ms ticks."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    exe = os.path.join(ROOT, "oracle", "relay_model")
+    if not os.path.exists(exe):
+        try:
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except Exception:
+            return None
+    if not os.path.exists(exe):
+        return None
+    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
+    from easydarwin_amd.trace import Trace, UDP
+    n_sess, dur = 64, 3000
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=4_000_000, gop=60, idr_bytes=120_000)]
+    tr = Trace()
+    per = []
+    for s in range(n_sess):
+        tr.add_session(make_sdp(tracks))
+        per.append(session_packets(tracks, dur, 0xEA5D + 1 + s, t0=(s * 7) % 33))
+    from scenarios import _assemble
+    joins = [(0, s, s * args.subs + k, UDP) for s in range(n_sess) for k in range(args.subs)]
+    _assemble(tr, per, 100, dur, joins)
+    threads = min(16, os.cpu_count() or 1)
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "cpu.edtr")
+        tr.write(p)
+        # calibrate the repeat count to ~15 s of CPU replay
+        probe = json.loads(subprocess.run([exe, "--bench", p, str(threads), "1"], capture_output=True,
+                                          text=True, check=True).stdout)
+        rep = int(max(1, min(400, 15.0 / max(probe["seconds"], 1e-3))))
+        out = subprocess.run([exe, "--bench", p, str(threads), str(rep)], capture_output=True, text=True,
+                             check=True).stdout
+    r = json.loads(out)
+    return {"value": round(r["packets_per_s"], 1), "unit": "relayed RTP packets/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{rep} replays of {n_sess} H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x {dur/1000:.0f} s, "
+                      f"100-ms ticks, ingest+fan-out, memcpy sinks (oracle/relay_model --bench); "
+                      f"{r['relayed_packets']} relayed packets in {r['seconds']:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sessions", type=int, default=1024, help="sessions per GPU")
+    ap.add_argument("--subs", type=int, default=16, help="UDP subscribers per session")
+    ap.add_argument("--tick-ms", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    gids = shard_sessions(args.sessions * world, rank, world) if world > 1 else np.arange(args.sessions)
+    fleet = H264Fleet(gids, tick_ms=args.tick_ms)
+    steps, warm = args.steps, args.warmup
+    log(f"[bench] rank {rank}/{world}: {len(gids)} sessions x {args.subs} subs, generating {steps + warm} batches")
+    t_gen = time.time()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0xEA5D + rank)
+    batches = [make_batch_on_device(fleet.next_batch(), dev, gen) for _ in range(steps + warm)]
+    torch.cuda.synchronize(dev)
+    log(f"[bench] generated in {time.time() - t_gen:.1f}s; max batch {max(b['n'] for b in batches)} pkts, "
+        f"{max(b['bytes'] for b in batches) / 2**20:.0f} MiB")
+
+    # Output capacity per tick: every subscriber gets at most the packets of one batch (the
+    # first fan-out replays key pointer -> newest, which lies inside batch 0 at that point).
+    max_pk = max(b["n"] for b in batches)
+    max_out = int(max(b["n"] for b in batches) * args.subs * 1.05) + 1024
+    max_arena = int(max(b["bytes"] for b in batches) * args.subs * 1.05) // 16 * 16 + (1 << 20)
+    ctx = edgpu.Context(device=local, video_ring_packets=8192, video_ring_bytes=16 << 20,
+                        other_ring_packets=256, other_ring_bytes=64 << 10,
+                        out_arena_bytes=max_arena, max_out_packets=max_out,
+                        max_batch_packets=max_pk + 1, max_batch_bytes=1 << 20)
+    for _ in gids:
+        s = ctx.session_add(fleet.sdp())
+        for _k in range(args.subs):
+            ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+
+    for i in range(warm):
+        run_step(ctx, batches[i])
+    ctx.sync()
+    st = ctx.stats()
+    if st.status != 0:
+        raise SystemExit(f"engine status {st.status} after warmup")
+    ctx.kernel_times(0), ctx.kernel_times(1), ctx.kernel_times(2), ctx.kernel_times(3)
+    c0 = ctx.counters()
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(warm, warm + steps):
+        run_step(ctx, batches[i])
+    ctx.sync()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    c1 = ctx.counters()
+    st = ctx.stats()
+    if st.status != 0:
+        raise SystemExit(f"engine status {st.status}")
+    k_fan = ctx.kernel_times(0)
+    k_tick = ctx.kernel_times(1)
+    k_ing = ctx.kernel_times(2)
+    k_key = ctx.kernel_times(3)
+    relayed = c1["relayed_packets"] - c0["relayed_packets"]
+    out_bytes = c1["relayed_bytes"] - c0["relayed_bytes"]
+    in_bytes = c1["fanout_in_bytes"] - c0["fanout_in_bytes"]
+    launches = c1["fanout_launches"] - c0["fanout_launches"]
+    alg_bytes = out_bytes + in_bytes + 16 * relayed      # SURVEY.md §8.d per-launch definition
+
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tot = torch.tensor([relayed, out_bytes, in_bytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        relayed_all, out_all = int(tot[0].item()), int(tot[1].item())
+    else:
+        relayed_all, out_all = relayed, out_bytes
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    fan_ms = float(np.mean(k_fan)) if k_fan else float("nan")
+    achieved = (alg_bytes / max(launches, 1)) / (fan_ms / 1e3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
+    if os.path.exists(pmc) and world == 1 and args.subs == 16 and args.sessions == 1024:
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args)
+    res = {
+        "metric": "relayed RTP packets/sec (whole node) + achieved HBM GB/s, 1080p H.264 fan-out",
+        "value": round(relayed_all / dt, 1),
+        "unit": "relayed RTP packets/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": round(dt / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (PCG64 RTP/H.264 FU-A headers, GPU-random payload)",
+        "config": {"workload": f"C2: {args.sessions} H.264 1080p30 4 Mb/s streams/GPU x {args.subs} UDP subs, "
+                               f"{args.tick_ms}-ms ticks (ingest+keyframe+fan-out per step)",
+                   "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
+                   "parallelism": f"stream-hash shards x{world}, no data-path collective"},
+        "relayed_GBps": round(out_all / dt / 1e9, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_fanout", "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
+                     "avg_kernel_ms": round(fan_ms, 4)},
+        "kernel_ms": {"fanout": round(fan_ms, 4),
+                      "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,
+                      "ingest": round(float(np.mean(k_ing)), 4) if k_ing else None,
+                      "keyframe_index": round(float(np.mean(k_key)), 4) if k_key else None},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

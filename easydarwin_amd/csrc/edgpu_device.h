@@ -119,6 +119,12 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long ingested_bytes;
     int status;
     unsigned int nwork;
+    // cumulative (never reset)
+    unsigned long long cum_relayed_packets;
+    unsigned long long cum_relayed_bytes;
+    unsigned long long cum_fanout_in_bytes;
+    unsigned long long cum_ingested_packets;
+    unsigned long long cum_ingested_bytes;
 };
 
 struct TickParams {

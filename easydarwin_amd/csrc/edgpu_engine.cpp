@@ -82,6 +82,11 @@ struct edgpu_ctx {
     int fanout_blocks = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
+    // per-launch timing history: [which][slot][start,end]
+    static const int kHist = 256;
+    hipEvent_t hist[4][kHist][2] = {};
+    uint32_t hist_n[4] = {0, 0, 0, 0};
+    uint64_t fanout_launches = 0;
     bool timed_fanout = false, timed_ingest = false, timed_keyframe = false;
 
     std::vector<SessionHost> sessions;
@@ -175,12 +180,12 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     auto bad = [&](const char* what) { edgpu_ctx_destroy(x); return fail(EDGPU_OUT_OF_MEMORY, what); };
     if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return bad("stream");
     for (auto& e : x->ev) if (hipEventCreate(&e) != hipSuccess) return bad("event");
+    for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (hipEventCreate(&e) != hipSuccess) return bad("event");
     if (hipMalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
     if (hipMalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
     if (hipMalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
     if (hipMalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
     if (hipMalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
-    if (hipMalloc(&x->d_blob, c.max_batch_bytes) != hipSuccess) return bad("blob staging");
     if (hipMalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
     if (hipMalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
     if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
@@ -202,6 +207,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
                     (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals})
         if (p) (void)hipFree(p);
     for (auto& e : x->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->stream) (void)hipStreamDestroy(x->stream);
     delete x;
     return EDGPU_OK;
@@ -356,6 +362,14 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     return EDGPU_OK;
 }
 
+// Records the start / end events of launch kind `w` into the history ring.
+static hipError_t hist_mark(edgpu_ctx* x, int w, int end) {
+    const uint32_t slot = x->hist_n[w] % edgpu_ctx::kHist;
+    hipError_t e = hipEventRecord(x->hist[w][slot][end], x->stream);
+    if (end) x->hist_n[w]++;
+    return e;
+}
+
 static int rebuild_index(edgpu_ctx* x) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
     std::vector<uint32_t> idx;
@@ -388,7 +402,8 @@ static int rebuild_index(edgpu_ctx* x) {
 int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
-    if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets || blob_bytes > x->cfg.max_batch_bytes)
+    if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
+        (where == EDGPU_PTR_HOST && blob_bytes > x->cfg.max_batch_bytes))
         return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
@@ -407,6 +422,8 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
             if ((uint64_t)desc[i].slot * 16 + 4 + std::min<uint32_t>(desc[i].len, kMaxPacket) + 15 > blob_bytes + 15 ||
                 (uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
                 return fail(EDGPU_BAD_ARGUMENT, "packet slot outside blob");
+        if (!x->d_blob && hipMalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess)
+            return fail(EDGPU_OUT_OF_MEMORY, "blob staging");
         HIP_CHECK(hipMemcpyAsync(x->d_desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->stream));
         HIP_CHECK(hipMemcpyAsync(x->d_seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->stream));
         HIP_CHECK(hipMemcpyAsync(x->d_seg_sess, seg_sess, (size_t)nseg * 4, hipMemcpyHostToDevice, x->stream));
@@ -424,7 +441,9 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     p.totals = x->d_totals;
     HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
     HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
+    HIP_CHECK(hist_mark(x, 2, 0));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
+    HIP_CHECK(hist_mark(x, 2, 1));
     HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
     x->timed_ingest = true;
     x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
@@ -439,7 +458,9 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
     HIP_CHECK(hipEventRecord(x->ev[6], x->stream));
+    HIP_CHECK(hist_mark(x, 3, 0));
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
+    HIP_CHECK(hist_mark(x, 3, 1));
     HIP_CHECK(hipEventRecord(x->ev[7], x->stream));
     x->timed_keyframe = true;
     x->pending = false;
@@ -469,14 +490,19 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(hipMemsetAsync(x->d_totals, 0, 3 * sizeof(unsigned long long), x->stream));
     HIP_CHECK(hipMemsetAsync(&x->d_totals->status, 0, 2 * sizeof(int), x->stream));
     HIP_CHECK(hipEventRecord(x->ev[0], x->stream));
+    HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));
     FanoutParams f;
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
     f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
     f.totals = x->d_totals;
     HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
+    HIP_CHECK(hist_mark(x, 0, 0));
     HIP_CHECK(launch_fanout(f, (uint32_t)x->fanout_blocks, x->stream));
+    HIP_CHECK(hist_mark(x, 0, 1));
+    HIP_CHECK(hist_mark(x, 1, 1));
     HIP_CHECK(hipEventRecord(x->ev[2], x->stream));
+    x->fanout_launches++;
     x->timed_fanout = true;
     if (out) {
         out->arena = x->d_arena;
@@ -500,6 +526,37 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->ingested_bytes = t.ingested_bytes;
     out->status = t.status;
     out->_pad = t.nwork;
+    return EDGPU_OK;
+}
+
+int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
+    if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    TickTotals t;
+    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    out->relayed_packets = t.cum_relayed_packets;
+    out->relayed_bytes = t.cum_relayed_bytes;
+    out->fanout_in_bytes = t.cum_fanout_in_bytes;
+    out->fanout_launches = x->fanout_launches;
+    out->ingested_packets = t.cum_ingested_packets;
+    out->ingested_bytes = t.cum_ingested_bytes;
+    return EDGPU_OK;
+}
+
+int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, uint32_t* out_n) {
+    if (!x || which < 0 || which > 3 || (!out_ms && max_n)) return fail(EDGPU_BAD_ARGUMENT, "bad argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    const uint32_t n = std::min<uint32_t>(x->hist_n[which], edgpu_ctx::kHist);
+    const uint32_t first = x->hist_n[which] - n;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n && k < max_n; i++, k++) {
+        const uint32_t slot = (first + i) % edgpu_ctx::kHist;
+        HIP_CHECK(hipEventElapsedTime(&out_ms[k], x->hist[which][slot][0], x->hist[which][slot][1]));
+    }
+    x->hist_n[which] = 0;
+    if (out_n) *out_n = k;
     return EDGPU_OK;
 }
 

@@ -284,6 +284,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     if (tid == 0) {
         atomicAdd(&P.totals->ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->ingested_bytes, (unsigned long long)t2);
+        atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
+        atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
     }
 }
 
@@ -471,6 +473,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
         if (tid == nt - 1) {
             P.totals->arena_bytes = sh64[tid];
             P.totals->relayed_packets = sh32[tid];
+            P.totals->cum_relayed_packets += sh32[tid];
             if (sh64[tid] > P.T.arena_bytes || sh32[tid] > P.T.max_desc)
                 atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
         }
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
     __shared__ uint32_t m_vc[kChunkPackets];
     __shared__ uint32_t startmap[(kChunkWords + 31) / 32];
     __shared__ unsigned long long s_wire[4];
-    unsigned long long wire = 0;
+    unsigned long long wire = 0, inb = 0;
 
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
         const WorkItem it = P.work[w];
@@ -566,6 +569,7 @@ __global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
         if (tid < (int)np) {
             const PktMeta m = meta[(lo + tid) & D.pk_mask];
             m_vb[tid] = m.vbyte; m_id[tid] = m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
+            inb += m.len;
         }
         if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
         for (int k = tid; k < (int)((kChunkWords + 31) / 32); k += kFanoutThreads) startmap[k] = 0;
@@ -626,9 +630,14 @@ __global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
         }
         __syncthreads();
     }
-    unsigned long long tot;
+    unsigned long long tot, tin;
     (void)block_exclusive_scan<unsigned long long>(wire, s_wire, tot);
-    if (tid == 0 && tot) atomicAdd(&P.totals->relayed_bytes, tot);
+    (void)block_exclusive_scan<unsigned long long>(inb, s_wire, tin);
+    if (tid == 0 && tot) {
+        atomicAdd(&P.totals->relayed_bytes, tot);
+        atomicAdd(&P.totals->cum_relayed_bytes, tot);
+    }
+    if (tid == 0 && tin) atomicAdd(&P.totals->cum_fanout_in_bytes, tin);
 }
 
 }  // namespace edgpu

@@ -25,7 +25,7 @@ EXPORTED = [
     "edgpu_ctx_destroy", "edgpu_sync", "edgpu_session_add", "edgpu_session_tracks",
     "edgpu_subscriber_add", "edgpu_subscriber_remove", "edgpu_ingest", "edgpu_keyframe_index",
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
-    "edgpu_gop_span",
+    "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times",
 ]
 
 
@@ -71,6 +71,12 @@ class TickStats(C.Structure):
     _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
                 ("arena_bytes", C.c_uint64), ("ingested_packets", C.c_uint64),
                 ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32)]
+
+
+class Counters(C.Structure):
+    _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
+                ("fanout_in_bytes", C.c_uint64), ("fanout_launches", C.c_uint64),
+                ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64)]
 
 
 # numpy mirrors (same layout as the C structs)
@@ -122,6 +128,8 @@ def load(path: str = LIB_PATH):
         "edgpu_copy_to_host": (I32, [P, P, P, U64]),
         "edgpu_last_timings": (I32, [P, C.POINTER(C.c_float)]),
         "edgpu_gop_span": (I32, [P, U32, U32, C.POINTER(U64), C.POINTER(U64)]),
+        "edgpu_counters_get": (I32, [P, C.POINTER(Counters)]),
+        "edgpu_kernel_times": (I32, [P, I32, C.POINTER(C.c_float), U32, C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -219,6 +227,18 @@ class Context:
         a = (C.c_float * 4)()
         _check(self.lib.edgpu_last_timings(self.h, a))
         return {"fanout_ms": a[0], "tick_ms": a[1], "ingest_ms": a[2], "keyframe_ms": a[3]}
+
+    def counters(self) -> dict:
+        c = Counters()
+        _check(self.lib.edgpu_counters_get(self.h, C.byref(c)))
+        return {k: getattr(c, k) for k, _ in Counters._fields_}
+
+    def kernel_times(self, which: int) -> list:
+        """which: 0 fan-out kernel, 1 whole fan-out tick, 2 ingest, 3 keyframe index."""
+        buf = (C.c_float * 256)()
+        n = C.c_uint32()
+        _check(self.lib.edgpu_kernel_times(self.h, which, buf, 256, C.byref(n)))
+        return [buf[i] for i in range(n.value)]
 
     def gop_span(self, session: int, track: int):
         p, b = C.c_uint64(), C.c_uint64()

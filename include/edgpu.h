@@ -173,6 +173,24 @@ int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
 
+/* Cumulative counters since context creation (syncs).  fanout_in_bytes counts the
+ * ingested bytes the fan-out read (each referenced packet once per launch). */
+typedef struct edgpu_counters {
+    uint64_t relayed_packets;
+    uint64_t relayed_bytes;
+    uint64_t fanout_in_bytes;
+    uint64_t fanout_launches;
+    uint64_t ingested_packets;
+    uint64_t ingested_bytes;
+} edgpu_counters;
+int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
+
+/* Per-launch device durations (ms, HIP events on the ctx stream) recorded since the last
+ * call, oldest first, for `which` = 0 fan-out copy kernel, 1 whole fan-out tick (plan +
+ * copy), 2 ingest, 3 keyframe index.  Up to 256 launches are kept; the history is cleared
+ * after reading.  Syncs. */
+int  edgpu_kernel_times(edgpu_ctx* ctx, int which, float* out_ms, uint32_t max_n, uint32_t* out_n);
+
 /* Copies device memory of this context to the host (synchronous).  Convenience for hosts
  * and tests that read fan-out results. */
 int  edgpu_copy_to_host(edgpu_ctx* ctx, void* dst, const void* device_src, uint64_t bytes);

@@ -32,7 +32,7 @@
 // reads 0), Q17 (recycled bookmarks after >10 s lag), Q20 (TCP audio thinning), blocking sinks.
 //
 // Usage:  relay_model <trace.edtr> <capture.edcp>
-//         relay_model --bench <trace.edtr> <threads>   (memcpy sinks, prints JSON)
+//         relay_model --bench <trace.edtr> <threads> [repeat]   (memcpy sinks, prints JSON)
 
 #include <cstdint>
 #include <cstdio>
@@ -444,39 +444,83 @@ static int run_capture(const char* in, const char* out) {
     return 0;
 }
 
-// Bench: sessions sharded over threads (session % T), each thread replays the whole trace
-// but only applies its own sessions; sinks are memcpy into per-subscriber buffers that are
-// recycled every tick.  Reports relayed packets/s of the replay (ingest + fan-out).
-static int run_bench(const char* in, int threads) {
-    Reader r0;
-    if (!load(in, r0)) return 2;
+// Bench: the trace is parsed once, its events are split by session (session % T) into T
+// private lists (TICKs go to every list), then T threads replay their lists concurrently with
+// memcpy sinks recycled every tick.  Only the replay (ingest + fan-out) is timed.
+struct Ev { uint8_t type; int64_t t; uint32_t s, sub; uint8_t ch; bool tcp; const uint8_t* data; uint32_t len; };
+
+static int run_bench(const char* in, int threads, int repeat) {
+    Reader r;
+    if (!load(in, r)) return 2;
+    uint32_t nsess = r.get<uint32_t>();
+    std::vector<std::string> sdps;
+    for (uint32_t s = 0; s < nsess; s++) {
+        uint32_t n = r.get<uint32_t>();
+        sdps.emplace_back((const char*)&r.d[r.p], n);
+        r.p += n;
+    }
+    std::vector<std::vector<Ev>> lists(threads);
+    while (r.p < r.d.size()) {
+        Ev e{};
+        e.type = r.get<uint8_t>();
+        if (e.type == 0) break;
+        e.t = r.get<int64_t>();
+        if (e.type == 1) {
+            e.s = r.get<uint32_t>(); e.ch = r.get<uint8_t>(); e.len = r.get<uint32_t>();
+            e.data = &r.d[r.p]; r.p += e.len;
+            lists[e.s % threads].push_back(e);
+        } else if (e.type == 2) {
+            e.s = r.get<uint32_t>(); e.sub = r.get<uint32_t>(); e.tcp = r.get<uint8_t>() != 0; (void)r.get<uint8_t>();
+            lists[e.s % threads].push_back(e);
+        } else {
+            for (auto& l : lists) l.push_back(e);
+        }
+    }
     std::atomic<uint64_t> pkts{0}, bytes{0};
+    std::vector<double> busy(threads, 0.0);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; t++)
         th.emplace_back([&, t]() {
-            Reader r = r0;   // private copy of the cursor (shares nothing mutable)
+            ready++;
+            while (!go.load()) {}
+            auto a = std::chrono::steady_clock::now();
+            for (int rep = 0; rep < repeat; rep++) {
             relay::Model m;
+            for (uint32_t s = 0; s < nsess; s++) m.add_session(sdps[s]);   // ids stay global
             std::vector<std::unique_ptr<std::vector<uint8_t>>> sinks;
-            replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp) {
-                sinks.emplace_back(new std::vector<uint8_t>());
-                sinks.back()->reserve(1 << 20);
-                m.join(s, sub, tcp, sinks.back().get());
-            }, (uint32_t)t, (uint32_t)threads);
+            for (const Ev& e : lists[t]) {
+                if (e.t > m.now) m.now = e.t;
+                if (e.type == 1) m.push(e.s, e.ch / 2, e.ch & 1, e.data, e.len);
+                else if (e.type == 2) {
+                    sinks.emplace_back(new std::vector<uint8_t>());
+                    sinks.back()->reserve(1 << 20);
+                    m.join(e.s, e.sub, e.tcp, sinks.back().get());
+                } else m.tick();
+            }
             uint64_t p = 0, b = 0;
             for (auto& se : m.sessions) for (auto& o : se->outputs) { p += o->sink_pkts; b += o->sink_bytes; }
             pkts += p; bytes += b;
+            }
+            busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
         });
+    while (ready.load() < threads) {}
+    t0 = std::chrono::steady_clock::now();
+    go = true;
     for (auto& x : th) x.join();
     double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"threads\": %d, "
-           "\"packets_per_s\": %.1f}\n", (unsigned long long)pkts.load(), (unsigned long long)bytes.load(),
-           s, threads, pkts.load() / s);
+           "\"packets_per_s\": %.1f, \"max_thread_busy_s\": %.6f}\n", (unsigned long long)pkts.load(),
+           (unsigned long long)bytes.load(), s, threads, pkts.load() / s,
+           *std::max_element(busy.begin(), busy.end()));
     return 0;
 }
 
 int main(int argc, char** argv) {
-    if (argc == 4 && std::string(argv[1]) == "--bench") return run_bench(argv[2], atoi(argv[3]));
+    if ((argc == 4 || argc == 5) && std::string(argv[1]) == "--bench")
+        return run_bench(argv[2], atoi(argv[3]), argc == 5 ? atoi(argv[4]) : 1);
     if (argc != 3) { fprintf(stderr, "usage: %s trace capture | --bench trace threads\n", argv[0]); return 2; }
     return run_capture(argv[1], argv[2]);
 }
