@@ -1,0 +1,52 @@
+"""Summarise a tools/profile.sh run into profiles/: kernel stats (rocprofv3 --stats) and the
+per-launch HBM traffic of k_fanout from the separate FETCH_SIZE / WRITE_SIZE passes.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
+FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+Usage: python tools/summarize_profile.py gpurun_out/<run> <tag>
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+run, tag = sys.argv[1], sys.argv[2]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(ROOT, "profiles")
+
+
+def counters(path, name):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == name:
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+fetch = counters(os.path.join(run, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+write = counters(os.path.join(run, "write", "write_counter_collection.csv"), "WRITE_SIZE")
+stats = list(csv.DictReader(open(os.path.join(run, "kt", "kt_kernel_stats.csv"))))
+bench = json.load(open(os.path.join(run, "kt_bench.json")))
+avg_ns = {r["Name"]: float(r["AverageNs"]) for r in stats}
+res = {"tag": tag, "kernels": {}}
+for k in sorted(set(fetch) | set(write)):
+    # skip the warmup launches: the bench runs warmup + steps launches, report the timed ones
+    f = fetch.get(k, [])[-bench["steps"]:]
+    w = write.get(k, [])[-bench["steps"]:]
+    fk, wk = statistics.mean(f), statistics.mean(w)
+    res["kernels"][k] = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
+                         "hbm_read_bytes": 2 * fk * 1024, "hbm_write_bytes": wk * 1024,
+                         "hbm_bytes_per_launch": (2 * fk + wk) * 1024,
+                         "avg_duration_ns_rocprof": avg_ns.get(k)}
+fan = res["kernels"].get("k_fanout", {})
+res["hbm_bytes_per_launch"] = fan.get("hbm_bytes_per_launch")
+res["alg_bytes_per_launch"] = bench["roofline"]["alg_bytes_per_launch"]
+res["bench_avg_kernel_ms"] = bench["roofline"]["avg_kernel_ms"]
+res["rocprof_avg_kernel_ms"] = (avg_ns.get("k_fanout") or 0) / 1e6
+json.dump(res, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+shutil.copy(os.path.join(run, "kt", "kt_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+shutil.copy(os.path.join(run, "kt_bench.json"), os.path.join(prof, f"{tag}_bench.json"))
+print(json.dumps(res, indent=1))
