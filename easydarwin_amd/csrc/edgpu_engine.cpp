@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -22,8 +23,7 @@ namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
-hipError_t launch_fanout(const FanoutParams& p, uint32_t grid, hipStream_t st);
-int fanout_occupancy();
+hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 }  // namespace edgpu
 
 using namespace edgpu;
@@ -79,7 +79,7 @@ struct edgpu_ctx {
     edgpu_config cfg;
     int device = 0;
     int num_cus = 256;
-    int fanout_blocks = 0;
+    int fanout_variant = 1;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
@@ -190,7 +190,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipMalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
     if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
-    x->fanout_blocks = x->num_cus * fanout_occupancy();
+    if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
     *out = x;
     return EDGPU_OK;
 }
@@ -498,7 +498,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     f.totals = x->d_totals;
     HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
     HIP_CHECK(hist_mark(x, 0, 0));
-    HIP_CHECK(launch_fanout(f, (uint32_t)x->fanout_blocks, x->stream));
+    HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, x->stream));
     HIP_CHECK(hist_mark(x, 0, 1));
     HIP_CHECK(hist_mark(x, 1, 1));
     HIP_CHECK(hipEventRecord(x->ev[2], x->stream));

@@ -640,6 +640,171 @@ __global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
     if (tid == 0 && tin) atomicAdd(&P.totals->cum_fanout_in_bytes, tin);
 }
 
+
+// -----------------------------------------------------------------------------------------
+// k_fanout2: same contract as k_fanout, restructured for occupancy and latency:
+//   * THREADS-wide workgroups (512 = 8 waves), so a 32-packet chunk needs only
+//     ceil(4128 / THREADS) VGPR quads per lane;
+//   * the sender's sub-stream table is staged in LDS once per work item (one parallel load)
+//     instead of a dependent global load per sub-stream inside the store loop;
+//   * descriptors are written with one lane per (sub-stream, packet) pair.
+// NT selects non-temporal (streaming) stores for the arena and descriptors.
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+template <int THREADS, bool NT>
+__global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
+    constexpr int NW = (kChunkWords + THREADS - 1) / THREADS;
+    constexpr int NWAVES = THREADS / 64;
+    const uint32_t nwork = P.totals->nwork;
+    if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    __shared__ uint64_t m_vb[kChunkPackets + 1];
+    __shared__ uint32_t m_id[kChunkPackets];
+    __shared__ uint32_t m_len[kChunkPackets];
+    __shared__ uint32_t m_vc[kChunkPackets];
+    __shared__ uint32_t startmap[(kChunkWords + 31) / 32];
+    // per sub-stream (batch of THREADS) parameters
+    __shared__ int64_t  q_dw0[THREADS];      // arena word of chunk word 0
+    __shared__ int64_t  q_off[THREADS];      // out_base - vstart (+4 for UDP)
+    __shared__ uint32_t q_fw[THREADS];       // first chunk word to write (>= nwords: skip)
+    __shared__ uint32_t q_ch[THREADS];       // channel bits for TCP, 0 for UDP
+    __shared__ uint32_t q_db[THREADS];       // desc_base - vcstart
+    __shared__ uint32_t q_p0[THREADS];       // first chunk packet of this sub-stream
+    __shared__ uint32_t q_hl[THREADS];       // wire header bytes: 4 for TCP, 0 for UDP
+    __shared__ unsigned long long s_red[NWAVES];
+    unsigned long long wire = 0, inb = 0;
+    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const WorkItem it = P.work[w];
+        const SenderDev& D = P.senders[it.sender];
+        const uint64_t lo = D.umin + (uint64_t)it.chunk * kChunkPackets;
+        const uint64_t head = D.head;
+        const uint32_t np = (uint32_t)min((uint64_t)kChunkPackets, head - lo);
+        const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        if (tid < (int)np) {
+            const PktMeta m = meta[(lo + tid) & D.pk_mask];
+            m_vb[tid] = m.vbyte; m_id[tid] = (uint32_t)m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
+            inb += m.len;
+        }
+        if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
+        for (int k = tid; k < (int)((kChunkWords + 31) / 32); k += THREADS) startmap[k] = 0;
+        __syncthreads();
+        const uint64_t vb0 = m_vb[0];
+        const uint32_t nwords = (uint32_t)((m_vb[np] - vb0) >> 4);
+        if (tid < (int)np && m_len[tid] != 0) {
+            const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
+            atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
+        }
+        __syncthreads();
+        // Uniform values are forced into SGPRs so every load/store below is a scalar base +
+        // 32-bit lane offset (global_*_dwordx4 saddr form).
+        const u32x4* ring = reinterpret_cast<const u32x4*>(D.ring);
+        const uint32_t wmask = uni(D.word_mask);
+        const uint32_t nw = uni(nwords);
+        const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
+        const bool wraps = rstart + nw > wmask + 1;
+        const u32x4* rb = ring + rstart;
+        u32x4 r[NW];
+        uint32_t smask = 0;
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const uint32_t wi = tid + j * THREADS;
+            if (wi < nw) {
+                r[j] = wraps ? ring[(rstart + wi) & wmask] : rb[wi];
+                smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
+            }
+        }
+        const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
+        for (uint32_t q0 = qb; q0 < qe; q0 += THREADS) {
+            const uint32_t nq = min((uint32_t)THREADS, qe - q0);
+            if (tid < (int)nq) {
+                const SubDev& Q = P.subs[P.sub_index[q0 + tid]];
+                uint32_t fw = 0xFFFFFFFFu, p0 = 0xFFFFFFFFu;
+                if (Q.nonempty && Q.a < lo + np) {
+                    const uint64_t first = Q.a > lo ? Q.a : lo;
+                    p0 = (uint32_t)(first - lo);
+                    fw = (uint32_t)((m_vb[p0] - vb0) >> 4);
+                }
+                q_fw[tid] = fw;
+                q_p0[tid] = p0;
+                q_dw0[tid] = (int64_t)(Q.out_base >> 4) + ((int64_t)(vb0 - Q.vstart) >> 4);
+                q_off[tid] = (int64_t)(Q.out_base - Q.vstart) + (Q.transport ? 0 : 4);
+                q_ch[tid] = Q.transport ? ((uint32_t)Q.channel << 8) : 0u;
+                q_db[tid] = Q.desc_base - Q.vcstart;
+                q_hl[tid] = Q.transport ? 4u : 0u;
+            }
+            __syncthreads();
+            for (uint32_t q = 0; q < nq; q++) {
+                const uint32_t fw = uni(q_fw[q]);
+                if (fw >= nw) continue;
+                u32x4* ob = out + (int64_t)uni64((uint64_t)q_dw0[q]);
+                const uint32_t chbits = uni(q_ch[q]);
+                if (chbits == 0) {                       // UDP: the slots as they are
+#pragma unroll
+                    for (int j = 0; j < NW; j++) {
+                        const uint32_t wi = tid + j * THREADS;
+                        if (wi >= fw && wi < nw) {
+                            if (NT) __builtin_nontemporal_store(r[j], &ob[wi]);
+                            else ob[wi] = r[j];
+                        }
+                    }
+                } else {                                 // TCP: patch the '$' header's channel
+#pragma unroll
+                    for (int j = 0; j < NW; j++) {
+                        const uint32_t wi = tid + j * THREADS;
+                        if (wi >= fw && wi < nw) {
+                            const uint32_t pm = ((smask >> j) & 1u) ? chbits : 0u;
+                            r[j].x |= pm;                // ring header channel byte is 0
+                            if (NT) __builtin_nontemporal_store(r[j], &ob[wi]);
+                            else ob[wi] = r[j];
+                            r[j].x &= ~pm;
+                        }
+                    }
+                }
+            }
+            // descriptors: one lane per (sub-stream, packet)
+            for (uint32_t t = tid; t < nq * np; t += THREADS) {
+                const uint32_t q = t / np, p = t - q * np;
+                if (p < q_p0[q] || m_len[p] == 0) continue;
+                const uint32_t len = m_len[p];
+                const uint64_t off = (uint64_t)(q_off[q] + (int64_t)m_vb[p]);
+                const uint32_t wlen = len + q_hl[q];
+                const uint32_t di = q_db[q] + m_vc[p];
+                u32x4 dv;
+                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
+                if (NT) __builtin_nontemporal_store(dv, reinterpret_cast<u32x4*>(P.desc) + di);
+                else reinterpret_cast<u32x4*>(P.desc)[di] = dv;
+                wire += wlen;
+            }
+            __syncthreads();
+        }
+    }
+    // block reduction of the byte counters
+    unsigned long long a = wire, b = inb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+    if ((tid & 63) == 0) s_red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) s_red[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
+    }
+}
+
 }  // namespace edgpu
 
 // ---------------------------------------------------------------------------------------
@@ -665,14 +830,38 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
     return hipGetLastError();
 }
-hipError_t launch_fanout(const FanoutParams& p, uint32_t grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_fanout, dim3(grid), dim3(kFanoutThreads), 0, st, p);
-    return hipGetLastError();
-}
-int fanout_occupancy() {
+// Fan-out variants (EDGPU_FANOUT env var, for A/B measurement): 0 = k_fanout (256 threads,
+// register staging, per-sub-stream global loads), 1 = k_fanout2<512, NT>, 2 = k_fanout2<512>
+// with plain stores, 3 = k_fanout2<1024, NT>.
+static int occupancy_of(const void* fn, int threads) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_fanout, kFanoutThreads, 0) != hipSuccess) return 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
+}
+hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
+    switch (variant) {
+        case 0: {
+            static int occ = occupancy_of((const void*)k_fanout, kFanoutThreads);
+            hipLaunchKernelGGL(k_fanout, dim3(num_cus * occ), dim3(kFanoutThreads), 0, st, p);
+            break;
+        }
+        case 2: {
+            static int occ = occupancy_of((const void*)k_fanout2<512, false>, 512);
+            hipLaunchKernelGGL((k_fanout2<512, false>), dim3(num_cus * occ), dim3(512), 0, st, p);
+            break;
+        }
+        case 3: {
+            static int occ = occupancy_of((const void*)k_fanout2<1024, true>, 1024);
+            hipLaunchKernelGGL((k_fanout2<1024, true>), dim3(num_cus * occ), dim3(1024), 0, st, p);
+            break;
+        }
+        default: {
+            static int occ = occupancy_of((const void*)k_fanout2<512, true>, 512);
+            hipLaunchKernelGGL((k_fanout2<512, true>), dim3(num_cus * occ), dim3(512), 0, st, p);
+            break;
+        }
+    }
+    return hipGetLastError();
 }
 
 }  // namespace edgpu
