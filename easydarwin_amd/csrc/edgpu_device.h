@@ -135,6 +135,7 @@ struct TickParams {
     uint32_t nsenders;
     uint32_t nsubs;
     uint32_t nsub_blocks;
+    uint32_t chunk;                 // packets per fan-out work item (per kernel variant)
 };
 
 }  // namespace edgpu

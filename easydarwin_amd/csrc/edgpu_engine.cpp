@@ -24,6 +24,7 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
+int fanout_chunk(int variant);
 }  // namespace edgpu
 
 using namespace edgpu;
@@ -79,7 +80,7 @@ struct edgpu_ctx {
     edgpu_config cfg;
     int device = 0;
     int num_cus = 256;
-    int fanout_variant = 1;
+    int fanout_variant = 2;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
@@ -288,7 +289,7 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             D.key = -1;
             D.last_nonzero = -1;
             D.new_start = -1;
-            x->work_cap_needed += pk / kChunkPackets + 1;
+            x->work_cap_needed += pk / 16 + 1;          // smallest chunk of any variant
         }
         str[t].packet_count = 0;
     }
@@ -486,6 +487,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsenders = x->nsenders;
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
+    p.T.chunk = (uint32_t)fanout_chunk(x->fanout_variant);
     // reset per-tick totals (relayed_*, arena, status, nwork); keep the ingest counters
     HIP_CHECK(hipMemsetAsync(x->d_totals, 0, 3 * sizeof(unsigned long long), x->stream));
     HIP_CHECK(hipMemsetAsync(&x->d_totals->status, 0, 2 * sizeof(int), x->stream));

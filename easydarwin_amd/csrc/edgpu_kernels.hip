@@ -488,7 +488,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
         for (uint32_t s = s0; s < s1; s++) {
             const SenderDev& D = P.senders[s];
             const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
-            sum += (uint32_t)((span + kChunkPackets - 1) / kChunkPackets);
+            sum += (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
         }
         sh32[tid] = sum;
         __syncthreads();
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
         for (uint32_t s = s0; s < s1; s++) {
             SenderDev& D = P.senders[s];
             const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
-            const uint32_t k = (uint32_t)((span + kChunkPackets - 1) / kChunkPackets);
+            const uint32_t k = (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
             D.chunk_base = r; D.nchunks = k;
             r += k;
         }
@@ -655,18 +655,20 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
-template <int THREADS, bool NT>
-__global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
-    constexpr int NW = (kChunkWords + THREADS - 1) / THREADS;
+template <int THREADS, int CHUNK, bool NT, int WAVES>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WAVES)))
+void k_fanout2(FanoutParams P) {
+    constexpr int CWORDS = CHUNK * 129;                  // CHUNK * roundup16(4 + 2060) / 16
+    constexpr int NW = (CWORDS + THREADS - 1) / THREADS;
     constexpr int NWAVES = THREADS / 64;
     const uint32_t nwork = P.totals->nwork;
     if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
     const int tid = threadIdx.x;
-    __shared__ uint64_t m_vb[kChunkPackets + 1];
-    __shared__ uint32_t m_id[kChunkPackets];
-    __shared__ uint32_t m_len[kChunkPackets];
-    __shared__ uint32_t m_vc[kChunkPackets];
-    __shared__ uint32_t startmap[(kChunkWords + 31) / 32];
+    __shared__ uint64_t m_vb[CHUNK + 1];
+    __shared__ uint32_t m_id[CHUNK];
+    __shared__ uint32_t m_len[CHUNK];
+    __shared__ uint32_t m_vc[CHUNK];
+    __shared__ uint32_t startmap[(CWORDS + 31) / 32];
     // per sub-stream (batch of THREADS) parameters
     __shared__ int64_t  q_dw0[THREADS];      // arena word of chunk word 0
     __shared__ int64_t  q_off[THREADS];      // out_base - vstart (+4 for UDP)
@@ -682,9 +684,9 @@ __global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
         const WorkItem it = P.work[w];
         const SenderDev& D = P.senders[it.sender];
-        const uint64_t lo = D.umin + (uint64_t)it.chunk * kChunkPackets;
+        const uint64_t lo = D.umin + (uint64_t)it.chunk * CHUNK;
         const uint64_t head = D.head;
-        const uint32_t np = (uint32_t)min((uint64_t)kChunkPackets, head - lo);
+        const uint32_t np = (uint32_t)min((uint64_t)CHUNK, head - lo);
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
         if (tid < (int)np) {
             const PktMeta m = meta[(lo + tid) & D.pk_mask];
@@ -692,7 +694,7 @@ __global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
             inb += m.len;
         }
         if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
-        for (int k = tid; k < (int)((kChunkWords + 31) / 32); k += THREADS) startmap[k] = 0;
+        for (int k = tid; k < (int)((CWORDS + 31) / 32); k += THREADS) startmap[k] = 0;
         __syncthreads();
         const uint64_t vb0 = m_vb[0];
         const uint32_t nwords = (uint32_t)((m_vb[np] - vb0) >> 4);
@@ -701,23 +703,34 @@ __global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
             atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
         }
         __syncthreads();
-        // Uniform values are forced into SGPRs so every load/store below is a scalar base +
-        // 32-bit lane offset (global_*_dwordx4 saddr form).
-        const u32x4* ring = reinterpret_cast<const u32x4*>(D.ring);
+        // Chunk load: buffer loads through a descriptor built from wave-uniform values, so
+        // each lane needs one 32-bit offset; lanes past the chunk read 0 (range check).
         const uint32_t wmask = uni(D.word_mask);
         const uint32_t nw = uni(nwords);
         const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
         const bool wraps = rstart + nw > wmask + 1;
-        const u32x4* rb = ring + rstart;
         u32x4 r[NW];
+        if (!wraps) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<u32x4*>(D.ring) + rstart, 0, nw * 16, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < NW; j++)
+                r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(tid + j * THREADS) * 16u, 0, 0);
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<u32x4*>(D.ring), 0, (wmask + 1) * 16, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                const uint32_t wi = tid + j * THREADS;
+                r[j] = wi < nw ? __builtin_amdgcn_raw_buffer_load_b128(rs, ((rstart + wi) & wmask) * 16u, 0, 0)
+                               : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
         uint32_t smask = 0;
 #pragma unroll
         for (int j = 0; j < NW; j++) {
             const uint32_t wi = tid + j * THREADS;
-            if (wi < nw) {
-                r[j] = wraps ? ring[(rstart + wi) & wmask] : rb[wi];
-                smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
-            }
+            if (wi < nw) smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
         }
         const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
         for (uint32_t q0 = qb; q0 < qe; q0 += THREADS) {
@@ -742,28 +755,21 @@ __global__ __launch_bounds__(THREADS) void k_fanout2(FanoutParams P) {
             for (uint32_t q = 0; q < nq; q++) {
                 const uint32_t fw = uni(q_fw[q]);
                 if (fw >= nw) continue;
-                u32x4* ob = out + (int64_t)uni64((uint64_t)q_dw0[q]);
+                // Store descriptor over this sub-stream's part of the chunk [fw, nw): lanes
+                // outside it get an out-of-range offset and the hardware drops the store.
+                const int64_t dw0 = (int64_t)uni64((uint64_t)q_dw0[q]);
+                const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
+                    out + dw0 + fw, 0, (nw - fw) * 16, 0x00020000);
+                const uint32_t vbase = (uint32_t)(tid - (int)fw) * 16u;
                 const uint32_t chbits = uni(q_ch[q]);
-                if (chbits == 0) {                       // UDP: the slots as they are
 #pragma unroll
+                for (int j = 0; j < NW; j++)
+                    __builtin_amdgcn_raw_buffer_store_b128(r[j], os, vbase + j * THREADS * 16, 0, NT ? 2 : 0);
+                if (chbits) {            // TCP: rewrite each slot's '$' header dword with the channel
+#pragma unroll                          // (same lane, same address, program order)
                     for (int j = 0; j < NW; j++) {
-                        const uint32_t wi = tid + j * THREADS;
-                        if (wi >= fw && wi < nw) {
-                            if (NT) __builtin_nontemporal_store(r[j], &ob[wi]);
-                            else ob[wi] = r[j];
-                        }
-                    }
-                } else {                                 // TCP: patch the '$' header's channel
-#pragma unroll
-                    for (int j = 0; j < NW; j++) {
-                        const uint32_t wi = tid + j * THREADS;
-                        if (wi >= fw && wi < nw) {
-                            const uint32_t pm = ((smask >> j) & 1u) ? chbits : 0u;
-                            r[j].x |= pm;                // ring header channel byte is 0
-                            if (NT) __builtin_nontemporal_store(r[j], &ob[wi]);
-                            else ob[wi] = r[j];
-                            r[j].x &= ~pm;
-                        }
+                        const uint32_t off = ((smask >> j) & 1u) ? vbase + j * THREADS * 16 : 0xFFFFFFFFu;
+                        __builtin_amdgcn_raw_buffer_store_b32(r[j].x | chbits, os, off, 0, NT ? 2 : 0);
                     }
                 }
             }
@@ -830,38 +836,36 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
     return hipGetLastError();
 }
-// Fan-out variants (EDGPU_FANOUT env var, for A/B measurement): 0 = k_fanout (256 threads,
-// register staging, per-sub-stream global loads), 1 = k_fanout2<512, NT>, 2 = k_fanout2<512>
-// with plain stores, 3 = k_fanout2<1024, NT>.
+// Fan-out variants (EDGPU_FANOUT env var, for A/B measurement).  Each entry: kernel,
+// threads per workgroup, packets per work item.
 static int occupancy_of(const void* fn, int threads) {
     int blocks = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }
-hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
-    switch (variant) {
-        case 0: {
-            static int occ = occupancy_of((const void*)k_fanout, kFanoutThreads);
-            hipLaunchKernelGGL(k_fanout, dim3(num_cus * occ), dim3(kFanoutThreads), 0, st, p);
-            break;
-        }
-        case 2: {
-            static int occ = occupancy_of((const void*)k_fanout2<512, false>, 512);
-            hipLaunchKernelGGL((k_fanout2<512, false>), dim3(num_cus * occ), dim3(512), 0, st, p);
-            break;
-        }
-        case 3: {
-            static int occ = occupancy_of((const void*)k_fanout2<1024, true>, 1024);
-            hipLaunchKernelGGL((k_fanout2<1024, true>), dim3(num_cus * occ), dim3(1024), 0, st, p);
-            break;
-        }
-        default: {
-            static int occ = occupancy_of((const void*)k_fanout2<512, true>, 512);
-            hipLaunchKernelGGL((k_fanout2<512, true>), dim3(num_cus * occ), dim3(512), 0, st, p);
-            break;
-        }
-    }
-    return hipGetLastError();
+struct FanoutVariant { const void* fn; int threads; int chunk; };
+static const FanoutVariant kVariants[] = {
+    {(const void*)k_fanout, kFanoutThreads, kChunkPackets},                         // 0 legacy
+    {(const void*)k_fanout2<512, 32, true, 1>, 512, 32},                            // 1 nt
+    {(const void*)k_fanout2<512, 32, false, 1>, 512, 32},                           // 2
+    {(const void*)k_fanout2<1024, 32, false, 1>, 1024, 32},                         // 3
+    {(const void*)k_fanout2<512, 32, false, 6>, 512, 32},                           // 4
+    {(const void*)k_fanout2<512, 32, false, 8>, 512, 32},                           // 5
+    {(const void*)k_fanout2<256, 16, false, 8>, 256, 16},                           // 6
+    {(const void*)k_fanout2<512, 16, false, 8>, 512, 16},                           // 7
+    {(const void*)k_fanout2<1024, 32, false, 8>, 1024, 32},                         // 8
+};
+static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+int fanout_chunk(int variant) {
+    if (variant < 0 || variant >= kNumVariants) variant = 2;
+    return kVariants[variant].chunk;
 }
-
+hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
+    if (variant < 0 || variant >= kNumVariants) variant = 2;
+    static int occ[16] = {0};
+    const FanoutVariant& v = kVariants[variant];
+    if (!occ[variant]) occ[variant] = occupancy_of(v.fn, v.threads);
+    void* args[] = {(void*)&p};
+    return hipLaunchKernel(v.fn, dim3(num_cus * occ[variant]), dim3(v.threads), args, 0, st);
+}
 }  // namespace edgpu

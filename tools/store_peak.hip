@@ -1,19 +1,32 @@
-// tools/store_peak.hip -- calibration microbenchmark (not part of the product): the HBM
-// write / copy ceilings for the fan-out's access shape on this MI355X.
-//   write: every lane stores 16-B words to a contiguous region (8 GiB), plain vs nt
-//   fanout-shaped: 1 KiB read once from a source, written to 16 destinations 64 MiB apart
+// tools/store_peak.hip -- calibration microbenchmark (not part of the product): HBM write
+// and copy ceilings on this MI355X for the access shapes the fan-out uses.
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include <vector>
+#include <string>
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool NT>
+// grid-stride, one 16-B word per lane per iteration (1 KiB per wave instruction)
+template <bool NT, int UNROLL>
 __global__ __launch_bounds__(256) void k_write(u32x4* out, size_t nwords) {
+    const size_t stride = (size_t)gridDim.x * 256;
     size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
     u32x4 v = {(unsigned)i, 1u, 2u, 3u};
-    for (; i < nwords; i += (size_t)gridDim.x * 256) {
-        if (NT) __builtin_nontemporal_store(v, &out[i]); else out[i] = v;
+    for (; i + (UNROLL - 1) * stride < nwords; i += UNROLL * stride) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+            if (NT) __builtin_nontemporal_store(v, &out[i + u * stride]); else out[i + u * stride] = v;
+        }
     }
+    for (; i < nwords; i += stride) out[i] = v;
+}
+
+// block-contiguous: each block owns a contiguous span and sweeps it 1 KiB per wave-instruction
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_write_span(u32x4* out, size_t nwords) {
+    const size_t per = (nwords + gridDim.x - 1) / gridDim.x;
+    const size_t b = blockIdx.x * per, e = min(nwords, b + per);
+    u32x4 v = {1u, 1u, 2u, 3u};
+    for (size_t i = b + threadIdx.x; i < e; i += THREADS) out[i] = v;
 }
 
 template <bool NT, int FAN>
@@ -25,6 +38,10 @@ __global__ __launch_bounds__(256) void k_fan(const u32x4* in, u32x4* out, size_t
             if (NT) __builtin_nontemporal_store(v, &out[f * stride + i]); else out[f * stride + i] = v;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_copy(const u32x4* in, u32x4* out, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) out[i] = in[i];
 }
 
 template <typename F>
@@ -42,15 +59,27 @@ static float timeit(F f) {
 int main() {
     const size_t bytes = 8ull << 30, nw = bytes / 16;
     u32x4* out; hipMalloc(&out, bytes);
-    u32x4* in; hipMalloc(&in, bytes / 16);
-    hipMemset(in, 1, bytes / 16);
-    int grid = 256 * 8;
-    float t0 = timeit([&] { hipLaunchKernelGGL((k_write<false>), dim3(grid), dim3(256), 0, 0, out, nw); });
-    float t1 = timeit([&] { hipLaunchKernelGGL((k_write<true>), dim3(grid), dim3(256), 0, 0, out, nw); });
+    u32x4* in; hipMalloc(&in, bytes / 2);
+    hipMemset(in, 1, bytes / 2);
+    std::string js = "{";
+    auto add = [&](const char* k, double gbs) { char buf[128]; snprintf(buf, sizeof buf, "%s\"%s\": %.1f", js.size() > 1 ? ", " : "", k, gbs); js += buf; };
+    for (int g : {4, 8, 16, 64}) {
+        int grid = 256 * g;
+        char name[64];
+        snprintf(name, sizeof name, "write_plain_g%d", g);
+        add(name, bytes / timeit([&] { hipLaunchKernelGGL((k_write<false, 1>), dim3(grid), dim3(256), 0, 0, out, nw); }) / 1e6);
+        snprintf(name, sizeof name, "write_plain_u4_g%d", g);
+        add(name, bytes / timeit([&] { hipLaunchKernelGGL((k_write<false, 4>), dim3(grid), dim3(256), 0, 0, out, nw); }) / 1e6);
+    }
+    add("write_nt_g8", bytes / timeit([&] { hipLaunchKernelGGL((k_write<true, 1>), dim3(2048), dim3(256), 0, 0, out, nw); }) / 1e6);
+    add("write_span256_g2048", bytes / timeit([&] { hipLaunchKernelGGL((k_write_span<256>), dim3(2048), dim3(256), 0, 0, out, nw); }) / 1e6);
+    add("write_span1024_g1024", bytes / timeit([&] { hipLaunchKernelGGL((k_write_span<1024>), dim3(1024), dim3(1024), 0, 0, out, nw); }) / 1e6);
+    add("memset_async", bytes / timeit([&] { hipMemsetAsync(out, 0, bytes, 0); }) / 1e6);
+    add("copy_4GiB_rw", 2.0 * (bytes / 2) / timeit([&] { hipLaunchKernelGGL(k_copy, dim3(2048), dim3(256), 0, 0, in, out, nw / 2); }) / 1e6);
     const size_t nin = nw / 16, stride = nin;
-    float t2 = timeit([&] { hipLaunchKernelGGL((k_fan<false, 16>), dim3(grid), dim3(256), 0, 0, in, out, nin, stride); });
-    float t3 = timeit([&] { hipLaunchKernelGGL((k_fan<true, 16>), dim3(grid), dim3(256), 0, 0, in, out, nin, stride); });
-    printf("{\"write_plain_GBps\": %.1f, \"write_nt_GBps\": %.1f, \"fan16_plain_GBps\": %.1f, \"fan16_nt_GBps\": %.1f}\n",
-           bytes / t0 / 1e6, bytes / t1 / 1e6, (bytes + bytes / 16) / t2 / 1e6, (bytes + bytes / 16) / t3 / 1e6);
+    add("fan16_plain", (bytes + bytes / 16) / timeit([&] { hipLaunchKernelGGL((k_fan<false, 16>), dim3(2048), dim3(256), 0, 0, in, out, nin, stride); }) / 1e6);
+    add("write_1GiB_plain_g8", (bytes / 8) / timeit([&] { hipLaunchKernelGGL((k_write<false, 1>), dim3(2048), dim3(256), 0, 0, out, nw / 8); }) / 1e6);
+    js += "}";
+    printf("%s\n", js.c_str());
     return 0;
 }
