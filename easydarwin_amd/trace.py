@@ -59,6 +59,11 @@ class Trace:
 
     # -- serialisation ------------------------------------------------------------------
     def to_bytes(self) -> bytes:
+        # PKT and TICK times drive the virtual clock and must not go back; a JOIN's time is
+        # informational (the join takes effect at the next TICK, like a new output being
+        # picked up by the next ReflectPackets).
+        times = [ev[1] for ev in self.events if ev[0] != JOIN]
+        assert all(a <= b for a, b in zip(times, times[1:])), "trace events must be time-ordered"
         out = [b"EDTR", struct.pack("<II", 1, len(self.sdps))]
         for s in self.sdps:
             b = s.encode()
