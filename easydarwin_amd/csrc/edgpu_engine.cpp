@@ -607,4 +607,55 @@ int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out
     return EDGPU_OK;
 }
 
+int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst, uint64_t cap,
+                   uint64_t* out_len, uint32_t* out_packets) {
+    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks || (!dst && cap))
+        return fail(EDGPU_BAD_ARGUMENT, "bad argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    SenderDev D;
+    HIP_CHECK(hipMemcpyAsync(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D),
+                             hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    if (out_len) *out_len = 0;
+    if (out_packets) *out_packets = 0;
+    if (D.key < 0 || (uint64_t)D.key >= D.head) return EDGPU_OK;
+    const uint64_t k = (uint64_t)D.key, n = D.head - k, pkcap = (uint64_t)D.pk_mask + 1;
+    const uint64_t bcap = ((uint64_t)D.word_mask + 1) * 16;
+    if (n > pkcap) return fail(EDGPU_RING_OVERFLOW, "GOP no longer in the packet ring");
+    std::vector<PktMeta> meta(n);
+    const PktMeta* dmeta = reinterpret_cast<const PktMeta*>(D.meta);
+    for (uint64_t i = 0; i < n;) {            // ring segments
+        const uint64_t pos = (k + i) & D.pk_mask, run = std::min(n - i, pkcap - pos);
+        HIP_CHECK(hipMemcpyAsync(&meta[i], dmeta + pos, run * sizeof(PktMeta), hipMemcpyDeviceToHost, x->stream));
+        i += run;
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    const uint64_t vb0 = meta[0].vbyte, span = D.vbyte_end - vb0;
+    if (span > bcap) return fail(EDGPU_RING_OVERFLOW, "GOP no longer in the byte ring");
+    std::vector<uint8_t> bytes(span);
+    const uint8_t* ring = reinterpret_cast<const uint8_t*>(D.ring);
+    for (uint64_t i = 0; i < span;) {
+        const uint64_t pos = (vb0 + i) & (bcap - 1), run = std::min(span - i, bcap - pos);
+        HIP_CHECK(hipMemcpyAsync(&bytes[i], ring + pos, run, hipMemcpyDeviceToHost, x->stream));
+        i += run;
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    uint64_t len = 0; uint32_t np = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (meta[i].len == 0) continue;
+        const uint64_t need = (uint64_t)meta[i].len + 4;
+        if (len + need > cap) return fail(EDGPU_OUT_OVERFLOW, "destination too small for the GOP");
+        dst[len] = 0x28;                                  // BUF_STX
+        dst[len + 1] = (uint8_t)(meta[i].len >> 8);
+        dst[len + 2] = (uint8_t)meta[i].len;
+        memcpy(dst + len + 3, &bytes[meta[i].vbyte - vb0 + 4], meta[i].len);
+        dst[len + 3 + meta[i].len] = 0x29;                // BUF_ETX
+        len += need;
+        np++;
+    }
+    if (out_len) *out_len = len;
+    if (out_packets) *out_packets = np;
+    return EDGPU_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,178 @@
+// reflector_adapter.cpp -- see reflector_adapter.h.
+#include "reflector_adapter.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace edgpu_reflector {
+
+Reflector::Reflector(const edgpu_config* cfg) {
+    fStatus = edgpu_ctx_create(cfg, &fCtx);
+}
+
+Reflector::~Reflector() {
+    if (fCtx) edgpu_ctx_destroy(fCtx);
+}
+
+int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession) {
+    if (!fCtx) return kRequestFailed;
+    uint32_t s = 0, n = 0;
+    int err = edgpu_session_add(fCtx, sdp.data(), (uint32_t)sdp.size(), udpPush ? 1 : 0, &s);
+    if (err) return err;
+    if ((err = edgpu_session_tracks(fCtx, s, &n))) return err;
+    if (fTracks.size() <= s) fTracks.resize(s + 1, 0);
+    fTracks[s] = n;
+    if (outSession) *outSession = s;
+    return kNoErr;
+}
+
+uint32_t Reflector::GetNumStreams(uint32_t session) const {
+    return session < fTracks.size() ? fTracks[session] : 0;
+}
+
+int Reflector::AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle) {
+    if (!fCtx) return kRequestFailed;
+    return edgpu_subscriber_add(fCtx, session, interleaved ? EDGPU_TRANSPORT_TCP : EDGPU_TRANSPORT_UDP, outHandle);
+}
+
+int Reflector::RemoveOutput(uint32_t handle) {
+    if (!fCtx) return kRequestFailed;
+    return edgpu_subscriber_remove(fCtx, handle);
+}
+
+void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
+                           bool isRTCP, int64_t nowMs) {
+    // ReflectorStream::PushPacket ignores empty packets (ReflectorStream.cpp:533); the
+    // '$' framing caps a pushed packet at 65535 bytes.
+    if (packetLen == 0 || track >= GetNumStreams(session)) return;
+    packetLen = std::min<uint32_t>(packetLen, 65535);
+    Pushed p;
+    p.session = session;
+    p.channel = (uint8_t)(2 * track + (isRTCP ? 1 : 0));
+    p.t = nowMs;
+    p.off = (uint32_t)fBytes.size();
+    p.len = packetLen;
+    fBytes.insert(fBytes.end(), packet, packet + packetLen);
+    fPushed.push_back(p);
+}
+
+int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
+    if (!fCtx) return kRequestFailed;
+    int err;
+    if (!fPushed.empty()) {
+        // group by session (stable: arrival order within a session) into 16-B slots with the
+        // packet 4 bytes in -- the edgpu_ingest batch layout
+        std::vector<uint32_t> order(fPushed.size());
+        for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return fPushed[a].session < fPushed[b].session; });
+        std::vector<edgpu_pkt_desc> desc(order.size());
+        std::vector<uint32_t> segOff, segSess;
+        uint64_t blobBytes = 0;
+        for (uint32_t i : order) {
+            const uint32_t clamped = std::min<uint32_t>(fPushed[i].len, 2060);
+            blobBytes += (clamped + 4 + 15) & ~15u;
+        }
+        std::vector<uint8_t> blob(std::max<uint64_t>(blobBytes, 16), 0);
+        uint64_t off = 0;
+        for (uint32_t k = 0; k < order.size(); k++) {
+            const Pushed& p = fPushed[order[k]];
+            if (segSess.empty() || segSess.back() != p.session) { segOff.push_back(k); segSess.push_back(p.session); }
+            const uint32_t clamped = std::min<uint32_t>(p.len, 2060);   // bytes past 2060 are never read
+            desc[k].slot = (uint32_t)(off / 16);
+            desc[k].len = (uint16_t)p.len;
+            desc[k].channel = p.channel;
+            desc[k].flags = 0;
+            desc[k].arrival_ms = p.t;
+            memcpy(&blob[off + 4], &fBytes[p.off], clamped);
+            off += (clamped + 4 + 15) & ~15u;
+        }
+        segOff.push_back((uint32_t)order.size());
+        err = edgpu_ingest(fCtx, desc.data(), (uint32_t)desc.size(), segOff.data(), segSess.data(),
+                           (uint32_t)segSess.size(), blob.data(), blobBytes, EDGPU_PTR_HOST);
+        if (err) return err;
+        if ((err = edgpu_keyframe_index(fCtx))) return err;
+        fPushed.clear();
+        fBytes.clear();
+    }
+    edgpu_fanout_result res;
+    if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
+    edgpu_tick_stats st;
+    if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
+    if (st.status) return st.status;
+    if (!sink || st.relayed_packets == 0) return kNoErr;
+    std::vector<edgpu_substream_out> subs(res.n_substreams);
+    std::vector<edgpu_out_desc> d(st.relayed_packets);
+    fArena.resize(st.arena_bytes);
+    if ((err = edgpu_copy_to_host(fCtx, subs.data(), res.substreams, subs.size() * sizeof(subs[0])))) return err;
+    if ((err = edgpu_copy_to_host(fCtx, d.data(), res.desc, d.size() * sizeof(d[0])))) return err;
+    if ((err = edgpu_copy_to_host(fCtx, fArena.data(), res.arena, fArena.size()))) return err;
+    for (const edgpu_substream_out& q : subs)
+        for (uint32_t i = 0; i < q.desc_count; i++) {
+            const edgpu_out_desc& o = d[q.desc_base + i];
+            err = sink->WritePacket(q.subscriber, q.track, q.kind != 0, q.transport == EDGPU_TRANSPORT_TCP,
+                                    &fArena[o.offset], o.len, o.packet_id);
+            if (err) return err;
+        }
+    return kNoErr;
+}
+
+// ---------------------------------------------------------------------------------------
+static const unsigned char kSTX = 0x28, kETX = 0x29;   // BUF_STX / BUF_ETX
+
+CKeyFrameCache::CKeyFrameCache(int len) : mem_size(len) {
+    _memory = (char*)malloc(mem_size);
+    curdatalen = 0;
+}
+
+CKeyFrameCache::~CKeyFrameCache() {
+    free(_memory);
+    _memory = nullptr;
+    mem_size = 0;
+    curdatalen = 0;
+}
+
+bool CKeyFrameCache::PutOnePacket(char* buf, int len, int nalutype, int start) {
+    if (buf == nullptr || len == 0) return false;
+    if (nalutype == 7 && start == 1) curdatalen = 0;          // a new SPS starts a new GOP
+    if (len + 4 > 5 * 1024) return false;                      // the reference's 5 KiB TLV scratch
+    unsigned char rec[5 * 1024];
+    rec[0] = kSTX;
+    rec[1] = (unsigned char)((unsigned)len >> 8);
+    rec[2] = (unsigned char)len;
+    memcpy(rec + 3, buf, len);
+    rec[3 + len] = kETX;
+    return SetBuf((char*)rec, len + 4);
+}
+
+bool CKeyFrameCache::GetOnePacket(char* outbuf, int& outLen, int curOffset) {
+    if (curOffset >= curdatalen) return false;
+    if ((unsigned char)_memory[curOffset] != kSTX) return false;
+    const int pkgLen = ((unsigned char)_memory[curOffset + 1] << 8) | (unsigned char)_memory[curOffset + 2];
+    if (pkgLen >= curdatalen) return false;
+    if ((unsigned char)_memory[curOffset + 3 + pkgLen] != kETX) return false;
+    memcpy(outbuf, _memory + curOffset + 3, pkgLen);
+    outLen = pkgLen;
+    return true;
+}
+
+bool CKeyFrameCache::SetBuf(char* frameBuf, int len) {
+    if (frameBuf == nullptr || len == 0) return false;
+    if (len + curdatalen > mem_size) return false;
+    memcpy(_memory + curdatalen, frameBuf, len);
+    curdatalen += len;
+    return true;
+}
+
+int CKeyFrameCache::LoadGOP(Reflector& r, uint32_t session, uint32_t track, uint32_t* outPackets) {
+    uint64_t n = 0;
+    uint32_t k = 0;
+    const int err = edgpu_gop_copy(r.Context(), session, track, (uint8_t*)_memory, (uint64_t)mem_size, &n, &k);
+    if (err) return err;
+    curdatalen = (int)n;
+    if (outPackets) *outPackets = k;
+    return kNoErr;
+}
+
+}  // namespace edgpu_reflector

@@ -1,0 +1,95 @@
+// reflector_adapter.h -- C++ module-side seams of QTSSReflectorModule, implemented on top of
+// the edgpu C ABI.  A reflector module built against this header keeps the reference's call
+// pattern (SURVEY.md §8.b "internal seams"):
+//
+//   reference                                         here
+//   ReflectorSession::SetupReflectorSession           Reflector::SetupReflectorSession
+//     (ReflectorSession.cpp:140-188)
+//   ReflectorSession::AddOutput / RemoveOutput        Reflector::AddOutput / RemoveOutput
+//     (ReflectorSession.cpp:209-279)
+//   ReflectorStream::PushPacket(char*, UInt32, bool)  Reflector::PushPacket (same arguments
+//     (ReflectorStream.cpp:529-576)                     plus the session/track it belongs to)
+//   ReflectorSocket::Run -> ReflectPackets            Reflector::ReflectPackets(now, sink)
+//     (ReflectorStream.cpp:1676-1714, 1024-1136)
+//   ReflectorOutput::WritePacket (pure virtual,       OutputSink::WritePacket, called once per
+//     ReflectorOutput.h:114) -> QTSS_Write ->           send-ready packet with the bytes already
+//     RTPStream::Write framing                           framed for the subscriber's transport
+//   CKeyFrameCache (keyframecache.h:45-72)            edgpu_reflector::CKeyFrameCache, same
+//                                                        public API + LoadGOP() from HBM
+//
+// Threading mirrors the reference: one Reflector per GPU; its calls are serialised by the
+// caller (the reference's per-stream fBucketMutex / demuxer mutex).
+#pragma once
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "edgpu.h"
+
+namespace edgpu_reflector {
+
+// QTSS_Error values (QTSS.h:61-76)
+enum { kNoErr = 0, kRequestFailed = -1, kBadArgument = -10, kWouldBlock = -14 };
+
+// The egress seam.  `wire` points at the bytes to put on the wire for this subscriber: the
+// UDP datagram, or the complete '$' ch BE16(len) + packet frame for an RTSP-interleaved
+// subscriber (RTSPSessionInterface.cpp:329-344).  Return kNoErr to continue.
+class OutputSink {
+public:
+    virtual ~OutputSink() {}
+    virtual int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved,
+                            const uint8_t* wire, uint32_t wireLen, uint32_t packetID) = 0;
+};
+
+class Reflector {
+public:
+    explicit Reflector(const edgpu_config* cfg = nullptr);
+    ~Reflector();
+    Reflector(const Reflector&) = delete;
+    Reflector& operator=(const Reflector&) = delete;
+
+    int  Status() const { return fStatus; }                 // construction result
+    // push session from its SDP; udpPush: RTCP arrives on a bound odd port (Q12/Q14)
+    int  SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession);
+    uint32_t GetNumStreams(uint32_t session) const;
+    // player joins every track of `session`; takes effect at the next ReflectPackets
+    int  AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle);
+    int  RemoveOutput(uint32_t handle);
+    // one pushed packet, exactly as ProcessRTPData hands it to ReflectorStream::PushPacket
+    void PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
+                    bool isRTCP, int64_t nowMs);
+    // ingest everything pushed since the last call, update the keyframe index, fan out at
+    // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order)
+    int  ReflectPackets(int64_t nowMs, OutputSink* sink);
+    edgpu_ctx* Context() { return fCtx; }
+
+private:
+    struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint32_t off, len; };
+    edgpu_ctx* fCtx = nullptr;
+    int fStatus = kRequestFailed;
+    std::vector<uint32_t> fTracks;                          // per session
+    std::vector<Pushed> fPushed;                            // arrival order
+    std::vector<uint8_t> fBytes;
+    std::vector<uint8_t> fArena;                            // host copy of one tick's output
+};
+
+// CKeyFrameCache with the reference's public API and TLV record format
+// ([0x28][BE16 len][bytes][0x29], keyframecache.cpp:103-143).  PutOnePacket/GetOnePacket/
+// SetBuf behave as in the reference except that PutOnePacket does not append to ./data.264
+// or rewrite buf[13] (debug side effects, keyframecache.cpp:25-50).  LoadGOP() fills the
+// cache from the GPU's GOP index (key pointer -> newest) instead of per-packet PutOnePacket.
+class CKeyFrameCache {
+public:
+    char* _memory;
+    int curdatalen;
+    int mem_size;
+
+    explicit CKeyFrameCache(int len);
+    ~CKeyFrameCache();
+    bool PutOnePacket(char* buf, int len, int nalutype, int start);
+    bool GetOnePacket(char* outbuf, int& outLen, int curOffset);
+    bool SetBuf(char* frameBuf, int len);
+    int  LoadGOP(Reflector& r, uint32_t session, uint32_t track, uint32_t* outPackets = nullptr);
+};
+
+}  // namespace edgpu_reflector

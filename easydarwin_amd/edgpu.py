@@ -25,7 +25,7 @@ EXPORTED = [
     "edgpu_ctx_destroy", "edgpu_sync", "edgpu_session_add", "edgpu_session_tracks",
     "edgpu_subscriber_add", "edgpu_subscriber_remove", "edgpu_ingest", "edgpu_keyframe_index",
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
-    "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times",
+    "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
 ]
 
 
@@ -130,6 +130,7 @@ def load(path: str = LIB_PATH):
         "edgpu_gop_span": (I32, [P, U32, U32, C.POINTER(U64), C.POINTER(U64)]),
         "edgpu_counters_get": (I32, [P, C.POINTER(Counters)]),
         "edgpu_kernel_times": (I32, [P, I32, C.POINTER(C.c_float), U32, C.POINTER(U32)]),
+        "edgpu_gop_copy": (I32, [P, U32, U32, P, U64, C.POINTER(U64), C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -244,6 +245,13 @@ class Context:
         p, b = C.c_uint64(), C.c_uint64()
         _check(self.lib.edgpu_gop_span(self.h, session, track, C.byref(p), C.byref(b)))
         return p.value, b.value
+
+    def gop_copy(self, session: int, track: int, cap: int = 8 << 20) -> tuple:
+        """CKeyFrameCache TLV image of the track's GOP (key pointer -> newest)."""
+        buf = np.empty(cap, dtype=np.uint8)
+        n, k = C.c_uint64(), C.c_uint32()
+        _check(self.lib.edgpu_gop_copy(self.h, session, track, _ptr(buf), cap, C.byref(n), C.byref(k)))
+        return buf[:n.value].tobytes(), k.value
 
     def copy_to_host(self, dev_ptr, nbytes: int) -> np.ndarray:
         out = np.empty(int(nbytes), dtype=np.uint8)

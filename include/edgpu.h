@@ -205,6 +205,14 @@ int  edgpu_last_timings(edgpu_ctx* ctx, float out_ms[4]);
 int  edgpu_gop_span(edgpu_ctx* ctx, uint32_t session, uint32_t track,
                     uint64_t* out_packets, uint64_t* out_bytes);
 
+/* Copies the GOP a joining subscriber of `session`/`track` would receive (key pointer ->
+ * newest, RTP sender) to host memory in CKeyFrameCache's TLV record format
+ * [0x28][BE16 len][packet][0x29] (CommonUtilitiesLib/keyframecache.cpp:103-143), so the
+ * keyframecache interface is served from the GPU's GOP index.  Empty packets (SSRC-filtered)
+ * are skipped.  Returns EDGPU_OUT_OVERFLOW if `cap` is too small.  Syncs. */
+int  edgpu_gop_copy(edgpu_ctx* ctx, uint32_t session, uint32_t track, uint8_t* dst, uint64_t cap,
+                    uint64_t* out_len, uint32_t* out_packets);
+
 #ifdef __cplusplus
 }
 #endif

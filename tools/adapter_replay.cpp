@@ -1,0 +1,104 @@
+// tools/adapter_replay.cpp -- drives the C++ module-side adapter (reflector_adapter.h) with an
+// event trace, the way the reflector module would: PKT -> Reflector::PushPacket (track =
+// channel/2, RTCP = channel&1, as ProcessRTPData does, QTSSReflectorModule.cpp:654-671),
+// JOIN -> AddOutput, TICK -> ReflectPackets(now, sink).  Writes the capture format of
+// easydarwin_amd/trace.py so tests compare it with the reference harness byte for byte.
+// Usage: adapter_replay <trace.edtr> <capture.edcp>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "reflector_adapter.h"
+
+using namespace edgpu_reflector;
+
+struct Rec { uint32_t sub = 0, session = 0; bool tcp = false; std::string img[2]; uint64_t n[2] = {0, 0}; };
+
+class CaptureSink : public OutputSink {
+public:
+    std::map<std::pair<uint32_t, uint16_t>, Rec>* recs;      // (handle, track)
+    int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
+                    uint32_t wireLen, uint32_t) override {
+        Rec& r = (*recs)[{subscriber, track}];
+        std::string& s = r.img[isRTCP ? 1 : 0];
+        if (!interleaved) { s.push_back((char)(wireLen >> 8)); s.push_back((char)wireLen); }
+        s.append((const char*)wire, wireLen);
+        r.n[isRTCP ? 1 : 0]++;
+        return kNoErr;
+    }
+};
+
+int main(int argc, char** argv) {
+    if (argc != 3) { fprintf(stderr, "usage: %s trace capture\n", argv[0]); return 2; }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) { perror(argv[1]); return 2; }
+    std::vector<uint8_t> d;
+    fseek(f, 0, SEEK_END); d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
+    if (fread(d.data(), 1, d.size(), f) != d.size()) return 2;
+    fclose(f);
+    size_t p = 4;
+    auto get = [&](auto& v) { memcpy(&v, &d[p], sizeof(v)); p += sizeof(v); };
+    uint32_t ver, nsess;
+    get(ver); get(nsess);
+    Reflector R;
+    if (R.Status()) { fprintf(stderr, "edgpu: %s\n", edgpu_last_error()); return 3; }
+    for (uint32_t s = 0; s < nsess; s++) {
+        uint32_t n; get(n);
+        uint32_t sid;
+        if (R.SetupReflectorSession(std::string((const char*)&d[p], n), false, &sid)) return 3;
+        p += n;
+    }
+    std::map<std::pair<uint32_t, uint16_t>, Rec> recs;
+    std::map<uint32_t, std::tuple<uint32_t, uint32_t, bool>> handles;   // handle -> (sub, session, tcp)
+    CaptureSink sink;
+    sink.recs = &recs;
+    while (p < d.size()) {
+        uint8_t type; get(type);
+        if (type == 0) break;
+        int64_t t; get(t);
+        if (type == 1) {
+            uint32_t s, len; uint8_t ch;
+            get(s); get(ch); get(len);
+            R.PushPacket(s, ch / 2, (const char*)&d[p], len, ch & 1, t);
+            p += len;
+        } else if (type == 2) {
+            uint32_t s, sub; uint8_t tr, ua;
+            get(s); get(sub); get(tr); get(ua);
+            uint32_t h;
+            if (R.AddOutput(s, tr != 0, &h)) return 3;
+            handles[h] = std::make_tuple(sub, s, tr != 0);
+            for (uint16_t x = 0; x < R.GetNumStreams(s); x++) recs[{h, x}];
+        } else if (type == 3) {
+            int err = R.ReflectPackets(t, &sink);
+            if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
+        } else return 3;
+    }
+    std::vector<std::tuple<uint32_t, uint16_t, Rec*>> out;
+    for (auto& kv : recs) {
+        Rec& r = kv.second;
+        auto h = handles[kv.first.first];
+        r.sub = std::get<0>(h); r.session = std::get<1>(h); r.tcp = std::get<2>(h);
+        out.emplace_back(r.sub, kv.first.second, &r);
+    }
+    std::stable_sort(out.begin(), out.end(), [](auto& a, auto& b) {
+        return std::get<0>(a) != std::get<0>(b) ? std::get<0>(a) < std::get<0>(b) : std::get<1>(a) < std::get<1>(b); });
+    FILE* o = fopen(argv[2], "wb");
+    fwrite("EDCP", 1, 4, o);
+    uint32_t n = (uint32_t)out.size() * 2;
+    fwrite(&n, 4, 1, o);
+    for (auto& e : out)
+        for (int k = 0; k < 2; k++) {
+            Rec& r = *std::get<2>(e);
+            uint16_t tr = std::get<1>(e);
+            uint8_t kind = (uint8_t)k, tcp = r.tcp;
+            uint64_t np = r.n[k], nb = r.img[k].size();
+            fwrite(&r.sub, 4, 1, o); fwrite(&r.session, 4, 1, o); fwrite(&tr, 2, 1, o);
+            fwrite(&kind, 1, 1, o); fwrite(&tcp, 1, 1, o); fwrite(&np, 8, 1, o); fwrite(&nb, 8, 1, o);
+            fwrite(r.img[k].data(), 1, nb, o);
+        }
+    fclose(o);
+    return 0;
+}
