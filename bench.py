@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from easydarwin_amd import edgpu  # noqa: E402
+from easydarwin_amd.dist import reduce_run  # noqa: E402
 from easydarwin_amd.workload import H264Fleet, shard_sessions  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
@@ -201,15 +202,7 @@ def main():
     launches = c1["fanout_launches"] - c0["fanout_launches"]
     alg_bytes = out_bytes + in_bytes + 16 * relayed      # SURVEY.md §8.d per-launch definition
 
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        tot = torch.tensor([relayed, out_bytes, in_bytes], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        relayed_all, out_all = int(tot[0].item()), int(tot[1].item())
-    else:
-        relayed_all, out_all = relayed, out_bytes
+    dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev)
 
     if rank != 0:
         if dist:

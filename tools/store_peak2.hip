@@ -35,6 +35,27 @@ __global__ __launch_bounds__(T) void k_b(const u32x4* in, u32x4* out, size_t nin
         }
     }
 }
+// C: chunk-major layout: chunk c's 16 copies are adjacent (block writes 16*CW contiguous)
+template <int T, int NW>
+__global__ __launch_bounds__(T) void k_c(const u32x4* in, u32x4* out, size_t nin) {
+    const size_t cw = (size_t)T * NW;
+    for (size_t c = blockIdx.x; c * cw < nin; c += gridDim.x) {
+        u32x4 r[NW];
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            size_t i = c * cw + j * T + threadIdx.x;
+            r[j] = i < nin ? in[i] : u32x4{0, 0, 0, 0};
+        }
+        u32x4* o = out + c * cw * 16;
+        for (int f = 0; f < 16; f++) {
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                size_t i = c * cw + j * T + threadIdx.x;
+                if (i < nin) o[f * cw + j * T + threadIdx.x] = r[j];
+            }
+        }
+    }
+}
 template <typename F>
 static float timeit(F f) {
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
@@ -64,6 +85,11 @@ int main() {
     add("B256x2_read_odd_g4096", timeit([&] { hipLaunchKernelGGL((k_b<256, 2, true>), dim3(4096), dim3(256), 0, 0, in, out, nin, s_odd); }));
     add("B256x2_noread_odd_g4096", timeit([&] { hipLaunchKernelGGL((k_b<256, 2, false>), dim3(4096), dim3(256), 0, 0, in, out, nin, s_odd); }));
     add("B1024x4_read_odd_g256", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(256), dim3(1024), 0, 0, in, out, nin, s_odd); }));
+    add("B512x6_read_s528k", timeit([&] { hipLaunchKernelGGL((k_b<512, 6, true>), dim3(512), dim3(512), 0, 0, in, out, nin, (size_t)33000); }));
+    add("C512x6_read", timeit([&] { hipLaunchKernelGGL((k_c<512, 6>), dim3(512), dim3(512), 0, 0, in, out, nin); }));
+    add("C512x6_read_g2048", timeit([&] { hipLaunchKernelGGL((k_c<512, 6>), dim3(2048), dim3(512), 0, 0, in, out, nin); }));
+    add("C1024x4_read_g256", timeit([&] { hipLaunchKernelGGL((k_c<1024, 4>), dim3(256), dim3(1024), 0, 0, in, out, nin); }));
+    add("C256x8_read_g2048", timeit([&] { hipLaunchKernelGGL((k_c<256, 8>), dim3(2048), dim3(256), 0, 0, in, out, nin); }));
     js += "}";
     printf("%s\n", js.c_str());
     return 0;
