@@ -669,7 +669,7 @@ void k_fanout2(FanoutParams P) {
     __shared__ uint32_t m_len[CHUNK];
     __shared__ uint32_t m_vc[CHUNK];
     __shared__ uint32_t startmap[(CWORDS + 31) / 32];
-    // per sub-stream (batch of THREADS) parameters
+    // per sub-stream parameters (one batch of up to THREADS sub-streams)
     __shared__ int64_t  q_dw0[THREADS];      // arena word of chunk word 0
     __shared__ int64_t  q_off[THREADS];      // out_base - vstart (+4 for UDP)
     __shared__ uint32_t q_fw[THREADS];       // first chunk word to write (>= nwords: skip)
@@ -688,6 +688,7 @@ void k_fanout2(FanoutParams P) {
         const uint64_t head = D.head;
         const uint32_t np = (uint32_t)min((uint64_t)CHUNK, head - lo);
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        // ---- phase 1: packet metadata of the chunk -> LDS --------------------------------
         if (tid < (int)np) {
             const PktMeta m = meta[(lo + tid) & D.pk_mask];
             m_vb[tid] = m.vbyte; m_id[tid] = (uint32_t)m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
@@ -697,44 +698,16 @@ void k_fanout2(FanoutParams P) {
         for (int k = tid; k < (int)((CWORDS + 31) / 32); k += THREADS) startmap[k] = 0;
         __syncthreads();
         const uint64_t vb0 = m_vb[0];
-        const uint32_t nwords = (uint32_t)((m_vb[np] - vb0) >> 4);
+        const uint32_t nw = uni((uint32_t)((m_vb[np] - vb0) >> 4));
         if (tid < (int)np && m_len[tid] != 0) {
             const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
             atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
         }
-        __syncthreads();
-        // Chunk load: buffer loads through a descriptor built from wave-uniform values, so
-        // each lane needs one 32-bit offset; lanes past the chunk read 0 (range check).
-        const uint32_t wmask = uni(D.word_mask);
-        const uint32_t nw = uni(nwords);
-        const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
-        const bool wraps = rstart + nw > wmask + 1;
-        u32x4 r[NW];
-        if (!wraps) {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<u32x4*>(D.ring) + rstart, 0, nw * 16, 0x00020000);
-#pragma unroll
-            for (int j = 0; j < NW; j++)
-                r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(tid + j * THREADS) * 16u, 0, 0);
-        } else {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<u32x4*>(D.ring), 0, (wmask + 1) * 16, 0x00020000);
-#pragma unroll
-            for (int j = 0; j < NW; j++) {
-                const uint32_t wi = tid + j * THREADS;
-                r[j] = wi < nw ? __builtin_amdgcn_raw_buffer_load_b128(rs, ((rstart + wi) & wmask) * 16u, 0, 0)
-                               : u32x4{0u, 0u, 0u, 0u};
-            }
-        }
-        uint32_t smask = 0;
-#pragma unroll
-        for (int j = 0; j < NW; j++) {
-            const uint32_t wi = tid + j * THREADS;
-            if (wi < nw) smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
-        }
         const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
         for (uint32_t q0 = qb; q0 < qe; q0 += THREADS) {
             const uint32_t nq = min((uint32_t)THREADS, qe - q0);
+            // ---- phase 2: this batch's sub-stream parameters -> LDS (before the chunk is
+            // loaded, so this 64-bit bookkeeping never overlaps the live chunk registers) ----
             if (tid < (int)nq) {
                 const SubDev& Q = P.subs[P.sub_index[q0 + tid]];
                 uint32_t fw = 0xFFFFFFFFu, p0 = 0xFFFFFFFFu;
@@ -752,6 +725,35 @@ void k_fanout2(FanoutParams P) {
                 q_hl[tid] = Q.transport ? 4u : 0u;
             }
             __syncthreads();
+            // ---- phase 3: the chunk HBM -> VGPRs, once ------------------------------------
+            // Buffer loads through a descriptor built from wave-uniform values: one 32-bit
+            // offset per lane, lanes past the chunk read 0 (range check).
+            const uint32_t wmask = uni(D.word_mask);
+            const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
+            const bool wraps = rstart + nw > wmask + 1;
+            u32x4 r[NW];
+            if (!wraps) {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<u32x4*>(D.ring) + rstart, 0, nw * 16, 0x00020000);
+#pragma unroll
+                for (int j = 0; j < NW; j++)
+                    r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(tid + j * THREADS) * 16u, 0, 0);
+            } else {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<u32x4*>(D.ring), 0, (wmask + 1) * 16, 0x00020000);
+#pragma unroll
+                for (int j = 0; j < NW; j++) {
+                    const uint32_t wi = tid + j * THREADS;
+                    r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu, 0, 0);
+                }
+            }
+            uint32_t smask = 0;
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                const uint32_t wi = tid + j * THREADS;
+                if (wi < nw) smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
+            }
+            // ---- phase 4: write the chunk to every sub-stream ------------------------------
             for (uint32_t q = 0; q < nq; q++) {
                 const uint32_t fw = uni(q_fw[q]);
                 if (fw >= nw) continue;
@@ -773,7 +775,7 @@ void k_fanout2(FanoutParams P) {
                     }
                 }
             }
-            // descriptors: one lane per (sub-stream, packet)
+            // ---- phase 5: descriptors, one lane per (sub-stream, packet); chunk regs dead ---
             for (uint32_t t = tid; t < nq * np; t += THREADS) {
                 const uint32_t q = t / np, p = t - q * np;
                 if (p < q_p0[q] || m_len[p] == 0) continue;
