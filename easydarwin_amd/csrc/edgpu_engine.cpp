@@ -80,7 +80,8 @@ struct edgpu_ctx {
     edgpu_config cfg;
     int device = 0;
     int num_cus = 256;
-    int fanout_variant = 2;
+    int fanout_variant = 3;
+    uint32_t ablate = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
@@ -192,6 +193,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
+    if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
     *out = x;
     return EDGPU_OK;
 }
@@ -498,6 +500,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
     f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
     f.totals = x->d_totals;
+    f.ablate = x->ablate;
     HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
     HIP_CHECK(hist_mark(x, 0, 0));
     HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, x->stream));

@@ -754,7 +754,7 @@ void k_fanout2(FanoutParams P) {
                 if (wi < nw) smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
             }
             // ---- phase 4: write the chunk to every sub-stream ------------------------------
-            for (uint32_t q = 0; q < nq; q++) {
+            for (uint32_t q = 0; q < nq && !(P.ablate & 2u); q++) {
                 const uint32_t fw = uni(q_fw[q]);
                 if (fw >= nw) continue;
                 // Store descriptor over this sub-stream's part of the chunk [fw, nw): lanes
@@ -776,7 +776,7 @@ void k_fanout2(FanoutParams P) {
                 }
             }
             // ---- phase 5: descriptors, one lane per (sub-stream, packet); chunk regs dead ---
-            for (uint32_t t = tid; t < nq * np; t += THREADS) {
+            for (uint32_t t = tid; t < (P.ablate & 1u ? 0u : nq * np); t += THREADS) {
                 const uint32_t q = t / np, p = t - q * np;
                 if (p < q_p0[q] || m_len[p] == 0) continue;
                 const uint32_t len = m_len[p];
@@ -793,6 +793,164 @@ void k_fanout2(FanoutParams P) {
         }
     }
     // block reduction of the byte counters
+    unsigned long long a = wire, b = inb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+    if ((tid & 63) == 0) s_red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) s_red[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
+    }
+}
+
+// -----------------------------------------------------------------------------------------
+// k_fanout3: LDS-staged, line-aligned write-many.  The chunk is loaded from HBM into LDS once;
+// for every sub-stream each lane then reads the word that lands on its lane of a 128-B-
+// aligned destination window (the realignment is a per-sub-stream shift of the LDS read
+// index), so every 1 KiB wave store covers whole cache lines.  A 16-B misaligned
+// destination costs ~30 % of write bandwidth on MI355X (tools/store_peak2.hip), and the
+// sub-streams' pieces start at arbitrary 16-B offsets.  TCP channel bytes are patched in
+// registers before the single store.
+// -----------------------------------------------------------------------------------------
+template <int THREADS, int CHUNK>
+constexpr int fanout3_lds() {
+    return CHUNK * 129 * 16 + (CHUNK + 2) * 8 + CHUNK * 12 + ((((CHUNK * 129 + 31) / 32) + 3) & ~3) * 4 +
+           (THREADS < 256 ? THREADS : 256) * 36 + (THREADS / 64) * 8;
+}
+
+template <int THREADS, int CHUNK>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
+void k_fanout3(FanoutParams P) {
+    constexpr int CWORDS = CHUNK * 129;
+    constexpr int NW = (CWORDS + 7 + THREADS - 1) / THREADS;
+    constexpr int NWAVES = THREADS / 64;
+    constexpr int QB = THREADS < 256 ? THREADS : 256;                  // sub-streams per LDS batch
+    const uint32_t nwork = P.totals->nwork;
+    if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    // All LDS is one dynamic region carved at 16-B-aligned offsets (Guideline 17: no static
+    // __shared__ in front of it), so the ds_read_b128 of the chunk words stay aligned.
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int SM = ((CWORDS + 31) / 32 + 3) & ~3;                  // startmap words, x4
+    u32x4* cbuf = reinterpret_cast<u32x4*>(lds);                       // CWORDS words
+    uint64_t* m_vb = reinterpret_cast<uint64_t*>(cbuf + CWORDS);       // CHUNK + 2
+    uint32_t* m_id = reinterpret_cast<uint32_t*>(m_vb + CHUNK + 2);    // CHUNK (multiple of 4)
+    uint32_t* m_len = m_id + CHUNK;
+    uint32_t* m_vc = m_len + CHUNK;
+    uint32_t* startmap = m_vc + CHUNK;                                 // SM
+    int64_t* q_dw0 = reinterpret_cast<int64_t*>(startmap + SM);        // QB
+    int64_t* q_off = q_dw0 + QB;
+    uint32_t* q_fw = reinterpret_cast<uint32_t*>(q_off + QB);
+    uint32_t* q_ch = q_fw + QB;
+    uint32_t* q_db = q_ch + QB;
+    uint32_t* q_p0 = q_db + QB;
+    uint32_t* q_hl = q_p0 + QB;
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(q_hl + QB);   // NWAVES
+    unsigned long long wire = 0, inb = 0;
+    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const WorkItem it = P.work[w];
+        const SenderDev& D = P.senders[it.sender];
+        const uint64_t lo = D.umin + (uint64_t)it.chunk * CHUNK;
+        const uint64_t head = D.head;
+        const uint32_t np = (uint32_t)min((uint64_t)CHUNK, head - lo);
+        const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        if (tid < (int)np) {
+            const PktMeta m = meta[(lo + tid) & D.pk_mask];
+            m_vb[tid] = m.vbyte; m_id[tid] = (uint32_t)m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
+            inb += m.len;
+        }
+        if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
+        for (int k = tid; k < (int)((CWORDS + 31) / 32); k += THREADS) startmap[k] = 0;
+        __syncthreads();
+        const uint64_t vb0 = m_vb[0];
+        const uint32_t nw = uni((uint32_t)((m_vb[np] - vb0) >> 4));
+        if (tid < (int)np && m_len[tid] != 0) {
+            const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
+            atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
+        }
+        // chunk HBM -> LDS (buffer loads, one 32-bit offset per lane; wrap handled per word)
+        {
+            const uint32_t wmask = uni(D.word_mask);
+            const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
+            const bool wraps = rstart + nw > wmask + 1;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<u32x4*>(D.ring) + (wraps ? 0u : rstart), 0,
+                wraps ? (wmask + 1) * 16 : nw * 16, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < (CWORDS + THREADS - 1) / THREADS; j++) {
+                const uint32_t wi = tid + j * THREADS;
+                if (wi < nw)
+                    cbuf[wi] = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (wraps ? ((rstart + wi) & wmask) : wi) * 16u, 0, 0);
+            }
+        }
+        const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
+        for (uint32_t q0 = qb; q0 < qe; q0 += QB) {
+            const uint32_t nq = min((uint32_t)QB, qe - q0);
+            if (tid < (int)nq) {
+                const SubDev& Q = P.subs[P.sub_index[q0 + tid]];
+                uint32_t fw = 0xFFFFFFFFu, p0 = 0xFFFFFFFFu;
+                if (Q.nonempty && Q.a < lo + np) {
+                    const uint64_t first = Q.a > lo ? Q.a : lo;
+                    p0 = (uint32_t)(first - lo);
+                    fw = (uint32_t)((m_vb[p0] - vb0) >> 4);
+                }
+                q_fw[tid] = fw;
+                q_p0[tid] = p0;
+                q_dw0[tid] = (int64_t)(Q.out_base >> 4) + ((int64_t)(vb0 - Q.vstart) >> 4);
+                q_off[tid] = (int64_t)(Q.out_base - Q.vstart) + (Q.transport ? 0 : 4);
+                q_ch[tid] = Q.transport ? ((uint32_t)Q.channel << 8) : 0u;
+                q_db[tid] = Q.desc_base - Q.vcstart;
+                q_hl[tid] = Q.transport ? 4u : 0u;
+            }
+            __syncthreads();
+            for (uint32_t q = 0; q < nq && !(P.ablate & 2u); q++) {
+                const uint32_t fw = uni(q_fw[q]);
+                if (fw >= nw) continue;
+                const int64_t A = (int64_t)uni64((uint64_t)q_dw0[q]) + fw;     // first dest word
+                const uint32_t s = (uint32_t)(A & 7);                          // words past a 128-B line
+                // descriptor from the exact first word; lanes below it get a wrapped (huge)
+                // offset and are dropped by the range check, as are lanes past the chunk
+                const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
+                    out + A, 0, (nw - fw) * 16, 0x00020000);
+                const uint32_t chbits = uni(q_ch[q]);
+#pragma unroll
+                for (int j = 0; j < NW; j++) {
+                    const uint32_t lane_w = tid + j * THREADS;               // word in the aligned window
+                    const uint32_t src = fw + lane_w - s;                    // chunk word it carries
+                    const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
+                    u32x4 v = cbuf[srcc];
+                    if (chbits && ((startmap[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chbits;
+                    __builtin_amdgcn_raw_buffer_store_b128(v, os, (lane_w - s) * 16u, 0, 0);
+                }
+            }
+            for (uint32_t t = tid; t < (P.ablate & 1u ? 0u : nq * np); t += THREADS) {
+                const uint32_t q = t / np, p = t - q * np;
+                if (p < q_p0[q] || m_len[p] == 0) continue;
+                const uint32_t len = m_len[p];
+                const uint64_t off = (uint64_t)(q_off[q] + (int64_t)m_vb[p]);
+                const uint32_t wlen = len + q_hl[q];
+                const uint32_t di = q_db[q] + m_vc[p];
+                u32x4 dv;
+                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
+                reinterpret_cast<u32x4*>(P.desc)[di] = dv;
+                wire += wlen;
+            }
+            __syncthreads();
+        }
+    }
     unsigned long long a = wire, b = inb;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
@@ -840,22 +998,26 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
 }
 // Fan-out variants (EDGPU_FANOUT env var, for A/B measurement).  Each entry: kernel,
 // threads per workgroup, packets per work item.
-static int occupancy_of(const void* fn, int threads) {
+static int occupancy_of(const void* fn, int threads, int lds) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, lds) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }
-struct FanoutVariant { const void* fn; int threads; int chunk; };
+struct FanoutVariant { const void* fn; int threads; int chunk; int lds; };
 static const FanoutVariant kVariants[] = {
-    {(const void*)k_fanout, kFanoutThreads, kChunkPackets},                         // 0 legacy
-    {(const void*)k_fanout2<512, 32, true, 1>, 512, 32},                            // 1 nt
-    {(const void*)k_fanout2<512, 32, false, 1>, 512, 32},                           // 2
-    {(const void*)k_fanout2<1024, 32, false, 1>, 1024, 32},                         // 3
-    {(const void*)k_fanout2<512, 32, false, 6>, 512, 32},                           // 4
-    {(const void*)k_fanout2<512, 32, false, 8>, 512, 32},                           // 5
-    {(const void*)k_fanout2<256, 16, false, 8>, 256, 16},                           // 6
-    {(const void*)k_fanout2<512, 16, false, 8>, 512, 16},                           // 7
-    {(const void*)k_fanout2<1024, 32, false, 8>, 1024, 32},                         // 8
+    {(const void*)k_fanout, kFanoutThreads, kChunkPackets, 0},                      // 0 legacy
+    {(const void*)k_fanout2<512, 32, true, 1>, 512, 32, 0},                         // 1 nt
+    {(const void*)k_fanout2<512, 32, false, 1>, 512, 32, 0},                        // 2
+    {(const void*)k_fanout2<1024, 32, false, 1>, 1024, 32, 0},                      // 3
+    {(const void*)k_fanout2<512, 32, false, 6>, 512, 32, 0},                        // 4
+    {(const void*)k_fanout2<512, 32, false, 8>, 512, 32, 0},                        // 5
+    {(const void*)k_fanout2<256, 16, false, 8>, 256, 16, 0},                        // 6
+    {(const void*)k_fanout2<512, 16, false, 8>, 512, 16, 0},                        // 7
+    {(const void*)k_fanout2<1024, 32, false, 8>, 1024, 32, 0},                      // 8
+    {(const void*)k_fanout3<1024, 32>, 1024, 32, fanout3_lds<1024, 32>()},          // 9  LDS, aligned
+    {(const void*)k_fanout3<512, 32>, 512, 32, fanout3_lds<512, 32>()},             // 10
+    {(const void*)k_fanout3<512, 16>, 512, 16, fanout3_lds<512, 16>()},             // 11
+    {(const void*)k_fanout3<256, 16>, 256, 16, fanout3_lds<256, 16>()},             // 12
 };
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 int fanout_chunk(int variant) {
@@ -864,10 +1026,13 @@ int fanout_chunk(int variant) {
 }
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
     if (variant < 0 || variant >= kNumVariants) variant = 2;
-    static int occ[16] = {0};
+    static int occ[32] = {0};
     const FanoutVariant& v = kVariants[variant];
-    if (!occ[variant]) occ[variant] = occupancy_of(v.fn, v.threads);
+    if (!occ[variant]) {
+        if (v.lds > 48 * 1024) (void)hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, v.lds);
+        occ[variant] = occupancy_of(v.fn, v.threads, v.lds);
+    }
     void* args[] = {(void*)&p};
-    return hipLaunchKernel(v.fn, dim3(num_cus * occ[variant]), dim3(v.threads), args, 0, st);
+    return hipLaunchKernel(v.fn, dim3(num_cus * occ[variant]), dim3(v.threads), args, v.lds, st);
 }
 }  // namespace edgpu

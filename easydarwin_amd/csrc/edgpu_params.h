@@ -53,6 +53,7 @@ struct FanoutParams {
     uint8_t* arena;
     edgpu_out_desc* desc;
     TickTotals* totals;
+    uint32_t ablate;            // timing-only builds: bit0 skip descriptors, bit1 skip arena stores
 };
 
 }  // namespace edgpu

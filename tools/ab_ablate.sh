@@ -1,0 +1,9 @@
+#!/bin/bash
+# Ablation timing (GPU box): fan-out variant $2 with EDGPU_ABLATE = 0 (full), 1 (no
+# descriptors), 2 (no arena stores), 3 (neither).  Outputs are wrong in 1-3: timing only.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; V=$2
+mkdir -p $R/gpurun_out/$TAG
+for a in 0 1 2 3; do
+  EDGPU_FANOUT=$V EDGPU_ABLATE=$a timeout -k 10 300 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline > $R/gpurun_out/$TAG/a$a.json 2> $R/gpurun_out/$TAG/a$a.err || exit 1
+done

@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void k_a(const u32x4* in, u32x4* out, size_t n
 // B: block-chunked like k_fanout2: block owns chunk of CW words (register staged), writes the
 // chunk to 16 destinations one after the other (each a contiguous span)
 template <int T, int NW, bool READ>
-__global__ __launch_bounds__(T) void k_b(const u32x4* in, u32x4* out, size_t nin, size_t stride) {
+__global__ __launch_bounds__(T) void k_b(const u32x4* in, u32x4* out, size_t nin, size_t stride, size_t mis = 0) {
     const size_t cw = (size_t)T * NW;
     for (size_t c = blockIdx.x; c * cw < nin; c += gridDim.x) {
         u32x4 r[NW];
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(T) void k_b(const u32x4* in, u32x4* out, size_t nin
 #pragma unroll
             for (int j = 0; j < NW; j++) {
                 size_t i = c * cw + j * T + threadIdx.x;
-                if (i < nin) out[f * stride + i] = r[j];
+                if (i < nin) out[f * stride + i + mis * (f + 1)] = r[j];
             }
         }
     }
@@ -90,6 +90,11 @@ int main() {
     add("C512x6_read_g2048", timeit([&] { hipLaunchKernelGGL((k_c<512, 6>), dim3(2048), dim3(512), 0, 0, in, out, nin); }));
     add("C1024x4_read_g256", timeit([&] { hipLaunchKernelGGL((k_c<1024, 4>), dim3(256), dim3(1024), 0, 0, in, out, nin); }));
     add("C256x8_read_g2048", timeit([&] { hipLaunchKernelGGL((k_c<256, 8>), dim3(2048), dim3(256), 0, 0, in, out, nin); }));
+    add("B1024x4_read_odd_mis1", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(256), dim3(1024), 0, 0, in, out, nin, s_odd, (size_t)1); }));
+    add("B1024x4_read_odd_mis3", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(256), dim3(1024), 0, 0, in, out, nin, s_odd, (size_t)3); }));
+    add("B1024x4_read_odd_al", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(256), dim3(1024), 0, 0, in, out, nin, s_odd, (size_t)0); }));
+    add("B1024x4_read_odd_al_g512", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(512), dim3(1024), 0, 0, in, out, nin, s_odd, (size_t)0); }));
+    add("B1024x4_read_odd_mis1_g512", timeit([&] { hipLaunchKernelGGL((k_b<1024, 4, true>), dim3(512), dim3(1024), 0, 0, in, out, nin, s_odd, (size_t)1); }));
     js += "}";
     printf("%s\n", js.c_str());
     return 0;
