@@ -80,7 +80,7 @@ struct edgpu_ctx {
     edgpu_config cfg;
     int device = 0;
     int num_cus = 256;
-    int fanout_variant = 3;
+    int fanout_variant = 9;
     uint32_t ablate = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
