@@ -104,10 +104,10 @@ def cpu_baseline(args) -> dict | None:
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "cpu.edtr")
         tr.write(p)
-        # calibrate the repeat count to ~15 s of CPU replay
-        probe = json.loads(subprocess.run([exe, "--bench", p, str(threads), "1"], capture_output=True,
+        # calibrate the repeat count to ~15 s of CPU replay (the probe itself is warm)
+        probe = json.loads(subprocess.run([exe, "--bench", p, str(threads), "8"], capture_output=True,
                                           text=True, check=True).stdout)
-        rep = int(max(1, min(400, 15.0 / max(probe["seconds"], 1e-3))))
+        rep = int(max(1, min(5000, 8 * 15.0 / max(probe["seconds"], 1e-3))))
         out = subprocess.run([exe, "--bench", p, str(threads), str(rep)], capture_output=True, text=True,
                              check=True).stdout
     r = json.loads(out)
@@ -211,11 +211,15 @@ def main():
 
     fan_ms = float(np.mean(k_fan)) if k_fan else float("nan")
     achieved = (alg_bytes / max(launches, 1)) / (fan_ms / 1e3) / 1e9
+    # HBM traffic per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
+    # kernel and config (tools/profile.sh + tools/summarize_profile.py); null when absent
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
     if os.path.exists(pmc) and world == 1 and args.subs == 16 and args.sessions == 1024:
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc))
+            if pj.get("fanout_kernel") == "k_fanout3":
+                traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args)
@@ -239,7 +243,7 @@ def main():
         "relayed_GBps": round(out_all / dt / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_fanout", "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
+                     "kernel": "k_fanout3", "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
                      "avg_kernel_ms": round(fan_ms, 4)},
         "kernel_ms": {"fanout": round(fan_ms, 4),
                       "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,

@@ -41,11 +41,13 @@ for k in sorted(set(fetch) | set(write)):
                          "hbm_read_bytes": 2 * fk * 1024, "hbm_write_bytes": wk * 1024,
                          "hbm_bytes_per_launch": (2 * fk + wk) * 1024,
                          "avg_duration_ns_rocprof": avg_ns.get(k)}
-fan = res["kernels"].get("k_fanout", {})
+fan_name = next((k for k in res["kernels"] if k.startswith("k_fanout")), None)
+fan = res["kernels"].get(fan_name, {})
+res["fanout_kernel"] = fan_name
 res["hbm_bytes_per_launch"] = fan.get("hbm_bytes_per_launch")
 res["alg_bytes_per_launch"] = bench["roofline"]["alg_bytes_per_launch"]
 res["bench_avg_kernel_ms"] = bench["roofline"]["avg_kernel_ms"]
-res["rocprof_avg_kernel_ms"] = (avg_ns.get("k_fanout") or 0) / 1e6
+res["rocprof_avg_kernel_ms"] = (avg_ns.get(fan_name) or 0) / 1e6
 json.dump(res, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
 shutil.copy(os.path.join(run, "kt", "kt_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
 shutil.copy(os.path.join(run, "kt_bench.json"), os.path.join(prof, f"{tag}_bench.json"))
