@@ -115,6 +115,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __shared__ uint32_t p_src[kIngestThreads];
     __shared__ uint32_t p_slotb[kIngestThreads];
     __shared__ uint64_t p_vb[kIngestThreads];
+    __shared__ uint32_t p_wpre[kIngestThreads];
     __shared__ uint64_t scan64[4];
     __shared__ uint32_t scan32[4];
 
@@ -230,22 +231,25 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         p_slotb[tid] = slotb;
         p_vb[tid] = vb;
         __syncthreads();
-        // ---- copy packet bytes into the byte rings: one wave per packet, 16 B per lane ----
+        // ---- copy packet bytes into the byte rings: the chunk's slots are one flat list of
+        // 16-B words, every lane copies words (packet found by binary search of the word
+        // prefix in LDS), so lanes stay busy whatever the packet sizes ----
         {
-            const int lane = tid & 63, wid = tid >> 6;
-            for (uint32_t p = wid; p < n; p += kIngestThreads / 64) {
-                const uint32_t sb = p_slotb[p];
-                if (sb == 0) continue;
-                const uint32_t s = p_snd[p];
-                const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16);
-                u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
-                const uint64_t w0 = p_vb[p] >> 4;
-                const uint32_t wm = s_wmask[s];
-                for (uint32_t w = lane; w < sb / 16; w += 64) {
-                    u32x4 v = src[w];
-                    if (w == 0) v.x = slot_header(p_len[p]);
-                    ring[(w0 + w) & wm] = v;
+            uint32_t wtot;
+            const uint32_t wpre = block_exclusive_scan<uint32_t>(slotb >> 4, scan32, wtot);
+            p_wpre[tid] = wpre;
+            __syncthreads();
+            for (uint32_t w = tid; w < wtot; w += kIngestThreads) {
+                uint32_t lo = 0, hi = n;                  // last packet with p_wpre <= w
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (p_wpre[mid] <= w) lo = mid; else hi = mid;
                 }
+                const uint32_t p = lo, k = w - p_wpre[p];
+                const uint32_t s = p_snd[p];
+                u32x4 v = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16)[k];
+                if (k == 0) v.x = slot_header(p_len[p]);
+                reinterpret_cast<u32x4*>(s_ring[s])[((p_vb[p] >> 4) + k) & s_wmask[s]] = v;
             }
         }
         // ---- advance per-sender / per-stream state ----
@@ -824,7 +828,7 @@ void k_fanout2(FanoutParams P) {
 // -----------------------------------------------------------------------------------------
 template <int THREADS, int CHUNK>
 constexpr int fanout3_lds() {
-    return CHUNK * 129 * 16 + (CHUNK + 2) * 8 + CHUNK * 12 + ((((CHUNK * 129 + 31) / 32) + 3) & ~3) * 4 +
+    return CHUNK * 129 * 16 + (CHUNK + 2) * 8 + CHUNK * 16 + ((((CHUNK * 129 + 31) / 32) + 3) & ~3) * 4 +
            (THREADS < 256 ? THREADS : 256) * 36 + (THREADS / 64) * 8;
 }
 
@@ -847,7 +851,8 @@ void k_fanout3(FanoutParams P) {
     uint32_t* m_id = reinterpret_cast<uint32_t*>(m_vb + CHUNK + 2);    // CHUNK (multiple of 4)
     uint32_t* m_len = m_id + CHUNK;
     uint32_t* m_vc = m_len + CHUNK;
-    uint32_t* startmap = m_vc + CHUNK;                                 // SM
+    uint32_t* m_nzp = m_vc + CHUNK;                                    // CHUNK: ordinal -> packet
+    uint32_t* startmap = m_nzp + CHUNK;                                // SM
     int64_t* q_dw0 = reinterpret_cast<int64_t*>(startmap + SM);        // QB
     int64_t* q_off = q_dw0 + QB;
     uint32_t* q_fw = reinterpret_cast<uint32_t*>(q_off + QB);
@@ -879,6 +884,7 @@ void k_fanout3(FanoutParams P) {
         if (tid < (int)np && m_len[tid] != 0) {
             const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
             atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
+            m_nzp[m_vc[tid] - m_vc[0]] = tid;              // non-empty ordinal -> packet
         }
         // chunk HBM -> LDS (buffer loads, one 32-bit offset per lane; wrap handled per word)
         {
@@ -936,17 +942,32 @@ void k_fanout3(FanoutParams P) {
                     __builtin_amdgcn_raw_buffer_store_b128(v, os, (lane_w - s) * 16u, 0, 0);
                 }
             }
-            for (uint32_t t = tid; t < (P.ablate & 1u ? 0u : nq * np); t += THREADS) {
-                const uint32_t q = t / np, p = t - q * np;
-                if (p < q_p0[q] || m_len[p] == 0) continue;
-                const uint32_t len = m_len[p];
-                const uint64_t off = (uint64_t)(q_off[q] + (int64_t)m_vb[p]);
-                const uint32_t wlen = len + q_hl[q];
-                const uint32_t di = q_db[q] + m_vc[p];
-                u32x4 dv;
-                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
-                reinterpret_cast<u32x4*>(P.desc)[di] = dv;
-                wire += wlen;
+            // descriptors: one wave per sub-stream, lanes mapped onto a 128-B-aligned window of
+            // the sub-stream's descriptor array (8 descriptors per line)
+            {
+                const int lane = tid & 63, wv = tid >> 6;
+                // non-empty packets of this chunk: ordinals [0, nzc)
+                const uint32_t nzc = (uint32_t)__builtin_amdgcn_readfirstlane(
+                    (int)(np ? m_vc[np - 1] - m_vc[0] + (m_len[np - 1] != 0) : 0));
+                for (uint32_t q = wv; q < (P.ablate & 1u ? 0u : nq); q += NWAVES) {
+                    const uint32_t p0 = q_p0[q];
+                    if (p0 >= np) continue;
+                    const uint32_t o0 = m_vc[p0] - m_vc[0];                   // first ordinal
+                    if (o0 >= nzc) continue;
+                    const uint32_t d0 = q_db[q] + m_vc[p0];                   // its descriptor
+                    const uint32_t sh = d0 & 7;
+                    const uint32_t o = o0 + lane - sh;                        // ordinal of this lane
+                    if (lane >= (int)sh && o < nzc) {
+                        const uint32_t p = m_nzp[o];
+                        const uint32_t len = m_len[p];
+                        const uint64_t off = (uint64_t)(q_off[q] + (int64_t)m_vb[p]);
+                        const uint32_t wlen = len + q_hl[q];
+                        u32x4 dv;
+                        dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
+                        reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                        wire += wlen;
+                    }
+                }
             }
             __syncthreads();
         }
