@@ -82,6 +82,7 @@ struct edgpu_ctx {
     int num_cus = 256;
     int fanout_variant = 9;
     uint32_t ablate = 0;
+    uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
@@ -118,6 +119,7 @@ struct edgpu_ctx {
     uint8_t* d_blob = nullptr;
     uint32_t* d_pflags = nullptr;
     uint64_t* d_pidx = nullptr;
+    CopyJob* d_jobs = nullptr;
     // pending batch for keyframe_index
     const uint32_t* pend_seg = nullptr;
     const uint32_t* pend_seg_sess = nullptr;
@@ -188,12 +190,14 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipMalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
     if (hipMalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
     if (hipMalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
+    if (hipMalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
     if (hipMalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
     if (hipMalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
     if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
+    if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     *out = x;
     return EDGPU_OK;
 }
@@ -206,7 +210,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
-    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx,
+    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals})
         if (p) (void)hipFree(p);
     for (auto& e : x->ev) if (e) (void)hipEventDestroy(e);
@@ -439,6 +443,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
+    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = x->ingest_mode;
     p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;

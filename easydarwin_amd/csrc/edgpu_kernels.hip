@@ -55,6 +55,24 @@ __device__ bool key_frame_first_packet(const uint8_t* p, uint32_t len) {
     return t == 5 || t == 7 || t == 8;
 }
 
+// Header bytes held in registers: hdr[k] holds packet bytes 4k..4k+3 (little-endian).
+__device__ __forceinline__ uint32_t hbyte(const uint32_t* h, int i) { return (h[i >> 2] >> (8 * (i & 3))) & 0xFF; }
+__device__ __forceinline__ uint32_t hbe16(const uint32_t* h, int i) { return hbyte(h, i) << 8 | hbyte(h, i + 1); }
+__device__ __forceinline__ uint32_t hbe32(const uint32_t* h, int i) { return __builtin_bswap32(h[i >> 2]); }
+
+// key_frame_first_packet for the CSRC-free header (h = 12): every byte the rule can read
+// (12..21) is already in registers; reads past `len` are excluded by its own length guards
+// (len >= 20 here).
+__device__ __forceinline__ bool key_frame_first_packet_cc0(const uint32_t* h, uint32_t len) {
+    uint32_t t = hbyte(h, 12) & 0x1F;
+    if (t == 24) { if (len > 15) t = hbyte(h, 15) & 0x1F; }
+    else if (t == 25) { if (len > 17) t = hbyte(h, 17) & 0x1F; }
+    else if (t == 26) { if (len > 20) t = hbyte(h, 20) & 0x1F; }
+    else if (t == 27) { if (len > 21) t = hbyte(h, 21) & 0x1F; }
+    else if (t == 28 || t == 29) { if (len > 13 && (hbyte(h, 13) & 0x80)) t = hbyte(h, 13) & 0x1F; }
+    return t == 5 || t == 7 || t == 8;
+}
+
 // ReflectorPacket::GetSSRC (ReflectorStream.h:145-158)
 __device__ __forceinline__ uint32_t packet_ssrc(const uint8_t* p, uint32_t len, bool rtcp) {
     if (len < 8) return 0;
@@ -106,6 +124,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __shared__ uint64_t s_count[kMaxTracks];
     __shared__ uint64_t c_tot[kMaxSendersPerSession];
     __shared__ uint32_t c_ttot[kMaxTracks];
+    __shared__ int c_last[kMaxSendersPerSession];   // (tid << 10 | rank) of the chunk's newest non-empty packet
     // per packet of the current chunk
     __shared__ uint8_t p_snd[kIngestThreads];
     __shared__ uint8_t p_acc[kIngestThreads];
@@ -115,7 +134,6 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __shared__ uint32_t p_src[kIngestThreads];
     __shared__ uint32_t p_slotb[kIngestThreads];
     __shared__ uint64_t p_vb[kIngestThreads];
-    __shared__ uint32_t p_wpre[kIngestThreads];
     __shared__ uint64_t scan64[4];
     __shared__ uint32_t scan32[4];
 
@@ -134,10 +152,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         const uint32_t n = min((uint32_t)kIngestThreads, e - base);
         const uint32_t i = base + tid;
         const bool valid = (uint32_t)tid < n;
+        if (tid < (int)nsnd) c_last[tid] = -1;
         uint32_t len = 0, track = 0, ls = 0, fl = 0, slot = 0;
         int64_t arrival = 0;
         bool acc = false;
         const uint8_t* pk = nullptr;
+        uint32_t hdr[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};   // packet bytes 0..27, little-endian words
         if (valid) {
             const edgpu_pkt_desc d = P.desc[i];
             len = min((uint32_t)d.len, (uint32_t)kMaxPacket);
@@ -147,10 +167,17 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             slot = d.slot;
             acc = track < S.ntracks && len > 0;       // ProcessRTPData: inIndex < numStreams
             pk = P.blob + (uint64_t)slot * 16 + 4;
+            // the slot's first 32 bytes (packet bytes 0..27) in two 16-B loads: every header
+            // field the reflector reads for a CSRC-free packet comes from these registers
+            const u32x4* sw = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)slot * 16);
+            const u32x4 w0 = len > 0 ? sw[0] : u32x4{0u, 0u, 0u, 0u};
+            const u32x4 w1 = len > 12 ? sw[1] : u32x4{0u, 0u, 0u, 0u};
+            hdr[0] = w0.y; hdr[1] = w0.z; hdr[2] = w0.w; hdr[3] = w1.x;
+            hdr[4] = w1.y; hdr[5] = w1.z; hdr[6] = w1.w;
             if (acc) fl = s_flags[ls];
             // UDP push: socket B is the odd port, so only SRs survive (Q14)
             if (acc && (fl & kSndRtcpPort))
-                acc = len >= 8 && len >= 4 * be16(pk + 2) + 4 && (pk[0] >> 6) == 2 && pk[1] == 200;
+                acc = len >= 8 && len >= 4 * hbe16(hdr, 2) + 4 && (hbyte(hdr, 0) >> 6) == 2 && hbyte(hdr, 1) == 200;
             in_pk += 1;
             in_bytes += len;
         }
@@ -158,7 +185,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         p_acc[tid] = acc;
         p_len[tid] = (uint16_t)len;
         p_src[tid] = slot;
-        p_ssrc[tid] = acc ? packet_ssrc(pk, len, (fl & kSndRtcpPort) != 0) : 0;
+        p_ssrc[tid] = !acc ? 0u : (len < 8 ? 0u : (fl & kSndRtcpPort) ? hbe32(hdr, 4) : (len < 12 ? 0u : hbe32(hdr, 8)));
         p_ts[tid] = arrival / 1000;          // OS::Milliseconds() / 1000, truncating
         // ---- SSRC latch filter (sequential per socket; fast path when nothing changes) ----
         if (P.filter_ssrc) {
@@ -191,7 +218,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         // ---- per-sender queue index / slot offset / non-empty count ----
         uint32_t my_rank = 0, my_nzpre = 0;
         uint64_t my_slotpre = 0;
-        for (uint32_t s = 0; s < nsnd; s++) {
+        for (uint32_t s = 0; s < ((P.ablate & 64u) ? 0u : nsnd); s++) {
             const bool mine = acc && ls == s;
             const uint64_t x = mine ? (1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20) : 0ull;
             uint64_t tot;
@@ -199,6 +226,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             if (mine) { my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20; }
             if (tid == 0) c_tot[s] = tot;
         }
+        if (nz) atomicMax(&c_last[ls], tid << 10 | (int)my_rank);
         uint32_t my_trank = 0;
         for (uint32_t t = 0; t < S.ntracks; t++) {
             const bool mine = acc && track == t;
@@ -220,7 +248,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             reinterpret_cast<PktMeta*>(s_meta[ls])[idx & s_pkmask[ls]] = m;
             const bool by_port_rtp = !(fl & kSndRtcpPort);
             const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len >= 20 &&
-                             key_frame_first_packet(pk, len);
+                             ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len)
+                                                          : key_frame_first_packet(pk, len));
             const bool aud = by_port_rtp && (fl & kSndAudio);
             P.pflags[i] = 1u | (key ? 2u : 0u) | (aud ? 4u : 0u) | ls << 8;
             P.pidx[i] = idx;
@@ -231,41 +260,39 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         p_slotb[tid] = slotb;
         p_vb[tid] = vb;
         __syncthreads();
-        // ---- copy packet bytes into the byte rings: the chunk's slots are one flat list of
-        // 16-B words, every lane copies words (packet found by binary search of the word
-        // prefix in LDS), so lanes stay busy whatever the packet sizes ----
-        {
-            uint32_t wtot;
-            const uint32_t wpre = block_exclusive_scan<uint32_t>(slotb >> 4, scan32, wtot);
-            p_wpre[tid] = wpre;
-            __syncthreads();
-            for (uint32_t w = tid; w < wtot; w += kIngestThreads) {
-                uint32_t lo = 0, hi = n;                  // last packet with p_wpre <= w
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (p_wpre[mid] <= w) lo = mid; else hi = mid;
-                }
-                const uint32_t p = lo, k = w - p_wpre[p];
+        // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
+        // k_ingest_copy's flat grid over packets (copy_mode 1) ----
+        if (P.copy_mode == 0) {
+            const int lane = tid & 63, wid = tid >> 6;
+            for (uint32_t p = wid; p < n; p += kIngestThreads / 64) {
+                const uint32_t sb = p_slotb[p];
+                if (sb == 0) continue;
                 const uint32_t s = p_snd[p];
-                u32x4 v = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16)[k];
-                if (k == 0) v.x = slot_header(p_len[p]);
-                reinterpret_cast<u32x4*>(s_ring[s])[((p_vb[p] >> 4) + k) & s_wmask[s]] = v;
+                const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16);
+                u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
+                const uint64_t w0 = p_vb[p] >> 4;
+                const uint32_t wm = s_wmask[s];
+                for (uint32_t w = lane; w < sb / 16; w += 64) {
+                    u32x4 v = src[w];
+                    if (w == 0) v.x = slot_header(p_len[p]);
+                    ring[(w0 + w) & wm] = v;
+                }
             }
+        } else if (valid) {
+            CopyJob j;
+            j.ring = acc ? s_ring[ls] : 0ull;
+            j.vword = vb >> 4;
+            j.wmask = acc ? s_wmask[ls] : 0u;
+            j.src_slot = slot;
+            j.len = slotb ? len : 0u;
+            j.sender = S.first_sender + ls;
+            P.jobs[i] = j;
         }
         // ---- advance per-sender / per-stream state ----
         if (tid < (int)nsnd) {
             const uint64_t t = c_tot[tid];
             const uint32_t cnt = t & 1023;
-            if (cnt) {
-                for (int p = (int)n - 1; p >= 0; p--)
-                    if (p_snd[p] == tid && p_slotb[p] != 0) {
-                        // queue index of packet p = head + (#accepted of this sender before p)
-                        uint32_t r = 0;
-                        for (int q = 0; q < p; q++) r += (p_acc[q] && p_snd[q] == tid);
-                        s_lastnz[tid] = (int64_t)(s_head[tid] + r);
-                        break;
-                    }
-            }
+            if (c_last[tid] >= 0) s_lastnz[tid] = (int64_t)(s_head[tid] + (c_last[tid] & 1023));
             s_head[tid] += cnt;
             s_vcount[tid] += (uint32_t)((t >> 10) & 1023);
             s_vbyte[tid] += t >> 20;
@@ -285,11 +312,38 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     const uint64_t a1 = block_exclusive_scan<uint64_t>(in_pk, scan64, t1);
     const uint64_t a2 = block_exclusive_scan<uint64_t>(in_bytes, scan64, t2);
     (void)a1; (void)a2;
-    if (tid == 0) {
+    if (tid == 0 && !(P.ablate & 16u)) {
         atomicAdd(&P.totals->ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->ingested_bytes, (unsigned long long)t2);
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
+    }
+}
+
+// =========================================================================================
+// Slot copy, blob -> byte rings.  Each group of kCopyLanes lanes copies one packet's slot as
+// 16-B words, rewriting word 0's 4-byte prefix to the '$' 0 BE16(len) frame header.  A flat
+// grid over packets keeps every CU busy regardless of how packets spread over sessions.
+// =========================================================================================
+constexpr int kCopyThreads = 256, kCopyLanes = 16;
+
+__global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
+    const uint32_t g = blockIdx.x * (kCopyThreads / kCopyLanes) + threadIdx.x / kCopyLanes;
+    const uint32_t lane = threadIdx.x % kCopyLanes;
+    if (g >= P.npk) return;
+    const CopyJob j = P.jobs[g];
+    if (j.len == 0) return;
+    const uint32_t nw = (j.len + 4 + 15) >> 4;
+    // words a later packet of the same batch laps are left to it (k_ingest has already
+    // advanced vbyte_end), so a batch larger than the ring stays deterministic
+    const uint64_t vend = P.senders[j.sender].vbyte_end >> 4, cap = (uint64_t)j.wmask + 1;
+    const uint64_t live = vend > cap ? vend - cap : 0ull;
+    const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)j.src_slot * 16);
+    u32x4* ring = reinterpret_cast<u32x4*>(j.ring);
+    for (uint32_t k = lane; k < nw; k += kCopyLanes) {
+        u32x4 v = src[k];
+        if (k == 0) v.x = slot_header(j.len);
+        if (j.vword + k >= live) ring[(j.vword + k) & j.wmask] = v;
     }
 }
 
@@ -1001,6 +1055,10 @@ namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     hipLaunchKernelGGL(k_ingest, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    if (p.npk && p.copy_mode == 1) {
+        const uint32_t per = kCopyThreads / kCopyLanes;
+        hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+    }
     return hipGetLastError();
 }
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {

@@ -16,6 +16,10 @@ struct IngestParams {
     StreamDev* streams;
     uint32_t* pflags;       // per desc: bit0 enqueued, bit1 video key, bit2 audio event, bits 8-15 local sender
     uint64_t* pidx;         // per desc: sender queue index
+    CopyJob* jobs;          // per desc: slot copy for k_ingest_copy
+    uint32_t npk;           // descriptors in the batch
+    uint32_t copy_mode;     // 0: copy inside k_ingest, 1: k_ingest_copy (EDGPU_INGEST)
+    uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7)
     uint32_t filter_ssrc;
     uint32_t ssrc_timeout_s;
     TickTotals* totals;
