@@ -65,7 +65,8 @@ struct SenderDev {
     uint32_t session;
     uint32_t stream;                // global stream (track) index
     uint32_t track;
-    uint32_t _pad0, _pad1;
+    uint64_t floor;                 // oldest index this sender ever held (> 0 only for a
+                                    // replica session built from a session image)
     // dynamic (ingest)
     uint64_t head;                  // packets ever enqueued
     uint64_t vbyte_end;             // virtual bytes ever enqueued
@@ -79,6 +80,54 @@ struct SenderDev {
     uint64_t tail;                  // oldest index still intact in both rings
     uint64_t umin;                  // min range start over this sender's sub-streams
     uint32_t chunk_base, nchunks;   // fan-out work items
+};
+
+// ---- Session images (cross-GPU keyframe fast start) ----
+// A session image is a self-contained, position-independent copy of the part of a
+// session's sender rings that a joining subscriber can still be served from: [64-B
+// ImgHeader][ImgStream x ntracks][ImgSender x 2*ntracks][per sender: PktMeta x nmeta, then
+// the slot bytes], every section 16-B aligned.  A delta image carries the packets after a
+// given queue index instead.
+constexpr uint32_t kImageMagic = 0x49474445u;   // "EDGI"
+constexpr uint32_t kImageVersion = 1;
+constexpr uint64_t kImageFull = ~0ull;
+
+struct ImgHeader {                  // 64 B
+    uint32_t magic, version, ntracks, nsenders;
+    uint64_t bytes;                 // whole image
+    int64_t  now;                   // export time (ms)
+    uint32_t video_key_flag, delta;
+    uint64_t _pad[3];
+};
+
+struct ImgStream {                  // 16 B
+    uint64_t packet_count, _pad;
+};
+
+struct ImgSender {                  // 96 B
+    uint64_t floor;                 // first queue index carried
+    uint64_t head;
+    uint64_t vbyte_floor;           // vbyte of `floor` (= vbyte_end when nothing is carried)
+    uint64_t vbyte_end;
+    uint32_t vcount_end, valid_ssrc;
+    int64_t  last_valid_s;
+    int64_t  key;
+    int64_t  last_nonzero;
+    uint64_t meta_off, bytes_off;   // from the image start
+    uint32_t delta, flags;
+    uint64_t _pad;
+};
+
+struct ImgPlan {                    // one sender of one image (export or import)
+    uint32_t sender;                // global sender index in this context
+    uint32_t session;               // session in this context
+    uint32_t ls;                    // local sender index in the session
+    uint32_t first;                 // 1 for the session's first sender
+    uint64_t from;                  // export: kImageFull or the first index of a delta
+    uint64_t image_base;            // byte offset of the image in the buffer
+    uint64_t floor, vbyte_floor, nmeta, nbytes;
+    uint64_t meta_off, bytes_off;   // from the image start
+    uint64_t image_bytes;           // export: size of the whole image
 };
 
 struct StreamDev {

@@ -22,6 +22,7 @@
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 int fanout_chunk(int variant);
@@ -128,6 +129,9 @@ struct edgpu_ctx {
 
     uint8_t* d_arena = nullptr;
     edgpu_out_desc* d_out_desc = nullptr;
+    // session images
+    DevVec<ImgPlan> d_img_plan;
+    int* d_img_status = nullptr;
     TickTotals* d_totals = nullptr;
 };
 
@@ -210,6 +214,8 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
+    x->d_img_plan.release();
+    if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals})
         if (p) (void)hipFree(p);
@@ -663,6 +669,125 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
     }
     if (out_len) *out_len = len;
     if (out_packets) *out_packets = np;
+    return EDGPU_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Session images (cross-GPU keyframe fast start)
+
+static int image_launch(edgpu_ctx* x, std::vector<ImgPlan>& plan, int64_t now_ms, uint8_t* buf, int phase) {
+    if (!x->d_img_status && hipMalloc(&x->d_img_status, sizeof(int)) != hipSuccess)
+        return fail(EDGPU_OUT_OF_MEMORY, "image status");
+    HIP_CHECK(x->d_img_plan.reserve(std::max<size_t>(plan.size(), 1), x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_img_plan.ptr, plan.data(), plan.size() * sizeof(ImgPlan), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemsetAsync(x->d_img_status, 0, sizeof(int), x->stream));
+    ImageParams p;
+    p.senders = x->d_senders.ptr; p.sessions = x->d_sessions.ptr; p.streams = x->d_streams.ptr;
+    p.plan = x->d_img_plan.ptr; p.nplan = (uint32_t)plan.size();
+    p.now = now_ms; p.over_buffer_ms = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
+    p.buf = buf; p.status = x->d_img_status;
+    HIP_CHECK(launch_image(p, phase, x->stream));
+    int status = 0;
+    if (phase == 0)
+        HIP_CHECK(hipMemcpyAsync(plan.data(), x->d_img_plan.ptr, plan.size() * sizeof(ImgPlan), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipMemcpyAsync(&status, x->d_img_status, sizeof(int), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    if (status) return fail(status, phase == 2 ? "session image rejected by the replica" : "session image export");
+    return EDGPU_OK;
+}
+
+int edgpu_session_export(edgpu_ctx* x, const uint32_t* sessions, uint32_t n, int64_t now_ms,
+                         const uint64_t* from, void* dst, uint64_t cap, uint64_t* offsets, uint64_t* heads) {
+    if (!x || (n && (!sessions || !offsets))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    HIP_CHECK(hipSetDevice(x->device));
+    std::vector<ImgPlan> plan;
+    for (uint32_t i = 0; i < n; i++) {
+        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        const SessionHost& sh = x->sessions[sessions[i]];
+        for (uint32_t ls = 0; ls < 2 * sh.ntracks; ls++) {
+            ImgPlan E;
+            memset(&E, 0, sizeof(E));
+            E.sender = sh.first_sender + ls; E.session = sessions[i]; E.ls = ls; E.first = ls == 0;
+            E.from = from ? from[plan.size()] : kImageFull;
+            plan.push_back(E);
+        }
+    }
+    offsets[0] = 0;
+    if (plan.empty()) return EDGPU_OK;
+    int r = image_launch(x, plan, now_ms, nullptr, 0);
+    if (r) return r;
+    uint64_t base = 0;
+    for (uint32_t i = 0, k = 0; i < n; i++) {
+        const uint32_t nt = x->sessions[sessions[i]].ntracks, ns = 2 * nt;
+        uint64_t cur = sizeof(ImgHeader) + nt * sizeof(ImgStream) + ns * sizeof(ImgSender);
+        for (uint32_t ls = 0; ls < ns; ls++) {
+            ImgPlan& E = plan[k + ls];
+            E.image_base = base;
+            E.meta_off = cur; cur += E.nmeta * sizeof(PktMeta);
+            E.bytes_off = cur; cur += E.nbytes;
+            if (heads) heads[k + ls] = E.floor + E.nmeta;
+        }
+        cur = (cur + 15) & ~15ull;
+        for (uint32_t ls = 0; ls < ns; ls++) plan[k + ls].image_bytes = cur;
+        offsets[i] = base;
+        base += cur;
+        k += ns;
+    }
+    offsets[n] = base;
+    if (!dst) return EDGPU_OK;                         // size query
+    if (base > cap) return fail(EDGPU_OUT_OVERFLOW, "image buffer too small");
+    return image_launch(x, plan, now_ms, (uint8_t*)dst, 1);
+}
+
+int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offsets, uint32_t n,
+                         const uint32_t* sessions) {
+    if (!x || (n && (!images || !offsets || !sessions))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    HIP_CHECK(hipSetDevice(x->device));
+    std::vector<ImgPlan> plan;
+    for (uint32_t i = 0; i < n; i++) {
+        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (offsets[i] % 16 || offsets[i + 1] < offsets[i] + sizeof(ImgHeader))
+            return fail(EDGPU_BAD_ARGUMENT, "bad image offsets");
+        const SessionHost& sh = x->sessions[sessions[i]];
+        for (uint32_t ls = 0; ls < 2 * sh.ntracks; ls++) {
+            ImgPlan E;
+            memset(&E, 0, sizeof(E));
+            E.sender = sh.first_sender + ls; E.session = sessions[i]; E.ls = ls; E.first = ls == 0;
+            E.image_base = offsets[i];
+            plan.push_back(E);
+        }
+    }
+    if (plan.empty()) return EDGPU_OK;
+    return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);
+}
+
+int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
+    if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    *out = nullptr;
+    if (hipMalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "device buffer");
+    return EDGPU_OK;
+}
+
+int edgpu_device_free(edgpu_ctx* x, void* p) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (!p) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(hipFree(p));
+    return EDGPU_OK;
+}
+
+int edgpu_memcpy_peer(edgpu_ctx* x, void* dst, int src_device, const void* src, uint64_t bytes) {
+    if (!x || (bytes && (!dst || !src))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!bytes) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    if (src_device == x->device)
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, x->stream));
+    else
+        HIP_CHECK(hipMemcpyPeerAsync(dst, x->device, src, src_device, bytes, x->stream));
     return EDGPU_OK;
 }
 

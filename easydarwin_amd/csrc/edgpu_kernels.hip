@@ -422,6 +422,7 @@ __global__ void k_plan_senders(PlanParams P) {
     const uint64_t pk_cap = (uint64_t)D.pk_mask + 1;
     const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16;
     uint64_t lo = head > pk_cap ? head - pk_cap : 0;
+    lo = max(lo, D.floor);                                    // a replica holds nothing older
     const uint64_t vend = D.vbyte_end;
     // oldest packet whose slot is still intact in the byte ring
     uint64_t tail = lower_bound_meta(meta, D.pk_mask, lo, head,
@@ -435,7 +436,7 @@ __global__ void k_plan_senders(PlanParams P) {
         const int64_t cutoff = P.T.now - P.T.over_buffer_ms;  // now - arrival <= over buffer
         const uint64_t f = lower_bound_meta(meta, D.pk_mask, tail, head,
                                             [&](const PktMeta& m) { return m.arrival >= cutoff; });
-        if (f < head) ns = (f == tail && tail > 0) ? -2 : (int64_t)f;   // -2: window exceeds ring
+        if (f < head) ns = (f == tail && tail > D.floor) ? -2 : (int64_t)f;   // -2: window exceeds ring
     }
     D.new_start = ns;
     D.umin = head;
@@ -1046,6 +1047,128 @@ void k_fanout3(FanoutParams P) {
     }
 }
 
+// =========================================================================================
+// Session images: export the serveable part of a session's rings into a
+// contiguous buffer that another GPU imports into a replica session; a subscriber joining
+// the replica receives exactly what it would receive joining the owner.
+// =========================================================================================
+
+__device__ __forceinline__ void set_status(int* st, int code) { atomicCAS(st, 0, code); }
+
+__device__ uint64_t sender_tail(const SenderDev& D) {
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint64_t head = D.head, pk_cap = (uint64_t)D.pk_mask + 1;
+    const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16, vend = D.vbyte_end;
+    uint64_t lo = head > pk_cap ? head - pk_cap : 0;
+    lo = max(lo, D.floor);
+    return lower_bound_meta(meta, D.pk_mask, lo, head,
+                            [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
+}
+
+// Export plan, one thread per sender: which packets the image carries.  A full image starts
+// at the key pointer, or (no key) at the oldest packet inside the new-output window -- the
+// same start k_plan_senders would pick for a new output at `now` or later (Q7).
+__global__ void k_image_plan(ImageParams P) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.nplan) return;
+    ImgPlan& E = P.plan[j];
+    const SenderDev& D = P.senders[E.sender];
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint64_t head = D.head, tail = sender_tail(D);
+    uint64_t floor = head;
+    if (E.from != kImageFull) {
+        floor = E.from;
+        if (floor > head) { set_status(P.status, EDGPU_BAD_ARGUMENT); floor = head; }
+        else if (floor < tail) { set_status(P.status, EDGPU_RING_OVERFLOW); floor = tail; }
+    } else if (D.key >= 0) {
+        floor = (uint64_t)D.key;
+        if (floor < tail) { set_status(P.status, EDGPU_RING_OVERFLOW); floor = tail; }
+    } else if (head > tail) {
+        const int64_t cutoff = P.now - P.over_buffer_ms;
+        floor = lower_bound_meta(meta, D.pk_mask, tail, head, [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        if (floor < head && floor == tail && tail > D.floor) set_status(P.status, EDGPU_RING_OVERFLOW);
+    }
+    E.floor = floor;
+    E.vbyte_floor = floor < head ? meta[floor & D.pk_mask].vbyte : D.vbyte_end;
+    E.nmeta = head - floor;
+    E.nbytes = D.vbyte_end - E.vbyte_floor;
+}
+
+// Export pack, one workgroup per sender: metadata and slot bytes out of the rings (unwrapped).
+__global__ __launch_bounds__(256) void k_image_pack(ImageParams P) {
+    const ImgPlan E = P.plan[blockIdx.x];
+    const SenderDev& D = P.senders[E.sender];
+    uint8_t* img = P.buf + E.image_base;
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    PktMeta* om = reinterpret_cast<PktMeta*>(img + E.meta_off);
+    for (uint64_t i = threadIdx.x; i < E.nmeta; i += blockDim.x) om[i] = meta[(E.floor + i) & D.pk_mask];
+    const u32x4* ring = reinterpret_cast<const u32x4*>(D.ring);
+    u32x4* ob = reinterpret_cast<u32x4*>(img + E.bytes_off);
+    const uint64_t w0 = E.vbyte_floor >> 4, nw = E.nbytes >> 4;
+    for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x) ob[w] = ring[(w0 + w) & D.word_mask];
+    if (threadIdx.x == 0) {
+        const SessionDev& S = P.sessions[E.session];
+        ImgSender r;
+        r.floor = E.floor; r.head = D.head; r.vbyte_floor = E.vbyte_floor; r.vbyte_end = D.vbyte_end;
+        r.vcount_end = D.vcount_end; r.valid_ssrc = D.valid_ssrc; r.last_valid_s = D.last_valid_s;
+        r.key = D.key; r.last_nonzero = D.last_nonzero;
+        r.meta_off = E.meta_off; r.bytes_off = E.bytes_off;
+        r.delta = E.from != kImageFull; r.flags = D.flags; r._pad = 0;
+        reinterpret_cast<ImgSender*>(img + sizeof(ImgHeader) + S.ntracks * sizeof(ImgStream))[E.ls] = r;
+        if (E.first) {
+            ImgHeader h;
+            h.magic = kImageMagic; h.version = kImageVersion; h.ntracks = S.ntracks; h.nsenders = 2 * S.ntracks;
+            h.bytes = E.image_bytes; h.now = P.now; h.video_key_flag = S.video_key_flag; h.delta = r.delta;
+            h._pad[0] = h._pad[1] = h._pad[2] = 0;
+            *reinterpret_cast<ImgHeader*>(img) = h;
+            ImgStream* st = reinterpret_cast<ImgStream*>(img + sizeof(ImgHeader));
+            for (uint32_t t = 0; t < S.ntracks; t++) st[t] = ImgStream{P.streams[S.first_stream + t].packet_count, 0};
+        }
+    }
+}
+
+// Import, one workgroup per (image, sender): validate, copy into the replica's rings at the
+// same virtual positions, then take over the owner's sender state.
+__global__ __launch_bounds__(256) void k_image_apply(ImageParams P) {
+    const ImgPlan E = P.plan[blockIdx.x];
+    SenderDev& D = P.senders[E.sender];
+    const SessionDev& S = P.sessions[E.session];
+    const uint8_t* img = P.buf + E.image_base;
+    const ImgHeader h = *reinterpret_cast<const ImgHeader*>(img);
+    if (h.magic != kImageMagic || h.version != kImageVersion || h.ntracks != S.ntracks || h.nsenders != 2 * S.ntracks) {
+        if (threadIdx.x == 0) set_status(P.status, EDGPU_BAD_ARGUMENT);
+        return;
+    }
+    const ImgSender r = reinterpret_cast<const ImgSender*>(img + sizeof(ImgHeader) + h.ntracks * sizeof(ImgStream))[E.ls];
+    const uint64_t nmeta = r.head - r.floor, nbytes = r.vbyte_end - r.vbyte_floor;
+    if ((r.delta && r.floor != D.head) || (r.flags & ~kSndRtcpPort) != (D.flags & ~kSndRtcpPort)) {
+        if (threadIdx.x == 0) set_status(P.status, EDGPU_BAD_ARGUMENT);
+        return;
+    }
+    if (nmeta > (uint64_t)D.pk_mask + 1 || nbytes > ((uint64_t)D.word_mask + 1) * 16) {
+        if (threadIdx.x == 0) set_status(P.status, EDGPU_RING_OVERFLOW);
+        return;
+    }
+    const PktMeta* im = reinterpret_cast<const PktMeta*>(img + r.meta_off);
+    PktMeta* meta = reinterpret_cast<PktMeta*>(D.meta);
+    for (uint64_t i = threadIdx.x; i < nmeta; i += blockDim.x) meta[(r.floor + i) & D.pk_mask] = im[i];
+    const u32x4* ib = reinterpret_cast<const u32x4*>(img + r.bytes_off);
+    u32x4* ring = reinterpret_cast<u32x4*>(D.ring);
+    const uint64_t w0 = r.vbyte_floor >> 4, nw = nbytes >> 4;
+    for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x) ring[(w0 + w) & D.word_mask] = ib[w];
+    if (threadIdx.x == 0) {
+        if (!r.delta) D.floor = r.floor;
+        D.head = r.head; D.vbyte_end = r.vbyte_end; D.vcount_end = r.vcount_end;
+        D.valid_ssrc = r.valid_ssrc; D.last_valid_s = r.last_valid_s;
+        D.key = r.key; D.last_nonzero = r.last_nonzero;
+        if (E.first) {
+            const ImgStream* st = reinterpret_cast<const ImgStream*>(img + sizeof(ImgHeader));
+            for (uint32_t t = 0; t < S.ntracks; t++) P.streams[S.first_stream + t].packet_count = st[t].packet_count;
+            P.sessions[E.session].video_key_flag = h.video_key_flag;
+        }
+    }
+}
+
 }  // namespace edgpu
 
 // ---------------------------------------------------------------------------------------
@@ -1059,6 +1182,13 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
         const uint32_t per = kCopyThreads / kCopyLanes;
         hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
+    return hipGetLastError();
+}
+hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
+    if (p.nplan == 0) return hipSuccess;
+    if (phase == 0) hipLaunchKernelGGL(k_image_plan, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
+    else if (phase == 1) hipLaunchKernelGGL(k_image_pack, dim3(p.nplan), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {

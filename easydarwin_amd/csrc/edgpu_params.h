@@ -60,4 +60,16 @@ struct FanoutParams {
     uint32_t ablate;            // timing-only builds: bit0 skip descriptors, bit1 skip arena stores
 };
 
+struct ImageParams {
+    SenderDev* senders;
+    SessionDev* sessions;
+    StreamDev* streams;
+    ImgPlan* plan;
+    uint32_t nplan;
+    int64_t now;
+    int64_t over_buffer_ms;
+    uint8_t* buf;           // export: destination images; import: source images
+    int* status;            // first error wins
+};
+
 }  // namespace edgpu

@@ -1,6 +1,8 @@
 """Multi-GPU plumbing for the relay: one process per GPU, sessions sharded by
-FNV-1a-64 of the stream ID, no collective on the data path.  torch.distributed (RCCL on the
-GPU box, gloo in CPU tests) only brackets the timed region and reduces the results."""
+FNV-1a-64 of the stream ID, no collective on the steady-state data path.  torch.distributed
+(RCCL on the GPU box, gloo in CPU tests) brackets the timed region, reduces the results, and
+carries the one real exchange: session images for subscribers whose egress GPU is not the
+stream's owner (exchange_images, BASELINE config C4)."""
 from __future__ import annotations
 
 import os
@@ -29,3 +31,55 @@ def reduce_run(elapsed_s: float, counts: list, device=None):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     return float(t.item()), [int(round(x)) for x in c.tolist()]
+
+
+def subscriber_rank(sub_id: int, world: int) -> int:
+    """Egress GPU of a subscriber (BASELINE config C4: hash(subID) % nGPU)."""
+    return fnv1a64(f"sub{int(sub_id)}") % world
+
+
+def exchange_images(requests, export_fn, import_fn, make_buf, world: int, rank: int):
+    """One round of the only cross-GPU exchange on the path: session images
+    from their owners to the ranks that serve replicas of them.
+
+    requests   global sessions this rank needs images of this round (owned elsewhere)
+    export_fn  (sessions, dst_rank) -> (uint8 tensor, offsets[n+1]); images of `sessions`,
+               owned here, for `dst_rank` (full the first time, deltas afterwards)
+    import_fn  (tensor, offsets, sessions, src_rank) -> None
+    make_buf   nbytes -> uint8 tensor on the communication device
+
+    Control metadata (which sessions, image offsets) goes through all_gather_object; the
+    image bytes go point-to-point in one batch_isend_irecv group (ncclGroupStart/End with
+    ncclSend/ncclRecv pairs under RCCL).  Returns (bytes sent, bytes received)."""
+    reqs = [None] * world
+    dist.all_gather_object(reqs, sorted(int(g) for g in requests))
+    outgoing = {}
+    for r in range(world):
+        if r == rank:
+            continue
+        mine = [g for g in reqs[r] if owner(g, world) == rank]
+        if mine:
+            buf, offs = export_fn(mine, r)
+            outgoing[r] = (mine, buf, [int(x) for x in offs])
+    meta = [None] * world
+    dist.all_gather_object(meta, {r: (m, offs) for r, (m, _, offs) in outgoing.items()})
+    incoming = {}
+    for src in range(world):
+        if src != rank and rank in meta[src]:
+            sess, offs = meta[src][rank]
+            incoming[src] = (sess, offs, make_buf(max(offs[-1], 1)))
+    ops = []
+    for r, (_, buf, offs) in sorted(outgoing.items()):
+        if offs[-1]:
+            ops.append(dist.P2POp(dist.isend, buf[:offs[-1]], r))
+    for src, (_, offs, buf) in sorted(incoming.items()):
+        if offs[-1]:
+            ops.append(dist.P2POp(dist.irecv, buf[:offs[-1]], src))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for src, (sess, offs, buf) in sorted(incoming.items()):
+        import_fn(buf, offs, sess, src)
+    sent = sum(o[-1] for _, _, o in outgoing.values())
+    recv = sum(o[-1] for _, o, _ in incoming.values())
+    return sent, recv

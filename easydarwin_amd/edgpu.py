@@ -26,7 +26,10 @@ EXPORTED = [
     "edgpu_subscriber_add", "edgpu_subscriber_remove", "edgpu_ingest", "edgpu_keyframe_index",
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
+    "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
+    "edgpu_device_free",
 ]
+IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 
 
 class Config(C.Structure):
@@ -131,6 +134,11 @@ def load(path: str = LIB_PATH):
         "edgpu_counters_get": (I32, [P, C.POINTER(Counters)]),
         "edgpu_kernel_times": (I32, [P, I32, C.POINTER(C.c_float), U32, C.POINTER(U32)]),
         "edgpu_gop_copy": (I32, [P, U32, U32, P, U64, C.POINTER(U64), C.POINTER(U32)]),
+        "edgpu_session_export": (I32, [P, P, U32, I64, P, P, U64, P, P]),
+        "edgpu_session_import": (I32, [P, P, P, U32, P]),
+        "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
+        "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
+        "edgpu_device_free": (I32, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -253,6 +261,39 @@ class Context:
         _check(self.lib.edgpu_gop_copy(self.h, session, track, _ptr(buf), cap, C.byref(n), C.byref(k)))
         return buf[:n.value].tobytes(), k.value
 
+    # ---- cross-GPU keyframe fast start (session images) ----
+    def senders_of(self, sessions) -> int:
+        return int(sum(2 * self.session_tracks(int(s)) for s in sessions))
+
+    def session_export(self, sessions, now_ms: int, dst_ptr: int = 0, cap: int = 0, since=None):
+        """Export session images.  dst_ptr 0 = size query.  `since`: None (full images) or,
+        per sender of each session in order, IMAGE_FULL or a previous call's head.
+        Returns (offsets[n+1], heads[n_senders])."""
+        sess = np.ascontiguousarray(sessions, dtype=np.uint32)
+        offsets = np.zeros(len(sess) + 1, dtype=np.uint64)
+        heads = np.zeros(self.senders_of(sess), dtype=np.uint64)
+        frm = None if since is None else np.ascontiguousarray(since, dtype=np.uint64)
+        if frm is not None and len(frm) != len(heads):
+            raise ValueError("`since` needs one entry per sender")
+        _check(self.lib.edgpu_session_export(self.h, _ptr(sess), len(sess), int(now_ms),
+                                             None if frm is None else _ptr(frm),
+                                             C.c_void_p(dst_ptr) if dst_ptr else None, int(cap),
+                                             _ptr(offsets), _ptr(heads)))
+        return offsets, heads
+
+    def session_import(self, images_ptr: int, offsets, sessions):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sess = np.ascontiguousarray(sessions, dtype=np.uint32)
+        if len(offsets) != len(sess) + 1:
+            raise ValueError("offsets must have len(sessions) + 1 entries")
+        _check(self.lib.edgpu_session_import(self.h, C.c_void_p(images_ptr), _ptr(offsets), len(sess), _ptr(sess)))
+
+    def memcpy_peer(self, dst_ptr: int, src_device: int, src_ptr: int, nbytes: int):
+        _check(self.lib.edgpu_memcpy_peer(self.h, C.c_void_p(dst_ptr), int(src_device), C.c_void_p(src_ptr), int(nbytes)))
+
+    def device_alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
     def copy_to_host(self, dev_ptr, nbytes: int) -> np.ndarray:
         out = np.empty(int(nbytes), dtype=np.uint8)
         if nbytes:
@@ -268,6 +309,26 @@ class Context:
         desc = self.copy_to_host(r.desc, st.relayed_packets * OUT_DTYPE.itemsize).view(OUT_DTYPE)
         arena = self.copy_to_host(r.arena, st.arena_bytes)
         return st, subs, desc, arena
+
+
+class DeviceBuffer:
+    """Device memory owned by a context (edgpu_device_alloc); freed with the object."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        out = C.c_void_p()
+        _check(ctx.lib.edgpu_device_alloc(ctx.h, int(nbytes), C.byref(out)))
+        self.ctx, self.ptr, self.nbytes = ctx, int(out.value), int(nbytes)
+
+    def free(self):
+        if self.ptr and self.ctx.h:
+            _check(self.ctx.lib.edgpu_device_free(self.ctx.h, C.c_void_p(self.ptr)))
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def build_batch(pkts):

@@ -32,17 +32,34 @@ def _wire_images(subs, desc, arena, images):
                 parts.append(struct.pack(">H", ln) + arena[off:off + ln].tobytes())
 
 
-def replay(trace: Trace, ctx: edgpu.Context | None = None, **cfg):
-    """Returns (capture_bytes, per-tick stats list)."""
+def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None, **cfg):
+    """Returns (capture_bytes, per-tick stats list).
+
+    replica=None: subscribers join the context that ingests (the owner).
+    replica="all" / "late": every subscriber joins a replica session on a second context,
+    kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
+    every replica before the first packet; "late" creates a fresh replica for every joining
+    subscriber at its join tick, from a full image taken mid-stream (the C4 fast-start
+    path)."""
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
+    rep = link = None
+    if replica is not None:
+        from .replica import ReplicaLink
+        assert replica in ("all", "late")
+        dev = int(cfg.get("device", 0))
+        rep = edgpu.Context(**cfg)
+        link = ReplicaLink(ctx, dev, rep, dev)
     try:
         sess_tracks = []
+        rsess = {}
         for sdp in trace.sdps:
             sid = ctx.session_add(sdp)
             assert sid == len(sess_tracks)
             sess_tracks.append(ctx.session_tracks(sid))
+            if replica == "all":
+                rsess[sid] = link.add(sid, sdp)
         subs_meta = {}          # handle -> (sub_id, session, tcp)
         images = {}
         pending, joins, stats = [], [], []
@@ -59,15 +76,24 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, **cfg):
                     ctx.ingest_host(desc, seg_off, seg_sess, blob)
                     ctx.keyframe_index()
                     pending = []
+                if link is not None:
+                    for (_, jt, s, sub_id, transport, _ua) in joins:
+                        if replica == "late" or s not in rsess:
+                            rsess[s] = link.add(s, trace.sdps[s])     # "late": a fresh replica per join
+                    link.sync(t)
+                out = ctx if rep is None else rep
                 for (_, jt, s, sub_id, transport, _ua) in joins:
-                    h = ctx.subscriber_add(s, edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP)
+                    h = out.subscriber_add(s if rep is None else rsess[s],
+                                           edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP)
                     subs_meta[h] = (sub_id, s, transport)
                     for tr in range(sess_tracks[s]):
                         for k in (0, 1):
                             images[(h, tr, k)] = []
                 joins = []
-                r = ctx.fanout(t)
-                st, subs, desc, arena = ctx.read_tick(r)
+                if rep is not None:
+                    ctx.fanout(t)                      # the owner ticks too (no subscribers here)
+                r = out.fanout(t)
+                st, subs, desc, arena = out.read_tick(r)
                 stats.append((t, st.relayed_packets, st.relayed_bytes))
                 _wire_images(subs, desc, arena, images)
         # capture: one record per (subscriber, track, kind), sorted by subscriber id
@@ -83,5 +109,9 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, **cfg):
             out.append(data)
         return b"".join(out), stats
     finally:
+        if link is not None:
+            link.close()
+        if rep is not None:
+            rep.close()
         if own:
             ctx.close()

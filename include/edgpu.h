@@ -213,6 +213,51 @@ int  edgpu_gop_span(edgpu_ctx* ctx, uint32_t session, uint32_t track,
 int  edgpu_gop_copy(edgpu_ctx* ctx, uint32_t session, uint32_t track, uint8_t* dst, uint64_t cap,
                     uint64_t* out_len, uint32_t* out_packets);
 
+/* ---- Cross-GPU keyframe fast start (BASELINE config C4) ----
+ * Streams are owned by one GPU (FNV-1a-64 of the stream ID); a subscriber whose egress GPU
+ * differs joins a *replica session* there.  The owner exports a session image -- the part
+ * of each sender ring a new output can still be served from: key pointer -> newest, or the
+ * new-output window when there is no key (ReflectorStream.cpp:1058-1069, 1201-1231) --
+ * which travels once per (session, destination GPU) over xGMI (edgpu_memcpy_peer inside a
+ * process, RCCL send/recv between processes), and the replica imports it.  A subscriber
+ * joining the replica then receives exactly what it would have received joining the owner.
+ * Later ticks ship delta images (packets after the previous export's heads), so a replica
+ * follows its owner without re-sending the GOP.  Replica sessions are created with
+ * edgpu_session_add from the owner's SDP and are never passed to edgpu_ingest.
+ *
+ * Image format (16-B aligned sections): 64-B header {magic "EDGI", version 1, ntracks,
+ * nsenders, bytes, export time, session video-key flag, delta}, per track the packet-id
+ * counter, per sender its ring state, then per sender the packet metadata (32 B each) and
+ * the slot bytes ('$' 0 BE16(len) + packet + pad) of the packets carried. */
+#define EDGPU_IMAGE_FULL 0xFFFFFFFFFFFFFFFFull
+
+/* Exports images of `sessions[0..n)` into device memory `dst` (capacity `cap`), image i
+ * at dst + offsets[i], offsets[n] = total bytes.  `from` is NULL (full images) or holds, per
+ * sender of each listed session in order (2 * ntracks per session: track t RTP = 2t,
+ * RTCP = 2t+1), EDGPU_IMAGE_FULL or the first queue index of a delta (a previous call's
+ * `heads` value).  `heads` (optional, same shape) receives each sender's newest index + 1.
+ * With dst == NULL only offsets/heads are computed (size query).  Syncs. */
+int  edgpu_session_export(edgpu_ctx* ctx, const uint32_t* sessions, uint32_t n, int64_t now_ms,
+                          const uint64_t* from, void* dst, uint64_t cap, uint64_t* offsets,
+                          uint64_t* heads);
+
+/* Applies images (device memory readable by this context's GPU; offsets as returned by the
+ * export, n + 1 entries) to replica sessions `sessions[0..n)` of this context.  A delta
+ * must start at the replica's current head.  Returns EDGPU_BAD_ARGUMENT for a mismatched
+ * or out-of-order image, EDGPU_RING_OVERFLOW if the replica's rings are too small.  Syncs. */
+int  edgpu_session_import(edgpu_ctx* ctx, const void* images, const uint64_t* offsets, uint32_t n,
+                          const uint32_t* sessions);
+
+/* Enqueues a device-to-device copy from GPU `src_device` into this context's GPU on the
+ * context stream (hipMemcpyPeerAsync over xGMI; a plain device copy when the devices are
+ * the same).  Stream-ordered before the next call on this context. */
+int  edgpu_memcpy_peer(edgpu_ctx* ctx, void* dst, int src_device, const void* src, uint64_t bytes);
+
+/* Device memory on this context's GPU for image buffers (hipMalloc / hipFree).  Peer access
+ * to it is enabled for every GPU that can reach this one, so RCCL and peer copies may use it. */
+int  edgpu_device_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
+int  edgpu_device_free(edgpu_ctx* ctx, void* ptr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,90 @@
+"""CPU, gloo: the cross-GPU image exchange (easydarwin_amd.dist.exchange_images, SURVEY.md
+§8.e / C4) routes each requested session's image from its owner to the requesting rank,
+intact, over batched point-to-point send/recv -- with a stand-in image source (the GPU
+export/import is tested in tests/test_gpu_replica.py)."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from easydarwin_amd.dist import owner, subscriber_rank
+
+N_SESS = 24
+
+
+def _image(g, dst, version):
+    """Deterministic stand-in for a session image: length and bytes depend on all three."""
+    seed = hashlib.sha256(f"{g}:{dst}:{version}".encode()).digest()
+    n = 48 + 16 * (g % 7) + 16 * version
+    return np.frombuffer((seed * (n // 32 + 1))[:n], dtype=np.uint8)
+
+
+def _worker(rank, world, port, out_q):
+    import torch.distributed as dist
+    from easydarwin_amd.dist import exchange_images
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    versions = {}                                   # (session, dst) -> images shipped so far
+    got = []
+
+    def export_fn(sessions, dst):
+        parts, offs = [], [0]
+        for g in sessions:
+            assert owner(g, world) == rank
+            v = versions.get((g, dst), 0)
+            versions[(g, dst)] = v + 1
+            parts.append(_image(g, dst, v))
+            offs.append(offs[-1] + len(parts[-1]))
+        return torch.from_numpy(np.concatenate(parts)), offs
+
+    def import_fn(buf, offs, sessions, src):
+        for i, g in enumerate(sessions):
+            got.append((g, src, bytes(buf[offs[i]:offs[i + 1]].numpy())))
+
+    # subscribers 0..59 spread over sessions; a rank needs every session one of its
+    # subscribers watches and another rank owns
+    subs = [(sub, sub % N_SESS) for sub in range(60)]
+    need = sorted({g for sub, g in subs if subscriber_rank(sub, world) == rank and owner(g, world) != rank})
+    rounds = []
+    for r in range(2):                              # join burst, then one delta round
+        got.clear()
+        sent, recv = exchange_images(need, export_fn, import_fn,
+                                     lambda n: torch.empty(n, dtype=torch.uint8), world, rank)
+        rounds.append((sorted(got), sent, recv))
+    out_q.put((rank, need, rounds))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_routes_images(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total_sent = total_recv = 0
+    for rank, need, rounds in res:
+        assert need, "every rank should need some remote session in this layout"
+        for version, (got, sent, recv) in enumerate(rounds):
+            want = sorted((g, owner(g, world), bytes(_image(g, rank, version))) for g in need)
+            assert got == want
+            total_sent += sent
+            total_recv += recv
+    assert total_sent == total_recv > 0
