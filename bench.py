@@ -218,7 +218,7 @@ def main():
     if os.path.exists(pmc) and world == 1 and args.subs == 16 and args.sessions == 1024:
         try:
             pj = json.load(open(pmc))
-            if pj.get("fanout_kernel") == "k_fanout3":
+            if pj.get("fanout_kernel") == ctx.fanout_kernel().split("<")[0]:   # rocprofv3 -T names
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -243,7 +243,7 @@ def main():
         "relayed_GBps": round(out_all / dt / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_fanout3", "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
+                     "kernel": ctx.fanout_kernel(), "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
                      "avg_kernel_ms": round(fan_ms, 4)},
         "kernel_ms": {"fanout": round(fan_ms, 4),
                       "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,

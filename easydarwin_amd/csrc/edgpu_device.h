@@ -20,10 +20,7 @@ namespace edgpu {
 
 enum : uint32_t {
     kMaxPacket = 2060,              // ReflectorPacket::kMaxReflectorPacketSize (ReflectorStream.h:126)
-    kChunkPackets = 32,             // fan-out work item = 32 consecutive packets of one sender
-    kChunkWords = 32 * 129,         // 32 * roundup16(4 + 2060) / 16
-    kFanoutThreads = 256,
-    kFanoutRegWords = (kChunkWords + kFanoutThreads - 1) / kFanoutThreads,   // 17
+    kSlotWordsMax = 129,            // roundup16(4 + 2060) / 16: 16-B words of the largest slot
     kIngestThreads = 256,
     kMaxTracks = 16,                // per session
     kMaxSendersPerSession = 2 * kMaxTracks,
@@ -164,9 +161,29 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint32_t nonempty;              // range [a, head) is non-empty
 };
 
-struct WorkItem {
+// One fan-out work item: up to `chunk` consecutive packets of one sender, with everything the
+// copy kernel needs before it can issue the chunk's loads (k_plan_final fills it, so the
+// kernel's first dependent load is this 64-B record).
+struct FanWork {                    // 64 B
+    uint64_t ring;                  // sender byte ring (device pointer)
+    uint64_t meta;                  // sender PktMeta ring (device pointer)
+    uint32_t wmask, pkmask;         // ring words - 1, ring packets - 1
     uint32_t sender;
-    uint32_t chunk;
+    uint32_t np;                    // packets in the chunk
+    uint32_t nw;                    // 16-B words the chunk's slots span
+    uint32_t vc0;                   // vcount of the chunk's first packet
+    uint32_t qb, qe;                // the sender's sub-streams: FanSub[qb, qe)
+    uint64_t lo;                    // queue index of the chunk's first packet
+    uint64_t vb0;                   // vbyte of the chunk's first packet
+};
+
+// Per-sub-stream copy parameters of a tick, in sender order (FanWork::qb/qe index them).
+struct FanSub {                     // 32 B
+    int64_t  dw;                    // arena word of virtual ring word V is dw + V
+    int64_t  off;                   // wire offset of a packet with vbyte vb is off + vb
+    uint64_t a;                     // first packet index this tick; ~0: nothing to send
+    uint32_t ch;                    // bit 0: RTSP-interleaved; bits 8..15: channel byte
+    uint32_t db;                    // descriptor index of a packet with vcount vc is db + vc
 };
 
 struct TickTotals {                 // device-side, mirrors edgpu_tick_stats

@@ -26,6 +26,7 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 int fanout_chunk(int variant);
+const char* fanout_name(int variant);
 }  // namespace edgpu
 
 using namespace edgpu;
@@ -81,7 +82,7 @@ struct edgpu_ctx {
     edgpu_config cfg;
     int device = 0;
     int num_cus = 256;
-    int fanout_variant = 9;
+    int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
     uint32_t ablate = 0;
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
     hipStream_t stream = nullptr;
@@ -107,8 +108,10 @@ struct edgpu_ctx {
     DevVec<SubDev> d_subs;
     DevVec<uint32_t> d_sub_index;
     DevVec<uint32_t> d_sub_range;
+    DevVec<uint32_t> d_sub_pos;
+    DevVec<FanSub> d_fansub;
     DevVec<edgpu_substream_out> d_sub_out;
-    DevVec<WorkItem> d_work;
+    DevVec<FanWork> d_work;
     DevVec<uint64_t> d_blk_bytes, d_blk_bytes_base;
     DevVec<uint32_t> d_blk_count, d_blk_count_base;
     bool index_dirty = true;
@@ -212,7 +215,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->stream) (void)hipStreamSynchronize(x->stream);
     for (void* p : x->ring_allocs) (void)hipFree(p);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
-    x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_out.release(); x->d_work.release();
+    x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
     x->d_img_plan.release();
     if (x->d_img_status) (void)hipFree(x->d_img_status);
@@ -396,7 +399,12 @@ static int rebuild_index(edgpu_ctx* x) {
         range[2 * s] = k; range[2 * s + 1] = e;
         k = e;
     }
+    std::vector<uint32_t> pos(nsub, 0xFFFFFFFFu);
+    for (uint32_t k = 0; k < idx.size(); k++) pos[idx[k]] = k;
     HIP_CHECK(x->d_sub_index.reserve(std::max<size_t>(idx.size(), 1), x->stream));
+    HIP_CHECK(x->d_fansub.reserve(std::max<size_t>(idx.size(), 1), x->stream));
+    HIP_CHECK(x->d_sub_pos.reserve(std::max<size_t>(nsub, 1), x->stream));
+    if (nsub) HIP_CHECK(hipMemcpyAsync(x->d_sub_pos.ptr, pos.data(), nsub * 4, hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(x->d_sub_range.reserve(std::max<size_t>(range.size(), 2), x->stream));
     if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_index.ptr, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, x->stream));
     if (!range.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_range.ptr, range.data(), range.size() * 4, hipMemcpyHostToDevice, x->stream));
@@ -489,6 +497,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
     PlanParams p;
     p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
+    p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
     p.sub_out = x->d_sub_out.ptr; p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
     p.blk_bytes_base = x->d_blk_bytes_base.ptr; p.blk_count_base = x->d_blk_count_base.ptr;
@@ -509,7 +518,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(launch_plan(p, x->stream));
     FanoutParams f;
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
-    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
+    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
     f.totals = x->d_totals;
     f.ablate = x->ablate;
     HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
@@ -527,6 +536,10 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
         out->n_substreams = nsub;
     }
     return EDGPU_OK;
+}
+
+const char* edgpu_fanout_kernel(edgpu_ctx* x) {
+    return x ? fanout_name(x->fanout_variant) : "";
 }
 
 int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {

@@ -594,282 +594,49 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         o.out_base = Q.out_base;
         o.out_bytes = Q.bytes;
         P.sub_out[q] = o;
+        const uint32_t pos = P.sub_pos[q];
+        if (pos != 0xFFFFFFFFu) {
+            FanSub f;
+            f.dw = (int64_t)(Q.out_base >> 4) - (int64_t)(Q.vstart >> 4);
+            f.off = (int64_t)(Q.out_base - Q.vstart) + (Q.transport ? 0 : 4);
+            f.a = Q.nonempty ? Q.a : ~0ull;
+            f.ch = Q.transport ? ((uint32_t)Q.channel << 8 | 1u) : 0u;
+            f.db = Q.desc_base - Q.vcstart;
+            P.fansub[pos] = f;
+        }
     }
     // work items: thread q doubles as sender q
     if (q < P.T.nsenders) {
         const SenderDev& D = P.senders[q];
-        for (uint32_t k = 0; k < D.nchunks; k++) P.work[D.chunk_base + k] = WorkItem{q, k};
-    }
-}
-
-// =========================================================================================
-// Fan-out: register-staged, write-many copy
-// =========================================================================================
-
-__global__ __launch_bounds__(kFanoutThreads) void k_fanout(FanoutParams P) {
-    const uint32_t nwork = P.totals->nwork;
-    if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
-    const int tid = threadIdx.x;
-    __shared__ uint64_t m_vb[kChunkPackets + 1];
-    __shared__ uint64_t m_id[kChunkPackets];
-    __shared__ uint32_t m_len[kChunkPackets];
-    __shared__ uint32_t m_vc[kChunkPackets];
-    __shared__ uint32_t startmap[(kChunkWords + 31) / 32];
-    __shared__ unsigned long long s_wire[4];
-    unsigned long long wire = 0, inb = 0;
-
-    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const WorkItem it = P.work[w];
-        const SenderDev& D = P.senders[it.sender];
-        const uint64_t lo = D.umin + (uint64_t)it.chunk * kChunkPackets;
-        const uint64_t head = D.head;
-        const uint32_t np = (uint32_t)min((uint64_t)kChunkPackets, head - lo);
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
-        if (tid < (int)np) {
-            const PktMeta m = meta[(lo + tid) & D.pk_mask];
-            m_vb[tid] = m.vbyte; m_id[tid] = m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
-            inb += m.len;
+        FanWork it;
+        it.ring = D.ring; it.meta = D.meta; it.wmask = D.word_mask; it.pkmask = D.pk_mask;
+        it.sender = q; it.qb = P.sub_range[2 * q]; it.qe = P.sub_range[2 * q + 1];
+        const uint64_t head = D.head;
+        uint64_t lo = D.umin;
+        PktMeta m = meta[lo & D.pk_mask];
+        for (uint32_t k = 0; k < D.nchunks; k++) {
+            const uint64_t hi = min(lo + P.T.chunk, head);
+            const PktMeta mn = hi < head ? meta[hi & D.pk_mask] : PktMeta{D.vbyte_end, 0, 0, 0, 0};
+            it.np = (uint32_t)(hi - lo);
+            it.nw = (uint32_t)((mn.vbyte - m.vbyte) >> 4);
+            it.vc0 = m.vcount;
+            it.lo = lo;
+            it.vb0 = m.vbyte;
+            P.work[D.chunk_base + k] = it;
+            lo = hi;
+            m = mn;
         }
-        if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
-        for (int k = tid; k < (int)((kChunkWords + 31) / 32); k += kFanoutThreads) startmap[k] = 0;
-        __syncthreads();
-        const uint64_t vb0 = m_vb[0];
-        const uint32_t nwords = (uint32_t)((m_vb[np] - vb0) >> 4);
-        if (tid < (int)np && m_len[tid] != 0) {
-            const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
-            atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
-        }
-        __syncthreads();
-        // load the chunk once (HBM -> VGPRs)
-        const u32x4* ring = reinterpret_cast<const u32x4*>(D.ring);
-        const uint64_t rw0 = vb0 >> 4;
-        u32x4 r[kFanoutRegWords];
-        uint32_t smask = 0;
-#pragma unroll
-        for (int j = 0; j < (int)kFanoutRegWords; j++) {
-            const uint32_t wi = tid + j * kFanoutThreads;
-            if (wi < nwords) {
-                r[j] = ring[(rw0 + wi) & D.word_mask];
-                smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
-            }
-        }
-        // write it to every sub-stream of the sender
-        const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
-        for (uint32_t qi = qb; qi < qe; qi++) {
-            const SubDev& Q = P.subs[P.sub_index[qi]];
-            if (!Q.nonempty || Q.a >= lo + np) continue;
-            const uint64_t first = Q.a > lo ? Q.a : lo;
-            const uint32_t fw = (uint32_t)((m_vb[first - lo] - vb0) >> 4);
-            // arena word of chunk word 0 (may precede the sub-stream's region; only words
-            // >= fw are written)
-            const int64_t dw0 = (int64_t)(Q.out_base >> 4) + ((int64_t)(vb0 - Q.vstart) >> 4);
-            u32x4* out = reinterpret_cast<u32x4*>(P.arena);
-            const uint32_t chbits = Q.transport ? ((uint32_t)Q.channel << 8) : 0u;
-#pragma unroll
-            for (int j = 0; j < (int)kFanoutRegWords; j++) {
-                const uint32_t wi = tid + j * kFanoutThreads;
-                if (wi >= fw && wi < nwords) {
-                    u32x4 v = r[j];
-                    if ((smask >> j) & 1u) v.x |= chbits;
-                    __builtin_nontemporal_store(v, &out[dw0 + wi]);
-                }
-            }
-            // descriptors for this sub-stream's packets in the chunk
-            const uint32_t p0 = (uint32_t)(first - lo);
-            if (tid >= (int)p0 && tid < (int)np && m_len[tid] != 0) {
-                const uint32_t len = m_len[tid];
-                const uint64_t off = Q.out_base + (m_vb[tid] - Q.vstart) + (Q.transport ? 0 : 4);
-                const uint32_t wlen = len + (Q.transport ? 4 : 0);
-                const uint32_t di = Q.desc_base + (m_vc[tid] - Q.vcstart);
-                u32x4 dv;
-                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = (uint32_t)m_id[tid];
-                __builtin_nontemporal_store(dv, reinterpret_cast<u32x4*>(P.desc) + di);
-                wire += wlen;
-            }
-        }
-        __syncthreads();
     }
-    unsigned long long tot, tin;
-    (void)block_exclusive_scan<unsigned long long>(wire, s_wire, tot);
-    (void)block_exclusive_scan<unsigned long long>(inb, s_wire, tin);
-    if (tid == 0 && tot) {
-        atomicAdd(&P.totals->relayed_bytes, tot);
-        atomicAdd(&P.totals->cum_relayed_bytes, tot);
-    }
-    if (tid == 0 && tin) atomicAdd(&P.totals->cum_fanout_in_bytes, tin);
 }
 
+// =========================================================================================
+// Fan-out
+// =========================================================================================
 
-// -----------------------------------------------------------------------------------------
-// k_fanout2: same contract as k_fanout, restructured for occupancy and latency:
-//   * THREADS-wide workgroups (512 = 8 waves), so a 32-packet chunk needs only
-//     ceil(4128 / THREADS) VGPR quads per lane;
-//   * the sender's sub-stream table is staged in LDS once per work item (one parallel load)
-//     instead of a dependent global load per sub-stream inside the store loop;
-//   * descriptors are written with one lane per (sub-stream, packet) pair.
-// NT selects non-temporal (streaming) stores for the arena and descriptors.
-// -----------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
-}
-
-template <int THREADS, int CHUNK, bool NT, int WAVES>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WAVES)))
-void k_fanout2(FanoutParams P) {
-    constexpr int CWORDS = CHUNK * 129;                  // CHUNK * roundup16(4 + 2060) / 16
-    constexpr int NW = (CWORDS + THREADS - 1) / THREADS;
-    constexpr int NWAVES = THREADS / 64;
-    const uint32_t nwork = P.totals->nwork;
-    if (P.totals->status == EDGPU_OUT_OVERFLOW) return;
-    const int tid = threadIdx.x;
-    __shared__ uint64_t m_vb[CHUNK + 1];
-    __shared__ uint32_t m_id[CHUNK];
-    __shared__ uint32_t m_len[CHUNK];
-    __shared__ uint32_t m_vc[CHUNK];
-    __shared__ uint32_t startmap[(CWORDS + 31) / 32];
-    // per sub-stream parameters (one batch of up to THREADS sub-streams)
-    __shared__ int64_t  q_dw0[THREADS];      // arena word of chunk word 0
-    __shared__ int64_t  q_off[THREADS];      // out_base - vstart (+4 for UDP)
-    __shared__ uint32_t q_fw[THREADS];       // first chunk word to write (>= nwords: skip)
-    __shared__ uint32_t q_ch[THREADS];       // channel bits for TCP, 0 for UDP
-    __shared__ uint32_t q_db[THREADS];       // desc_base - vcstart
-    __shared__ uint32_t q_p0[THREADS];       // first chunk packet of this sub-stream
-    __shared__ uint32_t q_hl[THREADS];       // wire header bytes: 4 for TCP, 0 for UDP
-    __shared__ unsigned long long s_red[NWAVES];
-    unsigned long long wire = 0, inb = 0;
-    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
-
-    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const WorkItem it = P.work[w];
-        const SenderDev& D = P.senders[it.sender];
-        const uint64_t lo = D.umin + (uint64_t)it.chunk * CHUNK;
-        const uint64_t head = D.head;
-        const uint32_t np = (uint32_t)min((uint64_t)CHUNK, head - lo);
-        const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
-        // ---- phase 1: packet metadata of the chunk -> LDS --------------------------------
-        if (tid < (int)np) {
-            const PktMeta m = meta[(lo + tid) & D.pk_mask];
-            m_vb[tid] = m.vbyte; m_id[tid] = (uint32_t)m.id; m_len[tid] = m.len; m_vc[tid] = m.vcount;
-            inb += m.len;
-        }
-        if (tid == (int)np) m_vb[np] = (lo + np == head) ? D.vbyte_end : meta[(lo + np) & D.pk_mask].vbyte;
-        for (int k = tid; k < (int)((CWORDS + 31) / 32); k += THREADS) startmap[k] = 0;
-        __syncthreads();
-        const uint64_t vb0 = m_vb[0];
-        const uint32_t nw = uni((uint32_t)((m_vb[np] - vb0) >> 4));
-        if (tid < (int)np && m_len[tid] != 0) {
-            const uint32_t sw = (uint32_t)((m_vb[tid] - vb0) >> 4);
-            atomicOr(&startmap[sw >> 5], 1u << (sw & 31));
-        }
-        const uint32_t qb = P.sub_range[2 * it.sender], qe = P.sub_range[2 * it.sender + 1];
-        for (uint32_t q0 = qb; q0 < qe; q0 += THREADS) {
-            const uint32_t nq = min((uint32_t)THREADS, qe - q0);
-            // ---- phase 2: this batch's sub-stream parameters -> LDS (before the chunk is
-            // loaded, so this 64-bit bookkeeping never overlaps the live chunk registers) ----
-            if (tid < (int)nq) {
-                const SubDev& Q = P.subs[P.sub_index[q0 + tid]];
-                uint32_t fw = 0xFFFFFFFFu, p0 = 0xFFFFFFFFu;
-                if (Q.nonempty && Q.a < lo + np) {
-                    const uint64_t first = Q.a > lo ? Q.a : lo;
-                    p0 = (uint32_t)(first - lo);
-                    fw = (uint32_t)((m_vb[p0] - vb0) >> 4);
-                }
-                q_fw[tid] = fw;
-                q_p0[tid] = p0;
-                q_dw0[tid] = (int64_t)(Q.out_base >> 4) + ((int64_t)(vb0 - Q.vstart) >> 4);
-                q_off[tid] = (int64_t)(Q.out_base - Q.vstart) + (Q.transport ? 0 : 4);
-                q_ch[tid] = Q.transport ? ((uint32_t)Q.channel << 8) : 0u;
-                q_db[tid] = Q.desc_base - Q.vcstart;
-                q_hl[tid] = Q.transport ? 4u : 0u;
-            }
-            __syncthreads();
-            // ---- phase 3: the chunk HBM -> VGPRs, once ------------------------------------
-            // Buffer loads through a descriptor built from wave-uniform values: one 32-bit
-            // offset per lane, lanes past the chunk read 0 (range check).
-            const uint32_t wmask = uni(D.word_mask);
-            const uint32_t rstart = uni((uint32_t)((vb0 >> 4) & wmask));
-            const bool wraps = rstart + nw > wmask + 1;
-            u32x4 r[NW];
-            if (!wraps) {
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    reinterpret_cast<u32x4*>(D.ring) + rstart, 0, nw * 16, 0x00020000);
-#pragma unroll
-                for (int j = 0; j < NW; j++)
-                    r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(tid + j * THREADS) * 16u, 0, 0);
-            } else {
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    reinterpret_cast<u32x4*>(D.ring), 0, (wmask + 1) * 16, 0x00020000);
-#pragma unroll
-                for (int j = 0; j < NW; j++) {
-                    const uint32_t wi = tid + j * THREADS;
-                    r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu, 0, 0);
-                }
-            }
-            uint32_t smask = 0;
-#pragma unroll
-            for (int j = 0; j < NW; j++) {
-                const uint32_t wi = tid + j * THREADS;
-                if (wi < nw) smask |= ((startmap[wi >> 5] >> (wi & 31)) & 1u) << j;
-            }
-            // ---- phase 4: write the chunk to every sub-stream ------------------------------
-            for (uint32_t q = 0; q < nq && !(P.ablate & 2u); q++) {
-                const uint32_t fw = uni(q_fw[q]);
-                if (fw >= nw) continue;
-                // Store descriptor over this sub-stream's part of the chunk [fw, nw): lanes
-                // outside it get an out-of-range offset and the hardware drops the store.
-                const int64_t dw0 = (int64_t)uni64((uint64_t)q_dw0[q]);
-                const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
-                    out + dw0 + fw, 0, (nw - fw) * 16, 0x00020000);
-                const uint32_t vbase = (uint32_t)(tid - (int)fw) * 16u;
-                const uint32_t chbits = uni(q_ch[q]);
-#pragma unroll
-                for (int j = 0; j < NW; j++)
-                    __builtin_amdgcn_raw_buffer_store_b128(r[j], os, vbase + j * THREADS * 16, 0, NT ? 2 : 0);
-                if (chbits) {            // TCP: rewrite each slot's '$' header dword with the channel
-#pragma unroll                          // (same lane, same address, program order)
-                    for (int j = 0; j < NW; j++) {
-                        const uint32_t off = ((smask >> j) & 1u) ? vbase + j * THREADS * 16 : 0xFFFFFFFFu;
-                        __builtin_amdgcn_raw_buffer_store_b32(r[j].x | chbits, os, off, 0, NT ? 2 : 0);
-                    }
-                }
-            }
-            // ---- phase 5: descriptors, one lane per (sub-stream, packet); chunk regs dead ---
-            for (uint32_t t = tid; t < (P.ablate & 1u ? 0u : nq * np); t += THREADS) {
-                const uint32_t q = t / np, p = t - q * np;
-                if (p < q_p0[q] || m_len[p] == 0) continue;
-                const uint32_t len = m_len[p];
-                const uint64_t off = (uint64_t)(q_off[q] + (int64_t)m_vb[p]);
-                const uint32_t wlen = len + q_hl[q];
-                const uint32_t di = q_db[q] + m_vc[p];
-                u32x4 dv;
-                dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
-                if (NT) __builtin_nontemporal_store(dv, reinterpret_cast<u32x4*>(P.desc) + di);
-                else reinterpret_cast<u32x4*>(P.desc)[di] = dv;
-                wire += wlen;
-            }
-            __syncthreads();
-        }
-    }
-    // block reduction of the byte counters
-    unsigned long long a = wire, b = inb;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
-    if ((tid & 63) == 0) s_red[tid >> 6] = a;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long tot = 0;
-        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
-        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
-    }
-    __syncthreads();
-    if ((tid & 63) == 0) s_red[tid >> 6] = b;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long tot = 0;
-        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
-        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
-    }
 }
 
 // -----------------------------------------------------------------------------------------
@@ -920,9 +687,9 @@ void k_fanout3(FanoutParams P) {
     u32x4* out = reinterpret_cast<u32x4*>(P.arena);
 
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const WorkItem it = P.work[w];
+        const FanWork it = P.work[w];
         const SenderDev& D = P.senders[it.sender];
-        const uint64_t lo = D.umin + (uint64_t)it.chunk * CHUNK;
+        const uint64_t lo = it.lo;
         const uint64_t head = D.head;
         const uint32_t np = (uint32_t)min((uint64_t)CHUNK, head - lo);
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
@@ -1039,6 +806,206 @@ void k_fanout3(FanoutParams P) {
     }
     __syncthreads();
     if ((tid & 63) == 0) s_red[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
+    }
+}
+
+// -----------------------------------------------------------------------------------------
+// k_fanout4: k_fanout3's line-aligned LDS write-many, restructured so that loading a chunk never
+// stalls the store stream.
+//   * Everything a work item needs before its loads comes from one 64-B FanWork record
+//     (k_plan_final), read through the constant address space, so it lands in SGPRs: the
+//     ring's buffer resource is scalar and the chunk's 16-B loads issue back to back.
+//     (k_fanout3 built that resource from a per-lane load, which the compiler lowers to a
+//     waterfall loop that waits for every load in turn.)
+//   * Sub-stream parameters are one 32-B FanSub per sub-stream in sender order, also scalar
+//     loads: no sub_index -> SubDev chain and no per-sender LDS batch.
+//   * The NEXT item's chunk words and packet metadata are loaded into registers as soon as
+//     this item's LDS image is complete, so their HBM latency runs under this item's stores;
+//     the LDS image is refilled from those registers after the end-of-item barrier.
+//   * The slot-start bitmap (TCP channel patch) is double-buffered by item parity, so
+//     clearing it needs no extra barrier.
+// Stores: per sub-stream, lanes walk the destination in whole 128-B lines (k_fanout3), with a
+// uniform trip count, so no store instruction is issued for words past the chunk.
+// -----------------------------------------------------------------------------------------
+// Loads a record written by an earlier kernel through the constant address space: uniform
+// addresses become scalar (s_load) loads, whose results live in SGPRs.
+template <typename T>
+__device__ __forceinline__ T const_load(const T* p) {
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    static_assert(sizeof(T) % 4 == 0, "");
+    T v;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+    cu32* src = (cu32*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) d[i] = src[i];
+    return v;
+}
+
+template <int THREADS, int CHUNK>
+constexpr int fanout4_lds() {
+    return CHUNK * kSlotWordsMax * 16 + (CHUNK + 2) * 8 + 4 * CHUNK * 4 +
+           2 * ((((CHUNK * kSlotWordsMax + 31) / 32) + 3) & ~3) * 4 + (THREADS / 64) * 8;
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+
+// Issues one work item's loads into registers: the chunk's slot words (NL per lane) and, for
+// lanes < np, the packet's metadata as raw words (ma = vbyte, id low; mb = len, vcount), decoded
+// only when the LDS image is written, so the registers stay exactly as loaded while the loads
+// are in flight.  All are buffer loads (vector-memory counter only; a flat load would also hold
+// the LDS counter that the store loop waits on).
+template <int THREADS, int NL>
+__device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r)[NL], u32x3& ma, u32x2& mb) {
+    const uint32_t wmask = it.wmask, nw = it.nw;
+    const uint32_t rstart = (uint32_t)(it.vb0 >> 4) & wmask;
+    const bool wraps = rstart + nw > wmask + 1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<u32x4*>(it.ring) + (wraps ? 0u : rstart), 0, wraps ? (wmask + 1) * 16 : nw * 16, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const uint32_t wi = tid + j * THREADS;
+        if ((uint32_t)(j * THREADS) < nw)              // uniform: no load past the chunk's lines
+            r[j] = __builtin_amdgcn_raw_buffer_load_b128(
+                rs, wraps ? (wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu) : wi * 16u, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(it.meta), 0, (it.pkmask + 1) * (uint32_t)sizeof(PktMeta), 0x00020000);
+    const uint32_t mo = (uint32_t)tid < it.np ? (uint32_t)((it.lo + tid) & it.pkmask) * (uint32_t)sizeof(PktMeta) : 0xFFFFFFE0u;
+    ma = __builtin_amdgcn_raw_buffer_load_b96(ms, mo, 0, 0);
+    mb = __builtin_amdgcn_raw_buffer_load_b64(ms, mo + 24u, 0, 0);
+}
+
+template <int THREADS, int CHUNK>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
+void k_fanout4(FanoutParams P) {
+    constexpr int CWORDS = CHUNK * kSlotWordsMax;
+    constexpr int NL = (CWORDS + THREADS - 1) / THREADS;              // chunk words per lane
+    constexpr int NWAVES = THREADS / 64;
+    constexpr int SM = ((CWORDS + 31) / 32 + 3) & ~3;                  // bitmap words, x4
+    static_assert(CHUNK <= 56, "descriptor windows assume one wave covers a chunk's packets");
+    const uint32_t nwork = uni(P.totals->nwork);
+    if (uni((uint32_t)P.totals->status) == (uint32_t)EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wv = uni((uint32_t)tid >> 6);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    u32x4* cbuf = reinterpret_cast<u32x4*>(lds);                       // CWORDS words
+    uint64_t* m_vb = reinterpret_cast<uint64_t*>(cbuf + CWORDS);       // CHUNK + 2
+    uint32_t* m_id = reinterpret_cast<uint32_t*>(m_vb + CHUNK + 2);
+    uint32_t* m_len = m_id + CHUNK;
+    uint32_t* m_vc = m_len + CHUNK;
+    uint32_t* m_nzp = m_vc + CHUNK;                                    // non-empty ordinal -> packet
+    uint32_t* smap = m_nzp + CHUNK;                                    // 2 x SM, by item parity
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smap + 2 * SM);
+    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+    unsigned long long wire = 0, inb = 0;
+
+    for (int k = tid; k < 2 * SM; k += THREADS) smap[k] = 0;
+    u32x4 r[NL];
+    u32x3 ma;
+    u32x2 mb;
+    uint32_t w = blockIdx.x;
+    FanWork nx;
+    if (w < nwork) {
+        nx = const_load(P.work + w);
+        fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+    }
+    for (uint32_t par = 0; w < nwork; w += gridDim.x, par ^= 1u) {
+        const FanWork it = nx;
+        const uint64_t lo = it.lo, vb0 = it.vb0;
+        const uint32_t np = it.np, nw = it.nw, vc0 = it.vc0;
+        uint32_t* sm = smap + par * SM;
+        // ---- this item's LDS image, from the registers loaded one item earlier ----------
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+            const uint32_t wi = tid + j * THREADS;
+            if ((uint32_t)(j * THREADS) < nw && wi < nw) cbuf[wi] = r[j];
+        }
+        if ((uint32_t)tid < np) {
+            const uint64_t vbyte = (uint64_t)ma.y << 32 | ma.x;
+            const uint32_t len = mb.x, vcount = mb.y;
+            m_vb[tid] = vbyte; m_id[tid] = ma.z; m_len[tid] = len; m_vc[tid] = vcount;
+            inb += len;
+            if (len != 0) {
+                const uint32_t sw = (uint32_t)((vbyte - vb0) >> 4);
+                atomicOr(&sm[sw >> 5], 1u << (sw & 31));
+                m_nzp[vcount - vc0] = tid;
+            }
+        }
+        if (tid == 0) m_vb[np] = vb0 + (uint64_t)nw * 16;
+        __syncthreads();
+        // ---- the other parity's bitmap is free now: clear it for the next item ----------
+        for (int k = tid; k < SM; k += THREADS) smap[(par ^ 1u) * SM + k] = 0;
+        // ---- next item's loads, in flight under this item's stores ------------------------
+        const uint32_t wn = w + gridDim.x;
+        if (wn < nwork) {
+            nx = const_load(P.work + wn);
+            fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+        }
+        // ---- write the chunk to every sub-stream of the sender ----------------------------
+        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+            const FanSub f = const_load(P.fansub + q);
+            if (f.a >= lo + np) continue;
+            const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+            const uint32_t fw = uni((uint32_t)((m_vb[p0] - vb0) >> 4));
+            const int64_t A = f.dw + (int64_t)(vb0 >> 4) + fw;                 // first dest word
+            const uint32_t s = (uint32_t)(A & 7);                              // words past a line
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
+            const uint32_t chb = f.ch & 0xFF00u;
+            const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            for (uint32_t j = 0; j < nj; j++) {
+                const uint32_t lw = tid + j * THREADS;                         // word of the aligned window
+                const uint32_t src = fw + lw - s;                              // chunk word it carries
+                const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
+                u32x4 v = cbuf[srcc];
+                if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
+                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, 0);
+            }
+        }
+        // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
+        {
+            const uint32_t nzc = np ? m_vc[np - 1] - vc0 + (m_len[np - 1] != 0) : 0u;
+            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+                const FanSub f = const_load(P.fansub + q);
+                if (f.a >= lo + np) continue;
+                const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+                const uint32_t o0 = m_vc[p0] - vc0;                            // first ordinal
+                if (o0 >= nzc) continue;
+                const uint32_t d0 = f.db + m_vc[p0];
+                const uint32_t sh = d0 & 7;
+                const uint32_t o = o0 + lane - sh;
+                if ((uint32_t)lane >= sh && o < nzc) {
+                    const uint32_t p = m_nzp[o];
+                    const uint32_t len = m_len[p];
+                    const uint64_t off = (uint64_t)(f.off + (int64_t)m_vb[p]);
+                    const uint32_t wlen = len + ((f.ch & 1u) ? 4u : 0u);
+                    u32x4 dv;
+                    dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
+                    reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    wire += wlen;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    unsigned long long a = wire, b = inb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+    if (lane == 0) s_red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
+    }
+    __syncthreads();
+    if (lane == 0) s_red[tid >> 6] = b;
     __syncthreads();
     if (tid == 0) {
         unsigned long long tot = 0;
@@ -1214,27 +1181,27 @@ static int occupancy_of(const void* fn, int threads, int lds) {
 }
 struct FanoutVariant { const void* fn; int threads; int chunk; int lds; };
 static const FanoutVariant kVariants[] = {
-    {(const void*)k_fanout, kFanoutThreads, kChunkPackets, 0},                      // 0 legacy
-    {(const void*)k_fanout2<512, 32, true, 1>, 512, 32, 0},                         // 1 nt
-    {(const void*)k_fanout2<512, 32, false, 1>, 512, 32, 0},                        // 2
-    {(const void*)k_fanout2<1024, 32, false, 1>, 1024, 32, 0},                      // 3
-    {(const void*)k_fanout2<512, 32, false, 6>, 512, 32, 0},                        // 4
-    {(const void*)k_fanout2<512, 32, false, 8>, 512, 32, 0},                        // 5
-    {(const void*)k_fanout2<256, 16, false, 8>, 256, 16, 0},                        // 6
-    {(const void*)k_fanout2<512, 16, false, 8>, 512, 16, 0},                        // 7
-    {(const void*)k_fanout2<1024, 32, false, 8>, 1024, 32, 0},                      // 8
-    {(const void*)k_fanout3<1024, 32>, 1024, 32, fanout3_lds<1024, 32>()},          // 9  LDS, aligned
-    {(const void*)k_fanout3<512, 32>, 512, 32, fanout3_lds<512, 32>()},             // 10
-    {(const void*)k_fanout3<512, 16>, 512, 16, fanout3_lds<512, 16>()},             // 11
-    {(const void*)k_fanout3<256, 16>, 256, 16, fanout3_lds<256, 16>()},             // 12
+    {(const void*)k_fanout3<1024, 32>, 1024, 32, fanout3_lds<1024, 32>()},          // 0 r01 LDS, aligned
+    {(const void*)k_fanout3<512, 16>, 512, 16, fanout3_lds<512, 16>()},             // 1
+    {(const void*)k_fanout4<1024, 32>, 1024, 32, fanout4_lds<1024, 32>()},          // 2 scalar headers, prefetch
+    {(const void*)k_fanout4<512, 32>, 512, 32, fanout4_lds<512, 32>()},             // 3
+    {(const void*)k_fanout4<1024, 16>, 1024, 16, fanout4_lds<1024, 16>()},          // 4
+    {(const void*)k_fanout4<512, 16>, 512, 16, fanout4_lds<512, 16>()},             // 5
 };
+static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
+                                            "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+static const int kDefaultVariant = 2;
 int fanout_chunk(int variant) {
-    if (variant < 0 || variant >= kNumVariants) variant = 2;
+    if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
     return kVariants[variant].chunk;
 }
+const char* fanout_name(int variant) {
+    if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
+    return kVariantNames[variant];
+}
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
-    if (variant < 0 || variant >= kNumVariants) variant = 2;
+    if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
     static int occ[32] = {0};
     const FanoutVariant& v = kVariants[variant];
     if (!occ[variant]) {

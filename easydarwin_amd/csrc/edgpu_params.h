@@ -38,8 +38,11 @@ struct PlanParams {
     SenderDev* senders;
     SubDev* subs;
     const uint32_t* sub_index;
+    const uint32_t* sub_pos;    // SubDev index -> position in sub_index order (~0: inactive)
+    const uint32_t* sub_range;  // per sender [begin, end) into sub_index
     edgpu_substream_out* sub_out;
-    WorkItem* work;
+    FanWork* work;
+    FanSub* fansub;             // per sub_index position
     uint64_t* blk_bytes;        // per K2 block partials
     uint32_t* blk_count;
     uint64_t* blk_bytes_base;
@@ -53,7 +56,8 @@ struct FanoutParams {
     const uint32_t* sub_range;  // per sender [begin, end) into sub_index
     const SubDev* subs;
     const uint32_t* sub_index;
-    const WorkItem* work;
+    const FanWork* work;
+    const FanSub* fansub;
     uint8_t* arena;
     edgpu_out_desc* desc;
     TickTotals* totals;

@@ -27,7 +27,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
-    "edgpu_device_free",
+    "edgpu_device_free", "edgpu_fanout_kernel",
 ]
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 
@@ -139,6 +139,7 @@ def load(path: str = LIB_PATH):
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
+        "edgpu_fanout_kernel": (C.c_char_p, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -236,6 +237,10 @@ class Context:
         a = (C.c_float * 4)()
         _check(self.lib.edgpu_last_timings(self.h, a))
         return {"fanout_ms": a[0], "tick_ms": a[1], "ingest_ms": a[2], "keyframe_ms": a[3]}
+
+    def fanout_kernel(self) -> str:
+        """Name of the fan-out copy kernel this context launches."""
+        return self.lib.edgpu_fanout_kernel(self.h).decode()
 
     def counters(self) -> dict:
         c = Counters()

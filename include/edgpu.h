@@ -173,6 +173,9 @@ int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
 
+/* Name of the fan-out copy kernel this context launches (for measurement reports). */
+const char* edgpu_fanout_kernel(edgpu_ctx* ctx);
+
 /* Cumulative counters since context creation (syncs).  fanout_in_bytes counts the
  * ingested bytes the fan-out read (each referenced packet once per launch). */
 typedef struct edgpu_counters {
