@@ -127,6 +127,9 @@ def main():
     ap.add_argument("--subs", type=int, default=16, help="UDP subscribers per session")
     ap.add_argument("--tick-ms", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="tick pipelining: ingest(t+1) beside the fan-out copy of t on a second stream "
+                         "(measured slower on C2: both phases are HBM-bound and contend)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,7 +164,8 @@ def main():
     ctx = edgpu.Context(device=local, video_ring_packets=8192, video_ring_bytes=16 << 20,
                         other_ring_packets=256, other_ring_bytes=64 << 10,
                         out_arena_bytes=max_arena, max_out_packets=max_out,
-                        max_batch_packets=max_pk + 1, max_batch_bytes=1 << 20)
+                        max_batch_packets=max_pk + 1, max_batch_bytes=1 << 20,
+                        overlap_ticks=1 if args.overlap else 0)
     for _ in gids:
         s = ctx.session_add(fleet.sdp())
         for _k in range(args.subs):

@@ -77,6 +77,7 @@ struct SenderDev {
     uint64_t tail;                  // oldest index still intact in both rings
     uint64_t umin;                  // min range start over this sender's sub-streams
     uint32_t chunk_base, nchunks;   // fan-out work items
+    uint64_t fan_lo, fan_vlo;       // oldest packet index / vbyte the last fan-out reads
 };
 
 // ---- Session images (cross-GPU keyframe fast start) ----
@@ -200,6 +201,8 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long cum_fanout_in_bytes;
     unsigned long long cum_ingested_packets;
     unsigned long long cum_ingested_bytes;
+    int ingest_status;              // sticky: an ingest lapped data an in-flight fan-out reads
+    int _pad;
 };
 
 struct TickParams {

@@ -86,6 +86,12 @@ struct edgpu_ctx {
     uint32_t ablate = 0;
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
     hipStream_t stream = nullptr;
+    // tick pipelining (edgpu_config.overlap_ticks): the fan-out copy kernel runs on `copy`,
+    // ordered after its plan by ev_plan; the next plan waits for ev_copy
+    bool overlap = false;
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_plan = nullptr, ev_copy = nullptr;
+    int cur = 0;                    // output buffer of the current tick (0 / 1)
     hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
@@ -130,8 +136,9 @@ struct edgpu_ctx {
     uint32_t pend_nseg = 0;
     bool pending = false;
 
-    uint8_t* d_arena = nullptr;
-    edgpu_out_desc* d_out_desc = nullptr;
+    uint8_t* d_arena_buf[2] = {nullptr, nullptr};
+    edgpu_out_desc* d_out_desc_buf[2] = {nullptr, nullptr};
+    DevVec<edgpu_substream_out> d_sub_out_buf2;   // second sub-stream table (overlap)
     // session images
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
@@ -198,8 +205,16 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipMalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
     if (hipMalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
     if (hipMalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
-    if (hipMalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
-    if (hipMalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
+    x->overlap = c.overlap_ticks != 0;
+    for (int k = 0; k < (x->overlap ? 2 : 1); k++) {
+        if (hipMalloc(&x->d_arena_buf[k], c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
+        if (hipMalloc(&x->d_out_desc_buf[k], sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
+    }
+    if (x->overlap) {
+        if (hipStreamCreateWithFlags(&x->copy, hipStreamNonBlocking) != hipSuccess) return bad("copy stream");
+        if (hipEventCreateWithFlags(&x->ev_plan, hipEventDisableTiming) != hipSuccess) return bad("event");
+        if (hipEventCreateWithFlags(&x->ev_copy, hipEventDisableTiming) != hipSuccess) return bad("event");
+    }
     if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
@@ -213,25 +228,37 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (!x) return EDGPU_OK;
     (void)hipSetDevice(x->device);
     if (x->stream) (void)hipStreamSynchronize(x->stream);
+    if (x->copy) (void)hipStreamSynchronize(x->copy);
     for (void* p : x->ring_allocs) (void)hipFree(p);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
-    x->d_img_plan.release();
+    x->d_img_plan.release(); x->d_sub_out_buf2.release();
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
-                    (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals})
+                    (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
+                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
         if (p) (void)hipFree(p);
     for (auto& e : x->ev) if (e) (void)hipEventDestroy(e);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
+    if (x->ev_plan) (void)hipEventDestroy(x->ev_plan);
+    if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
+    if (x->copy) (void)hipStreamDestroy(x->copy);
     if (x->stream) (void)hipStreamDestroy(x->stream);
     delete x;
     return EDGPU_OK;
 }
 
+// Waits for everything the context has enqueued (both streams with overlap_ticks).
+static hipError_t sync_all(edgpu_ctx* x) {
+    hipError_t e = hipStreamSynchronize(x->stream);
+    if (e == hipSuccess && x->copy) e = hipStreamSynchronize(x->copy);
+    return e;
+}
+
 int edgpu_sync(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(sync_all(x));
     return EDGPU_OK;
 }
 
@@ -379,9 +406,9 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
 }
 
 // Records the start / end events of launch kind `w` into the history ring.
-static hipError_t hist_mark(edgpu_ctx* x, int w, int end) {
+static hipError_t hist_mark(edgpu_ctx* x, int w, int end, hipStream_t st = nullptr) {
     const uint32_t slot = x->hist_n[w] % edgpu_ctx::kHist;
-    hipError_t e = hipEventRecord(x->hist[w][slot][end], x->stream);
+    hipError_t e = hipEventRecord(x->hist[w][slot][end], st ? st : x->stream);
     if (end) x->hist_n[w]++;
     return e;
 }
@@ -410,6 +437,7 @@ static int rebuild_index(edgpu_ctx* x) {
     if (!range.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_range.ptr, range.data(), range.size() * 4, hipMemcpyHostToDevice, x->stream));
     const uint32_t nblk = (nsub + 255) / 256;
     HIP_CHECK(x->d_sub_out.reserve(std::max<uint32_t>(nsub, 1), x->stream));
+    if (x->overlap) HIP_CHECK(x->d_sub_out_buf2.reserve(std::max<uint32_t>(nsub, 1), x->stream));
     HIP_CHECK(x->d_blk_bytes.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_bytes_base.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_count.reserve(std::max<uint32_t>(nblk, 1), x->stream));
@@ -459,6 +487,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = x->ingest_mode;
     p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
+    p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;
     HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
@@ -493,12 +522,22 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     HIP_CHECK(hipSetDevice(x->device));
+    if (x->overlap) {
+        // the index rebuild may reallocate tables the in-flight copy reads
+        if (x->index_dirty) HIP_CHECK(hipStreamSynchronize(x->copy));
+        // this tick's plan rewrites the work list and sub-stream records the previous copy reads
+        HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
+        x->cur ^= 1;
+    }
     if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    edgpu_substream_out* sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
+    uint8_t* arena = x->d_arena_buf[x->cur];
+    edgpu_out_desc* odesc = x->d_out_desc_buf[x->cur];
     PlanParams p;
     p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
     p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
-    p.sub_out = x->d_sub_out.ptr; p.work = x->d_work.ptr;
+    p.sub_out = sub_out; p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
     p.blk_bytes_base = x->d_blk_bytes_base.ptr; p.blk_count_base = x->d_blk_count_base.ptr;
     p.totals = x->d_totals;
@@ -518,21 +557,30 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(launch_plan(p, x->stream));
     FanoutParams f;
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
-    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr; f.arena = x->d_arena; f.desc = x->d_out_desc;
+    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr; f.arena = arena; f.desc = odesc;
+    f.arena_words = x->cfg.out_arena_bytes / 16;
+    f.max_desc = x->cfg.max_out_packets;
     f.totals = x->d_totals;
     f.ablate = x->ablate;
-    HIP_CHECK(hipEventRecord(x->ev[1], x->stream));
-    HIP_CHECK(hist_mark(x, 0, 0));
-    HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, x->stream));
-    HIP_CHECK(hist_mark(x, 0, 1));
-    HIP_CHECK(hist_mark(x, 1, 1));
-    HIP_CHECK(hipEventRecord(x->ev[2], x->stream));
+    hipStream_t cs = x->stream;
+    if (x->overlap) {
+        HIP_CHECK(hipEventRecord(x->ev_plan, x->stream));
+        HIP_CHECK(hipStreamWaitEvent(x->copy, x->ev_plan, 0));
+        cs = x->copy;
+    }
+    HIP_CHECK(hipEventRecord(x->ev[1], cs));
+    HIP_CHECK(hist_mark(x, 0, 0, cs));
+    HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, cs));
+    HIP_CHECK(hist_mark(x, 0, 1, cs));
+    HIP_CHECK(hist_mark(x, 1, 1, cs));
+    HIP_CHECK(hipEventRecord(x->ev[2], cs));
+    if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_launches++;
     x->timed_fanout = true;
     if (out) {
-        out->arena = x->d_arena;
-        out->desc = x->d_out_desc;
-        out->substreams = x->d_sub_out.ptr;
+        out->arena = arena;
+        out->desc = odesc;
+        out->substreams = sub_out;
         out->n_substreams = nsub;
     }
     return EDGPU_OK;
@@ -546,6 +594,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
+    HIP_CHECK(sync_all(x));
     HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
     out->relayed_packets = t.relayed_packets;
@@ -553,7 +602,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->arena_bytes = t.arena_bytes;
     out->ingested_packets = t.ingested_packets;
     out->ingested_bytes = t.ingested_bytes;
-    out->status = t.status;
+    out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
     return EDGPU_OK;
 }
@@ -562,6 +611,7 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
+    HIP_CHECK(sync_all(x));
     HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
     out->relayed_packets = t.cum_relayed_packets;
@@ -576,7 +626,7 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
 int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, uint32_t* out_n) {
     if (!x || which < 0 || which > 3 || (!out_ms && max_n)) return fail(EDGPU_BAD_ARGUMENT, "bad argument");
     HIP_CHECK(hipSetDevice(x->device));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(sync_all(x));
     const uint32_t n = std::min<uint32_t>(x->hist_n[which], edgpu_ctx::kHist);
     const uint32_t first = x->hist_n[which] - n;
     uint32_t k = 0;
@@ -593,6 +643,7 @@ int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes)
     if (!x || (!dst && bytes) || (!src && bytes)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (!bytes) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(sync_all(x));
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
     return EDGPU_OK;
@@ -601,7 +652,7 @@ int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes)
 int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     if (!x || !out_ms) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(sync_all(x));
     out_ms[0] = out_ms[1] = out_ms[2] = out_ms[3] = 0.f;
     if (x->timed_fanout) {
         HIP_CHECK(hipEventElapsedTime(&out_ms[0], x->ev[1], x->ev[2]));
@@ -773,6 +824,7 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
         }
     }
     if (plan.empty()) return EDGPU_OK;
+    if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
     return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);
 }
 

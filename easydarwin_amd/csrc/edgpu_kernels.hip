@@ -55,6 +55,8 @@ __device__ bool key_frame_first_packet(const uint8_t* p, uint32_t len) {
     return t == 5 || t == 7 || t == 8;
 }
 
+__device__ __forceinline__ void set_status(int* st, int code) { atomicCAS(st, 0, code); }
+
 // Header bytes held in registers: hdr[k] holds packet bytes 4k..4k+3 (little-endian).
 __device__ __forceinline__ uint32_t hbyte(const uint32_t* h, int i) { return (h[i >> 2] >> (8 * (i & 3))) & 0xFF; }
 __device__ __forceinline__ uint32_t hbe16(const uint32_t* h, int i) { return hbyte(h, i) << 8 | hbyte(h, i + 1); }
@@ -305,6 +307,11 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         SenderDev& D = P.senders[S.first_sender + tid];
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
+        // tick pipelining: this batch must not lap what the previous tick's fan-out (possibly
+        // still running on the other stream) reads
+        if (P.overlap && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
+                          s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
+            atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);
     }
     if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];
     // block totals
@@ -615,6 +622,9 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         const uint64_t head = D.head;
         uint64_t lo = D.umin;
         PktMeta m = meta[lo & D.pk_mask];
+        SenderDev& Dw = P.senders[q];
+        Dw.fan_lo = D.nchunks ? lo : head;
+        Dw.fan_vlo = D.nchunks ? m.vbyte : D.vbyte_end;
         for (uint32_t k = 0; k < D.nchunks; k++) {
             const uint64_t hi = min(lo + P.T.chunk, head);
             const PktMeta mn = hi < head ? meta[hi & D.pk_mask] : PktMeta{D.vbyte_end, 0, 0, 0, 0};
@@ -786,7 +796,7 @@ void k_fanout3(FanoutParams P) {
                         const uint32_t wlen = len + q_hl[q];
                         u32x4 dv;
                         dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
-                        reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                        if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
                         wire += wlen;
                     }
                 }
@@ -955,6 +965,7 @@ void k_fanout4(FanoutParams P) {
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
             const uint32_t fw = uni((uint32_t)((m_vb[p0] - vb0) >> 4));
             const int64_t A = f.dw + (int64_t)(vb0 >> 4) + fw;                 // first dest word
+            if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
             const uint32_t s = (uint32_t)(A & 7);                              // words past a line
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
             const uint32_t chb = f.ch & 0xFF00u;
@@ -987,7 +998,7 @@ void k_fanout4(FanoutParams P) {
                     const uint32_t wlen = len + ((f.ch & 1u) ? 4u : 0u);
                     u32x4 dv;
                     dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
-                    reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
                     wire += wlen;
                 }
             }
@@ -1014,13 +1025,204 @@ void k_fanout4(FanoutParams P) {
     }
 }
 
+// -----------------------------------------------------------------------------------------
+// k_fanout5: the write-many at low wave count with asynchronous chunk staging.  Measured on
+// the box (tools/store_peak3.hip): the same line-aligned window stores reach ~5.8 TB/s with 4
+// waves per CU and no load phases, against ~5.3 TB/s at 32 waves per CU with load phases
+// between chunks.  So each CU runs few waves, and the next chunk (slot words and packet
+// metadata) is staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into the other half of a
+// double-buffered LDS image while the current chunk is written out.  Barriers are raw
+// s_barrier with explicit counter waits, so the DMA stays in flight across them; the one
+// vmcnt(0) per item (which also retires that item's stores) is where the next image lands.
+// -----------------------------------------------------------------------------------------
+template <int THREADS, int CHUNK>
+struct Fan5 {
+    static constexpr int CWORDS = CHUNK * kSlotWordsMax;
+    static constexpr int NLD = (CWORDS + THREADS - 1) / THREADS;       // DMA words per lane
+    static constexpr int CBUF = NLD * THREADS;                         // words per image
+    static constexpr int SM = ((CWORDS + 31) / 32 + 3) & ~3;
+    static constexpr int NWAVES = THREADS / 64;
+    // per buffer: chunk words, 2 metadata words per packet; then bitmaps, ordinals, reduction
+    static constexpr int lds() {
+        return 2 * CBUF * 16 + 2 * 2 * CHUNK * 16 + 2 * SM * 4 + 2 * CHUNK * 4 + NWAVES * 8;
+    }
+};
+
+template <int THREADS, int CHUNK>
+constexpr int fanout5_lds() { return Fan5<THREADS, CHUNK>::lds(); }
+
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// One global_load_lds_dwordx4: 16 B per lane from `g` into LDS at M0 + 16 * lane.  Issued from
+// inline asm so the compiler's counter pass does not see an LDS write in flight (it would
+// otherwise wait for the DMA before every later LDS access, serialising the pipeline); the
+// kernel waits for it explicitly (vmcnt(0) at the top of the next item).
+__device__ __forceinline__ void glds16(const void* g, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "s"(lds_base) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(void* p) { return uni((uint32_t)(size_t)(lptr_t)p); }
+
+// LDS-DMA of one work item into image `img` / metadata `mimg` (both wave-linear: lane l of a
+// wave-instruction lands at base + 16 l).  Lanes past the chunk re-read a valid word.
+template <int THREADS, int CHUNK>
+__device__ __forceinline__ void fan5_stage(const FanWork& it, int tid, u32x4* img, u32x4* mimg) {
+    using F = Fan5<THREADS, CHUNK>;
+    const uint32_t wmask = it.wmask, nw = it.nw;
+    const uint32_t r0 = (uint32_t)(it.vb0 >> 4);
+    const u32x4* ring = reinterpret_cast<const u32x4*>(it.ring);
+    const uint32_t wbase = uni((uint32_t)tid & ~63u);
+    const uint32_t ibase = lds_addr(img) + wbase * 16u;
+#pragma unroll
+    for (int j = 0; j < F::NLD; j++) {
+        if ((uint32_t)(j * THREADS) < nw) {                    // uniform
+            const uint32_t wi = j * THREADS + tid;
+            const uint32_t src = (r0 + min(wi, nw - 1)) & wmask;
+            glds16(ring + src, ibase + (uint32_t)(j * THREADS) * 16u);
+        }
+    }
+    if (tid < 2 * CHUNK && it.np) {      // metadata: 2 words per packet; exec-masked lanes write nothing
+        const uint32_t p = min((uint32_t)tid >> 1, it.np - 1);
+        const u32x4* meta = reinterpret_cast<const u32x4*>(it.meta);
+        const uint64_t e = (it.lo + p) & it.pkmask;
+        glds16(meta + 2 * e + (tid & 1), lds_addr(mimg) + wbase * 16u);
+    }
+}
+
+template <int THREADS, int CHUNK>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
+void k_fanout5(FanoutParams P) {
+    using F = Fan5<THREADS, CHUNK>;
+    constexpr int CWORDS = F::CWORDS, SM = F::SM, NWAVES = F::NWAVES;
+    static_assert(CHUNK <= 56 && 2 * CHUNK <= THREADS, "");
+    const uint32_t nwork = uni(P.totals->nwork);
+    if (uni((uint32_t)P.totals->status) == (uint32_t)EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wv = uni((uint32_t)tid >> 6);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    u32x4* cimg = reinterpret_cast<u32x4*>(lds);                       // 2 x CBUF words
+    u32x4* mimg = cimg + 2 * F::CBUF;                                  // 2 x 2*CHUNK words
+    uint32_t* smap = reinterpret_cast<uint32_t*>(mimg + 4 * CHUNK);    // 2 x SM
+    uint32_t* nzp = smap + 2 * SM;                                     // 2 x CHUNK
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(nzp + 2 * CHUNK);
+    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+    unsigned long long wire = 0, inb = 0;
+
+    for (int k = tid; k < 2 * SM; k += THREADS) smap[k] = 0;
+    uint32_t w = blockIdx.x;
+    FanWork cur, nxt;
+    if (w < nwork) {
+        cur = const_load(P.work + w);
+        fan5_stage<THREADS, CHUNK>(cur, tid, cimg, mimg);
+    }
+    if (w + gridDim.x < nwork) nxt = const_load(P.work + w + gridDim.x);
+    for (uint32_t b = 0; w < nwork; w += gridDim.x, b ^= 1u) {
+        const uint64_t lo = cur.lo, vb0 = cur.vb0;
+        const uint32_t np = cur.np, nw = cur.nw, vc0 = cur.vc0;
+        u32x4* cb = cimg + b * F::CBUF;
+        const u32x4* mb = mimg + b * 2 * CHUNK;
+        uint32_t* sm = smap + b * SM;
+        uint32_t* nz = nzp + b * CHUNK;
+        // this item's image has landed (this also retires the previous item's stores), and
+        // every wave is past the previous item: the other buffer is free
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const uint32_t wn = w + gridDim.x;
+        if (wn < nwork) fan5_stage<THREADS, CHUNK>(nxt, tid, cimg + (b ^ 1u) * F::CBUF, mimg + (b ^ 1u) * 2 * CHUNK);
+        // slot-start bitmap and non-empty ordinals of this item; clear the other bitmap
+        for (int k = tid; k < SM; k += THREADS) smap[(b ^ 1u) * SM + k] = 0;
+        if ((uint32_t)tid < np) {
+            const u32x4 m0 = mb[2 * tid], m1 = mb[2 * tid + 1];
+            const uint64_t vbyte = (uint64_t)m0.y << 32 | m0.x;
+            inb += m1.z;
+            if (m1.z != 0) {
+                const uint32_t sw = (uint32_t)((vbyte - vb0) >> 4);
+                atomicOr(&sm[sw >> 5], 1u << (sw & 31));
+                nz[m1.w - vc0] = tid;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const FanWork it = cur;
+        cur = nxt;
+        if (wn + gridDim.x < nwork) nxt = const_load(P.work + wn + gridDim.x);
+        // ---- write the chunk to every sub-stream of the sender (k_fanout3's line-aligned
+        // windows, uniform trip count) ----
+        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+            const FanSub f = const_load(P.fansub + q);
+            if (f.a >= lo + np) continue;
+            const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+            const u32x4 mp = mb[2 * p0];
+            const uint32_t fw = uni((uint32_t)((((uint64_t)mp.y << 32 | mp.x) - vb0) >> 4));
+            const int64_t A = f.dw + (int64_t)(vb0 >> 4) + fw;
+            if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
+            const uint32_t s = (uint32_t)(A & 7);
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
+            const uint32_t chb = f.ch & 0xFF00u;
+            const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            for (uint32_t j = 0; j < nj; j++) {
+                const uint32_t lw = tid + j * THREADS;
+                const uint32_t src = fw + lw - s;
+                const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
+                u32x4 v = cb[srcc];
+                if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
+                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, 0);
+            }
+        }
+        // ---- descriptors: one wave per sub-stream, 128-B-aligned windows ----
+        {
+            const u32x4 ml = mb[2 * (np - 1) + 1];
+            const uint32_t nzc = np ? ml.w - vc0 + (ml.z != 0) : 0u;
+            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+                const FanSub f = const_load(P.fansub + q);
+                if (f.a >= lo + np) continue;
+                const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+                const uint32_t vcp0 = mb[2 * p0 + 1].w;
+                const uint32_t o0 = vcp0 - vc0;
+                if (o0 >= nzc) continue;
+                const uint32_t d0 = f.db + vcp0;
+                const uint32_t sh = d0 & 7;
+                const uint32_t o = o0 + lane - sh;
+                if ((uint32_t)lane >= sh && o < nzc) {
+                    const uint32_t p = nz[o];
+                    const u32x4 m0 = mb[2 * p], m1 = mb[2 * p + 1];
+                    const uint64_t off = (uint64_t)(f.off + (int64_t)((uint64_t)m0.y << 32 | m0.x));
+                    const uint32_t wlen = m1.z + ((f.ch & 1u) ? 4u : 0u);
+                    u32x4 dv;
+                    dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m0.z;
+                    if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    wire += wlen;
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned long long a = wire, bb = inb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); bb += __shfl_down(bb, o, 64); }
+    if (lane == 0) s_red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
+    }
+    __syncthreads();
+    if (lane == 0) s_red[tid >> 6] = bb;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < NWAVES; i++) tot += s_red[i];
+        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
+    }
+}
+
 // =========================================================================================
 // Session images: export the serveable part of a session's rings into a
 // contiguous buffer that another GPU imports into a replica session; a subscriber joining
 // the replica receives exactly what it would receive joining the owner.
 // =========================================================================================
-
-__device__ __forceinline__ void set_status(int* st, int code) { atomicCAS(st, 0, code); }
 
 __device__ uint64_t sender_tail(const SenderDev& D) {
     const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
@@ -1187,9 +1389,14 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<512, 32>, 512, 32, fanout4_lds<512, 32>()},             // 3
     {(const void*)k_fanout4<1024, 16>, 1024, 16, fanout4_lds<1024, 16>()},          // 4
     {(const void*)k_fanout4<512, 16>, 512, 16, fanout4_lds<512, 16>()},             // 5
+    {(const void*)k_fanout5<256, 32>, 256, 32, fanout5_lds<256, 32>()},             // 6 LDS-DMA, 4 waves/CU
+    {(const void*)k_fanout5<512, 32>, 512, 32, fanout5_lds<512, 32>()},             // 7
+    {(const void*)k_fanout5<128, 16>, 128, 16, fanout5_lds<128, 16>()},             // 8
+    {(const void*)k_fanout5<256, 16>, 256, 16, fanout5_lds<256, 16>()},             // 9
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
-                                            "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>"};
+                                            "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
+                                            "k_fanout5<256,32>", "k_fanout5<512,32>", "k_fanout5<128,16>", "k_fanout5<256,16>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 2;
 int fanout_chunk(int variant) {

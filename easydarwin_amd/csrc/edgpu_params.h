@@ -22,6 +22,7 @@ struct IngestParams {
     uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7)
     uint32_t filter_ssrc;
     uint32_t ssrc_timeout_s;
+    uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
     TickTotals* totals;
 };
 
@@ -60,6 +61,8 @@ struct FanoutParams {
     const FanSub* fansub;
     uint8_t* arena;
     edgpu_out_desc* desc;
+    uint64_t arena_words;       // capacities: stores outside them are dropped and flagged
+    uint32_t max_desc;
     TickTotals* totals;
     uint32_t ablate;            // timing-only builds: bit0 skip descriptors, bit1 skip arena stores
 };

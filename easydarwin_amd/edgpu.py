@@ -47,6 +47,7 @@ class Config(C.Structure):
         ("max_out_packets", C.c_uint32),
         ("max_batch_packets", C.c_uint32),
         ("max_batch_bytes", C.c_uint64),
+        ("overlap_ticks", C.c_uint32),
     ]
 
 

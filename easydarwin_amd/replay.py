@@ -35,6 +35,10 @@ def _wire_images(subs, desc, arena, images):
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
+    With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
+    has been ingested and indexed, so that ingest runs while the previous fan-out copy may
+    still be in flight (the pipelined mode's contract: results stay valid one extra tick).
+
     replica=None: subscribers join the context that ingests (the owner).
     replica="all" / "late": every subscriber joins a replica session on a second context,
     kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
@@ -63,6 +67,18 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         subs_meta = {}          # handle -> (sub_id, session, tcp)
         images = {}
         pending, joins, stats = [], [], []
+        lag = bool(cfg.get("overlap_ticks")) and replica is None
+        unread = None                       # (ctx, result) of a tick not read back yet
+
+        def drain():
+            nonlocal unread
+            if unread is not None:
+                c, r, tt = unread
+                st, subs, desc, arena = c.read_tick(r)
+                stats.append((tt, st.relayed_packets, st.relayed_bytes))
+                _wire_images(subs, desc, arena, images)
+                unread = None
+
         for ev in trace.events:
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
@@ -92,10 +108,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 joins = []
                 if rep is not None:
                     ctx.fanout(t)                      # the owner ticks too (no subscribers here)
-                r = out.fanout(t)
-                st, subs, desc, arena = out.read_tick(r)
-                stats.append((t, st.relayed_packets, st.relayed_bytes))
-                _wire_images(subs, desc, arena, images)
+                drain()                              # the previous tick, after this batch's ingest
+                unread = (out, out.fanout(t), t)
+                if not lag:
+                    drain()
+        drain()
         # capture: one record per (subscriber, track, kind), sorted by subscriber id
         recs = []
         for (h, tr, k), parts in images.items():

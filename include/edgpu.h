@@ -83,6 +83,12 @@ typedef struct edgpu_config {
     uint32_t max_out_packets;               /* descriptor capacity per tick (1 Mi)       */
     uint32_t max_batch_packets;             /* ingest batch capacity (1 Mi)              */
     uint64_t max_batch_bytes;               /* ingest blob capacity (1 GiB)              */
+    /* 1: tick pipelining.  The fan-out copy of tick t runs on a second HIP stream, so the
+     * next edgpu_ingest / edgpu_keyframe_index overlap it; arena, descriptors and the
+     * sub-stream table are double-buffered (a tick's result stays valid until the second
+     * edgpu_fanout after it).  Each sender ring must then hold the in-flight fan-out window
+     * plus one ingest batch, else EDGPU_RING_OVERFLOW.  0 (default): one stream. */
+    uint32_t overlap_ticks;
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu
 
@@ -123,7 +129,8 @@ typedef struct edgpu_substream_out {
     uint64_t out_bytes;     /* arena bytes spanned (slot-padded) */
 } edgpu_substream_out;
 
-/* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout. */
+/* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout (the second
+ * next one with overlap_ticks). */
 typedef struct edgpu_fanout_result {
     const uint8_t*              arena;          /* device */
     const edgpu_out_desc*       desc;           /* device */

@@ -30,9 +30,12 @@ def _trace(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [0, 1], ids=["serial", "overlap"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
-def test_engine_matches_reference(name):
-    cap, stats = replay(_trace(name))
+def test_engine_matches_reference(name, overlap):
+    """overlap=1: tick pipelining (edgpu_config.overlap_ticks) with each tick read back only
+    after the next batch was ingested, so ingest runs beside the in-flight fan-out copy."""
+    cap, stats = replay(_trace(name), overlap_ticks=overlap)
     fix = _fixture(name)
     got = capture_summary(read_capture(cap))
     want = fix["substreams"]

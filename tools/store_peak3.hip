@@ -124,6 +124,31 @@ __global__ __launch_bounds__(THREADS) void k_fan_cm(const u32x4* in, u32x4* out,
         __syncthreads();
     }
 }
+// k_fan_cm variants: MODE 1 = no chunk reads (LDS filled once), MODE 2 = non-temporal stores
+template <int THREADS, int CW, int MODE>
+__global__ __launch_bounds__(THREADS) void k_fan_cmx(const u32x4* in, u32x4* out, int nitems) {
+    __shared__ u32x4 cbuf[CW];
+    if (MODE == 1) { for (int i = threadIdx.x; i < CW; i += THREADS) cbuf[i] = in[i]; __syncthreads(); }
+    for (int w = blockIdx.x; w < nitems; w += gridDim.x) {
+        if (MODE != 1) {
+            for (int i = threadIdx.x; i < CW; i += THREADS) cbuf[i] = in[(size_t)w * CW + i];
+            __syncthreads();
+        }
+        const size_t base = (size_t)w * (16 * CW + 8);
+        for (int f = 0; f < 16; f++) {
+            const size_t A = base + (size_t)f * CW + ((w * 7 + 3) & 7);
+            const unsigned s = (unsigned)(A & 7);
+            for (unsigned lw = threadIdx.x; lw < CW + s; lw += THREADS) {
+                const unsigned src = lw - s;
+                if (src < (unsigned)CW) {
+                    if (MODE == 2) __builtin_nontemporal_store(cbuf[src], &out[A - s + lw]);
+                    else out[A - s + lw] = cbuf[src];
+                }
+            }
+        }
+        if (MODE != 1) __syncthreads();
+    }
+}
 // the same region written as ONE flat sweep of 16*CW words (copy boundaries inside lines)
 template <int THREADS, int CW>
 __global__ __launch_bounds__(THREADS) void k_fan_cmflat(const u32x4* in, u32x4* out, int nitems) {
@@ -161,22 +186,6 @@ int main() {
     add("memset0", bytes / timeit([&] { hipMemsetAsync(out, 0, bytes, 0); }) / 1e6);
     add("memset5a", bytes / timeit([&] { hipMemsetAsync(out, 0x5a, bytes, 0); }) / 1e6);
     add("memsetD32_rnd", bytes / timeit([&] { hipMemsetD32Async((hipDeviceptr_t)out, 0x9E3779B9, bytes / 4, 0); }) / 1e6);
-    for (int t : {64, 128, 512, 1024}) {
-        char n[64];
-        snprintf(n, sizeof n, "gs_wg%d_g2048", t);
-        add(n, bytes / timeit([&] { hipLaunchKernelGGL((k_gsT), dim3(2048 * 256 / t), dim3(t), 0, 0, out, nw); }) / 1e6);
-        snprintf(n, sizeof n, "gs_wg%d_g65536", t);
-        add(n, bytes / timeit([&] { hipLaunchKernelGGL((k_gsT), dim3(65536 * 256 / t), dim3(t), 0, 0, out, nw); }) / 1e6);
-    }
-    for (int g : {1, 2, 4, 8}) {
-        char n[64];
-        snprintf(n, sizeof n, "gs_const_g%d", g);
-        add(n, bytes / timeit([&] { hipLaunchKernelGGL((k_gs<false>), dim3(256 * g * 4), dim3(256), 0, 0, out, nw); }) / 1e6);
-        snprintf(n, sizeof n, "gs_rnd_g%d", g);
-        add(n, bytes / timeit([&] { hipLaunchKernelGGL((k_gs<true>), dim3(256 * g * 4), dim3(256), 0, 0, out, nw); }) / 1e6);
-        snprintf(n, sizeof n, "x4_const_g%d", g);
-        add(n, bytes / timeit([&] { hipLaunchKernelGGL((k_x4<false>), dim3(256 * g * 4), dim3(256), 0, 0, out, nw); }) / 1e6);
-    }
     add("span1024_const_g512", bytes / timeit([&] { hipLaunchKernelGGL((k_span<1024, false>), dim3(512), dim3(1024), 0, 0, out, nw); }) / 1e6);
     add("span1024_rnd_g512", bytes / timeit([&] { hipLaunchKernelGGL((k_span<1024, true>), dim3(512), dim3(1024), 0, 0, out, nw); }) / 1e6);
     add("span256_rnd_g8192", bytes / timeit([&] { hipLaunchKernelGGL((k_span<256, true>), dim3(8192), dim3(256), 0, 0, out, nw); }) / 1e6);
@@ -193,14 +202,10 @@ int main() {
     add("fan_aligned_512x1024", fb / timeit([&] { hipLaunchKernelGGL((k_fan<512, CW, true>), dim3(512), dim3(512), 0, 0, in, out, nitems, nch, region); }) / 1e6);
     add("fan_aligned_256x1024", fb / timeit([&] { hipLaunchKernelGGL((k_fan<256, CW, true>), dim3(512), dim3(256), 0, 0, in, out, nitems, nch, region); }) / 1e6);
     add("fan_cm_1024x512", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cm<1024, CW>), dim3(512), dim3(1024), 0, 0, in, out, nitems); }) / 1e6);
-    add("fan_cm_256x256", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cm<256, CW>), dim3(256), dim3(256), 0, 0, in, out, nitems); }) / 1e6);
-    add("fan_cm_512x512", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cm<512, CW>), dim3(512), dim3(512), 0, 0, in, out, nitems); }) / 1e6);
-    add("fan_cmflat_1024x512", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmflat<1024, CW>), dim3(512), dim3(1024), 0, 0, in, out, nitems); }) / 1e6);
-    add("fan_cmflat_256x256", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmflat<256, CW>), dim3(256), dim3(256), 0, 0, in, out, nitems); }) / 1e6);
-    add("gs_256x256", bytes / timeit([&] { hipLaunchKernelGGL((k_gs<false>), dim3(256), dim3(256), 0, 0, out, nw); }) / 1e6);
-    add("gs_512x256", bytes / timeit([&] { hipLaunchKernelGGL((k_gs<false>), dim3(512), dim3(256), 0, 0, out, nw); }) / 1e6);
-    add("gs_rnd_256x256", bytes / timeit([&] { hipLaunchKernelGGL((k_gs<true>), dim3(256), dim3(256), 0, 0, out, nw); }) / 1e6);
-    add("span256_g256", bytes / timeit([&] { hipLaunchKernelGGL((k_span<256, false>), dim3(256), dim3(256), 0, 0, out, nw); }) / 1e6);
+    add("fan_cm_noread_1024x512", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmx<1024, CW, 1>), dim3(512), dim3(1024), 0, 0, in, out, nitems); }) / 1e6);
+    add("fan_cm_nt_1024x512", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmx<1024, CW, 2>), dim3(512), dim3(1024), 0, 0, in, out, nitems); }) / 1e6);
+    add("fan_cm_noread_256x256", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmx<256, CW, 1>), dim3(256), dim3(256), 0, 0, in, out, nitems); }) / 1e6);
+    add("fan_cm_noread_1024x256", fb / timeit([&] { hipLaunchKernelGGL((k_fan_cmx<1024, CW, 1>), dim3(256), dim3(1024), 0, 0, in, out, nitems); }) / 1e6);
     add("fan_aligned_256x256", fb / timeit([&] { hipLaunchKernelGGL((k_fan<256, CW, true>), dim3(256), dim3(256), 0, 0, in, out, nitems, nch, region); }) / 1e6);
     {
         const size_t nout = (size_t)nsend * 16 * nch * CW;
