@@ -39,7 +39,8 @@ struct PktMeta {                    // 32 B
     uint64_t vbyte;                 // virtual offset of the packet's slot
     uint64_t id;                    // fStreamCountID
     int64_t  arrival;               // fTimeArrived
-    uint32_t len;                   // fPacketPtr.Len (0 = rejected by the SSRC filter)
+    uint16_t len;                   // fPacketPtr.Len (0 = rejected by the SSRC filter), <= 2060
+    uint16_t seq;                   // GetPacketRTPSeqNum (ReflectorStream.h:180-189): 0 if len < 4
     uint32_t vcount;                // number of non-empty packets before this one (mod 2^32)
 };
 
@@ -160,6 +161,26 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint64_t out_base;
     uint32_t desc_base;
     uint32_t nonempty;              // range [a, head) is non-empty
+    // RTP-Info players (FilterPacket, RTPSessionOutput.cpp:249-280): RTP packets with
+    // seq < first_seq are skipped until the client stream's first write, RTP or RTCP
+    uint16_t first_seq;             // qtssRTPStrFirstSeqNumber (0 unless RTP-Info)
+    uint8_t  rtp_info;              // filter armed
+    uint8_t  sent_any;              // this sub-stream has written a packet (its packet count > 0)
+};
+
+// RTP-Info PLAY query for one track (ReflectorSession HaveStreamBuffers,
+// QTSSReflectorModule.cpp:1804-1865).
+struct FirstInfoQuery {
+    uint32_t rtp_sender;            // the track's RTP sender
+    uint32_t rtcp_sender;           // its RTCP sender for a TCP push (packets there are RTP by
+                                    // port, Q12, and set HasFirstRTP too), else ~0
+    int64_t  cutoff;                // now - (over-buffer - min(rtp-info offset, over-buffer))
+};
+struct FirstInfoResult {
+    uint32_t found;                 // 0: !HasFirstRTP, 1: packet found, 2: none in the window
+    uint32_t seq;                   // GetPacketRTPSeqNum of the packet
+    uint32_t rtptime;               // GetPacketRTPTime (0 if len < 8)
+    uint32_t _pad;
 };
 
 // One fan-out work item: up to `chunk` consecutive packets of one sender, with everything the

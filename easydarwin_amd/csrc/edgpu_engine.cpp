@@ -22,6 +22,8 @@
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
+                                    uint32_t n, hipStream_t st);
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
@@ -168,6 +170,7 @@ static void fill_defaults(edgpu_config& c) {
     if (!c.max_out_packets) c.max_out_packets = 1u << 20;
     if (!c.max_batch_packets) c.max_batch_packets = 1u << 20;
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;
+    if (!c.reflector_rtp_info_offset_msec) c.reflector_rtp_info_offset_msec = 500;
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -354,12 +357,58 @@ int edgpu_session_tracks(edgpu_ctx* x, uint32_t session, uint32_t* out_tracks) {
     return EDGPU_OK;
 }
 
+// HaveStreamBuffers for an RTP-Info PLAY (QTSSReflectorModule.cpp:1804-1865), every track
+// at once on the device: first_seq[t] / info[t] on success, EDGPU_WOULD_BLOCK when a track
+// has nothing buffered.
+static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms, std::vector<uint16_t>& first_seq,
+                             edgpu_rtp_info* info) {
+    std::vector<FirstInfoQuery> q(sh.ntracks);
+    const int64_t over = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
+    const int64_t window = over - std::min<int64_t>(x->cfg.reflector_rtp_info_offset_msec, over);
+    for (uint32_t t = 0; t < sh.ntracks; t++) {
+        q[t].rtp_sender = sh.first_sender + 2 * t;
+        q[t].rtcp_sender = sh.udp_push ? 0xFFFFFFFFu : sh.first_sender + 2 * t + 1;
+        q[t].cutoff = now_ms - window;                  // age <= window  <=>  arrival >= cutoff
+    }
+    FirstInfoQuery* dq = nullptr;
+    FirstInfoResult* dr = nullptr;
+    HIP_CHECK(hipMallocAsync((void**)&dq, q.size() * sizeof(FirstInfoQuery), x->stream));
+    HIP_CHECK(hipMallocAsync((void**)&dr, q.size() * sizeof(FirstInfoResult), x->stream));
+    std::vector<FirstInfoResult> r(sh.ntracks);
+    HIP_CHECK(hipMemcpyAsync(dq, q.data(), q.size() * sizeof(FirstInfoQuery), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(launch_first_packet_info(dq, dr, x->d_senders.ptr, sh.ntracks, x->stream));
+    HIP_CHECK(hipMemcpyAsync(r.data(), dr, r.size() * sizeof(FirstInfoResult), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipFreeAsync(dq, x->stream));
+    HIP_CHECK(hipFreeAsync(dr, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    for (uint32_t t = 0; t < sh.ntracks; t++) {
+        if (r[t].found != 1)
+            return fail(EDGPU_WOULD_BLOCK, r[t].found == 0 ? "RTP-Info PLAY: no RTP packet received yet (retry)"
+                                                           : "RTP-Info PLAY: nothing buffered in the window (retry)");
+        first_seq[t] = (uint16_t)r[t].seq;
+        if (info) { info[t].seq = (uint16_t)r[t].seq; info[t]._pad = 0; info[t].rtptime = r[t].rtptime; }
+    }
+    return EDGPU_OK;
+}
+
 int edgpu_subscriber_add(edgpu_ctx* x, uint32_t session, int transport, uint32_t* out_handle) {
+    return edgpu_subscriber_play(x, session, transport, 0, 0, out_handle, nullptr);
+}
+
+int edgpu_subscriber_play(edgpu_ctx* x, uint32_t session, int transport, uint32_t flags, int64_t now_ms,
+                          uint32_t* out_handle, edgpu_rtp_info* out_info) {
     if (!x || session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (transport != EDGPU_TRANSPORT_UDP && transport != EDGPU_TRANSPORT_TCP)
         return fail(EDGPU_BAD_ARGUMENT, "bad transport");
+    if (flags & ~EDGPU_PLAY_RTP_INFO) return fail(EDGPU_BAD_ARGUMENT, "bad play flags");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     HIP_CHECK(hipSetDevice(x->device));
     const SessionHost& sh = x->sessions[session];
+    std::vector<uint16_t> first_seq(sh.ntracks, 0);
+    if (flags & EDGPU_PLAY_RTP_INFO) {
+        const int r = first_packet_info(x, sh, now_ms, first_seq, out_info);
+        if (r) return r;
+    }
     const uint32_t handle = (uint32_t)x->subscribers.size();
     const uint32_t first = (uint32_t)x->sub_sender.size();
     const uint32_t n = 2 * sh.ntracks;
@@ -377,6 +426,8 @@ int edgpu_subscriber_add(edgpu_ctx* x, uint32_t session, int transport, uint32_t
             Q.channel = (uint8_t)(2 * t + k);        // GetTwoChannelNumbers in SETUP order
             Q.active = 1;
             Q.bookmark = -1;
+            Q.first_seq = k == 0 ? first_seq[t] : 0;
+            Q.rtp_info = (k == 0 && (flags & EDGPU_PLAY_RTP_INFO)) ? 1 : 0;
             x->sub_sender.push_back(Q.sender);
             x->sub_active.push_back(1);
         }

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             m.vbyte = vb;
             m.id = s_count[track] + my_trank + 1;        // fStreamCountID = ++fPacketCount
             m.arrival = arrival;
-            m.len = len;
+            m.len = (uint16_t)len;
+            m.seq = len >= 4 ? (uint16_t)hbe16(hdr, 2) : (uint16_t)0;
             m.vcount = s_vcount[ls] + my_nzpre;
             reinterpret_cast<PktMeta*>(s_meta[ls])[idx & s_pkmask[ls]] = m;
             const bool by_port_rtp = !(fl & kSndRtcpPort);
@@ -467,6 +468,12 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
             uint64_t a = 0;
             if (Q.bookmark >= 0) {                     // GetBookMarkedPacket: resume after it
                 a = (uint64_t)Q.bookmark + 1;
+                // SendPacketsToOutput restarts AT the bookmarked packet (ReflectorStream.cpp:
+                // 1138-1198); it went out or was empty at its first visit, so it is skipped --
+                // unless the RTP-Info first-seq filter held it back and has just been lifted
+                // by the client stream's first write (no RTP id recorded yet): then it goes now
+                if (Q.rtp_info && Q.kind == 0 && !Q.has_last && (Q.sent_any || P.subs[q + 1].sent_any))
+                    a = (uint64_t)Q.bookmark;
                 have = true;
                 if (a < D.tail && a < head) { atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW); a = D.tail; }
             } else if (D.new_start >= 0) {             // new output: key pointer / buffer start
@@ -479,6 +486,19 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
                 atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW);
             }
             if (have) {
+                // FilterPacket (RTPSessionOutput.cpp:249-280, Q10): until the client stream's
+                // first write -- RTP or RTCP, its packet count (:643-653) -- RTP packets with
+                // seq < FirstSeqNumber are skipped, a plain u16 compare with no wrap handling.
+                // Zero-length packets never reach the filter (:571-572).  The RTP sender is
+                // reflected before the RTCP sender in a tick, so the RTCP sibling's writes of
+                // this tick do not count yet.
+                if (Q.rtp_info && Q.kind == 0 && !Q.sent_any && !P.subs[q + 1].sent_any) {
+                    while (a < head) {
+                        const PktMeta m = meta[a & D.pk_mask];
+                        if (m.len != 0 && m.seq >= Q.first_seq) break;
+                        a++;
+                    }
+                }
                 if (a < head) {
                     const PktMeta m = meta[a & D.pk_mask];
                     Q.a = a;
@@ -601,6 +621,7 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         o.out_base = Q.out_base;
         o.out_bytes = Q.bytes;
         P.sub_out[q] = o;
+        if (Q.count > 0) Q.sent_any = 1;
         const uint32_t pos = P.sub_pos[q];
         if (pos != 0xFFFFFFFFu) {
             FanSub f;
@@ -939,7 +960,7 @@ void k_fanout4(FanoutParams P) {
         }
         if ((uint32_t)tid < np) {
             const uint64_t vbyte = (uint64_t)ma.y << 32 | ma.x;
-            const uint32_t len = mb.x, vcount = mb.y;
+            const uint32_t len = mb.x & 0xFFFFu, vcount = mb.y;          // len:16 | seq:16
             m_vb[tid] = vbyte; m_id[tid] = ma.z; m_len[tid] = len; m_vc[tid] = vcount;
             inb += len;
             if (len != 0) {
@@ -1058,7 +1079,9 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // otherwise wait for the DMA before every later LDS access, serialising the pipeline); the
 // kernel waits for it explicitly (vmcnt(0) at the top of the next item).
 __device__ __forceinline__ void glds16(const void* g, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "s"(lds_base) : "memory", "m0");
+    uint32_t keep;                                     // M0 is reserved: save and restore it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
 }
 __device__ __forceinline__ uint32_t lds_addr(void* p) { return uni((uint32_t)(size_t)(lptr_t)p); }
 
@@ -1134,8 +1157,8 @@ void k_fanout5(FanoutParams P) {
         if ((uint32_t)tid < np) {
             const u32x4 m0 = mb[2 * tid], m1 = mb[2 * tid + 1];
             const uint64_t vbyte = (uint64_t)m0.y << 32 | m0.x;
-            inb += m1.z;
-            if (m1.z != 0) {
+            inb += m1.z & 0xFFFFu;                                     // len:16 | seq:16
+            if ((m1.z & 0xFFFFu) != 0) {
                 const uint32_t sw = (uint32_t)((vbyte - vb0) >> 4);
                 atomicOr(&sm[sw >> 5], 1u << (sw & 31));
                 nz[m1.w - vc0] = tid;
@@ -1172,7 +1195,7 @@ void k_fanout5(FanoutParams P) {
         // ---- descriptors: one wave per sub-stream, 128-B-aligned windows ----
         {
             const u32x4 ml = mb[2 * (np - 1) + 1];
-            const uint32_t nzc = np ? ml.w - vc0 + (ml.z != 0) : 0u;
+            const uint32_t nzc = np ? ml.w - vc0 + ((ml.z & 0xFFFFu) != 0) : 0u;
             for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
                 const FanSub f = const_load(P.fansub + q);
                 if (f.a >= lo + np) continue;
@@ -1187,7 +1210,7 @@ void k_fanout5(FanoutParams P) {
                     const uint32_t p = nz[o];
                     const u32x4 m0 = mb[2 * p], m1 = mb[2 * p + 1];
                     const uint64_t off = (uint64_t)(f.off + (int64_t)((uint64_t)m0.y << 32 | m0.x));
-                    const uint32_t wlen = m1.z + ((f.ch & 1u) ? 4u : 0u);
+                    const uint32_t wlen = (m1.z & 0xFFFFu) + ((f.ch & 1u) ? 4u : 0u);
                     u32x4 dv;
                     dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m0.z;
                     if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
@@ -1234,6 +1257,36 @@ __device__ uint64_t sender_tail(const SenderDev& D) {
                             [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
 }
 
+// RTP-Info PLAY (HaveStreamBuffers, QTSSReflectorModule.cpp:1804-1865): per track,
+// HasFirstRTP and ReflectorSender::GetFirstPacketInfo (ReflectorStream.cpp:728-753) -- the
+// oldest RTP-sender packet whose age is within the window (GetClientBufferStartPacketOffset,
+// :1201-1231), its sequence number and RTP timestamp (ReflectorStream.h:160-189).
+__global__ void k_first_packet_info(const FirstInfoQuery* Q, FirstInfoResult* R, const SenderDev* senders, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const FirstInfoQuery q = Q[i];
+    const SenderDev& D = senders[q.rtp_sender];
+    FirstInfoResult r{0u, 0u, 0u, 0u};
+    const bool has_rtp = D.head > 0 || (q.rtcp_sender != 0xFFFFFFFFu && senders[q.rtcp_sender].head > 0);
+    if (has_rtp) {
+        const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        const uint64_t f = lower_bound_meta(meta, D.pk_mask, sender_tail(D), D.head,
+                                            [&](const PktMeta& m) { return m.arrival >= q.cutoff; });
+        r.found = 2;
+        if (f < D.head) {
+            const PktMeta m = meta[f & D.pk_mask];
+            r.found = 1;
+            r.seq = m.seq;
+            if (m.len >= 8) {     // packet bytes 4..7 sit in the slot's first 16-B word
+                const uint8_t* ring = reinterpret_cast<const uint8_t*>(D.ring);
+                const uint64_t mask = ((uint64_t)D.word_mask + 1) * 16 - 1;
+                r.rtptime = __builtin_bswap32(*reinterpret_cast<const uint32_t*>(ring + ((m.vbyte + 8) & mask)));
+            }
+        }
+    }
+    R[i] = r;
+}
+
 // Export plan, one thread per sender: which packets the image carries.  A full image starts
 // at the key pointer, or (no key) at the oldest packet inside the new-output window -- the
 // same start k_plan_senders would pick for a new output at `now` or later (Q7).
@@ -1256,6 +1309,13 @@ __global__ void k_image_plan(ImageParams P) {
         const int64_t cutoff = P.now - P.over_buffer_ms;
         floor = lower_bound_meta(meta, D.pk_mask, tail, head, [&](const PktMeta& m) { return m.arrival >= cutoff; });
         if (floor < head && floor == tail && tail > D.floor) set_status(P.status, EDGPU_RING_OVERFLOW);
+    }
+    if (E.from == kImageFull && head > tail && floor > tail) {
+        // an RTP-Info PLAY on the replica reads the first packet of the over-buffer window
+        // (GetFirstPacketInfo, ReflectorStream.cpp:728-753), which may precede the key pointer
+        const int64_t cutoff = P.now - P.over_buffer_ms;
+        const uint64_t w = lower_bound_meta(meta, D.pk_mask, tail, head, [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        if (w < floor) floor = w;
     }
     E.floor = floor;
     E.vbyte_floor = floor < head ? meta[floor & D.pk_mask].vbyte : D.vbyte_end;
@@ -1358,6 +1418,12 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
     if (phase == 0) hipLaunchKernelGGL(k_image_plan, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
     else if (phase == 1) hipLaunchKernelGGL(k_image_pack, dim3(p.nplan), dim3(256), 0, st, p);
     else hipLaunchKernelGGL(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
+                                    uint32_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_first_packet_info, dim3((n + 63) / 64), dim3(64), 0, st, q, r, senders, n);
     return hipGetLastError();
 }
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {

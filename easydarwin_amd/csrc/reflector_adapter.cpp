@@ -36,6 +36,18 @@ int Reflector::AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle
     return edgpu_subscriber_add(fCtx, session, interleaved ? EDGPU_TRANSPORT_TCP : EDGPU_TRANSPORT_UDP, outHandle);
 }
 
+int Reflector::PlayRTPInfo(uint32_t session, bool interleaved, int64_t nowMs, uint32_t* outHandle,
+                           std::vector<edgpu_rtp_info>* outInfo) {
+    if (!fCtx) return kRequestFailed;
+    int err = FlushIngest();
+    if (err) return err;
+    std::vector<edgpu_rtp_info> info(std::max<uint32_t>(GetNumStreams(session), 1));
+    err = edgpu_subscriber_play(fCtx, session, interleaved ? EDGPU_TRANSPORT_TCP : EDGPU_TRANSPORT_UDP,
+                                EDGPU_PLAY_RTP_INFO, nowMs, outHandle, info.data());
+    if (!err && outInfo) *outInfo = info;
+    return err;
+}
+
 int Reflector::RemoveOutput(uint32_t handle) {
     if (!fCtx) return kRequestFailed;
     return edgpu_subscriber_remove(fCtx, handle);
@@ -57,8 +69,7 @@ void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet,
     fPushed.push_back(p);
 }
 
-int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
-    if (!fCtx) return kRequestFailed;
+int Reflector::FlushIngest() {
     int err;
     if (!fPushed.empty()) {
         // group by session (stable: arrival order within a session) into 16-B slots with the
@@ -96,6 +107,13 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fPushed.clear();
         fBytes.clear();
     }
+    return kNoErr;
+}
+
+int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
+    if (!fCtx) return kRequestFailed;
+    int err = FlushIngest();
+    if (err) return err;
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
     edgpu_tick_stats st;

@@ -54,6 +54,12 @@ public:
     uint32_t GetNumStreams(uint32_t session) const;
     // player joins every track of `session`; takes effect at the next ReflectPackets
     int  AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle);
+    // PLAY of an RTP-Info player (UA "vlc"/"Android"; DoPlay + HaveStreamBuffers,
+    // QTSSReflectorModule.cpp:1804-1865, 1971-2004): first ingests what was pushed so far,
+    // then fills outInfo[track] for the RTP-Info header.  kWouldBlock: nothing buffered yet,
+    // retry the PLAY later (the reference's 100 ms idle timer); no output was added.
+    int  PlayRTPInfo(uint32_t session, bool interleaved, int64_t nowMs, uint32_t* outHandle,
+                     std::vector<edgpu_rtp_info>* outInfo);
     int  RemoveOutput(uint32_t handle);
     // one pushed packet, exactly as ProcessRTPData hands it to ReflectorStream::PushPacket
     void PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
@@ -64,6 +70,7 @@ public:
     edgpu_ctx* Context() { return fCtx; }
 
 private:
+    int  FlushIngest();                                     // edgpu_ingest + keyframe index
     struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint32_t off, len; };
     edgpu_ctx* fCtx = nullptr;
     int fStatus = kRequestFailed;

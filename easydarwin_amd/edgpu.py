@@ -18,6 +18,7 @@ OK, ERR, BAD_ARGUMENT, WOULD_BLOCK = 0, -1, -10, -14
 NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW = -101, -102, -103, -104
 TRANSPORT_UDP, TRANSPORT_TCP = 0, 1
 PTR_HOST, PTR_DEVICE = 0, 1
+PLAY_RTP_INFO = 1
 FALSE = 0xFFFFFFFF
 
 EXPORTED = [
@@ -27,7 +28,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
-    "edgpu_device_free", "edgpu_fanout_kernel",
+    "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
 ]
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 
@@ -48,7 +49,12 @@ class Config(C.Structure):
         ("max_batch_packets", C.c_uint32),
         ("max_batch_bytes", C.c_uint64),
         ("overlap_ticks", C.c_uint32),
+        ("reflector_rtp_info_offset_msec", C.c_uint32),
     ]
+
+
+class RtpInfo(C.Structure):
+    _fields_ = [("seq", C.c_uint16), ("_pad", C.c_uint16), ("rtptime", C.c_uint32)]
 
 
 class PktDesc(C.Structure):
@@ -141,6 +147,7 @@ def load(path: str = LIB_PATH):
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
         "edgpu_fanout_kernel": (C.c_char_p, [P]),
+        "edgpu_subscriber_play": (I32, [P, U32, I32, U32, I64, C.POINTER(U32), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -200,6 +207,18 @@ class Context:
         out = C.c_uint32()
         _check(self.lib.edgpu_subscriber_add(self.h, session, transport, C.byref(out)))
         return out.value
+
+    def subscriber_play(self, session: int, transport: int = TRANSPORT_UDP, rtp_info: bool = False,
+                        now_ms: int = 0):
+        """PLAY of a player; rtp_info=True for an RTP-Info player (UA vlc / Android).  Returns
+        (handle, [(first seq, first rtptime)] per track).  Raises EdgpuError with code
+        WOULD_BLOCK when an RTP-Info PLAY finds a track with nothing buffered."""
+        n = self.session_tracks(session)
+        info = (RtpInfo * max(n, 1))()
+        out = C.c_uint32()
+        _check(self.lib.edgpu_subscriber_play(self.h, session, transport, PLAY_RTP_INFO if rtp_info else 0,
+                                              int(now_ms), C.byref(out), info))
+        return out.value, [(info[i].seq, info[i].rtptime) for i in range(n)]
 
     def subscriber_remove(self, handle: int):
         _check(self.lib.edgpu_subscriber_remove(self.h, handle))

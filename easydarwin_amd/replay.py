@@ -79,28 +79,45 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 _wire_images(subs, desc, arena, images)
                 unread = None
 
+        clock = 0                           # the harness's virtual clock: max event time so far
+
+        def flush():
+            nonlocal pending
+            if pending:
+                desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
+                ctx.ingest_host(desc, seg_off, seg_sess, blob)
+                ctx.keyframe_index()
+                pending = []
+
         for ev in trace.events:
+            clock = max(clock, ev[1])
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
                 pending.append((s, ch, t, data))
             elif ev[0] == JOIN:
-                joins.append(ev)
+                # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):
+                # ingest what precedes it first; other joins wait for the tick
+                if ev[5] & 1 and rep is None:
+                    flush()
+                joins.append(ev + (clock,))
             elif ev[0] == TICK:
                 t = ev[1]
-                if pending:
-                    desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
-                    ctx.ingest_host(desc, seg_off, seg_sess, blob)
-                    ctx.keyframe_index()
-                    pending = []
+                flush()
                 if link is not None:
-                    for (_, jt, s, sub_id, transport, _ua) in joins:
+                    for (_, jt, s, sub_id, transport, _ua, _now) in joins:
                         if replica == "late" or s not in rsess:
                             rsess[s] = link.add(s, trace.sdps[s])     # "late": a fresh replica per join
                     link.sync(t)
                 out = ctx if rep is None else rep
-                for (_, jt, s, sub_id, transport, _ua) in joins:
-                    h = out.subscriber_add(s if rep is None else rsess[s],
-                                           edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP)
+                for (_, jt, s, sub_id, transport, ua, now_j) in joins:
+                    try:
+                        h, _info = out.subscriber_play(s if rep is None else rsess[s],
+                                                       edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
+                                                       rtp_info=bool(ua & 1), now_ms=now_j)
+                    except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
+                        if e.code != edgpu.WOULD_BLOCK:
+                            raise
+                        continue
                     subs_meta[h] = (sub_id, s, transport)
                     for tr in range(sess_tracks[s]):
                         for k in (0, 1):

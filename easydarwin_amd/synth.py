@@ -62,6 +62,8 @@ class _RTP:
         self.rng = rng
         self.tr = tr
         self.seq = int(rng.integers(0, 1 << 16))
+        if "seq0" in tr.extra:                  # pinned initial sequence number (wrap tests)
+            self.seq = int(tr.extra["seq0"]) & 0xFFFF
         self.ts0 = int(rng.integers(0, 1 << 32))
         self.ssrc = tr.ssrc if tr.ssrc is not None else int(rng.integers(1, 1 << 32))
         self.sent = 0

@@ -12,6 +12,8 @@
  *                          (RTPSessionOutput.cpp:73-88, ReflectorSession.cpp:209-253),
  *                          i.e. QTSSReflectorModule DoSetup/DoPlay for a player
  *                          (QTSSReflectorModule.cpp:1610-1622, 1942-1946)
+ *   edgpu_subscriber_play  the same for an RTP-Info player: DoPlay + HaveStreamBuffers
+ *                          (QTSSReflectorModule.cpp:1804-1865, 1971-2004)
  *   edgpu_subscriber_remove ReflectorSession::RemoveOutput (ReflectorSession.cpp:255-279)
  *   edgpu_ingest           ReflectorStream::PushPacket + ReflectorSocket::ProcessPacket
  *                          (ReflectorStream.cpp:529-576, 1769-2010), called per packet by
@@ -89,6 +91,8 @@ typedef struct edgpu_config {
      * edgpu_fanout after it).  Each sender ring must then hold the in-flight fan-out window
      * plus one ingest batch, else EDGPU_RING_OVERFLOW.  0 (default): one stream. */
     uint32_t overlap_ticks;
+    uint32_t reflector_rtp_info_offset_msec; /* RTP-Info first packet: within over-buffer minus
+                                               this (ReflectorStream.cpp:109-110); default 500 */
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu
 
@@ -170,6 +174,27 @@ int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks
 int  edgpu_subscriber_add(edgpu_ctx* ctx, uint32_t session, int transport,
                           uint32_t* out_handle);
 int  edgpu_subscriber_remove(edgpu_ctx* ctx, uint32_t handle);
+
+/* PLAY of a player that needs RTP-Info (DoPlay's rtpInfoEnabled branch,
+ * QTSSReflectorModule.cpp:1867-2023: the kRequiresRTPInfoSeqAndTime player profile, user
+ * agents "Android" and "vlc").  For every track, HaveStreamBuffers (:1804-1865) needs a
+ * received RTP packet (HasFirstRTP) and a first packet no older than reflector_buffer_size
+ * minus reflector_rtp_info_offset_msec at `now_ms` (ReflectorSender::GetFirstPacketInfo,
+ * ReflectorStream.cpp:728-753).  Its sequence number and RTP timestamp go to out_info[track]
+ * (the PLAY response's RTP-Info), and until the player's first write on a track, RTP packets
+ * with a lower sequence number are not sent to it (FilterPacket, RTPSessionOutput.cpp:249-280;
+ * a plain 16-bit compare).  If a track has nothing buffered, no subscriber is added and
+ * EDGPU_WOULD_BLOCK is returned: the reference retries the PLAY from a 100 ms idle timer
+ * (:1985-2003).  Ingested packets must be indexed (edgpu_keyframe_index) first.
+ * flags: 0 (then this is edgpu_subscriber_add) or EDGPU_PLAY_RTP_INFO. */
+#define EDGPU_PLAY_RTP_INFO 1u
+typedef struct edgpu_rtp_info {
+    uint16_t seq;           /* qtssRTPStrFirstSeqNumber */
+    uint16_t _pad;
+    uint32_t rtptime;       /* qtssRTPStrFirstTimestamp */
+} edgpu_rtp_info;
+int  edgpu_subscriber_play(edgpu_ctx* ctx, uint32_t session, int transport, uint32_t flags,
+                           int64_t now_ms, uint32_t* out_handle, edgpu_rtp_info* out_info);
 
 int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets,
                   const uint32_t* seg_offsets, const uint32_t* seg_session,

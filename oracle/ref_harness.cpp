@@ -270,8 +270,23 @@ int main(int argc, char** argv) {
             UInt32 sub_id = r.get<UInt32>();
             UInt8 transport = r.get<UInt8>();
             UInt8 uaflags = r.get<UInt8>();
-            (void)uaflags;
             ReflectorSession* sess = sessions[s];
+            // RTP-Info player (ua_flags bit 0: the kRequiresRTPInfoSeqAndTime profile, UA
+            // "Android"/"vlc"): DoPlay's rtpInfoEnabled branch (QTSSReflectorModule.cpp:
+            // 1971-2004) runs HaveStreamBuffers (:1804-1865) with the reference's own
+            // HasFirstRTP / GetFirstPacketInfo; when a stream has nothing buffered the PLAY
+            // is deferred (idle-timer retry), which this trace model drops as a join.
+            std::vector<UInt16> firstSeq(sess->GetNumStreams(), 0);
+            if (uaflags & 1) {
+                bool have = true;
+                for (UInt32 x = 0; x < sess->GetNumStreams() && have; x++) {
+                    ReflectorStream* rs = sess->GetStreamByIndex(x);
+                    UInt32 ts = 0; SInt64 arr = 0;
+                    have = rs != NULL && rs->HasFirstRTP() &&
+                           rs->GetRTPSender()->GetFirstPacketInfo(&firstSeq[x], &ts, &arr);
+                }
+                if (!have) continue;
+            }
             Sub sb;
             sb.id = sub_id; sb.session = s;
             sb.client = new_obj();
@@ -285,8 +300,7 @@ int main(int argc, char** argv) {
                 void* cookie = sess->GetStreamByIndex(x)->GetStreamCookie();
                 set_value(st, g_cookie_attr, 0, &cookie, sizeof(cookie));
                 set_value(st, qtssRTPStrTransportType, 0, &st->transport, sizeof(UInt32));
-                UInt16 firstSeq = 0;
-                set_value(st, qtssRTPStrFirstSeqNumber, 0, &firstSeq, sizeof(firstSeq));
+                set_value(st, qtssRTPStrFirstSeqNumber, 0, &firstSeq[x], sizeof(UInt16));
                 QTSS_RTPStreamObject so = (QTSS_RTPStreamObject)st;
                 set_value(sb.client, qtssCliSesStreamObjects, x, &so, sizeof(so));
                 sb.streams.push_back(st);

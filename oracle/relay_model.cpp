@@ -23,6 +23,8 @@
 //             NeedRelocateBookMark                  ReflectorStream.cpp:1293-1353 (Q9)
 //             ReflectorOutput bookmarks             ReflectorOutput.h:137-194 (Q8)
 //             RTPSessionOutput::WritePacket         RTPSessionOutput.cpp:564-662 (Q1,Q10)
+//   RTP-Info  HaveStreamBuffers / GetFirstPacketInfo QTSSReflectorModule.cpp:1804-1865,
+//                                                   ReflectorStream.cpp:728-753
 //   egress    RTPStream::Write / InterleavedWrite   Server.tproj/RTPStream.cpp:1084-1147,
 //                                                   RTSPSessionInterface.cpp:270-344 (Q2)
 //   SDP       SDPSourceInfo::Parse m= / a=rtpmap    APICommonCode/SDPSourceInfo.cpp:259-353
@@ -58,6 +60,7 @@ struct Prefs {                                   // ReflectorStream::Initialize 
     int64_t over_buffer_ms = 1000;               // reflector_buffer_size_sec = 1
     int64_t max_packet_age_ms = 10000;           // 10 x over buffer
     int64_t relocate_age_ms = 2000;              // rtp_reflector_threshold_msec
+    int64_t first_packet_offset_ms = 500;        // ReflectorStream::sFirstPacketOffsetMsec (:70)
     uint32_t ssrc_timeout_s = 30;                // timeout_stream_SSRC_secs
     bool filter_ssrcs = true;                    // use_one_SSRC_per_stream
 };
@@ -137,6 +140,7 @@ struct Sender {
 struct Stream {
     TrackInfo info;
     uint64_t packet_count = 0;
+    bool has_first_rtp = false;     // ReflectorStream::HasFirstRTP (ReflectorStream.cpp:1942-1950)
     Sender snd[2];                  // [0] RTP (socket A), [1] RTCP (socket B)
 };
 
@@ -232,6 +236,7 @@ struct Model {
         snd.q.push_back(std::move(p));
         PacketRef it = std::prev(snd.q.end());
         const bool rtp_by_port = !snd.rtcp_port;
+        if (rtp_by_port) st.has_first_rtp = true;                 // fIsRTCP by port (Q12)
         if (rtp_by_port && st.info.type == kVideo && st.info.name == "H264/90000" &&
             key_frame_first_packet(it->data.data(), it->len)) {
             if (snd.has_key) snd.key->needed = false;
@@ -248,16 +253,38 @@ struct Model {
     }
 
     // ---- join ---------------------------------------------------------------------------
-    void join(int session, uint32_t sub_id, bool tcp, std::vector<uint8_t>* sink = nullptr) {
+    // RTP-Info player (DoPlay's rtpInfoEnabled branch, QTSSReflectorModule.cpp:1971-2004):
+    // HaveStreamBuffers (:1804-1865) needs, per track, HasFirstRTP and a first packet
+    // (ReflectorSender::GetFirstPacketInfo, ReflectorStream.cpp:728-753: the oldest RTP-sender
+    // packet no older than over-buffer - min(offset, over-buffer), pinned); its sequence number
+    // (0 when len < 4, ReflectorStream.h:180-189) becomes qtssRTPStrFirstSeqNumber.  Without
+    // buffers the PLAY is retried later: here the join is dropped (returns false).
+    bool join(int session, uint32_t sub_id, bool tcp, std::vector<uint8_t>* sink = nullptr, bool rtp_info = false) {
         Session& se = *sessions[session];
+        std::vector<uint16_t> first(se.streams.size(), 0);
+        if (rtp_info) {
+            const int64_t window = prefs.over_buffer_ms - std::min(prefs.first_packet_offset_ms, prefs.over_buffer_ms);
+            for (size_t x = 0; x < se.streams.size(); x++) {
+                Stream& st = se.streams[x];
+                if (!st.has_first_rtp) return false;
+                Packet* fp = nullptr;
+                for (Packet& p : st.snd[0].q)
+                    if (now - p.arrival <= window) { fp = &p; break; }
+                if (!fp) return false;
+                first[x] = fp->len >= 4 ? be16(&fp->data[2]) : 0;
+                fp->needed = true;
+            }
+        }
         auto o = std::make_unique<Output>();
         o->sub_id = sub_id;
         o->tcp = tcp;
         o->has_bm.assign(se.streams.size(), {false, false});
         o->bm.resize(se.streams.size());
         o->ss.resize(se.streams.size());
+        for (size_t x = 0; x < se.streams.size(); x++) o->ss[x].first_seq = first[x];
         if (sink) { o->capture = false; o->sink = sink; }
         se.outputs.push_back(std::move(o));
+        return true;
     }
 
     // ---- fan-out ------------------------------------------------------------------------
@@ -403,8 +430,8 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
             uint32_t s = r.get<uint32_t>();
             uint32_t sub = r.get<uint32_t>();
             uint8_t tr = r.get<uint8_t>();
-            (void)r.get<uint8_t>();
-            if (s % nshards == shard) on_join(s, sub, tr != 0);
+            uint8_t ua = r.get<uint8_t>();
+            if (s % nshards == shard) on_join(s, sub, tr != 0, (ua & 1) != 0);
         } else if (type == 3) {
             m.tick();
         } else {
@@ -418,7 +445,7 @@ static int run_capture(const char* in, const char* out) {
     Reader r;
     if (!load(in, r)) return 2;
     relay::Model m;
-    replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp) { m.join(s, sub, tcp); });
+    replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp, bool rtp_info) { m.join(s, sub, tcp, nullptr, rtp_info); });
     struct Rec { uint32_t sub, sess; uint16_t track; relay::Output* o; };
     std::vector<Rec> recs;
     for (uint32_t s = 0; s < m.sessions.size(); s++)
@@ -447,7 +474,7 @@ static int run_capture(const char* in, const char* out) {
 // Bench: the trace is parsed once, its events are split by session (session % T) into T
 // private lists (TICKs go to every list), then T threads replay their lists concurrently with
 // memcpy sinks recycled every tick.  Only the replay (ingest + fan-out) is timed.
-struct Ev { uint8_t type; int64_t t; uint32_t s, sub; uint8_t ch; bool tcp; const uint8_t* data; uint32_t len; };
+struct Ev { uint8_t type; int64_t t; uint32_t s, sub; uint8_t ch; bool tcp; uint8_t ua; const uint8_t* data; uint32_t len; };
 
 static int run_bench(const char* in, int threads, int repeat) {
     Reader r;
@@ -470,7 +497,7 @@ static int run_bench(const char* in, int threads, int repeat) {
             e.data = &r.d[r.p]; r.p += e.len;
             lists[e.s % threads].push_back(e);
         } else if (e.type == 2) {
-            e.s = r.get<uint32_t>(); e.sub = r.get<uint32_t>(); e.tcp = r.get<uint8_t>() != 0; (void)r.get<uint8_t>();
+            e.s = r.get<uint32_t>(); e.sub = r.get<uint32_t>(); e.tcp = r.get<uint8_t>() != 0; e.ua = r.get<uint8_t>();
             lists[e.s % threads].push_back(e);
         } else {
             for (auto& l : lists) l.push_back(e);
@@ -497,7 +524,7 @@ static int run_bench(const char* in, int threads, int repeat) {
                 else if (e.type == 2) {
                     sinks.emplace_back(new std::vector<uint8_t>());
                     sinks.back()->reserve(1 << 20);
-                    m.join(e.s, e.sub, e.tcp, sinks.back().get());
+                    m.join(e.s, e.sub, e.tcp, sinks.back().get(), (e.ua & 1) != 0);
                 } else m.tick();
             }
             uint64_t p = 0, b = 0;

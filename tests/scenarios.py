@@ -19,6 +19,11 @@ parity consequence:
 * ``stall``         a 12 s pusher stall with subscribers attached (Q16 retention, bookmarks).
 * ``anchor``        video + two audio tracks: the session-wide audio anchor flag (Q6).
 * ``tiny``          a 1-session, 2-subscriber smoke case (used by ``smoke()``).
+* ``rtpinfo``       RTP-Info players (UA "vlc"/"Android", ua_flags bit 0): the first-seq
+                    filter (Q10) that starts them ~500 ms back instead of at the key pointer,
+                    its u16 compare across a sequence wrap, the RTCP write that lifts it, and
+                    PLAYs deferred for want of buffered packets (before the first packet, and
+                    during a pusher stall).
 """
 from __future__ import annotations
 
@@ -33,6 +38,7 @@ from easydarwin_amd.trace import TCP, UDP, Trace
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
               joins: list[tuple], tick_times=None):
+    # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
     and ticks.  Within one tick interval the order is: packets (time order, session order),
     then joins, then the TICK at the interval end."""
@@ -50,8 +56,8 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
             tr.pkt(t, s, ch, data)
             i += 1
         while j < len(joins) and joins[j][0] <= tt:
-            t, s, sub, transport = joins[j]
-            tr.join(t, s, sub, transport)
+            t, s, sub, transport = joins[j][:4]
+            tr.join(t, s, sub, transport, joins[j][4] if len(joins[j]) > 4 else 0)
             j += 1
         tr.tick(tt)
     return tr
@@ -227,7 +233,52 @@ def tiny() -> Trace:
     return _assemble(tr, [pk], 100, 1200, joins)
 
 
+VLC = 1                                    # ua_flags bit 0: RTP-Info player profile
+
+
+def rtpinfo() -> Trace:
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 60))
+    tr = Trace()
+    # session 0: steady H.264 + PCMA push with pusher SRs on the video RTCP channel
+    s0 = [TrackSpec("video", "H264/90000", 96, bitrate=600_000, gop=60, idr_bytes=9_000, rtcp_every_ms=900),
+          TrackSpec("audio", "PCMA/8000", 8)]
+    tr.add_session(make_sdp(s0))
+    pk0 = session_packets(s0, 6000, SEED_BASE + 61)
+    # session 1: starts at 1 s with its video sequence about to wrap, stalls 2.6-3.9 s
+    s1 = [TrackSpec("video", "H264/90000", 96, bitrate=500_000, gop=45, idr_bytes=8_000,
+                    extra={"seq0": 65536 - 30}),
+          TrackSpec("audio", "PCMU/8000", 0)]
+    tr.add_session(make_sdp(s1))
+    pk1 = session_packets(s1, 1600, SEED_BASE + 62, t0=1000)
+    pk1 += session_packets(s1, 2000, SEED_BASE + 63, t0=3900)
+    # session 2: video only; at 2 s the pusher restarts its sequence numbers far below the
+    # RTP-Info first seq of a player joining then, so the filter holds that player's RTP
+    # sub-stream until its first RTCP write (an SR of the same NTP second passes the TCP
+    # push's SSRC latch, Q12/Q13) lifts it
+    s2 = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=30, idr_bytes=5_000,
+                    ssrc=0x2222AAAA, extra={"seq0": 40_000})]
+    tr.add_session(make_sdp(s2))
+    s2b = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=30, idr_bytes=5_000,
+                     rtcp_every_ms=250, ssrc=0x2222AAAA, extra={"seq0": 100})]
+    pk2 = session_packets(s2, 2000, SEED_BASE + 64)
+    pk2 += session_packets(s2b, 3000, SEED_BASE + 65, t0=2000)
+    joins = [
+        (0, 0, 1, UDP, VLC), (0, 0, 2, TCP),                    # at the first packets
+        (1300, 0, 3, TCP, VLC), (1300, 0, 4, UDP),              # mid-GOP: ~500 ms back vs key
+        (2700, 0, 5, UDP, VLC), (4450, 0, 6, TCP, VLC),
+        (0, 1, 10, UDP, VLC),                                   # no packet yet: deferred
+        (1800, 1, 11, TCP, VLC), (1800, 1, 12, UDP),            # after the seq wrap
+        (3300, 1, 13, UDP, VLC), (3700, 1, 14, TCP, VLC),       # stalled pusher: deferred
+        (4200, 1, 15, UDP, VLC),
+        (1900, 2, 20, TCP, VLC), (1900, 2, 21, UDP),            # before the restart
+        (1950, 2, 23, TCP, VLC),                                # at the restart: held by the filter
+        (2300, 2, 22, UDP, VLC),
+    ]
+    del rng
+    return _assemble(tr, [pk0, pk1, pk2], 100, 6000, joins)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
-    "nokey": nokey, "stall": stall, "anchor": anchor,
+    "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
 }

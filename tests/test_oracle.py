@@ -55,7 +55,7 @@ def test_port_matches_golden_digests(name, oracle_bins, tmp_path):
     assert hashlib.sha256(cap).hexdigest() == fix["capture_sha256"]
 
 
-@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor"])
+@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor", "rtpinfo"])
 def test_reference_harness_reproduces_fixture(name, oracle_bins, tmp_path):
     if oracle_bins["ref"] is None:
         pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")
@@ -78,3 +78,17 @@ def test_golden_index_counts():
     for name in SCENARIOS:
         fix = _fix(name)
         assert idx[name]["relayed_packets"] == sum(v[0] for v in fix["substreams"].values())
+
+
+def test_rtp_info_players_start_later_and_deferred_plays_drop():
+    """Q10 from the reference's own output (rtpinfo fixture): an RTP-Info player (UA vlc)
+    joining mid-GOP starts at the packet ~500 ms back (GetFirstPacketInfo) rather than at the
+    key pointer a plain player starts from; PLAYs with nothing buffered (before the first
+    packet, during a stall) never become subscribers."""
+    sub = _fix("rtpinfo")["substreams"]
+    subs = {int(k.split("/")[0]) for k in sub}
+    assert not subs & {10, 13, 14}
+    assert {1, 2, 3, 4, 5, 6, 11, 12, 15, 20, 21, 22, 23} <= subs
+    assert sub["3/0/0"][0] < sub["4/0/0"][0]          # same join tick, vlc vs plain (video)
+    assert sub["3/1/0"][0] < sub["4/1/0"][0]          # and the audio anchor start
+    assert sub["1/0/0"][0] == sub["2/0/0"][0]          # at the first packets both see everything

@@ -55,10 +55,12 @@ int main(int argc, char** argv) {
     std::map<uint32_t, std::tuple<uint32_t, uint32_t, bool>> handles;   // handle -> (sub, session, tcp)
     CaptureSink sink;
     sink.recs = &recs;
+    int64_t now = 0;
     while (p < d.size()) {
         uint8_t type; get(type);
         if (type == 0) break;
         int64_t t; get(t);
+        if (t > now) now = t;                 // the reflector's clock (max event time so far)
         if (type == 1) {
             uint32_t s, len; uint8_t ch;
             get(s); get(ch); get(len);
@@ -68,7 +70,13 @@ int main(int argc, char** argv) {
             uint32_t s, sub; uint8_t tr, ua;
             get(s); get(sub); get(tr); get(ua);
             uint32_t h;
-            if (R.AddOutput(s, tr != 0, &h)) return 3;
+            if (ua & 1) {                     // RTP-Info player: PLAY now, or deferred
+                const int err = R.PlayRTPInfo(s, tr != 0, now, &h, nullptr);
+                if (err == kWouldBlock) continue;
+                if (err) return 3;
+            } else if (R.AddOutput(s, tr != 0, &h)) {
+                return 3;
+            }
             handles[h] = std::make_tuple(sub, s, tr != 0);
             for (uint16_t x = 0; x < R.GetNumStreams(s); x++) recs[{h, x}];
         } else if (type == 3) {
