@@ -357,6 +357,36 @@ int edgpu_session_tracks(edgpu_ctx* x, uint32_t session, uint32_t* out_tracks) {
     return EDGPU_OK;
 }
 
+// Appends one subscriber's sub-streams (RTPSessionOutput + ReflectorSession::AddOutput) to the
+// host tables and to `v` (the SubDev records still to be uploaded); returns its handle.
+static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport, uint32_t flags,
+                                  const uint16_t* first_seq, std::vector<SubDev>& v) {
+    const SessionHost& sh = x->sessions[session];
+    const uint32_t handle = (uint32_t)x->subscribers.size();
+    const uint32_t first = (uint32_t)x->sub_sender.size();
+    for (uint32_t t = 0; t < sh.ntracks; t++)
+        for (uint32_t k = 0; k < 2; k++) {
+            SubDev Q;
+            memset(&Q, 0, sizeof(Q));
+            Q.handle = handle;
+            Q.sender = sh.first_sender + 2 * t + k;
+            Q.track = (uint16_t)t;
+            Q.kind = (uint8_t)k;
+            Q.transport = (uint8_t)transport;
+            Q.channel = (uint8_t)(2 * t + k);        // GetTwoChannelNumbers in SETUP order
+            Q.active = 1;
+            Q.bookmark = -1;
+            Q.first_seq = (k == 0 && first_seq) ? first_seq[t] : 0;
+            Q.rtp_info = (k == 0 && (flags & EDGPU_PLAY_RTP_INFO)) ? 1 : 0;
+            x->sub_sender.push_back(Q.sender);
+            x->sub_active.push_back(1);
+            v.push_back(Q);
+        }
+    x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true});
+    x->index_dirty = true;
+    return handle;
+}
+
 // HaveStreamBuffers for an RTP-Info PLAY (QTSSReflectorModule.cpp:1804-1865), every track
 // at once on the device: first_seq[t] / info[t] on success, EDGPU_WOULD_BLOCK when a track
 // has nothing buffered.
@@ -409,33 +439,35 @@ int edgpu_subscriber_play(edgpu_ctx* x, uint32_t session, int transport, uint32_
         const int r = first_packet_info(x, sh, now_ms, first_seq, out_info);
         if (r) return r;
     }
-    const uint32_t handle = (uint32_t)x->subscribers.size();
+    std::vector<SubDev> v;
     const uint32_t first = (uint32_t)x->sub_sender.size();
-    const uint32_t n = 2 * sh.ntracks;
-    HIP_CHECK(x->d_subs.reserve(first + n, x->stream));
-    std::vector<SubDev> v(n);
-    for (uint32_t t = 0; t < sh.ntracks; t++)
-        for (uint32_t k = 0; k < 2; k++) {
-            SubDev& Q = v[2 * t + k];
-            memset(&Q, 0, sizeof(Q));
-            Q.handle = handle;
-            Q.sender = sh.first_sender + 2 * t + k;
-            Q.track = (uint16_t)t;
-            Q.kind = (uint8_t)k;
-            Q.transport = (uint8_t)transport;
-            Q.channel = (uint8_t)(2 * t + k);        // GetTwoChannelNumbers in SETUP order
-            Q.active = 1;
-            Q.bookmark = -1;
-            Q.first_seq = k == 0 ? first_seq[t] : 0;
-            Q.rtp_info = (k == 0 && (flags & EDGPU_PLAY_RTP_INFO)) ? 1 : 0;
-            x->sub_sender.push_back(Q.sender);
-            x->sub_active.push_back(1);
-        }
-    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), n * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
+    const uint32_t handle = append_subscriber(x, session, transport, flags, first_seq.data(), v);
+    HIP_CHECK(x->d_subs.reserve(first + v.size(), x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), v.size() * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
-    x->subscribers.push_back(SubscriberHost{session, first, n, true});
-    x->index_dirty = true;
     if (out_handle) *out_handle = handle;
+    return EDGPU_OK;
+}
+
+int edgpu_subscribers_add(edgpu_ctx* x, uint32_t n, const uint32_t* sessions, const int32_t* transports,
+                          uint32_t* out_handles) {
+    if (!x || (n && (!sessions || !transports))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    for (uint32_t i = 0; i < n; i++) {
+        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (transports[i] != EDGPU_TRANSPORT_UDP && transports[i] != EDGPU_TRANSPORT_TCP)
+            return fail(EDGPU_BAD_ARGUMENT, "bad transport");
+    }
+    if (!n) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    std::vector<SubDev> v;
+    const uint32_t first = (uint32_t)x->sub_sender.size();
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t h = append_subscriber(x, sessions[i], transports[i], 0, nullptr, v);
+        if (out_handles) out_handles[i] = h;
+    }
+    HIP_CHECK(x->d_subs.reserve(first + v.size(), x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), v.size() * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
     return EDGPU_OK;
 }
 

@@ -29,6 +29,7 @@ EXPORTED = [
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
+    "edgpu_subscribers_add",
 ]
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 
@@ -148,6 +149,7 @@ def load(path: str = LIB_PATH):
         "edgpu_device_free": (I32, [P, P]),
         "edgpu_fanout_kernel": (C.c_char_p, [P]),
         "edgpu_subscriber_play": (I32, [P, U32, I32, U32, I64, C.POINTER(U32), P]),
+        "edgpu_subscribers_add": (I32, [P, U32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -219,6 +221,14 @@ class Context:
         _check(self.lib.edgpu_subscriber_play(self.h, session, transport, PLAY_RTP_INFO if rtp_info else 0,
                                               int(now_ms), C.byref(out), info))
         return out.value, [(info[i].seq, info[i].rtptime) for i in range(n)]
+
+    def subscribers_add(self, sessions, transports) -> np.ndarray:
+        """Burst join: one subscriber per (session, transport); returns their handles."""
+        ses = np.ascontiguousarray(sessions, dtype=np.uint32)
+        trn = np.ascontiguousarray(np.broadcast_to(transports, ses.shape), dtype=np.int32)
+        out = np.zeros(len(ses), dtype=np.uint32)
+        _check(self.lib.edgpu_subscribers_add(self.h, len(ses), _ptr(ses), _ptr(trn), _ptr(out)))
+        return out
 
     def subscriber_remove(self, handle: int):
         _check(self.lib.edgpu_subscriber_remove(self.h, handle))

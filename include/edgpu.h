@@ -174,6 +174,10 @@ int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks
 int  edgpu_subscriber_add(edgpu_ctx* ctx, uint32_t session, int transport,
                           uint32_t* out_handle);
 int  edgpu_subscriber_remove(edgpu_ctx* ctx, uint32_t handle);
+/* A burst of joins (e.g. BASELINE config C4's 10k mid-GOP joins) in one call: subscriber i
+ * joins sessions[i] with transports[i]; handles as edgpu_subscriber_add would return them. */
+int  edgpu_subscribers_add(edgpu_ctx* ctx, uint32_t n, const uint32_t* sessions,
+                           const int32_t* transports, uint32_t* out_handles);
 
 /* PLAY of a player that needs RTP-Info (DoPlay's rtpInfoEnabled branch,
  * QTSSReflectorModule.cpp:1867-2023: the kRequiresRTPInfoSeqAndTime player profile, user
