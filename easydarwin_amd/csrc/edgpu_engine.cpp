@@ -27,6 +27,7 @@ hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r,
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
+hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
 int fanout_chunk(int variant);
 const char* fanout_name(int variant);
 }  // namespace edgpu
@@ -141,6 +142,19 @@ struct edgpu_ctx {
     uint8_t* d_arena_buf[2] = {nullptr, nullptr};
     edgpu_out_desc* d_out_desc_buf[2] = {nullptr, nullptr};
     DevVec<edgpu_substream_out> d_sub_out_buf2;   // second sub-stream table (overlap)
+    // RTSP-interleaved ingest: per-session carried partial frame (device) and its length
+    // (host mirror, read back with every call's results), per-call walk tables
+    std::vector<uint32_t> carry_len;
+    DevVec<uint8_t> d_carry;
+    DevVec<TcpGroup> d_tcp_groups;
+    DevVec<TcpRead> d_tcp_reads;
+    DevVec<uint32_t> d_tcp_chunk_group, d_tcp_ncand;
+    DevVec<TcpCand> d_tcp_cands;
+    DevVec<uint8_t> d_tcp_links;
+    DevVec<TcpChunkRes> d_tcp_chunkres;
+    DevVec<edgpu_tcp_result> d_tcp_results;
+    TcpTotals* d_tcp_tot = nullptr;
+    uint8_t* d_tcp_raw = nullptr;
     // session images
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
@@ -237,6 +251,11 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
     x->d_img_plan.release(); x->d_sub_out_buf2.release();
+    x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
+    x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
+    x->d_tcp_results.release();
+    if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
+    if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
@@ -531,6 +550,33 @@ static int rebuild_index(edgpu_ctx* x) {
     return EDGPU_OK;
 }
 
+// Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
+// edgpu_keyframe_index.  `before` (optional) is enqueued between the timing events, so the
+// ingest time of edgpu_ingest_interleaved includes its deframe kernels.
+static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
+                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, hipError_t (*before)(edgpu_ctx*, void*),
+                          void* arg = nullptr) {
+    IngestParams p;
+    p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
+    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
+    p.pflags = x->d_pflags; p.pidx = x->d_pidx;
+    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode;
+    p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
+    p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
+    p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
+    p.totals = x->d_totals;
+    HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
+    HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
+    HIP_CHECK(hist_mark(x, 2, 0));
+    if (before) HIP_CHECK(before(x, arg));
+    HIP_CHECK(launch_ingest(p, nseg, x->stream));
+    HIP_CHECK(hist_mark(x, 2, 1));
+    HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
+    x->timed_ingest = true;
+    x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
+    return EDGPU_OK;
+}
+
 int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
@@ -564,23 +610,99 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
     }
-    IngestParams p;
-    p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
-    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
-    p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = x->ingest_mode;
-    p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
-    p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
-    p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
-    p.totals = x->d_totals;
-    HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
-    HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
-    HIP_CHECK(hist_mark(x, 2, 0));
-    HIP_CHECK(launch_ingest(p, nseg, x->stream));
-    HIP_CHECK(hist_mark(x, 2, 1));
-    HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
-    x->timed_ingest = true;
-    x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
+    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode, nullptr);
+}
+
+int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t n, const uint8_t* bytes,
+                             uint64_t nbytes, int where, edgpu_tcp_result* results) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (n && (!reads || !bytes || !results)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (where != EDGPU_PTR_HOST && where != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
+    if (where == EDGPU_PTR_DEVICE && ((uintptr_t)bytes & 15)) return fail(EDGPU_BAD_ARGUMENT, "device bytes must be 16-B aligned");
+    if (where == EDGPU_PTR_HOST && nbytes > x->cfg.max_batch_bytes) return fail(EDGPU_BAD_ARGUMENT, "reads exceed max_batch_bytes");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    if (!n) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    x->carry_len.resize(x->sessions.size(), 0);
+    // one group per session: its reads are a run of consecutive entries, contiguous in `bytes`
+    std::vector<TcpGroup> groups;
+    std::vector<TcpRead> rd(n);
+    std::vector<uint32_t> chunk_group;
+    std::vector<uint8_t> seen(x->sessions.size(), 0);
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t s = reads[i].session;
+        if (s >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in reads");
+        if (x->sessions[s].udp_push) return fail(EDGPU_BAD_ARGUMENT, "interleaved reads for a UDP-push session");
+        if (seen[s]) return fail(EDGPU_BAD_ARGUMENT, "a session's reads must be consecutive entries");
+        seen[s] = 1;
+        uint64_t pos = x->carry_len[s];
+        uint32_t j = i;
+        for (; j < n && reads[j].session == s; j++) {
+            if (reads[j].offset > nbytes || reads[j].len > nbytes - reads[j].offset)
+                return fail(EDGPU_BAD_ARGUMENT, "read outside bytes");
+            if (j > i && reads[j].offset != reads[j - 1].offset + reads[j - 1].len)
+                return fail(EDGPU_BAD_ARGUMENT, "a session's reads must be contiguous in bytes");
+            rd[j].start = pos; rd[j].arrival = reads[j].arrival_ms; rd[j].len = reads[j].len; rd[j]._pad = 0;
+            pos += reads[j].len;
+        }
+        TcpGroup G;
+        memset(&G, 0, sizeof(G));
+        G.session = s; G.first_read = i; G.nreads = j - i;
+        G.first_chunk = (uint32_t)chunk_group.size();
+        G.carry_len = x->carry_len[s];
+        G.raw_off = reads[i].offset;
+        G.len = pos;
+        G.nchunks = (uint32_t)((pos + kTcpChunk - 1) / kTcpChunk);
+        chunk_group.insert(chunk_group.end(), G.nchunks, (uint32_t)groups.size());
+        groups.push_back(G);
+        i = j;
+    }
+    const uint32_t ng = (uint32_t)groups.size(), nc = (uint32_t)chunk_group.size();
+    HIP_CHECK(x->d_carry.reserve((size_t)x->sessions.size() * kTcpCarry, x->stream));
+    HIP_CHECK(x->d_tcp_groups.reserve(ng, x->stream));
+    HIP_CHECK(x->d_tcp_reads.reserve(n, x->stream));
+    HIP_CHECK(x->d_tcp_results.reserve(n, x->stream));
+    HIP_CHECK(x->d_tcp_chunk_group.reserve(std::max<uint32_t>(nc, 1), x->stream));
+    HIP_CHECK(x->d_tcp_ncand.reserve(std::max<uint32_t>(nc, 1), x->stream));
+    HIP_CHECK(x->d_tcp_chunkres.reserve(std::max<uint32_t>(nc, 1), x->stream));
+    HIP_CHECK(x->d_tcp_cands.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
+    HIP_CHECK(x->d_tcp_links.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
+    if (!x->d_tcp_tot && hipMalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
+    if (!x->d_blob && hipMalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "blob staging");
+    const uint8_t* raw = bytes;
+    if (where == EDGPU_PTR_HOST) {
+        if (!x->d_tcp_raw && hipMalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
+            return fail(EDGPU_OUT_OF_MEMORY, "read staging");
+        HIP_CHECK(hipMemcpyAsync(x->d_tcp_raw, bytes, nbytes, hipMemcpyHostToDevice, x->stream));
+        raw = x->d_tcp_raw;
+    }
+    HIP_CHECK(hipMemcpyAsync(x->d_tcp_groups.ptr, groups.data(), ng * sizeof(TcpGroup), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_tcp_reads.ptr, rd.data(), n * sizeof(TcpRead), hipMemcpyHostToDevice, x->stream));
+    if (nc) HIP_CHECK(hipMemcpyAsync(x->d_tcp_chunk_group.ptr, chunk_group.data(), nc * 4, hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemsetAsync(x->d_tcp_results.ptr, 0, n * sizeof(edgpu_tcp_result), x->stream));
+    TcpParams p;
+    p.groups = x->d_tcp_groups.ptr; p.ngroups = ng; p.nchunks = nc;
+    p.reads = x->d_tcp_reads.ptr; p.chunk_group = x->d_tcp_chunk_group.ptr;
+    p.cands = x->d_tcp_cands.ptr; p.links = x->d_tcp_links.ptr; p.ncand = x->d_tcp_ncand.ptr;
+    p.chunkres = x->d_tcp_chunkres.ptr;
+    p.raw = raw; p.raw_bytes = nbytes;
+    p.carry = x->d_carry.ptr;
+    p.blob = x->d_blob; p.blob_cap = x->cfg.max_batch_bytes;
+    p.desc = x->d_desc; p.max_desc = x->cfg.max_batch_packets;
+    p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
+    p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
+    struct Launch { static hipError_t go(edgpu_ctx* c, void* a) { return launch_deframe(*static_cast<const TcpParams*>(a), c->stream); } };
+    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, x->d_blob, 0, &Launch::go, &p);
+    if (r) return r;
+    TcpTotals tot;
+    HIP_CHECK(hipMemcpyAsync(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipMemcpyAsync(&tot, x->d_tcp_tot, sizeof(tot), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    if (tot.status) {
+        x->pending = false;                 // the ingest ran over empty segments
+        return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets / max_batch_bytes");
+    }
+    for (const TcpGroup& G : groups) x->carry_len[G.session] = results[G.first_read + G.nreads - 1].carry;
     return EDGPU_OK;
 }
 

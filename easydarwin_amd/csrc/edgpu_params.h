@@ -67,6 +67,64 @@ struct FanoutParams {
     uint32_t ablate;            // timing-only builds: bit0 skip descriptors, bit1 skip arena stores
 };
 
+// ---- RTSP-interleaved ingest ('$'-deframe of pusher TCP reads, edgpu_ingest_interleaved) ----
+// A session's stream in one call = its carried bytes (a partial frame from the previous call)
+// followed by its reads.  The stream is cut into kTcpChunk-byte chunks walked in parallel from
+// every '$' that can start a frame in the chunk's first kTcpMaxFrame bytes; the true walk is
+// then stitched chunk to chunk (k_tcp_resolve).
+constexpr uint32_t kTcpChunk = 16384;      // stream bytes per walk chunk
+constexpr uint32_t kTcpCands = 64;         // candidates kept per chunk (more: sequential walk)
+constexpr uint32_t kTcpMaxFrame = 2047;    // usable request-buffer bytes (QTSS_MAX_REQUEST_BUFFER_SIZE - 1)
+constexpr uint32_t kTcpCarry = 2048;       // per-session carry buffer
+constexpr uint32_t kTcpNone = 0xFFFFFFFFu;
+
+// walk outcome codes (TcpCand.code, TcpGroup.code)
+constexpr uint32_t kWalkRun = 0;           // reached the chunk end / the stream end
+constexpr uint32_t kWalkPartial = 1;       // incomplete frame at `exit`: carried
+constexpr uint32_t kWalkMessage = 2;       // non-'$' byte at a frame boundary: an RTSP message
+constexpr uint32_t kWalkDropped = 3;       // frame longer than the request buffer: connection dropped
+
+struct TcpGroup {           // one pusher connection's reads in this call
+    uint32_t session, first_read, nreads, first_chunk;
+    uint32_t nchunks, carry_len;
+    uint64_t raw_off;       // raw-buffer offset of the first read
+    uint64_t len;           // stream bytes: carry_len + the reads' bytes
+    // k_tcp_resolve
+    uint32_t nframes, code;
+    uint64_t slot_bytes;
+    uint64_t stop;          // stream position where the walk ended (len: everything framed)
+    // k_tcp_scan
+    uint32_t frame_base, _pad;
+    uint64_t slot_base;
+};
+
+struct TcpRead { uint64_t start; int64_t arrival; uint32_t len, _pad; };   // start: stream position
+struct TcpCand { uint32_t q, exit, nframes, code; uint64_t sbytes; };      // q / exit: chunk offsets
+struct TcpChunkRes { uint32_t entry, fbase; uint64_t sbase; };            // entry kTcpNone: idle chunk
+struct TcpTotals { uint32_t frames; int32_t status; uint64_t slot_bytes; };
+
+struct TcpParams {
+    TcpGroup* groups;
+    uint32_t ngroups, nchunks;
+    const TcpRead* reads;
+    const uint32_t* chunk_group;
+    TcpCand* cands;         // nchunks x kTcpCands
+    uint8_t* links;         // nchunks x kTcpCands: next chunk's candidate, 0xFE terminal, 0xFF search
+    uint32_t* ncand;
+    TcpChunkRes* chunkres;
+    const uint8_t* raw;
+    uint64_t raw_bytes;
+    uint8_t* carry;         // per session kTcpCarry bytes
+    uint8_t* blob;          // frame slots for k_ingest
+    uint64_t blob_cap;
+    edgpu_pkt_desc* desc;
+    uint32_t max_desc;
+    uint32_t* seg_off;      // ngroups + 1
+    uint32_t* seg_sess;
+    edgpu_tcp_result* results;
+    TcpTotals* tot;
+};
+
 struct ImageParams {
     SenderDev* senders;
     SessionDev* sessions;

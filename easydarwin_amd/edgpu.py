@@ -29,8 +29,9 @@ EXPORTED = [
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
-    "edgpu_subscribers_add",
+    "edgpu_subscribers_add", "edgpu_ingest_interleaved",
 ]
+TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 
 
@@ -97,6 +98,9 @@ OUT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("packet_id", "<u4")])
 SUB_DTYPE = np.dtype([("subscriber", "<u4"), ("track", "<u2"), ("kind", "u1"), ("transport", "u1"),
                       ("desc_base", "<u4"), ("desc_count", "<u4"), ("out_base", "<u8"),
                       ("out_bytes", "<u8")])
+TCP_READ_DTYPE = np.dtype([("session", "<u4"), ("len", "<u4"), ("offset", "<u8"), ("arrival_ms", "<i8")])
+TCP_RESULT_DTYPE = np.dtype([("frames", "<u4"), ("consumed", "<u4"), ("status", "<i4"), ("carry", "<u4")])
+assert TCP_READ_DTYPE.itemsize == 24 and TCP_RESULT_DTYPE.itemsize == 16
 assert PKT_DTYPE.itemsize == C.sizeof(PktDesc) == 16
 assert OUT_DTYPE.itemsize == C.sizeof(OutDesc) == 16
 assert SUB_DTYPE.itemsize == C.sizeof(SubstreamOut) == 32
@@ -150,6 +154,7 @@ def load(path: str = LIB_PATH):
         "edgpu_fanout_kernel": (C.c_char_p, [P]),
         "edgpu_subscriber_play": (I32, [P, U32, I32, U32, I64, C.POINTER(U32), P]),
         "edgpu_subscribers_add": (I32, [P, U32, P, P, P]),
+        "edgpu_ingest_interleaved": (I32, [P, P, U32, P, U64, I32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -246,6 +251,23 @@ class Context:
         _check(self.lib.edgpu_ingest(self.h, C.c_void_p(desc_ptr), n, C.c_void_p(seg_ptr),
                                      C.c_void_p(seg_sess_ptr), nseg, C.c_void_p(blob_ptr),
                                      blob_bytes, PTR_DEVICE))
+
+    def ingest_interleaved(self, reads: np.ndarray, data, device_ptr: int | None = None) -> np.ndarray:
+        """RTSP-interleaved push ingest: `reads` (TCP_READ_DTYPE: session, len, offset,
+        arrival_ms; a session's reads consecutive and contiguous in the bytes) over `data`
+        (host bytes / uint8 array), or over device memory at `device_ptr` (then `data` is its
+        byte count).  Returns the per-read results (TCP_RESULT_DTYPE)."""
+        reads = np.ascontiguousarray(reads, dtype=TCP_READ_DTYPE)
+        out = np.zeros(len(reads), dtype=TCP_RESULT_DTYPE)
+        if device_ptr is None:
+            buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+                np.ascontiguousarray(data, dtype=np.uint8)
+            _check(self.lib.edgpu_ingest_interleaved(self.h, _ptr(reads), len(reads), _ptr(buf), buf.nbytes,
+                                                     PTR_HOST, _ptr(out)))
+        else:
+            _check(self.lib.edgpu_ingest_interleaved(self.h, _ptr(reads), len(reads), C.c_void_p(device_ptr),
+                                                     int(data), PTR_DEVICE, _ptr(out)))
+        return out
 
     def keyframe_index(self):
         _check(self.lib.edgpu_keyframe_index(self.h))

@@ -5,9 +5,18 @@ is a byte comparison.
 Batch semantics: all PKT events since the previous TICK form one ``edgpu_ingest`` batch
 (grouped by session, arrival order kept), followed by ``edgpu_keyframe_index``; JOINs since
 the previous TICK become ``edgpu_subscriber_add``; the TICK itself is ``edgpu_fanout(now)``.
+
+``interleaved=seed`` feeds the same packets as a pusher's RTSP connection would carry them
+('$' ch BE16(len) frames) through ``edgpu_ingest_interleaved`` instead: each session's
+frames are cut into random TCP reads (cuts only between or inside frames of one arrival time,
+so every frame completes in a read with its own arrival time), a random prefix of a
+session's next-batch frame is sent early (carried on the device across calls), and RTSP
+keep-alive requests sit between frames; the replay answers EDGPU_TCP_MESSAGE like the host
+RTSP stack (consume the request through its blank line, resubmit the rest).
 """
 from __future__ import annotations
 
+import random
 import struct
 
 import numpy as np
@@ -32,7 +41,103 @@ def _wire_images(subs, desc, arena, images):
                 parts.append(struct.pack(">H", ln) + arena[off:off + ln].tobytes())
 
 
-def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None, **cfg):
+RTSP_KEEPALIVE = (b"SET_PARAMETER rtsp://127.0.0.1/live/replay RTSP/1.0\r\nCSeq: 7\r\n"
+                  b"Session: 51234\r\nContent-Length: 0\r\n\r\n")
+
+
+def tcp_plan(batches, seed: int, messages: float = 0.1, carry: float = 0.5):
+    """Per ingest batch (list of (session, channel, t, packet)): {session: [(read bytes, arrival)]}."""
+    rng = random.Random(seed)
+    per = []
+    for b in batches:
+        d = {}
+        for s, ch, t, data in b:
+            d.setdefault(s, []).append((t, struct.pack(">BBH", 0x24, ch, len(data)) + data))
+        per.append(d)
+    plan, carry_in = [], {}
+    for k, d in enumerate(per):
+        out = {}
+        for s, frames in d.items():
+            groups = []
+            for t, fb in frames:
+                if groups and groups[-1][0] == t:
+                    groups[-1][1].append(fb)
+                else:
+                    groups.append((t, [fb]))
+            pre = carry_in.pop(s, 0)
+            reads = []
+            for gi, (t, fbs) in enumerate(groups):
+                data = b"".join(fbs)[pre if gi == 0 else 0:]
+                if gi > 0 and rng.random() < messages:
+                    data = RTSP_KEEPALIVE + data
+                p = 0
+                while p < len(data):
+                    n = rng.choice([1, 3, rng.randint(1, 200), rng.randint(1, 4000), len(data)])
+                    reads.append((data[p:p + n], t))
+                    p += n
+            if k + 1 < len(per) and s in per[k + 1] and rng.random() < carry:
+                first = per[k + 1][s][0][1]
+                m = rng.randint(1, len(first) - 1)
+                reads.append((first[:m], reads[-1][1] if reads else 0))
+                carry_in[s] = m
+            out[s] = reads
+        plan.append(out)
+    return plan
+
+
+def ingest_tcp(ctx: edgpu.Context, reads_by_session: dict):
+    """One batch of pusher reads through edgpu_ingest_interleaved (+ keyframe index), handing
+    RTSP requests to a minimal "RTSP stack" that skips them and resubmits what follows."""
+    todo = {s: list(rs) for s, rs in reads_by_session.items() if rs}
+    calls = 0
+    while todo:
+        rows, blob = [], bytearray()
+        for s, rs in todo.items():
+            for b, t in rs:
+                rows.append((s, len(b), len(blob), t))
+                blob += b
+        res = ctx.ingest_interleaved(np.array(rows, dtype=edgpu.TCP_READ_DTYPE), bytes(blob))
+        ctx.keyframe_index()
+        calls += 1
+        nxt, i = {}, 0
+        for s, rs in todo.items():
+            r = res[i:i + len(rs)]
+            i += len(rs)
+            bad = np.nonzero(r["status"])[0]
+            if not len(bad):
+                continue
+            j = int(bad[0])
+            if int(r["status"][j]) != edgpu.TCP_MESSAGE:
+                raise RuntimeError(f"session {s}: pusher connection dropped (status {int(r['status'][j])})")
+            rest = [(rs[j][0][int(r["consumed"][j]):], rs[j][1])] + rs[j + 1:]
+            buf = b"".join(b for b, _ in rest)
+            end = buf.index(b"\r\n\r\n") + 4
+            new, p = [], 0
+            for b, t in rest:
+                lo, p = p, p + len(b)
+                if p > end:
+                    new.append((b[max(0, end - lo):], t))
+            if new:
+                nxt[s] = new
+        todo = nxt
+    return calls
+
+
+def _batches(trace: Trace, flush_on_rtpinfo: bool):
+    out, cur = [], []
+    for ev in trace.events:
+        if ev[0] == PKT:
+            _, t, s, ch, data = ev
+            cur.append((s, ch, t, data))
+        elif (ev[0] == JOIN and ev[5] & 1 and flush_on_rtpinfo) or ev[0] == TICK:
+            if cur:
+                out.append(cur)
+                cur = []
+    return out
+
+
+def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
+           interleaved: int | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -80,13 +185,19 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 unread = None
 
         clock = 0                           # the harness's virtual clock: max event time so far
+        plan = tcp_plan(_batches(trace, rep is None), interleaved) if interleaved is not None else None
+        nflush = 0
 
         def flush():
-            nonlocal pending
+            nonlocal pending, nflush
             if pending:
-                desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
-                ctx.ingest_host(desc, seg_off, seg_sess, blob)
-                ctx.keyframe_index()
+                if plan is not None:
+                    ingest_tcp(ctx, plan[nflush])
+                else:
+                    desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
+                    ctx.ingest_host(desc, seg_off, seg_sess, blob)
+                    ctx.keyframe_index()
+                nflush += 1
                 pending = []
 
         for ev in trace.events:

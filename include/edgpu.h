@@ -18,6 +18,9 @@
  *   edgpu_ingest           ReflectorStream::PushPacket + ReflectorSocket::ProcessPacket
  *                          (ReflectorStream.cpp:529-576, 1769-2010), called per packet by
  *                          ProcessRTPData (QTSSReflectorModule.cpp:604-678)
+ *   edgpu_ingest_interleaved RTSPRequestStream::ReadRequest's '$' deframing of a pusher's
+ *                          RTSP connection (Server.tproj/RTSPRequestStream.cpp:65-171) +
+ *                          edgpu_ingest of the frames
  *   edgpu_keyframe_index   the keyframe index update + audio anchor inside ProcessPacket
  *                          (ReflectorStream.cpp:1876-1934, IsKeyFrameFirstPacket :1403-1513)
  *   edgpu_fanout           ReflectorSender::ReflectPackets / SendPacketsToOutput /
@@ -204,6 +207,51 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
                   const uint32_t* seg_offsets, const uint32_t* seg_session,
                   uint32_t n_segments, const uint8_t* blob, uint64_t blob_bytes,
                   int ptr_location);
+/* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
+ * Replaces RTSPRequestStream::ReadRequest's '$' branch (Server.tproj/RTSPRequestStream.cpp:
+ * 65-171, RTSPSession.cpp:240-262) and the per-frame hand-off to ProcessRTPData
+ * (RTSPSession.cpp:2131-2178, QTSSReflectorModule.cpp:604-678): each connection's bytes are
+ * split into '$' ch BE16(len) frames, frame i of a session becomes a packet on channel `ch`
+ * (track ch/2, RTCP when odd) with the arrival time of the read that completed it, and the
+ * packets are ingested exactly as edgpu_ingest would (same batch semantics; run
+ * edgpu_keyframe_index next).  A frame split across calls is carried on the device (at most
+ * 2046 bytes per session).
+ *
+ * reads[i] is one read of session reads[i].session (an RTSP-interleaved, udp_push = 0
+ * session): `len` bytes at bytes + offset.  A session's reads are consecutive entries of
+ * `reads`, in arrival order, and contiguous in `bytes`.  `bytes` is host memory
+ * (EDGPU_PTR_HOST, staged) or device memory on the ctx GPU (EDGPU_PTR_DEVICE, 16-B aligned).
+ *
+ * results[i] (host memory) reports read i: `frames` it completed, `consumed` bytes the engine
+ * took (framed or carried), and `status`:
+ *   EDGPU_TCP_MESSAGE  a non-'$' byte at a frame boundary: an RTSP request (e.g. a
+ *                      SET_PARAMETER keep-alive or TEARDOWN) starts at byte `consumed` of this
+ *                      read; the rest of this read and the session's later reads in this call
+ *                      are the host RTSP stack's.  The session's carry is cleared.
+ *   EDGPU_TCP_DROPPED  a frame longer than the 2047-byte request buffer: the reference asks the
+ *                      socket for 0 bytes and treats the connection as closed (Socket.cpp:
+ *                      383-388); set on the read that fills the buffer and later reads.
+ * `carry` is the session's carried byte count after the call.  Returns EDGPU_OUT_OVERFLOW
+ * (nothing ingested, no carry changed) when the frames exceed max_batch_packets or their
+ * 16-B slots max_batch_bytes.  Syncs (the results are read back). */
+#define EDGPU_TCP_MESSAGE  1
+#define EDGPU_TCP_DROPPED  2
+typedef struct edgpu_tcp_read {
+    uint32_t session;
+    uint32_t len;
+    uint64_t offset;        /* byte offset of the read in `bytes` */
+    int64_t  arrival_ms;    /* OS::Milliseconds() when the read returned */
+} edgpu_tcp_read;
+typedef struct edgpu_tcp_result {
+    uint32_t frames;
+    uint32_t consumed;
+    int32_t  status;        /* 0, EDGPU_TCP_MESSAGE or EDGPU_TCP_DROPPED */
+    uint32_t carry;
+} edgpu_tcp_result;
+int  edgpu_ingest_interleaved(edgpu_ctx* ctx, const edgpu_tcp_read* reads, uint32_t n_reads,
+                              const uint8_t* bytes, uint64_t n_bytes, int ptr_location,
+                              edgpu_tcp_result* results);
+
 int  edgpu_keyframe_index(edgpu_ctx* ctx);
 int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
 

@@ -81,3 +81,61 @@ def read_events(path: str) -> list[tuple]:
         p += blen
         out.append((kind, read, ch, a, data if kind == FRAME else (b"" if kind == TOO_LONG else None)))
     return out
+
+
+# ---- the engine boundary's per-read report (include/edgpu.h, edgpu_ingest_interleaved) ----
+TCP_MESSAGE, TCP_DROPPED = 1, 2
+
+
+def ingest_reads(carry: dict, rows, blob: bytes):
+    """Restatement of edgpu_ingest_interleaved on the framing above.
+
+    carry: session -> carried bytes (updated).  rows: (session, len, offset, arrival_ms) with a
+    session's reads consecutive and contiguous.  Returns (results, frames): results[i] =
+    [frames, consumed, status, carry] per read; frames = [(session, channel, arrival, packet)]
+    in stream order (a frame's arrival is that of the read holding its last byte)."""
+    import bisect
+    results = [[0, 0, 0, 0] for _ in rows]
+    frames = []
+    i, n = 0, len(rows)
+    while i < n:
+        s = rows[i][0]
+        j = i
+        while j < n and rows[j][0] == s:
+            j += 1
+        stream = carry.get(s, b"")
+        starts = []
+        for k in range(i, j):
+            starts.append(len(stream))
+            stream += blob[rows[k][2]:rows[k][2] + rows[k][1]]
+        L, pos, code = len(stream), 0, "end"
+        while pos < L:
+            if stream[pos] != 0x24:
+                code = "message"
+                break
+            if pos + 4 > L:
+                code = "partial"
+                break
+            flen = 4 + (stream[pos + 2] << 8 | stream[pos + 3])
+            if flen > MAX_FRAME:
+                code = "dropped" if L - pos >= MAX_FRAME else "partial"
+                break
+            if pos + flen > L:
+                code = "partial"
+                break
+            r = bisect.bisect_right(starts, pos + flen - 1) - 1
+            frames.append((s, stream[pos + 1], rows[i + r][3], stream[pos + 4:pos + flen]))
+            results[i + r][0] += 1
+            pos += flen
+        carry[s] = stream[pos:] if code == "partial" else b""
+        for k in range(i, j):
+            st, ln = starts[k - i], rows[k][1]
+            consumed, status = ln, 0
+            if code in ("message", "dropped"):
+                consumed = max(0, min(pos - st, ln))
+                at = pos if code == "message" else pos + MAX_FRAME - 1
+                if st + ln > at:
+                    status = TCP_MESSAGE if code == "message" else TCP_DROPPED
+            results[k][1:] = [consumed, status, len(carry[s])]
+        i = j
+    return results, frames

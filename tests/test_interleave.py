@@ -88,3 +88,103 @@ def test_restatement_matches_live_reference(seed, tmp_path):
     data = b"".join(parts)
     reads = _split(rng, data, 1, rng.choice([3, 200, 4096, 70000]), zero=0.05)
     assert _summ(deframe(reads)) == _summ(_ref(reads, tmp_path))
+
+
+# ---- the boundary's per-read report (oracle.interleave.ingest_reads) vs the framing ----
+
+def _rows(reads, session=0, t0=0):
+    rows, off = [], 0
+    for k, r in enumerate(reads):
+        rows.append((session, len(r), off, t0 + k))
+        off += len(r)
+    return rows, b"".join(reads)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_ingest_report_agrees_with_framing(name):
+    from oracle.interleave import TCP_DROPPED, TCP_MESSAGE, ingest_reads
+    reads = case(name)
+    ev = deframe(reads)
+    # one call
+    rows, blob = _rows(reads)
+    res, frames = ingest_reads({}, rows, blob)
+    fr = [e for e in ev if e[0] == FRAME]
+    assert [(f[1], f[3]) for f in frames] == [(e[2], e[4]) for e in fr]
+    assert [f[2] for f in frames] == [e[1] for e in fr]             # arrival = completing read
+    per_read = [0] * len(reads)
+    for e in fr:
+        per_read[e[1]] += 1
+    assert [r[0] for r in res] == per_read
+    last = ev[-1] if ev else None
+    if last and last[0] == MESSAGE:
+        k = next(i for i, r in enumerate(res) if r[2])
+        assert res[k][2] == TCP_MESSAGE and sum(len(x) for x in reads[:k]) + res[k][1] == last[3]
+    elif last and last[0] == 3:
+        k = next(i for i, r in enumerate(res) if r[2])
+        assert res[k][2] == TCP_DROPPED and k == last[1]
+    else:
+        assert not any(r[2] for r in res)
+    # the same reads over several calls (device carry between them)
+    rng = random.Random(name)
+    carry, frames2, k = {}, [], 0
+    while k < len(reads):
+        m = rng.randint(1, 40)
+        rows, blob = _rows(reads[k:k + m], t0=k)
+        r2, f2 = ingest_reads(carry, rows, blob)
+        frames2 += f2
+        if any(x[2] for x in r2):
+            break
+        k += m
+    assert [(f[1], f[3], f[2]) for f in frames2] == [(f[1], f[3], f[2]) for f in frames]
+
+
+# ---- the replay's pusher model (easydarwin_amd/replay.py tcp_plan / ingest_tcp) on CPU ----
+
+class _RestatedCtx:
+    """Answers ingest_interleaved from the restatement, so the host-side replay logic
+    (read splitting, carried prefixes, RTSP keep-alives) is checked without a GPU."""
+
+    def __init__(self):
+        self.carry, self.frames = {}, []
+
+    def ingest_interleaved(self, rows, data):
+        import numpy as np
+        from easydarwin_amd import edgpu
+        from oracle.interleave import ingest_reads
+        rr = [(int(r["session"]), int(r["len"]), int(r["offset"]), int(r["arrival_ms"])) for r in rows]
+        res, fr = ingest_reads(self.carry, rr, data)
+        self.frames += fr
+        return np.array([tuple(r) for r in res], dtype=edgpu.TCP_RESULT_DTYPE)
+
+    def keyframe_index(self):
+        pass
+
+
+def _scenario_names():
+    from scenarios import SCENARIOS
+    return list(SCENARIOS)
+
+
+@pytest.mark.parametrize("name", _scenario_names())
+def test_replay_pusher_model_delivers_every_packet(name):
+    from easydarwin_amd.replay import _batches, ingest_tcp, tcp_plan
+    from easydarwin_amd.trace import PKT
+    from scenarios import SCENARIOS
+    tr = SCENARIOS[name]()
+    if any(len(ev[4]) > 2043 for ev in tr.events if ev[0] == PKT):
+        pytest.skip("packets above 2043 bytes cannot travel RTSP-interleaved (connection dropped)")
+    batches = _batches(tr, True)
+    plan = tcp_plan(batches, seed=7)
+    ctx = _RestatedCtx()
+    calls = 0
+    for b, p in zip(batches, plan):
+        ctx.frames = []
+        calls += ingest_tcp(ctx, p)
+        got, want = {}, {}
+        for s, ch, t, data in ctx.frames:
+            got.setdefault(s, []).append((ch, t, data))
+        for s, ch, t, data in b:
+            want.setdefault(s, []).append((ch, t, data))
+        assert got == want
+    assert calls >= len(batches)                    # more when keep-alives were answered
+    assert not any(ctx.carry.values())
