@@ -68,9 +68,44 @@ def make_batch_on_device(b: dict, dev: torch.device, gen: torch.Generator):
             "bytes": total, "t": b["t_end"], "in_bytes": int(b["len"].astype(np.int64).sum())}
 
 
+def make_tcp_on_device(bt: dict, b: dict, dev: torch.device, read_bytes: int = 65536):
+    """The same batch as the pushers' RTSP connections carry it: per session, its packets as
+    '$' ch BE16(len) frames back to back in HBM, cut into `read_bytes` TCP reads (a read's
+    arrival is that of the frame holding its last byte).  Built once, outside the timing."""
+    flen = b["len"].astype(np.int64) + 4
+    raw_off = np.concatenate([[0], np.cumsum(flen)[:-1]])
+    slot_off = bt["desc"].cpu().numpy().view(edgpu.PKT_DTYPE)["slot"].astype(np.int64) * 16
+    total = int(flen.sum())
+    # gather: raw[raw_off_i + k] = slot bytes [slot_off_i + k] (the slot = 4-B prefix + packet)
+    delta = torch.from_numpy(slot_off - raw_off).to(dev)
+    idx = torch.repeat_interleave(delta, torch.from_numpy(flen).to(dev)) + torch.arange(total, device=dev)
+    raw = bt["blob"][idx]
+    del idx
+    hdr = np.stack([np.full(len(flen), 0x24, np.uint8), b["channel"].astype(np.uint8),
+                    (b["len"] >> 8).astype(np.uint8), (b["len"] & 0xFF).astype(np.uint8)], axis=1)
+    pos = torch.from_numpy(raw_off).to(dev)
+    hd = torch.from_numpy(hdr).to(dev)
+    for k in range(4):
+        raw[pos + k] = hd[:, k]
+    seg = b["seg_off"].astype(np.int64)
+    rows = []
+    frame_end = raw_off + flen
+    for s in range(len(seg) - 1):
+        lo = int(raw_off[seg[s]]) if seg[s + 1] > seg[s] else 0
+        hi = int(frame_end[seg[s + 1] - 1]) if seg[s + 1] > seg[s] else 0
+        for o in range(lo, hi, read_bytes):
+            ln = min(read_bytes, hi - o)
+            last = int(np.searchsorted(frame_end, o + ln, side="left"))
+            rows.append((s, ln, o, int(b["arrival"][min(last, len(flen) - 1)])))
+    return {"raw": raw, "reads": np.array(rows, dtype=edgpu.TCP_READ_DTYPE), "raw_bytes": total}
+
+
 def run_step(ctx: edgpu.Context, bt: dict):
-    ctx.ingest_device(bt["desc"].data_ptr(), bt["n"], bt["seg"].data_ptr(), bt["sess"].data_ptr(),
-                      bt["nseg"], bt["blob"].data_ptr(), bt["bytes"])
+    if "tcp" in bt:
+        ctx.ingest_interleaved(bt["tcp"]["reads"], bt["tcp"]["raw_bytes"], device_ptr=bt["tcp"]["raw"].data_ptr())
+    else:
+        ctx.ingest_device(bt["desc"].data_ptr(), bt["n"], bt["seg"].data_ptr(), bt["sess"].data_ptr(),
+                          bt["nseg"], bt["blob"].data_ptr(), bt["bytes"])
     ctx.keyframe_index()
     ctx.fanout(bt["t"])
 
@@ -130,6 +165,10 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="tick pipelining: ingest(t+1) beside the fan-out copy of t on a second stream "
                          "(measured slower on C2: both phases are HBM-bound and contend)")
+    ap.add_argument("--ingest", choices=["desc", "tcp"], default="desc",
+                    help="desc: packets handed over as descriptors + slots (edgpu_ingest, the reflector's "
+                         "per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP reads, "
+                         "deframed on the GPU (edgpu_ingest_interleaved)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,7 +190,15 @@ def main():
     t_gen = time.time()
     gen = torch.Generator(device=dev)
     gen.manual_seed(0xEA5D + rank)
-    batches = [make_batch_on_device(fleet.next_batch(), dev, gen) for _ in range(steps + warm)]
+    batches = []
+    for _ in range(steps + warm):
+        b = fleet.next_batch()
+        bt = make_batch_on_device(b, dev, gen)
+        if args.ingest == "tcp":
+            bt["tcp"] = make_tcp_on_device(bt, b, dev)
+            bt.pop("blob")
+            bt["raw_bytes"] = bt["tcp"]["raw_bytes"]
+        batches.append(bt)
     torch.cuda.synchronize(dev)
     log(f"[bench] generated in {time.time() - t_gen:.1f}s; max batch {max(b['n'] for b in batches)} pkts, "
         f"{max(b['bytes'] for b in batches) / 2**20:.0f} MiB")
@@ -164,7 +211,8 @@ def main():
     ctx = edgpu.Context(device=local, video_ring_packets=8192, video_ring_bytes=16 << 20,
                         other_ring_packets=256, other_ring_bytes=64 << 10,
                         out_arena_bytes=max_arena, max_out_packets=max_out,
-                        max_batch_packets=max_pk + 1, max_batch_bytes=1 << 20,
+                        max_batch_packets=max_pk + 1,
+                        max_batch_bytes=(max(b["bytes"] for b in batches) + (1 << 20)) if args.ingest == "tcp" else 1 << 20,
                         overlap_ticks=1 if args.overlap else 0)
     for _ in gids:
         s = ctx.session_add(fleet.sdp())
@@ -241,7 +289,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (PCG64 RTP/H.264 FU-A headers, GPU-random payload)",
         "config": {"workload": f"C2: {args.sessions} H.264 1080p30 4 Mb/s streams/GPU x {args.subs} UDP subs, "
-                               f"{args.tick_ms}-ms ticks (ingest+keyframe+fan-out per step)",
+                               f"{args.tick_ms}-ms ticks (ingest+keyframe+fan-out per step)"
+                               + (", RTSP-interleaved TCP push reads deframed on the GPU" if args.ingest == "tcp" else ""),
+                   "ingest": args.ingest,
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"},
         "relayed_GBps": round(out_all / dt / 1e9, 2),

@@ -9,30 +9,35 @@
 //
 // Here a session's stream (carried partial frame ++ this call's reads) is cut into 16 KiB
 // chunks.  A frame starts at most kTcpMaxFrame - 1 bytes before a chunk boundary, so the true
-// walk enters each chunk at a '$' within its first kTcpMaxFrame bytes.  k_tcp_walk walks every
-// such candidate to the chunk end at once (one lane each) and links its exit to the next
-// chunk's candidate; k_tcp_resolve follows the links (LDS) per session and scans frame and
-// slot counts; k_tcp_scan lays sessions out in the ingest staging; k_tcp_emit re-walks each
-// chunk from its true entry and writes every frame into a 16-B slot ('$' header word, packet,
-// zero pad) with its edgpu_pkt_desc; k_tcp_finish carries the partial frame and reports per
-// read.  k_ingest then runs unchanged on the emitted batch.
+// walk enters each chunk at a '$' within its first kTcpMaxFrame bytes.
+//   k_tcp_walk     one wave per chunk: finds those candidates (one load round, 32 bytes a
+//                  lane), walks every candidate to the chunk end at once (a lane each; header
+//                  bytes only), records its first kTcpFrames frame starts and links its exit to
+//                  the next chunk's candidate.
+//   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
+//                  scans the chunks' frame counts.
+//   k_tcp_scan     sessions -> ingest segments, capacity check.
+//   k_tcp_emit     one wave per chunk: a descriptor and a source address per frame of the true
+//                  walk (lanes in parallel from the recorded starts); the frame bytes stay where
+//                  they are -- k_ingest copies them from the TCP bytes into the sender rings
+//                  (IngestParams.src_addr).  Only a frame that starts in the carried bytes is
+//                  staged (contiguous copy).
+//   k_tcp_finish   one workgroup per session: carry the partial frame, per-read report.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "edgpu.h"
 #include "edgpu_device.h"
 #include "edgpu_params.h"
+#include "edgpu_bytes.h"
 
 namespace edgpu {
 
 namespace {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// A session's stream in this call: carry[0, clen) ++ raw[raw_off, raw_off + len - clen).
+// A session's stream in this call: carry[0, clen) ++ raw[0, len - clen).
 struct TcpView {
     const uint8_t* carry;
-    const uint8_t* raw;     // raw + raw_off
-    const uint8_t* raw_end; // end of the raw buffer (bounds for wide loads)
+    const uint8_t* raw;     // P.raw + raw_off
     uint32_t clen;
     uint64_t len;
 };
@@ -41,7 +46,6 @@ __device__ __forceinline__ TcpView tcp_view(const TcpParams& P, const TcpGroup& 
     TcpView v;
     v.carry = P.carry + (uint64_t)G.session * kTcpCarry;
     v.raw = P.raw + G.raw_off;
-    v.raw_end = P.raw + P.raw_bytes;
     v.clen = G.carry_len;
     v.len = G.len;
     return v;
@@ -55,51 +59,78 @@ __device__ __forceinline__ uint32_t tbyte(const TcpView& v, uint64_t p) {
 // or why the walk stops there.
 __device__ __forceinline__ uint32_t tcp_step(const TcpView& v, uint64_t pos, uint32_t& flen) {
     if (pos >= v.len) return kWalkPartial;                         // nothing left (carry 0)
-    if (tbyte(v, pos) != 0x24u) return kWalkMessage;
+    uint32_t b0, b2, b3;
+    if (pos >= v.clen && pos + 4 <= v.len) {                       // the common case: 3 loads at once
+        const uint8_t* q = v.raw + (pos - v.clen);
+        b0 = q[0]; b2 = q[2]; b3 = q[3];
+    } else {
+        b0 = tbyte(v, pos);
+        b2 = pos + 2 < v.len ? tbyte(v, pos + 2) : 0u;
+        b3 = pos + 3 < v.len ? tbyte(v, pos + 3) : 0u;
+    }
+    if (b0 != 0x24u) return kWalkMessage;
     if (pos + 4 > v.len) return kWalkPartial;
-    flen = 4 + (tbyte(v, pos + 2) << 8 | tbyte(v, pos + 3));
+    flen = 4 + (b2 << 8 | b3);
     if (flen > kTcpMaxFrame) return v.len - pos >= kTcpMaxFrame ? kWalkDropped : kWalkPartial;
     if (pos + flen > v.len) return kWalkPartial;
     return kWalkRun;
 }
 
-// Walks from `pos` until reaching `end` or a stop; counts frames and their slot bytes.
-__device__ __forceinline__ uint32_t tcp_walk(const TcpView& v, uint64_t& pos, uint64_t end, uint32_t& nf,
-                                             uint64_t& sb) {
+// Walks from `pos` until reaching `end` or a stop; counts frames, recording the first
+// kTcpFrames starts (chunk offsets from `start`) in `rec` when given.
+__device__ __forceinline__ uint32_t tcp_walk(const TcpView& v, uint64_t& pos, uint64_t start, uint64_t end,
+                                             uint32_t& nf, uint16_t* rec) {
     nf = 0;
-    sb = 0;
     while (pos < end) {
         uint32_t flen = 0;
         const uint32_t code = tcp_step(v, pos, flen);
         if (code != kWalkRun) return code;
+        if (rec && nf < kTcpFrames) rec[nf] = (uint16_t)(pos - start);
         nf++;
-        sb += (flen + 15) & ~15u;
         pos += flen;
     }
     return kWalkRun;
 }
 
-// '$' bytes among the first kTcpMaxFrame bytes of the chunk at `start` (offsets, in order, the
+// '$' bytes among the first kTcpMaxFrame bytes of the chunk at `start` (offsets, in order; the
 // first kTcpCands kept in `list`); the stream's first chunk has the single candidate 0.  One
-// wave; returns the full count (> kTcpCands: overflow).
+// wave, 32 bytes a lane in one round of independent loads; returns the full count
+// (> kTcpCands: overflow).
 __device__ uint32_t tcp_candidates(const TcpView& v, uint64_t start, uint16_t* list, int lane) {
     if (start == 0) {
         if (lane == 0) list[0] = 0;
         return 1;
     }
     const uint64_t wend = min(start + (uint64_t)kTcpMaxFrame, v.len);
-    uint32_t n = 0;
-    for (uint64_t o = start; o < wend; o += 64) {
-        const uint64_t p = o + (uint64_t)lane;
-        const bool is = p < wend && tbyte(v, p) == 0x24u;
-        const uint64_t m = __ballot(is);
-        if (is) {
-            const uint32_t i = n + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-            if (i < kTcpCands) list[i] = (uint16_t)(p - start);
+    const uint64_t b = start + 32ull * (uint64_t)lane;
+    uint32_t mask = 0;
+    if (b < wend) {
+        const uint32_t n = (uint32_t)min<uint64_t>(32, wend - b);
+        if (b >= v.clen) {
+            const uint8_t* q = v.raw + (b - v.clen);
+#pragma unroll
+            for (int i = 0; i < 32; i++)
+                if ((uint32_t)i < n && q[i] == 0x24u) mask |= 1u << i;
+        } else {
+            for (uint32_t i = 0; i < n; i++)
+                if (tbyte(v, b + i) == 0x24u) mask |= 1u << i;
         }
-        n += (uint32_t)__popcll(m);
     }
-    return n;
+    const uint32_t cnt = (uint32_t)__popc(mask);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    uint32_t idx = incl - cnt;
+    while (mask) {
+        const int i = __ffs(mask) - 1;
+        mask &= mask - 1;
+        if (idx < kTcpCands) list[idx] = (uint16_t)(b + i - start);
+        idx++;
+    }
+    return __shfl(incl, 63, 64);
 }
 
 template <typename T>
@@ -143,10 +174,10 @@ __global__ __launch_bounds__(64) void k_tcp_walk(TcpParams P) {
     __syncthreads();
     if (lane == 0) P.ncand[c] = n;
     if (n > kTcpCands || (uint32_t)lane >= n) return;
+    const size_t ci = (size_t)c * kTcpCands + lane;
     uint64_t pos = start + own[lane];
     uint32_t nf;
-    uint64_t sb;
-    const uint32_t code = tcp_walk(v, pos, end, nf, sb);
+    const uint32_t code = tcp_walk(v, pos, start, end, nf, P.offs + ci * kTcpFrames);
     uint8_t link = 0xFE;
     if (code == kWalkRun && pos < v.len) {                  // continues in the next chunk
         link = 0xFF;
@@ -161,9 +192,8 @@ __global__ __launch_bounds__(64) void k_tcp_walk(TcpParams P) {
     r.exit = (uint32_t)(pos - start);
     r.nframes = nf;
     r.code = code;
-    r.sbytes = sb;
-    P.cands[(size_t)c * kTcpCands + lane] = r;
-    P.links[(size_t)c * kTcpCands + lane] = link;
+    P.cands[ci] = r;
+    P.links[ci] = link;
 }
 
 // ---- k_tcp_resolve: one workgroup per session; thread 0 follows the links ----
@@ -177,8 +207,6 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
     __shared__ uint8_t s_link[kPiece * kTcpCands];
     __shared__ uint8_t s_idx[kPiece];                 // candidate index, 0xFD sequential, 0xFF idle
     __shared__ uint32_t s_nf[kPiece], s_exit[kPiece], s_code[kPiece], s_entry[kPiece];
-    __shared__ uint64_t s_sb[kPiece];
-    __shared__ uint64_t scan64[4];
     __shared__ uint32_t scan32[4];
     __shared__ uint32_t s_stop_code;
     __shared__ uint64_t s_stop;
@@ -188,7 +216,6 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
     uint64_t entry = 0;
     bool stopped = false;
     uint32_t fb = 0;
-    uint64_t sbb = 0;
     for (uint32_t k0 = 0; k0 < G.nchunks; k0 += kPiece) {
         const uint32_t np = min(kPiece, G.nchunks - k0);
         const uint32_t c0 = G.first_chunk + k0;
@@ -220,12 +247,11 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
                     if (j < 0) {
                         uint64_t pos = entry;
                         uint32_t nf = 0, code;
-                        uint64_t sb = 0;
-                        if (n <= kTcpCands) code = kWalkMessage;              // not a '$'
-                        else code = tcp_walk(v, pos, end, nf, sb);            // too many candidates
+                        if (n <= kTcpCands) code = kWalkMessage;                        // not a '$'
+                        else code = tcp_walk(v, pos, start, end, nf, nullptr);          // too many candidates
                         s_idx[kk] = 0xFD;
                         s_entry[kk] = (uint32_t)(entry - start);
-                        s_nf[kk] = nf; s_sb[kk] = sb; s_code[kk] = code; s_exit[kk] = (uint32_t)(pos - start);
+                        s_nf[kk] = nf; s_code[kk] = code; s_exit[kk] = (uint32_t)(pos - start);
                         if (code != kWalkRun || pos >= v.len) stopped = true;
                         else entry = pos;
                         continue;
@@ -244,10 +270,8 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
             }
         }
         __syncthreads();
-        // per chunk of the piece: its true walk's counts, then the scan
-        uint32_t nf = 0;
-        uint64_t sb = 0;
-        uint32_t ent = kTcpNone;
+        // per chunk of the piece: its true walk's frame count, then the scan
+        uint32_t nf = 0, ent = kTcpNone, cand = kTcpNone;
         if ((uint32_t)tid < np) {
             const uint32_t c = c0 + tid;
             const uint64_t start = (uint64_t)(k0 + tid) * kTcpChunk;
@@ -256,33 +280,30 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
             bool terminal = false;
             if (idx < kTcpCands) {
                 const TcpCand r = P.cands[(size_t)c * kTcpCands + idx];
-                nf = r.nframes; sb = r.sbytes; ent = r.q; code = r.code; ex = r.exit;
+                nf = r.nframes; ent = r.q; code = r.code; ex = r.exit; cand = idx;
                 terminal = s_link[tid * kTcpCands + idx] == 0xFE;
             } else if (idx == 0xFD) {
-                nf = s_nf[tid]; sb = s_sb[tid]; ent = s_entry[tid]; code = s_code[tid]; ex = s_exit[tid];
+                nf = s_nf[tid]; ent = s_entry[tid]; code = s_code[tid]; ex = s_exit[tid];
                 terminal = code != kWalkRun || start + ex >= v.len;
             }
             if (terminal) { s_stop_code = code; s_stop = start + ex; }
         }
         uint32_t tnf;
-        uint64_t tsb;
         const uint32_t pnf = block_exclusive_scan256<uint32_t>(nf, scan32, tnf);
-        const uint64_t psb = block_exclusive_scan256<uint64_t>(sb, scan64, tsb);
         if ((uint32_t)tid < np) {
             TcpChunkRes R;
-            R.entry = (nf || ent != kTcpNone) ? ent : kTcpNone;
+            R.entry = nf ? ent : kTcpNone;
             R.fbase = fb + pnf;
-            R.sbase = sbb + psb;
+            R.nframes = nf;
+            R.cand = cand;
             P.chunkres[c0 + tid] = R;
         }
         fb += tnf;
-        sbb += tsb;
         __syncthreads();
     }
     if (tid == 0) {
         TcpGroup& W = P.groups[g];
         W.nframes = fb;
-        W.slot_bytes = sbb;
         // a walk that ran off the end of the stream stops there: everything framed
         const uint32_t code = s_stop_code;
         W.code = (code == kWalkPartial && s_stop >= v.len) ? kWalkRun : code;
@@ -293,27 +314,18 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
 // ---- k_tcp_scan: one workgroup; sessions -> ingest segments ----
 __global__ __launch_bounds__(256) void k_tcp_scan(TcpParams P) {
     const int tid = threadIdx.x;
-    __shared__ uint64_t scan64[4];
     __shared__ uint32_t scan32[4];
     uint32_t fb = 0;
-    uint64_t sbb = 0;
     for (uint32_t g0 = 0; g0 < P.ngroups; g0 += 256) {
         const uint32_t g = g0 + tid;
         const bool ok = g < P.ngroups;
         const uint32_t nf = ok ? P.groups[g].nframes : 0u;
-        const uint64_t sb = ok ? P.groups[g].slot_bytes : 0ull;
         uint32_t tnf;
-        uint64_t tsb;
         const uint32_t pnf = block_exclusive_scan256<uint32_t>(nf, scan32, tnf);
-        const uint64_t psb = block_exclusive_scan256<uint64_t>(sb, scan64, tsb);
-        if (ok) {
-            P.groups[g].frame_base = fb + pnf;
-            P.groups[g].slot_base = sbb + psb;
-        }
+        if (ok) P.groups[g].frame_base = fb + pnf;
         fb += tnf;
-        sbb += tsb;
     }
-    const bool over = fb > P.max_desc || sbb > P.blob_cap;
+    const bool over = fb > P.max_desc;
     for (uint32_t g = tid; g < P.ngroups; g += 256) {
         P.seg_off[g] = over ? 0u : P.groups[g].frame_base;
         P.seg_sess[g] = P.groups[g].session;
@@ -321,51 +333,11 @@ __global__ __launch_bounds__(256) void k_tcp_scan(TcpParams P) {
     if (tid == 0) {
         P.seg_off[P.ngroups] = over ? 0u : fb;
         P.tot->frames = fb;
-        P.tot->slot_bytes = sbb;
         P.tot->status = over ? EDGPU_OUT_OVERFLOW : 0;
     }
 }
 
-// 16 stream bytes at `p` (< len) as one slot word; bytes at or past `lim` read 0.
-__device__ __forceinline__ u32x4 tcp_word(const TcpView& v, uint64_t p, uint64_t lim) {
-    if (p >= v.clen) {
-        // two aligned 16-B loads + byte funnel (the raw buffer is 16-B aligned)
-        const uint8_t* a = v.raw + (p - v.clen);
-        const uintptr_t al = (uintptr_t)a & ~(uintptr_t)15;
-        const uint32_t sh = (uint32_t)((uintptr_t)a & 15);
-        if (al + 32 <= (uintptr_t)v.raw_end) {
-            const u32x4 w0 = *reinterpret_cast<const u32x4*>(al);
-            const u32x4 w1 = sh ? *reinterpret_cast<const u32x4*>(al + 16) : w0;
-            const uint32_t d[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-            const uint32_t q = sh >> 2, r = sh & 3;
-            uint32_t o[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                // d[i + q], d[i + q + 1] without dynamic register indexing (q is wave-uniform)
-                uint32_t lo = d[i], hi = d[i + 1];
-                if (q == 1) { lo = d[i + 1]; hi = d[i + 2]; }
-                else if (q == 2) { lo = d[i + 2]; hi = d[i + 3]; }
-                else if (q == 3) { lo = d[i + 3]; hi = d[i + 4]; }
-                o[i] = r ? __builtin_amdgcn_alignbyte(hi, lo, r) : lo;
-            }
-            if (p + 16 > lim) {                                  // zero the slot padding
-                const uint32_t nb = (uint32_t)(lim - p);
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int keep = (int)nb - 4 * i;
-                    o[i] = keep >= 4 ? o[i] : keep <= 0 ? 0u : (o[i] & ((1u << (8 * keep)) - 1));
-                }
-            }
-            return u32x4{o[0], o[1], o[2], o[3]};
-        }
-    }
-    uint32_t o[4] = {0u, 0u, 0u, 0u};
-    for (int b = 0; b < 16; b++)
-        if (p + b < lim) o[b >> 2] |= tbyte(v, p + b) << (8 * (b & 3));
-    return u32x4{o[0], o[1], o[2], o[3]};
-}
-
-// ---- k_tcp_emit: one wave per chunk; frames -> slots + descriptors ----
+// ---- k_tcp_emit: one wave per chunk; frames -> descriptors + source addresses ----
 __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
     const uint32_t c = blockIdx.x;
     const int lane = threadIdx.x;
@@ -377,74 +349,72 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
     const TcpView v = tcp_view(P, G);
     const uint64_t start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
     const uint64_t end = min(start + kTcpChunk, v.len);
+    const TcpRead* rd = P.reads + G.first_read;
     __shared__ uint64_t s_pos[64];
-    __shared__ uint32_t s_flen[64];
     __shared__ uint32_t s_m;
     __shared__ uint64_t s_next;
+    __shared__ uint64_t s_stage;           // stream position of a frame to stage, ~0: none
+    if (lane == 0) s_stage = ~0ull;
+    const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
+    const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
+    uint32_t done = 0;
     uint64_t pos = start + R.entry;
-    uint32_t fidx = G.frame_base + R.fbase;
-    uint64_t soff = G.slot_base + R.sbase;
-    const TcpRead* rd = P.reads + G.first_read;
-    while (pos < end) {
-        if (lane == 0) {                                  // next up to 64 frames of the chain
-            uint32_t m = 0;
-            uint64_t p = pos;
-            while (m < 64 && p < end) {
-                uint32_t flen = 0;
-                if (tcp_step(v, p, flen) != kWalkRun) { p = ~0ull; break; }
-                s_pos[m] = p;
-                s_flen[m] = flen;
-                m++;
-                p += flen;
-            }
-            s_m = m;
-            s_next = p;
-        }
-        __syncthreads();
-        const uint32_t m = s_m;
-        // lane f: descriptor of frame f (arrival of the read holding its last byte)
-        uint64_t my_soff = 0;
-        {
-            const uint32_t sl = (uint32_t)lane < m ? ((s_flen[lane] + 15) & ~15u) : 0u;
-            uint64_t x = sl;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint64_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            my_soff = soff + x - sl;
-            if ((uint32_t)lane < m) {
-                const uint64_t p = s_pos[lane];
-                const uint32_t flen = s_flen[lane];
-                const uint64_t last = p + flen - 1;
-                int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (rd[mid].start <= last) lo = mid; else hi = mid - 1;
+    while (done < R.nframes) {
+        uint32_t m;
+        if (recorded) {
+            m = min(64u, R.nframes - done);
+        } else {                                          // re-walk: the next up to 64 frames
+            if (lane == 0) {
+                uint32_t mm = 0;
+                uint64_t p = pos;
+                while (mm < 64 && p < end) {
+                    uint32_t flen = 0;
+                    if (tcp_step(v, p, flen) != kWalkRun) break;
+                    s_pos[mm++] = p;
+                    p += flen;
                 }
-                edgpu_pkt_desc d;
-                d.slot = (uint32_t)(my_soff >> 4);
-                d.len = (uint16_t)(flen - 4);
-                d.channel = (uint8_t)tbyte(v, p + 1);
-                d.flags = 0;
-                d.arrival_ms = rd[lo].arrival;
-                P.desc[fidx + lane] = d;
-                atomicAdd(&P.results[G.first_read + lo].frames, 1u);
+                s_m = mm;
+                s_next = p;
             }
-            soff += __shfl(x, 63, 64);
+            __syncthreads();
+            m = s_m;
+            pos = s_next;
         }
-        // slot words: the frame as received ('$' ch BE16(len) + packet), zero padded
-        for (uint32_t f = 0; f < m; f++) {
-            const uint64_t p = s_pos[f];
-            const uint32_t flen = s_flen[f];
-            const uint64_t so = __shfl(my_soff, (int)f, 64);
-            u32x4* dst = reinterpret_cast<u32x4*>(P.blob + so);
-            const uint32_t nw = (flen + 15) >> 4;
-            for (uint32_t w = lane; w < nw; w += 64) dst[w] = tcp_word(v, p + 16 * w, p + flen);
+        if ((uint32_t)lane < m) {
+            const uint64_t p = recorded ? start + rec[done + lane] : s_pos[lane];
+            uint32_t flen = 0;
+            tcp_step(v, p, flen);
+            const uint64_t last = p + flen - 1;
+            int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rd[mid].start <= last) lo = mid; else hi = mid - 1;
+            }
+            const uint32_t fi = G.frame_base + R.fbase + done + lane;
+            edgpu_pkt_desc d;
+            d.slot = 0;
+            d.len = (uint16_t)(flen - 4);
+            d.channel = (uint8_t)tbyte(v, p + 1);
+            d.flags = 0;
+            d.arrival_ms = rd[lo].arrival;
+            P.desc[fi] = d;
+            const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
+            if (p < v.clen) s_stage = p;
+            P.src_addr[fi] = (uint64_t)(uintptr_t)a;
+            atomicAdd(&P.results[G.first_read + lo].frames, 1u);
         }
-        fidx += m;
-        pos = s_next;
+        done += m;
         __syncthreads();
+        if (m == 0) break;
+    }
+    // a frame that starts in the carried bytes: staged contiguously (the only one per session)
+    const uint64_t sp = s_stage;
+    if (sp != ~0ull) {
+        uint32_t flen = 0;
+        tcp_step(v, sp, flen);
+        uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
+        for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
+            dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
     }
 }
 
@@ -491,6 +461,11 @@ hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(256), 0, st, p);
     if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);
+    return hipGetLastError();
+}
+
+// After k_ingest has copied the frames out of the staged / carried bytes.
+hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st) {
     hipLaunchKernelGGL(k_tcp_finish, dim3(p.ngroups), dim3(256), 0, st, p);
     return hipGetLastError();
 }

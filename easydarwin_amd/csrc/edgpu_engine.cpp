@@ -28,6 +28,7 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
+hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
 int fanout_chunk(int variant);
 const char* fanout_name(int variant);
 }  // namespace edgpu
@@ -150,7 +151,9 @@ struct edgpu_ctx {
     DevVec<TcpRead> d_tcp_reads;
     DevVec<uint32_t> d_tcp_chunk_group, d_tcp_ncand;
     DevVec<TcpCand> d_tcp_cands;
-    DevVec<uint8_t> d_tcp_links;
+    DevVec<uint16_t> d_tcp_offs;
+    DevVec<uint8_t> d_tcp_links, d_tcp_stage;
+    uint64_t* d_tcp_src = nullptr;      // per frame source address (max_batch_packets)
     DevVec<TcpChunkRes> d_tcp_chunkres;
     DevVec<edgpu_tcp_result> d_tcp_results;
     TcpTotals* d_tcp_tot = nullptr;
@@ -253,7 +256,8 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_img_plan.release(); x->d_sub_out_buf2.release();
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
-    x->d_tcp_results.release();
+    x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release();
+    if (x->d_tcp_src) (void)hipFree(x->d_tcp_src);
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
     if (x->d_img_status) (void)hipFree(x->d_img_status);
@@ -551,13 +555,13 @@ static int rebuild_index(edgpu_ctx* x) {
 }
 
 // Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
-// edgpu_keyframe_index.  `before` (optional) is enqueued between the timing events, so the
-// ingest time of edgpu_ingest_interleaved includes its deframe kernels.
+// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first
+// and k_tcp_finish after, all inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
-                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, hipError_t (*before)(edgpu_ctx*, void*),
-                          void* arg = nullptr) {
+                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr) {
     IngestParams p;
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
+    p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode;
@@ -568,8 +572,9 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
     HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
     HIP_CHECK(hist_mark(x, 2, 0));
-    if (before) HIP_CHECK(before(x, arg));
+    if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
+    if (tcp) HIP_CHECK(launch_deframe_finish(*tcp, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
     x->timed_ingest = true;
@@ -610,7 +615,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
     }
-    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode, nullptr);
+    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode);
 }
 
 int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t n, const uint8_t* bytes,
@@ -667,8 +672,11 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(x->d_tcp_chunkres.reserve(std::max<uint32_t>(nc, 1), x->stream));
     HIP_CHECK(x->d_tcp_cands.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
     HIP_CHECK(x->d_tcp_links.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
+    HIP_CHECK(x->d_tcp_offs.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands * kTcpFrames, x->stream));
+    HIP_CHECK(x->d_tcp_stage.reserve((size_t)ng * kTcpCarry, x->stream));
     if (!x->d_tcp_tot && hipMalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
-    if (!x->d_blob && hipMalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "blob staging");
+    if (!x->d_tcp_src && hipMalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
+        return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
     const uint8_t* raw = bytes;
     if (where == EDGPU_PTR_HOST) {
         if (!x->d_tcp_raw && hipMalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
@@ -687,12 +695,11 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.chunkres = x->d_tcp_chunkres.ptr;
     p.raw = raw; p.raw_bytes = nbytes;
     p.carry = x->d_carry.ptr;
-    p.blob = x->d_blob; p.blob_cap = x->cfg.max_batch_bytes;
-    p.desc = x->d_desc; p.max_desc = x->cfg.max_batch_packets;
+    p.offs = x->d_tcp_offs.ptr; p.stage = x->d_tcp_stage.ptr;
+    p.desc = x->d_desc; p.src_addr = x->d_tcp_src; p.max_desc = x->cfg.max_batch_packets;
     p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
-    struct Launch { static hipError_t go(edgpu_ctx* c, void* a) { return launch_deframe(*static_cast<const TcpParams*>(a), c->stream); } };
-    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, x->d_blob, 0, &Launch::go, &p);
+    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p);
     if (r) return r;
     TcpTotals tot;
     HIP_CHECK(hipMemcpyAsync(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result), hipMemcpyDeviceToHost, x->stream));
@@ -700,7 +707,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(hipStreamSynchronize(x->stream));
     if (tot.status) {
         x->pending = false;                 // the ingest ran over empty segments
-        return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets / max_batch_bytes");
+        return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets");
     }
     for (const TcpGroup& G : groups) x->carry_len[G.session] = results[G.first_read + G.nreads - 1].carry;
     return EDGPU_OK;

@@ -23,6 +23,7 @@
 #include "edgpu.h"
 #include "edgpu_device.h"
 #include "edgpu_params.h"
+#include "edgpu_bytes.h"
 
 namespace edgpu {
 
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __shared__ uint16_t p_len[kIngestThreads];
     __shared__ uint32_t p_ssrc[kIngestThreads];
     __shared__ int64_t p_ts[kIngestThreads];
-    __shared__ uint32_t p_src[kIngestThreads];
+    __shared__ uint64_t p_src[kIngestThreads];     // slot / frame start address
     __shared__ uint32_t p_slotb[kIngestThreads];
     __shared__ uint64_t p_vb[kIngestThreads];
     __shared__ uint64_t scan64[4];
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         const bool valid = (uint32_t)tid < n;
         if (tid < (int)nsnd) c_last[tid] = -1;
         uint32_t len = 0, track = 0, ls = 0, fl = 0, slot = 0;
+        uint64_t src = 0;
         int64_t arrival = 0;
         bool acc = false;
         const uint8_t* pk = nullptr;
@@ -168,12 +170,22 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             arrival = d.arrival_ms;
             slot = d.slot;
             acc = track < S.ntracks && len > 0;       // ProcessRTPData: inIndex < numStreams
-            pk = P.blob + (uint64_t)slot * 16 + 4;
+            const uint8_t* sp = P.src_addr ? reinterpret_cast<const uint8_t*>(P.src_addr[i])
+                                           : P.blob + (uint64_t)slot * 16;
+            src = (uint64_t)(uintptr_t)sp;
+            pk = sp + 4;
             // the slot's first 32 bytes (packet bytes 0..27) in two 16-B loads: every header
             // field the reflector reads for a CSRC-free packet comes from these registers
-            const u32x4* sw = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)slot * 16);
-            const u32x4 w0 = len > 0 ? sw[0] : u32x4{0u, 0u, 0u, 0u};
-            const u32x4 w1 = len > 12 ? sw[1] : u32x4{0u, 0u, 0u, 0u};
+            u32x4 w0 = u32x4{0u, 0u, 0u, 0u}, w1 = w0;
+            if (P.src_addr) {                              // a frame inside the TCP byte stream
+                const uint8_t* lim = sp + 4 + len;
+                if (len > 0) w0 = load16_unaligned(sp, lim);
+                if (len > 12) w1 = load16_unaligned(sp + 16, lim);
+            } else {
+                const u32x4* sw = reinterpret_cast<const u32x4*>(sp);
+                if (len > 0) w0 = sw[0];
+                if (len > 12) w1 = sw[1];
+            }
             hdr[0] = w0.y; hdr[1] = w0.z; hdr[2] = w0.w; hdr[3] = w1.x;
             hdr[4] = w1.y; hdr[5] = w1.z; hdr[6] = w1.w;
             if (acc) fl = s_flags[ls];
@@ -186,7 +198,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         p_snd[tid] = (uint8_t)ls;
         p_acc[tid] = acc;
         p_len[tid] = (uint16_t)len;
-        p_src[tid] = slot;
+        p_src[tid] = src;
         p_ssrc[tid] = !acc ? 0u : (len < 8 ? 0u : (fl & kSndRtcpPort) ? hbe32(hdr, 4) : (len < 12 ? 0u : hbe32(hdr, 8)));
         p_ts[tid] = arrival / 1000;          // OS::Milliseconds() / 1000, truncating
         // ---- SSRC latch filter (sequential per socket; fast path when nothing changes) ----
@@ -271,14 +283,24 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
                 const uint32_t sb = p_slotb[p];
                 if (sb == 0) continue;
                 const uint32_t s = p_snd[p];
-                const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)p_src[p] * 16);
+                const uint8_t* sp = reinterpret_cast<const uint8_t*>(p_src[p]);
+                const u32x4* src = reinterpret_cast<const u32x4*>(sp);
                 u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
                 const uint64_t w0 = p_vb[p] >> 4;
                 const uint32_t wm = s_wmask[s];
-                for (uint32_t w = lane; w < sb / 16; w += 64) {
-                    u32x4 v = src[w];
-                    if (w == 0) v.x = slot_header(p_len[p]);
-                    ring[(w0 + w) & wm] = v;
+                if (P.src_addr) {
+                    const uint8_t* lim = sp + 4 + p_len[p];
+                    for (uint32_t w = lane; w < sb / 16; w += 64) {
+                        u32x4 v = load16_unaligned(sp + 16 * w, lim);
+                        if (w == 0) v.x = slot_header(p_len[p]);
+                        ring[(w0 + w) & wm] = v;
+                    }
+                } else {
+                    for (uint32_t w = lane; w < sb / 16; w += 64) {
+                        u32x4 v = src[w];
+                        if (w == 0) v.x = slot_header(p_len[p]);
+                        ring[(w0 + w) & wm] = v;
+                    }
                 }
             }
         } else if (valid) {

@@ -11,6 +11,8 @@ struct IngestParams {
     const uint32_t* seg_off;
     const uint32_t* seg_sess;
     const uint8_t* blob;
+    const uint64_t* src_addr;   // per desc: device address of the frame ('$' header first, any
+                                // alignment) instead of blob + slot * 16 (interleaved ingest); or null
     SessionDev* sessions;
     SenderDev* senders;
     StreamDev* streams;
@@ -74,8 +76,9 @@ struct FanoutParams {
 // then stitched chunk to chunk (k_tcp_resolve).
 constexpr uint32_t kTcpChunk = 16384;      // stream bytes per walk chunk
 constexpr uint32_t kTcpCands = 64;         // candidates kept per chunk (more: sequential walk)
+constexpr uint32_t kTcpFrames = 32;        // frame starts recorded per candidate walk
 constexpr uint32_t kTcpMaxFrame = 2047;    // usable request-buffer bytes (QTSS_MAX_REQUEST_BUFFER_SIZE - 1)
-constexpr uint32_t kTcpCarry = 2048;       // per-session carry buffer
+constexpr uint32_t kTcpCarry = 2048;       // per-session carry buffer / staged frame
 constexpr uint32_t kTcpNone = 0xFFFFFFFFu;
 
 // walk outcome codes (TcpCand.code, TcpGroup.code)
@@ -91,17 +94,15 @@ struct TcpGroup {           // one pusher connection's reads in this call
     uint64_t len;           // stream bytes: carry_len + the reads' bytes
     // k_tcp_resolve
     uint32_t nframes, code;
-    uint64_t slot_bytes;
     uint64_t stop;          // stream position where the walk ended (len: everything framed)
     // k_tcp_scan
     uint32_t frame_base, _pad;
-    uint64_t slot_base;
 };
 
 struct TcpRead { uint64_t start; int64_t arrival; uint32_t len, _pad; };   // start: stream position
-struct TcpCand { uint32_t q, exit, nframes, code; uint64_t sbytes; };      // q / exit: chunk offsets
-struct TcpChunkRes { uint32_t entry, fbase; uint64_t sbase; };            // entry kTcpNone: idle chunk
-struct TcpTotals { uint32_t frames; int32_t status; uint64_t slot_bytes; };
+struct TcpCand { uint32_t q, exit, nframes, code; };                        // q / exit: chunk offsets
+struct TcpChunkRes { uint32_t entry, fbase, nframes, cand; };   // entry kTcpNone: idle; cand kTcpNone: re-walk
+struct TcpTotals { uint32_t frames; int32_t status; };
 
 struct TcpParams {
     TcpGroup* groups;
@@ -109,15 +110,16 @@ struct TcpParams {
     const TcpRead* reads;
     const uint32_t* chunk_group;
     TcpCand* cands;         // nchunks x kTcpCands
+    uint16_t* offs;         // nchunks x kTcpCands x kTcpFrames: frame starts of each candidate walk
     uint8_t* links;         // nchunks x kTcpCands: next chunk's candidate, 0xFE terminal, 0xFF search
     uint32_t* ncand;
     TcpChunkRes* chunkres;
     const uint8_t* raw;
     uint64_t raw_bytes;
     uint8_t* carry;         // per session kTcpCarry bytes
-    uint8_t* blob;          // frame slots for k_ingest
-    uint64_t blob_cap;
+    uint8_t* stage;         // per group kTcpCarry bytes: a frame that starts in the carried bytes
     edgpu_pkt_desc* desc;
+    uint64_t* src_addr;     // per frame: its address for k_ingest (IngestParams.src_addr)
     uint32_t max_desc;
     uint32_t* seg_off;      // ngroups + 1
     uint32_t* seg_sess;

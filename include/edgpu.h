@@ -232,8 +232,9 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
  *                      socket for 0 bytes and treats the connection as closed (Socket.cpp:
  *                      383-388); set on the read that fills the buffer and later reads.
  * `carry` is the session's carried byte count after the call.  Returns EDGPU_OUT_OVERFLOW
- * (nothing ingested, no carry changed) when the frames exceed max_batch_packets or their
- * 16-B slots max_batch_bytes.  Syncs (the results are read back). */
+ * (nothing ingested, no carry changed) when the frames exceed max_batch_packets.  Host reads
+ * are staged in a max_batch_bytes buffer; device reads are read in place (the frames are
+ * copied from them into the sender rings).  Syncs (the results are read back). */
 #define EDGPU_TCP_MESSAGE  1
 #define EDGPU_TCP_DROPPED  2
 typedef struct edgpu_tcp_read {
