@@ -166,6 +166,13 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint16_t first_seq;             // qtssRTPStrFirstSeqNumber (0 unless RTP-Info)
     uint8_t  rtp_info;              // filter armed
     uint8_t  sent_any;              // this sub-stream has written a packet (its packet count > 0)
+    // egress backpressure (edgpu_fanout_blocked): the state before this tick's commit, and
+    // whether the bookmarked packet is still to be sent (the next tick starts AT it)
+    uint64_t prev_last_id;
+    uint8_t  prev_has_last;
+    uint8_t  prev_sent_any;
+    uint8_t  resume_at;
+    uint8_t  _pad1[5];
 };
 
 // RTP-Info PLAY query for one track (ReflectorSession HaveStreamBuffers,

@@ -22,6 +22,7 @@
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
                                     uint32_t n, hipStream_t st);
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
@@ -102,6 +103,7 @@ struct edgpu_ctx {
     hipEvent_t hist[4][kHist][2] = {};
     uint32_t hist_n[4] = {0, 0, 0, 0};
     uint64_t fanout_launches = 0;
+    int64_t last_now = 0;               // clock of the last edgpu_fanout (backpressure reports)
     bool timed_fanout = false, timed_ingest = false, timed_keyframe = false;
 
     std::vector<SessionHost> sessions;
@@ -713,6 +715,30 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     return EDGPU_OK;
 }
 
+int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n) {
+    if (!x || (n && !reports)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!n) return EDGPU_OK;
+    if (x->fanout_launches == 0) return fail(EDGPU_ERR, "no fan-out tick to report on");
+    if (x->pending) return fail(EDGPU_ERR, "backpressure reports must precede the next edgpu_ingest");
+    const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    for (uint32_t i = 0; i < n; i++)
+        if (reports[i].substream >= nsub) return fail(EDGPU_BAD_ARGUMENT, "bad sub-stream index");
+    HIP_CHECK(hipSetDevice(x->device));
+    edgpu_blocked* d = nullptr;
+    HIP_CHECK(hipMallocAsync((void**)&d, n * sizeof(edgpu_blocked), x->stream));
+    HIP_CHECK(hipMemcpyAsync(d, reports, n * sizeof(edgpu_blocked), hipMemcpyHostToDevice, x->stream));
+    BlockedParams p;
+    p.reports = d; p.n = n;
+    p.subs = x->d_subs.ptr; p.senders = x->d_senders.ptr; p.sessions = x->d_sessions.ptr;
+    p.now = x->last_now;
+    p.relocate_ms = x->cfg.rtp_reflector_threshold_msec;
+    p.totals = x->d_totals;
+    HIP_CHECK(launch_blocked(p, x->stream));
+    HIP_CHECK(hipFreeAsync(d, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));   // `reports` is the caller's host memory
+    return EDGPU_OK;
+}
+
 int edgpu_keyframe_index(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!x->pending) return fail(EDGPU_ERR, "no ingested batch pending a keyframe index");
@@ -743,6 +769,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     }
     if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    x->last_now = now_ms;
     edgpu_substream_out* sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
     uint8_t* arena = x->d_arena_buf[x->cur];
     edgpu_out_desc* odesc = x->d_out_desc_buf[x->cur];

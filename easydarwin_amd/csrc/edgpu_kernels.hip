@@ -488,8 +488,12 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
             const uint64_t head = D.head;
             bool have = false;
             uint64_t a = 0;
+            Q.prev_last_id = Q.last_id;                 // for edgpu_fanout_blocked
+            Q.prev_has_last = Q.has_last;
+            Q.prev_sent_any = Q.sent_any;
             if (Q.bookmark >= 0) {                     // GetBookMarkedPacket: resume after it
-                a = (uint64_t)Q.bookmark + 1;
+                // (AT it when a blocked write left it unsent, or after a Q9 relocation)
+                a = (uint64_t)Q.bookmark + (Q.resume_at ? 0u : 1u);
                 // SendPacketsToOutput restarts AT the bookmarked packet (ReflectorStream.cpp:
                 // 1138-1198); it went out or was empty at its first visit, so it is skipped --
                 // unless the RTP-Info first-seq filter held it back and has just been lifted
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
                 }
                 // SendPacketsToOutput returns the newest visited packet; with sinks that never
                 // block NeedRelocateBookMark (Q9) cannot fire: the bookmark is the newest packet.
-                if (head > 0) Q.bookmark = (int64_t)(head - 1);
+                if (head > 0) { Q.bookmark = (int64_t)(head - 1); Q.resume_at = 0; }
                 if (count > 0) {
                     Q.last_id = meta[(uint64_t)D.last_nonzero & D.pk_mask].id;
                     Q.has_last = 1;
@@ -681,6 +685,55 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             m = mn;
         }
     }
+}
+
+// Egress backpressure (edgpu_fanout_blocked): one lane per report.  The sub-stream's tick
+// wrote the non-empty packets of [a, head) in order; the socket took the first `sent`.
+// SendPacketsToOutput stopped at the next one (ReflectorStream.cpp:1138-1198): it becomes the
+// bookmark, relocated to the key frame when too old (NeedRelocateBookMark, :1293-1322, Q9);
+// the stream's last-sent id is the last packet written (RTPSessionOutput.cpp:620-639).
+__global__ void k_blocked(BlockedParams P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const edgpu_blocked b = P.reports[i];
+    SubDev& Q = P.subs[b.substream];
+    if (!Q.nonempty || b.sent >= Q.count) return;
+    const SenderDev& D = P.senders[Q.sender];
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint64_t head = D.head;
+    // vcount = non-empty packets before a packet: the k-th written packet is the first whose
+    // inclusive count exceeds vcstart + k
+    auto kth = [&](uint32_t k) {
+        return lower_bound_meta(meta, D.pk_mask, Q.a, head, [&](const PktMeta& m) {
+            return m.vcount + (m.len != 0 ? 1u : 0u) > Q.vcstart + k; });
+    };
+    const uint64_t x = kth(b.sent);
+    if (b.sent > 0) {
+        Q.last_id = meta[kth(b.sent - 1) & D.pk_mask].id;
+        Q.has_last = 1;
+    } else {
+        Q.last_id = Q.prev_last_id;
+        Q.has_last = Q.prev_has_last;
+        Q.sent_any = Q.prev_sent_any;
+    }
+    uint64_t unsent_bytes = 0;
+    for (uint64_t k = x; k < head; k++) {
+        const uint32_t len = meta[k & D.pk_mask].len;
+        if (len) unsent_bytes += len + (Q.transport ? 4u : 0u);
+    }
+    const unsigned long long np = Q.count - b.sent;
+    atomicAdd(&P.totals->relayed_packets, 0ull - np);
+    atomicAdd(&P.totals->cum_relayed_packets, 0ull - np);
+    atomicAdd(&P.totals->relayed_bytes, 0ull - unsent_bytes);
+    atomicAdd(&P.totals->cum_relayed_bytes, 0ull - unsent_bytes);
+    int64_t bm = (int64_t)x;
+    const PktMeta mx = meta[x & D.pk_mask];
+    if (P.now - mx.arrival > P.relocate_ms && D.key >= 0 && meta[(uint64_t)D.key & D.pk_mask].arrival > mx.arrival) {
+        bm = D.key;
+        atomicExch(&P.sessions[D.session].video_key_flag, 1u);
+    }
+    Q.bookmark = bm;
+    Q.resume_at = 1;
 }
 
 // =========================================================================================
@@ -1448,6 +1501,11 @@ hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r,
     hipLaunchKernelGGL(k_first_packet_info, dim3((n + 63) / 64), dim3(64), 0, st, q, r, senders, n);
     return hipGetLastError();
 }
+hipError_t launch_blocked(const BlockedParams& p, hipStream_t st) {
+    if (p.n) hipLaunchKernelGGL(k_blocked, dim3((p.n + 63) / 64), dim3(64), 0, st, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     hipLaunchKernelGGL(k_keyframe, dim3(nseg), dim3(64), 0, st, p);

@@ -127,6 +127,17 @@ struct TcpParams {
     TcpTotals* tot;
 };
 
+struct BlockedParams {
+    const edgpu_blocked* reports;
+    uint32_t n;
+    SubDev* subs;
+    const SenderDev* senders;
+    SessionDev* sessions;
+    int64_t now;                // the tick's clock
+    int64_t relocate_ms;        // sRelocatePacketAgeMSec (rtp_reflector_threshold_msec)
+    TickTotals* totals;
+};
+
 struct ImageParams {
     SenderDev* senders;
     SessionDev* sessions;

@@ -29,7 +29,7 @@ EXPORTED = [
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
-    "edgpu_subscribers_add", "edgpu_ingest_interleaved",
+    "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -155,6 +155,7 @@ def load(path: str = LIB_PATH):
         "edgpu_subscriber_play": (I32, [P, U32, I32, U32, I64, C.POINTER(U32), P]),
         "edgpu_subscribers_add": (I32, [P, U32, P, P, P]),
         "edgpu_ingest_interleaved": (I32, [P, P, U32, P, U64, I32, P]),
+        "edgpu_fanout_blocked": (I32, [P, P, U32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -268,6 +269,12 @@ class Context:
             _check(self.lib.edgpu_ingest_interleaved(self.h, _ptr(reads), len(reads), C.c_void_p(device_ptr),
                                                      int(data), PTR_DEVICE, _ptr(out)))
         return out
+
+    def fanout_blocked(self, reports):
+        """Egress backpressure for the last tick: [(substream index, packets sent)]."""
+        a = np.ascontiguousarray(np.array(list(reports), dtype=np.uint32).reshape(-1, 2))
+        if len(a):
+            _check(self.lib.edgpu_fanout_blocked(self.h, _ptr(a), len(a)))
 
     def keyframe_index(self):
         _check(self.lib.edgpu_keyframe_index(self.h))

@@ -22,15 +22,24 @@ import struct
 import numpy as np
 
 from . import edgpu
-from .trace import JOIN, PKT, TICK, Trace
+from .trace import BLOCK, JOIN, PKT, TICK, Trace
 
 
-def _wire_images(subs, desc, arena, images):
-    for s in subs:
+def _wire_images(subs, desc, arena, images, budgets=None):
+    """Appends each sub-stream's packets of the tick to its wire image.  `budgets` maps
+    (handle, track, kind) -> the writes its socket accepted this tick (BLOCK events); the
+    rest would have blocked.  Returns the edgpu_fanout_blocked reports."""
+    reports = []
+    for q, s in enumerate(subs):
         n = int(s["desc_count"])
         if n == 0:
             continue
         key = (int(s["subscriber"]), int(s["track"]), int(s["kind"]))
+        if budgets and key in budgets and budgets[key] < n:
+            n = budgets[key]
+            reports.append((q, n))
+            if n == 0:
+                continue
         d = desc[int(s["desc_base"]):int(s["desc_base"]) + n]
         tcp = int(s["transport"]) == edgpu.TRANSPORT_TCP
         parts = images[key]
@@ -39,6 +48,7 @@ def _wire_images(subs, desc, arena, images):
                 parts.append(arena[off:off + ln].tobytes())
             else:
                 parts.append(struct.pack(">H", ln) + arena[off:off + ln].tobytes())
+    return reports
 
 
 RTSP_KEEPALIVE = (b"SET_PARAMETER rtsp://127.0.0.1/live/replay RTSP/1.0\r\nCSeq: 7\r\n"
@@ -178,10 +188,13 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         def drain():
             nonlocal unread
             if unread is not None:
-                c, r, tt = unread
+                c, r, tt, budgets = unread
                 st, subs, desc, arena = c.read_tick(r)
+                reports = _wire_images(subs, desc, arena, images, budgets)
+                if reports:
+                    c.fanout_blocked(reports)
+                    st = c.stats()
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
-                _wire_images(subs, desc, arena, images)
                 unread = None
 
         clock = 0                           # the harness's virtual clock: max event time so far
@@ -200,7 +213,13 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 nflush += 1
                 pending = []
 
+        blocks = {}                         # (sub_id, track, kind) -> budget for the next TICK
+        if lag and any(ev[0] == BLOCK for ev in trace.events):
+            raise ValueError("backpressure reports need each tick read before the next ingest")
         for ev in trace.events:
+            if ev[0] == BLOCK:
+                blocks[(ev[2], ev[3], ev[4])] = ev[5]
+                continue
             clock = max(clock, ev[1])
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
@@ -237,7 +256,13 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 if rep is not None:
                     ctx.fanout(t)                      # the owner ticks too (no subscribers here)
                 drain()                              # the previous tick, after this batch's ingest
-                unread = (out, out.fanout(t), t)
+                by_handle = {}
+                for (sub_id, trk, kind), b in blocks.items():
+                    for h, meta in subs_meta.items():
+                        if meta[0] == sub_id:
+                            by_handle[(h, trk, kind)] = b
+                blocks = {}
+                unread = (out, out.fanout(t), t, by_handle)
                 if not lag:
                     drain()
         drain()

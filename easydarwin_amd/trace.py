@@ -9,7 +9,10 @@ list.  It mirrors the reference's entry points:
 * ``JOIN`` -> SETUP+PLAY of one subscriber on every track of a session
   (QTSSReflectorModule.cpp:1610-1622, 1942-1946);
 * ``TICK`` -> ``ReflectorSender::ReflectPackets`` on every sender
-  (ReflectorStream.cpp:1709-1714).
+  (ReflectorStream.cpp:1709-1714);
+* ``BLOCK`` -> during the next TICK, one subscriber sub-stream's socket accepts ``budget``
+  more writes and then returns QTSS_WouldBlock (EAGAIN) for the rest of that tick
+  (egress backpressure: SendPacketsToOutput's blocked branch, ReflectorStream.cpp:1158-1190).
 
 Every event carries the virtual clock value (ms) that ``OS::Milliseconds`` returns while it
 is applied.  The GPU engine's batch boundary is the TICK: all PKTs since the previous TICK
@@ -22,6 +25,7 @@ Binary layout (little endian)::
     event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
              | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
              | u8 3 i64 t                                                    (TICK)
+             | u8 4 i64 t u32 sub_id u16 track u8 kind u32 budget           (BLOCK)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
 
@@ -35,7 +39,7 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK = 1, 2, 3
+PKT, JOIN, TICK, BLOCK = 1, 2, 3, 4
 UDP, TCP = 0, 1
 
 
@@ -57,12 +61,15 @@ class Trace:
     def tick(self, t: int):
         self.events.append((TICK, int(t)))
 
+    def block(self, t: int, sub_id: int, track: int, kind: int, budget: int):
+        self.events.append((BLOCK, int(t), sub_id, track, kind, budget))
+
     # -- serialisation ------------------------------------------------------------------
     def to_bytes(self) -> bytes:
         # PKT and TICK times drive the virtual clock and must not go back; a JOIN's time is
         # informational (the join takes effect at the next TICK, like a new output being
         # picked up by the next ReflectPackets).
-        times = [ev[1] for ev in self.events if ev[0] != JOIN]
+        times = [ev[1] for ev in self.events if ev[0] not in (JOIN, BLOCK)]
         assert all(a <= b for a, b in zip(times, times[1:])), "trace events must be time-ordered"
         out = [b"EDTR", struct.pack("<II", 1, len(self.sdps))]
         for s in self.sdps:
@@ -77,6 +84,9 @@ class Trace:
             elif ev[0] == JOIN:
                 _, t, s, sub, tr, ua = ev
                 out.append(struct.pack("<BqIIBB", JOIN, t, s, sub, tr, ua))
+            elif ev[0] == BLOCK:
+                _, t, sub, trk, kind, budget = ev
+                out.append(struct.pack("<BqIHBI", BLOCK, t, sub, trk, kind, budget))
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -115,6 +125,10 @@ class Trace:
                 _, t = struct.unpack_from("<Bq", buf, p)
                 p += 9
                 tr.events.append((TICK, t))
+            elif typ == BLOCK:
+                _, t, sub, trk, kind, budget = struct.unpack_from("<BqIHBI", buf, p)
+                p += 20
+                tr.events.append((BLOCK, t, sub, trk, kind, budget))
             else:
                 raise ValueError(f"bad event {typ} at {p}")
         return tr

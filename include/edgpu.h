@@ -256,6 +256,24 @@ int  edgpu_ingest_interleaved(edgpu_ctx* ctx, const edgpu_tcp_read* reads, uint3
 int  edgpu_keyframe_index(edgpu_ctx* ctx);
 int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
 
+/* Egress backpressure.  The host writes a tick's sub-streams to their sockets; when a socket
+ * stops accepting (EAGAIN -> QTSS_WouldBlock, RTPStream::Write -> RTPSessionOutput::
+ * WritePacket, RTPSessionOutput.cpp:600-615) after `sent` of the sub-stream's desc_count
+ * packets, report it here, after edgpu_fanout and before the next edgpu_ingest.  The engine
+ * then keeps the state ReflectorSender::SendPacketsToOutput leaves for a blocked output
+ * (ReflectorStream.cpp:1138-1198): the bookmark is the blocked packet -- moved to the key
+ * frame when it is older than rtp_reflector_threshold_msec and the key frame is newer
+ * (NeedRelocateBookMark, :1293-1322, Q9; the session's video-key flag is set, so the next
+ * audio packet becomes the audio anchor) -- the last-sent packet id is the last packet
+ * written, and the next edgpu_fanout resumes at the bookmark.  The tick's relayed counters
+ * drop the unsent packets.  `substream` indexes the tick's edgpu_substream_out table.
+ * Reports with sent >= desc_count are no-ops. */
+typedef struct edgpu_blocked {
+    uint32_t substream;
+    uint32_t sent;
+} edgpu_blocked;
+int  edgpu_fanout_blocked(edgpu_ctx* ctx, const edgpu_blocked* reports, uint32_t n);
+
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
 
 /* Name of the fan-out copy kernel this context launches (for measurement reports). */

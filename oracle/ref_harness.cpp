@@ -17,7 +17,10 @@
 //   * PKT events call ReflectorStream::PushPacket (as ProcessRTPData does,
 //     QTSSReflectorModule.cpp:604-678: track = channel/2, RTCP = channel&1);
 //   * TICK events call ReflectPackets on every sender (RTP then RTCP, track order), as
-//     ReflectorSocket::Run does (ReflectorStream.cpp:1709-1714).
+//     ReflectorSocket::Run does (ReflectorStream.cpp:1709-1714);
+//   * BLOCK events give one sub-stream's socket a write budget for the next TICK: after
+//     `budget` accepted writes QTSS_Write returns QTSS_WouldBlock (EAGAIN, RTPStream.cpp:
+//     1145-1147) until the TICK ends -- the blocked-client path of SendPacketsToOutput.
 //
 // Usage: ref_harness <trace.edtr> <capture.edcp>
 // Trace / capture formats: see easydarwin_amd/trace.py (shared with the port oracle and
@@ -68,6 +71,7 @@ struct FakeObj {
     UInt32 rtp_channel = 0, rtcp_channel = 1;
     std::string cap[2];          // [0] RTP writes, [1] RTCP writes (wire image)
     UInt64 npk[2] = {0, 0};
+    SInt64 budget[2] = {-1, -1}; // writes the socket accepts this tick (-1: unlimited)
 };
 static std::vector<std::unique_ptr<FakeObj>> g_objs;
 static FakeObj* new_obj() { g_objs.emplace_back(new FakeObj()); return g_objs.back().get(); }
@@ -134,12 +138,15 @@ static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf
 }
 // QTSS_Write(stream, QTSS_PacketStruct*, len, outLen, flags): RTPStream::Write's framing
 // (RTPStream.cpp:1098-1145) -- UDP datagram, or '$' ch BE16(len) + packet on the RTP or
-// RTCP channel (RTSPSessionInterface.cpp:329-344).  Sinks never block (Q20).
+// RTCP channel (RTSPSessionInterface.cpp:329-344).  A sink blocks only when a BLOCK event
+// set its budget for this tick.
 static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* outLen, UInt32 flags, ...) {
     FakeObj* s = (FakeObj*)stream;
     const QTSS_PacketStruct* pkt = (const QTSS_PacketStruct*)buf;
     int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (len == 0) return QTSS_NoErr;
+    if (s->budget[k] == 0) return QTSS_WouldBlock;
+    if (s->budget[k] > 0) s->budget[k]--;
     std::string& c = s->cap[k];
     if (s->transport == qtssRTPTransportTypeTCP) {
         c.push_back('$');
@@ -327,6 +334,14 @@ int main(int argc, char** argv) {
                     st->GetRTCPSender()->ReflectPackets(&wake, freeA);
                 }
             }
+            for (auto& o : g_objs) o->budget[0] = o->budget[1] = -1;
+        } else if (type == 4) {     // BLOCK
+            UInt32 sub_id = r.get<UInt32>();
+            UInt16 track = r.get<UInt16>();
+            UInt8 kind = r.get<UInt8>();
+            UInt32 budget = r.get<UInt32>();
+            for (auto& sb : subs)
+                if (sb.id == sub_id && track < sb.streams.size()) sb.streams[track]->budget[kind & 1] = budget;
         } else {
             fprintf(stderr, "bad event type %u at %zu\n", type, r.p);
             return 3;

@@ -31,7 +31,7 @@
 //
 // Out of parity scope (documented in DESIGN.md): bytes read past the packet length by the
 // key detector when 12+4*CC >= len (the reference reads stale buffer memory there; this model
-// reads 0), Q17 (recycled bookmarks after >10 s lag), Q20 (TCP audio thinning), blocking sinks.
+// reads 0), Q17 (recycled bookmarks after >10 s lag), Q20 (TCP audio thinning).
 //
 // Usage:  relay_model <trace.edtr> <capture.edcp>
 //         relay_model --bench <trace.edtr> <threads> [repeat]   (memcpy sinks, prints JSON)
@@ -151,6 +151,7 @@ struct SubStreamState {             // one client RTP stream object (per track)
     uint16_t first_seq = 0;         // qtssRTPStrFirstSeqNumber (0 unless RTP-Info)
     std::string cap[2];             // wire images
     uint64_t npk[2] = {0, 0};
+    int64_t budget[2] = {-1, -1};   // socket writes accepted this tick (-1: never blocks)
 };
 
 struct Output {
@@ -288,14 +289,17 @@ struct Model {
     }
 
     // ---- fan-out ------------------------------------------------------------------------
-    void write_packet(Output& o, int track, int kind, const Packet& p) {
-        if (p.len == 0) return;                                   // SSRC-rejected survivor
+    // false: the socket would block (QTSS_WouldBlock) -- SendPacketsToOutput stops here
+    bool write_packet(Output& o, int track, int kind, const Packet& p) {
+        if (p.len == 0) return true;                              // SSRC-rejected survivor
         SubStreamState& s = o.ss[track];
         if (kind == 0 && s.packet_count == 0) {                   // FilterPacket (Q10)
             uint16_t seq = p.len >= 4 ? be16(&p.data[2]) : 0;
-            if (seq < s.first_seq) return;
+            if (seq < s.first_seq) return true;
         }
-        if (s.has_last[kind] && p.id <= s.last_id[kind]) return;  // PacketAlreadySent (Q8)
+        if (s.has_last[kind] && p.id <= s.last_id[kind]) return true;  // PacketAlreadySent (Q8)
+        if (s.budget[kind] == 0) return false;                    // EAGAIN: nothing written
+        if (s.budget[kind] > 0) s.budget[kind]--;
         if (o.capture) {
             std::string& c = s.cap[kind];
             if (o.tcp) { c.push_back('$'); c.push_back((char)(2 * track + kind)); }
@@ -316,6 +320,7 @@ struct Model {
         s.has_last[kind] = true;
         s.last_id[kind] = p.id;
         s.packet_count++;
+        return true;
     }
 
     PacketRef buffer_start(Sender& snd, bool& found) {
@@ -346,9 +351,9 @@ struct Model {
             PacketRef last = start;
             for (PacketRef it = start; it != snd.q.end(); ++it) {
                 last = it;
-                write_packet(o, track, kind, *it);
+                if (!write_packet(o, track, kind, *it)) break;   // blocked: retry from here
             }
-            // NeedRelocateBookMark (Q9): only fires for a lagging bookmark.
+            // NeedRelocateBookMark (Q9): fires for a lagging bookmark (a blocked output).
             if (now - last->arrival > prefs.relocate_age_ms && snd.has_key &&
                 snd.key->arrival > last->arrival) {
                 last = snd.key;
@@ -384,6 +389,15 @@ struct Model {
                 reflect(*se, x, 0);
                 reflect(*se, x, 1);
             }
+        for (auto& se : sessions)
+            for (auto& o : se->outputs)
+                for (auto& ss : o->ss) ss.budget[0] = ss.budget[1] = -1;
+    }
+
+    void block(uint32_t sub_id, uint32_t track, uint32_t kind, uint32_t budget) {
+        for (auto& se : sessions)
+            for (auto& o : se->outputs)
+                if (o->sub_id == sub_id && track < o->ss.size()) o->ss[track].budget[kind & 1] = budget;
     }
 };
 
@@ -434,6 +448,12 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
             if (s % nshards == shard) on_join(s, sub, tr != 0, (ua & 1) != 0);
         } else if (type == 3) {
             m.tick();
+        } else if (type == 4) {
+            uint32_t sub = r.get<uint32_t>();
+            uint16_t trk = r.get<uint16_t>();
+            uint8_t kind = r.get<uint8_t>();
+            uint32_t budget = r.get<uint32_t>();
+            m.block(sub, trk, kind, budget);
         } else {
             fprintf(stderr, "bad event %u\n", type);
             exit(3);
@@ -499,6 +519,8 @@ static int run_bench(const char* in, int threads, int repeat) {
         } else if (e.type == 2) {
             e.s = r.get<uint32_t>(); e.sub = r.get<uint32_t>(); e.tcp = r.get<uint8_t>() != 0; e.ua = r.get<uint8_t>();
             lists[e.s % threads].push_back(e);
+        } else if (e.type == 4) {
+            r.p += 11;                          // BLOCK: the bench's sinks never block
         } else {
             for (auto& l : lists) l.push_back(e);
         }

@@ -24,6 +24,9 @@ parity consequence:
                     its u16 compare across a sequence wrap, the RTCP write that lifts it, and
                     PLAYs deferred for want of buffered packets (before the first packet, and
                     during a pusher stall).
+* ``backpressure``  sockets that stop accepting writes mid-tick (QTSS_WouldBlock): bookmarks
+                    at the blocked packet, Q9 relocation to the newest key frame after 2 s,
+                    RTCP sub-streams, an RTP-Info player blocked before its first write.
 """
 from __future__ import annotations
 
@@ -37,11 +40,12 @@ from easydarwin_amd.trace import TCP, UDP, Trace
 
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
-              joins: list[tuple], tick_times=None):
+              joins: list[tuple], tick_times=None, blocks=None):
     # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
+    # blocks: {tick time: [(sub, track, kind, budget)]}
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
     and ticks.  Within one tick interval the order is: packets (time order, session order),
-    then joins, then the TICK at the interval end."""
+    then joins, then the tick's socket budgets (BLOCK), then the TICK at the interval end."""
     pkts = []
     for s, lst in enumerate(per_session):
         for k, (t, ch, data) in enumerate(lst):
@@ -59,6 +63,8 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
             t, s, sub, transport = joins[j][:4]
             tr.join(t, s, sub, transport, joins[j][4] if len(joins[j]) > 4 else 0)
             j += 1
+        for sub, trk, kind, budget in (blocks or {}).get(tt, []):
+            tr.block(tt, sub, trk, kind, budget)
         tr.tick(tt)
     return tr
 
@@ -278,7 +284,59 @@ def rtpinfo() -> Trace:
     return _assemble(tr, [pk0, pk1, pk2], 100, 6000, joins)
 
 
+def backpressure() -> Trace:
+    """Egress backpressure: sockets that accept only part of a
+    tick's writes (EAGAIN -> QTSS_WouldBlock).  SendPacketsToOutput stops at the blocked
+    packet and bookmarks it; the next tick resumes there.  A socket blocked for longer than
+    the 2 s relocation age has its bookmark moved to the newest key frame (Q9), which also
+    arms the session's audio anchor (Q6).  Covers UDP and TCP subscribers, RTP and RTCP
+    sub-streams (pusher SRs on the video RTCP channel), an RTP-Info player blocked before its
+    first write (the first-seq filter stays armed), a subscriber blocked on its very first
+    packet, and an audio-only session (no key frame: no relocation)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 70))
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=1_000_000, gop=30, idr_bytes=12_000,
+                        rtcp_every_ms=500),
+              TrackSpec("audio", "PCMA/8000", 8)]
+    tracks2 = [TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    tr.add_session(make_sdp(tracks))
+    tr.add_session(make_sdp(tracks2))
+    pk0 = session_packets(tracks, 8000, SEED_BASE + 71)
+    pk1 = session_packets(tracks2, 8000, SEED_BASE + 72)
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (300, 0, 3, UDP), (1200, 0, 4, TCP),
+             (1500, 0, 5, UDP, VLC), (2000, 0, 6, TCP), (0, 1, 7, UDP), (500, 1, 8, TCP)]
+    ticks = list(range(0, 8001, 100))
+    blocks = {}
+
+    def add(t, *b):
+        blocks.setdefault(t, []).append(b)
+    for t in ticks:
+        if t % 300 == 0 and t > 0:
+            add(t, 2, 0, 0, int(rng.integers(0, 6)))          # TCP video: short budgets
+            add(t, 2, 1, 0, int(rng.integers(0, 2)))          # TCP audio
+        if 1000 <= t < 4200:
+            add(t, 3, 0, 0, 0)                                # UDP video blocked > 2 s: Q9
+        if 4200 <= t < 4600:
+            add(t, 3, 0, 0, 1)                                # ... then a trickle
+        if 1800 <= t < 2600 and t % 200 == 0:
+            add(t, 4, 0, 1, 0)                                # RTCP sub-stream (pusher SRs)
+        if t in (1500, 1600):
+            add(t, 5, 0, 0, 0)                                # RTP-Info: blocked before a write
+            add(t, 5, 0, 1, 0)
+            add(t, 5, 1, 0, 0)
+        if t == 1700:
+            add(t, 5, 0, 0, 2)
+        if t == 2000:
+            add(t, 6, 0, 0, 0)                                # blocked on its first packet
+        if 2000 <= t < 5000 and t % 100 == 0:
+            add(t, 7, 0, 0, 0 if t < 4500 else 3)             # audio-only: no key to jump to
+        if t % 700 == 0 and t >= 700:
+            add(t, 8, 0, 0, int(rng.integers(0, 4)))
+    return _assemble(tr, [pk0, pk1], 100, 8000, joins, tick_times=ticks, blocks=blocks)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
+    "backpressure": backpressure,
 }
