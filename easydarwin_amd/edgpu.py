@@ -30,6 +30,8 @@ EXPORTED = [
     "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
+    "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
+    "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -83,6 +85,12 @@ class TickStats(C.Structure):
     _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
                 ("arena_bytes", C.c_uint64), ("ingested_packets", C.c_uint64),
                 ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32)]
+
+
+class EgressStats(C.Structure):
+    _fields_ = [("udp_datagrams", C.c_uint64), ("udp_bytes", C.c_uint64), ("udp_dropped", C.c_uint64),
+                ("tcp_frames", C.c_uint64), ("tcp_bytes", C.c_uint64), ("blocked_substreams", C.c_uint32),
+                ("_pad", C.c_uint32), ("copy_ms", C.c_double), ("send_ms", C.c_double)]
 
 
 class Counters(C.Structure):
@@ -156,6 +164,14 @@ def load(path: str = LIB_PATH):
         "edgpu_subscribers_add": (I32, [P, U32, P, P, P]),
         "edgpu_ingest_interleaved": (I32, [P, P, U32, P, U64, I32, P]),
         "edgpu_fanout_blocked": (I32, [P, P, U32]),
+        "edgpu_egress_create": (I32, [P, U32, C.POINTER(P)]),
+        "edgpu_egress_destroy": (I32, [P]),
+        "edgpu_egress_last_error": (C.c_char_p, [P]),
+        "edgpu_egress_udp": (I32, [P, U32, U32, I32, I32, U32, C.c_uint16, C.c_uint16]),
+        "edgpu_egress_tcp": (I32, [P, U32, I32]),
+        "edgpu_egress_send": (I32, [P, C.POINTER(FanoutResult), C.POINTER(EgressStats)]),
+        "edgpu_egress_flush": (I32, [P, C.POINTER(U64)]),
+        "edgpu_egress_blocked": (I32, [P, P, U32, C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -373,6 +389,55 @@ class Context:
         desc = self.copy_to_host(r.desc, st.relayed_packets * OUT_DTYPE.itemsize).view(OUT_DTYPE)
         arena = self.copy_to_host(r.arena, st.arena_bytes)
         return st, subs, desc, arena
+
+
+class Egress:
+    """Socket egress of fan-out ticks (edgpu_egress_*): UDP via sendmmsg, RTSP-interleaved TCP
+    via writev with the reference's all-or-nothing buffering; TCP backpressure is reported to
+    the engine automatically."""
+
+    def __init__(self, ctx: Context, threads: int = 1):
+        self.ctx, self.lib = ctx, ctx.lib
+        h = C.c_void_p()
+        _check(self.lib.edgpu_egress_create(ctx.h, threads, C.byref(h)))
+        self.h = h
+
+    def _chk(self, rc):
+        if rc != OK:
+            raise EdgpuError(rc, self.lib.edgpu_egress_last_error(self.h).decode(errors="replace"))
+
+    def udp(self, subscriber: int, track: int, ip: str, rtp_port: int, rtcp_port: int,
+            rtp_fd: int = -1, rtcp_fd: int = -1):
+        import socket
+        ip_be = int.from_bytes(socket.inet_aton(ip), "little")
+        self._chk(self.lib.edgpu_egress_udp(self.h, subscriber, track, rtp_fd, rtcp_fd, ip_be,
+                                            socket.htons(rtp_port), socket.htons(rtcp_port)))
+
+    def tcp(self, subscriber: int, fd: int):
+        self._chk(self.lib.edgpu_egress_tcp(self.h, subscriber, fd))
+
+    def send(self, r: FanoutResult) -> EgressStats:
+        s = EgressStats()
+        self._chk(self.lib.edgpu_egress_send(self.h, C.byref(r), C.byref(s)))
+        return s
+
+    def blocked(self):
+        """The (sub-stream, sent) reports of the last send."""
+        cap = 1 << 16
+        buf = np.zeros((cap, 2), dtype=np.uint32)
+        n = C.c_uint32()
+        self._chk(self.lib.edgpu_egress_blocked(self.h, _ptr(buf), cap, C.byref(n)))
+        return [tuple(map(int, x)) for x in buf[:min(n.value, cap)]]
+
+    def flush(self) -> int:
+        left = C.c_uint64()
+        self._chk(self.lib.edgpu_egress_flush(self.h, C.byref(left)))
+        return left.value
+
+    def close(self):
+        if self.h:
+            self.lib.edgpu_egress_destroy(self.h)
+            self.h = None
 
 
 class DeviceBuffer:

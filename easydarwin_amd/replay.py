@@ -147,7 +147,7 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
-           interleaved: int | None = None, **cfg):
+           interleaved: int | None = None, sockets: dict | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -159,7 +159,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
     every replica before the first packet; "late" creates a fresh replica for every joining
     subscriber at its join tick, from a full image taken mid-stream (the C4 fast-start
-    path)."""
+    path).
+
+    sockets={...}: every tick leaves through the engine's socket egress to loopback receivers
+    (easydarwin_amd/egress.py SocketSink, constructed with these keyword arguments) and the
+    capture is rebuilt from the bytes the receivers read."""
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
@@ -187,6 +191,12 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
 
         def drain():
             nonlocal unread
+            if unread is not None and sink is not None:
+                c, r, tt, _ = unread
+                sink.tick(r, tt)
+                st = c.stats()
+                stats.append((tt, st.relayed_packets, st.relayed_bytes))
+                unread = None
             if unread is not None:
                 c, r, tt, budgets = unread
                 st, subs, desc, arena = c.read_tick(r)
@@ -213,6 +223,12 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 nflush += 1
                 pending = []
 
+        sink = None
+        if sockets is not None:
+            from .egress import SocketSink
+            if any(ev[0] == BLOCK for ev in trace.events) or lag:
+                raise ValueError("socket egress replays take neither BLOCK events nor overlap_ticks")
+            sink = SocketSink(ctx if rep is None else rep, **{k: v for k, v in sockets.items() if k != "report"})
         blocks = {}                         # (sub_id, track, kind) -> budget for the next TICK
         if lag and any(ev[0] == BLOCK for ev in trace.events):
             raise ValueError("backpressure reports need each tick read before the next ingest")
@@ -249,6 +265,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                             raise
                         continue
                     subs_meta[h] = (sub_id, s, transport)
+                    if sink is not None:
+                        sink.join(h, sub_id, sess_tracks[s], bool(transport))
                     for tr in range(sess_tracks[s]):
                         for k in (0, 1):
                             images[(h, tr, k)] = []
@@ -266,16 +284,25 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 if not lag:
                     drain()
         drain()
+        wire = None
+        if sink is not None:
+            wire = sink.finish()
+            sink.close()
+            if isinstance(sockets, dict) and "report" in sockets:
+                sockets["report"].extend(sink.blocked)
         # capture: one record per (subscriber, track, kind), sorted by subscriber id
         recs = []
         for (h, tr, k), parts in images.items():
             sub_id, s, transport = subs_meta[h]
-            recs.append((sub_id, s, tr, k, transport, parts))
+            if wire is not None:
+                n, data = wire.get((h, tr, k), (0, b""))
+            else:
+                n, data = len(parts), b"".join(parts)
+            recs.append((sub_id, s, tr, k, transport, n, data))
         recs.sort(key=lambda r: (r[0], r[2], r[3]))
         out = [b"EDCP", struct.pack("<I", len(recs))]
-        for sub_id, s, tr, k, transport, parts in recs:
-            data = b"".join(parts)
-            out.append(struct.pack("<IIHBBQQ", sub_id, s, tr, k, transport, len(parts), len(data)))
+        for sub_id, s, tr, k, transport, n, data in recs:
+            out.append(struct.pack("<IIHBBQQ", sub_id, s, tr, k, transport, n, len(data)))
             out.append(data)
         return b"".join(out), stats
     finally:

@@ -274,6 +274,40 @@ typedef struct edgpu_blocked {
 } edgpu_blocked;
 int  edgpu_fanout_blocked(edgpu_ctx* ctx, const edgpu_blocked* reports, uint32_t n);
 
+/* ---- Socket egress (host side) ----
+ * Sends a fan-out tick to the subscribers' sockets as RTPStream::Write does
+ * (Server.tproj/RTPStream.cpp:1084-1147): UDP datagrams through the sub-stream's RTP / RTCP
+ * socket with send errors ignored (a full socket drops the datagram, as the reference's
+ * (void)SendTo); RTSP-interleaved frames on the subscriber's RTSP connection with
+ * RTSPResponseStream::WriteV(kAllOrNothing) semantics (RTSPResponseStream.cpp:36-140: a frame
+ * that goes out in part counts as sent and its tail is buffered; a frame that gets no byte
+ * blocks).  Blocked TCP sub-streams are reported with edgpu_fanout_blocked before returning.
+ * The tick's arena, descriptors and sub-stream table are copied once into pinned host memory;
+ * `threads` workers own disjoint subscribers and send with sendmmsg / writev. */
+typedef struct edgpu_egress edgpu_egress;
+typedef struct edgpu_egress_stats {
+    uint64_t udp_datagrams, udp_bytes;
+    uint64_t udp_dropped;       /* SendTo failures, ignored like the reference */
+    uint64_t tcp_frames, tcp_bytes;
+    uint32_t blocked_substreams;
+    uint32_t _pad;
+    double   copy_ms, send_ms;  /* device -> pinned host copy; socket writes */
+} edgpu_egress_stats;
+int  edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out);
+int  edgpu_egress_destroy(edgpu_egress* eg);
+const char* edgpu_egress_last_error(edgpu_egress* eg);
+/* UDP subscriber track: datagrams leave through rtp_fd / rtcp_fd (-1: a per-worker socket) to
+ * ipv4:port (network byte order, as in sockaddr_in). */
+int  edgpu_egress_udp(edgpu_egress* eg, uint32_t subscriber, uint32_t track, int rtp_fd, int rtcp_fd,
+                      uint32_t ipv4_be, uint16_t rtp_port_be, uint16_t rtcp_port_be);
+/* RTSP-interleaved subscriber: its (non-blocking) RTSP connection. */
+int  edgpu_egress_tcp(edgpu_egress* eg, uint32_t subscriber, int fd);
+int  edgpu_egress_send(edgpu_egress* eg, const edgpu_fanout_result* r, edgpu_egress_stats* out);
+/* The (sub-stream, sent) backpressure reports of the last edgpu_egress_send (*n = count). */
+int  edgpu_egress_blocked(edgpu_egress* eg, edgpu_blocked* out, uint32_t cap, uint32_t* n);
+/* Writes buffered TCP tails that fit now; *pending = bytes still buffered. */
+int  edgpu_egress_flush(edgpu_egress* eg, uint64_t* pending);
+
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
 
 /* Name of the fan-out copy kernel this context launches (for measurement reports). */
