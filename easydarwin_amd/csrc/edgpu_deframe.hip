@@ -94,43 +94,54 @@ __device__ __forceinline__ uint32_t tcp_walk(const TcpView& v, uint64_t& pos, ui
 
 // '$' bytes among the first kTcpMaxFrame bytes of the chunk at `start` (offsets, in order; the
 // first kTcpCands kept in `list`); the stream's first chunk has the single candidate 0.  One
-// wave, 32 bytes a lane in one round of independent loads; returns the full count
-// (> kTcpCands: overflow).
+// wave: aligned 16-B blocks, one per lane per round (the window spans at most 129 blocks),
+// a per-byte '$' mask, and a wave prefix sum for the order; returns the full count
+// (> kTcpCands: overflow).  Chunks after the first start past the carried bytes (a chunk is
+// longer than the carry), so the window lies in the raw reads.
+__device__ __forceinline__ uint32_t dollar_mask(u32x4 w) {
+    uint32_t m = 0;
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        m |= (((d[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0x24u ? 1u : 0u) << i;
+    return m;
+}
+
 __device__ uint32_t tcp_candidates(const TcpView& v, uint64_t start, uint16_t* list, int lane) {
     if (start == 0) {
         if (lane == 0) list[0] = 0;
         return 1;
     }
     const uint64_t wend = min(start + (uint64_t)kTcpMaxFrame, v.len);
-    const uint64_t b = start + 32ull * (uint64_t)lane;
-    uint32_t mask = 0;
-    if (b < wend) {
-        const uint32_t n = (uint32_t)min<uint64_t>(32, wend - b);
-        if (b >= v.clen) {
-            const uint8_t* q = v.raw + (b - v.clen);
-#pragma unroll
-            for (int i = 0; i < 32; i++)
-                if ((uint32_t)i < n && q[i] == 0x24u) mask |= 1u << i;
-        } else {
-            for (uint32_t i = 0; i < n; i++)
-                if (tbyte(v, b + i) == 0x24u) mask |= 1u << i;
+    const uintptr_t lo = (uintptr_t)(v.raw + (start - v.clen));
+    const uintptr_t hi = (uintptr_t)(v.raw + (wend - v.clen));
+    const uintptr_t al = lo & ~(uintptr_t)15;
+    uint32_t n = 0;
+    for (uint32_t round = 0; al + 16 * 64 * (uintptr_t)round < hi; round++) {
+        const uintptr_t b = al + 16 * (uintptr_t)(lane + 64 * round);
+        uint32_t mask = 0;
+        if (b < hi) {
+            mask = dollar_mask(*reinterpret_cast<const u32x4*>(b));
+            if (b < lo) mask &= ~((1u << (uint32_t)(lo - b)) - 1u);
+            if (b + 16 > hi) mask &= (1u << (uint32_t)(hi - b)) - 1u;
         }
-    }
-    const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
+        const uint32_t cnt = (uint32_t)__popc(mask);
+        uint32_t incl = cnt;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        uint32_t idx = n + incl - cnt;
+        while (mask) {
+            const int i = __ffs(mask) - 1;
+            mask &= mask - 1;
+            if (idx < kTcpCands) list[idx] = (uint16_t)(b + i - lo);
+            idx++;
+        }
+        n += __shfl(incl, 63, 64);
     }
-    uint32_t idx = incl - cnt;
-    while (mask) {
-        const int i = __ffs(mask) - 1;
-        mask &= mask - 1;
-        if (idx < kTcpCands) list[idx] = (uint16_t)(b + i - start);
-        idx++;
-    }
-    return __shfl(incl, 63, 64);
+    return n;
 }
 
 template <typename T>
@@ -158,20 +169,29 @@ __device__ __forceinline__ T block_exclusive_scan256(T v, T* scratch, T& total) 
 
 }  // namespace
 
-// ---- k_tcp_walk: one wave per chunk ----
-__global__ __launch_bounds__(64) void k_tcp_walk(TcpParams P) {
-    const uint32_t c = blockIdx.x;
-    const int lane = threadIdx.x;
-    const uint32_t g = P.chunk_group[c];
-    const TcpGroup G = P.groups[g];
-    const TcpView v = tcp_view(P, G);
-    const uint32_t k = c - G.first_chunk;
-    const uint64_t start = (uint64_t)k * kTcpChunk;
-    const uint64_t end = min(start + kTcpChunk, v.len);
-    __shared__ uint16_t own[kTcpCands], next[kTcpCands];
-    const uint32_t n = tcp_candidates(v, start, own, lane);
-    const uint32_t nn = end < v.len ? tcp_candidates(v, end, next, lane) : 0u;
+// ---- k_tcp_walk: one wave per chunk, 4 chunks per workgroup (residency) ----
+constexpr int kWalkWaves = 4;
+
+__global__ __launch_bounds__(64 * kWalkWaves) void k_tcp_walk(TcpParams P) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t c = blockIdx.x * kWalkWaves + wid;
+    const bool valid = c < P.nchunks;
+    __shared__ uint16_t s_own[kWalkWaves][kTcpCands], s_next[kWalkWaves][kTcpCands];
+    uint16_t* own = s_own[wid];
+    uint16_t* next = s_next[wid];
+    TcpView v{};
+    uint64_t start = 0, end = 0;
+    uint32_t n = 0, nn = 0;
+    if (valid) {
+        const TcpGroup G = P.groups[P.chunk_group[c]];
+        v = tcp_view(P, G);
+        start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
+        end = min(start + kTcpChunk, v.len);
+        n = tcp_candidates(v, start, own, lane);
+        nn = end < v.len ? tcp_candidates(v, end, next, lane) : 0u;
+    }
     __syncthreads();
+    if (!valid) return;
     if (lane == 0) P.ncand[c] = n;
     if (n > kTcpCands || (uint32_t)lane >= n) return;
     const size_t ci = (size_t)c * kTcpCands + lane;
@@ -457,7 +477,8 @@ __global__ __launch_bounds__(256) void k_tcp_finish(TcpParams P) {
 }
 
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
-    if (p.nchunks) hipLaunchKernelGGL(k_tcp_walk, dim3(p.nchunks), dim3(64), 0, st, p);
+    if (p.nchunks)
+        hipLaunchKernelGGL(k_tcp_walk, dim3((p.nchunks + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(256), 0, st, p);
     if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);

@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
                 u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
                 const uint64_t w0 = p_vb[p] >> 4;
                 const uint32_t wm = s_wmask[s];
-                if (P.src_addr) {
+                if (P.src_addr) {                          // a frame inside the TCP byte stream
                     const uint8_t* lim = sp + 4 + p_len[p];
                     for (uint32_t w = lane; w < sb / 16; w += 64) {
                         u32x4 v = load16_unaligned(sp + 16 * w, lim);
