@@ -126,13 +126,20 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if ((err = edgpu_copy_to_host(fCtx, subs.data(), res.substreams, subs.size() * sizeof(subs[0])))) return err;
     if ((err = edgpu_copy_to_host(fCtx, d.data(), res.desc, d.size() * sizeof(d[0])))) return err;
     if ((err = edgpu_copy_to_host(fCtx, fArena.data(), res.arena, fArena.size()))) return err;
-    for (const edgpu_substream_out& q : subs)
+    // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stops this
+    // output's sub-stream for the tick; the engine then bookmarks the blocked packet
+    std::vector<edgpu_blocked> blocked;
+    for (uint32_t s = 0; s < (uint32_t)subs.size(); s++) {
+        const edgpu_substream_out& q = subs[s];
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = d[q.desc_base + i];
             err = sink->WritePacket(q.subscriber, q.track, q.kind != 0, q.transport == EDGPU_TRANSPORT_TCP,
                                     &fArena[o.offset], o.len, o.packet_id);
+            if (err == kWouldBlock) { blocked.push_back(edgpu_blocked{s, i}); break; }
             if (err) return err;
         }
+    }
+    if (!blocked.empty()) return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
     return kNoErr;
 }
 

@@ -33,7 +33,9 @@ enum { kNoErr = 0, kRequestFailed = -1, kBadArgument = -10, kWouldBlock = -14 };
 
 // The egress seam.  `wire` points at the bytes to put on the wire for this subscriber: the
 // UDP datagram, or the complete '$' ch BE16(len) + packet frame for an RTSP-interleaved
-// subscriber (RTSPSessionInterface.cpp:329-344).  Return kNoErr to continue.
+// subscriber (RTSPSessionInterface.cpp:329-344).  Return kNoErr to continue, kWouldBlock when
+// the socket is flow-controlled (EAGAIN): the rest of this sub-stream's packets are not
+// offered this tick and the next tick resumes at this packet, as SendPacketsToOutput does.
 class OutputSink {
 public:
     virtual ~OutputSink() {}

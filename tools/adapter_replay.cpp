@@ -1,7 +1,8 @@
 // tools/adapter_replay.cpp -- drives the C++ module-side adapter (reflector_adapter.h) with an
 // event trace, the way the reflector module would: PKT -> Reflector::PushPacket (track =
 // channel/2, RTCP = channel&1, as ProcessRTPData does, QTSSReflectorModule.cpp:654-671),
-// JOIN -> AddOutput, TICK -> ReflectPackets(now, sink).  Writes the capture format of
+// JOIN -> AddOutput, TICK -> ReflectPackets(now, sink), BLOCK -> the sink returns kWouldBlock
+// after the scripted number of writes in the next tick.  Writes the capture format of
 // easydarwin_amd/trace.py so tests compare it with the reference harness byte for byte.
 // Usage: adapter_replay <trace.edtr> <capture.edcp>
 #include <cstdio>
@@ -20,8 +21,14 @@ struct Rec { uint32_t sub = 0, session = 0; bool tcp = false; std::string img[2]
 class CaptureSink : public OutputSink {
 public:
     std::map<std::pair<uint32_t, uint16_t>, Rec>* recs;      // (handle, track)
+    std::map<std::tuple<uint32_t, uint16_t, int>, int64_t> budget;   // BLOCK: writes left this tick
     int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
                     uint32_t wireLen, uint32_t) override {
+        auto b = budget.find(std::make_tuple(subscriber, track, isRTCP ? 1 : 0));
+        if (b != budget.end()) {
+            if (b->second == 0) return kWouldBlock;
+            b->second--;
+        }
         Rec& r = (*recs)[{subscriber, track}];
         std::string& s = r.img[isRTCP ? 1 : 0];
         if (!interleaved) { s.push_back((char)(wireLen >> 8)); s.push_back((char)wireLen); }
@@ -82,6 +89,12 @@ int main(int argc, char** argv) {
         } else if (type == 3) {
             int err = R.ReflectPackets(t, &sink);
             if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
+            sink.budget.clear();
+        } else if (type == 4) {               // BLOCK: the sub-stream's socket takes `budget` writes
+            uint32_t sub, budget; uint16_t trk; uint8_t kind;
+            get(sub); get(trk); get(kind); get(budget);
+            for (auto& kv : handles)
+                if (std::get<0>(kv.second) == sub) sink.budget[std::make_tuple(kv.first, trk, (int)(kind & 1))] = budget;
         } else return 3;
     }
     std::vector<std::tuple<uint32_t, uint16_t, Rec*>> out;
