@@ -110,6 +110,71 @@ def run_step(ctx: edgpu.Context, bt: dict):
     ctx.fanout(bt["t"])
 
 
+def _sample_trace(args, n_sess=64, dur=3000):
+    """The CPU baseline's bounded sample of the bench workload: n_sess H.264 1080p 4 Mb/s
+    sessions x subs UDP subscribers x dur ms at 100-ms ticks."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
+    from easydarwin_amd.trace import Trace, UDP
+    from scenarios import _assemble
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=4_000_000, gop=60, idr_bytes=120_000)]
+    tr = Trace()
+    per = []
+    for s in range(n_sess):
+        tr.add_session(make_sdp(tracks))
+        per.append(session_packets(tracks, dur, 0xEA5D + 1 + s, t0=(s * 7) % 33))
+    joins = [(0, s, s * args.subs + k, UDP) for s in range(n_sess) for k in range(args.subs)]
+    _assemble(tr, per, 100, dur, joins)
+    return tr
+
+
+def _shard(tr, k: int, n: int):
+    """Sessions s with s % n == k (renumbered), their events, and every TICK."""
+    from easydarwin_amd.trace import BLOCK, JOIN, PKT, Trace
+    keep = {s: i for i, s in enumerate(range(k, len(tr.sdps), n))}
+    out = Trace(sdps=[tr.sdps[s] for s in keep])
+    for ev in tr.events:
+        if ev[0] in (PKT, JOIN):
+            if ev[2] in keep:
+                out.events.append((ev[0], ev[1], keep[ev[2]]) + tuple(ev[3:]))
+        elif ev[0] != BLOCK:
+            out.events.append(ev)
+    return out
+
+
+def cpu_baseline_reference(args) -> dict | None:
+    """The REFERENCE reflector itself (oracle/_ref/ref_harness --bench: EasyDarwin's
+    ReflectorStream / ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS
+    server, memcpy sinks) on the same bounded sample, sessions sharded over one process per
+    core, all running at once; value = relayed packets / the longest process's replay time."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    procs_n = min(16, os.cpu_count() or 1)
+    tr = _sample_trace(args)
+    with tempfile.TemporaryDirectory() as td:
+        paths = []
+        for k in range(procs_n):
+            p = os.path.join(td, f"s{k}.edtr")
+            _shard(tr, k, procs_n).write(p)
+            paths.append(p)
+        probe = json.loads(subprocess.run([exe, "--bench", paths[0], "1"], capture_output=True, text=True,
+                                          check=True).stdout)
+        rep = int(max(1, min(2000, 1.5 / max(probe["seconds"], 1e-4))))     # ~1.5 s per process
+        procs = [subprocess.Popen([exe, "--bench", p, str(rep)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                  text=True) for p in paths]
+        outs = [json.loads(pr.communicate()[0]) for pr in procs]
+        if any(pr.returncode for pr in procs):
+            return None
+    pk = sum(o["relayed_packets"] for o in outs)
+    secs = max(o["seconds"] for o in outs)
+    return {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
+            "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench, compiled from the reference "
+                      f"sources) on 64 H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x 3 s at 100-ms ticks, "
+                      f"sessions sharded over {procs_n} processes, each replaying its shard {rep} times; "
+                      f"{pk} relayed packets, longest process {secs:.2f} s (memcpy sinks, no sockets)"}
+
+
 def cpu_baseline(args) -> dict | None:
     """The CPU restatement (oracle/relay_model, memcpy sinks, sessions sharded over threads)
     on a bounded sample of the same workload: 64 sessions x subs x 3 s at 100-ms ticks."""
@@ -123,18 +188,8 @@ def cpu_baseline(args) -> dict | None:
             return None
     if not os.path.exists(exe):
         return None
-    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
-    from easydarwin_amd.trace import Trace, UDP
     n_sess, dur = 64, 3000
-    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=4_000_000, gop=60, idr_bytes=120_000)]
-    tr = Trace()
-    per = []
-    for s in range(n_sess):
-        tr.add_session(make_sdp(tracks))
-        per.append(session_packets(tracks, dur, 0xEA5D + 1 + s, t0=(s * 7) % 33))
-    from scenarios import _assemble
-    joins = [(0, s, s * args.subs + k, UDP) for s in range(n_sess) for k in range(args.subs)]
-    _assemble(tr, per, 100, dur, joins)
+    tr = _sample_trace(args, n_sess, dur)
     threads = min(16, os.cpu_count() or 1)
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "cpu.edtr")
@@ -274,7 +329,14 @@ def main():
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args)
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline_reference(args)
+        port = cpu_baseline(args)
+        if cpu is None:
+            cpu = port
+        elif port is not None:
+            cpu["restatement"] = {"value": port["value"], "cores": port["cores"], "kind": "port"}
     res = {
         "metric": "relayed RTP packets/sec (whole node) + achieved HBM GB/s, 1080p H.264 fan-out",
         "value": round(relayed_all / dt, 1),

@@ -23,9 +23,12 @@
 //     1145-1147) until the TICK ends -- the blocked-client path of SendPacketsToOutput.
 //
 // Usage: ref_harness <trace.edtr> <capture.edcp>
+//        ref_harness --bench <trace.edtr>    (memcpy sinks, no capture; prints the replay's
+//                                             relayed packets / bytes and seconds as JSON)
 // Trace / capture formats: see easydarwin_amd/trace.py (shared with the port oracle and
 // the GPU engine's replay driver).
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -140,6 +143,10 @@ static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf
 // (RTPStream.cpp:1098-1145) -- UDP datagram, or '$' ch BE16(len) + packet on the RTP or
 // RTCP channel (RTSPSessionInterface.cpp:329-344).  A sink blocks only when a BLOCK event
 // set its budget for this tick.
+// Bench mode (--bench): the sink is a memcpy into a scratch buffer (no capture), counted.
+static bool g_bench = false;
+static UInt64 g_bench_pkts = 0, g_bench_bytes = 0;
+static char g_scratch[70000];
 static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* outLen, UInt32 flags, ...) {
     FakeObj* s = (FakeObj*)stream;
     const QTSS_PacketStruct* pkt = (const QTSS_PacketStruct*)buf;
@@ -147,6 +154,14 @@ static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* ou
     if (len == 0) return QTSS_NoErr;
     if (s->budget[k] == 0) return QTSS_WouldBlock;
     if (s->budget[k] > 0) s->budget[k]--;
+    if (g_bench) {
+        const UInt32 h = s->transport == qtssRTPTransportTypeTCP ? 4 : 0;
+        memcpy(g_scratch + h, pkt->packetData, len);
+        g_bench_pkts++;
+        g_bench_bytes += len + h;
+        if (outLen) *outLen = len;
+        return QTSS_NoErr;
+    }
     std::string& c = s->cap[k];
     if (s->transport == qtssRTPTransportTypeTCP) {
         c.push_back('$');
@@ -181,7 +196,17 @@ struct Sub {
 };
 
 int main(int argc, char** argv) {
-    if (argc != 3) { fprintf(stderr, "usage: %s trace.edtr capture.edcp\n", argv[0]); return 2; }
+    int reps = 1;
+    if (argc >= 3 && strcmp(argv[1], "--bench") == 0) {
+        g_bench = true;
+        argv[1] = argv[2];
+        if (argc == 4) reps = atoi(argv[3]);
+        argc = 3;
+    }
+    if (argc != 3 || reps < 1) {
+        fprintf(stderr, "usage: %s trace.edtr capture.edcp | --bench trace.edtr [repeat]\n", argv[0]);
+        return 2;
+    }
     FILE* f = fopen(argv[1], "rb");
     if (!f) { perror(argv[1]); return 2; }
     Reader r;
@@ -226,6 +251,14 @@ int main(int argc, char** argv) {
         return 3;
     }
 
+    // The replay; bench mode repeats it with fresh sessions, subscribers and clock each pass.
+    const size_t p0 = r.p;
+    std::vector<Sub> subs;
+    double bench_secs = 0;
+    for (int rep = 0; rep < reps; rep++) {
+    r.p = p0;
+    g_now = 0;
+    subs.clear();
     // Sessions.
     UInt32 nsess = r.get<UInt32>();
     std::vector<ReflectorSession*> sessions(nsess, nullptr);
@@ -255,8 +288,8 @@ int main(int argc, char** argv) {
         sessions[s] = sess;
     }
 
-    std::vector<Sub> subs;
     std::vector<char> pktbuf(70000);
+    const auto t_start = std::chrono::steady_clock::now();
     while (!r.done()) {
         UInt8 type = r.get<UInt8>();
         if (type == 0) break;
@@ -346,6 +379,15 @@ int main(int argc, char** argv) {
             fprintf(stderr, "bad event type %u at %zu\n", type, r.p);
             return 3;
         }
+    }
+
+    bench_secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    }   // rep
+
+    if (g_bench) {                  // the replays only: PushPacket + ReflectPackets + joins
+        printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"repeat\": %d}\n",
+               (unsigned long long)g_bench_pkts, (unsigned long long)g_bench_bytes, bench_secs, reps);
+        return 0;
     }
 
     // Capture: one record per (subscriber, track, kind), sorted by (sub, track, kind).
