@@ -45,6 +45,23 @@ static int fail(int code, const std::string& msg) { g_err = msg; return code; }
             return fail(EDGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+// Device allocations.  EDGPU_POISON=1 (debugging) fills every new allocation with 0xA5 so a
+// read of memory the engine never wrote shows up deterministically instead of depending on
+// what a previous process left in HBM.
+static bool poison_on() {
+    static const int v = getenv("EDGPU_POISON") ? atoi(getenv("EDGPU_POISON")) : 0;
+    return v != 0;
+}
+template <typename T>
+static hipError_t dmalloc(T** p, size_t n) {
+    hipError_t e = hipMalloc((void**)p, n);
+    if (e == hipSuccess && poison_on()) {
+        e = hipMemset(*p, 0xA5, n);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    return e;
+}
+
 // Growable device array of POD T.
 template <typename T>
 struct DevVec {
@@ -54,7 +71,7 @@ struct DevVec {
         if (n <= cap) return hipSuccess;
         size_t nc = std::max<size_t>(n, cap ? cap * 2 : 64);
         T* np = nullptr;
-        hipError_t e = hipMalloc(&np, nc * sizeof(T));
+        hipError_t e = dmalloc(&np, nc * sizeof(T));
         if (e != hipSuccess) return e;
         if (ptr) {
             e = hipMemcpyAsync(np, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice, st);
@@ -221,23 +238,23 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return bad("stream");
     for (auto& e : x->ev) if (hipEventCreate(&e) != hipSuccess) return bad("event");
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (hipEventCreate(&e) != hipSuccess) return bad("event");
-    if (hipMalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
-    if (hipMalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
-    if (hipMalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
-    if (hipMalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
-    if (hipMalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
-    if (hipMalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
+    if (dmalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
+    if (dmalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
+    if (dmalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
+    if (dmalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
+    if (dmalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
+    if (dmalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
     x->overlap = c.overlap_ticks != 0;
     for (int k = 0; k < (x->overlap ? 2 : 1); k++) {
-        if (hipMalloc(&x->d_arena_buf[k], c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
-        if (hipMalloc(&x->d_out_desc_buf[k], sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
+        if (dmalloc(&x->d_arena_buf[k], c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
+        if (dmalloc(&x->d_out_desc_buf[k], sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
     }
     if (x->overlap) {
         if (hipStreamCreateWithFlags(&x->copy, hipStreamNonBlocking) != hipSuccess) return bad("copy stream");
         if (hipEventCreateWithFlags(&x->ev_plan, hipEventDisableTiming) != hipSuccess) return bad("event");
         if (hipEventCreateWithFlags(&x->ev_copy, hipEventDisableTiming) != hipSuccess) return bad("event");
     }
-    if (hipMalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
@@ -344,9 +361,9 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             const uint64_t pk = big ? x->cfg.video_ring_packets : x->cfg.other_ring_packets;
             const uint64_t by = big ? x->cfg.video_ring_bytes : x->cfg.other_ring_bytes;
             void* meta = nullptr; void* ring = nullptr;
-            if (hipMalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring");
+            if (dmalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring");
             x->ring_allocs.push_back(meta);
-            if (hipMalloc(&ring, by) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring");
+            if (dmalloc(&ring, by) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring");
             x->ring_allocs.push_back(ring);
             D.meta = (uint64_t)(uintptr_t)meta;
             D.ring = (uint64_t)(uintptr_t)ring;
@@ -607,7 +624,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
             if ((uint64_t)desc[i].slot * 16 + 4 + std::min<uint32_t>(desc[i].len, kMaxPacket) + 15 > blob_bytes + 15 ||
                 (uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
                 return fail(EDGPU_BAD_ARGUMENT, "packet slot outside blob");
-        if (!x->d_blob && hipMalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess)
+        if (!x->d_blob && dmalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess)
             return fail(EDGPU_OUT_OF_MEMORY, "blob staging");
         HIP_CHECK(hipMemcpyAsync(x->d_desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->stream));
         HIP_CHECK(hipMemcpyAsync(x->d_seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->stream));
@@ -676,12 +693,12 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(x->d_tcp_links.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
     HIP_CHECK(x->d_tcp_offs.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands * kTcpFrames, x->stream));
     HIP_CHECK(x->d_tcp_stage.reserve((size_t)ng * kTcpCarry, x->stream));
-    if (!x->d_tcp_tot && hipMalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
-    if (!x->d_tcp_src && hipMalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
+    if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
+    if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
     const uint8_t* raw = bytes;
     if (where == EDGPU_PTR_HOST) {
-        if (!x->d_tcp_raw && hipMalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
+        if (!x->d_tcp_raw && dmalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
             return fail(EDGPU_OUT_OF_MEMORY, "read staging");
         HIP_CHECK(hipMemcpyAsync(x->d_tcp_raw, bytes, nbytes, hipMemcpyHostToDevice, x->stream));
         raw = x->d_tcp_raw;
@@ -979,7 +996,7 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
 // Session images (cross-GPU keyframe fast start)
 
 static int image_launch(edgpu_ctx* x, std::vector<ImgPlan>& plan, int64_t now_ms, uint8_t* buf, int phase) {
-    if (!x->d_img_status && hipMalloc(&x->d_img_status, sizeof(int)) != hipSuccess)
+    if (!x->d_img_status && dmalloc(&x->d_img_status, sizeof(int)) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "image status");
     HIP_CHECK(x->d_img_plan.reserve(std::max<size_t>(plan.size(), 1), x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_img_plan.ptr, plan.data(), plan.size() * sizeof(ImgPlan), hipMemcpyHostToDevice, x->stream));
@@ -1071,7 +1088,7 @@ int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
     *out = nullptr;
-    if (hipMalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "device buffer");
+    if (dmalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "device buffer");
     return EDGPU_OK;
 }
 

@@ -966,7 +966,7 @@ typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 // only when the LDS image is written, so the registers stay exactly as loaded while the loads
 // are in flight.  All are buffer loads (vector-memory counter only; a flat load would also hold
 // the LDS counter that the store loop waits on).
-template <int THREADS, int NL>
+template <int THREADS, int NL, int LAUX = 0>
 __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r)[NL], u32x3& ma, u32x2& mb) {
     const uint32_t wmask = it.wmask, nw = it.nw;
     const uint32_t rstart = (uint32_t)(it.vb0 >> 4) & wmask;
@@ -978,7 +978,7 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
         const uint32_t wi = tid + j * THREADS;
         if ((uint32_t)(j * THREADS) < nw)              // uniform: no load past the chunk's lines
             r[j] = __builtin_amdgcn_raw_buffer_load_b128(
-                rs, wraps ? (wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu) : wi * 16u, 0, 0);
+                rs, wraps ? (wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu) : wi * 16u, 0, LAUX);
     }
     const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(it.meta), 0, (it.pkmask + 1) * (uint32_t)sizeof(PktMeta), 0x00020000);
@@ -987,7 +987,9 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
     mb = __builtin_amdgcn_raw_buffer_load_b64(ms, mo + 24u, 0, 0);
 }
 
-template <int THREADS, int CHUNK>
+// AUX: cache policy of the arena stores (0 plain; A/B variants: 2 nt, 16 sc1, 17 sc0 sc1);
+// DNT: non-temporal descriptor stores; LAUX: cache policy of the chunk loads.
+template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1020,7 +1022,7 @@ void k_fanout4(FanoutParams P) {
     FanWork nx;
     if (w < nwork) {
         nx = const_load(P.work + w);
-        fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+        fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb);
     }
     for (uint32_t par = 0; w < nwork; w += gridDim.x, par ^= 1u) {
         const FanWork it = nx;
@@ -1052,7 +1054,7 @@ void k_fanout4(FanoutParams P) {
         const uint32_t wn = w + gridDim.x;
         if (wn < nwork) {
             nx = const_load(P.work + wn);
-            fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+            fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb);
         }
         // ---- write the chunk to every sub-stream of the sender ----------------------------
         for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
@@ -1072,7 +1074,7 @@ void k_fanout4(FanoutParams P) {
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
                 u32x4 v = cbuf[srcc];
                 if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
-                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, AUX);
             }
         }
         // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
@@ -1094,7 +1096,10 @@ void k_fanout4(FanoutParams P) {
                     const uint32_t wlen = len + ((f.ch & 1u) ? 4u : 0u);
                     u32x4 dv;
                     dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m_id[p];
-                    if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    if (d0 - sh + lane < P.max_desc) {
+                        if constexpr (DNT) __builtin_nontemporal_store(dv, reinterpret_cast<u32x4*>(P.desc) + d0 - sh + lane);
+                        else reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    }
                     wire += wlen;
                 }
             }
@@ -1539,12 +1544,21 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout5<512, 32>, 512, 32, fanout5_lds<512, 32>()},             // 7
     {(const void*)k_fanout5<128, 16>, 128, 16, fanout5_lds<128, 16>()},             // 8
     {(const void*)k_fanout5<256, 16>, 256, 16, fanout5_lds<256, 16>()},             // 9
+    {(const void*)k_fanout4<1024, 32, 2>, 1024, 32, fanout4_lds<1024, 32>()},       // 10 nt arena stores
+    {(const void*)k_fanout4<1024, 32, 16>, 1024, 32, fanout4_lds<1024, 32>()},      // 11 sc1
+    {(const void*)k_fanout4<1024, 32, 17>, 1024, 32, fanout4_lds<1024, 32>()},      // 12 sc0 sc1
+    {(const void*)k_fanout4<1024, 32, 2, 1>, 1024, 32, fanout4_lds<1024, 32>()},    // 13 nt arena + descriptors
+    {(const void*)k_fanout4<1024, 32, 2, 1, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 14 ... + nt chunk loads
+    {(const void*)k_fanout4<1024, 32, 2, 0, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 15 nt arena + nt loads
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
-                                            "k_fanout5<256,32>", "k_fanout5<512,32>", "k_fanout5<128,16>", "k_fanout5<256,16>"};
+                                            "k_fanout5<256,32>", "k_fanout5<512,32>", "k_fanout5<128,16>", "k_fanout5<256,16>",
+                                            "k_fanout4<1024,32,nt>", "k_fanout4<1024,32,sc1>", "k_fanout4<1024,32,sc0sc1>",
+                                            "k_fanout4<1024,32,nt,ntdesc>", "k_fanout4<1024,32,nt,ntdesc,ntload>",
+                                            "k_fanout4<1024,32,nt,ntload>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-static const int kDefaultVariant = 2;
+static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 int fanout_chunk(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
     return kVariants[variant].chunk;

@@ -10,7 +10,7 @@ import pytest
 
 from easydarwin_amd import edgpu
 from easydarwin_amd.replay import replay
-from easydarwin_amd.trace import PKT, TICK, Trace
+from easydarwin_amd.trace import PKT, TICK, Trace, capture_summary, read_capture
 from scenarios import SCENARIOS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,7 +25,12 @@ def test_adapter_replay_matches_reference(name, tmp_path):
     t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
     t.write_bytes(SCENARIOS[name]().to_bytes())
     subprocess.run([TOOL, str(t), str(c)], check=True)
-    assert hashlib.sha256(c.read_bytes()).hexdigest() == fix["capture_sha256"]
+    cap = c.read_bytes()
+    if hashlib.sha256(cap).hexdigest() != fix["capture_sha256"]:
+        got = capture_summary(read_capture(cap))
+        bad = {k: (got.get(k, [None])[:2], fix["substreams"][k][:2]) for k in fix["substreams"]
+               if got.get(k) != fix["substreams"][k]}
+        pytest.fail(f"{len(bad)} sub-streams differ ([packets, bytes] got vs want): {dict(list(bad.items())[:6])}")
 
 
 @pytest.mark.gpu
