@@ -177,6 +177,12 @@ struct edgpu_ctx {
     DevVec<edgpu_tcp_result> d_tcp_results;
     TcpTotals* d_tcp_tot = nullptr;
     uint8_t* d_tcp_raw = nullptr;
+    // RTP-Info PLAY query (kMaxTracks entries) and backpressure reports
+    FirstInfoQuery* d_fpi_q = nullptr;
+    FirstInfoResult* d_fpi_r = nullptr;
+    FirstInfoQuery* h_fpi_q = nullptr;          // pinned
+    FirstInfoResult* h_fpi_r = nullptr;         // pinned
+    DevVec<edgpu_blocked> d_blocked;
     // session images
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
@@ -275,7 +281,11 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_img_plan.release(); x->d_sub_out_buf2.release();
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
-    x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release();
+    x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
+    if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
+    if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
+    if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
+    if (x->h_fpi_r) (void)hipHostFree(x->h_fpi_r);
     if (x->d_tcp_src) (void)hipFree(x->d_tcp_src);
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
@@ -442,17 +452,31 @@ static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms
         q[t].rtcp_sender = sh.udp_push ? 0xFFFFFFFFu : sh.first_sender + 2 * t + 1;
         q[t].cutoff = now_ms - window;                  // age <= window  <=>  arrival >= cutoff
     }
-    FirstInfoQuery* dq = nullptr;
-    FirstInfoResult* dr = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&dq, q.size() * sizeof(FirstInfoQuery), x->stream));
-    HIP_CHECK(hipMallocAsync((void**)&dr, q.size() * sizeof(FirstInfoResult), x->stream));
-    std::vector<FirstInfoResult> r(sh.ntracks);
-    HIP_CHECK(hipMemcpyAsync(dq, q.data(), q.size() * sizeof(FirstInfoQuery), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(launch_first_packet_info(dq, dr, x->d_senders.ptr, sh.ntracks, x->stream));
-    HIP_CHECK(hipMemcpyAsync(r.data(), dr, r.size() * sizeof(FirstInfoResult), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipFreeAsync(dq, x->stream));
-    HIP_CHECK(hipFreeAsync(dr, x->stream));
+    // Persistent device buffers and pinned host staging (kMaxTracks entries).  Per-call
+    // hipMallocAsync buffers were recycled from the previous PLAY and the result copy could
+    // return that PLAY's results (observed on gfx950 / ROCm 7.2), so they are not used here.
+    if (!x->d_fpi_q) {
+        if (dmalloc(&x->d_fpi_q, kMaxTracks * sizeof(FirstInfoQuery)) != hipSuccess ||
+            dmalloc(&x->d_fpi_r, kMaxTracks * sizeof(FirstInfoResult)) != hipSuccess ||
+            hipHostMalloc((void**)&x->h_fpi_q, kMaxTracks * sizeof(FirstInfoQuery), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&x->h_fpi_r, kMaxTracks * sizeof(FirstInfoResult), hipHostMallocDefault) != hipSuccess)
+            return fail(EDGPU_OUT_OF_MEMORY, "RTP-Info query buffers");
+    }
+    memcpy(x->h_fpi_q, q.data(), q.size() * sizeof(FirstInfoQuery));
+    HIP_CHECK(hipMemcpyAsync(x->d_fpi_q, x->h_fpi_q, q.size() * sizeof(FirstInfoQuery), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(launch_first_packet_info(x->d_fpi_q, x->d_fpi_r, x->d_senders.ptr, sh.ntracks, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->h_fpi_r, x->d_fpi_r, q.size() * sizeof(FirstInfoResult), hipMemcpyDeviceToHost, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
+    std::vector<FirstInfoResult> r(x->h_fpi_r, x->h_fpi_r + sh.ntracks);
+    if (getenv("EDGPU_DEBUG_PLAY")) {                    // debugging: the PLAY's inputs and results
+        for (uint32_t t = 0; t < sh.ntracks; t++) {
+            SenderDev d[2];
+            HIP_CHECK(hipMemcpy(d, x->d_senders.ptr + q[t].rtp_sender, 2 * sizeof(SenderDev), hipMemcpyDeviceToHost));
+            fprintf(stderr, "play now=%lld track=%u cutoff=%lld head=%llu/%llu found=%u seq=%u\n", (long long)now_ms, t,
+                    (long long)q[t].cutoff, (unsigned long long)d[0].head, (unsigned long long)d[1].head, r[t].found,
+                    r[t].seq);
+        }
+    }
     for (uint32_t t = 0; t < sh.ntracks; t++) {
         if (r[t].found != 1)
             return fail(EDGPU_WOULD_BLOCK, r[t].found == 0 ? "RTP-Info PLAY: no RTP packet received yet (retry)"
@@ -630,6 +654,9 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         HIP_CHECK(hipMemcpyAsync(x->d_seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->stream));
         HIP_CHECK(hipMemcpyAsync(x->d_seg_sess, seg_sess, (size_t)nseg * 4, hipMemcpyHostToDevice, x->stream));
         HIP_CHECK(hipMemcpyAsync(x->d_blob, blob, blob_bytes, hipMemcpyHostToDevice, x->stream));
+        // The caller's buffers are pageable host memory it may free or reuse as soon as this
+        // returns, and an async copy from pageable memory may still be reading them: wait.
+        HIP_CHECK(hipStreamSynchronize(x->stream));
         dd = x->d_desc; ds = x->d_seg; dss = x->d_seg_sess; db = x->d_blob;
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
@@ -741,8 +768,8 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n)
     for (uint32_t i = 0; i < n; i++)
         if (reports[i].substream >= nsub) return fail(EDGPU_BAD_ARGUMENT, "bad sub-stream index");
     HIP_CHECK(hipSetDevice(x->device));
-    edgpu_blocked* d = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&d, n * sizeof(edgpu_blocked), x->stream));
+    HIP_CHECK(x->d_blocked.reserve(n, x->stream));
+    edgpu_blocked* d = x->d_blocked.ptr;
     HIP_CHECK(hipMemcpyAsync(d, reports, n * sizeof(edgpu_blocked), hipMemcpyHostToDevice, x->stream));
     BlockedParams p;
     p.reports = d; p.n = n;
@@ -751,7 +778,6 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n)
     p.relocate_ms = x->cfg.rtp_reflector_threshold_msec;
     p.totals = x->d_totals;
     HIP_CHECK(launch_blocked(p, x->stream));
-    HIP_CHECK(hipFreeAsync(d, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));   // `reports` is the caller's host memory
     return EDGPU_OK;
 }

@@ -66,7 +66,7 @@ extern "C" {
 #define EDGPU_TRANSPORT_TCP      1     /* RTSP-interleaved '$' framing */
 
 /* pointer-location flags for edgpu_ingest */
-#define EDGPU_PTR_HOST           0     /* engine stages through pinned memory */
+#define EDGPU_PTR_HOST           0     /* host memory: copied to the device before the call returns */
 #define EDGPU_PTR_DEVICE         1     /* already resident in HBM on the ctx device */
 
 /* Engine configuration.  Reflector prefs keep the reference's XML key names
