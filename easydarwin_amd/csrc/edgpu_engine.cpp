@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -88,10 +89,36 @@ struct DevVec {
 
 struct TrackHost { uint32_t type = 0; std::string name; };   // 1 video, 2 audio
 
+// A track's receiver-report state toward a UDP pusher (ReflectorStream fields
+// fReceiverReportBuffer / fDestRTCPAddr / fDestRTCPPort and the RTCP sender's fLastRRTime).
+struct SourceHost {
+    uint32_t rr_ssrc = 0;
+    std::vector<uint8_t> cname;     // RTCPSRPacket::GetACName, padded
+    uint32_t addr = 0;              // 0: unknown (SendReceiverReport returns early)
+    uint16_t port = 0;
+    int64_t last_rr = 0;
+};
+
 struct SessionHost {
     uint32_t first_sender, ntracks, first_stream;
     bool udp_push;
+    uint32_t eyes = 0;              // client outputs (ReflectorStream::fEyeCount, every track)
+    std::vector<SourceHost> src;    // per track
 };
+
+// RTCPSRPacket::GetACName (RTCPSRPacket.cpp:87-117): item type 1, length byte, "QTSS<secs>",
+// a NUL, zero padding to the next multiple of 4 -- at least one more byte.
+static std::vector<uint8_t> source_cname(int64_t secs) {
+    char b[48];
+    const int n = snprintf(b + 1, sizeof(b) - 1, " QTSS%lld", (long long)secs) + 1;
+    b[0] = 1;
+    b[1] = (char)(n - 2);
+    uint32_t len = (uint32_t)n + 1;
+    len += 4 - (len % 4);
+    std::vector<uint8_t> c(len, 0);
+    memcpy(c.data(), b, (size_t)n);
+    return c;
+}
 
 struct SubscriberHost {
     uint32_t session;
@@ -125,6 +152,7 @@ struct edgpu_ctx {
 
     std::vector<SessionHost> sessions;
     std::vector<SubscriberHost> subscribers;
+    std::vector<edgpu_source_report> source_reports;   // queued by the last edgpu_fanout
     std::vector<uint32_t> sub_sender;   // host mirror: SubDev index -> sender
     std::vector<uint8_t> sub_active;
     uint32_t nsenders = 0, nstreams = 0;
@@ -352,6 +380,11 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
         return fail(EDGPU_BAD_ARGUMENT, "SDP must describe 1..16 tracks");
     const uint32_t sid = (uint32_t)x->sessions.size();
     SessionHost sh{x->nsenders, (uint32_t)tracks.size(), x->nstreams, udp_push != 0};
+    // receiver-report identity, as the ReflectorStream constructor draws it (:164-201)
+    const int64_t wall_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+        std::chrono::system_clock::now().time_since_epoch()).count();
+    sh.src.resize(sh.ntracks);
+    for (auto& h : sh.src) { h.rr_ssrc = (uint32_t)::rand(); h.cname = source_cname(wall_ms / 1000); }
     const uint32_t nsnd = 2 * sh.ntracks;
     HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
     HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));
@@ -435,6 +468,7 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             v.push_back(Q);
         }
     x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true});
+    x->sessions[session].eyes++;                 // AddOutput(..., isClient) -> IncEyeCount
     x->index_dirty = true;
     return handle;
 }
@@ -550,7 +584,96 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     }
     HIP_CHECK(hipStreamSynchronize(x->stream));
     s.active = false;
+    x->sessions[s.session].eyes--;               // RemoveOutput(..., isClient) -> DecEyeCount
     x->index_dirty = true;
+    return EDGPU_OK;
+}
+
+// ---- UDP pushers: source addresses and receiver reports ------------------------------------
+// RTCPPacket::ParsePacket (RTCPPacket.cpp:40-63) + the SR-first test of ProcessPacket
+// (ReflectorStream.cpp:1799-1815) from a datagram's length and first 4 bytes.
+static bool rtcp_sr_first(const uint8_t* h, uint32_t len) {
+    if (len < 8) return false;
+    const uint32_t words = (uint32_t)h[2] << 8 | h[3];
+    return len >= words * 4 + 4 && (h[0] >> 6) == 2 && h[1] == 200;
+}
+
+int edgpu_udp_sources(edgpu_ctx* x, const edgpu_udp_source* src, uint32_t n) {
+    if (!x || (n && !src)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    for (uint32_t i = 0; i < n; i++)
+        if (src[i].session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    for (uint32_t i = 0; i < n; i++) {
+        const edgpu_udp_source& d = src[i];
+        SessionHost& sh = x->sessions[d.session];
+        const uint32_t track = d.channel >> 1;
+        if (track >= sh.ntracks || d.len == 0 || d.addr == 0) continue;
+        // fIsRTCP by local-port parity: only a UDP push binds an odd RTCP port (Q12)
+        const bool rtcp = sh.udp_push && (d.channel & 1);
+        if (rtcp && !rtcp_sr_first(d.head, d.len)) continue;      // dropped before the update
+        SourceHost& h = sh.src[track];
+        if (h.addr == 0 || rtcp) {                                // NAT_WORKAROUND
+            h.addr = d.addr;
+            h.port = (uint16_t)(d.port + ((!rtcp && !(d.port & 1)) ? 1 : 0));
+        }
+    }
+    return EDGPU_OK;
+}
+
+// The RTCP senders' report timers of one tick (ReflectorStream.cpp:1039-1047, 510-527).
+static void queue_source_reports(edgpu_ctx* x, int64_t now) {
+    x->source_reports.clear();
+    for (uint32_t si = 0; si < x->sessions.size(); si++) {
+        SessionHost& sh = x->sessions[si];
+        for (uint32_t t = 0; t < sh.ntracks; t++) {
+            SourceHost& h = sh.src[t];
+            if (!(now > h.last_rr + 5000)) continue;              // kRRInterval
+            h.last_rr = now;
+            if (h.addr == 0) continue;
+            edgpu_source_report r;
+            memset(&r, 0, sizeof(r));
+            r.session = si; r.track = (uint16_t)t; r.addr = h.addr; r.port = h.port;
+            uint32_t n = 0;
+            auto w32 = [&](uint32_t v) {
+                r.bytes[n] = (uint8_t)(v >> 24); r.bytes[n + 1] = (uint8_t)(v >> 16);
+                r.bytes[n + 2] = (uint8_t)(v >> 8); r.bytes[n + 3] = (uint8_t)v; n += 4;
+            };
+            // htonl(eye) & 0x7fffffff on the little-endian host masks bit 31 of the swapped
+            // word, i.e. bit 7 of the count's low byte on the wire (:519-521)
+            const uint32_t eye = sh.eyes & 0xFFFFFF7Fu;
+            w32(0x80c90001u); w32(h.rr_ssrc);                                  // RR, no blocks
+            w32(0x81ca0000u + (uint32_t)(h.cname.size() >> 2) + 1); w32(h.rr_ssrc);   // SDES
+            memcpy(r.bytes + n, h.cname.data(), h.cname.size()); n += (uint32_t)h.cname.size();
+            w32(0x80cc0008u); w32(h.rr_ssrc); w32(0x51545353u); w32(0);        // APP 'QTSS'
+            w32(4); w32(0x6579000cu); w32(eye); w32(eye); w32(0);              // eye count
+            r.len = n;
+            x->source_reports.push_back(r);
+        }
+    }
+}
+
+int edgpu_source_reports(edgpu_ctx* x, edgpu_source_report* out, uint32_t cap, uint32_t* n_out) {
+    if (!x || !n_out || (cap && !out)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    const uint32_t n = (uint32_t)x->source_reports.size();
+    *n_out = n;
+    if (n > cap) return fail(EDGPU_BAD_ARGUMENT, "report buffer too small");
+    if (n) memcpy(out, x->source_reports.data(), n * sizeof(edgpu_source_report));
+    return EDGPU_OK;
+}
+
+int edgpu_session_eyes_add(edgpu_ctx* x, uint32_t session, int32_t delta) {
+    if (!x || session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    SessionHost& sh = x->sessions[session];
+    if (delta < 0 && (uint32_t)(-(int64_t)delta) > sh.eyes) return fail(EDGPU_BAD_ARGUMENT, "eye count below zero");
+    sh.eyes = (uint32_t)((int64_t)sh.eyes + delta);
+    return EDGPU_OK;
+}
+
+int edgpu_source_identity(edgpu_ctx* x, uint32_t session, uint32_t track, uint32_t ssrc, int64_t cname_secs) {
+    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks)
+        return fail(EDGPU_BAD_ARGUMENT, "bad session / track");
+    SourceHost& h = x->sessions[session].src[track];
+    h.rr_ssrc = ssrc;
+    h.cname = source_cname(cname_secs);
     return EDGPU_OK;
 }
 
@@ -813,6 +936,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
     x->last_now = now_ms;
+    queue_source_reports(x, now_ms);
     edgpu_substream_out* sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
     uint8_t* arena = x->d_arena_buf[x->cur];
     edgpu_out_desc* odesc = x->d_out_desc_buf[x->cur];

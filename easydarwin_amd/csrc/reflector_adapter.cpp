@@ -69,6 +69,26 @@ void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet,
     fPushed.push_back(p);
 }
 
+void Reflector::ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort, const char* packet,
+                                 uint32_t packetLen, uint32_t remoteAddr, uint16_t remotePort, int64_t nowMs) {
+    if (packetLen == 0 || track >= GetNumStreams(session)) return;
+    PushPacket(session, track, packet, packetLen, rtcpPort, nowMs);
+    edgpu_udp_source u;
+    memset(&u, 0, sizeof(u));
+    u.session = session;
+    u.channel = (uint8_t)(2 * track + (rtcpPort ? 1 : 0));
+    u.port = remotePort;
+    u.addr = remoteAddr;
+    u.len = packetLen;
+    memcpy(u.head, packet, std::min<uint32_t>(packetLen, 4));
+    fSources.push_back(u);
+}
+
+int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs) {
+    if (!fCtx) return kRequestFailed;
+    return edgpu_source_identity(fCtx, session, track, ssrc, cnameSecs);
+}
+
 int Reflector::FlushIngest() {
     int err;
     if (!fPushed.empty()) {
@@ -107,6 +127,10 @@ int Reflector::FlushIngest() {
         fPushed.clear();
         fBytes.clear();
     }
+    if (!fSources.empty()) {
+        if ((err = edgpu_udp_sources(fCtx, fSources.data(), (uint32_t)fSources.size()))) return err;
+        fSources.clear();
+    }
     return kNoErr;
 }
 
@@ -116,6 +140,14 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if (err) return err;
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
+    uint32_t nrr = 0;
+    if ((err = edgpu_source_reports(fCtx, nullptr, 0, &nrr)) && nrr == 0) return err;
+    if (nrr && sink) {
+        std::vector<edgpu_source_report> rr(nrr);
+        if ((err = edgpu_source_reports(fCtx, rr.data(), nrr, &nrr))) return err;
+        for (const edgpu_source_report& r : rr)
+            sink->SendReceiverReport(r.session, r.track, r.addr, r.port, r.bytes, r.len);
+    }
     edgpu_tick_stats st;
     if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
     if (st.status) return st.status;

@@ -11,6 +11,11 @@
 //     (ReflectorStream.cpp:529-576)                     plus the session/track it belongs to)
 //   ReflectorSocket::Run -> ReflectPackets            Reflector::ReflectPackets(now, sink)
 //     (ReflectorStream.cpp:1676-1714, 1024-1136)
+//   ReflectorSocket::GetIncomingData ->               Reflector::ProcessUDPPacket (a UDP
+//     ProcessPacket(now, pkt, addr, port)               pusher's datagram with its source)
+//     (ReflectorStream.cpp:1716-1735, 1769-1875)
+//   ReflectorStream::SendReceiverReport ->            OutputSink::SendReceiverReport, from
+//     UDPSocket::SendTo (ReflectorStream.cpp:510-527)   ReflectPackets on the 5-s timer
 //   ReflectorOutput::WritePacket (pure virtual,       OutputSink::WritePacket, called once per
 //     ReflectorOutput.h:114) -> QTSS_Write ->           send-ready packet with the bytes already
 //     RTPStream::Write framing                           framed for the subscriber's transport
@@ -41,6 +46,13 @@ public:
     virtual ~OutputSink() {}
     virtual int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved,
                             const uint8_t* wire, uint32_t wireLen, uint32_t packetID) = 0;
+    // A receiver report for a UDP pusher: send `rr` from the track's RTCP socket to
+    // (addr, port), both in host order (ReflectorStream::SendReceiverReport's SendTo, whose
+    // result the reference ignores).
+    virtual void SendReceiverReport(uint32_t session, uint16_t track, uint32_t addr, uint16_t port,
+                                    const uint8_t* rr, uint32_t len) {
+        (void)session; (void)track; (void)addr; (void)port; (void)rr; (void)len;
+    }
 };
 
 class Reflector {
@@ -66,6 +78,12 @@ public:
     // one pushed packet, exactly as ProcessRTPData hands it to ReflectorStream::PushPacket
     void PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
                     bool isRTCP, int64_t nowMs);
+    // one datagram read from a UDP push session's socket pair (rtcpPort: the odd port), with
+    // the source address GetIncomingData's RecvFrom returns (host order)
+    void ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort, const char* packet,
+                          uint32_t packetLen, uint32_t remoteAddr, uint16_t remotePort, int64_t nowMs);
+    // the receiver-report SSRC / CNAME time a track's ReflectorStream would have drawn
+    int  SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs);
     // ingest everything pushed since the last call, update the keyframe index, fan out at
     // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order)
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
@@ -78,6 +96,7 @@ private:
     int fStatus = kRequestFailed;
     std::vector<uint32_t> fTracks;                          // per session
     std::vector<Pushed> fPushed;                            // arrival order
+    std::vector<edgpu_udp_source> fSources;                 // UDP datagrams' sources, same order
     std::vector<uint8_t> fBytes;
     std::vector<uint8_t> fArena;                            // host copy of one tick's output
 };

@@ -32,6 +32,7 @@ EXPORTED = [
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
     "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
+    "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -108,6 +109,12 @@ SUB_DTYPE = np.dtype([("subscriber", "<u4"), ("track", "<u2"), ("kind", "u1"), (
                       ("out_bytes", "<u8")])
 TCP_READ_DTYPE = np.dtype([("session", "<u4"), ("len", "<u4"), ("offset", "<u8"), ("arrival_ms", "<i8")])
 TCP_RESULT_DTYPE = np.dtype([("frames", "<u4"), ("consumed", "<u4"), ("status", "<i4"), ("carry", "<u4")])
+UDP_SOURCE_DTYPE = np.dtype([("session", "<u4"), ("channel", "u1"), ("_pad", "u1"), ("port", "<u2"),
+                             ("addr", "<u4"), ("len", "<u4"), ("head", "u1", (4,))])
+RR_MAX = 96
+SOURCE_REPORT_DTYPE = np.dtype([("session", "<u4"), ("track", "<u2"), ("port", "<u2"), ("addr", "<u4"),
+                                ("len", "<u4"), ("bytes", "u1", (RR_MAX,))])
+assert UDP_SOURCE_DTYPE.itemsize == 20 and SOURCE_REPORT_DTYPE.itemsize == 112
 assert TCP_READ_DTYPE.itemsize == 24 and TCP_RESULT_DTYPE.itemsize == 16
 assert PKT_DTYPE.itemsize == C.sizeof(PktDesc) == 16
 assert OUT_DTYPE.itemsize == C.sizeof(OutDesc) == 16
@@ -172,6 +179,10 @@ def load(path: str = LIB_PATH):
         "edgpu_egress_send": (I32, [P, C.POINTER(FanoutResult), C.POINTER(EgressStats)]),
         "edgpu_egress_flush": (I32, [P, C.POINTER(U64)]),
         "edgpu_egress_blocked": (I32, [P, P, U32, C.POINTER(U32)]),
+        "edgpu_udp_sources": (I32, [P, P, U32]),
+        "edgpu_source_reports": (I32, [P, P, U32, C.POINTER(U32)]),
+        "edgpu_source_identity": (I32, [P, U32, U32, U32, I64]),
+        "edgpu_session_eyes_add": (I32, [P, U32, C.c_int32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -294,6 +305,39 @@ class Context:
 
     def keyframe_index(self):
         _check(self.lib.edgpu_keyframe_index(self.h))
+
+    def udp_sources(self, rows):
+        """Source addresses of UDP-pushed datagrams, in arrival order:
+        [(session, channel, addr, port, datagram bytes)] (only len and the first 4 bytes
+        travel)."""
+        a = np.zeros(len(rows), dtype=UDP_SOURCE_DTYPE)
+        for i, (s, ch, addr, port, data) in enumerate(rows):
+            h = bytes(data[:4]).ljust(4, b"\0")
+            a[i] = (s, ch, 0, port, addr, len(data), np.frombuffer(h, dtype=np.uint8))
+        if len(a):
+            _check(self.lib.edgpu_udp_sources(self.h, _ptr(a), len(a)))
+
+    def source_reports(self) -> list:
+        """Receiver reports queued by the last fanout: [(session, track, addr, port, bytes)]."""
+        n = C.c_uint32(0)
+        cap = 64
+        while True:
+            buf = np.zeros(cap, dtype=SOURCE_REPORT_DTYPE)
+            rc = self.lib.edgpu_source_reports(self.h, _ptr(buf), cap, C.byref(n))
+            if rc == 0:
+                break
+            if n.value <= cap:
+                _check(rc)
+            cap = n.value
+        return [(int(r["session"]), int(r["track"]), int(r["addr"]), int(r["port"]),
+                 bytes(r["bytes"][:int(r["len"])])) for r in buf[:n.value]]
+
+    def source_identity(self, session: int, track: int, ssrc: int, cname_secs: int):
+        _check(self.lib.edgpu_source_identity(self.h, session, track, ssrc, int(cname_secs)))
+
+    def session_eyes_add(self, session: int, delta: int):
+        """Subscribers of an owned session joined (+) or left (-) on another context."""
+        _check(self.lib.edgpu_session_eyes_add(self.h, session, int(delta)))
 
     def fanout(self, now_ms: int) -> FanoutResult:
         r = FanoutResult()

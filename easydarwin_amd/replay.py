@@ -6,6 +6,11 @@ Batch semantics: all PKT events since the previous TICK form one ``edgpu_ingest`
 (grouped by session, arrival order kept), followed by ``edgpu_keyframe_index``; JOINs since
 the previous TICK become ``edgpu_subscriber_add``; the TICK itself is ``edgpu_fanout(now)``.
 
+UPKT events (UDP pushers) are ingested like PKTs and their source addresses go to
+``edgpu_udp_sources`` with the batch; the receiver reports each ``edgpu_fanout`` queues
+(``edgpu_source_reports``) form the capture's EDRR trailer.  Each track's report identity is
+set to what the reference harness's deterministic ``rand()`` gives it (trace.rr_ssrc).
+
 ``interleaved=seed`` feeds the same packets as a pusher's RTSP connection would carry them
 ('$' ch BE16(len) frames) through ``edgpu_ingest_interleaved`` instead: each session's
 frames are cut into random TCP reads (cuts only between or inside frames of one arrival time,
@@ -22,7 +27,7 @@ import struct
 import numpy as np
 
 from . import edgpu
-from .trace import BLOCK, JOIN, PKT, TICK, Trace
+from .trace import BLOCK, JOIN, PKT, TICK, UPKT, Trace, pack_source_reports, rr_ssrc
 
 
 def _wire_images(subs, desc, arena, images, budgets=None):
@@ -134,15 +139,20 @@ def ingest_tcp(ctx: edgpu.Context, reads_by_session: dict):
 
 
 def _batches(trace: Trace, flush_on_rtpinfo: bool):
-    out, cur = [], []
+    """The pushers' interleaved packets of every ingest batch (a batch holding only UDP
+    pushers' datagrams is an empty entry, so the list stays aligned with the flushes)."""
+    out, cur, any_pkt = [], [], False
     for ev in trace.events:
         if ev[0] == PKT:
             _, t, s, ch, data = ev
             cur.append((s, ch, t, data))
+            any_pkt = True
+        elif ev[0] == UPKT:
+            any_pkt = True
         elif (ev[0] == JOIN and ev[5] & 1 and flush_on_rtpinfo) or ev[0] == TICK:
-            if cur:
+            if any_pkt:
                 out.append(cur)
-                cur = []
+                cur, any_pkt = [], False
     return out
 
 
@@ -177,12 +187,18 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     try:
         sess_tracks = []
         rsess = {}
-        for sdp in trace.sdps:
-            sid = ctx.session_add(sdp)
+        rand_calls = 0
+        for i, sdp in enumerate(trace.sdps):
+            sid = ctx.session_add(sdp, udp_push=trace.udp_push(i))
             assert sid == len(sess_tracks)
             sess_tracks.append(ctx.session_tracks(sid))
+            for tr in range(sess_tracks[-1]):
+                ctx.source_identity(sid, tr, rr_ssrc(rand_calls), 0)
+                rand_calls += 1
             if replica == "all":
                 rsess[sid] = link.add(sid, sdp)
+        reports = []                        # (t, session, track, addr, port, bytes)
+        sources = []                        # this batch's UDP datagram sources
         subs_meta = {}          # handle -> (sub_id, session, tcp)
         images = {}
         pending, joins, stats = [], [], []
@@ -212,16 +228,24 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         nflush = 0
 
         def flush():
-            nonlocal pending, nflush
+            nonlocal pending, nflush, sources
             if pending:
+                udp = [p for p in pending if p[4]]
                 if plan is not None:
-                    ingest_tcp(ctx, plan[nflush])
+                    if len(udp) < len(pending):
+                        ingest_tcp(ctx, plan[nflush])
+                    batch = udp                  # UDP pushers' datagrams: a plain batch
                 else:
-                    desc, seg_off, seg_sess, blob = edgpu.build_batch(pending)
+                    batch = pending
+                if batch:
+                    desc, seg_off, seg_sess, blob = edgpu.build_batch([p[:4] for p in batch])
                     ctx.ingest_host(desc, seg_off, seg_sess, blob)
                     ctx.keyframe_index()
                 nflush += 1
                 pending = []
+            if sources:
+                ctx.udp_sources(sources)
+                sources = []
 
         sink = None
         if sockets is not None:
@@ -239,7 +263,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             clock = max(clock, ev[1])
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
-                pending.append((s, ch, t, data))
+                pending.append((s, ch, t, data, False))
+            elif ev[0] == UPKT:
+                _, t, s, ch, addr, port, data = ev
+                pending.append((s, ch, t, data, True))
+                sources.append((s, ch, addr, port, data))
             elif ev[0] == JOIN:
                 # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):
                 # ingest what precedes it first; other joins wait for the tick
@@ -265,6 +293,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                             raise
                         continue
                     subs_meta[h] = (sub_id, s, transport)
+                    if rep is not None:
+                        ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
                     if sink is not None:
                         sink.join(h, sub_id, sess_tracks[s], bool(transport))
                     for tr in range(sess_tracks[s]):
@@ -273,6 +303,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 joins = []
                 if rep is not None:
                     ctx.fanout(t)                      # the owner ticks too (no subscribers here)
+                    reports.extend((t,) + r for r in ctx.source_reports())
                 drain()                              # the previous tick, after this batch's ingest
                 by_handle = {}
                 for (sub_id, trk, kind), b in blocks.items():
@@ -281,6 +312,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                             by_handle[(h, trk, kind)] = b
                 blocks = {}
                 unread = (out, out.fanout(t), t, by_handle)
+                if rep is None:
+                    reports.extend((t,) + r for r in ctx.source_reports())
                 if not lag:
                     drain()
         drain()
@@ -304,6 +337,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         for sub_id, s, tr, k, transport, n, data in recs:
             out.append(struct.pack("<IIHBBQQ", sub_id, s, tr, k, transport, n, len(data)))
             out.append(data)
+        out.append(pack_source_reports(reports))
         return b"".join(out), stats
     finally:
         if link is not None:

@@ -12,7 +12,11 @@ list.  It mirrors the reference's entry points:
   (ReflectorStream.cpp:1709-1714);
 * ``BLOCK`` -> during the next TICK, one subscriber sub-stream's socket accepts ``budget``
   more writes and then returns QTSS_WouldBlock (EAGAIN) for the rest of that tick
-  (egress backpressure: SendPacketsToOutput's blocked branch, ReflectorStream.cpp:1158-1190).
+  (egress backpressure: SendPacketsToOutput's blocked branch, ReflectorStream.cpp:1158-1190);
+* ``UPKT`` -> a UDP datagram from a pusher's address arriving on a UDP-push session's RTP
+  (even) or RTCP (odd) port: ``ReflectorSocket::GetIncomingData`` -> ``ProcessPacket`` with
+  the remote address (ReflectorStream.cpp:1716-1735, 1769-1875), which also records the
+  source's RTCP address for the receiver reports (NAT_WORKAROUND, :1843-1855).
 
 Every event carries the virtual clock value (ms) that ``OS::Milliseconds`` returns while it
 is applied.  The GPU engine's batch boundary is the TICK: all PKTs since the previous TICK
@@ -21,17 +25,32 @@ ReflectorStream.cpp:1676-1714).
 
 Binary layout (little endian)::
 
-    trace   := "EDTR" u32 version=1 u32 n_sessions { u32 sdp_len sdp_bytes }* event* u8 0
+    trace   := "EDTR" u32 version u32 n_sessions { u32 sdp_len sdp_bytes [u8 flags] }*
+               event* u8 0
+               (version 1: no flags byte; version 2: flags bit 0 = UDP push)
     event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
              | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
              | u8 3 i64 t                                                    (TICK)
              | u8 4 i64 t u32 sub_id u16 track u8 kind u32 budget           (BLOCK)
+             | u8 5 i64 t u32 session u8 channel u32 addr u16 port u32 len bytes[len]
+                                                                             (UPKT, v2)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
+               [ "EDRR" u32 m { i64 t u32 session u16 track u32 addr u16 port u32 len
+                               bytes[len] }* ]
 
 ``kind`` is 0 for the RTP sub-stream, 1 for RTCP.  The capture bytes are the sub-stream's
 *wire image*: UDP = ``BE16(len) + datagram`` per packet; TCP = the exact interleaved byte
-stream ``'$' ch BE16(len) + packet`` (RTSPSessionInterface.cpp:329-344).
+stream ``'$' ch BE16(len) + packet`` (RTSPSessionInterface.cpp:329-344).  The optional
+``EDRR`` trailer lists the receiver reports sent to UDP pushers
+(ReflectorStream::SendReceiverReport, ReflectorStream.cpp:510-527), in send order; it is
+present only when at least one was sent.  ``addr`` is IPv4 in host order.
+
+The reference draws each ReflectorStream's receiver-report SSRC from ``rand()``
+(ReflectorStream.cpp:167) and its CNAME from the clock (RTCPSRPacket.cpp:87-117).  The
+harness makes ``rand()`` deterministic (:func:`rr_ssrc` of the call count: one call per
+ReflectorStream, in session then track order) and runs on a virtual clock that is 0 when the
+sessions are created, so a replay feeds the engine the same identities.
 """
 from __future__ import annotations
 
@@ -39,7 +58,7 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK, BLOCK = 1, 2, 3, 4
+PKT, JOIN, TICK, BLOCK, UPKT = 1, 2, 3, 4, 5
 UDP, TCP = 0, 1
 
 
@@ -47,10 +66,19 @@ UDP, TCP = 0, 1
 class Trace:
     sdps: list[str] = field(default_factory=list)
     events: list[tuple] = field(default_factory=list)   # (type, t, ...) in file order
+    flags: list[int] = field(default_factory=list)      # per session: bit 0 = UDP push
 
-    def add_session(self, sdp: str) -> int:
+    def add_session(self, sdp: str, udp_push: bool = False) -> int:
         self.sdps.append(sdp)
+        self.flags.append(1 if udp_push else 0)
         return len(self.sdps) - 1
+
+    def udp_push(self, session: int) -> bool:
+        return bool(self.flags[session] & 1) if session < len(self.flags) else False
+
+    @property
+    def version(self) -> int:
+        return 2 if any(self.flags) or any(ev[0] == UPKT for ev in self.events) else 1
 
     def pkt(self, t: int, session: int, channel: int, data: bytes):
         self.events.append((PKT, int(t), session, channel, bytes(data)))
@@ -64,6 +92,9 @@ class Trace:
     def block(self, t: int, sub_id: int, track: int, kind: int, budget: int):
         self.events.append((BLOCK, int(t), sub_id, track, kind, budget))
 
+    def upkt(self, t: int, session: int, channel: int, addr: int, port: int, data: bytes):
+        self.events.append((UPKT, int(t), session, channel, int(addr), int(port), bytes(data)))
+
     # -- serialisation ------------------------------------------------------------------
     def to_bytes(self) -> bytes:
         # PKT and TICK times drive the virtual clock and must not go back; a JOIN's time is
@@ -71,11 +102,14 @@ class Trace:
         # picked up by the next ReflectPackets).
         times = [ev[1] for ev in self.events if ev[0] not in (JOIN, BLOCK)]
         assert all(a <= b for a, b in zip(times, times[1:])), "trace events must be time-ordered"
-        out = [b"EDTR", struct.pack("<II", 1, len(self.sdps))]
-        for s in self.sdps:
+        ver = self.version
+        out = [b"EDTR", struct.pack("<II", ver, len(self.sdps))]
+        for i, s in enumerate(self.sdps):
             b = s.encode()
             out.append(struct.pack("<I", len(b)))
             out.append(b)
+            if ver >= 2:
+                out.append(struct.pack("<B", self.flags[i] if i < len(self.flags) else 0))
         for ev in self.events:
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
@@ -87,6 +121,10 @@ class Trace:
             elif ev[0] == BLOCK:
                 _, t, sub, trk, kind, budget = ev
                 out.append(struct.pack("<BqIHBI", BLOCK, t, sub, trk, kind, budget))
+            elif ev[0] == UPKT:
+                _, t, s, ch, addr, port, data = ev
+                out.append(struct.pack("<BqIBIHI", UPKT, t, s, ch, addr, port, len(data)))
+                out.append(data)
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -100,7 +138,7 @@ class Trace:
     def from_bytes(buf: bytes) -> "Trace":
         assert buf[:4] == b"EDTR"
         ver, n = struct.unpack_from("<II", buf, 4)
-        assert ver == 1
+        assert ver in (1, 2)
         p = 12
         tr = Trace()
         for _ in range(n):
@@ -108,6 +146,11 @@ class Trace:
             p += 4
             tr.sdps.append(buf[p:p + ln].decode())
             p += ln
+            fl = 0
+            if ver >= 2:
+                fl = buf[p]
+                p += 1
+            tr.flags.append(fl)
         while p < len(buf):
             typ = buf[p]
             if typ == 0:
@@ -129,6 +172,11 @@ class Trace:
                 _, t, sub, trk, kind, budget = struct.unpack_from("<BqIHBI", buf, p)
                 p += 20
                 tr.events.append((BLOCK, t, sub, trk, kind, budget))
+            elif typ == UPKT:
+                _, t, s, ch, addr, port, ln = struct.unpack_from("<BqIBIHI", buf, p)
+                p += 24
+                tr.events.append((UPKT, t, s, ch, addr, port, bytes(buf[p:p + ln])))
+                p += ln
             else:
                 raise ValueError(f"bad event {typ} at {p}")
         return tr
@@ -168,6 +216,44 @@ def read_capture(path_or_bytes) -> dict:
         p += nb
         ss = SubStream(sub, sess, track, kind, tcp, npk, data)
         out[ss.key] = ss
+    return out
+
+
+def rr_ssrc(k: int) -> int:
+    """The harness's deterministic rand(): the value of its k-th call (0-based)."""
+    return ((k + 1) * 0x9E3779B1 + 0x7F4A7C15) & 0x7FFFFFFF
+
+
+def pack_source_reports(reports) -> bytes:
+    """reports: [(t, session, track, addr, port, bytes)] -> the capture's EDRR trailer."""
+    if not reports:
+        return b""
+    out = [b"EDRR", struct.pack("<I", len(reports))]
+    for t, s, trk, addr, port, data in reports:
+        out.append(struct.pack("<qIHIHI", t, s, trk, addr, port, len(data)))
+        out.append(bytes(data))
+    return b"".join(out)
+
+
+def read_source_reports(buf: bytes) -> list:
+    """The EDRR trailer of a capture: [(t, session, track, addr, port, bytes)]."""
+    assert buf[:4] == b"EDCP", "bad capture magic"
+    (n,) = struct.unpack_from("<I", buf, 4)
+    p = 8
+    for _ in range(n):
+        nb = struct.unpack_from("<Q", buf, p + 20)[0]
+        p += 28 + nb
+    if p >= len(buf):
+        return []
+    assert buf[p:p + 4] == b"EDRR", "bad capture trailer"
+    (m,) = struct.unpack_from("<I", buf, p + 4)
+    p += 8
+    out = []
+    for _ in range(m):
+        t, s, trk, addr, port, ln = struct.unpack_from("<qIHIHI", buf, p)
+        p += 24
+        out.append((t, s, trk, addr, port, bytes(buf[p:p + ln])))
+        p += ln
     return out
 
 

@@ -28,6 +28,10 @@
  *                          RTPStream::Write (ReflectorStream.cpp:1024-1198,
  *                          RTPSessionOutput.cpp:564-662, Server.tproj/RTPStream.cpp:1084-1147,
  *                          RTSPSessionInterface.cpp:329-344), for every sender at once
+ *   edgpu_udp_sources      the pusher RTCP-address update in ProcessPacket for UDP pushers
+ *                          (ReflectorStream.cpp:1836-1866, NAT_WORKAROUND)
+ *   edgpu_source_reports   ReflectorStream::SendReceiverReport on the RTCP sender's 5-s
+ *                          timer (ReflectorStream.cpp:164-201, 510-527, 1039-1047)
  *
  * Conventions
  *   - Every function returns an int status using QTSS_Error values (QTSS.h:61-76):
@@ -273,6 +277,60 @@ typedef struct edgpu_blocked {
     uint32_t sent;
 } edgpu_blocked;
 int  edgpu_fanout_blocked(edgpu_ctx* ctx, const edgpu_blocked* reports, uint32_t n);
+
+/* ---- UDP pushers: source addresses and receiver reports ----
+ * A UDP push session (edgpu_session_add udp_push=1) receives datagrams on a bound even/odd
+ * port pair; the host's socket reader passes the packets to edgpu_ingest (channel =
+ * 2*track + 1 for the odd, RTCP port) and, in the same arrival order, their source
+ * addresses here -- ReflectorSocket::ProcessPacket's remote address (ReflectorStream.cpp:
+ * 1769-1866).  The engine keeps each track's pusher RTCP address as the reference does
+ * with NAT_WORKAROUND (ReflectorStream.h:63, .cpp:1843-1855): set by the first datagram,
+ * moved by every RTCP-port datagram that passes the SR-only gate (RTCPPacket::ParsePacket
+ * + type 200, Q14), an even RTP source port followed by +1.  Datagrams from address 0,
+ * empty ones and tracks out of range change nothing.  `head` = the datagram's first 4
+ * bytes (what the SR gate reads with `len`).  Only RTCP datagrams and a track's first RTP
+ * datagram can change the address, so a reader may pass just those.
+ * Replaces: the fDestRTCPAddr/fDestRTCPPort update inside ReflectorSocket::ProcessPacket. */
+typedef struct edgpu_udp_source {
+    uint32_t session;
+    uint8_t  channel;
+    uint8_t  _pad;
+    uint16_t port;        /* host order */
+    uint32_t addr;        /* IPv4, host order */
+    uint32_t len;
+    uint8_t  head[4];
+} edgpu_udp_source;
+int  edgpu_udp_sources(edgpu_ctx* ctx, const edgpu_udp_source* src, uint32_t n);
+
+/* Receiver reports to UDP pushers.  Every edgpu_fanout(now) runs, for each track, the RTCP
+ * sender's report timer (ReflectorSender::ReflectPackets, ReflectorStream.cpp:1039-1047):
+ * when now > last + kRRInterval (5000 ms) the timer restarts at now and, if the pusher's
+ * RTCP address is known, one report is queued -- ReflectorStream::SendReceiverReport
+ * (:510-527): RR (header + SSRC), SDES CNAME, and the 'QTSS' APP packet carrying the eye
+ * count (client subscribers of the session, ReflectorSession.cpp:215-268) twice, built as
+ * the ReflectorStream constructor lays it out (:164-201).  edgpu_source_reports returns the
+ * reports queued by the last edgpu_fanout (session then track order) for the host to send
+ * from the track's RTCP socket to (addr, port).
+ * Identity: the reference draws the report SSRC from rand() and the CNAME from
+ * OS::Milliseconds()/1000 when the stream is created (RTCPSRPacket.cpp:87-117); the engine
+ * does the same at edgpu_session_add, and edgpu_source_identity overrides both. */
+#define EDGPU_RR_MAX 96
+typedef struct edgpu_source_report {
+    uint32_t session;
+    uint16_t track;
+    uint16_t port;        /* host order */
+    uint32_t addr;        /* IPv4, host order */
+    uint32_t len;
+    uint8_t  bytes[EDGPU_RR_MAX];
+} edgpu_source_report;
+int  edgpu_source_reports(edgpu_ctx* ctx, edgpu_source_report* out, uint32_t cap, uint32_t* n_out);
+int  edgpu_source_identity(edgpu_ctx* ctx, uint32_t session, uint32_t track, uint32_t ssrc,
+                           int64_t cname_secs);
+/* Subscribers of `session` served by other contexts (replica sessions on other GPUs, §8.e):
+ * the owner's eye count is its own clients plus these, as the single reference process
+ * counts every output (IncEyeCount / DecEyeCount).  `delta` is +1 per remote join, -1 per
+ * remote leave. */
+int  edgpu_session_eyes_add(edgpu_ctx* ctx, uint32_t session, int32_t delta);
 
 /* ---- Socket egress (host side) ----
  * Sends a fan-out tick to the subscribers' sockets as RTPStream::Write does

@@ -20,7 +20,21 @@
 //     ReflectorSocket::Run does (ReflectorStream.cpp:1709-1714);
 //   * BLOCK events give one sub-stream's socket a write budget for the next TICK: after
 //     `budget` accepted writes QTSS_Write returns QTSS_WouldBlock (EAGAIN, RTPStream.cpp:
-//     1145-1147) until the TICK ends -- the blocked-client path of SendPacketsToOutput.
+//     1145-1147) until the TICK ends -- the blocked-client path of SendPacketsToOutput;
+//   * UDP-push sessions (trace v2, session flag bit 0) get their socket pair bound on
+//     loopback to an even/odd port pair, as UDPSocketPool::CreateUDPSocketPair binds it
+//     (UDPSocketPool.cpp), so GetLocalPort()&1 tells RTCP from RTP; UPKT events are the
+//     datagrams GetIncomingData reads (ReflectorStream.cpp:1716-1735): clamped to the
+//     2060-byte receive buffer, then ReflectorSocket::ProcessPacket(now, packet, remote
+//     addr, remote port), which applies the UDP RTCP SR gate (Q14) and records the pusher's
+//     RTCP address (NAT_WORKAROUND, :1843-1855).  The session is still set up through the
+//     TCP-transport branch of BindSockets (no UDPSocketPool search, no event registration);
+//     the transport type is read nowhere on the packet path;
+//   * UDPSocket::SendTo is link-wrapped: the only caller on this path is
+//     ReflectorStream::SendReceiverReport (:510-527, every kRRInterval from the RTCP sender's
+//     ReflectPackets, :1039-1047), whose datagrams go to the capture's EDRR trailer;
+//   * rand() is link-wrapped to a deterministic sequence (trace.py rr_ssrc): its only caller
+//     on this path is the ReflectorStream constructor's receiver-report SSRC (:167).
 //
 // Usage: ref_harness <trace.edtr> <capture.edcp>
 //        ref_harness --bench <trace.edtr>    (memcpy sinks, no capture; prints the replay's
@@ -61,6 +75,29 @@ UInt32       QTSServerInterface::sNumModulesInRole[QTSSModule::kNumRoles];
 // Virtual clock.
 static SInt64 g_now = 0;
 extern "C" SInt64 __wrap__ZN2OS12MillisecondsEv() { return g_now; }
+
+// Deterministic rand() (easydarwin_amd/trace.py rr_ssrc).
+static UInt32 g_rand_calls = 0;
+extern "C" int __wrap_rand() {
+    const UInt32 k = g_rand_calls++;
+    return (int)(((k + 1) * 0x9E3779B1u + 0x7F4A7C15u) & 0x7FFFFFFFu);
+}
+
+// Receiver reports to UDP pushers: UDPSocket::SendTo(addr, port, buf, len).
+struct SentReport { SInt64 t; UInt32 session; UInt16 track; UInt32 addr; UInt16 port; std::string bytes; };
+static std::vector<SentReport> g_reports;
+static std::map<const void*, std::pair<UInt32, UInt16>> g_rtcp_sockets;   // socket B -> (session, track)
+extern "C" OS_Error __wrap__ZN9UDPSocket6SendToEjtPvj(void* self, UInt32 addr, UInt16 port, void* buf, UInt32 len) {
+    auto it = g_rtcp_sockets.find(self);
+    SentReport r;
+    r.t = g_now;
+    r.session = it == g_rtcp_sockets.end() ? 0xFFFFFFFFu : it->second.first;
+    r.track = it == g_rtcp_sockets.end() ? 0xFFFF : it->second.second;
+    r.addr = addr; r.port = port;
+    r.bytes.assign((const char*)buf, len);
+    g_reports.push_back(r);
+    return OS_NoErr;
+}
 
 // ---------------------------------------------------------------------------------------
 // Attribute store.  Values have stable storage because RTPSessionOutput writes through
@@ -216,7 +253,7 @@ int main(int argc, char** argv) {
     if (memcmp(&r.d[0], "EDTR", 4) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
     r.p = 4;
     UInt32 version = r.get<UInt32>();
-    if (version != 1) { fprintf(stderr, "bad version\n"); return 2; }
+    if (version != 1 && version != 2) { fprintf(stderr, "bad version\n"); return 2; }
 
     static NoopAssert logger;
     SetAssertLogger(&logger);
@@ -258,6 +295,9 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < reps; rep++) {
     r.p = p0;
     g_now = 0;
+    g_rand_calls = 0;
+    g_reports.clear();
+    g_rtcp_sockets.clear();
     subs.clear();
     // Sessions.
     UInt32 nsess = r.get<UInt32>();
@@ -266,6 +306,7 @@ int main(int argc, char** argv) {
         UInt32 sdplen = r.get<UInt32>();
         std::string sdp((const char*)&r.d[r.p], sdplen);
         r.p += sdplen;
+        const UInt8 sflags = version >= 2 ? r.get<UInt8>() : 0;
         char* sdpbuf = new char[sdplen + 1];
         memcpy(sdpbuf, sdp.data(), sdplen); sdpbuf[sdplen] = 0;
         SDPSourceInfo* info = new SDPSourceInfo(sdpbuf, sdplen);
@@ -286,6 +327,21 @@ int main(int argc, char** argv) {
             ReflectorSession::kMarkSetup | ReflectorSession::kIsPushSession, true, 30);
         if (err != QTSS_NoErr) { fprintf(stderr, "setup failed %d\n", (int)err); return 3; }
         sessions[s] = sess;
+        for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+            UDPSocketPair* pr = sess->GetStreamByIndex(x)->GetSocketPair();
+            g_rtcp_sockets[pr->GetSocketB()] = std::make_pair(s, (UInt16)x);
+            if (!(sflags & 1)) continue;
+            // UDP push: bind the pair to an even/odd loopback port pair
+            if (pr->GetSocketA()->Open() != OS_NoErr || pr->GetSocketB()->Open() != OS_NoErr) {
+                fprintf(stderr, "socket open failed\n"); return 3;
+            }
+            static UInt16 port = 41000;
+            bool bound = false;
+            for (int tries = 0; tries < 2000 && !bound; tries++, port += 2)
+                bound = pr->GetSocketA()->Bind(INADDR_LOOPBACK, port) == OS_NoErr &&
+                        pr->GetSocketB()->Bind(INADDR_LOOPBACK, port + 1) == OS_NoErr;
+            if (!bound) { fprintf(stderr, "no loopback port pair\n"); return 3; }
+        }
     }
 
     std::vector<char> pktbuf(70000);
@@ -368,6 +424,30 @@ int main(int argc, char** argv) {
                 }
             }
             for (auto& o : g_objs) o->budget[0] = o->budget[1] = -1;
+        } else if (type == 5) {     // UPKT: a datagram read by ReflectorSocket::GetIncomingData
+            UInt32 s = r.get<UInt32>();
+            UInt8 ch = r.get<UInt8>();
+            UInt32 addr = r.get<UInt32>();
+            UInt16 port = r.get<UInt16>();
+            UInt32 len = r.get<UInt32>();
+            memcpy(pktbuf.data(), &r.d[r.p], len);
+            r.p += len;
+            ReflectorSession* sess = sessions[s];
+            UInt32 idx = ch / 2;
+            // an empty read is GetIncomingData's "no more data" (ProcessPacket then re-arms the
+            // socket's event), not a datagram: traces carry none
+            if (idx >= sess->GetNumStreams() || len == 0) continue;
+            UDPSocketPair* pr = sess->GetStreamByIndex(idx)->GetSocketPair();
+            ReflectorSocket* so = (ReflectorSocket*)((ch & 1) ? pr->GetSocketB() : pr->GetSocketA());
+            ReflectorPacket* pk = so->GetPacket();
+            if (pk == NULL) continue;
+            // RecvFrom into the packet's kMaxReflectorPacketSize (2060, private) buffer
+            // truncates the datagram; SetPacketData stores the same bytes (at exactly 2060 it
+            // logs its '>' assert, which the harness's logger counts and ignores)
+            const UInt32 n = std::min<UInt32>(len, 2060u);
+            pk->SetPacketData(pktbuf.data(), n);
+            OSMutexLocker locker(so->GetDemuxer()->GetMutex());
+            so->ProcessPacket(g_now, pk, addr, port);
         } else if (type == 4) {     // BLOCK
             UInt32 sub_id = r.get<UInt32>();
             UInt16 track = r.get<UInt16>();
@@ -411,6 +491,17 @@ int main(int argc, char** argv) {
                 u64 = st->cap[k].size(); fwrite(&u64, 8, 1, o);
                 fwrite(st->cap[k].data(), 1, st->cap[k].size(), o);
             }
+        }
+    }
+    if (!g_reports.empty()) {               // EDRR trailer: receiver reports sent to pushers
+        fwrite("EDRR", 1, 4, o);
+        UInt32 m = (UInt32)g_reports.size();
+        fwrite(&m, 4, 1, o);
+        for (auto& rr : g_reports) {
+            UInt32 ln = (UInt32)rr.bytes.size();
+            fwrite(&rr.t, 8, 1, o); fwrite(&rr.session, 4, 1, o); fwrite(&rr.track, 2, 1, o);
+            fwrite(&rr.addr, 4, 1, o); fwrite(&rr.port, 2, 1, o); fwrite(&ln, 4, 1, o);
+            fwrite(rr.bytes.data(), 1, ln, o);
         }
     }
     fclose(o);

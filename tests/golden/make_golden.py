@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
-from easydarwin_amd.trace import capture_summary, read_capture  # noqa: E402
+from easydarwin_amd.trace import capture_summary, read_capture, read_source_reports  # noqa: E402
 from scenarios import SCENARIOS  # noqa: E402
 
 FULL = {"tiny", "nal", "clamp", "ssrc"}          # small enough to commit byte for byte
@@ -59,6 +59,9 @@ def main():
                 "source": "oracle/_ref/ref_harness (EasyDarwin reference reflector)",
                 "substreams": capture_summary(cap),
             }
+            rr = read_source_reports(rb)
+            if rr:                       # receiver reports to UDP pushers (EDRR trailer)
+                fix["source_reports"] = [[t, s, trk, addr, port, data.hex()] for t, s, trk, addr, port, data in rr]
             with open(os.path.join(HERE, name + ".json"), "w") as f:
                 json.dump(fix, f, indent=1, sort_keys=True)
             if name in FULL:

@@ -27,6 +27,10 @@ parity consequence:
 * ``backpressure``  sockets that stop accepting writes mid-tick (QTSS_WouldBlock): bookmarks
                     at the blocked packet, Q9 relocation to the newest key frame after 2 s,
                     RTCP sub-streams, an RTP-Info player blocked before its first write.
+* ``udppush``       UDP pushers (datagrams with source addresses on bound even/odd ports):
+                    the RTCP SR-only gate (Q14), the pusher's RTCP address learnt from the
+                    first datagram and moved by later SRs (NAT_WORKAROUND), and the receiver
+                    reports with the eye count sent to it every 5 s.
 """
 from __future__ import annotations
 
@@ -46,18 +50,22 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
     and ticks.  Within one tick interval the order is: packets (time order, session order),
     then joins, then the tick's socket budgets (BLOCK), then the TICK at the interval end."""
+    # a packet (t, ch, data, addr, port) is a UDP datagram from a pusher (UPKT)
     pkts = []
     for s, lst in enumerate(per_session):
-        for k, (t, ch, data) in enumerate(lst):
-            pkts.append((t, s, k, ch, data))
+        for k, p in enumerate(lst):
+            pkts.append((p[0], s, k) + tuple(p[1:]))
     pkts.sort(key=lambda x: (x[0], x[1], x[2]))
     joins = sorted(joins)
     ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
     i = j = 0
     for tt in ticks:
         while i < len(pkts) and pkts[i][0] <= tt:
-            t, s, _, ch, data = pkts[i]
-            tr.pkt(t, s, ch, data)
+            t, s, _, ch, data = pkts[i][:5]
+            if len(pkts[i]) > 5:
+                tr.upkt(t, s, ch, pkts[i][5], pkts[i][6], data)
+            else:
+                tr.pkt(t, s, ch, data)
             i += 1
         while j < len(joins) and joins[j][0] <= tt:
             t, s, sub, transport = joins[j][:4]
@@ -335,8 +343,67 @@ def backpressure() -> Trace:
     return _assemble(tr, [pk0, pk1], 100, 8000, joins, tick_times=ticks, blocks=blocks)
 
 
+def _ip(a, b, c, d):
+    return a << 24 | b << 16 | c << 8 | d
+
+
+def udppush() -> Trace:
+    """UDP pushers: datagrams read from bound sockets with the
+    pusher's address (ReflectorSocket::ProcessPacket, ReflectorStream.cpp:1769-1875).
+
+    * session 0 (H.264 + PCMA, SRs every 700 ms): RTP from an even port (RTCP address =
+      port + 1), SRs from the odd port, a NAT rebinding that moves the SRs to a new port,
+      a receiver report (PT 201) and a truncated SR from elsewhere (rejected by the SR-only
+      gate, Q14, so they neither relay nor move the address), an SR with a foreign SSRC
+      (zero-length after the SSRC filter, but it still moves the address) and an oversized
+      datagram (clamped to 2060);
+    * session 1 (audio only): RTP from an odd port (no +1), first datagram only after the
+      first 5 s report time, so that report is skipped and the timer still restarts;
+    * session 2: an RTSP-interleaved (TCP) push, which never learns an address: no reports;
+    * session 3: 130 subscribers, so the eye count has bit 7 set, which the reference's
+      ``htonl(n) & 0x7fffffff`` clears on a little-endian host (ReflectorStream.cpp:519-521).
+    Subscribers join over time, so the reports' eye counts change (ReflectorSession.cpp:
+    215-268)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 80))
+    dur = 16_500
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=500_000, gop=30, idr_bytes=6_000,
+                   rtcp_every_ms=700),
+         TrackSpec("audio", "PCMA/8000", 8)]
+    a = [TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    tr.add_session(make_sdp(v), udp_push=True)
+    tr.add_session(make_sdp(a), udp_push=True)
+    tr.add_session(make_sdp(a))
+    tr.add_session(make_sdp(a), udp_push=True)
+    src0, src1 = _ip(10, 0, 0, 5), _ip(192, 168, 7, 21)
+    pk0 = []
+    for t, ch, data in session_packets(v, dur, SEED_BASE + 81):
+        port = 6000 + (ch & 1)
+        if ch & 1 and t >= 7000:
+            port = 7001                                   # NAT rebinding of the SR flow
+        pk0.append((t, ch, data, src0, port))
+    ssrc_v = struct.unpack(">I", pk0[0][2][8:12])[0]
+    pk0 += [
+        (2050, 1, struct.pack(">BBHI", 0x81, 201, 7, 0x1234) + bytes(24), _ip(10, 9, 9, 9), 9999),
+        (2150, 1, rtcp_sr(ssrc_v, 2150, 0, 1, 1)[:20], _ip(10, 9, 9, 9), 9999),   # truncated
+        (3050, 0, rtp_header(1, 0, ssrc_v, 96, False) + b"\x41" * 50, _ip(10, 1, 1, 1), 4000),
+        (14750, 1, rtcp_sr(0x0BADF00D, 14750, 0, 1, 1), src0, 8001),   # foreign SSRC
+        (12550, 0, rtp_header(2, 0, ssrc_v, 96, False) + b"\x41" +
+         rng.integers(0, 256, size=2999, dtype=np.uint8).tobytes(), src0, 6000),
+    ]
+    pk0.sort(key=lambda p: p[0])
+    pk1 = [(t, ch, data, src1, 5001) for t, ch, data in session_packets(a, dur, SEED_BASE + 82, t0=6000)
+           if t >= 6000]
+    pk2 = session_packets(a, dur, SEED_BASE + 83)
+    pk3 = [(t, 0, rtp_header(t // 100, t * 8, 0x3333, 0, False) + bytes(40), _ip(172, 16, 0, 3), 30000)
+           for t in range(0, 5301, 100)]
+    joins = [(0, 0, 1, UDP), (3000, 0, 2, TCP), (9000, 0, 3, UDP), (500, 1, 4, UDP),
+             (12000, 1, 5, TCP), (0, 2, 6, UDP)] + [(0, 3, 1000 + k, UDP) for k in range(130)]
+    return _assemble(tr, [pk0, pk1, pk2, pk3], 100, dur, joins)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
-    "backpressure": backpressure,
+    "backpressure": backpressure, "udppush": udppush,
 }

@@ -50,11 +50,14 @@ int main(void) {
          sizeof(edgpu_tick_stats));
   printf("%zu %zu %zu %zu\n", offsetof(edgpu_config, video_ring_bytes), offsetof(edgpu_config, max_batch_bytes),
          offsetof(edgpu_pkt_desc, arrival_ms), offsetof(edgpu_substream_out, out_base));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(edgpu_udp_source), offsetof(edgpu_udp_source, addr),
+         offsetof(edgpu_udp_source, head), sizeof(edgpu_source_report), offsetof(edgpu_source_report, len),
+         offsetof(edgpu_source_report, bytes));
   return 0;
 }''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
-    a, b = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:2]
+    a, b, c = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:3]
     sizes = [int(x) for x in a.split()]
     offs = [int(x) for x in b.split()]
     assert sizes == [ctypes.sizeof(edgpu.Config), ctypes.sizeof(edgpu.PktDesc), ctypes.sizeof(edgpu.OutDesc),
@@ -64,6 +67,9 @@ int main(void) {
                     edgpu.PktDesc.arrival_ms.offset, edgpu.SubstreamOut.out_base.offset]
     assert sizes[1] == edgpu.PKT_DTYPE.itemsize and sizes[2] == edgpu.OUT_DTYPE.itemsize
     assert sizes[3] == edgpu.SUB_DTYPE.itemsize
+    u, r = edgpu.UDP_SOURCE_DTYPE, edgpu.SOURCE_REPORT_DTYPE
+    assert [int(x) for x in c.split()] == [u.itemsize, u.fields["addr"][1], u.fields["head"][1],
+                                           r.itemsize, r.fields["len"][1], r.fields["bytes"][1]]
 
 
 def test_no_device_fails_loudly():

@@ -55,7 +55,7 @@ def test_port_matches_golden_digests(name, oracle_bins, tmp_path):
     assert hashlib.sha256(cap).hexdigest() == fix["capture_sha256"]
 
 
-@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor", "rtpinfo", "backpressure"])
+@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor", "rtpinfo", "backpressure", "udppush"])
 def test_reference_harness_reproduces_fixture(name, oracle_bins, tmp_path):
     if oracle_bins["ref"] is None:
         pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")
@@ -92,3 +92,25 @@ def test_rtp_info_players_start_later_and_deferred_plays_drop():
     assert sub["3/0/0"][0] < sub["4/0/0"][0]          # same join tick, vlc vs plain (video)
     assert sub["3/1/0"][0] < sub["4/1/0"][0]          # and the audio anchor start
     assert sub["1/0/0"][0] == sub["2/0/0"][0]          # at the first packets both see everything
+
+
+def test_udppush_reports_pin_reference_quirks():
+    """The reference's receiver reports to UDP pushers (fixture from the real reflector):
+    the 5-s timer, the NAT_WORKAROUND address moves, the SR-only gate and the eye-count
+    masking all show in the committed reports."""
+    rr = _fix("udppush")["source_reports"]
+    by = {(t, s, trk): (addr, port, bytes.fromhex(h)) for t, s, trk, addr, port, h in rr}
+    assert sorted({t for t, *_ in rr}) == [5100, 10200, 15300]      # now > last + 5000
+    assert not any(s == 2 for _, s, *_ in rr)                       # TCP push: no address
+    assert (5100, 1, 0) not in by and (10200, 1, 0) in by           # timer ran before the 1st packet
+    src0 = 10 << 24 | 5
+    assert by[(5100, 0, 0)][:2] == (src0, 6001)                     # even RTP port + 1
+    assert by[(10200, 0, 0)][:2] == (src0, 7001)                    # SRs moved it (NAT)
+    assert by[(15300, 0, 0)][:2] == (src0, 8001)                    # foreign-SSRC SR still moves it
+    assert by[(10200, 1, 0)][1] == 5001                             # odd RTP port: no + 1
+    eye = lambda b: int.from_bytes(b[-12:-8], "big")               # noqa: E731
+    assert [eye(by[(t, 0, 0)][2]) for t in (5100, 10200, 15300)] == [2, 3, 3]
+    assert eye(by[(5100, 3, 0)][2]) == 130 & ~0x80                  # htonl(n) & 0x7fffffff on LE
+    b = by[(5100, 0, 0)][2]
+    assert b[:4] == bytes.fromhex("80c90001") and b[16:24] == b"\x01\x05QTSS0\x00"
+    assert len(b) == 16 + 36 + 12

@@ -2,7 +2,8 @@
 // event trace, the way the reflector module would: PKT -> Reflector::PushPacket (track =
 // channel/2, RTCP = channel&1, as ProcessRTPData does, QTSSReflectorModule.cpp:654-671),
 // JOIN -> AddOutput, TICK -> ReflectPackets(now, sink), BLOCK -> the sink returns kWouldBlock
-// after the scripted number of writes in the next tick.  Writes the capture format of
+// after the scripted number of writes in the next tick, UPKT (UDP push) -> ProcessUDPPacket;
+// receiver reports reach the sink's SendReceiverReport.  Writes the capture format of
 // easydarwin_amd/trace.py so tests compare it with the reference harness byte for byte.
 // Usage: adapter_replay <trace.edtr> <capture.edcp>
 #include <cstdio>
@@ -18,8 +19,16 @@ using namespace edgpu_reflector;
 
 struct Rec { uint32_t sub = 0, session = 0; bool tcp = false; std::string img[2]; uint64_t n[2] = {0, 0}; };
 
+struct Report { int64_t t; uint32_t session; uint16_t track; uint32_t addr; uint16_t port; std::string bytes; };
+
 class CaptureSink : public OutputSink {
 public:
+    std::vector<Report> reports;
+    int64_t now = 0;
+    void SendReceiverReport(uint32_t session, uint16_t track, uint32_t addr, uint16_t port, const uint8_t* rr,
+                            uint32_t len) override {
+        reports.push_back(Report{now, session, track, addr, port, std::string((const char*)rr, len)});
+    }
     std::map<std::pair<uint32_t, uint16_t>, Rec>* recs;      // (handle, track)
     std::map<std::tuple<uint32_t, uint16_t, int>, int64_t> budget;   // BLOCK: writes left this tick
     int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
@@ -52,11 +61,19 @@ int main(int argc, char** argv) {
     get(ver); get(nsess);
     Reflector R;
     if (R.Status()) { fprintf(stderr, "edgpu: %s\n", edgpu_last_error()); return 3; }
+    uint32_t rand_calls = 0;                  // the harness's deterministic rand() (trace.py rr_ssrc)
     for (uint32_t s = 0; s < nsess; s++) {
         uint32_t n; get(n);
         uint32_t sid;
-        if (R.SetupReflectorSession(std::string((const char*)&d[p], n), false, &sid)) return 3;
+        std::string sdp((const char*)&d[p], n);
         p += n;
+        uint8_t fl = 0;
+        if (ver >= 2) get(fl);
+        if (R.SetupReflectorSession(sdp, (fl & 1) != 0, &sid)) return 3;
+        for (uint32_t x = 0; x < R.GetNumStreams(sid); x++) {
+            const uint32_t k = rand_calls++;
+            if (R.SetSourceIdentity(sid, x, ((k + 1) * 0x9E3779B1u + 0x7F4A7C15u) & 0x7FFFFFFFu, 0)) return 3;
+        }
     }
     std::map<std::pair<uint32_t, uint16_t>, Rec> recs;
     std::map<uint32_t, std::tuple<uint32_t, uint32_t, bool>> handles;   // handle -> (sub, session, tcp)
@@ -86,7 +103,13 @@ int main(int argc, char** argv) {
             }
             handles[h] = std::make_tuple(sub, s, tr != 0);
             for (uint16_t x = 0; x < R.GetNumStreams(s); x++) recs[{h, x}];
+        } else if (type == 5) {               // UPKT: a UDP pusher's datagram
+            uint32_t s, addr, len; uint8_t ch; uint16_t port;
+            get(s); get(ch); get(addr); get(port); get(len);
+            R.ProcessUDPPacket(s, ch / 2, ch & 1, (const char*)&d[p], len, addr, port, t);
+            p += len;
         } else if (type == 3) {
+            sink.now = t;
             int err = R.ReflectPackets(t, &sink);
             if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
             sink.budget.clear();
@@ -120,6 +143,17 @@ int main(int argc, char** argv) {
             fwrite(&kind, 1, 1, o); fwrite(&tcp, 1, 1, o); fwrite(&np, 8, 1, o); fwrite(&nb, 8, 1, o);
             fwrite(r.img[k].data(), 1, nb, o);
         }
+    if (!sink.reports.empty()) {              // EDRR trailer
+        fwrite("EDRR", 1, 4, o);
+        uint32_t m = (uint32_t)sink.reports.size();
+        fwrite(&m, 4, 1, o);
+        for (auto& rr : sink.reports) {
+            uint32_t ln = (uint32_t)rr.bytes.size();
+            fwrite(&rr.t, 8, 1, o); fwrite(&rr.session, 4, 1, o); fwrite(&rr.track, 2, 1, o);
+            fwrite(&rr.addr, 4, 1, o); fwrite(&rr.port, 2, 1, o); fwrite(&ln, 4, 1, o);
+            fwrite(rr.bytes.data(), 1, ln, o);
+        }
+    }
     fclose(o);
     return 0;
 }
