@@ -277,30 +277,60 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         __syncthreads();
         // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
-        if (P.copy_mode == 0) {
+        if (P.copy_mode == 0 && P.src_addr) {          // frames inside the TCP byte stream
             const int lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += kIngestThreads / 64) {
                 const uint32_t sb = p_slotb[p];
                 if (sb == 0) continue;
                 const uint32_t s = p_snd[p];
                 const uint8_t* sp = reinterpret_cast<const uint8_t*>(p_src[p]);
-                const u32x4* src = reinterpret_cast<const u32x4*>(sp);
                 u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
                 const uint64_t w0 = p_vb[p] >> 4;
                 const uint32_t wm = s_wmask[s];
-                if (P.src_addr) {                          // a frame inside the TCP byte stream
-                    const uint8_t* lim = sp + 4 + p_len[p];
-                    for (uint32_t w = lane; w < sb / 16; w += 64) {
-                        u32x4 v = load16_unaligned(sp + 16 * w, lim);
-                        if (w == 0) v.x = slot_header(p_len[p]);
-                        ring[(w0 + w) & wm] = v;
-                    }
-                } else {
-                    for (uint32_t w = lane; w < sb / 16; w += 64) {
-                        u32x4 v = src[w];
-                        if (w == 0) v.x = slot_header(p_len[p]);
-                        ring[(w0 + w) & wm] = v;
-                    }
+                const uint8_t* lim = sp + 4 + p_len[p];
+                for (uint32_t w = lane; w < sb / 16; w += 64) {
+                    u32x4 v = load16_unaligned(sp + 16 * w, lim);
+                    if (w == 0) v.x = slot_header(p_len[p]);
+                    ring[(w0 + w) & wm] = v;
+                }
+            }
+        } else if (P.copy_mode == 0) {
+            // Two packets per wave per round, and a slot is at most 129 words (2060 + 4 B), so
+            // every lane issues all of its loads (<= 6 x 16 B) before its first store: a wave
+            // keeps two whole slots in flight instead of waiting out one load latency per 64
+            // words of one slot.
+            const int lane = tid & 63, wid = tid >> 6;
+            constexpr uint32_t kW = kIngestThreads / 64;
+            for (uint32_t p = wid; p < n; p += 2 * kW) {
+                const uint32_t q = p + kW;
+                const uint32_t na = p_slotb[p] / 16, nb = q < n ? p_slotb[q] / 16 : 0u;
+                const u32x4* sa = reinterpret_cast<const u32x4*>(p_src[p]);
+                const u32x4* sbp = reinterpret_cast<const u32x4*>(q < n ? p_src[q] : 0ull);
+                const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+                u32x4 a0 = z, a1 = z, a2 = z, b0 = z, b1 = z, b2 = z;
+                if (lane < na) a0 = sa[lane];
+                if (lane + 64 < na) a1 = sa[lane + 64];
+                if (lane + 128 < na) a2 = sa[lane + 128];
+                if (lane < nb) b0 = sbp[lane];
+                if (lane + 64 < nb) b1 = sbp[lane + 64];
+                if (lane + 128 < nb) b2 = sbp[lane + 128];
+                if (na) {
+                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[p]]);
+                    const uint64_t w0 = p_vb[p] >> 4;
+                    const uint32_t wm = s_wmask[p_snd[p]];
+                    if (lane == 0) a0.x = slot_header(p_len[p]);
+                    if (lane < na) ring[(w0 + lane) & wm] = a0;
+                    if (lane + 64 < na) ring[(w0 + lane + 64) & wm] = a1;
+                    if (lane + 128 < na) ring[(w0 + lane + 128) & wm] = a2;
+                }
+                if (nb) {
+                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[q]]);
+                    const uint64_t w0 = p_vb[q] >> 4;
+                    const uint32_t wm = s_wmask[p_snd[q]];
+                    if (lane == 0) b0.x = slot_header(p_len[q]);
+                    if (lane < nb) ring[(w0 + lane) & wm] = b0;
+                    if (lane + 64 < nb) ring[(w0 + lane + 64) & wm] = b1;
+                    if (lane + 128 < nb) ring[(w0 + lane + 128) & wm] = b2;
                 }
             }
         } else if (valid) {
