@@ -288,11 +288,16 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
                 const uint64_t w0 = p_vb[p] >> 4;
                 const uint32_t wm = s_wmask[s];
                 const uint8_t* lim = sp + 4 + p_len[p];
-                for (uint32_t w = lane; w < sb / 16; w += 64) {
-                    u32x4 v = load16_unaligned(sp + 16 * w, lim);
-                    if (w == 0) v.x = slot_header(p_len[p]);
-                    ring[(w0 + w) & wm] = v;
-                }
+                // all of a lane's (<= 3) words are loaded before its first store, as below
+                const uint32_t nw = sb / 16;
+                const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+                u32x4 v0 = lane < nw ? load16_unaligned(sp + 16 * lane, lim) : z;
+                const u32x4 v1 = lane + 64 < nw ? load16_unaligned(sp + 16 * (lane + 64), lim) : z;
+                const u32x4 v2 = lane + 128 < nw ? load16_unaligned(sp + 16 * (lane + 128), lim) : z;
+                if (lane == 0) v0.x = slot_header(p_len[p]);
+                if (lane < nw) ring[(w0 + lane) & wm] = v0;
+                if (lane + 64 < nw) ring[(w0 + lane + 64) & wm] = v1;
+                if (lane + 128 < nw) ring[(w0 + lane + 128) & wm] = v2;
             }
         } else if (P.copy_mode == 0) {
             // Two packets per wave per round, and a slot is at most 129 words (2060 + 4 B), so
