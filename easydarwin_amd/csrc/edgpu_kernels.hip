@@ -694,30 +694,37 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             P.fansub[pos] = f;
         }
     }
-    // work items: thread q doubles as sender q
-    if (q < P.T.nsenders) {
-        const SenderDev& D = P.senders[q];
+    // work items: one wave per sender (waves stride over senders), one lane per chunk.  Chunk
+    // k covers packets [umin + k * chunk, min(umin + (k + 1) * chunk, head)), so every lane
+    // loads its two boundary records at once instead of walking the chunks one by one.
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; s < P.T.nsenders; s += nwaves) {
+        const SenderDev& D = P.senders[s];
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+        const uint64_t head = D.head, umin = D.umin, vend = D.vbyte_end;
+        const uint32_t nch = D.nchunks, chunk_base = D.chunk_base, pkmask = D.pk_mask;
+        if (lane == 0) {
+            SenderDev& Dw = P.senders[s];
+            Dw.fan_lo = nch ? umin : head;
+            Dw.fan_vlo = nch ? meta[umin & pkmask].vbyte : vend;
+        }
         FanWork it;
-        it.ring = D.ring; it.meta = D.meta; it.wmask = D.word_mask; it.pkmask = D.pk_mask;
-        it.sender = q; it.qb = P.sub_range[2 * q]; it.qe = P.sub_range[2 * q + 1];
-        const uint64_t head = D.head;
-        uint64_t lo = D.umin;
-        PktMeta m = meta[lo & D.pk_mask];
-        SenderDev& Dw = P.senders[q];
-        Dw.fan_lo = D.nchunks ? lo : head;
-        Dw.fan_vlo = D.nchunks ? m.vbyte : D.vbyte_end;
-        for (uint32_t k = 0; k < D.nchunks; k++) {
+        it.ring = D.ring; it.meta = D.meta; it.wmask = D.word_mask; it.pkmask = pkmask;
+        it.sender = s; it.qb = P.sub_range[2 * s]; it.qe = P.sub_range[2 * s + 1];
+        for (uint32_t k = lane; k < nch; k += 64) {
+            const uint64_t lo = umin + (uint64_t)k * P.T.chunk;
             const uint64_t hi = min(lo + P.T.chunk, head);
-            const PktMeta mn = hi < head ? meta[hi & D.pk_mask] : PktMeta{D.vbyte_end, 0, 0, 0, 0};
+            const PktMeta& m = meta[lo & pkmask];
+            const uint64_t vb0 = m.vbyte;
+            const uint32_t vc0 = m.vcount;
+            const uint64_t vb1 = hi < head ? meta[hi & pkmask].vbyte : vend;
             it.np = (uint32_t)(hi - lo);
-            it.nw = (uint32_t)((mn.vbyte - m.vbyte) >> 4);
-            it.vc0 = m.vcount;
+            it.nw = (uint32_t)((vb1 - vb0) >> 4);
+            it.vc0 = vc0;
             it.lo = lo;
-            it.vb0 = m.vbyte;
-            P.work[D.chunk_base + k] = it;
-            lo = hi;
-            m = mn;
+            it.vb0 = vb0;
+            P.work[chunk_base + k] = it;
         }
     }
 }
