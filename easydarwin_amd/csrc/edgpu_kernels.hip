@@ -591,12 +591,30 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
     if (threadIdx.x == 0) { P.blk_bytes[blockIdx.x] = tb; P.blk_count[blockIdx.x] = tc; }
 }
 
+// Inclusive scan over a workgroup of up to 1024 threads: shuffles inside each wave, then the
+// wave totals (wsum, one per wave) through LDS.  Every thread of the block must call it.
+template <typename T>
+__device__ __forceinline__ T wave_block_inclusive_scan(T v, T* wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    T base = 0;
+    for (int i = 0; i < w; i++) base += wsum[i];
+    __syncthreads();                                  // wsum may be reused by the next call
+    return v + base;
+}
+
 // K3: single workgroup -- scans over K2 block partials and over senders' chunk counts.
 __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
     const int tid = threadIdx.x;
     const int nt = blockDim.x;
-    __shared__ uint64_t sh64[1024];
-    __shared__ uint32_t sh32[1024];
+    __shared__ uint64_t sh64[16];
+    __shared__ uint32_t sh32[16];
     // (a) block partial scan
     {
         const uint32_t n = P.T.nsub_blocks;
@@ -604,24 +622,18 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
         const uint32_t b0 = tid * per, b1 = min(n, b0 + per);
         uint64_t sbytes = 0; uint32_t scount = 0;
         for (uint32_t i = b0; i < b1; i++) { sbytes += P.blk_bytes[i]; scount += P.blk_count[i]; }
-        sh64[tid] = sbytes; sh32[tid] = scount;
-        __syncthreads();
-        for (int o = 1; o < nt; o <<= 1) {
-            uint64_t y = tid >= o ? sh64[tid - o] : 0; uint32_t z = tid >= o ? sh32[tid - o] : 0;
-            __syncthreads();
-            sh64[tid] += y; sh32[tid] += z;
-            __syncthreads();
-        }
-        uint64_t rb = sh64[tid] - sbytes; uint32_t rc = sh32[tid] - scount;
+        const uint64_t ib = wave_block_inclusive_scan<uint64_t>(sbytes, sh64);
+        const uint32_t ic = wave_block_inclusive_scan<uint32_t>(scount, sh32);
+        uint64_t rb = ib - sbytes; uint32_t rc = ic - scount;
         for (uint32_t i = b0; i < b1; i++) {
             P.blk_bytes_base[i] = rb; P.blk_count_base[i] = rc;
             rb += P.blk_bytes[i]; rc += P.blk_count[i];
         }
         if (tid == nt - 1) {
-            P.totals->arena_bytes = sh64[tid];
-            P.totals->relayed_packets = sh32[tid];
-            P.totals->cum_relayed_packets += sh32[tid];
-            if (sh64[tid] > P.T.arena_bytes || sh32[tid] > P.T.max_desc)
+            P.totals->arena_bytes = ib;
+            P.totals->relayed_packets = ic;
+            P.totals->cum_relayed_packets += ic;
+            if (ib > P.T.arena_bytes || ic > P.T.max_desc)
                 atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
         }
         __syncthreads();
@@ -637,15 +649,8 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
             const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
             sum += (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
         }
-        sh32[tid] = sum;
-        __syncthreads();
-        for (int o = 1; o < nt; o <<= 1) {
-            uint32_t z = tid >= o ? sh32[tid - o] : 0;
-            __syncthreads();
-            sh32[tid] += z;
-            __syncthreads();
-        }
-        uint32_t r = sh32[tid] - sum;
+        const uint32_t isum = wave_block_inclusive_scan<uint32_t>(sum, sh32);
+        uint32_t r = isum - sum;
         for (uint32_t s = s0; s < s1; s++) {
             SenderDev& D = P.senders[s];
             const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
@@ -653,7 +658,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
             D.chunk_base = r; D.nchunks = k;
             r += k;
         }
-        if (tid == nt - 1) P.totals->nwork = sh32[tid];
+        if (tid == nt - 1) P.totals->nwork = isum;
     }
 }
 
