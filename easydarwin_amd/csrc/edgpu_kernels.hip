@@ -1238,7 +1238,7 @@ __device__ __forceinline__ void fan5_stage(const FanWork& it, int tid, u32x4* im
     }
 }
 
-template <int THREADS, int CHUNK>
+template <int THREADS, int CHUNK, int AUX = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
 void k_fanout5(FanoutParams P) {
     using F = Fan5<THREADS, CHUNK>;
@@ -1316,7 +1316,7 @@ void k_fanout5(FanoutParams P) {
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
                 u32x4 v = cb[srcc];
                 if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
-                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, AUX);
             }
         }
         // ---- descriptors: one wave per sub-stream, 128-B-aligned windows ----
@@ -1597,13 +1597,18 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 32, 2, 1>, 1024, 32, fanout4_lds<1024, 32>()},    // 13 nt arena + descriptors
     {(const void*)k_fanout4<1024, 32, 2, 1, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 14 ... + nt chunk loads
     {(const void*)k_fanout4<1024, 32, 2, 0, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 15 nt arena + nt loads
+    {(const void*)k_fanout5<256, 32, 2>, 256, 32, fanout5_lds<256, 32>()},          // 16 LDS-DMA + nt arena
+    {(const void*)k_fanout5<512, 32, 2>, 512, 32, fanout5_lds<512, 32>()},          // 17
+    {(const void*)k_fanout4<512, 32, 2>, 512, 32, fanout4_lds<512, 32>()},          // 18 nt, 512 threads
+    {(const void*)k_fanout4<1024, 16, 2>, 1024, 16, fanout4_lds<1024, 16>()},       // 19 nt, 16-packet chunks
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
                                             "k_fanout5<256,32>", "k_fanout5<512,32>", "k_fanout5<128,16>", "k_fanout5<256,16>",
                                             "k_fanout4<1024,32,nt>", "k_fanout4<1024,32,sc1>", "k_fanout4<1024,32,sc0sc1>",
                                             "k_fanout4<1024,32,nt,ntdesc>", "k_fanout4<1024,32,nt,ntdesc,ntload>",
-                                            "k_fanout4<1024,32,nt,ntload>"};
+                                            "k_fanout4<1024,32,nt,ntload>", "k_fanout5<256,32,nt>", "k_fanout5<512,32,nt>",
+                                            "k_fanout4<512,32,nt>", "k_fanout4<1024,16,nt>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 int fanout_chunk(int variant) {
