@@ -112,6 +112,9 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
 // Ingest
 // =========================================================================================
 
+// DEPTH: packets per wave per slot-copy round; 4 by default (125 VGPRs, still 4 waves/SIMD),
+// EDGPU_INGEST_DEPTH=2 for A/B runs
+template <uint32_t DEPTH>
 __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     const uint32_t seg = blockIdx.x;
     const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
@@ -300,42 +303,37 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
                 if (lane + 128 < nw) ring[(w0 + lane + 128) & wm] = v2;
             }
         } else if (P.copy_mode == 0) {
-            // Two packets per wave per round, and a slot is at most 129 words (2060 + 4 B), so
-            // every lane issues all of its loads (<= 6 x 16 B) before its first store: a wave
-            // keeps two whole slots in flight instead of waiting out one load latency per 64
-            // words of one slot.
-            const int lane = tid & 63, wid = tid >> 6;
-            constexpr uint32_t kW = kIngestThreads / 64;
-            for (uint32_t p = wid; p < n; p += 2 * kW) {
-                const uint32_t q = p + kW;
-                const uint32_t na = p_slotb[p] / 16, nb = q < n ? p_slotb[q] / 16 : 0u;
-                const u32x4* sa = reinterpret_cast<const u32x4*>(p_src[p]);
-                const u32x4* sbp = reinterpret_cast<const u32x4*>(q < n ? p_src[q] : 0ull);
-                const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-                u32x4 a0 = z, a1 = z, a2 = z, b0 = z, b1 = z, b2 = z;
-                if (lane < na) a0 = sa[lane];
-                if (lane + 64 < na) a1 = sa[lane + 64];
-                if (lane + 128 < na) a2 = sa[lane + 128];
-                if (lane < nb) b0 = sbp[lane];
-                if (lane + 64 < nb) b1 = sbp[lane + 64];
-                if (lane + 128 < nb) b2 = sbp[lane + 128];
-                if (na) {
-                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[p]]);
-                    const uint64_t w0 = p_vb[p] >> 4;
-                    const uint32_t wm = s_wmask[p_snd[p]];
-                    if (lane == 0) a0.x = slot_header(p_len[p]);
-                    if (lane < na) ring[(w0 + lane) & wm] = a0;
-                    if (lane + 64 < na) ring[(w0 + lane + 64) & wm] = a1;
-                    if (lane + 128 < na) ring[(w0 + lane + 128) & wm] = a2;
+            // kDepth packets per wave per round, and a slot is at most 129 words (2060 + 4 B),
+            // so every lane issues all of its loads (<= 3 x 16 B per packet) before its first
+            // store: a wave keeps kDepth whole slots in flight instead of waiting out one load
+            // latency per 64 words of one slot.
+            constexpr uint32_t kDepth = DEPTH, kW = kIngestThreads / 64;
+            const uint32_t lane = tid & 63, wid = tid >> 6;
+            for (uint32_t p = wid; p < n; p += kDepth * kW) {
+                uint32_t nw[kDepth];
+                u32x4 v[kDepth][3];
+#pragma unroll
+                for (uint32_t d = 0; d < kDepth; d++) {
+                    const uint32_t pd = p + d * kW;
+                    nw[d] = pd < n ? p_slotb[pd] / 16 : 0u;
+                    const u32x4* sp = reinterpret_cast<const u32x4*>(pd < n ? p_src[pd] : 0ull);
+#pragma unroll
+                    for (uint32_t k = 0; k < 3; k++) {
+                        v[d][k] = u32x4{0u, 0u, 0u, 0u};
+                        if (lane + 64 * k < nw[d]) v[d][k] = sp[lane + 64 * k];
+                    }
                 }
-                if (nb) {
-                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[q]]);
-                    const uint64_t w0 = p_vb[q] >> 4;
-                    const uint32_t wm = s_wmask[p_snd[q]];
-                    if (lane == 0) b0.x = slot_header(p_len[q]);
-                    if (lane < nb) ring[(w0 + lane) & wm] = b0;
-                    if (lane + 64 < nb) ring[(w0 + lane + 64) & wm] = b1;
-                    if (lane + 128 < nb) ring[(w0 + lane + 128) & wm] = b2;
+#pragma unroll
+                for (uint32_t d = 0; d < kDepth; d++) {
+                    if (nw[d] == 0) continue;
+                    const uint32_t pd = p + d * kW;
+                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[pd]]);
+                    const uint64_t w0 = p_vb[pd] >> 4;
+                    const uint32_t wm = s_wmask[p_snd[pd]];
+                    if (lane == 0) v[d][0].x = slot_header(p_len[pd]);
+#pragma unroll
+                    for (uint32_t k = 0; k < 3; k++)
+                        if (lane + 64 * k < nw[d]) ring[(w0 + lane + 64 * k) & wm] = v[d][k];
                 }
             }
         } else if (valid) {
@@ -1533,7 +1531,9 @@ namespace edgpu {
 
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ingest, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
+    if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     if (p.npk && p.copy_mode == 1) {
         const uint32_t per = kCopyThreads / kCopyLanes;
         hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
