@@ -475,10 +475,31 @@ __device__ uint64_t lower_bound_meta(const PktMeta* meta, uint32_t mask, uint64_
     return lo;
 }
 
-// K1: per sender -- ring tail, fFirstPacketInQueueForNewOutput (ReflectorStream.cpp:1058-1069).
-__global__ void k_plan_senders(PlanParams P) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.T.nsenders) return;
+// lower_bound_meta for a whole wave: each round the 64 lanes probe 64 evenly spaced records
+// and a ballot narrows the range 64-fold, so a 16k-record ring takes 3 dependent loads, not 14.
+// Every lane of the wave must call it with the same arguments; all lanes get the result.
+template <typename Pred>
+__device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, uint64_t lo, uint64_t hi, Pred pred) {
+    const uint64_t lane = threadIdx.x & 63;
+    while (lo < hi) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t probe = min(lo + (lane + 1) * step - 1, hi - 1);
+        const unsigned long long t = __ballot(pred(meta[probe & mask]) ? 1 : 0);
+        if (t == 0) return hi;                               // pred(hi - 1) is false
+        const uint64_t j = (uint64_t)(__ffsll(t) - 1);       // first probe that holds
+        // the answer is in (probe j-1, probe j]: search below probe j, which is the fallback
+        const uint64_t pj = min(lo + (j + 1) * step - 1, hi - 1);
+        lo = j == 0 ? lo : min(lo + j * step - 1, hi - 1) + 1;
+        hi = pj;
+    }
+    return hi;
+}
+
+// K1: per sender, one wave each -- ring tail, fFirstPacketInQueueForNewOutput
+// (ReflectorStream.cpp:1058-1069).
+__global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
+    const uint32_t s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (s >= P.T.nsenders) return;                             // uniform per wave
     SenderDev& D = P.senders[s];
     const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
     const uint64_t head = D.head;
@@ -488,22 +509,24 @@ __global__ void k_plan_senders(PlanParams P) {
     lo = max(lo, D.floor);                                    // a replica holds nothing older
     const uint64_t vend = D.vbyte_end;
     // oldest packet whose slot is still intact in the byte ring
-    uint64_t tail = lower_bound_meta(meta, D.pk_mask, lo, head,
-                                     [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
-    D.tail = tail;
+    const uint64_t tail = wave_lower_bound_meta(meta, D.pk_mask, lo, head,
+                                                [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
     int64_t ns = -1;
     if (D.key >= 0) {
         ns = D.key;
         if ((uint64_t)ns < tail) ns = -2;                      // key packet overwritten
     } else if (head > tail) {
         const int64_t cutoff = P.T.now - P.T.over_buffer_ms;  // now - arrival <= over buffer
-        const uint64_t f = lower_bound_meta(meta, D.pk_mask, tail, head,
-                                            [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        const uint64_t f = wave_lower_bound_meta(meta, D.pk_mask, tail, head,
+                                                 [&](const PktMeta& m) { return m.arrival >= cutoff; });
         if (f < head) ns = (f == tail && tail > D.floor) ? -2 : (int64_t)f;   // -2: window exceeds ring
     }
-    D.new_start = ns;
-    D.umin = head;
-    D.nchunks = 0;
+    if ((threadIdx.x & 63) == 0) {
+        D.tail = tail;
+        D.new_start = ns;
+        D.umin = head;
+        D.nchunks = 0;
+    }
 }
 
 // K2: per sub-stream -- this tick's range and the bookmark / last-id commit
@@ -1565,7 +1588,7 @@ hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t s
 }
 hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     const uint32_t nsb = p.T.nsenders ? (p.T.nsenders + 255) / 256 : 0;
-    if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3(nsb), dim3(256), 0, st, p);
+    if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3((p.T.nsenders + 3) / 4), dim3(256), 0, st, p);
     if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
