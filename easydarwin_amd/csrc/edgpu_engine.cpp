@@ -22,6 +22,7 @@
 
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
+hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
@@ -141,11 +142,11 @@ struct edgpu_ctx {
     hipStream_t copy = nullptr;
     hipEvent_t ev_plan = nullptr, ev_copy = nullptr;
     int cur = 0;                    // output buffer of the current tick (0 / 1)
-    hipEvent_t ev[8] = {};
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
     hipEvent_t hist[4][kHist][2] = {};
     uint32_t hist_n[4] = {0, 0, 0, 0};
+    uint32_t last_slot[4] = {0, 0, 0, 0};   // each ring's newest complete pair (edgpu_last_timings)
     uint64_t fanout_launches = 0;
     int64_t last_now = 0;               // clock of the last edgpu_fanout (backpressure reports)
     bool timed_fanout = false, timed_ingest = false, timed_keyframe = false;
@@ -270,7 +271,6 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipSetDevice(c.device) != hipSuccess) { delete x; return fail(EDGPU_NO_DEVICE, "hipSetDevice failed"); }
     auto bad = [&](const char* what) { edgpu_ctx_destroy(x); return fail(EDGPU_OUT_OF_MEMORY, what); };
     if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return bad("stream");
-    for (auto& e : x->ev) if (hipEventCreate(&e) != hipSuccess) return bad("event");
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (hipEventCreate(&e) != hipSuccess) return bad("event");
     if (dmalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
     if (dmalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
@@ -322,7 +322,6 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
                     (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
         if (p) (void)hipFree(p);
-    for (auto& e : x->ev) if (e) (void)hipEventDestroy(e);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->ev_plan) (void)hipEventDestroy(x->ev_plan);
     if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
@@ -681,7 +680,7 @@ int edgpu_source_identity(edgpu_ctx* x, uint32_t session, uint32_t track, uint32
 static hipError_t hist_mark(edgpu_ctx* x, int w, int end, hipStream_t st = nullptr) {
     const uint32_t slot = x->hist_n[w] % edgpu_ctx::kHist;
     hipError_t e = hipEventRecord(x->hist[w][slot][end], st ? st : x->stream);
-    if (end) x->hist_n[w]++;
+    if (end) { x->last_slot[w] = slot; x->hist_n[w]++; }
     return e;
 }
 
@@ -735,14 +734,12 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;
-    HIP_CHECK(hipMemsetAsync(&x->d_totals->ingested_packets, 0, 2 * sizeof(unsigned long long), x->stream));
-    HIP_CHECK(hipEventRecord(x->ev[4], x->stream));
+    HIP_CHECK(launch_ingest_reset(x->d_totals, x->stream));
     HIP_CHECK(hist_mark(x, 2, 0));
     if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
     if (tcp) HIP_CHECK(launch_deframe_finish(*tcp, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
-    HIP_CHECK(hipEventRecord(x->ev[5], x->stream));
     x->timed_ingest = true;
     x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
     return EDGPU_OK;
@@ -912,11 +909,9 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     KeyframeParams p;
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
-    HIP_CHECK(hipEventRecord(x->ev[6], x->stream));
     HIP_CHECK(hist_mark(x, 3, 0));
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
-    HIP_CHECK(hipEventRecord(x->ev[7], x->stream));
     x->timed_keyframe = true;
     x->pending = false;
     return EDGPU_OK;
@@ -955,10 +950,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
     p.T.chunk = (uint32_t)fanout_chunk(x->fanout_variant);
-    // reset per-tick totals (relayed_*, arena, status, nwork); keep the ingest counters
-    HIP_CHECK(hipMemsetAsync(x->d_totals, 0, 3 * sizeof(unsigned long long), x->stream));
-    HIP_CHECK(hipMemsetAsync(&x->d_totals->status, 0, 2 * sizeof(int), x->stream));
-    HIP_CHECK(hipEventRecord(x->ev[0], x->stream));
+    // the per-tick totals (relayed_*, arena, status, nwork) are reset by the plan's first kernel
     HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));
     FanoutParams f;
@@ -974,12 +966,10 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
         HIP_CHECK(hipStreamWaitEvent(x->copy, x->ev_plan, 0));
         cs = x->copy;
     }
-    HIP_CHECK(hipEventRecord(x->ev[1], cs));
     HIP_CHECK(hist_mark(x, 0, 0, cs));
     HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
     HIP_CHECK(hist_mark(x, 1, 1, cs));
-    HIP_CHECK(hipEventRecord(x->ev[2], cs));
     if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_launches++;
     x->timed_fanout = true;
@@ -1060,12 +1050,17 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     HIP_CHECK(hipSetDevice(x->device));
     HIP_CHECK(sync_all(x));
     out_ms[0] = out_ms[1] = out_ms[2] = out_ms[3] = 0.f;
+    // the newest pair of each history ring: every timed point is recorded once per tick (an
+    // event record costs the GPU ~5 us of idle between the kernels around it)
+    auto last = [&](int w, float* o) {
+        return hipEventElapsedTime(o, x->hist[w][x->last_slot[w]][0], x->hist[w][x->last_slot[w]][1]);
+    };
     if (x->timed_fanout) {
-        HIP_CHECK(hipEventElapsedTime(&out_ms[0], x->ev[1], x->ev[2]));
-        HIP_CHECK(hipEventElapsedTime(&out_ms[1], x->ev[0], x->ev[2]));
+        HIP_CHECK(last(0, &out_ms[0]));
+        HIP_CHECK(last(1, &out_ms[1]));
     }
-    if (x->timed_ingest) HIP_CHECK(hipEventElapsedTime(&out_ms[2], x->ev[4], x->ev[5]));
-    if (x->timed_keyframe) HIP_CHECK(hipEventElapsedTime(&out_ms[3], x->ev[6], x->ev[7]));
+    if (x->timed_ingest) HIP_CHECK(last(2, &out_ms[2]));
+    if (x->timed_keyframe) HIP_CHECK(last(3, &out_ms[3]));
     return EDGPU_OK;
 }
 

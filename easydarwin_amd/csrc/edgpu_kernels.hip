@@ -497,7 +497,22 @@ __device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, ui
 
 // K1: per sender, one wave each -- ring tail, fFirstPacketInQueueForNewOutput
 // (ReflectorStream.cpp:1058-1069).
+__device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
+    t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
+    t->status = 0; t->nwork = 0;
+}
+
+// Per-tick counter resets as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
+// kernels): which = 0 fan-out totals (when k_plan_senders, which does it itself, does not run),
+// 1 ingest totals.
+__global__ void k_totals_reset(TickTotals* t, int which) {
+    if (threadIdx.x != 0) return;
+    if (which == 0) reset_tick_totals(t);
+    else { t->ingested_packets = 0; t->ingested_bytes = 0; }
+}
+
 __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) reset_tick_totals(P.totals);   // no later kernel has run
     const uint32_t s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     if (s >= P.T.nsenders) return;                             // uniform per wave
     SenderDev& D = P.senders[s];
@@ -1552,6 +1567,11 @@ __global__ __launch_bounds__(256) void k_image_apply(ImageParams P) {
 // Launch wrappers (internal C++ API used by edgpu_engine.cpp)
 namespace edgpu {
 
+hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st) {
+    hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, totals, 1);
+    return hipGetLastError();
+}
+
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
@@ -1589,6 +1609,7 @@ hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t s
 hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     const uint32_t nsb = p.T.nsenders ? (p.T.nsenders + 255) / 256 : 0;
     if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3((p.T.nsenders + 3) / 4), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 0);
     if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
