@@ -145,7 +145,8 @@ struct edgpu_ctx {
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
     hipEvent_t hist[4][kHist][2] = {};
-    uint32_t hist_n[4] = {0, 0, 0, 0};
+    uint32_t hist_n[4] = {0, 0, 0, 0};      // pairs recorded (monotonic: rings 0 and 1 stay in step)
+    uint32_t hist_rd[4] = {0, 0, 0, 0};     // pairs already returned by edgpu_kernel_times
     uint32_t last_slot[4] = {0, 0, 0, 0};   // each ring's newest complete pair (edgpu_last_timings)
     uint64_t fanout_launches = 0;
     int64_t last_now = 0;               // clock of the last edgpu_fanout (backpressure reports)
@@ -684,6 +685,12 @@ static hipError_t hist_mark(edgpu_ctx* x, int w, int end, hipStream_t st = nullp
     return e;
 }
 
+// End event of a history pair: the whole-tick ring (1) ends where its tick's copy kernel (ring
+// 0, same slot: both advance once per edgpu_fanout) ends, so that point is recorded once.
+static hipEvent_t hist_end(edgpu_ctx* x, int w, uint32_t slot) {
+    return x->hist[w == 1 ? 0 : w][slot][1];
+}
+
 static int rebuild_index(edgpu_ctx* x) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
     std::vector<uint32_t> idx;
@@ -969,7 +976,8 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(hist_mark(x, 0, 0, cs));
     HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
-    HIP_CHECK(hist_mark(x, 1, 1, cs));
+    x->last_slot[1] = x->hist_n[1] % edgpu_ctx::kHist;   // ring 1 ends at ring 0's end event
+    x->hist_n[1]++;
     if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_launches++;
     x->timed_fanout = true;
@@ -1023,14 +1031,14 @@ int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, u
     if (!x || which < 0 || which > 3 || (!out_ms && max_n)) return fail(EDGPU_BAD_ARGUMENT, "bad argument");
     HIP_CHECK(hipSetDevice(x->device));
     HIP_CHECK(sync_all(x));
-    const uint32_t n = std::min<uint32_t>(x->hist_n[which], edgpu_ctx::kHist);
+    const uint32_t n = std::min<uint32_t>(x->hist_n[which] - x->hist_rd[which], edgpu_ctx::kHist);
     const uint32_t first = x->hist_n[which] - n;
     uint32_t k = 0;
     for (uint32_t i = 0; i < n && k < max_n; i++, k++) {
         const uint32_t slot = (first + i) % edgpu_ctx::kHist;
-        HIP_CHECK(hipEventElapsedTime(&out_ms[k], x->hist[which][slot][0], x->hist[which][slot][1]));
+        HIP_CHECK(hipEventElapsedTime(&out_ms[k], x->hist[which][slot][0], hist_end(x, which, slot)));
     }
-    x->hist_n[which] = 0;
+    x->hist_rd[which] = x->hist_n[which];
     if (out_n) *out_n = k;
     return EDGPU_OK;
 }
@@ -1053,7 +1061,7 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     // the newest pair of each history ring: every timed point is recorded once per tick (an
     // event record costs the GPU ~5 us of idle between the kernels around it)
     auto last = [&](int w, float* o) {
-        return hipEventElapsedTime(o, x->hist[w][x->last_slot[w]][0], x->hist[w][x->last_slot[w]][1]);
+        return hipEventElapsedTime(o, x->hist[w][x->last_slot[w]][0], hist_end(x, w, x->last_slot[w]));
     };
     if (x->timed_fanout) {
         HIP_CHECK(last(0, &out_ms[0]));
