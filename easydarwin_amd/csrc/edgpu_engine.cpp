@@ -147,6 +147,7 @@ struct edgpu_ctx {
     hipEvent_t hist[4][kHist][2] = {};
     uint32_t hist_n[4] = {0, 0, 0, 0};      // pairs recorded (monotonic: rings 0 and 1 stay in step)
     uint32_t hist_rd[4] = {0, 0, 0, 0};     // pairs already returned by edgpu_kernel_times
+    uint32_t kf_from[kHist] = {};           // keyframe ring (3) slot -> the ingest slot it starts at
     uint32_t last_slot[4] = {0, 0, 0, 0};   // each ring's newest complete pair (edgpu_last_timings)
     uint64_t fanout_launches = 0;
     int64_t last_now = 0;               // clock of the last edgpu_fanout (backpressure reports)
@@ -691,6 +692,11 @@ static hipEvent_t hist_end(edgpu_ctx* x, int w, uint32_t slot) {
     return x->hist[w == 1 ? 0 : w][slot][1];
 }
 
+// Start event of a history pair: the keyframe ring (3) starts at the end of its ingest (ring 2).
+static hipEvent_t hist_start(edgpu_ctx* x, int w, uint32_t slot) {
+    return w == 3 ? x->hist[2][x->kf_from[slot]][1] : x->hist[w][slot][0];
+}
+
 static int rebuild_index(edgpu_ctx* x) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
     std::vector<uint32_t> idx;
@@ -916,7 +922,8 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     KeyframeParams p;
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
-    HIP_CHECK(hist_mark(x, 3, 0));
+    // the index starts where the ingest it indexes ended: that point is already recorded
+    x->kf_from[x->hist_n[3] % edgpu_ctx::kHist] = x->last_slot[2];
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
     x->timed_keyframe = true;
@@ -1036,7 +1043,7 @@ int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, u
     uint32_t k = 0;
     for (uint32_t i = 0; i < n && k < max_n; i++, k++) {
         const uint32_t slot = (first + i) % edgpu_ctx::kHist;
-        HIP_CHECK(hipEventElapsedTime(&out_ms[k], x->hist[which][slot][0], hist_end(x, which, slot)));
+        HIP_CHECK(hipEventElapsedTime(&out_ms[k], hist_start(x, which, slot), hist_end(x, which, slot)));
     }
     x->hist_rd[which] = x->hist_n[which];
     if (out_n) *out_n = k;
@@ -1061,7 +1068,7 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     // the newest pair of each history ring: every timed point is recorded once per tick (an
     // event record costs the GPU ~5 us of idle between the kernels around it)
     auto last = [&](int w, float* o) {
-        return hipEventElapsedTime(o, x->hist[w][x->last_slot[w]][0], hist_end(x, w, x->last_slot[w]));
+        return hipEventElapsedTime(o, hist_start(x, w, x->last_slot[w]), hist_end(x, w, x->last_slot[w]));
     };
     if (x->timed_fanout) {
         HIP_CHECK(last(0, &out_ms[0]));
