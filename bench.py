@@ -110,9 +110,19 @@ def run_step(ctx: edgpu.Context, bt: dict):
     ctx.fanout(bt["t"])
 
 
-def _sample_trace(args, n_sess=64, dur=3000):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _sample_trace(args, n_sess=64, dur=3000, tick=100):
     """The CPU baseline's bounded sample of the bench workload: n_sess H.264 1080p 4 Mb/s
-    sessions x subs UDP subscribers x dur ms at 100-ms ticks."""
+    sessions x subs UDP subscribers x dur ms at `tick`-ms ticks."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
     from easydarwin_amd.trace import Trace, UDP
@@ -124,7 +134,7 @@ def _sample_trace(args, n_sess=64, dur=3000):
         tr.add_session(make_sdp(tracks))
         per.append(session_packets(tracks, dur, 0xEA5D + 1 + s, t0=(s * 7) % 33))
     joins = [(0, s, s * args.subs + k, UDP) for s in range(n_sess) for k in range(args.subs)]
-    _assemble(tr, per, 100, dur, joins)
+    _assemble(tr, per, tick, dur, joins)
     return tr
 
 
@@ -142,16 +152,11 @@ def _shard(tr, k: int, n: int):
     return out
 
 
-def cpu_baseline_reference(args) -> dict | None:
-    """The REFERENCE reflector itself (oracle/_ref/ref_harness --bench: EasyDarwin's
-    ReflectorStream / ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS
-    server, memcpy sinks) on the same bounded sample, sessions sharded over one process per
-    core, all running at once; value = relayed packets / the longest process's replay time."""
+def _reference_replay(args, tick: int, procs_n: int):
+    """One timed run of the reference reflector on the bounded sample at `tick`-ms ticks:
+    (relayed packets, relayed bytes, longest process seconds, repeats)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    if not os.path.exists(exe):
-        return None
-    procs_n = min(16, os.cpu_count() or 1)
-    tr = _sample_trace(args)
+    tr = _sample_trace(args, tick=tick)
     with tempfile.TemporaryDirectory() as td:
         paths = []
         for k in range(procs_n):
@@ -166,13 +171,37 @@ def cpu_baseline_reference(args) -> dict | None:
         outs = [json.loads(pr.communicate()[0]) for pr in procs]
         if any(pr.returncode for pr in procs):
             return None
-    pk = sum(o["relayed_packets"] for o in outs)
-    secs = max(o["seconds"] for o in outs)
-    return {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
-            "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench, compiled from the reference "
-                      f"sources) on 64 H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x 3 s at 100-ms ticks, "
-                      f"sessions sharded over {procs_n} processes, each replaying its shard {rep} times; "
-                      f"{pk} relayed packets, longest process {secs:.2f} s (memcpy sinks, no sockets)"}
+    return (sum(o["relayed_packets"] for o in outs), sum(o["relayed_bytes"] for o in outs),
+            max(o["seconds"] for o in outs), rep)
+
+
+def cpu_baseline_reference(args) -> dict | None:
+    """The REFERENCE reflector itself (oracle/_ref/ref_harness --bench: EasyDarwin's
+    ReflectorStream / ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS
+    server, memcpy sinks) on the same bounded sample, sessions sharded over one process per
+    core, all running at once; value = relayed packets / the longest process's replay time.
+    Run at 100-ms ticks (the reflector's own wakeup scale, RS.cpp:1125-1131) and at the GPU
+    step's 1000-ms tick."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    procs_n = min(16, os.cpu_count() or 1)
+    r100 = _reference_replay(args, 100, procs_n)
+    r1000 = _reference_replay(args, 1000, procs_n)
+    if r100 is None:
+        return None
+    pk, by, secs, rep = r100
+    out = {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
+           "cpu_model": cpu_model(), "GBps": round(by / secs / 1e9, 3), "tick_ms": 100,
+           "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench, compiled from the reference "
+                     f"sources) on 64 H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x 3 s at 100-ms ticks, "
+                     f"sessions sharded over {procs_n} processes, each replaying its shard {rep} times; "
+                     f"{pk} relayed packets, longest process {secs:.2f} s (memcpy sinks, no sockets)"}
+    if r1000 is not None:
+        pk1, by1, secs1, rep1 = r1000
+        out["tick_1000ms"] = {"value": round(pk1 / secs1, 1), "GBps": round(by1 / secs1 / 1e9, 3),
+                              "relayed_packets": pk1, "seconds": round(secs1, 3), "repeat": rep1}
+    return out
 
 
 def cpu_baseline(args) -> dict | None:
@@ -202,7 +231,7 @@ def cpu_baseline(args) -> dict | None:
                              check=True).stdout
     r = json.loads(out)
     return {"value": round(r["packets_per_s"], 1), "unit": "relayed RTP packets/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "GBps": round(r["relayed_bytes"] / r["seconds"] / 1e9, 3),
             "sample": f"{rep} replays of {n_sess} H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x {dur/1000:.0f} s, "
                       f"100-ms ticks, ingest+fan-out, memcpy sinks (oracle/relay_model --bench); "
                       f"{r['relayed_packets']} relayed packets in {r['seconds']:.2f} s"}
@@ -224,7 +253,17 @@ def main():
                     help="desc: packets handed over as descriptors + slots (edgpu_ingest, the reflector's "
                          "per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP reads, "
                          "deframed on the GPU (edgpu_ingest_interleaved)")
+    ap.add_argument("--ablation-study", action="store_true",
+                    help="allow EDGPU_ABLATE (timing experiments that skip work): the line is then not a "
+                         "valid measurement and says so")
     args = ap.parse_args()
+
+    # Engine switches that change what is measured are recorded in the line; EDGPU_ABLATE skips
+    # work inside the timed region, so a bench under it is refused unless it is an ablation study.
+    knobs = {k: os.environ[k] for k in ("EDGPU_FANOUT", "EDGPU_INGEST_DEPTH", "EDGPU_INGEST", "EDGPU_ABLATE",
+                                        "EDGPU_POISON") if k in os.environ}
+    if "EDGPU_ABLATE" in knobs and not args.ablation_study:
+        raise SystemExit("EDGPU_ABLATE is set: ablations skip work in the timed region (use --ablation-study)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -320,13 +359,19 @@ def main():
     achieved = (alg_bytes / max(launches, 1)) / (fan_ms / 1e3) / 1e9
     # HBM traffic per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
     # kernel and config (tools/profile.sh + tools/summarize_profile.py); null when absent
-    traffic = None
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of exactly this kernel
+    # variant and workload (tools/profile.sh + tools/summarize_profile.py); null otherwise
+    traffic, traffic_source = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
-    if os.path.exists(pmc) and world == 1 and args.subs == 16 and args.sessions == 1024:
+    if os.path.exists(pmc) and world == 1:
         try:
             pj = json.load(open(pmc))
-            if pj.get("fanout_kernel") == ctx.fanout_kernel().split("<")[0]:   # rocprofv3 -T names
+            wl = pj.get("workload", {})
+            if (pj.get("bench_fanout_kernel") == ctx.fanout_kernel() and wl.get("sessions_per_gpu") == args.sessions
+                    and wl.get("subs_per_session") == args.subs and wl.get("ingest") == args.ingest
+                    and wl.get("tick_ms", 1000) == args.tick_ms):
                 traffic = pj.get("hbm_bytes_per_launch")
+                traffic_source = f"profiles/{pj.get('tag')}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes)"
         except Exception:
             traffic = None
     cpu = None
@@ -355,10 +400,12 @@ def main():
                                + (", RTSP-interleaved TCP push reads deframed on the GPU" if args.ingest == "tcp" else ""),
                    "ingest": args.ingest,
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
+                   "tick_ms": args.tick_ms,
+                   "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"},
         "relayed_GBps": round(out_all / dt / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": ctx.fanout_kernel(), "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),
                      "avg_kernel_ms": round(fan_ms, 4)},
         "kernel_ms": {"fanout": round(fan_ms, 4),

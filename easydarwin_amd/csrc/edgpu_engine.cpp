@@ -145,10 +145,18 @@ struct edgpu_ctx {
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
     hipEvent_t hist[4][kHist][2] = {};
-    uint32_t hist_n[4] = {0, 0, 0, 0};      // pairs recorded (monotonic: rings 0 and 1 stay in step)
+    uint32_t hist_n[4] = {0, 0, 0, 0};      // pairs recorded (monotonic sequence numbers)
     uint32_t hist_rd[4] = {0, 0, 0, 0};     // pairs already returned by edgpu_kernel_times
-    uint32_t kf_from[kHist] = {};           // keyframe ring (3) slot -> the ingest slot it starts at
-    uint32_t last_slot[4] = {0, 0, 0, 0};   // each ring's newest complete pair (edgpu_last_timings)
+    // Borrowed end points.  A whole-tick entry (ring 1) ends at its copy kernel's end event
+    // (ring 0 sequence number in tick_end[slot]); a keyframe entry (ring 3) starts at the end
+    // event of the ingest it indexes (ring 2 sequence number in kf_from[slot]) when nothing ran
+    // on the host between the two, else at its own start event (kf_from[slot] = kOwnStart).
+    // A borrowed event is valid while its ring has not recorded kHist more pairs since.
+    static const uint32_t kOwnStart = 0xFFFFFFFFu;
+    uint32_t tick_end[kHist] = {};
+    uint32_t kf_from[kHist] = {};
+    uint32_t last_seq[4] = {0, 0, 0, 0};    // each ring's newest complete pair (edgpu_last_timings)
+    bool kf_share = false;                  // the last ingest's end event may start the keyframe entry
     uint64_t fanout_launches = 0;
     int64_t last_now = 0;               // clock of the last edgpu_fanout (backpressure reports)
     bool timed_fanout = false, timed_ingest = false, timed_keyframe = false;
@@ -678,23 +686,36 @@ int edgpu_source_identity(edgpu_ctx* x, uint32_t session, uint32_t track, uint32
     return EDGPU_OK;
 }
 
-// Records the start / end events of launch kind `w` into the history ring.
+// Records the start / end event of launch kind `w` into the history ring.  A pair counts (its
+// sequence number advances) only once its end event is recorded.
 static hipError_t hist_mark(edgpu_ctx* x, int w, int end, hipStream_t st = nullptr) {
-    const uint32_t slot = x->hist_n[w] % edgpu_ctx::kHist;
-    hipError_t e = hipEventRecord(x->hist[w][slot][end], st ? st : x->stream);
-    if (end) { x->last_slot[w] = slot; x->hist_n[w]++; }
+    const uint32_t seq = x->hist_n[w];
+    hipError_t e = hipEventRecord(x->hist[w][seq % edgpu_ctx::kHist][end], st ? st : x->stream);
+    if (e == hipSuccess && end) { x->last_seq[w] = seq; x->hist_n[w] = seq + 1; }
     return e;
 }
 
-// End event of a history pair: the whole-tick ring (1) ends where its tick's copy kernel (ring
-// 0, same slot: both advance once per edgpu_fanout) ends, so that point is recorded once.
-static hipEvent_t hist_end(edgpu_ctx* x, int w, uint32_t slot) {
-    return x->hist[w == 1 ? 0 : w][slot][1];
+// Whether ring `w`'s pair `seq` still holds its events (not overwritten since).
+static bool hist_live(const edgpu_ctx* x, int w, uint32_t seq) {
+    return x->hist_n[w] - seq <= (uint32_t)edgpu_ctx::kHist && x->hist_n[w] != seq;
 }
 
-// Start event of a history pair: the keyframe ring (3) starts at the end of its ingest (ring 2).
-static hipEvent_t hist_start(edgpu_ctx* x, int w, uint32_t slot) {
-    return w == 3 ? x->hist[2][x->kf_from[slot]][1] : x->hist[w][slot][0];
+// Start / end events of pair `seq` of ring `w`, resolving the borrowed end points; false when a
+// borrowed pair has been overwritten (the entry is skipped).
+static bool hist_pair(const edgpu_ctx* x, int w, uint32_t seq, hipEvent_t* a, hipEvent_t* b) {
+    const uint32_t slot = seq % edgpu_ctx::kHist;
+    *a = x->hist[w][slot][0];
+    *b = x->hist[w][slot][1];
+    if (w == 1) {
+        const uint32_t s0 = x->tick_end[slot];
+        if (!hist_live(x, 0, s0)) return false;
+        *b = x->hist[0][s0 % edgpu_ctx::kHist][1];
+    } else if (w == 3 && x->kf_from[slot] != edgpu_ctx::kOwnStart) {
+        const uint32_t s2 = x->kf_from[slot];
+        if (!hist_live(x, 2, s2)) return false;
+        *a = x->hist[2][s2 % edgpu_ctx::kHist][1];
+    }
+    return true;
 }
 
 static int rebuild_index(edgpu_ctx* x) {
@@ -754,6 +775,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     if (tcp) HIP_CHECK(launch_deframe_finish(*tcp, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
+    x->kf_share = tcp == nullptr;       // the interleaved path syncs and reads back results next
     x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
     return EDGPU_OK;
 }
@@ -761,6 +783,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
 int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
         (where == EDGPU_PTR_HOST && blob_bytes > x->cfg.max_batch_bytes))
         return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
@@ -922,8 +945,16 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     KeyframeParams p;
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
-    // the index starts where the ingest it indexes ended: that point is already recorded
-    x->kf_from[x->hist_n[3] % edgpu_ctx::kHist] = x->last_slot[2];
+    // the index starts where the ingest it indexes ended when the host did nothing in between
+    // (that point is already recorded: an event record costs the GPU ~5 us of idle), else here
+    const uint32_t kslot = x->hist_n[3] % edgpu_ctx::kHist;
+    if (x->kf_share && x->last_seq[2] + 1 == x->hist_n[2]) {
+        x->kf_from[kslot] = x->last_seq[2];
+    } else {
+        x->kf_from[kslot] = edgpu_ctx::kOwnStart;
+        HIP_CHECK(hist_mark(x, 3, 0));
+    }
+    x->kf_share = false;
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
     x->timed_keyframe = true;
@@ -983,8 +1014,12 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(hist_mark(x, 0, 0, cs));
     HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
-    x->last_slot[1] = x->hist_n[1] % edgpu_ctx::kHist;   // ring 1 ends at ring 0's end event
-    x->hist_n[1]++;
+    {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
+        const uint32_t s1 = x->hist_n[1];
+        x->tick_end[s1 % edgpu_ctx::kHist] = x->last_seq[0];
+        x->last_seq[1] = s1;
+        x->hist_n[1] = s1 + 1;
+    }
     if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_launches++;
     x->timed_fanout = true;
@@ -1041,9 +1076,11 @@ int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, u
     const uint32_t n = std::min<uint32_t>(x->hist_n[which] - x->hist_rd[which], edgpu_ctx::kHist);
     const uint32_t first = x->hist_n[which] - n;
     uint32_t k = 0;
-    for (uint32_t i = 0; i < n && k < max_n; i++, k++) {
-        const uint32_t slot = (first + i) % edgpu_ctx::kHist;
-        HIP_CHECK(hipEventElapsedTime(&out_ms[k], hist_start(x, which, slot), hist_end(x, which, slot)));
+    for (uint32_t i = 0; i < n && k < max_n; i++) {
+        hipEvent_t a, b;
+        if (!hist_pair(x, which, first + i, &a, &b)) continue;     // a borrowed event was reused
+        HIP_CHECK(hipEventElapsedTime(&out_ms[k], a, b));
+        k++;
     }
     x->hist_rd[which] = x->hist_n[which];
     if (out_n) *out_n = k;
@@ -1068,7 +1105,9 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     // the newest pair of each history ring: every timed point is recorded once per tick (an
     // event record costs the GPU ~5 us of idle between the kernels around it)
     auto last = [&](int w, float* o) {
-        return hipEventElapsedTime(o, hist_start(x, w, x->last_slot[w]), hist_end(x, w, x->last_slot[w]));
+        hipEvent_t a, b;
+        if (!hist_pair(x, w, x->last_seq[w], &a, &b)) return hipSuccess;
+        return hipEventElapsedTime(o, a, b);
     };
     if (x->timed_fanout) {
         HIP_CHECK(last(0, &out_ms[0]));

@@ -1645,6 +1645,9 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout5<512, 32, 2>, 512, 32, fanout5_lds<512, 32>()},          // 17
     {(const void*)k_fanout4<512, 32, 2>, 512, 32, fanout4_lds<512, 32>()},          // 18 nt, 512 threads
     {(const void*)k_fanout4<1024, 16, 2>, 1024, 16, fanout4_lds<1024, 16>()},       // 19 nt, 16-packet chunks
+    {(const void*)k_fanout4<1024, 36, 2>, 1024, 36, fanout4_lds<1024, 36>()},       // 20 nt, 36 (2 WG/CU)
+    {(const void*)k_fanout4<1024, 48, 2>, 1024, 48, fanout4_lds<1024, 48>()},       // 21 nt, 48 (1 WG/CU)
+    {(const void*)k_fanout4<1024, 56, 2>, 1024, 56, fanout4_lds<1024, 56>()},       // 22 nt, 56 (1 WG/CU)
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1652,7 +1655,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt>", "k_fanout4<1024,32,sc1>", "k_fanout4<1024,32,sc0sc1>",
                                             "k_fanout4<1024,32,nt,ntdesc>", "k_fanout4<1024,32,nt,ntdesc,ntload>",
                                             "k_fanout4<1024,32,nt,ntload>", "k_fanout5<256,32,nt>", "k_fanout5<512,32,nt>",
-                                            "k_fanout4<512,32,nt>", "k_fanout4<1024,16,nt>"};
+                                            "k_fanout4<512,32,nt>", "k_fanout4<1024,16,nt>",
+                                            "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 int fanout_chunk(int variant) {

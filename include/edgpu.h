@@ -386,7 +386,10 @@ int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 /* Per-launch device durations (ms, HIP events on the ctx stream) recorded since the last
  * call, oldest first, for `which` = 0 fan-out copy kernel, 1 whole fan-out tick (plan +
  * copy), 2 ingest, 3 keyframe index.  Up to 256 launches are kept; the history is cleared
- * after reading.  Syncs. */
+ * after reading.  [3] runs from the end of the ingest it indexes when that ingest was
+ * enqueued without a host round trip (edgpu_ingest: it then includes the launch gap between
+ * the two calls), else from its own start event (edgpu_ingest_interleaved, which syncs and
+ * reads results back in between).  Syncs. */
 int  edgpu_kernel_times(edgpu_ctx* ctx, int which, float* out_ms, uint32_t max_n, uint32_t* out_n);
 
 /* Copies device memory of this context to the host (synchronous).  Convenience for hosts

@@ -1,0 +1,92 @@
+"""GPU: C-ABI call-order contracts and the timing history of the engine.
+
+* edgpu_ingest refuses to run while the previous batch still needs edgpu_keyframe_index
+  (two ingests in a row would otherwise drop the first batch's key pointers and audio anchor);
+* every per-launch duration edgpu_kernel_times returns is >= 0 and a whole-tick duration is
+  never shorter than its copy kernel's, over more ticks than the history holds and across a
+  failed RTSP-interleaved ingest (which clears the pending batch without an index);
+* an RTP-Info PLAY on a session with nothing buffered right after a PLAY that found packets
+  reports EDGPU_WOULD_BLOCK (the stale-result regression of DESIGN §4.9).
+"""
+import numpy as np
+import pytest
+
+from easydarwin_amd import edgpu
+from easydarwin_amd.synth import TrackSpec, make_sdp
+
+H264 = [TrackSpec("video", "H264/90000", 96)]
+
+
+def _rtp(seq, ts, ssrc=0x1234, payload=b"\x65" + b"\x00" * 40):
+    return bytes([0x80, 96, seq >> 8, seq & 0xFF]) + ts.to_bytes(4, "big") + ssrc.to_bytes(4, "big") + payload
+
+
+def _ingest(ctx, pkts):
+    desc, seg_off, seg_sess, blob = edgpu.build_batch(pkts)
+    ctx.ingest_host(desc, seg_off, seg_sess, blob)
+
+
+@pytest.mark.gpu
+def test_ingest_refused_while_index_pending():
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(H264))
+        _ingest(ctx, [(s, 0, 0, _rtp(1, 0))])
+        with pytest.raises(edgpu.EdgpuError) as e:
+            _ingest(ctx, [(s, 0, 1, _rtp(2, 0))])
+        assert e.value.code == edgpu.ERR
+        ctx.keyframe_index()
+        _ingest(ctx, [(s, 0, 2, _rtp(3, 0))])
+        ctx.keyframe_index()
+        ctx.fanout(10)
+        assert ctx.stats().status == 0
+
+
+@pytest.mark.gpu
+def test_kernel_times_nonnegative_and_paired():
+    with edgpu.Context(max_batch_packets=64) as ctx:
+        sess = [ctx.session_add(make_sdp(H264)) for _ in range(3)]
+        for s in sess:
+            ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+            ctx.subscriber_add(s, edgpu.TRANSPORT_TCP)
+        seq = 0
+        for tick in range(300):
+            t = 10 * tick
+            if tick == 150:
+                # 100 frames > max_batch_packets: the interleaved ingest runs on the device and
+                # fails (EDGPU_OUT_OVERFLOW) without a keyframe index
+                raw = b"".join(b"$\x00" + len(p).to_bytes(2, "big") + p for p in (_rtp(k, 0) for k in range(100)))
+                reads = np.zeros(1, dtype=edgpu.TCP_READ_DTYPE)
+                reads[0] = (sess[0], len(raw), 0, t)
+                with pytest.raises(edgpu.EdgpuError) as e:
+                    ctx.ingest_interleaved(reads, raw)
+                assert e.value.code == edgpu.OUT_OVERFLOW
+            pkts = []
+            for s in sess:
+                for _ in range(2):
+                    pkts.append((s, 0, t, _rtp(seq & 0xFFFF, 90 * t)))
+                    seq += 1
+            _ingest(ctx, pkts)
+            ctx.keyframe_index()
+            ctx.fanout(t)
+            if tick % 100 == 99:
+                ring = [ctx.kernel_times(w) for w in range(4)]
+                assert len(ring[0]) == len(ring[1]) > 0
+                for w in range(4):
+                    assert ring[w] and min(ring[w]) >= 0.0, (w, ring[w][:8])
+                assert all(b >= a for a, b in zip(ring[0], ring[1]))
+        tm = ctx.timings()
+        assert tm["tick_ms"] >= tm["fanout_ms"] >= 0.0 and tm["keyframe_ms"] >= 0.0
+
+
+@pytest.mark.gpu
+def test_rtp_info_play_on_empty_session_after_a_found_play():
+    with edgpu.Context() as ctx:
+        full = ctx.session_add(make_sdp(H264))
+        empty = ctx.session_add(make_sdp(H264))
+        _ingest(ctx, [(full, 0, 100 + k, _rtp(500 + k, 9000 * k)) for k in range(5)])
+        ctx.keyframe_index()
+        _h, info = ctx.subscriber_play(full, rtp_info=True, now_ms=200)
+        assert info == [(500, 0)]
+        with pytest.raises(edgpu.EdgpuError) as e:
+            ctx.subscriber_play(empty, rtp_info=True, now_ms=200)
+        assert e.value.code == edgpu.WOULD_BLOCK

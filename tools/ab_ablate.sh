@@ -5,5 +5,5 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; V=$2
 mkdir -p $R/gpurun_out/$TAG
 for a in 0 1 2 3; do
-  EDGPU_FANOUT=$V EDGPU_ABLATE=$a timeout -k 10 300 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline > $R/gpurun_out/$TAG/a$a.json 2> $R/gpurun_out/$TAG/a$a.err || exit 1
+  EDGPU_FANOUT=$V EDGPU_ABLATE=$a timeout -k 10 300 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline --ablation-study > $R/gpurun_out/$TAG/a$a.json 2> $R/gpurun_out/$TAG/a$a.err || exit 1
 done
