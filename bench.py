@@ -253,6 +253,9 @@ def main():
                     help="desc: packets handed over as descriptors + slots (edgpu_ingest, the reflector's "
                          "per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP reads, "
                          "deframed on the GPU (edgpu_ingest_interleaved)")
+    ap.add_argument("--rewrite", action="store_true",
+                    help="per-output rewrite stage on every subscriber (seq/ts deltas + SSRC override, "
+                         "edgpu_subscriber_rewrite); the reference's parity mode is the identity (default)")
     ap.add_argument("--ablation-study", action="store_true",
                     help="allow EDGPU_ABLATE (timing experiments that skip work): the line is then not a "
                          "valid measurement and says so")
@@ -311,7 +314,9 @@ def main():
     for _ in gids:
         s = ctx.session_add(fleet.sdp())
         for _k in range(args.subs):
-            ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+            h = ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+            if args.rewrite:
+                ctx.subscriber_rewrite(h, 0, seq_delta=h * 7919 + 1, ts_delta=h * 0x9E3779B1, ssrc=0x5EED0000 + h)
 
     for i in range(warm):
         run_step(ctx, batches[i])
@@ -401,6 +406,7 @@ def main():
                    "ingest": args.ingest,
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
                    "tick_ms": args.tick_ms,
+                   "rewrite": "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)",
                    "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"},
         "relayed_GBps": round(out_all / dt / 1e9, 2),

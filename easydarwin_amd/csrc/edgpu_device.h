@@ -173,6 +173,23 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint8_t  prev_sent_any;
     uint8_t  resume_at;
     uint8_t  _pad1[5];
+    // per-output rewrite (edgpu_subscriber_rewrite): kRw* flags | seq delta << 16, 0 = identity
+    uint32_t rw;
+    uint32_t rw_ts;                 // RTP timestamp delta (mod 2^32)
+    uint32_t rw_ssrc;               // replacement SSRC (kRwSsrc), host order
+    uint32_t _pad2;
+};
+
+// SubDev.rw / FanSub.rw: the per-output rewrite stage (north_star item 3).  The reference
+// rewrites nothing (Q1: RTPSessionOutput::PacketShouldBeThinned returns false at
+// RTPSessionOutput.cpp:685-687, the RTCP rewrite call is commented out at :600-601), so parity
+// runs with rw = 0; a host that renumbers a subscriber's streams (e.g. after a source switch)
+// sets it.  Every field a rewrite touches sits in a slot's first 16-B word, except an SR's RTP
+// timestamp (second word).
+enum : uint32_t {
+    kRwActive = 1u << 0,            // any rewrite on this sub-stream
+    kRwSsrc   = 1u << 1,            // replace the SSRC (RTP bytes 8-11, RTCP sender SSRC bytes 4-7)
+    kRwRtcp   = 1u << 2,            // the sub-stream carries RTCP (kind 1)
 };
 
 // RTP-Info PLAY query for one track (ReflectorSession HaveStreamBuffers,
@@ -207,12 +224,16 @@ struct FanWork {                    // 64 B
 };
 
 // Per-sub-stream copy parameters of a tick, in sender order (FanWork::qb/qe index them).
-struct FanSub {                     // 32 B
+struct FanSub {                     // 48 B
     int64_t  dw;                    // arena word of virtual ring word V is dw + V
     int64_t  off;                   // wire offset of a packet with vbyte vb is off + vb
     uint64_t a;                     // first packet index this tick; ~0: nothing to send
     uint32_t ch;                    // bit 0: RTSP-interleaved; bits 8..15: channel byte
     uint32_t db;                    // descriptor index of a packet with vcount vc is db + vc
+    uint32_t rw;                    // SubDev.rw
+    uint32_t rw_ts;                 // timestamp delta
+    uint32_t rw_ssrc_be;            // replacement SSRC as stored (big-endian bytes)
+    uint32_t _pad;
 };
 
 struct TickTotals {                 // device-side, mirrors edgpu_tick_stats

@@ -33,6 +33,7 @@ hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStr
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
 hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
 int fanout_chunk(int variant);
+bool fanout_rewrites(int variant);
 const char* fanout_name(int variant);
 }  // namespace edgpu
 
@@ -166,6 +167,8 @@ struct edgpu_ctx {
     std::vector<edgpu_source_report> source_reports;   // queued by the last edgpu_fanout
     std::vector<uint32_t> sub_sender;   // host mirror: SubDev index -> sender
     std::vector<uint8_t> sub_active;
+    std::vector<uint8_t> sub_rw;        // host mirror: SubDev has a non-identity rewrite
+    uint32_t n_rw = 0;                  // active sub-streams with a rewrite
     uint32_t nsenders = 0, nstreams = 0;
     std::vector<void*> ring_allocs;
     uint64_t work_cap_needed = 0;
@@ -474,6 +477,7 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             Q.rtp_info = (k == 0 && (flags & EDGPU_PLAY_RTP_INFO)) ? 1 : 0;
             x->sub_sender.push_back(Q.sender);
             x->sub_active.push_back(1);
+            x->sub_rw.push_back(0);
             v.push_back(Q);
         }
     x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true});
@@ -588,6 +592,7 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     const uint8_t zero = 0;
     for (uint32_t i = 0; i < s.nsub; i++) {
         x->sub_active[s.first_sub + i] = 0;
+        if (x->sub_rw[s.first_sub + i]) { x->sub_rw[s.first_sub + i] = 0; x->n_rw--; }
         HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(x->d_subs.ptr + s.first_sub + i) + offsetof(SubDev, active),
                                  &zero, 1, hipMemcpyHostToDevice, x->stream));
     }
@@ -595,6 +600,34 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     s.active = false;
     x->sessions[s.session].eyes--;               // RemoveOutput(..., isClient) -> DecEyeCount
     x->index_dirty = true;
+    return EDGPU_OK;
+}
+
+int edgpu_subscriber_rewrite(edgpu_ctx* x, uint32_t handle, uint32_t track, const edgpu_rewrite* rw) {
+    if (!x || handle >= x->subscribers.size() || !x->subscribers[handle].active)
+        return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
+    SubscriberHost& s = x->subscribers[handle];
+    if (track >= s.nsub / 2) return fail(EDGPU_BAD_ARGUMENT, "bad track");
+    if (rw && (rw->flags & ~EDGPU_REWRITE_SSRC)) return fail(EDGPU_BAD_ARGUMENT, "bad rewrite flags");
+    const bool on = rw && (rw->seq_delta || rw->ts_delta || (rw->flags & EDGPU_REWRITE_SSRC));
+    if (on && !fanout_rewrites(x->fanout_variant))
+        return fail(EDGPU_ERR, "the selected fan-out variant (EDGPU_FANOUT) has no rewrite stage");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    HIP_CHECK(hipSetDevice(x->device));
+    for (uint32_t k = 0; k < 2; k++) {
+        const uint32_t q = s.first_sub + 2 * track + k;
+        uint32_t v[3] = {0, 0, 0};
+        if (on) {
+            v[0] = kRwActive | (k ? kRwRtcp : 0u) | ((rw->flags & EDGPU_REWRITE_SSRC) ? kRwSsrc : 0u) |
+                   (uint32_t)rw->seq_delta << 16;
+            v[1] = rw->ts_delta;
+            v[2] = rw->ssrc;
+        }
+        HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(x->d_subs.ptr + q) + offsetof(SubDev, rw), v, sizeof(v),
+                                 hipMemcpyHostToDevice, x->stream));
+        if (on != (bool)x->sub_rw[q]) { x->sub_rw[q] = on; x->n_rw += on ? 1 : -1; }
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));     // `v` is stack memory
     return EDGPU_OK;
 }
 

@@ -732,6 +732,10 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             f.a = Q.nonempty ? Q.a : ~0ull;
             f.ch = Q.transport ? ((uint32_t)Q.channel << 8 | 1u) : 0u;
             f.db = Q.desc_base - Q.vcstart;
+            f.rw = Q.rw;
+            f.rw_ts = Q.rw_ts;
+            f.rw_ssrc_be = __builtin_bswap32(Q.rw_ssrc);
+            f._pad = 0;
             P.fansub[pos] = f;
         }
     }
@@ -1011,7 +1015,7 @@ void k_fanout3(FanoutParams P) {
 //     ring's buffer resource is scalar and the chunk's 16-B loads issue back to back.
 //     (k_fanout3 built that resource from a per-lane load, which the compiler lowers to a
 //     waterfall loop that waits for every load in turn.)
-//   * Sub-stream parameters are one 32-B FanSub per sub-stream in sender order, also scalar
+//   * Sub-stream parameters are one 48-B FanSub per sub-stream in sender order, also scalar
 //     loads: no sub_index -> SubDev chain and no per-sender LDS batch.
 //   * The NEXT item's chunk words and packet metadata are loaded into registers as soon as
 //     this item's LDS image is complete, so their HBM latency runs under this item's stores;
@@ -1032,6 +1036,35 @@ __device__ __forceinline__ T const_load(const T* p) {
     cu32* src = (cu32*)p;
 #pragma unroll
     for (int i = 0; i < (int)(sizeof(T) / 4); i++) d[i] = src[i];
+    return v;
+}
+
+// The per-output patch of one 16-B arena word (word `w` of the chunk's LDS image `cb`, slot
+// starts marked in bitmap `sm`): the RTSP-interleaved channel byte (RTSPSessionInterface.cpp:
+// 329-336) and the rewrite stage (kRw*).  A slot's first word holds the 4-B '$' 0 BE16(len)
+// header and packet bytes 0..11: RTP seq (bytes 2-3), timestamp (4-7) and SSRC (8-11), or an
+// RTCP packet's sender SSRC (4-7); an SR's RTP timestamp (packet bytes 16-19) is in the second
+// word.  Fields past the packet's length are left alone; CSRC lists and extensions are never
+// touched.
+__device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w, const uint32_t* sm, const u32x4* cb) {
+    if ((sm[w >> 5] >> (w & 31)) & 1u) {
+        if (f.ch & 1u) v.x |= f.ch & 0xFF00u;
+        if (f.rw) {
+            const uint32_t len = ((v.x >> 8) & 0xFF00u) | (v.x >> 24);
+            if (f.rw & kRwRtcp) {
+                if ((f.rw & kRwSsrc) && len >= 8) v.z = f.rw_ssrc_be;
+            } else if (len >= 12) {
+                const uint32_t seq = ((((v.y >> 8) & 0xFF00u) | (v.y >> 24)) + (f.rw >> 16)) & 0xFFFFu;
+                v.y = (v.y & 0xFFFFu) | (seq >> 8) << 16 | (seq & 0xFFu) << 24;
+                v.z = __builtin_bswap32(__builtin_bswap32(v.z) + f.rw_ts);
+                if (f.rw & kRwSsrc) v.w = f.rw_ssrc_be;
+            }
+        }
+    } else if ((f.rw & kRwRtcp) && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {
+        const u32x4 h = cb[w - 1];
+        const uint32_t len = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
+        if (len >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
+    }
     return v;
 }
 
@@ -1149,14 +1182,14 @@ void k_fanout4(FanoutParams P) {
             if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
             const uint32_t s = (uint32_t)(A & 7);                              // words past a line
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
-            const uint32_t chb = f.ch & 0xFF00u;
+            const bool patch = (f.ch & 1u) || f.rw;                            // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
             for (uint32_t j = 0; j < nj; j++) {
                 const uint32_t lw = tid + j * THREADS;                         // word of the aligned window
                 const uint32_t src = fw + lw - s;                              // chunk word it carries
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
                 u32x4 v = cbuf[srcc];
-                if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
+                if (patch) v = fan_patch(v, f, srcc, sm, cbuf);
                 __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, AUX);
             }
         }
@@ -1344,14 +1377,14 @@ void k_fanout5(FanoutParams P) {
             if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
             const uint32_t s = (uint32_t)(A & 7);
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
-            const uint32_t chb = f.ch & 0xFF00u;
+            const bool patch = (f.ch & 1u) || f.rw;                            // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
             for (uint32_t j = 0; j < nj; j++) {
                 const uint32_t lw = tid + j * THREADS;
                 const uint32_t src = fw + lw - s;
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
                 u32x4 v = cb[srcc];
-                if ((f.ch & 1u) && ((sm[srcc >> 5] >> (srcc & 31)) & 1u)) v.x |= chb;
+                if (patch) v = fan_patch(v, f, srcc, sm, cb);
                 __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, AUX);
             }
         }
@@ -1659,6 +1692,11 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
+// k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
+bool fanout_rewrites(int variant) {
+    if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
+    return variant > 1;
+}
 int fanout_chunk(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
     return kVariants[variant].chunk;

@@ -33,6 +33,7 @@ EXPORTED = [
     "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
+    "edgpu_subscriber_rewrite",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -60,6 +61,13 @@ class Config(C.Structure):
 
 class RtpInfo(C.Structure):
     _fields_ = [("seq", C.c_uint16), ("_pad", C.c_uint16), ("rtptime", C.c_uint32)]
+
+
+REWRITE_SSRC = 1
+
+
+class Rewrite(C.Structure):
+    _fields_ = [("seq_delta", C.c_uint16), ("flags", C.c_uint16), ("ts_delta", C.c_uint32), ("ssrc", C.c_uint32)]
 
 
 class PktDesc(C.Structure):
@@ -183,6 +191,7 @@ def load(path: str = LIB_PATH):
         "edgpu_source_reports": (I32, [P, P, U32, C.POINTER(U32)]),
         "edgpu_source_identity": (I32, [P, U32, U32, U32, I64]),
         "edgpu_session_eyes_add": (I32, [P, U32, C.c_int32]),
+        "edgpu_subscriber_rewrite": (I32, [P, U32, U32, C.POINTER(Rewrite)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -262,6 +271,13 @@ class Context:
         out = np.zeros(len(ses), dtype=np.uint32)
         _check(self.lib.edgpu_subscribers_add(self.h, len(ses), _ptr(ses), _ptr(trn), _ptr(out)))
         return out
+
+    def subscriber_rewrite(self, handle: int, track: int, seq_delta: int = 0, ts_delta: int = 0,
+                           ssrc: int | None = None):
+        """Per-output rewrite of one subscriber track (identity: all defaults)."""
+        rw = Rewrite(seq_delta & 0xFFFF, REWRITE_SSRC if ssrc is not None else 0, ts_delta & 0xFFFFFFFF,
+                     (ssrc or 0) & 0xFFFFFFFF)
+        _check(self.lib.edgpu_subscriber_rewrite(self.h, handle, track, C.byref(rw)))
 
     def subscriber_remove(self, handle: int):
         _check(self.lib.edgpu_subscriber_remove(self.h, handle))

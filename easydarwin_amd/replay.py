@@ -157,7 +157,7 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
-           interleaved: int | None = None, sockets: dict | None = None, **cfg):
+           interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -173,7 +173,10 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
 
     sockets={...}: every tick leaves through the engine's socket egress to loopback receivers
     (easydarwin_amd/egress.py SocketSink, constructed with these keyword arguments) and the
-    capture is rebuilt from the bytes the receivers read."""
+    capture is rebuilt from the bytes the receivers read.
+
+    rewrite={sub_id: (seq_delta, ts_delta, ssrc or None)}: the per-output rewrite stage
+    (edgpu_subscriber_rewrite) on every track of those subscribers, set at their join."""
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
@@ -293,6 +296,9 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                             raise
                         continue
                     subs_meta[h] = (sub_id, s, transport)
+                    if rewrite and sub_id in rewrite:
+                        for tr in range(sess_tracks[s]):
+                            out.subscriber_rewrite(h, tr, *rewrite[sub_id])
                     if rep is not None:
                         ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
                     if sink is not None:

@@ -15,6 +15,8 @@
  *   edgpu_subscriber_play  the same for an RTP-Info player: DoPlay + HaveStreamBuffers
  *                          (QTSSReflectorModule.cpp:1804-1865, 1971-2004)
  *   edgpu_subscriber_remove ReflectorSession::RemoveOutput (ReflectorSession.cpp:255-279)
+ *   edgpu_subscriber_rewrite the per-output seq / timestamp / SSRC rewrite the reference leaves
+ *                          dead (RTPSessionOutput.cpp:403-561, 600-601, 685-773)
  *   edgpu_ingest           ReflectorStream::PushPacket + ReflectorSocket::ProcessPacket
  *                          (ReflectorStream.cpp:529-576, 1769-2010), called per packet by
  *                          ProcessRTPData (QTSSReflectorModule.cpp:604-678)
@@ -206,6 +208,28 @@ typedef struct edgpu_rtp_info {
 } edgpu_rtp_info;
 int  edgpu_subscriber_play(edgpu_ctx* ctx, uint32_t session, int transport, uint32_t flags,
                            int64_t now_ms, uint32_t* out_handle, edgpu_rtp_info* out_info);
+
+/* Per-output rewrite stage (north_star item 3).  From the next edgpu_fanout, every packet
+ * written to subscriber `handle`'s track `track` is rewritten in flight:
+ *   RTP sub-stream:  sequence number += seq_delta (mod 2^16), timestamp += ts_delta (mod 2^32),
+ *                    SSRC = ssrc when flags has EDGPU_REWRITE_SSRC -- for packets of >= 12 bytes;
+ *   RTCP sub-stream: sender SSRC (bytes 4-7) = ssrc with EDGPU_REWRITE_SSRC (>= 8 bytes), and the
+ *                    RTP timestamp of a sender report (PT 200, bytes 16-19) += ts_delta (>= 20 B).
+ * CSRC lists, extensions and payloads are never touched; lengths and descriptors are unchanged.
+ * NULL (or all-zero deltas without EDGPU_REWRITE_SSRC) is the identity, the default.  The
+ * reference never rewrites (Q1: RTPSessionOutput::PacketShouldBeThinned returns false at
+ * RTPSessionOutput.cpp:685-687, and the RTCP rewrite RewriteRTCP / TrackRTCPPackets,
+ * :403-561, is not called, :600-601), so parity runs use the identity; FilterPacket's first-seq
+ * test and an RTP-Info PLAY's reply see the source's sequence numbers (a host that rewrites an
+ * RTP-Info player's stream adjusts its RTP-Info header by the same deltas). */
+#define EDGPU_REWRITE_SSRC 1u
+typedef struct edgpu_rewrite {
+    uint16_t seq_delta;
+    uint16_t flags;
+    uint32_t ts_delta;
+    uint32_t ssrc;          /* host order */
+} edgpu_rewrite;
+int  edgpu_subscriber_rewrite(edgpu_ctx* ctx, uint32_t handle, uint32_t track, const edgpu_rewrite* rw);
 
 int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets,
                   const uint32_t* seg_offsets, const uint32_t* seg_session,

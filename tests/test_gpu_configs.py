@@ -153,12 +153,12 @@ def test_c4_burst_joins_match_owner_gop():
             f = min(key_first, win_first)
             size = 64 + 16 + 2 * 96 + 32 * (len(pk) - f) + sum(sb for _, sb in pk[f:])
             assert int(offs[j + 1] - offs[j]) == (size + 15) // 16 * 16
-        src = owner.device_alloc(total)
-        dst = replica.device_alloc(total)
-        offs2, _ = owner.session_export([osess[g] for g in need], now, src.ptr, src.nbytes)
+        img_src = owner.device_alloc(total)
+        img_dst = replica.device_alloc(total)
+        offs2, _ = owner.session_export([osess[g] for g in need], now, img_src.ptr, img_src.nbytes)
         assert np.array_equal(offs, offs2)
-        replica.memcpy_peer(dst.ptr, 0, src.ptr, total)
-        replica.session_import(dst.ptr, offs, [rsess[g] for g in need])
+        replica.memcpy_peer(img_dst.ptr, 0, img_src.ptr, total)
+        replica.session_import(img_dst.ptr, offs, [rsess[g] for g in need])
         h_own = owner.subscribers_add([osess[g] for g in sess_of[~remote]], edgpu.TRANSPORT_UDP)
         h_rep = replica.subscribers_add([rsess[g] for g in sess_of[remote]], edgpu.TRANSPORT_UDP)
         c0o, c0r = owner.counters(), replica.counters()
@@ -189,5 +189,5 @@ def test_c4_burst_joins_match_owner_gop():
                     assert ln == int(desc["len"][i])
                     src = blob[int(slot_off[i]) + 4:int(slot_off[i]) + 4 + ln]
                     assert np.array_equal(region[o - int(q["out_base"]):o - int(q["out_base"]) + ln], src)
-        src.free()
-        dst.free()
+        img_src.free()
+        img_dst.free()
