@@ -1047,25 +1047,32 @@ __device__ __forceinline__ T const_load(const T* p) {
 // word.  Fields past the packet's length are left alone; CSRC lists and extensions are never
 // touched.
 __device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w, const uint32_t* sm, const u32x4* cb) {
-    if ((sm[w >> 5] >> (w & 31)) & 1u) {
-        if (f.ch & 1u) v.x |= f.ch & 0xFF00u;
-        if (f.rw) {
-            const uint32_t len = ((v.x >> 8) & 0xFF00u) | (v.x >> 24);
-            if (f.rw & kRwRtcp) {
-                if ((f.rw & kRwSsrc) && len >= 8) v.z = f.rw_ssrc_be;
-            } else if (len >= 12) {
-                const uint32_t seq = ((((v.y >> 8) & 0xFF00u) | (v.y >> 24)) + (f.rw >> 16)) & 0xFFFFu;
-                v.y = (v.y & 0xFFFFu) | (seq >> 8) << 16 | (seq & 0xFFu) << 24;
-                v.z = __builtin_bswap32(__builtin_bswap32(v.z) + f.rw_ts);
-                if (f.rw & kRwSsrc) v.w = f.rw_ssrc_be;
+    // branch-free on the per-word test (every wave holds a slot start or two): the patched
+    // word is computed for every lane and selected where the word starts a slot; the flags
+    // (f.ch, f.rw) are uniform, so their branches are scalar
+    const bool start = (sm[w >> 5] >> (w & 31)) & 1u;
+    u32x4 p = v;
+    if (f.ch & 1u) p.x |= f.ch & 0xFF00u;
+    if (f.rw) {
+        const uint32_t len = ((v.x >> 8) & 0xFF00u) | (v.x >> 24);
+        if (!(f.rw & kRwRtcp)) {
+            const bool ok = len >= 12;
+            const uint32_t seq = (((v.y >> 8) & 0xFF00u) | (v.y >> 24)) + (f.rw >> 16);
+            const uint32_t ny = (v.y & 0xFFFFu) | ((seq >> 8) & 0xFFu) << 16 | (seq & 0xFFu) << 24;
+            const uint32_t nz = __builtin_bswap32(__builtin_bswap32(v.z) + f.rw_ts);
+            p.y = ok ? ny : v.y;
+            p.z = ok ? nz : v.z;
+            if (f.rw & kRwSsrc) p.w = ok ? f.rw_ssrc_be : v.w;
+        } else {
+            if (f.rw & kRwSsrc) p.z = len >= 8 ? f.rw_ssrc_be : v.z;
+            if (!start && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {   // RTCP only: rare
+                const u32x4 h = cb[w - 1];
+                const uint32_t hl = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
+                if (hl >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
             }
         }
-    } else if ((f.rw & kRwRtcp) && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {
-        const u32x4 h = cb[w - 1];
-        const uint32_t len = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
-        if (len >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
     }
-    return v;
+    return start ? p : v;
 }
 
 template <int THREADS, int CHUNK>
@@ -1105,8 +1112,12 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 
 // AUX: cache policy of the arena stores (0 plain; A/B variants: 2 nt, 16 sc1, 17 sc0 sc1);
 // DNT: non-temporal descriptor stores; LAUX: cache policy of the chunk loads.
-template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS)))
+// SU: store-loop unroll (SU LDS reads in flight before the SU stores of a sub-stream window;
+// needs the VGPRs of 1 workgroup per CU at 1024 threads)
+// WPE: minimum waves per SIMD the register allocation must allow (8 = two 1024-thread
+// workgroups per CU, i.e. <= 64 VGPRs); 0 leaves it to the compiler.
+template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
     constexpr int NL = (CWORDS + THREADS - 1) / THREADS;              // chunk words per lane
@@ -1184,13 +1195,21 @@ void k_fanout4(FanoutParams P) {
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
             const bool patch = (f.ch & 1u) || f.rw;                            // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
-            for (uint32_t j = 0; j < nj; j++) {
-                const uint32_t lw = tid + j * THREADS;                         // word of the aligned window
-                const uint32_t src = fw + lw - s;                              // chunk word it carries
-                const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
-                u32x4 v = cbuf[srcc];
-                if (patch) v = fan_patch(v, f, srcc, sm, cbuf);
-                __builtin_amdgcn_raw_buffer_store_b128(v, os, (lw - s) * 16u, 0, AUX);
+            for (uint32_t j = 0; j < nj; j += SU) {
+                u32x4 v[SU];
+                uint32_t srcc[SU];
+#pragma unroll
+                for (int k = 0; k < SU; k++) {
+                    const uint32_t src = fw + tid + (j + k) * THREADS - s;     // chunk word of the lane's
+                    srcc[k] = src < (uint32_t)CWORDS ? src : 0u;               // word of the aligned window
+                    if (k == 0 || j + k < nj) v[k] = cbuf[srcc[k]];            // uniform guard
+                }
+#pragma unroll
+                for (int k = 0; k < SU; k++) {
+                    if (k > 0 && j + k >= nj) break;
+                    if (patch) v[k] = fan_patch(v[k], f, srcc[k], sm, cbuf);
+                    __builtin_amdgcn_raw_buffer_store_b128(v[k], os, (tid + (j + k) * THREADS - s) * 16u, 0, AUX);
+                }
             }
         }
         // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
@@ -1681,6 +1700,10 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 36, 2>, 1024, 36, fanout4_lds<1024, 36>()},       // 20 nt, 36 (2 WG/CU)
     {(const void*)k_fanout4<1024, 48, 2>, 1024, 48, fanout4_lds<1024, 48>()},       // 21 nt, 48 (1 WG/CU)
     {(const void*)k_fanout4<1024, 56, 2>, 1024, 56, fanout4_lds<1024, 56>()},       // 22 nt, 56 (1 WG/CU)
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 4>, 1024, 56, fanout4_lds<1024, 56>()}, // 23 + 4-deep store loop
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 2>, 1024, 56, fanout4_lds<1024, 56>()}, // 24 + 2-deep
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 25 32, 2-deep
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 8>, 1024, 32, fanout4_lds<1024, 32>()}, // 26 32, <= 64 VGPRs
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1689,7 +1712,9 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt,ntdesc>", "k_fanout4<1024,32,nt,ntdesc,ntload>",
                                             "k_fanout4<1024,32,nt,ntload>", "k_fanout5<256,32,nt>", "k_fanout5<512,32,nt>",
                                             "k_fanout4<512,32,nt>", "k_fanout4<1024,16,nt>",
-                                            "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>"};
+                                            "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>",
+                                            "k_fanout4<1024,56,nt,su4>", "k_fanout4<1024,56,nt,su2>",
+                                            "k_fanout4<1024,32,nt,su2>", "k_fanout4<1024,32,nt,wpe8>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)

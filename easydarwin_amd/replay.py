@@ -27,7 +27,7 @@ import struct
 import numpy as np
 
 from . import edgpu
-from .trace import BLOCK, JOIN, PKT, TICK, UPKT, Trace, pack_source_reports, rr_ssrc
+from .trace import BLOCK, JOIN, LEAVE, PKT, TICK, UPKT, Trace, pack_source_reports, rr_ssrc
 
 
 def _wire_images(subs, desc, arena, images, budgets=None):
@@ -257,6 +257,30 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 raise ValueError("socket egress replays take neither BLOCK events nor overlap_ticks")
             sink = SocketSink(ctx if rep is None else rep, **{k: v for k, v in sockets.items() if k != "report"})
         blocks = {}                         # (sub_id, track, kind) -> budget for the next TICK
+        gone = set()                        # handles removed by LEAVE
+
+        def do_join(j):
+            (_, jt, s, sub_id, transport, ua, now_j) = j
+            out = ctx if rep is None else rep
+            try:
+                h, _info = out.subscriber_play(s if rep is None else rsess[s],
+                                               edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
+                                               rtp_info=bool(ua & 1), now_ms=now_j)
+            except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
+                if e.code != edgpu.WOULD_BLOCK:
+                    raise
+                return
+            subs_meta[h] = (sub_id, s, transport)
+            if rewrite and sub_id in rewrite:
+                for tr in range(sess_tracks[s]):
+                    out.subscriber_rewrite(h, tr, *rewrite[sub_id])
+            if rep is not None:
+                ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
+            if sink is not None:
+                sink.join(h, sub_id, sess_tracks[s], bool(transport))
+            for tr in range(sess_tracks[s]):
+                for k in (0, 1):
+                    images[(h, tr, k)] = []
         if lag and any(ev[0] == BLOCK for ev in trace.events):
             raise ValueError("backpressure reports need each tick read before the next ingest")
         for ev in trace.events:
@@ -277,6 +301,23 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 if ev[5] & 1 and rep is None:
                     flush()
                 joins.append(ev + (clock,))
+            elif ev[0] == LEAVE:
+                # RemoveOutput applies at once: a join still waiting for its tick is made now
+                # (the output existed, with nothing sent yet), and the output stops at the next
+                # tick (edgpu_subscriber_remove)
+                sub_id = ev[2]
+                for j in [j for j in joins if j[3] == sub_id]:
+                    if link is not None and (replica == "late" or j[2] not in rsess):
+                        rsess[j[2]] = link.add(j[2], trace.sdps[j[2]])
+                    do_join(j)
+                joins = [j for j in joins if j[3] != sub_id]
+                for h, meta in subs_meta.items():
+                    if meta[0] == sub_id and h not in gone:
+                        (ctx if rep is None else rep).subscriber_remove(h)
+                        gone.add(h)
+                        if rep is not None:
+                            ctx.session_eyes_add(meta[1], -1)
+                        break
             elif ev[0] == TICK:
                 t = ev[1]
                 flush()
@@ -286,26 +327,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                             rsess[s] = link.add(s, trace.sdps[s])     # "late": a fresh replica per join
                     link.sync(t)
                 out = ctx if rep is None else rep
-                for (_, jt, s, sub_id, transport, ua, now_j) in joins:
-                    try:
-                        h, _info = out.subscriber_play(s if rep is None else rsess[s],
-                                                       edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
-                                                       rtp_info=bool(ua & 1), now_ms=now_j)
-                    except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
-                        if e.code != edgpu.WOULD_BLOCK:
-                            raise
-                        continue
-                    subs_meta[h] = (sub_id, s, transport)
-                    if rewrite and sub_id in rewrite:
-                        for tr in range(sess_tracks[s]):
-                            out.subscriber_rewrite(h, tr, *rewrite[sub_id])
-                    if rep is not None:
-                        ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
-                    if sink is not None:
-                        sink.join(h, sub_id, sess_tracks[s], bool(transport))
-                    for tr in range(sess_tracks[s]):
-                        for k in (0, 1):
-                            images[(h, tr, k)] = []
+                for j in joins:
+                    do_join(j)
                 joins = []
                 if rep is not None:
                     ctx.fanout(t)                      # the owner ticks too (no subscribers here)
@@ -314,7 +337,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 by_handle = {}
                 for (sub_id, trk, kind), b in blocks.items():
                     for h, meta in subs_meta.items():
-                        if meta[0] == sub_id:
+                        if meta[0] == sub_id and h not in gone:
                             by_handle[(h, trk, kind)] = b
                 blocks = {}
                 unread = (out, out.fanout(t), t, by_handle)

@@ -13,6 +13,13 @@ list.  It mirrors the reference's entry points:
 * ``BLOCK`` -> during the next TICK, one subscriber sub-stream's socket accepts ``budget``
   more writes and then returns QTSS_WouldBlock (EAGAIN) for the rest of that tick
   (egress backpressure: SendPacketsToOutput's blocked branch, ReflectorStream.cpp:1158-1190);
+* ``LEAVE`` -> a subscriber's TEARDOWN / disconnect: ``ReflectorSession::RemoveOutput(output,
+  isClient=true)`` then ``delete`` of the RTPSessionOutput, as QTSSReflectorModule's
+  RemoveOutput does (QTSSReflectorModule.cpp:2133-2196; ReflectorSession.cpp:255-279,
+  ReflectorStream.cpp:338-362): the output leaves every track's bucket and the eye count
+  drops (DecEyeCount, ReflectorStream.h:445).  It takes effect immediately (a LEAVE before the
+  subscriber's first TICK means it never receives anything); a LEAVE of a subscriber that is
+  not an output (a deferred RTP-Info PLAY) changes nothing.
 * ``UPKT`` -> a UDP datagram from a pusher's address arriving on a UDP-push session's RTP
   (even) or RTCP (odd) port: ``ReflectorSocket::GetIncomingData`` -> ``ProcessPacket`` with
   the remote address (ReflectorStream.cpp:1716-1735, 1769-1875), which also records the
@@ -34,6 +41,7 @@ Binary layout (little endian)::
              | u8 4 i64 t u32 sub_id u16 track u8 kind u32 budget           (BLOCK)
              | u8 5 i64 t u32 session u8 channel u32 addr u16 port u32 len bytes[len]
                                                                              (UPKT, v2)
+             | u8 6 i64 t u32 sub_id                                         (LEAVE)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
                [ "EDRR" u32 m { i64 t u32 session u16 track u32 addr u16 port u32 len
@@ -58,7 +66,7 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK, BLOCK, UPKT = 1, 2, 3, 4, 5
+PKT, JOIN, TICK, BLOCK, UPKT, LEAVE = 1, 2, 3, 4, 5, 6
 UDP, TCP = 0, 1
 
 
@@ -92,6 +100,9 @@ class Trace:
     def block(self, t: int, sub_id: int, track: int, kind: int, budget: int):
         self.events.append((BLOCK, int(t), sub_id, track, kind, budget))
 
+    def leave(self, t: int, sub_id: int):
+        self.events.append((LEAVE, int(t), sub_id))
+
     def upkt(self, t: int, session: int, channel: int, addr: int, port: int, data: bytes):
         self.events.append((UPKT, int(t), session, channel, int(addr), int(port), bytes(data)))
 
@@ -99,8 +110,8 @@ class Trace:
     def to_bytes(self) -> bytes:
         # PKT and TICK times drive the virtual clock and must not go back; a JOIN's time is
         # informational (the join takes effect at the next TICK, like a new output being
-        # picked up by the next ReflectPackets).
-        times = [ev[1] for ev in self.events if ev[0] not in (JOIN, BLOCK)]
+        # picked up by the next ReflectPackets), and so is a LEAVE's (it applies in order).
+        times = [ev[1] for ev in self.events if ev[0] not in (JOIN, BLOCK, LEAVE)]
         assert all(a <= b for a, b in zip(times, times[1:])), "trace events must be time-ordered"
         ver = self.version
         out = [b"EDTR", struct.pack("<II", ver, len(self.sdps))]
@@ -125,6 +136,8 @@ class Trace:
                 _, t, s, ch, addr, port, data = ev
                 out.append(struct.pack("<BqIBIHI", UPKT, t, s, ch, addr, port, len(data)))
                 out.append(data)
+            elif ev[0] == LEAVE:
+                out.append(struct.pack("<BqI", LEAVE, ev[1], ev[2]))
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -172,6 +185,10 @@ class Trace:
                 _, t, sub, trk, kind, budget = struct.unpack_from("<BqIHBI", buf, p)
                 p += 20
                 tr.events.append((BLOCK, t, sub, trk, kind, budget))
+            elif typ == LEAVE:
+                _, t, sub = struct.unpack_from("<BqI", buf, p)
+                p += 13
+                tr.events.append((LEAVE, t, sub))
             elif typ == UPKT:
                 _, t, s, ch, addr, port, ln = struct.unpack_from("<BqIBIHI", buf, p)
                 p += 24

@@ -33,6 +33,10 @@
 //   * UDPSocket::SendTo is link-wrapped: the only caller on this path is
 //     ReflectorStream::SendReceiverReport (:510-527, every kRRInterval from the RTCP sender's
 //     ReflectPackets, :1039-1047), whose datagrams go to the capture's EDRR trailer;
+//   * LEAVE events remove a subscriber as QTSSReflectorModule's RemoveOutput does
+//     (QTSSReflectorModule.cpp:2133-2196): ReflectorSession::RemoveOutput(output, true) -- out
+//     of every track's bucket, DecEyeCount -- then delete the RTPSessionOutput; its capture so
+//     far is kept;
 //   * rand() is link-wrapped to a deterministic sequence (trace.py rr_ssrc): its only caller
 //     on this path is the ReflectorStream constructor's receiver-report SSRC (:167).
 //
@@ -448,6 +452,14 @@ int main(int argc, char** argv) {
             pk->SetPacketData(pktbuf.data(), n);
             OSMutexLocker locker(so->GetDemuxer()->GetMutex());
             so->ProcessPacket(g_now, pk, addr, port);
+        } else if (type == 6) {     // LEAVE
+            UInt32 sub_id = r.get<UInt32>();
+            for (auto& sb : subs)
+                if (sb.id == sub_id && sb.output != NULL) {
+                    sessions[sb.session]->RemoveOutput(sb.output, true);
+                    delete sb.output;
+                    sb.output = NULL;
+                }
         } else if (type == 4) {     // BLOCK
             UInt32 sub_id = r.get<UInt32>();
             UInt16 track = r.get<UInt16>();

@@ -202,6 +202,7 @@ struct Session {
     std::vector<Stream> streams;
     bool video_key_flag = false;      // ReflectorSession::fHasVideoKeyFrameUpdate
     std::vector<std::unique_ptr<Output>> outputs;   // bucket order == join order here
+    std::vector<std::unique_ptr<Output>> left;      // removed outputs (their captures stay)
     bool udp_push = false;
 };
 
@@ -462,6 +463,20 @@ struct Model {
         reports.push_back({now, si, (uint16_t)x, st.dest_addr, st.dest_port, std::move(b)});
     }
 
+    // ReflectorSession::RemoveOutput(output, isClient) + delete (QTSSReflectorModule.cpp:
+    // 2133-2196, ReflectorSession.cpp:255-279): out of every track's bucket, so the eye count
+    // drops (DecEyeCount).  Its bookmarked packets stay pinned (fNeededByOutput is not
+    // cleared), exactly as when the reference deletes the output.
+    void leave(uint32_t sub_id) {
+        for (auto& se : sessions)
+            for (size_t i = 0; i < se->outputs.size(); i++)
+                if (se->outputs[i]->sub_id == sub_id) {
+                    se->left.push_back(std::move(se->outputs[i]));
+                    se->outputs.erase(se->outputs.begin() + (long)i);
+                    return;
+                }
+    }
+
     void block(uint32_t sub_id, uint32_t track, uint32_t kind, uint32_t budget) {
         for (auto& se : sessions)
             for (auto& o : se->outputs)
@@ -527,6 +542,8 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
             uint8_t kind = r.get<uint8_t>();
             uint32_t budget = r.get<uint32_t>();
             m.block(sub, trk, kind, budget);
+        } else if (type == 6) {                 // LEAVE
+            m.leave(r.get<uint32_t>());
         } else if (type == 5) {                 // UPKT: a datagram from the pusher's address
             uint32_t s = r.get<uint32_t>();
             uint8_t ch = r.get<uint8_t>();
@@ -550,8 +567,9 @@ static int run_capture(const char* in, const char* out) {
     struct Rec { uint32_t sub, sess; uint16_t track; relay::Output* o; };
     std::vector<Rec> recs;
     for (uint32_t s = 0; s < m.sessions.size(); s++)
-        for (auto& o : m.sessions[s]->outputs)
-            for (uint16_t x = 0; x < m.sessions[s]->streams.size(); x++) recs.push_back({o->sub_id, s, x, o.get()});
+        for (auto* v : {&m.sessions[s]->outputs, &m.sessions[s]->left})
+            for (auto& o : *v)
+                for (uint16_t x = 0; x < m.sessions[s]->streams.size(); x++) recs.push_back({o->sub_id, s, x, o.get()});
     std::stable_sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) {
         return a.sub != b.sub ? a.sub < b.sub : a.track < b.track; });
     FILE* f = fopen(out, "wb");
@@ -621,6 +639,9 @@ static int run_bench(const char* in, int threads, int repeat) {
             lists[e.s % threads].push_back(e);
         } else if (e.type == 4) {
             r.p += 11;                          // BLOCK: the bench's sinks never block
+        } else if (e.type == 6) {
+            e.sub = r.get<uint32_t>();
+            for (auto& l : lists) l.push_back(e);
         } else {
             for (auto& l : lists) l.push_back(e);
         }
@@ -648,10 +669,14 @@ static int run_bench(const char* in, int threads, int repeat) {
                     sinks.emplace_back(new std::vector<uint8_t>());
                     sinks.back()->reserve(1 << 20);
                     m.join(e.s, e.sub, e.tcp, sinks.back().get(), (e.ua & 1) != 0);
+                } else if (e.type == 6) {
+                    m.leave(e.sub);
                 } else m.tick();
             }
             uint64_t p = 0, b = 0;
-            for (auto& se : m.sessions) for (auto& o : se->outputs) { p += o->sink_pkts; b += o->sink_bytes; }
+            for (auto& se : m.sessions)
+                for (auto* v : {&se->outputs, &se->left})
+                    for (auto& o : *v) { p += o->sink_pkts; b += o->sink_bytes; }
             pkts += p; bytes += b;
             }
             busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();

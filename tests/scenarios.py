@@ -31,6 +31,9 @@ parity consequence:
                     the RTCP SR-only gate (Q14), the pusher's RTCP address learnt from the
                     first datagram and moved by later SRs (NAT_WORKAROUND), and the receiver
                     reports with the eye count sent to it every 5 s.
+* ``leave``         subscribers leaving (RemoveOutput): between ticks, while blocked, leave +
+                    new output in one tick, join + leave before a tick, an RTP-Info player,
+                    and the eye counts of the receiver reports after leaves.
 """
 from __future__ import annotations
 
@@ -44,19 +47,21 @@ from easydarwin_amd.trace import TCP, UDP, Trace
 
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
-              joins: list[tuple], tick_times=None, blocks=None):
+              joins: list[tuple], tick_times=None, blocks=None, leaves=None):
     # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
     # blocks: {tick time: [(sub, track, kind, budget)]}
+    # leaves: [(t, sub)]
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
     and ticks.  Within one tick interval the order is: packets (time order, session order),
-    then joins, then the tick's socket budgets (BLOCK), then the TICK at the interval end."""
+    then joins and leaves (time order; a join before a leave of the same time), then the
+    tick's socket budgets (BLOCK), then the TICK at the interval end."""
     # a packet (t, ch, data, addr, port) is a UDP datagram from a pusher (UPKT)
     pkts = []
     for s, lst in enumerate(per_session):
         for k, p in enumerate(lst):
             pkts.append((p[0], s, k) + tuple(p[1:]))
     pkts.sort(key=lambda x: (x[0], x[1], x[2]))
-    joins = sorted(joins)
+    joins = sorted([(j[0], 0) + tuple(j[1:]) for j in joins] + [(t, 1, sub) for t, sub in (leaves or [])])
     ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
     i = j = 0
     for tt in ticks:
@@ -68,8 +73,11 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
                 tr.pkt(t, s, ch, data)
             i += 1
         while j < len(joins) and joins[j][0] <= tt:
-            t, s, sub, transport = joins[j][:4]
-            tr.join(t, s, sub, transport, joins[j][4] if len(joins[j]) > 4 else 0)
+            if joins[j][1] == 1:
+                tr.leave(joins[j][0], joins[j][2])
+            else:
+                t, _, s, sub, transport = joins[j][:5]
+                tr.join(t, s, sub, transport, joins[j][5] if len(joins[j]) > 5 else 0)
             j += 1
         for sub, trk, kind, budget in (blocks or {}).get(tt, []):
             tr.block(tt, sub, trk, kind, budget)
@@ -402,8 +410,45 @@ def udppush() -> Trace:
     return _assemble(tr, [pk0, pk1, pk2, pk3], 100, dur, joins)
 
 
+def leave() -> Trace:
+    """Subscribers leaving (TEARDOWN / disconnect): QTSSReflectorModule's
+    RemoveOutput -> ReflectorSession::RemoveOutput(output, isClient) + delete
+    (QTSSReflectorModule.cpp:2133-2196, ReflectorSession.cpp:255-279, ReflectorStream.cpp:
+    338-362).
+
+    * session 0 (RTSP-interleaved push, H.264 + PCMA, pusher SRs on the video RTCP channel):
+      a leave between two ticks (1), a TCP subscriber leaving while its socket is blocked (2),
+      a leave and a new output of the same player in one tick interval (3 -> 4), a join and a
+      leave before any tick (5: never receives), an RTP-Info player leaving (6), a control
+      subscriber that stays (7);
+    * session 1 (UDP push): subscribers come and go around the 5-s receiver-report times, so
+      the eye counts the reports carry (DecEyeCount) change: 5, then 3, 4 and 2; a deferred
+      RTP-Info PLAY (15: before the first packet, never an output) and a sub id that was
+      never used leave without effect."""
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=600_000, gop=30, idr_bytes=8_000, rtcp_every_ms=600),
+         TrackSpec("audio", "PCMA/8000", 8)]
+    u = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=30, idr_bytes=5_000, rtcp_every_ms=700)]
+    tr = Trace()
+    tr.add_session(make_sdp(v))
+    tr.add_session(make_sdp(u), udp_push=True)
+    dur = 16_000
+    pk0 = session_packets(v, 6000, SEED_BASE + 90)
+    src = _ip(10, 0, 0, 9)
+    pk1 = [(t, ch, data, src, 7000 + (ch & 1)) for t, ch, data in session_packets(u, dur, SEED_BASE + 91, t0=100)]
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (300, 0, 3, UDP), (1000, 0, 5, TCP), (1300, 0, 6, UDP, VLC),
+             (0, 0, 7, TCP), (2550, 0, 4, UDP),
+             (0, 1, 15, UDP, VLC), (100, 1, 10, UDP), (100, 1, 11, TCP), (200, 1, 12, UDP), (400, 1, 13, UDP),
+             (600, 1, 14, TCP), (8000, 1, 16, UDP)]
+    leaves = [(1550, 1), (2450, 2), (2550, 3), (1000, 5), (3000, 6), (500, 15), (6000, 10), (6000, 11),
+              (11000, 12), (11000, 16), (11050, 99)]
+    blocks = {}
+    for t in range(2000, 2500, 100):
+        blocks.setdefault(t, []).extend([(2, 0, 0, 0), (2, 1, 0, 1)])
+    return _assemble(tr, [pk0, pk1], 100, dur, joins, blocks=blocks, leaves=leaves)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
-    "backpressure": backpressure, "udppush": udppush,
+    "backpressure": backpressure, "udppush": udppush, "leave": leave,
 }

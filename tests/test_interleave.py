@@ -186,5 +186,5 @@ def test_replay_pusher_model_delivers_every_packet(name):
         for s, ch, t, data in b:
             want.setdefault(s, []).append((ch, t, data))
         assert got == want
-    assert calls >= len(batches)                    # more when keep-alives were answered
+    assert calls >= sum(1 for b in batches if b)    # more when keep-alives were answered
     assert not any(ctx.carry.values())

@@ -2,7 +2,8 @@
 // event trace, the way the reflector module would: PKT -> Reflector::PushPacket (track =
 // channel/2, RTCP = channel&1, as ProcessRTPData does, QTSSReflectorModule.cpp:654-671),
 // JOIN -> AddOutput, TICK -> ReflectPackets(now, sink), BLOCK -> the sink returns kWouldBlock
-// after the scripted number of writes in the next tick, UPKT (UDP push) -> ProcessUDPPacket;
+// after the scripted number of writes in the next tick, UPKT (UDP push) -> ProcessUDPPacket,
+// LEAVE -> RemoveOutput;
 // receiver reports reach the sink's SendReceiverReport.  Writes the capture format of
 // easydarwin_amd/trace.py so tests compare it with the reference harness byte for byte.
 // Usage: adapter_replay <trace.edtr> <capture.edcp>
@@ -113,6 +114,10 @@ int main(int argc, char** argv) {
             int err = R.ReflectPackets(t, &sink);
             if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
             sink.budget.clear();
+        } else if (type == 6) {               // LEAVE: ReflectorSession::RemoveOutput
+            uint32_t sub; get(sub);
+            for (auto& kv : handles)
+                if (std::get<0>(kv.second) == sub && R.RemoveOutput(kv.first) == kNoErr) break;
         } else if (type == 4) {               // BLOCK: the sub-stream's socket takes `budget` writes
             uint32_t sub, budget; uint16_t trk; uint8_t kind;
             get(sub); get(trk); get(kind); get(budget);
