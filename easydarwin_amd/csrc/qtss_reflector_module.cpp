@@ -1,0 +1,564 @@
+// qtss_reflector_module.cpp -- QTSSReflectorModule for EasyDarwin, backed by the MI355X relay
+// engine: the drop-in for the reference module's live-relay path.
+//
+// The server loads it like the reference module -- QTSSReflectorModule_Main hands back the
+// dispatch function (QTSSReflectorModule.cpp:228-262) -- and drives it through the same roles:
+//
+//   role                      reference handler (QTSSReflectorModule.cpp)   here
+//   Register                  Register (:265-365)                           roles + attributes
+//   Initialize / Shutdown     Initialize (:368-409) / Shutdown              engine context, tick thread
+//   RTSPPreProcessor          ProcessRTSPRequest (:681-729)                 ANNOUNCE / DESCRIBE / SETUP /
+//                                                                           PLAY / RECORD / PAUSE / TEARDOWN
+//   RTSPIncomingData          ProcessRTPData (:604-678)                     '$' frame -> PushPacket
+//   ClientSessionClosing      DestroySession (:2070-2131)                   RemoveOutput
+//
+// and writes every relayed packet back through QTSS_Write (callback 10) on the subscriber's
+// RTP stream object with qtssWriteFlagsIsRTP / IsRTCP | WriteBurstBegin, exactly as
+// RTPSessionOutput::WritePacket does (RTPSessionOutput.cpp:564-662); the server's
+// RTPStream::Write then frames it (UDP datagram or '$' ch BE16(len), RTPStream.cpp:1048-1259).
+// QTSS_WouldBlock from the server stops that sub-stream for the tick and the engine bookmarks
+// the blocked packet (SendPacketsToOutput, ReflectorStream.cpp:1138-1198).
+//
+// What runs where: every packet-rate step (ingest parse, SSRC latch, keyframe index, fan-out
+// planning and the write-many copy) runs on the GPU through the edgpu C ABI (via
+// edgpu_reflector::Reflector, reflector_adapter.h); this file is RTSP-session bookkeeping.
+// Reflect cadence: the reference reflects from ReflectorSocket tasks on packet arrival and
+// sender wakeups (ReflectorStream.cpp:1676-1714); here a tick thread reflects every
+// edgpu_tick_msec (default 20 ms), or the host calls EDGPU_QTSSReflectorModule_Tick.
+//
+// Scope: RTSP-interleaved pushers (EasyPusher's default transport) and
+// UDP / TCP players.  A UDP-transport push SETUP is refused (those pushers reach the engine
+// through edgpu_udp_sources from a host socket reader, as the C++ adapter's ProcessUDPPacket
+// does); RTSPRoute / RTSPAuthorize / Easy_GetDeviceStream (redirects, access files, the CMS
+// control plane) are not registered.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "qtss_module_abi.h"
+#include "reflector_adapter.h"
+
+using namespace edqtss;
+
+namespace {
+
+// ---- the module side of the callback table (QTSS_Private.cpp's stubs) ----------------------
+QTSS_Callbacks* sCallbacks = nullptr;
+
+template <typename... A>
+QTSS_Error cb(uint32_t index, A... args) {
+    if (!sCallbacks || index >= kLastCallback || !sCallbacks->addr[index]) return QTSS_Unimplemented;
+    return (sCallbacks->addr[index])(args...);
+}
+int64_t Milliseconds() {
+    int64_t t = 0;
+    if (cb(kMillisecondsCallback, &t) != QTSS_NoErr)
+        t = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    return t;
+}
+QTSS_Error GetValuePtr(QTSS_Object o, QTSS_AttributeID id, uint32_t idx, void** buf, uint32_t* len) {
+    *buf = nullptr;
+    *len = 0;
+    return cb(kGetAttributePtrByIDCallback, o, id, idx, buf, len);
+}
+QTSS_Error GetValue(QTSS_Object o, QTSS_AttributeID id, uint32_t idx, void* buf, uint32_t* len) {
+    return cb(kGetAttributeByIDCallback, o, id, idx, buf, len);
+}
+QTSS_Error SetValue(QTSS_Object o, QTSS_AttributeID id, uint32_t idx, const void* buf, uint32_t len) {
+    return cb(kSetAttributeByIDCallback, o, id, idx, buf, len);
+}
+std::string GetString(QTSS_Object o, QTSS_AttributeID id) {
+    void* p = nullptr;
+    uint32_t n = 0;
+    if (GetValuePtr(o, id, 0, &p, &n) != QTSS_NoErr || !p) return std::string();
+    return std::string((const char*)p, n);
+}
+template <typename T>
+bool GetPOD(QTSS_Object o, QTSS_AttributeID id, T* out) {
+    void* p = nullptr;
+    uint32_t n = 0;
+    if (GetValuePtr(o, id, 0, &p, &n) != QTSS_NoErr || !p || n != sizeof(T)) return false;
+    memcpy(out, p, sizeof(T));
+    return true;
+}
+
+// ---- module state ---------------------------------------------------------------------------
+// attributes the module adds (the reference's names, QTSSReflectorModule.cpp:313-346)
+QTSS_AttributeID sOutputAttr, sClientBroadcastSessionAttr, sRTSPBroadcastSessionAttr, sStreamCookieAttr,
+    sRequestBodyAttr, sBufferOffsetAttr, sRTPInfoWaitTimeAttr;
+
+struct Session {                        // a pushed stream ("<path>-<channel>", QRM:1384)
+    std::string name;
+    uint32_t engine = 0;                // edgpu session
+    std::vector<uint32_t> trackIDs;     // a=control:trackID=N per m= line, SDP order
+    std::vector<bool> setupToReceive;   // StreamInfo::fSetupToReceive
+    std::string sdp;
+};
+
+struct Output {                         // one player (RTPSessionOutput)
+    QTSS_Object client = nullptr;
+    uint32_t session = 0;
+    bool tcp = false;
+    bool joined = false;                // engine subscriber exists
+    bool paused = false;
+    uint32_t handle = 0;
+    std::vector<QTSS_Object> streams;   // per track: the RTP stream object SETUP created (or null)
+};
+
+struct Module {
+    std::mutex mu;                      // the reference's session-map / bucket mutexes, one lock here
+    std::unique_ptr<edgpu_reflector::Reflector> R;
+    std::map<std::string, std::string> announced;         // CSdpCache: stream name -> SDP
+    std::map<std::string, uint32_t> byName;
+    std::vector<Session> sessions;
+    std::map<uint32_t, Output*> byHandle;
+    std::vector<std::unique_ptr<Output>> outputs;
+    std::vector<std::string> rtpInfoPlayers{"Android", "vlc"};  // player_requires_rtp_header_info
+    int32_t rtpInfoWaitLoops = 10;      // sWaitTimeLoopCount: 100-ms PLAY retries before 404
+    uint32_t tickMs = 20;
+    bool manualTick = false;
+    std::thread ticker;
+    std::atomic<bool> stop{false};
+    QTSS_Error tickErr = QTSS_NoErr;
+};
+Module* M = nullptr;
+
+// "<file path without /trackID=N and leading '/'>-<channel>", the stream ID of the reference
+// (theStreamName, QRM:923-925 / 1384), channel from the query's "channel=" (EASY_TAG_CHANNEL)
+std::string StreamName(QTSS_Object req) {
+    std::string path = GetString(req, qtssRTSPReqFilePath);
+    const size_t tr = path.find("/trackID=");
+    if (tr != std::string::npos) path.resize(tr);
+    while (!path.empty() && path[0] == '/') path.erase(0, 1);
+    uint32_t channel = 1;
+    const std::string q = GetString(req, qtssRTSPReqQueryString);
+    const size_t c = q.find("channel=");
+    if (c != std::string::npos && (c == 0 || q[c - 1] == '&')) channel = (uint32_t)strtoul(q.c_str() + c + 8, nullptr, 10);
+    return path + "-" + std::to_string(channel);
+}
+
+uint32_t TrackFromRequest(QTSS_Object req, bool* ok) {
+    const std::string digits = GetString(req, qtssRTSPReqFileDigit);
+    *ok = !digits.empty();
+    return (uint32_t)strtoul(digits.c_str(), nullptr, 10);
+}
+
+// a=control:trackID=N per m= section, in SDP order (SDPSourceInfo.cpp:260-353 reads the same
+// lines; a section without one gets its 1-based position)
+std::vector<uint32_t> SdpTrackIDs(const std::string& sdp) {
+    std::vector<uint32_t> ids;
+    size_t p = 0;
+    while (p < sdp.size()) {
+        size_t e = sdp.find_first_of("\r\n", p);
+        if (e == std::string::npos) e = sdp.size();
+        const std::string line = sdp.substr(p, e - p);
+        p = e;
+        while (p < sdp.size() && (sdp[p] == '\r' || sdp[p] == '\n')) p++;
+        if (line.compare(0, 2, "m=") == 0) ids.push_back((uint32_t)ids.size() + 1);
+        else if (!ids.empty() && line.compare(0, 18, "a=control:trackID=") == 0)
+            ids.back() = (uint32_t)strtoul(line.c_str() + 18, nullptr, 10);
+    }
+    return ids;
+}
+
+int TrackIndex(const Session& s, uint32_t trackID) {
+    for (size_t i = 0; i < s.trackIDs.size(); i++)
+        if (s.trackIDs[i] == trackID) return (int)i;
+    return -1;
+}
+
+// ---- the egress seam: RTPSessionOutput::WritePacket -> QTSS_Write ---------------------------
+class QTSSSink : public edgpu_reflector::OutputSink {
+public:
+    int64_t now = 0;
+    int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
+                    uint32_t wireLen, uint32_t) override {
+        auto it = M->byHandle.find(subscriber);
+        if (it == M->byHandle.end()) return edgpu_reflector::kNoErr;
+        Output& o = *it->second;
+        // not playing (paused): WritePacket returns QTSS_WouldBlock (RTPSessionOutput.cpp:575-579)
+        if (o.paused) return edgpu_reflector::kWouldBlock;
+        if (track >= o.streams.size() || !o.streams[track]) return edgpu_reflector::kNoErr;   // track not SETUP
+        // the server frames interleaved packets itself (RTPStream::Write): hand it the packet
+        const uint8_t* pkt = interleaved ? wire + 4 : wire;
+        const uint32_t len = interleaved ? wireLen - 4 : wireLen;
+        QTSS_PacketStruct ps;
+        ps.packetData = const_cast<uint8_t*>(pkt);
+        ps.packetTransmitTime = now;
+        ps.suggestedWakeupTime = -1;
+        const uint32_t flags = (isRTCP ? qtssWriteFlagsIsRTCP : qtssWriteFlagsIsRTP) | qtssWriteFlagsWriteBurstBegin;
+        const QTSS_Error err = cb(kWriteCallback, o.streams[track], (const void*)&ps, len, (uint32_t*)nullptr, flags);
+        // only QTSS_WouldBlock stops SendPacketsToOutput (ReflectorStream.cpp:1158-1190)
+        return err == QTSS_WouldBlock ? edgpu_reflector::kWouldBlock : edgpu_reflector::kNoErr;
+    }
+};
+
+QTSS_Error Tick() {
+    std::lock_guard<std::mutex> g(M->mu);
+    if (!M->R) return QTSS_RequestFailed;
+    QTSSSink sink;
+    sink.now = Milliseconds();
+    const int err = M->R->ReflectPackets(sink.now, &sink);
+    return err == 0 ? QTSS_NoErr : QTSS_RequestFailed;
+}
+
+// ---- roles ----------------------------------------------------------------------------------
+QTSS_Error Register(QTSS_Register_Params* p) {
+    for (QTSS_Role r : {QTSS_Initialize_Role, QTSS_Shutdown_Role, QTSS_RTSPPreProcessor_Role,
+                        QTSS_ClientSessionClosing_Role, QTSS_RTSPIncomingData_Role, QTSS_RereadPrefs_Role})
+        (void)cb(kAddRoleCallback, r);
+    struct { QTSS_ObjectType type; const char* name; QTSS_AttrDataType dt; QTSS_AttributeID* id; } attrs[] = {
+        {qtssClientSessionObjectType, "QTSSReflectorModuleRTPInfoWaitTime", qtssAttrDataTypeSInt32, &sRTPInfoWaitTimeAttr},
+        {qtssClientSessionObjectType, "QTSSReflectorModuleOutput", qtssAttrDataTypeVoidPointer, &sOutputAttr},
+        {qtssRTPStreamObjectType, "QTSSReflectorModuleStreamCookie", qtssAttrDataTypeVoidPointer, &sStreamCookieAttr},
+        {qtssRTSPRequestObjectType, "QTSSReflectorModuleRequestBuffer", qtssAttrDataTypeVoidPointer, &sRequestBodyAttr},
+        {qtssRTSPRequestObjectType, "QTSSReflectorModuleRequestBufferLen", qtssAttrDataTypeUInt32, &sBufferOffsetAttr},
+        {qtssClientSessionObjectType, "QTSSReflectorModuleBroadcasterSession", qtssAttrDataTypeVoidPointer,
+         &sClientBroadcastSessionAttr},
+        {qtssRTSPSessionObjectType, "QTSSReflectorModuleBroadcasterSession", qtssAttrDataTypeVoidPointer,
+         &sRTSPBroadcastSessionAttr},
+    };
+    for (auto& a : attrs) {
+        (void)cb(kAddStaticAttributeCallback, a.type, a.name, (void*)nullptr, a.dt);
+        (void)cb(kIDForTagCallback, a.type, a.name, a.id);
+    }
+    if (p) snprintf(p->outModuleName, sizeof(p->outModuleName), "%s", "QTSSReflectorModule");
+    return QTSS_NoErr;
+}
+
+QTSS_Error Initialize(QTSS_Initialize_Params*) {
+    std::lock_guard<std::mutex> g(M->mu);
+    if (const char* v = getenv("EDGPU_QTSS_TICK_MSEC")) M->tickMs = (uint32_t)std::max(1, atoi(v));
+    if (const char* v = getenv("EDGPU_QTSS_MANUAL_TICK")) M->manualTick = atoi(v) != 0;
+    edgpu_config cfg;
+    edgpu_config_default(&cfg);
+    if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
+    M->R.reset(new edgpu_reflector::Reflector(&cfg));
+    if (M->R->Status() != 0) {
+        fprintf(stderr, "QTSSReflectorModule: edgpu context: %s\n", edgpu_last_error());
+        M->R.reset();
+        return QTSS_RequestFailed;          // no gfx950 device: fail loudly, no CPU fallback
+    }
+    if (!M->manualTick) {
+        M->stop = false;
+        M->ticker = std::thread([] {
+            while (!M->stop.load()) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(M->tickMs));
+                if (M->stop.load()) break;
+                const QTSS_Error e = Tick();
+                if (e) M->tickErr = e;
+            }
+        });
+    }
+    return QTSS_NoErr;
+}
+
+QTSS_Error Shutdown() {
+    M->stop = true;
+    if (M->ticker.joinable()) M->ticker.join();
+    std::lock_guard<std::mutex> g(M->mu);
+    M->R.reset();
+    return QTSS_NoErr;
+}
+
+// ANNOUNCE (DoAnnounce, QRM:898-1174): read the request body (QTSS_Read, resumable), keep the
+// SDP under the stream name for the pusher's SETUPs and the players' DESCRIBE
+QTSS_Error DoAnnounce(QTSS_StandardRTSP_Params* p) {
+    const std::string path = GetString(p->inRTSPRequest, qtssRTSPReqFilePath);
+    if (path.size() < 4 || path.compare(path.size() - 4, 4, ".sdp") != 0) return QTSS_RequestFailed;
+    uint32_t clen = 0;
+    if (!GetPOD(p->inRTSPRequest, qtssRTSPReqContentLen, &clen)) return QTSS_RequestFailed;
+    std::string* body = nullptr;
+    if (!GetPOD(p->inRTSPRequest, sRequestBodyAttr, &body) || !body) {
+        body = new std::string();
+        (void)SetValue(p->inRTSPRequest, sRequestBodyAttr, 0, &body, sizeof(body));
+    }
+    if (body->size() < clen) {
+        const size_t off = body->size();
+        body->resize(clen);
+        uint32_t got = 0;
+        const QTSS_Error e = cb(kReadCallback, p->inRTSPRequest, (void*)&(*body)[off], (uint32_t)(clen - off), &got);
+        if (e != QTSS_NoErr && e != QTSS_WouldBlock) { delete body; (void)SetValue(p->inRTSPRequest, sRequestBodyAttr, 0, nullptr, 0); return QTSS_RequestFailed; }
+        body->resize(off + got);
+        if (body->size() < clen) {               // the rest arrives later: ask to be called again
+            (void)cb(kRequestEventCallback, p->inRTSPRequest, (uint32_t)1 /* QTSS_ReadableEvent */);
+            return QTSS_NoErr;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(M->mu);
+        M->announced[StreamName(p->inRTSPRequest)] = *body;
+    }
+    delete body;
+    std::string* none = nullptr;
+    (void)SetValue(p->inRTSPRequest, sRequestBodyAttr, 0, &none, sizeof(none));
+    return cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
+}
+
+// DESCRIBE (DoDescribe, QRM:1176-1377): the announced SDP
+QTSS_Error DoDescribe(QTSS_StandardRTSP_Params* p) {
+    std::string sdp;
+    {
+        std::lock_guard<std::mutex> g(M->mu);
+        auto it = M->announced.find(StreamName(p->inRTSPRequest));
+        if (it == M->announced.end()) return QTSS_RequestFailed;
+        sdp = it->second;
+    }
+    const std::string n = std::to_string(sdp.size());
+    (void)cb(kAppendRTSPHeadersCallback, p->inRTSPRequest, (uint32_t)qtssContentLengthHeader, n.c_str(), (uint32_t)n.size());
+    (void)cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
+    return cb(kWriteCallback, p->inRTSPRequest, (const void*)sdp.data(), (uint32_t)sdp.size(), (uint32_t*)nullptr,
+              (uint32_t)qtssWriteFlagsNoFlags);
+}
+
+// FindOrCreateSession (QRM:1379-1545): the engine session of an announced stream
+Session* FindOrCreateSession(const std::string& name) {
+    auto it = M->byName.find(name);
+    if (it != M->byName.end()) return &M->sessions[it->second];
+    auto a = M->announced.find(name);
+    if (a == M->announced.end() || !M->R) return nullptr;
+    Session s;
+    s.name = name;
+    s.sdp = a->second;
+    if (M->R->SetupReflectorSession(s.sdp, false, &s.engine) != 0) return nullptr;
+    s.trackIDs = SdpTrackIDs(s.sdp);
+    s.trackIDs.resize(M->R->GetNumStreams(s.engine));
+    for (size_t i = 0; i < s.trackIDs.size(); i++) if (!s.trackIDs[i]) s.trackIDs[i] = (uint32_t)i + 1;
+    s.setupToReceive.assign(s.trackIDs.size(), false);
+    M->sessions.push_back(s);
+    M->byName[name] = (uint32_t)M->sessions.size() - 1;
+    return &M->sessions.back();
+}
+
+// SETUP (DoSetup, QRM:1597-1800)
+QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
+    uint32_t mode = qtssRTPTransportModePlay, transport = qtssRTPTransportTypeUDP;
+    (void)GetPOD(p->inRTSPRequest, qtssRTSPReqTransportMode, &mode);
+    (void)GetPOD(p->inRTSPRequest, qtssRTSPReqTransportType, &transport);
+    const bool isPush = mode == qtssRTPTransportModeRecord;
+    bool digitOK = false;
+    const uint32_t trackID = TrackFromRequest(p->inRTSPRequest, &digitOK);
+    std::lock_guard<std::mutex> g(M->mu);
+    if (isPush) {
+        // RTSP-interleaved pushers only: the engine's host reader takes UDP pushers' datagrams
+        if (transport != qtssRTPTransportTypeTCP) return QTSS_RequestFailed;
+        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest));
+        if (!s || !digitOK) return QTSS_RequestFailed;
+        const int t = TrackIndex(*s, trackID);
+        if (t < 0 || s->setupToReceive[t]) return QTSS_RequestFailed;      // bad / duplicate track
+        QTSS_Object stream = nullptr;
+        QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
+        if (e != QTSS_NoErr) return e;
+        s->setupToReceive[t] = true;
+        const uintptr_t sid = (uintptr_t)(s - &M->sessions[0]) + 1;
+        (void)SetValue(p->inClientSession, sClientBroadcastSessionAttr, 0, &sid, sizeof(sid));
+        return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)0);
+    }
+    // a player: the first SETUP creates its output (QRM:1628-1650)
+    Output* o = nullptr;
+    if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {
+        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest));
+        if (!s) return QTSS_RequestFailed;
+        M->outputs.emplace_back(new Output());
+        o = M->outputs.back().get();
+        o->client = p->inClientSession;
+        o->session = (uint32_t)(s - &M->sessions[0]);
+        o->tcp = transport == qtssRTPTransportTypeTCP;
+        o->streams.assign(s->trackIDs.size(), nullptr);
+        (void)SetValue(p->inClientSession, sOutputAttr, 0, &o, sizeof(o));
+    }
+    const Session& s = M->sessions[o->session];
+    const int t = digitOK ? TrackIndex(s, trackID) : -1;
+    if (t < 0) return QTSS_RequestFailed;
+    QTSS_Object stream = nullptr;
+    QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
+    if (e != QTSS_NoErr) return e;
+    (void)SetValue(stream, qtssRTPStrTrackID, 0, &trackID, sizeof(trackID));
+    const uintptr_t cookie = ((uintptr_t)o->session << 16) | (uint32_t)t;          // the stream cookie
+    (void)SetValue(stream, sStreamCookieAttr, 0, &cookie, sizeof(cookie));
+    o->streams[t] = stream;
+    return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)qtssSetupRespDontWriteSSRC);
+}
+
+bool RequiresRTPInfo(QTSS_Object client) {
+    const std::string ua = GetString(client, qtssCliSesFirstUserAgent);
+    if (ua.empty()) return false;
+    for (const std::string& pl : M->rtpInfoPlayers)
+        if (pl == "*" || ua.find(pl) != std::string::npos) return true;     // FindStringInAttributeList
+    return false;
+}
+
+// PLAY / RECORD (DoPlay, QRM:1867-2023)
+QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
+    uint32_t flags = 0;
+    if (!o) {                                             // the pusher's RECORD / PLAY
+        uintptr_t sid = 0;
+        if (!GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &sid) || !sid) return QTSS_RequestFailed;
+        (void)SetValue(p->inRTSPSession, sRTSPBroadcastSessionAttr, 0, &sid, sizeof(sid));
+        const bool keep = true;
+        (void)SetValue(p->inRTSPRequest, qtssRTSPReqRespKeepAlive, 0, &keep, sizeof(keep));
+    } else {
+        std::unique_lock<std::mutex> g(M->mu);
+        if (o->joined && o->paused) {                     // resume after PAUSE
+            o->paused = false;
+        } else if (!o->joined) {
+            const bool tcp = o->tcp;
+            uint32_t h = 0;
+            int err;
+            if (RequiresRTPInfo(o->client)) {
+                flags = qtssPlayRespWriteTrackInfo;
+                std::vector<edgpu_rtp_info> info;
+                err = M->R->PlayRTPInfo(M->sessions[o->session].engine, tcp, Milliseconds(), &h, &info);
+                if (err == edgpu_reflector::kWouldBlock) {
+                    // nothing buffered yet: retry the PLAY from the idle timer, then give up (QRM:1985-2003)
+                    int32_t loops = 0;
+                    uint32_t n = sizeof(loops);
+                    if (GetValue(p->inClientSession, sRTPInfoWaitTimeAttr, 0, &loops, &n) != QTSS_NoErr)
+                        loops = M->rtpInfoWaitLoops;
+                    else if (loops < 1)
+                        return QTSS_RequestFailed;
+                    else
+                        loops--;
+                    (void)SetValue(p->inClientSession, sRTPInfoWaitTimeAttr, 0, &loops, sizeof(loops));
+                    g.unlock();
+                    return cb(kSetIdleTimerCallback, (int64_t)100);
+                }
+                if (err) return QTSS_RequestFailed;
+                for (size_t t = 0; t < o->streams.size() && t < info.size(); t++) {
+                    if (!o->streams[t]) continue;
+                    (void)SetValue(o->streams[t], qtssRTPStrFirstSeqNumber, 0, &info[t].seq, sizeof(info[t].seq));
+                    (void)SetValue(o->streams[t], qtssRTPStrFirstTimestamp, 0, &info[t].rtptime, sizeof(info[t].rtptime));
+                }
+            } else if ((err = M->R->AddOutput(M->sessions[o->session].engine, tcp, &h)) != 0) {
+                return QTSS_RequestFailed;
+            }
+            o->handle = h;
+            o->joined = true;
+            M->byHandle[h] = o;
+        }
+        g.unlock();
+        const QTSS_Error e = cb(kPlayCallback, p->inClientSession, p->inRTSPRequest,
+                                (uint32_t)(flags ? qtssPlayRespWriteTrackInfo : qtssPlayFlagsAppendServerInfo));
+        if (e != QTSS_NoErr && e != QTSS_Unimplemented) return e;
+    }
+    return cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, flags);
+}
+
+void RemoveOutputLocked(Output* o) {
+    if (o->joined && M->R) (void)M->R->RemoveOutput(o->handle);
+    M->byHandle.erase(o->handle);
+    for (auto it = M->outputs.begin(); it != M->outputs.end(); ++it)
+        if (it->get() == o) { M->outputs.erase(it); break; }
+}
+
+QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
+    QTSS_RTSPMethod method = 0;
+    if (!GetPOD(p->inRTSPRequest, qtssRTSPReqMethod, &method)) return QTSS_RequestFailed;
+    if (method == qtssAnnounceMethod) return DoAnnounce(p);
+    if (method == qtssDescribeMethod) return DoDescribe(p);
+    if (method == qtssSetupMethod) return DoSetup(p);
+    Output* o = nullptr;
+    if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {     // a broadcaster's session
+        if (method == qtssPlayMethod || method == qtssRecordMethod) return DoPlay(p, nullptr);
+        return QTSS_RequestFailed;
+    }
+    switch (method) {
+    case qtssPlayMethod:
+        return DoPlay(p, o);
+    case qtssTeardownMethod:
+        (void)cb(kTeardownCallback, p->inClientSession);
+        (void)cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
+        break;
+    case qtssPauseMethod: {
+        {
+            std::lock_guard<std::mutex> g(M->mu);
+            o->paused = true;
+        }
+        (void)cb(kPauseCallback, p->inClientSession);
+        (void)cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
+        break;
+    }
+    default:
+        break;
+    }
+    return QTSS_NoErr;
+}
+
+// RTSPIncomingData (ProcessRTPData, QRM:604-678): one '$' ch BE16(len) frame of a pusher
+QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
+    uintptr_t sid = 0;
+    if (!GetPOD(p->inRTSPSession, sRTSPBroadcastSessionAttr, &sid) || !sid) return QTSS_NoErr;
+    if (!p->inPacketData || p->inPacketLen < 4) return QTSS_NoErr;
+    const uint8_t* d = (const uint8_t*)p->inPacketData;
+    const uint8_t channel = d[1];
+    const uint32_t len = (uint32_t)d[2] << 8 | d[3];
+    std::lock_guard<std::mutex> g(M->mu);
+    if (!M->R || sid > M->sessions.size()) return QTSS_NoErr;
+    const Session& s = M->sessions[sid - 1];
+    const uint32_t track = channel / 2;
+    if (track >= s.trackIDs.size()) return QTSS_NoErr;
+    M->R->PushPacket(s.engine, track, (const char*)d + 4, len, (channel & 1) != 0, Milliseconds());
+    return QTSS_NoErr;
+}
+
+// ClientSessionClosing (DestroySession, QRM:2070-2131 -> RemoveOutput :2133-2196)
+QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
+    Output* o = nullptr;
+    if (GetPOD(p->inClientSession, sOutputAttr, &o) && o) {
+        std::lock_guard<std::mutex> g(M->mu);
+        RemoveOutputLocked(o);
+        Output* none = nullptr;
+        (void)SetValue(p->inClientSession, sOutputAttr, 0, &none, sizeof(none));
+        return QTSS_NoErr;
+    }
+    uintptr_t sid = 0;
+    if (GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &sid) && sid) {
+        // the pusher left: its tracks can be set up again (the session and its rings stay, as
+        // the reference keeps a session while outputs hold references to it)
+        std::lock_guard<std::mutex> g(M->mu);
+        if (sid <= M->sessions.size()) {
+            Session& s = M->sessions[sid - 1];
+            s.setupToReceive.assign(s.setupToReceive.size(), false);
+        }
+    }
+    return QTSS_NoErr;
+}
+
+QTSS_Error Dispatch(QTSS_Role role, QTSS_RoleParams* p) {
+    switch (role) {
+    case QTSS_Register_Role: return Register(p ? &p->regParams : nullptr);
+    case QTSS_Initialize_Role: return Initialize(p ? &p->initParams : nullptr);
+    case QTSS_Shutdown_Role: return Shutdown();
+    case QTSS_RereadPrefs_Role: return QTSS_NoErr;
+    case QTSS_RTSPPreProcessor_Role: return ProcessRTSPRequest(&p->rtspRequestParams);
+    case QTSS_RTSPIncomingData_Role: return ProcessRTPData(&p->rtspIncomingDataParams);
+    case QTSS_ClientSessionClosing_Role: return DestroySession(&p->clientSessionClosingParams);
+    default: return QTSS_NoErr;
+    }
+}
+
+}  // namespace
+
+extern "C" QTSS_Error QTSSReflectorModule_Main(void* inPrivateArgs) {
+    // _stublibrary_main (QTSS_Private.cpp:44-59)
+    QTSS_PrivateArgs* a = (QTSS_PrivateArgs*)inPrivateArgs;
+    if (!a) return QTSS_BadArgument;
+    sCallbacks = a->inCallbacks;
+    a->outStubLibraryVersion = kApiVersion;
+    a->outDispatchFunction = Dispatch;
+    if (!M) M = new Module();
+    return QTSS_NoErr;
+}
+
+extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
+    if (!M) return QTSS_RequestFailed;
+    return Tick();
+}

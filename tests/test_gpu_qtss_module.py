@@ -1,0 +1,34 @@
+"""GPU: the QTSS reflector module as a drop-in.
+
+tools/qtss_replay is a fake EasyDarwin server: it dlopens libQTSSReflectorModule.so, calls
+QTSSReflectorModule_Main with a QTSS_PrivateArgs block and a callback table, and drives the
+module through its roles -- ANNOUNCE / SETUP (record, interleaved) / RECORD for every pusher,
+RTSPIncomingData for every pushed '$' frame, SETUP + PLAY for every player (UA "vlc" for an
+RTP-Info player), ClientSessionClosing for a leave -- with a virtual clock and manual reflect
+ticks.  The module's QTSS_Write calls on the players' RTP stream objects, framed as
+RTPStream::Write frames them, must reproduce the REFERENCE reflector's per-subscriber capture
+byte for byte (the golden fixtures, tests/golden/*.json).  Scenarios with UDP pushers are not
+replayed here (the module serves RTSP-interleaved pushers, qtss_reflector_module.cpp).
+"""
+import hashlib
+import os
+import subprocess
+
+import pytest
+
+from test_gpu_parity import _fixture, _trace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODULE = os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so")
+REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
+TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "anchor", "rtpinfo", "backpressure"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TCP_PUSH)
+def test_module_matches_reference(name, tmp_path):
+    t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    t.write_bytes(_trace(name).to_bytes())
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]

@@ -1,0 +1,393 @@
+// tools/qtss_replay.cpp -- a fake EasyDarwin server that loads the reflector MODULE
+// (libQTSSReflectorModule.so) through the QTSS plugin ABI and replays an event trace through
+// its roles, the way Server.tproj would drive the reference QTSSReflectorModule:
+//
+//   * dlopen + QTSSReflectorModule_Main(QTSS_PrivateArgs) -> dispatch function
+//     (QTSServer::LoadCompiledInModules / QTSSModule::SetupModule, QTSS_Private.cpp:44-59);
+//     Register (the roles it adds are checked), then Initialize;
+//   * every push session: ANNOUNCE (SDP body read through QTSS_Read), SETUP per track in
+//     record mode over TCP (RTSP-interleaved, EasyPusher's default), RECORD;
+//   * PKT -> RTSPIncomingData with the '$' ch BE16(len) frame (RTSPSession::
+//     HandleIncomingDataPacket, RTSPSession.cpp:2131-2178);
+//   * JOIN -> a player's SETUP per track (UDP or TCP) and PLAY, user agent "vlc" for an
+//     RTP-Info player (ua_flags bit 0); a PLAY the module defers (QTSS_SetIdleTimer instead of
+//     QTSS_Play) is dropped, as the reference harness drops it;
+//   * LEAVE -> ClientSessionClosing for the player's client session;
+//   * TICK -> EDGPU_QTSSReflectorModule_Tick at the virtual clock (manual-tick mode);
+//   * BLOCK -> the player's RTP stream object accepts `budget` QTSS_Writes in the next tick,
+//     then returns QTSS_WouldBlock (the EAGAIN path of RTPStream::Write).
+// QTSS_Write on an RTP stream object frames the packet as RTPStream::Write does (UDP: the
+// datagram; TCP: '$' channel BE16(len), channels 2*track / 2*track+1 in SETUP order,
+// RTPStream.cpp:472-473, 1084-1147) into per-(subscriber, track, kind) captures, written in the
+// format of easydarwin_amd/trace.py -- so the module's output compares byte for byte with the
+// reference reflector's captures.  UDP-push sessions are skipped (the module serves
+// RTSP-interleaved pushers; see qtss_reflector_module.cpp).
+//
+// Test infrastructure (tests/test_gpu_qtss_module.py, tests/test_qtss_abi.py); not shipped.
+// Usage: qtss_replay <module.so> <trace.edtr> <capture.edcp>
+//        qtss_replay <module.so> --register      (Register role only; no GPU needed)
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "qtss_module_abi.h"
+
+using namespace edqtss;
+
+// ---- objects and attributes -----------------------------------------------------------------
+struct Obj {
+    uint32_t type = 0;
+    std::map<uint32_t, std::vector<std::string>> attrs;   // id -> values by index (stable storage)
+    // RTP stream objects
+    uint32_t sub = 0, session = 0, track = 0;
+    bool tcp = false;
+    uint8_t channel[2] = {0, 1};
+    std::string cap[2];
+    uint64_t npk[2] = {0, 0};
+    int64_t budget[2] = {-1, -1};
+    // RTSP request objects: the body QTSS_Read returns
+    std::string body;
+    size_t body_off = 0;
+    // client sessions
+    bool played = false, idle_timer = false, torn_down = false;
+};
+static std::vector<std::unique_ptr<Obj>> g_objs;
+static Obj* new_obj(uint32_t type) { g_objs.emplace_back(new Obj()); g_objs.back()->type = type; return g_objs.back().get(); }
+
+static void set_attr(Obj* o, uint32_t id, uint32_t idx, const void* p, uint32_t len) {
+    auto& v = o->attrs[id];
+    if (v.size() <= idx) v.resize(idx + 1);
+    v[idx].assign((const char*)p, len);
+}
+template <typename T> static void set_pod(Obj* o, uint32_t id, T v) { set_attr(o, id, 0, &v, sizeof(v)); }
+
+static int64_t g_now = 0;
+static std::set<uint32_t> g_roles;
+static std::map<std::string, uint32_t> g_attr_ids;
+static std::vector<Obj*> g_streams;                  // every RTP stream object, creation order
+
+// ---- callbacks (QTSS_Private.h indices; signatures of the QTSS_Private.cpp stubs) -----------
+static QTSS_Error cb_milliseconds(int64_t* out, ...) { *out = g_now; return QTSS_NoErr; }
+static QTSS_Error cb_add_role(uint32_t role, ...) { g_roles.insert(role); return QTSS_NoErr; }
+static QTSS_Error cb_add_static_attr(uint32_t type, const char* name, void*, uint32_t, ...) {
+    const std::string key = std::to_string(type) + ":" + name;
+    if (!g_attr_ids.count(key)) g_attr_ids[key] = 0x40000000u + (uint32_t)g_attr_ids.size();
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_id_for_tag(uint32_t type, const char* name, uint32_t* out, ...) {
+    auto it = g_attr_ids.find(std::to_string(type) + ":" + name);
+    if (it == g_attr_ids.end()) return QTSS_AttrDoesntExist;
+    *out = it->second;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_get_value_ptr(Obj* o, uint32_t id, uint32_t idx, void** out, uint32_t* len, ...) {
+    if (!o) return QTSS_BadArgument;
+    auto it = o->attrs.find(id);
+    if (it == o->attrs.end() || idx >= it->second.size()) { *len = 0; return QTSS_ValueNotFound; }
+    *out = (void*)it->second[idx].data();
+    *len = (uint32_t)it->second[idx].size();
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_get_value(Obj* o, uint32_t id, uint32_t idx, void* buf, uint32_t* len, ...) {
+    if (!o) return QTSS_BadArgument;
+    auto it = o->attrs.find(id);
+    if (it == o->attrs.end() || idx >= it->second.size()) return QTSS_ValueNotFound;
+    const std::string& v = it->second[idx];
+    if (*len < v.size()) { *len = (uint32_t)v.size(); return QTSS_NotEnoughSpace; }
+    memcpy(buf, v.data(), v.size());
+    *len = (uint32_t)v.size();
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* buf, uint32_t len, ...) {
+    if (!o) return QTSS_BadArgument;
+    set_attr(o, id, idx, buf, len);
+    return QTSS_NoErr;
+}
+// QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
+static uint64_t g_writes = 0;
+static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
+    if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
+    const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
+    if (!(flags & (qtssWriteFlagsIsRTP | qtssWriteFlagsIsRTCP)) || !(flags & qtssWriteFlagsWriteBurstBegin)) {
+        fprintf(stderr, "QTSS_Write on an RTP stream without RTP/RTCP + burst flags (0x%x)\n", flags);
+        exit(4);
+    }
+    if (o->budget[k] == 0) return QTSS_WouldBlock;
+    if (o->budget[k] > 0) o->budget[k]--;
+    const QTSS_PacketStruct* ps = (const QTSS_PacketStruct*)buf;
+    std::string& c = o->cap[k];
+    if (o->tcp) { c.push_back('$'); c.push_back((char)o->channel[k]); }
+    c.push_back((char)(len >> 8));
+    c.push_back((char)(len & 0xFF));
+    c.append((const char*)ps->packetData, len);
+    o->npk[k]++;
+    g_writes++;
+    if (outLen) *outLen = len;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_read(Obj* o, void* buf, uint32_t len, uint32_t* outLen, ...) {
+    const size_t n = std::min<size_t>(len, o->body.size() - o->body_off);
+    memcpy(buf, o->body.data() + o->body_off, n);
+    o->body_off += n;
+    *outLen = (uint32_t)n;
+    return QTSS_NoErr;
+}
+// QTSS_AddRTPStream: a new stream object on the client session; the interleaved channel pair
+// is the next even pair of the RTSP session in SETUP order (RTPStream.cpp:472-473)
+static std::map<Obj*, Obj*> g_rtsp_of_client;
+static std::map<Obj*, uint32_t> g_next_channel;
+static QTSS_Error cb_add_rtp_stream(Obj* client, Obj* req, Obj** out, uint32_t, ...) {
+    Obj* s = new_obj(qtssRTPStreamObjectType);
+    uint32_t tt = qtssRTPTransportTypeUDP;
+    auto it = req->attrs.find(qtssRTSPReqTransportType);
+    if (it != req->attrs.end() && !it->second.empty()) memcpy(&tt, it->second[0].data(), 4);
+    s->tcp = tt == qtssRTPTransportTypeTCP;
+    set_pod(s, qtssRTPStrTransportType, tt);
+    uint32_t& ch = g_next_channel[g_rtsp_of_client[client]];
+    s->channel[0] = (uint8_t)ch; s->channel[1] = (uint8_t)(ch + 1);
+    ch += 2;
+    auto& v = client->attrs[qtssCliSesStreamObjects];
+    const std::string ref((const char*)&s, sizeof(s));
+    v.push_back(ref);
+    g_streams.push_back(s);
+    *out = s;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_play(Obj* client, Obj*, uint32_t, ...) {
+    client->played = true;
+    set_pod<uint32_t>(client, qtssCliSesState, qtssPlayingState);
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_pause(Obj* client, ...) { set_pod<uint32_t>(client, qtssCliSesState, qtssPausedState); return QTSS_NoErr; }
+static QTSS_Error cb_teardown(Obj* client, ...) { client->torn_down = true; return QTSS_NoErr; }
+static Obj* g_current_client = nullptr;
+static QTSS_Error cb_set_idle_timer(int64_t, ...) { if (g_current_client) g_current_client->idle_timer = true; return QTSS_NoErr; }
+static QTSS_Error cb_ok(...) { return QTSS_NoErr; }
+static QTSS_Error cb_unimplemented(...) { return QTSS_Unimplemented; }
+
+// ---- trace ----------------------------------------------------------------------------------
+struct Reader {
+    std::vector<uint8_t> d; size_t p = 0;
+    template <class T> T get() { T v; memcpy(&v, &d[p], sizeof(T)); p += sizeof(T); return v; }
+};
+
+struct Player { uint32_t sub, session; Obj* rtsp; Obj* client; std::vector<Obj*> streams; bool left = false; };
+
+static QTSS_DispatchFuncPtr g_dispatch = nullptr;
+
+static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::string& path, const std::string& digit,
+                          uint32_t mode, uint32_t transport, const std::string& body = std::string()) {
+    Obj* req = new_obj(qtssRTSPRequestObjectType);
+    set_pod<uint32_t>(req, qtssRTSPReqMethod, method);
+    set_attr(req, qtssRTSPReqFilePath, 0, path.data(), (uint32_t)path.size());
+    if (!digit.empty()) set_attr(req, qtssRTSPReqFileDigit, 0, digit.data(), (uint32_t)digit.size());
+    set_pod<uint32_t>(req, qtssRTSPReqTransportMode, mode);
+    set_pod<uint32_t>(req, qtssRTSPReqTransportType, transport);
+    if (!body.empty()) { req->body = body; set_pod<uint32_t>(req, qtssRTSPReqContentLen, (uint32_t)body.size()); }
+    QTSS_RoleParams p;
+    memset(&p, 0, sizeof(p));
+    p.rtspRequestParams.inRTSPSession = rtsp;
+    p.rtspRequestParams.inRTSPRequest = req;
+    p.rtspRequestParams.inClientSession = client;
+    g_current_client = client;
+    const QTSS_Error e = g_dispatch(QTSS_RTSPPreProcessor_Role, &p);
+    g_current_client = nullptr;
+    return e;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s module.so trace.edtr capture.edcp | module.so --register\n", argv[0]); return 2; }
+    void* so = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+    if (!so) { fprintf(stderr, "dlopen: %s\n", dlerror()); return 3; }
+    auto main_fn = (QTSS_Error (*)(void*))dlsym(so, "QTSSReflectorModule_Main");
+    auto tick_fn = (QTSS_Error (*)(void))dlsym(so, "EDGPU_QTSSReflectorModule_Tick");
+    if (!main_fn || !tick_fn) { fprintf(stderr, "module entry points missing\n"); return 3; }
+
+    static QTSS_Callbacks cbs;
+    for (auto& a : cbs.addr) a = (QTSS_CallbackProcPtr)cb_unimplemented;
+    cbs.addr[kMillisecondsCallback] = (QTSS_CallbackProcPtr)cb_milliseconds;
+    cbs.addr[kAddRoleCallback] = (QTSS_CallbackProcPtr)cb_add_role;
+    cbs.addr[kAddStaticAttributeCallback] = (QTSS_CallbackProcPtr)cb_add_static_attr;
+    cbs.addr[kIDForTagCallback] = (QTSS_CallbackProcPtr)cb_id_for_tag;
+    cbs.addr[kGetAttributePtrByIDCallback] = (QTSS_CallbackProcPtr)cb_get_value_ptr;
+    cbs.addr[kGetAttributeByIDCallback] = (QTSS_CallbackProcPtr)cb_get_value;
+    cbs.addr[kSetAttributeByIDCallback] = (QTSS_CallbackProcPtr)cb_set_value;
+    cbs.addr[kWriteCallback] = (QTSS_CallbackProcPtr)cb_write;
+    cbs.addr[kReadCallback] = (QTSS_CallbackProcPtr)cb_read;
+    cbs.addr[kAddRTPStreamCallback] = (QTSS_CallbackProcPtr)cb_add_rtp_stream;
+    cbs.addr[kPlayCallback] = (QTSS_CallbackProcPtr)cb_play;
+    cbs.addr[kPauseCallback] = (QTSS_CallbackProcPtr)cb_pause;
+    cbs.addr[kTeardownCallback] = (QTSS_CallbackProcPtr)cb_teardown;
+    cbs.addr[kSetIdleTimerCallback] = (QTSS_CallbackProcPtr)cb_set_idle_timer;
+    cbs.addr[kSendStandardRTSPCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kAppendRTSPHeadersCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kRequestEventCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    QTSS_PrivateArgs args;
+    memset(&args, 0, sizeof(args));
+    args.inServerAPIVersion = kApiVersion;
+    args.inCallbacks = &cbs;
+    if (main_fn(&args) != QTSS_NoErr || args.outStubLibraryVersion != kApiVersion || !args.outDispatchFunction) {
+        fprintf(stderr, "module main failed\n"); return 3;
+    }
+    g_dispatch = args.outDispatchFunction;
+    QTSS_RoleParams rp;
+    memset(&rp, 0, sizeof(rp));
+    if (g_dispatch(QTSS_Register_Role, &rp) != QTSS_NoErr) { fprintf(stderr, "Register failed\n"); return 3; }
+    for (uint32_t r : {QTSS_Initialize_Role, QTSS_Shutdown_Role, QTSS_RTSPPreProcessor_Role, QTSS_ClientSessionClosing_Role,
+                       QTSS_RTSPIncomingData_Role})
+        if (!g_roles.count(r)) { fprintf(stderr, "role 0x%08x not registered\n", r); return 3; }
+    if (strcmp(argv[2], "--register") == 0) {
+        printf("{\"module\": \"%s\", \"roles\": %zu, \"attributes\": %zu}\n", rp.regParams.outModuleName, g_roles.size(),
+               g_attr_ids.size());
+        return 0;
+    }
+    if (argc != 4) return 2;
+    setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
+    memset(&rp, 0, sizeof(rp));
+    if (g_dispatch(QTSS_Initialize_Role, &rp) != QTSS_NoErr) { fprintf(stderr, "Initialize failed (no GPU?)\n"); return 3; }
+
+    Reader r;
+    FILE* f = fopen(argv[2], "rb");
+    if (!f) { perror(argv[2]); return 2; }
+    fseek(f, 0, SEEK_END); r.d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
+    if (fread(r.d.data(), 1, r.d.size(), f) != r.d.size()) return 2;
+    fclose(f);
+    r.p = 4;
+    const uint32_t ver = r.get<uint32_t>();
+    const uint32_t nsess = r.get<uint32_t>();
+    std::vector<std::string> paths(nsess);
+    std::vector<uint32_t> ntracks(nsess, 0);
+    std::vector<Obj*> push_rtsp(nsess, nullptr), push_client(nsess, nullptr);
+    for (uint32_t s = 0; s < nsess; s++) {
+        const uint32_t n = r.get<uint32_t>();
+        std::string sdp((const char*)&r.d[r.p], n);
+        r.p += n;
+        const uint8_t fl = ver >= 2 ? r.get<uint8_t>() : 0;
+        for (size_t k = sdp.find("m="); k != std::string::npos; k = sdp.find("\nm=", k + 1)) ntracks[s]++;
+        paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
+        if (fl & 1) continue;                                    // UDP push: not through the module
+        push_rtsp[s] = new_obj(qtssRTSPSessionObjectType);
+        push_client[s] = new_obj(qtssClientSessionObjectType);
+        g_rtsp_of_client[push_client[s]] = push_rtsp[s];
+        if (request(push_rtsp[s], push_client[s], qtssAnnounceMethod, paths[s], "", 0, qtssRTPTransportTypeTCP, sdp))
+            { fprintf(stderr, "ANNOUNCE failed\n"); return 3; }
+        for (uint32_t t = 0; t < ntracks[s]; t++)
+            if (request(push_rtsp[s], push_client[s], qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(t + 1),
+                        std::to_string(t + 1), qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
+                { fprintf(stderr, "push SETUP failed\n"); return 3; }
+        if (request(push_rtsp[s], push_client[s], qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
+            { fprintf(stderr, "RECORD failed\n"); return 3; }
+    }
+    std::vector<Player> players;
+    std::vector<char> frame(70000);
+    while (r.p < r.d.size()) {
+        const uint8_t type = r.get<uint8_t>();
+        if (type == 0) break;
+        const int64_t t = r.get<int64_t>();
+        if (t > g_now) g_now = t;
+        if (type == 1) {                                         // PKT -> RTSPIncomingData
+            const uint32_t s = r.get<uint32_t>();
+            const uint8_t ch = r.get<uint8_t>();
+            const uint32_t len = r.get<uint32_t>();
+            frame[0] = '$'; frame[1] = (char)ch; frame[2] = (char)(len >> 8); frame[3] = (char)len;
+            memcpy(&frame[4], &r.d[r.p], len);
+            r.p += len;
+            if (!push_rtsp[s]) continue;
+            QTSS_RoleParams p;
+            memset(&p, 0, sizeof(p));
+            p.rtspIncomingDataParams.inRTSPSession = push_rtsp[s];
+            p.rtspIncomingDataParams.inClientSession = push_client[s];
+            p.rtspIncomingDataParams.inPacketData = frame.data();
+            p.rtspIncomingDataParams.inPacketLen = len + 4;
+            (void)g_dispatch(QTSS_RTSPIncomingData_Role, &p);
+        } else if (type == 2) {                                  // JOIN -> SETUP x tracks + PLAY
+            const uint32_t s = r.get<uint32_t>(), sub = r.get<uint32_t>();
+            const uint8_t tr = r.get<uint8_t>(), ua = r.get<uint8_t>();
+            if (!push_rtsp[s]) continue;
+            Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_obj(qtssClientSessionObjectType), {}};
+            g_rtsp_of_client[pl.client] = pl.rtsp;
+            const std::string agent = (ua & 1) ? "LibVLC/3.0.8 (LIVE555 Streaming Media v2016.11.28)" : "EasyPlayer/1.0";
+            set_attr(pl.client, qtssCliSesFirstUserAgent, 0, agent.data(), (uint32_t)agent.size());
+            const uint32_t tt = tr ? qtssRTPTransportTypeTCP : qtssRTPTransportTypeUDP;
+            const size_t before = g_streams.size();
+            for (uint32_t x = 0; x < ntracks[s]; x++)
+                if (request(pl.rtsp, pl.client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(x + 1),
+                            std::to_string(x + 1), qtssRTPTransportModePlay, tt))
+                    { fprintf(stderr, "player SETUP failed\n"); return 3; }
+            for (size_t k = before; k < g_streams.size(); k++) {
+                g_streams[k]->sub = sub; g_streams[k]->session = s; g_streams[k]->track = (uint32_t)(k - before);
+                pl.streams.push_back(g_streams[k]);
+            }
+            (void)request(pl.rtsp, pl.client, qtssPlayMethod, paths[s], "", qtssRTPTransportModePlay, tt);
+            if (!pl.client->played) {                           // deferred RTP-Info PLAY: dropped
+                QTSS_RoleParams p;
+                memset(&p, 0, sizeof(p));
+                p.clientSessionClosingParams.inClientSession = pl.client;
+                (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                continue;
+            }
+            players.push_back(pl);
+        } else if (type == 3) {                                  // TICK
+            const QTSS_Error e = tick_fn();
+            if (e) { fprintf(stderr, "tick failed %d\n", (int)e); return 3; }
+            for (Obj* st : g_streams) st->budget[0] = st->budget[1] = -1;
+        } else if (type == 4) {                                  // BLOCK
+            const uint32_t sub = r.get<uint32_t>();
+            const uint16_t trk = r.get<uint16_t>();
+            const uint8_t kind = r.get<uint8_t>();
+            const uint32_t budget = r.get<uint32_t>();
+            for (auto& pl : players)
+                if (pl.sub == sub && !pl.left && trk < pl.streams.size()) pl.streams[trk]->budget[kind & 1] = budget;
+        } else if (type == 5) {                                  // UPKT: a UDP pusher (not served)
+            r.p += 4 + 1 + 4 + 2;
+            const uint32_t len = r.get<uint32_t>();
+            r.p += len;
+        } else if (type == 6) {                                  // LEAVE -> ClientSessionClosing
+            const uint32_t sub = r.get<uint32_t>();
+            for (auto& pl : players)
+                if (pl.sub == sub && !pl.left) {
+                    QTSS_RoleParams p;
+                    memset(&p, 0, sizeof(p));
+                    p.clientSessionClosingParams.inClientSession = pl.client;
+                    (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                    pl.left = true;
+                }
+        } else {
+            fprintf(stderr, "bad event %u\n", type);
+            return 3;
+        }
+    }
+    memset(&rp, 0, sizeof(rp));
+    (void)g_dispatch(QTSS_Shutdown_Role, &rp);
+
+    // capture: (sub, track, kind) records, subscriber order
+    std::vector<Obj*> st;
+    for (auto& pl : players) for (Obj* s : pl.streams) st.push_back(s);
+    std::stable_sort(st.begin(), st.end(), [](Obj* a, Obj* b) { return a->sub != b->sub ? a->sub < b->sub : a->track < b->track; });
+    FILE* o = fopen(argv[3], "wb");
+    if (!o) { perror(argv[3]); return 2; }
+    fwrite("EDCP", 1, 4, o);
+    const uint32_t n = (uint32_t)st.size() * 2;
+    fwrite(&n, 4, 1, o);
+    for (Obj* s : st)
+        for (int k = 0; k < 2; k++) {
+            const uint16_t track = (uint16_t)s->track;
+            const uint8_t kind = (uint8_t)k, tcp = s->tcp;
+            const uint64_t np = s->npk[k], nb = s->cap[k].size();
+            fwrite(&s->sub, 4, 1, o); fwrite(&s->session, 4, 1, o); fwrite(&track, 2, 1, o);
+            fwrite(&kind, 1, 1, o); fwrite(&tcp, 1, 1, o); fwrite(&np, 8, 1, o); fwrite(&nb, 8, 1, o);
+            fwrite(s->cap[k].data(), 1, nb, o);
+        }
+    fclose(o);
+    fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes\n", players.size(), (unsigned long long)g_writes);
+    return 0;
+}
