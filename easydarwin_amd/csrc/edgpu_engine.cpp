@@ -89,7 +89,7 @@ struct DevVec {
     void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; cap = 0; }
 };
 
-struct TrackHost { uint32_t type = 0; std::string name; };   // 1 video, 2 audio
+struct TrackHost { uint32_t type = 0; std::string name; uint32_t track_id = 0; };   // type: 1 video, 2 audio
 
 // A track's receiver-report state toward a UDP pusher (ReflectorStream fields
 // fReceiverReportBuffer / fDestRTCPAddr / fDestRTCPPort and the RTCP sender's fLastRRTime).
@@ -357,31 +357,71 @@ int edgpu_sync(edgpu_ctx* x) {
     return EDGPU_OK;
 }
 
-// SDP restatement: a track per m= line (media word -> payload type), named by the rest of
-// its first a=rtpmap line after the first space (SDPSourceInfo.cpp:259-353).
+// SDP restatement of SDPSourceInfo::Parse (SDPSourceInfo.cpp:172-420), pinned byte for byte
+// to the reference by tests/golden/sdp_vectors.json (tests/test_cold_parsers.py):
+//   * lines end at CR or LF; empty lines are skipped;
+//   * every line whose first byte is 'm' is a track (trackID = its 1-based position); two
+//     bytes in, a StringParser "word" (letters, '-', '_') names the media: exactly "video"
+//     or "audio", else unknown -- so "m=video2" is video and "m=VIDEO" is not;
+//   * 'a' lines before the first track are ignored; "a=" + word "rtpmap": the first such line of
+//     a track that has a space after the word names the track with the REST of the line after
+//     that space (trailing blanks included: the H.264 gate, Q3, is an exact compare), later
+//     rtpmap lines are ignored; word "control": after the ':' and the first '=', the first
+//     run of digits is the trackID (0 when there is none).
+static bool sdp_word_char(char c) {
+    return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '-' || c == '_';
+}
 static std::vector<TrackHost> parse_sdp(const char* sdp, uint32_t n) {
     std::vector<TrackHost> t;
-    std::string s(sdp, n);
+    const std::string s(sdp, n);
     size_t p = 0;
     while (p < s.size()) {
         size_t e = s.find_first_of("\r\n", p);
         if (e == std::string::npos) e = s.size();
-        std::string line = s.substr(p, e - p);
-        p = e;
-        while (p < s.size() && (s[p] == '\r' || s[p] == '\n')) p++;
-        if (line.size() < 2 || line[1] != '=') continue;
+        const std::string line = s.substr(p, e - p);
+        p = e < s.size() ? e + 1 : e;
+        if (line.empty()) continue;
+        size_t w = std::min<size_t>(2, line.size()), we = w;
+        while (we < line.size() && sdp_word_char(line[we])) we++;
+        const std::string word = line.substr(w, we - w);
         if (line[0] == 'm') {
-            size_t sp = line.find(' ', 2);
-            std::string media = line.substr(2, sp == std::string::npos ? std::string::npos : sp - 2);
             TrackHost th;
-            th.type = media == "video" ? 1 : media == "audio" ? 2 : 0;
+            th.type = word == "video" ? 1 : word == "audio" ? 2 : 0;
+            th.track_id = (uint32_t)t.size() + 1;
             t.push_back(th);
-        } else if (line[0] == 'a' && !t.empty() && line.compare(2, 7, "rtpmap:") == 0 && t.back().name.empty()) {
-            size_t sp = line.find(' ', 2);
-            if (sp != std::string::npos) t.back().name = line.substr(sp + 1);
+        } else if (line[0] == 'a' && !t.empty()) {
+            if (word == "rtpmap") {
+                const size_t sp = line.find(' ', we);
+                if (t.back().name.empty() && sp != std::string::npos) t.back().name = line.substr(sp + 1);
+            } else if (word == "control") {
+                uint32_t id = 0;
+                const size_t colon = line.find(':', we);
+                const size_t eq = colon == std::string::npos ? std::string::npos : line.find('=', colon + 1);
+                if (eq != std::string::npos) {
+                    size_t d = eq + 1;
+                    while (d < line.size() && !(line[d] >= '0' && line[d] <= '9')) d++;
+                    for (; d < line.size() && line[d] >= '0' && line[d] <= '9'; d++) id = id * 10 + (uint32_t)(line[d] - '0');
+                }
+                t.back().track_id = id;
+            }
         }
     }
     return t;
+}
+
+int edgpu_sdp_parse(const char* sdp, uint32_t sdp_len, edgpu_sdp_track* out, uint32_t cap, uint32_t* n_tracks) {
+    if ((!sdp && sdp_len) || !n_tracks || (cap && !out)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    const std::vector<TrackHost> t = parse_sdp(sdp ? sdp : "", sdp_len);
+    *n_tracks = (uint32_t)t.size();
+    if (t.size() > cap) return fail(EDGPU_BAD_ARGUMENT, "track buffer too small");
+    for (size_t i = 0; i < t.size(); i++) {
+        memset(&out[i], 0, sizeof(out[i]));
+        out[i].payload_type = t[i].type;
+        out[i].track_id = t[i].track_id;
+        out[i].name_len = (uint32_t)std::min<size_t>(t[i].name.size(), sizeof(out[i].name));
+        memcpy(out[i].name, t[i].name.data(), out[i].name_len);
+    }
+    return EDGPU_OK;
 }
 
 int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_push, uint32_t* out_session) {

@@ -151,21 +151,14 @@ uint32_t TrackFromRequest(QTSS_Object req, bool* ok) {
     return (uint32_t)strtoul(digits.c_str(), nullptr, 10);
 }
 
-// a=control:trackID=N per m= section, in SDP order (SDPSourceInfo.cpp:260-353 reads the same
-// lines; a section without one gets its 1-based position)
+// each track's trackID as SDPSourceInfo::Parse assigns it (a=control, else the position;
+// GetStreamInfoByTrackID, SourceInfo.cpp) -- the engine's parse, edgpu_sdp_parse
 std::vector<uint32_t> SdpTrackIDs(const std::string& sdp) {
-    std::vector<uint32_t> ids;
-    size_t p = 0;
-    while (p < sdp.size()) {
-        size_t e = sdp.find_first_of("\r\n", p);
-        if (e == std::string::npos) e = sdp.size();
-        const std::string line = sdp.substr(p, e - p);
-        p = e;
-        while (p < sdp.size() && (sdp[p] == '\r' || sdp[p] == '\n')) p++;
-        if (line.compare(0, 2, "m=") == 0) ids.push_back((uint32_t)ids.size() + 1);
-        else if (!ids.empty() && line.compare(0, 18, "a=control:trackID=") == 0)
-            ids.back() = (uint32_t)strtoul(line.c_str() + 18, nullptr, 10);
-    }
+    std::vector<edgpu_sdp_track> t(64);
+    uint32_t n = 0;
+    if (edgpu_sdp_parse(sdp.data(), (uint32_t)sdp.size(), t.data(), (uint32_t)t.size(), &n) != 0) return {};
+    std::vector<uint32_t> ids(n);
+    for (uint32_t i = 0; i < n; i++) ids[i] = t[i].track_id;
     return ids;
 }
 
@@ -331,7 +324,6 @@ Session* FindOrCreateSession(const std::string& name) {
     if (M->R->SetupReflectorSession(s.sdp, false, &s.engine) != 0) return nullptr;
     s.trackIDs = SdpTrackIDs(s.sdp);
     s.trackIDs.resize(M->R->GetNumStreams(s.engine));
-    for (size_t i = 0; i < s.trackIDs.size(); i++) if (!s.trackIDs[i]) s.trackIDs[i] = (uint32_t)i + 1;
     s.setupToReceive.assign(s.trackIDs.size(), false);
     M->sessions.push_back(s);
     M->byName[name] = (uint32_t)M->sessions.size() - 1;

@@ -193,7 +193,14 @@ CKeyFrameCache::~CKeyFrameCache() {
 bool CKeyFrameCache::PutOnePacket(char* buf, int len, int nalutype, int start) {
     if (buf == nullptr || len == 0) return false;
     if (nalutype == 7 && start == 1) curdatalen = 0;          // a new SPS starts a new GOP
-    if (len + 4 > 5 * 1024) return false;                      // the reference's 5 KiB TLV scratch
+    // the caller's packet is rewritten in place: byte 13 (the NAL header of an FU-A start
+    // fragment after a 12-byte RTP header) becomes 0x67 (SPS) or 0x41 (keyframecache.cpp:
+    // 27-40); the reference does it for any length (past the packet when len < 14) -- here
+    // only inside the packet.  The reference's ./data.264 debug dump is not reproduced.
+    if (start == 1 && len >= 14) buf[13] = (char)(nalutype == 7 ? 0x67 : 0x41);
+    // the reference's 5 KiB TLV scratch: it overruns it for len > 5116 (FrameBuffer::Encode
+    // ignores the capacity, keyframecache.h:24-45); refused here
+    if (len < 0 || len + 4 > 5 * 1024) return false;
     unsigned char rec[5 * 1024];
     rec[0] = kSTX;
     rec[1] = (unsigned char)((unsigned)len >> 8);

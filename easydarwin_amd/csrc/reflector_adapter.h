@@ -103,9 +103,12 @@ private:
 
 // CKeyFrameCache with the reference's public API and TLV record format
 // ([0x28][BE16 len][bytes][0x29], keyframecache.cpp:103-143).  PutOnePacket/GetOnePacket/
-// SetBuf behave as in the reference except that PutOnePacket does not append to ./data.264
-// or rewrite buf[13] (debug side effects, keyframecache.cpp:25-50).  LoadGOP() fills the
-// cache from the GPU's GOP index (key pointer -> newest) instead of per-packet PutOnePacket.
+// SetBuf behave as in the reference, pinned to it by tests/golden/keyframecache_vectors.json
+// -- including PutOnePacket's in-place rewrite of the caller's buf[13] (0x67 for an SPS start,
+// else 0x41) -- except: no ./data.264 debug dump (keyframecache.cpp:25-50), no write past a
+// packet shorter than 14 bytes, and packets over 5116 bytes are refused where the reference
+// overruns its 5 KiB scratch.  LoadGOP() fills the cache from the GPU's GOP index (key
+// pointer -> newest) instead of per-packet PutOnePacket.
 class CKeyFrameCache {
 public:
     char* _memory;

@@ -33,7 +33,7 @@ EXPORTED = [
     "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
-    "edgpu_subscriber_rewrite",
+    "edgpu_subscriber_rewrite", "edgpu_sdp_parse",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -68,6 +68,11 @@ REWRITE_SSRC = 1
 
 class Rewrite(C.Structure):
     _fields_ = [("seq_delta", C.c_uint16), ("flags", C.c_uint16), ("ts_delta", C.c_uint32), ("ssrc", C.c_uint32)]
+
+
+class SdpTrack(C.Structure):
+    _fields_ = [("payload_type", C.c_uint32), ("track_id", C.c_uint32), ("name_len", C.c_uint32),
+                ("name", C.c_char * 244)]
 
 
 class PktDesc(C.Structure):
@@ -192,6 +197,7 @@ def load(path: str = LIB_PATH):
         "edgpu_source_identity": (I32, [P, U32, U32, U32, I64]),
         "edgpu_session_eyes_add": (I32, [P, U32, C.c_int32]),
         "edgpu_subscriber_rewrite": (I32, [P, U32, U32, C.POINTER(Rewrite)]),
+        "edgpu_sdp_parse": (I32, [C.c_char_p, U32, C.POINTER(SdpTrack), U32, C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -208,6 +214,16 @@ def _check(rc: int):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def sdp_parse(sdp: bytes) -> list:
+    """The engine's SDP parse (edgpu_sdp_parse, host only): [(payload type, name bytes, trackID)]."""
+    lib = load()
+    n = C.c_uint32()
+    cap = 64
+    buf = (SdpTrack * cap)()
+    _check(lib.edgpu_sdp_parse(sdp, len(sdp), buf, cap, C.byref(n)))
+    return [(buf[i].payload_type, bytes(buf[i].name[:buf[i].name_len]), buf[i].track_id) for i in range(n.value)]
 
 
 class Context:

@@ -178,6 +178,20 @@ int  edgpu_session_add(edgpu_ctx* ctx, const char* sdp, uint32_t sdp_len, int ud
                        uint32_t* out_session);
 int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks);
 
+/* The SDP parse edgpu_session_add applies (host only, no context, no GPU): the restatement of
+ * SDPSourceInfo::Parse (APICommonCode/SDPSourceInfo.cpp:172-420) -- one track per line
+ * starting with 'm', its payload type (1 video, 2 audio, 0 other), its rtpmap payload name
+ * (the text the H.264 keyframe gate compares, ReflectorStream.cpp:1879, Q3) and its trackID
+ * (a=control, else its position).  Names longer than 244 bytes are truncated here (not in the
+ * session).  *n_tracks receives the count; EDGPU_BAD_ARGUMENT if it exceeds `cap`. */
+typedef struct edgpu_sdp_track {
+    uint32_t payload_type;
+    uint32_t track_id;
+    uint32_t name_len;
+    char     name[244];
+} edgpu_sdp_track;
+int  edgpu_sdp_parse(const char* sdp, uint32_t sdp_len, edgpu_sdp_track* out, uint32_t cap, uint32_t* n_tracks);
+
 /* Subscribers: a join takes effect at the next edgpu_fanout, like a new output being
  * picked up by the next ReflectPackets. */
 int  edgpu_subscriber_add(edgpu_ctx* ctx, uint32_t session, int transport,
