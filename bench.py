@@ -100,8 +100,23 @@ def make_tcp_on_device(bt: dict, b: dict, dev: torch.device, read_bytes: int = 6
     return {"raw": raw, "reads": np.array(rows, dtype=edgpu.TCP_READ_DTYPE), "raw_bytes": total}
 
 
+def make_pinned(ctx: edgpu.Context, bt: dict):
+    """The batch in pinned host memory (edgpu_host_alloc), as a host socket reader would have
+    written it: descriptors, segments, sessions and the slot blob."""
+    parts = {}
+    for k in ("desc", "seg", "sess", "blob"):
+        a = bt[k].cpu().numpy().view(np.uint8).ravel()
+        hb = ctx.host_alloc(a.nbytes)
+        hb.array[:] = a
+        parts[k] = hb
+    return parts
+
+
 def run_step(ctx: edgpu.Context, bt: dict):
-    if "tcp" in bt:
+    if "pinned" in bt:
+        p = bt["pinned"]
+        ctx.ingest_pinned(p["desc"].ptr, bt["n"], p["seg"].ptr, p["sess"].ptr, bt["nseg"], p["blob"].ptr, bt["bytes"])
+    elif "tcp" in bt:
         ctx.ingest_interleaved(bt["tcp"]["reads"], bt["tcp"]["raw_bytes"], device_ptr=bt["tcp"]["raw"].data_ptr())
     else:
         ctx.ingest_device(bt["desc"].data_ptr(), bt["n"], bt["seg"].data_ptr(), bt["sess"].data_ptr(),
@@ -249,10 +264,12 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="tick pipelining: ingest(t+1) beside the fan-out copy of t on a second stream "
                          "(measured slower on C2: both phases are HBM-bound and contend)")
-    ap.add_argument("--ingest", choices=["desc", "tcp"], default="desc",
-                    help="desc: packets handed over as descriptors + slots (edgpu_ingest, the reflector's "
-                         "per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP reads, "
-                         "deframed on the GPU (edgpu_ingest_interleaved)")
+    ap.add_argument("--ingest", choices=["desc", "tcp", "host"], default="desc",
+                    help="desc: packets handed over as descriptors + slots in HBM (edgpu_ingest, the "
+                         "reflector's per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP "
+                         "reads in HBM, deframed on the GPU (edgpu_ingest_interleaved); host: the batches in "
+                         "pinned host memory, copied over PCIe on the copy stream beside the previous fan-out "
+                         "(EDGPU_PTR_PINNED) -- a separate line, PCIe-bound")
     ap.add_argument("--rewrite", action="store_true",
                     help="per-output rewrite stage on every subscriber (seq/ts deltas + SSRC override, "
                          "edgpu_subscriber_rewrite); the reference's parity mode is the identity (default)")
@@ -309,8 +326,14 @@ def main():
                         other_ring_packets=256, other_ring_bytes=64 << 10,
                         out_arena_bytes=max_arena, max_out_packets=max_out,
                         max_batch_packets=max_pk + 1,
-                        max_batch_bytes=(max(b["bytes"] for b in batches) + (1 << 20)) if args.ingest == "tcp" else 1 << 20,
+                        max_batch_bytes=(max(b["bytes"] for b in batches) + (1 << 20)) if args.ingest in ("tcp", "host")
+                        else 1 << 20,
                         overlap_ticks=1 if args.overlap else 0)
+    if args.ingest == "host":
+        for bt in batches:
+            bt["pinned"] = make_pinned(ctx, bt)
+            bt.pop("blob")
+        torch.cuda.empty_cache()
     for _ in gids:
         s = ctx.session_add(fleet.sdp())
         for _k in range(args.subs):
@@ -402,7 +425,8 @@ def main():
         "data": "synthetic (PCG64 RTP/H.264 FU-A headers, GPU-random payload)",
         "config": {"workload": f"C2: {args.sessions} H.264 1080p30 4 Mb/s streams/GPU x {args.subs} UDP subs, "
                                f"{args.tick_ms}-ms ticks (ingest+keyframe+fan-out per step)"
-                               + (", RTSP-interleaved TCP push reads deframed on the GPU" if args.ingest == "tcp" else ""),
+                               + (", RTSP-interleaved TCP push reads deframed on the GPU" if args.ingest == "tcp" else "")
+                               + (", batches in pinned host memory (PCIe H2D overlapped)" if args.ingest == "host" else ""),
                    "ingest": args.ingest,
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
                    "tick_ms": args.tick_ms,
@@ -410,6 +434,8 @@ def main():
                    "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"},
         "relayed_GBps": round(out_all / dt / 1e9, 2),
+        **({"pcie_H2D_GBps": round(sum(batches[i]["bytes"] + 16 * batches[i]["n"] for i in range(warm, warm + steps))
+                                   / dt / 1e9, 2)} if args.ingest == "host" else {}),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": ctx.fanout_kernel(), "alg_bytes_per_launch": int(alg_bytes / max(launches, 1)),

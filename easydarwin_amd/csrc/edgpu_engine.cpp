@@ -195,6 +195,19 @@ struct edgpu_ctx {
     uint32_t* d_pflags = nullptr;
     uint64_t* d_pidx = nullptr;
     CopyJob* d_jobs = nullptr;
+    // pinned-host ingest (EDGPU_PTR_PINNED): two device staging sets filled on `h2d`
+    struct PinStage {
+        edgpu_pkt_desc* desc = nullptr;
+        uint32_t* seg = nullptr;
+        uint32_t* sess = nullptr;
+        uint8_t* blob = nullptr;
+        hipEvent_t copied = nullptr;        // its H2D copy is done (h2d stream)
+        hipEvent_t consumed = nullptr;      // k_ingest + keyframe index read it (main stream)
+        bool issued = false;
+    } pin[2];
+    hipStream_t h2d = nullptr;
+    int pin_next = 0;
+    int pend_stage = -1;                    // staging set of the batch pending a keyframe index
     // pending batch for keyframe_index
     const uint32_t* pend_seg = nullptr;
     const uint32_t* pend_seg_sess = nullptr;
@@ -336,6 +349,13 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
                     (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
+    if (x->h2d) (void)hipStreamSynchronize(x->h2d);
+    for (auto& st : x->pin) {
+        for (void* p : {(void*)st.desc, (void*)st.seg, (void*)st.sess, (void*)st.blob}) if (p) (void)hipFree(p);
+        if (st.copied) (void)hipEventDestroy(st.copied);
+        if (st.consumed) (void)hipEventDestroy(st.consumed);
+    }
+    if (x->h2d) (void)hipStreamDestroy(x->h2d);
     if (x->ev_plan) (void)hipEventDestroy(x->ev_plan);
     if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
     if (x->copy) (void)hipStreamDestroy(x->copy);
@@ -853,12 +873,76 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     return EDGPU_OK;
 }
 
+// A host batch's structure: segment bounds, session ids, slots inside the blob.
+static int validate_host_batch(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
+                               const uint32_t* seg_sess, uint32_t nseg, uint64_t blob_bytes) {
+    if (nseg && seg_off[nseg] != n) return fail(EDGPU_BAD_ARGUMENT, "seg_offsets[n_segments] != n_packets");
+    for (uint32_t s = 0; s < nseg; s++) {
+        if (seg_off[s] > seg_off[s + 1]) return fail(EDGPU_BAD_ARGUMENT, "segments not monotone");
+        if (seg_sess[s] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in batch");
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if ((uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
+            return fail(EDGPU_BAD_ARGUMENT, "packet slot outside blob");
+    return EDGPU_OK;
+}
+
+int edgpu_host_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
+    if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    HIP_CHECK(hipSetDevice(x->device));
+    *out = nullptr;
+    if (hipHostMalloc(out, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess)
+        return fail(EDGPU_OUT_OF_MEMORY, "pinned host buffer");
+    return EDGPU_OK;
+}
+
+int edgpu_host_free(edgpu_ctx* x, void* p) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (!p) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    if (x->h2d) HIP_CHECK(hipStreamSynchronize(x->h2d));
+    HIP_CHECK(hipHostFree(p));
+    return EDGPU_OK;
+}
+
+// EDGPU_PTR_PINNED: copies the batch into staging set k on the copy stream; the context stream
+// waits for it.  Returns the device pointers of the set.
+static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
+                        const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int* out_k) {
+    if (!x->h2d) HIP_CHECK(hipStreamCreateWithFlags(&x->h2d, hipStreamNonBlocking));
+    const int k = x->pin_next;
+    edgpu_ctx::PinStage& S = x->pin[k];
+    if (!S.desc) {
+        const size_t np = x->cfg.max_batch_packets;
+        if (dmalloc(&S.desc, sizeof(edgpu_pkt_desc) * np) != hipSuccess || dmalloc(&S.seg, 4 * (np + 1)) != hipSuccess ||
+            dmalloc(&S.sess, 4 * np) != hipSuccess || dmalloc(&S.blob, x->cfg.max_batch_bytes) != hipSuccess)
+            return fail(EDGPU_OUT_OF_MEMORY, "pinned-ingest staging");
+        HIP_CHECK(hipEventCreateWithFlags(&S.copied, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&S.consumed, hipEventDisableTiming));
+    }
+    // the previous batch's copy must be done before its host buffers are handed back (contract),
+    // and this set's previous batch must have been read by its ingest + keyframe index
+    edgpu_ctx::PinStage& P = x->pin[k ^ 1];
+    if (P.issued) HIP_CHECK(hipEventSynchronize(P.copied));
+    if (S.issued) HIP_CHECK(hipStreamWaitEvent(x->h2d, S.consumed, 0));
+    HIP_CHECK(hipMemcpyAsync(S.desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->h2d));
+    HIP_CHECK(hipMemcpyAsync(S.seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->h2d));
+    HIP_CHECK(hipMemcpyAsync(S.sess, seg_sess, (size_t)nseg * 4, hipMemcpyHostToDevice, x->h2d));
+    HIP_CHECK(hipMemcpyAsync(S.blob, blob, blob_bytes, hipMemcpyHostToDevice, x->h2d));
+    HIP_CHECK(hipEventRecord(S.copied, x->h2d));
+    HIP_CHECK(hipStreamWaitEvent(x->stream, S.copied, 0));
+    S.issued = true;
+    x->pin_next = k ^ 1;
+    *out_k = k;
+    return EDGPU_OK;
+}
+
 int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
-        (where == EDGPU_PTR_HOST && blob_bytes > x->cfg.max_batch_bytes))
+        (where != EDGPU_PTR_DEVICE && blob_bytes > x->cfg.max_batch_bytes))
         return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
@@ -866,17 +950,20 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     const uint32_t* ds = seg_off;
     const uint32_t* dss = seg_sess;
     const uint8_t* db = blob;
+    if (where == EDGPU_PTR_PINNED) {
+        int r = validate_host_batch(x, desc, n, seg_off, seg_sess, nseg, blob_bytes);
+        if (r) return r;
+        int k = 0;
+        if ((r = stage_pinned(x, desc, n, seg_off, seg_sess, nseg, blob, blob_bytes, &k))) return r;
+        const edgpu_ctx::PinStage& S = x->pin[k];
+        r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, x->ingest_mode);
+        if (!r) x->pend_stage = k;
+        return r;
+    }
     if (where == EDGPU_PTR_HOST) {
         // validate on the host (segment bounds, session ids, slot bounds) before any launch
-        if (nseg && seg_off[nseg] != n) return fail(EDGPU_BAD_ARGUMENT, "seg_offsets[n_segments] != n_packets");
-        for (uint32_t s = 0; s < nseg; s++) {
-            if (seg_off[s] > seg_off[s + 1]) return fail(EDGPU_BAD_ARGUMENT, "segments not monotone");
-            if (seg_sess[s] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in batch");
-        }
-        for (uint32_t i = 0; i < n; i++)
-            if ((uint64_t)desc[i].slot * 16 + 4 + std::min<uint32_t>(desc[i].len, kMaxPacket) + 15 > blob_bytes + 15 ||
-                (uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
-                return fail(EDGPU_BAD_ARGUMENT, "packet slot outside blob");
+        int r = validate_host_batch(x, desc, n, seg_off, seg_sess, nseg, blob_bytes);
+        if (r) return r;
         if (!x->d_blob && dmalloc(&x->d_blob, x->cfg.max_batch_bytes) != hipSuccess)
             return fail(EDGPU_OUT_OF_MEMORY, "blob staging");
         HIP_CHECK(hipMemcpyAsync(x->d_desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->stream));
@@ -1030,6 +1117,10 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     x->kf_share = false;
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
+    if (x->pend_stage >= 0) {                   // the pinned staging set may be refilled now
+        HIP_CHECK(hipEventRecord(x->pin[x->pend_stage].consumed, x->stream));
+        x->pend_stage = -1;
+    }
     x->timed_keyframe = true;
     x->pending = false;
     return EDGPU_OK;

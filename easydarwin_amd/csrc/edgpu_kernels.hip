@@ -1046,11 +1046,8 @@ __device__ __forceinline__ T const_load(const T* p) {
 // RTCP packet's sender SSRC (4-7); an SR's RTP timestamp (packet bytes 16-19) is in the second
 // word.  Fields past the packet's length are left alone; CSRC lists and extensions are never
 // touched.
-__device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w, const uint32_t* sm, const u32x4* cb) {
-    // branch-free on the per-word test (every wave holds a slot start or two): the patched
-    // word is computed for every lane and selected where the word starts a slot; the flags
-    // (f.ch, f.rw) are uniform, so their branches are scalar
-    const bool start = (sm[w >> 5] >> (w & 31)) & 1u;
+// The patched form of a slot's first word (computed for every lane, selected by `start`).
+__device__ __forceinline__ u32x4 fan_patch_start(u32x4 v, const FanSub& f, bool start) {
     u32x4 p = v;
     if (f.ch & 1u) p.x |= f.ch & 0xFF00u;
     if (f.rw) {
@@ -1063,16 +1060,38 @@ __device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w,
             p.y = ok ? ny : v.y;
             p.z = ok ? nz : v.z;
             if (f.rw & kRwSsrc) p.w = ok ? f.rw_ssrc_be : v.w;
-        } else {
-            if (f.rw & kRwSsrc) p.z = len >= 8 ? f.rw_ssrc_be : v.z;
-            if (!start && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {   // RTCP only: rare
-                const u32x4 h = cb[w - 1];
-                const uint32_t hl = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
-                if (hl >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
-            }
+        } else if (f.rw & kRwSsrc) {
+            p.z = len >= 8 ? f.rw_ssrc_be : v.z;
         }
     }
     return start ? p : v;
+}
+
+// The per-output patch of one 16-B arena word (word `w` of the chunk's LDS image `cb`, slot
+// starts marked in bitmap `sm`): the RTSP-interleaved channel byte (RTSPSessionInterface.cpp:
+// 329-336) and the rewrite stage (kRw*).  A slot's first word holds the 4-B '$' 0 BE16(len)
+// header and packet bytes 0..11: RTP seq (bytes 2-3), timestamp (4-7) and SSRC (8-11), or an
+// RTCP packet's sender SSRC (4-7); an SR's RTP timestamp (packet bytes 16-19) is in the second
+// word.  Fields past the packet's length are left alone; CSRC lists and extensions are never
+// touched.  Branch-free on the per-word test; the flags (f.ch, f.rw) are uniform.
+__device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w, const uint32_t* sm, const u32x4* cb) {
+    const bool start = (sm[w >> 5] >> (w & 31)) & 1u;
+    if ((f.rw & kRwRtcp) && !start && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {   // RTCP only: rare
+        const u32x4 h = cb[w - 1];
+        const uint32_t hl = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
+        if (hl >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
+    }
+    return fan_patch_start(v, f, start);
+}
+
+// Bits [c0, c0 + 64) of a slot-start bitmap of `nw32` words as one wave-uniform mask (bit l =
+// word c0 + l; words before 0 or past the bitmap read as 0).  Every lane reads the same three
+// LDS words (a broadcast), so the per-word test becomes a shift of an SGPR pair.
+__device__ __forceinline__ uint64_t row_mask(const uint32_t* sm, int c0, int nw32) {
+    const int b = c0 >> 5, sh = c0 & 31;
+    auto word = [&](int i) -> uint64_t { return (i >= 0 && i < nw32) ? (uint64_t)sm[i] : 0ull; };
+    const uint64_t lo = word(b) | word(b + 1) << 32, hi = word(b + 2);
+    return (lo >> sh) | (sh ? hi << (64 - sh) : 0ull);
 }
 
 template <int THREADS, int CHUNK>
@@ -1116,7 +1135,9 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 // needs the VGPRs of 1 workgroup per CU at 1024 threads)
 // WPE: minimum waves per SIMD the register allocation must allow (8 = two 1024-thread
 // workgroups per CU, i.e. <= 64 VGPRs); 0 leaves it to the compiler.
-template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0>
+// PM: how the store loop finds slot starts for the per-output patch: 0 one bitmap bit per lane
+// (LDS read per word), 1 one wave-uniform 64-bit mask per wave row (row_mask).
+template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1207,7 +1228,15 @@ void k_fanout4(FanoutParams P) {
 #pragma unroll
                 for (int k = 0; k < SU; k++) {
                     if (k > 0 && j + k >= nj) break;
-                    if (patch) v[k] = fan_patch(v[k], f, srcc[k], sm, cbuf);
+                    if (patch) {
+                        if (PM == 0 || (f.rw & kRwRtcp)) {
+                            v[k] = fan_patch(v[k], f, srcc[k], sm, cbuf);
+                        } else {
+                            const int c0 = (int)(fw + (j + k) * THREADS + wv * 64u) - (int)s;
+                            const uint64_t m = uni64(row_mask(sm, c0, SM));
+                            if (m) v[k] = fan_patch_start(v[k], f, (m >> lane) & 1u);
+                        }
+                    }
                     __builtin_amdgcn_raw_buffer_store_b128(v[k], os, (tid + (j + k) * THREADS - s) * 16u, 0, AUX);
                 }
             }
@@ -1704,6 +1733,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 2>, 1024, 56, fanout4_lds<1024, 56>()}, // 24 + 2-deep
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 25 32, 2-deep
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 8>, 1024, 32, fanout4_lds<1024, 32>()}, // 26 32, <= 64 VGPRs
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 27 row-mask patch
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 28 56, row-mask
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1714,7 +1745,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<512,32,nt>", "k_fanout4<1024,16,nt>",
                                             "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>",
                                             "k_fanout4<1024,56,nt,su4>", "k_fanout4<1024,56,nt,su2>",
-                                            "k_fanout4<1024,32,nt,su2>", "k_fanout4<1024,32,nt,wpe8>"};
+                                            "k_fanout4<1024,32,nt,su2>", "k_fanout4<1024,32,nt,wpe8>",
+                                            "k_fanout4<1024,32,nt,rowmask>", "k_fanout4<1024,56,nt,rowmask>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
@@ -1732,7 +1764,7 @@ const char* fanout_name(int variant) {
 }
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
-    static int occ[32] = {0};
+    static int occ[64] = {0};
     const FanoutVariant& v = kVariants[variant];
     if (!occ[variant]) {
         if (v.lds > 48 * 1024) (void)hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, v.lds);

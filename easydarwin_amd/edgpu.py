@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, "libedgpu.so")
 OK, ERR, BAD_ARGUMENT, WOULD_BLOCK = 0, -1, -10, -14
 NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW = -101, -102, -103, -104
 TRANSPORT_UDP, TRANSPORT_TCP = 0, 1
-PTR_HOST, PTR_DEVICE = 0, 1
+PTR_HOST, PTR_DEVICE, PTR_PINNED = 0, 1, 2
 PLAY_RTP_INFO = 1
 FALSE = 0xFFFFFFFF
 
@@ -33,7 +33,7 @@ EXPORTED = [
     "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
-    "edgpu_subscriber_rewrite", "edgpu_sdp_parse",
+    "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -198,6 +198,8 @@ def load(path: str = LIB_PATH):
         "edgpu_session_eyes_add": (I32, [P, U32, C.c_int32]),
         "edgpu_subscriber_rewrite": (I32, [P, U32, U32, C.POINTER(Rewrite)]),
         "edgpu_sdp_parse": (I32, [C.c_char_p, U32, C.POINTER(SdpTrack), U32, C.POINTER(U32)]),
+        "edgpu_host_alloc": (I32, [P, U64, C.POINTER(P)]),
+        "edgpu_host_free": (I32, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -311,6 +313,16 @@ class Context:
         _check(self.lib.edgpu_ingest(self.h, C.c_void_p(desc_ptr), n, C.c_void_p(seg_ptr),
                                      C.c_void_p(seg_sess_ptr), nseg, C.c_void_p(blob_ptr),
                                      blob_bytes, PTR_DEVICE))
+
+    def ingest_pinned(self, desc_ptr: int, n: int, seg_ptr: int, seg_sess_ptr: int, nseg: int,
+                      blob_ptr: int, blob_bytes: int):
+        """A batch in pinned host memory (edgpu_host_alloc): copied on the copy stream, asynchronous."""
+        _check(self.lib.edgpu_ingest(self.h, C.c_void_p(desc_ptr), n, C.c_void_p(seg_ptr),
+                                     C.c_void_p(seg_sess_ptr), nseg, C.c_void_p(blob_ptr),
+                                     blob_bytes, PTR_PINNED))
+
+    def host_alloc(self, nbytes: int) -> "HostBuffer":
+        return HostBuffer(self, nbytes)
 
     def ingest_interleaved(self, reads: np.ndarray, data, device_ptr: int | None = None) -> np.ndarray:
         """RTSP-interleaved push ingest: `reads` (TCP_READ_DTYPE: session, len, offset,
@@ -514,6 +526,28 @@ class Egress:
         if self.h:
             self.lib.edgpu_egress_destroy(self.h)
             self.h = None
+
+
+class HostBuffer:
+    """Pinned host memory owned by a context (edgpu_host_alloc); `.array` is a uint8 view."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        out = C.c_void_p()
+        _check(ctx.lib.edgpu_host_alloc(ctx.h, int(nbytes), C.byref(out)))
+        self.ctx, self.ptr, self.nbytes = ctx, int(out.value), int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))[:self.nbytes]
+
+    def free(self):
+        if self.ptr and self.ctx.h:
+            self.array = None
+            _check(self.ctx.lib.edgpu_host_free(self.ctx.h, C.c_void_p(self.ptr)))
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class DeviceBuffer:

@@ -157,7 +157,8 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
-           interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None, **cfg):
+           interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None,
+           pinned: bool = False, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -176,7 +177,10 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     capture is rebuilt from the bytes the receivers read.
 
     rewrite={sub_id: (seq_delta, ts_delta, ssrc or None)}: the per-output rewrite stage
-    (edgpu_subscriber_rewrite) on every track of those subscribers, set at their join."""
+    (edgpu_subscriber_rewrite) on every track of those subscribers, set at their join.
+
+    pinned=True: every ingest batch is written into pinned host buffers (edgpu_host_alloc,
+    two sets used alternately) and handed over as EDGPU_PTR_PINNED (asynchronous copy)."""
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
@@ -226,6 +230,23 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
                 unread = None
 
+        pin_sets = [{}, {}]                 # pinned host batch buffers, used alternately
+        pin_next = [0]
+
+        def pin_ingest(desc, seg_off, seg_sess, blob):
+            bufs = pin_sets[pin_next[0]]
+            pin_next[0] ^= 1
+            ptrs = []
+            for k, a in (("desc", desc), ("seg", seg_off), ("sess", seg_sess), ("blob", blob)):
+                raw = np.ascontiguousarray(a).view(np.uint8).ravel()
+                if k not in bufs or bufs[k].nbytes < raw.nbytes:
+                    if k in bufs:
+                        bufs[k].free()
+                    bufs[k] = ctx.host_alloc(max(raw.nbytes, 4096) * 2)
+                bufs[k].array[:raw.nbytes] = raw
+                ptrs.append(bufs[k].ptr)
+            ctx.ingest_pinned(ptrs[0], len(desc), ptrs[1], ptrs[2], len(seg_sess), ptrs[3], blob.nbytes)
+
         clock = 0                           # the harness's virtual clock: max event time so far
         plan = tcp_plan(_batches(trace, rep is None), interleaved) if interleaved is not None else None
         nflush = 0
@@ -242,7 +263,10 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     batch = pending
                 if batch:
                     desc, seg_off, seg_sess, blob = edgpu.build_batch([p[:4] for p in batch])
-                    ctx.ingest_host(desc, seg_off, seg_sess, blob)
+                    if pinned:
+                        pin_ingest(desc, seg_off, seg_sess, blob)
+                    else:
+                        ctx.ingest_host(desc, seg_off, seg_sess, blob)
                     ctx.keyframe_index()
                 nflush += 1
                 pending = []

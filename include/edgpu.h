@@ -74,6 +74,8 @@ extern "C" {
 /* pointer-location flags for edgpu_ingest */
 #define EDGPU_PTR_HOST           0     /* host memory: copied to the device before the call returns */
 #define EDGPU_PTR_DEVICE         1     /* already resident in HBM on the ctx device */
+#define EDGPU_PTR_PINNED         2     /* pinned host memory from edgpu_host_alloc: copied to HBM
+                                          asynchronously on the context's copy stream (below) */
 
 /* Engine configuration.  Reflector prefs keep the reference's XML key names
  * (WinNTSupport/easydarwin.xml:131-163, read at ReflectorStream.cpp:87-117 and
@@ -249,6 +251,19 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
                   const uint32_t* seg_offsets, const uint32_t* seg_session,
                   uint32_t n_segments, const uint8_t* blob, uint64_t blob_bytes,
                   int ptr_location);
+
+/* Pinned host staging for edgpu_ingest (north_star: "C++ host code batches ingested RTP
+ * packets ... into pinned HBM ring buffers"; replaces the per-packet memcpy into a
+ * ReflectorPacket, ReflectorStream.h:104-114).  The host (its socket reader) writes a batch --
+ * descriptors, segments and the slot blob -- straight into buffers from edgpu_host_alloc and
+ * calls edgpu_ingest(..., EDGPU_PTR_PINNED): the batch is validated on the host, copied to one
+ * of two device staging sets on a dedicated copy stream, and k_ingest waits for that copy on
+ * the context stream -- so the PCIe transfer of batch t+1 overlaps the fan-out of batch t, and
+ * the call returns without waiting for the GPU.  Buffer reuse: a pinned batch may be rewritten
+ * once the NEXT edgpu_ingest has returned (that call waits for the previous batch's copy), so
+ * two host batches used alternately never stall the reader on the GPU. */
+int  edgpu_host_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
+int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
 /* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
  * Replaces RTSPRequestStream::ReadRequest's '$' branch (Server.tproj/RTSPRequestStream.cpp:
  * 65-171, RTSPSession.cpp:240-262) and the per-frame hand-off to ProcessRTPData

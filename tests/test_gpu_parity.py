@@ -50,3 +50,12 @@ def test_engine_matches_reference(name, overlap):
     if os.path.exists(full):
         with open(full, "rb") as f:
             assert cap == f.read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mixed", "c1", "backpressure", "rtpinfo", "leave"])
+def test_pinned_host_ingest_matches_reference(name):
+    """Batches written into pinned host buffers (edgpu_host_alloc, two sets alternating) and
+    ingested asynchronously (EDGPU_PTR_PINNED: copy stream + event) give the reference bytes."""
+    cap, _ = replay(_trace(name), pinned=True)
+    assert hashlib.sha256(cap).hexdigest() == _fixture(name)["capture_sha256"]

@@ -315,7 +315,7 @@ int main(int argc, char** argv) {
             if (!push_rtsp[s]) continue;
             Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_obj(qtssClientSessionObjectType), {}};
             g_rtsp_of_client[pl.client] = pl.rtsp;
-            const std::string agent = (ua & 1) ? "LibVLC/3.0.8 (LIVE555 Streaming Media v2016.11.28)" : "EasyPlayer/1.0";
+            const std::string agent = (ua & 1) ? "vlc/3.0.8 LibVLC/3.0.8" : "EasyPlayer/1.0";   // case-sensitive match
             set_attr(pl.client, qtssCliSesFirstUserAgent, 0, agent.data(), (uint32_t)agent.size());
             const uint32_t tt = tr ? qtssRTPTransportTypeTCP : qtssRTPTransportTypeUDP;
             const size_t before = g_streams.size();
