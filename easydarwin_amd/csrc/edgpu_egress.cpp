@@ -8,11 +8,19 @@
 //     kAllOrNothing (RTSPResponseStream.cpp:36-140): data left in the stream's output buffer
 //     goes first; if it cannot all go, or none of the new frame goes, the write is EAGAIN ->
 //     QTSS_WouldBlock; a frame that goes out partly counts as sent and its tail is buffered.
-// Here one call sends a whole tick: the arena, descriptors and sub-stream table are copied to
-// pinned host memory once, worker threads own disjoint subscribers (a TCP connection's frames
-// keep the reference's per-connection order: track, RTP before RTCP), UDP datagrams leave in
-// sendmmsg batches, TCP frames in writev batches, and the sub-streams that blocked are reported
-// to the engine (edgpu_fanout_blocked) so the next tick resumes where the reference would.
+// Here one call sends a whole tick: the tick's DISTINCT bytes are brought to pinned host memory
+// in one copy -- sub-streams flagged EDGPU_SUB_IDENTITY (UDP, no rewrite) of one sender carry the
+// same bytes, each a suffix of the longest, so only that one region per sender crosses PCIe
+// (edgpu_arena_gather packs the regions on the device first); TCP and rewritten sub-streams
+// bring their own (EDGPU_EGRESS_DEDUP=0 copies the whole write-many arena instead).  Worker
+// threads own disjoint subscribers (a TCP connection's frames keep the reference's
+// per-connection order: track, RTP before RTCP), UDP datagrams leave in sendmmsg batches, TCP
+// frames in sendmsg batches (MSG_NOSIGNAL: a reset peer raises no SIGPIPE), and the sub-streams
+// that blocked are reported to the engine (edgpu_fanout_blocked) so the next tick resumes
+// where the reference would.  Only EAGAIN blocks a TCP write; any other error marks the
+// connection dead: like the reference, whose WritePacket counts a failed non-EAGAIN write as
+// written (RTPSessionOutput.cpp:612-653), nothing is resent, and edgpu_egress_disconnected
+// lists it for the host to tear down (ClientSessionClosing).
 // Host code only: it uses the public C ABI of the engine.
 #include <hip/hip_runtime.h>
 
@@ -43,6 +51,8 @@ struct UdpDest {
 struct TcpConn {
     int fd = -1;
     std::string pending;                // RTSPResponseStream output buffer (unsent tail)
+    int dead = 0;                       // errno of a failed (non-EAGAIN) write, 0 = alive
+    bool reported = false;
 };
 
 struct Worker {
@@ -56,14 +66,20 @@ struct Worker {
 struct edgpu_egress {
     edgpu_ctx* ctx = nullptr;
     uint32_t nthreads = 1;
+    bool dedup = true;
     std::map<uint64_t, UdpDest> udp;    // (subscriber << 16 | track)
     std::map<uint32_t, TcpConn> tcp;    // subscriber
-    uint8_t* h_arena = nullptr;
+    uint8_t* h_arena = nullptr;         // pinned: the tick's bytes (whole arena, or the gathered regions)
     size_t h_arena_cap = 0;
+    void* d_gather = nullptr;           // device staging of the gathered regions
+    uint64_t d_gather_cap = 0;
     std::vector<edgpu_out_desc> desc;
     std::vector<edgpu_substream_out> subs;
+    std::vector<const uint8_t*> base;   // per sub-stream: host address of its arena region's start
     std::vector<Worker> workers;
     std::vector<edgpu_blocked> last_blocked;
+    std::vector<uint32_t> disconnected;
+    uint64_t copied_bytes = 0;
     std::string err;
 };
 
@@ -74,8 +90,9 @@ static int eg_fail(edgpu_egress* e, int code, const std::string& m) {
 
 // One UDP sub-stream: every datagram is offered to the socket once (errors ignored, like the
 // reference's (void)SendTo); EAGAIN / ENOBUFS drop the datagram.
-static void send_udp(edgpu_egress* e, Worker& w, const edgpu_substream_out& s, const UdpDest& d) {
+static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d) {
     const int k = s.kind ? 1 : 0;
+    const uint8_t* base = e->base[q] - s.out_base;
     const int fd = d.fd[k] >= 0 ? d.fd[k] : w.udp_fd;
     const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
     constexpr uint32_t kBatch = 256;
@@ -85,7 +102,7 @@ static void send_udp(edgpu_egress* e, Worker& w, const edgpu_substream_out& s, c
     while (i < s.desc_count) {
         const uint32_t n = std::min(kBatch, s.desc_count - i);
         for (uint32_t j = 0; j < n; j++) {
-            iov[j].iov_base = e->h_arena + ds[i + j].offset;
+            iov[j].iov_base = const_cast<uint8_t*>(base + ds[i + j].offset);
             iov[j].iov_len = ds[i + j].len;
             memset(&msgs[j].msg_hdr, 0, sizeof(msgs[j].msg_hdr));
             msgs[j].msg_hdr.msg_name = const_cast<sockaddr_in*>(&d.addr[k]);
@@ -115,6 +132,8 @@ static void send_udp(edgpu_egress* e, Worker& w, const edgpu_substream_out& s, c
 // then buffered) are sent; the first frame that gets no byte blocks the sub-stream.
 static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, TcpConn& c) {
     const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
+    const uint8_t* base = e->base[q] - s.out_base;
+    if (c.dead) return;                                   // counted as written, never resent
     uint32_t i = 0;
     while (i < s.desc_count) {
         constexpr uint32_t kBatch = 512;
@@ -125,13 +144,22 @@ static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
         const uint32_t n = std::min(kBatch, s.desc_count - i);
         size_t total = plen;
         for (uint32_t j = 0; j < n; j++) {
-            iov[nv].iov_base = e->h_arena + ds[i + j].offset;
+            iov[nv].iov_base = const_cast<uint8_t*>(base + ds[i + j].offset);
             iov[nv].iov_len = ds[i + j].len;
             total += ds[i + j].len;
             nv++;
         }
-        ssize_t r = writev(c.fd, iov, (int)nv);
+        msghdr mh;
+        memset(&mh, 0, sizeof(mh));
+        mh.msg_iov = iov;
+        mh.msg_iovlen = nv;
+        ssize_t r = sendmsg(c.fd, &mh, MSG_NOSIGNAL);
         if (r < 0 && errno == EINTR) continue;
+        if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) {   // peer gone: not backpressure
+            c.dead = errno;
+            c.pending.clear();
+            return;
+        }
         size_t wrote = r > 0 ? (size_t)r : 0;
         if (wrote < plen) {                               // the old tail is still not out
             c.pending.erase(0, wrote);
@@ -145,7 +173,7 @@ static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
         w.tcp_frames += j;
         if (j < n && wrote > 0) {                         // partly out: counted sent, tail buffered
             const edgpu_out_desc& d = ds[i + j];
-            c.pending.assign(reinterpret_cast<const char*>(e->h_arena + d.offset) + wrote, d.len - wrote);
+            c.pending.assign(reinterpret_cast<const char*>(base + d.offset) + wrote, d.len - wrote);
             w.tcp_bytes += d.len;
             w.tcp_frames++;
             j++;
@@ -168,6 +196,7 @@ int edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out) {
     edgpu_egress* e = new edgpu_egress();
     e->ctx = ctx;
     e->nthreads = std::max(1u, std::min(threads, 64u));
+    if (const char* v = getenv("EDGPU_EGRESS_DEDUP")) e->dedup = atoi(v) != 0;
     e->workers.resize(e->nthreads);
     for (Worker& w : e->workers) {
         w.udp_fd = socket(AF_INET, SOCK_DGRAM, 0);
@@ -183,6 +212,7 @@ int edgpu_egress_destroy(edgpu_egress* e) {
     if (!e) return EDGPU_OK;
     for (Worker& w : e->workers) if (w.udp_fd >= 0) close(w.udp_fd);
     if (e->h_arena) (void)hipHostFree(e->h_arena);
+    if (e->d_gather) (void)edgpu_device_free(e->ctx, e->d_gather);
     delete e;
     return EDGPU_OK;
 }
@@ -218,20 +248,76 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     int rc = edgpu_tick_stats_get(e->ctx, &st);
     if (rc) return eg_fail(e, rc, "tick stats");
     if (st.status) return eg_fail(e, st.status, "device-side status after fan-out");
-    if (st.arena_bytes > e->h_arena_cap) {
+    e->desc.resize(st.relayed_packets);
+    e->subs.resize(r->n_substreams);
+    if ((rc = edgpu_copy_to_host(e->ctx, e->desc.data(), r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
+        (rc = edgpu_copy_to_host(e->ctx, e->subs.data(), r->substreams, r->n_substreams * sizeof(edgpu_substream_out))))
+        return eg_fail(e, rc, "copy to host");
+    // the regions to bring over: one per identity sender (its longest sub-stream) + every other
+    // non-empty sub-stream; `src[q]` = (region index, byte offset of q's region in it)
+    const uint32_t nq = (uint32_t)e->subs.size();
+    std::vector<edgpu_region> reg;
+    std::vector<std::pair<uint32_t, uint64_t>> src(nq, {0xFFFFFFFFu, 0});
+    uint64_t need = 0;
+    if (e->dedup) {
+        std::map<uint32_t, uint32_t> rep;                 // sender -> its longest identity sub-stream
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = e->subs[q];
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
+            auto it = rep.find(s.sender);
+            if (it == rep.end() || e->subs[it->second].out_bytes < s.out_bytes) rep[s.sender] = q;
+        }
+        std::map<uint32_t, uint32_t> rep_reg;             // sender -> region index
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = e->subs[q];
+            if (!s.desc_count) continue;
+            if (s.flags & EDGPU_SUB_IDENTITY) {
+                const edgpu_substream_out& R = e->subs[rep[s.sender]];
+                auto it = rep_reg.find(s.sender);
+                if (it == rep_reg.end()) {
+                    it = rep_reg.emplace(s.sender, (uint32_t)reg.size()).first;
+                    reg.push_back(edgpu_region{R.out_base, R.out_bytes});
+                    need += R.out_bytes;
+                }
+                src[q] = {it->second, R.out_bytes - s.out_bytes};  // q is a suffix of the longest
+            } else {
+                src[q] = {(uint32_t)reg.size(), 0};
+                reg.push_back(edgpu_region{s.out_base, s.out_bytes});
+                need += s.out_bytes;
+            }
+        }
+    } else {
+        need = st.arena_bytes;
+    }
+    if (need > e->h_arena_cap) {
         if (e->h_arena) (void)hipHostFree(e->h_arena);
         e->h_arena = nullptr;
-        const size_t cap = std::max<size_t>(st.arena_bytes, 1 << 20);
+        const size_t cap = std::max<size_t>(need, 1 << 20);
         if (hipHostMalloc((void**)&e->h_arena, cap, hipHostMallocDefault) != hipSuccess)
             return eg_fail(e, EDGPU_OUT_OF_MEMORY, "pinned arena");
         e->h_arena_cap = cap;
     }
-    e->desc.resize(st.relayed_packets);
-    e->subs.resize(r->n_substreams);
-    if ((rc = edgpu_copy_to_host(e->ctx, e->h_arena, r->arena, st.arena_bytes)) ||
-        (rc = edgpu_copy_to_host(e->ctx, e->desc.data(), r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
-        (rc = edgpu_copy_to_host(e->ctx, e->subs.data(), r->substreams, r->n_substreams * sizeof(edgpu_substream_out))))
-        return eg_fail(e, rc, "copy to host");
+    e->base.assign(nq, nullptr);
+    if (e->dedup) {
+        if (need > e->d_gather_cap) {
+            if (e->d_gather) (void)edgpu_device_free(e->ctx, e->d_gather);
+            e->d_gather = nullptr;
+            e->d_gather_cap = 0;
+            if ((rc = edgpu_device_alloc(e->ctx, need, &e->d_gather))) return eg_fail(e, rc, "gather buffer");
+            e->d_gather_cap = need;
+        }
+        if ((rc = edgpu_arena_gather(e->ctx, r, reg.data(), (uint32_t)reg.size(), e->d_gather, e->d_gather_cap)) ||
+            (rc = edgpu_copy_to_host(e->ctx, e->h_arena, e->d_gather, need)))
+            return eg_fail(e, rc, "gather / copy to host");
+        std::vector<uint64_t> roff(reg.size() + 1, 0);
+        for (size_t i = 0; i < reg.size(); i++) roff[i + 1] = roff[i] + reg[i].bytes;
+        for (uint32_t q = 0; q < nq; q++)
+            if (src[q].first != 0xFFFFFFFFu) e->base[q] = e->h_arena + roff[src[q].first] + src[q].second;
+    } else {
+        if ((rc = edgpu_copy_to_host(e->ctx, e->h_arena, r->arena, st.arena_bytes))) return eg_fail(e, rc, "copy to host");
+        for (uint32_t q = 0; q < nq; q++) e->base[q] = e->h_arena + e->subs[q].out_base;
+    }
+    e->copied_bytes = need;
     auto t1 = std::chrono::steady_clock::now();
     for (Worker& w : e->workers) { w.blocked.clear(); w.udp_datagrams = w.udp_bytes = w.udp_dropped = w.tcp_frames = w.tcp_bytes = 0; }
     auto run = [&](uint32_t k) {
@@ -244,7 +330,7 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
                 if (it != e->tcp.end()) send_tcp(e, w, q, s, it->second);
             } else {
                 auto it = e->udp.find((uint64_t)s.subscriber << 16 | s.track);
-                if (it != e->udp.end()) send_udp(e, w, s, it->second);
+                if (it != e->udp.end()) send_udp(e, w, q, s, it->second);
             }
         }
     };
@@ -269,6 +355,9 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     s.copy_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     s.send_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     e->last_blocked = blocked;
+    for (auto& kv : e->tcp)
+        if (kv.second.dead && !kv.second.reported) { e->disconnected.push_back(kv.first); kv.second.reported = true; }
+    s.copied_bytes = e->copied_bytes;
     if (!blocked.empty() && (rc = edgpu_fanout_blocked(e->ctx, blocked.data(), (uint32_t)blocked.size())))
         return eg_fail(e, rc, "backpressure report");
     if (out) *out = s;
@@ -283,18 +372,29 @@ int edgpu_egress_blocked(edgpu_egress* e, edgpu_blocked* out, uint32_t cap, uint
     return EDGPU_OK;
 }
 
+int edgpu_egress_disconnected(edgpu_egress* e, uint32_t* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n || (cap && !out)) return EDGPU_BAD_ARGUMENT;
+    const uint32_t k = (uint32_t)std::min<size_t>(cap, e->disconnected.size());
+    std::copy(e->disconnected.begin(), e->disconnected.begin() + k, out);
+    *n = (uint32_t)e->disconnected.size();
+    e->disconnected.erase(e->disconnected.begin(), e->disconnected.begin() + k);
+    return EDGPU_OK;
+}
+
 int edgpu_egress_flush(edgpu_egress* e, uint64_t* out_pending) {
     if (!e) return EDGPU_BAD_ARGUMENT;
     uint64_t left = 0;
     for (auto& kv : e->tcp) {
         TcpConn& c = kv.second;
-        while (!c.pending.empty()) {
-            const ssize_t r = write(c.fd, c.pending.data(), c.pending.size());
+        while (!c.pending.empty() && !c.dead) {
+            const ssize_t r = send(c.fd, c.pending.data(), c.pending.size(), MSG_NOSIGNAL);
             if (r < 0 && errno == EINTR) continue;
+            if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) { c.dead = errno; c.pending.clear(); break; }
             if (r <= 0) break;
             c.pending.erase(0, (size_t)r);
         }
         left += c.pending.size();
+        if (c.dead && !c.reported) { e->disconnected.push_back(kv.first); c.reported = true; }
     }
     if (out_pending) *out_pending = left;
     return EDGPU_OK;

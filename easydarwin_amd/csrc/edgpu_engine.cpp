@@ -32,6 +32,8 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
 hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
+hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
+                               uint8_t* dst, hipStream_t st);
 int fanout_chunk(int variant);
 bool fanout_rewrites(int variant);
 const char* fanout_name(int variant);
@@ -238,6 +240,8 @@ struct edgpu_ctx {
     FirstInfoQuery* h_fpi_q = nullptr;          // pinned
     FirstInfoResult* h_fpi_r = nullptr;         // pinned
     DevVec<edgpu_blocked> d_blocked;
+    DevVec<edgpu_region> d_gather_reg;          // edgpu_arena_gather
+    DevVec<uint64_t> d_gather_off;
     // session images
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
@@ -336,6 +340,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
+    x->d_gather_reg.release(); x->d_gather_off.release();
     if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
@@ -1214,6 +1219,30 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->ingested_bytes = t.ingested_bytes;
     out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
+    return EDGPU_OK;
+}
+
+int edgpu_arena_gather(edgpu_ctx* x, const edgpu_fanout_result* r, const edgpu_region* reg, uint32_t n, void* dst,
+                       uint64_t cap) {
+    if (!x || !r || (n && (!reg || !dst))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!n) return EDGPU_OK;
+    std::vector<uint64_t> off(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((reg[i].offset | reg[i].bytes) & 15) return fail(EDGPU_BAD_ARGUMENT, "regions must be 16-B aligned");
+        if (reg[i].offset + reg[i].bytes > x->cfg.out_arena_bytes) return fail(EDGPU_BAD_ARGUMENT, "region outside the arena");
+        off[i] = total;
+        total += reg[i].bytes;
+    }
+    if (total > cap) return fail(EDGPU_OUT_OVERFLOW, "gather destination too small");
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(sync_all(x));                      // the tick's copy (overlap_ticks: second stream) is done
+    HIP_CHECK(x->d_gather_reg.reserve(n, x->stream));
+    HIP_CHECK(x->d_gather_off.reserve(n, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_gather_reg.ptr, reg, n * sizeof(edgpu_region), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_gather_off.ptr, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(launch_arena_gather(r->arena, x->d_gather_reg.ptr, x->d_gather_off.ptr, n, (uint8_t*)dst, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));  // `reg` and `off` are host memory
     return EDGPU_OK;
 }
 

@@ -722,6 +722,8 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         o.desc_count = Q.count;
         o.out_base = Q.out_base;
         o.out_bytes = Q.bytes;
+        o.sender = Q.sender;
+        o.flags = (!Q.transport && !Q.rw) ? EDGPU_SUB_IDENTITY : 0u;
         P.sub_out[q] = o;
         if (Q.count > 0) Q.sent_any = 1;
         const uint32_t pos = P.sub_pos[q];
@@ -1647,6 +1649,21 @@ __global__ __launch_bounds__(256) void k_image_apply(ImageParams P) {
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (internal C++ API used by edgpu_engine.cpp)
 namespace edgpu {
+
+// edgpu_arena_gather: one workgroup per region, 16-B words (offsets / lengths are slot-aligned)
+__global__ __launch_bounds__(256) void k_arena_gather(const u32x4* arena, const edgpu_region* reg, const uint64_t* dst_off,
+                                                      u32x4* dst) {
+    const edgpu_region r = reg[blockIdx.x];
+    const u32x4* s = arena + r.offset / 16;
+    u32x4* d = dst + dst_off[blockIdx.x] / 16;
+    for (uint64_t w = threadIdx.x; w < r.bytes / 16; w += blockDim.x) __builtin_nontemporal_store(s[w], d + w);
+}
+hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
+                               uint8_t* dst, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_arena_gather, dim3(n), dim3(256), 0, st, reinterpret_cast<const u32x4*>(arena), reg,
+                              dst_off, reinterpret_cast<u32x4*>(dst));
+    return hipGetLastError();
+}
 
 hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st) {
     hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, totals, 1);

@@ -34,6 +34,7 @@ EXPORTED = [
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
+    "edgpu_arena_gather", "edgpu_egress_disconnected",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -87,7 +88,8 @@ class OutDesc(C.Structure):
 class SubstreamOut(C.Structure):
     _fields_ = [("subscriber", C.c_uint32), ("track", C.c_uint16), ("kind", C.c_uint8),
                 ("transport", C.c_uint8), ("desc_base", C.c_uint32), ("desc_count", C.c_uint32),
-                ("out_base", C.c_uint64), ("out_bytes", C.c_uint64)]
+                ("out_base", C.c_uint64), ("out_bytes", C.c_uint64), ("sender", C.c_uint32),
+                ("flags", C.c_uint32)]
 
 
 class FanoutResult(C.Structure):
@@ -104,7 +106,8 @@ class TickStats(C.Structure):
 class EgressStats(C.Structure):
     _fields_ = [("udp_datagrams", C.c_uint64), ("udp_bytes", C.c_uint64), ("udp_dropped", C.c_uint64),
                 ("tcp_frames", C.c_uint64), ("tcp_bytes", C.c_uint64), ("blocked_substreams", C.c_uint32),
-                ("_pad", C.c_uint32), ("copy_ms", C.c_double), ("send_ms", C.c_double)]
+                ("_pad", C.c_uint32), ("copy_ms", C.c_double), ("send_ms", C.c_double),
+                ("copied_bytes", C.c_uint64)]
 
 
 class Counters(C.Structure):
@@ -119,7 +122,8 @@ PKT_DTYPE = np.dtype([("slot", "<u4"), ("len", "<u2"), ("channel", "u1"), ("flag
 OUT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("packet_id", "<u4")])
 SUB_DTYPE = np.dtype([("subscriber", "<u4"), ("track", "<u2"), ("kind", "u1"), ("transport", "u1"),
                       ("desc_base", "<u4"), ("desc_count", "<u4"), ("out_base", "<u8"),
-                      ("out_bytes", "<u8")])
+                      ("out_bytes", "<u8"), ("sender", "<u4"), ("flags", "<u4")])
+SUB_IDENTITY = 1
 TCP_READ_DTYPE = np.dtype([("session", "<u4"), ("len", "<u4"), ("offset", "<u8"), ("arrival_ms", "<i8")])
 TCP_RESULT_DTYPE = np.dtype([("frames", "<u4"), ("consumed", "<u4"), ("status", "<i4"), ("carry", "<u4")])
 UDP_SOURCE_DTYPE = np.dtype([("session", "<u4"), ("channel", "u1"), ("_pad", "u1"), ("port", "<u2"),
@@ -131,7 +135,7 @@ assert UDP_SOURCE_DTYPE.itemsize == 20 and SOURCE_REPORT_DTYPE.itemsize == 112
 assert TCP_READ_DTYPE.itemsize == 24 and TCP_RESULT_DTYPE.itemsize == 16
 assert PKT_DTYPE.itemsize == C.sizeof(PktDesc) == 16
 assert OUT_DTYPE.itemsize == C.sizeof(OutDesc) == 16
-assert SUB_DTYPE.itemsize == C.sizeof(SubstreamOut) == 32
+assert SUB_DTYPE.itemsize == C.sizeof(SubstreamOut) == 40
 
 
 class EdgpuError(RuntimeError):
@@ -200,6 +204,8 @@ def load(path: str = LIB_PATH):
         "edgpu_sdp_parse": (I32, [C.c_char_p, U32, C.POINTER(SdpTrack), U32, C.POINTER(U32)]),
         "edgpu_host_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_host_free": (I32, [P, P]),
+        "edgpu_arena_gather": (I32, [P, C.POINTER(FanoutResult), P, U32, P, U64]),
+        "edgpu_egress_disconnected": (I32, [P, P, U32, C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -516,6 +522,13 @@ class Egress:
         n = C.c_uint32()
         self._chk(self.lib.edgpu_egress_blocked(self.h, _ptr(buf), cap, C.byref(n)))
         return [tuple(map(int, x)) for x in buf[:min(n.value, cap)]]
+
+    def disconnected(self) -> list:
+        """Subscribers whose RTSP connection failed (not EAGAIN) since the last call."""
+        buf = np.zeros(4096, dtype=np.uint32)
+        n = C.c_uint32()
+        self._chk(self.lib.edgpu_egress_disconnected(self.h, _ptr(buf), len(buf), C.byref(n)))
+        return [int(x) for x in buf[:min(n.value, len(buf))]]
 
     def flush(self) -> int:
         left = C.c_uint64()

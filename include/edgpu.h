@@ -142,7 +142,12 @@ typedef struct edgpu_substream_out {
     uint32_t desc_count;
     uint64_t out_base;      /* arena offset of the first slot */
     uint64_t out_bytes;     /* arena bytes spanned (slot-padded) */
+    uint32_t sender;        /* the engine sender (track x RTP|RTCP of a session) it relays */
+    uint32_t flags;         /* EDGPU_SUB_IDENTITY: its bytes are the sender's packets unmodified
+                               (UDP, no rewrite) -- two such sub-streams of one sender carry the
+                               same bytes, the shorter one a suffix of the longer */
 } edgpu_substream_out;
+#define EDGPU_SUB_IDENTITY 1u
 
 /* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout (the second
  * next one with overlap_ticks). */
@@ -393,8 +398,9 @@ int  edgpu_session_eyes_add(edgpu_ctx* ctx, uint32_t session, int32_t delta);
  * RTSPResponseStream::WriteV(kAllOrNothing) semantics (RTSPResponseStream.cpp:36-140: a frame
  * that goes out in part counts as sent and its tail is buffered; a frame that gets no byte
  * blocks).  Blocked TCP sub-streams are reported with edgpu_fanout_blocked before returning.
- * The tick's arena, descriptors and sub-stream table are copied once into pinned host memory;
- * `threads` workers own disjoint subscribers and send with sendmmsg / writev. */
+ * The tick's distinct bytes come over PCIe in one copy (identity UDP sub-streams of a sender share
+ * one region, edgpu_arena_gather), with the descriptors and sub-stream table; `threads` workers
+ * own disjoint subscribers and send with sendmmsg / sendmsg. */
 typedef struct edgpu_egress edgpu_egress;
 typedef struct edgpu_egress_stats {
     uint64_t udp_datagrams, udp_bytes;
@@ -403,6 +409,7 @@ typedef struct edgpu_egress_stats {
     uint32_t blocked_substreams;
     uint32_t _pad;
     double   copy_ms, send_ms;  /* device -> pinned host copy; socket writes */
+    uint64_t copied_bytes;      /* bytes brought over PCIe for this tick */
 } edgpu_egress_stats;
 int  edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out);
 int  edgpu_egress_destroy(edgpu_egress* eg);
@@ -418,8 +425,23 @@ int  edgpu_egress_send(edgpu_egress* eg, const edgpu_fanout_result* r, edgpu_egr
 int  edgpu_egress_blocked(edgpu_egress* eg, edgpu_blocked* out, uint32_t cap, uint32_t* n);
 /* Writes buffered TCP tails that fit now; *pending = bytes still buffered. */
 int  edgpu_egress_flush(edgpu_egress* eg, uint64_t* pending);
+/* Subscribers whose RTSP connection failed with an error other than EAGAIN since the last
+ * call (reset / closed peer): their frames are no longer written (the reference counts such a
+ * write as done, RTPSessionOutput.cpp:612-653); the host tears the session down
+ * (ClientSessionClosing -> edgpu_subscriber_remove).  Sockets are written with MSG_NOSIGNAL. */
+int  edgpu_egress_disconnected(edgpu_egress* eg, uint32_t* out, uint32_t cap, uint32_t* n);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
+
+/* Packs regions of a fan-out arena (16-B aligned offsets and lengths; in the order given)
+ * back to back into device memory `dst` on the context stream -- so a host egress can bring
+ * the distinct bytes of a tick over PCIe in one copy instead of the whole write-many arena. */
+typedef struct edgpu_region {
+    uint64_t offset;        /* arena byte offset, multiple of 16 */
+    uint64_t bytes;         /* multiple of 16 */
+} edgpu_region;
+int  edgpu_arena_gather(edgpu_ctx* ctx, const edgpu_fanout_result* r, const edgpu_region* regions, uint32_t n,
+                        void* dst_device, uint64_t dst_cap);
 
 /* Name of the fan-out copy kernel this context launches (for measurement reports). */
 const char* edgpu_fanout_kernel(edgpu_ctx* ctx);

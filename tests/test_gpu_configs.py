@@ -87,7 +87,7 @@ def test_c3_per_gpu_shape_properties():
             per_sess = np.diff(seg)
             want = np.array([c for c, _ in first]) if t == 0 else per_sess
             assert st.relayed_packets == int(want.sum()) * subs
-            subs_tab = ctx.copy_to_host(r.substreams, r.n_substreams * 32).view(edgpu.SUB_DTYPE)
+            subs_tab = ctx.copy_to_host(r.substreams, r.n_substreams * edgpu.SUB_DTYPE.itemsize).view(edgpu.SUB_DTYPE)
             rtp = subs_tab[subs_tab["kind"] == 0]
             assert len(rtp) == n_sess * subs
             assert np.all(subs_tab[subs_tab["kind"] == 1]["desc_count"] == 0)
@@ -172,7 +172,7 @@ def test_c4_burst_joins_match_owner_gop():
         for ctx, r, handles, sess in ((owner, ro, h_own, sess_of[~remote]), (replica, rr, h_rep, sess_of[remote])):
             st = ctx.stats()
             assert st.status == 0
-            tab = ctx.copy_to_host(r.substreams, r.n_substreams * 32).view(edgpu.SUB_DTYPE)
+            tab = ctx.copy_to_host(r.substreams, r.n_substreams * edgpu.SUB_DTYPE.itemsize).view(edgpu.SUB_DTYPE)
             rtp = tab[tab["kind"] == 0]
             by_handle = {int(q["subscriber"]): q for q in rtp}
             counts = np.array([int(by_handle[int(h)]["desc_count"]) for h in handles])

@@ -77,3 +77,51 @@ def test_tcp_backpressure_over_sockets(name, oracle_bins, tmp_path):
         got = capture_summary(read_capture(cap))
         bad = [k for k in want if got.get(k) != want[k]]
         assert not bad, f"{which}: {len(bad)} sub-streams differ, e.g. {bad[:3]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dedup", ["0", "1"])
+def test_egress_copy_modes_match_reference(dedup, monkeypatch):
+    """EDGPU_EGRESS_DEDUP=1 (default) brings one region per identity sender over PCIe
+    (edgpu_arena_gather) instead of the whole write-many arena: same bytes on the wire."""
+    monkeypatch.setenv("EDGPU_EGRESS_DEDUP", dedup)
+    cap, _ = replay(SCENARIOS["udppush"](), sockets={"threads": 2})
+    assert hashlib.sha256(cap).hexdigest() == _fixture("udppush")["capture_sha256"]
+
+
+@pytest.mark.gpu
+def test_egress_dedup_copies_less_and_reports_dead_peers():
+    import numpy as np
+    from easydarwin_amd import edgpu
+    from easydarwin_amd.egress import SocketSink
+    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=800_000, gop=30, idr_bytes=9_000)]
+    pk = session_packets(tracks, 3000, 0xEA5D + 99)
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(tracks))
+        sink = SocketSink(ctx, threads=2)
+        hs = [ctx.subscriber_add(s, edgpu.TRANSPORT_UDP) for _ in range(4)]
+        ht = [ctx.subscriber_add(s, edgpu.TRANSPORT_TCP) for _ in range(2)]
+        for i, h in enumerate(hs + ht):
+            sink.join(h, 100 + i, 1, h in ht)
+        sent_copy, arena = [], []
+        for tick in range(1, 31):
+            t = tick * 100
+            batch = [(s, ch, tt, d) for tt, ch, d in pk if t - 100 < tt <= t]
+            if batch:
+                desc, so, ss, blob = edgpu.build_batch(batch)
+                ctx.ingest_host(desc, so, ss, blob)
+                ctx.keyframe_index()
+            r = ctx.fanout(t)
+            st = sink.tick(r, t)
+            sent_copy.append(st.copied_bytes)
+            arena.append(ctx.stats().arena_bytes)
+            if tick == 10:
+                sink.tcp[ht[0]][1].close()          # the player's end goes away: EPIPE, not EAGAIN
+        assert sum(sent_copy) * 4 < sum(arena)      # 4 identical UDP copies + 2 TCP: > 4x less
+        assert sink.eg.disconnected() == [ht[0]]
+        assert sink.eg.disconnected() == []         # reported once
+        # the other TCP player and the UDP players kept receiving after the disconnect
+        sink.drain()
+        assert len(sink.tcp[ht[1]][2]) > 0 and all(len(sink.parts[(h, 0, 0)]) > 0 for h in hs)
+        sink.close()

@@ -108,7 +108,7 @@ def test_c2_full_size_properties(overlap):
                 # steady state: every subscriber receives exactly this tick's packets
                 assert st.relayed_packets == int(per_sess.sum()) * subs
                 assert st.relayed_bytes == int(b["len"].astype(np.int64).sum()) * subs
-            subs_tab = ctx.copy_to_host(r.substreams, r.n_substreams * 32).view(edgpu.SUB_DTYPE)
+            subs_tab = ctx.copy_to_host(r.substreams, r.n_substreams * edgpu.SUB_DTYPE.itemsize).view(edgpu.SUB_DTYPE)
             d = ctx.copy_to_host(r.desc, st.relayed_packets * 16).view(edgpu.OUT_DTYPE)
             rtp = subs_tab[subs_tab["kind"] == 0]
             assert len(rtp) == n_sess * subs
