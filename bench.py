@@ -167,9 +167,10 @@ def _shard(tr, k: int, n: int):
     return out
 
 
-def _reference_replay(args, tick: int, procs_n: int):
+def _reference_replay(args, tick: int, procs_n: int, mode: str = "--bench"):
     """One timed run of the reference reflector on the bounded sample at `tick`-ms ticks:
-    (relayed packets, relayed bytes, longest process seconds, repeats)."""
+    (relayed packets, relayed bytes, longest process seconds, repeats).  mode "--bench-udp"
+    sends every subscriber packet with a real sendto() to loopback instead of a memcpy."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     tr = _sample_trace(args, tick=tick)
     with tempfile.TemporaryDirectory() as td:
@@ -178,10 +179,10 @@ def _reference_replay(args, tick: int, procs_n: int):
             p = os.path.join(td, f"s{k}.edtr")
             _shard(tr, k, procs_n).write(p)
             paths.append(p)
-        probe = json.loads(subprocess.run([exe, "--bench", paths[0], "1"], capture_output=True, text=True,
+        probe = json.loads(subprocess.run([exe, mode, paths[0], "1"], capture_output=True, text=True,
                                           check=True).stdout)
         rep = int(max(1, min(2000, 1.5 / max(probe["seconds"], 1e-4))))     # ~1.5 s per process
-        procs = [subprocess.Popen([exe, "--bench", p, str(rep)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+        procs = [subprocess.Popen([exe, mode, p, str(rep)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
                                   text=True) for p in paths]
         outs = [json.loads(pr.communicate()[0]) for pr in procs]
         if any(pr.returncode for pr in procs):
@@ -203,6 +204,7 @@ def cpu_baseline_reference(args) -> dict | None:
     procs_n = min(16, os.cpu_count() or 1)
     r100 = _reference_replay(args, 100, procs_n)
     r1000 = _reference_replay(args, 1000, procs_n)
+    rudp = _reference_replay(args, 100, procs_n, "--bench-udp")
     if r100 is None:
         return None
     pk, by, secs, rep = r100
@@ -216,6 +218,12 @@ def cpu_baseline_reference(args) -> dict | None:
         pk1, by1, secs1, rep1 = r1000
         out["tick_1000ms"] = {"value": round(pk1 / secs1, 1), "GBps": round(by1 / secs1 / 1e9, 3),
                               "relayed_packets": pk1, "seconds": round(secs1, 3), "repeat": rep1}
+    if rudp is not None:            # the full write path: one sendto() per subscriber packet
+        pku, byu, secsu, repu = rudp
+        out["with_udp_sockets"] = {"value": round(pku / secsu, 1), "unit": "datagrams/s",
+                                   "GBps": round(byu / secsu / 1e9, 3), "relayed_packets": pku,
+                                   "seconds": round(secsu, 3), "repeat": repu, "tick_ms": 100,
+                                   "sink": "one unread 127.0.0.1 UDP socket per process"}
     return out
 
 

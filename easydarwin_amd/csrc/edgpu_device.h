@@ -149,7 +149,7 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint8_t  channel;               // interleaved channel 2*track + kind (RTPStream.cpp:472-473)
     uint8_t  active;
     uint8_t  has_last;
-    uint8_t  _pad0;
+    uint8_t  was_new;               // no bookmark when this tick began (ReflectPackets' firstPacket)
     int64_t  bookmark;              // ReflectorOutput bookmark index, -1 = none
     uint64_t last_id;               // qtssReflectorStreamLast{RTP,RTCP}PacketID
     // per tick

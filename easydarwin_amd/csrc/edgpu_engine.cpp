@@ -32,6 +32,8 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
 hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
+hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
+                               hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
 int fanout_chunk(int variant);
@@ -241,6 +243,7 @@ struct edgpu_ctx {
     FirstInfoResult* h_fpi_r = nullptr;         // pinned
     DevVec<edgpu_blocked> d_blocked;
     DevVec<edgpu_region> d_gather_reg;          // edgpu_arena_gather
+    DevVec<int64_t> d_arrivals;                 // edgpu_fanout_arrivals
     DevVec<uint64_t> d_gather_off;
     // session images
     DevVec<ImgPlan> d_img_plan;
@@ -340,7 +343,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
-    x->d_gather_reg.release(); x->d_gather_off.release();
+    x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release();
     if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
@@ -1219,6 +1222,30 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->ingested_bytes = t.ingested_bytes;
     out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
+    return EDGPU_OK;
+}
+
+int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
+    if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
+    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_arrivals needs serial ticks");
+    HIP_CHECK(hipSetDevice(x->device));
+    TickTotals t;
+    HIP_CHECK(sync_all(x));
+    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    if (t.status) return fail(t.status, "the last tick failed");
+    if (n < t.relayed_packets) return fail(EDGPU_OUT_OVERFLOW, "arrival array smaller than the tick's descriptors");
+    if (!t.relayed_packets) return EDGPU_OK;
+    int64_t* dst = out;
+    if (kind == EDGPU_PTR_HOST) {
+        HIP_CHECK(x->d_arrivals.reserve(t.relayed_packets, x->stream));
+        dst = x->d_arrivals.ptr;
+    }
+    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, (uint32_t)x->sub_sender.size(), dst, x->stream));
+    if (kind == EDGPU_PTR_HOST)
+        HIP_CHECK(hipMemcpyAsync(out, dst, (size_t)t.relayed_packets * sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
     return EDGPU_OK;
 }
 

@@ -553,6 +553,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
     if (q < P.T.nsubs) {
         SubDev& Q = P.subs[q];
         Q.nonempty = 0; Q.count = 0; Q.bytes = 0;
+        Q.was_new = Q.active && Q.bookmark < 0;
         if (Q.active) {
             SenderDev& D = P.senders[Q.sender];
             const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
@@ -723,7 +724,7 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         o.out_base = Q.out_base;
         o.out_bytes = Q.bytes;
         o.sender = Q.sender;
-        o.flags = (!Q.transport && !Q.rw) ? EDGPU_SUB_IDENTITY : 0u;
+        o.flags = ((!Q.transport && !Q.rw) ? EDGPU_SUB_IDENTITY : 0u) | (Q.was_new ? EDGPU_SUB_NEW : 0u);
         P.sub_out[q] = o;
         if (Q.count > 0) Q.sent_any = 1;
         const uint32_t pos = P.sub_pos[q];
@@ -1662,6 +1663,30 @@ hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, co
                                uint8_t* dst, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_arena_gather, dim3(n), dim3(256), 0, st, reinterpret_cast<const u32x4*>(arena), reg,
                               dst_off, reinterpret_cast<u32x4*>(dst));
+    return hipGetLastError();
+}
+
+// edgpu_fanout_arrivals: the arrival time of every descriptor of the last tick.  One wave per
+// sub-stream walks its range [a, head) of the sender's metadata ring; descriptor i is the i-th
+// non-empty packet from `a` (vcount - vcstart), exactly as k_fanout4 numbered them.
+__global__ __launch_bounds__(256) void k_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs,
+                                                      int64_t* out) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (q >= nsubs) return;
+    const SubDev& Q = subs[q];
+    if (!Q.active || !Q.nonempty || Q.count == 0) return;
+    const SenderDev& D = senders[Q.sender];
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    for (uint64_t p = Q.a + lane; p < D.head; p += 64) {
+        const PktMeta m = meta[p & D.pk_mask];
+        const uint32_t i = m.vcount - Q.vcstart;
+        if (m.len != 0 && i < Q.count) out[Q.desc_base + i] = m.arrival;
+    }
+}
+hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
+                               hipStream_t st) {
+    if (nsubs) hipLaunchKernelGGL(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, out);
     return hipGetLastError();
 }
 

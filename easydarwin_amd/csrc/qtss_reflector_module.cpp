@@ -95,12 +95,14 @@ bool GetPOD(QTSS_Object o, QTSS_AttributeID id, T* out) {
 QTSS_AttributeID sOutputAttr, sClientBroadcastSessionAttr, sRTSPBroadcastSessionAttr, sStreamCookieAttr,
     sRequestBodyAttr, sBufferOffsetAttr, sRTPInfoWaitTimeAttr;
 
+struct Output;
 struct Session {                        // a pushed stream ("<path>-<channel>", QRM:1384)
     std::string name;
     uint32_t engine = 0;                // edgpu session
     std::vector<uint32_t> trackIDs;     // a=control:trackID=N per m= line, SDP order
     std::vector<bool> setupToReceive;   // StreamInfo::fSetupToReceive
     std::string sdp;
+    std::vector<Output*> slots;         // the streams' bucket arrays: outputs in bucket order
 };
 
 struct Output {                         // one player (RTPSessionOutput)
@@ -111,6 +113,8 @@ struct Output {                         // one player (RTPSessionOutput)
     bool paused = false;
     uint32_t handle = 0;
     std::vector<QTSS_Object> streams;   // per track: the RTP stream object SETUP created (or null)
+    int32_t slot = -1;                  // position in the session's buckets (sBucketSize members each)
+    int64_t bufferDelayMs = 0;          // RTPSessionOutput::fBufferDelayMSecs
 };
 
 struct Module {
@@ -124,6 +128,9 @@ struct Module {
     std::vector<std::string> rtpInfoPlayers{"Android", "vlc"};  // player_requires_rtp_header_info
     int32_t rtpInfoWaitLoops = 10;      // sWaitTimeLoopCount: 100-ms PLAY retries before 404
     uint32_t tickMs = 20;
+    int64_t overBufferMs = 10000;       // ReflectorStream::sOverBufferInMsec (reflector_buffer_size_sec)
+    int64_t bucketDelayMs = 73;         // ReflectorStream::sBucketDelayInMsec
+    uint32_t bucketSize = 16;           // ReflectorStream::sBucketSize
     bool manualTick = false;
     std::thread ticker;
     std::atomic<bool> stop{false};
@@ -172,25 +179,52 @@ int TrackIndex(const Session& s, uint32_t trackID) {
 class QTSSSink : public edgpu_reflector::OutputSink {
 public:
     int64_t now = 0;
-    int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
-                    uint32_t wireLen, uint32_t) override {
-        auto it = M->byHandle.find(subscriber);
+    std::map<uint32_t, int32_t> firstNewSlot;      // per sender: bucket position of its first new output
+    bool WantsArrivals() const override { return true; }
+    // ReflectPackets sets `firstPacket` at the first output (in bucket order) without a bookmark
+    // and never clears it for the rest of that sender's outputs (ReflectorStream.cpp:1086-1104)
+    void BeginTick(const edgpu_substream_out* subs, uint32_t n) override {
+        firstNewSlot.clear();
+        for (uint32_t i = 0; i < n; i++) {
+            if (!(subs[i].flags & EDGPU_SUB_NEW)) continue;
+            auto it = M->byHandle.find(subs[i].subscriber);
+            if (it == M->byHandle.end() || it->second->slot < 0) continue;
+            auto f = firstNewSlot.find(subs[i].sender);
+            if (f == firstNewSlot.end() || it->second->slot < f->second) firstNewSlot[subs[i].sender] = it->second->slot;
+        }
+    }
+    int WritePacket(uint32_t, uint16_t, bool, bool, const uint8_t*, uint32_t, uint32_t) override {
+        return edgpu_reflector::kRequestFailed;                  // Write() below is the entry point
+    }
+    int Write(const edgpu_reflector::PacketWrite& w) override {
+        auto it = M->byHandle.find(w.subscriber);
         if (it == M->byHandle.end()) return edgpu_reflector::kNoErr;
         Output& o = *it->second;
         // not playing (paused): WritePacket returns QTSS_WouldBlock (RTPSessionOutput.cpp:575-579)
         if (o.paused) return edgpu_reflector::kWouldBlock;
-        if (track >= o.streams.size() || !o.streams[track]) return edgpu_reflector::kNoErr;   // track not SETUP
+        if (w.track >= o.streams.size() || !o.streams[w.track]) return edgpu_reflector::kNoErr;   // track not SETUP
         // the server frames interleaved packets itself (RTPStream::Write): hand it the packet
-        const uint8_t* pkt = interleaved ? wire + 4 : wire;
-        const uint32_t len = interleaved ? wireLen - 4 : wireLen;
+        const uint8_t* pkt = w.interleaved ? w.wire + 4 : w.wire;
+        const uint32_t len = w.interleaved ? w.wireLen - 4 : w.wireLen;
+        const auto f = firstNewSlot.find(w.sender);
+        const bool firstPacket = f != firstNewSlot.end() && o.slot >= f->second;
+        // the transmit time (RTPSessionOutput.cpp:603-608): now - bucket delay, moved to the
+        // packet's arrival + the output's buffer delay while that delay is positive
+        const int64_t bucketDelay = M->bucketDelayMs * (int64_t)(o.slot < 0 ? 0 : (uint32_t)o.slot / M->bucketSize);
         QTSS_PacketStruct ps;
         ps.packetData = const_cast<uint8_t*>(pkt);
-        ps.packetTransmitTime = now;
+        ps.packetTransmitTime = now - bucketDelay;
+        if (o.bufferDelayMs > 0) ps.packetTransmitTime += o.bufferDelayMs - (now - w.arrivalMs);
         ps.suggestedWakeupTime = -1;
-        const uint32_t flags = (isRTCP ? qtssWriteFlagsIsRTCP : qtssWriteFlagsIsRTP) | qtssWriteFlagsWriteBurstBegin;
-        const QTSS_Error err = cb(kWriteCallback, o.streams[track], (const void*)&ps, len, (uint32_t*)nullptr, flags);
-        // only QTSS_WouldBlock stops SendPacketsToOutput (ReflectorStream.cpp:1158-1190)
-        return err == QTSS_WouldBlock ? edgpu_reflector::kWouldBlock : edgpu_reflector::kNoErr;
+        const uint32_t flags = (w.isRTCP ? qtssWriteFlagsIsRTCP : qtssWriteFlagsIsRTP) | qtssWriteFlagsWriteBurstBegin;
+        const QTSS_Error err = cb(kWriteCallback, o.streams[w.track], (const void*)&ps, len, (uint32_t*)nullptr, flags);
+        // only QTSS_WouldBlock stops SendPacketsToOutput (ReflectorStream.cpp:1158-1190); blocked
+        // on a first-packet pass, the output's buffer delay becomes this packet's age (:617-622)
+        if (err == QTSS_WouldBlock) {
+            if (firstPacket) o.bufferDelayMs = now - w.arrivalMs;
+            return edgpu_reflector::kWouldBlock;
+        }
+        return edgpu_reflector::kNoErr;
     }
 };
 
@@ -234,6 +268,7 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
     edgpu_config cfg;
     edgpu_config_default(&cfg);
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
+    M->overBufferMs = (int64_t)cfg.reflector_buffer_size_sec * 1000;
     M->R.reset(new edgpu_reflector::Reflector(&cfg));
     if (M->R->Status() != 0) {
         fprintf(stderr, "QTSSReflectorModule: edgpu context: %s\n", edgpu_last_error());
@@ -435,6 +470,14 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
             o->handle = h;
             o->joined = true;
             M->byHandle[h] = o;
+            // ReflectorSession::AddOutput: the first free bucket member (ReflectorStream.cpp:281-336)
+            std::vector<Output*>& slots = M->sessions[o->session].slots;
+            size_t k = 0;
+            while (k < slots.size() && slots[k]) k++;
+            if (k == slots.size()) slots.push_back(nullptr);
+            slots[k] = o;
+            o->slot = (int32_t)k;
+            o->bufferDelayMs = M->overBufferMs;         // RTPSessionOutput(): fBufferDelayMSecs
         }
         g.unlock();
         const QTSS_Error e = cb(kPlayCallback, p->inClientSession, p->inRTSPRequest,
@@ -446,6 +489,7 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
 
 void RemoveOutputLocked(Output* o) {
     if (o->joined && M->R) (void)M->R->RemoveOutput(o->handle);
+    if (o->slot >= 0) M->sessions[o->session].slots[o->slot] = nullptr;
     M->byHandle.erase(o->handle);
     for (auto it = M->outputs.begin(); it != M->outputs.end(); ++it)
         if (it->get() == o) { M->outputs.erase(it); break; }

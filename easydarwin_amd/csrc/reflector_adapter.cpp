@@ -158,6 +158,12 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if ((err = edgpu_copy_to_host(fCtx, subs.data(), res.substreams, subs.size() * sizeof(subs[0])))) return err;
     if ((err = edgpu_copy_to_host(fCtx, d.data(), res.desc, d.size() * sizeof(d[0])))) return err;
     if ((err = edgpu_copy_to_host(fCtx, fArena.data(), res.arena, fArena.size()))) return err;
+    std::vector<int64_t> arrival;
+    if (sink->WantsArrivals()) {
+        arrival.resize(d.size());
+        if ((err = edgpu_fanout_arrivals(fCtx, arrival.data(), (uint32_t)arrival.size(), EDGPU_PTR_HOST))) return err;
+    }
+    sink->BeginTick(subs.data(), (uint32_t)subs.size());
     // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stops this
     // output's sub-stream for the tick; the engine then bookmarks the blocked packet
     std::vector<edgpu_blocked> blocked;
@@ -165,8 +171,18 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         const edgpu_substream_out& q = subs[s];
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = d[q.desc_base + i];
-            err = sink->WritePacket(q.subscriber, q.track, q.kind != 0, q.transport == EDGPU_TRANSPORT_TCP,
-                                    &fArena[o.offset], o.len, o.packet_id);
+            PacketWrite w;
+            w.subscriber = q.subscriber;
+            w.track = q.track;
+            w.isRTCP = q.kind != 0;
+            w.interleaved = q.transport == EDGPU_TRANSPORT_TCP;
+            w.wire = &fArena[o.offset];
+            w.wireLen = o.len;
+            w.packetID = o.packet_id;
+            w.arrivalMs = arrival.empty() ? -1 : arrival[q.desc_base + i];
+            w.sender = q.sender;
+            w.newOutput = (q.flags & EDGPU_SUB_NEW) != 0;
+            err = sink->Write(w);
             if (err == kWouldBlock) { blocked.push_back(edgpu_blocked{s, i}); break; }
             if (err) return err;
         }

@@ -41,11 +41,35 @@ enum { kNoErr = 0, kRequestFailed = -1, kBadArgument = -10, kWouldBlock = -14 };
 // subscriber (RTSPSessionInterface.cpp:329-344).  Return kNoErr to continue, kWouldBlock when
 // the socket is flow-controlled (EAGAIN): the rest of this sub-stream's packets are not
 // offered this tick and the next tick resumes at this packet, as SendPacketsToOutput does.
+// One write of a tick, with what RTPSessionOutput::WritePacket needs beyond the bytes to build
+// the QTSS_PacketStruct transmit time (RTPSessionOutput.cpp:603-608).
+struct PacketWrite {
+    uint32_t subscriber;
+    uint16_t track;
+    bool isRTCP, interleaved;
+    const uint8_t* wire;
+    uint32_t wireLen;
+    uint32_t packetID;
+    int64_t arrivalMs;              // the packet's fTimeArrived; -1 unless the sink WantsArrivals()
+    uint32_t sender;                // engine sender (the ReflectorSender this write comes from)
+    bool newOutput;                 // the output had no bookmark on this sender when the tick began
+};
+
 class OutputSink {
 public:
     virtual ~OutputSink() {}
     virtual int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved,
                             const uint8_t* wire, uint32_t wireLen, uint32_t packetID) = 0;
+    // Sinks that model the transmit time override these three: ReflectPackets then reads the
+    // tick's arrival times (edgpu_fanout_arrivals), shows the sink the whole sub-stream table
+    // first (the reference walks each sender's outputs in bucket order, so whether an earlier
+    // output was new decides `firstPacket` for the later ones, ReflectorStream.cpp:1086-1108),
+    // and calls Write for every packet.
+    virtual bool WantsArrivals() const { return false; }
+    virtual void BeginTick(const edgpu_substream_out* subs, uint32_t n) { (void)subs; (void)n; }
+    virtual int Write(const PacketWrite& w) {
+        return WritePacket(w.subscriber, w.track, w.isRTCP, w.interleaved, w.wire, w.wireLen, w.packetID);
+    }
     // A receiver report for a UDP pusher: send `rr` from the track's RTCP socket to
     // (addr, port), both in host order (ReflectorStream::SendReceiverReport's SendTo, whose
     // result the reference ignores).

@@ -34,7 +34,7 @@ EXPORTED = [
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
-    "edgpu_arena_gather", "edgpu_egress_disconnected",
+    "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -124,6 +124,7 @@ SUB_DTYPE = np.dtype([("subscriber", "<u4"), ("track", "<u2"), ("kind", "u1"), (
                       ("desc_base", "<u4"), ("desc_count", "<u4"), ("out_base", "<u8"),
                       ("out_bytes", "<u8"), ("sender", "<u4"), ("flags", "<u4")])
 SUB_IDENTITY = 1
+SUB_NEW = 2             # the output had no bookmark on this sender when the tick began
 TCP_READ_DTYPE = np.dtype([("session", "<u4"), ("len", "<u4"), ("offset", "<u8"), ("arrival_ms", "<i8")])
 TCP_RESULT_DTYPE = np.dtype([("frames", "<u4"), ("consumed", "<u4"), ("status", "<i4"), ("carry", "<u4")])
 UDP_SOURCE_DTYPE = np.dtype([("session", "<u4"), ("channel", "u1"), ("_pad", "u1"), ("port", "<u2"),
@@ -206,6 +207,7 @@ def load(path: str = LIB_PATH):
         "edgpu_host_free": (I32, [P, P]),
         "edgpu_arena_gather": (I32, [P, C.POINTER(FanoutResult), P, U32, P, U64]),
         "edgpu_egress_disconnected": (I32, [P, P, U32, C.POINTER(U32)]),
+        "edgpu_fanout_arrivals": (I32, [P, P, U32, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -473,6 +475,12 @@ class Context:
         if nbytes:
             _check(self.lib.edgpu_copy_to_host(self.h, _ptr(out), C.c_void_p(dev_ptr), int(nbytes)))
         return out
+
+    def fanout_arrivals(self, n: int) -> np.ndarray:
+        """Arrival time (ms) of each of the last tick's `n` descriptors (edgpu_fanout_arrivals)."""
+        out = np.zeros(max(int(n), 1), dtype=np.int64)
+        _check(self.lib.edgpu_fanout_arrivals(self.h, _ptr(out), out.size, PTR_HOST))
+        return out[:n]
 
     def read_tick(self, r: FanoutResult):
         """(stats, substream table, descriptors, arena) of the last fan-out, on the host."""

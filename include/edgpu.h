@@ -145,9 +145,14 @@ typedef struct edgpu_substream_out {
     uint32_t sender;        /* the engine sender (track x RTP|RTCP of a session) it relays */
     uint32_t flags;         /* EDGPU_SUB_IDENTITY: its bytes are the sender's packets unmodified
                                (UDP, no rewrite) -- two such sub-streams of one sender carry the
-                               same bytes, the shorter one a suffix of the longer */
+                               same bytes, the shorter one a suffix of the longer.
+                               EDGPU_SUB_NEW: the output had no bookmark on this sender when the
+                               tick began (GetBookMarkedPacket == NULL: ReflectPackets takes the
+                               new-output start and sets `firstPacket`, ReflectorStream.cpp:
+                               1097-1104) */
 } edgpu_substream_out;
 #define EDGPU_SUB_IDENTITY 1u
+#define EDGPU_SUB_NEW      2u
 
 /* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout (the second
  * next one with overlap_ticks). */
@@ -432,6 +437,15 @@ int  edgpu_egress_flush(edgpu_egress* eg, uint64_t* pending);
 int  edgpu_egress_disconnected(edgpu_egress* eg, uint32_t* out, uint32_t cap, uint32_t* n);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
+
+/* The arrival time (fTimeArrived, OS::Milliseconds() at PushPacket) of each descriptor of
+ * the last edgpu_fanout: out[i] for desc[i], i < the tick's relayed packets (serial ticks;
+ * call before the next edgpu_fanout).  RTPSessionOutput::WritePacket derives the
+ * QTSS_PacketStruct transmit time from it (RTPSessionOutput.cpp:604-608), which the server's
+ * RTPStream::Write hands to its thinning and over-buffer logic (RTPStream.cpp:1062,1119-1137).
+ * `out` is host memory (ptr_kind EDGPU_PTR_HOST) or device memory (EDGPU_PTR_DEVICE); `n`
+ * must be at least the tick's relayed packets. */
+int  edgpu_fanout_arrivals(edgpu_ctx* ctx, int64_t* out, uint32_t n, int ptr_kind);
 
 /* Packs regions of a fan-out arena (16-B aligned offsets and lengths; in the order given)
  * back to back into device memory `dst` on the context stream -- so a host egress can bring

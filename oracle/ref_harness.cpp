@@ -43,8 +43,17 @@
 // Usage: ref_harness <trace.edtr> <capture.edcp>
 //        ref_harness --bench <trace.edtr>    (memcpy sinks, no capture; prints the replay's
 //                                             relayed packets / bytes and seconds as JSON)
+//        ref_harness --bench-udp <trace.edtr> (the same, but every UDP subscriber write is a
+//                                             real sendto() to a loopback socket, one syscall
+//                                             per packet as RTPStream::Write's SendTo,
+//                                             RTPStream.cpp:1139-1145)
 // Trace / capture formats: see easydarwin_amd/trace.py (shared with the port oracle and
 // the GPU engine's replay driver).
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdarg>
@@ -116,6 +125,7 @@ struct FakeObj {
     std::string cap[2];          // [0] RTP writes, [1] RTCP writes (wire image)
     UInt64 npk[2] = {0, 0};
     SInt64 budget[2] = {-1, -1}; // writes the socket accepts this tick (-1: unlimited)
+    std::vector<SInt64> tt[2];   // QTSS_PacketStruct.packetTransmitTime of each accepted write
 };
 static std::vector<std::unique_ptr<FakeObj>> g_objs;
 static FakeObj* new_obj() { g_objs.emplace_back(new FakeObj()); return g_objs.back().get(); }
@@ -188,6 +198,8 @@ static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf
 static bool g_bench = false;
 static UInt64 g_bench_pkts = 0, g_bench_bytes = 0;
 static char g_scratch[70000];
+static int g_udp_fd = -1;                      // --bench-udp: the subscribers' UDP socket
+static sockaddr_in g_udp_dst;                  // an unread loopback socket (drops when full)
 static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* outLen, UInt32 flags, ...) {
     FakeObj* s = (FakeObj*)stream;
     const QTSS_PacketStruct* pkt = (const QTSS_PacketStruct*)buf;
@@ -197,7 +209,10 @@ static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* ou
     if (s->budget[k] > 0) s->budget[k]--;
     if (g_bench) {
         const UInt32 h = s->transport == qtssRTPTransportTypeTCP ? 4 : 0;
-        memcpy(g_scratch + h, pkt->packetData, len);
+        if (g_udp_fd >= 0 && h == 0)
+            (void)::sendto(g_udp_fd, pkt->packetData, len, 0, (const sockaddr*)&g_udp_dst, sizeof(g_udp_dst));
+        else
+            memcpy(g_scratch + h, pkt->packetData, len);
         g_bench_pkts++;
         g_bench_bytes += len + h;
         if (outLen) *outLen = len;
@@ -212,6 +227,7 @@ static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* ou
     c.push_back((char)(len & 0xff));
     c.append((const char*)pkt->packetData, len);
     s->npk[k]++;
+    s->tt[k].push_back(pkt->packetTransmitTime);
     if (outLen) *outLen = len;
     return QTSS_NoErr;
 }
@@ -238,14 +254,28 @@ struct Sub {
 
 int main(int argc, char** argv) {
     int reps = 1;
-    if (argc >= 3 && strcmp(argv[1], "--bench") == 0) {
+    const bool udp = argc >= 3 && strcmp(argv[1], "--bench-udp") == 0;
+    if (argc >= 3 && (strcmp(argv[1], "--bench") == 0 || udp)) {
         g_bench = true;
+        if (udp) {
+            const int rx = ::socket(AF_INET, SOCK_DGRAM, 0);
+            g_udp_fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+            memset(&g_udp_dst, 0, sizeof(g_udp_dst));
+            g_udp_dst.sin_family = AF_INET;
+            g_udp_dst.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+            socklen_t al = sizeof(g_udp_dst);
+            if (rx < 0 || g_udp_fd < 0 || ::bind(rx, (sockaddr*)&g_udp_dst, sizeof(g_udp_dst)) != 0 ||
+                ::getsockname(rx, (sockaddr*)&g_udp_dst, &al) != 0) {
+                perror("udp sink");
+                return 2;
+            }
+        }
         argv[1] = argv[2];
         if (argc == 4) reps = atoi(argv[3]);
         argc = 3;
     }
     if (argc != 3 || reps < 1) {
-        fprintf(stderr, "usage: %s trace.edtr capture.edcp | --bench trace.edtr [repeat]\n", argv[0]);
+        fprintf(stderr, "usage: %s trace.edtr capture.edcp | --bench[-udp] trace.edtr [repeat]\n", argv[0]);
         return 2;
     }
     FILE* f = fopen(argv[1], "rb");
@@ -517,6 +547,24 @@ int main(int argc, char** argv) {
         }
     }
     fclose(o);
+    // EDGPU_TT_OUT=<path>: the transmit time RTPSessionOutput::WritePacket put in every accepted
+    // write's QTSS_PacketStruct (RTPSessionOutput.cpp:603-608; the input of the server's
+    // thinning, RTPStream::UpdateQualityLevel, and over-buffer window), in capture order:
+    // "EDTT" u32 records, per record u32 n + n x i64
+    if (const char* ttp = getenv("EDGPU_TT_OUT")) {
+        FILE* t = fopen(ttp, "wb");
+        if (!t) { perror(ttp); return 2; }
+        fwrite("EDTT", 1, 4, t);
+        fwrite(&nrec, 4, 1, t);
+        for (auto& sb : subs)
+            for (FakeObj* st : sb.streams)
+                for (int k = 0; k < 2; k++) {
+                    const UInt32 n = (UInt32)st->tt[k].size();
+                    fwrite(&n, 4, 1, t);
+                    fwrite(st->tt[k].data(), 8, n, t);
+                }
+        fclose(t);
+    }
     fprintf(stderr, "ref_harness: %zu subs, %lu asserts logged\n", subs.size(), logger.count);
     return 0;
 }

@@ -6,8 +6,10 @@ For every scenario in tests/scenarios.py:
      read-only reference sources, oracle/_ref/Makefile) -> capture;
   3. replay it through oracle/relay_model (the clean-room restatement) -> capture, and
      require byte equality with (2);
-  4. commit <name>.json = {trace sha256, per sub-stream [packets, bytes, sha256]} and, for the
-     small scenarios, the trace and the reference capture themselves (<name>.edtr/.edcp).
+  4. commit <name>.json = {trace sha256, per sub-stream [packets, bytes, sha256], sha256 of the
+     QTSS_PacketStruct transmit times RTPSessionOutput::WritePacket gave every accepted write
+     (EDGPU_TT_OUT, pinned for the QTSS module drop-in)} and, for the small scenarios, the
+     trace and the reference capture themselves (<name>.edtr/.edcp).
 
 Run here (needs /root/reference):  python tests/golden/make_golden.py
 The fixtures are data only (inputs + expected outputs); nothing here is reference source.
@@ -44,7 +46,9 @@ def main():
             with open(tpath, "wb") as f:
                 f.write(trace)
             rc, pc = tpath + ".ref", tpath + ".port"
-            subprocess.run([ref, tpath, rc], check=True, stderr=subprocess.DEVNULL)
+            tt = tpath + ".edtt"
+            subprocess.run([ref, tpath, rc], check=True, stderr=subprocess.DEVNULL,
+                           env=dict(os.environ, EDGPU_TT_OUT=tt))
             subprocess.run([port, tpath, pc], check=True)
             rb, pb = open(rc, "rb").read(), open(pc, "rb").read()
             if rb != pb:
@@ -58,6 +62,7 @@ def main():
                 "generator": "tests/scenarios.py:%s (numpy PCG64, seed base 0xEA5D)" % name,
                 "source": "oracle/_ref/ref_harness (EasyDarwin reference reflector)",
                 "substreams": capture_summary(cap),
+                "transmit_sha256": hashlib.sha256(open(tt, "rb").read()).hexdigest(),
             }
             rr = read_source_reports(rb)
             if rr:                       # receiver reports to UDP pushers (EDRR trailer)

@@ -7,7 +7,11 @@ RTSPIncomingData for every pushed '$' frame, SETUP + PLAY for every player (UA "
 RTP-Info player), ClientSessionClosing for a leave -- with a virtual clock and manual reflect
 ticks.  The module's QTSS_Write calls on the players' RTP stream objects, framed as
 RTPStream::Write frames them, must reproduce the REFERENCE reflector's per-subscriber capture
-byte for byte (the golden fixtures, tests/golden/*.json).  Scenarios with UDP pushers are not
+byte for byte (the golden fixtures, tests/golden/*.json), and the QTSS_PacketStruct transmit
+time of every write must be the one the reference's RTPSessionOutput::WritePacket computed
+(RTPSessionOutput.cpp:603-622: bucket delay, buffer delay, its reset on a blocked first-packet
+pass) -- the input of the server's own thinning and over-buffer logic under QTSS_Write
+(RTPStream.cpp:936-1045, 1119-1137; Q20).  Scenarios with UDP pushers are not
 replayed here (the module serves RTSP-interleaved pushers, qtss_reflector_module.cpp).
 """
 import hashlib
@@ -27,8 +31,10 @@ TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "an
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", TCP_PUSH)
 def test_module_matches_reference(name, tmp_path):
-    t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
     t.write_bytes(_trace(name).to_bytes())
-    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
     assert r.returncode == 0, r.stderr[-2000:]
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]
+    assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]

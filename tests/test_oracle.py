@@ -59,8 +59,14 @@ def test_port_matches_golden_digests(name, oracle_bins, tmp_path):
 def test_reference_harness_reproduces_fixture(name, oracle_bins, tmp_path):
     if oracle_bins["ref"] is None:
         pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")
-    cap = _run(oracle_bins["ref"], SCENARIOS[name]().to_bytes(), tmp_path, name)
+    tt = tmp_path / f"{name}.edtt"
+    os.environ["EDGPU_TT_OUT"] = str(tt)
+    try:
+        cap = _run(oracle_bins["ref"], SCENARIOS[name]().to_bytes(), tmp_path, name)
+    finally:
+        del os.environ["EDGPU_TT_OUT"]
     assert hashlib.sha256(cap).hexdigest() == _fix(name)["capture_sha256"]
+    assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fix(name)["transmit_sha256"]
 
 
 def test_key_pointer_skips_sps_pps_on_join():
@@ -114,3 +120,19 @@ def test_udppush_reports_pin_reference_quirks():
     b = by[(5100, 0, 0)][2]
     assert b[:4] == bytes.fromhex("80c90001") and b[16:24] == b"\x01\x05QTSS0\x00"
     assert len(b) == 16 + 36 + 12
+
+
+def test_reference_bench_modes_relay_the_same_packets(oracle_bins, tmp_path):
+    """bench.py's CPU baselines: --bench (memcpy sinks) and --bench-udp (one sendto() per
+    subscriber packet to loopback) replay the same trace and relay the same packets."""
+    if oracle_bins["ref"] is None:
+        pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")
+    t = tmp_path / "mixed.edtr"
+    t.write_bytes(SCENARIOS["mixed"]().to_bytes())
+    out = {}
+    for mode in ("--bench", "--bench-udp"):
+        r = subprocess.run([oracle_bins["ref"], mode, str(t), "2"], check=True, capture_output=True, text=True)
+        out[mode] = json.loads(r.stdout)
+    assert out["--bench"]["relayed_packets"] > 0
+    for k in ("relayed_packets", "relayed_bytes", "repeat"):
+        assert out["--bench"][k] == out["--bench-udp"][k]

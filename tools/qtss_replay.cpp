@@ -53,6 +53,7 @@ struct Obj {
     uint8_t channel[2] = {0, 1};
     std::string cap[2];
     uint64_t npk[2] = {0, 0};
+    std::vector<int64_t> tt[2];                 // packetTransmitTime of each accepted write
     int64_t budget[2] = {-1, -1};
     // RTSP request objects: the body QTSS_Read returns
     std::string body;
@@ -130,6 +131,7 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
     c.push_back((char)(len & 0xFF));
     c.append((const char*)ps->packetData, len);
     o->npk[k]++;
+    o->tt[k].push_back(ps->packetTransmitTime);
     g_writes++;
     if (outLen) *outLen = len;
     return QTSS_NoErr;
@@ -388,6 +390,20 @@ int main(int argc, char** argv) {
             fwrite(s->cap[k].data(), 1, nb, o);
         }
     fclose(o);
+    // EDGPU_TT_OUT=<path>: the transmit times in capture order, the reference harness's format
+    if (const char* ttp = getenv("EDGPU_TT_OUT")) {
+        FILE* t = fopen(ttp, "wb");
+        if (!t) { perror(ttp); return 2; }
+        fwrite("EDTT", 1, 4, t);
+        fwrite(&n, 4, 1, t);
+        for (Obj* s : st)
+            for (int k = 0; k < 2; k++) {
+                const uint32_t m = (uint32_t)s->tt[k].size();
+                fwrite(&m, 4, 1, t);
+                fwrite(s->tt[k].data(), 8, m, t);
+            }
+        fclose(t);
+    }
     fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes\n", players.size(), (unsigned long long)g_writes);
     return 0;
 }
