@@ -241,6 +241,7 @@ struct edgpu_ctx {
     FirstInfoResult* d_fpi_r = nullptr;
     FirstInfoQuery* h_fpi_q = nullptr;          // pinned
     FirstInfoResult* h_fpi_r = nullptr;         // pinned
+    uint8_t* h_stage = nullptr;                 // pinned bounce buffer of Readback (kStageBytes)
     DevVec<edgpu_blocked> d_blocked;
     DevVec<edgpu_region> d_gather_reg;          // edgpu_arena_gather
     DevVec<int64_t> d_arrivals;                 // edgpu_fanout_arrivals
@@ -348,6 +349,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
     if (x->h_fpi_r) (void)hipHostFree(x->h_fpi_r);
+    if (x->h_stage) (void)hipHostFree(x->h_stage);
     if (x->d_tcp_src) (void)hipFree(x->d_tcp_src);
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
@@ -378,6 +380,43 @@ static hipError_t sync_all(edgpu_ctx* x) {
     if (e == hipSuccess && x->copy) e = hipStreamSynchronize(x->copy);
     return e;
 }
+
+// Device -> host reads.  Every read of the engine is enqueued on the context stream after the
+// work that produces it and completes at one hipStreamSynchronize before the host looks at the
+// destination.  Reads that fit go through a pinned bounce buffer, so no small read (a totals
+// record, a sender header, per-read reports) is a pageable async copy into the caller's or the
+// stack's memory; larger ones (GOP bytes, whole ticks) copy straight into the destination, which
+// HIP completes through its own staging before the synchronize returns.
+static constexpr size_t kStageBytes = 64 << 10;
+struct Readback {
+    edgpu_ctx* x;
+    struct Item { void* dst; size_t off, bytes; };
+    std::vector<Item> staged;
+    size_t used = 0;
+    explicit Readback(edgpu_ctx* c) : x(c) {}
+    hipError_t add(void* dst, const void* src, size_t bytes) {
+        if (!bytes) return hipSuccess;
+        if (!x->h_stage) {
+            hipError_t e = hipHostMalloc((void**)&x->h_stage, kStageBytes, hipHostMallocDefault);
+            if (e != hipSuccess) { x->h_stage = nullptr; return e; }
+        }
+        if (bytes <= kStageBytes - used) {
+            staged.push_back({dst, used, bytes});
+            hipError_t e = hipMemcpyAsync(x->h_stage + used, src, bytes, hipMemcpyDeviceToHost, x->stream);
+            used += (bytes + 15) & ~size_t(15);
+            return e;
+        }
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream);
+    }
+    hipError_t run() {
+        hipError_t e = hipStreamSynchronize(x->stream);
+        if (e != hipSuccess) return e;
+        for (const Item& it : staged) memcpy(it.dst, x->h_stage + it.off, it.bytes);
+        staged.clear();
+        used = 0;
+        return hipSuccess;
+    }
+};
 
 int edgpu_sync(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
@@ -586,7 +625,9 @@ static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms
     if (getenv("EDGPU_DEBUG_PLAY")) {                    // debugging: the PLAY's inputs and results
         for (uint32_t t = 0; t < sh.ntracks; t++) {
             SenderDev d[2];
-            HIP_CHECK(hipMemcpy(d, x->d_senders.ptr + q[t].rtp_sender, 2 * sizeof(SenderDev), hipMemcpyDeviceToHost));
+            Readback rb(x);
+            HIP_CHECK(rb.add(d, x->d_senders.ptr + q[t].rtp_sender, 2 * sizeof(SenderDev)));
+            HIP_CHECK(rb.run());
             fprintf(stderr, "play now=%lld track=%u cutoff=%lld head=%llu/%llu found=%u seq=%u\n", (long long)now_ms, t,
                     (long long)q[t].cutoff, (unsigned long long)d[0].head, (unsigned long long)d[1].head, r[t].found,
                     r[t].seq);
@@ -1072,9 +1113,10 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p);
     if (r) return r;
     TcpTotals tot;
-    HIP_CHECK(hipMemcpyAsync(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipMemcpyAsync(&tot, x->d_tcp_tot, sizeof(tot), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    HIP_CHECK(rb.add(&tot, x->d_tcp_tot, sizeof(tot)));
+    HIP_CHECK(rb.add(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result)));
+    HIP_CHECK(rb.run());
     if (tot.status) {
         x->pending = false;                 // the ingest ran over empty segments
         return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets");
@@ -1213,8 +1255,11 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
     HIP_CHECK(sync_all(x));
-    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
+        HIP_CHECK(rb.run());
+    }
     out->relayed_packets = t.relayed_packets;
     out->relayed_bytes = t.relayed_bytes;
     out->arena_bytes = t.arena_bytes;
@@ -1232,8 +1277,11 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
     HIP_CHECK(sync_all(x));
-    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
+        HIP_CHECK(rb.run());
+    }
     if (t.status) return fail(t.status, "the last tick failed");
     if (n < t.relayed_packets) return fail(EDGPU_OUT_OVERFLOW, "arrival array smaller than the tick's descriptors");
     if (!t.relayed_packets) return EDGPU_OK;
@@ -1243,9 +1291,9 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
         dst = x->d_arrivals.ptr;
     }
     HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, (uint32_t)x->sub_sender.size(), dst, x->stream));
-    if (kind == EDGPU_PTR_HOST)
-        HIP_CHECK(hipMemcpyAsync(out, dst, (size_t)t.relayed_packets * sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    if (kind == EDGPU_PTR_HOST) HIP_CHECK(rb.add(out, dst, (size_t)t.relayed_packets * sizeof(int64_t)));
+    HIP_CHECK(rb.run());
     return EDGPU_OK;
 }
 
@@ -1278,8 +1326,11 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
     HIP_CHECK(sync_all(x));
-    HIP_CHECK(hipMemcpyAsync(&t, x->d_totals, sizeof(t), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
+        HIP_CHECK(rb.run());
+    }
     out->relayed_packets = t.cum_relayed_packets;
     out->relayed_bytes = t.cum_relayed_bytes;
     out->fanout_in_bytes = t.cum_fanout_in_bytes;
@@ -1312,8 +1363,9 @@ int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes)
     if (!bytes) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
     HIP_CHECK(sync_all(x));
-    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    HIP_CHECK(rb.add(dst, src, bytes));
+    HIP_CHECK(rb.run());
     return EDGPU_OK;
 }
 
@@ -1343,15 +1395,14 @@ int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out
         return fail(EDGPU_BAD_ARGUMENT, "bad session/track");
     HIP_CHECK(hipSetDevice(x->device));
     SenderDev D;
-    HIP_CHECK(hipMemcpyAsync(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D),
-                             hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    HIP_CHECK(rb.add(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D)));
+    HIP_CHECK(rb.run());
     uint64_t pk = 0, by = 0;
     if (D.key >= 0) {
         PktMeta m;
-        HIP_CHECK(hipMemcpyAsync(&m, reinterpret_cast<PktMeta*>(D.meta) + ((uint64_t)D.key & D.pk_mask), sizeof(m),
-                                 hipMemcpyDeviceToHost, x->stream));
-        HIP_CHECK(hipStreamSynchronize(x->stream));
+        HIP_CHECK(rb.add(&m, reinterpret_cast<PktMeta*>(D.meta) + ((uint64_t)D.key & D.pk_mask), sizeof(m)));
+        HIP_CHECK(rb.run());
         pk = D.head - (uint64_t)D.key;
         by = D.vbyte_end - m.vbyte;
     }
@@ -1366,9 +1417,9 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
         return fail(EDGPU_BAD_ARGUMENT, "bad argument");
     HIP_CHECK(hipSetDevice(x->device));
     SenderDev D;
-    HIP_CHECK(hipMemcpyAsync(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D),
-                             hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    HIP_CHECK(rb.add(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D)));
+    HIP_CHECK(rb.run());
     if (out_len) *out_len = 0;
     if (out_packets) *out_packets = 0;
     if (D.key < 0 || (uint64_t)D.key >= D.head) return EDGPU_OK;
@@ -1379,20 +1430,20 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
     const PktMeta* dmeta = reinterpret_cast<const PktMeta*>(D.meta);
     for (uint64_t i = 0; i < n;) {            // ring segments
         const uint64_t pos = (k + i) & D.pk_mask, run = std::min(n - i, pkcap - pos);
-        HIP_CHECK(hipMemcpyAsync(&meta[i], dmeta + pos, run * sizeof(PktMeta), hipMemcpyDeviceToHost, x->stream));
+        HIP_CHECK(rb.add(&meta[i], dmeta + pos, run * sizeof(PktMeta)));
         i += run;
     }
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(rb.run());
     const uint64_t vb0 = meta[0].vbyte, span = D.vbyte_end - vb0;
     if (span > bcap) return fail(EDGPU_RING_OVERFLOW, "GOP no longer in the byte ring");
     std::vector<uint8_t> bytes(span);
     const uint8_t* ring = reinterpret_cast<const uint8_t*>(D.ring);
     for (uint64_t i = 0; i < span;) {
         const uint64_t pos = (vb0 + i) & (bcap - 1), run = std::min(span - i, bcap - pos);
-        HIP_CHECK(hipMemcpyAsync(&bytes[i], ring + pos, run, hipMemcpyDeviceToHost, x->stream));
+        HIP_CHECK(rb.add(&bytes[i], ring + pos, run));
         i += run;
     }
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(rb.run());
     uint64_t len = 0; uint32_t np = 0;
     for (uint64_t i = 0; i < n; i++) {
         if (meta[i].len == 0) continue;
@@ -1427,10 +1478,10 @@ static int image_launch(edgpu_ctx* x, std::vector<ImgPlan>& plan, int64_t now_ms
     p.buf = buf; p.status = x->d_img_status;
     HIP_CHECK(launch_image(p, phase, x->stream));
     int status = 0;
-    if (phase == 0)
-        HIP_CHECK(hipMemcpyAsync(plan.data(), x->d_img_plan.ptr, plan.size() * sizeof(ImgPlan), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipMemcpyAsync(&status, x->d_img_status, sizeof(int), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    Readback rb(x);
+    HIP_CHECK(rb.add(&status, x->d_img_status, sizeof(int)));
+    if (phase == 0) HIP_CHECK(rb.add(plan.data(), x->d_img_plan.ptr, plan.size() * sizeof(ImgPlan)));
+    HIP_CHECK(rb.run());
     if (status) return fail(status, phase == 2 ? "session image rejected by the replica" : "session image export");
     return EDGPU_OK;
 }

@@ -92,3 +92,15 @@ def test_build_batch_layout():
         off = int(d["slot"]) * 16 + 4
         assert blob[off:off + len(data)].tobytes() == data
     assert np.all(desc["slot"][1:] > desc["slot"][:-1])
+
+
+def test_engine_reads_back_only_through_readback():
+    """every device->host copy of the engine goes through Readback (pinned
+    bounce buffer for small reads, one stream synchronize before the host reads the
+    destination) or the pinned RTP-Info staging -- no bare async copy into caller / stack memory."""
+    src = open(os.path.join(ROOT, "easydarwin_amd", "csrc", "edgpu_engine.cpp")).read()
+    body = src[src.index("struct Readback {"):]
+    body = body[body.index("\n};\n") + 4:]                 # everything after the helper
+    lines = [ln for ln in body.splitlines() if "DeviceToHost" in ln]
+    assert lines == ["    HIP_CHECK(hipMemcpyAsync(x->h_fpi_r, x->d_fpi_r, q.size() * sizeof(FirstInfoResult), "
+                     "hipMemcpyDeviceToHost, x->stream));"], lines
