@@ -606,9 +606,9 @@ static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms
         q[t].rtcp_sender = sh.udp_push ? 0xFFFFFFFFu : sh.first_sender + 2 * t + 1;
         q[t].cutoff = now_ms - window;                  // age <= window  <=>  arrival >= cutoff
     }
-    // Persistent device buffers and pinned host staging (kMaxTracks entries).  Per-call
-    // hipMallocAsync buffers were recycled from the previous PLAY and the result copy could
-    // return that PLAY's results (observed on gfx950 / ROCm 7.2), so they are not used here.
+    // Persistent device buffers and pinned host staging (kMaxTracks entries).  Round 1 took
+    // per-call buffers from the stream-ordered pool: the query copy into a recycled block was
+    // sometimes lost and the kernel answered the previous PLAY's query.
     if (!x->d_fpi_q) {
         if (dmalloc(&x->d_fpi_q, kMaxTracks * sizeof(FirstInfoQuery)) != hipSuccess ||
             dmalloc(&x->d_fpi_r, kMaxTracks * sizeof(FirstInfoResult)) != hipSuccess ||

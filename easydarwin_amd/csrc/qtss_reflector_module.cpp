@@ -268,7 +268,8 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
     edgpu_config cfg;
     edgpu_config_default(&cfg);
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
-    M->overBufferMs = (int64_t)cfg.reflector_buffer_size_sec * 1000;
+    // 0 selects the engine's default of 1 s (edgpu_config.reflector_buffer_size_sec)
+    M->overBufferMs = (int64_t)(cfg.reflector_buffer_size_sec ? cfg.reflector_buffer_size_sec : 1) * 1000;
     M->R.reset(new edgpu_reflector::Reflector(&cfg));
     if (M->R->Status() != 0) {
         fprintf(stderr, "QTSSReflectorModule: edgpu context: %s\n", edgpu_last_error());

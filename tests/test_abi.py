@@ -104,3 +104,13 @@ def test_engine_reads_back_only_through_readback():
     lines = [ln for ln in body.splitlines() if "DeviceToHost" in ln]
     assert lines == ["    HIP_CHECK(hipMemcpyAsync(x->h_fpi_r, x->d_fpi_r, q.size() * sizeof(FirstInfoResult), "
                      "hipMemcpyDeviceToHost, x->stream));"], lines
+
+
+def test_no_stream_ordered_pool_allocations():
+    """host->device copies into recycled hipMallocAsync blocks were lost on this
+    stack, so the engine allocates nothing from the stream-ordered pool."""
+    csrc = os.path.join(ROOT, "easydarwin_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".cpp", ".hip", ".h")):
+            src = open(os.path.join(csrc, f)).read()
+            assert "hipMallocAsync" not in src and "hipFreeAsync" not in src, f

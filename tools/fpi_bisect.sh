@@ -17,7 +17,9 @@ for v in ${VARIANTS:-A B C}; do
   for k in $(seq 1 ${RUNS:-20}); do
     timeout -k 5 60 ./$v/tools/adapter_replay rtpinfo.edtr /tmp/bisect_$v.edcp > /dev/null 2> /tmp/bisect_$v.log || { echo "{\"variant\": \"$v\", \"error\": $?}"; exit 1; }
     got=$(sha256sum /tmp/bisect_$v.edcp | cut -d' ' -f1)
-    [ "$got" = "$want" ] || { bad=$((bad+1)); cp /tmp/bisect_$v.edcp ../../gpurun_out/bisect/${v}_$k.edcp; cp /tmp/bisect_$v.log ../../gpurun_out/bisect/${v}_$k.log; }
+    [ "$got" = "$want" ] || { bad=$((bad+1)); cp /tmp/bisect_$v.log ../../gpurun_out/bisect/${v}_$k.log;
+                              [ $bad = 1 ] && cp /tmp/bisect_$v.edcp ../../gpurun_out/bisect/${v}_first.edcp; }
+    [ "$got" = "$want" ] && [ $k = 1 ] && cp /tmp/bisect_$v.log ../../gpurun_out/bisect/${v}_good.log
   done
   echo "{\"variant\": \"$v\", \"runs\": ${RUNS:-20}, \"mismatches\": $bad}"
 done
