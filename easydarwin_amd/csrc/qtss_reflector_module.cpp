@@ -198,11 +198,17 @@ public:
     }
     int Write(const edgpu_reflector::PacketWrite& w) override {
         auto it = M->byHandle.find(w.subscriber);
-        if (it == M->byHandle.end()) return edgpu_reflector::kNoErr;
+        if (it == M->byHandle.end()) {
+            if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: write for unknown handle %u\n", w.subscriber);
+            return edgpu_reflector::kNoErr;
+        }
         Output& o = *it->second;
         // not playing (paused): WritePacket returns QTSS_WouldBlock (RTPSessionOutput.cpp:575-579)
         if (o.paused) return edgpu_reflector::kWouldBlock;
-        if (w.track >= o.streams.size() || !o.streams[w.track]) return edgpu_reflector::kNoErr;   // track not SETUP
+        if (w.track >= o.streams.size() || !o.streams[w.track]) {                               // track not SETUP
+            if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: handle %u track %u not set up\n", w.subscriber, w.track);
+            return edgpu_reflector::kNoErr;
+        }
         // the server frames interleaved packets itself (RTPStream::Write): hand it the packet
         const uint8_t* pkt = w.interleaved ? w.wire + 4 : w.wire;
         const uint32_t len = w.interleaved ? w.wireLen - 4 : w.wireLen;
@@ -445,6 +451,9 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
                 flags = qtssPlayRespWriteTrackInfo;
                 std::vector<edgpu_rtp_info> info;
                 err = M->R->PlayRTPInfo(M->sessions[o->session].engine, tcp, Milliseconds(), &h, &info);
+                if (getenv("EDGPU_QTSS_DEBUG"))
+                    fprintf(stderr, "QTSSReflectorModule: RTP-Info PLAY session=%u now=%lld err=%d %s\n", o->session,
+                            (long long)Milliseconds(), err, err ? edgpu_last_error() : "");
                 if (err == edgpu_reflector::kWouldBlock) {
                     // nothing buffered yet: retry the PLAY from the idle timer, then give up (QRM:1985-2003)
                     int32_t loops = 0;
@@ -478,6 +487,8 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
             if (k == slots.size()) slots.push_back(nullptr);
             slots[k] = o;
             o->slot = (int32_t)k;
+            if (getenv("EDGPU_QTSS_DEBUG"))
+                fprintf(stderr, "QTSSReflectorModule: output joined session=%u handle=%u slot=%zu tcp=%d\n", o->session, h, k, (int)tcp);
             o->bufferDelayMs = M->overBufferMs;         // RTPSessionOutput(): fBufferDelayMSecs
         }
         g.unlock();
@@ -489,9 +500,11 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
 }
 
 void RemoveOutputLocked(Output* o) {
-    if (o->joined && M->R) (void)M->R->RemoveOutput(o->handle);
+    if (o->joined) {                    // an output whose PLAY never succeeded has no handle
+        if (M->R) (void)M->R->RemoveOutput(o->handle);
+        M->byHandle.erase(o->handle);
+    }
     if (o->slot >= 0) M->sessions[o->session].slots[o->slot] = nullptr;
-    M->byHandle.erase(o->handle);
     for (auto it = M->outputs.begin(); it != M->outputs.end(); ++it)
         if (it->get() == o) { M->outputs.erase(it); break; }
 }

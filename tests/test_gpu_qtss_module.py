@@ -38,3 +38,22 @@ def test_module_matches_reference(name, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["leave", "udppush"])
+def test_module_matches_reference_for_interleaved_pushers(name, tmp_path):
+    """Scenarios that mix UDP and RTSP-interleaved pushers: the module serves the interleaved
+    ones (UDP-push SETUPs are refused and their players skipped), so every sub-stream of a
+    player of an interleaved push session must equal the reference's -- for `leave`, players
+    leaving mid-tick, while blocked, and leave + rejoin in one tick."""
+    from easydarwin_amd.trace import JOIN, capture_summary, read_capture
+    tr = _trace(name)
+    t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    t.write_bytes(tr.to_bytes())
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    tcp_subs = {ev[3] for ev in tr.events if ev[0] == JOIN and not tr.udp_push(ev[2])}
+    want = {k: v for k, v in _fixture(name)["substreams"].items() if int(k.split("/")[0]) in tcp_subs}
+    got = capture_summary(read_capture(c.read_bytes()))
+    assert want and got == want
