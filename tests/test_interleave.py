@@ -188,3 +188,37 @@ def test_replay_pusher_model_delivers_every_packet(name):
         assert got == want
     assert calls >= sum(1 for b in batches if b)    # more when keep-alives were answered
     assert not any(ctx.carry.values())
+
+
+@pytest.mark.parametrize("name", ["tiny", "nal", "clamp", "ssrc"])
+def test_interleaved_output_parses_back_through_reference_reader(name, tmp_path):
+    """The subscriber-side '$' ch BE16(len) framing of every RTSP-interleaved sub-stream in the
+    committed reference captures (the engine reproduces them byte for byte) is read back by the
+    reference's own RTSPRequestStream (oracle/_ref/ref_deframe): the same packets, in order, on
+    the channel RTPStream assigns (2 * track + RTCP, RTPStream.cpp:472-473).  The capture's
+    framing is the harness's restatement of RTSPSessionInterface::InterleavedWrite
+    (RTSPSessionInterface.cpp:329-344), whose class needs the server singleton to construct;
+    this pins it against compiled reference code from the other side of the wire."""
+    if not os.path.exists(REF):
+        pytest.skip("oracle/_ref/ref_deframe not built (reference tree absent)")
+    from easydarwin_amd.trace import read_capture, split_wire_image
+    gold_dir = os.path.dirname(GOLD)
+    cap = read_capture(open(os.path.join(gold_dir, name + ".edcp"), "rb").read())
+    rng = random.Random(name)
+    checked = 0
+    for (sub, track, kind), v in cap.items():
+        if not v.tcp or not v.data:
+            continue
+        pkts = split_wire_image(v.data, 1)
+        fits = []
+        for p in pkts:                       # the reader's 2047-byte request buffer (QTSS.h:47)
+            if len(p) + 4 > 2047:
+                break
+            fits.append(p)
+        data = v.data[:sum(len(p) + 4 for p in fits)]
+        reads = _split(rng, data, 1, 3000, zero=0.0)
+        ev = _ref(reads, tmp_path)
+        got = [(ch, b) for k, _r, ch, _a, b in ev if k == FRAME]
+        assert got == [(2 * track + kind, p) for p in fits], (sub, track, kind)
+        checked += len(fits)
+    assert checked > 0
