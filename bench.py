@@ -263,7 +263,7 @@ def cpu_baseline(args) -> dict | None:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)   # C2: a 10-s window of 1-s batches
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sessions", type=int, default=1024, help="sessions per GPU")
     ap.add_argument("--subs", type=int, default=16, help="UDP subscribers per session")

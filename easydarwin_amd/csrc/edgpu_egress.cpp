@@ -35,6 +35,7 @@
 #include <vector>
 
 #include <netinet/in.h>
+#include <netinet/udp.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -55,8 +56,13 @@ struct TcpConn {
     bool reported = false;
 };
 
+#ifndef UDP_SEGMENT
+#define UDP_SEGMENT 103
+#endif
+
 struct Worker {
     int udp_fd = -1;
+    bool gso = true;                    // UDP generic segmentation offload still usable
     std::vector<edgpu_blocked> blocked;
     uint64_t udp_datagrams = 0, udp_bytes = 0, udp_dropped = 0, tcp_frames = 0, tcp_bytes = 0;
 };
@@ -67,6 +73,7 @@ struct edgpu_egress {
     edgpu_ctx* ctx = nullptr;
     uint32_t nthreads = 1;
     bool dedup = true;
+    bool gso = true;                    // EDGPU_EGRESS_GSO=0: one datagram per message
     std::map<uint64_t, UdpDest> udp;    // (subscriber << 16 | track)
     std::map<uint32_t, TcpConn> tcp;    // subscriber
     uint8_t* h_arena = nullptr;         // pinned: the tick's bytes (whole arena, or the gathered regions)
@@ -90,22 +97,28 @@ static int eg_fail(edgpu_egress* e, int code, const std::string& m) {
 
 // One UDP sub-stream: every datagram is offered to the socket once (errors ignored, like the
 // reference's (void)SendTo); EAGAIN / ENOBUFS drop the datagram.
-static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d) {
-    const int k = s.kind ? 1 : 0;
-    const uint8_t* base = e->base[q] - s.out_base;
-    const int fd = d.fd[k] >= 0 ? d.fd[k] : w.udp_fd;
-    const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
+//
+// With UDP GSO (UDP_SEGMENT, Linux >= 4.18) a run of datagrams of one length L to the
+// sub-stream's destination -- FU-A fragments of one frame all have the same size -- goes down as
+// ONE message whose kernel-side segmentation puts exactly the same datagrams on the wire, one
+// per L bytes (the last may be shorter); up to 64 per message and 64 KiB.  The datagrams stay
+// where they are in the pinned tick (one iovec each).  What changes is only failure
+// granularity: a full socket drops a whole message instead of one datagram.  A message the
+// route refuses (EINVAL, e.g. a smaller MTU) is resent one datagram at a time; a socket without
+// GSO (EIO / EOPNOTSUPP) turns it off for that worker.  Datagrams over 1472 B go one per message.
+static void send_udp_plain(Worker& w, int fd, const sockaddr_in* to, const uint8_t* base, const edgpu_out_desc* ds,
+                           uint32_t count) {
     constexpr uint32_t kBatch = 256;
     mmsghdr msgs[kBatch];
     iovec iov[kBatch];
     uint32_t i = 0;
-    while (i < s.desc_count) {
-        const uint32_t n = std::min(kBatch, s.desc_count - i);
+    while (i < count) {
+        const uint32_t n = std::min(kBatch, count - i);
         for (uint32_t j = 0; j < n; j++) {
             iov[j].iov_base = const_cast<uint8_t*>(base + ds[i + j].offset);
             iov[j].iov_len = ds[i + j].len;
             memset(&msgs[j].msg_hdr, 0, sizeof(msgs[j].msg_hdr));
-            msgs[j].msg_hdr.msg_name = const_cast<sockaddr_in*>(&d.addr[k]);
+            msgs[j].msg_hdr.msg_name = const_cast<sockaddr_in*>(to);
             msgs[j].msg_hdr.msg_namelen = sizeof(sockaddr_in);
             msgs[j].msg_hdr.msg_iov = &iov[j];
             msgs[j].msg_hdr.msg_iovlen = 1;
@@ -124,6 +137,81 @@ static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
             }
         }
         i += n;
+    }
+}
+
+static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d) {
+    const int k = s.kind ? 1 : 0;
+    const uint8_t* base = e->base[q] - s.out_base;
+    const int fd = d.fd[k] >= 0 ? d.fd[k] : w.udp_fd;
+    const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
+    if (!e->gso || !w.gso) { send_udp_plain(w, fd, &d.addr[k], base, ds, s.desc_count); return; }
+    constexpr uint32_t kMsgs = 64, kSegs = 64, kMaxPayload = 65507, kMaxSeg = 1472;
+    struct Msg { uint32_t first, n, seg; };
+    mmsghdr msgs[kMsgs];
+    Msg mi[kMsgs];
+    iovec iov[kMsgs * kSegs];
+    alignas(cmsghdr) char ctl[kMsgs][CMSG_SPACE(sizeof(uint16_t))];
+    uint32_t i = 0;
+    while (i < s.desc_count) {
+        // build up to kMsgs messages: runs of equal-length datagrams (+ one shorter tail)
+        uint32_t nm = 0, niov = 0;
+        while (nm < kMsgs && i < s.desc_count) {
+            const uint32_t L = ds[i].len;
+            // a segment must fit the path MTU: only datagrams that fit a 1500-B Ethernet frame
+            const uint32_t cap = (L && L <= kMaxSeg) ? std::min(kSegs, kMaxPayload / L) : 1;
+            uint32_t n = 1;
+            while (n < cap && i + n < s.desc_count && ds[i + n].len == L) n++;
+            if (n < cap && i + n < s.desc_count && ds[i + n].len < L && ds[i + n].len > 0) n++;   // shorter last segment
+            Msg& m = mi[nm];
+            m.first = i; m.n = n; m.seg = L;
+            mmsghdr& h = msgs[nm];
+            memset(&h.msg_hdr, 0, sizeof(h.msg_hdr));
+            h.msg_hdr.msg_name = const_cast<sockaddr_in*>(&d.addr[k]);
+            h.msg_hdr.msg_namelen = sizeof(sockaddr_in);
+            h.msg_hdr.msg_iov = &iov[niov];
+            h.msg_hdr.msg_iovlen = n;
+            for (uint32_t j = 0; j < n; j++) {
+                iov[niov + j].iov_base = const_cast<uint8_t*>(base + ds[i + j].offset);
+                iov[niov + j].iov_len = ds[i + j].len;
+            }
+            if (n > 1) {
+                h.msg_hdr.msg_control = ctl[nm];
+                h.msg_hdr.msg_controllen = CMSG_SPACE(sizeof(uint16_t));
+                cmsghdr* c = CMSG_FIRSTHDR(&h.msg_hdr);
+                c->cmsg_level = SOL_UDP;
+                c->cmsg_type = UDP_SEGMENT;
+                c->cmsg_len = CMSG_LEN(sizeof(uint16_t));
+                const uint16_t seg = (uint16_t)L;
+                memcpy(CMSG_DATA(c), &seg, sizeof(seg));
+            }
+            niov += n;
+            i += n;
+            nm++;
+        }
+        uint32_t done = 0;
+        while (done < nm) {
+            const int r = sendmmsg(fd, msgs + done, nm - done, MSG_DONTWAIT);
+            if (r > 0) {
+                for (int j = 0; j < r; j++) {
+                    const Msg& m = mi[done + j];
+                    for (uint32_t t = 0; t < m.n; t++) w.udp_bytes += ds[m.first + t].len;
+                    w.udp_datagrams += m.n;
+                }
+                done += (uint32_t)r;
+                continue;
+            }
+            if (r < 0 && errno == EINTR) continue;
+            const Msg& m = mi[done];
+            if (r < 0 && (errno == EIO || errno == EINVAL || errno == EOPNOTSUPP) && m.n > 1) {
+                if (errno != EINVAL) w.gso = false;       // no GSO on this socket at all
+                send_udp_plain(w, fd, &d.addr[k], base, ds + m.first, m.n);   // resend this one plainly
+            } else {
+                w.udp_dropped += m.n;                     // a full socket: the message is lost
+            }
+            done++;
+        }
+        if (!w.gso && i < s.desc_count) { send_udp_plain(w, fd, &d.addr[k], base, ds + i, s.desc_count - i); return; }
     }
 }
 
@@ -197,6 +285,7 @@ int edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out) {
     e->ctx = ctx;
     e->nthreads = std::max(1u, std::min(threads, 64u));
     if (const char* v = getenv("EDGPU_EGRESS_DEDUP")) e->dedup = atoi(v) != 0;
+    if (const char* v = getenv("EDGPU_EGRESS_GSO")) e->gso = atoi(v) != 0;
     e->workers.resize(e->nthreads);
     for (Worker& w : e->workers) {
         w.udp_fd = socket(AF_INET, SOCK_DGRAM, 0);

@@ -42,8 +42,12 @@ def main():
     ap.add_argument("--dedup", type=int, default=1,
                     help="1: copy each tick's distinct bytes once (identity UDP sub-streams share their "
                          "sender's region); 0: copy the whole write-many arena (round 1)")
+    ap.add_argument("--gso", type=int, default=1,
+                    help="1: runs of equal-length datagrams to one subscriber leave as one UDP GSO message; "
+                         "0: one datagram per message")
     args = ap.parse_args()
     os.environ["EDGPU_EGRESS_DEDUP"] = str(args.dedup)     # read by edgpu_egress_create
+    os.environ["EDGPU_EGRESS_GSO"] = str(args.gso)
     dev = torch.device("cuda", 0)
     fleet = H264Fleet(np.arange(args.sessions), tick_ms=args.tick_ms)
     gen = torch.Generator(device=dev)
@@ -89,6 +93,7 @@ def main():
         "workload": f"C2 stream set ({args.sessions} x 4 Mb/s H.264 1080p30) x {args.subs} UDP subs, "
                     f"{args.tick_ms}-ms ticks, egress over loopback UDP with {args.threads} threads",
         "dedup": args.dedup,
+        "gso": args.gso,
         "per_tick_mean": {k: round(v, 3) for k, v in tot.items()},
         "egress_datagrams_per_s": round(tot["datagrams"] / (tot["copy_ms"] + tot["send_ms"]) * 1e3, 1),
         "egress_GBps": round(tot["bytes"] / (tot["copy_ms"] + tot["send_ms"]) / 1e6, 3),
