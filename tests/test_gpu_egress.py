@@ -80,13 +80,17 @@ def test_tcp_backpressure_over_sockets(name, oracle_bins, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dedup", ["0", "1"])
-def test_egress_copy_modes_match_reference(dedup, monkeypatch):
+@pytest.mark.parametrize("dedup,gso", [("0", "1"), ("1", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("name", ["udppush", "c1", "mixed"])
+def test_egress_copy_modes_match_reference(name, dedup, gso, monkeypatch):
     """EDGPU_EGRESS_DEDUP=1 (default) brings one region per identity sender over PCIe
-    (edgpu_arena_gather) instead of the whole write-many arena: same bytes on the wire."""
+    (edgpu_arena_gather) instead of the whole write-many arena; EDGPU_EGRESS_GSO=1 (default)
+    sends runs of equal-length datagrams as UDP GSO messages: the same datagrams on the wire
+    in every combination."""
     monkeypatch.setenv("EDGPU_EGRESS_DEDUP", dedup)
-    cap, _ = replay(SCENARIOS["udppush"](), sockets={"threads": 2})
-    assert hashlib.sha256(cap).hexdigest() == _fixture("udppush")["capture_sha256"]
+    monkeypatch.setenv("EDGPU_EGRESS_GSO", gso)
+    cap, _ = replay(SCENARIOS[name](), sockets={"threads": 2})
+    assert hashlib.sha256(cap).hexdigest() == _fixture(name)["capture_sha256"]
 
 
 @pytest.mark.gpu
