@@ -31,6 +31,7 @@
 // through edgpu_udp_sources from a host socket reader, as the C++ adapter's ProcessUDPPacket
 // does); RTSPRoute / RTSPAuthorize / Easy_GetDeviceStream (redirects, access files, the CMS
 // control plane) are not registered.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -549,7 +550,8 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     if (!p->inPacketData || p->inPacketLen < 4) return QTSS_NoErr;
     const uint8_t* d = (const uint8_t*)p->inPacketData;
     const uint8_t channel = d[1];
-    const uint32_t len = (uint32_t)d[2] << 8 | d[3];
+    // the frame's own length, as the reference reads it; never past the buffer the server gave
+    const uint32_t len = std::min<uint32_t>((uint32_t)d[2] << 8 | d[3], p->inPacketLen - 4);
     std::lock_guard<std::mutex> g(M->mu);
     if (!M->R || sid > M->sessions.size()) return QTSS_NoErr;
     const Session& s = M->sessions[sid - 1];
