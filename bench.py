@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from easydarwin_amd import edgpu  # noqa: E402
 from easydarwin_amd.dist import reduce_run  # noqa: E402
-from easydarwin_amd.workload import H264Fleet, shard_sessions  # noqa: E402
+from easydarwin_amd.workload import H264Fleet, owned_sessions  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 
@@ -305,7 +305,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    gids = shard_sessions(args.sessions * world, rank, world) if world > 1 else np.arange(args.sessions)
+    # every rank owns exactly args.sessions streams of the hash-sharded population (weak scaling)
+    gids = owned_sessions(args.sessions, rank, world) if world > 1 else np.arange(args.sessions)
     fleet = H264Fleet(gids, tick_ms=args.tick_ms)
     steps, warm = args.steps, args.warmup
     log(f"[bench] rank {rank}/{world}: {len(gids)} sessions x {args.subs} subs, generating {steps + warm} batches")

@@ -9,7 +9,8 @@ arrive at their frame time; one batch = one tick interval (default 1 s).
 Only the RTP/FU headers are synthesised on the host; payload bytes are filled on the GPU
 (they are never inspected by the relay, only moved).  Session ids are global so that a
 multi-GPU run shards one workload: rank r owns the sessions whose FNV-1a-64 stream-ID hash
-is r mod N.
+is r mod N; the benchmark's population (owned_sessions) gives every rank the
+same number of them.
 """
 from __future__ import annotations
 
@@ -38,6 +39,19 @@ def stream_id(g: int) -> str:
 
 def shard_sessions(n_global: int, rank: int, world: int) -> np.ndarray:
     return np.array([g for g in range(n_global) if fnv1a64(stream_id(g)) % world == rank], dtype=np.int64)
+
+
+def owned_sessions(per_rank: int, rank: int, world: int) -> np.ndarray:
+    """The first `per_rank` stream IDs (in ID order) whose FNV-1a hash owner is `rank`: a global
+    population of world x per_rank streams in which every GPU owns exactly per_rank, so a weak-
+    scaling run keeps the per-GPU work fixed while streams still shard by hash.  For world = 1
+    this is range(per_rank)."""
+    out, g = [], 0
+    while len(out) < per_rank:
+        if fnv1a64(stream_id(g)) % world == rank:
+            out.append(g)
+        g += 1
+    return np.array(out, dtype=np.int64)
 
 
 class H264Fleet:

@@ -96,3 +96,16 @@ def test_two_rank_output_invariance(oracle_bins):
     assert elapsed == 2.0                       # max over ranks
     assert counts[1] == 2                        # sum over ranks
     assert counts[0] == sum(v[0] for v in single.values())
+
+
+def test_owned_sessions_balance_a_hash_sharded_population():
+    """bench.py's weak-scaling population: every rank owns exactly `per_rank` stream IDs, each
+    owned by its FNV-1a hash, none twice; one GPU gets range(per_rank)."""
+    from easydarwin_amd.workload import fnv1a64, owned_sessions, stream_id
+    for world in (1, 2, 8):
+        parts = [owned_sessions(256, r, world) for r in range(world)]
+        assert all(len(p) == 256 for p in parts)
+        assert len(set().union(*[set(p.tolist()) for p in parts])) == 256 * world
+        for r, p in enumerate(parts):
+            assert all(fnv1a64(stream_id(int(g))) % world == r for g in p)
+    assert owned_sessions(64, 0, 1).tolist() == list(range(64))

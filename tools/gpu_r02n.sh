@@ -1,0 +1,8 @@
+# round 2, run n: full GPU suite (GSO egress, module fixes)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02n
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1; rc=$?
+echo "gpu tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/gputest.log | tail -15
+exit $rc
