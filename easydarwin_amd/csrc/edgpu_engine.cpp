@@ -140,6 +140,8 @@ struct edgpu_ctx {
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
     uint32_t ablate = 0;
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
+    uint32_t tcp_copy = 2;          // EDGPU_INGEST_TCP: 2 DPP neighbour word, two frames per wave round;
+                                    // 1 one frame per round; 0 two loads per word
     hipStream_t stream = nullptr;
     // tick pipelining (edgpu_config.overlap_ticks): the fan-out copy kernel runs on `copy`,
     // ordered after its plan by ev_plan; the next plan waits for ev_copy
@@ -327,6 +329,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
+    if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 2);
     *out = x;
     return EDGPU_OK;
 }
@@ -905,7 +908,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode;
+    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;

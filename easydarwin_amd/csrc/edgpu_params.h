@@ -21,6 +21,9 @@ struct IngestParams {
     CopyJob* jobs;          // per desc: slot copy for k_ingest_copy
     uint32_t npk;           // descriptors in the batch
     uint32_t copy_mode;     // 0: copy inside k_ingest, 1: k_ingest_copy (EDGPU_INGEST)
+    uint32_t tcp_copy;      // frames in the TCP byte stream: 1 one aligned load per word + the
+                            // neighbour word by DPP, 2 the same with two frames per wave round
+                            // (default); 0 two aligned loads per word (EDGPU_INGEST_TCP)
     uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7)
     uint32_t filter_ssrc;
     uint32_t ssrc_timeout_s;
