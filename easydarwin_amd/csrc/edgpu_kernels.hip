@@ -1163,7 +1163,8 @@ typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 // are in flight.  All are buffer loads (vector-memory counter only; a flat load would also hold
 // the LDS counter that the store loop waits on).
 template <int THREADS, int NL, int LAUX = 0>
-__device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r)[NL], u32x3& ma, u32x2& mb) {
+__device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r)[NL], u32x3& ma, u32x2& mb,
+                                           bool skip_words = false) {
     const uint32_t wmask = it.wmask, nw = it.nw;
     const uint32_t rstart = (uint32_t)(it.vb0 >> 4) & wmask;
     const bool wraps = rstart + nw > wmask + 1;
@@ -1172,7 +1173,7 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 #pragma unroll
     for (int j = 0; j < NL; j++) {
         const uint32_t wi = tid + j * THREADS;
-        if ((uint32_t)(j * THREADS) < nw)              // uniform: no load past the chunk's lines
+        if ((uint32_t)(j * THREADS) < nw && !skip_words)   // uniform: no load past the chunk's lines
             r[j] = __builtin_amdgcn_raw_buffer_load_b128(
                 rs, wraps ? (wi < nw ? ((rstart + wi) & wmask) * 16u : 0xFFFFFFFFu) : wi * 16u, 0, LAUX);
     }
@@ -1224,7 +1225,7 @@ void k_fanout4(FanoutParams P) {
     FanWork nx;
     if (w < nwork) {
         nx = const_load(P.work + w);
-        fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb);
+        fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
     }
     for (uint32_t par = 0; w < nwork; w += gridDim.x, par ^= 1u) {
         const FanWork it = nx;
@@ -1256,7 +1257,7 @@ void k_fanout4(FanoutParams P) {
         const uint32_t wn = w + gridDim.x;
         if (wn < nwork) {
             nx = const_load(P.work + wn);
-            fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb);
+            fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
         }
         // ---- write the chunk to every sub-stream of the sender ----------------------------
         for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
