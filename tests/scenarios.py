@@ -452,3 +452,59 @@ SCENARIOS = {
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
     "backpressure": backpressure, "udppush": udppush, "leave": leave,
 }
+
+
+def random_scenario(seed: int) -> Trace:
+    """A random mix of everything above, for differential tests on fresh inputs (the oracle
+    pins itself on the fixtures; these traces are not committed): 1-3 sessions, each an
+    RTSP-interleaved or a UDP push of H.264 / MPEG-4 / MJPEG video and/or AAC / G.711 audio,
+    pusher SRs, jittered sizes; UDP, TCP and RTP-Info players joining at random times; random
+    leaves; random socket budgets (BLOCK) on TCP and UDP sub-streams; ticks every 50-200 ms.
+    Kept inside the parity scope of DESIGN.md §4.4 (no lag past the 10-s retention)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 1000 + seed))
+    vids = ["H264/90000", "H264/90000", "MP4V-ES/90000", "JPEG/90000"]
+    auds = [("MPEG4-GENERIC/48000/2", 97), ("PCMA/8000", 8), ("PCMU/8000", 0)]
+    dur = int(rng.integers(2000, 6001))
+    tick = int(rng.choice([50, 100, 100, 200]))
+    tr = Trace()
+    per, joins, leaves, blocks = [], [], [], {}
+    sub = 1
+    nsess = int(rng.integers(1, 4))
+    for s in range(nsess):
+        tracks = []
+        kinds = int(rng.integers(0, 3))                 # 0 video, 1 audio, 2 both
+        if kinds != 1:
+            tracks.append(TrackSpec("video", str(rng.choice(vids)), 96, bitrate=int(rng.integers(200_000, 1_500_000)),
+                                    gop=int(rng.choice([15, 30, 60])), idr_bytes=int(rng.integers(3_000, 20_000)),
+                                    jitter_sizes=bool(rng.random() < 0.3),
+                                    rtcp_every_ms=int(rng.choice([0, 0, 400, 900]))))
+        if kinds != 0:
+            name, pt = auds[int(rng.integers(0, 3))]
+            tracks.append(TrackSpec("audio", name, pt, jitter_sizes=bool(rng.random() < 0.2),
+                                    rtcp_every_ms=int(rng.choice([0, 0, 1000]))))
+        udp = bool(rng.random() < 0.3)
+        tr.add_session(make_sdp(tracks), udp_push=udp)
+        t0 = int(rng.integers(0, 400))
+        pk = session_packets(tracks, dur, SEED_BASE + 2000 + seed * 8 + s, t0=t0)
+        if udp:
+            src = _ip(10, 1, int(rng.integers(0, 256)), int(rng.integers(1, 255)))
+            port = 6000 + 2 * int(rng.integers(0, 100))
+            pk = [(t, ch, data, src, port + (ch & 1)) for t, ch, data in pk]
+        per.append(pk)
+        for _ in range(int(rng.integers(1, 6))):
+            t = int(rng.integers(0, dur - 200)) if rng.random() < 0.7 else 0
+            transport = TCP if rng.random() < 0.5 else UDP
+            ua = VLC if rng.random() < 0.25 else 0
+            joins.append((t, s, sub, transport, ua))
+            if rng.random() < 0.3:
+                leaves.append((int(rng.integers(t, dur)), sub))
+            ntr = len(tracks)
+            for _b in range(int(rng.integers(0, 4))):
+                bt = (int(rng.integers(t, dur)) // tick) * tick
+                for k in range(int(rng.integers(1, 6))):
+                    tt = bt + k * tick
+                    if tt <= dur:
+                        blocks.setdefault(tt, []).append((sub, int(rng.integers(0, ntr)), int(rng.integers(0, 2)),
+                                                          int(rng.integers(0, 5))))
+            sub += 1
+    return _assemble(tr, per, tick, dur, joins, blocks=blocks, leaves=leaves)

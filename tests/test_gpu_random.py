@@ -1,0 +1,68 @@
+"""GPU: differential parity on fresh random traces (tests/scenarios.py random_scenario: random
+sessions, codecs, UDP / interleaved pushers, UDP / TCP / RTP-Info players, leaves and socket
+budgets).  The oracle is the clean-room restatement, which test_random_parity.py pins to the
+real reference on the same seeds; where the prebuilt reference harness travelled with the
+tree it is run too (the QTSS module's transmit times).  Every path the golden scenarios take
+is taken here: the C ABI replay, the same with the pushers' packets sent RTSP-interleaved
+through the GPU deframer, the C++ adapter, and the QTSS module in the fake server."""
+import os
+import subprocess
+
+import pytest
+
+from easydarwin_amd.replay import replay
+from easydarwin_amd.trace import PKT, UPKT
+from scenarios import random_scenario
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ADAPTER = os.path.join(ROOT, "tools", "adapter_replay")
+MODULE = os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so")
+QREPLAY = os.path.join(ROOT, "tools", "qtss_replay")
+SEEDS = range(24)
+
+
+def _oracle(binary, trace_bytes, tmp_path, tag, env=None):
+    t, c = tmp_path / f"{tag}.edtr", tmp_path / f"{tag}.edcp"
+    t.write_bytes(trace_bytes)
+    subprocess.run([binary, str(t), str(c)], check=True, stderr=subprocess.DEVNULL,
+                   env=dict(os.environ, **(env or {})))
+    return c.read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_engine_paths_match_oracle_on_random_traces(seed, oracle_bins, tmp_path):
+    tr = random_scenario(seed)
+    tb = tr.to_bytes()
+    want = _oracle(oracle_bins["port"], tb, tmp_path, "port")
+    cap, _ = replay(tr)
+    assert cap == want, "C ABI replay"
+    if all(len(ev[4]) <= 2043 for ev in tr.events if ev[0] == PKT):
+        cap, _ = replay(tr, interleaved=1 + seed % 2)
+        assert cap == want, "interleaved push"
+    t, c = tmp_path / "a.edtr", tmp_path / "a.edcp"
+    t.write_bytes(tb)
+    subprocess.run([ADAPTER, str(t), str(c)], check=True, timeout=120)
+    assert c.read_bytes() == want, "C++ adapter"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_module_matches_reference_on_random_traces(seed, oracle_bins, tmp_path):
+    """Traces whose pushers are all RTSP-interleaved, through the QTSS module: the capture, and
+    (with the reference harness at hand) every write's transmit time."""
+    tr = random_scenario(seed)
+    if any(ev[0] == UPKT for ev in tr.events) or any(tr.udp_push(s) for s in range(len(tr.sdps))):
+        pytest.skip("UDP pushers: not served by the module")
+    tb = tr.to_bytes()
+    want = _oracle(oracle_bins["port"], tb, tmp_path, "port")
+    t, c, tt = tmp_path / "m.edtr", tmp_path / "m.edcp", tmp_path / "m.edtt"
+    t.write_bytes(tb)
+    r = subprocess.run([QREPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert c.read_bytes() == want
+    if oracle_bins["ref"] is not None:
+        rtt = tmp_path / "r.edtt"
+        _oracle(oracle_bins["ref"], tb, tmp_path, "ref", env={"EDGPU_TT_OUT": str(rtt)})
+        assert tt.read_bytes() == rtt.read_bytes()
