@@ -280,7 +280,9 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         __syncthreads();
         // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
-        if (P.copy_mode == 0 && P.src_addr && P.tcp_copy >= 1) {   // frames inside the TCP byte stream
+        if (P.ablate & 32u) {
+            // timing ablation only: no slot copy
+        } else if (P.copy_mode == 0 && P.src_addr && P.tcp_copy >= 1) {   // frames inside the TCP byte stream
             // The frame's bytes [sp, lim) are misaligned by sh = sp & 15.  Each lane loads ONE
             // aligned block (blocks holding a byte of the frame only); slot word w is blocks w
             // and w + 1 funnelled by sh, and block w + 1 comes from the next lane by DPP (lane

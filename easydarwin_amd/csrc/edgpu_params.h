@@ -24,7 +24,8 @@ struct IngestParams {
     uint32_t tcp_copy;      // frames in the TCP byte stream: 1 one aligned load per word + the
                             // neighbour word by DPP, 2 the same with two frames per wave round
                             // (default); 0 two aligned loads per word (EDGPU_INGEST_TCP)
-    uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7)
+    uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7: 16 no totals, 32 no slot
+                            // copy, 64 no per-sender scans)
     uint32_t filter_ssrc;
     uint32_t ssrc_timeout_s;
     uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
