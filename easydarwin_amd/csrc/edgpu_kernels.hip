@@ -1150,10 +1150,14 @@ __device__ __forceinline__ uint64_t row_mask(const uint32_t* sm, int c0, int nw3
     return (lo >> sh) | (sh ? hi << (64 - sh) : 0ull);
 }
 
-template <int THREADS, int CHUNK>
+// LFS: FanSub records staged in LDS per work item (up to kLfs), so the store loop's per-window
+// record read is an LDS broadcast instead of a scalar load that can miss the scalar cache
+constexpr int kLfs = 64;
+template <int THREADS, int CHUNK, int LFS = 0>
 constexpr int fanout4_lds() {
     return CHUNK * kSlotWordsMax * 16 + (CHUNK + 2) * 8 + 4 * CHUNK * 4 +
-           2 * ((((CHUNK * kSlotWordsMax + 31) / 32) + 3) & ~3) * 4 + (THREADS / 64) * 8;
+           2 * ((((CHUNK * kSlotWordsMax + 31) / 32) + 3) & ~3) * 4 + (THREADS / 64) * 8 +
+           (LFS ? kLfs * (int)sizeof(FanSub) : 0);
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1194,7 +1198,8 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 // workgroups per CU, i.e. <= 64 VGPRs); 0 leaves it to the compiler.
 // PM: how the store loop finds slot starts for the per-output patch: 0 one bitmap bit per lane
 // (LDS read per word), 1 one wave-uniform 64-bit mask per wave row (row_mask).
-template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0>
+template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0,
+          int LFS = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1216,6 +1221,24 @@ void k_fanout4(FanoutParams P) {
     uint32_t* m_nzp = m_vc + CHUNK;                                    // non-empty ordinal -> packet
     uint32_t* smap = m_nzp + CHUNK;                                    // 2 x SM, by item parity
     unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smap + 2 * SM);
+    uint32_t* s_fs = reinterpret_cast<uint32_t*>(s_red + NWAVES);       // LFS: kLfs FanSub records
+    constexpr uint32_t kFsw = sizeof(FanSub) / 4;                      // dwords per record
+    static_assert(!LFS || kLfs * kFsw <= (uint32_t)THREADS, "one staged dword per lane");
+    // the item's FanSub q as SGPRs: from the LDS copy (LFS) or a scalar load
+    auto fansub = [&](const FanWork& w, uint32_t q) -> FanSub {
+        if constexpr (LFS) {
+            if (q - w.qb < (uint32_t)kLfs) {
+                FanSub f;
+                uint32_t* d = reinterpret_cast<uint32_t*>(&f);
+                const uint32_t* src = s_fs + (q - w.qb) * kFsw;
+#pragma unroll
+                for (uint32_t i = 0; i < kFsw; i++) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)src[i]);
+                return f;
+            }
+        }
+        return const_load(P.fansub + q);
+    };
+    uint32_t fsw = 0;                                                  // LFS: this lane's staged dword
     u32x4* out = reinterpret_cast<u32x4*>(P.arena);
     unsigned long long wire = 0, inb = 0;
 
@@ -1228,6 +1251,10 @@ void k_fanout4(FanoutParams P) {
     if (w < nwork) {
         nx = const_load(P.work + w);
         fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
+        if constexpr (LFS) {
+            const uint32_t nq = min(nx.qe - nx.qb, (uint32_t)kLfs);
+            if ((uint32_t)tid < nq * kFsw) fsw = reinterpret_cast<const uint32_t*>(P.fansub + nx.qb)[tid];
+        }
     }
     for (uint32_t par = 0; w < nwork; w += gridDim.x, par ^= 1u) {
         const FanWork it = nx;
@@ -1252,6 +1279,9 @@ void k_fanout4(FanoutParams P) {
             }
         }
         if (tid == 0) m_vb[np] = vb0 + (uint64_t)nw * 16;
+        if constexpr (LFS) {
+            if ((uint32_t)tid < min(it.qe - it.qb, (uint32_t)kLfs) * kFsw) s_fs[tid] = fsw;
+        }
         __syncthreads();
         // ---- the other parity's bitmap is free now: clear it for the next item ----------
         for (int k = tid; k < SM; k += THREADS) smap[(par ^ 1u) * SM + k] = 0;
@@ -1260,10 +1290,14 @@ void k_fanout4(FanoutParams P) {
         if (wn < nwork) {
             nx = const_load(P.work + wn);
             fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
+            if constexpr (LFS) {
+                const uint32_t nq = min(nx.qe - nx.qb, (uint32_t)kLfs);
+                if ((uint32_t)tid < nq * kFsw) fsw = reinterpret_cast<const uint32_t*>(P.fansub + nx.qb)[tid];
+            }
         }
         // ---- write the chunk to every sub-stream of the sender ----------------------------
         for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
-            const FanSub f = const_load(P.fansub + q);
+            const FanSub f = fansub(it, q);
             if (f.a >= lo + np) continue;
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
             const uint32_t fw = uni((uint32_t)((m_vb[p0] - vb0) >> 4));
@@ -1302,7 +1336,7 @@ void k_fanout4(FanoutParams P) {
         {
             const uint32_t nzc = np ? m_vc[np - 1] - vc0 + (m_len[np - 1] != 0) : 0u;
             for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
-                const FanSub f = const_load(P.fansub + q);
+                const FanSub f = fansub(it, q);
                 if (f.a >= lo + np) continue;
                 const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
                 const uint32_t o0 = m_vc[p0] - vc0;                            // first ordinal
@@ -1831,6 +1865,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 8>, 1024, 32, fanout4_lds<1024, 32>()}, // 26 32, <= 64 VGPRs
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 27 row-mask patch
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 28 56, row-mask
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32, 1>()}, // 29 LDS FanSub
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 1>, 1024, 56, fanout4_lds<1024, 56, 1>()}, // 30 56, LDS FanSub
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1842,7 +1878,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,36,nt>", "k_fanout4<1024,48,nt>", "k_fanout4<1024,56,nt>",
                                             "k_fanout4<1024,56,nt,su4>", "k_fanout4<1024,56,nt,su2>",
                                             "k_fanout4<1024,32,nt,su2>", "k_fanout4<1024,32,nt,wpe8>",
-                                            "k_fanout4<1024,32,nt,rowmask>", "k_fanout4<1024,56,nt,rowmask>"};
+                                            "k_fanout4<1024,32,nt,rowmask>", "k_fanout4<1024,56,nt,rowmask>",
+                                            "k_fanout4<1024,32,nt,ldsfansub>", "k_fanout4<1024,56,nt,ldsfansub>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
