@@ -84,8 +84,9 @@ __device__ __forceinline__ uint32_t packet_ssrc(const uint8_t* p, uint32_t len, 
     return be32(p + 8);
 }
 
-// 256-thread exclusive scan (4 waves of 64).  `scratch` holds 4 entries.
-template <typename T>
+// Exclusive scan over a workgroup of NW waves of 64 (256 threads by default).  `scratch` holds
+// NW entries.
+template <typename T, int NW = 4>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T x = v;
@@ -98,7 +99,7 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     __syncthreads();
     T base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
+    for (int w = 0; w < NW; w++) {
         T t = scratch[w];
         if (w < wid) base += t;
         tot += t;
@@ -114,8 +115,11 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
 
 // DEPTH: packets per wave per slot-copy round; 4 by default (125 VGPRs, still 4 waves/SIMD),
 // EDGPU_INGEST_DEPTH=2 for A/B runs
-template <uint32_t DEPTH>
-__global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
+// THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
+// for A/B: one round for a C2 session's ~375 packets per tick)
+template <uint32_t DEPTH, int THREADS = kIngestThreads>
+__global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
+    constexpr int NW = THREADS / 64;
     const uint32_t seg = blockIdx.x;
     const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
     const SessionDev S = P.sessions[P.seg_sess[seg]];
@@ -132,16 +136,16 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __shared__ uint32_t c_ttot[kMaxTracks];
     __shared__ int c_last[kMaxSendersPerSession];   // (tid << 10 | rank) of the chunk's newest non-empty packet
     // per packet of the current chunk
-    __shared__ uint8_t p_snd[kIngestThreads];
-    __shared__ uint8_t p_acc[kIngestThreads];
-    __shared__ uint16_t p_len[kIngestThreads];
-    __shared__ uint32_t p_ssrc[kIngestThreads];
-    __shared__ int64_t p_ts[kIngestThreads];
-    __shared__ uint64_t p_src[kIngestThreads];     // slot / frame start address
-    __shared__ uint32_t p_slotb[kIngestThreads];
-    __shared__ uint64_t p_vb[kIngestThreads];
-    __shared__ uint64_t scan64[4];
-    __shared__ uint32_t scan32[4];
+    __shared__ uint8_t p_snd[THREADS];
+    __shared__ uint8_t p_acc[THREADS];
+    __shared__ uint16_t p_len[THREADS];
+    __shared__ uint32_t p_ssrc[THREADS];
+    __shared__ int64_t p_ts[THREADS];
+    __shared__ uint64_t p_src[THREADS];     // slot / frame start address
+    __shared__ uint32_t p_slotb[THREADS];
+    __shared__ uint64_t p_vb[THREADS];
+    __shared__ uint64_t scan64[NW];
+    __shared__ uint32_t scan32[NW];
 
     if (tid < (int)nsnd) {
         const SenderDev& D = P.senders[S.first_sender + tid];
@@ -154,8 +158,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     __syncthreads();
 
     uint64_t in_pk = 0, in_bytes = 0;
-    for (uint32_t base = b; base < e; base += kIngestThreads) {
-        const uint32_t n = min((uint32_t)kIngestThreads, e - base);
+    for (uint32_t base = b; base < e; base += THREADS) {
+        const uint32_t n = min((uint32_t)THREADS, e - base);
         const uint32_t i = base + tid;
         const bool valid = (uint32_t)tid < n;
         if (tid < (int)nsnd) c_last[tid] = -1;
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             const bool mine = acc && ls == s;
             const uint64_t x = mine ? (1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20) : 0ull;
             uint64_t tot;
-            const uint64_t pre = block_exclusive_scan<uint64_t>(x, scan64, tot);
+            const uint64_t pre = block_exclusive_scan<uint64_t, NW>(x, scan64, tot);
             if (mine) { my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20; }
             if (tid == 0) c_tot[s] = tot;
         }
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
         for (uint32_t t = 0; t < S.ntracks; t++) {
             const bool mine = acc && track == t;
             uint32_t tot;
-            const uint32_t pre = block_exclusive_scan<uint32_t>(mine ? 1u : 0u, scan32, tot);
+            const uint32_t pre = block_exclusive_scan<uint32_t, NW>(mine ? 1u : 0u, scan32, tot);
             if (mine) my_trank = pre;
             if (tid == 0) c_ttot[t] = tot;
         }
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             // 63 takes the next round's lane 0 by readlane).  A wave takes TD frames per round
             // (EDGPU_INGEST_TCP=2: two) and issues all their loads before its first store.
             const int lane = tid & 63, wid = tid >> 6;
-            constexpr uint32_t kW = kIngestThreads / 64;
+            constexpr uint32_t kW = THREADS / 64;
             const uint32_t TD = P.tcp_copy == 2 ? 2u : 1u;                     // uniform
             auto lane0 = [](u32x4 v) {
                 return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             }
         } else if (P.copy_mode == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
             const int lane = tid & 63, wid = tid >> 6;
-            for (uint32_t p = wid; p < n; p += kIngestThreads / 64) {
+            for (uint32_t p = wid; p < n; p += THREADS / 64) {
                 const uint32_t sb = p_slotb[p];
                 if (sb == 0) continue;
                 const uint32_t s = p_snd[p];
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
             // so every lane issues all of its loads (<= 3 x 16 B per packet) before its first
             // store: a wave keeps kDepth whole slots in flight instead of waiting out one load
             // latency per 64 words of one slot.
-            constexpr uint32_t kDepth = DEPTH, kW = kIngestThreads / 64;
+            constexpr uint32_t kDepth = DEPTH, kW = THREADS / 64;
             const uint32_t lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += kDepth * kW) {
                 uint32_t nw[kDepth];
@@ -425,8 +429,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest(IngestParams P) {
     if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];
     // block totals
     uint64_t t1, t2;
-    const uint64_t a1 = block_exclusive_scan<uint64_t>(in_pk, scan64, t1);
-    const uint64_t a2 = block_exclusive_scan<uint64_t>(in_bytes, scan64, t2);
+    const uint64_t a1 = block_exclusive_scan<uint64_t, NW>(in_pk, scan64, t1);
+    const uint64_t a2 = block_exclusive_scan<uint64_t, NW>(in_bytes, scan64, t2);
     (void)a1; (void)a2;
     if (tid == 0 && !(P.ablate & 16u)) {
         atomicAdd(&P.totals->ingested_packets, (unsigned long long)t1);
@@ -1786,7 +1790,9 @@ hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st) {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
-    if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();
+    if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
+    else if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     if (p.npk && p.copy_mode == 1) {
         const uint32_t per = kCopyThreads / kCopyLanes;
