@@ -41,7 +41,9 @@
  *     QTSS_BadArgument, EDGPU_WOULD_BLOCK = QTSS_WouldBlock, plus engine-specific codes
  *     below -100 (capacity / device errors).  edgpu_last_error() gives a message.
  *   - One context per GPU.  Calls on a context are externally serialised (the reference's
- *     per-stream fBucketMutex); contexts on different GPUs run concurrently.
+ *     per-stream fBucketMutex); different contexts -- on different GPUs, or several on one GPU
+ *     (replica sessions) -- may be called from different threads at the same time.
+ *     edgpu_last_error() is per thread.
  *   - All device work runs on the context's HIP stream and is asynchronous unless stated.
  *     Pointers flagged EDGPU_PTR_DEVICE must stay valid until edgpu_sync() returns.
  *   - No torch or HIP types in the ABI: plain pointers and sizes.

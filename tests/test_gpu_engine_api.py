@@ -90,3 +90,36 @@ def test_rtp_info_play_on_empty_session_after_a_found_play():
         with pytest.raises(edgpu.EdgpuError) as e:
             ctx.subscriber_play(empty, rtp_info=True, now_ms=200)
         assert e.value.code == edgpu.WOULD_BLOCK
+
+
+@pytest.mark.gpu
+def test_contexts_run_concurrently_from_threads():
+    """One context per thread (calls on a context are serialized by the caller,
+    many contexts run at once): four host threads each replay a different golden scenario on
+    their own context at the same time, and each capture is the reference's."""
+    import hashlib
+    import json
+    import os
+    import threading
+
+    from easydarwin_amd.replay import replay
+    from scenarios import SCENARIOS
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    names = ["mixed", "rtpinfo", "backpressure", "udppush"]
+    traces = {n: SCENARIOS[n]() for n in names}
+    out, errs = {}, []
+
+    def run(n):
+        try:
+            out[n] = replay(traces[n])[0]
+        except Exception as e:          # surfaced below
+            errs.append((n, repr(e)))
+    th = [threading.Thread(target=run, args=(n,)) for n in names]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for n in names:
+        want = json.load(open(os.path.join(gold, n + ".json")))["capture_sha256"]
+        assert hashlib.sha256(out[n]).hexdigest() == want, n
