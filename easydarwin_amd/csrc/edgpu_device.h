@@ -251,7 +251,7 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long cum_ingested_packets;
     unsigned long long cum_ingested_bytes;
     int ingest_status;              // sticky: an ingest lapped data an in-flight fan-out reads
-    int _pad;
+    unsigned int fan_next;          // dynamic fan-out variants: next work item to claim (per tick)
 };
 
 struct TickParams {

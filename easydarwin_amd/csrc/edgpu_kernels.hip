@@ -556,7 +556,7 @@ __device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, ui
 // (ReflectorStream.cpp:1058-1069).
 __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
-    t->status = 0; t->nwork = 0;
+    t->status = 0; t->nwork = 0; t->fan_next = 0;
 }
 
 // Per-tick counter resets as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
@@ -1202,8 +1202,10 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 // workgroups per CU, i.e. <= 64 VGPRs); 0 leaves it to the compiler.
 // PM: how the store loop finds slot starts for the per-output patch: 0 one bitmap bit per lane
 // (LDS read per word), 1 one wave-uniform 64-bit mask per wave row (row_mask).
+// DYN: work items claimed from a tick-global counter (one atomic per item, two items ahead of
+// use) instead of a static stride over blockIdx, so unequal items cannot leave a long tail.
 template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0,
-          int LFS = 0>
+          int LFS = 0, int DYN = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1250,7 +1252,18 @@ void k_fanout4(FanoutParams P) {
     u32x4 r[NL];
     u32x3 ma;
     u32x2 mb;
+    // DYN: s_claim[par] holds the item claimed for use two items later (written by thread 0
+    // after an image barrier, read by everyone after the next one)
+    __shared__ uint32_t s_claim[2];
     uint32_t w = blockIdx.x;
+    if constexpr (DYN) {
+        if (tid == 0) {
+            s_claim[0] = atomicAdd(&P.totals->fan_next, 1u);
+            s_claim[1] = atomicAdd(&P.totals->fan_next, 1u);
+        }
+        __syncthreads();
+        w = s_claim[0];
+    }
     FanWork nx;
     if (w < nwork) {
         nx = const_load(P.work + w);
@@ -1260,7 +1273,9 @@ void k_fanout4(FanoutParams P) {
             if ((uint32_t)tid < nq * kFsw) fsw = reinterpret_cast<const uint32_t*>(P.fansub + nx.qb)[tid];
         }
     }
-    for (uint32_t par = 0; w < nwork; w += gridDim.x, par ^= 1u) {
+    uint32_t wnext = DYN ? s_claim[1] : 0u;      // DYN: the item to prefetch during this one
+    uint32_t wpref = 0;                          // the item whose loads are in flight
+    for (uint32_t par = 0; w < nwork; w = wpref, par ^= 1u) {
         const FanWork it = nx;
         const uint64_t lo = it.lo, vb0 = it.vb0;
         const uint32_t np = it.np, nw = it.nw, vc0 = it.vc0;
@@ -1290,7 +1305,12 @@ void k_fanout4(FanoutParams P) {
         // ---- the other parity's bitmap is free now: clear it for the next item ----------
         for (int k = tid; k < SM; k += THREADS) smap[(par ^ 1u) * SM + k] = 0;
         // ---- next item's loads, in flight under this item's stores ------------------------
-        const uint32_t wn = w + gridDim.x;
+        uint32_t wn = w + gridDim.x;
+        if constexpr (DYN) {
+            wn = wnext;                                            // claimed one item ago
+            if (tid == 0) s_claim[par] = atomicAdd(&P.totals->fan_next, 1u);   // for the item after it
+        }
+        wpref = wn;
         if (wn < nwork) {
             nx = const_load(P.work + wn);
             fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
@@ -1364,6 +1384,7 @@ void k_fanout4(FanoutParams P) {
             }
         }
         __syncthreads();
+        if constexpr (DYN) wnext = s_claim[par];                  // visible after the barrier
     }
     unsigned long long a = wire, b = inb;
 #pragma unroll
@@ -1873,6 +1894,10 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 28 56, row-mask
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32, 1>()}, // 29 LDS FanSub
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 1>, 1024, 56, fanout4_lds<1024, 56, 1>()}, // 30 56, LDS FanSub
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 31 dynamic items
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 32 56, dynamic
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 8, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 33 32, <= 64 VGPRs, dynamic
+    {(const void*)k_fanout4<1024, 48, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 48, fanout4_lds<1024, 48>()}, // 34 48, dynamic
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1885,9 +1910,11 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,56,nt,su4>", "k_fanout4<1024,56,nt,su2>",
                                             "k_fanout4<1024,32,nt,su2>", "k_fanout4<1024,32,nt,wpe8>",
                                             "k_fanout4<1024,32,nt,rowmask>", "k_fanout4<1024,56,nt,rowmask>",
-                                            "k_fanout4<1024,32,nt,ldsfansub>", "k_fanout4<1024,56,nt,ldsfansub>"};
+                                            "k_fanout4<1024,32,nt,ldsfansub>", "k_fanout4<1024,56,nt,ldsfansub>",
+                                            "k_fanout4<1024,32,nt,dyn>", "k_fanout4<1024,56,nt,dyn>",
+                                            "k_fanout4<1024,32,nt,wpe8,dyn>", "k_fanout4<1024,48,nt,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-static const int kDefaultVariant = 10;   // k_fanout4<1024,32> with non-temporal arena stores
+static const int kDefaultVariant = 31;   // k_fanout4<1024,32>, non-temporal arena stores, items claimed dynamically
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
 bool fanout_rewrites(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;

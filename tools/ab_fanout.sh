@@ -4,6 +4,9 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 mkdir -p $R/gpurun_out/$TAG
+k=0
 for v in "$@"; do
-  EDGPU_FANOUT=$v timeout -k 10 300 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline $BENCH_EXTRA > $R/gpurun_out/$TAG/v$v$TAGSUF.json 2> $R/gpurun_out/$TAG/v$v$TAGSUF.err || exit 1
+  k=$((k+1))                                    # a variant listed twice keeps both runs (vN.json, vN_rK.json)
+  f=v$v$TAGSUF; [ -e $R/gpurun_out/$TAG/$f.json ] && f=v$v${TAGSUF}_r$k
+  EDGPU_FANOUT=$v timeout -k 10 300 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline $BENCH_EXTRA > $R/gpurun_out/$TAG/$f.json 2> $R/gpurun_out/$TAG/$f.err || exit 1
 done
