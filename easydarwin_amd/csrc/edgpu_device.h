@@ -263,6 +263,13 @@ struct TickParams {
     uint32_t nsubs;
     uint32_t nsub_blocks;
     uint32_t chunk;                 // packets per fan-out work item (per kernel variant)
+    uint32_t order;                 // work-item order: 0 sender-major, 1 newest chunks first (kFanRanks)
 };
+
+// Newest-chunks-first work order (TickParams.order 1): items are grouped by their chunk's rank
+// counted from the sender's newest packet, rank 0 first; ranks >= kFanRanks - 1 share the last
+// group.  Each group's cursor sits on its own 64-B line (kFanCursorStride words).
+constexpr uint32_t kFanRanks = 512;
+constexpr uint32_t kFanCursorStride = 16;
 
 }  // namespace edgpu

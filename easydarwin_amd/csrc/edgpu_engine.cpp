@@ -252,6 +252,8 @@ struct edgpu_ctx {
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
     TickTotals* d_totals = nullptr;
+    uint32_t* d_rank = nullptr;     // newest-chunks-first order: group bases + cursors
+    uint32_t fan_order = 0;         // EDGPU_FAN_ORDER: 0 sender-major work items, 1 newest chunks first
 };
 
 extern "C" {
@@ -326,7 +328,9 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    if (dmalloc(&x->d_rank, (size_t)kFanRanks * (1 + kFanCursorStride) * 4) != hipSuccess) return bad("rank groups");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
+    if (const char* v = getenv("EDGPU_FAN_ORDER")) x->fan_order = atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 2);
@@ -359,7 +363,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
-                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
+                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals, (void*)x->d_rank})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->h2d) (void)hipStreamSynchronize(x->h2d);
@@ -1212,6 +1216,8 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
     p.T.chunk = (uint32_t)fanout_chunk(x->fanout_variant);
+    p.T.order = x->fan_order;
+    p.rank_base = x->d_rank;
     // the per-tick totals (relayed_*, arena, status, nwork) are reset by the plan's first kernel
     HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));

@@ -745,14 +745,37 @@ __global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
         }
         const uint32_t isum = wave_block_inclusive_scan<uint32_t>(sum, sh32);
         uint32_t r = isum - sum;
+        __shared__ uint32_t hist[kFanRanks];
+        if (P.T.order) for (uint32_t b = tid; b < kFanRanks; b += nt) hist[b] = 0;
+        __syncthreads();
         for (uint32_t s = s0; s < s1; s++) {
             SenderDev& D = P.senders[s];
             const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
             const uint32_t k = (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
             D.chunk_base = r; D.nchunks = k;
             r += k;
+            if (P.T.order) {                  // this sender's items per rank group
+                for (uint32_t g = 0; g < min(k, kFanRanks - 1); g++) atomicAdd(&hist[g], 1u);
+                if (k >= kFanRanks) atomicAdd(&hist[kFanRanks - 1], k - (kFanRanks - 1));
+            }
         }
         if (tid == nt - 1) P.totals->nwork = isum;
+        if (P.T.order) {                      // group bases (exclusive scan), cursors cleared
+            __syncthreads();
+            constexpr uint32_t per = (kFanRanks + 1023) / 1024;
+            uint32_t v[per], tsum = 0;
+            for (uint32_t j = 0; j < per; j++) {
+                const uint32_t b = tid * per + j;
+                v[j] = b < kFanRanks && tid * per < kFanRanks ? hist[b] : 0u;
+                tsum += v[j];
+            }
+            uint32_t base = wave_block_inclusive_scan<uint32_t>(tsum, sh32) - tsum;
+            for (uint32_t j = 0; j < per; j++) {
+                const uint32_t b = tid * per + j;
+                if (b < kFanRanks) { P.rank_base[b] = base; P.rank_base[kFanRanks + b * kFanCursorStride] = 0; }
+                base += v[j];
+            }
+        }
     }
 }
 
@@ -829,7 +852,12 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             it.vc0 = vc0;
             it.lo = lo;
             it.vb0 = vb0;
-            P.work[chunk_base + k] = it;
+            uint32_t pos = chunk_base + k;
+            if (P.T.order) {                  // newest chunks first: rank from the sender's head
+                const uint32_t g = min(nch - 1 - k, kFanRanks - 1);
+                pos = P.rank_base[g] + atomicAdd(&P.rank_base[kFanRanks + g * kFanCursorStride], 1u);
+            }
+            P.work[pos] = it;
         }
     }
 }
@@ -1204,8 +1232,10 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 // (LDS read per word), 1 one wave-uniform 64-bit mask per wave row (row_mask).
 // DYN: work items claimed from a tick-global counter (one atomic per item, two items ahead of
 // use) instead of a static stride over blockIdx, so unequal items cannot leave a long tail.
+// PACE (A/B of store issue rate): 1 every window takes the patch path (an identity window then
+// pays the rewrite's bitmap read per word); 2 s_sleep after every store row.
 template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0,
-          int LFS = 0, int DYN = 0>
+          int LFS = 0, int DYN = 0, int PACE = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1329,7 +1359,7 @@ void k_fanout4(FanoutParams P) {
             if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
             const uint32_t s = (uint32_t)(A & 7);                              // words past a line
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
-            const bool patch = (f.ch & 1u) || f.rw;                            // uniform
+            const bool patch = PACE == 1 || (f.ch & 1u) || f.rw;               // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
             for (uint32_t j = 0; j < nj; j += SU) {
                 u32x4 v[SU];
@@ -1354,6 +1384,7 @@ void k_fanout4(FanoutParams P) {
                     }
                     __builtin_amdgcn_raw_buffer_store_b128(v[k], os, (tid + (j + k) * THREADS - s) * 16u, 0, AUX);
                 }
+                if constexpr (PACE == 2) __builtin_amdgcn_s_sleep(1);
             }
         }
         // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
@@ -1898,6 +1929,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 32 56, dynamic
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 8, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 33 32, <= 64 VGPRs, dynamic
     {(const void*)k_fanout4<1024, 48, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 48, fanout4_lds<1024, 48>()}, // 34 48, dynamic
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 35 dyn, patch path always
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 36 dyn, s_sleep per row
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1912,7 +1945,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt,rowmask>", "k_fanout4<1024,56,nt,rowmask>",
                                             "k_fanout4<1024,32,nt,ldsfansub>", "k_fanout4<1024,56,nt,ldsfansub>",
                                             "k_fanout4<1024,32,nt,dyn>", "k_fanout4<1024,56,nt,dyn>",
-                                            "k_fanout4<1024,32,nt,wpe8,dyn>", "k_fanout4<1024,48,nt,dyn>"};
+                                            "k_fanout4<1024,32,nt,wpe8,dyn>", "k_fanout4<1024,48,nt,dyn>",
+                                            "k_fanout4<1024,32,nt,dyn,patchall>", "k_fanout4<1024,32,nt,dyn,sleep>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 31;   // k_fanout4<1024,32>, non-temporal arena stores, items claimed dynamically
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)

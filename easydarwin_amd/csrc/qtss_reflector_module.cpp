@@ -26,13 +26,24 @@
 // sender wakeups (ReflectorStream.cpp:1676-1714); here a tick thread reflects every
 // edgpu_tick_msec (default 20 ms), or the host calls EDGPU_QTSSReflectorModule_Tick.
 //
-// Scope: RTSP-interleaved pushers (EasyPusher's default transport) and
-// UDP / TCP players.  A UDP-transport push SETUP is refused (those pushers reach the engine
-// through edgpu_udp_sources from a host socket reader, as the C++ adapter's ProcessUDPPacket
-// does); RTSPRoute / RTSPAuthorize / Easy_GetDeviceStream (redirects, access files, the CMS
-// control plane) are not registered.
+// Scope: RTSP-interleaved pushers (EasyPusher's default transport), UDP
+// pushers and UDP / TCP players.  A UDP push SETUP binds the track's even/odd socket pair as
+// ReflectorStream::BindSockets does (ReflectorStream.cpp:388-500, UDPSocketPool.cpp:81-150) and
+// answers with its port (qtssRTSPReqSetUpServerPort, QTSSReflectorModule.cpp:1686-1688); a
+// reader thread hands every datagram with its source address to the engine
+// (ReflectorSocket::GetIncomingData -> ProcessPacket, ReflectorStream.cpp:1716-1735, 1769-1875)
+// and the receiver reports go out of the track's RTCP socket (SendReceiverReport, :510-527).
+// RTSPRoute / RTSPAuthorize / Easy_GetDeviceStream (redirects, access files, the CMS control
+// plane) are not registered.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -100,10 +111,20 @@ struct Output;
 struct Session {                        // a pushed stream ("<path>-<channel>", QRM:1384)
     std::string name;
     uint32_t engine = 0;                // edgpu session
+    bool udpPush = false;               // pushed over UDP: RTCP on the odd port (Q12/Q14)
     std::vector<uint32_t> trackIDs;     // a=control:trackID=N per m= line, SDP order
+    std::vector<uint16_t> sdpPorts;     // the m= lines' ports (StreamInfo::fPort)
+    std::vector<int> pair;              // UDP push: the track's socket pair (index into Module::udp)
     std::vector<bool> setupToReceive;   // StreamInfo::fSetupToReceive
     std::string sdp;
     std::vector<Output*> slots;         // the streams' bucket arrays: outputs in bucket order
+};
+
+// One track of a UDP push session: RTP on an even port, RTCP on the next (ReflectorSocket A/B)
+struct UdpPair {
+    int fd[2] = {-1, -1};
+    uint16_t port = 0;
+    uint32_t session = 0, track = 0;    // Module::sessions index, track index
 };
 
 struct Output {                         // one player (RTPSessionOutput)
@@ -133,7 +154,8 @@ struct Module {
     int64_t bucketDelayMs = 73;         // ReflectorStream::sBucketDelayInMsec
     uint32_t bucketSize = 16;           // ReflectorStream::sBucketSize
     bool manualTick = false;
-    std::thread ticker;
+    std::vector<UdpPair> udp;
+    std::thread ticker, reader;
     std::atomic<bool> stop{false};
     QTSS_Error tickErr = QTSS_NoErr;
 };
@@ -168,6 +190,21 @@ std::vector<uint32_t> SdpTrackIDs(const std::string& sdp) {
     std::vector<uint32_t> ids(n);
     for (uint32_t i = 0; i < n; i++) ids[i] = t[i].track_id;
     return ids;
+}
+
+// each m= line's port (SDPSourceInfo::Parse reads it into StreamInfo::fPort,
+// SDPSourceInfo.cpp:260-353); 0 when absent
+std::vector<uint16_t> SdpPorts(const std::string& sdp) {
+    std::vector<uint16_t> ports;
+    for (size_t k = 0; k < sdp.size();) {
+        const size_t e = std::min(sdp.find_first_of("\r\n", k), sdp.size());
+        if (sdp.compare(k, 2, "m=") == 0) {
+            const size_t sp = sdp.find(' ', k);
+            ports.push_back(sp < e ? (uint16_t)strtoul(sdp.c_str() + sp + 1, nullptr, 10) : (uint16_t)0);
+        }
+        k = e + 1;
+    }
+    return ports;
 }
 
 int TrackIndex(const Session& s, uint32_t trackID) {
@@ -233,7 +270,103 @@ public:
         }
         return edgpu_reflector::kNoErr;
     }
+    // ReflectorStream::SendReceiverReport (ReflectorStream.cpp:510-527): from the track's RTCP
+    // socket to the pusher's RTCP address; the send result is ignored, as there
+    void SendReceiverReport(uint32_t session, uint16_t track, uint32_t addr, uint16_t port, const uint8_t* rr,
+                            uint32_t len) override {
+        for (const Session& s : M->sessions) {
+            if (s.engine != session || track >= s.pair.size() || s.pair[track] < 0) continue;
+            sockaddr_in to;
+            memset(&to, 0, sizeof(to));
+            to.sin_family = AF_INET;
+            to.sin_addr.s_addr = htonl(addr);
+            to.sin_port = htons(port);
+            (void)sendto(M->udp[s.pair[track]].fd[1], rr, len, MSG_NOSIGNAL, (const sockaddr*)&to, sizeof(to));
+            return;
+        }
+    }
 };
+
+// ---- UDP push sockets -----------------------------------------------------------------------
+// A socket pair on INADDR_ANY: `port` only when nonzero, else the first free even/odd pair
+// from 6970 up (UDPSocketPool::CreateUDPSocketPair, UDPSocketPool.cpp:81-150; BindSockets
+// retries a push with port 0 when the SDP's port is taken, ReflectorStream.cpp:432-443).
+// 1 MiB receive buffers (:466-472).  Non-blocking: the reader drains each socket to EAGAIN.
+bool BindPair(uint16_t port, UdpPair* out) {
+    auto open1 = [](uint16_t p) -> int {
+        const int fd = socket(AF_INET, SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+        if (fd < 0) return -1;
+        const int rcv = 1 << 20;
+        (void)setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof(rcv));
+        sockaddr_in a;
+        memset(&a, 0, sizeof(a));
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_ANY);
+        a.sin_port = htons(p);
+        if (bind(fd, (const sockaddr*)&a, sizeof(a)) != 0) { close(fd); return -1; }
+        return fd;
+    };
+    auto try_pair = [&](uint32_t p) {
+        const int a = open1((uint16_t)p);
+        if (a < 0) return false;
+        const int b = open1((uint16_t)(p + 1));
+        if (b < 0) { close(a); return false; }
+        out->fd[0] = a; out->fd[1] = b; out->port = (uint16_t)p;
+        return true;
+    };
+    if (port != 0 && port < 65535 && try_pair(port)) return true;
+    for (uint32_t p = 6970; p + 1 < 65536; p += 2)
+        if (try_pair(p)) return true;
+    return false;
+}
+
+// ReflectorSocket::GetIncomingData (ReflectorStream.cpp:1716-1735): every datagram waiting on a
+// UDP push socket, read like RecvFrom into a kMaxReflectorPacketSize (2060) buffer -- a longer
+// datagram is truncated there -- and handed to the engine with its source address (the UDP RTCP
+// SR gate, Q14, and the pusher's RTCP address, :1769-1875, are the engine's).  An empty
+// datagram is the reference's "no more data" read: nothing to ingest.
+uint32_t DrainUDPLocked() {
+    if (!M->R) return 0;
+    char buf[2060];
+    uint32_t n = 0;
+    for (const UdpPair& u : M->udp) {
+        const Session& s = M->sessions[u.session];
+        for (int k = 0; k < 2; k++) {
+            for (;;) {
+                sockaddr_in from;
+                socklen_t fl = sizeof(from);
+                const ssize_t r = recvfrom(u.fd[k], buf, sizeof(buf), MSG_DONTWAIT, (sockaddr*)&from, &fl);
+                if (r < 0) {
+                    if (errno == EINTR) continue;
+                    break;                                            // EAGAIN: drained
+                }
+                if (r == 0) continue;
+                M->R->ProcessUDPPacket(s.engine, u.track, k == 1, buf, (uint32_t)r, ntohl(from.sin_addr.s_addr),
+                                       ntohs(from.sin_port), Milliseconds());
+                n++;
+            }
+        }
+    }
+    return n;
+}
+
+// the reader thread: poll every UDP push socket, drain what arrived
+void ReaderLoop() {
+    std::vector<pollfd> pf;
+    while (!M->stop.load()) {
+        {
+            std::lock_guard<std::mutex> g(M->mu);
+            pf.clear();
+            for (const UdpPair& u : M->udp)
+                for (int k = 0; k < 2; k++) pf.push_back(pollfd{u.fd[k], POLLIN, 0});
+        }
+        if (pf.empty()) { std::this_thread::sleep_for(std::chrono::milliseconds(5)); continue; }
+        if (poll(pf.data(), pf.size(), 10) > 0) {
+            std::lock_guard<std::mutex> g(M->mu);
+            (void)DrainUDPLocked();
+        }
+    }
+}
 
 QTSS_Error Tick() {
     std::lock_guard<std::mutex> g(M->mu);
@@ -285,6 +418,7 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
     }
     if (!M->manualTick) {
         M->stop = false;
+        M->reader = std::thread(ReaderLoop);
         M->ticker = std::thread([] {
             while (!M->stop.load()) {
                 std::this_thread::sleep_for(std::chrono::milliseconds(M->tickMs));
@@ -300,7 +434,12 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
 QTSS_Error Shutdown() {
     M->stop = true;
     if (M->ticker.joinable()) M->ticker.join();
+    if (M->reader.joinable()) M->reader.join();
     std::lock_guard<std::mutex> g(M->mu);
+    for (UdpPair& u : M->udp)
+        for (int fd : u.fd)
+            if (fd >= 0) close(fd);
+    M->udp.clear();
     M->R.reset();
     return QTSS_NoErr;
 }
@@ -355,8 +494,9 @@ QTSS_Error DoDescribe(QTSS_StandardRTSP_Params* p) {
               (uint32_t)qtssWriteFlagsNoFlags);
 }
 
-// FindOrCreateSession (QRM:1379-1545): the engine session of an announced stream
-Session* FindOrCreateSession(const std::string& name) {
+// FindOrCreateSession (QRM:1379-1545): the engine session of an announced stream; the first
+// SETUP decides whether it is pushed over UDP
+Session* FindOrCreateSession(const std::string& name, bool udpPush = false) {
     auto it = M->byName.find(name);
     if (it != M->byName.end()) return &M->sessions[it->second];
     auto a = M->announced.find(name);
@@ -364,10 +504,18 @@ Session* FindOrCreateSession(const std::string& name) {
     Session s;
     s.name = name;
     s.sdp = a->second;
-    if (M->R->SetupReflectorSession(s.sdp, false, &s.engine) != 0) return nullptr;
+    s.udpPush = udpPush;
+    if (M->R->SetupReflectorSession(s.sdp, udpPush, &s.engine) != 0) return nullptr;
     s.trackIDs = SdpTrackIDs(s.sdp);
     s.trackIDs.resize(M->R->GetNumStreams(s.engine));
+    s.sdpPorts = SdpPorts(s.sdp);
+    s.sdpPorts.resize(s.trackIDs.size(), 0);
+    s.pair.assign(s.trackIDs.size(), -1);
     s.setupToReceive.assign(s.trackIDs.size(), false);
+    // each ReflectorStream draws its receiver-report SSRC from rand() and its CNAME from
+    // OS::Milliseconds()/1000 when it is built (ReflectorStream.cpp:164-201, RTCPSRPacket.cpp:87-117)
+    for (uint32_t t = 0; t < s.trackIDs.size(); t++)
+        (void)M->R->SetSourceIdentity(s.engine, t, (uint32_t)rand(), Milliseconds() / 1000);
     M->sessions.push_back(s);
     M->byName[name] = (uint32_t)M->sessions.size() - 1;
     return &M->sessions.back();
@@ -383,12 +531,24 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     const uint32_t trackID = TrackFromRequest(p->inRTSPRequest, &digitOK);
     std::lock_guard<std::mutex> g(M->mu);
     if (isPush) {
-        // RTSP-interleaved pushers only: the engine's host reader takes UDP pushers' datagrams
-        if (transport != qtssRTPTransportTypeTCP) return QTSS_RequestFailed;
-        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest));
-        if (!s || !digitOK) return QTSS_RequestFailed;
+        const bool udp = transport != qtssRTPTransportTypeTCP;
+        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest), udp);
+        if (!s || !digitOK || s->udpPush != udp) return QTSS_RequestFailed;
         const int t = TrackIndex(*s, trackID);
         if (t < 0 || s->setupToReceive[t]) return QTSS_RequestFailed;      // bad / duplicate track
+        if (udp) {
+            // the track's socket pair (BindSockets) and its port in the SETUP response
+            if (s->pair[t] < 0) {
+                UdpPair u;
+                if (!BindPair(s->sdpPorts[t], &u)) return QTSS_RequestFailed;      // sCantBindReflectorSocketErr
+                u.session = (uint32_t)(s - &M->sessions[0]);
+                u.track = (uint32_t)t;
+                M->udp.push_back(u);
+                s->pair[t] = (int)M->udp.size() - 1;
+            }
+            const uint16_t port = M->udp[s->pair[t]].port;
+            (void)SetValue(p->inRTSPRequest, qtssRTSPReqSetUpServerPort, 0, &port, sizeof(port));
+        }
         QTSS_Object stream = nullptr;
         QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
         if (e != QTSS_NoErr) return e;
@@ -613,4 +773,12 @@ extern "C" QTSS_Error QTSSReflectorModule_Main(void* inPrivateArgs) {
 extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
     if (!M) return QTSS_RequestFailed;
     return Tick();
+}
+
+// Manual mode (EDGPU_QTSS_MANUAL_TICK=1, no reader thread): read every datagram waiting on the
+// UDP push sockets now; returns how many were handed to the engine.
+extern "C" uint32_t EDGPU_QTSSReflectorModule_PollUDP(void) {
+    if (!M) return 0;
+    std::lock_guard<std::mutex> g(M->mu);
+    return DrainUDPLocked();
 }

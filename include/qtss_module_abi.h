@@ -116,6 +116,7 @@ enum : uint32_t {
     qtssRTSPReqFilePath = 2, qtssRTSPReqFileName = 5, qtssRTSPReqFileDigit = 6,
     qtssRTSPReqMethod = 9, qtssRTSPReqRespKeepAlive = 13, qtssRTSPReqQueryString = 23,
     qtssRTSPReqContentLen = 25, qtssRTSPReqTransportType = 28, qtssRTSPReqTransportMode = 29,
+    qtssRTSPReqSetUpServerPort = 30,                 // UInt16: server_port of a push SETUP's response
 };
 
 // RTSP header ids (QTSSRTSPProtocol.h:68-100)

@@ -39,7 +39,7 @@ SAME(qtssRTPStrTransportType); SAME(qtssCliSesStreamObjects); SAME(qtssCliSesSta
 SAME(qtssCliSesFirstUserAgent); SAME(qtssRTSPReqFilePath); SAME(qtssRTSPReqFileName);
 SAME(qtssRTSPReqFileDigit); SAME(qtssRTSPReqMethod); SAME(qtssRTSPReqRespKeepAlive);
 SAME(qtssRTSPReqQueryString); SAME(qtssRTSPReqContentLen); SAME(qtssRTSPReqTransportType);
-SAME(qtssRTSPReqTransportMode); SAME(qtssCacheControlHeader); SAME(qtssContentLengthHeader);
+SAME(qtssRTSPReqTransportMode); SAME(qtssRTSPReqSetUpServerPort); SAME(qtssCacheControlHeader); SAME(qtssContentLengthHeader);
 SAME(QTSS_Register_Role); SAME(QTSS_Initialize_Role); SAME(QTSS_Shutdown_Role); SAME(QTSS_RereadPrefs_Role);
 SAME(QTSS_Interval_Role); SAME(QTSS_RTSPRoute_Role); SAME(QTSS_RTSPAuthorize_Role);
 SAME(QTSS_RTSPPreProcessor_Role); SAME(QTSS_RTSPIncomingData_Role); SAME(QTSS_ClientSessionClosing_Role);

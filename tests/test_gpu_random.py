@@ -11,7 +11,7 @@ import subprocess
 import pytest
 
 from easydarwin_amd.replay import replay
-from easydarwin_amd.trace import PKT, UPKT
+from easydarwin_amd.trace import PKT
 from scenarios import random_scenario
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -49,11 +49,11 @@ def test_engine_paths_match_oracle_on_random_traces(seed, oracle_bins, tmp_path)
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", SEEDS)
 def test_module_matches_reference_on_random_traces(seed, oracle_bins, tmp_path):
-    """Traces whose pushers are all RTSP-interleaved, through the QTSS module: the capture, and
-    (with the reference harness at hand) every write's transmit time."""
+    """Every random trace through the QTSS module -- RTSP-interleaved pushers as RTSPIncomingData,
+    UDP pushers as loopback datagrams to the socket pairs the module bound: the capture
+    (receiver reports included), and (with the reference harness at hand) every write's
+    transmit time."""
     tr = random_scenario(seed)
-    if any(ev[0] == UPKT for ev in tr.events) or any(tr.udp_push(s) for s in range(len(tr.sdps))):
-        pytest.skip("UDP pushers: not served by the module")
     tb = tr.to_bytes()
     want = _oracle(oracle_bins["port"], tb, tmp_path, "port")
     t, c, tt = tmp_path / "m.edtr", tmp_path / "m.edcp", tmp_path / "m.edtt"

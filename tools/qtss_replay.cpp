@@ -6,9 +6,17 @@
 //     (QTSServer::LoadCompiledInModules / QTSSModule::SetupModule, QTSS_Private.cpp:44-59);
 //     Register (the roles it adds are checked), then Initialize;
 //   * every push session: ANNOUNCE (SDP body read through QTSS_Read), SETUP per track in
-//     record mode over TCP (RTSP-interleaved, EasyPusher's default), RECORD;
+//     record mode -- over TCP (RTSP-interleaved, EasyPusher's default), or over UDP for a
+//     UDP-push session (trace flag bit 0), whose SETUP response carries the port of the socket
+//     pair the module bound (qtssRTSPReqSetUpServerPort) -- then RECORD;
 //   * PKT -> RTSPIncomingData with the '$' ch BE16(len) frame (RTSPSession::
 //     HandleIncomingDataPacket, RTSPSession.cpp:2131-2178);
+//   * UPKT -> a real loopback datagram to the module's RTP (even) or RTCP (odd) socket, sent
+//     from a socket bound to the trace's source port on 127.0.0.x (one loopback address per
+//     source address of the trace), then EDGPU_QTSSReflectorModule_PollUDP, so the module reads
+//     it at the event's virtual time; the receiver reports the module sends back are read off
+//     those sockets after every TICK and written, with the trace's own addresses, as the
+//     capture's EDRR trailer (the reference harness's SendTo record);
 //   * JOIN -> a player's SETUP per track (UDP or TCP) and PLAY, user agent "vlc" for an
 //     RTP-Info player (ua_flags bit 0); a PLAY the module defers (QTSS_SetIdleTimer instead of
 //     QTSS_Play) is dropped, as the reference harness drops it;
@@ -20,13 +28,20 @@
 // datagram; TCP: '$' channel BE16(len), channels 2*track / 2*track+1 in SETUP order,
 // RTPStream.cpp:472-473, 1084-1147) into per-(subscriber, track, kind) captures, written in the
 // format of easydarwin_amd/trace.py -- so the module's output compares byte for byte with the
-// reference reflector's captures.  UDP-push sessions are skipped (the module serves
-// RTSP-interleaved pushers; see qtss_reflector_module.cpp).
+// reference reflector's captures.  rand() is interposed (the executable exports it,
+// -rdynamic): the module's calls get the reference harness's deterministic sequence
+// (trace.py rr_ssrc), which sets each stream's receiver-report SSRC as the reference's
+// ReflectorStream constructor draws it.
 //
 // Test infrastructure (tests/test_gpu_qtss_module.py, tests/test_qtss_abi.py); not shipped.
 // Usage: qtss_replay <module.so> <trace.edtr> <capture.edcp>
 //        qtss_replay <module.so> --register      (Register role only; no GPU needed)
+#include <arpa/inet.h>
 #include <dlfcn.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -72,6 +87,18 @@ static void set_attr(Obj* o, uint32_t id, uint32_t idx, const void* p, uint32_t 
 template <typename T> static void set_pod(Obj* o, uint32_t id, T v) { set_attr(o, id, 0, &v, sizeof(v)); }
 
 static int64_t g_now = 0;
+
+// the reference harness's deterministic rand() (trace.py rr_ssrc), for the module's own calls;
+// other callers (the engine's default identity draw, which the module overrides) get 0
+static uint32_t g_rand_calls = 0;
+extern "C" int rand(void) {
+    Dl_info di;
+    if (dladdr(__builtin_return_address(0), &di) && di.dli_fname && strstr(di.dli_fname, "libQTSSReflectorModule")) {
+        const uint32_t k = g_rand_calls++;
+        return (int)(((k + 1) * 0x9E3779B1u + 0x7F4A7C15u) & 0x7FFFFFFFu);
+    }
+    return 0;
+}
 static std::set<uint32_t> g_roles;
 static std::map<std::string, uint32_t> g_attr_ids;
 static std::vector<Obj*> g_streams;                  // every RTP stream object, creation order
@@ -186,9 +213,68 @@ struct Player { uint32_t sub, session; Obj* rtsp; Obj* client; std::vector<Obj*>
 
 static QTSS_DispatchFuncPtr g_dispatch = nullptr;
 
+// ---- UDP pushers: one loopback socket per (source address, port) of the trace ----------------
+static std::map<uint32_t, uint32_t> g_loop_of;                      // trace IPv4 -> 127.0.0.x (host order)
+static std::map<std::pair<uint32_t, uint16_t>, int> g_src_fd;       // (trace addr, port) -> bound socket
+static int source_socket(uint32_t addr, uint16_t port) {
+    const auto key = std::make_pair(addr, port);
+    auto it = g_src_fd.find(key);
+    if (it != g_src_fd.end()) return it->second;
+    if (!g_loop_of.count(addr)) {
+        const uint32_t l = 0x7F000002u + (uint32_t)g_loop_of.size();
+        g_loop_of[addr] = l;
+    }
+    const int fd = socket(AF_INET, SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    sockaddr_in a;
+    memset(&a, 0, sizeof(a));
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(g_loop_of[addr]);
+    a.sin_port = htons(port);
+    if (fd < 0 || bind(fd, (const sockaddr*)&a, sizeof(a)) != 0) {
+        fprintf(stderr, "cannot bind a source socket for %08x:%u on loopback\n", addr, port);
+        exit(3);
+    }
+    g_src_fd[key] = fd;
+    return fd;
+}
+struct Report { int64_t t; uint32_t session; uint16_t track; uint32_t addr; uint16_t port; std::string bytes; };
+static std::vector<Report> g_reports;
+static std::map<uint16_t, std::pair<uint32_t, uint16_t>> g_rtcp_owner;   // module RTCP port -> (session, track)
+// the receiver reports the module sent during the last TICK, in its send order (session, track)
+static void read_reports() {
+    std::vector<Report> got;
+    std::vector<pollfd> pf;
+    std::vector<std::pair<uint32_t, uint16_t>> key;
+    for (auto& e : g_src_fd) { pf.push_back(pollfd{e.second, POLLIN, 0}); key.push_back(e.first); }
+    if (pf.empty()) return;
+    while (poll(pf.data(), pf.size(), 2) > 0) {
+        for (size_t i = 0; i < pf.size(); i++) {
+            if (!(pf[i].revents & POLLIN)) continue;
+            char buf[2048];
+            sockaddr_in from;
+            socklen_t fl = sizeof(from);
+            ssize_t n;
+            while ((n = recvfrom(pf[i].fd, buf, sizeof(buf), 0, (sockaddr*)&from, &fl)) >= 0) {
+                const auto o = g_rtcp_owner.find(ntohs(from.sin_port));
+                Report r{g_now, o == g_rtcp_owner.end() ? 0xFFFFFFFFu : o->second.first,
+                         (uint16_t)(o == g_rtcp_owner.end() ? 0xFFFF : o->second.second), key[i].first, key[i].second,
+                         std::string(buf, (size_t)n)};
+                got.push_back(r);
+                fl = sizeof(from);
+            }
+        }
+    }
+    std::stable_sort(got.begin(), got.end(), [](const Report& a, const Report& b) {
+        return a.session != b.session ? a.session < b.session : a.track < b.track;
+    });
+    g_reports.insert(g_reports.end(), got.begin(), got.end());
+}
+
 static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::string& path, const std::string& digit,
-                          uint32_t mode, uint32_t transport, const std::string& body = std::string()) {
+                          uint32_t mode, uint32_t transport, const std::string& body = std::string(),
+                          Obj** outReq = nullptr) {
     Obj* req = new_obj(qtssRTSPRequestObjectType);
+    if (outReq) *outReq = req;
     set_pod<uint32_t>(req, qtssRTSPReqMethod, method);
     set_attr(req, qtssRTSPReqFilePath, 0, path.data(), (uint32_t)path.size());
     if (!digit.empty()) set_attr(req, qtssRTSPReqFileDigit, 0, digit.data(), (uint32_t)digit.size());
@@ -212,7 +298,8 @@ int main(int argc, char** argv) {
     if (!so) { fprintf(stderr, "dlopen: %s\n", dlerror()); return 3; }
     auto main_fn = (QTSS_Error (*)(void*))dlsym(so, "QTSSReflectorModule_Main");
     auto tick_fn = (QTSS_Error (*)(void))dlsym(so, "EDGPU_QTSSReflectorModule_Tick");
-    if (!main_fn || !tick_fn) { fprintf(stderr, "module entry points missing\n"); return 3; }
+    auto poll_fn = (uint32_t (*)(void))dlsym(so, "EDGPU_QTSSReflectorModule_PollUDP");
+    if (!main_fn || !tick_fn || !poll_fn) { fprintf(stderr, "module entry points missing\n"); return 3; }
 
     static QTSS_Callbacks cbs;
     for (auto& a : cbs.addr) a = (QTSS_CallbackProcPtr)cb_unimplemented;
@@ -269,6 +356,7 @@ int main(int argc, char** argv) {
     std::vector<std::string> paths(nsess);
     std::vector<uint32_t> ntracks(nsess, 0);
     std::vector<Obj*> push_rtsp(nsess, nullptr), push_client(nsess, nullptr);
+    std::vector<std::vector<uint16_t>> server_port(nsess);     // UDP push: the module's RTP port per track
     for (uint32_t s = 0; s < nsess; s++) {
         const uint32_t n = r.get<uint32_t>();
         std::string sdp((const char*)&r.d[r.p], n);
@@ -276,17 +364,27 @@ int main(int argc, char** argv) {
         const uint8_t fl = ver >= 2 ? r.get<uint8_t>() : 0;
         for (size_t k = sdp.find("m="); k != std::string::npos; k = sdp.find("\nm=", k + 1)) ntracks[s]++;
         paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
-        if (fl & 1) continue;                                    // UDP push: not through the module
+        const uint32_t tt = (fl & 1) ? qtssRTPTransportTypeUDP : qtssRTPTransportTypeTCP;
         push_rtsp[s] = new_obj(qtssRTSPSessionObjectType);
         push_client[s] = new_obj(qtssClientSessionObjectType);
         g_rtsp_of_client[push_client[s]] = push_rtsp[s];
-        if (request(push_rtsp[s], push_client[s], qtssAnnounceMethod, paths[s], "", 0, qtssRTPTransportTypeTCP, sdp))
+        if (request(push_rtsp[s], push_client[s], qtssAnnounceMethod, paths[s], "", 0, tt, sdp))
             { fprintf(stderr, "ANNOUNCE failed\n"); return 3; }
-        for (uint32_t t = 0; t < ntracks[s]; t++)
+        for (uint32_t t = 0; t < ntracks[s]; t++) {
+            Obj* req = nullptr;
             if (request(push_rtsp[s], push_client[s], qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(t + 1),
-                        std::to_string(t + 1), qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
+                        std::to_string(t + 1), qtssRTPTransportModeRecord, tt, std::string(), &req))
                 { fprintf(stderr, "push SETUP failed\n"); return 3; }
-        if (request(push_rtsp[s], push_client[s], qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
+            if (fl & 1) {
+                auto it = req->attrs.find(qtssRTSPReqSetUpServerPort);
+                uint16_t port = 0;
+                if (it != req->attrs.end() && !it->second.empty() && it->second[0].size() == 2) memcpy(&port, it->second[0].data(), 2);
+                if (port == 0 || (port & 1)) { fprintf(stderr, "UDP push SETUP: no even server port\n"); return 3; }
+                server_port[s].push_back(port);
+                g_rtcp_owner[(uint16_t)(port + 1)] = std::make_pair(s, (uint16_t)t);
+            }
+        }
+        if (request(push_rtsp[s], push_client[s], qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, tt))
             { fprintf(stderr, "RECORD failed\n"); return 3; }
     }
     std::vector<Player> players;
@@ -341,6 +439,7 @@ int main(int argc, char** argv) {
         } else if (type == 3) {                                  // TICK
             const QTSS_Error e = tick_fn();
             if (e) { fprintf(stderr, "tick failed %d\n", (int)e); return 3; }
+            read_reports();
             for (Obj* st : g_streams) st->budget[0] = st->budget[1] = -1;
         } else if (type == 4) {                                  // BLOCK
             const uint32_t sub = r.get<uint32_t>();
@@ -349,10 +448,28 @@ int main(int argc, char** argv) {
             const uint32_t budget = r.get<uint32_t>();
             for (auto& pl : players)
                 if (pl.sub == sub && !pl.left && trk < pl.streams.size()) pl.streams[trk]->budget[kind & 1] = budget;
-        } else if (type == 5) {                                  // UPKT: a UDP pusher (not served)
-            r.p += 4 + 1 + 4 + 2;
+        } else if (type == 5) {                                  // UPKT -> a loopback datagram
+            const uint32_t s = r.get<uint32_t>();
+            const uint8_t ch = r.get<uint8_t>();
+            const uint32_t addr = r.get<uint32_t>();
+            const uint16_t port = r.get<uint16_t>();
             const uint32_t len = r.get<uint32_t>();
+            const uint8_t* data = &r.d[r.p];
             r.p += len;
+            if (len == 0 || ch / 2 >= server_port[s].size()) continue;
+            const int fd = source_socket(addr, port);
+            (void)source_socket(addr, (uint16_t)(port | 1));        // where the receiver reports may go
+            sockaddr_in to;
+            memset(&to, 0, sizeof(to));
+            to.sin_family = AF_INET;
+            to.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+            to.sin_port = htons((uint16_t)(server_port[s][ch / 2] + (ch & 1)));
+            if (sendto(fd, data, len, 0, (const sockaddr*)&to, sizeof(to)) != (ssize_t)len) { perror("sendto"); return 3; }
+            // the module reads it now, at this event's virtual time
+            for (int i = 0; poll_fn() == 0; i++) {
+                if (i > 5000) { fprintf(stderr, "UPKT datagram never reached the module\n"); return 3; }
+                usleep(100);
+            }
         } else if (type == 6) {                                  // LEAVE -> ClientSessionClosing
             const uint32_t sub = r.get<uint32_t>();
             for (auto& pl : players)
@@ -389,6 +506,17 @@ int main(int argc, char** argv) {
             fwrite(&kind, 1, 1, o); fwrite(&tcp, 1, 1, o); fwrite(&np, 8, 1, o); fwrite(&nb, 8, 1, o);
             fwrite(s->cap[k].data(), 1, nb, o);
         }
+    if (!g_reports.empty()) {               // EDRR trailer: receiver reports sent to pushers
+        fwrite("EDRR", 1, 4, o);
+        const uint32_t m = (uint32_t)g_reports.size();
+        fwrite(&m, 4, 1, o);
+        for (const Report& rr : g_reports) {
+            const uint32_t ln = (uint32_t)rr.bytes.size();
+            fwrite(&rr.t, 8, 1, o); fwrite(&rr.session, 4, 1, o); fwrite(&rr.track, 2, 1, o);
+            fwrite(&rr.addr, 4, 1, o); fwrite(&rr.port, 2, 1, o); fwrite(&ln, 4, 1, o);
+            fwrite(rr.bytes.data(), 1, ln, o);
+        }
+    }
     fclose(o);
     // EDGPU_TT_OUT=<path>: the transmit times in capture order, the reference harness's format
     if (const char* ttp = getenv("EDGPU_TT_OUT")) {
