@@ -135,6 +135,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
     __shared__ uint64_t c_tot[kMaxSendersPerSession];
     __shared__ uint32_t c_ttot[kMaxTracks];
     __shared__ int c_last[kMaxSendersPerSession];   // (tid << 10 | rank) of the chunk's newest non-empty packet
+    __shared__ int c_lastacc[kMaxSendersPerSession];  // lane of the chunk's newest accepted packet, per socket
     // per packet of the current chunk
     __shared__ uint8_t p_snd[THREADS];
     __shared__ uint8_t p_acc[THREADS];
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         s_meta[tid] = D.meta; s_ring[tid] = D.ring;
     }
     if (tid < (int)S.ntracks) s_count[tid] = P.streams[S.first_stream + tid].packet_count;
+    if (tid < (int)nsnd) c_lastacc[tid] = -1;
     __syncthreads();
 
     uint64_t in_pk = 0, in_bytes = 0;
@@ -211,12 +213,10 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         // ---- SSRC latch filter (sequential per socket; fast path when nothing changes) ----
         if (P.filter_ssrc) {
             const bool ok = !acc || (s_valid[ls] != 0 && p_ssrc[tid] == s_valid[ls]);
+            if (acc) atomicMax(&c_lastacc[ls], tid);       // newest accepted packet per socket
             const int allok = __syncthreads_and(ok ? 1 : 0);
             if (allok) {
-                if (tid < (int)nsnd) {                     // newest accepted packet per socket
-                    for (int p = (int)n - 1; p >= 0; p--)
-                        if (p_acc[p] && p_snd[p] == tid) { s_lastv[tid] = p_ts[p]; break; }
-                }
+                if (tid < (int)nsnd && c_lastacc[tid] >= 0) s_lastv[tid] = p_ts[c_lastacc[tid]];
             } else if (tid == 0) {
                 for (uint32_t p = 0; p < n; p++) {
                     if (!p_acc[p]) continue;
@@ -413,6 +413,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
             s_vbyte[tid] += t >> 20;
         }
         if (tid < (int)S.ntracks) s_count[tid] += c_ttot[tid];
+        if (tid < (int)nsnd) c_lastacc[tid] = -1;
         __syncthreads();
     }
 
