@@ -77,7 +77,7 @@ struct SenderDev {
     int64_t  new_start;             // fFirstPacketInQueueForNewOutput, -1 = NULL
     uint64_t tail;                  // oldest index still intact in both rings
     uint64_t umin;                  // min range start over this sender's sub-streams
-    uint32_t chunk_base, nchunks;   // fan-out work items
+    uint32_t _pad_items[2];
     uint64_t fan_lo, fan_vlo;       // oldest packet index / vbyte the last fan-out reads
 };
 
@@ -263,13 +263,6 @@ struct TickParams {
     uint32_t nsubs;
     uint32_t nsub_blocks;
     uint32_t chunk;                 // packets per fan-out work item (per kernel variant)
-    uint32_t order;                 // work-item order: 0 sender-major, 1 newest chunks first (kFanRanks)
 };
-
-// Newest-chunks-first work order (TickParams.order 1): items are grouped by their chunk's rank
-// counted from the sender's newest packet, rank 0 first; ranks >= kFanRanks - 1 share the last
-// group.  Each group's cursor sits on its own 64-B line (kFanCursorStride words).
-constexpr uint32_t kFanRanks = 512;
-constexpr uint32_t kFanCursorStride = 16;
 
 }  // namespace edgpu

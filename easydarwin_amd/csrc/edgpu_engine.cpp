@@ -189,8 +189,8 @@ struct edgpu_ctx {
     DevVec<FanSub> d_fansub;
     DevVec<edgpu_substream_out> d_sub_out;
     DevVec<FanWork> d_work;
-    DevVec<uint64_t> d_blk_bytes, d_blk_bytes_base;
-    DevVec<uint32_t> d_blk_count, d_blk_count_base;
+    DevVec<uint64_t> d_blk_bytes;
+    DevVec<uint32_t> d_blk_count;
     bool index_dirty = true;
 
     // ingest staging
@@ -252,8 +252,6 @@ struct edgpu_ctx {
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
     TickTotals* d_totals = nullptr;
-    uint32_t* d_rank = nullptr;     // newest-chunks-first order: group bases + cursors
-    uint32_t fan_order = 0;         // EDGPU_FAN_ORDER: 0 sender-major work items, 1 newest chunks first
 };
 
 extern "C" {
@@ -328,9 +326,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
-    if (dmalloc(&x->d_rank, (size_t)kFanRanks * (1 + kFanCursorStride) * 4) != hipSuccess) return bad("rank groups");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
-    if (const char* v = getenv("EDGPU_FAN_ORDER")) x->fan_order = atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 2);
@@ -346,7 +342,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     for (void* p : x->ring_allocs) (void)hipFree(p);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
-    x->d_blk_bytes.release(); x->d_blk_bytes_base.release(); x->d_blk_count.release(); x->d_blk_count_base.release();
+    x->d_blk_bytes.release(); x->d_blk_count.release();
     x->d_img_plan.release(); x->d_sub_out_buf2.release();
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
@@ -363,7 +359,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
-                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals, (void*)x->d_rank})
+                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->h2d) (void)hipStreamSynchronize(x->h2d);
@@ -893,9 +889,7 @@ static int rebuild_index(edgpu_ctx* x) {
     HIP_CHECK(x->d_sub_out.reserve(std::max<uint32_t>(nsub, 1), x->stream));
     if (x->overlap) HIP_CHECK(x->d_sub_out_buf2.reserve(std::max<uint32_t>(nsub, 1), x->stream));
     HIP_CHECK(x->d_blk_bytes.reserve(std::max<uint32_t>(nblk, 1), x->stream));
-    HIP_CHECK(x->d_blk_bytes_base.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_count.reserve(std::max<uint32_t>(nblk, 1), x->stream));
-    HIP_CHECK(x->d_blk_count_base.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_work.reserve(std::max<uint64_t>(x->work_cap_needed, 1), x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
     x->index_dirty = false;
@@ -1206,7 +1200,6 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
     p.sub_out = sub_out; p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
-    p.blk_bytes_base = x->d_blk_bytes_base.ptr; p.blk_count_base = x->d_blk_count_base.ptr;
     p.totals = x->d_totals;
     p.T.now = now_ms;
     p.T.over_buffer_ms = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
@@ -1216,8 +1209,6 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
     p.T.chunk = (uint32_t)fanout_chunk(x->fanout_variant);
-    p.T.order = x->fan_order;
-    p.rank_base = x->d_rank;
     // the per-tick totals (relayed_*, arena, status, nwork) are reset by the plan's first kernel
     HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));

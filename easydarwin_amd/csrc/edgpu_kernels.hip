@@ -598,7 +598,6 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
         D.tail = tail;
         D.new_start = ns;
         D.umin = head;
-        D.nchunks = 0;
     }
 }
 
@@ -704,97 +703,45 @@ __device__ __forceinline__ T wave_block_inclusive_scan(T v, T* wsum) {
     return v + base;
 }
 
-// K3: single workgroup -- scans over K2 block partials and over senders' chunk counts.
-__global__ __launch_bounds__(1024) void k_plan_scan(PlanParams P) {
-    const int tid = threadIdx.x;
-    const int nt = blockDim.x;
-    __shared__ uint64_t sh64[16];
-    __shared__ uint32_t sh32[16];
-    // (a) block partial scan
-    {
-        const uint32_t n = P.T.nsub_blocks;
-        const uint32_t per = (n + nt - 1) / nt;
-        const uint32_t b0 = tid * per, b1 = min(n, b0 + per);
-        uint64_t sbytes = 0; uint32_t scount = 0;
-        for (uint32_t i = b0; i < b1; i++) { sbytes += P.blk_bytes[i]; scount += P.blk_count[i]; }
-        const uint64_t ib = wave_block_inclusive_scan<uint64_t>(sbytes, sh64);
-        const uint32_t ic = wave_block_inclusive_scan<uint32_t>(scount, sh32);
-        uint64_t rb = ib - sbytes; uint32_t rc = ic - scount;
-        for (uint32_t i = b0; i < b1; i++) {
-            P.blk_bytes_base[i] = rb; P.blk_count_base[i] = rc;
-            rb += P.blk_bytes[i]; rc += P.blk_count[i];
-        }
-        if (tid == nt - 1) {
-            P.totals->arena_bytes = ib;
-            P.totals->relayed_packets = ic;
-            P.totals->cum_relayed_packets += ic;
-            if (ib > P.T.arena_bytes || ic > P.T.max_desc)
-                atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
-        }
-        __syncthreads();
-    }
-    // (b) sender chunk scan
-    {
-        const uint32_t n = P.T.nsenders;
-        const uint32_t per = (n + nt - 1) / nt;
-        const uint32_t s0 = tid * per, s1 = min(n, s0 + per);
-        uint32_t sum = 0;
-        for (uint32_t s = s0; s < s1; s++) {
-            const SenderDev& D = P.senders[s];
-            const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
-            sum += (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
-        }
-        const uint32_t isum = wave_block_inclusive_scan<uint32_t>(sum, sh32);
-        uint32_t r = isum - sum;
-        __shared__ uint32_t hist[kFanRanks];
-        if (P.T.order) for (uint32_t b = tid; b < kFanRanks; b += nt) hist[b] = 0;
-        __syncthreads();
-        for (uint32_t s = s0; s < s1; s++) {
-            SenderDev& D = P.senders[s];
-            const uint64_t span = D.head > D.umin ? D.head - D.umin : 0;
-            const uint32_t k = (uint32_t)((span + P.T.chunk - 1) / P.T.chunk);
-            D.chunk_base = r; D.nchunks = k;
-            r += k;
-            if (P.T.order) {                  // this sender's items per rank group
-                for (uint32_t g = 0; g < min(k, kFanRanks - 1); g++) atomicAdd(&hist[g], 1u);
-                if (k >= kFanRanks) atomicAdd(&hist[kFanRanks - 1], k - (kFanRanks - 1));
-            }
-        }
-        if (tid == nt - 1) P.totals->nwork = isum;
-        if (P.T.order) {                      // group bases (exclusive scan), cursors cleared
-            __syncthreads();
-            constexpr uint32_t per = (kFanRanks + 1023) / 1024;
-            uint32_t v[per], tsum = 0;
-            for (uint32_t j = 0; j < per; j++) {
-                const uint32_t b = tid * per + j;
-                v[j] = b < kFanRanks && tid * per < kFanRanks ? hist[b] : 0u;
-                tsum += v[j];
-            }
-            uint32_t base = wave_block_inclusive_scan<uint32_t>(tsum, sh32) - tsum;
-            for (uint32_t j = 0; j < per; j++) {
-                const uint32_t b = tid * per + j;
-                if (b < kFanRanks) { P.rank_base[b] = base; P.rank_base[kFanRanks + b * kFanCursorStride] = 0; }
-                base += v[j];
-            }
-        }
-    }
-}
-
-// K3b: per sub-stream -- final arena / descriptor offsets and the public sub-stream table;
-// per sender -- work items.
+// K3: per sub-stream -- final arena / descriptor offsets and the public sub-stream table;
+// per sender -- work items.  Each block adds up the K2 partials of the blocks before it (a few
+// hundred at most), so the offsets need no separate scan launch; block 0 adds up all of them
+// for the tick totals.  A sender's work items take their place with one atomicAdd on the
+// tick's item count: items are independent, so their order only shapes the copy kernel's
+// schedule (each sender's chunks stay consecutive).
 __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t bytes = 0; uint32_t count = 0;
-    if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
     __shared__ uint64_t sb[4];
     __shared__ uint32_t sc[4];
+    uint64_t base_b = 0; uint32_t base_c = 0;
+    {
+        const uint32_t nb = P.T.nsub_blocks;
+        const uint32_t lim = blockIdx.x == 0 ? nb : min((uint32_t)blockIdx.x, nb);
+        uint64_t xb = 0; uint32_t xc = 0;
+        for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x) { xb += P.blk_bytes[i]; xc += P.blk_count[i]; }
+        uint64_t tb; uint32_t tc;
+        (void)block_exclusive_scan<uint64_t>(xb, sb, tb);
+        (void)block_exclusive_scan<uint32_t>(xc, sc, tc);
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) {
+                P.totals->arena_bytes = tb;
+                P.totals->relayed_packets = tc;
+                P.totals->cum_relayed_packets += tc;
+                if (tb > P.T.arena_bytes || tc > P.T.max_desc) atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
+            }
+        } else {
+            base_b = tb; base_c = tc;
+        }
+    }
+    uint64_t bytes = 0; uint32_t count = 0;
+    if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
     uint64_t tb; uint32_t tc;
     const uint64_t pb = block_exclusive_scan<uint64_t>(bytes, sb, tb);
     const uint32_t pc = block_exclusive_scan<uint32_t>(count, sc, tc);
     if (q < P.T.nsubs) {
         SubDev& Q = P.subs[q];
-        Q.out_base = P.blk_bytes_base[blockIdx.x] + pb;
-        Q.desc_base = P.blk_count_base[blockIdx.x] + pc;
+        Q.out_base = base_b + pb;
+        Q.desc_base = base_c + pc;
         edgpu_substream_out o;
         o.subscriber = Q.handle;
         o.track = Q.track;
@@ -828,11 +775,32 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
     // loads its two boundary records at once instead of walking the chunks one by one.
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; s < P.T.nsenders; s += nwaves) {
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    auto chunks_of = [&](const SenderDev& D) {
+        return (uint32_t)(((D.head > D.umin ? D.head - D.umin : 0) + P.T.chunk - 1) / P.T.chunk);
+    };
+    // the wave's senders are gw, gw + nwaves, ...: lane j reserves the items of the j-th, so its
+    // first 64 senders cost one round of atomics in flight together, not one round trip each
+    uint32_t res_nch = 0, res_base = 0;
+    if (gw + lane * nwaves < P.T.nsenders) {
+        res_nch = chunks_of(P.senders[gw + lane * nwaves]);
+        if (res_nch) res_base = atomicAdd(&P.totals->nwork, res_nch);
+    }
+    uint32_t j = 0;
+    for (uint32_t s = gw; s < P.T.nsenders; s += nwaves, j++) {
         const SenderDev& D = P.senders[s];
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
         const uint64_t head = D.head, umin = D.umin, vend = D.vbyte_end;
-        const uint32_t nch = D.nchunks, chunk_base = D.chunk_base, pkmask = D.pk_mask;
+        const uint32_t pkmask = D.pk_mask;
+        uint32_t nch, chunk_base = 0;
+        if (j < 64) {
+            nch = (uint32_t)__shfl((int)res_nch, (int)j, 64);
+            chunk_base = (uint32_t)__shfl((int)res_base, (int)j, 64);
+        } else {
+            nch = chunks_of(D);
+            if (lane == 0 && nch) chunk_base = atomicAdd(&P.totals->nwork, nch);
+            chunk_base = (uint32_t)__shfl((int)chunk_base, 0, 64);
+        }
         if (lane == 0) {
             SenderDev& Dw = P.senders[s];
             Dw.fan_lo = nch ? umin : head;
@@ -853,12 +821,7 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             it.vc0 = vc0;
             it.lo = lo;
             it.vb0 = vb0;
-            uint32_t pos = chunk_base + k;
-            if (P.T.order) {                  // newest chunks first: rank from the sender's head
-                const uint32_t g = min(nch - 1 - k, kFanRanks - 1);
-                pos = P.rank_base[g] + atomicAdd(&P.rank_base[kFanRanks + g * kFanCursorStride], 1u);
-            }
-            P.work[pos] = it;
+            P.work[chunk_base + k] = it;
         }
     }
 }
@@ -1235,8 +1198,11 @@ __device__ __forceinline__ void fan4_issue(const FanWork& it, int tid, u32x4 (&r
 // use) instead of a static stride over blockIdx, so unequal items cannot leave a long tail.
 // PACE (A/B of store issue rate): 1 every window takes the patch path (an identity window then
 // pays the rewrite's bitmap read per word); 2 s_sleep after every store row.
+// HW: the two halves of the workgroup write two sub-streams' windows at once (each half walks
+// its window with THREADS/2 lanes), so one window's record / offset chain overlaps the other's
+// stores.
 template <int THREADS, int CHUNK, int AUX = 0, int DNT = 0, int LAUX = 0, int SU = 1, int WPE = 0, int PM = 0,
-          int LFS = 0, int DYN = 0, int PACE = 0>
+          int LFS = 0, int DYN = 0, int PACE = 0, int HW = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS), amdgpu_waves_per_eu(WPE ? WPE : 1)))
 void k_fanout4(FanoutParams P) {
     constexpr int CWORDS = CHUNK * kSlotWordsMax;
@@ -1351,7 +1317,10 @@ void k_fanout4(FanoutParams P) {
             }
         }
         // ---- write the chunk to every sub-stream of the sender ----------------------------
-        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+        constexpr uint32_t WT = HW ? THREADS / 2 : THREADS;                    // lanes per window
+        const uint32_t wtid = HW ? (uint32_t)tid % WT : (uint32_t)tid;
+        const uint32_t q0 = HW ? uni((uint32_t)tid / WT) : 0u;
+        for (uint32_t q = it.qb + q0; q < it.qe && !(P.ablate & 2u); q += HW ? 2u : 1u) {
             const FanSub f = fansub(it, q);
             if (f.a >= lo + np) continue;
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -1361,13 +1330,13 @@ void k_fanout4(FanoutParams P) {
             const uint32_t s = (uint32_t)(A & 7);                              // words past a line
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
             const bool patch = PACE == 1 || (f.ch & 1u) || f.rw;               // uniform
-            const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            const uint32_t nj = (nw - fw + s + WT - 1) / WT;
             for (uint32_t j = 0; j < nj; j += SU) {
                 u32x4 v[SU];
                 uint32_t srcc[SU];
 #pragma unroll
                 for (int k = 0; k < SU; k++) {
-                    const uint32_t src = fw + tid + (j + k) * THREADS - s;     // chunk word of the lane's
+                    const uint32_t src = fw + wtid + (j + k) * WT - s;         // chunk word of the lane's
                     srcc[k] = src < (uint32_t)CWORDS ? src : 0u;               // word of the aligned window
                     if (k == 0 || j + k < nj) v[k] = cbuf[srcc[k]];            // uniform guard
                 }
@@ -1378,12 +1347,12 @@ void k_fanout4(FanoutParams P) {
                         if (PM == 0 || (f.rw & kRwRtcp)) {
                             v[k] = fan_patch(v[k], f, srcc[k], sm, cbuf);
                         } else {
-                            const int c0 = (int)(fw + (j + k) * THREADS + wv * 64u) - (int)s;
+                            const int c0 = (int)(fw + (j + k) * WT + (wtid & ~63u)) - (int)s;
                             const uint64_t m = uni64(row_mask(sm, c0, SM));
                             if (m) v[k] = fan_patch_start(v[k], f, (m >> lane) & 1u);
                         }
                     }
-                    __builtin_amdgcn_raw_buffer_store_b128(v[k], os, (tid + (j + k) * THREADS - s) * 16u, 0, AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(v[k], os, (wtid + (j + k) * WT - s) * 16u, 0, AUX);
                 }
                 if constexpr (PACE == 2) __builtin_amdgcn_s_sleep(1);
             }
@@ -1881,7 +1850,6 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3((p.T.nsenders + 3) / 4), dim3(256), 0, st, p);
     else hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 0);
     if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
-    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
     if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
     return hipGetLastError();
@@ -1932,6 +1900,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 48, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 48, fanout4_lds<1024, 48>()}, // 34 48, dynamic
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 35 dyn, patch path always
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 36 dyn, s_sleep per row
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 37 dyn, two windows at once
+    {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 0, 1, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 38 56, dyn, two windows
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1947,7 +1917,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt,ldsfansub>", "k_fanout4<1024,56,nt,ldsfansub>",
                                             "k_fanout4<1024,32,nt,dyn>", "k_fanout4<1024,56,nt,dyn>",
                                             "k_fanout4<1024,32,nt,wpe8,dyn>", "k_fanout4<1024,48,nt,dyn>",
-                                            "k_fanout4<1024,32,nt,dyn,patchall>", "k_fanout4<1024,32,nt,dyn,sleep>"};
+                                            "k_fanout4<1024,32,nt,dyn,patchall>", "k_fanout4<1024,32,nt,dyn,sleep>",
+                                            "k_fanout4<1024,32,nt,dyn,2win>", "k_fanout4<1024,56,nt,dyn,2win>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 31;   // k_fanout4<1024,32>, non-temporal arena stores, items claimed dynamically
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)

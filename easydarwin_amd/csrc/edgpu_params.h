@@ -52,9 +52,6 @@ struct PlanParams {
     FanSub* fansub;             // per sub_index position
     uint64_t* blk_bytes;        // per K2 block partials
     uint32_t* blk_count;
-    uint64_t* blk_bytes_base;
-    uint32_t* blk_count_base;
-    uint32_t* rank_base;        // order 1: kFanRanks group bases, then kFanRanks cursors (strided)
     TickTotals* totals;
     TickParams T;
 };
