@@ -252,6 +252,10 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long cum_ingested_bytes;
     int ingest_status;              // sticky: an ingest lapped data an in-flight fan-out reads
     unsigned int fan_next;          // dynamic fan-out variants: next work item to claim (per tick)
+    unsigned int _pad;
+    // the cumulative ingest counters at the last index update: ingested_* = cum - mark, set by
+    // the keyframe index after every ingest (no reset launch before the ingest)
+    unsigned long long ingest_mark_packets, ingest_mark_bytes;
 };
 
 struct TickParams {

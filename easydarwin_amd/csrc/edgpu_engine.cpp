@@ -22,7 +22,6 @@
 
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
-hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
@@ -911,7 +910,6 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;
-    HIP_CHECK(launch_ingest_reset(x->d_totals, x->stream));
     HIP_CHECK(hist_mark(x, 2, 0));
     if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
@@ -1155,7 +1153,7 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     HIP_CHECK(hipSetDevice(x->device));
     KeyframeParams p;
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr;
+    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.totals = x->d_totals;
     // the index starts where the ingest it indexes ended when the host did nothing in between
     // (that point is already recorded: an event record costs the GPU ~5 us of idle), else here
     const uint32_t kslot = x->hist_n[3] % edgpu_ctx::kHist;

@@ -434,8 +434,6 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
     const uint64_t a2 = block_exclusive_scan<uint64_t, NW>(in_bytes, scan64, t2);
     (void)a1; (void)a2;
     if (tid == 0 && !(P.ablate & 16u)) {
-        atomicAdd(&P.totals->ingested_packets, (unsigned long long)t1);
-        atomicAdd(&P.totals->ingested_bytes, (unsigned long long)t2);
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
     }
@@ -472,8 +470,16 @@ __global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
 // Keyframe index + audio anchor: one wave per session segment.
 // =========================================================================================
 
+// The last ingest's counters from the cumulative ones (run once the ingest has finished).
+__device__ __forceinline__ void mark_ingest_totals(TickTotals* t) {
+    const unsigned long long p = t->cum_ingested_packets, b = t->cum_ingested_bytes;
+    t->ingested_packets = p - t->ingest_mark_packets; t->ingested_bytes = b - t->ingest_mark_bytes;
+    t->ingest_mark_packets = p; t->ingest_mark_bytes = b;
+}
+
 __global__ __launch_bounds__(64) void k_keyframe(KeyframeParams P) {
     const uint32_t seg = blockIdx.x;
+    if (seg == 0 && threadIdx.x == 0) mark_ingest_totals(P.totals);   // the ingest has finished
     const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
     const uint32_t sess = P.seg_sess[seg];
     const SessionDev S = P.sessions[sess];
@@ -560,13 +566,13 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->status = 0; t->nwork = 0; t->fan_next = 0;
 }
 
-// Per-tick counter resets as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
-// kernels): which = 0 fan-out totals (when k_plan_senders, which does it itself, does not run),
-// 1 ingest totals.
+// Per-tick counter updates as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
+// kernels): which = 0 fan-out totals reset (when k_plan_senders, which does it itself, does not
+// run), 1 the ingest counters of an empty batch (when k_keyframe, which does it itself, does not).
 __global__ void k_totals_reset(TickTotals* t, int which) {
     if (threadIdx.x != 0) return;
     if (which == 0) reset_tick_totals(t);
-    else { t->ingested_packets = 0; t->ingested_bytes = 0; }
+    else mark_ingest_totals(t);
 }
 
 __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
@@ -1408,6 +1414,188 @@ void k_fanout4(FanoutParams P) {
 }
 
 // -----------------------------------------------------------------------------------------
+// k_fanout6: k_fanout4<..., nt, dyn> with TWO LDS images and one barrier per work item.
+// k_fanout4 fills its single image from the prefetch registers, waits at a barrier, writes the
+// item out, and waits again before the image may be refilled: every wave idles twice per item
+// while the slowest one catches up.  Here a wave that has written out item i from image i&1
+// fills image (i+1)&1 from the registers right away -- the other waves may still be reading
+// image i&1 -- and the one barrier then means both "image i+1 complete" and "image i free".
+// The slot-start bitmaps rotate through three buffers so that each is cleared one barrier
+// before it is filled.  LDS: two 66-KB images (one 1024-thread workgroup per CU, as k_fanout4's
+// default already runs).
+// -----------------------------------------------------------------------------------------
+template <int THREADS, int CHUNK>
+struct Fan6 {
+    static constexpr int CWORDS = CHUNK * kSlotWordsMax;
+    static constexpr int NL = (CWORDS + THREADS - 1) / THREADS;
+    static constexpr int NWAVES = THREADS / 64;
+    static constexpr int SM = ((CWORDS + 31) / 32 + 3) & ~3;
+    // per image: chunk words, then m_vb (CHUNK + 2 x u64), m_id / m_len / m_vc / m_nzp (CHUNK x u32)
+    static constexpr int IMG = CWORDS * 16 + (CHUNK + 2) * 8 + 4 * CHUNK * 4;
+    static constexpr int lds() { return 2 * IMG + 3 * SM * 4 + NWAVES * 8; }
+};
+template <int THREADS, int CHUNK>
+constexpr int fanout6_lds() { return Fan6<THREADS, CHUNK>::lds(); }
+
+template <int THREADS, int CHUNK, int AUX = 2>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanout6(FanoutParams P) {
+    using F = Fan6<THREADS, CHUNK>;
+    constexpr int CWORDS = F::CWORDS, NL = F::NL, NWAVES = F::NWAVES, SM = F::SM;
+    static_assert(CHUNK <= 56, "descriptor windows assume one wave covers a chunk's packets");
+    const uint32_t nwork = uni(P.totals->nwork);
+    if (uni((uint32_t)P.totals->status) == (uint32_t)EDGPU_OUT_OVERFLOW) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wv = uni((uint32_t)tid >> 6);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    struct Img { u32x4* cb; uint64_t* vb; uint32_t *id, *len, *vc, *nzp; };
+    auto img = [&](uint32_t b) {
+        unsigned char* base = lds + b * F::IMG;
+        Img m;
+        m.cb = reinterpret_cast<u32x4*>(base);
+        m.vb = reinterpret_cast<uint64_t*>(base + CWORDS * 16);
+        m.id = reinterpret_cast<uint32_t*>(m.vb + CHUNK + 2);
+        m.len = m.id + CHUNK; m.vc = m.len + CHUNK; m.nzp = m.vc + CHUNK;
+        return m;
+    };
+    uint32_t* smb = reinterpret_cast<uint32_t*>(lds + 2 * F::IMG);       // 3 x SM bitmap words
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smb + 3 * SM);
+    u32x4* out = reinterpret_cast<u32x4*>(P.arena);
+    unsigned long long wire = 0, inb = 0;
+    u32x4 r[NL];
+    u32x3 ma;
+    u32x2 mb;
+    __shared__ uint32_t s_claim[2];
+
+    // one item's LDS image and slot-start bitmap (bitmap `sm` cleared beforehand), from the
+    // registers its loads landed in
+    auto fill = [&](const FanWork& it, const Img& m, uint32_t* sm) {
+        const uint32_t nw = it.nw, np = it.np;
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+            const uint32_t wi = tid + j * THREADS;
+            if ((uint32_t)(j * THREADS) < nw && wi < nw) m.cb[wi] = r[j];
+        }
+        if ((uint32_t)tid < np) {
+            const uint64_t vbyte = (uint64_t)ma.y << 32 | ma.x;
+            const uint32_t len = mb.x & 0xFFFFu, vcount = mb.y;          // len:16 | seq:16
+            m.vb[tid] = vbyte; m.id[tid] = ma.z; m.len[tid] = len; m.vc[tid] = vcount;
+            inb += len;
+            if (len != 0) {
+                const uint32_t sw = (uint32_t)((vbyte - it.vb0) >> 4);
+                atomicOr(&sm[sw >> 5], 1u << (sw & 31));
+                m.nzp[vcount - it.vc0] = tid;
+            }
+        }
+        if (tid == 0) m.vb[np] = it.vb0 + (uint64_t)nw * 16;
+    };
+
+    for (int k = tid; k < 3 * SM; k += THREADS) smb[k] = 0;
+    if (tid == 0) { s_claim[0] = atomicAdd(&P.totals->fan_next, 1u); s_claim[1] = atomicAdd(&P.totals->fan_next, 1u); }
+    __syncthreads();
+    uint32_t w = s_claim[0], wnext = s_claim[1];
+    FanWork cur, nx;
+    if (w < nwork) {
+        cur = const_load(P.work + w);
+        fan4_issue<THREADS, NL>(cur, tid, r, ma, mb);
+        fill(cur, img(0), smb);
+    }
+    if (wnext < nwork) {
+        nx = const_load(P.work + wnext);
+        fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+    }
+    __syncthreads();                                   // image 0 complete; s_claim read by all
+    if (tid == 0) s_claim[0] = atomicAdd(&P.totals->fan_next, 1u);      // the item after next
+    for (uint32_t i = 0; w < nwork; i++) {
+        const FanWork it = cur;
+        const Img m = img(i & 1u);
+        uint32_t* sm = smb + (i % 3u) * SM;
+        const uint64_t lo = it.lo, vb0 = it.vb0;
+        const uint32_t np = it.np, nw = it.nw, vc0 = it.vc0;
+        // ---- write the chunk to every sub-stream of the sender ----------------------------
+        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+            const FanSub f = const_load(P.fansub + q);
+            if (f.a >= lo + np) continue;
+            const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+            const uint32_t fw = uni((uint32_t)((m.vb[p0] - vb0) >> 4));
+            const int64_t A = f.dw + (int64_t)(vb0 >> 4) + fw;                 // first dest word
+            if (A < 0 || (uint64_t)A + (nw - fw) > P.arena_words) { set_status(&P.totals->status, EDGPU_OUT_OVERFLOW); continue; }
+            const uint32_t s = (uint32_t)(A & 7);                              // words past a line
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
+            const bool patch = (f.ch & 1u) || f.rw;                            // uniform
+            const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            for (uint32_t j = 0; j < nj; j++) {
+                const uint32_t src = fw + tid + j * THREADS - s;               // chunk word of the lane's
+                const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;       // word of the aligned window
+                u32x4 v = m.cb[srcc];
+                if (patch) v = fan_patch(v, f, srcc, sm, m.cb);
+                __builtin_amdgcn_raw_buffer_store_b128(v, os, (tid + j * THREADS - s) * 16u, 0, AUX);
+            }
+        }
+        // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
+        {
+            const uint32_t nzc = np ? m.vc[np - 1] - vc0 + (m.len[np - 1] != 0) : 0u;
+            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+                const FanSub f = const_load(P.fansub + q);
+                if (f.a >= lo + np) continue;
+                const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
+                const uint32_t o0 = m.vc[p0] - vc0;                            // first ordinal
+                if (o0 >= nzc) continue;
+                const uint32_t d0 = f.db + m.vc[p0];
+                const uint32_t sh = d0 & 7;
+                const uint32_t o = o0 + lane - sh;
+                if ((uint32_t)lane >= sh && o < nzc) {
+                    const uint32_t p = m.nzp[o];
+                    const uint32_t len = m.len[p];
+                    const uint64_t off = (uint64_t)(f.off + (int64_t)m.vb[p]);
+                    const uint32_t wlen = len + ((f.ch & 1u) ? 4u : 0u);
+                    u32x4 dv;
+                    dv.x = (uint32_t)off; dv.y = (uint32_t)(off >> 32); dv.z = wlen; dv.w = m.id[p];
+                    if (d0 - sh + lane < P.max_desc) reinterpret_cast<u32x4*>(P.desc)[d0 - sh + lane] = dv;
+                    wire += wlen;
+                }
+            }
+        }
+        // ---- the next item's image, while other waves may still read this one ------------
+        // Bitmap buffers rotate by three: item i+2's (last read by item i-1, before the previous
+        // barrier) is cleared now, one barrier before it is filled; item i+1's was cleared one
+        // item ago.
+        {
+            uint32_t* sc = smb + ((i + 2) % 3u) * SM;
+            for (int k = tid; k < SM; k += THREADS) sc[k] = 0;
+        }
+        if (wnext < nwork) fill(nx, img((i + 1) & 1u), smb + ((i + 1) % 3u) * SM);
+        __syncthreads();                     // image i+1 complete, image i free, s_claim visible
+        cur = nx;
+        w = wnext;
+        wnext = s_claim[i & 1u];
+        if (wnext < nwork) {
+            nx = const_load(P.work + wnext);
+            fan4_issue<THREADS, NL>(nx, tid, r, ma, mb);
+        }
+        if (tid == 0) s_claim[(i + 1) & 1u] = atomicAdd(&P.totals->fan_next, 1u);
+    }
+    unsigned long long a = wire, b = inb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+    if (lane == 0) s_red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int k = 0; k < NWAVES; k++) tot += s_red[k];
+        if (tot) { atomicAdd(&P.totals->relayed_bytes, tot); atomicAdd(&P.totals->cum_relayed_bytes, tot); }
+    }
+    __syncthreads();
+    if (lane == 0) s_red[tid >> 6] = b;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long tot = 0;
+        for (int k = 0; k < NWAVES; k++) tot += s_red[k];
+        if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
+    }
+}
+
+// -----------------------------------------------------------------------------------------
 // k_fanout5: the write-many at low wave count with asynchronous chunk staging.  Measured on
 // the box (tools/store_peak3.hip): the same line-aligned window stores reach ~5.8 TB/s with 4
 // waves per CU and no load phases, against ~5.3 TB/s at 32 waves per CU with load phases
@@ -1804,10 +1992,6 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
     return hipGetLastError();
 }
 
-hipError_t launch_ingest_reset(TickTotals* totals, hipStream_t st) {
-    hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, totals, 1);
-    return hipGetLastError();
-}
 
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
@@ -1841,7 +2025,10 @@ hipError_t launch_blocked(const BlockedParams& p, hipStream_t st) {
 }
 
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {
-    if (nseg == 0) return hipSuccess;
+    if (nseg == 0) {                         // still the (empty) ingest's counters
+        hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 1);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_keyframe, dim3(nseg), dim3(64), 0, st, p);
     return hipGetLastError();
 }
@@ -1902,6 +2089,11 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 2>, 1024, 32, fanout4_lds<1024, 32>()}, // 36 dyn, s_sleep per row
     {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 37 dyn, two windows at once
     {(const void*)k_fanout4<1024, 56, 2, 0, 0, 1, 0, 0, 0, 1, 0, 1>, 1024, 56, fanout4_lds<1024, 56>()}, // 38 56, dyn, two windows
+    {(const void*)k_fanout6<1024, 32>, 1024, 32, fanout6_lds<1024, 32>()},          // 39 two images, one barrier per item
+    {(const void*)k_fanout6<1024, 16>, 1024, 16, fanout6_lds<1024, 16>()},          // 40 same, 16-packet chunks (2 WG/CU)
+    {(const void*)k_fanout6<1024, 18>, 1024, 18, fanout6_lds<1024, 18>()},          // 41 18 packets (2 WG/CU)
+    {(const void*)k_fanout6<1024, 12>, 1024, 12, fanout6_lds<1024, 12>()},          // 42 12 packets (2 WG/CU)
+    {(const void*)k_fanout6<512, 16>, 512, 16, fanout6_lds<512, 16>()},             // 43 16 packets, 512 threads
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -1918,7 +2110,9 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt,dyn>", "k_fanout4<1024,56,nt,dyn>",
                                             "k_fanout4<1024,32,nt,wpe8,dyn>", "k_fanout4<1024,48,nt,dyn>",
                                             "k_fanout4<1024,32,nt,dyn,patchall>", "k_fanout4<1024,32,nt,dyn,sleep>",
-                                            "k_fanout4<1024,32,nt,dyn,2win>", "k_fanout4<1024,56,nt,dyn,2win>"};
+                                            "k_fanout4<1024,32,nt,dyn,2win>", "k_fanout4<1024,56,nt,dyn,2win>",
+                                            "k_fanout6<1024,32,nt,dyn>", "k_fanout6<1024,16,nt,dyn>",
+                                            "k_fanout6<1024,18,nt,dyn>", "k_fanout6<1024,12,nt,dyn>", "k_fanout6<512,16,nt,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static const int kDefaultVariant = 31;   // k_fanout4<1024,32>, non-temporal arena stores, items claimed dynamically
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)

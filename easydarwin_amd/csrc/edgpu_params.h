@@ -39,6 +39,7 @@ struct KeyframeParams {
     const uint64_t* pidx;
     SessionDev* sessions;
     SenderDev* senders;
+    TickTotals* totals;
 };
 
 struct PlanParams {
