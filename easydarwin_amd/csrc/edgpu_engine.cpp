@@ -36,6 +36,7 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
 int fanout_chunk(int variant);
+int fanout_default(bool patching);
 bool fanout_rewrites(int variant);
 const char* fanout_name(int variant);
 }  // namespace edgpu
@@ -130,6 +131,7 @@ struct SubscriberHost {
     uint32_t first_sub;         // first SubDev index
     uint32_t nsub;
     bool active;
+    int transport;
 };
 
 struct edgpu_ctx {
@@ -174,6 +176,7 @@ struct edgpu_ctx {
     std::vector<uint8_t> sub_active;
     std::vector<uint8_t> sub_rw;        // host mirror: SubDev has a non-identity rewrite
     uint32_t n_rw = 0;                  // active sub-streams with a rewrite
+    uint32_t n_tcp = 0;                 // active RTSP-interleaved sub-streams (channel-byte patch)
     uint32_t nsenders = 0, nstreams = 0;
     std::vector<void*> ring_allocs;
     uint64_t work_cap_needed = 0;
@@ -589,7 +592,8 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             x->sub_rw.push_back(0);
             v.push_back(Q);
         }
-    x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true});
+    x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true, transport});
+    if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += 2 * sh.ntracks;
     x->sessions[session].eyes++;                 // AddOutput(..., isClient) -> IncEyeCount
     x->index_dirty = true;
     return handle;
@@ -709,6 +713,7 @@ int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     }
     HIP_CHECK(hipStreamSynchronize(x->stream));
     s.active = false;
+    if (s.transport == EDGPU_TRANSPORT_TCP) x->n_tcp -= s.nsub;
     x->sessions[s.session].eyes--;               // RemoveOutput(..., isClient) -> DecEyeCount
     x->index_dirty = true;
     return EDGPU_OK;
@@ -1175,6 +1180,12 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     return EDGPU_OK;
 }
 
+// The copy kernel for this tick: EDGPU_FANOUT when set, else the default for whether any active
+// sub-stream needs a per-output patch (TCP channel byte or rewrite).
+static int pick_fanout_variant(const edgpu_ctx* x) {
+    return x->fanout_variant >= 0 ? x->fanout_variant : fanout_default(x->n_rw + x->n_tcp > 0);
+}
+
 int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
@@ -1206,7 +1217,8 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsenders = x->nsenders;
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
-    p.T.chunk = (uint32_t)fanout_chunk(x->fanout_variant);
+    const int variant = pick_fanout_variant(x);
+    p.T.chunk = (uint32_t)fanout_chunk(variant);
     // the per-tick totals (relayed_*, arena, status, nwork) are reset by the plan's first kernel
     HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));
@@ -1224,7 +1236,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
         cs = x->copy;
     }
     HIP_CHECK(hist_mark(x, 0, 0, cs));
-    HIP_CHECK(launch_fanout(f, x->fanout_variant, x->num_cus, cs));
+    HIP_CHECK(launch_fanout(f, variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
     {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
         const uint32_t s1 = x->hist_n[1];
@@ -1245,7 +1257,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
 }
 
 const char* edgpu_fanout_kernel(edgpu_ctx* x) {
-    return x ? fanout_name(x->fanout_variant) : "";
+    return x ? fanout_name(pick_fanout_variant(x)) : "";
 }
 
 int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {

@@ -2048,7 +2048,7 @@ static int occupancy_of(const void* fn, int threads, int lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, lds) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }
-struct FanoutVariant { const void* fn; int threads; int chunk; int lds; };
+struct FanoutVariant { const void* fn; int threads; int chunk; int lds; int max_wg_per_cu = 0; };
 static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout3<1024, 32>, 1024, 32, fanout3_lds<1024, 32>()},          // 0 r01 LDS, aligned
     {(const void*)k_fanout3<512, 16>, 512, 16, fanout3_lds<512, 16>()},             // 1
@@ -2094,6 +2094,9 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout6<1024, 18>, 1024, 18, fanout6_lds<1024, 18>()},          // 41 18 packets (2 WG/CU)
     {(const void*)k_fanout6<1024, 12>, 1024, 12, fanout6_lds<1024, 12>()},          // 42 12 packets (2 WG/CU)
     {(const void*)k_fanout6<512, 16>, 512, 16, fanout6_lds<512, 16>()},             // 43 16 packets, 512 threads
+    {(const void*)k_fanout6<1024, 16>, 1024, 16, fanout6_lds<1024, 16>(), 1},       // 44 = 40 at one workgroup per CU
+    {(const void*)k_fanout6<1024, 18>, 1024, 18, fanout6_lds<1024, 18>(), 1},       // 45 = 41 at one workgroup per CU
+    {(const void*)k_fanout4<1024, 16, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 16, fanout4_lds<1024, 16>()}, // 46 16, dynamic (k_fanout4)
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2112,9 +2115,20 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,32,nt,dyn,patchall>", "k_fanout4<1024,32,nt,dyn,sleep>",
                                             "k_fanout4<1024,32,nt,dyn,2win>", "k_fanout4<1024,56,nt,dyn,2win>",
                                             "k_fanout6<1024,32,nt,dyn>", "k_fanout6<1024,16,nt,dyn>",
-                                            "k_fanout6<1024,18,nt,dyn>", "k_fanout6<1024,12,nt,dyn>", "k_fanout6<512,16,nt,dyn>"};
+                                            "k_fanout6<1024,18,nt,dyn>", "k_fanout6<1024,12,nt,dyn>", "k_fanout6<512,16,nt,dyn>",
+                                            "k_fanout6<1024,16,nt,dyn,1wg>", "k_fanout6<1024,18,nt,dyn,1wg>",
+                                            "k_fanout4<1024,16,nt,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-static const int kDefaultVariant = 31;   // k_fanout4<1024,32>, non-temporal arena stores, items claimed dynamically
+static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
+              "one name per fan-out variant");
+// Defaults (items claimed dynamically, non-temporal arena stores): k_fanout6<1024,16> when no
+// sub-stream of the tick needs a per-output patch (all UDP, identity: the reference's parity
+// mode), k_fanout4<1024,32> when some do (RTSP-interleaved channel byte or a rewrite).  The
+// 16-packet chunks are ~4 % faster on identity windows but ~25 % slower through the patch path
+// (profiles/r02z9_*).
+static const int kDefaultVariant = 31;   // k_fanout4<1024,32,nt,dyn>: the patching default
+static const int kDefaultPlain = 40;     // k_fanout6<1024,16,nt,dyn>: every sub-stream identity UDP
+int fanout_default(bool patching) { return patching ? kDefaultVariant : kDefaultPlain; }
 // k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
 bool fanout_rewrites(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
@@ -2135,6 +2149,7 @@ hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStr
     if (!occ[variant]) {
         if (v.lds > 48 * 1024) (void)hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, v.lds);
         occ[variant] = occupancy_of(v.fn, v.threads, v.lds);
+        if (v.max_wg_per_cu && occ[variant] > v.max_wg_per_cu) occ[variant] = v.max_wg_per_cu;
     }
     void* args[] = {(void*)&p};
     return hipLaunchKernel(v.fn, dim3(num_cus * occ[variant]), dim3(v.threads), args, v.lds, st);

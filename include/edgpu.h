@@ -459,7 +459,9 @@ typedef struct edgpu_region {
 int  edgpu_arena_gather(edgpu_ctx* ctx, const edgpu_fanout_result* r, const edgpu_region* regions, uint32_t n,
                         void* dst_device, uint64_t dst_cap);
 
-/* Name of the fan-out copy kernel this context launches (for measurement reports). */
+/* Name of the fan-out copy kernel this context's next edgpu_fanout launches (for measurement
+ * reports): unless EDGPU_FANOUT selects one, it depends on whether any active sub-stream is
+ * RTSP-interleaved or rewrites (a per-output patch), see DESIGN.md §3. */
 const char* edgpu_fanout_kernel(edgpu_ctx* ctx);
 
 /* Cumulative counters since context creation (syncs).  fanout_in_bytes counts the
