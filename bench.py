@@ -394,11 +394,10 @@ def main():
 
     fan_ms = float(np.mean(k_fan)) if k_fan else float("nan")
     achieved = (alg_bytes / max(launches, 1)) / (fan_ms / 1e3) / 1e9
-    # HBM traffic per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # kernel and config (tools/profile.sh + tools/summarize_profile.py); null when absent
     # HBM traffic per launch from the committed rocprofv3 PMC passes of exactly this kernel
     # variant and workload (tools/profile.sh + tools/summarize_profile.py); null otherwise
     traffic, traffic_source = None, None
+    rewrite_desc = "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)"
     pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
     if os.path.exists(pmc) and world == 1:
         try:
@@ -406,7 +405,8 @@ def main():
             wl = pj.get("workload", {})
             if (pj.get("bench_fanout_kernel") == ctx.fanout_kernel() and wl.get("sessions_per_gpu") == args.sessions
                     and wl.get("subs_per_session") == args.subs and wl.get("ingest") == args.ingest
-                    and wl.get("tick_ms", 1000) == args.tick_ms):
+                    and wl.get("tick_ms", 1000) == args.tick_ms
+                    and wl.get("rewrite", "identity (reference parity mode)") == rewrite_desc):
                 traffic = pj.get("hbm_bytes_per_launch")
                 traffic_source = f"profiles/{pj.get('tag')}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes)"
         except Exception:
@@ -439,7 +439,7 @@ def main():
                    "ingest": args.ingest,
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
                    "tick_ms": args.tick_ms,
-                   "rewrite": "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)",
+                   "rewrite": rewrite_desc,
                    "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"},
         "relayed_GBps": round(out_all / dt / 1e9, 2),

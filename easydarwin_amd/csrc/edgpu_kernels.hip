@@ -2097,6 +2097,9 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout6<1024, 16>, 1024, 16, fanout6_lds<1024, 16>(), 1},       // 44 = 40 at one workgroup per CU
     {(const void*)k_fanout6<1024, 18>, 1024, 18, fanout6_lds<1024, 18>(), 1},       // 45 = 41 at one workgroup per CU
     {(const void*)k_fanout4<1024, 16, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 16, fanout4_lds<1024, 16>()}, // 46 16, dynamic (k_fanout4)
+    {(const void*)k_fanout4<1024, 16, 2, 0, 0, 1, 0, 1, 0, 1>, 1024, 16, fanout4_lds<1024, 16>()}, // 47 16, dynamic, row-mask patch
+    {(const void*)k_fanout4<1024, 24, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 24, fanout4_lds<1024, 24>()}, // 48 24, dynamic
+    {(const void*)k_fanout4<1024, 24, 2, 0, 0, 1, 0, 1, 0, 1>, 1024, 24, fanout4_lds<1024, 24>()}, // 49 24, dynamic, row-mask patch
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2117,7 +2120,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<1024,32,nt,dyn>", "k_fanout6<1024,16,nt,dyn>",
                                             "k_fanout6<1024,18,nt,dyn>", "k_fanout6<1024,12,nt,dyn>", "k_fanout6<512,16,nt,dyn>",
                                             "k_fanout6<1024,16,nt,dyn,1wg>", "k_fanout6<1024,18,nt,dyn,1wg>",
-                                            "k_fanout4<1024,16,nt,dyn>"};
+                                            "k_fanout4<1024,16,nt,dyn>", "k_fanout4<1024,16,nt,rowmask,dyn>",
+                                            "k_fanout4<1024,24,nt,dyn>", "k_fanout4<1024,24,nt,rowmask,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");

@@ -51,7 +51,7 @@ fan_name = next((k for k in res["kernels"] if k.startswith("k_fanout")), None)
 fan = res["kernels"].get(fan_name, {})
 res["fanout_kernel"] = fan_name                              # rocprofv3 -T (truncated) name
 res["bench_fanout_kernel"] = bench["roofline"]["kernel"]     # the engine's variant name (template args)
-res["workload"] = {k: bench["config"].get(k) for k in ("sessions_per_gpu", "subs_per_session", "ingest", "tick_ms")}
+res["workload"] = {k: bench["config"].get(k) for k in ("sessions_per_gpu", "subs_per_session", "ingest", "tick_ms", "rewrite")}
 res["hbm_bytes_per_launch"] = fan.get("hbm_bytes_per_launch")
 res["alg_bytes_per_launch"] = bench["roofline"]["alg_bytes_per_launch"]
 res["bench_avg_kernel_ms"] = bench["roofline"]["avg_kernel_ms"]
