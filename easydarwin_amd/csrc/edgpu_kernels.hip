@@ -1437,7 +1437,11 @@ struct Fan6 {
 template <int THREADS, int CHUNK>
 constexpr int fanout6_lds() { return Fan6<THREADS, CHUNK>::lds(); }
 
-template <int THREADS, int CHUNK, int AUX = 2>
+// PP: the per-output patch as per-packet fix-ups.  The rows store every word that is not a
+// packet's first word (nor, for an RTCP rewrite, its second); then one wave writes those words,
+// patched, one lane per packet of the window.  The words are disjoint, so no ordering is
+// needed, and the patch arithmetic runs once per packet instead of on every stored word.
+template <int THREADS, int CHUNK, int AUX = 2, int PP = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanout6(FanoutParams P) {
     using F = Fan6<THREADS, CHUNK>;
     constexpr int CWORDS = F::CWORDS, NL = F::NL, NWAVES = F::NWAVES, SM = F::SM;
@@ -1524,6 +1528,33 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
             const bool patch = (f.ch & 1u) || f.rw;                            // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            if (PP && patch) {
+                const bool second = (f.rw & kRwRtcp) != 0;                     // the SR timestamp word too
+                for (uint32_t j = 0; j < nj; j++) {
+                    const uint32_t src = fw + tid + j * THREADS - s;
+                    const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;
+                    const u32x4 v = m.cb[srcc];
+                    bool skip = (sm[srcc >> 5] >> (srcc & 31)) & 1u;
+                    if (second && srcc > 0) skip |= (sm[(srcc - 1) >> 5] >> ((srcc - 1) & 31)) & 1u;
+                    if (!skip) __builtin_amdgcn_raw_buffer_store_b128(v, os, (tid + j * THREADS - s) * 16u, 0, AUX);
+                }
+                if (wv == (q - it.qb) % NWAVES) {                              // one wave: the packets
+                    const uint32_t p = p0 + lane;
+                    const uint32_t len = p < np ? m.len[p] : 0u;
+                    if (len != 0) {
+                        const uint32_t st = (uint32_t)((m.vb[p] - vb0) >> 4);  // the slot's first word
+                        const u32x4 h = m.cb[st];
+                        __builtin_amdgcn_raw_buffer_store_b128(fan_patch_start(h, f, true), os, (st - fw) * 16u, 0, AUX);
+                        if (second && len >= 13) {                             // a second word in the slot
+                            u32x4 v1 = m.cb[st + 1];
+                            if (len >= 20 && ((h.y >> 8) & 0xFFu) == 200u)     // an SR: its RTP timestamp
+                                v1.y = __builtin_bswap32(__builtin_bswap32(v1.y) + f.rw_ts);
+                            __builtin_amdgcn_raw_buffer_store_b128(v1, os, (st + 1 - fw) * 16u, 0, AUX);
+                        }
+                    }
+                }
+                continue;
+            }
             for (uint32_t j = 0; j < nj; j++) {
                 const uint32_t src = fw + tid + j * THREADS - s;               // chunk word of the lane's
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;       // word of the aligned window
@@ -2100,6 +2131,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 16, 2, 0, 0, 1, 0, 1, 0, 1>, 1024, 16, fanout4_lds<1024, 16>()}, // 47 16, dynamic, row-mask patch
     {(const void*)k_fanout4<1024, 24, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 24, fanout4_lds<1024, 24>()}, // 48 24, dynamic
     {(const void*)k_fanout4<1024, 24, 2, 0, 0, 1, 0, 1, 0, 1>, 1024, 24, fanout4_lds<1024, 24>()}, // 49 24, dynamic, row-mask patch
+    {(const void*)k_fanout6<1024, 16, 2, 1>, 1024, 16, fanout6_lds<1024, 16>()},    // 50 16, per-packet patch
+    {(const void*)k_fanout6<1024, 32, 2, 1>, 1024, 32, fanout6_lds<1024, 32>()},    // 51 32, per-packet patch
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2121,7 +2154,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<1024,18,nt,dyn>", "k_fanout6<1024,12,nt,dyn>", "k_fanout6<512,16,nt,dyn>",
                                             "k_fanout6<1024,16,nt,dyn,1wg>", "k_fanout6<1024,18,nt,dyn,1wg>",
                                             "k_fanout4<1024,16,nt,dyn>", "k_fanout4<1024,16,nt,rowmask,dyn>",
-                                            "k_fanout4<1024,24,nt,dyn>", "k_fanout4<1024,24,nt,rowmask,dyn>"};
+                                            "k_fanout4<1024,24,nt,dyn>", "k_fanout4<1024,24,nt,rowmask,dyn>",
+                                            "k_fanout6<1024,16,nt,dyn,pp>", "k_fanout6<1024,32,nt,dyn,pp>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
