@@ -6,8 +6,13 @@
   never shorter than its copy kernel's, over more ticks than the history holds and across a
   failed RTSP-interleaved ingest (which clears the pending batch without an index);
 * an RTP-Info PLAY on a session with nothing buffered right after a PLAY that found packets
-  reports EDGPU_WOULD_BLOCK (the stale-result regression of DESIGN §4.9).
+  reports EDGPU_WOULD_BLOCK (the stale-result regression of DESIGN §4.9);
+* the copy kernel follows the active sub-streams' need for a per-output patch:
+  k_fanout6<1024,16> while all are identity UDP, k_fanout4<1024,32> while one is TCP or
+  rewrites, and every packet is relayed across the switches.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -123,3 +128,37 @@ def test_contexts_run_concurrently_from_threads():
     for n in names:
         want = json.load(open(os.path.join(gold, n + ".json")))["capture_sha256"]
         assert hashlib.sha256(out[n]).hexdigest() == want, n
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif("EDGPU_FANOUT" in os.environ, reason="EDGPU_FANOUT pins one variant")
+def test_fanout_kernel_follows_patching_substreams():
+    plain, patching = "k_fanout6<1024,16,", "k_fanout4<1024,32,"
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(H264))
+        u = ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+        seq, relayed = 0, 0
+
+        def tick(expect_kernel, expect_relayed):
+            nonlocal seq, relayed
+            assert ctx.fanout_kernel().startswith(expect_kernel)
+            # one IDR packet (the key pointer) first, then non-key slices
+            pk = [(s, 0, 10 * seq + k, _rtp(seq + k, 3000 * seq, payload=(b"\x65" if seq + k == 0 else b"\x41") + b"\x00" * 40))
+                  for k in range(5)]
+            seq += 5
+            _ingest(ctx, pk)
+            ctx.keyframe_index()
+            ctx.fanout(10 * seq)
+            st = ctx.stats()
+            assert st.status == 0
+            assert st.relayed_packets == expect_relayed
+
+        tick(plain, 5)                       # the first tick: the UDP output starts at the key packet
+        t = ctx.subscriber_add(s, edgpu.TRANSPORT_TCP)
+        tick(patching, 15)                   # UDP: 5 new; the joining TCP output: key packet -> newest
+        ctx.subscriber_remove(t)
+        tick(plain, 5)
+        ctx.subscriber_rewrite(u, 0, seq_delta=7)
+        tick(patching, 5)
+        ctx.subscriber_rewrite(u, 0)         # identity again
+        tick(plain, 5)
