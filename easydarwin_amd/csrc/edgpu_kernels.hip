@@ -2133,6 +2133,10 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout4<1024, 24, 2, 0, 0, 1, 0, 1, 0, 1>, 1024, 24, fanout4_lds<1024, 24>()}, // 49 24, dynamic, row-mask patch
     {(const void*)k_fanout6<1024, 16, 2, 1>, 1024, 16, fanout6_lds<1024, 16>()},    // 50 16, per-packet patch
     {(const void*)k_fanout6<1024, 32, 2, 1>, 1024, 32, fanout6_lds<1024, 32>()},    // 51 32, per-packet patch
+    {(const void*)k_fanout6<1024, 14>, 1024, 14, fanout6_lds<1024, 14>()},          // 52 14 packets
+    {(const void*)k_fanout6<1024, 20>, 1024, 20, fanout6_lds<1024, 20>()},          // 53 20
+    {(const void*)k_fanout6<1024, 22>, 1024, 22, fanout6_lds<1024, 22>()},          // 54 22 (a C2 window: 2 rows)
+    {(const void*)k_fanout6<1024, 23>, 1024, 23, fanout6_lds<1024, 23>()},          // 55 23
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2155,7 +2159,9 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<1024,16,nt,dyn,1wg>", "k_fanout6<1024,18,nt,dyn,1wg>",
                                             "k_fanout4<1024,16,nt,dyn>", "k_fanout4<1024,16,nt,rowmask,dyn>",
                                             "k_fanout4<1024,24,nt,dyn>", "k_fanout4<1024,24,nt,rowmask,dyn>",
-                                            "k_fanout6<1024,16,nt,dyn,pp>", "k_fanout6<1024,32,nt,dyn,pp>"};
+                                            "k_fanout6<1024,16,nt,dyn,pp>", "k_fanout6<1024,32,nt,dyn,pp>",
+                                            "k_fanout6<1024,14,nt,dyn>", "k_fanout6<1024,20,nt,dyn>",
+                                            "k_fanout6<1024,22,nt,dyn>", "k_fanout6<1024,23,nt,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
