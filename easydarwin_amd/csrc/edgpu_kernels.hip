@@ -2137,6 +2137,10 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout6<1024, 20>, 1024, 20, fanout6_lds<1024, 20>()},          // 53 20
     {(const void*)k_fanout6<1024, 22>, 1024, 22, fanout6_lds<1024, 22>()},          // 54 22 (a C2 window: 2 rows)
     {(const void*)k_fanout6<1024, 23>, 1024, 23, fanout6_lds<1024, 23>()},          // 55 23
+    {(const void*)k_fanout6<768, 16>, 768, 16, fanout6_lds<768, 16>()},             // 56 768 threads: a C2 window in 2 rows
+    {(const void*)k_fanout6<768, 18>, 768, 18, fanout6_lds<768, 18>()},             // 57
+    {(const void*)k_fanout6<896, 16>, 896, 16, fanout6_lds<896, 16>()},             // 58
+    {(const void*)k_fanout6<768, 12>, 768, 12, fanout6_lds<768, 12>()},             // 59
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2161,7 +2165,9 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout4<1024,24,nt,dyn>", "k_fanout4<1024,24,nt,rowmask,dyn>",
                                             "k_fanout6<1024,16,nt,dyn,pp>", "k_fanout6<1024,32,nt,dyn,pp>",
                                             "k_fanout6<1024,14,nt,dyn>", "k_fanout6<1024,20,nt,dyn>",
-                                            "k_fanout6<1024,22,nt,dyn>", "k_fanout6<1024,23,nt,dyn>"};
+                                            "k_fanout6<1024,22,nt,dyn>", "k_fanout6<1024,23,nt,dyn>",
+                                            "k_fanout6<768,16,nt,dyn>", "k_fanout6<768,18,nt,dyn>",
+                                            "k_fanout6<896,16,nt,dyn>", "k_fanout6<768,12,nt,dyn>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
