@@ -1441,7 +1441,10 @@ constexpr int fanout6_lds() { return Fan6<THREADS, CHUNK>::lds(); }
 // packet's first word (nor, for an RTCP rewrite, its second); then one wave writes those words,
 // patched, one lane per packet of the window.  The words are disjoint, so no ordering is
 // needed, and the patch arithmetic runs once per packet instead of on every stored word.
-template <int THREADS, int CHUNK, int AUX = 2, int PP = 0>
+// PF: each sub-stream window's FanSub record is loaded one window ahead (while the previous
+// window's rows are stored), instead of in up to three dependent scalar-load round trips at the
+// window's start.
+template <int THREADS, int CHUNK, int AUX = 2, int PP = 0, int PF = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanout6(FanoutParams P) {
     using F = Fan6<THREADS, CHUNK>;
     constexpr int CWORDS = F::CWORDS, NL = F::NL, NWAVES = F::NWAVES, SM = F::SM;
@@ -1517,8 +1520,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
         const uint64_t lo = it.lo, vb0 = it.vb0;
         const uint32_t np = it.np, nw = it.nw, vc0 = it.vc0;
         // ---- write the chunk to every sub-stream of the sender ----------------------------
+        FanSub fnext;
+        bool have_next = false;                                            // PF: fnext is record q
         for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
-            const FanSub f = const_load(P.fansub + q);
+            const FanSub f = (PF && have_next) ? fnext : const_load(P.fansub + q);
+            have_next = false;
             if (f.a >= lo + np) continue;
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
             const uint32_t fw = uni((uint32_t)((m.vb[p0] - vb0) >> 4));
@@ -1528,6 +1534,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out + A, 0, (nw - fw) * 16, 0x00020000);
             const bool patch = (f.ch & 1u) || f.rw;                            // uniform
             const uint32_t nj = (nw - fw + s + THREADS - 1) / THREADS;
+            if (PF && q + 1 < it.qe) { fnext = const_load(P.fansub + q + 1); have_next = true; }
             if (PP && patch) {
                 const bool second = (f.rw & kRwRtcp) != 0;                     // the SR timestamp word too
                 for (uint32_t j = 0; j < nj; j++) {
@@ -2141,6 +2148,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout6<768, 18>, 768, 18, fanout6_lds<768, 18>()},             // 57
     {(const void*)k_fanout6<896, 16>, 896, 16, fanout6_lds<896, 16>()},             // 58
     {(const void*)k_fanout6<768, 12>, 768, 12, fanout6_lds<768, 12>()},             // 59
+    {(const void*)k_fanout6<1024, 16, 2, 0, 1>, 1024, 16, fanout6_lds<1024, 16>()}, // 60 16, FanSub one window ahead
+    {(const void*)k_fanout6<1024, 32, 2, 0, 1>, 1024, 32, fanout6_lds<1024, 32>()}, // 61 32, same
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2167,7 +2176,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<1024,14,nt,dyn>", "k_fanout6<1024,20,nt,dyn>",
                                             "k_fanout6<1024,22,nt,dyn>", "k_fanout6<1024,23,nt,dyn>",
                                             "k_fanout6<768,16,nt,dyn>", "k_fanout6<768,18,nt,dyn>",
-                                            "k_fanout6<896,16,nt,dyn>", "k_fanout6<768,12,nt,dyn>"};
+                                            "k_fanout6<896,16,nt,dyn>", "k_fanout6<768,12,nt,dyn>",
+                                            "k_fanout6<1024,16,nt,dyn,pf>", "k_fanout6<1024,32,nt,dyn,pf>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
