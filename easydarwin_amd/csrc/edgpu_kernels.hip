@@ -113,6 +113,63 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
 // Ingest
 // =========================================================================================
 
+// Slot copy of RTSP-interleaved frames inside the TCP byte stream (k_ingest, copy_mode 0).  The
+// frame's bytes [sp, lim) are misaligned by sh = sp & 15.  Each lane loads ONE aligned block
+// (blocks holding a byte of the frame only); slot word w is blocks w and w + 1 funnelled by sh,
+// and block w + 1 comes from the next lane by DPP (lane 63 takes the next round's lane 0 by
+// readlane).  A wave takes TD frames per round (EDGPU_INGEST_TCP=1 / 2: one / two)
+// and issues all their loads before its first store.  Four frames per round (162 VGPRs, 3 waves
+// per SIMD) measured slower: ingest incl. deframe 0.563 vs 0.435 ms (profiles/r02z21_*).
+template <uint32_t TD, int THREADS>
+__device__ __forceinline__ void tcp_slot_copy(uint32_t n, const uint32_t* p_slotb, const uint64_t* p_src,
+                                              const uint16_t* p_len, const uint8_t* p_snd, const uint64_t* p_vb,
+                                              const uint64_t* s_ring, const uint32_t* s_wmask) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t kW = THREADS / 64;
+    auto lane0 = [](u32x4 v) {
+        return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                     (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+    };
+    for (uint32_t p = wid; p < n; p += TD * kW) {
+        u32x4 b[TD][4];
+        uint32_t sb[TD], fl[TD], sh[TD];
+#pragma unroll
+        for (uint32_t d = 0; d < TD; d++) {
+            const uint32_t pd = p + d * kW;
+            sb[d] = pd < n ? p_slotb[pd] : 0u;
+            const uint8_t* sp = reinterpret_cast<const uint8_t*>(sb[d] ? p_src[pd] : 0ull);
+            fl[d] = sb[d] ? 4u + p_len[pd] : 0u;                          // frame bytes
+            const uintptr_t a0 = (uintptr_t)sp & ~(uintptr_t)15;
+            sh[d] = (uint32_t)((uintptr_t)sp & 15);
+            const uint32_t nblk = sb[d] ? (uint32_t)(((uintptr_t)sp + fl[d] - 1 - a0) >> 4) + 1 : 0u;
+            const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            b[d][0] = (uint32_t)lane < nblk ? ab[lane] : z;
+            b[d][1] = (uint32_t)lane + 64 < nblk ? ab[lane + 64] : z;
+            b[d][2] = (uint32_t)lane + 128 < nblk ? ab[lane + 128] : z;
+            b[d][3] = lane == 0 && 192u < nblk ? ab[192] : z;           // lane 63 of round 2's neighbour
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < TD; d++) {
+            if (sb[d] == 0) continue;                                    // uniform
+            const uint32_t pd = p + d * kW;
+            const uint32_t s = p_snd[pd];
+            u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
+            const uint64_t w0 = p_vb[pd] >> 4;
+            const uint32_t wm = s_wmask[s];
+            const uint32_t nw = sb[d] / 16;
+            u32x4 v0 = funnel16(b[d][0], wave_next(b[d][0], lane0(b[d][1])), sh[d]);
+            const u32x4 v1 = funnel16(b[d][1], wave_next(b[d][1], lane0(b[d][2])), sh[d]);
+            const u32x4 v2 = funnel16(b[d][2], wave_next(b[d][2], lane0(b[d][3])), sh[d]);
+            const int rem = (int)fl[d] - 16 * lane;                         // frame bytes from word `lane`
+            if (lane == 0) v0.x = slot_header(p_len[pd]);
+            if ((uint32_t)lane < nw) ring[(w0 + lane) & wm] = keep16(v0, rem);
+            if ((uint32_t)lane + 64 < nw) ring[(w0 + lane + 64) & wm] = keep16(v1, rem - 1024);
+            if ((uint32_t)lane + 128 < nw) ring[(w0 + lane + 128) & wm] = keep16(v2, rem - 2048);
+        }
+    }
+}
+
 // DEPTH: packets per wave per slot-copy round; 4 by default (125 VGPRs, still 4 waves/SIMD),
 // EDGPU_INGEST_DEPTH=2 for A/B runs
 // THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
@@ -287,56 +344,8 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         if (P.ablate & 32u) {
             // timing ablation only: no slot copy
         } else if (P.copy_mode == 0 && P.src_addr && P.tcp_copy >= 1) {   // frames inside the TCP byte stream
-            // The frame's bytes [sp, lim) are misaligned by sh = sp & 15.  Each lane loads ONE
-            // aligned block (blocks holding a byte of the frame only); slot word w is blocks w
-            // and w + 1 funnelled by sh, and block w + 1 comes from the next lane by DPP (lane
-            // 63 takes the next round's lane 0 by readlane).  A wave takes TD frames per round
-            // (EDGPU_INGEST_TCP=2: two) and issues all their loads before its first store.
-            const int lane = tid & 63, wid = tid >> 6;
-            constexpr uint32_t kW = THREADS / 64;
-            const uint32_t TD = P.tcp_copy == 2 ? 2u : 1u;                     // uniform
-            auto lane0 = [](u32x4 v) {
-                return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
-                             (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
-            };
-            for (uint32_t p = wid; p < n; p += TD * kW) {
-                u32x4 b[2][4];
-                uint32_t sb[2], fl[2], sh[2];
-#pragma unroll
-                for (uint32_t d = 0; d < 2; d++) {
-                    const uint32_t pd = p + d * kW;
-                    sb[d] = (d < TD && pd < n) ? p_slotb[pd] : 0u;
-                    const uint8_t* sp = reinterpret_cast<const uint8_t*>(sb[d] ? p_src[pd] : 0ull);
-                    fl[d] = sb[d] ? 4u + p_len[pd] : 0u;                          // frame bytes
-                    const uintptr_t a0 = (uintptr_t)sp & ~(uintptr_t)15;
-                    sh[d] = (uint32_t)((uintptr_t)sp & 15);
-                    const uint32_t nblk = sb[d] ? (uint32_t)(((uintptr_t)sp + fl[d] - 1 - a0) >> 4) + 1 : 0u;
-                    const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
-                    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-                    b[d][0] = (uint32_t)lane < nblk ? ab[lane] : z;
-                    b[d][1] = (uint32_t)lane + 64 < nblk ? ab[lane + 64] : z;
-                    b[d][2] = (uint32_t)lane + 128 < nblk ? ab[lane + 128] : z;
-                    b[d][3] = lane == 0 && 192u < nblk ? ab[192] : z;           // lane 63 of round 2's neighbour
-                }
-#pragma unroll
-                for (uint32_t d = 0; d < 2; d++) {
-                    if (sb[d] == 0) continue;                                    // uniform
-                    const uint32_t pd = p + d * kW;
-                    const uint32_t s = p_snd[pd];
-                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
-                    const uint64_t w0 = p_vb[pd] >> 4;
-                    const uint32_t wm = s_wmask[s];
-                    const uint32_t nw = sb[d] / 16;
-                    u32x4 v0 = funnel16(b[d][0], wave_next(b[d][0], lane0(b[d][1])), sh[d]);
-                    const u32x4 v1 = funnel16(b[d][1], wave_next(b[d][1], lane0(b[d][2])), sh[d]);
-                    const u32x4 v2 = funnel16(b[d][2], wave_next(b[d][2], lane0(b[d][3])), sh[d]);
-                    const int rem = (int)fl[d] - 16 * lane;                         // frame bytes from word `lane`
-                    if (lane == 0) v0.x = slot_header(p_len[pd]);
-                    if ((uint32_t)lane < nw) ring[(w0 + lane) & wm] = keep16(v0, rem);
-                    if ((uint32_t)lane + 64 < nw) ring[(w0 + lane + 64) & wm] = keep16(v1, rem - 1024);
-                    if ((uint32_t)lane + 128 < nw) ring[(w0 + lane + 128) & wm] = keep16(v2, rem - 2048);
-                }
-            }
+            if (P.tcp_copy >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+            else tcp_slot_copy<1, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
         } else if (P.copy_mode == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
             const int lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += THREADS / 64) {
