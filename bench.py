@@ -299,10 +299,20 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dist = None
+    # EDGPU_BENCH_BACKEND=gloo: a rehearsal of the N-rank path with several ranks sharing the GPUs
+    # there are (rank r on GPU r % count, host-side reductions); the driver's runs use RCCL
+    backend = os.environ.get("EDGPU_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"EDGPU_BENCH_BACKEND={backend}: nccl or gloo")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     # every rank owns exactly args.sessions streams of the hash-sharded population (weak scaling)
@@ -385,7 +395,7 @@ def main():
     launches = c1["fanout_launches"] - c0["fanout_launches"]
     alg_bytes = out_bytes + in_bytes + 16 * relayed      # SURVEY.md §8.d per-launch definition
 
-    dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev)
+    dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None)
 
     if rank != 0:
         if dist:
@@ -441,7 +451,8 @@ def main():
                    "tick_ms": args.tick_ms,
                    "rewrite": rewrite_desc,
                    "engine_env": knobs,
-                   "parallelism": f"stream-hash shards x{world}, no data-path collective"},
+                   "parallelism": f"stream-hash shards x{world}, no data-path collective"
+                                  + ("" if backend == "nccl" or world == 1 else f" ({backend} rehearsal, ranks sharing GPUs)")},
         "relayed_GBps": round(out_all / dt / 1e9, 2),
         **({"pcie_H2D_GBps": round(sum(batches[i]["bytes"] + 16 * batches[i]["n"] for i in range(warm, warm + steps))
                                    / dt / 1e9, 2)} if args.ingest == "host" else {}),
