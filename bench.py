@@ -278,6 +278,9 @@ def main():
                          "reads in HBM, deframed on the GPU (edgpu_ingest_interleaved); host: the batches in "
                          "pinned host memory, copied over PCIe on the copy stream beside the previous fan-out "
                          "(EDGPU_PTR_PINNED) -- a separate line, PCIe-bound")
+    ap.add_argument("--rewrite-same-ssrc", action="store_true",
+                    help="diagnostic: every subscriber's SSRC overridden with its stream's own SSRC, so the "
+                         "copy kernel takes its patch path while the bytes stay the identity's")
     ap.add_argument("--rewrite", action="store_true",
                     help="per-output rewrite stage on every subscriber (seq/ts deltas + SSRC override, "
                          "edgpu_subscriber_rewrite); the reference's parity mode is the identity (default)")
@@ -353,11 +356,13 @@ def main():
             bt["pinned"] = make_pinned(ctx, bt)
             bt.pop("blob")
         torch.cuda.empty_cache()
-    for _ in gids:
+    for si, _ in enumerate(gids):
         s = ctx.session_add(fleet.sdp())
         for _k in range(args.subs):
             h = ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
-            if args.rewrite:
+            if args.rewrite_same_ssrc:      # the patch path runs, the bytes stay the identity's
+                ctx.subscriber_rewrite(h, 0, ssrc=int(fleet.ssrc[si]))
+            elif args.rewrite:
                 ctx.subscriber_rewrite(h, 0, seq_delta=h * 7919 + 1, ts_delta=h * 0x9E3779B1, ssrc=0x5EED0000 + h)
 
     for i in range(warm):
@@ -407,7 +412,9 @@ def main():
     # HBM traffic per launch from the committed rocprofv3 PMC passes of exactly this kernel
     # variant and workload (tools/profile.sh + tools/summarize_profile.py); null otherwise
     traffic, traffic_source = None, None
-    rewrite_desc = "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)"
+    rewrite_desc = ("SSRC override with the stream's own SSRC (diagnostic: patch path, identity bytes)"
+                    if args.rewrite_same_ssrc else
+                    "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)")
     pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
     if os.path.exists(pmc) and world == 1:
         try:
