@@ -1151,6 +1151,36 @@ __device__ __forceinline__ u32x4 fan_patch(u32x4 v, const FanSub& f, uint32_t w,
     return fan_patch_start(v, f, start);
 }
 
+// fan_patch with the slot-start test as a divergent branch: the patch arithmetic runs only on
+// lanes that hold a slot's first word (and only in waves that have one), in place, with no
+// per-dword selects.  Same result as fan_patch.
+__device__ __forceinline__ u32x4 fan_patch_branchy(u32x4 v, const FanSub& f, uint32_t w, const uint32_t* sm,
+                                                   const u32x4* cb) {
+    const bool start = (sm[w >> 5] >> (w & 31)) & 1u;
+    if ((f.rw & kRwRtcp) && !start && w > 0 && ((sm[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)) {   // RTCP only: rare
+        const u32x4 h = cb[w - 1];
+        const uint32_t hl = ((h.x >> 8) & 0xFF00u) | (h.x >> 24);
+        if (hl >= 20 && ((h.y >> 8) & 0xFFu) == 200u) v.y = __builtin_bswap32(__builtin_bswap32(v.y) + f.rw_ts);
+    }
+    if (start) {
+        if (f.ch & 1u) v.x |= f.ch & 0xFF00u;
+        if (f.rw) {
+            const uint32_t len = ((v.x >> 8) & 0xFF00u) | (v.x >> 24);
+            if (!(f.rw & kRwRtcp)) {
+                if (len >= 12) {
+                    const uint32_t seq = (((v.y >> 8) & 0xFF00u) | (v.y >> 24)) + (f.rw >> 16);
+                    v.y = (v.y & 0xFFFFu) | ((seq >> 8) & 0xFFu) << 16 | (seq & 0xFFu) << 24;
+                    v.z = __builtin_bswap32(__builtin_bswap32(v.z) + f.rw_ts);
+                    if (f.rw & kRwSsrc) v.w = f.rw_ssrc_be;
+                }
+            } else if ((f.rw & kRwSsrc) && len >= 8) {
+                v.z = f.rw_ssrc_be;
+            }
+        }
+    }
+    return v;
+}
+
 // Bits [c0, c0 + 64) of a slot-start bitmap of `nw32` words as one wave-uniform mask (bit l =
 // word c0 + l; words before 0 or past the bitmap read as 0).  Every lane reads the same three
 // LDS words (a broadcast), so the per-word test becomes a shift of an SGPR pair.
@@ -1453,7 +1483,8 @@ constexpr int fanout6_lds() { return Fan6<THREADS, CHUNK>::lds(); }
 // PF: each sub-stream window's FanSub record is loaded one window ahead (while the previous
 // window's rows are stored), instead of in up to three dependent scalar-load round trips at the
 // window's start.
-template <int THREADS, int CHUNK, int AUX = 2, int PP = 0, int PF = 0>
+// BP: the patch as a divergent branch on the slot-start test (fan_patch_branchy).
+template <int THREADS, int CHUNK, int AUX = 2, int PP = 0, int PF = 0, int BP = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanout6(FanoutParams P) {
     using F = Fan6<THREADS, CHUNK>;
     constexpr int CWORDS = F::CWORDS, NL = F::NL, NWAVES = F::NWAVES, SM = F::SM;
@@ -1575,7 +1606,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
                 const uint32_t src = fw + tid + j * THREADS - s;               // chunk word of the lane's
                 const uint32_t srcc = src < (uint32_t)CWORDS ? src : 0u;       // word of the aligned window
                 u32x4 v = m.cb[srcc];
-                if (patch) v = fan_patch(v, f, srcc, sm, m.cb);
+                if (patch) v = BP ? fan_patch_branchy(v, f, srcc, sm, m.cb) : fan_patch(v, f, srcc, sm, m.cb);
                 __builtin_amdgcn_raw_buffer_store_b128(v, os, (tid + j * THREADS - s) * 16u, 0, AUX);
             }
         }
@@ -2159,6 +2190,8 @@ static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout6<768, 12>, 768, 12, fanout6_lds<768, 12>()},             // 59
     {(const void*)k_fanout6<1024, 16, 2, 0, 1>, 1024, 16, fanout6_lds<1024, 16>()}, // 60 16, FanSub one window ahead
     {(const void*)k_fanout6<1024, 32, 2, 0, 1>, 1024, 32, fanout6_lds<1024, 32>()}, // 61 32, same
+    {(const void*)k_fanout6<1024, 16, 2, 0, 0, 1>, 1024, 16, fanout6_lds<1024, 16>()}, // 62 16, branchy patch
+    {(const void*)k_fanout6<1024, 32, 2, 0, 0, 1>, 1024, 32, fanout6_lds<1024, 32>()}, // 63 32, branchy patch
 };
 static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512,16>", "k_fanout4<1024,32>",
                                             "k_fanout4<512,32>", "k_fanout4<1024,16>", "k_fanout4<512,16>",
@@ -2186,7 +2219,8 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<1024,22,nt,dyn>", "k_fanout6<1024,23,nt,dyn>",
                                             "k_fanout6<768,16,nt,dyn>", "k_fanout6<768,18,nt,dyn>",
                                             "k_fanout6<896,16,nt,dyn>", "k_fanout6<768,12,nt,dyn>",
-                                            "k_fanout6<1024,16,nt,dyn,pf>", "k_fanout6<1024,32,nt,dyn,pf>"};
+                                            "k_fanout6<1024,16,nt,dyn,pf>", "k_fanout6<1024,32,nt,dyn,pf>",
+                                            "k_fanout6<1024,16,nt,dyn,bp>", "k_fanout6<1024,32,nt,dyn,bp>"};
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
