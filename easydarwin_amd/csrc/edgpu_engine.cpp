@@ -141,7 +141,8 @@ struct edgpu_ctx {
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
     uint32_t ablate = 0;
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
-    uint32_t tcp_copy = 2;          // EDGPU_INGEST_TCP: 2 DPP neighbour word, two frames per wave round;
+    uint32_t tcp_copy = 3;          // EDGPU_INGEST_TCP: 3 frame state in SGPRs, DPP neighbour word, two
+                                    // frames per wave round; 2 the same with per-lane frame state;
                                     // 1 one frame per round; 0 two loads per word
     hipStream_t stream = nullptr;
     // tick pipelining (edgpu_config.overlap_ticks): the fan-out copy kernel runs on `copy`,
@@ -331,7 +332,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
-    if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 2);
+    if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 3);
     *out = x;
     return EDGPU_OK;
 }

@@ -170,6 +170,66 @@ __device__ __forceinline__ void tcp_slot_copy(uint32_t n, const uint32_t* p_slot
     }
 }
 
+// tcp_slot_copy with the per-frame state in SGPRs: a frame's slot size, length and source
+// address are uniform across the wave (readfirstlane), and the one block past lane 63's second
+// round (block 192, needed by lane 63 of round 2 only) is a scalar load.  Fewer VGPRs per frame
+// in flight (12 instead of 16 + 3), so more frames per round fit the occupancy.
+// (EDGPU_INGEST_TCP=3: two frames per round, 4: four.)
+template <uint32_t TD, int THREADS>
+__device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_slotb, const uint64_t* p_src,
+                                                const uint16_t* p_len, const uint8_t* p_snd, const uint64_t* p_vb,
+                                                const uint64_t* s_ring, const uint32_t* s_wmask) {
+    typedef __attribute__((address_space(4))) const u32x4 cu32x4;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t kW = THREADS / 64;
+    auto lane0 = [](u32x4 v) {
+        return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                     (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+    };
+    auto uni64 = [](uint64_t x) {
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32;
+    };
+    for (uint32_t p = wid; p < n; p += TD * kW) {
+        u32x4 b[TD][3], b3[TD];
+        uint32_t sb[TD], fl[TD], sh[TD];
+#pragma unroll
+        for (uint32_t d = 0; d < TD; d++) {
+            const uint32_t pd = p + d * kW;                              // uniform
+            sb[d] = pd < n ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p_slotb[pd]) : 0u;
+            const uint64_t sp = sb[d] ? uni64(p_src[pd]) : 0ull;
+            fl[d] = sb[d] ? 4u + (uint32_t)__builtin_amdgcn_readfirstlane((int)p_len[pd]) : 0u;
+            const uint64_t a0 = sp & ~15ull;
+            sh[d] = (uint32_t)(sp & 15);
+            const uint32_t nblk = sb[d] ? (uint32_t)((sp + fl[d] - 1 - a0) >> 4) + 1 : 0u;
+            const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            b[d][0] = (uint32_t)lane < nblk ? ab[lane] : z;
+            b[d][1] = (uint32_t)lane + 64 < nblk ? ab[lane + 64] : z;
+            b[d][2] = (uint32_t)lane + 128 < nblk ? ab[lane + 128] : z;
+            b3[d] = 192u < nblk ? *(cu32x4*)(ab + 192) : z;              // scalar
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < TD; d++) {
+            if (sb[d] == 0) continue;                                    // uniform
+            const uint32_t pd = p + d * kW;
+            const uint32_t s = p_snd[pd];
+            u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
+            const uint64_t w0 = p_vb[pd] >> 4;
+            const uint32_t wm = s_wmask[s];
+            const uint32_t nw = sb[d] / 16;
+            u32x4 v0 = funnel16(b[d][0], wave_next(b[d][0], lane0(b[d][1])), sh[d]);
+            const u32x4 v1 = funnel16(b[d][1], wave_next(b[d][1], lane0(b[d][2])), sh[d]);
+            const u32x4 v2 = funnel16(b[d][2], wave_next(b[d][2], b3[d]), sh[d]);
+            const int rem = (int)fl[d] - 16 * lane;                         // frame bytes from word `lane`
+            if (lane == 0) v0.x = slot_header(fl[d] - 4u);
+            if ((uint32_t)lane < nw) ring[(w0 + lane) & wm] = keep16(v0, rem);
+            if ((uint32_t)lane + 64 < nw) ring[(w0 + lane + 64) & wm] = keep16(v1, rem - 1024);
+            if ((uint32_t)lane + 128 < nw) ring[(w0 + lane + 128) & wm] = keep16(v2, rem - 2048);
+        }
+    }
+}
+
 // DEPTH: packets per wave per slot-copy round; 4 by default (125 VGPRs, still 4 waves/SIMD),
 // EDGPU_INGEST_DEPTH=2 for A/B runs
 // THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
@@ -344,7 +404,8 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         if (P.ablate & 32u) {
             // timing ablation only: no slot copy
         } else if (P.copy_mode == 0 && P.src_addr && P.tcp_copy >= 1) {   // frames inside the TCP byte stream
-            if (P.tcp_copy >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+            if (P.tcp_copy == 3) tcp_slot_copy_s<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+            else if (P.tcp_copy >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else tcp_slot_copy<1, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
         } else if (P.copy_mode == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
             const int lane = tid & 63, wid = tid >> 6;
