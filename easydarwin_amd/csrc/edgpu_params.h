@@ -77,7 +77,12 @@ struct FanoutParams {
 // followed by its reads.  The stream is cut into kTcpChunk-byte chunks walked in parallel from
 // every '$' that can start a frame in the chunk's first kTcpMaxFrame bytes; the true walk is
 // then stitched chunk to chunk (k_tcp_resolve).
-constexpr uint32_t kTcpChunk = 16384;      // stream bytes per walk chunk
+#ifndef EDGPU_TCP_CHUNK
+#define EDGPU_TCP_CHUNK 32768                // 32 KiB: ingest incl. deframe 0.405 vs 0.421 ms at 16 KiB,
+                                             // 0.479 at 8 KiB (profiles/r02z28_tcp_chunk_ab/)
+#endif
+constexpr uint32_t kTcpChunk = EDGPU_TCP_CHUNK;   // stream bytes per walk chunk
+static_assert(kTcpChunk >= 4096 && kTcpChunk + 2 * 2051 <= 65536, "chunk offsets are 16-bit");
 constexpr uint32_t kTcpCands = 64;         // candidates kept per chunk (more: sequential walk)
 constexpr uint32_t kTcpFrames = 32;        // frame starts recorded per candidate walk
 constexpr uint32_t kTcpMaxFrame = 2047;    // usable request-buffer bytes (QTSS_MAX_REQUEST_BUFFER_SIZE - 1)
