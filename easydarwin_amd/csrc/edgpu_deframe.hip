@@ -78,6 +78,14 @@ __device__ __forceinline__ uint32_t tcp_step(const TcpView& v, uint64_t pos, uin
 
 // Walks from `pos` until reaching `end` or a stop; counts frames, recording the first
 // kTcpFrames starts (chunk offsets from `start`) in `rec` when given.
+//
+// Each step's header load waits on the previous frame's length, so a chunk's ~23 frames are ~23
+// HBM latencies in a row.  With kTcpSpec > 0 the walk also guesses: after a frame of length L it
+// loads the headers at pos + j·L (j < kTcpSpec) at once, as if the next frames had length L too
+// (FU-A fragments of one video frame all do), then checks them in order.  A guessed header is
+// used only once every frame before it had length exactly L, i.e. once it is known to be the
+// true next frame start, and each is judged by tcp_step's own rules, so the walk's frames, stop
+// code and exit are the sequential walk's; a wrong guess costs nothing but its loads.
 __device__ __forceinline__ uint32_t tcp_walk(const TcpView& v, uint64_t& pos, uint64_t start, uint64_t end,
                                              uint32_t& nf, uint16_t* rec) {
     nf = 0;
@@ -88,6 +96,36 @@ __device__ __forceinline__ uint32_t tcp_walk(const TcpView& v, uint64_t& pos, ui
         if (rec && nf < kTcpFrames) rec[nf] = (uint16_t)(pos - start);
         nf++;
         pos += flen;
+        if constexpr (kTcpSpec > 0) {
+            const uint32_t L = flen;
+            bool more = pos >= v.clen;                        // guesses only in the raw reads
+            while (more) {                                    // one burst of kTcpSpec guesses
+                more = false;
+                uint32_t h[kTcpSpec ? kTcpSpec : 1];          // b0 | b2 << 8 | b3 << 16, or ~0u
+#pragma unroll
+                for (uint32_t j = 0; j < kTcpSpec; j++) {
+                    const uint64_t q = pos + (uint64_t)j * L;
+                    h[j] = ~0u;
+                    if (q < end && q + 4 <= v.len) {          // tcp_step's fast branch at q
+                        const uint8_t* b = v.raw + (q - v.clen);
+                        h[j] = (uint32_t)b[0] | (uint32_t)b[2] << 8 | (uint32_t)b[3] << 16;
+                    }
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kTcpSpec; j++) {
+                    if (h[j] == ~0u) break;                   // past the chunk / near the stream end
+                    if ((h[j] & 0xFFu) != 0x24u) return kWalkMessage;
+                    const uint32_t fl = 4 + ((h[j] >> 8 & 0xFFu) << 8 | (h[j] >> 16));
+                    if (fl > kTcpMaxFrame) return v.len - pos >= kTcpMaxFrame ? kWalkDropped : kWalkPartial;
+                    if (pos + fl > v.len) return kWalkPartial;
+                    if (rec && nf < kTcpFrames) rec[nf] = (uint16_t)(pos - start);
+                    nf++;
+                    pos += fl;
+                    if (fl != L) break;                       // later guesses are off the chain
+                    if (j == kTcpSpec - 1) more = true;       // every guess held: guess on
+                }
+            }
+        }
     }
     return kWalkRun;
 }
@@ -107,7 +145,7 @@ __device__ __forceinline__ uint32_t dollar_mask(u32x4 w) {
     return m;
 }
 
-__device__ uint32_t tcp_candidates(const TcpView& v, uint64_t start, uint16_t* list, int lane) {
+[[maybe_unused]] __device__ uint32_t tcp_candidates(const TcpView& v, uint64_t start, uint16_t* list, int lane) {
     if (start == 0) {
         if (lane == 0) list[0] = 0;
         return 1;
@@ -142,6 +180,71 @@ __device__ uint32_t tcp_candidates(const TcpView& v, uint64_t start, uint16_t* l
         n += __shfl(incl, 63, 64);
     }
     return n;
+}
+
+// The same over two windows (a chunk's own and the next chunk's) with every block of both
+// loaded before the first is scanned: one load latency instead of up to six in a row.  A window
+// spans at most 129 blocks, so three rounds of 64 lanes hold it.
+struct CandWin {
+    uintptr_t lo = 0, hi = 0, al = 0;
+    bool first = false, none = true;
+};
+
+[[maybe_unused]] __device__ __forceinline__ CandWin cand_window(const TcpView& v, uint64_t start, bool want) {
+    CandWin w;
+    if (!want) return w;
+    w.none = false;
+    if (start == 0) { w.first = true; return w; }
+    const uint64_t wend = min(start + (uint64_t)kTcpMaxFrame, v.len);
+    w.lo = (uintptr_t)(v.raw + (start - v.clen));
+    w.hi = (uintptr_t)(v.raw + (wend - v.clen));
+    w.al = w.lo & ~(uintptr_t)15;
+    return w;
+}
+
+[[maybe_unused]] __device__ __forceinline__ uint32_t cand_scan(const CandWin& w, const u32x4 (&blk)[3], uint16_t* list, int lane) {
+    if (w.none) return 0;
+    if (w.first) {
+        if (lane == 0) list[0] = 0;
+        return 1;
+    }
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t round = 0; round < 3; round++) {
+        if (w.al + 16 * 64 * (uintptr_t)round >= w.hi) break;          // uniform
+        const uintptr_t b = w.al + 16 * (uintptr_t)(lane + 64 * round);
+        uint32_t mask = 0;
+        if (b < w.hi) {
+            mask = dollar_mask(blk[round]);
+            if (b < w.lo) mask &= ~((1u << (uint32_t)(w.lo - b)) - 1u);
+            if (b + 16 > w.hi) mask &= (1u << (uint32_t)(w.hi - b)) - 1u;
+        }
+        const uint32_t cnt = (uint32_t)__popc(mask);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        uint32_t idx = n + incl - cnt;
+        while (mask) {
+            const int i = __ffs(mask) - 1;
+            mask &= mask - 1;
+            if (idx < kTcpCands) list[idx] = (uint16_t)(b + i - w.lo);
+            idx++;
+        }
+        n += __shfl(incl, 63, 64);
+    }
+    return n;
+}
+
+[[maybe_unused]] __device__ __forceinline__ void cand_load(const CandWin& w, u32x4 (&blk)[3], int lane) {
+#pragma unroll
+    for (uint32_t round = 0; round < 3; round++) {
+        const uintptr_t b = w.al + 16 * (uintptr_t)(lane + 64 * round);
+        blk[round] = u32x4{0u, 0u, 0u, 0u};
+        if (!w.none && !w.first && b < w.hi) blk[round] = *reinterpret_cast<const u32x4*>(b);
+    }
 }
 
 template <typename T>
@@ -187,8 +290,17 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_tcp_walk(TcpParams P) {
         v = tcp_view(P, G);
         start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
         end = min(start + kTcpChunk, v.len);
-        n = tcp_candidates(v, start, own, lane);
-        nn = end < v.len ? tcp_candidates(v, end, next, lane) : 0u;
+        if constexpr (kTcpSpec > 0) {
+            const CandWin wo = cand_window(v, start, true), wn = cand_window(v, end, end < v.len);
+            u32x4 bo[3], bn[3];
+            cand_load(wo, bo, lane);
+            cand_load(wn, bn, lane);
+            n = cand_scan(wo, bo, own, lane);
+            nn = cand_scan(wn, bn, next, lane);
+        } else {
+            n = tcp_candidates(v, start, own, lane);
+            nn = end < v.len ? tcp_candidates(v, end, next, lane) : 0u;
+        }
     }
     __syncthreads();
     if (!valid) return;

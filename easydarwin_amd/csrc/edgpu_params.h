@@ -82,6 +82,11 @@ struct FanoutParams {
                                              // 0.479 at 8 KiB (profiles/r02z28_tcp_chunk_ab/)
 #endif
 constexpr uint32_t kTcpChunk = EDGPU_TCP_CHUNK;   // stream bytes per walk chunk
+#ifndef EDGPU_TCP_SPEC
+#define EDGPU_TCP_SPEC 0                     // frame headers guessed per burst of the walk (0: none);
+                                             // 4 / 8 / 16 measured slower (profiles/r02z30_tcp_spec_ab/)
+#endif
+constexpr uint32_t kTcpSpec = EDGPU_TCP_SPEC;
 static_assert(kTcpChunk >= 4096 && kTcpChunk + 2 * 2051 <= 65536, "chunk offsets are 16-bit");
 constexpr uint32_t kTcpCands = 64;         // candidates kept per chunk (more: sequential walk)
 constexpr uint32_t kTcpFrames = 32;        // frame starts recorded per candidate walk

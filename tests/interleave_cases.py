@@ -79,8 +79,26 @@ def case(name: str) -> list[bytes]:
     if name == "big":
         data = b"".join(_frames(rng, 6000, 12, 1460, dollar=0.05))
         return _split(rng, data, 1, 65536)
+    if name in ("fua_runs", "fua_oversize", "fua_partial"):
+        # runs of equal-length FU-A frames (the walk's guessed headers all hold) broken by
+        # shorter tails, audio frames, and -- where a guess would land -- an RTSP message, an
+        # oversize frame or the end of the stream mid-frame
+        out = []
+        for run in range(10):
+            out += [_frame(0, _payload(rng, 1400)) for _ in range(rng.randint(5, 40))]
+            if name == "fua_runs" and run == 6:
+                out.append(RTSP_REQ)
+            if name == "fua_oversize" and run == 7:
+                out.append(_frame(0, _payload(rng, 2044)))
+            out.append(_frame(0, _payload(rng, rng.randint(12, 1399))))
+            if rng.random() < 0.5:
+                out.append(_frame(2, _payload(rng, rng.randint(200, 400))))
+        data = b"".join(out)
+        if name == "fua_partial":
+            data += b"".join(_frame(0, _payload(rng, 1400)) for _ in range(9)) + _frame(0, _payload(rng, 1400))[:700]
+        return _split(rng, data, 1, 20000)
     raise KeyError(name)
 
 
 CASES = ["rtp_mix", "tiny_reads", "max_frame", "rtsp_tail", "oversize", "oversize_short",
-         "dollar_payload", "big"]
+         "dollar_payload", "big", "fua_runs", "fua_oversize", "fua_partial"]
