@@ -7,13 +7,13 @@
 // frame that cannot fit the 2047 usable buffer bytes ends the connection.  The CPU walks that
 // chain one header at a time.
 //
-// Here a session's stream (carried partial frame ++ this call's reads) is cut into 16 KiB
+// Here a session's stream (carried partial frame ++ this call's reads) is cut into 32 KiB
 // chunks.  A frame starts at most kTcpMaxFrame - 1 bytes before a chunk boundary, so the true
 // walk enters each chunk at a '$' within its first kTcpMaxFrame bytes.
-//   k_tcp_walk     one wave per chunk: finds those candidates (one load round, 32 bytes a
-//                  lane), walks every candidate to the chunk end at once (a lane each; header
-//                  bytes only), records its first kTcpFrames frame starts and links its exit to
-//                  the next chunk's candidate.
+//   k_tcp_walk     two chunks per wave: finds their candidates (aligned 16-B loads, all
+//                  lanes), walks every candidate to the chunk end at once (a lane each, half a
+//                  wave per chunk; header bytes only), records its first kTcpFrames frame starts
+//                  and links its exit to the next chunk's candidate.
 //   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
 //                  scans the chunks' frame counts.
 //   k_tcp_scan     sessions -> ingest segments, capacity check.
@@ -272,60 +272,94 @@ __device__ __forceinline__ T block_exclusive_scan256(T v, T* scratch, T& total) 
 
 }  // namespace
 
-// ---- k_tcp_walk: one wave per chunk, 4 chunks per workgroup (residency) ----
+// ---- k_tcp_walk: CPW chunks per wave (kTcpWalkCpw), 4 waves per workgroup ----
+// The walk is bound by how many waves are resident (~16k chunks at 32 KiB, ~2 waves per wave
+// slot; profiles/r02z31_tcp_walk_sq/), and a chunk's true walk keeps one lane busy while its few
+// false candidates end within a step or two.  With CPW = 2 a wave finds both chunks' candidates
+// (all 64 lanes, one chunk after the other) and then walks them side by side, lanes 0-31 and
+// 32-63 (candidates past 32 in a second pass): half the waves for the same chains.
 constexpr int kWalkWaves = 4;
 
-__global__ __launch_bounds__(64 * kWalkWaves) void k_tcp_walk(TcpParams P) {
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t c = blockIdx.x * kWalkWaves + wid;
-    const bool valid = c < P.nchunks;
-    __shared__ uint16_t s_own[kWalkWaves][kTcpCands], s_next[kWalkWaves][kTcpCands];
-    uint16_t* own = s_own[wid];
-    uint16_t* next = s_next[wid];
-    TcpView v{};
-    uint64_t start = 0, end = 0;
-    uint32_t n = 0, nn = 0;
-    if (valid) {
-        const TcpGroup G = P.groups[P.chunk_group[c]];
-        v = tcp_view(P, G);
-        start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
-        end = min(start + kTcpChunk, v.len);
-        if constexpr (kTcpSpec > 0) {
-            const CandWin wo = cand_window(v, start, true), wn = cand_window(v, end, end < v.len);
-            u32x4 bo[3], bn[3];
-            cand_load(wo, bo, lane);
-            cand_load(wn, bn, lane);
-            n = cand_scan(wo, bo, own, lane);
-            nn = cand_scan(wn, bn, next, lane);
-        } else {
-            n = tcp_candidates(v, start, own, lane);
-            nn = end < v.len ? tcp_candidates(v, end, next, lane) : 0u;
-        }
+namespace {
+
+struct WalkChunk {
+    TcpView v;
+    uint64_t start, end;
+    uint32_t c, n, nn;
+    bool valid;
+};
+
+__device__ __forceinline__ WalkChunk walk_chunk_setup(const TcpParams& P, uint32_t c, uint16_t* own, uint16_t* next,
+                                                      int lane) {
+    WalkChunk w{};
+    w.c = c;
+    w.valid = c < P.nchunks;
+    if (!w.valid) return w;
+    const TcpGroup G = P.groups[P.chunk_group[c]];
+    w.v = tcp_view(P, G);
+    w.start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
+    w.end = min(w.start + kTcpChunk, w.v.len);
+    if constexpr (EDGPU_TCP_CAND_FUSED) {              // both windows' blocks loaded at once (A/B)
+        const CandWin wo = cand_window(w.v, w.start, true), wn = cand_window(w.v, w.end, w.end < w.v.len);
+        u32x4 bo[3], bn[3];
+        cand_load(wo, bo, lane);
+        cand_load(wn, bn, lane);
+        w.n = cand_scan(wo, bo, own, lane);
+        w.nn = cand_scan(wn, bn, next, lane);
+    } else {
+        w.n = tcp_candidates(w.v, w.start, own, lane);
+        w.nn = w.end < w.v.len ? tcp_candidates(w.v, w.end, next, lane) : 0u;
     }
-    __syncthreads();
-    if (!valid) return;
-    if (lane == 0) P.ncand[c] = n;
-    if (n > kTcpCands || (uint32_t)lane >= n) return;
-    const size_t ci = (size_t)c * kTcpCands + lane;
-    uint64_t pos = start + own[lane];
+    return w;
+}
+
+// Candidate k of chunk w: walk to the chunk end, record the frame starts, link the exit to the
+// next chunk's candidate.
+__device__ __forceinline__ void walk_candidate(const TcpParams& P, const WalkChunk& w, uint32_t k,
+                                               const uint16_t* own, const uint16_t* next) {
+    const size_t ci = (size_t)w.c * kTcpCands + k;
+    uint64_t pos = w.start + own[k];
     uint32_t nf;
-    const uint32_t code = tcp_walk(v, pos, start, end, nf, P.offs + ci * kTcpFrames);
+    const uint32_t code = tcp_walk(w.v, pos, w.start, w.end, nf, P.offs + ci * kTcpFrames);
     uint8_t link = 0xFE;
-    if (code == kWalkRun && pos < v.len) {                  // continues in the next chunk
+    if (code == kWalkRun && pos < w.v.len) {                // continues in the next chunk
         link = 0xFF;
-        if (nn <= kTcpCands) {
-            const uint32_t q = (uint32_t)(pos - end);
-            for (uint32_t i = 0; i < nn; i++)
+        if (w.nn <= kTcpCands) {
+            const uint32_t q = (uint32_t)(pos - w.end);
+            for (uint32_t i = 0; i < w.nn; i++)
                 if (next[i] == q) { link = (uint8_t)i; break; }
         }
     }
     TcpCand r;
-    r.q = own[lane];
-    r.exit = (uint32_t)(pos - start);
+    r.q = own[k];
+    r.exit = (uint32_t)(pos - w.start);
     r.nframes = nf;
     r.code = code;
     P.cands[ci] = r;
     P.links[ci] = link;
+}
+
+}  // namespace
+
+template <int CPW>
+__global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu(EDGPU_TCP_WALK_WPE)))
+void k_tcp_walk(TcpParams P) {
+    static_assert(CPW == 1 || CPW == 2, "one or two chunks per wave");
+    constexpr uint32_t LPC = 64 / CPW;                      // walking lanes per chunk
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ uint16_t s_own[kWalkWaves][CPW][kTcpCands], s_next[kWalkWaves][CPW][kTcpCands];
+    const uint32_t c0 = (blockIdx.x * kWalkWaves + wid) * CPW;
+    const WalkChunk a = walk_chunk_setup(P, c0, s_own[wid][0], s_next[wid][0], lane);
+    WalkChunk b{};
+    if constexpr (CPW == 2) b = walk_chunk_setup(P, c0 + 1, s_own[wid][CPW - 1], s_next[wid][CPW - 1], lane);
+    __syncthreads();
+    const int h = CPW == 2 && lane >= 32 ? 1 : 0;
+    const WalkChunk w = h ? b : a;
+    const uint32_t sub = (uint32_t)lane % LPC;
+    if (!w.valid) return;
+    if (sub == 0) P.ncand[w.c] = w.n;
+    if (w.n > kTcpCands) return;
+    for (uint32_t k = sub; k < w.n; k += LPC) walk_candidate(P, w, k, s_own[wid][h], s_next[wid][h]);
 }
 
 // ---- k_tcp_resolve: one workgroup per session; thread 0 follows the links ----
@@ -590,7 +624,8 @@ __global__ __launch_bounds__(256) void k_tcp_finish(TcpParams P) {
 
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
     if (p.nchunks)
-        hipLaunchKernelGGL(k_tcp_walk, dim3((p.nchunks + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, st, p);
+        hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
+                           dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(256), 0, st, p);
     if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);

@@ -84,9 +84,21 @@ struct FanoutParams {
 constexpr uint32_t kTcpChunk = EDGPU_TCP_CHUNK;   // stream bytes per walk chunk
 #ifndef EDGPU_TCP_SPEC
 #define EDGPU_TCP_SPEC 0                     // frame headers guessed per burst of the walk (0: none);
-                                             // 4 / 8 / 16 measured slower (profiles/r02z30_tcp_spec_ab/)
+                                             // 4 / 8 / 16 measured slower (profiles/r02z30_tcp_spec_ab/,
+                                             // r02z33_tcp_walk_spec_ab/)
 #endif
 constexpr uint32_t kTcpSpec = EDGPU_TCP_SPEC;
+#ifndef EDGPU_TCP_CAND_FUSED
+#define EDGPU_TCP_CAND_FUSED 0               // 1: a chunk's two candidate windows loaded at once (A/B)
+#endif
+#ifndef EDGPU_TCP_WALK_CPW
+#define EDGPU_TCP_WALK_CPW 2                 // chunks walked side by side per wave (1 or 2): walk
+                                             // ~100 -> 60 us (profiles/r02z32_tcp_walk_ab/)
+#endif
+constexpr int kTcpWalkCpw = EDGPU_TCP_WALK_CPW;
+#ifndef EDGPU_TCP_WALK_WPE
+#define EDGPU_TCP_WALK_WPE 8                 // waves per SIMD asked of k_tcp_walk's registers (63 VGPRs, no spill)
+#endif
 static_assert(kTcpChunk >= 4096 && kTcpChunk + 2 * 2051 <= 65536, "chunk offsets are 16-bit");
 constexpr uint32_t kTcpCands = 64;         // candidates kept per chunk (more: sequential walk)
 constexpr uint32_t kTcpFrames = 32;        // frame starts recorded per candidate walk
