@@ -292,7 +292,7 @@ def main():
     # Engine switches that change what is measured are recorded in the line; EDGPU_ABLATE skips
     # work inside the timed region, so a bench under it is refused unless it is an ablation study.
     knobs = {k: os.environ[k] for k in ("EDGPU_FANOUT", "EDGPU_INGEST_DEPTH", "EDGPU_INGEST", "EDGPU_INGEST_TCP", "EDGPU_INGEST_THREADS", "EDGPU_ABLATE",
-                                        "EDGPU_POISON") if k in os.environ}
+                                        "EDGPU_POISON", "EDGPU_LIB") if k in os.environ}
     if "EDGPU_ABLATE" in knobs and not args.ablation_study:
         raise SystemExit("EDGPU_ABLATE is set: ablations skip work in the timed region (use --ablation-study)")
 

@@ -41,6 +41,7 @@
 #include <unistd.h>
 
 #include "edgpu.h"
+#include "tick_regions.h"
 
 namespace {
 
@@ -342,41 +343,14 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     if ((rc = edgpu_copy_to_host(e->ctx, e->desc.data(), r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
         (rc = edgpu_copy_to_host(e->ctx, e->subs.data(), r->substreams, r->n_substreams * sizeof(edgpu_substream_out))))
         return eg_fail(e, rc, "copy to host");
-    // the regions to bring over: one per identity sender (its longest sub-stream) + every other
-    // non-empty sub-stream; `src[q]` = (region index, byte offset of q's region in it)
+    // the distinct bytes: one region per identity sender (its longest sub-stream) + every other
+    // non-empty sub-stream (tick_regions.h)
     const uint32_t nq = (uint32_t)e->subs.size();
-    std::vector<edgpu_region> reg;
-    std::vector<std::pair<uint32_t, uint64_t>> src(nq, {0xFFFFFFFFu, 0});
-    uint64_t need = 0;
+    edgpu_host::TickRegions tr;
+    uint64_t need = st.arena_bytes;
     if (e->dedup) {
-        std::map<uint32_t, uint32_t> rep;                 // sender -> its longest identity sub-stream
-        for (uint32_t q = 0; q < nq; q++) {
-            const edgpu_substream_out& s = e->subs[q];
-            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
-            auto it = rep.find(s.sender);
-            if (it == rep.end() || e->subs[it->second].out_bytes < s.out_bytes) rep[s.sender] = q;
-        }
-        std::map<uint32_t, uint32_t> rep_reg;             // sender -> region index
-        for (uint32_t q = 0; q < nq; q++) {
-            const edgpu_substream_out& s = e->subs[q];
-            if (!s.desc_count) continue;
-            if (s.flags & EDGPU_SUB_IDENTITY) {
-                const edgpu_substream_out& R = e->subs[rep[s.sender]];
-                auto it = rep_reg.find(s.sender);
-                if (it == rep_reg.end()) {
-                    it = rep_reg.emplace(s.sender, (uint32_t)reg.size()).first;
-                    reg.push_back(edgpu_region{R.out_base, R.out_bytes});
-                    need += R.out_bytes;
-                }
-                src[q] = {it->second, R.out_bytes - s.out_bytes};  // q is a suffix of the longest
-            } else {
-                src[q] = {(uint32_t)reg.size(), 0};
-                reg.push_back(edgpu_region{s.out_base, s.out_bytes});
-                need += s.out_bytes;
-            }
-        }
-    } else {
-        need = st.arena_bytes;
+        tr = edgpu_host::tick_regions(e->subs.data(), nq);
+        need = tr.bytes;
     }
     if (need > e->h_arena_cap) {
         if (e->h_arena) (void)hipHostFree(e->h_arena);
@@ -395,13 +369,11 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
             if ((rc = edgpu_device_alloc(e->ctx, need, &e->d_gather))) return eg_fail(e, rc, "gather buffer");
             e->d_gather_cap = need;
         }
-        if ((rc = edgpu_arena_gather(e->ctx, r, reg.data(), (uint32_t)reg.size(), e->d_gather, e->d_gather_cap)) ||
+        if ((rc = edgpu_arena_gather(e->ctx, r, tr.reg.data(), (uint32_t)tr.reg.size(), e->d_gather, e->d_gather_cap)) ||
             (rc = edgpu_copy_to_host(e->ctx, e->h_arena, e->d_gather, need)))
             return eg_fail(e, rc, "gather / copy to host");
-        std::vector<uint64_t> roff(reg.size() + 1, 0);
-        for (size_t i = 0; i < reg.size(); i++) roff[i + 1] = roff[i] + reg[i].bytes;
         for (uint32_t q = 0; q < nq; q++)
-            if (src[q].first != 0xFFFFFFFFu) e->base[q] = e->h_arena + roff[src[q].first] + src[q].second;
+            if (tr.src[q].first != edgpu_host::TickRegions::kNone) e->base[q] = tr.at(e->h_arena, q);
     } else {
         if ((rc = edgpu_copy_to_host(e->ctx, e->h_arena, r->arena, st.arena_bytes))) return eg_fail(e, rc, "copy to host");
         for (uint32_t q = 0; q < nq; q++) e->base[q] = e->h_arena + e->subs[q].out_base;

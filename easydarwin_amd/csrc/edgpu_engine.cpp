@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -110,6 +111,8 @@ struct SessionHost {
     bool udp_push;
     uint32_t eyes = 0;              // client outputs (ReflectorStream::fEyeCount, every track)
     std::vector<SourceHost> src;    // per track
+    bool alive = true;              // false after edgpu_session_remove (its id may be reused)
+    std::vector<uint32_t> subs;     // attached subscriber handles
 };
 
 // RTCPSRPacket::GetACName (RTCPSRPacket.cpp:87-117): item type 1, length byte, "QTSS<secs>",
@@ -179,8 +182,11 @@ struct edgpu_ctx {
     uint32_t n_rw = 0;                  // active sub-streams with a rewrite
     uint32_t n_tcp = 0;                 // active RTSP-interleaved sub-streams (channel-byte patch)
     uint32_t nsenders = 0, nstreams = 0;
-    std::vector<void*> ring_allocs;
+    std::vector<void*> snd_meta, snd_ring;   // per sender: its rings (null once its session is removed)
+    std::vector<uint32_t> dead_sessions;     // removed session ids, reused by edgpu_session_add
+    std::map<uint32_t, std::vector<uint32_t>> free_subs;   // SubDev ranges of removed subscribers, by size
     uint64_t work_cap_needed = 0;
+    void* d_null = nullptr;                  // zeroed 4 KiB: the rings of a removed session's senders
 
     DevVec<SessionDev> d_sessions;
     DevVec<SenderDev> d_senders;
@@ -257,6 +263,8 @@ struct edgpu_ctx {
     TickTotals* d_totals = nullptr;
 };
 
+static bool live_session(const edgpu_ctx* x, uint32_t s) { return s < x->sessions.size() && x->sessions[s].alive; }
+
 extern "C" {
 
 const char* edgpu_version(void) { return "edgpu 0.1 (gfx950)"; }
@@ -328,11 +336,14 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
         if (hipEventCreateWithFlags(&x->ev_copy, hipEventDisableTiming) != hipSuccess) return bad("event");
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    if (hipMalloc(&x->d_null, 4096) != hipSuccess || hipMemset(x->d_null, 0, 4096) != hipSuccess) return bad("null ring");
     if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
-    if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);   // timing experiments only
+#ifdef EDGPU_AB_VARIANTS                         // measurement builds only (edgpu_params.h)
+    if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 3);
+#endif
     *out = x;
     return EDGPU_OK;
 }
@@ -342,7 +353,9 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     (void)hipSetDevice(x->device);
     if (x->stream) (void)hipStreamSynchronize(x->stream);
     if (x->copy) (void)hipStreamSynchronize(x->copy);
-    for (void* p : x->ring_allocs) (void)hipFree(p);
+    for (void* p : x->snd_meta) if (p) (void)hipFree(p);
+    for (void* p : x->snd_ring) if (p) (void)hipFree(p);
+    if (x->d_null) (void)hipFree(x->d_null);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_count.release();
@@ -497,26 +510,63 @@ int edgpu_sdp_parse(const char* sdp, uint32_t sdp_len, edgpu_sdp_track* out, uin
     return EDGPU_OK;
 }
 
+// A removed session's sender records: rings point at the zeroed null buffer (a one-packet,
+// one-word ring), nothing enqueued, so every per-sender kernel finds an empty sender.
+static SenderDev dead_sender(const edgpu_ctx* x, uint32_t sid) {
+    SenderDev D;
+    memset(&D, 0, sizeof(D));
+    D.meta = D.ring = (uint64_t)(uintptr_t)x->d_null;
+    D.session = sid;
+    D.key = -1;
+    D.last_nonzero = -1;
+    D.new_start = -1;
+    return D;
+}
+
 int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_push, uint32_t* out_session) {
     if (!x || !sdp) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
     std::vector<TrackHost> tracks = parse_sdp(sdp, sdp_len);
     if (tracks.empty() || tracks.size() > kMaxTracks)
         return fail(EDGPU_BAD_ARGUMENT, "SDP must describe 1..16 tracks");
-    const uint32_t sid = (uint32_t)x->sessions.size();
-    SessionHost sh{x->nsenders, (uint32_t)tracks.size(), x->nstreams, udp_push != 0};
+    // a removed session with as many tracks gives its id and table rows (senders, streams)
+    uint32_t sid = (uint32_t)x->sessions.size();
+    bool reuse = false;
+    for (size_t k = 0; k < x->dead_sessions.size(); k++)
+        if (x->sessions[x->dead_sessions[k]].ntracks == tracks.size()) {
+            sid = x->dead_sessions[k];
+            x->dead_sessions.erase(x->dead_sessions.begin() + (long)k);
+            reuse = true;
+            break;
+        }
+    const uint32_t ntracks = (uint32_t)tracks.size();
+    const uint32_t first_sender = reuse ? x->sessions[sid].first_sender : x->nsenders;
+    const uint32_t first_stream = reuse ? x->sessions[sid].first_stream : x->nstreams;
+    SessionHost sh{first_sender, ntracks, first_stream, udp_push != 0};
     // receiver-report identity, as the ReflectorStream constructor draws it (:164-201)
     const int64_t wall_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
         std::chrono::system_clock::now().time_since_epoch()).count();
     sh.src.resize(sh.ntracks);
     for (auto& h : sh.src) { h.rr_ssrc = (uint32_t)::rand(); h.cname = source_cname(wall_ms / 1000); }
     const uint32_t nsnd = 2 * sh.ntracks;
-    HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
-    HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));
-    HIP_CHECK(x->d_streams.reserve(x->nstreams + sh.ntracks, x->stream));
-    HIP_CHECK(x->d_sub_range.reserve(2 * (x->nsenders + nsnd), x->stream));
+    if (!reuse) {
+        HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
+        HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));
+        HIP_CHECK(x->d_streams.reserve(x->nstreams + sh.ntracks, x->stream));
+        HIP_CHECK(x->d_sub_range.reserve(2 * (x->nsenders + nsnd), x->stream));
+        x->snd_meta.resize(x->nsenders + nsnd, nullptr);
+        x->snd_ring.resize(x->nsenders + nsnd, nullptr);
+    }
     std::vector<SenderDev> snd(nsnd);
     std::vector<StreamDev> str(sh.ntracks);
+    auto undo = [&](uint32_t upto) {            // frees the rings allocated so far
+        for (uint32_t i = 0; i < upto; i++)
+            for (auto* v : {&x->snd_meta, &x->snd_ring}) {
+                void*& p = (*v)[first_sender + i];
+                if (p) (void)hipFree(p);
+                p = nullptr;
+            }
+    };
     for (uint32_t t = 0; t < sh.ntracks; t++) {
         uint32_t base = 0;
         if (tracks[t].type == 1) base |= kSndVideo;
@@ -529,17 +579,18 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             const uint64_t pk = big ? x->cfg.video_ring_packets : x->cfg.other_ring_packets;
             const uint64_t by = big ? x->cfg.video_ring_bytes : x->cfg.other_ring_bytes;
             void* meta = nullptr; void* ring = nullptr;
-            if (dmalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring");
-            x->ring_allocs.push_back(meta);
-            if (dmalloc(&ring, by) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring");
-            x->ring_allocs.push_back(ring);
+            const uint32_t gs = first_sender + 2 * t + k;
+            if (dmalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) { undo(2 * t + k); return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring"); }
+            x->snd_meta[gs] = meta;
+            if (dmalloc(&ring, by) != hipSuccess) { undo(2 * t + k + 1); return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring"); }
+            x->snd_ring[gs] = ring;
             D.meta = (uint64_t)(uintptr_t)meta;
             D.ring = (uint64_t)(uintptr_t)ring;
             D.pk_mask = (uint32_t)(pk - 1);
             D.word_mask = (uint32_t)(by / 16 - 1);
             D.flags = base | (k ? kSndRtcpKind : 0u) | ((k && sh.udp_push) ? kSndRtcpPort : 0u);
             D.session = sid;
-            D.stream = x->nstreams + t;
+            D.stream = first_stream + t;
             D.track = t;
             D.key = -1;
             D.last_nonzero = -1;
@@ -549,31 +600,117 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
         str[t].packet_count = 0;
     }
     SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream};
-    HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + x->nsenders, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + x->nstreams, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + sid, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
-    x->sessions.push_back(sh);
-    x->nsenders += nsnd;
-    x->nstreams += sh.ntracks;
+    if (reuse) {
+        x->sessions[sid] = sh;
+    } else {
+        x->sessions.push_back(sh);
+        x->nsenders += nsnd;
+        x->nstreams += sh.ntracks;
+    }
+    if (sid < x->carry_len.size()) x->carry_len[sid] = 0;     // no interleaved frame carried over
     x->index_dirty = true;
     if (out_session) *out_session = sid;
     return EDGPU_OK;
 }
 
+// Deactivates subscriber `handle`'s sub-streams (host mirror + device flag, enqueued; the caller
+// synchronises) and returns its SubDev range to the free list.
+static int detach_subscriber(edgpu_ctx* x, uint32_t handle) {
+    SubscriberHost& s = x->subscribers[handle];
+    static const uint8_t zero = 0;              // the copies are enqueued: static storage
+    for (uint32_t i = 0; i < s.nsub; i++) {
+        x->sub_active[s.first_sub + i] = 0;
+        if (x->sub_rw[s.first_sub + i]) { x->sub_rw[s.first_sub + i] = 0; x->n_rw--; }
+        HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(x->d_subs.ptr + s.first_sub + i) + offsetof(SubDev, active),
+                                 &zero, 1, hipMemcpyHostToDevice, x->stream));
+    }
+    s.active = false;
+    if (s.transport == EDGPU_TRANSPORT_TCP) x->n_tcp -= s.nsub;
+    SessionHost& sh = x->sessions[s.session];
+    sh.eyes--;                                   // RemoveOutput(..., isClient) -> DecEyeCount
+    sh.subs.erase(std::find(sh.subs.begin(), sh.subs.end(), handle));
+    x->free_subs[s.nsub].push_back(s.first_sub);
+    x->index_dirty = true;
+    return EDGPU_OK;
+}
+
+int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
+    if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (flags & ~EDGPU_SESSION_KILL_OUTPUTS) return fail(EDGPU_BAD_ARGUMENT, "bad flags");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    SessionHost& sh = x->sessions[session];
+    if (!sh.subs.empty() && !(flags & EDGPU_SESSION_KILL_OUTPUTS))
+        return fail(EDGPU_ERR, "session still has outputs (the reference keeps a ReflectorSession while outputs "
+                               "hold references to it; pass EDGPU_SESSION_KILL_OUTPUTS to tear them down)");
+    HIP_CHECK(hipSetDevice(x->device));
+    // TearDownAllOutputs: every attached subscriber goes with it
+    while (!sh.subs.empty()) { int r = detach_subscriber(x, sh.subs.back()); if (r) return r; }
+    // the rings may still be read by a fan-out copy in flight (overlap_ticks) or a pinned batch
+    HIP_CHECK(sync_all(x));
+    if (x->h2d) HIP_CHECK(hipStreamSynchronize(x->h2d));
+    const uint32_t nsnd = 2 * sh.ntracks;
+    std::vector<SenderDev> old(nsnd), snd(nsnd, dead_sender(x, session));
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(old.data(), x->d_senders.ptr + sh.first_sender, nsnd * sizeof(SenderDev)));
+        HIP_CHECK(rb.run());
+    }
+    for (uint32_t i = 0; i < nsnd; i++) {
+        const uint32_t gs = sh.first_sender + i;
+        x->work_cap_needed -= ((uint64_t)old[i].pk_mask + 1) / 16 + 1;
+        snd[i].stream = old[i].stream;
+        snd[i].track = old[i].track;
+        for (auto* v : {&x->snd_meta, &x->snd_ring}) {
+            void*& p = (*v)[gs];
+            if (p) HIP_CHECK(hipFree(p));
+            p = nullptr;
+        }
+    }
+    std::vector<StreamDev> str(sh.ntracks);
+    for (auto& st : str) st.packet_count = 0;
+    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream};
+    HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sh.first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + sh.first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + session, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    sh.alive = false;
+    sh.eyes = 0;
+    for (auto& h : sh.src) h = SourceHost();
+    if (session < x->carry_len.size()) x->carry_len[session] = 0;
+    x->dead_sessions.push_back(session);
+    x->index_dirty = true;
+    return EDGPU_OK;
+}
+
 int edgpu_session_tracks(edgpu_ctx* x, uint32_t session, uint32_t* out_tracks) {
-    if (!x || session >= x->sessions.size() || !out_tracks) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (!x || !live_session(x, session) || !out_tracks) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     *out_tracks = x->sessions[session].ntracks;
     return EDGPU_OK;
 }
 
-// Appends one subscriber's sub-streams (RTPSessionOutput + ReflectorSession::AddOutput) to the
-// host tables and to `v` (the SubDev records still to be uploaded); returns its handle.
+// Adds one subscriber's sub-streams (RTPSessionOutput + ReflectorSession::AddOutput) to the
+// host tables -- in a removed subscriber's SubDev range of the same size when there is one,
+// else at the end -- and its records to `v` as (SubDev index, record) for upload_subs; returns
+// its handle (handles are never reused).
 static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport, uint32_t flags,
-                                  const uint16_t* first_seq, std::vector<SubDev>& v) {
-    const SessionHost& sh = x->sessions[session];
+                                  const uint16_t* first_seq, std::vector<std::pair<uint32_t, SubDev>>& v) {
+    SessionHost& sh = x->sessions[session];
     const uint32_t handle = (uint32_t)x->subscribers.size();
-    const uint32_t first = (uint32_t)x->sub_sender.size();
+    const uint32_t nsub = 2 * sh.ntracks;
+    uint32_t first = (uint32_t)x->sub_sender.size();
+    auto fr = x->free_subs.find(nsub);
+    if (fr != x->free_subs.end() && !fr->second.empty()) {
+        first = fr->second.back();
+        fr->second.pop_back();
+    } else {
+        x->sub_sender.resize(first + nsub, 0);
+        x->sub_active.resize(first + nsub, 0);
+        x->sub_rw.resize(first + nsub, 0);
+    }
     for (uint32_t t = 0; t < sh.ntracks; t++)
         for (uint32_t k = 0; k < 2; k++) {
             SubDev Q;
@@ -588,16 +725,35 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             Q.bookmark = -1;
             Q.first_seq = (k == 0 && first_seq) ? first_seq[t] : 0;
             Q.rtp_info = (k == 0 && (flags & EDGPU_PLAY_RTP_INFO)) ? 1 : 0;
-            x->sub_sender.push_back(Q.sender);
-            x->sub_active.push_back(1);
-            x->sub_rw.push_back(0);
-            v.push_back(Q);
+            const uint32_t q = first + 2 * t + k;
+            x->sub_sender[q] = Q.sender;
+            x->sub_active[q] = 1;
+            x->sub_rw[q] = 0;
+            v.emplace_back(q, Q);
         }
-    x->subscribers.push_back(SubscriberHost{session, first, 2 * sh.ntracks, true, transport});
-    if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += 2 * sh.ntracks;
-    x->sessions[session].eyes++;                 // AddOutput(..., isClient) -> IncEyeCount
+    x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport});
+    if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += nsub;
+    sh.eyes++;                                   // AddOutput(..., isClient) -> IncEyeCount
+    sh.subs.push_back(handle);
     x->index_dirty = true;
     return handle;
+}
+
+// Uploads SubDev records (index, record) -- consecutive indices in one copy each run.
+static int upload_subs(edgpu_ctx* x, const std::vector<std::pair<uint32_t, SubDev>>& v) {
+    if (v.empty()) return EDGPU_OK;
+    HIP_CHECK(x->d_subs.reserve(x->sub_sender.size(), x->stream));
+    std::vector<SubDev> run;
+    for (size_t i = 0; i < v.size();) {
+        size_t j = i;
+        run.clear();
+        while (j < v.size() && v[j].first == v[i].first + (j - i)) run.push_back(v[j++].second);
+        HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + v[i].first, run.data(), run.size() * sizeof(SubDev),
+                                 hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipStreamSynchronize(x->stream));     // `run` is reused
+        i = j;
+    }
+    return EDGPU_OK;
 }
 
 // HaveStreamBuffers for an RTP-Info PLAY (QTSSReflectorModule.cpp:1804-1865), every track
@@ -656,7 +812,7 @@ int edgpu_subscriber_add(edgpu_ctx* x, uint32_t session, int transport, uint32_t
 
 int edgpu_subscriber_play(edgpu_ctx* x, uint32_t session, int transport, uint32_t flags, int64_t now_ms,
                           uint32_t* out_handle, edgpu_rtp_info* out_info) {
-    if (!x || session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (transport != EDGPU_TRANSPORT_UDP && transport != EDGPU_TRANSPORT_TCP)
         return fail(EDGPU_BAD_ARGUMENT, "bad transport");
     if (flags & ~EDGPU_PLAY_RTP_INFO) return fail(EDGPU_BAD_ARGUMENT, "bad play flags");
@@ -668,12 +824,10 @@ int edgpu_subscriber_play(edgpu_ctx* x, uint32_t session, int transport, uint32_
         const int r = first_packet_info(x, sh, now_ms, first_seq, out_info);
         if (r) return r;
     }
-    std::vector<SubDev> v;
-    const uint32_t first = (uint32_t)x->sub_sender.size();
+    std::vector<std::pair<uint32_t, SubDev>> v;
     const uint32_t handle = append_subscriber(x, session, transport, flags, first_seq.data(), v);
-    HIP_CHECK(x->d_subs.reserve(first + v.size(), x->stream));
-    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), v.size() * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    const int r = upload_subs(x, v);
+    if (r) return r;
     if (out_handle) *out_handle = handle;
     return EDGPU_OK;
 }
@@ -682,41 +836,27 @@ int edgpu_subscribers_add(edgpu_ctx* x, uint32_t n, const uint32_t* sessions, co
                           uint32_t* out_handles) {
     if (!x || (n && (!sessions || !transports))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     for (uint32_t i = 0; i < n; i++) {
-        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
         if (transports[i] != EDGPU_TRANSPORT_UDP && transports[i] != EDGPU_TRANSPORT_TCP)
             return fail(EDGPU_BAD_ARGUMENT, "bad transport");
     }
     if (!n) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
-    std::vector<SubDev> v;
-    const uint32_t first = (uint32_t)x->sub_sender.size();
+    std::vector<std::pair<uint32_t, SubDev>> v;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t h = append_subscriber(x, sessions[i], transports[i], 0, nullptr, v);
         if (out_handles) out_handles[i] = h;
     }
-    HIP_CHECK(x->d_subs.reserve(first + v.size(), x->stream));
-    HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + first, v.data(), v.size() * sizeof(SubDev), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
-    return EDGPU_OK;
+    return upload_subs(x, v);
 }
 
 int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     if (!x || handle >= x->subscribers.size() || !x->subscribers[handle].active)
         return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
     HIP_CHECK(hipSetDevice(x->device));
-    SubscriberHost& s = x->subscribers[handle];
-    const uint8_t zero = 0;
-    for (uint32_t i = 0; i < s.nsub; i++) {
-        x->sub_active[s.first_sub + i] = 0;
-        if (x->sub_rw[s.first_sub + i]) { x->sub_rw[s.first_sub + i] = 0; x->n_rw--; }
-        HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(x->d_subs.ptr + s.first_sub + i) + offsetof(SubDev, active),
-                                 &zero, 1, hipMemcpyHostToDevice, x->stream));
-    }
+    const int r = detach_subscriber(x, handle);
+    if (r) return r;
     HIP_CHECK(hipStreamSynchronize(x->stream));
-    s.active = false;
-    if (s.transport == EDGPU_TRANSPORT_TCP) x->n_tcp -= s.nsub;
-    x->sessions[s.session].eyes--;               // RemoveOutput(..., isClient) -> DecEyeCount
-    x->index_dirty = true;
     return EDGPU_OK;
 }
 
@@ -760,7 +900,7 @@ static bool rtcp_sr_first(const uint8_t* h, uint32_t len) {
 int edgpu_udp_sources(edgpu_ctx* x, const edgpu_udp_source* src, uint32_t n) {
     if (!x || (n && !src)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     for (uint32_t i = 0; i < n; i++)
-        if (src[i].session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (!live_session(x, src[i].session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     for (uint32_t i = 0; i < n; i++) {
         const edgpu_udp_source& d = src[i];
         SessionHost& sh = x->sessions[d.session];
@@ -783,6 +923,7 @@ static void queue_source_reports(edgpu_ctx* x, int64_t now) {
     x->source_reports.clear();
     for (uint32_t si = 0; si < x->sessions.size(); si++) {
         SessionHost& sh = x->sessions[si];
+        if (!sh.alive) continue;
         for (uint32_t t = 0; t < sh.ntracks; t++) {
             SourceHost& h = sh.src[t];
             if (!(now > h.last_rr + 5000)) continue;              // kRRInterval
@@ -820,7 +961,7 @@ int edgpu_source_reports(edgpu_ctx* x, edgpu_source_report* out, uint32_t cap, u
 }
 
 int edgpu_session_eyes_add(edgpu_ctx* x, uint32_t session, int32_t delta) {
-    if (!x || session >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     SessionHost& sh = x->sessions[session];
     if (delta < 0 && (uint32_t)(-(int64_t)delta) > sh.eyes) return fail(EDGPU_BAD_ARGUMENT, "eye count below zero");
     sh.eyes = (uint32_t)((int64_t)sh.eyes + delta);
@@ -828,7 +969,7 @@ int edgpu_session_eyes_add(edgpu_ctx* x, uint32_t session, int32_t delta) {
 }
 
 int edgpu_source_identity(edgpu_ctx* x, uint32_t session, uint32_t track, uint32_t ssrc, int64_t cname_secs) {
-    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks)
+    if (!x || !live_session(x, session) || track >= x->sessions[session].ntracks)
         return fail(EDGPU_BAD_ARGUMENT, "bad session / track");
     SourceHost& h = x->sessions[session].src[track];
     h.rr_ssrc = ssrc;
@@ -933,7 +1074,7 @@ static int validate_host_batch(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_
     if (nseg && seg_off[nseg] != n) return fail(EDGPU_BAD_ARGUMENT, "seg_offsets[n_segments] != n_packets");
     for (uint32_t s = 0; s < nseg; s++) {
         if (seg_off[s] > seg_off[s + 1]) return fail(EDGPU_BAD_ARGUMENT, "segments not monotone");
-        if (seg_sess[s] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in batch");
+        if (!live_session(x, seg_sess[s])) return fail(EDGPU_BAD_ARGUMENT, "unknown session in batch");
     }
     for (uint32_t i = 0; i < n; i++)
         if ((uint64_t)desc[i].slot * 16 + ((std::min<uint32_t>(desc[i].len, kMaxPacket) + 4 + 15) & ~15u) > blob_bytes)
@@ -1052,7 +1193,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     std::vector<uint8_t> seen(x->sessions.size(), 0);
     for (uint32_t i = 0; i < n;) {
         const uint32_t s = reads[i].session;
-        if (s >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "unknown session in reads");
+        if (!live_session(x, s)) return fail(EDGPU_BAD_ARGUMENT, "unknown session in reads");
         if (x->sessions[s].udp_push) return fail(EDGPU_BAD_ARGUMENT, "interleaved reads for a UDP-push session");
         if (seen[s]) return fail(EDGPU_BAD_ARGUMENT, "a session's reads must be consecutive entries");
         seen[s] = 1;
@@ -1402,7 +1543,7 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
 }
 
 int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out_packets, uint64_t* out_bytes) {
-    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks)
+    if (!x || !live_session(x, session) || track >= x->sessions[session].ntracks)
         return fail(EDGPU_BAD_ARGUMENT, "bad session/track");
     HIP_CHECK(hipSetDevice(x->device));
     SenderDev D;
@@ -1424,7 +1565,7 @@ int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out
 
 int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst, uint64_t cap,
                    uint64_t* out_len, uint32_t* out_packets) {
-    if (!x || session >= x->sessions.size() || track >= x->sessions[session].ntracks || (!dst && cap))
+    if (!x || !live_session(x, session) || track >= x->sessions[session].ntracks || (!dst && cap))
         return fail(EDGPU_BAD_ARGUMENT, "bad argument");
     HIP_CHECK(hipSetDevice(x->device));
     SenderDev D;
@@ -1504,7 +1645,7 @@ int edgpu_session_export(edgpu_ctx* x, const uint32_t* sessions, uint32_t n, int
     HIP_CHECK(hipSetDevice(x->device));
     std::vector<ImgPlan> plan;
     for (uint32_t i = 0; i < n; i++) {
-        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
         const SessionHost& sh = x->sessions[sessions[i]];
         for (uint32_t ls = 0; ls < 2 * sh.ntracks; ls++) {
             ImgPlan E;
@@ -1548,7 +1689,7 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     HIP_CHECK(hipSetDevice(x->device));
     std::vector<ImgPlan> plan;
     for (uint32_t i = 0; i < n; i++) {
-        if (sessions[i] >= x->sessions.size()) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+        if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
         if (offsets[i] % 16 || offsets[i + 1] < offsets[i] + sizeof(ImgHeader))
             return fail(EDGPU_BAD_ARGUMENT, "bad image offsets");
         const SessionHost& sh = x->sessions[sessions[i]];

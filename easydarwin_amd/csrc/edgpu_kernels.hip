@@ -356,7 +356,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         // ---- per-sender queue index / slot offset / non-empty count ----
         uint32_t my_rank = 0, my_nzpre = 0;
         uint64_t my_slotpre = 0;
-        for (uint32_t s = 0; s < ((P.ablate & 64u) ? 0u : nsnd); s++) {
+        for (uint32_t s = 0; s < ((EDGPU_ABL(P) & 64u) ? 0u : nsnd); s++) {
             const bool mine = acc && ls == s;
             const uint64_t x = mine ? (1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20) : 0ull;
             uint64_t tot;
@@ -401,13 +401,13 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         __syncthreads();
         // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
-        if (P.ablate & 32u) {
+        if (EDGPU_ABL(P) & 32u) {
             // timing ablation only: no slot copy
-        } else if (P.copy_mode == 0 && P.src_addr && P.tcp_copy >= 1) {   // frames inside the TCP byte stream
-            if (P.tcp_copy == 3) tcp_slot_copy_s<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
-            else if (P.tcp_copy >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+        } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr && EDGPU_TCP_COPY(P) >= 1) {   // frames inside the TCP byte stream
+            if (EDGPU_TCP_COPY(P) == 3) tcp_slot_copy_s<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+            else if (EDGPU_TCP_COPY(P) >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else tcp_slot_copy<1, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
-        } else if (P.copy_mode == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
+        } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
             const int lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += THREADS / 64) {
                 const uint32_t sb = p_slotb[p];
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
                 if (lane + 64 < nw) ring[(w0 + lane + 64) & wm] = v1;
                 if (lane + 128 < nw) ring[(w0 + lane + 128) & wm] = v2;
             }
-        } else if (P.copy_mode == 0) {
+        } else if (EDGPU_COPY_MODE(P) == 0) {
             // kDepth packets per wave per round, and a slot is at most 129 words (2060 + 4 B),
             // so every lane issues all of its loads (<= 3 x 16 B per packet) before its first
             // store: a wave keeps kDepth whole slots in flight instead of waiting out one load
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
     const uint64_t a1 = block_exclusive_scan<uint64_t, NW>(in_pk, scan64, t1);
     const uint64_t a2 = block_exclusive_scan<uint64_t, NW>(in_bytes, scan64, t2);
     (void)a1; (void)a2;
-    if (tid == 0 && !(P.ablate & 16u)) {
+    if (tid == 0 && !(EDGPU_ABL(P) & 16u)) {
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
     }
@@ -1065,7 +1065,7 @@ void k_fanout3(FanoutParams P) {
                 q_hl[tid] = Q.transport ? 4u : 0u;
             }
             __syncthreads();
-            for (uint32_t q = 0; q < nq && !(P.ablate & 2u); q++) {
+            for (uint32_t q = 0; q < nq && !(EDGPU_ABL(P) & 2u); q++) {
                 const uint32_t fw = uni(q_fw[q]);
                 if (fw >= nw) continue;
                 const int64_t A = (int64_t)uni64((uint64_t)q_dw0[q]) + fw;     // first dest word
@@ -1092,7 +1092,7 @@ void k_fanout3(FanoutParams P) {
                 // non-empty packets of this chunk: ordinals [0, nzc)
                 const uint32_t nzc = (uint32_t)__builtin_amdgcn_readfirstlane(
                     (int)(np ? m_vc[np - 1] - m_vc[0] + (m_len[np - 1] != 0) : 0));
-                for (uint32_t q = wv; q < (P.ablate & 1u ? 0u : nq); q += NWAVES) {
+                for (uint32_t q = wv; q < (EDGPU_ABL(P) & 1u ? 0u : nq); q += NWAVES) {
                     const uint32_t p0 = q_p0[q];
                     if (p0 >= np) continue;
                     const uint32_t o0 = m_vc[p0] - m_vc[0];                   // first ordinal
@@ -1370,7 +1370,7 @@ void k_fanout4(FanoutParams P) {
     FanWork nx;
     if (w < nwork) {
         nx = const_load(P.work + w);
-        fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
+        fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (EDGPU_ABL(P) & 4u) != 0);
         if constexpr (LFS) {
             const uint32_t nq = min(nx.qe - nx.qb, (uint32_t)kLfs);
             if ((uint32_t)tid < nq * kFsw) fsw = reinterpret_cast<const uint32_t*>(P.fansub + nx.qb)[tid];
@@ -1416,7 +1416,7 @@ void k_fanout4(FanoutParams P) {
         wpref = wn;
         if (wn < nwork) {
             nx = const_load(P.work + wn);
-            fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (P.ablate & 4u) != 0);
+            fan4_issue<THREADS, NL, LAUX>(nx, tid, r, ma, mb, (EDGPU_ABL(P) & 4u) != 0);
             if constexpr (LFS) {
                 const uint32_t nq = min(nx.qe - nx.qb, (uint32_t)kLfs);
                 if ((uint32_t)tid < nq * kFsw) fsw = reinterpret_cast<const uint32_t*>(P.fansub + nx.qb)[tid];
@@ -1426,7 +1426,7 @@ void k_fanout4(FanoutParams P) {
         constexpr uint32_t WT = HW ? THREADS / 2 : THREADS;                    // lanes per window
         const uint32_t wtid = HW ? (uint32_t)tid % WT : (uint32_t)tid;
         const uint32_t q0 = HW ? uni((uint32_t)tid / WT) : 0u;
-        for (uint32_t q = it.qb + q0; q < it.qe && !(P.ablate & 2u); q += HW ? 2u : 1u) {
+        for (uint32_t q = it.qb + q0; q < it.qe && !(EDGPU_ABL(P) & 2u); q += HW ? 2u : 1u) {
             const FanSub f = fansub(it, q);
             if (f.a >= lo + np) continue;
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -1466,7 +1466,7 @@ void k_fanout4(FanoutParams P) {
         // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
         {
             const uint32_t nzc = np ? m_vc[np - 1] - vc0 + (m_len[np - 1] != 0) : 0u;
-            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+            for (uint32_t q = it.qb + wv; q < it.qe && !(EDGPU_ABL(P) & 1u); q += NWAVES) {
                 const FanSub f = fansub(it, q);
                 if (f.a >= lo + np) continue;
                 const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -1623,7 +1623,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
         // ---- write the chunk to every sub-stream of the sender ----------------------------
         FanSub fnext;
         bool have_next = false;                                            // PF: fnext is record q
-        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+        for (uint32_t q = it.qb; q < it.qe && !(EDGPU_ABL(P) & 2u); q++) {
             const FanSub f = (PF && have_next) ? fnext : const_load(P.fansub + q);
             have_next = false;
             if (f.a >= lo + np) continue;
@@ -1674,7 +1674,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
         // ---- descriptors: one wave per sub-stream, a 128-B-aligned window of its array ----
         {
             const uint32_t nzc = np ? m.vc[np - 1] - vc0 + (m.len[np - 1] != 0) : 0u;
-            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+            for (uint32_t q = it.qb + wv; q < it.qe && !(EDGPU_ABL(P) & 1u); q += NWAVES) {
                 const FanSub f = const_load(P.fansub + q);
                 if (f.a >= lo + np) continue;
                 const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -1859,7 +1859,7 @@ void k_fanout5(FanoutParams P) {
         if (wn + gridDim.x < nwork) nxt = const_load(P.work + wn + gridDim.x);
         // ---- write the chunk to every sub-stream of the sender (k_fanout3's line-aligned
         // windows, uniform trip count) ----
-        for (uint32_t q = it.qb; q < it.qe && !(P.ablate & 2u); q++) {
+        for (uint32_t q = it.qb; q < it.qe && !(EDGPU_ABL(P) & 2u); q++) {
             const FanSub f = const_load(P.fansub + q);
             if (f.a >= lo + np) continue;
             const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -1884,7 +1884,7 @@ void k_fanout5(FanoutParams P) {
         {
             const u32x4 ml = mb[2 * (np - 1) + 1];
             const uint32_t nzc = np ? ml.w - vc0 + ((ml.z & 0xFFFFu) != 0) : 0u;
-            for (uint32_t q = it.qb + wv; q < it.qe && !(P.ablate & 1u); q += NWAVES) {
+            for (uint32_t q = it.qb + wv; q < it.qe && !(EDGPU_ABL(P) & 1u); q += NWAVES) {
                 const FanSub f = const_load(P.fansub + q);
                 if (f.a >= lo + np) continue;
                 const uint32_t p0 = f.a > lo ? (uint32_t)(f.a - lo) : 0u;
@@ -2139,7 +2139,7 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
     else if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
-    if (p.npk && p.copy_mode == 1) {
+    if (p.npk && EDGPU_COPY_MODE(p) == 1) {
         const uint32_t per = kCopyThreads / kCopyLanes;
         hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
@@ -2188,6 +2188,7 @@ static int occupancy_of(const void* fn, int threads, int lds) {
     return blocks > 0 ? blocks : 1;
 }
 struct FanoutVariant { const void* fn; int threads; int chunk; int lds; int max_wg_per_cu = 0; };
+#ifdef EDGPU_AB_VARIANTS
 static const FanoutVariant kVariants[] = {
     {(const void*)k_fanout3<1024, 32>, 1024, 32, fanout3_lds<1024, 32>()},          // 0 r01 LDS, aligned
     {(const void*)k_fanout3<512, 16>, 512, 16, fanout3_lds<512, 16>()},             // 1
@@ -2282,6 +2283,15 @@ static const char* const kVariantNames[] = {"k_fanout3<1024,32>", "k_fanout3<512
                                             "k_fanout6<896,16,nt,dyn>", "k_fanout6<768,12,nt,dyn>",
                                             "k_fanout6<1024,16,nt,dyn,pf>", "k_fanout6<1024,32,nt,dyn,pf>",
                                             "k_fanout6<1024,16,nt,dyn,bp>", "k_fanout6<1024,32,nt,dyn,bp>"};
+#else
+// The shipped library: the two defaults.  The measurement build above keeps
+// their numbers (31 and 40) and every variant they were chosen over.
+static const FanoutVariant kVariants[] = {
+    {(const void*)k_fanout4<1024, 32, 2, 0, 0, 1, 0, 0, 0, 1>, 1024, 32, fanout4_lds<1024, 32>()}, // 0 = AB 31
+    {(const void*)k_fanout6<1024, 16>, 1024, 16, fanout6_lds<1024, 16>()},                           // 1 = AB 40
+};
+static const char* const kVariantNames[] = {"k_fanout4<1024,32,nt,dyn>", "k_fanout6<1024,16,nt,dyn>"};
+#endif
 static const int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVariants) / sizeof(kVariants[0]),
               "one name per fan-out variant");
@@ -2290,13 +2300,20 @@ static_assert(sizeof(kVariantNames) / sizeof(kVariantNames[0]) == sizeof(kVarian
 // mode), k_fanout4<1024,32> when some do (RTSP-interleaved channel byte or a rewrite).  The
 // 16-packet chunks are ~4 % faster on identity windows but ~25 % slower through the patch path
 // (profiles/r02z9_*).
+#ifdef EDGPU_AB_VARIANTS
 static const int kDefaultVariant = 31;   // k_fanout4<1024,32,nt,dyn>: the patching default
 static const int kDefaultPlain = 40;     // k_fanout6<1024,16,nt,dyn>: every sub-stream identity UDP
+static const int kFirstRewriting = 2;    // k_fanout3 (0, 1) reads SubDev directly and has no rewrite stage
+#else
+static const int kDefaultVariant = 0;
+static const int kDefaultPlain = 1;
+static const int kFirstRewriting = 0;
+#endif
 int fanout_default(bool patching) { return patching ? kDefaultVariant : kDefaultPlain; }
-// k_fanout3 reads SubDev directly and has no rewrite stage (edgpu_subscriber_rewrite refuses it)
+// edgpu_subscriber_rewrite refuses a variant without a rewrite stage
 bool fanout_rewrites(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
-    return variant > 1;
+    return variant >= kFirstRewriting;
 }
 int fanout_chunk(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;

@@ -4,6 +4,21 @@
 #include "edgpu.h"
 #include "edgpu_device.h"
 
+// Measurement builds (-DEDGPU_AB_VARIANTS: `make -C easydarwin_amd/csrc ab` ->
+// easydarwin_amd/ab/libedgpu_ab.so, loaded with EDGPU_LIB) carry every fan-out variant ever
+// measured, the EDGPU_ABLATE skip-work bits and the alternative ingest copy paths
+// (EDGPU_INGEST, EDGPU_INGEST_TCP).  The shipped libedgpu.so has the two default fan-out
+// kernels and no skip-work branch: these knobs are compile-time constants there.
+#ifdef EDGPU_AB_VARIANTS
+#define EDGPU_ABL(P) ((P).ablate)
+#define EDGPU_COPY_MODE(P) ((P).copy_mode)
+#define EDGPU_TCP_COPY(P) ((P).tcp_copy)
+#else
+#define EDGPU_ABL(P) 0u
+#define EDGPU_COPY_MODE(P) 0u
+#define EDGPU_TCP_COPY(P) 3u
+#endif
+
 namespace edgpu {
 
 struct IngestParams {

@@ -10,7 +10,7 @@
 //   RTSPPreProcessor          ProcessRTSPRequest (:681-729)                 ANNOUNCE / DESCRIBE / SETUP /
 //                                                                           PLAY / RECORD / PAUSE / TEARDOWN
 //   RTSPIncomingData          ProcessRTPData (:604-678)                     '$' frame -> PushPacket
-//   ClientSessionClosing      DestroySession (:2070-2131)                   RemoveOutput
+//   ClientSessionClosing      DestroySession (:2070-2131)                   RemoveOutput / pusher leave
 //
 // and writes every relayed packet back through QTSS_Write (callback 10) on the subscriber's
 // RTP stream object with qtssWriteFlagsIsRTP / IsRTCP | WriteBurstBegin, exactly as
@@ -25,6 +25,24 @@
 // Reflect cadence: the reference reflects from ReflectorSocket tasks on packet arrival and
 // sender wakeups (ReflectorStream.cpp:1676-1714); here a tick thread reflects every
 // edgpu_tick_msec (default 20 ms), or the host calls EDGPU_QTSSReflectorModule_Tick.
+//
+// Session lifecycle: reference-counted as the reference's session map does it -- the pusher
+// holds one reference (FindOrCreateSession's Register + Resolve, :1469-1477), every output one
+// (its first SETUP's Resolve, :1388, 1616-1622).  A pusher leaving (DestroySession's broadcaster
+// branch, :2082-2109) frees its tracks for a new pusher and, with kill_clients (the client
+// session's QTSSReflectorModuleTearDownClients attribute, set from the
+// kill_clients_when_broadcast_stops pref at RECORD, :1884; here EDGPU_QTSS_KILL_CLIENTS=1),
+// tears every output down (TearDownAllOutputs -> QTSS_Teardown, whose ClientSessionClosing then
+// removes it); at reference count 0 the session ends (RemoveOutput, :2162-2192): its engine
+// session and rings, its UDP socket pairs and its announced SDP (CSdpCache::eraseSdpMap) go.
+// A pusher of a session that players kept alive continues it as it is; after the end, the next
+// pusher gets a fresh one.  A player's SETUP needs the session to exist (a pusher's SETUP made it,
+// :1391-1396: an announced-only stream is not enough).
+//
+// Locking: `mu` guards the sessions / outputs bookkeeping and is held through a tick (the
+// egress callbacks); the pushers' ingest never takes it -- RTSPIncomingData routes through
+// `routeMu` (a small table: module session -> engine session) into the Reflector's own push
+// lock, and the UDP reader thread takes only `udpMu` -- so a pusher never waits for a tick.
 //
 // Scope: RTSP-interleaved pushers (EasyPusher's default transport), UDP
 // pushers and UDP / TCP players.  A UDP push SETUP binds the track's even/odd socket pair as
@@ -105,13 +123,16 @@ bool GetPOD(QTSS_Object o, QTSS_AttributeID id, T* out) {
 // ---- module state ---------------------------------------------------------------------------
 // attributes the module adds (the reference's names, QTSSReflectorModule.cpp:313-346)
 QTSS_AttributeID sOutputAttr, sClientBroadcastSessionAttr, sRTSPBroadcastSessionAttr, sStreamCookieAttr,
-    sRequestBodyAttr, sBufferOffsetAttr, sRTPInfoWaitTimeAttr;
+    sRequestBodyAttr, sBufferOffsetAttr, sRTPInfoWaitTimeAttr, sKillClientsEnabledAttr;
 
 struct Output;
 struct Session {                        // a pushed stream ("<path>-<channel>", QRM:1384)
+    uint32_t id = 0;                    // module session id (never reused; client attributes hold it)
     std::string name;
     uint32_t engine = 0;                // edgpu session
     bool udpPush = false;               // pushed over UDP: RTCP on the odd port (Q12/Q14)
+    bool pusher = false;                // a pusher is attached (its reference)
+    uint32_t refs = 0;                  // the session map's reference count: pusher + outputs
     std::vector<uint32_t> trackIDs;     // a=control:trackID=N per m= line, SDP order
     std::vector<uint16_t> sdpPorts;     // the m= lines' ports (StreamInfo::fPort)
     std::vector<int> pair;              // UDP push: the track's socket pair (index into Module::udp)
@@ -122,9 +143,9 @@ struct Session {                        // a pushed stream ("<path>-<channel>", 
 
 // One track of a UDP push session: RTP on an even port, RTCP on the next (ReflectorSocket A/B)
 struct UdpPair {
-    int fd[2] = {-1, -1};
+    int fd[2] = {-1, -1};               // -1 once its session ended
     uint16_t port = 0;
-    uint32_t session = 0, track = 0;    // Module::sessions index, track index
+    uint32_t engine = 0, track = 0;     // engine session, track index
 };
 
 struct Output {                         // one player (RTPSessionOutput)
@@ -143,8 +164,15 @@ struct Module {
     std::mutex mu;                      // the reference's session-map / bucket mutexes, one lock here
     std::unique_ptr<edgpu_reflector::Reflector> R;
     std::map<std::string, std::string> announced;         // CSdpCache: stream name -> SDP
-    std::map<std::string, uint32_t> byName;
-    std::vector<Session> sessions;
+    std::map<std::string, uint32_t> byName;               // registered sessions: name -> id
+    std::map<uint32_t, Session> sessions;                 // by module session id
+    uint32_t nextId = 1;
+    bool killClients = false;           // kill_clients_when_broadcast_stops (QRM:476-477)
+    // the pushers' path (RTSPIncomingData): module session id -> (engine session, tracks) while a
+    // pusher is attached; guarded by routeMu alone
+    std::mutex routeMu;
+    std::map<uint32_t, std::pair<uint32_t, uint32_t>> route;
+    std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
     std::map<uint32_t, Output*> byHandle;
     std::vector<std::unique_ptr<Output>> outputs;
     std::vector<std::string> rtpInfoPlayers{"Android", "vlc"};  // player_requires_rtp_header_info
@@ -274,14 +302,17 @@ public:
     // socket to the pusher's RTCP address; the send result is ignored, as there
     void SendReceiverReport(uint32_t session, uint16_t track, uint32_t addr, uint16_t port, const uint8_t* rr,
                             uint32_t len) override {
-        for (const Session& s : M->sessions) {
+        for (const auto& kv : M->sessions) {
+            const Session& s = kv.second;
             if (s.engine != session || track >= s.pair.size() || s.pair[track] < 0) continue;
             sockaddr_in to;
             memset(&to, 0, sizeof(to));
             to.sin_family = AF_INET;
             to.sin_addr.s_addr = htonl(addr);
             to.sin_port = htons(port);
-            (void)sendto(M->udp[s.pair[track]].fd[1], rr, len, MSG_NOSIGNAL, (const sockaddr*)&to, sizeof(to));
+            std::lock_guard<std::mutex> g(M->udpMu);
+            const int fd = M->udp[s.pair[track]].fd[1];
+            if (fd >= 0) (void)sendto(fd, rr, len, MSG_NOSIGNAL, (const sockaddr*)&to, sizeof(to));
             return;
         }
     }
@@ -324,14 +355,15 @@ bool BindPair(uint16_t port, UdpPair* out) {
 // UDP push socket, read like RecvFrom into a kMaxReflectorPacketSize (2060) buffer -- a longer
 // datagram is truncated there -- and handed to the engine with its source address (the UDP RTCP
 // SR gate, Q14, and the pusher's RTCP address, :1769-1875, are the engine's).  An empty
-// datagram is the reference's "no more data" read: nothing to ingest.
-uint32_t DrainUDPLocked() {
+// datagram is the reference's "no more data" read: nothing to ingest.  Takes udpMu only.
+uint32_t DrainUDP() {
     if (!M->R) return 0;
     char buf[2060];
     uint32_t n = 0;
+    std::lock_guard<std::mutex> g(M->udpMu);
     for (const UdpPair& u : M->udp) {
-        const Session& s = M->sessions[u.session];
         for (int k = 0; k < 2; k++) {
+            if (u.fd[k] < 0) continue;
             for (;;) {
                 sockaddr_in from;
                 socklen_t fl = sizeof(from);
@@ -341,7 +373,7 @@ uint32_t DrainUDPLocked() {
                     break;                                            // EAGAIN: drained
                 }
                 if (r == 0) continue;
-                M->R->ProcessUDPPacket(s.engine, u.track, k == 1, buf, (uint32_t)r, ntohl(from.sin_addr.s_addr),
+                M->R->ProcessUDPPacket(u.engine, u.track, k == 1, buf, (uint32_t)r, ntohl(from.sin_addr.s_addr),
                                        ntohs(from.sin_port), Milliseconds());
                 n++;
             }
@@ -350,21 +382,19 @@ uint32_t DrainUDPLocked() {
     return n;
 }
 
-// the reader thread: poll every UDP push socket, drain what arrived
+// the reader thread: poll every UDP push socket, drain what arrived (never waits for a tick)
 void ReaderLoop() {
     std::vector<pollfd> pf;
     while (!M->stop.load()) {
         {
-            std::lock_guard<std::mutex> g(M->mu);
+            std::lock_guard<std::mutex> g(M->udpMu);
             pf.clear();
             for (const UdpPair& u : M->udp)
-                for (int k = 0; k < 2; k++) pf.push_back(pollfd{u.fd[k], POLLIN, 0});
+                for (int k = 0; k < 2; k++)
+                    if (u.fd[k] >= 0) pf.push_back(pollfd{u.fd[k], POLLIN, 0});
         }
         if (pf.empty()) { std::this_thread::sleep_for(std::chrono::milliseconds(5)); continue; }
-        if (poll(pf.data(), pf.size(), 10) > 0) {
-            std::lock_guard<std::mutex> g(M->mu);
-            (void)DrainUDPLocked();
-        }
+        if (poll(pf.data(), pf.size(), 10) > 0) (void)DrainUDP();
     }
 }
 
@@ -390,6 +420,8 @@ QTSS_Error Register(QTSS_Register_Params* p) {
         {qtssRTSPRequestObjectType, "QTSSReflectorModuleRequestBufferLen", qtssAttrDataTypeUInt32, &sBufferOffsetAttr},
         {qtssClientSessionObjectType, "QTSSReflectorModuleBroadcasterSession", qtssAttrDataTypeVoidPointer,
          &sClientBroadcastSessionAttr},
+        {qtssClientSessionObjectType, "QTSSReflectorModuleTearDownClients", qtssAttrDataTypeBool16,
+         &sKillClientsEnabledAttr},
         {qtssRTSPSessionObjectType, "QTSSReflectorModuleBroadcasterSession", qtssAttrDataTypeVoidPointer,
          &sRTSPBroadcastSessionAttr},
     };
@@ -405,6 +437,7 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
     std::lock_guard<std::mutex> g(M->mu);
     if (const char* v = getenv("EDGPU_QTSS_TICK_MSEC")) M->tickMs = (uint32_t)std::max(1, atoi(v));
     if (const char* v = getenv("EDGPU_QTSS_MANUAL_TICK")) M->manualTick = atoi(v) != 0;
+    if (const char* v = getenv("EDGPU_QTSS_KILL_CLIENTS")) M->killClients = atoi(v) != 0;
     edgpu_config cfg;
     edgpu_config_default(&cfg);
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
@@ -436,10 +469,17 @@ QTSS_Error Shutdown() {
     if (M->ticker.joinable()) M->ticker.join();
     if (M->reader.joinable()) M->reader.join();
     std::lock_guard<std::mutex> g(M->mu);
-    for (UdpPair& u : M->udp)
-        for (int fd : u.fd)
-            if (fd >= 0) close(fd);
-    M->udp.clear();
+    {
+        std::lock_guard<std::mutex> u(M->udpMu);
+        for (UdpPair& p : M->udp)
+            for (int& fd : p.fd)
+                if (fd >= 0) { close(fd); fd = -1; }
+        M->udp.clear();
+    }
+    {
+        std::lock_guard<std::mutex> r(M->routeMu);
+        M->route.clear();
+    }
     M->R.reset();
     return QTSS_NoErr;
 }
@@ -494,14 +534,29 @@ QTSS_Error DoDescribe(QTSS_StandardRTSP_Params* p) {
               (uint32_t)qtssWriteFlagsNoFlags);
 }
 
-// FindOrCreateSession (QRM:1379-1545): the engine session of an announced stream; the first
-// SETUP decides whether it is pushed over UDP
-Session* FindOrCreateSession(const std::string& name, bool udpPush = false) {
+Session* FindSession(uint32_t id) {
+    auto it = M->sessions.find(id);
+    return it == M->sessions.end() ? nullptr : &it->second;
+}
+
+// The pushers' route to the engine (RTSPIncomingData reads it without `mu`).
+void SetRoute(const Session& s, bool on) {
+    std::lock_guard<std::mutex> g(M->routeMu);
+    if (on) M->route[s.id] = std::make_pair(s.engine, (uint32_t)s.trackIDs.size());
+    else M->route.erase(s.id);
+}
+
+// FindOrCreateSession (QRM:1379-1545).  A player only finds a registered session (:1391-1396);
+// a pusher's SETUP registers one from the announced SDP, and its transport decides whether the
+// session is pushed over UDP.  A found session is not set up again (:1521-1531).
+Session* FindOrCreateSession(const std::string& name, bool isPush, bool udpPush = false) {
     auto it = M->byName.find(name);
-    if (it != M->byName.end()) return &M->sessions[it->second];
+    if (it != M->byName.end()) return FindSession(it->second);
+    if (!isPush) return nullptr;
     auto a = M->announced.find(name);
     if (a == M->announced.end() || !M->R) return nullptr;
     Session s;
+    s.id = M->nextId++;
     s.name = name;
     s.sdp = a->second;
     s.udpPush = udpPush;
@@ -516,9 +571,30 @@ Session* FindOrCreateSession(const std::string& name, bool udpPush = false) {
     // OS::Milliseconds()/1000 when it is built (ReflectorStream.cpp:164-201, RTCPSRPacket.cpp:87-117)
     for (uint32_t t = 0; t < s.trackIDs.size(); t++)
         (void)M->R->SetSourceIdentity(s.engine, t, (uint32_t)rand(), Milliseconds() / 1000);
-    M->sessions.push_back(s);
-    M->byName[name] = (uint32_t)M->sessions.size() - 1;
-    return &M->sessions.back();
+    const uint32_t id = s.id;
+    M->sessions[id] = s;
+    M->byName[name] = id;
+    return &M->sessions[id];
+}
+
+// One reference of `s` released; at 0 the session ends (RemoveOutput, QRM:2162-2192): UnRegister,
+// CSdpCache::eraseSdpMap, kill -- the engine session with its rings, and the UDP socket pairs.
+void ReleaseLocked(Session* s) {
+    if (s->refs > 0) s->refs--;
+    if (s->refs > 0) return;
+    SetRoute(*s, false);
+    if (M->R) (void)M->R->RemoveSession(s->engine, false);
+    {
+        std::lock_guard<std::mutex> g(M->udpMu);
+        for (int pi : s->pair)
+            if (pi >= 0)
+                for (int& fd : M->udp[pi].fd)
+                    if (fd >= 0) { close(fd); fd = -1; }
+    }
+    M->byName.erase(s->name);
+    M->announced.erase(s->name);
+    if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: session %s ended\n", s->name.c_str());
+    M->sessions.erase(s->id);
 }
 
 // SETUP (DoSetup, QRM:1597-1800)
@@ -532,17 +608,28 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     std::lock_guard<std::mutex> g(M->mu);
     if (isPush) {
         const bool udp = transport != qtssRTPTransportTypeTCP;
-        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest), udp);
-        if (!s || !digitOK || s->udpPush != udp) return QTSS_RequestFailed;
+        // the pusher's first SETUP resolves (or registers) the session and holds its reference;
+        // its later SETUPs find it on the client session (QRM:1624-1645)
+        uintptr_t held = 0;
+        Session* s = nullptr;
+        if (GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &held) && held) s = FindSession((uint32_t)held);
+        const bool first = s == nullptr;
+        if (first) s = FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
+        if (!s) return QTSS_RequestFailed;
+        // the reference sets the session up for one transport; a pusher of the other cannot join it
+        // (DeleteReflectorPushSession: the reference it took goes back, :1548-1570)
+        auto refuse = [&]() { if (first && s->refs == 0) ReleaseLocked(s); return QTSS_RequestFailed; };
+        if (!digitOK || s->udpPush != udp) return refuse();
         const int t = TrackIndex(*s, trackID);
-        if (t < 0 || s->setupToReceive[t]) return QTSS_RequestFailed;      // bad / duplicate track
+        if (t < 0 || s->setupToReceive[t]) return refuse();              // bad / duplicate track
         if (udp) {
             // the track's socket pair (BindSockets) and its port in the SETUP response
             if (s->pair[t] < 0) {
                 UdpPair u;
-                if (!BindPair(s->sdpPorts[t], &u)) return QTSS_RequestFailed;      // sCantBindReflectorSocketErr
-                u.session = (uint32_t)(s - &M->sessions[0]);
+                if (!BindPair(s->sdpPorts[t], &u)) return refuse();        // sCantBindReflectorSocketErr
+                u.engine = s->engine;
                 u.track = (uint32_t)t;
+                std::lock_guard<std::mutex> ug(M->udpMu);
                 M->udp.push_back(u);
                 s->pair[t] = (int)M->udp.size() - 1;
             }
@@ -551,27 +638,34 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         }
         QTSS_Object stream = nullptr;
         QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
-        if (e != QTSS_NoErr) return e;
+        if (e != QTSS_NoErr) { (void)refuse(); return e; }
         s->setupToReceive[t] = true;
-        const uintptr_t sid = (uintptr_t)(s - &M->sessions[0]) + 1;
+        if (first) {                                     // the pusher's reference
+            s->refs++;
+            s->pusher = true;
+            SetRoute(*s, true);
+        }
+        const uintptr_t sid = s->id;
         (void)SetValue(p->inClientSession, sClientBroadcastSessionAttr, 0, &sid, sizeof(sid));
         return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)0);
     }
-    // a player: the first SETUP creates its output (QRM:1628-1650)
+    // a player: the first SETUP creates its output and takes a reference (QRM:1614-1622)
     Output* o = nullptr;
     if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {
-        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest));
+        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest), false);
         if (!s) return QTSS_RequestFailed;
         M->outputs.emplace_back(new Output());
         o = M->outputs.back().get();
         o->client = p->inClientSession;
-        o->session = (uint32_t)(s - &M->sessions[0]);
+        o->session = s->id;
         o->tcp = transport == qtssRTPTransportTypeTCP;
         o->streams.assign(s->trackIDs.size(), nullptr);
+        s->refs++;
         (void)SetValue(p->inClientSession, sOutputAttr, 0, &o, sizeof(o));
     }
-    const Session& s = M->sessions[o->session];
-    const int t = digitOK ? TrackIndex(s, trackID) : -1;
+    Session* s = FindSession(o->session);
+    if (!s) return QTSS_RequestFailed;
+    const int t = digitOK ? TrackIndex(*s, trackID) : -1;
     if (t < 0) return QTSS_RequestFailed;
     QTSS_Object stream = nullptr;
     QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
@@ -597,11 +691,16 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
     if (!o) {                                             // the pusher's RECORD / PLAY
         uintptr_t sid = 0;
         if (!GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &sid) || !sid) return QTSS_RequestFailed;
+        // the pref decides, per pusher, whether its leaving tears the players down (QRM:1884)
+        const uint16_t kill = M->killClients ? 1 : 0;
+        (void)SetValue(p->inClientSession, sKillClientsEnabledAttr, 0, &kill, sizeof(kill));
         (void)SetValue(p->inRTSPSession, sRTSPBroadcastSessionAttr, 0, &sid, sizeof(sid));
         const bool keep = true;
         (void)SetValue(p->inRTSPRequest, qtssRTSPReqRespKeepAlive, 0, &keep, sizeof(keep));
     } else {
         std::unique_lock<std::mutex> g(M->mu);
+        Session* s = FindSession(o->session);
+        if (!s) return QTSS_RequestFailed;
         if (o->joined && o->paused) {                     // resume after PAUSE
             o->paused = false;
         } else if (!o->joined) {
@@ -611,7 +710,7 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
             if (RequiresRTPInfo(o->client)) {
                 flags = qtssPlayRespWriteTrackInfo;
                 std::vector<edgpu_rtp_info> info;
-                err = M->R->PlayRTPInfo(M->sessions[o->session].engine, tcp, Milliseconds(), &h, &info);
+                err = M->R->PlayRTPInfo(s->engine, tcp, Milliseconds(), &h, &info);
                 if (getenv("EDGPU_QTSS_DEBUG"))
                     fprintf(stderr, "QTSSReflectorModule: RTP-Info PLAY session=%u now=%lld err=%d %s\n", o->session,
                             (long long)Milliseconds(), err, err ? edgpu_last_error() : "");
@@ -635,14 +734,14 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
                     (void)SetValue(o->streams[t], qtssRTPStrFirstSeqNumber, 0, &info[t].seq, sizeof(info[t].seq));
                     (void)SetValue(o->streams[t], qtssRTPStrFirstTimestamp, 0, &info[t].rtptime, sizeof(info[t].rtptime));
                 }
-            } else if ((err = M->R->AddOutput(M->sessions[o->session].engine, tcp, &h)) != 0) {
+            } else if ((err = M->R->AddOutput(s->engine, tcp, &h)) != 0) {
                 return QTSS_RequestFailed;
             }
             o->handle = h;
             o->joined = true;
             M->byHandle[h] = o;
             // ReflectorSession::AddOutput: the first free bucket member (ReflectorStream.cpp:281-336)
-            std::vector<Output*>& slots = M->sessions[o->session].slots;
+            std::vector<Output*>& slots = s->slots;
             size_t k = 0;
             while (k < slots.size() && slots[k]) k++;
             if (k == slots.size()) slots.push_back(nullptr);
@@ -660,14 +759,18 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
     return cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, flags);
 }
 
+// RemoveOutput(output, session, false) (QRM:2133-2196): out of the buckets, delete, and the
+// output's reference on the session goes
 void RemoveOutputLocked(Output* o) {
     if (o->joined) {                    // an output whose PLAY never succeeded has no handle
         if (M->R) (void)M->R->RemoveOutput(o->handle);
         M->byHandle.erase(o->handle);
     }
-    if (o->slot >= 0) M->sessions[o->session].slots[o->slot] = nullptr;
+    Session* s = FindSession(o->session);
+    if (s && o->slot >= 0) s->slots[o->slot] = nullptr;
     for (auto it = M->outputs.begin(); it != M->outputs.end(); ++it)
         if (it->get() == o) { M->outputs.erase(it); break; }
+    if (s) ReleaseLocked(s);
 }
 
 QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
@@ -703,7 +806,8 @@ QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
     return QTSS_NoErr;
 }
 
-// RTSPIncomingData (ProcessRTPData, QRM:604-678): one '$' ch BE16(len) frame of a pusher
+// RTSPIncomingData (ProcessRTPData, QRM:604-678): one '$' ch BE16(len) frame of a pusher.  Never
+// takes `mu`: the route table and the Reflector's push lock only, so it never waits for a tick.
 QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     uintptr_t sid = 0;
     if (!GetPOD(p->inRTSPSession, sRTSPBroadcastSessionAttr, &sid) || !sid) return QTSS_NoErr;
@@ -712,12 +816,13 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     const uint8_t channel = d[1];
     // the frame's own length, as the reference reads it; never past the buffer the server gave
     const uint32_t len = std::min<uint32_t>((uint32_t)d[2] << 8 | d[3], p->inPacketLen - 4);
-    std::lock_guard<std::mutex> g(M->mu);
-    if (!M->R || sid > M->sessions.size()) return QTSS_NoErr;
-    const Session& s = M->sessions[sid - 1];
+    const int64_t now = Milliseconds();
+    std::lock_guard<std::mutex> g(M->routeMu);
+    auto it = M->route.find((uint32_t)sid);
+    if (!M->R || it == M->route.end()) return QTSS_NoErr;      // no pusher attached any more
     const uint32_t track = channel / 2;
-    if (track >= s.trackIDs.size()) return QTSS_NoErr;
-    M->R->PushPacket(s.engine, track, (const char*)d + 4, len, (channel & 1) != 0, Milliseconds());
+    if (track >= it->second.second) return QTSS_NoErr;
+    M->R->PushPacket(it->second.first, track, (const char*)d + 4, len, (channel & 1) != 0, now);
     return QTSS_NoErr;
 }
 
@@ -733,12 +838,33 @@ QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
     }
     uintptr_t sid = 0;
     if (GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &sid) && sid) {
-        // the pusher left: its tracks can be set up again (the session and its rings stay, as
-        // the reference keeps a session while outputs hold references to it)
-        std::lock_guard<std::mutex> g(M->mu);
-        if (sid <= M->sessions.size()) {
-            Session& s = M->sessions[sid - 1];
-            s.setupToReceive.assign(s.setupToReceive.size(), false);
+        // the pusher left (DestroySession's broadcaster branch, QRM:2082-2109)
+        const uintptr_t none = 0;
+        (void)SetValue(p->inClientSession, sClientBroadcastSessionAttr, 0, &none, sizeof(none));
+        uint16_t kill = 0;
+        uint32_t n = sizeof(kill);
+        if (GetValue(p->inClientSession, sKillClientsEnabledAttr, 0, &kill, &n) != QTSS_NoErr) kill = 0;
+        std::vector<QTSS_Object> teardown;
+        {
+            std::lock_guard<std::mutex> g(M->mu);
+            Session* s = FindSession((uint32_t)sid);
+            if (!s || !s->pusher) return QTSS_NoErr;
+            s->setupToReceive.assign(s->setupToReceive.size(), false);   // a new pusher may set up
+            s->pusher = false;
+            SetRoute(*s, false);
+            // RemoveOutput(NULL, session, kill): TearDownAllOutputs asks the server to close every
+            // output's client session (RTPSessionOutput::TearDown); each then comes back through
+            // ClientSessionClosing and releases its reference
+            if (kill || M->killClients)
+                for (const auto& out : M->outputs)
+                    if (out->session == s->id) teardown.push_back(out->client);
+            ReleaseLocked(s);
+        }
+        // outside `mu`: the server may close the client session before QTSS_Teardown returns
+        const uint32_t reason = qtssCliSesTearDownBroadcastEnded;
+        for (QTSS_Object c : teardown) {
+            (void)SetValue(c, qtssCliTeardownReason, 0, &reason, sizeof(reason));
+            (void)cb(kTeardownCallback, c);
         }
     }
     return QTSS_NoErr;
@@ -779,6 +905,5 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
 // UDP push sockets now; returns how many were handed to the engine.
 extern "C" uint32_t EDGPU_QTSSReflectorModule_PollUDP(void) {
     if (!M) return 0;
-    std::lock_guard<std::mutex> g(M->mu);
-    return DrainUDPLocked();
+    return DrainUDP();
 }

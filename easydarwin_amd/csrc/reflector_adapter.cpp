@@ -1,18 +1,32 @@
 // reflector_adapter.cpp -- see reflector_adapter.h.
 #include "reflector_adapter.h"
+#include "tick_regions.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
 namespace edgpu_reflector {
+
+using Clock = std::chrono::steady_clock;
+static double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
 
 Reflector::Reflector(const edgpu_config* cfg) {
     fStatus = edgpu_ctx_create(cfg, &fCtx);
 }
 
 Reflector::~Reflector() {
-    if (fCtx) edgpu_ctx_destroy(fCtx);
+    if (!fCtx) return;
+    (void)edgpu_sync(fCtx);
+    for (Batch& b : fBatch)
+        for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
+            if (p) (void)edgpu_host_free(fCtx, p);
+    if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
+    if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
+    edgpu_ctx_destroy(fCtx);
 }
 
 int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession) {
@@ -21,13 +35,17 @@ int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint3
     int err = edgpu_session_add(fCtx, sdp.data(), (uint32_t)sdp.size(), udpPush ? 1 : 0, &s);
     if (err) return err;
     if ((err = edgpu_session_tracks(fCtx, s, &n))) return err;
-    if (fTracks.size() <= s) fTracks.resize(s + 1, 0);
-    fTracks[s] = n;
+    {
+        std::lock_guard<std::mutex> g(fPushMu);
+        if (fTracks.size() <= s) fTracks.resize(s + 1, 0);
+        fTracks[s] = n;
+    }
     if (outSession) *outSession = s;
     return kNoErr;
 }
 
 uint32_t Reflector::GetNumStreams(uint32_t session) const {
+    std::lock_guard<std::mutex> g(const_cast<std::mutex&>(fPushMu));
     return session < fTracks.size() ? fTracks[session] : 0;
 }
 
@@ -53,26 +71,64 @@ int Reflector::RemoveOutput(uint32_t handle) {
     return edgpu_subscriber_remove(fCtx, handle);
 }
 
+int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
+    if (!fCtx) return kRequestFailed;
+    // what was pushed to it before the end is ingested (the reference had queued it)
+    int err = FlushIngest();
+    if (err) return err;
+    {
+        // later pushes to it are dropped, and what another thread pushed since the flush is
+        // discarded (its id may be reused by the next session)
+        std::lock_guard<std::mutex> g(fPushMu);
+        if (session < fTracks.size()) fTracks[session] = 0;
+        Batch& b = fBatch[fFill];
+        b.pushed.erase(std::remove_if(b.pushed.begin(), b.pushed.end(),
+                                      [&](const Pushed& p) { return p.session == session; }), b.pushed.end());
+        b.sources.erase(std::remove_if(b.sources.begin(), b.sources.end(),
+                                       [&](const edgpu_udp_source& u) { return u.session == session; }), b.sources.end());
+    }
+    return edgpu_session_remove(fCtx, session, killOutputs ? EDGPU_SESSION_KILL_OUTPUTS : 0);
+}
+
+// Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
+// filled: the only host copy of the packet.  The pinned blob grows by doubling (a larger buffer,
+// the slots so far copied over); the batch being filled is never one whose DMA may be in flight.
+void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
+                       int64_t nowMs, const edgpu_udp_source* src) {
+    std::lock_guard<std::mutex> g(fPushMu);
+    if (session >= fTracks.size() || track >= fTracks[session]) return;
+    Batch& b = fBatch[fFill];
+    const uint32_t clamped = std::min<uint32_t>(packetLen, 2060);   // bytes past 2060 are never read (Q11)
+    const uint64_t slot = (clamped + 4 + 15) & ~15ull;
+    if (b.used + slot > b.cap) {
+        uint64_t cap = std::max<uint64_t>(b.cap ? b.cap * 2 : (4ull << 20), b.used + slot);
+        void* nb = nullptr;
+        if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return;          // out of pinned memory: dropped
+        if (b.used) memcpy(nb, b.blob, b.used);
+        if (b.blob) (void)edgpu_host_free(fCtx, b.blob);
+        b.blob = (uint8_t*)nb;
+        b.cap = cap;
+    }
+    uint8_t* d = b.blob + b.used;
+    memset(d, 0, 4);
+    memcpy(d + 4, packet, clamped);
+    if (slot > clamped + 4) memset(d + 4 + clamped, 0, slot - clamped - 4);
+    b.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, b.used, packetLen});
+    if (src) b.sources.push_back(*src);
+    b.used += slot;
+}
+
 void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
                            bool isRTCP, int64_t nowMs) {
     // ReflectorStream::PushPacket ignores empty packets (ReflectorStream.cpp:533); the
     // '$' framing caps a pushed packet at 65535 bytes.
-    if (packetLen == 0 || track >= GetNumStreams(session)) return;
-    packetLen = std::min<uint32_t>(packetLen, 65535);
-    Pushed p;
-    p.session = session;
-    p.channel = (uint8_t)(2 * track + (isRTCP ? 1 : 0));
-    p.t = nowMs;
-    p.off = (uint32_t)fBytes.size();
-    p.len = packetLen;
-    fBytes.insert(fBytes.end(), packet, packet + packetLen);
-    fPushed.push_back(p);
+    if (packetLen == 0 || !fCtx) return;
+    Append(session, track, packet, std::min<uint32_t>(packetLen, 65535), isRTCP, nowMs, nullptr);
 }
 
 void Reflector::ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort, const char* packet,
                                  uint32_t packetLen, uint32_t remoteAddr, uint16_t remotePort, int64_t nowMs) {
-    if (packetLen == 0 || track >= GetNumStreams(session)) return;
-    PushPacket(session, track, packet, packetLen, rtcpPort, nowMs);
+    if (packetLen == 0 || !fCtx) return;
     edgpu_udp_source u;
     memset(&u, 0, sizeof(u));
     u.session = session;
@@ -81,7 +137,7 @@ void Reflector::ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort
     u.addr = remoteAddr;
     u.len = packetLen;
     memcpy(u.head, packet, std::min<uint32_t>(packetLen, 4));
-    fSources.push_back(u);
+    Append(session, track, packet, packetLen, rtcpPort, nowMs, &u);
 }
 
 int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs) {
@@ -90,47 +146,67 @@ int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc
 }
 
 int Reflector::FlushIngest() {
-    int err;
-    if (!fPushed.empty()) {
-        // group by session (stable: arrival order within a session) into 16-B slots with the
-        // packet 4 bytes in -- the edgpu_ingest batch layout
-        std::vector<uint32_t> order(fPushed.size());
-        for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+    const auto t0 = Clock::now();
+    fTick.ingested_packets = fTick.ingested_bytes = 0;
+    // The batch to become the fill buffer was handed to edgpu_ingest two flushes ago; every call
+    // that flushed has synchronised the stream since (fan-out stats, PLAY, session removal), so its
+    // DMA is done -- this sync is the guarantee for error paths (idle stream: microseconds).
+    int err = edgpu_sync(fCtx);
+    if (err) return err;
+    Batch* bp;
+    {
+        std::lock_guard<std::mutex> g(fPushMu);
+        bp = &fBatch[fFill];
+        fFill ^= 1;
+    }
+    Batch& b = *bp;
+    if (!b.pushed.empty()) {
+        // descriptors grouped by session (stable: arrival order within a session); the slots
+        // stay where the pushers wrote them
+        const uint32_t n = (uint32_t)b.pushed.size();
+        std::vector<uint32_t> order(n);
+        for (uint32_t i = 0; i < n; i++) order[i] = i;
         std::stable_sort(order.begin(), order.end(),
-                         [&](uint32_t a, uint32_t b) { return fPushed[a].session < fPushed[b].session; });
-        std::vector<edgpu_pkt_desc> desc(order.size());
-        std::vector<uint32_t> segOff, segSess;
-        uint64_t blobBytes = 0;
-        for (uint32_t i : order) {
-            const uint32_t clamped = std::min<uint32_t>(fPushed[i].len, 2060);
-            blobBytes += (clamped + 4 + 15) & ~15u;
+                         [&](uint32_t x, uint32_t y) { return b.pushed[x].session < b.pushed[y].session; });
+        if (b.descCap < n) {
+            for (void* p : {(void*)b.desc, (void*)b.seg, (void*)b.segSess})
+                if (p) (void)edgpu_host_free(fCtx, p);
+            b.desc = nullptr; b.seg = b.segSess = nullptr; b.descCap = 0;
+            const uint64_t cap = std::max<uint64_t>(n, 4096);
+            void *d = nullptr, *sg = nullptr, *ss = nullptr;
+            if ((err = edgpu_host_alloc(fCtx, cap * sizeof(edgpu_pkt_desc), &d)) ||
+                (err = edgpu_host_alloc(fCtx, (cap + 1) * sizeof(uint32_t), &sg)) ||
+                (err = edgpu_host_alloc(fCtx, cap * sizeof(uint32_t), &ss))) {
+                for (void* p : {d, sg, ss}) if (p) (void)edgpu_host_free(fCtx, p);
+                return err;
+            }
+            b.desc = (edgpu_pkt_desc*)d; b.seg = (uint32_t*)sg; b.segSess = (uint32_t*)ss; b.descCap = cap;
         }
-        std::vector<uint8_t> blob(std::max<uint64_t>(blobBytes, 16), 0);
-        uint64_t off = 0;
-        for (uint32_t k = 0; k < order.size(); k++) {
-            const Pushed& p = fPushed[order[k]];
-            if (segSess.empty() || segSess.back() != p.session) { segOff.push_back(k); segSess.push_back(p.session); }
-            const uint32_t clamped = std::min<uint32_t>(p.len, 2060);   // bytes past 2060 are never read
-            desc[k].slot = (uint32_t)(off / 16);
-            desc[k].len = (uint16_t)p.len;
-            desc[k].channel = p.channel;
-            desc[k].flags = 0;
-            desc[k].arrival_ms = p.t;
-            memcpy(&blob[off + 4], &fBytes[p.off], clamped);
-            off += (clamped + 4 + 15) & ~15u;
+        uint32_t nseg = 0;
+        for (uint32_t k = 0; k < n; k++) {
+            const Pushed& p = b.pushed[order[k]];
+            if (nseg == 0 || b.segSess[nseg - 1] != p.session) { b.seg[nseg] = k; b.segSess[nseg] = p.session; nseg++; }
+            b.desc[k].slot = (uint32_t)(p.slot / 16);
+            b.desc[k].len = (uint16_t)p.len;
+            b.desc[k].channel = p.channel;
+            b.desc[k].flags = 0;
+            b.desc[k].arrival_ms = p.t;
+            fTick.ingested_bytes += p.len;
         }
-        segOff.push_back((uint32_t)order.size());
-        err = edgpu_ingest(fCtx, desc.data(), (uint32_t)desc.size(), segOff.data(), segSess.data(),
-                           (uint32_t)segSess.size(), blob.data(), blobBytes, EDGPU_PTR_HOST);
+        b.seg[nseg] = n;
+        fTick.ingested_packets = n;
+        err = edgpu_ingest(fCtx, b.desc, n, b.seg, b.segSess, nseg, b.blob, b.used, EDGPU_PTR_PINNED);
+        if (!err) err = edgpu_keyframe_index(fCtx);
+        b.pushed.clear();
+        b.used = 0;
+        if (err) { b.sources.clear(); return err; }
+    }
+    if (!b.sources.empty()) {
+        err = edgpu_udp_sources(fCtx, b.sources.data(), (uint32_t)b.sources.size());
+        b.sources.clear();
         if (err) return err;
-        if ((err = edgpu_keyframe_index(fCtx))) return err;
-        fPushed.clear();
-        fBytes.clear();
     }
-    if (!fSources.empty()) {
-        if ((err = edgpu_udp_sources(fCtx, fSources.data(), (uint32_t)fSources.size()))) return err;
-        fSources.clear();
-    }
+    fTick.ingest_ms = ms_since(t0);
     return kNoErr;
 }
 
@@ -138,6 +214,9 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if (!fCtx) return kRequestFailed;
     int err = FlushIngest();
     if (err) return err;
+    auto t0 = Clock::now();
+    fTick.readback_bytes = fTick.arena_bytes = fTick.writes = 0;
+    fTick.fanout_ms = fTick.readback_ms = fTick.write_ms = 0;
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
     uint32_t nrr = 0;
@@ -150,25 +229,51 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     }
     edgpu_tick_stats st;
     if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
+    fTick.fanout_ms = ms_since(t0);
     if (st.status) return st.status;
+    fTick.arena_bytes = st.arena_bytes;
     if (!sink || st.relayed_packets == 0) return kNoErr;
+    t0 = Clock::now();
     std::vector<edgpu_substream_out> subs(res.n_substreams);
     std::vector<edgpu_out_desc> d(st.relayed_packets);
-    fArena.resize(st.arena_bytes);
     if ((err = edgpu_copy_to_host(fCtx, subs.data(), res.substreams, subs.size() * sizeof(subs[0])))) return err;
     if ((err = edgpu_copy_to_host(fCtx, d.data(), res.desc, d.size() * sizeof(d[0])))) return err;
-    if ((err = edgpu_copy_to_host(fCtx, fArena.data(), res.arena, fArena.size()))) return err;
+    // the tick's distinct bytes only: one region per identity sender + the other sub-streams
+    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs.data(), (uint32_t)subs.size());
+    if (tr.bytes > fDevOutCap) {
+        if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
+        fDevOut = nullptr; fDevOutCap = 0;
+        if ((err = edgpu_device_alloc(fCtx, tr.bytes, &fDevOut))) return err;
+        fDevOutCap = tr.bytes;
+    }
+    if (tr.bytes > fHostOutCap) {
+        if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
+        fHostOut = nullptr; fHostOutCap = 0;
+        void* h = nullptr;
+        if ((err = edgpu_host_alloc(fCtx, std::max<uint64_t>(tr.bytes, 1 << 20), &h))) return err;
+        fHostOut = (uint8_t*)h;
+        fHostOutCap = std::max<uint64_t>(tr.bytes, 1 << 20);
+    }
+    if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fDevOut, fDevOutCap))) return err;
+    if ((err = edgpu_copy_to_host(fCtx, fHostOut, fDevOut, tr.bytes))) return err;
+    fTick.readback_bytes = tr.bytes + subs.size() * sizeof(subs[0]) + d.size() * sizeof(d[0]);
     std::vector<int64_t> arrival;
     if (sink->WantsArrivals()) {
         arrival.resize(d.size());
-        if ((err = edgpu_fanout_arrivals(fCtx, arrival.data(), (uint32_t)arrival.size(), EDGPU_PTR_HOST))) return err;
+        if ((err = edgpu_fanout_arrivals(fCtx, arrival.data(), (uint32_t)arrival.size(), EDGPU_PTR_HOST))) {
+            return err == EDGPU_BAD_ARGUMENT ? kBadArgument : err;   // overlap_ticks: no arrivals
+        }
     }
+    fTick.readback_ms = ms_since(t0);
+    t0 = Clock::now();
     sink->BeginTick(subs.data(), (uint32_t)subs.size());
     // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stops this
     // output's sub-stream for the tick; the engine then bookmarks the blocked packet
     std::vector<edgpu_blocked> blocked;
     for (uint32_t s = 0; s < (uint32_t)subs.size(); s++) {
         const edgpu_substream_out& q = subs[s];
+        if (!q.desc_count) continue;
+        const uint8_t* base = tr.at(fHostOut, s);
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = d[q.desc_base + i];
             PacketWrite w;
@@ -176,17 +281,19 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
             w.track = q.track;
             w.isRTCP = q.kind != 0;
             w.interleaved = q.transport == EDGPU_TRANSPORT_TCP;
-            w.wire = &fArena[o.offset];
+            w.wire = base + (o.offset - q.out_base);
             w.wireLen = o.len;
             w.packetID = o.packet_id;
             w.arrivalMs = arrival.empty() ? -1 : arrival[q.desc_base + i];
             w.sender = q.sender;
             w.newOutput = (q.flags & EDGPU_SUB_NEW) != 0;
+            fTick.writes++;
             err = sink->Write(w);
             if (err == kWouldBlock) { blocked.push_back(edgpu_blocked{s, i}); break; }
             if (err) return err;
         }
     }
+    fTick.write_ms = ms_since(t0);
     if (!blocked.empty()) return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
     return kNoErr;
 }

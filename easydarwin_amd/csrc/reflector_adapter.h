@@ -22,10 +22,22 @@
 //   CKeyFrameCache (keyframecache.h:45-72)            edgpu_reflector::CKeyFrameCache, same
 //                                                        public API + LoadGOP() from HBM
 //
-// Threading mirrors the reference: one Reflector per GPU; its calls are serialised by the
-// caller (the reference's per-stream fBucketMutex / demuxer mutex).
+// Threading: one Reflector per GPU.  PushPacket / ProcessUDPPacket -- the pushers' ingest
+// (RTSPIncomingData, the UDP socket reader) -- may be called from any thread at any time: they
+// append to a pending batch under a short lock of their own and never wait for a tick (the
+// reference takes only the demuxer / stream mutex per packet, ReflectorStream.cpp:529-576,
+// 1769-1875).  Every other call is serialised by the caller (the reference's session-map and
+// per-stream fBucketMutex), and ReflectPackets runs the tick without holding the push lock
+// except for swapping the pending batch.
+//
+// Copies: a pushed packet is copied once, into a pinned slot buffer (two, used alternately),
+// and reaches HBM by one asynchronous DMA (edgpu_ingest EDGPU_PTR_PINNED); a tick's output comes
+// back as its distinct bytes only (tick_regions.h + edgpu_arena_gather), not the write-many
+// arena (the reference copies a pushed packet once, ReflectorStream.h:104-114, and writes each
+// relayed packet from that copy).
 #pragma once
 #include <stdint.h>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -99,6 +111,9 @@ public:
     int  PlayRTPInfo(uint32_t session, bool interleaved, int64_t nowMs, uint32_t* outHandle,
                      std::vector<edgpu_rtp_info>* outInfo);
     int  RemoveOutput(uint32_t handle);
+    // the end of a push session (reference count 0, QTSSReflectorModule.cpp:2133-2196):
+    // packets still pending for it are ingested first; killOutputs tears its outputs down with it
+    int  RemoveSession(uint32_t session, bool killOutputs);
     // one pushed packet, exactly as ProcessRTPData hands it to ReflectorStream::PushPacket
     void PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
                     bool isRTCP, int64_t nowMs);
@@ -109,20 +124,45 @@ public:
     // the receiver-report SSRC / CNAME time a track's ReflectorStream would have drawn
     int  SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs);
     // ingest everything pushed since the last call, update the keyframe index, fan out at
-    // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order)
+    // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order).  A sink
+    // that WantsArrivals() needs serial ticks (no edgpu_config.overlap_ticks): kBadArgument.
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
     edgpu_ctx* Context() { return fCtx; }
 
+    // per-tick measurements of the last ReflectPackets (tools/bench_module)
+    struct TickInfo {
+        uint64_t ingested_packets = 0, ingested_bytes = 0;   // batch handed to edgpu_ingest
+        uint64_t readback_bytes = 0, arena_bytes = 0;       // PCIe bytes read back vs the arena
+        uint64_t writes = 0;                                // OutputSink::Write calls
+        double ingest_ms = 0, fanout_ms = 0, readback_ms = 0, write_ms = 0;
+    };
+    const TickInfo& LastTick() const { return fTick; }
+
 private:
     int  FlushIngest();                                     // edgpu_ingest + keyframe index
-    struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint32_t off, len; };
+    // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob
+    struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint64_t slot; uint32_t len; };
+    struct Batch {
+        uint8_t* blob = nullptr;                            // pinned (edgpu_host_alloc)
+        uint64_t cap = 0, used = 0;
+        std::vector<Pushed> pushed;                         // arrival order
+        std::vector<edgpu_udp_source> sources;              // UDP datagrams' sources, same order
+        // pinned descriptor / segment arrays, filled at the flush (grouped by session)
+        edgpu_pkt_desc* desc = nullptr; uint32_t* seg = nullptr; uint32_t* segSess = nullptr;
+        uint64_t descCap = 0;
+    };
+    void Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
+                int64_t nowMs, const edgpu_udp_source* src);
     edgpu_ctx* fCtx = nullptr;
     int fStatus = kRequestFailed;
-    std::vector<uint32_t> fTracks;                          // per session
-    std::vector<Pushed> fPushed;                            // arrival order
-    std::vector<edgpu_udp_source> fSources;                 // UDP datagrams' sources, same order
-    std::vector<uint8_t> fBytes;
-    std::vector<uint8_t> fArena;                            // host copy of one tick's output
+    std::mutex fPushMu;                                     // guards fBatch[fFill] and fTracks
+    Batch fBatch[2];
+    int fFill = 0;
+    std::vector<uint32_t> fTracks;                          // per session (0: none)
+    // readback buffers
+    uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes
+    void* fDevOut = nullptr; uint64_t fDevOutCap = 0;       // device: edgpu_arena_gather target
+    TickInfo fTick;
 };
 
 // CKeyFrameCache with the reference's public API and TLV record format

@@ -1,0 +1,64 @@
+// tick_regions.h -- the distinct bytes of a fan-out tick (host side, shared by the socket egress
+// and the module adapter).
+//
+// A tick's arena is write-many: every sub-stream has its own copy of the packets it relays.
+// Sub-streams flagged EDGPU_SUB_IDENTITY (UDP, no rewrite) of one sender carry the same bytes,
+// each a suffix of the longest (they all end at the sender's newest packet), so a host that
+// reads the tick back needs that longest region once per sender plus every other non-empty
+// sub-stream's region -- the copy edgpu_arena_gather packs on the device before one PCIe copy.
+#pragma once
+#include <stdint.h>
+
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "edgpu.h"
+
+namespace edgpu_host {
+
+struct TickRegions {
+    std::vector<edgpu_region> reg;                      // regions to gather, in order
+    std::vector<std::pair<uint32_t, uint64_t>> src;     // per sub-stream: (region, byte offset in it)
+    std::vector<uint64_t> reg_off;                      // region i starts at reg_off[i] of the gather
+    uint64_t bytes = 0;                                 // total gathered bytes
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+    // Host address of sub-stream q's first byte in the gathered copy at `base` (q non-empty).
+    const uint8_t* at(const uint8_t* base, uint32_t q) const { return base + reg_off[src[q].first] + src[q].second; }
+};
+
+inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
+    TickRegions t;
+    t.src.assign(nq, {TickRegions::kNone, 0});
+    std::map<uint32_t, uint32_t> rep;                   // sender -> its longest identity sub-stream
+    for (uint32_t q = 0; q < nq; q++) {
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
+        auto it = rep.find(s.sender);
+        if (it == rep.end() || subs[it->second].out_bytes < s.out_bytes) rep[s.sender] = q;
+    }
+    std::map<uint32_t, uint32_t> rep_reg;               // sender -> region index
+    for (uint32_t q = 0; q < nq; q++) {
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count) continue;
+        if (s.flags & EDGPU_SUB_IDENTITY) {
+            const edgpu_substream_out& R = subs[rep[s.sender]];
+            auto it = rep_reg.find(s.sender);
+            if (it == rep_reg.end()) {
+                it = rep_reg.emplace(s.sender, (uint32_t)t.reg.size()).first;
+                t.reg.push_back(edgpu_region{R.out_base, R.out_bytes});
+            }
+            t.src[q] = {it->second, R.out_bytes - s.out_bytes};   // q is a suffix of the longest
+        } else {
+            t.src[q] = {(uint32_t)t.reg.size(), 0};
+            t.reg.push_back(edgpu_region{s.out_base, s.out_bytes});
+        }
+    }
+    t.reg_off.assign(t.reg.size() + 1, 0);
+    for (size_t i = 0; i < t.reg.size(); i++) t.reg_off[i + 1] = t.reg_off[i] + t.reg[i].bytes;
+    t.bytes = t.reg_off.back();
+    return t;
+}
+
+}  // namespace edgpu_host

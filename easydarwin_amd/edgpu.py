@@ -12,13 +12,15 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libedgpu.so")
+# EDGPU_LIB: a measurement build (make -C easydarwin_amd/csrc ab) instead of the shipped library
+LIB_PATH = os.environ.get("EDGPU_LIB") or os.path.join(HERE, "libedgpu.so")
 
 OK, ERR, BAD_ARGUMENT, WOULD_BLOCK = 0, -1, -10, -14
 NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW = -101, -102, -103, -104
 TRANSPORT_UDP, TRANSPORT_TCP = 0, 1
 PTR_HOST, PTR_DEVICE, PTR_PINNED = 0, 1, 2
 PLAY_RTP_INFO = 1
+SESSION_KILL_OUTPUTS = 1          # edgpu_session_remove flags
 FALSE = 0xFFFFFFFF
 
 EXPORTED = [
@@ -34,7 +36,7 @@ EXPORTED = [
     "edgpu_egress_tcp", "edgpu_egress_send", "edgpu_egress_flush", "edgpu_egress_blocked",
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
-    "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals",
+    "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -167,6 +169,7 @@ def load(path: str = LIB_PATH):
         "edgpu_sync": (I32, [P]),
         "edgpu_session_add": (I32, [P, C.c_char_p, U32, I32, C.POINTER(U32)]),
         "edgpu_session_tracks": (I32, [P, U32, C.POINTER(U32)]),
+        "edgpu_session_remove": (I32, [P, U32, U32]),
         "edgpu_subscriber_add": (I32, [P, U32, I32, C.POINTER(U32)]),
         "edgpu_subscriber_remove": (I32, [P, U32]),
         "edgpu_ingest": (I32, [P, P, U32, P, P, U32, P, U64, I32]),
@@ -272,6 +275,11 @@ class Context:
         out = C.c_uint32()
         _check(self.lib.edgpu_session_tracks(self.h, session, C.byref(out)))
         return out.value
+
+    def session_remove(self, session: int, kill_outputs: bool = False):
+        """The end of a ReflectorSession (reference count 0); kill_outputs tears its subscribers
+        down with it (kill_clients_when_broadcast_stops)."""
+        _check(self.lib.edgpu_session_remove(self.h, session, SESSION_KILL_OUTPUTS if kill_outputs else 0))
 
     def subscriber_add(self, session: int, transport: int = TRANSPORT_UDP) -> int:
         out = C.c_uint32()

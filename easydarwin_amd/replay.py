@@ -6,6 +6,14 @@ Batch semantics: all PKT events since the previous TICK form one ``edgpu_ingest`
 (grouped by session, arrival order kept), followed by ``edgpu_keyframe_index``; JOINs since
 the previous TICK become ``edgpu_subscriber_add``; the TICK itself is ``edgpu_fanout(now)``.
 
+Session lifecycle (trace v3, PUBLISH / UNPUBLISH): the replay keeps the module's reference
+counts -- the pusher's and one per output -- and calls ``edgpu_session_remove`` when one
+reaches 0 (with EDGPU_SESSION_KILL_OUTPUTS for an UNPUBLISH with kill); a PUBLISH of a removed
+session adds a fresh engine session.  PUBLISH / UNPUBLISH end an ingest batch, and PKT / UPKT
+events of a session without a pusher are dropped, as the reference harness drops them.
+Without replicas, joins are made at their JOIN event (the engine applies them at the next
+fan-out either way), so a join that finds no session fails then, as in the reference.
+
 UPKT events (UDP pushers) are ingested like PKTs and their source addresses go to
 ``edgpu_udp_sources`` with the batch; the receiver reports each ``edgpu_fanout`` queues
 (``edgpu_source_reports``) form the capture's EDRR trailer.  Each track's report identity is
@@ -27,7 +35,8 @@ import struct
 import numpy as np
 
 from . import edgpu
-from .trace import BLOCK, JOIN, LEAVE, PKT, TICK, UPKT, Trace, pack_source_reports, rr_ssrc
+from .trace import (BLOCK, JOIN, LEAVE, PKT, PUBLISH, TICK, UNPUBLISH, UPKT, Trace, pack_source_reports,
+                    rr_ssrc)
 
 
 def _wire_images(subs, desc, arena, images, budgets=None):
@@ -60,8 +69,10 @@ RTSP_KEEPALIVE = (b"SET_PARAMETER rtsp://127.0.0.1/live/replay RTSP/1.0\r\nCSeq:
                   b"Session: 51234\r\nContent-Length: 0\r\n\r\n")
 
 
-def tcp_plan(batches, seed: int, messages: float = 0.1, carry: float = 0.5):
-    """Per ingest batch (list of (session, channel, t, packet)): {session: [(read bytes, arrival)]}."""
+def tcp_plan(batches, seed: int, messages: float = 0.1, carry: float = 0.5, barriers=()):
+    """Per ingest batch (list of (session, channel, t, packet)): {session: [(read bytes, arrival)]}.
+    No frame is carried from batch k into batch k + 1 for k in `barriers` (a pusher connection
+    ends there)."""
     rng = random.Random(seed)
     per = []
     for b in batches:
@@ -90,7 +101,7 @@ def tcp_plan(batches, seed: int, messages: float = 0.1, carry: float = 0.5):
                     n = rng.choice([1, 3, rng.randint(1, 200), rng.randint(1, 4000), len(data)])
                     reads.append((data[p:p + n], t))
                     p += n
-            if k + 1 < len(per) and s in per[k + 1] and rng.random() < carry:
+            if k + 1 < len(per) and s in per[k + 1] and k not in barriers and rng.random() < carry:
                 first = per[k + 1][s][0][1]
                 m = rng.randint(1, len(first) - 1)
                 reads.append((first[:m], reads[-1][1] if reads else 0))
@@ -140,20 +151,29 @@ def ingest_tcp(ctx: edgpu.Context, reads_by_session: dict):
 
 def _batches(trace: Trace, flush_on_rtpinfo: bool):
     """The pushers' interleaved packets of every ingest batch (a batch holding only UDP
-    pushers' datagrams is an empty entry, so the list stays aligned with the flushes)."""
-    out, cur, any_pkt = [], [], False
+    pushers' datagrams is an empty entry, so the list stays aligned with the flushes), and
+    the indices of the batches a PUBLISH / UNPUBLISH ends (no frame is carried past them)."""
+    out, cur, any_pkt, barriers = [], [], False, set()
+    published = [True] * len(trace.sdps)
     for ev in trace.events:
         if ev[0] == PKT:
             _, t, s, ch, data = ev
+            if not published[s]:
+                continue
             cur.append((s, ch, t, data))
             any_pkt = True
         elif ev[0] == UPKT:
-            any_pkt = True
-        elif (ev[0] == JOIN and ev[5] & 1 and flush_on_rtpinfo) or ev[0] == TICK:
+            if published[ev[2]]:
+                any_pkt = True
+        elif (ev[0] == JOIN and ev[5] & 1 and flush_on_rtpinfo) or ev[0] in (TICK, PUBLISH, UNPUBLISH):
             if any_pkt:
                 out.append(cur)
                 cur, any_pkt = [], False
-    return out
+            if ev[0] in (PUBLISH, UNPUBLISH):
+                if out:
+                    barriers.add(len(out) - 1)
+                published[ev[2]] = ev[0] == PUBLISH
+    return out, barriers
 
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
@@ -181,6 +201,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
 
     pinned=True: every ingest batch is written into pinned host buffers (edgpu_host_alloc,
     two sets used alternately) and handed over as EDGPU_PTR_PINNED (asynchronous copy)."""
+    if replica is not None and trace.has_lifecycle:
+        raise ValueError("replica replays take no PUBLISH / UNPUBLISH events")
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
@@ -195,13 +217,26 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         sess_tracks = []
         rsess = {}
         rand_calls = 0
+        # lifecycle: engine session of each trace session (None once removed), its pusher, and
+        # the trace session of each engine session (receiver reports name the trace's)
+        gen = [None] * len(trace.sdps)
+        published = [True] * len(trace.sdps)
+        trace_of = {}
+
+        def publish_fresh(i, now_s):
+            nonlocal rand_calls
+            sid = ctx.session_add(trace.sdps[i], udp_push=trace.udp_push(i))
+            gen[i] = sid
+            trace_of[sid] = i
+            for tr in range(ctx.session_tracks(sid)):
+                ctx.source_identity(sid, tr, rr_ssrc(rand_calls), now_s)
+                rand_calls += 1
+            return sid
+
         for i, sdp in enumerate(trace.sdps):
-            sid = ctx.session_add(sdp, udp_push=trace.udp_push(i))
+            sid = publish_fresh(i, 0)
             assert sid == len(sess_tracks)
             sess_tracks.append(ctx.session_tracks(sid))
-            for tr in range(sess_tracks[-1]):
-                ctx.source_identity(sid, tr, rr_ssrc(rand_calls), 0)
-                rand_calls += 1
             if replica == "all":
                 rsess[sid] = link.add(sid, sdp)
         reports = []                        # (t, session, track, addr, port, bytes)
@@ -248,7 +283,10 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             ctx.ingest_pinned(ptrs[0], len(desc), ptrs[1], ptrs[2], len(seg_sess), ptrs[3], blob.nbytes)
 
         clock = 0                           # the harness's virtual clock: max event time so far
-        plan = tcp_plan(_batches(trace, rep is None), interleaved) if interleaved is not None else None
+        plan = None
+        if interleaved is not None:
+            bl, barriers = _batches(trace, rep is None)
+            plan = tcp_plan(bl, interleaved, barriers=barriers)
         nflush = 0
 
         def flush():
@@ -257,12 +295,12 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 udp = [p for p in pending if p[4]]
                 if plan is not None:
                     if len(udp) < len(pending):
-                        ingest_tcp(ctx, plan[nflush])
+                        ingest_tcp(ctx, {gen[s]: rd for s, rd in plan[nflush].items()})
                     batch = udp                  # UDP pushers' datagrams: a plain batch
                 else:
                     batch = pending
                 if batch:
-                    desc, seg_off, seg_sess, blob = edgpu.build_batch([p[:4] for p in batch])
+                    desc, seg_off, seg_sess, blob = edgpu.build_batch([(gen[p[0]],) + p[1:4] for p in batch])
                     if pinned:
                         pin_ingest(desc, seg_off, seg_sess, blob)
                     else:
@@ -287,7 +325,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             (_, jt, s, sub_id, transport, ua, now_j) = j
             out = ctx if rep is None else rep
             try:
-                h, _info = out.subscriber_play(s if rep is None else rsess[s],
+                h, _info = out.subscriber_play(gen[s] if rep is None else rsess[s],
                                                edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
                                                rtp_info=bool(ua & 1), now_ms=now_j)
             except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
@@ -307,6 +345,16 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     images[(h, tr, k)] = []
         if lag and any(ev[0] == BLOCK for ev in trace.events):
             raise ValueError("backpressure reports need each tick read before the next ingest")
+
+        def outputs_of(s):
+            return [h for h, meta in subs_meta.items() if meta[1] == s and h not in gone]
+
+        def release_check(s):
+            """A session without pusher or outputs dies (RemoveOutput's refcount-0 branch)."""
+            if gen[s] is not None and not published[s] and not outputs_of(s):
+                ctx.session_remove(gen[s])
+                gen[s] = None
+
         for ev in trace.events:
             if ev[0] == BLOCK:
                 blocks[(ev[2], ev[3], ev[4])] = ev[5]
@@ -314,17 +362,42 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             clock = max(clock, ev[1])
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
-                pending.append((s, ch, t, data, False))
+                if published[s]:
+                    pending.append((s, ch, t, data, False))
             elif ev[0] == UPKT:
                 _, t, s, ch, addr, port, data = ev
-                pending.append((s, ch, t, data, True))
-                sources.append((s, ch, addr, port, data))
+                if published[s]:
+                    pending.append((s, ch, t, data, True))
+                    sources.append((gen[s], ch, addr, port, data))
             elif ev[0] == JOIN:
                 # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):
-                # ingest what precedes it first; other joins wait for the tick
+                # ingest what precedes it first
                 if ev[5] & 1 and rep is None:
                     flush()
-                joins.append(ev + (clock,))
+                if rep is None:
+                    if gen[ev[2]] is not None:          # else no session: the SETUP fails
+                        do_join(ev + (clock,))
+                else:
+                    joins.append(ev + (clock,))     # replicas: made at the tick
+            elif ev[0] == UNPUBLISH:
+                _, t, s, kill = ev
+                flush()
+                if published[s]:
+                    published[s] = False
+                    if kill:                            # TearDownAllOutputs
+                        for h in outputs_of(s):
+                            gone.add(h)
+                        if gen[s] is not None:
+                            ctx.session_remove(gen[s], kill_outputs=True)
+                            gen[s] = None
+                    release_check(s)
+            elif ev[0] == PUBLISH:
+                _, t, s = ev
+                flush()
+                if not published[s]:
+                    published[s] = True
+                    if gen[s] is None:
+                        publish_fresh(s, clock // 1000)
             elif ev[0] == LEAVE:
                 # RemoveOutput applies at once: a join still waiting for its tick is made now
                 # (the output existed, with nothing sent yet), and the output stops at the next
@@ -341,6 +414,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                         gone.add(h)
                         if rep is not None:
                             ctx.session_eyes_add(meta[1], -1)
+                        else:
+                            release_check(meta[1])
                         break
             elif ev[0] == TICK:
                 t = ev[1]
@@ -356,7 +431,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 joins = []
                 if rep is not None:
                     ctx.fanout(t)                      # the owner ticks too (no subscribers here)
-                    reports.extend((t,) + r for r in ctx.source_reports())
+                    reports.extend((t, trace_of[r[0]]) + tuple(r[1:]) for r in ctx.source_reports())
                 drain()                              # the previous tick, after this batch's ingest
                 by_handle = {}
                 for (sub_id, trk, kind), b in blocks.items():
@@ -366,7 +441,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 blocks = {}
                 unread = (out, out.fanout(t), t, by_handle)
                 if rep is None:
-                    reports.extend((t,) + r for r in ctx.source_reports())
+                    reports.extend((t, trace_of[r[0]]) + tuple(r[1:]) for r in ctx.source_reports())
                 if not lag:
                     drain()
         drain()

@@ -34,7 +34,8 @@ Binary layout (little endian)::
 
     trace   := "EDTR" u32 version u32 n_sessions { u32 sdp_len sdp_bytes [u8 flags] }*
                event* u8 0
-               (version 1: no flags byte; version 2: flags bit 0 = UDP push)
+               (version 1: no flags byte; version 2: flags bit 0 = UDP push;
+                version 3: as 2, with PUBLISH / UNPUBLISH events)
     event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
              | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
              | u8 3 i64 t                                                    (TICK)
@@ -42,6 +43,8 @@ Binary layout (little endian)::
              | u8 5 i64 t u32 session u8 channel u32 addr u16 port u32 len bytes[len]
                                                                              (UPKT, v2)
              | u8 6 i64 t u32 sub_id                                         (LEAVE)
+             | u8 7 i64 t u32 session u8 kill                                (UNPUBLISH, v3)
+             | u8 8 i64 t u32 session                                        (PUBLISH, v3)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
                [ "EDRR" u32 m { i64 t u32 session u16 track u32 addr u16 port u32 len
@@ -66,7 +69,7 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK, BLOCK, UPKT, LEAVE = 1, 2, 3, 4, 5, 6
+PKT, JOIN, TICK, BLOCK, UPKT, LEAVE, UNPUBLISH, PUBLISH = 1, 2, 3, 4, 5, 6, 7, 8
 UDP, TCP = 0, 1
 
 
@@ -86,7 +89,13 @@ class Trace:
 
     @property
     def version(self) -> int:
+        if any(ev[0] in (PUBLISH, UNPUBLISH) for ev in self.events):
+            return 3
         return 2 if any(self.flags) or any(ev[0] == UPKT for ev in self.events) else 1
+
+    @property
+    def has_lifecycle(self) -> bool:
+        return any(ev[0] in (PUBLISH, UNPUBLISH) for ev in self.events)
 
     def pkt(self, t: int, session: int, channel: int, data: bytes):
         self.events.append((PKT, int(t), session, channel, bytes(data)))
@@ -105,6 +114,12 @@ class Trace:
 
     def upkt(self, t: int, session: int, channel: int, addr: int, port: int, data: bytes):
         self.events.append((UPKT, int(t), session, channel, int(addr), int(port), bytes(data)))
+
+    def unpublish(self, t: int, session: int, kill: bool = False):
+        self.events.append((UNPUBLISH, int(t), session, 1 if kill else 0))
+
+    def publish(self, t: int, session: int):
+        self.events.append((PUBLISH, int(t), session))
 
     # -- serialisation ------------------------------------------------------------------
     def to_bytes(self) -> bytes:
@@ -138,6 +153,10 @@ class Trace:
                 out.append(data)
             elif ev[0] == LEAVE:
                 out.append(struct.pack("<BqI", LEAVE, ev[1], ev[2]))
+            elif ev[0] == UNPUBLISH:
+                out.append(struct.pack("<BqIB", UNPUBLISH, ev[1], ev[2], ev[3]))
+            elif ev[0] == PUBLISH:
+                out.append(struct.pack("<BqI", PUBLISH, ev[1], ev[2]))
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -151,7 +170,7 @@ class Trace:
     def from_bytes(buf: bytes) -> "Trace":
         assert buf[:4] == b"EDTR"
         ver, n = struct.unpack_from("<II", buf, 4)
-        assert ver in (1, 2)
+        assert ver in (1, 2, 3)
         p = 12
         tr = Trace()
         for _ in range(n):
@@ -189,6 +208,14 @@ class Trace:
                 _, t, sub = struct.unpack_from("<BqI", buf, p)
                 p += 13
                 tr.events.append((LEAVE, t, sub))
+            elif typ == UNPUBLISH:
+                _, t, s, kill = struct.unpack_from("<BqIB", buf, p)
+                p += 14
+                tr.events.append((UNPUBLISH, t, s, kill))
+            elif typ == PUBLISH:
+                _, t, s = struct.unpack_from("<BqI", buf, p)
+                p += 13
+                tr.events.append((PUBLISH, t, s))
             elif typ == UPKT:
                 _, t, s, ch, addr, port, ln = struct.unpack_from("<BqIBIHI", buf, p)
                 p += 24

@@ -8,6 +8,10 @@
  *   edgpu_session_add      ReflectorSession::SetupReflectorSession
  *                          (APIModules/QTSSReflectorModule/ReflectorSession.cpp:140-188) with the
  *                          SDP parse of SDPSourceInfo (APICommonCode/SDPSourceInfo.cpp:259-353)
+ *   edgpu_session_remove   the end of a ReflectorSession: RemoveOutput's refcount-0 branch
+ *                          (QTSSReflectorModule.cpp:2162-2192) with TearDownAllOutputs when a
+ *                          broadcast stops with kill_clients (:2156-2159, ReflectorSession.cpp:
+ *                          281-285)
  *   edgpu_subscriber_add   RTPSessionOutput ctor + ReflectorSession::AddOutput
  *                          (RTPSessionOutput.cpp:73-88, ReflectorSession.cpp:209-253),
  *                          i.e. QTSSReflectorModule DoSetup/DoPlay for a player
@@ -133,8 +137,11 @@ typedef struct edgpu_out_desc {
     uint32_t packet_id;     /* low 32 bits of fStreamCountID */
 } edgpu_out_desc;
 
-/* One sub-stream (subscriber x track x RTP|RTCP) of a fan-out tick, in subscriber-handle,
- * track, kind order.  Its packets are desc[desc_base .. desc_base + desc_count). */
+/* One sub-stream (subscriber x track x RTP|RTCP) of a fan-out tick.  The table is in the
+ * engine's sub-stream row order: a subscriber's rows are consecutive, in track, kind order, and
+ * subscribers follow their join order, except that a subscriber may take the rows a removed
+ * one left (edgpu_session_remove).  Rows of removed subscribers have desc_count 0.  Its
+ * packets are desc[desc_base .. desc_base + desc_count). */
 typedef struct edgpu_substream_out {
     uint32_t subscriber;    /* handle from edgpu_subscriber_add */
     uint16_t track;
@@ -191,6 +198,24 @@ int  edgpu_sync(edgpu_ctx* ctx);
 int  edgpu_session_add(edgpu_ctx* ctx, const char* sdp, uint32_t sdp_len, int udp_push,
                        uint32_t* out_session);
 int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks);
+
+/* Destroys a push session -- what the reference does when a ReflectorSession's reference
+ * count reaches 0 (its pusher gone, every output removed: RemoveOutput, QTSSReflectorModule.cpp:
+ * 2133-2196).  The reference counting itself is the host's (the module's session map): the
+ * engine keeps a session, its queues, packet ids, key pointers and SSRC latch, for as long as
+ * the host does -- a pusher that reconnects to a session its players kept alive continues it
+ * (FindOrCreateSession, :1479-1536), a pusher after edgpu_session_remove gets a fresh one from
+ * edgpu_session_add (ids from 1, unlatched SSRC filter, empty queues).
+ * flags: EDGPU_SESSION_KILL_OUTPUTS removes the session's subscribers with it
+ * (kill_clients_when_broadcast_stops: TearDownAllOutputs, :2156-2159; their handles become
+ * invalid); without it the call fails with EDGPU_ERR while a subscriber is attached.
+ * Frees the session's HBM rings.  The session id, and its sender / stream table rows, are
+ * reused by a later edgpu_session_add of a session with as many tracks; a removed subscriber's
+ * sub-stream rows are reused by a later subscriber of a session with as many tracks
+ * (subscriber handles are never reused).  Fails while an ingest is pending a keyframe index.
+ * Syncs (a fan-out copy in flight may still read the rings). */
+#define EDGPU_SESSION_KILL_OUTPUTS 1u
+int  edgpu_session_remove(edgpu_ctx* ctx, uint32_t session, uint32_t flags);
 
 /* The SDP parse edgpu_session_add applies (host only, no context, no GPU): the restatement of
  * SDPSourceInfo::Parse (APICommonCode/SDPSourceInfo.cpp:172-420) -- one track per line

@@ -80,6 +80,7 @@ enum : uint32_t {
     qtssRTPTransportModePlay = 0, qtssRTPTransportModeRecord = 1,
     qtssUnknownPayloadType = 0, qtssVideoPayloadType = 1, qtssAudioPayloadType = 2,
     qtssCliSesCloseClientTeardown = 0,
+    qtssCliSesTearDownBroadcastEnded = 4,            // QTSS_CliSesTeardownReason (QTSS.h:174-180)
 };
 
 // RTSP methods (QTSSRTSPProtocol.h:43-63)
@@ -90,8 +91,8 @@ enum : uint32_t {
 
 // attribute data types (QTSS.h:358-378)
 enum : uint32_t {
-    qtssAttrDataTypeCharArray = 1, qtssAttrDataTypeSInt32 = 5, qtssAttrDataTypeUInt32 = 6,
-    qtssAttrDataTypeVoidPointer = 13,
+    qtssAttrDataTypeCharArray = 1, qtssAttrDataTypeBool16 = 2, qtssAttrDataTypeSInt32 = 5,
+    qtssAttrDataTypeUInt32 = 6, qtssAttrDataTypeVoidPointer = 13,
 };
 
 // object types (QTSS.h:266-282)
@@ -112,6 +113,7 @@ enum : uint32_t {
     qtssRTPStrTransportType = 31,
     // client session object (QTSS.h:473-512)
     qtssCliSesStreamObjects = 0, qtssCliSesState = 7, qtssCliSesFirstUserAgent = 9,
+    qtssCliTeardownReason = 23,
     // RTSP request object (QTSS.h:588-623)
     qtssRTSPReqFilePath = 2, qtssRTSPReqFileName = 5, qtssRTSPReqFileDigit = 6,
     qtssRTSPReqMethod = 9, qtssRTSPReqRespKeepAlive = 13, qtssRTSPReqQueryString = 23,

@@ -38,7 +38,18 @@
 //     of every track's bucket, DecEyeCount -- then delete the RTPSessionOutput; its capture so
 //     far is kept;
 //   * rand() is link-wrapped to a deterministic sequence (trace.py rr_ssrc): its only caller
-//     on this path is the ReflectorStream constructor's receiver-report SSRC (:167).
+//     on this path is the ReflectorStream constructor's receiver-report SSRC (:167);
+//   * session lifecycle (trace v3): sessions live in a real OSRefTable, registered and resolved
+//     as FindOrCreateSession does (QTSSReflectorModule.cpp:1388, 1469-1477) -- the pusher holds
+//     one reference, every output one.  UNPUBLISH runs DestroySession's broadcaster branch
+//     (:2082-2109: fSetupToReceive cleared, RemoveSessionFromOutput) and RemoveOutput(NULL,
+//     session, kill) (:2133-2196): TearDownAllOutputs reaches every output's
+//     RTPSessionOutput::TearDown -> QTSS_Teardown (callback 22), after which the fake server
+//     closes those client sessions (DestroySession's player branch -> RemoveOutput(output)); at
+//     reference count 0 the session is UnRegistered and killed.  PUBLISH reuses a session that
+//     still exists (Resolve, not set up again, :1479-1536) or builds a fresh one (:1391-1478).
+//     PKT / UPKT of a session without a pusher are dropped; a JOIN of a session that no longer
+//     exists fails (FindOrCreateSession returns NULL for a player, :1391-1396).
 //
 // Usage: ref_harness <trace.edtr> <capture.edcp>
 //        ref_harness --bench <trace.edtr>    (memcpy sinks, no capture; prints the replay's
@@ -76,6 +87,7 @@
 #include "ReflectorStream.h"
 #include "RTPSessionOutput.h"
 #include "QTSServerInterface.h"
+#include "OSRef.h"
 
 // ---------------------------------------------------------------------------------------
 // The two server-side module tables ReflectorSession::SetSessionName reads
@@ -153,6 +165,9 @@ static UInt32 g_cookie_attr = 0;
 static QTSS_Error cb_fail(...) { return QTSS_RequestFailed; }
 static QTSS_Error cb_ok(...) { return QTSS_NoErr; }
 static QTSS_Error cb_milliseconds(SInt64* out, ...) { *out = g_now; return QTSS_NoErr; }
+// QTSS_Teardown(client session): the server closes it later (ClientSessionClosing); recorded here
+static std::vector<void*> g_torn_down;
+static QTSS_Error cb_teardown(void* client, ...) { g_torn_down.push_back(client); return QTSS_NoErr; }
 static QTSS_Error cb_id_for_tag(UInt32 type, const char* tag, QTSS_AttributeID* out, ...) {
     std::string key = std::to_string(type) + ":" + tag;
     auto it = g_attr_ids.find(key);
@@ -250,6 +265,15 @@ struct Sub {
     FakeObj* client;
     std::vector<FakeObj*> streams;
     RTPSessionOutput* output;
+    ReflectorSession* rsess;        // the ReflectorSession it is an output of
+};
+
+// One trace session (one stream name): the ReflectorSession registered under it, if any, and
+// whether a pusher is attached.
+struct Live {
+    ReflectorSession* sess = nullptr;
+    FakeObj* bcast = nullptr;       // the pusher's client session
+    bool published = false;
 };
 
 int main(int argc, char** argv) {
@@ -287,7 +311,7 @@ int main(int argc, char** argv) {
     if (memcmp(&r.d[0], "EDTR", 4) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
     r.p = 4;
     UInt32 version = r.get<UInt32>();
-    if (version != 1 && version != 2) { fprintf(stderr, "bad version\n"); return 2; }
+    if (version < 1 || version > 3) { fprintf(stderr, "bad version\n"); return 2; }
 
     static NoopAssert logger;
     SetAssertLogger(&logger);
@@ -304,6 +328,7 @@ int main(int argc, char** argv) {
     cbs.addr[kRefreshTimeOutCallback]      = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kLockObjectCallback]          = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kUnlockObjectCallback]        = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kTeardownCallback]            = (QTSS_CallbackProcPtr)cb_teardown;
     QTSS_PrivateArgs args;
     memset(&args, 0, sizeof(args));
     args.inServerAPIVersion = QTSS_API_VERSION;
@@ -333,17 +358,26 @@ int main(int argc, char** argv) {
     g_reports.clear();
     g_rtcp_sockets.clear();
     subs.clear();
-    // Sessions.
+    // Sessions: every one is set up and has its pusher at time 0.
     UInt32 nsess = r.get<UInt32>();
-    std::vector<ReflectorSession*> sessions(nsess, nullptr);
+    std::vector<std::string> sdps(nsess);
+    std::vector<UInt8> sflags(nsess, 0);
     for (UInt32 s = 0; s < nsess; s++) {
         UInt32 sdplen = r.get<UInt32>();
-        std::string sdp((const char*)&r.d[r.p], sdplen);
+        sdps[s].assign((const char*)&r.d[r.p], sdplen);
         r.p += sdplen;
-        const UInt8 sflags = version >= 2 ? r.get<UInt8>() : 0;
-        char* sdpbuf = new char[sdplen + 1];
-        memcpy(sdpbuf, sdp.data(), sdplen); sdpbuf[sdplen] = 0;
-        SDPSourceInfo* info = new SDPSourceInfo(sdpbuf, sdplen);
+        sflags[s] = version >= 2 ? r.get<UInt8>() : 0;
+    }
+    OSRefTable sessionMap;                         // sSessionMap (QTSSReflectorModule.cpp:89)
+    std::vector<Live> live(nsess);
+    // FindOrCreateSession's create branch for a push (QTSSReflectorModule.cpp:1391-1478):
+    // SDPSourceInfo -> ReflectorSession -> SetupReflectorSession(kMarkSetup|kIsPushSession),
+    // Register + Resolve (the pusher's reference)
+    auto create = [&](UInt32 s) -> bool {
+        const std::string& sdp = sdps[s];
+        char* sdpbuf = new char[sdp.size() + 1];
+        memcpy(sdpbuf, sdp.data(), sdp.size()); sdpbuf[sdp.size()] = 0;
+        SDPSourceInfo* info = new SDPSourceInfo(sdpbuf, (UInt32)sdp.size());
         char name[64];
         snprintf(name, sizeof(name), "live/stream%u.sdp", s);
         StrPtrLen nm(name);
@@ -359,24 +393,53 @@ int main(int argc, char** argv) {
         params.inClientSession = (QTSS_ClientSessionObject)bcast;
         QTSS_Error err = sess->SetupReflectorSession(info, &params,
             ReflectorSession::kMarkSetup | ReflectorSession::kIsPushSession, true, 30);
-        if (err != QTSS_NoErr) { fprintf(stderr, "setup failed %d\n", (int)err); return 3; }
-        sessions[s] = sess;
+        if (err != QTSS_NoErr) { fprintf(stderr, "setup failed %d\n", (int)err); return false; }
+        if (sessionMap.Register(sess->GetRef()) != OS_NoErr) { fprintf(stderr, "register failed\n"); return false; }
+        if (sessionMap.Resolve(sess->GetRef()->GetString()) != sess->GetRef()) { fprintf(stderr, "resolve failed\n"); return false; }
         for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
             UDPSocketPair* pr = sess->GetStreamByIndex(x)->GetSocketPair();
             g_rtcp_sockets[pr->GetSocketB()] = std::make_pair(s, (UInt16)x);
-            if (!(sflags & 1)) continue;
+            if (!(sflags[s] & 1)) continue;
             // UDP push: bind the pair to an even/odd loopback port pair
             if (pr->GetSocketA()->Open() != OS_NoErr || pr->GetSocketB()->Open() != OS_NoErr) {
-                fprintf(stderr, "socket open failed\n"); return 3;
+                fprintf(stderr, "socket open failed\n"); return false;
             }
             static UInt16 port = 41000;
             bool bound = false;
             for (int tries = 0; tries < 2000 && !bound; tries++, port += 2)
                 bound = pr->GetSocketA()->Bind(INADDR_LOOPBACK, port) == OS_NoErr &&
                         pr->GetSocketB()->Bind(INADDR_LOOPBACK, port + 1) == OS_NoErr;
-            if (!bound) { fprintf(stderr, "no loopback port pair\n"); return 3; }
+            if (!bound) { fprintf(stderr, "no loopback port pair\n"); return false; }
         }
-    }
+        live[s].sess = sess;
+        live[s].bcast = bcast;
+        live[s].published = true;
+        return true;
+    };
+    for (UInt32 s = 0; s < nsess; s++)
+        if (!create(s)) return 3;
+    // Releases one reference of live[s]'s session; at 0 it is UnRegistered and killed
+    // (RemoveOutput, QTSSReflectorModule.cpp:2162-2192; the kill event is a no-op without task
+    // threads, the object is simply dropped here)
+    auto release = [&](ReflectorSession* sess) {
+        OSRef* ref = sess->GetRef();
+        if (ref->GetRefCount() > 0) sessionMap.Release(ref);
+        if (ref->GetRefCount() == 0) {
+            sessionMap.UnRegister(ref);
+            sess->Signal(Task::kKillEvent);
+            for (Live& l : live)
+                if (l.sess == sess) { l.sess = nullptr; l.published = false; }
+        }
+    };
+    // DestroySession's player branch -> RemoveOutput(output, session, false): out of every
+    // track's bucket (ReflectorSession::RemoveOutput(output, true)), delete, release
+    auto remove_output = [&](Sub& sb) {
+        if (sb.output == NULL) return;
+        sb.rsess->RemoveOutput(sb.output, true);
+        delete sb.output;
+        sb.output = NULL;
+        release(sb.rsess);
+    };
 
     std::vector<char> pktbuf(70000);
     const auto t_start = std::chrono::steady_clock::now();
@@ -391,7 +454,8 @@ int main(int argc, char** argv) {
             UInt32 len = r.get<UInt32>();
             memcpy(pktbuf.data(), &r.d[r.p], len);
             r.p += len;
-            ReflectorSession* sess = sessions[s];
+            if (!live[s].published) continue;             // no pusher connection carries it
+            ReflectorSession* sess = live[s].sess;
             UInt32 idx = ch / 2;
             if (idx < sess->GetNumStreams())
                 sess->GetStreamByIndex(idx)->PushPacket(pktbuf.data(), len, (ch & 1) != 0);
@@ -400,7 +464,8 @@ int main(int argc, char** argv) {
             UInt32 sub_id = r.get<UInt32>();
             UInt8 transport = r.get<UInt8>();
             UInt8 uaflags = r.get<UInt8>();
-            ReflectorSession* sess = sessions[s];
+            ReflectorSession* sess = live[s].sess;
+            if (sess == nullptr) continue;                // no such session: the player's SETUP fails
             // RTP-Info player (ua_flags bit 0: the kRequiresRTPInfoSeqAndTime profile, UA
             // "Android"/"vlc"): DoPlay's rtpInfoEnabled branch (QTSSReflectorModule.cpp:
             // 1971-2004) runs HaveStreamBuffers (:1804-1865) with the reference's own
@@ -417,8 +482,12 @@ int main(int argc, char** argv) {
                 }
                 if (!have) continue;
             }
+            // the player's reference (FindOrCreateSession's Resolve, :1388)
+            if (sessionMap.Resolve(sess->GetRef()->GetString()) != sess->GetRef()) {
+                fprintf(stderr, "resolve failed\n"); return 3;
+            }
             Sub sb;
-            sb.id = sub_id; sb.session = s;
+            sb.id = sub_id; sb.session = s; sb.rsess = sess;
             sb.client = new_obj();
             UInt32 nstreams = sess->GetNumStreams();
             for (UInt32 x = 0; x < nstreams; x++) {
@@ -443,7 +512,8 @@ int main(int argc, char** argv) {
             subs.push_back(sb);
         } else if (type == 3) {     // TICK
             for (UInt32 s = 0; s < nsess; s++) {
-                ReflectorSession* sess = sessions[s];
+                ReflectorSession* sess = live[s].sess;
+                if (sess == nullptr) continue;
                 for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
                     ReflectorStream* st = sess->GetStreamByIndex(x);
                     OSQueue* freeA = NULL;
@@ -466,7 +536,8 @@ int main(int argc, char** argv) {
             UInt32 len = r.get<UInt32>();
             memcpy(pktbuf.data(), &r.d[r.p], len);
             r.p += len;
-            ReflectorSession* sess = sessions[s];
+            if (!live[s].published) continue;             // the pusher is gone
+            ReflectorSession* sess = live[s].sess;
             UInt32 idx = ch / 2;
             // an empty read is GetIncomingData's "no more data" (ProcessPacket then re-arms the
             // socket's event), not a datagram: traces carry none
@@ -485,11 +556,41 @@ int main(int argc, char** argv) {
         } else if (type == 6) {     // LEAVE
             UInt32 sub_id = r.get<UInt32>();
             for (auto& sb : subs)
-                if (sb.id == sub_id && sb.output != NULL) {
-                    sessions[sb.session]->RemoveOutput(sb.output, true);
-                    delete sb.output;
-                    sb.output = NULL;
+                if (sb.id == sub_id && sb.output != NULL) remove_output(sb);
+        } else if (type == 7) {     // UNPUBLISH: the pusher's client session closes
+            UInt32 s = r.get<UInt32>();
+            UInt8 kill = r.get<UInt8>();
+            if (!live[s].published) continue;
+            ReflectorSession* sess = live[s].sess;
+            live[s].published = false;
+            // DestroySession, broadcaster branch (QTSSReflectorModule.cpp:2082-2109)
+            SourceInfo* info = sess->GetSourceInfo();
+            for (UInt32 x = 0; info != NULL && x < info->GetNumStreams(); x++)
+                if (info->GetStreamInfo(x) != NULL) info->GetStreamInfo(x)->fSetupToReceive = false;
+            sess->RemoveSessionFromOutput((QTSS_ClientSessionObject)live[s].bcast);
+            // RemoveOutput(NULL, session, kill) (:2133-2196)
+            g_torn_down.clear();
+            if (kill) sess->TearDownAllOutputs();
+            std::vector<void*> closing = g_torn_down;
+            release(sess);
+            // the server closes every torn-down client session: ClientSessionClosing
+            for (auto& sb : subs)
+                if (sb.output != NULL && sb.rsess == sess &&
+                    std::find(closing.begin(), closing.end(), (void*)sb.client) != closing.end())
+                    remove_output(sb);
+        } else if (type == 8) {     // PUBLISH: a pusher's ANNOUNCE + SETUPs + RECORD
+            UInt32 s = r.get<UInt32>();
+            if (live[s].published) continue;              // duplicate broadcast: refused
+            if (live[s].sess != nullptr) {
+                // FindOrCreateSession's Resolve branch: the session is set up already
+                ReflectorSession* sess = live[s].sess;
+                if (sessionMap.Resolve(sess->GetRef()->GetString()) != sess->GetRef()) {
+                    fprintf(stderr, "resolve failed\n"); return 3;
                 }
+                live[s].published = true;
+            } else if (!create(s)) {
+                return 3;
+            }
         } else if (type == 4) {     // BLOCK
             UInt32 sub_id = r.get<UInt32>();
             UInt16 track = r.get<UInt16>();

@@ -34,6 +34,11 @@
 //             kRRInterval timer (RTCP sender)       ReflectorStream.cpp:1039-1047, h:343
 //             GetACName                             RTCPUtilitiesLib/RTCPSRPacket.cpp:87-117
 //             eye count (AddOutput isClient)        ReflectorSession.cpp:215-268
+//   lifecycle pusher leave: DestroySession           QTSSReflectorModule.cpp:2082-2109
+//             RemoveOutput / refcount / kill         QTSSReflectorModule.cpp:2133-2196
+//             re-push: FindOrCreateSession           QTSSReflectorModule.cpp:1379-1545
+//             (the pusher holds one reference, every output one; at 0 the session dies and a
+//             later PUBLISH builds a fresh one; a surviving session is reused as it is)
 //
 // Out of parity scope (documented in DESIGN.md): bytes read past the packet length by the
 // key detector when 12+4*CC >= len (the reference reads stale buffer memory there; this model
@@ -199,6 +204,8 @@ struct Output {
 };
 
 struct Session {
+    uint32_t idx = 0;                 // trace session (stream name)
+    bool published = true;            // a pusher is attached (holds a reference)
     std::vector<Stream> streams;
     bool video_key_flag = false;      // ReflectorSession::fHasVideoKeyFrameUpdate
     std::vector<std::unique_ptr<Output>> outputs;   // bucket order == join order here
@@ -208,13 +215,23 @@ struct Session {
 
 struct Model {
     Prefs prefs;
-    std::vector<std::unique_ptr<Session>> sessions;
+    std::vector<std::unique_ptr<Session>> sessions;   // by trace session; null once killed
+    std::vector<std::unique_ptr<Session>> dead;       // killed sessions (their captures stay)
+    std::vector<std::pair<std::string, bool>> sdps;   // per trace session: SDP, UDP push
     int64_t now = 0;
     uint32_t rand_calls = 0;
     std::vector<SourceReport> reports;
 
     int add_session(const std::string& sdp, bool udp_push = false) {
+        sdps.emplace_back(sdp, udp_push);
+        sessions.push_back(build(sdp, udp_push, (uint32_t)sessions.size()));
+        return (int)sessions.size() - 1;
+    }
+
+    // a fresh ReflectorSession: new streams, each drawing its report identity (rand(), clock)
+    std::unique_ptr<Session> build(const std::string& sdp, bool udp_push, uint32_t idx) {
         auto s = std::make_unique<Session>();
+        s->idx = idx;
         s->udp_push = udp_push;
         for (auto& ti : parse_sdp(sdp)) {
             Stream st;
@@ -226,8 +243,38 @@ struct Model {
             st.snd[1].rtcp_port = udp_push;     // socket B is the odd port only when bound (UDP push)
             s->streams.push_back(std::move(st));
         }
-        sessions.push_back(std::move(s));
-        return (int)sessions.size() - 1;
+        return s;
+    }
+
+    // ---- lifecycle (trace.py PUBLISH / UNPUBLISH) ---------------------------------------
+    // references: the pusher's plus one per output; at 0 the session is unregistered and
+    // killed (RemoveOutput, QTSSReflectorModule.cpp:2162-2192)
+    void release_check(uint32_t s) {
+        Session* se = sessions[s].get();
+        if (se && !se->published && se->outputs.empty()) {
+            dead.push_back(std::move(sessions[s]));
+            sessions[s].reset();
+        }
+    }
+    // DestroySession's broadcaster branch + RemoveOutput(NULL, session, kill): with kill every
+    // output is torn down (its client session closes: removed as by leave), then the pusher's
+    // reference goes
+    void unpublish(uint32_t s, bool kill) {
+        Session* se = s < sessions.size() ? sessions[s].get() : nullptr;
+        if (!se || !se->published) return;
+        se->published = false;
+        if (kill) {
+            for (auto& o : se->outputs) se->left.push_back(std::move(o));
+            se->outputs.clear();
+        }
+        release_check(s);
+    }
+    // FindOrCreateSession for a push: the existing session as it is, else a fresh one; a second
+    // pusher of a published session is refused
+    void publish(uint32_t s) {
+        if (s >= sessions.size()) return;
+        if (sessions[s]) { sessions[s]->published = true; return; }
+        sessions[s] = build(sdps[s].first, sdps[s].second, s);
     }
 
     // ---- ingest -------------------------------------------------------------------------
@@ -261,6 +308,7 @@ struct Model {
     // addr / port: the datagram's source (UDP push); 0 for an interleaved push
     void push(int session, int track, bool rtcp_socket, const uint8_t* data, uint32_t len,
               uint32_t addr = 0, uint16_t port = 0) {
+        if (!sessions[session] || !sessions[session]->published) return;   // no pusher: dropped
         Session& se = *sessions[session];
         if (track < 0 || track >= (int)se.streams.size() || len == 0) return;
         Stream& st = se.streams[track];
@@ -306,6 +354,7 @@ struct Model {
     // (0 when len < 4, ReflectorStream.h:180-189) becomes qtssRTPStrFirstSeqNumber.  Without
     // buffers the PLAY is retried later: here the join is dropped (returns false).
     bool join(int session, uint32_t sub_id, bool tcp, std::vector<uint8_t>* sink = nullptr, bool rtp_info = false) {
+        if (!sessions[session]) return false;        // no such session: the SETUP fails
         Session& se = *sessions[session];
         std::vector<uint16_t> first(se.streams.size(), 0);
         if (rtp_info) {
@@ -427,9 +476,11 @@ struct Model {
 
     void tick() {
         for (auto& se : sessions)
-            for (auto& o : se->outputs)
-                if (!o->capture) o->sink->clear();      // bench: sinks are recycled per tick
+            if (se)
+                for (auto& o : se->outputs)
+                    if (!o->capture) o->sink->clear();      // bench: sinks are recycled per tick
         for (uint32_t si = 0; si < sessions.size(); si++) {
+            if (!sessions[si]) continue;
             Session& se = *sessions[si];
             for (int x = 0; x < (int)se.streams.size(); x++) {
                 reflect(se, x, 0);
@@ -438,8 +489,9 @@ struct Model {
             }
         }
         for (auto& se : sessions)
-            for (auto& o : se->outputs)
-                for (auto& ss : o->ss) ss.budget[0] = ss.budget[1] = -1;
+            if (se)
+                for (auto& o : se->outputs)
+                    for (auto& ss : o->ss) ss.budget[0] = ss.budget[1] = -1;
     }
 
     // The RTCP sender's ReflectPackets: every kRRInterval (5 s) the timer restarts, and a
@@ -468,17 +520,22 @@ struct Model {
     // drops (DecEyeCount).  Its bookmarked packets stay pinned (fNeededByOutput is not
     // cleared), exactly as when the reference deletes the output.
     void leave(uint32_t sub_id) {
-        for (auto& se : sessions)
+        for (uint32_t s = 0; s < sessions.size(); s++) {
+            Session* se = sessions[s].get();
+            if (!se) continue;
             for (size_t i = 0; i < se->outputs.size(); i++)
                 if (se->outputs[i]->sub_id == sub_id) {
                     se->left.push_back(std::move(se->outputs[i]));
                     se->outputs.erase(se->outputs.begin() + (long)i);
+                    release_check(s);
                     return;
                 }
+        }
     }
 
     void block(uint32_t sub_id, uint32_t track, uint32_t kind, uint32_t budget) {
         for (auto& se : sessions)
+            if (se)
             for (auto& o : se->outputs)
                 if (o->sub_id == sub_id && track < o->ss.size()) o->ss[track].budget[kind & 1] = budget;
     }
@@ -503,7 +560,7 @@ static bool load(const char* path, Reader& r) {
     r.p = 4;
     const uint32_t v = r.get<uint32_t>();
     r.version = v;
-    return v == 1 || v == 2;
+    return v >= 1 && v <= 3;
 }
 
 // Replays a trace into `m`.  `sink_for` (bench mode) routes output bytes to memcpy sinks.
@@ -544,6 +601,13 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
             m.block(sub, trk, kind, budget);
         } else if (type == 6) {                 // LEAVE
             m.leave(r.get<uint32_t>());
+        } else if (type == 7) {                 // UNPUBLISH
+            uint32_t s = r.get<uint32_t>();
+            uint8_t kill = r.get<uint8_t>();
+            if (s % nshards == shard) m.unpublish(s, kill != 0);
+        } else if (type == 8) {                 // PUBLISH
+            uint32_t s = r.get<uint32_t>();
+            if (s % nshards == shard) m.publish(s);
         } else if (type == 5) {                 // UPKT: a datagram from the pusher's address
             uint32_t s = r.get<uint32_t>();
             uint8_t ch = r.get<uint8_t>();
@@ -566,10 +630,13 @@ static int run_capture(const char* in, const char* out) {
     replay(m, r, [&](uint32_t s, uint32_t sub, bool tcp, bool rtp_info) { m.join(s, sub, tcp, nullptr, rtp_info); });
     struct Rec { uint32_t sub, sess; uint16_t track; relay::Output* o; };
     std::vector<Rec> recs;
-    for (uint32_t s = 0; s < m.sessions.size(); s++)
-        for (auto* v : {&m.sessions[s]->outputs, &m.sessions[s]->left})
+    std::vector<relay::Session*> all;
+    for (auto& se : m.sessions) if (se) all.push_back(se.get());
+    for (auto& se : m.dead) all.push_back(se.get());
+    for (relay::Session* se : all)
+        for (auto* v : {&se->outputs, &se->left})
             for (auto& o : *v)
-                for (uint16_t x = 0; x < m.sessions[s]->streams.size(); x++) recs.push_back({o->sub_id, s, x, o.get()});
+                for (uint16_t x = 0; x < se->streams.size(); x++) recs.push_back({o->sub_id, se->idx, x, o.get()});
     std::stable_sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) {
         return a.sub != b.sub ? a.sub < b.sub : a.track < b.track; });
     FILE* f = fopen(out, "wb");
@@ -642,6 +709,9 @@ static int run_bench(const char* in, int threads, int repeat) {
         } else if (e.type == 6) {
             e.sub = r.get<uint32_t>();
             for (auto& l : lists) l.push_back(e);
+        } else if (e.type == 7 || e.type == 8) {
+            fprintf(stderr, "--bench models no session lifecycle (PUBLISH / UNPUBLISH events)\n");
+            return 2;
         } else {
             for (auto& l : lists) l.push_back(e);
         }

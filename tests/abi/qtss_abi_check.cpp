@@ -26,11 +26,11 @@ SAME(qtssPlayRespWriteTrackInfo); SAME(qtssSetupRespDontWriteSSRC);
 SAME(qtssPausedState); SAME(qtssPlayingState); SAME(qtssRTPTransportTypeUDP); SAME(qtssRTPTransportTypeTCP);
 SAME(qtssRTPTransportModePlay); SAME(qtssRTPTransportModeRecord);
 SAME(qtssUnknownPayloadType); SAME(qtssVideoPayloadType); SAME(qtssAudioPayloadType);
-SAME(qtssCliSesCloseClientTeardown);
+SAME(qtssCliSesCloseClientTeardown); SAME(qtssCliSesTearDownBroadcastEnded); SAME(qtssCliTeardownReason);
 SAME(qtssDescribeMethod); SAME(qtssSetupMethod); SAME(qtssTeardownMethod); SAME(qtssPlayMethod);
 SAME(qtssPauseMethod); SAME(qtssOptionsMethod); SAME(qtssAnnounceMethod); SAME(qtssRecordMethod);
 SAME(qtssAttrDataTypeCharArray); SAME(qtssAttrDataTypeSInt32); SAME(qtssAttrDataTypeUInt32);
-SAME(qtssAttrDataTypeVoidPointer);
+SAME(qtssAttrDataTypeVoidPointer); SAME(qtssAttrDataTypeBool16);
 SAME(qtssRTPStreamObjectType); SAME(qtssClientSessionObjectType); SAME(qtssRTSPSessionObjectType);
 SAME(qtssRTSPRequestObjectType); SAME(qtssTextMessagesObjectType); SAME(qtssModulePrefsObjectType);
 SAME(qtssRTPStrTrackID); SAME(qtssRTPStrPayloadName); SAME(qtssRTPStrPayloadType);

@@ -34,6 +34,16 @@ parity consequence:
 * ``leave``         subscribers leaving (RemoveOutput): between ticks, while blocked, leave +
                     new output in one tick, join + leave before a tick, an RTP-Info player,
                     and the eye counts of the receiver reports after leaves.
+* ``repush``        the session lifecycle: a pusher leaving with players attached and coming
+                    back with a new SSRC inside the 30 s latch (the surviving session is
+                    reused: zero-length packets, the old GOP for new joiners, until the
+                    latch resets), the last player leaving a pusher-less session (it dies; a
+                    join then fails; a re-push builds a fresh session: ids from 1, no stale
+                    GOP), ``kill_clients`` tearing a UDP push's players down (fresh receiver-
+                    report identities after the re-push), packets of a departed pusher
+                    dropped, duplicate PUBLISH / UNPUBLISH ignored.
+* ``threaded``      tick-invariant streams for the module's default (threaded) mode: players
+                    joined before the first packet, no H.264 key frames, TCP and UDP pushers.
 """
 from __future__ import annotations
 
@@ -47,19 +57,26 @@ from easydarwin_amd.trace import TCP, UDP, Trace
 
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
-              joins: list[tuple], tick_times=None, blocks=None, leaves=None):
+              joins: list[tuple], tick_times=None, blocks=None, leaves=None, pubs=None):
     # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
     # blocks: {tick time: [(sub, track, kind, budget)]}
     # leaves: [(t, sub)]
+    # pubs: [(t, "publish", session)] / [(t, "unpublish", session, kill)]
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
-    and ticks.  Within one tick interval the order is: packets (time order, session order),
-    then joins and leaves (time order; a join before a leave of the same time), then the
-    tick's socket budgets (BLOCK), then the TICK at the interval end."""
+    and ticks.  Within one tick interval the order is: packets and pusher PUBLISH / UNPUBLISH
+    events (time order: a PUBLISH before and an UNPUBLISH after the packets of its time), then
+    joins and leaves (time order; a join before a leave of the same time), then the tick's
+    socket budgets (BLOCK), then the TICK at the interval end."""
     # a packet (t, ch, data, addr, port) is a UDP datagram from a pusher (UPKT)
     pkts = []
     for s, lst in enumerate(per_session):
         for k, p in enumerate(lst):
             pkts.append((p[0], s, k) + tuple(p[1:]))
+    for p in (pubs or []):
+        if p[1] == "publish":
+            pkts.append((p[0], -1, 0, "P", p[2]))
+        else:
+            pkts.append((p[0], 1 << 30, 0, "U", p[2], p[3]))
     pkts.sort(key=lambda x: (x[0], x[1], x[2]))
     joins = sorted([(j[0], 0) + tuple(j[1:]) for j in joins] + [(t, 1, sub) for t, sub in (leaves or [])])
     ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
@@ -67,7 +84,11 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
     for tt in ticks:
         while i < len(pkts) and pkts[i][0] <= tt:
             t, s, _, ch, data = pkts[i][:5]
-            if len(pkts[i]) > 5:
+            if ch == "P":
+                tr.publish(t, data)
+            elif ch == "U":
+                tr.unpublish(t, data, pkts[i][5])
+            elif len(pkts[i]) > 5:
                 tr.upkt(t, s, ch, pkts[i][5], pkts[i][6], data)
             else:
                 tr.pkt(t, s, ch, data)
@@ -447,10 +468,95 @@ def leave() -> Trace:
     return _assemble(tr, [pk0, pk1], 100, dur, joins, blocks=blocks, leaves=leaves)
 
 
+def repush() -> Trace:
+    """Session lifecycle (QTSSReflectorModule.cpp:1379-1545, 2070-2196; the SSRC latch,
+    ReflectorStream.cpp:1732-1767).
+
+    * session 0 (RTSP-interleaved push, H.264 + PCMA, SRs on the video RTCP channel): players 1
+      (UDP) and 2 (TCP) stay through a pusher leave at 2 s (no kill: the players keep the
+      session alive); a new pusher with new SSRCs publishes at 3 s onto the surviving session,
+      so its packets are zero-length no-ops until the latch resets 30 s after the old SSRC's
+      last packet; player 3 joining at 4 s gets the OLD stream's GOP from the key pointer,
+      player 4 joining after the reset the new stream;
+    * session 1 (interleaved, video): its players leave at 1.5 s, its pusher at 2.5 s (the
+      session dies), a player joining at 2.6 s finds no session, the re-push at 3 s builds a
+      fresh session (packet ids from 1, unlatched filter, no stale GOP), player 13 joins it;
+    * session 2 (UDP push, receiver reports): the pusher leaves at 6 s with kill_clients, so
+      players 20 and 21 are torn down and the session dies; the re-push at 7 s draws new
+      report identities (rand(), CNAME at 7 s); player 22 joins at 8 s;
+    * session 3 (interleaved, video): the pusher leaves at 1 s with player 30 attached, its
+      packets until 1.5 s are dropped (no pusher), a re-push at 1.5 s continues the same
+      SSRC; a duplicate PUBLISH and an UNPUBLISH of a pusher-less session change nothing;
+      player 31 joins at 2 s."""
+    v0 = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=30, idr_bytes=3_000, rtcp_every_ms=900,
+                    ssrc=0x0A0A0001),
+          TrackSpec("audio", "PCMA/8000", 8, ssrc=0x0A0A0002)]
+    v0b = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=30, idr_bytes=3_000, rtcp_every_ms=900,
+                     ssrc=0x0B0B0001),
+           TrackSpec("audio", "PCMA/8000", 8, ssrc=0x0B0B0002)]
+    v1 = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=20, idr_bytes=4_000, ssrc=0x11110001)]
+    v1b = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=20, idr_bytes=4_000, ssrc=0x1111BBBB)]
+    u2 = [TrackSpec("video", "H264/90000", 96, bitrate=250_000, gop=30, idr_bytes=3_000, rtcp_every_ms=700,
+                    ssrc=0x22220001)]
+    u2b = [TrackSpec("video", "H264/90000", 96, bitrate=250_000, gop=30, idr_bytes=3_000, rtcp_every_ms=700,
+                     ssrc=0x2222BBBB)]
+    v3 = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=150_000, ssrc=0x33330001)]
+    tr = Trace()
+    tr.add_session(make_sdp(v0))
+    tr.add_session(make_sdp(v1))
+    tr.add_session(make_sdp(u2), udp_push=True)
+    tr.add_session(make_sdp(v3))
+    dur = 36_000
+    pk0 = session_packets(v0, 2000, SEED_BASE + 100)
+    pk0 += session_packets(v0b, dur - 3000, SEED_BASE + 101, t0=3000)
+    pk1 = session_packets(v1, 2500, SEED_BASE + 102)
+    pk1 += session_packets(v1b, 3000, SEED_BASE + 103, t0=3000)
+    src = _ip(10, 2, 0, 7)
+    pk2 = [(t, ch, d, src, 9000 + (ch & 1)) for t, ch, d in session_packets(u2, 6000, SEED_BASE + 104)]
+    pk2 += [(t, ch, d, _ip(10, 2, 0, 8), 9100 + (ch & 1))
+            for t, ch, d in session_packets(u2b, 5000, SEED_BASE + 105, t0=7000)]
+    pk3 = session_packets(v3, 4000, SEED_BASE + 106)           # keeps sending while unpublished
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (4000, 0, 3, UDP), (33_500, 0, 4, TCP),
+             (0, 1, 10, UDP), (0, 1, 11, TCP), (2600, 1, 12, UDP), (3500, 1, 13, TCP),
+             (0, 2, 20, UDP), (0, 2, 21, TCP), (8000, 2, 22, UDP),
+             (0, 3, 30, TCP), (2000, 3, 31, UDP)]
+    leaves = [(1500, 10), (1500, 11)]
+    pubs = [(2000, "unpublish", 0, 0), (3000, "publish", 0),
+            (2500, "unpublish", 1, 0), (3000, "publish", 1),
+            (6000, "unpublish", 2, 1), (7000, "publish", 2),
+            (1000, "unpublish", 3, 0), (1200, "unpublish", 3, 1), (1500, "publish", 3), (1800, "publish", 3)]
+    ticks = list(range(0, 3000, 100)) + list(range(3000, 12_000, 250)) + list(range(12_000, dur + 1, 500))
+    return _assemble(tr, [pk0, pk1, pk2, pk3], 100, dur, joins, tick_times=ticks, leaves=leaves, pubs=pubs)
+
+
+def threaded() -> Trace:
+    """The module in its default mode (its own tick thread and UDP reader thread, two pusher
+    threads; tests/test_gpu_qtss_module.py): every player joins before any packet, and no
+    stream carries an H.264 key frame, so each output starts at the first packet its first
+    tick sees inside the 1-s buffer window (the replay holds the pushers until every player has
+    received once) and follows its bookmarks from there -- the per-sub-stream bytes do not
+    depend on when the ticks run.  Two RTSP-interleaved pushers (MPEG-4 + PCMA, JPEG) and a UDP
+    pusher (MPEG-4 + PCMU)."""
+    a = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=400_000), TrackSpec("audio", "PCMA/8000", 8)]
+    b = [TrackSpec("video", "JPEG/90000", 26, bitrate=300_000)]
+    c = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=300_000), TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    tr.add_session(make_sdp(a))
+    tr.add_session(make_sdp(b))
+    tr.add_session(make_sdp(c), udp_push=True)
+    dur = 3000
+    pk = [session_packets(a, dur, SEED_BASE + 120, t0=100), session_packets(b, dur, SEED_BASE + 121, t0=100)]
+    src = _ip(10, 3, 0, 1)
+    pk.append([(t, ch, d, src, 8000 + (ch & 1)) for t, ch, d in session_packets(c, dur, SEED_BASE + 122, t0=100)])
+    joins = [(0, s, 10 * s + k, (UDP, TCP, UDP)[k]) for s in range(3) for k in range(3)]
+    return _assemble(tr, pk, 100, dur + 200, joins)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
-    "backpressure": backpressure, "udppush": udppush, "leave": leave,
+    "backpressure": backpressure, "udppush": udppush, "leave": leave, "repush": repush,
+    "threaded": threaded,
 }
 
 

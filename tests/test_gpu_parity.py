@@ -53,7 +53,7 @@ def test_engine_matches_reference(name, overlap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["mixed", "c1", "backpressure", "rtpinfo", "leave"])
+@pytest.mark.parametrize("name", ["mixed", "c1", "backpressure", "rtpinfo", "leave", "repush"])
 def test_pinned_host_ingest_matches_reference(name):
     """Batches written into pinned host buffers (edgpu_host_alloc, two sets alternating) and
     ingested asynchronously (EDGPU_PTR_PINNED: copy stream + event) give the reference bytes."""

@@ -15,6 +15,12 @@ pass) -- the input of the server's own thinning and over-buffer logic under QTSS
 track's socket pair and answers with its port; the replay sends every UPKT datagram over
 loopback from a socket bound to the trace's source port, and the receiver reports the module
 sends back (eye counts included) are part of the capture (its EDRR trailer).
+
+The session lifecycle (``repush``): pushers leaving with and without kill_clients, players
+keeping a session alive, fresh sessions after the last reference went -- the replay checks the
+module's reference counting at every player SETUP.  And the module's default mode
+(``threaded``): its own 5-ms tick thread and UDP reader thread, two pusher threads feeding
+RTSPIncomingData and loopback datagrams while the ticks run.
 """
 import hashlib
 import os
@@ -28,7 +34,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODULE = os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so")
 REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
 TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "anchor", "rtpinfo", "backpressure"]
-UDP_PUSH = ["udppush", "leave"]          # UDP pushers (with interleaved ones beside them)
+UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones beside them)
 
 
 @pytest.mark.gpu
@@ -46,3 +52,22 @@ def test_module_matches_reference(name, tmp_path):
         assert len(read_source_reports(c.read_bytes())) == len(fx["source_reports"])
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]
+
+
+@pytest.mark.gpu
+def test_module_threaded_default_mode_matches_reference(tmp_path):
+    """Tick thread + UDP reader thread + two pusher threads: the per-sub-stream bytes (tick
+    invariant for this trace) equal the reference capture's.  Transmit times and receiver-report
+    times depend on when the ticks ran and are not compared."""
+    from easydarwin_amd.trace import capture_summary, read_capture
+    t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    t.write_bytes(_trace("threaded").to_bytes())
+    for attempt in range(2):             # the same bytes whatever the tick timing: run it twice
+        r = subprocess.run([REPLAY, MODULE, str(t), str(c), "--threaded"], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got = capture_summary(read_capture(c.read_bytes()))
+        want = _fixture("threaded")["substreams"]
+        assert got.keys() == want.keys()
+        bad = {k: (got[k][:2], want[k][:2]) for k in want if got[k] != want[k]}
+        assert not bad, f"run {attempt}: {len(bad)} sub-streams differ: {dict(list(bad.items())[:6])}"

@@ -173,8 +173,8 @@ def test_replay_pusher_model_delivers_every_packet(name):
     tr = SCENARIOS[name]()
     if any(len(ev[4]) > 2043 for ev in tr.events if ev[0] == PKT):
         pytest.skip("packets above 2043 bytes cannot travel RTSP-interleaved (connection dropped)")
-    batches = _batches(tr, True)
-    plan = tcp_plan(batches, seed=7)
+    batches, barriers = _batches(tr, True)
+    plan = tcp_plan(batches, seed=7, barriers=barriers)
     ctx = _RestatedCtx()
     calls = 0
     for b, p in zip(batches, plan):

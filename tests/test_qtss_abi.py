@@ -45,4 +45,4 @@ def test_module_registers_through_the_plugin_abi():
     assert r.returncode == 0, r.stderr
     info = json.loads(r.stdout)
     assert info["module"] == "QTSSReflectorModule"
-    assert info["roles"] == 6 and info["attributes"] == 7
+    assert info["roles"] == 6 and info["attributes"] == 8

@@ -3,6 +3,9 @@
 # 1 no descriptors, 2 no arena stores, 4 no chunk-word loads (stores write whatever the
 # registers hold).  Outputs are wrong except at 0: timing only.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+# the measurement build (every variant, EDGPU_ABLATE): make -C easydarwin_amd/csrc ab
+export EDGPU_LIB=$R/easydarwin_amd/ab/libedgpu_ab.so
+[ -e $EDGPU_LIB ] || { echo "build $EDGPU_LIB first"; exit 2; }
 TAG=$1; V=$2
 mkdir -p $R/gpurun_out/$TAG
 for a in ${ABL:-0 1 2 3}; do

@@ -2,6 +2,9 @@
 # A/B the fan-out variants on the C2 bench (GPU box).  Usage: tools/ab_fanout.sh <out-tag> <variants...>
 # BENCH_EXTRA: extra bench.py flags (e.g. "--rewrite"); TAGSUF: suffix of the output files.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+# the measurement build (every variant, EDGPU_ABLATE): make -C easydarwin_amd/csrc ab
+export EDGPU_LIB=$R/easydarwin_amd/ab/libedgpu_ab.so
+[ -e $EDGPU_LIB ] || { echo "build $EDGPU_LIB first"; exit 2; }
 TAG=$1; shift
 mkdir -p $R/gpurun_out/$TAG
 k=0

@@ -2,6 +2,9 @@
 # Ingest A/B (GPU box): each argument is "MODE:ABLATE" -- EDGPU_INGEST copy mode (0 in-kernel,
 # 1 separate copy kernel) and EDGPU_ABLATE bits (16: no block-total atomics).  Timing only.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+# the measurement build (every variant, EDGPU_ABLATE): make -C easydarwin_amd/csrc ab
+export EDGPU_LIB=$R/easydarwin_amd/ab/libedgpu_ab.so
+[ -e $EDGPU_LIB ] || { echo "build $EDGPU_LIB first"; exit 2; }
 TAG=$1; shift
 mkdir -p $R/gpurun_out/$TAG
 for ma in "$@"; do

@@ -21,6 +21,13 @@
 //     RTP-Info player (ua_flags bit 0); a PLAY the module defers (QTSS_SetIdleTimer instead of
 //     QTSS_Play) is dropped, as the reference harness drops it;
 //   * LEAVE -> ClientSessionClosing for the player's client session;
+//   * UNPUBLISH (trace v3) -> ClientSessionClosing for the pusher's client session, with the
+//     module's QTSSReflectorModuleTearDownClients attribute set to the event's kill flag; then,
+//     as the server does after QTSS_Teardown, ClientSessionClosing for every player the module
+//     tore down; PUBLISH -> a new pusher connection: ANNOUNCE + SETUPs + RECORD (refused by the
+//     module while a pusher is attached -- then it only closes again).  The replay keeps the
+//     reference's reference counts itself and fails if the module disagrees: a player's SETUP
+//     must fail exactly when the session has ended;
 //   * TICK -> EDGPU_QTSSReflectorModule_Tick at the virtual clock (manual-tick mode);
 //   * BLOCK -> the player's RTP stream object accepts `budget` QTSS_Writes in the next tick,
 //     then returns QTSS_WouldBlock (the EAGAIN path of RTPStream::Write).
@@ -33,8 +40,16 @@
 // (trace.py rr_ssrc), which sets each stream's receiver-report SSRC as the reference's
 // ReflectorStream constructor draws it.
 //
+// --threaded: the module's default mode instead of manual ticks -- its own tick thread
+// (EDGPU_QTSS_TICK_MSEC=5 here) and UDP reader thread; the events up to the first packet (the
+// players' joins) are applied in order, then two pusher threads (sessions by parity) feed the
+// packets -- RTSPIncomingData and loopback datagrams -- while the ticks run, holding back after
+// each session's first packet time until every player's stream has been written once; the
+// trace's TICKs are not used.  For traces whose per-sub-stream bytes do not depend on tick
+// timing (tests/scenarios.py threaded).
+//
 // Test infrastructure (tests/test_gpu_qtss_module.py, tests/test_qtss_abi.py); not shipped.
-// Usage: qtss_replay <module.so> <trace.edtr> <capture.edcp>
+// Usage: qtss_replay <module.so> <trace.edtr> <capture.edcp> [--threaded]
 //        qtss_replay <module.so> --register      (Register role only; no GPU needed)
 #include <arpa/inet.h>
 #include <dlfcn.h>
@@ -44,6 +59,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +70,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "qtss_module_abi.h"
@@ -86,7 +105,11 @@ static void set_attr(Obj* o, uint32_t id, uint32_t idx, const void* p, uint32_t 
 }
 template <typename T> static void set_pod(Obj* o, uint32_t id, T v) { set_attr(o, id, 0, &v, sizeof(v)); }
 
-static int64_t g_now = 0;
+static std::atomic<int64_t> g_now{0};
+static void advance_clock(int64_t t) {
+    int64_t c = g_now.load();
+    while (t > c && !g_now.compare_exchange_weak(c, t)) {}
+}
 
 // the reference harness's deterministic rand() (trace.py rr_ssrc), for the module's own calls;
 // other callers (the engine's default identity draw, which the module overrides) get 0
@@ -104,7 +127,7 @@ static std::map<std::string, uint32_t> g_attr_ids;
 static std::vector<Obj*> g_streams;                  // every RTP stream object, creation order
 
 // ---- callbacks (QTSS_Private.h indices; signatures of the QTSS_Private.cpp stubs) -----------
-static QTSS_Error cb_milliseconds(int64_t* out, ...) { *out = g_now; return QTSS_NoErr; }
+static QTSS_Error cb_milliseconds(int64_t* out, ...) { *out = g_now.load(); return QTSS_NoErr; }
 static QTSS_Error cb_add_role(uint32_t role, ...) { g_roles.insert(role); return QTSS_NoErr; }
 static QTSS_Error cb_add_static_attr(uint32_t type, const char* name, void*, uint32_t, ...) {
     const std::string key = std::to_string(type) + ":" + name;
@@ -157,9 +180,9 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
     c.push_back((char)(len >> 8));
     c.push_back((char)(len & 0xFF));
     c.append((const char*)ps->packetData, len);
-    o->npk[k]++;
+    __atomic_add_fetch(&o->npk[k], 1, __ATOMIC_RELEASE);
     o->tt[k].push_back(ps->packetTransmitTime);
-    g_writes++;
+    __atomic_add_fetch(&g_writes, 1, __ATOMIC_RELEASE);
     if (outLen) *outLen = len;
     return QTSS_NoErr;
 }
@@ -256,7 +279,7 @@ static void read_reports() {
             ssize_t n;
             while ((n = recvfrom(pf[i].fd, buf, sizeof(buf), 0, (sockaddr*)&from, &fl)) >= 0) {
                 const auto o = g_rtcp_owner.find(ntohs(from.sin_port));
-                Report r{g_now, o == g_rtcp_owner.end() ? 0xFFFFFFFFu : o->second.first,
+                Report r{g_now.load(), o == g_rtcp_owner.end() ? 0xFFFFFFFFu : o->second.first,
                          (uint16_t)(o == g_rtcp_owner.end() ? 0xFFFF : o->second.second), key[i].first, key[i].second,
                          std::string(buf, (size_t)n)};
                 got.push_back(r);
@@ -339,8 +362,14 @@ int main(int argc, char** argv) {
                g_attr_ids.size());
         return 0;
     }
-    if (argc != 4) return 2;
-    setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
+    const bool threaded = argc == 5 && strcmp(argv[4], "--threaded") == 0;
+    if (argc != 4 && !threaded) return 2;
+    if (threaded) {
+        setenv("EDGPU_QTSS_MANUAL_TICK", "0", 1);
+        if (!getenv("EDGPU_QTSS_TICK_MSEC")) setenv("EDGPU_QTSS_TICK_MSEC", "5", 1);
+    } else {
+        setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
+    }
     memset(&rp, 0, sizeof(rp));
     if (g_dispatch(QTSS_Initialize_Role, &rp) != QTSS_NoErr) { fprintf(stderr, "Initialize failed (no GPU?)\n"); return 3; }
 
@@ -353,47 +382,77 @@ int main(int argc, char** argv) {
     r.p = 4;
     const uint32_t ver = r.get<uint32_t>();
     const uint32_t nsess = r.get<uint32_t>();
-    std::vector<std::string> paths(nsess);
+    std::vector<std::string> paths(nsess), sdps(nsess);
     std::vector<uint32_t> ntracks(nsess, 0);
+    std::vector<uint8_t> flags(nsess, 0);
     std::vector<Obj*> push_rtsp(nsess, nullptr), push_client(nsess, nullptr);
     std::vector<std::vector<uint16_t>> server_port(nsess);     // UDP push: the module's RTP port per track
-    for (uint32_t s = 0; s < nsess; s++) {
-        const uint32_t n = r.get<uint32_t>();
-        std::string sdp((const char*)&r.d[r.p], n);
-        r.p += n;
-        const uint8_t fl = ver >= 2 ? r.get<uint8_t>() : 0;
-        for (size_t k = sdp.find("m="); k != std::string::npos; k = sdp.find("\nm=", k + 1)) ntracks[s]++;
-        paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
-        const uint32_t tt = (fl & 1) ? qtssRTPTransportTypeUDP : qtssRTPTransportTypeTCP;
-        push_rtsp[s] = new_obj(qtssRTSPSessionObjectType);
-        push_client[s] = new_obj(qtssClientSessionObjectType);
-        g_rtsp_of_client[push_client[s]] = push_rtsp[s];
-        if (request(push_rtsp[s], push_client[s], qtssAnnounceMethod, paths[s], "", 0, tt, sdp))
-            { fprintf(stderr, "ANNOUNCE failed\n"); return 3; }
+    // the reference's reference counting, kept here to check the module's: does the session
+    // exist, and how many players hold it (the pusher's reference is push_rtsp[s] != nullptr)
+    std::vector<bool> alive(nsess, false);
+    std::vector<uint32_t> holders(nsess, 0);
+    // a pusher connection: ANNOUNCE, a record-mode SETUP per track, RECORD (false: refused)
+    auto publish = [&](uint32_t s) -> bool {
+        const uint32_t tt = (flags[s] & 1) ? qtssRTPTransportTypeUDP : qtssRTPTransportTypeTCP;
+        Obj* rtsp = new_obj(qtssRTSPSessionObjectType);
+        Obj* client = new_obj(qtssClientSessionObjectType);
+        g_rtsp_of_client[client] = rtsp;
+        if (request(rtsp, client, qtssAnnounceMethod, paths[s], "", 0, tt, sdps[s]))
+            { fprintf(stderr, "ANNOUNCE failed\n"); exit(3); }
+        std::vector<uint16_t> ports;
         for (uint32_t t = 0; t < ntracks[s]; t++) {
             Obj* req = nullptr;
-            if (request(push_rtsp[s], push_client[s], qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(t + 1),
-                        std::to_string(t + 1), qtssRTPTransportModeRecord, tt, std::string(), &req))
-                { fprintf(stderr, "push SETUP failed\n"); return 3; }
-            if (fl & 1) {
+            if (request(rtsp, client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(t + 1),
+                        std::to_string(t + 1), qtssRTPTransportModeRecord, tt, std::string(), &req)) {
+                QTSS_RoleParams p;                         // refused: the connection closes
+                memset(&p, 0, sizeof(p));
+                p.clientSessionClosingParams.inClientSession = client;
+                (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                return false;
+            }
+            if (flags[s] & 1) {
                 auto it = req->attrs.find(qtssRTSPReqSetUpServerPort);
                 uint16_t port = 0;
                 if (it != req->attrs.end() && !it->second.empty() && it->second[0].size() == 2) memcpy(&port, it->second[0].data(), 2);
-                if (port == 0 || (port & 1)) { fprintf(stderr, "UDP push SETUP: no even server port\n"); return 3; }
-                server_port[s].push_back(port);
+                if (port == 0 || (port & 1)) { fprintf(stderr, "UDP push SETUP: no even server port\n"); exit(3); }
+                ports.push_back(port);
                 g_rtcp_owner[(uint16_t)(port + 1)] = std::make_pair(s, (uint16_t)t);
             }
         }
-        if (request(push_rtsp[s], push_client[s], qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, tt))
-            { fprintf(stderr, "RECORD failed\n"); return 3; }
+        if (request(rtsp, client, qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, tt))
+            { fprintf(stderr, "RECORD failed\n"); exit(3); }
+        push_rtsp[s] = rtsp;
+        push_client[s] = client;
+        server_port[s] = ports;
+        alive[s] = true;
+        return true;
+    };
+    for (uint32_t s = 0; s < nsess; s++) {
+        const uint32_t n = r.get<uint32_t>();
+        sdps[s].assign((const char*)&r.d[r.p], n);
+        r.p += n;
+        flags[s] = ver >= 2 ? r.get<uint8_t>() : 0;
+        for (size_t k = sdps[s].find("m="); k != std::string::npos; k = sdps[s].find("\nm=", k + 1)) ntracks[s]++;
+        paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
+        if (!publish(s)) { fprintf(stderr, "push SETUP failed\n"); return 3; }
     }
+    auto close_client = [&](Obj* client) {
+        QTSS_RoleParams p;
+        memset(&p, 0, sizeof(p));
+        p.clientSessionClosingParams.inClientSession = client;
+        (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+    };
+    auto release_check = [&](uint32_t s) { if (!push_rtsp[s] && holders[s] == 0) alive[s] = false; };
     std::vector<Player> players;
     std::vector<char> frame(70000);
     while (r.p < r.d.size()) {
+        const size_t at = r.p;
         const uint8_t type = r.get<uint8_t>();
         if (type == 0) break;
         const int64_t t = r.get<int64_t>();
-        if (t > g_now) g_now = t;
+        if (threaded && (type == 1 || type == 5)) { r.p = at; break; }     // the pusher threads' part
+        if (threaded && type == 3) continue;                               // the module ticks itself
+        advance_clock(t);
         if (type == 1) {                                         // PKT -> RTSPIncomingData
             const uint32_t s = r.get<uint32_t>();
             const uint8_t ch = r.get<uint8_t>();
@@ -412,29 +471,32 @@ int main(int argc, char** argv) {
         } else if (type == 2) {                                  // JOIN -> SETUP x tracks + PLAY
             const uint32_t s = r.get<uint32_t>(), sub = r.get<uint32_t>();
             const uint8_t tr = r.get<uint8_t>(), ua = r.get<uint8_t>();
-            if (!push_rtsp[s]) continue;
             Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_obj(qtssClientSessionObjectType), {}};
             g_rtsp_of_client[pl.client] = pl.rtsp;
             const std::string agent = (ua & 1) ? "vlc/3.0.8 LibVLC/3.0.8" : "EasyPlayer/1.0";   // case-sensitive match
             set_attr(pl.client, qtssCliSesFirstUserAgent, 0, agent.data(), (uint32_t)agent.size());
             const uint32_t tt = tr ? qtssRTPTransportTypeTCP : qtssRTPTransportTypeUDP;
             const size_t before = g_streams.size();
-            for (uint32_t x = 0; x < ntracks[s]; x++)
-                if (request(pl.rtsp, pl.client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(x + 1),
-                            std::to_string(x + 1), qtssRTPTransportModePlay, tt))
-                    { fprintf(stderr, "player SETUP failed\n"); return 3; }
+            bool setup_ok = true;
+            for (uint32_t x = 0; x < ntracks[s] && setup_ok; x++)
+                setup_ok = request(pl.rtsp, pl.client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(x + 1),
+                                   std::to_string(x + 1), qtssRTPTransportModePlay, tt) == QTSS_NoErr;
+            if (setup_ok != alive[s]) {
+                fprintf(stderr, "player SETUP %s on a session that %s\n", setup_ok ? "succeeded" : "failed",
+                        alive[s] ? "exists" : "has ended");
+                return 3;
+            }
+            if (!setup_ok) { close_client(pl.client); continue; }     // no session: not an output
             for (size_t k = before; k < g_streams.size(); k++) {
                 g_streams[k]->sub = sub; g_streams[k]->session = s; g_streams[k]->track = (uint32_t)(k - before);
                 pl.streams.push_back(g_streams[k]);
             }
             (void)request(pl.rtsp, pl.client, qtssPlayMethod, paths[s], "", qtssRTPTransportModePlay, tt);
             if (!pl.client->played) {                           // deferred RTP-Info PLAY: dropped
-                QTSS_RoleParams p;
-                memset(&p, 0, sizeof(p));
-                p.clientSessionClosingParams.inClientSession = pl.client;
-                (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                close_client(pl.client);
                 continue;
             }
+            holders[s]++;
             players.push_back(pl);
         } else if (type == 3) {                                  // TICK
             const QTSS_Error e = tick_fn();
@@ -456,7 +518,7 @@ int main(int argc, char** argv) {
             const uint32_t len = r.get<uint32_t>();
             const uint8_t* data = &r.d[r.p];
             r.p += len;
-            if (len == 0 || ch / 2 >= server_port[s].size()) continue;
+            if (!push_rtsp[s] || len == 0 || ch / 2 >= server_port[s].size()) continue;
             const int fd = source_socket(addr, port);
             (void)source_socket(addr, (uint16_t)(port | 1));        // where the receiver reports may go
             sockaddr_in to;
@@ -474,15 +536,133 @@ int main(int argc, char** argv) {
             const uint32_t sub = r.get<uint32_t>();
             for (auto& pl : players)
                 if (pl.sub == sub && !pl.left) {
-                    QTSS_RoleParams p;
-                    memset(&p, 0, sizeof(p));
-                    p.clientSessionClosingParams.inClientSession = pl.client;
-                    (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                    close_client(pl.client);
                     pl.left = true;
+                    holders[pl.session]--;
+                    release_check(pl.session);
                 }
+        } else if (type == 7) {                                  // UNPUBLISH -> the pusher's session closes
+            const uint32_t s = r.get<uint32_t>();
+            const uint8_t kill = r.get<uint8_t>();
+            if (!push_rtsp[s]) continue;
+            auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleTearDownClients");
+            if (it == g_attr_ids.end()) { fprintf(stderr, "kill-clients attribute not registered\n"); return 3; }
+            const uint16_t k16 = kill;
+            set_attr(push_client[s], it->second, 0, &k16, sizeof(k16));
+            close_client(push_client[s]);
+            push_rtsp[s] = push_client[s] = nullptr;
+            // the server closes the client sessions the module tore down (QTSS_Teardown)
+            uint32_t torn = 0;
+            for (auto& pl : players)
+                if (!pl.left && pl.client->torn_down) {
+                    close_client(pl.client);
+                    pl.left = true;
+                    holders[pl.session]--;
+                    torn++;
+                }
+            if (kill && torn == 0 && holders[s] != 0) { fprintf(stderr, "kill_clients tore nothing down\n"); return 3; }
+            release_check(s);
+        } else if (type == 8) {                                  // PUBLISH -> a new pusher connection
+            const uint32_t s = r.get<uint32_t>();
+            if (push_rtsp[s]) {                                  // a duplicate broadcast must be refused
+                const std::vector<uint16_t> keep = server_port[s];
+                Obj* kr = push_rtsp[s]; Obj* kc = push_client[s];
+                if (publish(s)) { fprintf(stderr, "duplicate PUBLISH accepted\n"); return 3; }
+                push_rtsp[s] = kr; push_client[s] = kc; server_port[s] = keep;
+                continue;
+            }
+            if (!publish(s)) { fprintf(stderr, "PUBLISH refused\n"); return 3; }
         } else {
             fprintf(stderr, "bad event %u\n", type);
             return 3;
+        }
+    }
+    if (threaded) {
+        // the packets, split by session parity over two pusher threads
+        struct Ev { int64_t t; uint8_t type, ch; uint32_t s, addr, len; uint16_t port; const uint8_t* data; };
+        std::vector<Ev> lists[2];
+        std::map<uint32_t, int64_t> first_t;
+        std::set<std::pair<uint32_t, uint32_t>> rtp_tracks;          // (session, track) with RTP packets
+        while (r.p < r.d.size()) {
+            Ev e{};
+            e.type = r.get<uint8_t>();
+            if (e.type == 0) break;
+            e.t = r.get<int64_t>();
+            if (e.type == 3) continue;
+            if (e.type != 1 && e.type != 5) { fprintf(stderr, "--threaded: event %u after the first packet\n", e.type); return 3; }
+            e.s = r.get<uint32_t>(); e.ch = r.get<uint8_t>();
+            if (e.type == 5) { e.addr = r.get<uint32_t>(); e.port = r.get<uint16_t>(); }
+            e.len = r.get<uint32_t>();
+            e.data = &r.d[r.p];
+            r.p += e.len;
+            if (!first_t.count(e.s)) first_t[e.s] = e.t;
+            if (!(e.ch & 1)) rtp_tracks.insert({e.s, (uint32_t)e.ch / 2});
+            if (e.type == 5) { (void)source_socket(e.addr, e.port); (void)source_socket(e.addr, (uint16_t)(e.port | 1)); }
+            lists[e.s % 2].push_back(e);
+        }
+        std::atomic<int> failed{0};
+        auto pusher = [&](int k) {
+            std::vector<char> fr(70000);
+            bool gated = false;
+            for (size_t i = 0; i < lists[k].size(); i++) {
+                const Ev& e = lists[k][i];
+                if (!gated && e.t > first_t[e.s]) {
+                    // hold until every player of this thread's sessions has a write on each RTP
+                    // track that carries packets (its first tick took the buffer window)
+                    gated = true;
+                    const auto t0 = std::chrono::steady_clock::now();
+                    for (;;) {
+                        bool all = true;
+                        for (const Player& pl : players)
+                            if (pl.session % 2 == (uint32_t)k)
+                                for (const Obj* st : pl.streams)
+                                    if (rtp_tracks.count({pl.session, st->track}) &&
+                                        __atomic_load_n(&st->npk[0], __ATOMIC_ACQUIRE) == 0)
+                                        all = false;
+                        if (all) break;
+                        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) { failed = 1; return; }
+                        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                    }
+                }
+                advance_clock(e.t);
+                if (e.type == 1) {
+                    fr[0] = '$'; fr[1] = (char)e.ch; fr[2] = (char)(e.len >> 8); fr[3] = (char)e.len;
+                    memcpy(&fr[4], e.data, e.len);
+                    QTSS_RoleParams p;
+                    memset(&p, 0, sizeof(p));
+                    p.rtspIncomingDataParams.inRTSPSession = push_rtsp[e.s];
+                    p.rtspIncomingDataParams.inClientSession = push_client[e.s];
+                    p.rtspIncomingDataParams.inPacketData = fr.data();
+                    p.rtspIncomingDataParams.inPacketLen = e.len + 4;
+                    (void)g_dispatch(QTSS_RTSPIncomingData_Role, &p);
+                } else if (e.len && e.ch / 2 < server_port[e.s].size()) {
+                    const int fd = source_socket(e.addr, e.port);
+                    sockaddr_in to;
+                    memset(&to, 0, sizeof(to));
+                    to.sin_family = AF_INET;
+                    to.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+                    to.sin_port = htons((uint16_t)(server_port[e.s][e.ch / 2] + (e.ch & 1)));
+                    while (sendto(fd, e.data, e.len, 0, (const sockaddr*)&to, sizeof(to)) != (ssize_t)e.len) {
+                        if (errno != EAGAIN && errno != ENOBUFS) { failed = 2; return; }
+                        std::this_thread::sleep_for(std::chrono::microseconds(200));
+                    }
+                    // keep the reader's socket buffer from overflowing (a full one drops, as UDP does)
+                    if (i % 16 == 15) std::this_thread::sleep_for(std::chrono::microseconds(500));
+                }
+                if (i % 32 == 31) std::this_thread::sleep_for(std::chrono::microseconds(300));   // ticks interleave
+            }
+        };
+        std::thread a(pusher, 0), b(pusher, 1);
+        a.join();
+        b.join();
+        if (failed) { fprintf(stderr, "--threaded: pusher thread failed (%d)\n", failed.load()); return 3; }
+        // let the tick thread drain: until the writes stop growing for 200 ms
+        uint64_t last = ~0ull;
+        for (int quiet = 0; quiet < 40;) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+            const uint64_t w = __atomic_load_n(&g_writes, __ATOMIC_ACQUIRE);
+            quiet = w == last ? quiet + 1 : 0;
+            last = w;
         }
     }
     memset(&rp, 0, sizeof(rp));
