@@ -23,7 +23,10 @@ from test_gpu_parity import _fixture, _trace
 @pytest.mark.parametrize("mode", ["all", "late"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
 def test_replica_matches_reference(name, mode):
-    cap, _ = replay(_trace(name), replica=mode)
+    tr = _trace(name)
+    if tr.has_lifecycle:
+        pytest.skip("replica replays model no session lifecycle (a replica follows a live owner session)")
+    cap, _ = replay(tr, replica=mode)
     assert hashlib.sha256(cap).hexdigest() == _fixture(name)["capture_sha256"]
 
 
