@@ -1100,6 +1100,14 @@ int edgpu_host_free(edgpu_ctx* x, void* p) {
     return EDGPU_OK;
 }
 
+// The caller may rewrite a pinned batch once the next ingest call has returned: every ingest
+// entry point first waits for the outstanding pinned copies (normally long done).
+static int wait_pinned_copies(edgpu_ctx* x) {
+    for (auto& st : x->pin)
+        if (st.issued) HIP_CHECK(hipEventSynchronize(st.copied));
+    return EDGPU_OK;
+}
+
 // EDGPU_PTR_PINNED: copies the batch into staging set k on the copy stream; the context stream
 // waits for it.  Returns the device pointers of the set.
 static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
@@ -1153,8 +1161,10 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         const edgpu_ctx::PinStage& S = x->pin[k];
         r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, x->ingest_mode);
         if (!r) x->pend_stage = k;
+        else (void)hipEventRecord(S.consumed, x->stream);   // nothing will read the set: free it
         return r;
     }
+    { int r = wait_pinned_copies(x); if (r) return r; }
     if (where == EDGPU_PTR_HOST) {
         // validate on the host (segment bounds, session ids, slot bounds) before any launch
         int r = validate_host_batch(x, desc, n, seg_off, seg_sess, nseg, blob_bytes);
@@ -1185,6 +1195,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (!n) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
+    { int r = wait_pinned_copies(x); if (r) return r; }
     x->carry_len.resize(x->sessions.size(), 0);
     // one group per session: its reads are a run of consecutive entries, contiguous in `bytes`
     std::vector<TcpGroup> groups;
@@ -1404,6 +1415,8 @@ const char* edgpu_fanout_kernel(edgpu_ctx* x) {
 
 int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest (the ingest counters "
+                                           "of a batch are set by its index)");
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
     HIP_CHECK(sync_all(x));

@@ -177,7 +177,8 @@ typedef struct edgpu_tick_stats {
     uint64_t relayed_packets;   /* IncrementTotalPackets semantics (RTPStream.cpp:1213-1216) */
     uint64_t relayed_bytes;     /* wire bytes incl. '$' framing */
     uint64_t arena_bytes;
-    uint64_t ingested_packets;  /* last ingest batch */
+    uint64_t ingested_packets;  /* the batch the last edgpu_keyframe_index indexed (the counters
+                                   move at the index, not at edgpu_ingest) */
     uint64_t ingested_bytes;
     int32_t  status;            /* sticky device-side error (EDGPU_RING_OVERFLOW, ...) */
     uint32_t _pad;
@@ -297,8 +298,9 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
  * of two device staging sets on a dedicated copy stream, and k_ingest waits for that copy on
  * the context stream -- so the PCIe transfer of batch t+1 overlaps the fan-out of batch t, and
  * the call returns without waiting for the GPU.  Buffer reuse: a pinned batch may be rewritten
- * once the NEXT edgpu_ingest has returned (that call waits for the previous batch's copy), so
- * two host batches used alternately never stall the reader on the GPU. */
+ * once the NEXT ingest call (edgpu_ingest of any pointer kind, or edgpu_ingest_interleaved) has
+ * returned -- every ingest entry point waits for the previous pinned batch's copy -- so two host
+ * batches used alternately never stall the reader on the GPU. */
 int  edgpu_host_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
 /* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
@@ -432,7 +434,16 @@ int  edgpu_session_eyes_add(edgpu_ctx* ctx, uint32_t session, int32_t delta);
  * blocks).  Blocked TCP sub-streams are reported with edgpu_fanout_blocked before returning.
  * The tick's distinct bytes come over PCIe in one copy (identity UDP sub-streams of a sender share
  * one region, edgpu_arena_gather), with the descriptors and sub-stream table; `threads` workers
- * own disjoint subscribers and send with sendmmsg / sendmsg. */
+ * own disjoint subscribers and send with sendmmsg / sendmsg.
+ *
+ * UDP loss granularity.  By default (EDGPU_EGRESS_GSO unset or 1) runs of equal-length
+ * datagrams of a sub-stream (FU-A fragments of a frame) leave as UDP GSO messages (UDP_SEGMENT,
+ * up to 64 datagrams / 64 KiB each): the wire carries exactly the datagrams the reference
+ * sends, but a send the socket refuses (EAGAIN / ENOBUFS) drops the whole message, where the
+ * reference's per-packet (void)SendTo drops one datagram (RTPStream.cpp:1145).  What arrives is
+ * always an in-order subset of the tick's datagrams per sub-stream (no reordering, no
+ * duplicates; tests/test_gpu_egress.py).  EDGPU_EGRESS_GSO=0 is the reference-exact mode: one
+ * datagram per message, one datagram lost per refused send. */
 typedef struct edgpu_egress edgpu_egress;
 typedef struct edgpu_egress_stats {
     uint64_t udp_datagrams, udp_bytes;
@@ -463,7 +474,8 @@ int  edgpu_egress_flush(edgpu_egress* eg, uint64_t* pending);
  * (ClientSessionClosing -> edgpu_subscriber_remove).  Sockets are written with MSG_NOSIGNAL. */
 int  edgpu_egress_disconnected(edgpu_egress* eg, uint32_t* out, uint32_t cap, uint32_t* n);
 
-int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs */
+int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs; EDGPU_ERR while an
+                                                                       ingest awaits its index */
 
 /* The arrival time (fTimeArrived, OS::Milliseconds() at PushPacket) of each descriptor of
  * the last edgpu_fanout: out[i] for desc[i], i < the tick's relayed packets (serial ticks;

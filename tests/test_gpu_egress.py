@@ -132,3 +132,51 @@ def test_egress_dedup_copies_less_and_reports_dead_peers():
         assert len(sink.tcp[ht[1]][2]) > 0 and all(len(sink.parts[(h, 0, 0)]) > 0 for h in hs)
         sink.close()
         gone[0].close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gso", ["1", "0"])
+def test_udp_overload_loses_datagrams_without_reordering(gso, monkeypatch):
+    """A UDP subscriber that cannot keep up loses datagrams, as RTPStream::Write's ignored
+    SendTo result loses them (RTPStream.cpp:1145).  With GSO (EDGPU_EGRESS_GSO=1, the default)
+    a refused send drops a whole message of up to 64 equal-length datagrams instead of one
+    (include/edgpu.h, egress section); either way what arrives is, per sub-stream, an in-order
+    subset of what the tick sent: no reordering, no duplicates."""
+    import socket
+    from easydarwin_amd import edgpu
+    from easydarwin_amd.egress import SocketSink
+    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
+    monkeypatch.setenv("EDGPU_EGRESS_GSO", gso)
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=8_000_000, gop=30, idr_bytes=60_000)]
+    pk = session_packets(tracks, 4000, 0xEA5D + 98)
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(tracks))
+        sink = SocketSink(ctx, threads=2)
+        hs = [ctx.subscriber_add(s, edgpu.TRANSPORT_UDP) for _ in range(3)]
+        for i, h in enumerate(hs):
+            sink.join(h, 200 + i, 1, False)
+            sink.udp[(h, 0, 0)].setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)   # overloads
+        lost = 0
+        for tick in range(1, 5):
+            t = tick * 1000
+            batch = [(s, ch, tt, d) for tt, ch, d in pk if t - 1000 < tt <= t]
+            desc, so, ss, blob = edgpu.build_batch(batch)
+            ctx.ingest_host(desc, so, ss, blob)
+            ctx.keyframe_index()
+            r = ctx.fanout(t)
+            st, subs, dsc, arena = ctx.read_tick(r)
+            sent = {}
+            for q in subs:
+                if int(q["desc_count"]) and int(q["kind"]) == 0:
+                    d = dsc[int(q["desc_base"]):int(q["desc_base"]) + int(q["desc_count"])]
+                    sent[int(q["subscriber"])] = [arena[o:o + n].tobytes() for o, n in zip(d["offset"], d["len"])]
+            before = {h: len(sink.parts[(h, 0, 0)]) for h in hs}
+            sink.tick(r, t)
+            for h in hs:
+                got = [p[2:] for p in sink.parts[(h, 0, 0)][before[h]:]]
+                want = sent.get(h, [])
+                it = iter(want)
+                assert all(any(g == w for w in it) for g in got), f"tick {t} handle {h}: reordered or duplicated"
+                lost += len(want) - len(got)
+        assert lost > 0, "the receivers kept up: the test did not overload them"
+        sink.close()
