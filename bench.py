@@ -309,7 +309,10 @@ def main():
         raise SystemExit(f"EDGPU_BENCH_BACKEND={backend}: nccl or gloo")
     if backend == "gloo":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    # EDGPU_BENCH_FORCE_PG=1: the process group (RCCL, barriers, the device-side reduction) even at
+    # world size 1 -- the driver's N-rank code path exercised on a one-GPU box
+    force_pg = os.environ.get("EDGPU_BENCH_FORCE_PG") == "1"
+    if world > 1 or force_pg:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -400,7 +403,8 @@ def main():
     launches = c1["fanout_launches"] - c0["fanout_launches"]
     alg_bytes = out_bytes + in_bytes + 16 * relayed      # SURVEY.md §8.d per-launch definition
 
-    dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None)
+    dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None,
+                                          force=force_pg)
 
     if rank != 0:
         if dist:
@@ -459,7 +463,8 @@ def main():
                    "rewrite": rewrite_desc,
                    "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"
-                                  + ("" if backend == "nccl" or world == 1 else f" ({backend} rehearsal, ranks sharing GPUs)")},
+                                  + ("" if backend == "nccl" or world == 1 else f" ({backend} rehearsal, ranks sharing GPUs)"),
+                   "process_group": (backend if dist else None)},
         "relayed_GBps": round(out_all / dt / 1e9, 2),
         **({"pcie_H2D_GBps": round(sum(batches[i]["bytes"] + 16 * batches[i]["n"] for i in range(warm, warm + steps))
                                    / dt / 1e9, 2)} if args.ingest == "host" else {}),

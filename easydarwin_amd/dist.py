@@ -22,9 +22,10 @@ def env_world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def reduce_run(elapsed_s: float, counts: list, device=None):
-    """max of elapsed over ranks, sum of counts over ranks (whole-node throughput)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+def reduce_run(elapsed_s: float, counts: list, device=None, force: bool = False):
+    """max of elapsed over ranks, sum of counts over ranks (whole-node throughput).  force: run
+    the collectives even at world size 1 (exercises the RCCL path on one GPU)."""
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size() == 1 and not force):
         return elapsed_s, list(counts)
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
     c = torch.tensor([float(x) for x in counts], dtype=torch.float64, device=device)

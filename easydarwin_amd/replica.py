@@ -80,3 +80,62 @@ class ReplicaLink:
             k += n
         self.bytes_shipped += total
         return total
+
+
+class DistReplicaLink:
+    """The one-process-per-GPU form of ReplicaLink: the owner of global session g is rank
+    ``dist.owner(g, world)``; a rank that serves subscribers of a session it does not own keeps
+    a replica of it, and every ``sync`` round moves full images (first time) or deltas from the
+    owners with ``dist.exchange_images`` (RCCL point-to-point under the nccl backend, device
+    buffers; gloo in CPU-side tests, host buffers).  Every rank calls ``sync`` at the same
+    points (it is collective)."""
+
+    def __init__(self, ctx: edgpu.Context, world: int, rank: int, comm: str = "cuda"):
+        import torch
+        self.torch = torch
+        self.ctx, self.world, self.rank = ctx, world, rank
+        self.comm = comm                              # "cuda": RCCL device buffers; "cpu": gloo
+        self.local_of: dict[int, int] = {}            # owned global session -> engine session
+        self.replica_of: dict[int, int] = {}          # replicated global session -> engine session
+        self.heads: dict[tuple[int, int], np.ndarray] = {}   # (global session, dst rank) -> heads
+        self.bytes_sent = self.bytes_received = 0
+
+    def own(self, g: int, local: int):
+        self.local_of[int(g)] = int(local)
+
+    def want(self, g: int, sdp: str, udp_push: bool = False) -> int:
+        """Creates the replica of global session g here; its first sync brings the full image."""
+        rs = self.ctx.session_add(sdp, udp_push)
+        self.replica_of[int(g)] = rs
+        return rs
+
+    def _export(self, sessions, dst_rank, now_ms):
+        local = [self.local_of[g] for g in sessions]
+        nsnd = [self.ctx.senders_of([s]) for s in local]
+        since = np.concatenate([self.heads.get((g, dst_rank), np.full(n, edgpu.IMAGE_FULL, dtype=np.uint64))
+                                for g, n in zip(sessions, nsnd)])
+        offsets, _ = self.ctx.session_export(local, now_ms, since=since)              # size query
+        total = int(offsets[-1])
+        dev = self.torch.empty(max(total, 16), dtype=self.torch.uint8, device="cuda")
+        self.torch.cuda.synchronize()
+        offsets, heads = self.ctx.session_export(local, now_ms, dev.data_ptr(), dev.numel(), since=since)
+        k = 0
+        for g, n in zip(sessions, nsnd):
+            self.heads[(g, dst_rank)] = heads[k:k + n].copy()
+            k += n
+        return (dev if self.comm == "cuda" else dev.cpu()), offsets
+
+    def _import(self, buf, offsets, sessions, src_rank):
+        dev = buf if buf.is_cuda else buf.cuda()
+        self.torch.cuda.synchronize()
+        self.ctx.session_import(dev.data_ptr(), offsets, [self.replica_of[g] for g in sessions])
+
+    def sync(self, now_ms: int):
+        from .dist import exchange_images
+        sent, recv = exchange_images(
+            sorted(self.replica_of), lambda s, r: self._export(s, r, now_ms), self._import,
+            lambda n: self.torch.empty(n, dtype=self.torch.uint8, device="cuda" if self.comm == "cuda" else "cpu"),
+            self.world, self.rank)
+        self.bytes_sent += sent
+        self.bytes_received += recv
+        return sent, recv
