@@ -16,6 +16,7 @@ All W+K input batches are generated and made resident in HBM before timing.  Lau
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -419,8 +420,10 @@ def main():
     rewrite_desc = ("SSRC override with the stream's own SSRC (diagnostic: patch path, identity bytes)"
                     if args.rewrite_same_ssrc else
                     "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)")
-    pmc = os.path.join(ROOT, "profiles", "pmc_fanout_c2.json")
-    if os.path.exists(pmc) and world == 1:
+    ing_traffic = None
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_fanout_c2*.json"))):
+        if world != 1:
+            break
         try:
             pj = json.load(open(pmc))
             wl = pj.get("workload", {})
@@ -429,9 +432,25 @@ def main():
                     and wl.get("tick_ms", 1000) == args.tick_ms
                     and wl.get("rewrite", "identity (reference parity mode)") == rewrite_desc):
                 traffic = pj.get("hbm_bytes_per_launch")
+                ing_traffic = pj.get("ingest_hbm_bytes_per_launch")
                 traffic_source = f"profiles/{pj.get('tag')}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes)"
+                break
         except Exception:
             traffic = None
+    # the ingest side of a step (k_ingest, + the deframe kernels for RTSP-interleaved reads):
+    # algorithmic bytes = packet bytes read (slots of the batch blob + 16-B descriptors, or the
+    # '$'-framed TCP bytes) + slots written + 32-B packet metadata written
+    timed = batches[warm:warm + steps]
+    npk = float(np.mean([bt["n"] for bt in timed]))
+    slot_b = float(np.mean([bt["bytes"] for bt in timed]))
+    read_b = float(np.mean([bt["raw_bytes"] for bt in timed])) if args.ingest == "tcp" else slot_b + 16 * npk
+    ing_alg = read_b + slot_b + 32 * npk
+    ing_ms = float(np.mean(k_ing)) if k_ing else float("nan")
+    ing_ach = ing_alg / (ing_ms / 1e3) / 1e9
+    ingest = {"kernels": "k_ingest + k_tcp_* deframe" if args.ingest == "tcp" else "k_ingest",
+              "alg_bytes_per_launch": int(ing_alg), "avg_ms": round(ing_ms, 4), "achieved": round(ing_ach, 1),
+              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ing_ach / HBM_PEAK_GBS, 4),
+              "traffic": ing_traffic, "traffic_source": traffic_source if ing_traffic else None}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline_reference(args)
@@ -476,6 +495,7 @@ def main():
                       "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,
                       "ingest": round(float(np.mean(k_ing)), 4) if k_ing else None,
                       "keyframe_index": round(float(np.mean(k_key)), 4) if k_key else None},
+        "ingest": ingest,
         "cpu_baseline": cpu,
     }
     print(json.dumps(res), flush=True)

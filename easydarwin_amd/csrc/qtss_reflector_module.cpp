@@ -186,6 +186,7 @@ struct Module {
     std::thread ticker, reader;
     std::atomic<bool> stop{false};
     QTSS_Error tickErr = QTSS_NoErr;
+    EDGPU_QTSSTickInfo lastTick{};      // guarded by mu
 };
 Module* M = nullptr;
 
@@ -399,11 +400,18 @@ void ReaderLoop() {
 }
 
 QTSS_Error Tick() {
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(M->mu);
     if (!M->R) return QTSS_RequestFailed;
     QTSSSink sink;
     sink.now = Milliseconds();
     const int err = M->R->ReflectPackets(sink.now, &sink);
+    const edgpu_reflector::Reflector::TickInfo& t = M->R->LastTick();
+    EDGPU_QTSSTickInfo& o = M->lastTick;
+    o.ingested_packets = t.ingested_packets; o.ingested_bytes = t.ingested_bytes;
+    o.readback_bytes = t.readback_bytes; o.arena_bytes = t.arena_bytes; o.writes = t.writes;
+    o.ingest_ms = t.ingest_ms; o.fanout_ms = t.fanout_ms; o.readback_ms = t.readback_ms; o.write_ms = t.write_ms;
+    o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return err == 0 ? QTSS_NoErr : QTSS_RequestFailed;
 }
 
@@ -441,6 +449,11 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
     edgpu_config cfg;
     edgpu_config_default(&cfg);
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
+    // capacities for large fleets (edgpu_config; 0 / unset: the engine defaults): the fan-out
+    // arena and descriptors of one tick, the ingest batch of one tick
+    if (const char* v = getenv("EDGPU_QTSS_ARENA_MB")) cfg.out_arena_bytes = (uint64_t)atoll(v) << 20;
+    if (const char* v = getenv("EDGPU_QTSS_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)atoll(v);
+    if (const char* v = getenv("EDGPU_QTSS_MAX_BATCH_PACKETS")) cfg.max_batch_packets = (uint32_t)atoll(v);
     // 0 selects the engine's default of 1 s (edgpu_config.reflector_buffer_size_sec)
     M->overBufferMs = (int64_t)(cfg.reflector_buffer_size_sec ? cfg.reflector_buffer_size_sec : 1) * 1000;
     M->R.reset(new edgpu_reflector::Reflector(&cfg));
@@ -903,6 +916,13 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
 
 // Manual mode (EDGPU_QTSS_MANUAL_TICK=1, no reader thread): read every datagram waiting on the
 // UDP push sockets now; returns how many were handed to the engine.
+extern "C" QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out) {
+    if (!M || !out) return QTSS_BadArgument;
+    std::lock_guard<std::mutex> g(M->mu);
+    *out = M->lastTick;
+    return QTSS_NoErr;
+}
+
 extern "C" uint32_t EDGPU_QTSSReflectorModule_PollUDP(void) {
     if (!M) return 0;
     return DrainUDP();

@@ -219,6 +219,23 @@ edqtss::QTSS_Error QTSSReflectorModule_Main(void* inPrivateArgs);
  * It stands in for the ReflectorSocket tasks that run ReflectPackets in the reference
  * (ReflectorStream.cpp:1676-1714).  Returns a QTSS_Error. */
 edqtss::QTSS_Error EDGPU_QTSSReflectorModule_Tick(void);
+
+/* Engine extension, manual mode: reads every datagram waiting on the UDP push sockets now (the
+ * reader thread's work, ReflectorSocket::GetIncomingData, ReflectorStream.cpp:1716-1735);
+ * returns how many were handed to the engine. */
+uint32_t EDGPU_QTSSReflectorModule_PollUDP(void);
+
+/* Engine extension: measurements of the last tick (tools/qtss_replay --bench).  hold_ms is how
+ * long the tick held the module's session lock (RTSP roles wait that long; the pushers' ingest
+ * never does); readback_bytes is what crossed PCIe back (the tick's distinct bytes, descriptors
+ * and sub-stream table) against arena_bytes, the write-many output on the GPU. */
+typedef struct EDGPU_QTSSTickInfo {
+    uint64_t ingested_packets, ingested_bytes;
+    uint64_t readback_bytes, arena_bytes;
+    uint64_t writes;                    /* QTSS_Write calls */
+    double   ingest_ms, fanout_ms, readback_ms, write_ms, hold_ms;
+} EDGPU_QTSSTickInfo;
+edqtss::QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out);
 }
 
 #endif /* EDGPU_QTSS_MODULE_ABI_H */

@@ -560,12 +560,13 @@ SCENARIOS = {
 }
 
 
-def random_scenario(seed: int) -> Trace:
+def random_scenario(seed: int, lifecycle: bool = True) -> Trace:
     """A random mix of everything above, for differential tests on fresh inputs (the oracle
     pins itself on the fixtures; these traces are not committed): 1-3 sessions, each an
     RTSP-interleaved or a UDP push of H.264 / MPEG-4 / MJPEG video and/or AAC / G.711 audio,
     pusher SRs, jittered sizes; UDP, TCP and RTP-Info players joining at random times; random
-    leaves; random socket budgets (BLOCK) on TCP and UDP sub-streams; ticks every 50-200 ms.
+    leaves; random socket budgets (BLOCK) on TCP and UDP sub-streams; ticks every 50-200 ms;
+    pushers leaving and returning (PUBLISH / UNPUBLISH, with and without kill_clients).
     Kept inside the parity scope of DESIGN.md §4.4 (no lag past the 10-s retention)."""
     rng = np.random.Generator(np.random.PCG64(SEED_BASE + 1000 + seed))
     vids = ["H264/90000", "H264/90000", "MP4V-ES/90000", "JPEG/90000"]
@@ -613,4 +614,23 @@ def random_scenario(seed: int) -> Trace:
                         blocks.setdefault(tt, []).append((sub, int(rng.integers(0, ntr)), int(rng.integers(0, 2)),
                                                           int(rng.integers(0, 5))))
             sub += 1
-    return _assemble(tr, per, tick, dur, joins, blocks=blocks, leaves=leaves)
+    # session lifecycle, from its own generator (the traces above stay as they were): a pusher
+    # leaving (with or without kill_clients) and often coming back; its packets in between are
+    # dropped; sometimes a duplicate PUBLISH or UNPUBLISH
+    pubs = []
+    if lifecycle:
+        lrng = np.random.Generator(np.random.PCG64(SEED_BASE + 3000 + seed))
+        for s in range(nsess):
+            if lrng.random() >= 0.35:
+                continue
+            t1 = int(lrng.integers(200, max(dur - 400, 201)))
+            pubs.append((t1, "unpublish", s, 1 if lrng.random() < 0.4 else 0))
+            if lrng.random() < 0.2:
+                pubs.append((t1 + 10, "unpublish", s, 0))                  # no pusher: no effect
+            if lrng.random() < 0.7:
+                t2 = t1 + int(lrng.integers(50, 1500))
+                if t2 < dur:
+                    pubs.append((t2, "publish", s))
+                    if lrng.random() < 0.2:
+                        pubs.append((t2 + 10, "publish", s))            # duplicate: refused
+    return _assemble(tr, per, tick, dur, joins, blocks=blocks, leaves=leaves, pubs=pubs)

@@ -21,7 +21,9 @@ def _run(binary, trace, tmp_path, tag):
 def test_restatement_matches_reference_on_random_traces(seed, oracle_bins, tmp_path):
     if oracle_bins["ref"] is None:
         pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")
-    trace = random_scenario(seed).to_bytes()
+    tr = random_scenario(seed)
+    trace = tr.to_bytes()
     ref = _run(oracle_bins["ref"], trace, tmp_path, "ref")
     port = _run(oracle_bins["port"], trace, tmp_path, "port")
-    assert len(ref) > 16 and port == ref
+    # a trace whose only session ended before any player joined has an empty capture
+    assert port == ref and (len(ref) > 16 or tr.has_lifecycle)

@@ -48,8 +48,18 @@
 // trace's TICKs are not used.  For traces whose per-sub-stream bytes do not depend on tick
 // timing (tests/scenarios.py threaded).
 //
+// --bench <sessions> <subs> <seconds> [tick_ms] [pusher_threads]: the drop-in's throughput at a
+// BASELINE config C2-like load, no trace: `sessions` RTSP-interleaved H.264 1080p30 4 Mb/s
+// pushers (SPS / PPS / 120 KB IDR every 2 s, P frames for the rest, FU-A at 1400 B) generated
+// here, `subs` UDP players each, QTSS_Write sinks that only count; per tick the pusher threads
+// feed the frames of the tick interval through RTSPIncomingData, then the host ticks the module
+// (manual mode).  Prints one JSON line: relayed packets/s over push + tick time, and per tick the
+// module's lock hold, GPU, readback and write times and the PCIe bytes read back against the
+// write-many arena (EDGPU_QTSSReflectorModule_LastTick).
+//
 // Test infrastructure (tests/test_gpu_qtss_module.py, tests/test_qtss_abi.py); not shipped.
 // Usage: qtss_replay <module.so> <trace.edtr> <capture.edcp> [--threaded]
+//        qtss_replay <module.so> --bench <sessions> <subs> <seconds> [tick_ms] [pusher_threads]
 //        qtss_replay <module.so> --register      (Register role only; no GPU needed)
 #include <arpa/inet.h>
 #include <dlfcn.h>
@@ -165,8 +175,16 @@ static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* bu
 }
 // QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
 static uint64_t g_writes = 0;
+static bool g_count_only = false;                    // --bench: sinks count, no capture
+static uint64_t g_write_bytes = 0;
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
+    if (g_count_only) {
+        g_writes++;
+        g_write_bytes += len;
+        if (outLen) *outLen = len;
+        return QTSS_NoErr;
+    }
     const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (!(flags & (qtssWriteFlagsIsRTP | qtssWriteFlagsIsRTCP)) || !(flags & qtssWriteFlagsWriteBurstBegin)) {
         fprintf(stderr, "QTSS_Write on an RTP stream without RTP/RTCP + burst flags (0x%x)\n", flags);
@@ -315,6 +333,133 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     return e;
 }
 
+// ---- --bench ---------------------------------------------------------------------------------
+struct Pusher {                                        // one synthetic H.264 push (one track)
+    uint32_t seq = 0, ts = 0, ssrc = 0, frame = 0;
+};
+static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
+                     QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
+    (void)poll_fn;
+    if (argc < 6) { fprintf(stderr, "--bench <sessions> <subs> <seconds> [tick_ms] [threads]\n"); return 2; }
+    const uint32_t nsess = (uint32_t)atoi(argv[3]), nsub = (uint32_t)atoi(argv[4]);
+    const double seconds = atof(argv[5]);
+    const uint32_t tick_ms = argc > 6 ? (uint32_t)atoi(argv[6]) : 100;
+    const uint32_t nthreads = argc > 7 ? (uint32_t)atoi(argv[7]) : 4;
+    const std::string sdp = "v=0\r\no=- 0 0 IN IP4 127.0.0.1\r\ns=EasyPusher\r\nc=IN IP4 127.0.0.1\r\nt=0 0\r\n"
+                            "m=video 0 RTP/AVP 96\r\na=rtpmap:96 H264/90000\r\na=control:trackID=1\r\n";
+    g_count_only = true;
+    std::vector<Obj*> rtsp(nsess), client(nsess);
+    const auto s0 = std::chrono::steady_clock::now();
+    for (uint32_t s = 0; s < nsess; s++) {
+        const std::string path = "/live/bench" + std::to_string(s) + ".sdp";
+        rtsp[s] = new_obj(qtssRTSPSessionObjectType);
+        client[s] = new_obj(qtssClientSessionObjectType);
+        g_rtsp_of_client[client[s]] = rtsp[s];
+        if (request(rtsp[s], client[s], qtssAnnounceMethod, path, "", 0, qtssRTPTransportTypeTCP, sdp) ||
+            request(rtsp[s], client[s], qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModeRecord,
+                    qtssRTPTransportTypeTCP) ||
+            request(rtsp[s], client[s], qtssRecordMethod, path, "", qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
+            { fprintf(stderr, "bench: push setup failed\n"); return 3; }
+        for (uint32_t k = 0; k < nsub; k++) {
+            Obj* pr = new_obj(qtssRTSPSessionObjectType);
+            Obj* pc = new_obj(qtssClientSessionObjectType);
+            g_rtsp_of_client[pc] = pr;
+            if (request(pr, pc, qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModePlay, qtssRTPTransportTypeUDP) ||
+                request(pr, pc, qtssPlayMethod, path, "", qtssRTPTransportModePlay, qtssRTPTransportTypeUDP))
+                { fprintf(stderr, "bench: player setup failed\n"); return 3; }
+        }
+    }
+    const double setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+    // payload pool: random bytes, NAL / FU headers written per packet
+    std::vector<uint8_t> pool(1 << 20);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto& b : pool) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; b = (uint8_t)x; }
+    std::vector<Pusher> ps(nsess);
+    for (uint32_t s = 0; s < nsess; s++) { ps[s].seq = s * 7919u; ps[s].ts = s * 104729u; ps[s].ssrc = 0x10000000u + s; }
+    const uint32_t fps = 30, gop = 60, idr = 120000, p_frame = (4000000 / 8 * 2 - idr) / (gop - 1), mtu = 1400;
+    auto push_frame = [&](uint32_t s, std::vector<char>& fr, int64_t t) {
+        Pusher& P = ps[s];
+        auto one = [&](const uint8_t* hdr, uint32_t nh, uint32_t body, bool marker) {
+            const uint32_t len = 12 + nh + body;
+            fr[0] = '$'; fr[1] = 0; fr[2] = (char)(len >> 8); fr[3] = (char)len;
+            uint8_t* p = (uint8_t*)&fr[4];
+            p[0] = 0x80; p[1] = (uint8_t)(96 | (marker ? 0x80 : 0));
+            p[2] = (uint8_t)(P.seq >> 8); p[3] = (uint8_t)P.seq;
+            p[4] = (uint8_t)(P.ts >> 24); p[5] = (uint8_t)(P.ts >> 16); p[6] = (uint8_t)(P.ts >> 8); p[7] = (uint8_t)P.ts;
+            p[8] = (uint8_t)(P.ssrc >> 24); p[9] = (uint8_t)(P.ssrc >> 16); p[10] = (uint8_t)(P.ssrc >> 8); p[11] = (uint8_t)P.ssrc;
+            memcpy(p + 12, hdr, nh);
+            memcpy(p + 12 + nh, &pool[(P.seq * 1031u) % (pool.size() - 2048)], body);
+            P.seq++;
+            QTSS_RoleParams rp;
+            memset(&rp, 0, sizeof(rp));
+            rp.rtspIncomingDataParams.inRTSPSession = rtsp[s];
+            rp.rtspIncomingDataParams.inClientSession = client[s];
+            rp.rtspIncomingDataParams.inPacketData = fr.data();
+            rp.rtspIncomingDataParams.inPacketLen = len + 4;
+            advance_clock(t);
+            (void)g_dispatch(QTSS_RTSPIncomingData_Role, &rp);
+        };
+        auto nal = [&](uint8_t h, uint32_t n, bool last) {     // single NAL or FU-A fragments
+            if (12 + n <= mtu) { one(&h, 1, n - 1, last); return; }
+            uint32_t off = 0, body = n - 1;
+            while (off < body) {
+                const uint32_t k = std::min(mtu - 14, body - off);
+                const uint8_t fu[2] = {(uint8_t)((h & 0xE0) | 28),
+                                       (uint8_t)((off == 0 ? 0x80 : 0) | (off + k >= body ? 0x40 : 0) | (h & 0x1F))};
+                one(fu, 2, k, last && off + k >= body);
+                off += k;
+            }
+        };
+        if (P.frame % gop == 0) { nal(0x67, 24, false); nal(0x68, 8, false); nal(0x65, idr, true); }
+        else nal(0x41, p_frame, true);
+        P.frame++;
+        P.ts += 90000 / fps;
+    };
+    const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
+    double push_s = 0, tick_s = 0, hold = 0, hold_max = 0, gpu = 0, rb = 0, wr = 0, ing = 0;
+    uint64_t rb_bytes = 0, arena = 0, ingested = 0, writes0 = 0, timed_ticks = 0;
+    const uint32_t warm = std::min<uint32_t>(3, nticks / 4);
+    for (uint32_t k = 0; k < nticks; k++) {
+        const int64_t t_end = (int64_t)(k + 1) * tick_ms;
+        auto a = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (uint32_t w = 0; w < nthreads; w++)
+            th.emplace_back([&, w]() {
+                std::vector<char> fr(2100);
+                for (uint32_t s = w; s < nsess; s += nthreads)
+                    while ((int64_t)ps[s].frame * 1000 / fps < t_end) push_frame(s, fr, (int64_t)ps[s].frame * 1000 / fps);
+            });
+        for (auto& t : th) t.join();
+        advance_clock(t_end);
+        auto b = std::chrono::steady_clock::now();
+        if (tick_fn()) { fprintf(stderr, "bench: tick failed\n"); return 3; }
+        auto c = std::chrono::steady_clock::now();
+        EDGPU_QTSSTickInfo ti;
+        if (last_fn(&ti)) return 3;
+        if (k == warm) writes0 = g_writes;
+        if (k >= warm) {
+            timed_ticks++;
+            push_s += std::chrono::duration<double>(b - a).count();
+            tick_s += std::chrono::duration<double>(c - b).count();
+            hold += ti.hold_ms; hold_max = std::max(hold_max, ti.hold_ms);
+            gpu += ti.fanout_ms; rb += ti.readback_ms; wr += ti.write_ms; ing += ti.ingest_ms;
+            rb_bytes += ti.readback_bytes; arena += ti.arena_bytes; ingested += ti.ingested_packets;
+        }
+    }
+    const uint64_t relayed = g_writes - writes0 + 0;
+    const double n = (double)std::max<uint64_t>(timed_ticks, 1);
+    printf("{\"sessions\": %u, \"subs\": %u, \"tick_ms\": %u, \"pusher_threads\": %u, \"ticks_timed\": %llu, "
+           "\"setup_s\": %.3f, \"relayed_packets\": %llu, \"ingested_packets\": %llu, \"push_s\": %.4f, \"tick_s\": %.4f, "
+           "\"relayed_per_s\": %.1f, \"ingested_per_s\": %.1f, \"per_tick_ms\": {\"hold\": %.3f, \"hold_max\": %.3f, "
+           "\"ingest\": %.3f, \"gpu_fanout\": %.3f, \"readback\": %.3f, \"writes\": %.3f}, "
+           "\"per_tick_bytes\": {\"readback\": %.0f, \"arena\": %.0f}, \"virtual_s\": %.3f}\n",
+           nsess, nsub, tick_ms, nthreads, (unsigned long long)timed_ticks, setup_s, (unsigned long long)relayed,
+           (unsigned long long)ingested, push_s, tick_s, relayed / std::max(push_s + tick_s, 1e-9),
+           ingested / std::max(push_s + tick_s, 1e-9), hold / n, hold_max, ing / n, gpu / n, rb / n, wr / n,
+           rb_bytes / n, arena / n, timed_ticks * tick_ms / 1000.0);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s module.so trace.edtr capture.edcp | module.so --register\n", argv[0]); return 2; }
     void* so = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
@@ -363,15 +508,25 @@ int main(int argc, char** argv) {
         return 0;
     }
     const bool threaded = argc == 5 && strcmp(argv[4], "--threaded") == 0;
-    if (argc != 4 && !threaded) return 2;
+    const bool bench = strcmp(argv[2], "--bench") == 0;
+    if (argc != 4 && !threaded && !bench) return 2;
     if (threaded) {
         setenv("EDGPU_QTSS_MANUAL_TICK", "0", 1);
         if (!getenv("EDGPU_QTSS_TICK_MSEC")) setenv("EDGPU_QTSS_TICK_MSEC", "5", 1);
     } else {
         setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
     }
+    if (bench) setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
     memset(&rp, 0, sizeof(rp));
     if (g_dispatch(QTSS_Initialize_Role, &rp) != QTSS_NoErr) { fprintf(stderr, "Initialize failed (no GPU?)\n"); return 3; }
+    if (bench) {
+        auto last_fn = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
+        if (!last_fn) { fprintf(stderr, "module entry points missing\n"); return 3; }
+        const int rc = run_bench(argc, argv, poll_fn, tick_fn, last_fn);
+        memset(&rp, 0, sizeof(rp));
+        (void)g_dispatch(QTSS_Shutdown_Role, &rp);
+        return rc;
+    }
 
     Reader r;
     FILE* f = fopen(argv[2], "rb");

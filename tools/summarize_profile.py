@@ -53,11 +53,21 @@ res["fanout_kernel"] = fan_name                              # rocprofv3 -T (tru
 res["bench_fanout_kernel"] = bench["roofline"]["kernel"]     # the engine's variant name (template args)
 res["workload"] = {k: bench["config"].get(k) for k in ("sessions_per_gpu", "subs_per_session", "ingest", "tick_ms", "rewrite")}
 res["hbm_bytes_per_launch"] = fan.get("hbm_bytes_per_launch")
+# the ingest side of a step: k_ingest (+ the RTSP-interleaved deframe kernels k_tcp_*)
+ing = [k for k in res["kernels"] if k.startswith("k_ingest") or k.startswith("k_tcp")]
+res["ingest_kernels"] = ing
+res["ingest_hbm_bytes_per_launch"] = sum(res["kernels"][k]["hbm_bytes_per_launch"] for k in ing) if ing else None
+res["ingest_alg_bytes_per_launch"] = bench.get("ingest", {}).get("alg_bytes_per_launch")
 res["alg_bytes_per_launch"] = bench["roofline"]["alg_bytes_per_launch"]
 res["bench_avg_kernel_ms"] = bench["roofline"]["avg_kernel_ms"]
 res["rocprof_avg_kernel_ms"] = (avg_ns.get(fan_name) or 0) / 1e6          # all launches incl. warmup
 res["rocprof_avg_kernel_ms_timed"] = fan.get("avg_duration_ns_rocprof_timed", 0) / 1e6   # the bench's timed steps
 json.dump(res, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+# the registry bench.py reads traffic from: one file per workload (ingest mode, subs, tick, rewrite)
+wl = res["workload"]
+key = f"{wl['ingest']}_s{wl['sessions_per_gpu']}x{wl['subs_per_session']}_t{wl['tick_ms']}" + \
+      ("" if wl.get("rewrite", "identity").startswith("identity") else "_rw")
+json.dump(res, open(os.path.join(prof, f"pmc_fanout_c2_{key}.json"), "w"), indent=1)
 shutil.copy(os.path.join(run, "kt", "kt_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
 shutil.copy(os.path.join(run, "kt_bench.json"), os.path.join(prof, f"{tag}_bench.json"))
 print(json.dumps(res, indent=1))
