@@ -263,13 +263,23 @@ public:
     int WritePacket(uint32_t, uint16_t, bool, bool, const uint8_t*, uint32_t, uint32_t) override {
         return edgpu_reflector::kRequestFailed;                  // Write() below is the entry point
     }
+    // A sub-stream's packets come consecutively: the output and first-new slot found for the
+    // last write serve the next ones (a tick writes millions of packets at fleet scale).
+    uint32_t lastHandle = 0xFFFFFFFFu, lastSender = 0xFFFFFFFFu;
+    Output* lastOut = nullptr;
+    int32_t lastFirst = -1;
+    bool lastHasFirst = false;
     int Write(const edgpu_reflector::PacketWrite& w) override {
-        auto it = M->byHandle.find(w.subscriber);
-        if (it == M->byHandle.end()) {
+        if (w.subscriber != lastHandle) {
+            auto it = M->byHandle.find(w.subscriber);
+            lastHandle = w.subscriber;
+            lastOut = it == M->byHandle.end() ? nullptr : it->second;
+        }
+        if (!lastOut) {
             if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: write for unknown handle %u\n", w.subscriber);
             return edgpu_reflector::kNoErr;
         }
-        Output& o = *it->second;
+        Output& o = *lastOut;
         // not playing (paused): WritePacket returns QTSS_WouldBlock (RTPSessionOutput.cpp:575-579)
         if (o.paused) return edgpu_reflector::kWouldBlock;
         if (w.track >= o.streams.size() || !o.streams[w.track]) {                               // track not SETUP
@@ -279,8 +289,13 @@ public:
         // the server frames interleaved packets itself (RTPStream::Write): hand it the packet
         const uint8_t* pkt = w.interleaved ? w.wire + 4 : w.wire;
         const uint32_t len = w.interleaved ? w.wireLen - 4 : w.wireLen;
-        const auto f = firstNewSlot.find(w.sender);
-        const bool firstPacket = f != firstNewSlot.end() && o.slot >= f->second;
+        if (w.sender != lastSender) {
+            const auto f = firstNewSlot.find(w.sender);
+            lastSender = w.sender;
+            lastHasFirst = f != firstNewSlot.end();
+            lastFirst = lastHasFirst ? f->second : -1;
+        }
+        const bool firstPacket = lastHasFirst && o.slot >= lastFirst;
         // the transmit time (RTPSessionOutput.cpp:603-608): now - bucket delay, moved to the
         // packet's arrival + the output's buffer delay while that delay is positive
         const int64_t bucketDelay = M->bucketDelayMs * (int64_t)(o.slot < 0 ? 0 : (uint32_t)o.slot / M->bucketSize);
