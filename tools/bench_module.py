@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""The drop-in path's throughput: libQTSSReflectorModule.so in the fake QTSS server
+(tools/qtss_replay --bench) at C2 scale, next to the reference reflector on the same host.
+
+Module side: <sessions> RTSP-interleaved H.264 1080p 4 Mb/s pushers (synthetic FU-A packets,
+GOP 60, 120-KB IDR) fed through QTSS_RTSPIncomingData_Role from <threads> pusher threads,
+<subs> UDP players per session, manual ticks every <tick_ms> of virtual time; the QTSS_Write
+sink counts.  Reported: relayed packets/s over push + tick wall time, per-tick module-lock
+hold, engine ingest / fan-out / readback / QTSS_Write time, readback (PCIe) bytes per tick
+against the fan-out arena bytes per tick (what a whole-arena readback would move).
+
+Reference side: oracle/_ref/ref_harness --bench (EasyDarwin's reflector compiled from its
+sources, memcpy sinks) on bench.py's bounded sample (64 sessions x <subs> x 3 s at the same
+tick), sessions sharded over one process per core (bench.py _reference_replay).
+
+Prints one JSON object.  Needs a GPU (the module initialises an edgpu context).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def module_run(args) -> dict:
+    env = dict(os.environ)
+    # one tick carries every session's IDR at once (all GOPs start together): 1024 x 16 x ~150 KB
+    env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
+    env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
+    cmd = [os.path.join(ROOT, "tools", "qtss_replay"), os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"),
+           "--bench", str(args.sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
+    if r.returncode:
+        raise SystemExit(f"qtss_replay --bench failed ({r.returncode}): {r.stderr.strip()[-400:]}")
+    return json.loads(r.stdout)
+
+
+def reference_run(args) -> dict | None:
+    sys.path.insert(0, ROOT)
+    import bench
+    procs_n = min(16, os.cpu_count() or 1)
+    r = bench._reference_replay(argparse.Namespace(subs=args.subs), args.tick_ms, procs_n)
+    if r is None:
+        return None
+    pk, by, secs, rep = r
+    return {"relayed_per_s": round(pk / secs, 1), "cores": procs_n, "relayed_packets": pk, "seconds": round(secs, 3),
+            "sample": f"oracle/_ref/ref_harness --bench: 64 sessions x {args.subs} UDP subs x 3 s at {args.tick_ms}-ms "
+                      f"ticks, sharded over {procs_n} processes, {rep} replays each (memcpy sinks)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sessions", type=int, default=1024)
+    ap.add_argument("--subs", type=int, default=16)
+    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--tick-ms", type=int, default=100)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--arena-mb", type=int, default=4096)
+    ap.add_argument("--max-out-packets", type=int, default=4 << 20)
+    ap.add_argument("--timeout", type=int, default=300)
+    ap.add_argument("--no-reference", action="store_true")
+    args = ap.parse_args()
+    out = {"workload": f"C2 through the QTSS module: {args.sessions} RTSP-interleaved H.264 pushers x {args.subs} "
+                       f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads",
+           "module": module_run(args)}
+    m = out["module"]
+    pt = m["per_tick_bytes"]
+    out["readback_vs_arena"] = round(pt["readback"] / pt["arena"], 4) if pt["arena"] else None
+    if not args.no_reference:
+        out["reference"] = reference_run(args)
+        if out["reference"]:
+            out["module_vs_reference"] = round(m["relayed_per_s"] / out["reference"]["relayed_per_s"], 2)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

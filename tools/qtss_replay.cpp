@@ -333,6 +333,8 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     return e;
 }
 
+static void* g_so = nullptr;                         // the module (and, through it, libedgpu)
+
 // ---- --bench ---------------------------------------------------------------------------------
 struct Pusher {                                        // one synthetic H.264 push (one track)
     uint32_t seq = 0, ts = 0, ssrc = 0, frame = 0;
@@ -340,6 +342,8 @@ struct Pusher {                                        // one synthetic H.264 pu
 static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
                      QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
     (void)poll_fn;
+    // the engine's message for a failed tick (libedgpu is a dependency of the module)
+    auto last_error = (const char* (*)(void))dlsym(g_so, "edgpu_last_error");
     if (argc < 6) { fprintf(stderr, "--bench <sessions> <subs> <seconds> [tick_ms] [threads]\n"); return 2; }
     const uint32_t nsess = (uint32_t)atoi(argv[3]), nsub = (uint32_t)atoi(argv[4]);
     const double seconds = atof(argv[5]);
@@ -432,7 +436,10 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         for (auto& t : th) t.join();
         advance_clock(t_end);
         auto b = std::chrono::steady_clock::now();
-        if (tick_fn()) { fprintf(stderr, "bench: tick failed\n"); return 3; }
+        if (const QTSS_Error e = tick_fn()) {
+            fprintf(stderr, "bench: tick %u failed (%d): %s\n", k, (int)e, last_error ? last_error() : "?");
+            return 3;
+        }
         auto c = std::chrono::steady_clock::now();
         EDGPU_QTSSTickInfo ti;
         if (last_fn(&ti)) return 3;
@@ -464,6 +471,7 @@ int main(int argc, char** argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s module.so trace.edtr capture.edcp | module.so --register\n", argv[0]); return 2; }
     void* so = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
     if (!so) { fprintf(stderr, "dlopen: %s\n", dlerror()); return 3; }
+    g_so = so;
     auto main_fn = (QTSS_Error (*)(void*))dlsym(so, "QTSSReflectorModule_Main");
     auto tick_fn = (QTSS_Error (*)(void))dlsym(so, "EDGPU_QTSSReflectorModule_Tick");
     auto poll_fn = (uint32_t (*)(void))dlsym(so, "EDGPU_QTSSReflectorModule_PollUDP");
