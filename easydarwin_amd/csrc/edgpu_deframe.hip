@@ -520,7 +520,14 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
     __shared__ uint32_t s_m;
     __shared__ uint64_t s_next;
     __shared__ uint64_t s_stage;           // stream position of a frame to stage, ~0: none
+    // the session's read starts and arrivals (up to 64 reads) in LDS: a frame's read is found by
+    // a binary search there instead of a chain of dependent global loads
+    __shared__ uint64_t s_rstart[64];
+    __shared__ int64_t s_rarr[64];
+    const bool lds_reads = G.nreads <= 64;
+    if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
     if (lane == 0) s_stage = ~0ull;
+    __syncthreads();
     const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
     const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
     uint32_t done = 0;
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
             int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (rd[mid].start <= last) lo = mid; else hi = mid - 1;
+                if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
             }
             const uint32_t fi = G.frame_base + R.fbase + done + lane;
             edgpu_pkt_desc d;
@@ -562,7 +569,7 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
             d.len = (uint16_t)(flen - 4);
             d.channel = (uint8_t)tbyte(v, p + 1);
             d.flags = 0;
-            d.arrival_ms = rd[lo].arrival;
+            d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
             P.desc[fi] = d;
             const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
             if (p < v.clen) s_stage = p;

@@ -170,10 +170,55 @@ __device__ __forceinline__ void tcp_slot_copy(uint32_t n, const uint32_t* p_slot
     }
 }
 
+// Lane l's 16 frame bytes at offset 4Q + r of (its aligned block `a`, lane l + 1's block);
+// lane 63 takes the next round's first block `last`.  The word offset Q is a template argument
+// (the caller branches on it once per frame: it is wave-uniform), so only the Q + 1 dwords that
+// cross into the next lane move by DPP (wave_shl:1) and each output dword is one alignbyte --
+// no per-dword select among the four word offsets.
+template <uint32_t Q>
+__device__ __forceinline__ u32x4 funnel_next(u32x4 a, u32x4 last, uint32_t r) {
+    const uint32_t aa[4] = {a.x, a.y, a.z, a.w}, la[4] = {last.x, last.y, last.z, last.w};
+    uint32_t d[8] = {a.x, a.y, a.z, a.w, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k <= Q; k++)
+        d[4 + k] = (uint32_t)__builtin_amdgcn_update_dpp((int)la[k], (int)aa[k], 0x130, 0xF, 0xF, false);
+    return u32x4{__builtin_amdgcn_alignbyte(d[Q + 1], d[Q], r), __builtin_amdgcn_alignbyte(d[Q + 2], d[Q + 1], r),
+                 __builtin_amdgcn_alignbyte(d[Q + 3], d[Q + 2], r), __builtin_amdgcn_alignbyte(d[Q + 4], d[Q + 3], r)};
+}
+
+// One frame's slot words out of its aligned blocks b[k] (block lane + 64k; b3 = block 192):
+// rounds past the slot are skipped (uniform), and only the round holding the frame's end clears
+// the bytes past it.  Slot word w goes to ring word (w0 + w) & wm.
+template <uint32_t Q>
+__device__ __forceinline__ void tcp_frame_store(const u32x4 (&b)[3], u32x4 b3, uint32_t r, uint32_t fl, uint32_t nw,
+                                                u32x4* ring, uint64_t w0, uint32_t wm, int lane) {
+    auto lane0 = [](u32x4 v) {
+        return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                     (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+    };
+    const uint32_t lastk = (nw - 1) >> 6;                      // the round holding the slot's end
+    const uint32_t base = (uint32_t)w0 + (uint32_t)lane;      // wm < 2^32: low words suffice
+    const int rem = (int)fl - 16 * lane;                        // frame bytes from word `lane`
+    u32x4 v0 = funnel_next<Q>(b[0], lane0(b[1]), r);
+    if (lane == 0) v0.x = slot_header(fl - 4u);
+    if (lastk == 0) v0 = keep16(v0, rem);
+    if ((uint32_t)lane < nw) ring[base & wm] = v0;
+    if (lastk >= 1) {
+        u32x4 v1 = funnel_next<Q>(b[1], lane0(b[2]), r);
+        if (lastk == 1) v1 = keep16(v1, rem - 1024);
+        if ((uint32_t)lane + 64 < nw) ring[(base + 64) & wm] = v1;
+    }
+    if (lastk >= 2) {
+        const u32x4 v2 = keep16(funnel_next<Q>(b[2], b3, r), rem - 2048);
+        if ((uint32_t)lane + 128 < nw) ring[(base + 128) & wm] = v2;
+    }
+}
+
 // tcp_slot_copy with the per-frame state in SGPRs: a frame's slot size, length and source
 // address are uniform across the wave (readfirstlane), and the one block past lane 63's second
 // round (block 192, needed by lane 63 of round 2 only) is a scalar load.  Fewer VGPRs per frame
-// in flight (12 instead of 16 + 3), so more frames per round fit the occupancy.
+// in flight (12 instead of 16 + 3), so more frames per round fit the occupancy.  The stores go
+// through tcp_frame_store, specialised on the frame's word offset.
 // (EDGPU_INGEST_TCP=3: two frames per round, 4: four.)
 template <uint32_t TD, int THREADS>
 __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_slotb, const uint64_t* p_src,
@@ -182,10 +227,6 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
     typedef __attribute__((address_space(4))) const u32x4 cu32x4;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr uint32_t kW = THREADS / 64;
-    auto lane0 = [](u32x4 v) {
-        return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
-                     (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
-    };
     auto uni64 = [](uint64_t x) {
         return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32;
@@ -217,15 +258,13 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
             u32x4* ring = reinterpret_cast<u32x4*>(s_ring[s]);
             const uint64_t w0 = p_vb[pd] >> 4;
             const uint32_t wm = s_wmask[s];
-            const uint32_t nw = sb[d] / 16;
-            u32x4 v0 = funnel16(b[d][0], wave_next(b[d][0], lane0(b[d][1])), sh[d]);
-            const u32x4 v1 = funnel16(b[d][1], wave_next(b[d][1], lane0(b[d][2])), sh[d]);
-            const u32x4 v2 = funnel16(b[d][2], wave_next(b[d][2], b3[d]), sh[d]);
-            const int rem = (int)fl[d] - 16 * lane;                         // frame bytes from word `lane`
-            if (lane == 0) v0.x = slot_header(fl[d] - 4u);
-            if ((uint32_t)lane < nw) ring[(w0 + lane) & wm] = keep16(v0, rem);
-            if ((uint32_t)lane + 64 < nw) ring[(w0 + lane + 64) & wm] = keep16(v1, rem - 1024);
-            if ((uint32_t)lane + 128 < nw) ring[(w0 + lane + 128) & wm] = keep16(v2, rem - 2048);
+            const uint32_t nw = sb[d] / 16, r = sh[d] & 3;
+            switch (sh[d] >> 2) {                                        // uniform: one scalar branch
+            case 0: tcp_frame_store<0>(b[d], b3[d], r, fl[d], nw, ring, w0, wm, lane); break;
+            case 1: tcp_frame_store<1>(b[d], b3[d], r, fl[d], nw, ring, w0, wm, lane); break;
+            case 2: tcp_frame_store<2>(b[d], b3[d], r, fl[d], nw, ring, w0, wm, lane); break;
+            default: tcp_frame_store<3>(b[d], b3[d], r, fl[d], nw, ring, w0, wm, lane); break;
+            }
         }
     }
 }

@@ -69,6 +69,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -170,7 +171,7 @@ struct Module {
     bool killClients = false;           // kill_clients_when_broadcast_stops (QRM:476-477)
     // the pushers' path (RTSPIncomingData): module session id -> (engine session, tracks) while a
     // pusher is attached; guarded by routeMu alone
-    std::mutex routeMu;
+    std::shared_mutex routeMu;          // pushers share it; SETUP / session end take it alone
     std::map<uint32_t, std::pair<uint32_t, uint32_t>> route;
     std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
     std::map<uint32_t, Output*> byHandle;
@@ -264,12 +265,22 @@ public:
         return edgpu_reflector::kRequestFailed;                  // Write() below is the entry point
     }
     // A sub-stream's packets come consecutively: the output and first-new slot found for the
-    // last write serve the next ones (a tick writes millions of packets at fleet scale).
-    uint32_t lastHandle = 0xFFFFFFFFu, lastSender = 0xFFFFFFFFu;
-    Output* lastOut = nullptr;
-    int32_t lastFirst = -1;
-    bool lastHasFirst = false;
+    // last write serve the next ones (a tick writes millions of packets at fleet scale).  One
+    // cache per write thread; the tables they read are not modified during the write phase.
+    struct alignas(64) Cache {
+        uint32_t lastHandle = 0xFFFFFFFFu, lastSender = 0xFFFFFFFFu;
+        Output* lastOut = nullptr;
+        int32_t lastFirst = -1;
+        bool lastHasFirst = false;
+    };
+    Cache cache[64];
     int Write(const edgpu_reflector::PacketWrite& w) override {
+        Cache& c = cache[w.worker & 63];
+        uint32_t& lastHandle = c.lastHandle;
+        uint32_t& lastSender = c.lastSender;
+        Output*& lastOut = c.lastOut;
+        int32_t& lastFirst = c.lastFirst;
+        bool& lastHasFirst = c.lastHasFirst;
         if (w.subscriber != lastHandle) {
             auto it = M->byHandle.find(w.subscriber);
             lastHandle = w.subscriber;
@@ -427,6 +438,12 @@ QTSS_Error Tick() {
     o.readback_bytes = t.readback_bytes; o.arena_bytes = t.arena_bytes; o.writes = t.writes;
     o.ingest_ms = t.ingest_ms; o.fanout_ms = t.fanout_ms; o.readback_ms = t.readback_ms; o.write_ms = t.write_ms;
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    o.ticks++;
+    if (err) {
+        // the first failure is logged with the engine's message; later ones are counted
+        if (o.failed_ticks++ == 0) fprintf(stderr, "QTSSReflectorModule: tick failed (%d): %s\n", err, edgpu_last_error());
+        o.last_error = err;
+    }
     return err == 0 ? QTSS_NoErr : QTSS_RequestFailed;
 }
 
@@ -477,6 +494,10 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
         M->R.reset();
         return QTSS_RequestFailed;          // no gfx950 device: fail loudly, no CPU fallback
     }
+    // threads that make a tick's QTSS_Write calls (each player's writes stay on one thread)
+    uint32_t writers = 4;
+    if (const char* v = getenv("EDGPU_QTSS_WRITE_THREADS")) writers = (uint32_t)std::max(1, atoi(v));
+    M->R->SetWriteThreads(writers);
     if (!M->manualTick) {
         M->stop = false;
         M->reader = std::thread(ReaderLoop);
@@ -505,7 +526,7 @@ QTSS_Error Shutdown() {
         M->udp.clear();
     }
     {
-        std::lock_guard<std::mutex> r(M->routeMu);
+        std::lock_guard<std::shared_mutex> r(M->routeMu);
         M->route.clear();
     }
     M->R.reset();
@@ -569,7 +590,7 @@ Session* FindSession(uint32_t id) {
 
 // The pushers' route to the engine (RTSPIncomingData reads it without `mu`).
 void SetRoute(const Session& s, bool on) {
-    std::lock_guard<std::mutex> g(M->routeMu);
+    std::lock_guard<std::shared_mutex> g(M->routeMu);
     if (on) M->route[s.id] = std::make_pair(s.engine, (uint32_t)s.trackIDs.size());
     else M->route.erase(s.id);
 }
@@ -845,7 +866,7 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     // the frame's own length, as the reference reads it; never past the buffer the server gave
     const uint32_t len = std::min<uint32_t>((uint32_t)d[2] << 8 | d[3], p->inPacketLen - 4);
     const int64_t now = Milliseconds();
-    std::lock_guard<std::mutex> g(M->routeMu);
+    std::shared_lock<std::shared_mutex> g(M->routeMu);
     auto it = M->route.find((uint32_t)sid);
     if (!M->R || it == M->route.end()) return QTSS_NoErr;      // no pusher attached any more
     const uint32_t track = channel / 2;

@@ -19,6 +19,7 @@ Reflector::Reflector(const edgpu_config* cfg) {
 }
 
 Reflector::~Reflector() {
+    SetWriteThreads(1);
     if (!fCtx) return;
     (void)edgpu_sync(fCtx);
     for (Batch& b : fBatch)
@@ -91,31 +92,42 @@ int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
 }
 
 // Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
-// filled: the only host copy of the packet.  The pinned blob grows by doubling (a larger buffer,
-// the slots so far copied over); the batch being filled is never one whose DMA may be in flight.
+// filled: the only host copy of the packet.  The slot is reserved under the push lock and the
+// packet copied outside it (`copying` counts copies in flight; a flush or a growth waits for
+// them), so concurrent pushers serialise on a few stores only.  The pinned blob grows by
+// doubling (a larger buffer, the slots so far copied over); the batch being filled is never one
+// whose DMA may be in flight.
 void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
                        int64_t nowMs, const edgpu_udp_source* src) {
-    std::lock_guard<std::mutex> g(fPushMu);
-    if (session >= fTracks.size() || track >= fTracks[session]) return;
-    Batch& b = fBatch[fFill];
     const uint32_t clamped = std::min<uint32_t>(packetLen, 2060);   // bytes past 2060 are never read (Q11)
     const uint64_t slot = (clamped + 4 + 15) & ~15ull;
-    if (b.used + slot > b.cap) {
-        uint64_t cap = std::max<uint64_t>(b.cap ? b.cap * 2 : (4ull << 20), b.used + slot);
-        void* nb = nullptr;
-        if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return;          // out of pinned memory: dropped
-        if (b.used) memcpy(nb, b.blob, b.used);
-        if (b.blob) (void)edgpu_host_free(fCtx, b.blob);
-        b.blob = (uint8_t*)nb;
-        b.cap = cap;
+    Batch* bp;
+    uint8_t* d;
+    {
+        std::lock_guard<std::mutex> g(fPushMu);
+        if (session >= fTracks.size() || track >= fTracks[session]) return;
+        Batch& b = fBatch[fFill];
+        if (b.used + slot > b.cap) {
+            while (b.copying.load(std::memory_order_acquire)) std::this_thread::yield();
+            uint64_t cap = std::max<uint64_t>(b.cap ? b.cap * 2 : (4ull << 20), b.used + slot);
+            void* nb = nullptr;
+            if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return;      // out of pinned memory: dropped
+            if (b.used) memcpy(nb, b.blob, b.used);
+            if (b.blob) (void)edgpu_host_free(fCtx, b.blob);
+            b.blob = (uint8_t*)nb;
+            b.cap = cap;
+        }
+        d = b.blob + b.used;
+        b.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, b.used, packetLen});
+        if (src) b.sources.push_back(*src);
+        b.used += slot;
+        b.copying.fetch_add(1, std::memory_order_relaxed);
+        bp = &b;
     }
-    uint8_t* d = b.blob + b.used;
     memset(d, 0, 4);
     memcpy(d + 4, packet, clamped);
     if (slot > clamped + 4) memset(d + 4 + clamped, 0, slot - clamped - 4);
-    b.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, b.used, packetLen});
-    if (src) b.sources.push_back(*src);
-    b.used += slot;
+    bp->copying.fetch_sub(1, std::memory_order_release);
 }
 
 void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
@@ -160,6 +172,7 @@ int Reflector::FlushIngest() {
         fFill ^= 1;
     }
     Batch& b = *bp;
+    while (b.copying.load(std::memory_order_acquire)) std::this_thread::yield();   // pushers mid-copy
     if (!b.pushed.empty()) {
         // descriptors grouped by session (stable: arrival order within a session); the slots
         // stay where the pushers wrote them
@@ -267,15 +280,55 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     fTick.readback_ms = ms_since(t0);
     t0 = Clock::now();
     sink->BeginTick(subs.data(), (uint32_t)subs.size());
-    // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stops this
-    // output's sub-stream for the tick; the engine then bookmarks the blocked packet
+    WriteJob job;
+    job.subs = subs.data(); job.nsubs = (uint32_t)subs.size();
+    job.desc = d.data(); job.arrival = arrival.empty() ? nullptr : arrival.data();
+    job.sink = sink;
+    job.host = fHostOut;
+    job.regions = &tr;
+    const uint32_t nw = fNumWriters;
+    if (nw == 1) {
+        WriteSubscribers(job, 0, 1);
+    } else {
+        {
+            std::lock_guard<std::mutex> g(fPoolMu);
+            fJob = &job;
+            fJobsLeft = nw - 1;
+            fJobSeq++;
+        }
+        fPoolCv.notify_all();
+        WriteSubscribers(job, 0, nw);
+        std::unique_lock<std::mutex> g(fPoolMu);
+        fPoolDone.wait(g, [&] { return fJobsLeft == 0; });
+        fJob = nullptr;
+    }
+    // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stopped its
+    // sub-stream for the tick; the engine bookmarks the blocked packet (reports in sub-stream order)
     std::vector<edgpu_blocked> blocked;
-    for (uint32_t s = 0; s < (uint32_t)subs.size(); s++) {
-        const edgpu_substream_out& q = subs[s];
-        if (!q.desc_count) continue;
-        const uint8_t* base = tr.at(fHostOut, s);
+    for (uint32_t k = 0; k < nw; k++) {
+        fTick.writes += job.writes[k];
+        if (job.err[k]) return job.err[k];
+        blocked.insert(blocked.end(), job.blocked[k].begin(), job.blocked[k].end());
+    }
+    fTick.write_ms = ms_since(t0);
+    if (blocked.empty()) return kNoErr;
+    std::sort(blocked.begin(), blocked.end(),
+              [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
+    return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
+}
+
+// The writes of the subscribers h with h % nworkers == worker, sub-stream by sub-stream in table
+// order (the order one thread takes): a write that would block stops that sub-stream.
+void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers) {
+    j.writes[worker] = 0;
+    j.err[worker] = kNoErr;
+    j.blocked[worker].clear();
+    for (uint32_t s = 0; s < j.nsubs; s++) {
+        const edgpu_substream_out& q = j.subs[s];
+        if (!q.desc_count || q.subscriber % nworkers != worker) continue;
+        const uint8_t* base = j.regions->at(j.host, s);
         for (uint32_t i = 0; i < q.desc_count; i++) {
-            const edgpu_out_desc& o = d[q.desc_base + i];
+            const edgpu_out_desc& o = j.desc[q.desc_base + i];
             PacketWrite w;
             w.subscriber = q.subscriber;
             w.track = q.track;
@@ -284,18 +337,52 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
             w.wire = base + (o.offset - q.out_base);
             w.wireLen = o.len;
             w.packetID = o.packet_id;
-            w.arrivalMs = arrival.empty() ? -1 : arrival[q.desc_base + i];
+            w.arrivalMs = j.arrival ? j.arrival[q.desc_base + i] : -1;
             w.sender = q.sender;
             w.newOutput = (q.flags & EDGPU_SUB_NEW) != 0;
-            fTick.writes++;
-            err = sink->Write(w);
-            if (err == kWouldBlock) { blocked.push_back(edgpu_blocked{s, i}); break; }
-            if (err) return err;
+            w.worker = worker;
+            j.writes[worker]++;
+            const int err = j.sink->Write(w);
+            if (err == kWouldBlock) { j.blocked[worker].push_back(edgpu_blocked{s, i}); break; }
+            if (err) { j.err[worker] = err; return; }
         }
     }
-    fTick.write_ms = ms_since(t0);
-    if (!blocked.empty()) return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
-    return kNoErr;
+}
+
+void Reflector::WorkerLoop(uint32_t worker) {
+    uint64_t seen = 0;
+    for (;;) {
+        WriteJob* job;
+        uint32_t nw;
+        {
+            std::unique_lock<std::mutex> g(fPoolMu);
+            fPoolCv.wait(g, [&] { return fPoolStop || fJobSeq != seen; });
+            if (fPoolStop) return;
+            seen = fJobSeq;
+            job = fJob;
+            nw = fNumWriters;
+        }
+        WriteSubscribers(*job, worker, nw);
+        {
+            std::lock_guard<std::mutex> g(fPoolMu);
+            if (--fJobsLeft == 0) fPoolDone.notify_all();
+        }
+    }
+}
+
+void Reflector::SetWriteThreads(uint32_t n) {
+    n = std::max<uint32_t>(1, std::min<uint32_t>(n, 64));
+    if (n == fNumWriters && fWorkers.size() + 1 == n) return;
+    {
+        std::lock_guard<std::mutex> g(fPoolMu);
+        fPoolStop = true;
+    }
+    fPoolCv.notify_all();
+    for (std::thread& t : fWorkers) t.join();
+    fWorkers.clear();
+    fPoolStop = false;
+    fNumWriters = n;
+    for (uint32_t k = 1; k < n; k++) fWorkers.emplace_back([this, k] { WorkerLoop(k); });
 }
 
 // ---------------------------------------------------------------------------------------

@@ -23,12 +23,16 @@
 //                                                        public API + LoadGOP() from HBM
 //
 // Threading: one Reflector per GPU.  PushPacket / ProcessUDPPacket -- the pushers' ingest
-// (RTSPIncomingData, the UDP socket reader) -- may be called from any thread at any time: they
-// append to a pending batch under a short lock of their own and never wait for a tick (the
-// reference takes only the demuxer / stream mutex per packet, ReflectorStream.cpp:529-576,
-// 1769-1875).  Every other call is serialised by the caller (the reference's session-map and
-// per-stream fBucketMutex), and ReflectPackets runs the tick without holding the push lock
-// except for swapping the pending batch.
+// (RTSPIncomingData, the UDP socket reader) -- may be called from any thread at any time: each
+// reserves its slot in the pending batch under a short lock and copies the packet outside it,
+// and never waits for a tick (the reference takes only the demuxer / stream mutex per packet,
+// ReflectorStream.cpp:529-576, 1769-1875).  Every other call is serialised by the caller (the
+// reference's session-map and per-stream fBucketMutex), and ReflectPackets runs the tick
+// without holding the push lock except for swapping the pending batch.  With
+// SetWriteThreads(n > 1) ReflectPackets delivers a tick's packets from n threads: subscriber h
+// is served by worker h % n, so all of one subscriber's writes come from one thread, in the
+// order one thread would make them (the reference's ReflectorSocket tasks also write to
+// different outputs from different task threads, ReflectorStream.cpp:1676-1714).
 //
 // Copies: a pushed packet is copied once, into a pinned slot buffer (two, used alternately),
 // and reaches HBM by one asynchronous DMA (edgpu_ingest EDGPU_PTR_PINNED); a tick's output comes
@@ -37,11 +41,16 @@
 // relayed packet from that copy).
 #pragma once
 #include <stdint.h>
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
 #include "edgpu.h"
+
+namespace edgpu_host { struct TickRegions; }
 
 namespace edgpu_reflector {
 
@@ -65,6 +74,7 @@ struct PacketWrite {
     int64_t arrivalMs;              // the packet's fTimeArrived; -1 unless the sink WantsArrivals()
     uint32_t sender;                // engine sender (the ReflectorSender this write comes from)
     bool newOutput;                 // the output had no bookmark on this sender when the tick began
+    uint32_t worker;                // the delivering thread, 0 .. Reflector::WriteThreads() - 1
 };
 
 class OutputSink {
@@ -76,7 +86,9 @@ public:
     // tick's arrival times (edgpu_fanout_arrivals), shows the sink the whole sub-stream table
     // first (the reference walks each sender's outputs in bucket order, so whether an earlier
     // output was new decides `firstPacket` for the later ones, ReflectorStream.cpp:1086-1108),
-    // and calls Write for every packet.
+    // and calls Write for every packet.  Write / WritePacket are called concurrently for
+    // different subscribers when the Reflector has more than one write thread (w.worker tells
+    // them apart); BeginTick runs before, on the ticking thread.
     virtual bool WantsArrivals() const { return false; }
     virtual void BeginTick(const edgpu_substream_out* subs, uint32_t n) { (void)subs; (void)n; }
     virtual int Write(const PacketWrite& w) {
@@ -127,6 +139,9 @@ public:
     // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order).  A sink
     // that WantsArrivals() needs serial ticks (no edgpu_config.overlap_ticks): kBadArgument.
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
+    // threads that deliver a tick's writes (default 1; at most 64); call between ticks
+    void SetWriteThreads(uint32_t n);
+    uint32_t WriteThreads() const { return fNumWriters; }
     edgpu_ctx* Context() { return fCtx; }
 
     // per-tick measurements of the last ReflectPackets (tools/bench_module)
@@ -145,6 +160,7 @@ private:
     struct Batch {
         uint8_t* blob = nullptr;                            // pinned (edgpu_host_alloc)
         uint64_t cap = 0, used = 0;
+        std::atomic<uint32_t> copying{0};                   // reserved slots still being copied
         std::vector<Pushed> pushed;                         // arrival order
         std::vector<edgpu_udp_source> sources;              // UDP datagrams' sources, same order
         // pinned descriptor / segment arrays, filled at the flush (grouped by session)
@@ -153,6 +169,18 @@ private:
     };
     void Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
                 int64_t nowMs, const edgpu_udp_source* src);
+    // the write phase of a tick, for the subscribers of one worker
+    struct WriteJob {
+        const edgpu_substream_out* subs; uint32_t nsubs;
+        const edgpu_out_desc* desc; const int64_t* arrival;
+        const uint8_t* host; const edgpu_host::TickRegions* regions;   // the tick's bytes
+        OutputSink* sink;
+        std::vector<edgpu_blocked> blocked[64];
+        uint64_t writes[64];
+        int err[64];
+    };
+    void WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers);
+    void WorkerLoop(uint32_t worker);
     edgpu_ctx* fCtx = nullptr;
     int fStatus = kRequestFailed;
     std::mutex fPushMu;                                     // guards fBatch[fFill] and fTracks
@@ -163,6 +191,15 @@ private:
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes
     void* fDevOut = nullptr; uint64_t fDevOutCap = 0;       // device: edgpu_arena_gather target
     TickInfo fTick;
+    // write threads (workers 1..n-1; the ticking thread is worker 0)
+    uint32_t fNumWriters = 1;
+    std::vector<std::thread> fWorkers;
+    std::mutex fPoolMu;
+    std::condition_variable fPoolCv, fPoolDone;
+    WriteJob* fJob = nullptr;
+    uint64_t fJobSeq = 0;
+    uint32_t fJobsLeft = 0;
+    bool fPoolStop = false;
 };
 
 // CKeyFrameCache with the reference's public API and TLV record format

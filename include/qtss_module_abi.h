@@ -234,6 +234,8 @@ typedef struct EDGPU_QTSSTickInfo {
     uint64_t readback_bytes, arena_bytes;
     uint64_t writes;                    /* QTSS_Write calls */
     double   ingest_ms, fanout_ms, readback_ms, write_ms, hold_ms;
+    uint64_t ticks, failed_ticks;       /* since Initialize */
+    int64_t  last_error;                /* the engine's code of the newest failed tick, or 0 */
 } EDGPU_QTSSTickInfo;
 edqtss::QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out);
 }

@@ -176,16 +176,18 @@ static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* bu
 // QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
 static uint64_t g_writes = 0;
 static bool g_count_only = false;                    // --bench: sinks count, no capture
-static uint64_t g_write_bytes = 0;
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
+    const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (g_count_only) {
-        g_writes++;
-        g_write_bytes += len;
+        // the reference harness's bench sink: one memcpy of the packet, counted (the module's
+        // write threads call this concurrently for different players: per-stream counts)
+        thread_local static char scratch[70000];
+        memcpy(scratch, ((const QTSS_PacketStruct*)buf)->packetData, std::min<uint32_t>(len, sizeof(scratch)));
+        o->npk[k]++;
         if (outLen) *outLen = len;
         return QTSS_NoErr;
     }
-    const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (!(flags & (qtssWriteFlagsIsRTP | qtssWriteFlagsIsRTCP)) || !(flags & qtssWriteFlagsWriteBurstBegin)) {
         fprintf(stderr, "QTSS_Write on an RTP stream without RTP/RTCP + burst flags (0x%x)\n", flags);
         exit(4);
@@ -333,7 +335,12 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     return e;
 }
 
-static void* g_so = nullptr;                         // the module (and, through it, libedgpu)
+static void* g_so = nullptr;
+static uint64_t stream_writes() {                     // --bench: writes so far, over every stream
+    uint64_t n = 0;
+    for (const Obj* o : g_streams) n += o->npk[0] + o->npk[1];
+    return n;
+}                         // the module (and, through it, libedgpu)
 
 // ---- --bench ---------------------------------------------------------------------------------
 struct Pusher {                                        // one synthetic H.264 push (one track)
@@ -443,7 +450,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         auto c = std::chrono::steady_clock::now();
         EDGPU_QTSSTickInfo ti;
         if (last_fn(&ti)) return 3;
-        if (k == warm) writes0 = g_writes;
+        if (k == warm) writes0 = stream_writes();
         if (k >= warm) {
             timed_ticks++;
             push_s += std::chrono::duration<double>(b - a).count();
@@ -453,14 +460,15 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             rb_bytes += ti.readback_bytes; arena += ti.arena_bytes; ingested += ti.ingested_packets;
         }
     }
-    const uint64_t relayed = g_writes - writes0 + 0;
+    const uint64_t relayed = stream_writes() - writes0;
     const double n = (double)std::max<uint64_t>(timed_ticks, 1);
-    printf("{\"sessions\": %u, \"subs\": %u, \"tick_ms\": %u, \"pusher_threads\": %u, \"ticks_timed\": %llu, "
+    const char* wt = getenv("EDGPU_QTSS_WRITE_THREADS");
+    printf("{\"sessions\": %u, \"subs\": %u, \"tick_ms\": %u, \"pusher_threads\": %u, \"write_threads\": %s, \"ticks_timed\": %llu, "
            "\"setup_s\": %.3f, \"relayed_packets\": %llu, \"ingested_packets\": %llu, \"push_s\": %.4f, \"tick_s\": %.4f, "
            "\"relayed_per_s\": %.1f, \"ingested_per_s\": %.1f, \"per_tick_ms\": {\"hold\": %.3f, \"hold_max\": %.3f, "
            "\"ingest\": %.3f, \"gpu_fanout\": %.3f, \"readback\": %.3f, \"writes\": %.3f}, "
            "\"per_tick_bytes\": {\"readback\": %.0f, \"arena\": %.0f}, \"virtual_s\": %.3f}\n",
-           nsess, nsub, tick_ms, nthreads, (unsigned long long)timed_ticks, setup_s, (unsigned long long)relayed,
+           nsess, nsub, tick_ms, nthreads, wt ? wt : "4", (unsigned long long)timed_ticks, setup_s, (unsigned long long)relayed,
            (unsigned long long)ingested, push_s, tick_s, relayed / std::max(push_s + tick_s, 1e-9),
            ingested / std::max(push_s + tick_s, 1e-9), hold / n, hold_max, ing / n, gpu / n, rb / n, wr / n,
            rb_bytes / n, arena / n, timed_ticks * tick_ms / 1000.0);
@@ -763,27 +771,41 @@ int main(int argc, char** argv) {
             if (e.type == 5) { (void)source_socket(e.addr, e.port); (void)source_socket(e.addr, (uint16_t)(e.port | 1)); }
             lists[e.s % 2].push_back(e);
         }
-        std::atomic<int> failed{0};
+        std::atomic<int> failed{0}, at_gate{0};
+        // the gate: no event later than every session's first packet is pushed (so the virtual
+        // clock cannot move on) until both threads are there and every player has a write on
+        // each RTP track that carries packets -- each output's first tick then took its start
+        // inside the buffer window, and from there it follows its bookmarks
+        int64_t t_gate = 0;
+        for (const auto& kv : first_t) t_gate = std::max(t_gate, kv.second);
         auto pusher = [&](int k) {
             std::vector<char> fr(70000);
             bool gated = false;
             for (size_t i = 0; i < lists[k].size(); i++) {
                 const Ev& e = lists[k][i];
-                if (!gated && e.t > first_t[e.s]) {
-                    // hold until every player of this thread's sessions has a write on each RTP
-                    // track that carries packets (its first tick took the buffer window)
+                if (!gated && e.t > t_gate) {
                     gated = true;
+                    at_gate++;
                     const auto t0 = std::chrono::steady_clock::now();
                     for (;;) {
-                        bool all = true;
+                        bool all = at_gate.load() == 2;
                         for (const Player& pl : players)
-                            if (pl.session % 2 == (uint32_t)k)
+                            if (all)
                                 for (const Obj* st : pl.streams)
                                     if (rtp_tracks.count({pl.session, st->track}) &&
                                         __atomic_load_n(&st->npk[0], __ATOMIC_ACQUIRE) == 0)
                                         all = false;
                         if (all) break;
-                        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) { failed = 1; return; }
+                        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+                            for (const Player& pl : players)
+                                if (k == 0)
+                                    for (const Obj* st : pl.streams)
+                                        fprintf(stderr, "--threaded: sub %u session %u track %u: %llu RTP / %llu RTCP writes\n",
+                                                pl.sub, pl.session, st->track, (unsigned long long)st->npk[0],
+                                                (unsigned long long)st->npk[1]);
+                            failed = 1;
+                            return;
+                        }
                         std::this_thread::sleep_for(std::chrono::milliseconds(1));
                     }
                 }
@@ -814,11 +836,23 @@ int main(int argc, char** argv) {
                 }
                 if (i % 32 == 31) std::this_thread::sleep_for(std::chrono::microseconds(300));   // ticks interleave
             }
+            if (!gated) at_gate++;
         };
         std::thread a(pusher, 0), b(pusher, 1);
         a.join();
         b.join();
-        if (failed) { fprintf(stderr, "--threaded: pusher thread failed (%d)\n", failed.load()); return 3; }
+        if (failed) {
+            fprintf(stderr, "--threaded: pusher thread failed (%d)\n", failed.load());
+            auto last_fn = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
+            EDGPU_QTSSTickInfo ti;
+            if (last_fn && last_fn(&ti) == QTSS_NoErr)
+                fprintf(stderr, "--threaded: %llu ticks, %llu failed (last error %lld), clock %lld ms\n",
+                        (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks, (long long)ti.last_error,
+                        (long long)g_now.load());
+            memset(&rp, 0, sizeof(rp));
+            (void)g_dispatch(QTSS_Shutdown_Role, &rp);             // joins the module's threads
+            return 3;
+        }
         // let the tick thread drain: until the writes stop growing for 200 ms
         uint64_t last = ~0ull;
         for (int quiet = 0; quiet < 40;) {
