@@ -15,14 +15,15 @@
 //                  wave per chunk; header bytes only), records its first kTcpFrames frame starts
 //                  and links its exit to the next chunk's candidate.
 //   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
-//                  scans the chunks' frame counts.
-//   k_tcp_scan     sessions -> ingest segments, capacity check.
+//                  scans the chunks' frame counts; the last workgroup to finish places the
+//                  sessions' frames (ingest segments, capacity check).
 //   k_tcp_emit     one wave per chunk: a descriptor and a source address per frame of the true
 //                  walk (lanes in parallel from the recorded starts); the frame bytes stay where
 //                  they are -- k_ingest copies them from the TCP bytes into the sender rings
 //                  (IngestParams.src_addr).  Only a frame that starts in the carried bytes is
 //                  staged (contiguous copy).
-//   k_tcp_finish   one workgroup per session: carry the partial frame, per-read report.
+//                  The wave of a session's first chunk then carries the partial frame and
+//                  fills the per-read report.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "edgpu.h"
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         fb += tnf;
         __syncthreads();
     }
+    __shared__ uint32_t s_last;
     if (tid == 0) {
         TcpGroup& W = P.groups[g];
         W.nframes = fb;
@@ -474,47 +476,52 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         const uint32_t code = s_stop_code;
         W.code = (code == kWalkPartial && s_stop >= v.len) ? kWalkRun : code;
         W.stop = s_stop;
+        // sessions -> ingest segments: the last workgroup to finish places every session's
+        // frames (no separate scan launch); its atomic ticket orders the others' writes before
+        __threadfence();
+        s_last = atomicAdd(&P.tot->resolved, 1u) == P.ngroups - 1 ? 1u : 0u;
     }
-}
-
-// ---- k_tcp_scan: one workgroup; sessions -> ingest segments ----
-__global__ __launch_bounds__(256) void k_tcp_scan(TcpParams P) {
-    const int tid = threadIdx.x;
-    __shared__ uint32_t scan32[4];
-    uint32_t fb = 0;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    fb = 0;
     for (uint32_t g0 = 0; g0 < P.ngroups; g0 += 256) {
-        const uint32_t g = g0 + tid;
-        const bool ok = g < P.ngroups;
-        const uint32_t nf = ok ? P.groups[g].nframes : 0u;
+        const uint32_t gg = g0 + tid;
+        const bool ok = gg < P.ngroups;
+        // other workgroups' counts: read past this CU's cache
+        const uint32_t nf = ok ? __atomic_load_n(&P.groups[gg].nframes, __ATOMIC_RELAXED) : 0u;
         uint32_t tnf;
         const uint32_t pnf = block_exclusive_scan256<uint32_t>(nf, scan32, tnf);
-        if (ok) P.groups[g].frame_base = fb + pnf;
+        if (ok) P.groups[gg].frame_base = fb + pnf;
         fb += tnf;
     }
     const bool over = fb > P.max_desc;
-    for (uint32_t g = tid; g < P.ngroups; g += 256) {
-        P.seg_off[g] = over ? 0u : P.groups[g].frame_base;
-        P.seg_sess[g] = P.groups[g].session;
+    __syncthreads();
+    for (uint32_t gg = tid; gg < P.ngroups; gg += 256) {
+        P.seg_off[gg] = over ? 0u : P.groups[gg].frame_base;
+        P.seg_sess[gg] = P.groups[gg].session;
     }
     if (tid == 0) {
         P.seg_off[P.ngroups] = over ? 0u : fb;
         P.tot->frames = fb;
         P.tot->status = over ? EDGPU_OUT_OVERFLOW : 0;
+        P.tot->resolved = 0;                                  // the next call's tickets
     }
 }
 
 // ---- k_tcp_emit: one wave per chunk; frames -> descriptors + source addresses ----
+// The wave of a session's first chunk then finishes the session (what a separate pass did after
+// k_ingest): it carries the partial frame -- only that wave reads the carried bytes, and its
+// staging copy is done by then -- and fills the per-read report.  A session with no stream
+// bytes has no chunk; its report is the zeros the host cleared.
 __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
     const uint32_t c = blockIdx.x;
     const int lane = threadIdx.x;
-    if (P.tot->status != 0) return;
+    const bool over = P.tot->status != 0;
     const TcpChunkRes R = P.chunkres[c];
-    if (R.entry == kTcpNone) return;
     const uint32_t g = P.chunk_group[c];
     const TcpGroup G = P.groups[g];
     const TcpView v = tcp_view(P, G);
-    const uint64_t start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
-    const uint64_t end = min(start + kTcpChunk, v.len);
     const TcpRead* rd = P.reads + G.first_read;
     __shared__ uint64_t s_pos[64];
     __shared__ uint32_t s_m;
@@ -524,93 +531,91 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
     // a binary search there instead of a chain of dependent global loads
     __shared__ uint64_t s_rstart[64];
     __shared__ int64_t s_rarr[64];
-    const bool lds_reads = G.nreads <= 64;
-    if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
-    if (lane == 0) s_stage = ~0ull;
-    __syncthreads();
-    const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
-    const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
-    uint32_t done = 0;
-    uint64_t pos = start + R.entry;
-    while (done < R.nframes) {
-        uint32_t m;
-        if (recorded) {
-            m = min(64u, R.nframes - done);
-        } else {                                          // re-walk: the next up to 64 frames
-            if (lane == 0) {
-                uint32_t mm = 0;
-                uint64_t p = pos;
-                while (mm < 64 && p < end) {
-                    uint32_t flen = 0;
-                    if (tcp_step(v, p, flen) != kWalkRun) break;
-                    s_pos[mm++] = p;
-                    p += flen;
-                }
-                s_m = mm;
-                s_next = p;
-            }
-            __syncthreads();
-            m = s_m;
-            pos = s_next;
-        }
-        if ((uint32_t)lane < m) {
-            const uint64_t p = recorded ? start + rec[done + lane] : s_pos[lane];
-            uint32_t flen = 0;
-            tcp_step(v, p, flen);
-            const uint64_t last = p + flen - 1;
-            int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
-            }
-            const uint32_t fi = G.frame_base + R.fbase + done + lane;
-            edgpu_pkt_desc d;
-            d.slot = 0;
-            d.len = (uint16_t)(flen - 4);
-            d.channel = (uint8_t)tbyte(v, p + 1);
-            d.flags = 0;
-            d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
-            P.desc[fi] = d;
-            const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
-            if (p < v.clen) s_stage = p;
-            P.src_addr[fi] = (uint64_t)(uintptr_t)a;
-            atomicAdd(&P.results[G.first_read + lo].frames, 1u);
-        }
-        done += m;
-        __syncthreads();
-        if (m == 0) break;
-    }
-    // a frame that starts in the carried bytes: staged contiguously (the only one per session)
-    const uint64_t sp = s_stage;
-    if (sp != ~0ull) {
-        uint32_t flen = 0;
-        tcp_step(v, sp, flen);
-        uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
-        for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
-            dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
-    }
-}
-
-// ---- k_tcp_finish: one workgroup per session; carry + per-read results ----
-__global__ __launch_bounds__(256) void k_tcp_finish(TcpParams P) {
-    const uint32_t g = blockIdx.x;
-    const int tid = threadIdx.x;
-    const TcpGroup G = P.groups[g];
-    const bool over = P.tot->status != 0;
-    const TcpView v = tcp_view(P, G);
     __shared__ uint8_t s_carry[kTcpCarry];
+    if (!over && R.entry != kTcpNone) {                       // uniform
+        const uint64_t start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
+        const uint64_t end = min(start + kTcpChunk, v.len);
+        const bool lds_reads = G.nreads <= 64;
+        if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
+        if (lane == 0) s_stage = ~0ull;
+        __syncthreads();
+        const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
+        const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
+        uint32_t done = 0;
+        uint64_t pos = start + R.entry;
+        while (done < R.nframes) {
+            uint32_t m;
+            if (recorded) {
+                m = min(64u, R.nframes - done);
+            } else {                                          // re-walk: the next up to 64 frames
+                if (lane == 0) {
+                    uint32_t mm = 0;
+                    uint64_t p = pos;
+                    while (mm < 64 && p < end) {
+                        uint32_t flen = 0;
+                        if (tcp_step(v, p, flen) != kWalkRun) break;
+                        s_pos[mm++] = p;
+                        p += flen;
+                    }
+                    s_m = mm;
+                    s_next = p;
+                }
+                __syncthreads();
+                m = s_m;
+                pos = s_next;
+            }
+            if ((uint32_t)lane < m) {
+                const uint64_t p = recorded ? start + rec[done + lane] : s_pos[lane];
+                uint32_t flen = 0;
+                tcp_step(v, p, flen);
+                const uint64_t last = p + flen - 1;
+                int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t fi = G.frame_base + R.fbase + done + lane;
+                edgpu_pkt_desc d;
+                d.slot = 0;
+                d.len = (uint16_t)(flen - 4);
+                d.channel = (uint8_t)tbyte(v, p + 1);
+                d.flags = 0;
+                d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
+                P.desc[fi] = d;
+                const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
+                if (p < v.clen) s_stage = p;
+                P.src_addr[fi] = (uint64_t)(uintptr_t)a;
+                atomicAdd(&P.results[G.first_read + lo].frames, 1u);
+            }
+            done += m;
+            __syncthreads();
+            if (m == 0) break;
+        }
+        // a frame that starts in the carried bytes: staged contiguously (the only one per session)
+        const uint64_t sp = s_stage;
+        if (sp != ~0ull) {
+            uint32_t flen = 0;
+            tcp_step(v, sp, flen);
+            uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
+            for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
+                dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
+        }
+    }
+    if (c != G.first_chunk) return;                           // uniform
+    // ---- the session's finish: carry + per-read results ----
     const uint32_t code = G.code;
     const uint64_t stop = G.stop;
     uint32_t ncarry = 0;
     if (!over && code == kWalkPartial) ncarry = (uint32_t)(v.len - stop);
     if (over) ncarry = G.carry_len;
     if (!over) {
-        for (uint32_t b = tid; b < ncarry; b += 256) s_carry[b] = (uint8_t)tbyte(v, stop + b);
+        __syncthreads();                                      // the staging above has read the carry
+        for (uint32_t b = lane; b < ncarry; b += 64) s_carry[b] = (uint8_t)tbyte(v, stop + b);
         __syncthreads();
         uint8_t* dst = P.carry + (uint64_t)G.session * kTcpCarry;
-        for (uint32_t b = tid; b < ncarry; b += 256) dst[b] = s_carry[b];
+        for (uint32_t b = lane; b < ncarry; b += 64) dst[b] = s_carry[b];
     }
-    for (uint32_t i = tid; i < G.nreads; i += 256) {
+    for (uint32_t i = lane; i < G.nreads; i += 64) {
         const TcpRead r = P.reads[G.first_read + i];
         edgpu_tcp_result& o = P.results[G.first_read + i];
         uint32_t consumed = r.len;
@@ -634,14 +639,7 @@ hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
         hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
                            dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
-    hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(256), 0, st, p);
     if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);
-    return hipGetLastError();
-}
-
-// After k_ingest has copied the frames out of the staged / carried bytes.
-hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st) {
-    hipLaunchKernelGGL(k_tcp_finish, dim3(p.ngroups), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 

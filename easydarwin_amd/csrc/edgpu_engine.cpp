@@ -31,7 +31,6 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
-hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
                                hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
@@ -1043,8 +1042,8 @@ static int rebuild_index(edgpu_ctx* x) {
 }
 
 // Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
-// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first
-// and k_tcp_finish after, all inside the ingest timing events.
+// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
+// inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
                           uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr) {
     IngestParams p;
@@ -1060,7 +1059,6 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     HIP_CHECK(hist_mark(x, 2, 0));
     if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
-    if (tcp) HIP_CHECK(launch_deframe_finish(*tcp, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
     x->kf_share = tcp == nullptr;       // the interleaved path syncs and reads back results next
@@ -1242,7 +1240,10 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(x->d_tcp_links.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
     HIP_CHECK(x->d_tcp_offs.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands * kTcpFrames, x->stream));
     HIP_CHECK(x->d_tcp_stage.reserve((size_t)ng * kTcpCarry, x->stream));
-    if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
+    if (!x->d_tcp_tot) {
+        if (dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
+        HIP_CHECK(hipMemsetAsync(x->d_tcp_tot, 0, sizeof(TcpTotals), x->stream));   // k_tcp_resolve's tickets
+    }
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
     const uint8_t* raw = bytes;

@@ -274,7 +274,9 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
 // THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
 // for A/B: one round for a C2 session's ~375 packets per tick)
 template <uint32_t DEPTH, int THREADS = kIngestThreads>
-__global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
+// waves_per_eu(4): the kernel needs 4 waves per SIMD (4 resident 256-thread sessions per CU), and
+// the interleaved copy's four frames in flight fit 128 VGPRs that way
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_ingest(IngestParams P) {
     constexpr int NW = THREADS / 64;
     const uint32_t seg = blockIdx.x;
     const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(THREADS) void k_ingest(IngestParams P) {
         if (EDGPU_ABL(P) & 32u) {
             // timing ablation only: no slot copy
         } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr && EDGPU_TCP_COPY(P) >= 1) {   // frames inside the TCP byte stream
-            if (EDGPU_TCP_COPY(P) == 3) tcp_slot_copy_s<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
+            if (EDGPU_TCP_COPY(P) == 3) tcp_slot_copy_s<kTcpFramesPerRound, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else if (EDGPU_TCP_COPY(P) >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else tcp_slot_copy<1, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
         } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)

@@ -21,6 +21,14 @@
 
 namespace edgpu {
 
+// Interleaved frames a k_ingest wave copies per round (all their loads before the first
+// store): 4 since the copy is specialised on the frame's word offset (128 VGPRs, 4 waves per
+// SIMD); it was 2 (tools/build_ingest_ab.sh builds others)
+#ifndef EDGPU_TCP_TD
+#define EDGPU_TCP_TD 4
+#endif
+constexpr uint32_t kTcpFramesPerRound = EDGPU_TCP_TD;
+
 struct IngestParams {
     const edgpu_pkt_desc* desc;
     const uint32_t* seg_off;
@@ -142,7 +150,7 @@ struct TcpGroup {           // one pusher connection's reads in this call
 struct TcpRead { uint64_t start; int64_t arrival; uint32_t len, _pad; };   // start: stream position
 struct TcpCand { uint32_t q, exit, nframes, code; };                        // q / exit: chunk offsets
 struct TcpChunkRes { uint32_t entry, fbase, nframes, cand; };   // entry kTcpNone: idle; cand kTcpNone: re-walk
-struct TcpTotals { uint32_t frames; int32_t status; };
+struct TcpTotals { uint32_t frames; int32_t status; uint32_t resolved, _pad; };   // resolved: k_tcp_resolve tickets
 
 struct TcpParams {
     TcpGroup* groups;

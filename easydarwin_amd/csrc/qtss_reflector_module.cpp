@@ -41,8 +41,9 @@
 //
 // Locking: `mu` guards the sessions / outputs bookkeeping and is held through a tick (the
 // egress callbacks); the pushers' ingest never takes it -- RTSPIncomingData routes through
-// `routeMu` (a small table: module session -> engine session) into the Reflector's own push
-// lock, and the UDP reader thread takes only `udpMu` -- so a pusher never waits for a tick.
+// one stripe of the route table (module session -> engine session, striped by session id) into
+// one stripe of the Reflector's push path, and the UDP reader thread takes only `udpMu` -- so a
+// pusher never waits for a tick, and pushers of different sessions rarely share a lock.
 //
 // Scope: RTSP-interleaved pushers (EasyPusher's default transport), UDP
 // pushers and UDP / TCP players.  A UDP push SETUP binds the track's even/odd socket pair as
@@ -69,7 +70,6 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -170,9 +170,12 @@ struct Module {
     uint32_t nextId = 1;
     bool killClients = false;           // kill_clients_when_broadcast_stops (QRM:476-477)
     // the pushers' path (RTSPIncomingData): module session id -> (engine session, tracks) while a
-    // pusher is attached; guarded by routeMu alone
-    std::shared_mutex routeMu;          // pushers share it; SETUP / session end take it alone
-    std::map<uint32_t, std::pair<uint32_t, uint32_t>> route;
+    // pusher is attached; stripe id % kRouteStripes guards its part alone
+    static constexpr uint32_t kRouteStripes = 16;
+    struct alignas(64) RouteStripe {
+        std::mutex mu;
+        std::map<uint32_t, std::pair<uint32_t, uint32_t>> route;
+    } routes[kRouteStripes];
     std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
     std::map<uint32_t, Output*> byHandle;
     std::vector<std::unique_ptr<Output>> outputs;
@@ -525,9 +528,9 @@ QTSS_Error Shutdown() {
                 if (fd >= 0) { close(fd); fd = -1; }
         M->udp.clear();
     }
-    {
-        std::lock_guard<std::shared_mutex> r(M->routeMu);
-        M->route.clear();
+    for (Module::RouteStripe& r : M->routes) {
+        std::lock_guard<std::mutex> g(r.mu);
+        r.route.clear();
     }
     M->R.reset();
     return QTSS_NoErr;
@@ -590,9 +593,10 @@ Session* FindSession(uint32_t id) {
 
 // The pushers' route to the engine (RTSPIncomingData reads it without `mu`).
 void SetRoute(const Session& s, bool on) {
-    std::lock_guard<std::shared_mutex> g(M->routeMu);
-    if (on) M->route[s.id] = std::make_pair(s.engine, (uint32_t)s.trackIDs.size());
-    else M->route.erase(s.id);
+    Module::RouteStripe& r = M->routes[s.id % Module::kRouteStripes];
+    std::lock_guard<std::mutex> g(r.mu);
+    if (on) r.route[s.id] = std::make_pair(s.engine, (uint32_t)s.trackIDs.size());
+    else r.route.erase(s.id);
 }
 
 // FindOrCreateSession (QRM:1379-1545).  A player only finds a registered session (:1391-1396);
@@ -856,7 +860,7 @@ QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
 }
 
 // RTSPIncomingData (ProcessRTPData, QRM:604-678): one '$' ch BE16(len) frame of a pusher.  Never
-// takes `mu`: the route table and the Reflector's push lock only, so it never waits for a tick.
+// takes `mu`: one stripe of the route table and one of the Reflector's push path, so it never waits for a tick.
 QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     uintptr_t sid = 0;
     if (!GetPOD(p->inRTSPSession, sRTSPBroadcastSessionAttr, &sid) || !sid) return QTSS_NoErr;
@@ -866,9 +870,10 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     // the frame's own length, as the reference reads it; never past the buffer the server gave
     const uint32_t len = std::min<uint32_t>((uint32_t)d[2] << 8 | d[3], p->inPacketLen - 4);
     const int64_t now = Milliseconds();
-    std::shared_lock<std::shared_mutex> g(M->routeMu);
-    auto it = M->route.find((uint32_t)sid);
-    if (!M->R || it == M->route.end()) return QTSS_NoErr;      // no pusher attached any more
+    Module::RouteStripe& r = M->routes[(uint32_t)sid % Module::kRouteStripes];
+    std::lock_guard<std::mutex> g(r.mu);
+    auto it = r.route.find((uint32_t)sid);
+    if (!M->R || it == r.route.end()) return QTSS_NoErr;       // no pusher attached any more
     const uint32_t track = channel / 2;
     if (track >= it->second.second) return QTSS_NoErr;
     M->R->PushPacket(it->second.first, track, (const char*)d + 4, len, (channel & 1) != 0, now);

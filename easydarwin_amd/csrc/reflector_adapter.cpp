@@ -36,18 +36,40 @@ int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint3
     int err = edgpu_session_add(fCtx, sdp.data(), (uint32_t)sdp.size(), udpPush ? 1 : 0, &s);
     if (err) return err;
     if ((err = edgpu_session_tracks(fCtx, s, &n))) return err;
-    {
-        std::lock_guard<std::mutex> g(fPushMu);
-        if (fTracks.size() <= s) fTracks.resize(s + 1, 0);
-        fTracks[s] = n;
-    }
+    LockAllStripes();
+    if (fTracks.size() <= s) fTracks.resize(s + 1, 0);
+    fTracks[s] = n;
+    UnlockAllStripes();
     if (outSession) *outSession = s;
     return kNoErr;
 }
 
 uint32_t Reflector::GetNumStreams(uint32_t session) const {
-    std::lock_guard<std::mutex> g(const_cast<std::mutex&>(fPushMu));
+    std::lock_guard<std::mutex> g(const_cast<std::mutex&>(fStripe[session % kStripes].mu));
     return session < fTracks.size() ? fTracks[session] : 0;
+}
+
+void Reflector::LockAllStripes() {
+    for (StripeLock& l : fStripe) l.mu.lock();
+}
+
+void Reflector::UnlockAllStripes() {
+    for (uint32_t k = kStripes; k-- > 0;) fStripe[k].mu.unlock();
+}
+
+// A larger pinned blob for batch b (the caller holds every stripe lock): waits for the copies in
+// flight, moves the bytes so far over (the slots keep their offsets).
+bool Reflector::GrowBlob(Batch* b, uint64_t need) {
+    for (Stripe& st : b->st)
+        while (st.copying.load(std::memory_order_acquire)) std::this_thread::yield();
+    const uint64_t cap = std::max<uint64_t>(b->cap ? b->cap * 2 : (4ull << 20), need);
+    void* nb = nullptr;
+    if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return false;
+    if (b->next) memcpy(nb, b->blob, b->next);
+    if (b->blob) (void)edgpu_host_free(fCtx, b->blob);
+    b->blob = (uint8_t*)nb;
+    b->cap = cap;
+    return true;
 }
 
 int Reflector::AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle) {
@@ -80,54 +102,65 @@ int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
     {
         // later pushes to it are dropped, and what another thread pushed since the flush is
         // discarded (its id may be reused by the next session)
-        std::lock_guard<std::mutex> g(fPushMu);
+        std::lock_guard<std::mutex> g(fStripe[session % kStripes].mu);
         if (session < fTracks.size()) fTracks[session] = 0;
-        Batch& b = fBatch[fFill];
-        b.pushed.erase(std::remove_if(b.pushed.begin(), b.pushed.end(),
-                                      [&](const Pushed& p) { return p.session == session; }), b.pushed.end());
-        b.sources.erase(std::remove_if(b.sources.begin(), b.sources.end(),
-                                       [&](const edgpu_udp_source& u) { return u.session == session; }), b.sources.end());
+        Stripe& st = fBatch[fFill].st[session % kStripes];
+        st.pushed.erase(std::remove_if(st.pushed.begin(), st.pushed.end(),
+                                       [&](const Pushed& p) { return p.session == session; }), st.pushed.end());
+        st.sources.erase(std::remove_if(st.sources.begin(), st.sources.end(),
+                                        [&](const edgpu_udp_source& u) { return u.session == session; }), st.sources.end());
     }
     return edgpu_session_remove(fCtx, session, killOutputs ? EDGPU_SESSION_KILL_OUTPUTS : 0);
 }
 
 // Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
-// filled: the only host copy of the packet.  The slot is reserved under the push lock and the
-// packet copied outside it (`copying` counts copies in flight; a flush or a growth waits for
-// them), so concurrent pushers serialise on a few stores only.  The pinned blob grows by
-// doubling (a larger buffer, the slots so far copied over); the batch being filled is never one
-// whose DMA may be in flight.
+// filled: the only host copy of the packet.  Under its stripe's lock the pusher reserves the slot
+// in the stripe's slab (a new 64-KiB slab from the blob when it is full); it copies the packet
+// after releasing the lock (`copying` counts copies in flight: a flush or a blob growth waits
+// for them).  The pinned blob grows by doubling under every stripe lock (the slots so far
+// copied over); the batch being filled is never one whose DMA may be in flight.
 void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
                        int64_t nowMs, const edgpu_udp_source* src) {
     const uint32_t clamped = std::min<uint32_t>(packetLen, 2060);   // bytes past 2060 are never read (Q11)
     const uint64_t slot = (clamped + 4 + 15) & ~15ull;
-    Batch* bp;
-    uint8_t* d;
-    {
-        std::lock_guard<std::mutex> g(fPushMu);
+    const uint32_t k = session % kStripes;
+    Stripe* sp = nullptr;
+    uint8_t* d = nullptr;
+    for (;;) {
+        std::unique_lock<std::mutex> g(fStripe[k].mu);
         if (session >= fTracks.size() || track >= fTracks[session]) return;
         Batch& b = fBatch[fFill];
-        if (b.used + slot > b.cap) {
-            while (b.copying.load(std::memory_order_acquire)) std::this_thread::yield();
-            uint64_t cap = std::max<uint64_t>(b.cap ? b.cap * 2 : (4ull << 20), b.used + slot);
-            void* nb = nullptr;
-            if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return;      // out of pinned memory: dropped
-            if (b.used) memcpy(nb, b.blob, b.used);
-            if (b.blob) (void)edgpu_host_free(fCtx, b.blob);
-            b.blob = (uint8_t*)nb;
-            b.cap = cap;
+        Stripe& st = b.st[k];
+        if (st.used + slot > st.cap) {                       // a new slab
+            if (b.next + kSlab > b.cap) {
+                // grow under every stripe lock (taken in order: release ours first), then retry
+                g.unlock();
+                LockAllStripes();
+                Batch& bb = fBatch[fFill];
+                const bool ok = bb.next + kSlab <= bb.cap || GrowBlob(&bb, bb.next + kSlab);
+                UnlockAllStripes();
+                if (!ok) return;                             // out of pinned memory: dropped
+                continue;
+            }
+            // other stripes take slabs under their own locks: the bump pointer is a CAS
+            uint64_t off = __atomic_load_n(&b.next, __ATOMIC_RELAXED);
+            while (off + kSlab <= b.cap &&
+                   !__atomic_compare_exchange_n(&b.next, &off, off + kSlab, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+            if (off + kSlab > b.cap) continue;               // lost the race for the last slab: grow
+            st.slab = off; st.used = 0; st.cap = kSlab;
         }
-        d = b.blob + b.used;
-        b.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, b.used, packetLen});
-        if (src) b.sources.push_back(*src);
-        b.used += slot;
-        b.copying.fetch_add(1, std::memory_order_relaxed);
-        bp = &b;
+        d = b.blob + st.slab + st.used;
+        st.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, st.slab + st.used, packetLen});
+        if (src) st.sources.push_back(*src);
+        st.used += slot;
+        st.copying.fetch_add(1, std::memory_order_relaxed);
+        sp = &st;
+        break;
     }
     memset(d, 0, 4);
     memcpy(d + 4, packet, clamped);
     if (slot > clamped + 4) memset(d + 4 + clamped, 0, slot - clamped - 4);
-    bp->copying.fetch_sub(1, std::memory_order_release);
+    sp->copying.fetch_sub(1, std::memory_order_release);
 }
 
 void Reflector::PushPacket(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen,
@@ -165,22 +198,22 @@ int Reflector::FlushIngest() {
     // DMA is done -- this sync is the guarantee for error paths (idle stream: microseconds).
     int err = edgpu_sync(fCtx);
     if (err) return err;
-    Batch* bp;
-    {
-        std::lock_guard<std::mutex> g(fPushMu);
-        bp = &fBatch[fFill];
-        fFill ^= 1;
-    }
-    Batch& b = *bp;
-    while (b.copying.load(std::memory_order_acquire)) std::this_thread::yield();   // pushers mid-copy
-    if (!b.pushed.empty()) {
-        // descriptors grouped by session (stable: arrival order within a session); the slots
-        // stay where the pushers wrote them
-        const uint32_t n = (uint32_t)b.pushed.size();
-        std::vector<uint32_t> order(n);
-        for (uint32_t i = 0; i < n; i++) order[i] = i;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](uint32_t x, uint32_t y) { return b.pushed[x].session < b.pushed[y].session; });
+    LockAllStripes();
+    Batch& b = fBatch[fFill];
+    fFill ^= 1;
+    UnlockAllStripes();
+    for (Stripe& st : b.st)                                  // pushers mid-copy
+        while (st.copying.load(std::memory_order_acquire)) std::this_thread::yield();
+    uint32_t n = 0;
+    for (const Stripe& st : b.st) n += (uint32_t)st.pushed.size();
+    if (n) {
+        // descriptors grouped by session (a session's packets are all in one stripe, in arrival
+        // order); the slots stay where the pushers wrote them
+        std::vector<const Pushed*> order;
+        order.reserve(n);
+        for (const Stripe& st : b.st)
+            for (const Pushed& p : st.pushed) order.push_back(&p);
+        std::stable_sort(order.begin(), order.end(), [](const Pushed* x, const Pushed* y) { return x->session < y->session; });
         if (b.descCap < n) {
             for (void* p : {(void*)b.desc, (void*)b.seg, (void*)b.segSess})
                 if (p) (void)edgpu_host_free(fCtx, p);
@@ -197,7 +230,7 @@ int Reflector::FlushIngest() {
         }
         uint32_t nseg = 0;
         for (uint32_t k = 0; k < n; k++) {
-            const Pushed& p = b.pushed[order[k]];
+            const Pushed& p = *order[k];
             if (nseg == 0 || b.segSess[nseg - 1] != p.session) { b.seg[nseg] = k; b.segSess[nseg] = p.session; nseg++; }
             b.desc[k].slot = (uint32_t)(p.slot / 16);
             b.desc[k].len = (uint16_t)p.len;
@@ -208,17 +241,15 @@ int Reflector::FlushIngest() {
         }
         b.seg[nseg] = n;
         fTick.ingested_packets = n;
-        err = edgpu_ingest(fCtx, b.desc, n, b.seg, b.segSess, nseg, b.blob, b.used, EDGPU_PTR_PINNED);
+        err = edgpu_ingest(fCtx, b.desc, n, b.seg, b.segSess, nseg, b.blob, b.next, EDGPU_PTR_PINNED);
         if (!err) err = edgpu_keyframe_index(fCtx);
-        b.pushed.clear();
-        b.used = 0;
-        if (err) { b.sources.clear(); return err; }
     }
-    if (!b.sources.empty()) {
-        err = edgpu_udp_sources(fCtx, b.sources.data(), (uint32_t)b.sources.size());
-        b.sources.clear();
-        if (err) return err;
-    }
+    std::vector<edgpu_udp_source> sources;
+    for (const Stripe& st : b.st) sources.insert(sources.end(), st.sources.begin(), st.sources.end());
+    for (Stripe& st : b.st) { st.pushed.clear(); st.sources.clear(); st.slab = st.used = st.cap = 0; }
+    b.next = 0;
+    if (err) return err;
+    if (!sources.empty() && (err = edgpu_udp_sources(fCtx, sources.data(), (uint32_t)sources.size()))) return err;
     fTick.ingest_ms = ms_since(t0);
     return kNoErr;
 }

@@ -24,7 +24,8 @@
 //
 // Threading: one Reflector per GPU.  PushPacket / ProcessUDPPacket -- the pushers' ingest
 // (RTSPIncomingData, the UDP socket reader) -- may be called from any thread at any time: each
-// reserves its slot in the pending batch under a short lock and copies the packet outside it,
+// reserves its slot in the pending batch under a short lock (one of 16 stripes, by session) and
+// copies the packet outside it,
 // and never waits for a tick (the reference takes only the demuxer / stream mutex per packet,
 // ReflectorStream.cpp:529-576, 1769-1875).  Every other call is serialised by the caller (the
 // reference's session-map and per-stream fBucketMutex), and ReflectPackets runs the tick
@@ -157,16 +158,30 @@ private:
     int  FlushIngest();                                     // edgpu_ingest + keyframe index
     // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob
     struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint64_t slot; uint32_t len; };
+    // The push path is striped by session (session % kStripes): a pusher takes only its stripe's
+    // lock, and a stripe carves its slots out of 64-KiB slabs of the batch's pinned blob, so
+    // pushers of different sessions share no lock and no counter per packet.
+    static constexpr uint32_t kStripes = 16;
+    static constexpr uint64_t kSlab = 64 << 10;
+    struct Stripe {                                         // one stripe's part of a batch
+        std::vector<Pushed> pushed;                         // arrival order (per session)
+        std::vector<edgpu_udp_source> sources;              // UDP datagrams' sources, same order
+        uint64_t slab = 0, used = 0, cap = 0;               // the current slab: blob offset, used, size
+        std::atomic<uint32_t> copying{0};                   // reserved slots still being copied
+    };
     struct Batch {
         uint8_t* blob = nullptr;                            // pinned (edgpu_host_alloc)
-        uint64_t cap = 0, used = 0;
-        std::atomic<uint32_t> copying{0};                   // reserved slots still being copied
-        std::vector<Pushed> pushed;                         // arrival order
-        std::vector<edgpu_udp_source> sources;              // UDP datagrams' sources, same order
+        uint64_t cap = 0;
+        uint64_t next = 0;                                  // slab bump pointer (under a stripe lock + CAS)
+        Stripe st[kStripes];
         // pinned descriptor / segment arrays, filled at the flush (grouped by session)
         edgpu_pkt_desc* desc = nullptr; uint32_t* seg = nullptr; uint32_t* segSess = nullptr;
         uint64_t descCap = 0;
     };
+    struct alignas(64) StripeLock { std::mutex mu; };
+    void LockAllStripes();
+    void UnlockAllStripes();
+    bool GrowBlob(Batch* b, uint64_t need);                 // all stripes quiescent; false: no memory
     void Append(uint32_t session, uint32_t track, const char* packet, uint32_t packetLen, bool isRTCP,
                 int64_t nowMs, const edgpu_udp_source* src);
     // the write phase of a tick, for the subscribers of one worker
@@ -183,7 +198,9 @@ private:
     void WorkerLoop(uint32_t worker);
     edgpu_ctx* fCtx = nullptr;
     int fStatus = kRequestFailed;
-    std::mutex fPushMu;                                     // guards fBatch[fFill] and fTracks
+    // stripe k guards the fill batch's stripe k and fTracks[s] for s % kStripes == k; fFill and
+    // fTracks' size change under all stripe locks
+    StripeLock fStripe[kStripes];
     Batch fBatch[2];
     int fFill = 0;
     std::vector<uint32_t> fTracks;                          // per session (0: none)

@@ -100,6 +100,10 @@ def main():
     c1o, c1r = owner.counters(), replica.counters()
     relayed = (c1o["relayed_packets"] - c0o["relayed_packets"]) + (c1r["relayed_packets"] - c0r["relayed_packets"])
     rbytes = (c1o["relayed_bytes"] - c0o["relayed_bytes"]) + (c1r["relayed_bytes"] - c0r["relayed_bytes"])
+    # the burst's copy kernels (owner + replica fan-out) against HBM: B = out + in + 16 per packet
+    alg = rbytes + (c1o["fanout_in_bytes"] - c0o["fanout_in_bytes"]) + (c1r["fanout_in_bytes"] - c0r["fanout_in_bytes"]) \
+        + 16 * relayed
+    kms = (fo[-1] if fo else 0.0) + (fr[-1] if fr else 0.0)
     res = {
         "workload": f"C4: {args.joins} joins over {args.sessions} C2 sessions after {args.warm_ticks} s, "
                     f"egress GPU = hash(subID) % {args.gpus}; remote joins served by replica sessions",
@@ -112,6 +116,9 @@ def main():
         "burst_fanout_kernel_ms": {"owner": round(fo[-1], 4) if fo else None,
                                    "replica": round(fr[-1], 4) if fr else None},
         "relayed_packets": int(relayed), "relayed_bytes": int(rbytes),
+        "roofline": {"bound": "hbm", "kernel": owner.fanout_kernel(), "alg_bytes": int(alg),
+                     "achieved": round(alg / (kms / 1e3) / 1e9, 1) if kms else None, "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(alg / (kms / 1e3) / 1e9 / 8000.0, 4) if kms else None, "traffic": None},
         "relayed_packets_per_join": round(relayed / args.joins, 1),
         "xgmi_estimate_ms_one_link": round(total / 50e9 * 1e3, 3),
         "note": "one GPU: the replica context sits on the same device, so the image copy is device-local",

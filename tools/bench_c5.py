@@ -107,6 +107,12 @@ def main():
         "fanout_kernel": ctx.fanout_kernel(),
         "fanout_ms": round(fan_ms, 4), "ingest_ms": round(float(np.mean(k_ing)), 4),
         "fanout_achieved_GBps": round(alg / max(launches, 1) / (fan_ms / 1e3) / 1e9, 1),
+        # the copy kernel against HBM (bench.py's roofline block; PMC traffic: tools/profile.sh)
+        "roofline": {"bound": "hbm", "kernel": ctx.fanout_kernel(),
+                     "alg_bytes_per_launch": int(alg / max(launches, 1)),
+                     "achieved": round(alg / max(launches, 1) / (fan_ms / 1e3) / 1e9, 1), "peak": 8000.0,
+                     "unit": "GB/s", "frac": round(alg / max(launches, 1) / (fan_ms / 1e3) / 1e9 / 8000.0, 4),
+                     "traffic": None},
         "ingested_packets_per_tick": int(np.mean([b["n"] for b in batches[1:]])),
         "relayed_packets_per_tick": int(relayed / (len(batches) - 1)),
         "generation_s": round(gen_s, 1),
