@@ -26,8 +26,20 @@ Reflector::~Reflector() {
         for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
             if (p) (void)edgpu_host_free(fCtx, p);
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
+    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinArr})
+        if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
     if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
     edgpu_ctx_destroy(fCtx);
+}
+
+int Reflector::EnsurePinned(PinBuf& b, uint64_t bytes) {
+    if (bytes <= b.cap) return kNoErr;
+    if (b.p) (void)edgpu_host_free(fCtx, b.p);
+    b.p = nullptr; b.cap = 0;
+    const uint64_t cap = std::max<uint64_t>(bytes + bytes / 4, 1 << 16);
+    const int err = edgpu_host_alloc(fCtx, cap, &b.p);
+    if (!err) b.cap = cap;
+    return err;
 }
 
 int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession) {
@@ -278,12 +290,18 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     fTick.arena_bytes = st.arena_bytes;
     if (!sink || st.relayed_packets == 0) return kNoErr;
     t0 = Clock::now();
-    std::vector<edgpu_substream_out> subs(res.n_substreams);
-    std::vector<edgpu_out_desc> d(st.relayed_packets);
-    if ((err = edgpu_copy_to_host(fCtx, subs.data(), res.substreams, subs.size() * sizeof(subs[0])))) return err;
-    if ((err = edgpu_copy_to_host(fCtx, d.data(), res.desc, d.size() * sizeof(d[0])))) return err;
+    // the sub-stream table, descriptors (and arrivals) land in pinned buffers: one DMA each
+    const uint32_t nq = res.n_substreams;
+    const uint64_t nd = st.relayed_packets;
+    if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out))) ||
+        (err = EnsurePinned(fPinDesc, nd * sizeof(edgpu_out_desc))))
+        return err;
+    const edgpu_substream_out* subs = (const edgpu_substream_out*)fPinSubs.p;
+    const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
+    if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
+    if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
     // the tick's distinct bytes only: one region per identity sender + the other sub-streams
-    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs.data(), (uint32_t)subs.size());
+    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq);
     if (tr.bytes > fDevOutCap) {
         if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
         fDevOut = nullptr; fDevOutCap = 0;
@@ -300,20 +318,21 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     }
     if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fDevOut, fDevOutCap))) return err;
     if ((err = edgpu_copy_to_host(fCtx, fHostOut, fDevOut, tr.bytes))) return err;
-    fTick.readback_bytes = tr.bytes + subs.size() * sizeof(subs[0]) + d.size() * sizeof(d[0]);
-    std::vector<int64_t> arrival;
+    fTick.readback_bytes = tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
+    const int64_t* arrival = nullptr;
     if (sink->WantsArrivals()) {
-        arrival.resize(d.size());
-        if ((err = edgpu_fanout_arrivals(fCtx, arrival.data(), (uint32_t)arrival.size(), EDGPU_PTR_HOST))) {
+        if ((err = EnsurePinned(fPinArr, nd * sizeof(int64_t)))) return err;
+        if ((err = edgpu_fanout_arrivals(fCtx, (int64_t*)fPinArr.p, (uint32_t)nd, EDGPU_PTR_HOST))) {
             return err == EDGPU_BAD_ARGUMENT ? kBadArgument : err;   // overlap_ticks: no arrivals
         }
+        arrival = (const int64_t*)fPinArr.p;
     }
     fTick.readback_ms = ms_since(t0);
     t0 = Clock::now();
-    sink->BeginTick(subs.data(), (uint32_t)subs.size());
+    sink->BeginTick(subs, nq);
     WriteJob job;
-    job.subs = subs.data(); job.nsubs = (uint32_t)subs.size();
-    job.desc = d.data(); job.arrival = arrival.empty() ? nullptr : arrival.data();
+    job.subs = subs; job.nsubs = nq;
+    job.desc = d; job.arrival = arrival;
     job.sink = sink;
     job.host = fHostOut;
     job.regions = &tr;

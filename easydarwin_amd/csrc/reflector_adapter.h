@@ -205,6 +205,9 @@ private:
     int fFill = 0;
     std::vector<uint32_t> fTracks;                          // per session (0: none)
     // readback buffers
+    struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
+    int  EnsurePinned(PinBuf& b, uint64_t bytes);
+    PinBuf fPinSubs, fPinDesc, fPinArr;                     // sub-stream table, descriptors, arrivals
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes
     void* fDevOut = nullptr; uint64_t fDevOutCap = 0;       // device: edgpu_arena_gather target
     TickInfo fTick;
