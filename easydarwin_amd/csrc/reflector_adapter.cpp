@@ -367,15 +367,23 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
 }
 
-// The writes of the subscribers h with h % nworkers == worker, sub-stream by sub-stream in table
-// order (the order one thread takes): a write that would block stops that sub-stream.
+// The worker of a sub-stream: by its session (the sender of track t, kind k is the session's first
+// sender + 2t + k), so all of one subscriber's sub-streams -- and every subscriber of a session,
+// which read the same packet bytes -- go to one thread.
+static inline uint32_t writer_of(const edgpu_substream_out& q, uint32_t nworkers) {
+    const uint32_t session_key = q.sender - (2u * q.track + q.kind);
+    return (uint32_t)(((uint64_t)(session_key * 0x9E3779B1u) * nworkers) >> 32);
+}
+
+// The writes of the subscribers of one worker, sub-stream by sub-stream in table order (the order
+// one thread takes): a write that would block stops that sub-stream.
 void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers) {
     j.writes[worker] = 0;
     j.err[worker] = kNoErr;
     j.blocked[worker].clear();
     for (uint32_t s = 0; s < j.nsubs; s++) {
         const edgpu_substream_out& q = j.subs[s];
-        if (!q.desc_count || q.subscriber % nworkers != worker) continue;
+        if (!q.desc_count || (nworkers > 1 && writer_of(q, nworkers) != worker)) continue;
         const uint8_t* base = j.regions->at(j.host, s);
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = j.desc[q.desc_base + i];

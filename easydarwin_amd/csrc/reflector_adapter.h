@@ -30,10 +30,11 @@
 // ReflectorStream.cpp:529-576, 1769-1875).  Every other call is serialised by the caller (the
 // reference's session-map and per-stream fBucketMutex), and ReflectPackets runs the tick
 // without holding the push lock except for swapping the pending batch.  With
-// SetWriteThreads(n > 1) ReflectPackets delivers a tick's packets from n threads: subscriber h
-// is served by worker h % n, so all of one subscriber's writes come from one thread, in the
-// order one thread would make them (the reference's ReflectorSocket tasks also write to
-// different outputs from different task threads, ReflectorStream.cpp:1676-1714).
+// SetWriteThreads(n > 1) ReflectPackets delivers a tick's packets from n threads, split by
+// session: all of one subscriber's writes come from one thread, in the order one thread would
+// make them, and a session's subscribers -- the same packet bytes -- share that thread's caches
+// (the reference's ReflectorSocket tasks also write to different outputs from different task
+// threads, ReflectorStream.cpp:1676-1714).
 //
 // Copies: a pushed packet is copied once, into a pinned slot buffer (two, used alternately),
 // and reaches HBM by one asynchronous DMA (edgpu_ingest EDGPU_PTR_PINNED); a tick's output comes
