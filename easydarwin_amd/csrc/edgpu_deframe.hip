@@ -15,8 +15,8 @@
 //                  wave per chunk; header bytes only), records its first kTcpFrames frame starts
 //                  and links its exit to the next chunk's candidate.
 //   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
-//                  scans the chunks' frame counts; the last workgroup to finish places the
-//                  sessions' frames (ingest segments, capacity check).
+//                  scans the chunks' frame counts.
+//   k_tcp_scan     sessions -> ingest segments, capacity check (one workgroup).
 //   k_tcp_emit     one wave per chunk: a descriptor and a source address per frame of the true
 //                  walk (lanes in parallel from the recorded starts); the frame bytes stay where
 //                  they are -- k_ingest copies them from the TCP bytes into the sender rings
@@ -468,7 +468,6 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         fb += tnf;
         __syncthreads();
     }
-    __shared__ uint32_t s_last;
     if (tid == 0) {
         TcpGroup& W = P.groups[g];
         W.nframes = fb;
@@ -476,36 +475,49 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         const uint32_t code = s_stop_code;
         W.code = (code == kWalkPartial && s_stop >= v.len) ? kWalkRun : code;
         W.stop = s_stop;
-        // sessions -> ingest segments: the last workgroup to finish places every session's
-        // frames (no separate scan launch); its atomic ticket orders the others' writes before
-        __threadfence();
-        s_last = atomicAdd(&P.tot->resolved, 1u) == P.ngroups - 1 ? 1u : 0u;
     }
+}
+
+// ---- k_tcp_scan: one 1024-thread workgroup; sessions -> ingest segments ----
+// Each thread takes a run of consecutive sessions (one for up to 1024 sessions): all frame
+// counts are loaded at once, one block scan places them.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_tcp_scan(TcpParams P) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int NW = kScanThreads / 64;
+    __shared__ uint32_t s_w[NW];
+    const uint32_t per = (P.ngroups + kScanThreads - 1) / kScanThreads;
+    const uint32_t g0 = tid * per, g1 = min(g0 + per, P.ngroups);
+    uint32_t mine = 0;
+    for (uint32_t g = g0; g < g1; g++) mine += P.groups[g].nframes;
+    uint32_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
     __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    fb = 0;
-    for (uint32_t g0 = 0; g0 < P.ngroups; g0 += 256) {
-        const uint32_t gg = g0 + tid;
-        const bool ok = gg < P.ngroups;
-        // other workgroups' counts: read past this CU's cache
-        const uint32_t nf = ok ? __atomic_load_n(&P.groups[gg].nframes, __ATOMIC_RELAXED) : 0u;
-        uint32_t tnf;
-        const uint32_t pnf = block_exclusive_scan256<uint32_t>(nf, scan32, tnf);
-        if (ok) P.groups[gg].frame_base = fb + pnf;
-        fb += tnf;
+    uint32_t base = 0, fb = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const uint32_t t = s_w[w];
+        if (w < wid) base += t;
+        fb += t;
     }
     const bool over = fb > P.max_desc;
-    __syncthreads();
-    for (uint32_t gg = tid; gg < P.ngroups; gg += 256) {
-        P.seg_off[gg] = over ? 0u : P.groups[gg].frame_base;
-        P.seg_sess[gg] = P.groups[gg].session;
+    uint32_t at = base + x - mine;
+    for (uint32_t g = g0; g < g1; g++) {
+        const uint32_t nf = P.groups[g].nframes;
+        P.groups[g].frame_base = at;
+        P.seg_off[g] = over ? 0u : at;
+        P.seg_sess[g] = P.groups[g].session;
+        at += nf;
     }
     if (tid == 0) {
         P.seg_off[P.ngroups] = over ? 0u : fb;
         P.tot->frames = fb;
         P.tot->status = over ? EDGPU_OUT_OVERFLOW : 0;
-        P.tot->resolved = 0;                                  // the next call's tickets
     }
 }
 
@@ -639,6 +651,7 @@ hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
         hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
                            dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
     if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);
     return hipGetLastError();
 }

@@ -1240,10 +1240,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(x->d_tcp_links.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands, x->stream));
     HIP_CHECK(x->d_tcp_offs.reserve((size_t)std::max<uint32_t>(nc, 1) * kTcpCands * kTcpFrames, x->stream));
     HIP_CHECK(x->d_tcp_stage.reserve((size_t)ng * kTcpCarry, x->stream));
-    if (!x->d_tcp_tot) {
-        if (dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
-        HIP_CHECK(hipMemsetAsync(x->d_tcp_tot, 0, sizeof(TcpTotals), x->stream));   // k_tcp_resolve's tickets
-    }
+    if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
     const uint8_t* raw = bytes;

@@ -150,7 +150,7 @@ struct TcpGroup {           // one pusher connection's reads in this call
 struct TcpRead { uint64_t start; int64_t arrival; uint32_t len, _pad; };   // start: stream position
 struct TcpCand { uint32_t q, exit, nframes, code; };                        // q / exit: chunk offsets
 struct TcpChunkRes { uint32_t entry, fbase, nframes, cand; };   // entry kTcpNone: idle; cand kTcpNone: re-walk
-struct TcpTotals { uint32_t frames; int32_t status; uint32_t resolved, _pad; };   // resolved: k_tcp_resolve tickets
+struct TcpTotals { uint32_t frames; int32_t status; };
 
 struct TcpParams {
     TcpGroup* groups;
