@@ -352,7 +352,25 @@ void k_tcp_walk(TcpParams P) {
     const uint32_t c0 = (blockIdx.x * kWalkWaves + wid) * CPW;
     const WalkChunk a = walk_chunk_setup(P, c0, s_own[wid][0], s_next[wid][0], lane);
     WalkChunk b{};
-    if constexpr (CPW == 2) b = walk_chunk_setup(P, c0 + 1, s_own[wid][CPW - 1], s_next[wid][CPW - 1], lane);
+    if constexpr (CPW == 2) {
+        if (a.valid && a.end < a.v.len && c0 + 1 < P.nchunks && P.chunk_group[c0 + 1] == P.chunk_group[c0]) {
+            // the second chunk follows the first in the same stream: its own candidate window is
+            // the first chunk's next window, already scanned -- copy the list, scan only its next
+            b.c = c0 + 1;
+            b.valid = true;
+            b.v = a.v;
+            b.start = a.end;
+            b.end = min(b.start + kTcpChunk, b.v.len);
+            b.n = a.nn;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if ((uint32_t)lane < kTcpCands) s_own[wid][1][lane] = s_next[wid][0][lane];
+            b.nn = b.end < b.v.len ? tcp_candidates(b.v, b.end, s_next[wid][1], lane) : 0u;
+        } else {
+            b = walk_chunk_setup(P, c0 + 1, s_own[wid][CPW - 1], s_next[wid][CPW - 1], lane);
+        }
+    }
     __syncthreads();
     const int h = CPW == 2 && lane >= 32 ? 1 : 0;
     const WalkChunk w = h ? b : a;

@@ -1,4 +1,5 @@
-# round 3, run h: the session scan back as its own kernel, one 1024-thread round (folded into
+# round 3, run h: the walk reuses the first chunk's next-window candidates for the second chunk;
+# the session scan back as its own kernel, one 1024-thread round (folded into
 # k_tcp_resolve's last workgroup it cost 27 us); interleave + random parity, the --ingest tcp
 # line twice, a kernel trace of it
 set -o pipefail
