@@ -15,18 +15,17 @@
 //                  wave per chunk; header bytes only), records its first kTcpFrames frame starts
 //                  and links its exit to the next chunk's candidate.
 //   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
-//                  scans the chunks' frame counts, claims the session's range of descriptors
-//                  (capacity check), and writes a descriptor and a source address per frame
-//                  (a thread per frame from the recorded starts; chunks with more frames than
-//                  recorded are walked again by a wave).  The frame bytes stay where they are --
-//                  k_ingest copies them from the TCP bytes into the sender rings
+//                  scans the chunks' frame counts.
+//   k_tcp_scan     sessions -> ingest segments, capacity check (one workgroup).
+//   k_tcp_emit     one wave per chunk: a descriptor and a source address per frame of the true
+//                  walk (lanes in parallel from the recorded starts); the frame bytes stay where
+//                  they are -- k_ingest copies them from the TCP bytes into the sender rings
 //                  (IngestParams.src_addr).  Only a frame that starts in the carried bytes is
 //                  staged (contiguous copy).
-//   k_tcp_finish   one workgroup per session, after k_ingest: carry the partial frame,
-//                  per-read report.
+//                  The wave of a session's first chunk then carries the partial frame and
+//                  fills the per-read report.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <algorithm>
 #include "edgpu.h"
 #include "edgpu_device.h"
 #include "edgpu_params.h"
@@ -349,7 +348,6 @@ void k_tcp_walk(TcpParams P) {
     static_assert(CPW == 1 || CPW == 2, "one or two chunks per wave");
     constexpr uint32_t LPC = 64 / CPW;                      // walking lanes per chunk
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { P.tot->frames = 0; P.tot->status = 0; }
     __shared__ uint16_t s_own[kWalkWaves][CPW][kTcpCands], s_next[kWalkWaves][CPW][kTcpCands];
     const uint32_t c0 = (blockIdx.x * kWalkWaves + wid) * CPW;
     const WalkChunk a = walk_chunk_setup(P, c0, s_own[wid][0], s_next[wid][0], lane);
@@ -488,15 +486,6 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         fb += tnf;
         __syncthreads();
     }
-    // ---- the session's frames: a range of the batch's descriptors (claimed, so no pass over all
-    // sessions has to place them), then a descriptor and a source address per frame ----
-    __shared__ uint32_t s_base, s_ok;
-    __shared__ uint64_t s_stage;            // stream position of a frame to stage, ~0: none
-    __shared__ uint64_t s_rstart[64];       // the session's reads (up to 64) for the arrival search
-    __shared__ int64_t s_rarr[64];
-    __shared__ uint64_t s_pos[4][64];       // per wave: frames of a chunk walked again
-    __shared__ uint32_t s_m[4];
-    __shared__ uint64_t s_next[4];
     if (tid == 0) {
         TcpGroup& W = P.groups[g];
         W.nframes = fb;
@@ -504,138 +493,159 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
         const uint32_t code = s_stop_code;
         W.code = (code == kWalkPartial && s_stop >= v.len) ? kWalkRun : code;
         W.stop = s_stop;
-        uint32_t base = 0;
-        bool ok = true;
-        if (fb) {
-            base = atomicAdd(&P.tot->frames, fb);
-            ok = (uint64_t)base + fb <= P.max_desc;
-            if (!ok) atomicExch(&P.tot->status, (int32_t)EDGPU_OUT_OVERFLOW);   // k_ingest then runs none
-        }
-        P.seg_off[g] = ok ? base : 0u;
-        P.seg_end[g] = ok ? base + fb : 0u;
-        P.seg_sess[g] = G.session;
-        s_base = base;
-        s_ok = ok && fb ? 1u : 0u;
-        s_stage = ~0ull;
-    }
-    const bool lds_reads = G.nreads <= 64;
-    const TcpRead* rd = P.reads + G.first_read;
-    if (lds_reads && (uint32_t)tid < G.nreads) { s_rstart[tid] = rd[tid].start; s_rarr[tid] = rd[tid].arrival; }
-    __syncthreads();
-    if (!s_ok) return;                                        // uniform
-    const int lane = tid & 63, wid = tid >> 6;
-    auto emit = [&](uint32_t fi, uint64_t p) {
-        uint32_t flen = 0;
-        tcp_step(v, p, flen);
-        const uint64_t last = p + flen - 1;
-        int lo = 0, hi = (int)G.nreads - 1;                  // last read starting at or before `last`
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
-        }
-        edgpu_pkt_desc d;
-        d.slot = 0;
-        d.len = (uint16_t)(flen - 4);
-        d.channel = (uint8_t)tbyte(v, p + 1);
-        d.flags = 0;
-        d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
-        P.desc[fi] = d;
-        const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
-        if (p < v.clen) s_stage = p;
-        P.src_addr[fi] = (uint64_t)(uintptr_t)a;
-        atomicAdd(&P.results[G.first_read + lo].frames, 1u);
-    };
-    auto wave_sync = []() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    for (uint32_t k0 = 0; k0 < G.nchunks; k0 += kPiece) {
-        const uint32_t np = min(kPiece, G.nchunks - k0);
-        const uint32_t c0 = G.first_chunk + k0;
-        if ((uint32_t)tid < np) {                             // this piece's chunks (s_exit: frame base)
-            const TcpChunkRes R = P.chunkres[c0 + tid];
-            s_nf[tid] = R.nframes; s_exit[tid] = R.fbase; s_code[tid] = R.cand; s_entry[tid] = R.entry;
-        }
-        __syncthreads();
-        // frames whose chunk walk recorded their starts: one thread per frame
-        const uint32_t flo = s_exit[0], fhi = s_exit[np - 1] + s_nf[np - 1];
-        for (uint32_t f = flo + tid; f < fhi; f += 256) {
-            int lo = 0, hi = (int)np - 1;                    // the last chunk starting at or before f
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_exit[mid] <= f) lo = mid; else hi = mid - 1;
-            }
-            const uint32_t cand = s_code[lo];
-            if (cand == kTcpNone || s_nf[lo] > kTcpFrames) continue;      // walked again below
-            const uint16_t* rec = P.offs + ((size_t)(c0 + lo) * kTcpCands + cand) * kTcpFrames;
-            emit(s_base + f, (uint64_t)(k0 + lo) * kTcpChunk + rec[f - s_exit[lo]]);
-        }
-        // chunks with more frames than recorded, or found by the sequential walk: a wave each
-        // walks them again, 64 frames at a time
-        for (uint32_t kk = wid; kk < np; kk += 4) {
-            const uint32_t nfk = s_nf[kk], cand = s_code[kk];
-            if (nfk == 0 || (cand != kTcpNone && nfk <= kTcpFrames)) continue;   // uniform in the wave
-            const uint64_t start = (uint64_t)(k0 + kk) * kTcpChunk;
-            const uint64_t end = min(start + kTcpChunk, v.len);
-            uint64_t pos = start + s_entry[kk];
-            uint32_t done = 0;
-            while (done < nfk) {
-                if (lane == 0) {
-                    uint32_t mm = 0;
-                    uint64_t q = pos;
-                    while (mm < 64 && q < end) {
-                        uint32_t flen = 0;
-                        if (tcp_step(v, q, flen) != kWalkRun) break;
-                        s_pos[wid][mm++] = q;
-                        q += flen;
-                    }
-                    s_m[wid] = mm;
-                    s_next[wid] = q;
-                }
-                wave_sync();
-                const uint32_t m = s_m[wid];
-                pos = s_next[wid];
-                if ((uint32_t)lane < m) emit(s_base + s_exit[kk] + done + lane, s_pos[wid][lane]);
-                done += m;
-                wave_sync();
-                if (m == 0) break;
-            }
-        }
-        __syncthreads();
-    }
-    // a frame that starts in the carried bytes: staged contiguously (the only one per session)
-    const uint64_t sp = s_stage;
-    if (sp != ~0ull) {
-        uint32_t flen = 0;
-        tcp_step(v, sp, flen);
-        uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
-        for (uint32_t b = tid; b < ((flen + 15) & ~15u); b += 256)
-            dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
     }
 }
 
-// ---- k_tcp_finish: one workgroup per session; carry + per-read results ----
-// After k_ingest: the carry is rewritten only once every kernel that reads it is done.
-__global__ __launch_bounds__(256) void k_tcp_finish(TcpParams P) {
-    const uint32_t g = blockIdx.x;
-    const int tid = threadIdx.x;
-    const TcpGroup G = P.groups[g];
+// ---- k_tcp_scan: one 1024-thread workgroup; sessions -> ingest segments ----
+// Each thread takes a run of consecutive sessions (one for up to 1024 sessions): all frame
+// counts are loaded at once, one block scan places them.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_tcp_scan(TcpParams P) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int NW = kScanThreads / 64;
+    __shared__ uint32_t s_w[NW];
+    const uint32_t per = (P.ngroups + kScanThreads - 1) / kScanThreads;
+    const uint32_t g0 = tid * per, g1 = min(g0 + per, P.ngroups);
+    uint32_t mine = 0;
+    for (uint32_t g = g0; g < g1; g++) mine += P.groups[g].nframes;
+    uint32_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t base = 0, fb = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const uint32_t t = s_w[w];
+        if (w < wid) base += t;
+        fb += t;
+    }
+    const bool over = fb > P.max_desc;
+    uint32_t at = base + x - mine;
+    for (uint32_t g = g0; g < g1; g++) {
+        const uint32_t nf = P.groups[g].nframes;
+        P.groups[g].frame_base = at;
+        P.seg_off[g] = over ? 0u : at;
+        P.seg_sess[g] = P.groups[g].session;
+        at += nf;
+    }
+    if (tid == 0) {
+        P.seg_off[P.ngroups] = over ? 0u : fb;
+        P.tot->frames = fb;
+        P.tot->status = over ? EDGPU_OUT_OVERFLOW : 0;
+    }
+}
+
+// ---- k_tcp_emit: one wave per chunk; frames -> descriptors + source addresses ----
+// The wave of a session's first chunk then finishes the session (what a separate pass did after
+// k_ingest): it carries the partial frame -- only that wave reads the carried bytes, and its
+// staging copy is done by then -- and fills the per-read report.  A session with no stream
+// bytes has no chunk; its report is the zeros the host cleared.
+__global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
+    const uint32_t c = blockIdx.x;
+    const int lane = threadIdx.x;
     const bool over = P.tot->status != 0;
+    const TcpChunkRes R = P.chunkres[c];
+    const uint32_t g = P.chunk_group[c];
+    const TcpGroup G = P.groups[g];
     const TcpView v = tcp_view(P, G);
+    const TcpRead* rd = P.reads + G.first_read;
+    __shared__ uint64_t s_pos[64];
+    __shared__ uint32_t s_m;
+    __shared__ uint64_t s_next;
+    __shared__ uint64_t s_stage;           // stream position of a frame to stage, ~0: none
+    // the session's read starts and arrivals (up to 64 reads) in LDS: a frame's read is found by
+    // a binary search there instead of a chain of dependent global loads
+    __shared__ uint64_t s_rstart[64];
+    __shared__ int64_t s_rarr[64];
     __shared__ uint8_t s_carry[kTcpCarry];
+    if (!over && R.entry != kTcpNone) {                       // uniform
+        const uint64_t start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
+        const uint64_t end = min(start + kTcpChunk, v.len);
+        const bool lds_reads = G.nreads <= 64;
+        if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
+        if (lane == 0) s_stage = ~0ull;
+        __syncthreads();
+        const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
+        const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
+        uint32_t done = 0;
+        uint64_t pos = start + R.entry;
+        while (done < R.nframes) {
+            uint32_t m;
+            if (recorded) {
+                m = min(64u, R.nframes - done);
+            } else {                                          // re-walk: the next up to 64 frames
+                if (lane == 0) {
+                    uint32_t mm = 0;
+                    uint64_t p = pos;
+                    while (mm < 64 && p < end) {
+                        uint32_t flen = 0;
+                        if (tcp_step(v, p, flen) != kWalkRun) break;
+                        s_pos[mm++] = p;
+                        p += flen;
+                    }
+                    s_m = mm;
+                    s_next = p;
+                }
+                __syncthreads();
+                m = s_m;
+                pos = s_next;
+            }
+            if ((uint32_t)lane < m) {
+                const uint64_t p = recorded ? start + rec[done + lane] : s_pos[lane];
+                uint32_t flen = 0;
+                tcp_step(v, p, flen);
+                const uint64_t last = p + flen - 1;
+                int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t fi = G.frame_base + R.fbase + done + lane;
+                edgpu_pkt_desc d;
+                d.slot = 0;
+                d.len = (uint16_t)(flen - 4);
+                d.channel = (uint8_t)tbyte(v, p + 1);
+                d.flags = 0;
+                d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
+                P.desc[fi] = d;
+                const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
+                if (p < v.clen) s_stage = p;
+                P.src_addr[fi] = (uint64_t)(uintptr_t)a;
+                atomicAdd(&P.results[G.first_read + lo].frames, 1u);
+            }
+            done += m;
+            __syncthreads();
+            if (m == 0) break;
+        }
+        // a frame that starts in the carried bytes: staged contiguously (the only one per session)
+        const uint64_t sp = s_stage;
+        if (sp != ~0ull) {
+            uint32_t flen = 0;
+            tcp_step(v, sp, flen);
+            uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
+            for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
+                dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
+        }
+    }
+    if (c != G.first_chunk) return;                           // uniform
+    // ---- the session's finish: carry + per-read results ----
     const uint32_t code = G.code;
     const uint64_t stop = G.stop;
     uint32_t ncarry = 0;
     if (!over && code == kWalkPartial) ncarry = (uint32_t)(v.len - stop);
     if (over) ncarry = G.carry_len;
     if (!over) {
-        for (uint32_t b = tid; b < ncarry; b += 256) s_carry[b] = (uint8_t)tbyte(v, stop + b);
+        __syncthreads();                                      // the staging above has read the carry
+        for (uint32_t b = lane; b < ncarry; b += 64) s_carry[b] = (uint8_t)tbyte(v, stop + b);
         __syncthreads();
         uint8_t* dst = P.carry + (uint64_t)G.session * kTcpCarry;
-        for (uint32_t b = tid; b < ncarry; b += 256) dst[b] = s_carry[b];
+        for (uint32_t b = lane; b < ncarry; b += 64) dst[b] = s_carry[b];
     }
-    for (uint32_t i = tid; i < G.nreads; i += 256) {
+    for (uint32_t i = lane; i < G.nreads; i += 64) {
         const TcpRead r = P.reads[G.first_read + i];
         edgpu_tcp_result& o = P.results[G.first_read + i];
         uint32_t consumed = r.len;
@@ -655,17 +665,12 @@ __global__ __launch_bounds__(256) void k_tcp_finish(TcpParams P) {
 }
 
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
-    // at least one walk block: block 0 clears the call's totals (the sessions claim their frame
-    // ranges from them)
-    const uint32_t per = kWalkWaves * kTcpWalkCpw;
-    hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3(std::max<uint32_t>(1u, (p.nchunks + per - 1) / per)),
-                       dim3(64 * kWalkWaves), 0, st, p);
+    if (p.nchunks)
+        hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
+                           dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st) {
-    hipLaunchKernelGGL(k_tcp_finish, dim3(p.ngroups), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
+    if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);
     return hipGetLastError();
 }
 

@@ -31,7 +31,6 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
-hipError_t launch_deframe_finish(const TcpParams& p, hipStream_t st);
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
                                hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
@@ -206,7 +205,6 @@ struct edgpu_ctx {
     edgpu_pkt_desc* d_desc = nullptr;
     uint32_t* d_seg = nullptr;
     uint32_t* d_seg_sess = nullptr;
-    uint32_t* d_seg_end = nullptr;      // interleaved ingest: each session's claimed descriptor range end
     uint8_t* d_blob = nullptr;
     uint32_t* d_pflags = nullptr;
     uint64_t* d_pidx = nullptr;
@@ -226,7 +224,6 @@ struct edgpu_ctx {
     int pend_stage = -1;                    // staging set of the batch pending a keyframe index
     // pending batch for keyframe_index
     const uint32_t* pend_seg = nullptr;
-    const uint32_t* pend_seg_end = nullptr;     // interleaved batches: per-segment ends
     const uint32_t* pend_seg_sess = nullptr;
     uint32_t pend_nseg = 0;
     bool pending = false;
@@ -375,7 +372,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
     if (x->d_img_status) (void)hipFree(x->d_img_status);
-    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_end, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
+    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
                     (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
         if (p) (void)hipFree(p);
@@ -1045,14 +1042,12 @@ static int rebuild_index(edgpu_ctx* x) {
 }
 
 // Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
-// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first
-// and k_tcp_finish after, all inside the ingest timing events.
+// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
+// inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
                           uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr) {
     IngestParams p;
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
-    p.seg_end = tcp ? tcp->seg_end : nullptr;
-    p.skip_if = tcp ? &tcp->tot->status : nullptr;
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
@@ -1064,11 +1059,10 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     HIP_CHECK(hist_mark(x, 2, 0));
     if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
-    if (tcp) HIP_CHECK(launch_deframe_finish(*tcp, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
     x->kf_share = tcp == nullptr;       // the interleaved path syncs and reads back results next
-    x->pend_seg = ds; x->pend_seg_end = p.seg_end; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
+    x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
     return EDGPU_OK;
 }
 
@@ -1235,7 +1229,6 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
         i = j;
     }
     const uint32_t ng = (uint32_t)groups.size(), nc = (uint32_t)chunk_group.size();
-    if (ng > x->cfg.max_batch_packets) return fail(EDGPU_BAD_ARGUMENT, "more sessions in reads than max_batch_packets");
     HIP_CHECK(x->d_carry.reserve((size_t)x->sessions.size() * kTcpCarry, x->stream));
     HIP_CHECK(x->d_tcp_groups.reserve(ng, x->stream));
     HIP_CHECK(x->d_tcp_reads.reserve(n, x->stream));
@@ -1250,8 +1243,6 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
-    if (!x->d_seg_end && dmalloc(&x->d_seg_end, sizeof(uint32_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
-        return fail(EDGPU_OUT_OF_MEMORY, "segment ends");
     const uint8_t* raw = bytes;
     if (where == EDGPU_PTR_HOST) {
         if (!x->d_tcp_raw && dmalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
@@ -1272,7 +1263,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.carry = x->d_carry.ptr;
     p.offs = x->d_tcp_offs.ptr; p.stage = x->d_tcp_stage.ptr;
     p.desc = x->d_desc; p.src_addr = x->d_tcp_src; p.max_desc = x->cfg.max_batch_packets;
-    p.seg_off = x->d_seg; p.seg_end = x->d_seg_end; p.seg_sess = x->d_seg_sess;
+    p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
     int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p);
     if (r) return r;
@@ -1317,8 +1308,7 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     if (!x->pending) return fail(EDGPU_ERR, "no ingested batch pending a keyframe index");
     HIP_CHECK(hipSetDevice(x->device));
     KeyframeParams p;
-    p.seg_off = x->pend_seg; p.seg_end = x->pend_seg_end; p.seg_sess = x->pend_seg_sess;
-    p.pflags = x->d_pflags; p.pidx = x->d_pidx;
+    p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.totals = x->d_totals;
     // the index starts where the ingest it indexes ended when the host did nothing in between
     // (that point is already recorded: an event record costs the GPU ~5 us of idle), else here

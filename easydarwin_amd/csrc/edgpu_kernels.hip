@@ -279,8 +279,7 @@ template <uint32_t DEPTH, int THREADS = kIngestThreads>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_ingest(IngestParams P) {
     constexpr int NW = THREADS / 64;
     const uint32_t seg = blockIdx.x;
-    if (P.skip_if && *P.skip_if) return;                    // uniform
-    const uint32_t b = P.seg_off[seg], e = P.seg_end ? P.seg_end[seg] : P.seg_off[seg + 1];
+    const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
     const SessionDev S = P.sessions[P.seg_sess[seg]];
     const uint32_t nsnd = 2 * S.ntracks;
     const int tid = threadIdx.x;
@@ -592,7 +591,7 @@ __device__ __forceinline__ void mark_ingest_totals(TickTotals* t) {
 __global__ __launch_bounds__(64) void k_keyframe(KeyframeParams P) {
     const uint32_t seg = blockIdx.x;
     if (seg == 0 && threadIdx.x == 0) mark_ingest_totals(P.totals);   // the ingest has finished
-    const uint32_t b = P.seg_off[seg], e = P.seg_end ? P.seg_end[seg] : P.seg_off[seg + 1];
+    const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
     const uint32_t sess = P.seg_sess[seg];
     const SessionDev S = P.sessions[sess];
     const int lane = threadIdx.x;

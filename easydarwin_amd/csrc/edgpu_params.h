@@ -32,9 +32,7 @@ constexpr uint32_t kTcpFramesPerRound = EDGPU_TCP_TD;
 struct IngestParams {
     const edgpu_pkt_desc* desc;
     const uint32_t* seg_off;
-    const uint32_t* seg_end;    // per segment end, or null: segment s is [seg_off[s], seg_off[s + 1])
     const uint32_t* seg_sess;
-    const int32_t* skip_if;     // nonzero at run time: ingest nothing (an interleaved batch over capacity)
     const uint8_t* blob;
     const uint64_t* src_addr;   // per desc: device address of the frame ('$' header first, any
                                 // alignment) instead of blob + slot * 16 (interleaved ingest); or null
@@ -59,7 +57,6 @@ struct IngestParams {
 
 struct KeyframeParams {
     const uint32_t* seg_off;
-    const uint32_t* seg_end;    // as IngestParams.seg_end
     const uint32_t* seg_sess;
     const uint32_t* pflags;
     const uint64_t* pidx;
@@ -146,6 +143,8 @@ struct TcpGroup {           // one pusher connection's reads in this call
     // k_tcp_resolve
     uint32_t nframes, code;
     uint64_t stop;          // stream position where the walk ended (len: everything framed)
+    // k_tcp_scan
+    uint32_t frame_base, _pad;
 };
 
 struct TcpRead { uint64_t start; int64_t arrival; uint32_t len, _pad; };   // start: stream position
@@ -170,8 +169,7 @@ struct TcpParams {
     edgpu_pkt_desc* desc;
     uint64_t* src_addr;     // per frame: its address for k_ingest (IngestParams.src_addr)
     uint32_t max_desc;
-    uint32_t* seg_off;      // per session group: its claimed range of descriptors [seg_off, seg_end)
-    uint32_t* seg_end;
+    uint32_t* seg_off;      // ngroups + 1
     uint32_t* seg_sess;
     edgpu_tcp_result* results;
     TcpTotals* tot;
