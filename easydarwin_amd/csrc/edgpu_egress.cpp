@@ -79,9 +79,8 @@ struct edgpu_egress {
     std::map<uint32_t, TcpConn> tcp;    // subscriber
     uint8_t* h_arena = nullptr;         // pinned: the tick's bytes (whole arena, or the gathered regions)
     size_t h_arena_cap = 0;
-    void* d_gather = nullptr;           // device staging of the gathered regions
-    uint64_t d_gather_cap = 0;
-    std::vector<edgpu_out_desc> desc;
+    edgpu_out_desc* desc = nullptr;     // pinned: the tick's descriptors
+    uint64_t desc_cap = 0;
     std::vector<edgpu_substream_out> subs;
     std::vector<const uint8_t*> base;   // per sub-stream: host address of its arena region's start
     std::vector<Worker> workers;
@@ -145,7 +144,7 @@ static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
     const int k = s.kind ? 1 : 0;
     const uint8_t* base = e->base[q] - s.out_base;
     const int fd = d.fd[k] >= 0 ? d.fd[k] : w.udp_fd;
-    const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
+    const edgpu_out_desc* ds = e->desc + s.desc_base;
     if (!e->gso || !w.gso) { send_udp_plain(w, fd, &d.addr[k], base, ds, s.desc_count); return; }
     constexpr uint32_t kMsgs = 64, kSegs = 64, kMaxPayload = 65507, kMaxSeg = 1472;
     struct Msg { uint32_t first, n, seg; };
@@ -220,7 +219,7 @@ static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
 // buffered tail goes first; frames the socket took (the last one possibly in part, its tail
 // then buffered) are sent; the first frame that gets no byte blocks the sub-stream.
 static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, TcpConn& c) {
-    const edgpu_out_desc* ds = e->desc.data() + s.desc_base;
+    const edgpu_out_desc* ds = e->desc + s.desc_base;
     const uint8_t* base = e->base[q] - s.out_base;
     if (c.dead) return;                                   // counted as written, never resent
     uint32_t i = 0;
@@ -302,7 +301,7 @@ int edgpu_egress_destroy(edgpu_egress* e) {
     if (!e) return EDGPU_OK;
     for (Worker& w : e->workers) if (w.udp_fd >= 0) close(w.udp_fd);
     if (e->h_arena) (void)hipHostFree(e->h_arena);
-    if (e->d_gather) (void)edgpu_device_free(e->ctx, e->d_gather);
+    if (e->desc) (void)hipHostFree(e->desc);
     delete e;
     return EDGPU_OK;
 }
@@ -338,9 +337,17 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     int rc = edgpu_tick_stats_get(e->ctx, &st);
     if (rc) return eg_fail(e, rc, "tick stats");
     if (st.status) return eg_fail(e, st.status, "device-side status after fan-out");
-    e->desc.resize(st.relayed_packets);
+    if (st.relayed_packets > e->desc_cap) {
+        if (e->desc) (void)hipHostFree(e->desc);
+        e->desc = nullptr;
+        e->desc_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(st.relayed_packets, 1 << 16);
+        if (hipHostMalloc((void**)&e->desc, cap * sizeof(edgpu_out_desc), hipHostMallocDefault) != hipSuccess)
+            return eg_fail(e, EDGPU_OUT_OF_MEMORY, "pinned descriptors");
+        e->desc_cap = cap;
+    }
     e->subs.resize(r->n_substreams);
-    if ((rc = edgpu_copy_to_host(e->ctx, e->desc.data(), r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
+    if ((rc = edgpu_copy_to_host(e->ctx, e->desc, r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
         (rc = edgpu_copy_to_host(e->ctx, e->subs.data(), r->substreams, r->n_substreams * sizeof(edgpu_substream_out))))
         return eg_fail(e, rc, "copy to host");
     // the distinct bytes: one region per identity sender (its longest sub-stream) + every other
@@ -362,16 +369,9 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     }
     e->base.assign(nq, nullptr);
     if (e->dedup) {
-        if (need > e->d_gather_cap) {
-            if (e->d_gather) (void)edgpu_device_free(e->ctx, e->d_gather);
-            e->d_gather = nullptr;
-            e->d_gather_cap = 0;
-            if ((rc = edgpu_device_alloc(e->ctx, need, &e->d_gather))) return eg_fail(e, rc, "gather buffer");
-            e->d_gather_cap = need;
-        }
-        if ((rc = edgpu_arena_gather(e->ctx, r, tr.reg.data(), (uint32_t)tr.reg.size(), e->d_gather, e->d_gather_cap)) ||
-            (rc = edgpu_copy_to_host(e->ctx, e->h_arena, e->d_gather, need)))
-            return eg_fail(e, rc, "gather / copy to host");
+        // gathered straight into the pinned buffer: the kernel's stores cross PCIe (one pass)
+        if ((rc = edgpu_arena_gather(e->ctx, r, tr.reg.data(), (uint32_t)tr.reg.size(), e->h_arena, e->h_arena_cap)))
+            return eg_fail(e, rc, "gather to host");
         for (uint32_t q = 0; q < nq; q++)
             if (tr.src[q].first != edgpu_host::TickRegions::kNone) e->base[q] = tr.at(e->h_arena, q);
     } else {

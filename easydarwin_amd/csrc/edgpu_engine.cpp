@@ -35,6 +35,7 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
                                hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
+hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hipStream_t st);
 int fanout_chunk(int variant);
 int fanout_default(bool patching);
 bool fanout_rewrites(int variant);
@@ -424,7 +425,16 @@ struct Readback {
             used += (bytes + 15) & ~size_t(15);
             return e;
         }
+        // a large read into pinned memory: a copy kernel storing over PCIe beats the DMA copy
+        if (bytes >= kKernelCopyBytes && !(((uintptr_t)dst | (uintptr_t)src) & 15) && is_pinned(dst))
+            return launch_copy_to_pinned(dst, src, bytes, x->stream);
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream);
+    }
+    static constexpr size_t kKernelCopyBytes = 256 << 10;
+    static bool is_pinned(const void* p) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+        return a.type == hipMemoryTypeHost;
     }
     hipError_t run() {
         hipError_t e = hipStreamSynchronize(x->stream);

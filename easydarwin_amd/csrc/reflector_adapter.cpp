@@ -28,7 +28,6 @@ Reflector::~Reflector() {
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
     for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinArr})
         if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
-    if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
     edgpu_ctx_destroy(fCtx);
 }
 
@@ -302,12 +301,6 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
     // the tick's distinct bytes only: one region per identity sender + the other sub-streams
     const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq);
-    if (tr.bytes > fDevOutCap) {
-        if (fDevOut) (void)edgpu_device_free(fCtx, fDevOut);
-        fDevOut = nullptr; fDevOutCap = 0;
-        if ((err = edgpu_device_alloc(fCtx, tr.bytes, &fDevOut))) return err;
-        fDevOutCap = tr.bytes;
-    }
     if (tr.bytes > fHostOutCap) {
         if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
         fHostOut = nullptr; fHostOutCap = 0;
@@ -316,8 +309,8 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fHostOut = (uint8_t*)h;
         fHostOutCap = std::max<uint64_t>(tr.bytes, 1 << 20);
     }
-    if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fDevOut, fDevOutCap))) return err;
-    if ((err = edgpu_copy_to_host(fCtx, fHostOut, fDevOut, tr.bytes))) return err;
+    // gathered straight into the pinned buffer: the kernel's stores cross PCIe (one pass)
+    if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fHostOut, fHostOutCap))) return err;
     fTick.readback_bytes = tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
     const int64_t* arrival = nullptr;
     if (sink->WantsArrivals()) {
@@ -356,9 +349,10 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     // sub-stream for the tick; the engine bookmarks the blocked packet (reports in sub-stream order)
     std::vector<edgpu_blocked> blocked;
     for (uint32_t k = 0; k < nw; k++) {
-        fTick.writes += job.writes[k];
-        if (job.err[k]) return job.err[k];
-        blocked.insert(blocked.end(), job.blocked[k].begin(), job.blocked[k].end());
+        const WriteJob::Result& r = job.out[k];
+        fTick.writes += r.writes;
+        if (r.err) return r.err;
+        blocked.insert(blocked.end(), r.blocked.begin(), r.blocked.end());
     }
     fTick.write_ms = ms_since(t0);
     if (blocked.empty()) return kNoErr;
@@ -378,9 +372,10 @@ static inline uint32_t writer_of(const edgpu_substream_out& q, uint32_t nworkers
 // The writes of the subscribers of one worker, sub-stream by sub-stream in table order (the order
 // one thread takes): a write that would block stops that sub-stream.
 void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers) {
-    j.writes[worker] = 0;
-    j.err[worker] = kNoErr;
-    j.blocked[worker].clear();
+    WriteJob::Result& r = j.out[worker];
+    r.err = kNoErr;
+    r.blocked.clear();
+    uint64_t writes = 0;
     for (uint32_t s = 0; s < j.nsubs; s++) {
         const edgpu_substream_out& q = j.subs[s];
         if (!q.desc_count || (nworkers > 1 && writer_of(q, nworkers) != worker)) continue;
@@ -399,12 +394,13 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
             w.sender = q.sender;
             w.newOutput = (q.flags & EDGPU_SUB_NEW) != 0;
             w.worker = worker;
-            j.writes[worker]++;
+            writes++;
             const int err = j.sink->Write(w);
-            if (err == kWouldBlock) { j.blocked[worker].push_back(edgpu_blocked{s, i}); break; }
-            if (err) { j.err[worker] = err; return; }
+            if (err == kWouldBlock) { r.blocked.push_back(edgpu_blocked{s, i}); break; }
+            if (err) { r.err = err; r.writes = writes; return; }
         }
     }
+    r.writes = writes;
 }
 
 void Reflector::WorkerLoop(uint32_t worker) {

@@ -191,9 +191,10 @@ private:
         const edgpu_out_desc* desc; const int64_t* arrival;
         const uint8_t* host; const edgpu_host::TickRegions* regions;   // the tick's bytes
         OutputSink* sink;
-        std::vector<edgpu_blocked> blocked[64];
-        uint64_t writes[64];
-        int err[64];
+        // one line per worker: the writers' results must not share a cache line (a per-packet
+        // counter in a shared line serialised the write threads)
+        struct alignas(64) Result { std::vector<edgpu_blocked> blocked; uint64_t writes = 0; int err = 0; };
+        Result out[64];
     };
     void WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers);
     void WorkerLoop(uint32_t worker);
@@ -209,8 +210,7 @@ private:
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
     PinBuf fPinSubs, fPinDesc, fPinArr;                     // sub-stream table, descriptors, arrivals
-    uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes
-    void* fDevOut = nullptr; uint64_t fDevOutCap = 0;       // device: edgpu_arena_gather target
+    uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes (edgpu_arena_gather target)
     TickInfo fTick;
     // write threads (workers 1..n-1; the ticking thread is worker 0)
     uint32_t fNumWriters = 1;

@@ -29,6 +29,7 @@ def module_run(args) -> dict:
     # one tick carries every session's IDR at once (all GOPs start together): 1024 x 16 x ~150 KB
     env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
     env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
+    env.setdefault("EDGPU_QTSS_WRITE_THREADS", str(args.write_threads))
     cmd = [os.path.join(ROOT, "tools", "qtss_replay"), os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"),
            "--bench", str(args.sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
@@ -57,6 +58,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--tick-ms", type=int, default=100)
     ap.add_argument("--threads", type=int, default=8)
+    # QTSS_Write threads: the box's CPU share is 16 (the reference baseline runs 16 processes)
+    ap.add_argument("--write-threads", type=int, default=16)
     ap.add_argument("--arena-mb", type=int, default=4096)
     ap.add_argument("--max-out-packets", type=int, default=4 << 20)
     ap.add_argument("--timeout", type=int, default=300)
@@ -64,6 +67,7 @@ def main():
     args = ap.parse_args()
     out = {"workload": f"C2 through the QTSS module: {args.sessions} RTSP-interleaved H.264 pushers x {args.subs} "
                        f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads",
+           "write_threads": int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads)),
            "module": module_run(args)}
     m = out["module"]
     pt = m["per_tick_bytes"]
