@@ -341,7 +341,7 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
         if (e->desc) (void)hipHostFree(e->desc);
         e->desc = nullptr;
         e->desc_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(st.relayed_packets, 1 << 16);
+        const uint64_t cap = std::max<uint64_t>(st.relayed_packets + st.relayed_packets / 2, 1 << 16);
         if (hipHostMalloc((void**)&e->desc, cap * sizeof(edgpu_out_desc), hipHostMallocDefault) != hipSuccess)
             return eg_fail(e, EDGPU_OUT_OF_MEMORY, "pinned descriptors");
         e->desc_cap = cap;
@@ -362,7 +362,7 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     if (need > e->h_arena_cap) {
         if (e->h_arena) (void)hipHostFree(e->h_arena);
         e->h_arena = nullptr;
-        const size_t cap = std::max<size_t>(need, 1 << 20);
+        const size_t cap = std::max<size_t>(need + need / 2, 1 << 20);   // geometric: pinning is slow
         if (hipHostMalloc((void**)&e->h_arena, cap, hipHostMallocDefault) != hipSuccess)
             return eg_fail(e, EDGPU_OUT_OF_MEMORY, "pinned arena");
         e->h_arena_cap = cap;

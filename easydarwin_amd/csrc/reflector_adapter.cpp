@@ -301,13 +301,14 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
     // the tick's distinct bytes only: one region per identity sender + the other sub-streams
     const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq);
-    if (tr.bytes > fHostOutCap) {
+    if (tr.bytes > fHostOutCap) {            // grown geometrically: pinning costs ~40 ms per call
         if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
         fHostOut = nullptr; fHostOutCap = 0;
         void* h = nullptr;
-        if ((err = edgpu_host_alloc(fCtx, std::max<uint64_t>(tr.bytes, 1 << 20), &h))) return err;
+        const uint64_t cap = std::max<uint64_t>(tr.bytes + tr.bytes / 2, 1 << 20);
+        if ((err = edgpu_host_alloc(fCtx, cap, &h))) return err;
         fHostOut = (uint8_t*)h;
-        fHostOutCap = std::max<uint64_t>(tr.bytes, 1 << 20);
+        fHostOutCap = cap;
     }
     // gathered straight into the pinned buffer: the kernel's stores cross PCIe (one pass)
     if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fHostOut, fHostOutCap))) return err;

@@ -9,7 +9,7 @@
 #pragma once
 #include <stdint.h>
 
-#include <map>
+#include <algorithm>
 #include <utility>
 #include <vector>
 
@@ -31,25 +31,29 @@ struct TickRegions {
 inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
     TickRegions t;
     t.src.assign(nq, {TickRegions::kNone, 0});
-    std::map<uint32_t, uint32_t> rep;                   // sender -> its longest identity sub-stream
+    // per sender (engine sender ids are dense): its longest identity sub-stream, its region
+    uint32_t nsend = 0;
+    for (uint32_t q = 0; q < nq; q++)
+        if (subs[q].desc_count && (subs[q].flags & EDGPU_SUB_IDENTITY)) nsend = std::max(nsend, subs[q].sender + 1);
+    std::vector<uint32_t> rep(nsend, TickRegions::kNone), rep_reg(nsend, TickRegions::kNone);
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];
         if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
-        auto it = rep.find(s.sender);
-        if (it == rep.end() || subs[it->second].out_bytes < s.out_bytes) rep[s.sender] = q;
+        uint32_t& r = rep[s.sender];
+        if (r == TickRegions::kNone || subs[r].out_bytes < s.out_bytes) r = q;
     }
-    std::map<uint32_t, uint32_t> rep_reg;               // sender -> region index
+    t.reg.reserve(nq);
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];
         if (!s.desc_count) continue;
         if (s.flags & EDGPU_SUB_IDENTITY) {
             const edgpu_substream_out& R = subs[rep[s.sender]];
-            auto it = rep_reg.find(s.sender);
-            if (it == rep_reg.end()) {
-                it = rep_reg.emplace(s.sender, (uint32_t)t.reg.size()).first;
+            uint32_t& g = rep_reg[s.sender];
+            if (g == TickRegions::kNone) {
+                g = (uint32_t)t.reg.size();
                 t.reg.push_back(edgpu_region{R.out_base, R.out_bytes});
             }
-            t.src[q] = {it->second, R.out_bytes - s.out_bytes};   // q is a suffix of the longest
+            t.src[q] = {g, R.out_bytes - s.out_bytes};      // q is a suffix of the longest
         } else {
             t.src[q] = {(uint32_t)t.reg.size(), 0};
             t.reg.push_back(edgpu_region{s.out_base, s.out_bytes});
