@@ -164,7 +164,8 @@ private:
     // pushers of different sessions share no lock and no counter per packet.
     static constexpr uint32_t kStripes = 16;
     static constexpr uint64_t kSlab = 64 << 10;
-    struct Stripe {                                         // one stripe's part of a batch
+    struct alignas(64) Stripe {                             // one stripe's part of a batch (own lines:
+                                                            // its counters change per packet)
         std::vector<Pushed> pushed;                         // arrival order (per session)
         std::vector<edgpu_udp_source> sources;              // UDP datagrams' sources, same order
         uint64_t slab = 0, used = 0, cap = 0;               // the current slab: blob offset, used, size

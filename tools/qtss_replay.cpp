@@ -407,7 +407,6 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             rp.rtspIncomingDataParams.inClientSession = client[s];
             rp.rtspIncomingDataParams.inPacketData = fr.data();
             rp.rtspIncomingDataParams.inPacketLen = len + 4;
-            advance_clock(t);
             (void)g_dispatch(QTSS_RTSPIncomingData_Role, &rp);
         };
         auto nal = [&](uint8_t h, uint32_t n, bool last) {     // single NAL or FU-A fragments
@@ -421,6 +420,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                 off += k;
             }
         };
+        advance_clock(t);           // once per frame: the shared clock is one contended line
         if (P.frame % gop == 0) { nal(0x67, 24, false); nal(0x68, 8, false); nal(0x65, idr, true); }
         else nal(0x41, p_frame, true);
         P.frame++;
