@@ -17,13 +17,13 @@
 //   k_tcp_resolve  one workgroup per session: follows the links in LDS (one hop per chunk),
 //                  scans the chunks' frame counts.
 //   k_tcp_scan     sessions -> ingest segments, capacity check (one workgroup).
-//   k_tcp_emit     one wave per chunk: a descriptor and a source address per frame of the true
-//                  walk (lanes in parallel from the recorded starts); the frame bytes stay where
-//                  they are -- k_ingest copies them from the TCP bytes into the sender rings
-//                  (IngestParams.src_addr).  Only a frame that starts in the carried bytes is
-//                  staged (contiguous copy).
-//                  The wave of a session's first chunk then carries the partial frame and
-//                  fills the per-read report.
+//   k_tcp_finish   one wave per session: descriptors for the chunks the walk did not record
+//                  (re-walked), the staging of a frame that starts in the carried bytes, the new
+//                  carry and the per-read report.
+// k_ingest then finds every recorded frame itself -- its chunk from the per-chunk frame ends,
+// its start from the walk's records, its length and channel from its '$' header -- and copies
+// it out of the TCP bytes into the sender rings (IngestParams.tcp_groups): no per-frame
+// descriptor pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "edgpu.h"
@@ -539,46 +539,51 @@ __global__ __launch_bounds__(kScanThreads) void k_tcp_scan(TcpParams P) {
     }
 }
 
-// ---- k_tcp_emit: one wave per chunk; frames -> descriptors + source addresses ----
-// The wave of a session's first chunk then finishes the session (what a separate pass did after
-// k_ingest): it carries the partial frame -- only that wave reads the carried bytes, and its
-// staging copy is done by then -- and fills the per-read report.  A session with no stream
-// bytes has no chunk; its report is the zeros the host cleared.
-__global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
-    const uint32_t c = blockIdx.x;
+// ---- k_tcp_finish: one wave per session ----
+// k_ingest finds the frames of every chunk whose true walk was recorded itself (IngestParams.
+// tcp_groups).  This wave does the rest of the session: a descriptor and a source address per
+// frame of the chunks the walk did not record (re-walked here: a chunk entered by the sequential
+// fallback, or with more than kTcpFrames frames) and their per-read frame counts; the staging of
+// a frame that starts in the carried bytes (only the stream's first frame can), then the new
+// carry -- only this wave reads the carried bytes after the walk -- and the per-read report.
+// A session with no stream bytes has no chunk; its report is the zeros the host cleared.
+__global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
+    const uint32_t g = blockIdx.x;
     const int lane = threadIdx.x;
     const bool over = P.tot->status != 0;
-    const TcpChunkRes R = P.chunkres[c];
-    const uint32_t g = P.chunk_group[c];
     const TcpGroup G = P.groups[g];
     const TcpView v = tcp_view(P, G);
     const TcpRead* rd = P.reads + G.first_read;
     __shared__ uint64_t s_pos[64];
     __shared__ uint32_t s_m;
     __shared__ uint64_t s_next;
-    __shared__ uint64_t s_stage;           // stream position of a frame to stage, ~0: none
     // the session's read starts and arrivals (up to 64 reads) in LDS: a frame's read is found by
     // a binary search there instead of a chain of dependent global loads
     __shared__ uint64_t s_rstart[64];
     __shared__ int64_t s_rarr[64];
     __shared__ uint8_t s_carry[kTcpCarry];
-    if (!over && R.entry != kTcpNone) {                       // uniform
-        const uint64_t start = (uint64_t)(c - G.first_chunk) * kTcpChunk;
-        const uint64_t end = min(start + kTcpChunk, v.len);
-        const bool lds_reads = G.nreads <= 64;
-        if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
-        if (lane == 0) s_stage = ~0ull;
-        __syncthreads();
-        const bool recorded = R.cand != kTcpNone && R.nframes <= kTcpFrames;
-        const uint16_t* rec = P.offs + ((size_t)c * kTcpCands + (recorded ? R.cand : 0u)) * kTcpFrames;
-        uint32_t done = 0;
-        uint64_t pos = start + R.entry;
-        while (done < R.nframes) {
-            uint32_t m;
-            if (recorded) {
-                m = min(64u, R.nframes - done);
-            } else {                                          // re-walk: the next up to 64 frames
-                if (lane == 0) {
+    const bool lds_reads = G.nreads <= 64;
+    if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
+    __syncthreads();
+    for (uint32_t k0 = 0; !over && k0 < G.nchunks; k0 += 64) {
+        // the chunks the walk did not record, 64 at a time
+        const uint32_t k = k0 + (uint32_t)lane;
+        bool rewalk = false;
+        if (k < G.nchunks) {
+            const TcpChunkRes R = P.chunkres[G.first_chunk + k];
+            rewalk = R.entry != kTcpNone && (R.cand == kTcpNone || R.nframes > kTcpFrames);
+        }
+        uint64_t todo = __ballot(rewalk);
+        while (todo) {
+            const uint32_t kk = k0 + (uint32_t)(__ffsll((unsigned long long)todo) - 1);
+            todo &= todo - 1;
+            const TcpChunkRes R = P.chunkres[G.first_chunk + kk];
+            const uint64_t start = (uint64_t)kk * kTcpChunk;
+            const uint64_t end = min(start + kTcpChunk, v.len);
+            uint32_t done = 0;
+            uint64_t pos = start + R.entry;
+            while (done < R.nframes) {
+                if (lane == 0) {                              // the next up to 64 frames
                     uint32_t mm = 0;
                     uint64_t p = pos;
                     while (mm < 64 && p < end) {
@@ -591,48 +596,49 @@ __global__ __launch_bounds__(64) void k_tcp_emit(TcpParams P) {
                     s_next = p;
                 }
                 __syncthreads();
-                m = s_m;
+                const uint32_t m = s_m;
                 pos = s_next;
-            }
-            if ((uint32_t)lane < m) {
-                const uint64_t p = recorded ? start + rec[done + lane] : s_pos[lane];
-                uint32_t flen = 0;
-                tcp_step(v, p, flen);
-                const uint64_t last = p + flen - 1;
-                int lo = 0, hi = (int)G.nreads - 1;              // last read starting at or before `last`
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
+                if ((uint32_t)lane < m) {
+                    const uint64_t p = s_pos[lane];
+                    uint32_t flen = 0;
+                    tcp_step(v, p, flen);
+                    const uint64_t last = p + flen - 1;
+                    int lo = 0, hi = (int)G.nreads - 1;          // last read starting at or before `last`
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
+                    }
+                    const uint32_t fi = G.frame_base + R.fbase + done + lane;
+                    edgpu_pkt_desc d;
+                    d.slot = 0;
+                    d.len = (uint16_t)(flen - 4);
+                    d.channel = (uint8_t)tbyte(v, p + 1);
+                    d.flags = 0;
+                    d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
+                    P.desc[fi] = d;
+                    const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
+                    P.src_addr[fi] = (uint64_t)(uintptr_t)a;
+                    atomicAdd(&P.results[G.first_read + lo].frames, 1u);
                 }
-                const uint32_t fi = G.frame_base + R.fbase + done + lane;
-                edgpu_pkt_desc d;
-                d.slot = 0;
-                d.len = (uint16_t)(flen - 4);
-                d.channel = (uint8_t)tbyte(v, p + 1);
-                d.flags = 0;
-                d.arrival_ms = lds_reads ? s_rarr[lo] : rd[lo].arrival;
-                P.desc[fi] = d;
-                const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
-                if (p < v.clen) s_stage = p;
-                P.src_addr[fi] = (uint64_t)(uintptr_t)a;
-                atomicAdd(&P.results[G.first_read + lo].frames, 1u);
+                done += m;
+                __syncthreads();
+                if (m == 0) break;
             }
-            done += m;
-            __syncthreads();
-            if (m == 0) break;
-        }
-        // a frame that starts in the carried bytes: staged contiguously (the only one per session)
-        const uint64_t sp = s_stage;
-        if (sp != ~0ull) {
-            uint32_t flen = 0;
-            tcp_step(v, sp, flen);
-            uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
-            for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
-                dst[b] = b < flen ? (uint8_t)tbyte(v, sp + b) : 0u;
         }
     }
-    if (c != G.first_chunk) return;                           // uniform
-    // ---- the session's finish: carry + per-read results ----
+    // a frame that starts in the carried bytes -- the stream's first, at position 0 -- is staged
+    // contiguously for k_ingest before the carry is overwritten
+    if (!over && G.nchunks && v.clen) {
+        const TcpChunkRes R0 = P.chunkres[G.first_chunk];
+        if (R0.entry == 0) {                                  // uniform
+            uint32_t flen = 0;
+            tcp_step(v, 0, flen);
+            uint8_t* dst = P.stage + (uint64_t)g * kTcpCarry;
+            for (uint32_t b = lane; b < ((flen + 15) & ~15u); b += 64)
+                dst[b] = b < flen ? (uint8_t)tbyte(v, b) : 0u;
+        }
+    }
+    // ---- the carry + per-read results ----
     const uint32_t code = G.code;
     const uint64_t stop = G.stop;
     uint32_t ncarry = 0;
@@ -670,7 +676,7 @@ hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
                            dim3(64 * kWalkWaves), 0, st, p);
     hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
     hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
-    if (p.nchunks) hipLaunchKernelGGL(k_tcp_emit, dim3(p.nchunks), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(k_tcp_finish, dim3(p.ngroups), dim3(64), 0, st, p);
     return hipGetLastError();
 }
 

@@ -1066,6 +1066,13 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;
+    p.tcp_groups = tcp ? tcp->groups : nullptr;
+    p.tcp_chunkres = tcp ? tcp->chunkres : nullptr;
+    p.tcp_offs = tcp ? tcp->offs : nullptr;
+    p.tcp_reads = tcp ? tcp->reads : nullptr;
+    p.tcp_raw = tcp ? tcp->raw : nullptr;
+    p.tcp_stage = tcp ? tcp->stage : nullptr;
+    p.tcp_results = tcp ? tcp->results : nullptr;
     HIP_CHECK(hist_mark(x, 2, 0));
     if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));

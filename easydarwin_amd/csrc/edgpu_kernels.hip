@@ -305,6 +305,25 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint64_t p_vb[THREADS];
     __shared__ uint64_t scan64[NW];
     __shared__ uint32_t scan32[NW];
+    // interleaved ingest: the session's chunk table (frame end of each chunk, the recorded
+    // candidate or kTcpNone) and its reads, for every lane's frame lookup
+    constexpr uint32_t kLdsChunks = 256, kLdsReads = 64;
+    __shared__ uint32_t t_cend[kLdsChunks], t_crec[kLdsChunks];
+    __shared__ uint64_t t_rstart[kLdsReads];
+    __shared__ int64_t t_rarr[kLdsReads];
+    TcpGroup G{};
+    if (P.tcp_groups) {
+        G = P.tcp_groups[seg];
+        for (uint32_t c = tid; c < min(G.nchunks, kLdsChunks); c += THREADS) {
+            const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + c];
+            t_cend[c] = R.fbase + R.nframes;
+            t_crec[c] = R.entry != kTcpNone && R.nframes <= kTcpFrames ? R.cand : kTcpNone;
+        }
+        if (tid < (int)min(G.nreads, kLdsReads)) {
+            t_rstart[tid] = P.tcp_reads[G.first_read + tid].start;
+            t_rarr[tid] = P.tcp_reads[G.first_read + tid].arrival;
+        }
+    }
 
     if (tid < (int)nsnd) {
         const SenderDev& D = P.senders[S.first_sender + tid];
@@ -329,7 +348,93 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         bool acc = false;
         const uint8_t* pk = nullptr;
         uint32_t hdr[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};   // packet bytes 0..27, little-endian words
-        if (valid) {
+        bool direct = false;            // interleaved frame found here (counted per read below)
+        uint32_t rd_idx = 0;
+        if (valid && P.tcp_groups) {
+            // the frame's chunk: the first whose frame end passes the frame's session index
+            const uint32_t j = i - b;
+            uint32_t lo = 0, hi = G.nchunks - 1;
+            const bool lds = G.nchunks <= kLdsChunks;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                uint32_t ce;
+                if (lds) ce = t_cend[mid];
+                else { const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + mid]; ce = R.fbase + R.nframes; }
+                if (ce > j) hi = mid; else lo = mid + 1;
+            }
+            uint32_t rec, fbase;
+            if (lds) { rec = t_crec[lo]; fbase = lo ? t_cend[lo - 1] : 0u; }
+            else {
+                const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + lo];
+                rec = R.entry != kTcpNone && R.nframes <= kTcpFrames ? R.cand : kTcpNone;
+                fbase = R.fbase;
+            }
+            if (rec != kTcpNone) {
+                direct = true;
+                const uint64_t pos = (uint64_t)lo * kTcpChunk +
+                                     P.tcp_offs[((size_t)(G.first_chunk + lo) * kTcpCands + rec) * kTcpFrames + (j - fbase)];
+                const uint8_t* sp;
+                uintptr_t end;                                 // the stream's (or the stage's) end
+                if (pos >= G.carry_len) {
+                    sp = P.tcp_raw + G.raw_off + (pos - G.carry_len);
+                    end = (uintptr_t)(P.tcp_raw + G.raw_off + (G.len - G.carry_len));
+                } else {                                        // starts in the carried bytes: staged
+                    sp = P.tcp_stage + (uint64_t)seg * kTcpCarry;
+                    end = (uintptr_t)(sp + kTcpCarry);
+                }
+                // the frame's first 48 aligned bytes at once: '$' ch BE16(len) and packet bytes 0..27
+                const uintptr_t al = (uintptr_t)sp & ~(uintptr_t)15;
+                const uint32_t sh = (uint32_t)((uintptr_t)sp & 15);
+                const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+                const u32x4 k0 = *reinterpret_cast<const u32x4*>(al);
+                const u32x4 k1 = al + 16 < end ? *reinterpret_cast<const u32x4*>(al + 16) : z;
+                const u32x4 k2 = sh && al + 32 < end ? *reinterpret_cast<const u32x4*>(al + 32) : z;
+                const u32x4 f0 = funnel16(k0, k1, sh);       // frame bytes 0..15
+                const uint32_t flen = (f0.x >> 16 & 0xFFu) << 8 | f0.x >> 24;
+                len = min(flen, (uint32_t)kMaxPacket);
+                const uint32_t ch = f0.x >> 8 & 0xFFu;
+                track = ch >> 1;
+                ls = 2 * track + (ch & 1);
+                // the reads: the frame belongs to the read holding its last byte
+                const uint64_t last = pos + 4 + flen - 1;
+                uint32_t rl = 0, rh = G.nreads - 1;
+                while (rl < rh) {
+                    const uint32_t mid = (rl + rh + 1) >> 1;
+                    const uint64_t st = G.nreads <= kLdsReads ? t_rstart[mid] : P.tcp_reads[G.first_read + mid].start;
+                    if (st <= last) rl = mid; else rh = mid - 1;
+                }
+                rd_idx = rl;
+                arrival = G.nreads <= kLdsReads ? t_rarr[rl] : P.tcp_reads[G.first_read + rl].arrival;
+                slot = 0;
+                acc = track < S.ntracks && len > 0;
+                src = (uint64_t)(uintptr_t)sp;
+                pk = sp + 4;
+                // as load16_unaligned(sp, lim) / (sp + 16, lim) with lim = sp + 4 + len: a block
+                // past lim is not read (the word keeps the previous block's bytes)
+                const uintptr_t lim = (uintptr_t)sp + 4 + len;
+                const u32x4 w0 = sh && al + 16 < lim ? f0 : funnel16(k0, k0, sh);
+                const u32x4 w1 = len > 12 ? funnel16(k1, sh && al + 32 < lim ? k2 : k1, sh) : z;
+                hdr[0] = w0.y; hdr[1] = w0.z; hdr[2] = w0.w; hdr[3] = w1.x;
+                hdr[4] = w1.y; hdr[5] = w1.z; hdr[6] = w1.w;
+                if (acc) fl = s_flags[ls];
+                if (acc && (fl & kSndRtcpPort))
+                    acc = len >= 8 && len >= 4 * hbe16(hdr, 2) + 4 && (hbyte(hdr, 0) >> 6) == 2 && hbyte(hdr, 1) == 200;
+                in_pk += 1;
+                in_bytes += len;
+            }
+        }
+        // per read, the frames this round found here (one atomic per read and wave)
+        if (P.tcp_groups) {
+            uint64_t pend = __ballot(direct);
+            while (pend) {
+                const int leader = __ffsll((unsigned long long)pend) - 1;
+                const uint32_t key = (uint32_t)__shfl((int)rd_idx, leader, 64);
+                const uint64_t same = __ballot(direct && rd_idx == key);
+                if ((tid & 63) == leader) atomicAdd(&P.tcp_results[G.first_read + key].frames, (uint32_t)__popcll(same));
+                pend &= ~same;
+            }
+        }
+        if (valid && !direct) {
             const edgpu_pkt_desc d = P.desc[i];
             len = min((uint32_t)d.len, (uint32_t)kMaxPacket);
             track = d.channel >> 1;

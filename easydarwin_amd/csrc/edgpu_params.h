@@ -29,6 +29,10 @@ namespace edgpu {
 #endif
 constexpr uint32_t kTcpFramesPerRound = EDGPU_TCP_TD;
 
+struct TcpGroup;
+struct TcpChunkRes;
+struct TcpRead;
+
 struct IngestParams {
     const edgpu_pkt_desc* desc;
     const uint32_t* seg_off;
@@ -53,6 +57,18 @@ struct IngestParams {
     uint32_t ssrc_timeout_s;
     uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
     TickTotals* totals;
+    // Interleaved ingest (null otherwise): segment g is deframe group g, and k_ingest finds each
+    // frame itself -- its chunk from the per-chunk results, its start from the walk's recorded
+    // starts, its length and channel from its own '$' header, its arrival from the reads --
+    // instead of reading a per-frame descriptor.  Frames of chunks the walk did not record
+    // (cand kTcpNone, or more than kTcpFrames frames) come from desc / src_addr (k_tcp_finish).
+    const TcpGroup* tcp_groups;
+    const TcpChunkRes* tcp_chunkres;
+    const uint16_t* tcp_offs;
+    const TcpRead* tcp_reads;
+    const uint8_t* tcp_raw;
+    const uint8_t* tcp_stage;
+    edgpu_tcp_result* tcp_results;
 };
 
 struct KeyframeParams {
