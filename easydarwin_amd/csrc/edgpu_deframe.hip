@@ -345,18 +345,21 @@ __device__ __forceinline__ void walk_candidate(const TcpParams& P, const WalkChu
 template <int CPW>
 __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu(EDGPU_TCP_WALK_WPE)))
 void k_tcp_walk(TcpParams P) {
-    static_assert(CPW == 1 || CPW == 2, "one or two chunks per wave");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "one, two or four chunks per wave");
     constexpr uint32_t LPC = 64 / CPW;                      // walking lanes per chunk
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ uint16_t s_own[kWalkWaves][CPW][kTcpCands], s_next[kWalkWaves][CPW][kTcpCands];
+    __shared__ WalkChunk s_w[kWalkWaves][CPW];              // each chunk's setup, for its lanes
     const uint32_t c0 = (blockIdx.x * kWalkWaves + wid) * CPW;
-    const WalkChunk a = walk_chunk_setup(P, c0, s_own[wid][0], s_next[wid][0], lane);
-    WalkChunk b{};
-    if constexpr (CPW == 2) {
-        if (a.valid && a.end < a.v.len && c0 + 1 < P.nchunks && P.chunk_group[c0 + 1] == P.chunk_group[c0]) {
-            // the second chunk follows the first in the same stream: its own candidate window is
-            // the first chunk's next window, already scanned -- copy the list, scan only its next
-            b.c = c0 + 1;
+    WalkChunk a = walk_chunk_setup(P, c0, s_own[wid][0], s_next[wid][0], lane);
+    if (lane == 0) s_w[wid][0] = a;
+#pragma unroll
+    for (int h = 1; h < CPW; h++) {
+        WalkChunk b{};
+        if (a.valid && a.end < a.v.len && c0 + h < P.nchunks && P.chunk_group[c0 + h] == P.chunk_group[c0 + h - 1]) {
+            // chunk h follows chunk h - 1 in the same stream: its own candidate window is the
+            // previous chunk's next window, already scanned -- copy the list, scan only its next
+            b.c = c0 + h;
             b.valid = true;
             b.v = a.v;
             b.start = a.end;
@@ -365,20 +368,22 @@ void k_tcp_walk(TcpParams P) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if ((uint32_t)lane < kTcpCands) s_own[wid][1][lane] = s_next[wid][0][lane];
-            b.nn = b.end < b.v.len ? tcp_candidates(b.v, b.end, s_next[wid][1], lane) : 0u;
+            if ((uint32_t)lane < kTcpCands) s_own[wid][h][lane] = s_next[wid][h - 1][lane];
+            b.nn = b.end < b.v.len ? tcp_candidates(b.v, b.end, s_next[wid][h], lane) : 0u;
         } else {
-            b = walk_chunk_setup(P, c0 + 1, s_own[wid][CPW - 1], s_next[wid][CPW - 1], lane);
+            b = walk_chunk_setup(P, c0 + h, s_own[wid][h], s_next[wid][h], lane);
         }
+        if (lane == 0) s_w[wid][h] = b;
+        a = b;
     }
     __syncthreads();
-    const int h = CPW == 2 && lane >= 32 ? 1 : 0;
-    const WalkChunk w = h ? b : a;
+    const int h = lane / (int)LPC;                          // this lane's chunk
+    const WalkChunk m = CPW == 1 ? a : s_w[wid][h];
     const uint32_t sub = (uint32_t)lane % LPC;
-    if (!w.valid) return;
-    if (sub == 0) P.ncand[w.c] = w.n;
-    if (w.n > kTcpCands) return;
-    for (uint32_t k = sub; k < w.n; k += LPC) walk_candidate(P, w, k, s_own[wid][h], s_next[wid][h]);
+    if (!m.valid) return;
+    if (sub == 0) P.ncand[m.c] = m.n;
+    if (m.n > kTcpCands) return;
+    for (uint32_t k = sub; k < m.n; k += LPC) walk_candidate(P, m, k, s_own[wid][h], s_next[wid][h]);
 }
 
 // ---- k_tcp_resolve: one workgroup per session; thread 0 follows the links ----

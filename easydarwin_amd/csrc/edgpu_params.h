@@ -131,8 +131,10 @@ constexpr uint32_t kTcpSpec = EDGPU_TCP_SPEC;
 #define EDGPU_TCP_CAND_FUSED 0               // 1: a chunk's two candidate windows loaded at once (A/B)
 #endif
 #ifndef EDGPU_TCP_WALK_CPW
-#define EDGPU_TCP_WALK_CPW 2                 // chunks walked side by side per wave (1 or 2): walk
-                                             // ~100 -> 60 us (profiles/r02z32_tcp_walk_ab/)
+#define EDGPU_TCP_WALK_CPW 2                 // chunks walked side by side per wave (1, 2 or 4): walk
+                                             // ~100 -> 60 us (profiles/r02z32_tcp_walk_ab/); four
+                                             // (16 / 24 / 32 KiB chunks) slower: 0.289 / 0.285 /
+                                             // 0.289 vs 0.281 ms (profiles/r03t_walk_shape_ab/)
 #endif
 constexpr int kTcpWalkCpw = EDGPU_TCP_WALK_CPW;
 #ifndef EDGPU_TCP_WALK_WPE
