@@ -15,6 +15,7 @@ import hashlib
 import json
 import os
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -190,3 +191,62 @@ def test_argument_checks():
         two = f + f
         rows = [(tcp, len(f), 0, 0), (tcp, len(f), len(f), 0)]
         assert _as_list(_call(ctx, rows, two)) == [[1, len(f), 0, 0], [1, len(f), 0, 0]]
+
+
+@pytest.mark.gpu
+def test_long_session_frames_match_restatement():
+    """One session with ~9.5 MiB of frames in one call: more chunks than k_ingest keeps in LDS
+    (256) and more reads than k_ingest / k_tcp_finish keep in LDS (64), so the frame lookups take
+    their global-memory paths; audio bursts put > 32 frames into some chunks, which the walk does
+    not record (k_tcp_finish re-walks them).  Every relayed datagram and its arrival time equal
+    the restatement's frames, per channel, in order."""
+    from oracle.interleave import FRAME, deframe
+    rng = random.Random(11)
+    frames, seq = [], [0, 0]
+    for i in range(8800):
+        if i % 200 < 170:
+            ch, pt, body = 0, 96, bytes([0x41]) + rng.randbytes(rng.randint(980, 1380))
+        else:
+            ch, pt, body = 2, 97, rng.randbytes(rng.randint(40, 80))
+        k = ch // 2
+        hdr = struct.pack(">BBHII", 0x80, pt, seq[k] & 0xFFFF, 3000 * seq[k], 0x5EED0000 + k)
+        seq[k] += 1
+        frames.append(_frame(ch, hdr + body))
+    data = b"".join(frames)
+    reads, at = [], 0
+    while at < len(data):
+        n = rng.randint(80_000, 120_000)
+        reads.append(data[at:at + n])
+        at += n
+    assert len(reads) > 64 and len(data) > 256 * 32768
+    t0 = 50_000
+    rows, blob = _rows([(0, reads)], t0=t0)
+    want, _ = ingest_reads({}, rows, blob)
+    cfg = dict(max_batch_bytes=16 << 20, max_batch_packets=1 << 15, out_arena_bytes=32 << 20,
+               max_out_packets=1 << 15, video_ring_bytes=32 << 20, video_ring_packets=1 << 14,
+               other_ring_packets=1 << 12)
+    with edgpu.Context(**cfg) as ctx:
+        s = ctx.session_add(SDP)
+        ctx.subscriber_add(s)
+        got = _call(ctx, rows, blob)
+        ctx.keyframe_index()
+        assert _as_list(got) == want
+        r = ctx.fanout(t0 + len(reads))
+        st, subs, desc, arena = ctx.read_tick(r)
+        arr = ctx.fanout_arrivals(st.relayed_packets)
+    exp = {0: [], 1: []}
+    for kind, rd, ch, _, payload in deframe(reads):
+        assert kind == FRAME
+        exp[ch // 2].append((payload, t0 + rd))
+    seen = set()
+    for q in subs:
+        if int(q["kind"]) != 0 or int(q["desc_count"]) == 0:
+            continue
+        tr = int(q["track"])
+        b = int(q["desc_base"])
+        d = desc[b:b + int(q["desc_count"])]
+        pk = [arena[o:o + n].tobytes() for o, n in zip(d["offset"].tolist(), d["len"].tolist())]
+        assert pk == [p for p, _ in exp[tr]], f"track {tr} bytes"
+        assert arr[b:b + len(d)].tolist() == [t for _, t in exp[tr]], f"track {tr} arrivals"
+        seen.add(tr)
+    assert seen == {0, 1}
