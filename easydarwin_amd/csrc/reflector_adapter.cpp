@@ -16,6 +16,9 @@ static double ms_since(Clock::time_point t0) {
 
 Reflector::Reflector(const edgpu_config* cfg) {
     fStatus = edgpu_ctx_create(cfg, &fCtx);
+    // ticks with at least this many distinct bytes gather in parts, overlapped with the writes
+    // (EDGPU_GATHER_SPLIT_BYTES; tests set 0 to run the pipelined path on small ticks)
+    if (const char* v = getenv("EDGPU_GATHER_SPLIT_BYTES")) fGatherSplitBytes = strtoull(v, nullptr, 0);
 }
 
 Reflector::~Reflector() {
@@ -219,12 +222,18 @@ int Reflector::FlushIngest() {
     for (const Stripe& st : b.st) n += (uint32_t)st.pushed.size();
     if (n) {
         // descriptors grouped by session (a session's packets are all in one stripe, in arrival
-        // order); the slots stay where the pushers wrote them
-        std::vector<const Pushed*> order;
-        order.reserve(n);
+        // order): a stable counting sort by session id; the slots stay where the pushers wrote them
+        uint32_t nsess = 0;
         for (const Stripe& st : b.st)
-            for (const Pushed& p : st.pushed) order.push_back(&p);
-        std::stable_sort(order.begin(), order.end(), [](const Pushed* x, const Pushed* y) { return x->session < y->session; });
+            for (const Pushed& p : st.pushed) nsess = std::max(nsess, p.session + 1);
+        fSortCount.assign((size_t)nsess + 1, 0);
+        for (const Stripe& st : b.st)
+            for (const Pushed& p : st.pushed) fSortCount[p.session + 1]++;
+        for (uint32_t s = 0; s < nsess; s++) fSortCount[s + 1] += fSortCount[s];
+        fSortOrder.resize(n);
+        std::vector<const Pushed*>& order = fSortOrder;
+        for (const Stripe& st : b.st)
+            for (const Pushed& p : st.pushed) order[fSortCount[p.session]++] = &p;
         if (b.descCap < n) {
             for (void* p : {(void*)b.desc, (void*)b.seg, (void*)b.segSess})
                 if (p) (void)edgpu_host_free(fCtx, p);
@@ -310,8 +319,6 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fHostOut = (uint8_t*)h;
         fHostOutCap = cap;
     }
-    // gathered straight into the pinned buffer: the kernel's stores cross PCIe (one pass)
-    if ((err = edgpu_arena_gather(fCtx, &res, tr.reg.data(), (uint32_t)tr.reg.size(), fHostOut, fHostOutCap))) return err;
     fTick.readback_bytes = tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
     const int64_t* arrival = nullptr;
     if (sink->WantsArrivals()) {
@@ -321,6 +328,47 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         }
         arrival = (const int64_t*)fPinArr.p;
     }
+    // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
+    // PCIe, one pass) in up to kParts parts of the sub-stream table, each part's regions after the
+    // previous part's: with several write threads a gather thread brings part k + 1 over while the
+    // writers deliver part k (a sub-stream only uses regions created at or before its own index).
+    constexpr uint32_t kParts = 4;
+    uint32_t nparts = 1;
+    uint32_t part_q[kParts] = {nq, nq, nq, nq}, part_r[kParts + 1] = {0, 0, 0, 0, 0};
+    if (fNumWriters > 1 && tr.bytes >= fGatherSplitBytes) {
+        nparts = kParts;
+        uint32_t k = 0, rend = 0;
+        for (uint32_t q = 0; q < nq && k + 1 < kParts; q++) {
+            if (tr.src[q].first != edgpu_host::TickRegions::kNone) rend = std::max(rend, tr.src[q].first + 1);
+            if (tr.reg_off[rend] * kParts >= tr.bytes * (k + 1)) { part_q[k] = q + 1; part_r[k + 1] = rend; k++; }
+        }
+        for (; k < kParts; k++) { part_q[k] = nq; part_r[k + 1] = (uint32_t)tr.reg.size(); }
+        for (uint32_t i = 1; i <= kParts; i++) part_r[i] = std::max(part_r[i], part_r[i - 1]);
+    } else {
+        part_r[1] = (uint32_t)tr.reg.size();
+    }
+    auto gather = [&](uint32_t k) -> int {
+        const uint32_t r0 = part_r[k], r1 = part_r[k + 1];
+        if (r1 <= r0) return kNoErr;
+        return edgpu_arena_gather(fCtx, &res, tr.reg.data() + r0, r1 - r0, fHostOut + tr.reg_off[r0],
+                                  fHostOutCap - tr.reg_off[r0]);
+    };
+    if ((err = gather(0))) return err;
+    std::atomic<uint32_t> ready{1};
+    std::atomic<bool> failed{false};
+    int gatherErr = kNoErr;
+    std::thread gatherer;
+    if (nparts > 1)
+        gatherer = std::thread([&] {
+            for (uint32_t k = 1; k < nparts; k++) {
+                if ((gatherErr = gather(k))) {
+                    failed.store(true, std::memory_order_relaxed);
+                    ready.store(nparts, std::memory_order_release);   // release the waiting writers
+                    return;
+                }
+                ready.store(k + 1, std::memory_order_release);
+            }
+        });
     fTick.readback_ms = ms_since(t0);
     t0 = Clock::now();
     sink->BeginTick(subs, nq);
@@ -330,6 +378,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     job.sink = sink;
     job.host = fHostOut;
     job.regions = &tr;
+    job.nparts = nparts; job.part_q = part_q; job.ready = &ready; job.failed = &failed;
     const uint32_t nw = fNumWriters;
     if (nw == 1) {
         WriteSubscribers(job, 0, 1);
@@ -346,6 +395,8 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fPoolDone.wait(g, [&] { return fJobsLeft == 0; });
         fJob = nullptr;
     }
+    if (gatherer.joinable()) gatherer.join();
+    if (gatherErr) return gatherErr;
     // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stopped its
     // sub-stream for the tick; the engine bookmarks the blocked packet (reports in sub-stream order)
     std::vector<edgpu_blocked> blocked;
@@ -377,9 +428,15 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
     r.err = kNoErr;
     r.blocked.clear();
     uint64_t writes = 0;
+    uint32_t part = 0;
     for (uint32_t s = 0; s < j.nsubs; s++) {
         const edgpu_substream_out& q = j.subs[s];
         if (!q.desc_count || (nworkers > 1 && writer_of(q, nworkers) != worker)) continue;
+        while (part + 1 < j.nparts && s >= j.part_q[part]) part++;
+        // this sub-stream's bytes are in part `part` of the gather: wait for it (a failed
+        // gather also ends the wait; the tick then returns its error)
+        while (j.ready->load(std::memory_order_acquire) <= part) std::this_thread::yield();
+        if (j.failed->load(std::memory_order_relaxed)) { r.writes = writes; return; }
         const uint8_t* base = j.regions->at(j.host, s);
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = j.desc[q.desc_base + i];

@@ -192,6 +192,12 @@ private:
         const edgpu_out_desc* desc; const int64_t* arrival;
         const uint8_t* host; const edgpu_host::TickRegions* regions;   // the tick's bytes
         OutputSink* sink;
+        // the gather's parts: sub-streams [part_q[k-1], part_q[k]) need part k; `ready` counts the
+        // parts in the pinned buffer; `failed`: a gather failed (the writers stop)
+        uint32_t nparts = 1;
+        const uint32_t* part_q = nullptr;
+        std::atomic<uint32_t>* ready = nullptr;
+        std::atomic<bool>* failed = nullptr;
         // one line per worker: the writers' results must not share a cache line (a per-packet
         // counter in a shared line serialised the write threads)
         struct alignas(64) Result { std::vector<edgpu_blocked> blocked; uint64_t writes = 0; int err = 0; };
@@ -207,10 +213,13 @@ private:
     Batch fBatch[2];
     int fFill = 0;
     std::vector<uint32_t> fTracks;                          // per session (0: none)
+    std::vector<uint32_t> fSortCount;                       // FlushIngest's counting sort by session
+    std::vector<const Pushed*> fSortOrder;
     // readback buffers
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
     PinBuf fPinSubs, fPinDesc, fPinArr;                     // sub-stream table, descriptors, arrivals
+    uint64_t fGatherSplitBytes = 8ull << 20;               // see ReflectPackets
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes (edgpu_arena_gather target)
     TickInfo fTick;
     // write threads (workers 1..n-1; the ticking thread is worker 0)

@@ -38,12 +38,17 @@ UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gather", ["whole", "parts"])
 @pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH)
-def test_module_matches_reference(name, tmp_path):
+def test_module_matches_reference(name, gather, tmp_path):
+    """`parts`: every tick's readback gathered in parts, overlapped with the write threads
+    (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split)."""
     t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
     t.write_bytes(_trace(name).to_bytes())
-    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120,
-                       env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+    env = dict(os.environ, EDGPU_TT_OUT=str(tt))
+    if gather == "parts":
+        env["EDGPU_GATHER_SPLIT_BYTES"] = "0"
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     if name in UDP_PUSH:                 # name the part that differs before the whole-file hash
         from easydarwin_amd.trace import capture_summary, read_capture, read_source_reports
