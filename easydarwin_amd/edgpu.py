@@ -253,6 +253,7 @@ class Context:
         _check(lib.edgpu_ctx_create(C.byref(c), C.byref(h)))
         self.h = h
         self.lib = lib
+        self._ntracks = {}          # session -> tracks (senders_of without a C call per session)
 
     def close(self):
         if self.h:
@@ -269,6 +270,7 @@ class Context:
         b = sdp.encode()
         out = C.c_uint32()
         _check(self.lib.edgpu_session_add(self.h, b, len(b), int(udp_push), C.byref(out)))
+        self._ntracks[out.value] = self.session_tracks(out.value)
         return out.value
 
     def session_tracks(self, session: int) -> int:
@@ -280,6 +282,7 @@ class Context:
         """The end of a ReflectorSession (reference count 0); kill_outputs tears its subscribers
         down with it (kill_clients_when_broadcast_stops)."""
         _check(self.lib.edgpu_session_remove(self.h, session, SESSION_KILL_OUTPUTS if kill_outputs else 0))
+        self._ntracks.pop(session, None)
 
     def subscriber_add(self, session: int, transport: int = TRANSPORT_UDP) -> int:
         out = C.c_uint32()
@@ -447,7 +450,8 @@ class Context:
 
     # ---- cross-GPU keyframe fast start (session images) ----
     def senders_of(self, sessions) -> int:
-        return int(sum(2 * self.session_tracks(int(s)) for s in sessions))
+        nt = self._ntracks
+        return int(sum(2 * (nt[s] if s in nt else self.session_tracks(s)) for s in map(int, sessions)))
 
     def session_export(self, sessions, now_ms: int, dst_ptr: int = 0, cap: int = 0, since=None):
         """Export session images.  dst_ptr 0 = size query.  `since`: None (full images) or,
