@@ -112,12 +112,20 @@ def main():
                      "alg_bytes_per_launch": int(alg / max(launches, 1)),
                      "achieved": round(alg / max(launches, 1) / (fan_ms / 1e3) / 1e9, 1), "peak": 8000.0,
                      "unit": "GB/s", "frac": round(alg / max(launches, 1) / (fan_ms / 1e3) / 1e9 / 8000.0, 4),
-                     "traffic": None},
+                     "traffic": None, "traffic_source": None},
         "ingested_packets_per_tick": int(np.mean([b["n"] for b in batches[1:]])),
         "relayed_packets_per_tick": int(relayed / (len(batches) - 1)),
         "generation_s": round(gen_s, 1),
         "data": "synthetic (easydarwin_amd/synth.py, the generator behind the `mixed` golden scenario)",
     }
+    # HBM traffic per launch from the committed PMC passes of this kernel and workload
+    # (tools/summarize_pmc_c5.py -> profiles/pmc_c5.json)
+    pmc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_c5.json")
+    if os.path.exists(pmc):
+        pj = json.load(open(pmc))
+        if pj.get("bench_kernel") == res["fanout_kernel"] and pj.get("workload") == res["workload"]:
+            res["roofline"]["traffic"] = pj["hbm_bytes_per_launch"]
+            res["roofline"]["traffic_source"] = f"profiles/pmc_c5.json ({pj['tag']}: rocprofv3 FETCH_SIZE/WRITE_SIZE passes)"
     print(json.dumps(res), flush=True)
     ctx.close()
 
