@@ -329,24 +329,14 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         arrival = (const int64_t*)fPinArr.p;
     }
     // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
-    // PCIe, one pass) in up to kParts parts of the sub-stream table, each part's regions after the
+    // PCIe, one pass) in up to TickParts::kMax parts of the sub-stream table, each part's regions after the
     // previous part's: with several write threads a gather thread brings part k + 1 over while the
     // writers deliver part k (a sub-stream only uses regions created at or before its own index).
-    constexpr uint32_t kParts = 4;
-    uint32_t nparts = 1;
-    uint32_t part_q[kParts] = {nq, nq, nq, nq}, part_r[kParts + 1] = {0, 0, 0, 0, 0};
-    if (fNumWriters > 1 && tr.bytes >= fGatherSplitBytes) {
-        nparts = kParts;
-        uint32_t k = 0, rend = 0;
-        for (uint32_t q = 0; q < nq && k + 1 < kParts; q++) {
-            if (tr.src[q].first != edgpu_host::TickRegions::kNone) rend = std::max(rend, tr.src[q].first + 1);
-            if (tr.reg_off[rend] * kParts >= tr.bytes * (k + 1)) { part_q[k] = q + 1; part_r[k + 1] = rend; k++; }
-        }
-        for (; k < kParts; k++) { part_q[k] = nq; part_r[k + 1] = (uint32_t)tr.reg.size(); }
-        for (uint32_t i = 1; i <= kParts; i++) part_r[i] = std::max(part_r[i], part_r[i - 1]);
-    } else {
-        part_r[1] = (uint32_t)tr.reg.size();
-    }
+    const edgpu_host::TickParts parts =
+        edgpu_host::tick_parts(tr, nq, fNumWriters > 1 && tr.bytes >= fGatherSplitBytes ? edgpu_host::TickParts::kMax : 1);
+    const uint32_t nparts = parts.n;
+    const uint32_t* part_q = parts.q;
+    const uint32_t* part_r = parts.r;
     auto gather = [&](uint32_t k) -> int {
         const uint32_t r0 = part_r[k], r1 = part_r[k + 1];
         if (r1 <= r0) return kNoErr;

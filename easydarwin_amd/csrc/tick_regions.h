@@ -65,4 +65,31 @@ inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
     return t;
 }
 
+// The readback of a tick in up to K parts of the sub-stream table (Reflector::ReflectPackets
+// gathers part k + 1 while its writers deliver part k): sub-streams [q[k-1], q[k]) need regions
+// [0, r[k+1]) -- a sub-stream only uses regions created at or before its own index, so each part
+// adds the regions [r[k], r[k+1]).  Parts are cut at even fractions of the gathered bytes; with
+// k == 1 (or too few bytes) there is one part.
+struct TickParts {
+    static constexpr uint32_t kMax = 4;
+    uint32_t n = 1;
+    uint32_t q[kMax] = {0, 0, 0, 0};            // part k holds the sub-streams below q[k]
+    uint32_t r[kMax + 1] = {0, 0, 0, 0, 0};     // part k gathers regions [r[k], r[k + 1])
+};
+
+inline TickParts tick_parts(const TickRegions& tr, uint32_t nq, uint32_t k) {
+    TickParts p;
+    k = std::max<uint32_t>(1, std::min<uint32_t>(k, TickParts::kMax));
+    for (uint32_t i = 0; i < TickParts::kMax; i++) p.q[i] = nq;
+    p.n = k;
+    uint32_t cut = 0, rend = 0;
+    for (uint32_t q = 0; q < nq && cut + 1 < k; q++) {
+        if (tr.src[q].first != TickRegions::kNone) rend = std::max(rend, tr.src[q].first + 1);
+        if (tr.reg_off[rend] * k >= tr.bytes * (cut + 1)) { p.q[cut] = q + 1; p.r[cut + 1] = rend; cut++; }
+    }
+    for (; cut < k; cut++) { p.q[cut] = nq; p.r[cut + 1] = (uint32_t)tr.reg.size(); }
+    for (uint32_t i = 1; i <= k; i++) p.r[i] = std::max(p.r[i], p.r[i - 1]);
+    return p;
+}
+
 }  // namespace edgpu_host
