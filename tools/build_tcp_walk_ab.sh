@@ -10,7 +10,11 @@ mkdir -p $R/easydarwin_amd/ab /tmp/tcpab
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include -I$S"
 for a in "$@"; do
   tag=${a%%=*}; flags=${a#*=}
-  /opt/rocm/bin/hipcc $F $flags -c $S/edgpu_deframe.hip -o /tmp/tcpab/deframe_$tag.o
+  # edgpu_kernels.hip with the same flags: k_ingest finds interleaved frames by chunk (round 3)
+  /opt/rocm/bin/hipcc $F $flags -c $S/edgpu_kernels.hip -o /tmp/tcpab/kernels_$tag.o &
+  /opt/rocm/bin/hipcc $F $flags -c $S/edgpu_deframe.hip -o /tmp/tcpab/deframe_$tag.o &
+  /opt/rocm/bin/hipcc $F $flags -c $S/edgpu_engine.cpp -o /tmp/tcpab/engine_$tag.o &
+  wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/easydarwin_amd/ab/libedgpu_$tag.so \
-      $S/edgpu_kernels.o /tmp/tcpab/deframe_$tag.o $S/edgpu_egress.o $S/edgpu_engine.o $S/reflector_adapter.o -pthread
+      /tmp/tcpab/kernels_$tag.o /tmp/tcpab/deframe_$tag.o $S/edgpu_egress.o /tmp/tcpab/engine_$tag.o $S/reflector_adapter.o -pthread
 done
