@@ -256,6 +256,9 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     // the cumulative ingest counters at the last index update: ingested_* = cum - mark, set by
     // the keyframe index after every ingest (no reset launch before the ingest)
     unsigned long long ingest_mark_packets, ingest_mark_bytes;
+    // measurement builds: the copy kernel's workgroups' first start / first and last exit
+    // (s_memrealtime, 100 MHz) -- the tail of the dynamic schedule (EDGPU_FAN_TAIL=1 prints it)
+    unsigned long long fan_t0_min, fan_done_min, fan_done_max;
 };
 
 struct TickParams {

@@ -1447,6 +1447,11 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->ingested_bytes = t.ingested_bytes;
     out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
+#ifdef EDGPU_AB_VARIANTS
+    if (getenv("EDGPU_FAN_TAIL") && t.fan_done_max > t.fan_t0_min)   // 100-MHz s_memrealtime ticks
+        fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u\n",
+                (t.fan_done_max - t.fan_t0_min) / 100.0, (t.fan_done_min - t.fan_t0_min) / 100.0, t.nwork);
+#endif
     return EDGPU_OK;
 }
 

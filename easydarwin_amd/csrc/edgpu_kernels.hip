@@ -780,6 +780,7 @@ __device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, ui
 __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
     t->status = 0; t->nwork = 0; t->fan_next = 0;
+    t->fan_t0_min = ~0ull; t->fan_done_min = ~0ull; t->fan_done_max = 0;
 }
 
 // Per-tick counter updates as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
@@ -1746,6 +1747,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
 
     for (int k = tid; k < 3 * SM; k += THREADS) smb[k] = 0;
     if (tid == 0) { s_claim[0] = atomicAdd(&P.totals->fan_next, 1u); s_claim[1] = atomicAdd(&P.totals->fan_next, 1u); }
+#ifdef EDGPU_AB_VARIANTS
+    if (tid == 0) atomicMin(&P.totals->fan_t0_min, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     __syncthreads();
     uint32_t w = s_claim[0], wnext = s_claim[1];
     FanWork cur, nx;
@@ -1878,6 +1882,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, THREADS))) void k_fanou
         for (int k = 0; k < NWAVES; k++) tot += s_red[k];
         if (tot) atomicAdd(&P.totals->cum_fanout_in_bytes, tot);
     }
+#ifdef EDGPU_AB_VARIANTS
+    if (tid == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&P.totals->fan_done_min, t);
+        atomicMax(&P.totals->fan_done_max, t);
+    }
+#endif
 }
 
 // -----------------------------------------------------------------------------------------
