@@ -259,6 +259,8 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     // measurement builds: the copy kernel's workgroups' first start / first and last exit
     // (s_memrealtime, 100 MHz) -- the tail of the dynamic schedule (EDGPU_FAN_TAIL=1 prints it)
     unsigned long long fan_t0_min, fan_done_min, fan_done_max;
+    unsigned long long ing_t0_min, ing_done_min, ing_done_max;    // the same for k_ingest
+    unsigned long long ing_last_span, ing_last_first;             // ... of the last finished ingest
 };
 
 struct TickParams {

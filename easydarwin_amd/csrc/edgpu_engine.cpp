@@ -1449,8 +1449,9 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->_pad = t.nwork;
 #ifdef EDGPU_AB_VARIANTS
     if (getenv("EDGPU_FAN_TAIL") && t.fan_done_max > t.fan_t0_min)   // 100-MHz s_memrealtime ticks
-        fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u\n",
-                (t.fan_done_max - t.fan_t0_min) / 100.0, (t.fan_done_min - t.fan_t0_min) / 100.0, t.nwork);
+        fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u; ingest span %.1f us, first exit at %.1f us\n",
+                (t.fan_done_max - t.fan_t0_min) / 100.0, (t.fan_done_min - t.fan_t0_min) / 100.0, t.nwork,
+                t.ing_last_span / 100.0, t.ing_last_first / 100.0);
 #endif
     return EDGPU_OK;
 }

@@ -334,6 +334,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     if (tid < (int)S.ntracks) s_count[tid] = P.streams[S.first_stream + tid].packet_count;
     if (tid < (int)nsnd) c_lastacc[tid] = -1;
+#ifdef EDGPU_AB_VARIANTS
+    if (tid == 0) atomicMin(&P.totals->ing_t0_min, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     __syncthreads();
 
     uint64_t in_pk = 0, in_bytes = 0;
@@ -653,6 +656,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
     }
+#ifdef EDGPU_AB_VARIANTS
+    if (tid == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&P.totals->ing_done_min, t);
+        atomicMax(&P.totals->ing_done_max, t);
+    }
+#endif
 }
 
 // =========================================================================================
@@ -691,6 +701,11 @@ __device__ __forceinline__ void mark_ingest_totals(TickTotals* t) {
     const unsigned long long p = t->cum_ingested_packets, b = t->cum_ingested_bytes;
     t->ingested_packets = p - t->ingest_mark_packets; t->ingested_bytes = b - t->ingest_mark_bytes;
     t->ingest_mark_packets = p; t->ingest_mark_bytes = b;
+#ifdef EDGPU_AB_VARIANTS
+    // measurement builds: the finished ingest's span and first workgroup exit, then a reset
+    t->ing_last_span = t->ing_done_max - t->ing_t0_min; t->ing_last_first = t->ing_done_min - t->ing_t0_min;
+    t->ing_t0_min = ~0ull; t->ing_done_min = ~0ull; t->ing_done_max = 0;
+#endif
 }
 
 __global__ __launch_bounds__(64) void k_keyframe(KeyframeParams P) {
