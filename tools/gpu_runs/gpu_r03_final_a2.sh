@@ -1,0 +1,16 @@
+# round 3, final run A2 (the tree as committed, after the late changes): the full GPU suite, smoke(), and the default
+# bench line with its CPU baseline
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r03_final2
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu tests > $O/gputests.log 2>&1; rc=$?
+echo "gpu tests rc=$rc"; grep -E "FAIL|ERROR" $O/gputests.log | head -20; tail -1 $O/gputests.log
+[ $rc -eq 124 ] || [ $rc -eq 137 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rs=$?
+echo "smoke rc=$rs"; tail -3 $O/smoke.log
+[ $rs -ne 0 ] && exit $rs
+timeout -k 10 500 python bench.py > $O/bench_default.json 2> $O/bench_default.err; rb=$?
+echo "bench rc=$rb"; cat $O/bench_default.json
+exit $(( rc || rb ))
