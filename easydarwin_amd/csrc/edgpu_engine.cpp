@@ -153,6 +153,14 @@ struct edgpu_ctx {
     bool overlap = false;
     hipStream_t copy = nullptr;
     hipEvent_t ev_plan = nullptr, ev_copy = nullptr;
+    // the RTSP-interleaved deframe (k_tcp_*) runs on `aux`: it reads only the call's TCP bytes
+    // and writes deframe scratch, so it overlaps the previous tick's fan-out still on `stream`;
+    // k_ingest waits for ev_deframe
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_deframe = nullptr;
+    // the last keyframe index (it reads the segment tables the next deframe rewrites)
+    hipEvent_t ev_kf = nullptr;
+    bool kf_recorded = false;
     int cur = 0;                    // output buffer of the current tick (0 / 1)
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
@@ -388,6 +396,10 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->ev_plan) (void)hipEventDestroy(x->ev_plan);
     if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
     if (x->copy) (void)hipStreamDestroy(x->copy);
+    if (x->aux) (void)hipStreamSynchronize(x->aux);
+    if (x->ev_deframe) (void)hipEventDestroy(x->ev_deframe);
+    if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
+    if (x->aux) (void)hipStreamDestroy(x->aux);
     if (x->stream) (void)hipStreamDestroy(x->stream);
     delete x;
     return EDGPU_OK;
@@ -397,6 +409,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
 static hipError_t sync_all(edgpu_ctx* x) {
     hipError_t e = hipStreamSynchronize(x->stream);
     if (e == hipSuccess && x->copy) e = hipStreamSynchronize(x->copy);
+    if (e == hipSuccess && x->aux) e = hipStreamSynchronize(x->aux);
     return e;
 }
 
@@ -1055,7 +1068,8 @@ static int rebuild_index(edgpu_ctx* x) {
 // edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
 // inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
-                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr) {
+                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr,
+                          hipEvent_t deframed = nullptr) {
     IngestParams p;
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
     p.src_addr = tcp ? tcp->src_addr : nullptr;
@@ -1074,7 +1088,8 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.tcp_stage = tcp ? tcp->stage : nullptr;
     p.tcp_results = tcp ? tcp->results : nullptr;
     HIP_CHECK(hist_mark(x, 2, 0));
-    if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
+    if (deframed) HIP_CHECK(hipStreamWaitEvent(x->stream, deframed, 0));    // the deframe ran on aux
+    else if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
@@ -1260,17 +1275,24 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
+    if (!x->aux) {
+        HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&x->ev_deframe, hipEventDisableTiming));
+    }
+    // the deframe rewrites the segment tables the last keyframe index reads (a reserve above that
+    // grew has synchronised `stream`); the fan-out after that index keeps running
+    if (x->kf_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_kf, 0));
     const uint8_t* raw = bytes;
     if (where == EDGPU_PTR_HOST) {
         if (!x->d_tcp_raw && dmalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
             return fail(EDGPU_OUT_OF_MEMORY, "read staging");
-        HIP_CHECK(hipMemcpyAsync(x->d_tcp_raw, bytes, nbytes, hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipMemcpyAsync(x->d_tcp_raw, bytes, nbytes, hipMemcpyHostToDevice, x->aux));
         raw = x->d_tcp_raw;
     }
-    HIP_CHECK(hipMemcpyAsync(x->d_tcp_groups.ptr, groups.data(), ng * sizeof(TcpGroup), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipMemcpyAsync(x->d_tcp_reads.ptr, rd.data(), n * sizeof(TcpRead), hipMemcpyHostToDevice, x->stream));
-    if (nc) HIP_CHECK(hipMemcpyAsync(x->d_tcp_chunk_group.ptr, chunk_group.data(), nc * 4, hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipMemsetAsync(x->d_tcp_results.ptr, 0, n * sizeof(edgpu_tcp_result), x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_tcp_groups.ptr, groups.data(), ng * sizeof(TcpGroup), hipMemcpyHostToDevice, x->aux));
+    HIP_CHECK(hipMemcpyAsync(x->d_tcp_reads.ptr, rd.data(), n * sizeof(TcpRead), hipMemcpyHostToDevice, x->aux));
+    if (nc) HIP_CHECK(hipMemcpyAsync(x->d_tcp_chunk_group.ptr, chunk_group.data(), nc * 4, hipMemcpyHostToDevice, x->aux));
+    HIP_CHECK(hipMemsetAsync(x->d_tcp_results.ptr, 0, n * sizeof(edgpu_tcp_result), x->aux));
     TcpParams p;
     p.groups = x->d_tcp_groups.ptr; p.ngroups = ng; p.nchunks = nc;
     p.reads = x->d_tcp_reads.ptr; p.chunk_group = x->d_tcp_chunk_group.ptr;
@@ -1282,7 +1304,9 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.desc = x->d_desc; p.src_addr = x->d_tcp_src; p.max_desc = x->cfg.max_batch_packets;
     p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
-    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p);
+    HIP_CHECK(launch_deframe(p, x->aux));
+    HIP_CHECK(hipEventRecord(x->ev_deframe, x->aux));
+    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p, x->ev_deframe);
     if (r) return r;
     TcpTotals tot;
     Readback rb(x);
@@ -1339,6 +1363,9 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     x->kf_share = false;
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
+    if (!x->ev_kf) HIP_CHECK(hipEventCreateWithFlags(&x->ev_kf, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(x->ev_kf, x->stream));
+    x->kf_recorded = true;
     if (x->pend_stage >= 0) {                   // the pinned staging set may be refilled now
         HIP_CHECK(hipEventRecord(x->pin[x->pend_stage].consumed, x->stream));
         x->pend_stage = -1;
