@@ -30,6 +30,8 @@ def module_run(args) -> dict:
     env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
     env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
     env.setdefault("EDGPU_QTSS_WRITE_THREADS", str(args.write_threads))
+    if args.concurrent_push:
+        env["EDGPU_BENCH_CONCURRENT_PUSH"] = "1"
     cmd = [os.path.join(ROOT, "tools", "qtss_replay"), os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"),
            "--bench", str(args.sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
@@ -64,9 +66,13 @@ def main():
     ap.add_argument("--max-out-packets", type=int, default=4 << 20)
     ap.add_argument("--timeout", type=int, default=300)
     ap.add_argument("--no-reference", action="store_true")
+    # the pushers push the next tick's packets while a tick runs, as a server's RTSP threads do
+    # (default: pushing and ticking alternate, the conservative measure)
+    ap.add_argument("--concurrent-push", action="store_true")
     args = ap.parse_args()
     out = {"workload": f"C2 through the QTSS module: {args.sessions} RTSP-interleaved H.264 pushers x {args.subs} "
-                       f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads",
+                       f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads "
+                       f"({'concurrent with' if args.concurrent_push else 'alternating with'} the ticks)",
            "write_threads": int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads)),
            "module": module_run(args)}
     m = out["module"]
