@@ -285,6 +285,12 @@ def main():
     ap.add_argument("--rewrite", action="store_true",
                     help="per-output rewrite stage on every subscriber (seq/ts deltas + SSRC override, "
                          "edgpu_subscriber_rewrite); the reference's parity mode is the identity (default)")
+    ap.add_argument("--timing-steps", type=int, default=3,
+                    help="steps after the timed region that record every timing event (the ingest, "
+                         "keyframe and plan durations of the line)")
+    ap.add_argument("--all-timing-events", action="store_true",
+                    help="record every timing event inside the timed steps too (the ingest / keyframe / "
+                         "plan durations then come from them; each event costs the step 4-8 us)")
     ap.add_argument("--ablation-study", action="store_true",
                     help="allow EDGPU_ABLATE (timing experiments that skip work): the line is then not a "
                          "valid measurement and says so")
@@ -326,12 +332,13 @@ def main():
     gids = owned_sessions(args.sessions, rank, world) if world > 1 else np.arange(args.sessions)
     fleet = H264Fleet(gids, tick_ms=args.tick_ms)
     steps, warm = args.steps, args.warmup
-    log(f"[bench] rank {rank}/{world}: {len(gids)} sessions x {args.subs} subs, generating {steps + warm} batches")
+    extra = 0 if args.all_timing_events else args.timing_steps
+    log(f"[bench] rank {rank}/{world}: {len(gids)} sessions x {args.subs} subs, generating {steps + warm + extra} batches")
     t_gen = time.time()
     gen = torch.Generator(device=dev)
     gen.manual_seed(0xEA5D + rank)
     batches = []
-    for _ in range(steps + warm):
+    for _ in range(steps + warm + extra):
         b = fleet.next_batch()
         bt = make_batch_on_device(b, dev, gen)
         if args.ingest == "tcp":
@@ -377,6 +384,11 @@ def main():
         raise SystemExit(f"engine status {st.status} after warmup")
     ctx.kernel_times(0), ctx.kernel_times(1), ctx.kernel_times(2), ctx.kernel_times(3)
     c0 = ctx.counters()
+    # The timed steps record only the fan-out copy kernel's event pair (the roofline's duration):
+    # every event is a marker the stream waits on, 4-8 us of idle GPU each
+    # (profiles/r03ak_timing_events_ab/).  The ingest / keyframe / plan durations come from
+    # `extra` steps after the timed region, with every event recorded.
+    ctx.set_timing(ctx.TIMING_ALL if args.all_timing_events else ctx.TIMING_FANOUT)
 
     if dist:
         dist.barrier()
@@ -395,6 +407,14 @@ def main():
     if st.status != 0:
         raise SystemExit(f"engine status {st.status}")
     k_fan = ctx.kernel_times(0)
+    if extra:
+        ctx.set_timing(ctx.TIMING_ALL)
+        for i in range(warm + steps, warm + steps + extra):
+            run_step(ctx, batches[i])
+        ctx.sync()
+        if ctx.stats().status != 0:
+            raise SystemExit("engine status after the timing steps")
+        ctx.kernel_times(0)
     k_tick = ctx.kernel_times(1)
     k_ing = ctx.kernel_times(2)
     k_key = ctx.kernel_times(3)
@@ -500,6 +520,9 @@ def main():
                       "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,
                       "ingest": round(float(np.mean(k_ing)), 4) if k_ing else None,
                       "keyframe_index": round(float(np.mean(k_key)), 4) if k_key else None},
+        "timing_events": ("every kernel's, inside the timed steps" if args.all_timing_events else
+                          f"the fan-out copy kernel's pair inside the timed steps; ingest, keyframe and plan "
+                          f"from {extra} steps after them"),
         "ingest": ingest,
         "cpu_baseline": cpu,
     }

@@ -143,6 +143,7 @@ struct edgpu_ctx {
     int num_cus = 256;
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
     uint32_t ablate = 0;
+    int timing = EDGPU_TIMING_ALL;  // edgpu_set_timing: which per-launch event pairs are recorded
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
     uint32_t tcp_copy = 3;          // EDGPU_INGEST_TCP: 3 frame state in SGPRs, DPP neighbour word, two
                                     // frames per wave round; 2 the same with per-lane frame state;
@@ -1002,6 +1003,7 @@ int edgpu_source_identity(edgpu_ctx* x, uint32_t session, uint32_t track, uint32
 // Records the start / end event of launch kind `w` into the history ring.  A pair counts (its
 // sequence number advances) only once its end event is recorded.
 static hipError_t hist_mark(edgpu_ctx* x, int w, int end, hipStream_t st = nullptr) {
+    if (x->timing < (w == 0 ? EDGPU_TIMING_FANOUT : EDGPU_TIMING_ALL)) return hipSuccess;
     const uint32_t seq = x->hist_n[w];
     hipError_t e = hipEventRecord(x->hist[w][seq % edgpu_ctx::kHist][end], st ? st : x->stream);
     if (e == hipSuccess && end) { x->last_seq[w] = seq; x->hist_n[w] = seq + 1; }
@@ -1433,7 +1435,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     HIP_CHECK(hist_mark(x, 0, 0, cs));
     HIP_CHECK(launch_fanout(f, variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
-    {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
+    if (x->timing >= EDGPU_TIMING_ALL) {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
         const uint32_t s1 = x->hist_n[1];
         x->tick_end[s1 % edgpu_ctx::kHist] = x->last_seq[0];
         x->last_seq[1] = s1;
@@ -1582,6 +1584,12 @@ int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes)
     return EDGPU_OK;
 }
 
+int edgpu_set_timing(edgpu_ctx* x, int level) {
+    if (!x || level < EDGPU_TIMING_NONE || level > EDGPU_TIMING_ALL) return fail(EDGPU_BAD_ARGUMENT, "bad timing level");
+    x->timing = level;
+    return EDGPU_OK;
+}
+
 int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     if (!x || !out_ms) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     HIP_CHECK(hipSetDevice(x->device));
@@ -1591,6 +1599,7 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     // event record costs the GPU ~5 us of idle between the kernels around it)
     auto last = [&](int w, float* o) {
         hipEvent_t a, b;
+        if (x->hist_n[w] == 0) return hipSuccess;          // nothing recorded (edgpu_set_timing)
         if (!hist_pair(x, w, x->last_seq[w], &a, &b)) return hipSuccess;
         return hipEventElapsedTime(o, a, b);
     };

@@ -37,6 +37,7 @@ EXPORTED = [
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
     "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
+    "edgpu_set_timing",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -181,6 +182,7 @@ def load(path: str = LIB_PATH):
         "edgpu_gop_span": (I32, [P, U32, U32, C.POINTER(U64), C.POINTER(U64)]),
         "edgpu_counters_get": (I32, [P, C.POINTER(Counters)]),
         "edgpu_kernel_times": (I32, [P, I32, C.POINTER(C.c_float), U32, C.POINTER(U32)]),
+        "edgpu_set_timing": (I32, [P, I32]),
         "edgpu_gop_copy": (I32, [P, U32, U32, P, U64, C.POINTER(U64), C.POINTER(U32)]),
         "edgpu_session_export": (I32, [P, P, U32, I64, P, P, U64, P, P]),
         "edgpu_session_import": (I32, [P, P, P, U32, P]),
@@ -428,6 +430,13 @@ class Context:
         c = Counters()
         _check(self.lib.edgpu_counters_get(self.h, C.byref(c)))
         return {k: getattr(c, k) for k, _ in Counters._fields_}
+
+    TIMING_NONE, TIMING_FANOUT, TIMING_ALL = 0, 1, 2
+
+    def set_timing(self, level: int):
+        """Which per-launch timing events are recorded (edgpu_set_timing): TIMING_ALL (default),
+        TIMING_FANOUT (the fan-out copy kernel's pair only) or TIMING_NONE."""
+        _check(self.lib.edgpu_set_timing(self.h, level))
 
     def kernel_times(self, which: int) -> list:
         """which: 0 fan-out kernel, 1 whole fan-out tick, 2 ingest, 3 keyframe index."""

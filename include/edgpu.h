@@ -525,6 +525,16 @@ int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
  * reads results back in between).  Syncs. */
 int  edgpu_kernel_times(edgpu_ctx* ctx, int which, float* out_ms, uint32_t max_n, uint32_t* out_n);
 
+/* Which per-launch timing events the context records from now on (default EDGPU_TIMING_ALL).
+ * Every event is a marker the stream waits on between two kernels (4-8 us of idle GPU each on
+ * MI355X, profiles/r03ak_timing_events_ab/): EDGPU_TIMING_FANOUT keeps only the fan-out copy
+ * kernel's pair (edgpu_kernel_times which = 0), EDGPU_TIMING_NONE records none.  Rings not
+ * recorded return no entries; edgpu_last_timings reports their last recorded pair, or 0. */
+#define EDGPU_TIMING_NONE    0
+#define EDGPU_TIMING_FANOUT  1
+#define EDGPU_TIMING_ALL     2
+int  edgpu_set_timing(edgpu_ctx* ctx, int level);
+
 /* Copies device memory of this context to the host (synchronous).  Reads of 256 KiB or more
  * into pinned memory from edgpu_host_alloc are done by a copy kernel storing over PCIe (faster
  * than the DMA engine's device-to-host copy here); other reads are hipMemcpy copies. */

@@ -84,6 +84,36 @@ def test_kernel_times_nonnegative_and_paired():
 
 
 @pytest.mark.gpu
+def test_timing_levels_select_the_recorded_pairs():
+    with edgpu.Context() as ctx:
+        with pytest.raises(edgpu.EdgpuError):
+            ctx.set_timing(3)
+        s = ctx.session_add(make_sdp(H264))
+        ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+
+        def ticks(n, t0):
+            for k in range(n):
+                _ingest(ctx, [(s, 0, t0 + k, _rtp(t0 + k, 90 * k))])
+                ctx.keyframe_index()
+                ctx.fanout(t0 + k)
+
+        ctx.set_timing(ctx.TIMING_NONE)          # nothing recorded yet: last timings are 0
+        ticks(3, 0)
+        assert [ctx.kernel_times(w) for w in range(4)] == [[], [], [], []]
+        assert ctx.timings()["fanout_ms"] == 0.0
+        ctx.set_timing(ctx.TIMING_FANOUT)
+        ticks(4, 10)
+        ring = [ctx.kernel_times(w) for w in range(4)]
+        assert len(ring[0]) == 4 and min(ring[0]) >= 0.0 and ring[1:] == [[], [], []]
+        ctx.set_timing(ctx.TIMING_ALL)
+        ticks(5, 20)
+        ring = [ctx.kernel_times(w) for w in range(4)]
+        assert [len(r) for r in ring] == [5, 5, 5, 5]
+        assert all(b >= a for a, b in zip(ring[0], ring[1]))
+        assert ctx.stats().status == 0
+
+
+@pytest.mark.gpu
 def test_rtp_info_play_on_empty_session_after_a_found_play():
     with edgpu.Context() as ctx:
         full = ctx.session_add(make_sdp(H264))
