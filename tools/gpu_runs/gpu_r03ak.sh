@@ -1,6 +1,7 @@
 # round 3, run ak: what the engine's per-launch timing events cost a step (measurement build):
 # the default line with every timing event vs only the fan-out's two (EDGPU_MARKS_FAN_ONLY), 3 pairs
 set -o pipefail
+# (EDGPU_MARKS_FAN_ONLY was a temporary switch of that build, superseded by edgpu_set_timing: gpu_r03am.sh)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 export EDGPU_LIB=$GRAFT_REPO_ROOT/easydarwin_amd/ab/libedgpu_ab.so
