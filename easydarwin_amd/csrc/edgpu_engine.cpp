@@ -228,9 +228,13 @@ struct edgpu_ctx {
         hipEvent_t copied = nullptr;        // its H2D copy is done (h2d stream)
         hipEvent_t consumed = nullptr;      // k_ingest + keyframe index read it (main stream)
         bool issued = false;
+        uint64_t prestaged = 0;             // blob prefix copied ahead (edgpu_ingest_prestage)
     } pin[2];
     hipStream_t h2d = nullptr;
     int pin_next = 0;
+    // edgpu_ingest_prestage may run on another thread than the other calls: it and stage_pinned
+    // share the staging sets, pin_next and the h2d stream under pin_mu
+    std::mutex pin_mu;
     int pend_stage = -1;                    // staging set of the batch pending a keyframe index
     // pending batch for keyframe_index
     const uint32_t* pend_seg = nullptr;
@@ -1142,11 +1146,10 @@ static int wait_pinned_copies(edgpu_ctx* x) {
 
 // EDGPU_PTR_PINNED: copies the batch into staging set k on the copy stream; the context stream
 // waits for it.  Returns the device pointers of the set.
-static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
-                        const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int* out_k) {
+// The staging set the next pinned batch goes to, allocated (callers hold pin_mu).
+static int pin_set(edgpu_ctx* x, edgpu_ctx::PinStage** out) {
     if (!x->h2d) HIP_CHECK(hipStreamCreateWithFlags(&x->h2d, hipStreamNonBlocking));
-    const int k = x->pin_next;
-    edgpu_ctx::PinStage& S = x->pin[k];
+    edgpu_ctx::PinStage& S = x->pin[x->pin_next];
     if (!S.desc) {
         const size_t np = x->cfg.max_batch_packets;
         if (dmalloc(&S.desc, sizeof(edgpu_pkt_desc) * np) != hipSuccess || dmalloc(&S.seg, 4 * (np + 1)) != hipSuccess ||
@@ -1155,20 +1158,51 @@ static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, co
         HIP_CHECK(hipEventCreateWithFlags(&S.copied, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&S.consumed, hipEventDisableTiming));
     }
+    *out = &S;
+    return EDGPU_OK;
+}
+
+static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uint32_t* seg_off,
+                        const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int* out_k) {
+    std::lock_guard<std::mutex> g(x->pin_mu);
+    const int k = x->pin_next;
+    edgpu_ctx::PinStage* Sp = nullptr;
+    { int r = pin_set(x, &Sp); if (r) return r; }
+    edgpu_ctx::PinStage& S = *Sp;
     // the previous batch's copy must be done before its host buffers are handed back (contract),
     // and this set's previous batch must have been read by its ingest + keyframe index
     edgpu_ctx::PinStage& P = x->pin[k ^ 1];
     if (P.issued) HIP_CHECK(hipEventSynchronize(P.copied));
-    if (S.issued) HIP_CHECK(hipStreamWaitEvent(x->h2d, S.consumed, 0));
+    if (S.issued && S.prestaged == 0) HIP_CHECK(hipStreamWaitEvent(x->h2d, S.consumed, 0));   // (a prestage waited)
     HIP_CHECK(hipMemcpyAsync(S.desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->h2d));
     HIP_CHECK(hipMemcpyAsync(S.seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->h2d));
     HIP_CHECK(hipMemcpyAsync(S.sess, seg_sess, (size_t)nseg * 4, hipMemcpyHostToDevice, x->h2d));
-    HIP_CHECK(hipMemcpyAsync(S.blob, blob, blob_bytes, hipMemcpyHostToDevice, x->h2d));
+    if (blob_bytes > S.prestaged)           // the part of the blob not copied ahead
+        HIP_CHECK(hipMemcpyAsync(S.blob + S.prestaged, blob + S.prestaged, blob_bytes - S.prestaged,
+                                 hipMemcpyHostToDevice, x->h2d));
+    S.prestaged = 0;
     HIP_CHECK(hipEventRecord(S.copied, x->h2d));
     HIP_CHECK(hipStreamWaitEvent(x->stream, S.copied, 0));
     S.issued = true;
     x->pin_next = k ^ 1;
     *out_k = k;
+    return EDGPU_OK;
+}
+
+int edgpu_ingest_prestage(edgpu_ctx* x, const uint8_t* blob, uint64_t offset, uint64_t bytes) {
+    if (!x || !blob) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!bytes) return EDGPU_OK;
+    std::lock_guard<std::mutex> g(x->pin_mu);
+    edgpu_ctx::PinStage& N = x->pin[x->pin_next];
+    if (offset != N.prestaged) return fail(EDGPU_BAD_ARGUMENT, "a prestaged range must extend the staged prefix");
+    if (offset + bytes > x->cfg.max_batch_bytes) return fail(EDGPU_BAD_ARGUMENT, "prestaged bytes exceed max_batch_bytes");
+    HIP_CHECK(hipSetDevice(x->device));
+    edgpu_ctx::PinStage* Sp = nullptr;
+    { int r = pin_set(x, &Sp); if (r) return r; }
+    edgpu_ctx::PinStage& S = *Sp;
+    if (S.prestaged == 0 && S.issued) HIP_CHECK(hipStreamWaitEvent(x->h2d, S.consumed, 0));   // its last batch was read
+    HIP_CHECK(hipMemcpyAsync(S.blob + offset, blob + offset, bytes, hipMemcpyHostToDevice, x->h2d));
+    S.prestaged = offset + bytes;
     return EDGPU_OK;
 }
 
@@ -1187,7 +1221,11 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     const uint8_t* db = blob;
     if (where == EDGPU_PTR_PINNED) {
         int r = validate_host_batch(x, desc, n, seg_off, seg_sess, nseg, blob_bytes);
-        if (r) return r;
+        if (r) {                            // nothing will use what was copied ahead
+            std::lock_guard<std::mutex> g(x->pin_mu);
+            x->pin[x->pin_next].prestaged = 0;
+            return r;
+        }
         int k = 0;
         if ((r = stage_pinned(x, desc, n, seg_off, seg_sess, nseg, blob, blob_bytes, &k))) return r;
         const edgpu_ctx::PinStage& S = x->pin[k];

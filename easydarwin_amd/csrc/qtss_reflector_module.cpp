@@ -440,6 +440,7 @@ QTSS_Error Tick() {
     o.ingested_packets = t.ingested_packets; o.ingested_bytes = t.ingested_bytes;
     o.readback_bytes = t.readback_bytes; o.arena_bytes = t.arena_bytes; o.writes = t.writes;
     o.ingest_ms = t.ingest_ms; o.fanout_ms = t.fanout_ms; o.readback_ms = t.readback_ms; o.write_ms = t.write_ms;
+    o.prestaged_bytes = t.prestaged_bytes;
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     o.ticks++;
     if (err) {

@@ -19,10 +19,30 @@ Reflector::Reflector(const edgpu_config* cfg) {
     // ticks with at least this many distinct bytes gather in parts, overlapped with the writes
     // (EDGPU_GATHER_SPLIT_BYTES; tests set 0 to run the pipelined path on small ticks)
     if (const char* v = getenv("EDGPU_GATHER_SPLIT_BYTES")) fGatherSplitBytes = strtoull(v, nullptr, 0);
+    if (const char* v = getenv("EDGPU_PRESTAGE_BYTES")) fPrestageBytes = strtoull(v, nullptr, 0);
+    if (fStatus || !fCtx) return;
+    edgpu_config c;
+    if (cfg) c = *cfg; else edgpu_config_default(&c);
+    if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;      // 0: the engine's default (edgpu_ctx_create)
+    for (Batch& b : fBatch) {
+        b.nslabs = c.max_batch_bytes / kSlab + 1;
+        b.slabPend.reset(new std::atomic<uint32_t>[b.nslabs]);
+        b.slabSealed.reset(new std::atomic<uint8_t>[b.nslabs]);
+        for (uint64_t i = 0; i < b.nslabs; i++) { b.slabPend[i].store(0); b.slabSealed[i].store(0); }
+    }
+    if (fPrestageBytes) {
+        fStageArmed = fFill;
+        fStager = std::thread([this]() { StagerLoop(); });
+    }
 }
 
 Reflector::~Reflector() {
     SetWriteThreads(1);
+    if (fStager.joinable()) {
+        { std::lock_guard<std::mutex> g(fStageMu); fStageStop = true; }
+        fStageCv.notify_all();
+        fStager.join();
+    }
     if (!fCtx) return;
     (void)edgpu_sync(fCtx);
     for (Batch& b : fBatch)
@@ -80,10 +100,34 @@ bool Reflector::GrowBlob(Batch* b, uint64_t need) {
     void* nb = nullptr;
     if (edgpu_host_alloc(fCtx, cap, &nb) != 0) return false;
     if (b->next) memcpy(nb, b->blob, b->next);
+    // the stager reads the blob pointer under fStageMu; edgpu_host_free waits for its copies
+    std::lock_guard<std::mutex> g(fStageMu);
     if (b->blob) (void)edgpu_host_free(fCtx, b->blob);
     b->blob = (uint8_t*)nb;
     b->cap = cap;
     return true;
+}
+
+// Copies the finished prefix of the batch being filled to the device (edgpu_ingest_prestage)
+// whenever it has grown by fPrestageBytes, so that the tick's ingest finds most of its blob there.
+void Reflector::StagerLoop() {
+    std::unique_lock<std::mutex> lk(fStageMu);
+    while (!fStageStop) {
+        fStageCv.wait_for(lk, std::chrono::microseconds(200));
+        if (fStageStop || fStageArmed < 0) continue;
+        Batch& b = fBatch[fStageArmed];
+        const uint64_t lim = std::min<uint64_t>(__atomic_load_n(&b.next, __ATOMIC_ACQUIRE) / kSlab, b.nslabs);
+        uint64_t e = b.staged;
+        while (e < lim && b.slabSealed[e].load(std::memory_order_acquire) &&
+               b.slabPend[e].load(std::memory_order_acquire) == 0)
+            e++;
+        if ((e - b.staged) * kSlab < fPrestageBytes) continue;
+        if (edgpu_ingest_prestage(fCtx, b.blob, b.staged * kSlab, (e - b.staged) * kSlab) != 0) {
+            fStageArmed = -1;                                // the flush copies the rest
+            continue;
+        }
+        b.staged = e;
+    }
 }
 
 int Reflector::AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle) {
@@ -140,6 +184,7 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
     const uint32_t k = session % kStripes;
     Stripe* sp = nullptr;
     uint8_t* d = nullptr;
+    std::atomic<uint32_t>* pend = nullptr;
     for (;;) {
         std::unique_lock<std::mutex> g(fStripe[k].mu);
         if (session >= fTracks.size() || track >= fTracks[session]) return;
@@ -161,9 +206,15 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
             while (off + kSlab <= b.cap &&
                    !__atomic_compare_exchange_n(&b.next, &off, off + kSlab, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
             if (off + kSlab > b.cap) continue;               // lost the race for the last slab: grow
+            // the stripe's previous slab is complete once its copies in flight are
+            if (st.cap && st.slab / kSlab < b.nslabs) b.slabSealed[st.slab / kSlab].store(1, std::memory_order_release);
             st.slab = off; st.used = 0; st.cap = kSlab;
         }
         d = b.blob + st.slab + st.used;
+        if (st.slab / kSlab < b.nslabs) {
+            pend = &b.slabPend[st.slab / kSlab];
+            pend->fetch_add(1, std::memory_order_relaxed);
+        }
         st.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, st.slab + st.used, packetLen});
         if (src) st.sources.push_back(*src);
         st.used += slot;
@@ -174,6 +225,7 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
     memset(d, 0, 4);
     memcpy(d + 4, packet, clamped);
     if (slot > clamped + 4) memset(d + 4 + clamped, 0, slot - clamped - 4);
+    if (pend) pend->fetch_sub(1, std::memory_order_release);
     sp->copying.fetch_sub(1, std::memory_order_release);
 }
 
@@ -212,9 +264,20 @@ int Reflector::FlushIngest() {
     // DMA is done -- this sync is the guarantee for error paths (idle stream: microseconds).
     int err = edgpu_sync(fCtx);
     if (err) return err;
+    {   // the stager leaves this batch
+        std::lock_guard<std::mutex> g(fStageMu);
+        fStageArmed = -1;
+        fTick.prestaged_bytes = fBatch[fFill].staged * kSlab;
+    }
     LockAllStripes();
     Batch& b = fBatch[fFill];
     fFill ^= 1;
+    {   // the batch to be filled now starts with no slab sealed and nothing copied ahead
+        Batch& nb = fBatch[fFill];
+        std::lock_guard<std::mutex> g(fStageMu);
+        for (uint64_t i = 0; i < nb.nslabs; i++) nb.slabSealed[i].store(0, std::memory_order_relaxed);
+        nb.staged = 0;
+    }
     UnlockAllStripes();
     for (Stripe& st : b.st)                                  // pushers mid-copy
         while (st.copying.load(std::memory_order_acquire)) std::this_thread::yield();
@@ -268,6 +331,10 @@ int Reflector::FlushIngest() {
     for (const Stripe& st : b.st) sources.insert(sources.end(), st.sources.begin(), st.sources.end());
     for (Stripe& st : b.st) { st.pushed.clear(); st.sources.clear(); st.slab = st.used = st.cap = 0; }
     b.next = 0;
+    if (fStager.joinable() && !err) {   // the stager streams the batch being filled into the
+        std::lock_guard<std::mutex> g(fStageMu);   // staging set the next ingest uses
+        fStageArmed = fFill;
+    }
     if (err) return err;
     if (!sources.empty() && (err = edgpu_udp_sources(fCtx, sources.data(), (uint32_t)sources.size()))) return err;
     fTick.ingest_ms = ms_since(t0);

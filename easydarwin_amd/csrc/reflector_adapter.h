@@ -44,6 +44,7 @@
 #pragma once
 #include <stdint.h>
 #include <atomic>
+#include <memory>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -151,6 +152,7 @@ public:
         uint64_t ingested_packets = 0, ingested_bytes = 0;   // batch handed to edgpu_ingest
         uint64_t readback_bytes = 0, arena_bytes = 0;       // PCIe bytes read back vs the arena
         uint64_t writes = 0;                                // OutputSink::Write calls
+        uint64_t prestaged_bytes = 0;                       // of the batch, copied ahead while it filled
         double ingest_ms = 0, fanout_ms = 0, readback_ms = 0, write_ms = 0;
     };
     const TickInfo& LastTick() const { return fTick; }
@@ -179,6 +181,14 @@ private:
         // pinned descriptor / segment arrays, filled at the flush (grouped by session)
         edgpu_pkt_desc* desc = nullptr; uint32_t* seg = nullptr; uint32_t* segSess = nullptr;
         uint64_t descCap = 0;
+        // Streaming the blob to the device while it fills (edgpu_ingest_prestage): per slab, the
+        // copies still in flight and whether its stripe has moved on to another slab.  A sealed
+        // slab with none in flight is final; the stager thread copies the prefix of final slabs
+        // ahead, and the flush copies only the rest.
+        std::unique_ptr<std::atomic<uint32_t>[]> slabPend;
+        std::unique_ptr<std::atomic<uint8_t>[]> slabSealed;
+        uint64_t nslabs = 0;                                // slabs tracked (max_batch_bytes / kSlab)
+        uint64_t staged = 0;                                // slabs copied ahead (under fStageMu)
     };
     struct alignas(64) StripeLock { std::mutex mu; };
     void LockAllStripes();
@@ -204,6 +214,16 @@ private:
         Result out[64];
     };
     void WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers);
+    void StagerLoop();
+    // the stager thread (EDGPU_PRESTAGE_BYTES: the least it copies ahead at once, default 1 MiB;
+    // 0: no stager, the flush copies the whole blob); fStageMu guards fStageArmed (the batch it
+    // streams, -1 none), the batches' `staged` and their blob pointers against GrowBlob
+    std::thread fStager;
+    std::mutex fStageMu;
+    std::condition_variable fStageCv;
+    int fStageArmed = -1;
+    bool fStageStop = false;
+    uint64_t fPrestageBytes = 1ull << 20;
     void WorkerLoop(uint32_t worker);
     edgpu_ctx* fCtx = nullptr;
     int fStatus = kRequestFailed;

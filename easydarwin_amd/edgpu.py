@@ -37,7 +37,7 @@ EXPORTED = [
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
     "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
-    "edgpu_set_timing",
+    "edgpu_set_timing", "edgpu_ingest_prestage",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -183,6 +183,7 @@ def load(path: str = LIB_PATH):
         "edgpu_counters_get": (I32, [P, C.POINTER(Counters)]),
         "edgpu_kernel_times": (I32, [P, I32, C.POINTER(C.c_float), U32, C.POINTER(U32)]),
         "edgpu_set_timing": (I32, [P, I32]),
+        "edgpu_ingest_prestage": (I32, [P, P, C.c_uint64, C.c_uint64]),
         "edgpu_gop_copy": (I32, [P, U32, U32, P, U64, C.POINTER(U64), C.POINTER(U32)]),
         "edgpu_session_export": (I32, [P, P, U32, I64, P, P, U64, P, P]),
         "edgpu_session_import": (I32, [P, P, P, U32, P]),

@@ -303,6 +303,14 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
  * batches used alternately never stall the reader on the GPU. */
 int  edgpu_host_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
+/* Copies bytes [offset, offset + bytes) of the NEXT pinned batch's blob to the device ahead of
+ * its edgpu_ingest(..., EDGPU_PTR_PINNED), on the copy stream, while the host is still filling
+ * the rest: a host whose pushers write the blob in slabs streams each finished prefix (the
+ * QTSS module drop-in does, reflector_adapter.cpp), and the ingest call then copies only the
+ * remainder.  Ranges must extend the prefix staged so far (offset == bytes already staged) and
+ * those bytes must not change before the ingest (a blob moved to a larger buffer keeps them).
+ * May be called from another thread than the context's other calls. */
+int  edgpu_ingest_prestage(edgpu_ctx* ctx, const uint8_t* blob, uint64_t offset, uint64_t bytes);
 /* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
  * Replaces RTSPRequestStream::ReadRequest's '$' branch (Server.tproj/RTSPRequestStream.cpp:
  * 65-171, RTSPSession.cpp:240-262) and the per-frame hand-off to ProcessRTPData

@@ -236,6 +236,7 @@ typedef struct EDGPU_QTSSTickInfo {
     double   ingest_ms, fanout_ms, readback_ms, write_ms, hold_ms;
     uint64_t ticks, failed_ticks;       /* since Initialize */
     int64_t  last_error;                /* the engine's code of the newest failed tick, or 0 */
+    uint64_t prestaged_bytes;           /* of the tick's batch, copied to the device while it filled */
 } EDGPU_QTSSTickInfo;
 edqtss::QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out);
 }

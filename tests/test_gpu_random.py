@@ -66,3 +66,45 @@ def test_module_matches_reference_on_random_traces(seed, oracle_bins, tmp_path):
         rtt = tmp_path / "r.edtt"
         _oracle(oracle_bins["ref"], tb, tmp_path, "ref", env={"EDGPU_TT_OUT": str(rtt)})
         assert tt.read_bytes() == rtt.read_bytes()
+
+
+def _heavy_trace():
+    """Six 8 Mb/s H.264 + AAC pushers at 1000-ms ticks: a tick's batch fills many 64-KiB slabs
+    of the module's pinned blob, so its stager copies finished slabs ahead of the tick."""
+    from easydarwin_amd.synth import TrackSpec, make_sdp, session_packets
+    from easydarwin_amd.trace import TCP, UDP, Trace
+    from scenarios import _assemble
+    tracks = [TrackSpec("video", "H264/90000", 96, bitrate=8_000_000, gop=30, idr_bytes=80_000),
+              TrackSpec("audio", "MPEG4-GENERIC/48000/2", 97)]
+    tr = Trace()
+    per = []
+    for s in range(6):
+        tr.add_session(make_sdp(tracks))
+        per.append(session_packets(tracks, 3000, 0x5EA0 + s, t0=13 * s))
+    joins = [(0, s, 10 * s + k, UDP if k < 2 else TCP) for s in range(6) for k in range(3)]
+    joins += [(1500, s, 10 * s + 5, UDP) for s in range(6)]
+    return _assemble(tr, per, 1000, 3000, joins)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prestage", ["65536", "0"])
+def test_module_streams_batches_ahead_of_the_tick(prestage, oracle_bins, tmp_path):
+    """The module's batch copied to the device slab by slab while it fills
+    (edgpu_ingest_prestage from the adapter's stager thread; EDGPU_PRESTAGE_BYTES the least it
+    copies at once, 0 = the whole batch at the tick) relays the reference's bytes and transmit
+    times either way."""
+    tr = _heavy_trace()
+    tb = tr.to_bytes()
+    want = _oracle(oracle_bins["port"], tb, tmp_path, "port")
+    t, c, tt = tmp_path / "m.edtr", tmp_path / "m.edcp", tmp_path / "m.edtt"
+    t.write_bytes(tb)
+    r = subprocess.run([QREPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_PRESTAGE_BYTES=prestage))
+    assert r.returncode == 0, r.stderr[-2000:]
+    ahead = int(r.stderr.rsplit(" bytes copied ahead", 1)[0].rsplit(" ", 1)[1])
+    assert (ahead > 0) == (prestage != "0"), r.stderr[-300:]
+    assert c.read_bytes() == want
+    if oracle_bins["ref"] is not None:
+        rtt = tmp_path / "r.edtt"
+        _oracle(oracle_bins["ref"], tb, tmp_path, "ref", env={"EDGPU_TT_OUT": str(rtt)})
+        assert tt.read_bytes() == rtt.read_bytes()

@@ -175,6 +175,7 @@ static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* bu
 }
 // QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
 static uint64_t g_writes = 0;
+static uint64_t g_prestaged = 0;                      // batch bytes the module copied ahead (trace mode)
 static bool g_count_only = false;                    // --bench: sinks count, no capture
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
@@ -428,7 +429,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
     };
     const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
     double push_s = 0, tick_s = 0, wall_s = 0, hold = 0, hold_max = 0, gpu = 0, rb = 0, wr = 0, ing = 0;
-    uint64_t rb_bytes = 0, arena = 0, ingested = 0, writes0 = 0, timed_ticks = 0;
+    uint64_t rb_bytes = 0, arena = 0, ingested = 0, writes0 = 0, timed_ticks = 0, prestaged = 0, ingested_b = 0;
     const uint32_t warm = std::min<uint32_t>(3, nticks / 4);
     // EDGPU_BENCH_CONCURRENT_PUSH=1: the pushers push the next tick's packets while a tick runs
     // (as a server's RTSP threads do; the push path never waits on a tick); default: pushing and
@@ -480,6 +481,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             hold += ti.hold_ms; hold_max = std::max(hold_max, ti.hold_ms);
             gpu += ti.fanout_ms; rb += ti.readback_ms; wr += ti.write_ms; ing += ti.ingest_ms;
             rb_bytes += ti.readback_bytes; arena += ti.arena_bytes; ingested += ti.ingested_packets;
+            prestaged += ti.prestaged_bytes; ingested_b += ti.ingested_bytes;
         }
     }
     const uint64_t relayed = stream_writes() - writes0;
@@ -490,12 +492,13 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
            "\"tick_s\": %.4f, \"wall_s\": %.4f, "
            "\"relayed_per_s\": %.1f, \"ingested_per_s\": %.1f, \"per_tick_ms\": {\"hold\": %.3f, \"hold_max\": %.3f, "
            "\"ingest\": %.3f, \"gpu_fanout\": %.3f, \"readback\": %.3f, \"writes\": %.3f}, "
-           "\"per_tick_bytes\": {\"readback\": %.0f, \"arena\": %.0f}, \"virtual_s\": %.3f}\n",
+           "\"per_tick_bytes\": {\"readback\": %.0f, \"arena\": %.0f, \"ingested\": %.0f, \"prestaged\": %.0f}, "
+           "\"virtual_s\": %.3f}\n",
            nsess, nsub, tick_ms, nthreads, wt ? wt : "4", (unsigned long long)timed_ticks,
            concurrent ? "concurrent with the ticks" : "alternating with the ticks", setup_s, (unsigned long long)relayed,
            (unsigned long long)ingested, push_s, tick_s, wall_s, relayed / std::max(wall_s, 1e-9),
            ingested / std::max(wall_s, 1e-9), hold / n, hold_max, ing / n, gpu / n, rb / n, wr / n,
-           rb_bytes / n, arena / n, timed_ticks * tick_ms / 1000.0);
+           rb_bytes / n, arena / n, ingested_b / n, prestaged / n, timed_ticks * tick_ms / 1000.0);
     return 0;
 }
 
@@ -696,6 +699,9 @@ int main(int argc, char** argv) {
         } else if (type == 3) {                                  // TICK
             const QTSS_Error e = tick_fn();
             if (e) { fprintf(stderr, "tick failed %d\n", (int)e); return 3; }
+            static auto last_tick = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
+            EDGPU_QTSSTickInfo ti;
+            if (last_tick && last_tick(&ti) == QTSS_NoErr) g_prestaged += ti.prestaged_bytes;
             read_reports();
             for (Obj* st : g_streams) st->budget[0] = st->budget[1] = -1;
         } else if (type == 4) {                                  // BLOCK
@@ -933,6 +939,7 @@ int main(int argc, char** argv) {
             }
         fclose(t);
     }
-    fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes\n", players.size(), (unsigned long long)g_writes);
+    fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes, %llu bytes copied ahead of their ticks\n", players.size(),
+            (unsigned long long)g_writes, (unsigned long long)g_prestaged);
     return 0;
 }
