@@ -1211,8 +1211,13 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
-        (where != EDGPU_PTR_DEVICE && blob_bytes > x->cfg.max_batch_bytes))
+        (where != EDGPU_PTR_DEVICE && blob_bytes > x->cfg.max_batch_bytes)) {
+        if (where == EDGPU_PTR_PINNED) {    // the batch can never go in: drop what was copied ahead
+            std::lock_guard<std::mutex> g(x->pin_mu);
+            x->pin[x->pin_next].prestaged = 0;
+        }
         return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
+    }
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
     const edgpu_pkt_desc* dd = desc;

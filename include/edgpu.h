@@ -309,7 +309,8 @@ int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
  * QTSS module drop-in does, reflector_adapter.cpp), and the ingest call then copies only the
  * remainder.  Ranges must extend the prefix staged so far (offset == bytes already staged) and
  * those bytes must not change before the ingest (a blob moved to a larger buffer keeps them).
- * May be called from another thread than the context's other calls. */
+ * May be called from another thread than the context's other calls.  A pinned batch that
+ * edgpu_ingest refuses for its size or structure drops what was copied ahead of it. */
 int  edgpu_ingest_prestage(edgpu_ctx* ctx, const uint8_t* blob, uint64_t offset, uint64_t bytes);
 /* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
  * Replaces RTSPRequestStream::ReadRequest's '$' branch (Server.tproj/RTSPRequestStream.cpp:

@@ -13,6 +13,8 @@
 """
 import os
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -111,6 +113,68 @@ def test_timing_levels_select_the_recorded_pairs():
         assert [len(r) for r in ring] == [5, 5, 5, 5]
         assert all(b >= a for a, b in zip(ring[0], ring[1]))
         assert ctx.stats().status == 0
+
+
+@pytest.mark.gpu
+def test_prestaged_pinned_batches_relay_the_same_bytes():
+    """edgpu_ingest_prestage: a pinned batch's blob prefix copied ahead in pieces, then the
+    ingest copies the rest -- every tick's arena equals the one of a plain pinned ingest; a piece
+    that does not extend the staged prefix, or runs past max_batch_bytes, is refused, and a
+    batch refused by validation drops what was copied ahead of it."""
+    rng = np.random.default_rng(7)
+    ticks = []
+    seq = 0
+    for t in range(30):
+        pkts = []
+        for s in range(3):
+            for _ in range(int(rng.integers(1, 40))):
+                n = int(rng.integers(20, 1400))
+                pkts.append((s, 0, 10 * t, _rtp(seq & 0xFFFF, 90 * t, payload=bytes([0x41]) + rng.bytes(n))))
+                seq += 1
+        ticks.append(edgpu.build_batch(pkts))
+
+    def run(prestage):
+        out = []
+        with edgpu.Context(max_batch_bytes=1 << 20) as ctx:
+            for _ in range(3):
+                ctx.subscriber_add(ctx.session_add(make_sdp(H264)), edgpu.TRANSPORT_UDP)
+            bufs = []
+            for k in range(2):
+                bufs.append({n: ctx.host_alloc(1 << 20) for n in ("desc", "seg", "sess", "blob")})
+            for t, (desc, seg, sess, blob) in enumerate(ticks):
+                B = bufs[t % 2]
+                for name, a in (("desc", desc), ("seg", seg), ("sess", sess), ("blob", blob)):
+                    v = np.ascontiguousarray(a).view(np.uint8).ravel()
+                    B[name].array[:v.nbytes] = v
+                if prestage:
+                    cut = [0, blob.nbytes // 3, (2 * blob.nbytes) // 3]
+                    for a, b in zip(cut, cut[1:]):
+                        _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(B["blob"].ptr), a, b - a))
+                    if t == 5:              # a gap in the prefix: refused
+                        assert ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(B["blob"].ptr), cut[2] + 16, 16) != 0
+                    if t == 6:              # past max_batch_bytes: refused
+                        assert ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(B["blob"].ptr), cut[2], 2 << 20) != 0
+                ctx.ingest_pinned(B["desc"].ptr, len(desc), B["seg"].ptr, B["sess"].ptr, len(sess), B["blob"].ptr,
+                                  blob.nbytes)
+                ctx.keyframe_index()
+                r = ctx.fanout(10 * t)
+                st = ctx.stats()
+                assert st.status == 0
+                out.append(bytes(ctx.copy_to_host(r.arena, st.arena_bytes)))
+            if prestage:                    # a refused batch drops what was copied ahead of it
+                desc, seg, sess, blob = ticks[0]
+                _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(bufs[0]["blob"].ptr), 0, 64))
+                with pytest.raises(edgpu.EdgpuError):
+                    ctx.ingest_pinned(bufs[0]["desc"].ptr, len(desc), bufs[0]["seg"].ptr, bufs[0]["sess"].ptr,
+                                      len(sess), bufs[0]["blob"].ptr, 2 << 20)
+                _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(bufs[0]["blob"].ptr), 0, 64))
+        return out
+
+    assert run(True) == run(False)
+
+
+def _check_ok(rc):
+    assert rc == 0, edgpu.last_error() if hasattr(edgpu, "last_error") else rc
 
 
 @pytest.mark.gpu
