@@ -113,7 +113,9 @@ bool Reflector::GrowBlob(Batch* b, uint64_t need) {
 void Reflector::StagerLoop() {
     std::unique_lock<std::mutex> lk(fStageMu);
     while (!fStageStop) {
-        fStageCv.wait_for(lk, std::chrono::microseconds(200));
+        // idle (no batch armed) until a flush arms one; while armed, a look every 200 us
+        if (fStageArmed < 0) fStageCv.wait(lk, [&] { return fStageStop || fStageArmed >= 0; });
+        else fStageCv.wait_for(lk, std::chrono::microseconds(200));
         if (fStageStop || fStageArmed < 0) continue;
         Batch& b = fBatch[fStageArmed];
         const uint64_t lim = std::min<uint64_t>(__atomic_load_n(&b.next, __ATOMIC_ACQUIRE) / kSlab, b.nslabs);
@@ -332,8 +334,11 @@ int Reflector::FlushIngest() {
     for (Stripe& st : b.st) { st.pushed.clear(); st.sources.clear(); st.slab = st.used = st.cap = 0; }
     b.next = 0;
     if (fStager.joinable() && !err) {   // the stager streams the batch being filled into the
-        std::lock_guard<std::mutex> g(fStageMu);   // staging set the next ingest uses
-        fStageArmed = fFill;
+        {                               // staging set the next ingest uses
+            std::lock_guard<std::mutex> g(fStageMu);
+            fStageArmed = fFill;
+        }
+        fStageCv.notify_one();
     }
     if (err) return err;
     if (!sources.empty() && (err = edgpu_udp_sources(fCtx, sources.data(), (uint32_t)sources.size()))) return err;
