@@ -670,6 +670,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 // 16-B words, rewriting word 0's 4-byte prefix to the '$' 0 BE16(len) frame header.  A flat
 // grid over packets keeps every CU busy regardless of how packets spread over sessions.
 // =========================================================================================
+#ifdef EDGPU_AB_VARIANTS
 constexpr int kCopyThreads = 256, kCopyLanes = 16;
 
 __global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
@@ -691,6 +692,7 @@ __global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
         if (j.vword + k >= live) ring[(j.vword + k) & j.wmask] = v;
     }
 }
+#endif  // EDGPU_AB_VARIANTS
 
 // =========================================================================================
 // Keyframe index + audio anchor: one wave per session segment.
@@ -2324,6 +2326,7 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
 
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;
+#ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
     static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();
     if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
@@ -2333,6 +2336,9 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
         const uint32_t per = kCopyThreads / kCopyLanes;
         hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
+#else
+    hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+#endif
     return hipGetLastError();
 }
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
