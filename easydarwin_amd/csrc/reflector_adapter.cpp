@@ -19,6 +19,8 @@ Reflector::Reflector(const edgpu_config* cfg) {
     // ticks with at least this many distinct bytes gather in parts, overlapped with the writes
     // (EDGPU_GATHER_SPLIT_BYTES; tests set 0 to run the pipelined path on small ticks)
     if (const char* v = getenv("EDGPU_GATHER_SPLIT_BYTES")) fGatherSplitBytes = strtoull(v, nullptr, 0);
+    if (const char* v = getenv("EDGPU_GATHER_PARTS"))
+        fGatherParts = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)atoi(v), edgpu_host::TickParts::kMax));
     if (const char* v = getenv("EDGPU_PRESTAGE_BYTES")) fPrestageBytes = strtoull(v, nullptr, 0);
     if (fStatus || !fCtx) return;
     edgpu_config c;
@@ -405,7 +407,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     // previous part's: with several write threads a gather thread brings part k + 1 over while the
     // writers deliver part k (a sub-stream only uses regions created at or before its own index).
     const edgpu_host::TickParts parts =
-        edgpu_host::tick_parts(tr, nq, fNumWriters > 1 && tr.bytes >= fGatherSplitBytes ? edgpu_host::TickParts::kMax : 1);
+        edgpu_host::tick_parts(tr, nq, fNumWriters > 1 && tr.bytes >= fGatherSplitBytes ? fGatherParts : 1);
     const uint32_t nparts = parts.n;
     const uint32_t* part_q = parts.q;
     const uint32_t* part_r = parts.r;

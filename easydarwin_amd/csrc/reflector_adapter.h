@@ -240,6 +240,7 @@ private:
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
     PinBuf fPinSubs, fPinDesc, fPinArr;                     // sub-stream table, descriptors, arrivals
     uint64_t fGatherSplitBytes = 8ull << 20;               // see ReflectPackets
+    uint32_t fGatherParts = 4;                              // EDGPU_GATHER_PARTS (<= TickParts::kMax)
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes (edgpu_arena_gather target)
     TickInfo fTick;
     // write threads (workers 1..n-1; the ticking thread is worker 0)

@@ -71,10 +71,10 @@ inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
 // adds the regions [r[k], r[k+1]).  Parts are cut at even fractions of the gathered bytes; with
 // k == 1 (or too few bytes) there is one part.
 struct TickParts {
-    static constexpr uint32_t kMax = 4;
+    static constexpr uint32_t kMax = 8;
     uint32_t n = 1;
-    uint32_t q[kMax] = {0, 0, 0, 0};            // part k holds the sub-streams below q[k]
-    uint32_t r[kMax + 1] = {0, 0, 0, 0, 0};     // part k gathers regions [r[k], r[k + 1])
+    uint32_t q[kMax] = {};                      // part k holds the sub-streams below q[k]
+    uint32_t r[kMax + 1] = {};                  // part k gathers regions [r[k], r[k + 1])
 };
 
 inline TickParts tick_parts(const TickRegions& tr, uint32_t nq, uint32_t k) {

@@ -58,7 +58,7 @@ int main() {
                 CHECK(g.offset == o.out_base && g.bytes == o.out_bytes && tr.src[q].second == 0);
             }
         }
-        for (uint32_t k = 1; k <= 4; k++) {
+        for (uint32_t k = 1; k <= edgpu_host::TickParts::kMax; k++) {
             const edgpu_host::TickParts p = edgpu_host::tick_parts(tr, nq, k);
             CHECK(p.n == k);
             CHECK(p.r[0] == 0 && p.r[p.n] == tr.reg.size() && p.q[p.n - 1] == nq);
