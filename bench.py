@@ -35,6 +35,7 @@ from easydarwin_amd.dist import reduce_run  # noqa: E402
 from easydarwin_amd.workload import H264Fleet, owned_sessions  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+C2_SECONDS = 5                 # stream seconds of the CPU baseline's C2 replay (2.6 GB of packets)
 
 
 def log(*a):
@@ -168,10 +169,95 @@ def _shard(tr, k: int, n: int):
     return out
 
 
+def baseline_cores() -> tuple[int, str]:
+    """The host cores the CPU baseline runs on: the process's affinity mask, capped by the CPU share
+    the GPU box leases to a one-GPU job (it exports OMP_NUM_THREADS = that share); the reason is
+    stated in the line when fewer than the CPU's cores are used."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = min(aff, share) if share > 0 else aff
+    why = (f"affinity mask {aff} CPUs of {os.cpu_count()}; the box leases {share} CPUs to a one-GPU job "
+           f"(OMP_NUM_THREADS={share}), so {n} processes" if n < (os.cpu_count() or n) else
+           f"every CPU of the host ({n})")
+    return n, why
+
+
+def _fleet_shards(n_sess: int, subs: int, dur_ms: int, tick_ms: int, nshards: int, td: str) -> list[str]:
+    """The bench workload itself as reference-harness traces: the C2 fleet (easydarwin_amd/workload.py
+    H264Fleet, the same generator as the GPU steps) for `dur_ms` at `tick_ms`-ms ticks, every session
+    with `subs` UDP subscribers joined at t = 0, sessions s = k mod nshards in shard k (renumbered
+    s // nshards).  Packets carry the synthetic RTP / FU-A headers; the rest of each payload is zero
+    (the reflector only moves it).  Written vectorised (trace.py format, version 1)."""
+    import struct as st
+    from easydarwin_amd.workload import H264Fleet
+    fleet = H264Fleet(np.arange(n_sess), tick_ms=tick_ms)
+    sdp = fleet.sdp().encode()
+    files = []
+    for k in range(nshards):
+        mine = len(range(k, n_sess, nshards))
+        f = open(os.path.join(td, f"c2_{k}.edtr"), "wb")
+        f.write(b"EDTR" + st.pack("<II", 1, mine) + (st.pack("<I", len(sdp)) + sdp) * mine)
+        files.append(f)
+    rec = np.dtype([("type", "u1"), ("t", "<i8"), ("session", "<u4"), ("channel", "u1"), ("len", "<u4")])
+    for tick in range(0, dur_ms + 1, tick_ms):
+        b = fleet.next_batch() if tick < dur_ms else None
+        if tick == 0:                                 # players join before the first tick
+            for k in range(nshards):
+                mine = len(range(k, n_sess, nshards))
+                j = np.zeros(mine * subs, dtype=[("type", "u1"), ("t", "<i8"), ("session", "<u4"), ("sub", "<u4"),
+                                                  ("tr", "u1"), ("ua", "u1")])
+                j["type"] = 2
+                j["session"] = np.repeat(np.arange(mine), subs)
+                j["sub"] = np.arange(mine * subs)
+                files[k].write(j.tobytes())
+        tick_rec = st.pack("<Bq", 3, tick)
+        if tick > 0 and prev is not None:
+            sess = np.repeat(np.arange(n_sess), np.diff(prev["seg_off"].astype(np.int64)))
+            order = np.argsort(prev["arrival"], kind="stable")   # arrival order across sessions
+            ln = prev["len"].astype(np.int64)
+            for k in range(nshards):
+                sel = order[(sess[order] % nshards) == k]
+                n = len(sel)
+                hdr = np.zeros(n, dtype=rec)
+                hdr["type"] = 1
+                hdr["t"] = prev["arrival"][sel]
+                hdr["session"] = sess[sel] // nshards
+                hdr["len"] = ln[sel]
+                size = 18 + ln[sel]
+                off = np.concatenate([[0], np.cumsum(size)[:-1]])
+                out = np.zeros(int(size.sum()), dtype=np.uint8)
+                out[off[:, None] + np.arange(18)] = hdr.view(np.uint8).reshape(n, 18)
+                out[off[:, None] + 18 + np.arange(12)] = prev["hdr"][sel, 4:16]
+                out[off[:, None] + 30 + np.arange(2)] = prev["fu"][sel]
+                files[k].write(out.tobytes())
+        if tick > 0:
+            for f in files:
+                f.write(tick_rec)
+        prev = b
+    for f in files:
+        f.write(b"\x00")
+        f.close()
+    return [f.name for f in files]
+
+
+def _parallel_bench(exe: str, mode: str, paths: list[str], target_s: float, extra=()):
+    """Every shard replayed by its own process at once, each repeating its replay to about
+    `target_s` seconds: (relayed packets, relayed bytes, longest process seconds, repeats)."""
+    probe = json.loads(subprocess.run([exe, mode, paths[0], *extra, "1"], capture_output=True, text=True,
+                                      check=True).stdout)
+    rep = int(max(1, min(2000, target_s / max(probe["seconds"], 1e-4))))
+    procs = [subprocess.Popen([exe, mode, p, *extra, str(rep)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                              text=True) for p in paths]
+    outs = [json.loads(pr.communicate()[0]) for pr in procs]
+    if any(pr.returncode for pr in procs):
+        return None
+    return (sum(o["relayed_packets"] for o in outs), sum(o["relayed_bytes"] for o in outs),
+            max(o["seconds"] for o in outs), rep)
+
+
 def _reference_replay(args, tick: int, procs_n: int, mode: str = "--bench"):
-    """One timed run of the reference reflector on the bounded sample at `tick`-ms ticks:
-    (relayed packets, relayed bytes, longest process seconds, repeats).  mode "--bench-udp"
-    sends every subscriber packet with a real sendto() to loopback instead of a memcpy."""
+    """The cache-resident extra line (round 3's sample): 64 sessions x 3 s at `tick`-ms ticks,
+    sharded over procs_n processes: (relayed packets, relayed bytes, longest seconds, repeats)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     tr = _sample_trace(args, tick=tick)
     with tempfile.TemporaryDirectory() as td:
@@ -180,41 +266,46 @@ def _reference_replay(args, tick: int, procs_n: int, mode: str = "--bench"):
             p = os.path.join(td, f"s{k}.edtr")
             _shard(tr, k, procs_n).write(p)
             paths.append(p)
-        probe = json.loads(subprocess.run([exe, mode, paths[0], "1"], capture_output=True, text=True,
-                                          check=True).stdout)
-        rep = int(max(1, min(2000, 1.5 / max(probe["seconds"], 1e-4))))     # ~1.5 s per process
-        procs = [subprocess.Popen([exe, mode, p, str(rep)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
-                                  text=True) for p in paths]
-        outs = [json.loads(pr.communicate()[0]) for pr in procs]
-        if any(pr.returncode for pr in procs):
-            return None
-    return (sum(o["relayed_packets"] for o in outs), sum(o["relayed_bytes"] for o in outs),
-            max(o["seconds"] for o in outs), rep)
+        return _parallel_bench(exe, mode, paths, 1.5)
 
 
 def cpu_baseline_reference(args) -> dict | None:
     """The REFERENCE reflector itself (oracle/_ref/ref_harness --bench: EasyDarwin's
     ReflectorStream / ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS
-    server, memcpy sinks) on the same bounded sample, sessions sharded over one process per
-    core, all running at once; value = relayed packets / the longest process's replay time.
-    Run at 100-ms ticks (the reflector's own wakeup scale, RS.cpp:1125-1131) and at the GPU
-    step's 1000-ms tick."""
+    server, memcpy sinks) on the bench's own C2 workload: all args.sessions sessions x args.subs
+    UDP players for C2_SECONDS of stream at 100-ms ticks (the reflector's own wakeup scale,
+    RS.cpp:1125-1131), sessions sharded over one process per leased core, all running at once;
+    value = relayed packets / the longest process's replay time.  Extra lines: the same at the GPU
+    step's 1000-ms tick, with a real sendto() per subscriber packet, and round 3's cache-resident
+    64-session sample."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(exe):
         return None
-    procs_n = min(16, os.cpu_count() or 1)
-    r100 = _reference_replay(args, 100, procs_n)
-    r1000 = _reference_replay(args, 1000, procs_n)
-    rudp = _reference_replay(args, 100, procs_n, "--bench-udp")
+    procs_n, why = baseline_cores()
+    dur = C2_SECONDS * 1000
+    with tempfile.TemporaryDirectory(dir=os.environ.get("EDGPU_BASELINE_TMP")) as td:
+        t0 = time.time()
+        paths = _fleet_shards(args.sessions, args.subs, dur, 100, procs_n, td)
+        gen_s = time.time() - t0
+        trace_gb = sum(os.path.getsize(p) for p in paths) / 1e9
+        r100 = _parallel_bench(exe, "--bench", paths, 5.0)
+        rudp = _parallel_bench(exe, "--bench-udp", paths, 3.0)
+        port = os.path.join(ROOT, "oracle", "relay_model")
+        rport = _parallel_bench(port, "--bench", paths, 5.0, extra=("1",)) if os.path.exists(port) else None
+        for p in paths:
+            os.remove(p)
+        paths1 = _fleet_shards(args.sessions, args.subs, dur, 1000, procs_n, td)
+        r1000 = _parallel_bench(exe, "--bench", paths1, 5.0)
     if r100 is None:
         return None
     pk, by, secs, rep = r100
     out = {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
-           "cpu_model": cpu_model(), "GBps": round(by / secs / 1e9, 3), "tick_ms": 100,
+           "cpu_model": cpu_model(), "cores_note": why, "GBps": round(by / secs / 1e9, 3), "tick_ms": 100,
            "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench, compiled from the reference "
-                     f"sources) on 64 H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x 3 s at 100-ms ticks, "
-                     f"sessions sharded over {procs_n} processes, each replaying its shard {rep} times; "
-                     f"{pk} relayed packets, longest process {secs:.2f} s (memcpy sinks, no sockets)"}
+                     f"sources) on the bench's C2 workload itself: {args.sessions} H.264 1080p 4 Mb/s sessions x "
+                     f"{args.subs} UDP subs x {C2_SECONDS} s of stream ({trace_gb:.2f} GB of trace, generated in "
+                     f"{gen_s:.0f} s) at 100-ms ticks, sessions sharded over {procs_n} processes, each replaying its "
+                     f"shard {rep} times; {pk} relayed packets, longest process {secs:.2f} s (memcpy sinks)"}
     if r1000 is not None:
         pk1, by1, secs1, rep1 = r1000
         out["tick_1000ms"] = {"value": round(pk1 / secs1, 1), "GBps": round(by1 / secs1 / 1e9, 3),
@@ -225,13 +316,22 @@ def cpu_baseline_reference(args) -> dict | None:
                                    "GBps": round(byu / secsu / 1e9, 3), "relayed_packets": pku,
                                    "seconds": round(secsu, 3), "repeat": repu, "tick_ms": 100,
                                    "sink": "one unread 127.0.0.1 UDP socket per process"}
+    if rport is not None:          # the clean-room restatement on the same shards
+        pkp, byp, secsp, repp = rport
+        out["restatement"] = {"value": round(pkp / secsp, 1), "cores": procs_n, "kind": "port",
+                              "sample": f"oracle/relay_model --bench, one thread per process, the same shards, "
+                                        f"{repp} replays each"}
+    small = _reference_replay(args, 100, procs_n)
+    if small is not None:          # round 3's line: a 64-session sample that stays in cache
+        pks, bys, secss, reps = small
+        out["cache_resident_64_sessions"] = {"value": round(pks / secss, 1), "relayed_packets": pks,
+                                             "seconds": round(secss, 3), "repeat": reps, "tick_ms": 100}
     return out
 
 
 def cpu_baseline(args) -> dict | None:
-    """The CPU restatement (oracle/relay_model, memcpy sinks, sessions sharded over threads)
-    on a bounded sample of the same workload: 64 sessions x subs x 3 s at 100-ms ticks."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    """The CPU restatement (oracle/relay_model --bench, memcpy sinks) on the same C2 workload,
+    one process per leased core."""
     exe = os.path.join(ROOT, "oracle", "relay_model")
     if not os.path.exists(exe):
         try:
@@ -241,24 +341,18 @@ def cpu_baseline(args) -> dict | None:
             return None
     if not os.path.exists(exe):
         return None
-    n_sess, dur = 64, 3000
-    tr = _sample_trace(args, n_sess, dur)
-    threads = min(16, os.cpu_count() or 1)
-    with tempfile.TemporaryDirectory() as td:
-        p = os.path.join(td, "cpu.edtr")
-        tr.write(p)
-        # calibrate the repeat count to ~15 s of CPU replay (the probe itself is warm)
-        probe = json.loads(subprocess.run([exe, "--bench", p, str(threads), "8"], capture_output=True,
-                                          text=True, check=True).stdout)
-        rep = int(max(1, min(5000, 8 * 15.0 / max(probe["seconds"], 1e-3))))
-        out = subprocess.run([exe, "--bench", p, str(threads), str(rep)], capture_output=True, text=True,
-                             check=True).stdout
-    r = json.loads(out)
-    return {"value": round(r["packets_per_s"], 1), "unit": "relayed RTP packets/s", "cores": threads,
-            "kind": "port", "cpu_model": cpu_model(), "GBps": round(r["relayed_bytes"] / r["seconds"] / 1e9, 3),
-            "sample": f"{rep} replays of {n_sess} H.264 1080p 4 Mb/s sessions x {args.subs} UDP subs x {dur/1000:.0f} s, "
-                      f"100-ms ticks, ingest+fan-out, memcpy sinks (oracle/relay_model --bench); "
-                      f"{r['relayed_packets']} relayed packets in {r['seconds']:.2f} s"}
+    procs_n, why = baseline_cores()
+    with tempfile.TemporaryDirectory(dir=os.environ.get("EDGPU_BASELINE_TMP")) as td:
+        paths = _fleet_shards(args.sessions, args.subs, C2_SECONDS * 1000, 100, procs_n, td)
+        r = _parallel_bench(exe, "--bench", paths, 5.0, extra=("1",))
+    if r is None:
+        return None
+    pk, by, secs, rep = r
+    return {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "port",
+            "cpu_model": cpu_model(), "cores_note": why, "GBps": round(by / secs / 1e9, 3),
+            "sample": f"oracle/relay_model --bench (one thread per process) on the C2 workload: {args.sessions} sessions x "
+                      f"{args.subs} UDP subs x {C2_SECONDS} s at 100-ms ticks, sharded over {procs_n} processes, "
+                      f"{rep} replays each; {pk} relayed packets in {secs:.2f} s"}
 
 
 def main():
@@ -479,11 +573,8 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline_reference(args)
-        port = cpu_baseline(args)
-        if cpu is None:
-            cpu = port
-        elif port is not None:
-            cpu["restatement"] = {"value": port["value"], "cores": port["cores"], "kind": "port"}
+        if cpu is None:             # no reference build travelled with the tree: the restatement
+            cpu = cpu_baseline(args)
     res = {
         "metric": "relayed RTP packets/sec (whole node) + achieved HBM GB/s, 1080p H.264 fan-out",
         "value": round(relayed_all / dt, 1),

@@ -138,6 +138,10 @@ struct SessionDev {
     uint32_t ntracks;
     uint32_t video_key_flag;        // ReflectorSession::fHasVideoKeyFrameUpdate
     uint32_t first_stream;
+    // FilterInvalidSSRCs' settings, fixed when the session is set up (SetupReflectorSession's
+    // inFilterSSRCs / inTimeout, QTSSReflectorModule.cpp:1457 -> ReflectorStream.cpp:1732-1767)
+    uint32_t ssrc_filter;           // use_one_SSRC_per_stream
+    uint32_t ssrc_timeout_s;        // timeout_stream_SSRC_secs
 };
 
 struct SubDev {                     // one sub-stream: subscriber x sender
@@ -177,7 +181,8 @@ struct SubDev {                     // one sub-stream: subscriber x sender
     uint32_t rw;
     uint32_t rw_ts;                 // RTP timestamp delta (mod 2^32)
     uint32_t rw_ssrc;               // replacement SSRC (kRwSsrc), host order
-    uint32_t _pad2;
+    uint32_t pass;                  // the tick's copy pass that delivers this sub-stream (over-
+                                    // capacity ticks; out_base / desc_base are relative to it)
 };
 
 // SubDev.rw / FanSub.rw: the per-output rewrite stage (north_star item 3).  The reference
@@ -261,7 +266,17 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long fan_t0_min, fan_done_min, fan_done_max;
     unsigned long long ing_t0_min, ing_done_min, ing_done_max;    // the same for k_ingest
     unsigned long long ing_last_span, ing_last_first;             // ... of the last finished ingest
+    // Copy passes of an over-capacity tick (edgpu_fanout_next).  Slot k & 1 belongs to the k-th
+    // launched pass: the arena bytes and descriptors its sub-streams span, and the id of the next
+    // pass (kNoPass: none).  A pass's plan resets the other slot for the pass after it.
+    unsigned long long pass_bytes[2];
+    unsigned int pass_desc[2];
+    unsigned int pass_next[2];
+    unsigned int pass_slot;         // slot of the last launched pass
+    unsigned int _pad3;
+    unsigned long long cum_lost_passes;   // passes a tick still owed when the next tick was planned
 };
+constexpr uint32_t kNoPass = 0xFFFFFFFFu;
 
 struct TickParams {
     int64_t  now;
@@ -272,6 +287,8 @@ struct TickParams {
     uint32_t nsubs;
     uint32_t nsub_blocks;
     uint32_t chunk;                 // packets per fan-out work item (per kernel variant)
+    uint32_t pass_ord;              // k_plan_pass: ordinal of the pass (1, 2, ...) and its id
+    uint32_t pass_id;
 };
 
 }  // namespace edgpu

@@ -330,31 +330,29 @@ int edgpu_egress_tcp(edgpu_egress* e, uint32_t subscriber, int fd) {
     return EDGPU_OK;
 }
 
-int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egress_stats* out) {
-    if (!e || !r) return EDGPU_BAD_ARGUMENT;
-    auto t0 = std::chrono::steady_clock::now();
-    edgpu_tick_stats st;
-    int rc = edgpu_tick_stats_get(e->ctx, &st);
-    if (rc) return eg_fail(e, rc, "tick stats");
-    if (st.status) return eg_fail(e, st.status, "device-side status after fan-out");
-    if (st.relayed_packets > e->desc_cap) {
+// One copy pass of a tick (the whole tick unless it exceeded the arena, edgpu_fanout_next): its
+// bytes to pinned memory, its sub-streams to the sockets; blocked sub-streams are appended.
+static int send_pass(edgpu_egress* e, const edgpu_fanout_result* r, const edgpu_tick_stats& st,
+                     std::vector<edgpu_blocked>& blocked, edgpu_egress_stats& s) {
+    int rc;
+    if (st.pass_packets > e->desc_cap) {
         if (e->desc) (void)hipHostFree(e->desc);
         e->desc = nullptr;
         e->desc_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(st.relayed_packets + st.relayed_packets / 2, 1 << 16);
+        const uint64_t cap = std::max<uint64_t>((uint64_t)st.pass_packets + st.pass_packets / 2, 1 << 16);
         if (hipHostMalloc((void**)&e->desc, cap * sizeof(edgpu_out_desc), hipHostMallocDefault) != hipSuccess)
             return eg_fail(e, EDGPU_OUT_OF_MEMORY, "pinned descriptors");
         e->desc_cap = cap;
     }
     e->subs.resize(r->n_substreams);
-    if ((rc = edgpu_copy_to_host(e->ctx, e->desc, r->desc, st.relayed_packets * sizeof(edgpu_out_desc))) ||
+    if ((rc = edgpu_copy_to_host(e->ctx, e->desc, r->desc, (uint64_t)st.pass_packets * sizeof(edgpu_out_desc))) ||
         (rc = edgpu_copy_to_host(e->ctx, e->subs.data(), r->substreams, r->n_substreams * sizeof(edgpu_substream_out))))
         return eg_fail(e, rc, "copy to host");
     // the distinct bytes: one region per identity sender (its longest sub-stream) + every other
     // non-empty sub-stream (tick_regions.h)
     const uint32_t nq = (uint32_t)e->subs.size();
     edgpu_host::TickRegions tr;
-    uint64_t need = st.arena_bytes;
+    uint64_t need = st.pass_arena_bytes;
     if (e->dedup) {
         tr = edgpu_host::tick_regions(e->subs.data(), nq);
         need = tr.bytes;
@@ -375,10 +373,10 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
         for (uint32_t q = 0; q < nq; q++)
             if (tr.src[q].first != edgpu_host::TickRegions::kNone) e->base[q] = tr.at(e->h_arena, q);
     } else {
-        if ((rc = edgpu_copy_to_host(e->ctx, e->h_arena, r->arena, st.arena_bytes))) return eg_fail(e, rc, "copy to host");
+        if ((rc = edgpu_copy_to_host(e->ctx, e->h_arena, r->arena, st.pass_arena_bytes))) return eg_fail(e, rc, "copy to host");
         for (uint32_t q = 0; q < nq; q++) e->base[q] = e->h_arena + e->subs[q].out_base;
     }
-    e->copied_bytes = need;
+    e->copied_bytes += need;
     auto t1 = std::chrono::steady_clock::now();
     for (Worker& w : e->workers) { w.blocked.clear(); w.udp_datagrams = w.udp_bytes = w.udp_dropped = w.tcp_frames = w.tcp_bytes = 0; }
     auto run = [&](uint32_t k) {
@@ -402,23 +400,43 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
         for (uint32_t k = 0; k < e->nthreads; k++) th.emplace_back(run, k);
         for (auto& t : th) t.join();
     }
-    auto t2 = std::chrono::steady_clock::now();
-    std::vector<edgpu_blocked> blocked;
-    edgpu_egress_stats s;
-    memset(&s, 0, sizeof(s));
+    s.send_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     for (Worker& w : e->workers) {
         blocked.insert(blocked.end(), w.blocked.begin(), w.blocked.end());
         s.udp_datagrams += w.udp_datagrams; s.udp_bytes += w.udp_bytes; s.udp_dropped += w.udp_dropped;
         s.tcp_frames += w.tcp_frames; s.tcp_bytes += w.tcp_bytes;
     }
+    return EDGPU_OK;
+}
+
+int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egress_stats* out) {
+    if (!e || !r) return EDGPU_BAD_ARGUMENT;
+    auto t0 = std::chrono::steady_clock::now();
+    edgpu_egress_stats s;
+    memset(&s, 0, sizeof(s));
+    e->copied_bytes = 0;
+    std::vector<edgpu_blocked> blocked;
+    // every copy pass of the tick, in sub-stream row order: a connection's frames keep their order
+    edgpu_fanout_result cur = *r;
+    for (;;) {
+        edgpu_tick_stats st;
+        int rc = edgpu_tick_stats_get(e->ctx, &st);
+        if (rc) return eg_fail(e, rc, "tick stats");
+        if (st.status) return eg_fail(e, st.status, "device-side status after fan-out");
+        if ((rc = send_pass(e, &cur, st, blocked, s))) return rc;
+        if (!st.more_passes) break;
+        uint32_t launched = 0;
+        if ((rc = edgpu_fanout_next(e->ctx, &cur, &launched))) return eg_fail(e, rc, "next copy pass");
+        if (!launched) break;
+    }
     std::sort(blocked.begin(), blocked.end(), [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
     s.blocked_substreams = (uint32_t)blocked.size();
-    s.copy_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    s.send_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    s.copy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - s.send_ms;
     e->last_blocked = blocked;
     for (auto& kv : e->tcp)
         if (kv.second.dead && !kv.second.reported) { e->disconnected.push_back(kv.first); kv.second.reported = true; }
     s.copied_bytes = e->copied_bytes;
+    int rc;
     if (!blocked.empty() && (rc = edgpu_fanout_blocked(e->ctx, blocked.data(), (uint32_t)blocked.size())))
         return eg_fail(e, rc, "backpressure report");
     if (out) *out = s;

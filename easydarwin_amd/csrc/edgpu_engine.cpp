@@ -29,10 +29,11 @@ hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r,
                                     uint32_t n, hipStream_t st);
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
+hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
-hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
-                               hipStream_t st);
+hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
+                               int64_t* out, hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
 hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hipStream_t st);
@@ -209,7 +210,16 @@ struct edgpu_ctx {
     DevVec<FanWork> d_work;
     DevVec<uint64_t> d_blk_bytes;
     DevVec<uint32_t> d_blk_count;
+    DevVec<uint64_t> d_blk_maxb;
+    DevVec<uint32_t> d_blk_maxc;
     bool index_dirty = true;
+    // copy passes of the last tick (edgpu_fanout_next): the current pass's ordinal and id, the
+    // kernel and buffers of the tick, and what the host knows of a further pass (-1: not read
+    // back since the last launch, 0: none, 1: one is owed)
+    uint32_t pass_ord = 0, pass_id = 0;
+    int passes_more = 0;
+    int tick_variant = 0;
+    uint64_t fanout_passes = 0;
 
     // ingest staging
     edgpu_pkt_desc* d_desc = nullptr;
@@ -278,6 +288,15 @@ struct edgpu_ctx {
 
 static bool live_session(const edgpu_ctx* x, uint32_t s) { return s < x->sessions.size() && x->sessions[s].alive; }
 
+// Calls that move the rings or the sub-stream table on are refused while the context knows the
+// last tick still owes a copy pass (edgpu_fanout_next).
+static int owed_pass(const edgpu_ctx* x, const char* what) {
+    if (x->passes_more == 1)
+        return fail(EDGPU_ERR, std::string(what) + ": the last fan-out tick has a copy pass not yet delivered "
+                                                   "(edgpu_fanout_next)");
+    return EDGPU_OK;
+}
+
 extern "C" {
 
 const char* edgpu_version(void) { return "edgpu 0.1 (gfx950)"; }
@@ -302,6 +321,7 @@ static void fill_defaults(edgpu_config& c) {
     if (!c.max_batch_packets) c.max_batch_packets = 1u << 20;
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;
     if (!c.reflector_rtp_info_offset_msec) c.reflector_rtp_info_offset_msec = 500;
+    else if (c.reflector_rtp_info_offset_msec == EDGPU_FALSE) c.reflector_rtp_info_offset_msec = 0;
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -350,7 +370,12 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (hipMalloc(&x->d_null, 4096) != hipSuccess || hipMemset(x->d_null, 0, 4096) != hipSuccess) return bad("null ring");
-    if (hipMemset(x->d_totals, 0, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    {
+        TickTotals t0;
+        memset(&t0, 0, sizeof(t0));
+        t0.pass_next[0] = t0.pass_next[1] = kNoPass;
+        if (hipMemcpy(x->d_totals, &t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess) return bad("totals");
+    }
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
 #ifdef EDGPU_AB_VARIANTS                         // measurement builds only (edgpu_params.h)
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);
@@ -371,7 +396,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_null) (void)hipFree(x->d_null);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
-    x->d_blk_bytes.release(); x->d_blk_count.release();
+    x->d_blk_bytes.release(); x->d_blk_count.release(); x->d_blk_maxb.release(); x->d_blk_maxc.release();
     x->d_img_plan.release(); x->d_sub_out_buf2.release();
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
@@ -626,7 +651,8 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
         }
         str[t].packet_count = 0;
     }
-    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream};
+    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream, x->cfg.use_one_SSRC_per_stream,
+                  x->cfg.timeout_stream_SSRC_secs};
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + sid, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
@@ -669,6 +695,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (flags & ~EDGPU_SESSION_KILL_OUTPUTS) return fail(EDGPU_BAD_ARGUMENT, "bad flags");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    if (int r = owed_pass(x, "edgpu_session_remove")) return r;
     SessionHost& sh = x->sessions[session];
     if (!sh.subs.empty() && !(flags & EDGPU_SESSION_KILL_OUTPUTS))
         return fail(EDGPU_ERR, "session still has outputs (the reference keeps a ReflectorSession while outputs "
@@ -699,7 +726,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     }
     std::vector<StreamDev> str(sh.ntracks);
     for (auto& st : str) st.packet_count = 0;
-    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream};
+    SessionDev sd{sh.first_sender, sh.ntracks, 0u, sh.first_stream, 0u, 0u};
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sh.first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + sh.first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + session, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
@@ -710,6 +737,18 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     if (session < x->carry_len.size()) x->carry_len[session] = 0;
     x->dead_sessions.push_back(session);
     x->index_dirty = true;
+    return EDGPU_OK;
+}
+
+int edgpu_session_ssrc_prefs(edgpu_ctx* x, uint32_t session, uint32_t use_one_SSRC_per_stream,
+                             uint32_t timeout_stream_SSRC_secs) {
+    if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    HIP_CHECK(hipSetDevice(x->device));
+    const uint32_t v[2] = {use_one_SSRC_per_stream ? 1u : 0u, timeout_stream_SSRC_secs};
+    // stream-ordered before the next ingest, which reads them
+    HIP_CHECK(hipMemcpyAsync(&x->d_sessions.ptr[session].ssrc_filter, v, sizeof(v), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));   // `v` is on the stack
     return EDGPU_OK;
 }
 
@@ -1064,6 +1103,8 @@ static int rebuild_index(edgpu_ctx* x) {
     if (x->overlap) HIP_CHECK(x->d_sub_out_buf2.reserve(std::max<uint32_t>(nsub, 1), x->stream));
     HIP_CHECK(x->d_blk_bytes.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_count.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_blk_maxb.reserve(std::max<uint32_t>(nblk, 1), x->stream));
+    HIP_CHECK(x->d_blk_maxc.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_work.reserve(std::max<uint64_t>(x->work_cap_needed, 1), x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
     x->index_dirty = false;
@@ -1082,9 +1123,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
-    p.filter_ssrc = x->cfg.use_one_SSRC_per_stream;
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
-    p.ssrc_timeout_s = x->cfg.timeout_stream_SSRC_secs;
     p.totals = x->d_totals;
     p.tcp_groups = tcp ? tcp->groups : nullptr;
     p.tcp_chunkres = tcp ? tcp->chunkres : nullptr;
@@ -1190,7 +1229,13 @@ static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, co
 }
 
 int edgpu_ingest_prestage(edgpu_ctx* x, const uint8_t* blob, uint64_t offset, uint64_t bytes) {
-    if (!x || !blob) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!bytes && !offset) {                // discard: the next pinned batch is copied whole
+        std::lock_guard<std::mutex> g(x->pin_mu);
+        x->pin[x->pin_next].prestaged = 0;
+        return EDGPU_OK;
+    }
+    if (!blob) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (!bytes) return EDGPU_OK;
     std::lock_guard<std::mutex> g(x->pin_mu);
     edgpu_ctx::PinStage& N = x->pin[x->pin_next];
@@ -1210,13 +1255,14 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    if (n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
+    const int owed = owed_pass(x, "edgpu_ingest");
+    if (owed || n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
         (where != EDGPU_PTR_DEVICE && blob_bytes > x->cfg.max_batch_bytes)) {
         if (where == EDGPU_PTR_PINNED) {    // the batch can never go in: drop what was copied ahead
             std::lock_guard<std::mutex> g(x->pin_mu);
             x->pin[x->pin_next].prestaged = 0;
         }
-        return fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
+        return owed ? owed : fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
     }
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
@@ -1268,6 +1314,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (where == EDGPU_PTR_DEVICE && ((uintptr_t)bytes & 15)) return fail(EDGPU_BAD_ARGUMENT, "device bytes must be 16-B aligned");
     if (where == EDGPU_PTR_HOST && nbytes > x->cfg.max_batch_bytes) return fail(EDGPU_BAD_ARGUMENT, "reads exceed max_batch_bytes");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    if (int r = owed_pass(x, "edgpu_ingest_interleaved")) return r;
     if (!n) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
     { int r = wait_pinned_copies(x); if (r) return r; }
@@ -1426,29 +1473,16 @@ static int pick_fanout_variant(const edgpu_ctx* x) {
     return x->fanout_variant >= 0 ? x->fanout_variant : fanout_default(x->n_rw + x->n_tcp > 0);
 }
 
-int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
-    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
-    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
-    if (x->overlap) {
-        // the index rebuild may reallocate tables the in-flight copy reads
-        if (x->index_dirty) HIP_CHECK(hipStreamSynchronize(x->copy));
-        // this tick's plan rewrites the work list and sub-stream records the previous copy reads
-        HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
-        x->cur ^= 1;
-    }
-    if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
+// The plan parameters of the context's current tick (arena / descriptor buffers of x->cur).
+static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
-    x->last_now = now_ms;
-    queue_source_reports(x, now_ms);
-    edgpu_substream_out* sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
-    uint8_t* arena = x->d_arena_buf[x->cur];
-    edgpu_out_desc* odesc = x->d_out_desc_buf[x->cur];
     PlanParams p;
     p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
     p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
-    p.sub_out = sub_out; p.work = x->d_work.ptr;
+    p.sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
+    p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
+    p.blk_maxb = x->d_blk_maxb.ptr; p.blk_maxc = x->d_blk_maxc.ptr;
     p.totals = x->d_totals;
     p.T.now = now_ms;
     p.T.over_buffer_ms = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
@@ -1457,14 +1491,18 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     p.T.nsenders = x->nsenders;
     p.T.nsubs = nsub;
     p.T.nsub_blocks = (nsub + 255) / 256;
-    const int variant = pick_fanout_variant(x);
-    p.T.chunk = (uint32_t)fanout_chunk(variant);
-    // the per-tick totals (relayed_*, arena, status, nwork) are reset by the plan's first kernel
-    HIP_CHECK(hist_mark(x, 1, 0));
-    HIP_CHECK(launch_plan(p, x->stream));
+    p.T.chunk = (uint32_t)fanout_chunk(x->tick_variant);
+    p.T.pass_ord = x->pass_ord;
+    p.T.pass_id = x->pass_id;
+    return p;
+}
+
+// The copy kernel of the current pass (on the copy stream with overlap_ticks, after the plan).
+static int launch_copy_pass(edgpu_ctx* x, edgpu_fanout_result* out) {
     FanoutParams f;
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
-    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr; f.arena = arena; f.desc = odesc;
+    f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr;
+    f.arena = x->d_arena_buf[x->cur]; f.desc = x->d_out_desc_buf[x->cur];
     f.arena_words = x->cfg.out_arena_bytes / 16;
     f.max_desc = x->cfg.max_out_packets;
     f.totals = x->d_totals;
@@ -1476,23 +1514,78 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
         cs = x->copy;
     }
     HIP_CHECK(hist_mark(x, 0, 0, cs));
-    HIP_CHECK(launch_fanout(f, variant, x->num_cus, cs));
+    HIP_CHECK(launch_fanout(f, x->tick_variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
+    if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
+    x->fanout_passes++;
+    x->passes_more = -1;
+    if (out) {
+        out->arena = f.arena;
+        out->desc = f.desc;
+        out->substreams = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
+        out->n_substreams = (uint32_t)x->sub_sender.size();
+    }
+    return EDGPU_OK;
+}
+
+int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    if (int r = owed_pass(x, "edgpu_fanout")) return r;
+    HIP_CHECK(hipSetDevice(x->device));
+    if (x->overlap) {
+        // the index rebuild may reallocate tables the in-flight copy reads
+        if (x->index_dirty) HIP_CHECK(hipStreamSynchronize(x->copy));
+        // this tick's plan rewrites the work list and sub-stream records the previous copy reads
+        HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
+        x->cur ^= 1;
+    }
+    if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
+    x->last_now = now_ms;
+    queue_source_reports(x, now_ms);
+    x->tick_variant = pick_fanout_variant(x);
+    x->pass_ord = 0;
+    x->pass_id = 0;
+    const PlanParams p = plan_params(x, now_ms);
+    // the per-tick totals (relayed_*, arena, status, nwork, passes) are reset by the plan's first kernel
+    HIP_CHECK(hist_mark(x, 1, 0));
+    HIP_CHECK(launch_plan(p, x->stream));
+    if (int r = launch_copy_pass(x, out)) return r;
     if (x->timing >= EDGPU_TIMING_ALL) {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
         const uint32_t s1 = x->hist_n[1];
         x->tick_end[s1 % edgpu_ctx::kHist] = x->last_seq[0];
         x->last_seq[1] = s1;
         x->hist_n[1] = s1 + 1;
     }
-    if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_launches++;
     x->timed_fanout = true;
-    if (out) {
-        out->arena = arena;
-        out->desc = odesc;
-        out->substreams = sub_out;
-        out->n_substreams = nsub;
+    return EDGPU_OK;
+}
+
+int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched) {
+    if (!x || !launched) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    *launched = 0;
+    if (x->fanout_launches == 0) return fail(EDGPU_ERR, "no fan-out tick");
+    HIP_CHECK(hipSetDevice(x->device));
+    TickTotals t;
+    HIP_CHECK(sync_all(x));                  // the host has consumed the current pass
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
+        HIP_CHECK(rb.run());
     }
+    if (t.status) return fail(t.status, "the tick failed");
+    const uint32_t next = t.pass_next[x->pass_ord & 1u];
+    if (next == kNoPass) {
+        x->passes_more = 0;
+        return EDGPU_OK;
+    }
+    x->pass_ord++;
+    x->pass_id = next;
+    const PlanParams p = plan_params(x, x->last_now);
+    HIP_CHECK(launch_plan_pass(p, x->stream));
+    if (int r = launch_copy_pass(x, out)) return r;
+    *launched = 1;
     return EDGPU_OK;
 }
 
@@ -1519,6 +1612,13 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->ingested_bytes = t.ingested_bytes;
     out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
+    const uint32_t slot = x->pass_ord & 1u;
+    out->pass_arena_bytes = t.pass_bytes[slot];
+    out->pass_packets = t.pass_desc[slot];
+    out->pass = x->pass_ord;
+    out->more_passes = (x->fanout_launches && t.pass_next[slot] != kNoPass) ? 1u : 0u;
+    out->_pad2 = 0;
+    if (x->fanout_launches) x->passes_more = (int)out->more_passes;
 #ifdef EDGPU_AB_VARIANTS
     if (getenv("EDGPU_FAN_TAIL") && t.fan_done_max > t.fan_t0_min)   // 100-MHz s_memrealtime ticks
         fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u; ingest span %.1f us, first exit at %.1f us\n",
@@ -1541,16 +1641,18 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
         HIP_CHECK(rb.run());
     }
     if (t.status) return fail(t.status, "the last tick failed");
-    if (n < t.relayed_packets) return fail(EDGPU_OUT_OVERFLOW, "arrival array smaller than the tick's descriptors");
-    if (!t.relayed_packets) return EDGPU_OK;
+    const uint32_t npass = t.pass_desc[x->pass_ord & 1u];      // the current copy pass's descriptors
+    if (n < npass) return fail(EDGPU_OUT_OVERFLOW, "arrival array smaller than the pass's descriptors");
+    if (!npass) return EDGPU_OK;
     int64_t* dst = out;
     if (kind == EDGPU_PTR_HOST) {
-        HIP_CHECK(x->d_arrivals.reserve(t.relayed_packets, x->stream));
+        HIP_CHECK(x->d_arrivals.reserve(npass, x->stream));
         dst = x->d_arrivals.ptr;
     }
-    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, (uint32_t)x->sub_sender.size(), dst, x->stream));
+    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, (uint32_t)x->sub_sender.size(), x->pass_id, dst,
+                                  x->stream));
     Readback rb(x);
-    if (kind == EDGPU_PTR_HOST) HIP_CHECK(rb.add(out, dst, (size_t)t.relayed_packets * sizeof(int64_t)));
+    if (kind == EDGPU_PTR_HOST) HIP_CHECK(rb.add(out, dst, (size_t)npass * sizeof(int64_t)));
     HIP_CHECK(rb.run());
     return EDGPU_OK;
 }
@@ -1595,6 +1697,8 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     out->fanout_launches = x->fanout_launches;
     out->ingested_packets = t.cum_ingested_packets;
     out->ingested_bytes = t.cum_ingested_bytes;
+    out->fanout_passes = x->fanout_passes;
+    out->lost_passes = t.cum_lost_passes;
     return EDGPU_OK;
 }
 

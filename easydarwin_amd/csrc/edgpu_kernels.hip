@@ -109,6 +109,25 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     return base + x - v;
 }
 
+// Reduction over a workgroup of NW waves of 64 (every thread gets the result); `scratch` holds
+// NW entries and may be reused right after.
+struct OpSum { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
+struct OpMax { template <typename T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
+struct OpMin { template <typename T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
+template <typename T, typename Op, int NW = 4>
+__device__ __forceinline__ T block_reduce(T v, T* scratch) {
+    const Op op;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+    __syncthreads();
+    T r = scratch[0];
+#pragma unroll
+    for (int w = 1; w < NW; w++) r = op(r, scratch[w]);
+    __syncthreads();
+    return r;
+}
+
 // =========================================================================================
 // Ingest
 // =========================================================================================
@@ -477,7 +496,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         p_ssrc[tid] = !acc ? 0u : (len < 8 ? 0u : (fl & kSndRtcpPort) ? hbe32(hdr, 4) : (len < 12 ? 0u : hbe32(hdr, 8)));
         p_ts[tid] = arrival / 1000;          // OS::Milliseconds() / 1000, truncating
         // ---- SSRC latch filter (sequential per socket; fast path when nothing changes) ----
-        if (P.filter_ssrc) {
+        if (S.ssrc_filter) {
             const bool ok = !acc || (s_valid[ls] != 0 && p_ssrc[tid] == s_valid[ls]);
             if (acc) atomicMax(&c_lastacc[ls], tid);       // newest accepted packet per socket
             const int allok = __syncthreads_and(ok ? 1 : 0);
@@ -494,7 +513,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                         if (ssrc == s_valid[s]) { s_lastv[s] = now_s; continue; }
                         p_len[p] = 0;                      // wrong SSRC: stays queued, length 0
                     }
-                    if (s_lastv[s] + (int64_t)P.ssrc_timeout_s < now_s) s_valid[s] = 0;
+                    if (s_lastv[s] + (int64_t)S.ssrc_timeout_s < now_s) s_valid[s] = 0;
                 }
             }
             __syncthreads();
@@ -798,6 +817,10 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
     t->status = 0; t->nwork = 0; t->fan_next = 0;
     t->fan_t0_min = ~0ull; t->fan_done_min = ~0ull; t->fan_done_max = 0;
+    // a pass the previous tick still owed is lost now (its host never called edgpu_fanout_next)
+    if (t->pass_next[t->pass_slot & 1u] != kNoPass) t->cum_lost_passes++;
+    t->pass_slot = 0;
+    for (int k = 0; k < 2; k++) { t->pass_bytes[k] = 0; t->pass_desc[k] = 0; t->pass_next[k] = kNoPass; }
 }
 
 // Per-tick counter updates as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
@@ -916,13 +939,19 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
             }
         }
     }
-    // block partials for the output-offset scan
+    // block partials for the output-offset scan, and the block's largest sub-stream (the copy
+    // passes of an over-capacity tick are cut so that any sub-stream fits one, k_plan_final)
     __shared__ uint64_t sb[4];
     __shared__ uint32_t sc[4];
     uint64_t tb; uint32_t tc;
     (void)block_exclusive_scan<uint64_t>(bytes, sb, tb);
     (void)block_exclusive_scan<uint32_t>(count, sc, tc);
-    if (threadIdx.x == 0) { P.blk_bytes[blockIdx.x] = tb; P.blk_count[blockIdx.x] = tc; }
+    const uint64_t mb = block_reduce<uint64_t, OpMax>(bytes, sb);
+    const uint32_t mc = block_reduce<uint32_t, OpMax>(count, sc);
+    if (threadIdx.x == 0) {
+        P.blk_bytes[blockIdx.x] = tb; P.blk_count[blockIdx.x] = tc;
+        P.blk_maxb[blockIdx.x] = mb; P.blk_maxc[blockIdx.x] = mc;
+    }
 }
 
 // Inclusive scan over a workgroup of up to 1024 threads: shuffles inside each wave, then the
@@ -953,54 +982,87 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     __shared__ uint64_t sb[4];
     __shared__ uint32_t sc[4];
-    uint64_t base_b = 0; uint32_t base_c = 0;
+    // Every block adds up all the K2 partials (a few hundred at most): the tick's totals, the
+    // part before this block, and the largest sub-stream.
+    uint64_t base_b, tb_all, mb;
+    uint32_t base_c, tc_all, mc;
     {
         const uint32_t nb = P.T.nsub_blocks;
-        const uint32_t lim = blockIdx.x == 0 ? nb : min((uint32_t)blockIdx.x, nb);
-        uint64_t xb = 0; uint32_t xc = 0;
-        for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x) { xb += P.blk_bytes[i]; xc += P.blk_count[i]; }
-        uint64_t tb; uint32_t tc;
-        (void)block_exclusive_scan<uint64_t>(xb, sb, tb);
-        (void)block_exclusive_scan<uint32_t>(xc, sc, tc);
-        if (blockIdx.x == 0) {
-            if (threadIdx.x == 0) {
-                P.totals->arena_bytes = tb;
-                P.totals->relayed_packets = tc;
-                P.totals->cum_relayed_packets += tc;
-                if (tb > P.T.arena_bytes || tc > P.T.max_desc) atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
-            }
-        } else {
-            base_b = tb; base_c = tc;
+        uint64_t xb = 0, xba = 0, xmb = 0;
+        uint32_t xc = 0, xca = 0, xmc = 0;
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+            const uint64_t b = P.blk_bytes[i];
+            const uint32_t c = P.blk_count[i];
+            xba += b; xca += c;
+            if (i < blockIdx.x) { xb += b; xc += c; }
+            xmb = max(xmb, P.blk_maxb[i]); xmc = max(xmc, P.blk_maxc[i]);
         }
+        base_b = block_reduce<uint64_t, OpSum>(xb, sb); tb_all = block_reduce<uint64_t, OpSum>(xba, sb);
+        mb = block_reduce<uint64_t, OpMax>(xmb, sb);
+        base_c = block_reduce<uint32_t, OpSum>(xc, sc); tc_all = block_reduce<uint32_t, OpSum>(xca, sc);
+        mc = block_reduce<uint32_t, OpMax>(xmc, sc);
+    }
+    // An over-capacity tick is delivered in copy passes over consecutive sub-stream rows
+    // (edgpu_fanout_next), every pass within the arena and the descriptor array, so no output is
+    // lost: the reference walks every output of every sender in each ReflectPackets
+    // (ReflectorStream.cpp:1088-1120).  Row q belongs to pass  floor(B_q / W) + floor(C_q / Wc),
+    // B_q / C_q its tick-global byte / descriptor offsets, W = arena - largest sub-stream (+ 16)
+    // and Wc = descriptors - largest count + 1: both floors never fall from row to row, so a pass
+    // id names one (byte window, descriptor window) pair (ids may skip), and a pass's rows --
+    // which start inside its windows -- end within one arena / descriptor array of the windows'
+    // starts, their offsets in the pass.  A tick that fits is pass 0 with global offsets.
+    const bool fits = tb_all <= P.T.arena_bytes && tc_all <= P.T.max_desc;
+    const bool impossible = mb > P.T.arena_bytes || mc > P.T.max_desc;   // one sub-stream is too large
+    const uint64_t W = (fits || impossible) ? 16ull : ((P.T.arena_bytes - mb) & ~15ull) + 16;
+    const uint32_t Wc = (fits || impossible) ? 1u : P.T.max_desc - mc + 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        P.totals->arena_bytes = tb_all;
+        P.totals->relayed_packets = tc_all;
+        P.totals->cum_relayed_packets += tc_all;
+        if (!fits && impossible) atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
+        if (fits) { P.totals->pass_bytes[0] = tb_all; P.totals->pass_desc[0] = tc_all; }
     }
     uint64_t bytes = 0; uint32_t count = 0;
     if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
     uint64_t tb; uint32_t tc;
     const uint64_t pb = block_exclusive_scan<uint64_t>(bytes, sb, tb);
     const uint32_t pc = block_exclusive_scan<uint32_t>(count, sc, tc);
+    uint64_t end_b = 0; uint32_t end_c = 0, next = kNoPass;   // pass 0's extent, the next pass
     if (q < P.T.nsubs) {
         SubDev& Q = P.subs[q];
-        Q.out_base = base_b + pb;
-        Q.desc_base = base_c + pc;
+        uint64_t ob = base_b + pb;
+        uint32_t od = base_c + pc, pass = 0;
+        if (!fits) {
+            const uint64_t kb = ob / W;
+            const uint32_t kc = od / Wc;
+            pass = (uint32_t)kb + kc;
+            ob -= kb * W;
+            od -= kc * Wc;
+        }
+        Q.out_base = ob;
+        Q.desc_base = od;
+        Q.pass = pass;
         edgpu_substream_out o;
         o.subscriber = Q.handle;
         o.track = Q.track;
         o.kind = Q.kind;
         o.transport = Q.transport;
         o.desc_base = Q.desc_base;
-        o.desc_count = Q.count;
+        o.desc_count = pass == 0 ? Q.count : 0u;
         o.out_base = Q.out_base;
-        o.out_bytes = Q.bytes;
+        o.out_bytes = pass == 0 ? Q.bytes : 0ull;
         o.sender = Q.sender;
         o.flags = ((!Q.transport && !Q.rw) ? EDGPU_SUB_IDENTITY : 0u) | (Q.was_new ? EDGPU_SUB_NEW : 0u);
         P.sub_out[q] = o;
         if (Q.count > 0) Q.sent_any = 1;
+        if (pass == 0) { end_b = ob + Q.bytes; end_c = od + Q.count; }
+        else if (Q.count > 0) next = pass;
         const uint32_t pos = P.sub_pos[q];
         if (pos != 0xFFFFFFFFu) {
             FanSub f;
             f.dw = (int64_t)(Q.out_base >> 4) - (int64_t)(Q.vstart >> 4);
             f.off = (int64_t)(Q.out_base - Q.vstart) + (Q.transport ? 0 : 4);
-            f.a = Q.nonempty ? Q.a : ~0ull;
+            f.a = (Q.nonempty && pass == 0) ? Q.a : ~0ull;
             f.ch = Q.transport ? ((uint32_t)Q.channel << 8 | 1u) : 0u;
             f.db = Q.desc_base - Q.vcstart;
             f.rw = Q.rw;
@@ -1008,6 +1070,16 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             f.rw_ssrc_be = __builtin_bswap32(Q.rw_ssrc);
             f._pad = 0;
             P.fansub[pos] = f;
+        }
+    }
+    if (!fits) {                                       // uniform over the grid
+        end_b = block_reduce<uint64_t, OpMax>(end_b, sb);
+        end_c = block_reduce<uint32_t, OpMax>(end_c, sc);
+        next = block_reduce<uint32_t, OpMin>(next, sc);
+        if (threadIdx.x == 0) {
+            if (end_b) atomicMax(&P.totals->pass_bytes[0], (unsigned long long)end_b);
+            if (end_c) atomicMax(&P.totals->pass_desc[0], end_c);
+            if (next != kNoPass) atomicMin(&P.totals->pass_next[0], next);
         }
     }
     // work items: one wave per sender (waves stride over senders), one lane per chunk.  Chunk
@@ -1063,6 +1135,45 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
             it.vb0 = vb0;
             P.work[chunk_base + k] = it;
         }
+    }
+}
+
+// A later copy pass of an over-capacity tick (edgpu_fanout_next): the rows of pass T.pass_id
+// become the tick's visible sub-streams and the copy kernel's targets (FanSub.a; every other
+// row's record is skipped), with the pass's extent and the next pass id in slot pass_ord & 1.
+// The work items and the FanSub offsets planned for the tick are reused as they are.
+__global__ __launch_bounds__(256) void k_plan_pass(PlanParams P) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t slot = P.T.pass_ord & 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        P.totals->fan_next = 0;                       // the copy kernel claims items from 0 again
+        P.totals->pass_slot = slot;
+        P.totals->pass_bytes[slot ^ 1u] = 0; P.totals->pass_desc[slot ^ 1u] = 0;
+        P.totals->pass_next[slot ^ 1u] = kNoPass;     // for the pass after this one
+    }
+    __shared__ uint64_t sb[4];
+    __shared__ uint32_t sc[4];
+    uint64_t end_b = 0; uint32_t end_c = 0, next = kNoPass;
+    if (q < P.T.nsubs) {
+        const SubDev& Q = P.subs[q];
+        const bool in = Q.pass == P.T.pass_id;
+        edgpu_substream_out& o = P.sub_out[q];
+        o.desc_base = Q.desc_base;
+        o.out_base = Q.out_base;
+        o.desc_count = in ? Q.count : 0u;
+        o.out_bytes = in ? Q.bytes : 0ull;
+        if (in) { end_b = Q.out_base + Q.bytes; end_c = Q.desc_base + Q.count; }
+        else if (Q.count > 0 && Q.pass > P.T.pass_id) next = Q.pass;
+        const uint32_t pos = P.sub_pos[q];
+        if (pos != 0xFFFFFFFFu) P.fansub[pos].a = (in && Q.nonempty) ? Q.a : ~0ull;
+    }
+    end_b = block_reduce<uint64_t, OpMax>(end_b, sb);
+    end_c = block_reduce<uint32_t, OpMax>(end_c, sc);
+    next = block_reduce<uint32_t, OpMin>(next, sc);
+    if (threadIdx.x == 0) {
+        if (end_b) atomicMax(&P.totals->pass_bytes[slot], (unsigned long long)end_b);
+        if (end_c) atomicMax(&P.totals->pass_desc[slot], end_c);
+        if (next != kNoPass) atomicMin(&P.totals->pass_next[slot], next);
     }
 }
 
@@ -2303,12 +2414,12 @@ hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hip
 // sub-stream walks its range [a, head) of the sender's metadata ring; descriptor i is the i-th
 // non-empty packet from `a` (vcount - vcstart), exactly as k_fanout4 numbered them.
 __global__ __launch_bounds__(256) void k_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs,
-                                                      int64_t* out) {
+                                                      uint32_t pass, int64_t* out) {
     const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     if (q >= nsubs) return;
     const SubDev& Q = subs[q];
-    if (!Q.active || !Q.nonempty || Q.count == 0) return;
+    if (!Q.active || !Q.nonempty || Q.count == 0 || Q.pass != pass) return;   // the current copy pass's rows
     const SenderDev& D = senders[Q.sender];
     const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
     for (uint64_t p = Q.a + lane; p < D.head; p += 64) {
@@ -2317,9 +2428,9 @@ __global__ __launch_bounds__(256) void k_desc_arrival(const SubDev* subs, const 
         if (m.len != 0 && i < Q.count) out[Q.desc_base + i] = m.arrival;
     }
 }
-hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, int64_t* out,
-                               hipStream_t st) {
-    if (nsubs) hipLaunchKernelGGL(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, out);
+hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
+                               int64_t* out, hipStream_t st) {
+    if (nsubs) hipLaunchKernelGGL(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass, out);
     return hipGetLastError();
 }
 
@@ -2374,6 +2485,10 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
     if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st) {
+    hipLaunchKernelGGL(k_plan_pass, dim3(max(p.T.nsub_blocks, 1u)), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 // Fan-out variants (EDGPU_FANOUT env var, for A/B measurement).  Each entry: kernel,

@@ -53,8 +53,6 @@ struct IngestParams {
                             // (default); 0 two aligned loads per word (EDGPU_INGEST_TCP)
     uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7: 16 no totals, 32 no slot
                             // copy, 64 no per-sender scans)
-    uint32_t filter_ssrc;
-    uint32_t ssrc_timeout_s;
     uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
     TickTotals* totals;
     // Interleaved ingest (null otherwise): segment g is deframe group g, and k_ingest finds each
@@ -92,6 +90,8 @@ struct PlanParams {
     FanSub* fansub;             // per sub_index position
     uint64_t* blk_bytes;        // per K2 block partials
     uint32_t* blk_count;
+    uint64_t* blk_maxb;         // per K2 block: the largest sub-stream (bytes, descriptors)
+    uint32_t* blk_maxc;
     TickTotals* totals;
     TickParams T;
 };

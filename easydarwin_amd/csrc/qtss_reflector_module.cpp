@@ -26,12 +26,26 @@
 // sender wakeups (ReflectorStream.cpp:1676-1714); here a tick thread reflects every
 // edgpu_tick_msec (default 20 ms), or the host calls EDGPU_QTSSReflectorModule_Tick.
 //
+// Preferences: read from the server's prefs objects exactly where the reference reads them --
+// the QTSSReflectorModule prefs object (QTSSModuleUtils::GetModulePrefsObject) for
+// ReflectorStream::Initialize's prefs at Initialize (ReflectorStream.cpp:87-117: bucket delay,
+// buffer size -> over-buffer and the new-output window, relocation threshold with its 1000-ms
+// floor, RTP-Info offset; they configure the engine context) and for the module prefs at
+// Initialize and at every QTSS_RereadPrefs_Role (RereadPrefs, QTSSReflectorModule.cpp:454-537:
+// kill_clients_when_broadcast_stops, use_one_SSRC_per_stream and timeout_stream_SSRC_secs for
+// sessions set up from then on, the RTP-Info switches, disable_overbuffering), and the server's
+// prefs object for the RTP-Info players list at every PLAY (HavePlayerProfile,
+// QTSSModuleUtils.cpp:983-1046).  A missing pref, or one of the wrong type, takes the reference's
+// default and is added to the prefs object with it, as QTSSModuleUtils::GetAttribute does
+// (QTSSModuleUtils.cpp:679-721, 798-862).  Environment variables set only engine capacities and
+// the tick (EDGPU_QTSS_*).
+//
 // Session lifecycle: reference-counted as the reference's session map does it -- the pusher
 // holds one reference (FindOrCreateSession's Register + Resolve, :1469-1477), every output one
 // (its first SETUP's Resolve, :1388, 1616-1622).  A pusher leaving (DestroySession's broadcaster
 // branch, :2082-2109) frees its tracks for a new pusher and, with kill_clients (the client
 // session's QTSSReflectorModuleTearDownClients attribute, set from the
-// kill_clients_when_broadcast_stops pref at RECORD, :1884; here EDGPU_QTSS_KILL_CLIENTS=1),
+// kill_clients_when_broadcast_stops pref at RECORD, :1884),
 // tears every output down (TearDownAllOutputs -> QTSS_Teardown, whose ClientSessionClosing then
 // removes it); at reference count 0 the session ends (RemoveOutput, :2162-2192): its engine
 // session and rings, its UDP socket pairs and its announced SDP (CSdpCache::eraseSdpMap) go.
@@ -121,6 +135,30 @@ bool GetPOD(QTSS_Object o, QTSS_AttributeID id, T* out) {
     return true;
 }
 
+// ---- preferences (QTSSModuleUtils::GetAttribute, QTSSModuleUtils.cpp:679-721, 781-862) ------
+// The attribute ID of pref `name` of type `type` in `prefs`, or false when it is missing or of
+// another type (CheckAttributeDataType: the reference then recreates it with the default).
+bool PrefID(QTSS_Object prefs, const char* name, uint32_t type, QTSS_AttributeID* id) {
+    QTSS_Object info = nullptr;
+    if (!prefs || cb(kGetAttrInfoByNameCallback, prefs, name, &info) != QTSS_NoErr || !info) return false;
+    uint32_t t = qtssAttrDataTypeUnknown, n = sizeof(t);
+    if (GetValue(info, qtssAttrDataType, 0, &t, &n) != QTSS_NoErr || t != type) return false;
+    n = sizeof(*id);
+    return GetValue(info, qtssAttrID, 0, id, &n) == QTSS_NoErr;
+}
+// Reads pref `name` into *out; a missing / mistyped / unreadable pref takes the default, which is
+// added to the prefs object (CreateAttribute: QTSS_AddInstanceAttribute + QTSS_SetValue).
+template <typename T>
+void GetPref(QTSS_Object prefs, const char* name, uint32_t type, T* out, T def) {
+    QTSS_AttributeID id = 0;
+    uint32_t n = sizeof(T);
+    if (PrefID(prefs, name, type, &id) && GetValue(prefs, id, 0, out, &n) == QTSS_NoErr && n == sizeof(T)) return;
+    *out = def;
+    if (!prefs) return;
+    (void)cb(kAddInstanceAttributeCallback, prefs, name, (void*)nullptr, type);
+    if (PrefID(prefs, name, type, &id)) (void)SetValue(prefs, id, 0, &def, sizeof(T));
+}
+
 // ---- module state ---------------------------------------------------------------------------
 // attributes the module adds (the reference's names, QTSSReflectorModule.cpp:313-346)
 QTSS_AttributeID sOutputAttr, sClientBroadcastSessionAttr, sRTSPBroadcastSessionAttr, sStreamCookieAttr,
@@ -179,12 +217,22 @@ struct Module {
     std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
     std::map<uint32_t, Output*> byHandle;
     std::vector<std::unique_ptr<Output>> outputs;
-    std::vector<std::string> rtpInfoPlayers{"Android", "vlc"};  // player_requires_rtp_header_info
     int32_t rtpInfoWaitLoops = 10;      // sWaitTimeLoopCount: 100-ms PLAY retries before 404
     uint32_t tickMs = 20;
-    int64_t overBufferMs = 10000;       // ReflectorStream::sOverBufferInMsec (reflector_buffer_size_sec)
-    int64_t bucketDelayMs = 73;         // ReflectorStream::sBucketDelayInMsec
+    // ReflectorStream::Initialize's prefs (read once, at Initialize)
+    int64_t overBufferMs = 1000;        // sOverBufferInMsec (reflector_buffer_size_sec x 1000)
+    int64_t bucketDelayMs = 73;         // sBucketDelayInMsec (reflector_bucket_offset_delay_msec)
     uint32_t bucketSize = 16;           // ReflectorStream::sBucketSize
+    // RereadPrefs' module prefs (Initialize and QTSS_RereadPrefs_Role; guarded by mu)
+    bool oneSSRC = true;                // use_one_SSRC_per_stream (sessions set up from now on)
+    uint32_t timeoutSSRC = 30;          // timeout_stream_SSRC_secs
+    bool rtpInfoDisabled = false;       // disable_rtp_play_info
+    bool playerCompat = true;           // enable_player_compatibility
+    bool forceRTPInfo = false;          // force_rtp_info_sequence_and_time
+    bool disableOverbuffering = false;  // disable_overbuffering
+    QTSS_Object modPrefs = nullptr;     // this module's prefs object
+    QTSS_Object serverPrefs = nullptr;  // the server's prefs object (player_requires_rtp_header_info)
+    uint64_t rereads = 0;
     bool manualTick = false;
     std::vector<UdpPair> udp;
     std::thread ticker, reader;
@@ -441,11 +489,15 @@ QTSS_Error Tick() {
     o.readback_bytes = t.readback_bytes; o.arena_bytes = t.arena_bytes; o.writes = t.writes;
     o.ingest_ms = t.ingest_ms; o.fanout_ms = t.fanout_ms; o.readback_ms = t.readback_ms; o.write_ms = t.write_ms;
     o.prestaged_bytes = t.prestaged_bytes;
+    o.passes = t.passes;
+    o.rereads = M->rereads;
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     o.ticks++;
     if (err) {
         // the first failure is logged with the engine's message; later ones are counted
-        if (o.failed_ticks++ == 0) fprintf(stderr, "QTSSReflectorModule: tick failed (%d): %s\n", err, edgpu_last_error());
+        if (o.failed_ticks++ == 0)
+            fprintf(stderr, "QTSSReflectorModule: tick failed (%d): %s\n", err,
+                    M->R->LastError().empty() ? edgpu_last_error() : M->R->LastError().c_str());
         o.last_error = err;
     }
     return err == 0 ? QTSS_NoErr : QTSS_RequestFailed;
@@ -477,21 +529,57 @@ QTSS_Error Register(QTSS_Register_Params* p) {
     return QTSS_NoErr;
 }
 
-QTSS_Error Initialize(QTSS_Initialize_Params*) {
+// RereadPrefs' module prefs (QTSSReflectorModule.cpp:454-537: the names, types and defaults of
+// :100-166); sessions set up from now on take the SSRC ones (:1457).  Caller holds mu.
+void ReadModulePrefsLocked() {
+    QTSS_Object o = M->modPrefs;
+    GetPref<bool>(o, "disable_rtp_play_info", qtssAttrDataTypeBool16, &M->rtpInfoDisabled, false);
+    GetPref<bool>(o, "kill_clients_when_broadcast_stops", qtssAttrDataTypeBool16, &M->killClients, false);
+    GetPref<bool>(o, "use_one_SSRC_per_stream", qtssAttrDataTypeBool16, &M->oneSSRC, true);
+    GetPref<uint32_t>(o, "timeout_stream_SSRC_secs", qtssAttrDataTypeUInt32, &M->timeoutSSRC, 30u);
+    GetPref<bool>(o, "disable_overbuffering", qtssAttrDataTypeBool16, &M->disableOverbuffering, false);
+    GetPref<bool>(o, "enable_player_compatibility", qtssAttrDataTypeBool16, &M->playerCompat, true);
+    GetPref<bool>(o, "force_rtp_info_sequence_and_time", qtssAttrDataTypeBool16, &M->forceRTPInfo, false);
+}
+
+QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     std::lock_guard<std::mutex> g(M->mu);
     if (const char* v = getenv("EDGPU_QTSS_TICK_MSEC")) M->tickMs = (uint32_t)std::max(1, atoi(v));
     if (const char* v = getenv("EDGPU_QTSS_MANUAL_TICK")) M->manualTick = atoi(v) != 0;
-    if (const char* v = getenv("EDGPU_QTSS_KILL_CLIENTS")) M->killClients = atoi(v) != 0;
+    // the prefs objects: the server's (inPrefs) and this module's (GetModulePrefsObject:
+    // qtssModPrefs of the module object, QTSSModuleUtils.cpp:634-642)
+    M->serverPrefs = ip ? ip->inPrefs : nullptr;
+    M->modPrefs = nullptr;
+    if (ip && ip->inModule) {
+        uint32_t n = sizeof(M->modPrefs);
+        if (GetValue(ip->inModule, qtssModPrefs, 0, &M->modPrefs, &n) != QTSS_NoErr) M->modPrefs = nullptr;
+    }
+    // ReflectorStream::Initialize (ReflectorStream.cpp:87-117), read once
+    uint32_t bucket = 73, bufSec = 1, relocate = 2000, rtpInfoOffset = 500;
+    GetPref<uint32_t>(M->modPrefs, "reflector_bucket_offset_delay_msec", qtssAttrDataTypeUInt32, &bucket, 73u);
+    GetPref<uint32_t>(M->modPrefs, "reflector_buffer_size_sec", qtssAttrDataTypeUInt32, &bufSec, 1u);
+    GetPref<uint32_t>(M->modPrefs, "rtp_reflector_threshold_msec", qtssAttrDataTypeUInt32, &relocate, 2000u);
+    GetPref<uint32_t>(M->modPrefs, "reflector_rtp_info_offset_msec", qtssAttrDataTypeUInt32, &rtpInfoOffset, 500u);
+    M->bucketDelayMs = bucket;
+    M->overBufferMs = (int64_t)bufSec * 1000;
+    ReadModulePrefsLocked();
     edgpu_config cfg;
     edgpu_config_default(&cfg);
+    // the engine takes the prefs with the reference's meaning (0 in edgpu_config selects its
+    // default, so a 0 pref is passed as the smallest value; the threshold's 1000-ms floor is the
+    // engine's, as in ReflectorStream::Initialize)
+    cfg.reflector_buffer_size_sec = bufSec ? bufSec : 1;
+    cfg.rtp_reflector_threshold_msec = relocate ? relocate : 1000;
+    cfg.reflector_rtp_info_offset_msec = rtpInfoOffset ? rtpInfoOffset : EDGPU_FALSE;
+    cfg.timeout_stream_SSRC_secs = M->timeoutSSRC ? M->timeoutSSRC : 30;
+    cfg.use_one_SSRC_per_stream = M->oneSSRC ? 1u : EDGPU_FALSE;
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
     // capacities for large fleets (edgpu_config; 0 / unset: the engine defaults): the fan-out
     // arena and descriptors of one tick, the ingest batch of one tick
     if (const char* v = getenv("EDGPU_QTSS_ARENA_MB")) cfg.out_arena_bytes = (uint64_t)atoll(v) << 20;
+    if (const char* v = getenv("EDGPU_QTSS_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_QTSS_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)atoll(v);
     if (const char* v = getenv("EDGPU_QTSS_MAX_BATCH_PACKETS")) cfg.max_batch_packets = (uint32_t)atoll(v);
-    // 0 selects the engine's default of 1 s (edgpu_config.reflector_buffer_size_sec)
-    M->overBufferMs = (int64_t)(cfg.reflector_buffer_size_sec ? cfg.reflector_buffer_size_sec : 1) * 1000;
     M->R.reset(new edgpu_reflector::Reflector(&cfg));
     if (M->R->Status() != 0) {
         fprintf(stderr, "QTSSReflectorModule: edgpu context: %s\n", edgpu_last_error());
@@ -514,6 +602,15 @@ QTSS_Error Initialize(QTSS_Initialize_Params*) {
             }
         });
     }
+    return QTSS_NoErr;
+}
+
+// QTSS_RereadPrefs_Role (RereadPrefs, QTSSReflectorModule.cpp:454-537): the module prefs again;
+// ReflectorStream's are read once, at Initialize, as in the reference.
+QTSS_Error RereadPrefs() {
+    std::lock_guard<std::mutex> g(M->mu);
+    ReadModulePrefsLocked();
+    M->rereads++;
     return QTSS_NoErr;
 }
 
@@ -615,6 +712,11 @@ Session* FindOrCreateSession(const std::string& name, bool isPush, bool udpPush 
     s.sdp = a->second;
     s.udpPush = udpPush;
     if (M->R->SetupReflectorSession(s.sdp, udpPush, &s.engine) != 0) return nullptr;
+    // SetupReflectorSession(..., sOneSSRCPerStream, sTimeoutSSRCSecs) with the prefs of now (:1457)
+    if (M->R->SetSSRCFilter(s.engine, M->oneSSRC, M->timeoutSSRC) != 0) {
+        (void)M->R->RemoveSession(s.engine, false);
+        return nullptr;
+    }
     s.trackIDs = SdpTrackIDs(s.sdp);
     s.trackIDs.resize(M->R->GetNumStreams(s.engine));
     s.sdpPorts = SdpPorts(s.sdp);
@@ -651,6 +753,14 @@ void ReleaseLocked(Session* s) {
     M->sessions.erase(s->id);
 }
 
+// FindOrCreateSession's last step (QRM:1540-1542): the disable_overbuffering pref turns the
+// client session's overbuffering off (the server's RTPStream then sends at the transmit times)
+void DisableOverbufferingIfPref(QTSS_Object client) {
+    if (!M->disableOverbuffering) return;
+    const bool off = false;
+    (void)SetValue(client, qtssCliSesOverBufferEnabled, 0, &off, sizeof(off));
+}
+
 // SETUP (DoSetup, QRM:1597-1800)
 QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     uint32_t mode = qtssRTPTransportModePlay, transport = qtssRTPTransportTypeUDP;
@@ -670,6 +780,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         const bool first = s == nullptr;
         if (first) s = FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
         if (!s) return QTSS_RequestFailed;
+        if (first) DisableOverbufferingIfPref(p->inClientSession);
         // the reference sets the session up for one transport; a pusher of the other cannot join it
         // (DeleteReflectorPushSession: the reference it took goes back, :1548-1570)
         auto refuse = [&]() { if (first && s->refs == 0) ReleaseLocked(s); return QTSS_RequestFailed; };
@@ -708,6 +819,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {
         Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest), false);
         if (!s) return QTSS_RequestFailed;
+        DisableOverbufferingIfPref(p->inClientSession);
         M->outputs.emplace_back(new Output());
         o = M->outputs.back().get();
         o->client = p->inClientSession;
@@ -731,12 +843,37 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)qtssSetupRespDontWriteSSRC);
 }
 
-bool RequiresRTPInfo(QTSS_Object client) {
-    const std::string ua = GetString(client, qtssCliSesFirstUserAgent);
-    if (ua.empty()) return false;
-    for (const std::string& pl : M->rtpInfoPlayers)
-        if (pl == "*" || ua.find(pl) != std::string::npos) return true;     // FindStringInAttributeList
-    return false;
+// A value of the server's prefs as a string (QTSS_GetValueAsString: the server allocates it with
+// new[], the caller deletes it, as StrPtrLenDel does)
+bool PrefString(QTSS_Object o, QTSS_AttributeID id, uint32_t idx, std::string* out) {
+    char* c = nullptr;
+    if (cb(kGetValueAsStringCallback, o, id, idx, &c) != QTSS_NoErr || !c) return false;
+    out->assign(c);
+    delete[] c;
+    return true;
+}
+
+// DoPlay's rtpInfoEnabled (QTSSReflectorModule.cpp:1872, 1962-1969): the player profile
+// kRequiresRTPInfoSeqAndTime -- HavePlayerProfile, a case-sensitive substring of the first user
+// agent in the server's player_requires_rtp_header_info list, "*" matching any
+// (QTSSModuleUtils.cpp:983-1046) -- when enable_player_compatibility; forced on by
+// force_rtp_info_sequence_and_time, off with disable_rtp_play_info.  Caller holds mu.
+bool RequiresRTPInfoLocked(QTSS_Object client) {
+    bool on = false;
+    if (M->playerCompat) {
+        const std::string ua = GetString(client, qtssCliSesFirstUserAgent);
+        uint32_t n = 0;
+        if (!ua.empty() && M->serverPrefs &&
+            cb(kGetNumValuesCallback, M->serverPrefs, (QTSS_AttributeID)qtssPrefsPlayersReqRTPHeader, &n) == QTSS_NoErr)
+            for (uint32_t i = 0; i < n; i++) {
+                std::string pl;
+                if (!PrefString(M->serverPrefs, qtssPrefsPlayersReqRTPHeader, i, &pl)) break;
+                if (pl == "*" || ua.find(pl) != std::string::npos) { on = true; break; }
+            }
+    }
+    if (M->forceRTPInfo) on = true;
+    if (M->rtpInfoDisabled) on = false;
+    return on;
 }
 
 // PLAY / RECORD (DoPlay, QRM:1867-2023)
@@ -761,7 +898,7 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
             const bool tcp = o->tcp;
             uint32_t h = 0;
             int err;
-            if (RequiresRTPInfo(o->client)) {
+            if (RequiresRTPInfoLocked(o->client)) {
                 flags = qtssPlayRespWriteTrackInfo;
                 std::vector<edgpu_rtp_info> info;
                 err = M->R->PlayRTPInfo(s->engine, tcp, Milliseconds(), &h, &info);
@@ -930,7 +1067,7 @@ QTSS_Error Dispatch(QTSS_Role role, QTSS_RoleParams* p) {
     case QTSS_Register_Role: return Register(p ? &p->regParams : nullptr);
     case QTSS_Initialize_Role: return Initialize(p ? &p->initParams : nullptr);
     case QTSS_Shutdown_Role: return Shutdown();
-    case QTSS_RereadPrefs_Role: return QTSS_NoErr;
+    case QTSS_RereadPrefs_Role: return RereadPrefs();
     case QTSS_RTSPPreProcessor_Role: return ProcessRTSPRequest(&p->rtspRequestParams);
     case QTSS_RTSPIncomingData_Role: return ProcessRTPData(&p->rtspIncomingDataParams);
     case QTSS_ClientSessionClosing_Role: return DestroySession(&p->clientSessionClosingParams);

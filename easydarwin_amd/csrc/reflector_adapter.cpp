@@ -80,6 +80,11 @@ int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint3
     return kNoErr;
 }
 
+int Reflector::SetSSRCFilter(uint32_t session, bool oneSSRCPerStream, uint32_t timeoutSecs) {
+    if (!fCtx) return kRequestFailed;
+    return edgpu_session_ssrc_prefs(fCtx, session, oneSSRCPerStream ? 1 : 0, timeoutSecs);
+}
+
 uint32_t Reflector::GetNumStreams(uint32_t session) const {
     std::lock_guard<std::mutex> g(const_cast<std::mutex&>(fStripe[session % kStripes].mu));
     return session < fTracks.size() ? fTracks[session] : 0;
@@ -161,6 +166,9 @@ int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
     // what was pushed to it before the end is ingested (the reference had queued it)
     int err = FlushIngest();
     if (err) return err;
+    // the engine first: if it refuses (outputs still attached without killOutputs, a device
+    // error), the session lives on and its pushes keep flowing
+    if ((err = edgpu_session_remove(fCtx, session, killOutputs ? EDGPU_SESSION_KILL_OUTPUTS : 0))) return err;
     {
         // later pushes to it are dropped, and what another thread pushed since the flush is
         // discarded (its id may be reused by the next session)
@@ -172,7 +180,7 @@ int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
         st.sources.erase(std::remove_if(st.sources.begin(), st.sources.end(),
                                         [&](const edgpu_udp_source& u) { return u.session == session; }), st.sources.end());
     }
-    return edgpu_session_remove(fCtx, session, killOutputs ? EDGPU_SESSION_KILL_OUTPUTS : 0);
+    return kNoErr;
 }
 
 // Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
@@ -287,6 +295,11 @@ int Reflector::FlushIngest() {
         while (st.copying.load(std::memory_order_acquire)) std::this_thread::yield();
     uint32_t n = 0;
     for (const Stripe& st : b.st) n += (uint32_t)st.pushed.size();
+    // slabs of this batch the stager copied ahead: if no pinned ingest consumes them (nothing
+    // left to ingest, e.g. RemoveSession dropped the only session's packets, or an error below),
+    // the engine must drop them, or the next batch would keep this one's prefix
+    bool ingested = false;
+    auto drop_prestage = [&]() { if (fTick.prestaged_bytes && !ingested) (void)edgpu_ingest_prestage(fCtx, nullptr, 0, 0); };
     if (n) {
         // descriptors grouped by session (a session's packets are all in one stripe, in arrival
         // order): a stable counting sort by session id; the slots stay where the pushers wrote them
@@ -311,6 +324,7 @@ int Reflector::FlushIngest() {
                 (err = edgpu_host_alloc(fCtx, (cap + 1) * sizeof(uint32_t), &sg)) ||
                 (err = edgpu_host_alloc(fCtx, cap * sizeof(uint32_t), &ss))) {
                 for (void* p : {d, sg, ss}) if (p) (void)edgpu_host_free(fCtx, p);
+                drop_prestage();
                 return err;
             }
             b.desc = (edgpu_pkt_desc*)d; b.seg = (uint32_t*)sg; b.segSess = (uint32_t*)ss; b.descCap = cap;
@@ -329,8 +343,10 @@ int Reflector::FlushIngest() {
         b.seg[nseg] = n;
         fTick.ingested_packets = n;
         err = edgpu_ingest(fCtx, b.desc, n, b.seg, b.segSess, nseg, b.blob, b.next, EDGPU_PTR_PINNED);
+        ingested = true;                                     // (a refused batch drops the prestage itself)
         if (!err) err = edgpu_keyframe_index(fCtx);
     }
+    drop_prestage();
     std::vector<edgpu_udp_source> sources;
     for (const Stripe& st : b.st) sources.insert(sources.end(), st.sources.begin(), st.sources.end());
     for (Stripe& st : b.st) { st.pushed.clear(); st.sources.clear(); st.slab = st.used = st.cap = 0; }
@@ -350,11 +366,13 @@ int Reflector::FlushIngest() {
 
 int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if (!fCtx) return kRequestFailed;
+    fLastErr.clear();
     int err = FlushIngest();
     if (err) return err;
     auto t0 = Clock::now();
     fTick.readback_bytes = fTick.arena_bytes = fTick.writes = 0;
     fTick.fanout_ms = fTick.readback_ms = fTick.write_ms = 0;
+    fTick.passes = 0;
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
     uint32_t nrr = 0;
@@ -370,11 +388,37 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     fTick.fanout_ms = ms_since(t0);
     if (st.status) return st.status;
     fTick.arena_bytes = st.arena_bytes;
-    if (!sink || st.relayed_packets == 0) return kNoErr;
-    t0 = Clock::now();
+    // A tick over the arena comes in copy passes of consecutive sub-stream rows (edgpu_fanout_next):
+    // each is delivered before the next is copied, so every output gets the whole tick, in the order
+    // one pass would have written it.  Backpressure reports cover the whole tick.
+    std::vector<edgpu_blocked> blocked;
+    for (uint32_t pass = 0;; pass++) {
+        fTick.passes++;
+        if (sink && st.pass_packets) {
+            if ((err = DeliverPass(res, st, sink, pass == 0, &blocked))) return err;
+        }
+        if (!st.more_passes) break;
+        uint32_t launched = 0;
+        if ((err = edgpu_fanout_next(fCtx, &res, &launched))) return err;
+        if (!launched) break;
+        if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
+        if (st.status) return st.status;
+    }
+    if (blocked.empty()) return kNoErr;
+    std::sort(blocked.begin(), blocked.end(),
+              [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
+    return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
+}
+
+// One copy pass: its sub-stream table, descriptors (and arrivals) and distinct bytes come to pinned
+// memory, and the write threads deliver its sub-streams; the ones that blocked are appended.
+int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stats& st, OutputSink* sink,
+                           bool firstPass, std::vector<edgpu_blocked>* blockedOut) {
+    int err;
+    auto t0 = Clock::now();
     // the sub-stream table, descriptors (and arrivals) land in pinned buffers: one DMA each
     const uint32_t nq = res.n_substreams;
-    const uint64_t nd = st.relayed_packets;
+    const uint64_t nd = st.pass_packets;
     if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out))) ||
         (err = EnsurePinned(fPinDesc, nd * sizeof(edgpu_out_desc))))
         return err;
@@ -382,7 +426,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
     if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
     if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
-    // the tick's distinct bytes only: one region per identity sender + the other sub-streams
+    // the pass's distinct bytes only: one region per identity sender + the other sub-streams
     const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq);
     if (tr.bytes > fHostOutCap) {            // grown geometrically: pinning costs ~40 ms per call
         if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
@@ -393,7 +437,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fHostOut = (uint8_t*)h;
         fHostOutCap = cap;
     }
-    fTick.readback_bytes = tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
+    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
     const int64_t* arrival = nullptr;
     if (sink->WantsArrivals()) {
         if ((err = EnsurePinned(fPinArr, nd * sizeof(int64_t)))) return err;
@@ -421,11 +465,13 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     std::atomic<uint32_t> ready{1};
     std::atomic<bool> failed{false};
     int gatherErr = kNoErr;
+    std::string gatherMsg;
     std::thread gatherer;
     if (nparts > 1)
         gatherer = std::thread([&] {
             for (uint32_t k = 1; k < nparts; k++) {
                 if ((gatherErr = gather(k))) {
+                    gatherMsg = edgpu_last_error();          // per thread: keep it for the tick thread
                     failed.store(true, std::memory_order_relaxed);
                     ready.store(nparts, std::memory_order_release);   // release the waiting writers
                     return;
@@ -433,9 +479,9 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
                 ready.store(k + 1, std::memory_order_release);
             }
         });
-    fTick.readback_ms = ms_since(t0);
+    fTick.readback_ms += ms_since(t0);
     t0 = Clock::now();
-    sink->BeginTick(subs, nq);
+    if (firstPass) sink->BeginTick(subs, nq);               // every row carries its flags in every pass
     WriteJob job;
     job.subs = subs; job.nsubs = nq;
     job.desc = d; job.arrival = arrival;
@@ -460,21 +506,17 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
         fJob = nullptr;
     }
     if (gatherer.joinable()) gatherer.join();
-    if (gatherErr) return gatherErr;
+    if (gatherErr) return fail_with(gatherErr, gatherMsg);
     // SendPacketsToOutput (ReflectorStream.cpp:1138-1198): a write that would block stopped its
-    // sub-stream for the tick; the engine bookmarks the blocked packet (reports in sub-stream order)
-    std::vector<edgpu_blocked> blocked;
+    // sub-stream for the tick; the engine bookmarks the blocked packet
     for (uint32_t k = 0; k < nw; k++) {
         const WriteJob::Result& r = job.out[k];
         fTick.writes += r.writes;
         if (r.err) return r.err;
-        blocked.insert(blocked.end(), r.blocked.begin(), r.blocked.end());
+        blockedOut->insert(blockedOut->end(), r.blocked.begin(), r.blocked.end());
     }
-    fTick.write_ms = ms_since(t0);
-    if (blocked.empty()) return kNoErr;
-    std::sort(blocked.begin(), blocked.end(),
-              [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
-    return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
+    fTick.write_ms += ms_since(t0);
+    return kNoErr;
 }
 
 // The worker of a sub-stream: by its session (the sender of track t, kind k is the session's first

@@ -117,6 +117,9 @@ public:
     // push session from its SDP; udpPush: RTCP arrives on a bound odd port (Q12/Q14)
     int  SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession);
     uint32_t GetNumStreams(uint32_t session) const;
+    // the session's SSRC filter settings, from the module prefs when it is set up
+    // (SetupReflectorSession's inFilterSSRCs / inTimeout, QTSSReflectorModule.cpp:1457)
+    int  SetSSRCFilter(uint32_t session, bool oneSSRCPerStream, uint32_t timeoutSecs);
     // player joins every track of `session`; takes effect at the next ReflectPackets
     int  AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle);
     // PLAY of an RTP-Info player (UA "vlc"/"Android"; DoPlay + HaveStreamBuffers,
@@ -153,12 +156,21 @@ public:
         uint64_t readback_bytes = 0, arena_bytes = 0;       // PCIe bytes read back vs the arena
         uint64_t writes = 0;                                // OutputSink::Write calls
         uint64_t prestaged_bytes = 0;                       // of the batch, copied ahead while it filled
+        uint32_t passes = 0;                                // copy passes (> 1: the tick exceeded the arena)
         double ingest_ms = 0, fanout_ms = 0, readback_ms = 0, write_ms = 0;
     };
     const TickInfo& LastTick() const { return fTick; }
+    // the message of the last ReflectPackets failure that happened on another thread than the
+    // caller's (edgpu_last_error() is per thread); empty otherwise
+    const std::string& LastError() const { return fLastErr; }
 
 private:
     int  FlushIngest();                                     // edgpu_ingest + keyframe index
+    // one copy pass of a tick to the sink (ReflectPackets)
+    int  DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stats& st, OutputSink* sink, bool firstPass,
+                     std::vector<edgpu_blocked>* blockedOut);
+    int  fail_with(int code, const std::string& msg) { fLastErr = msg; return code; }
+    std::string fLastErr;
     // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob
     struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint64_t slot; uint32_t len; };
     // The push path is striped by session (session % kStripes): a pusher takes only its stripe's

@@ -37,7 +37,7 @@ EXPORTED = [
     "edgpu_udp_sources", "edgpu_source_reports", "edgpu_source_identity", "edgpu_session_eyes_add",
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
     "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
-    "edgpu_set_timing", "edgpu_ingest_prestage",
+    "edgpu_set_timing", "edgpu_ingest_prestage", "edgpu_fanout_next", "edgpu_session_ssrc_prefs",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -103,7 +103,9 @@ class FanoutResult(C.Structure):
 class TickStats(C.Structure):
     _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
                 ("arena_bytes", C.c_uint64), ("ingested_packets", C.c_uint64),
-                ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32)]
+                ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32),
+                ("pass_arena_bytes", C.c_uint64), ("pass_packets", C.c_uint32), ("pass_", C.c_uint32),
+                ("more_passes", C.c_uint32), ("_pad2", C.c_uint32)]
 
 
 class EgressStats(C.Structure):
@@ -116,7 +118,8 @@ class EgressStats(C.Structure):
 class Counters(C.Structure):
     _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
                 ("fanout_in_bytes", C.c_uint64), ("fanout_launches", C.c_uint64),
-                ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64)]
+                ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64),
+                ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64)]
 
 
 # numpy mirrors (same layout as the C structs)
@@ -170,12 +173,14 @@ def load(path: str = LIB_PATH):
         "edgpu_sync": (I32, [P]),
         "edgpu_session_add": (I32, [P, C.c_char_p, U32, I32, C.POINTER(U32)]),
         "edgpu_session_tracks": (I32, [P, U32, C.POINTER(U32)]),
+        "edgpu_session_ssrc_prefs": (I32, [P, U32, U32, U32]),
         "edgpu_session_remove": (I32, [P, U32, U32]),
         "edgpu_subscriber_add": (I32, [P, U32, I32, C.POINTER(U32)]),
         "edgpu_subscriber_remove": (I32, [P, U32]),
         "edgpu_ingest": (I32, [P, P, U32, P, P, U32, P, U64, I32]),
         "edgpu_keyframe_index": (I32, [P]),
         "edgpu_fanout": (I32, [P, I64, C.POINTER(FanoutResult)]),
+        "edgpu_fanout_next": (I32, [P, C.POINTER(FanoutResult), C.POINTER(U32)]),
         "edgpu_tick_stats_get": (I32, [P, C.POINTER(TickStats)]),
         "edgpu_copy_to_host": (I32, [P, P, P, U64]),
         "edgpu_last_timings": (I32, [P, C.POINTER(C.c_float)]),
@@ -280,6 +285,10 @@ class Context:
         out = C.c_uint32()
         _check(self.lib.edgpu_session_tracks(self.h, session, C.byref(out)))
         return out.value
+
+    def session_ssrc_prefs(self, session: int, use_one_ssrc: bool, timeout_s: int):
+        """The session's SSRC filter prefs (edgpu_session_ssrc_prefs)."""
+        _check(self.lib.edgpu_session_ssrc_prefs(self.h, session, 1 if use_one_ssrc else 0, int(timeout_s)))
 
     def session_remove(self, session: int, kill_outputs: bool = False):
         """The end of a ReflectorSession (reference count 0); kill_outputs tears its subscribers
@@ -410,6 +419,14 @@ class Context:
         _check(self.lib.edgpu_fanout(self.h, int(now_ms), C.byref(r)))
         return r
 
+    def fanout_next(self):
+        """The next copy pass of an over-capacity tick (edgpu_fanout_next): its result, or None
+        when the tick is complete."""
+        r = FanoutResult()
+        launched = C.c_uint32()
+        _check(self.lib.edgpu_fanout_next(self.h, C.byref(r), C.byref(launched)))
+        return r if launched.value else None
+
     def stats(self) -> TickStats:
         s = TickStats()
         _check(self.lib.edgpu_tick_stats_get(self.h, C.byref(s)))
@@ -505,14 +522,26 @@ class Context:
         return out[:n]
 
     def read_tick(self, r: FanoutResult):
-        """(stats, substream table, descriptors, arena) of the last fan-out, on the host."""
+        """(stats, substream table, descriptors, arena) of the current copy pass of the last
+        fan-out (the whole tick unless it exceeded the arena: st.more_passes, fanout_next), on
+        the host."""
         st = self.stats()
         if st.status != OK:
             raise EdgpuError(st.status, "device-side status after fan-out")
         subs = self.copy_to_host(r.substreams, r.n_substreams * SUB_DTYPE.itemsize).view(SUB_DTYPE)
-        desc = self.copy_to_host(r.desc, st.relayed_packets * OUT_DTYPE.itemsize).view(OUT_DTYPE)
-        arena = self.copy_to_host(r.arena, st.arena_bytes)
+        desc = self.copy_to_host(r.desc, st.pass_packets * OUT_DTYPE.itemsize).view(OUT_DTYPE)
+        arena = self.copy_to_host(r.arena, st.pass_arena_bytes)
         return st, subs, desc, arena
+
+    def read_passes(self, r: FanoutResult, consume):
+        """Reads every copy pass of the tick whose first pass is `r`: consume(stats, subs, desc,
+        arena) per pass, in sub-stream row order.  Returns the number of passes."""
+        n = 0
+        while r is not None:
+            consume(*self.read_tick(r))
+            n += 1
+            r = self.fanout_next()
+        return n
 
 
 class Egress:

@@ -14,6 +14,11 @@ events of a session without a pusher are dropped, as the reference harness drops
 Without replicas, joins are made at their JOIN event (the engine applies them at the next
 fan-out either way), so a join that finds no session fails then, as in the reference.
 
+Preferences (trace v4): the stream prefs configure the context (edgpu_config), the module prefs
+are kept as the module keeps them and change at PREFS events (RereadPrefs): a new session's SSRC
+filter settings (edgpu_session_ssrc_prefs), a pusher's kill-clients attribute at its RECORD and
+the kill at its leave, and which players take the RTP-Info PLAY (trace.rtp_info_player).
+
 UPKT events (UDP pushers) are ingested like PKTs and their source addresses go to
 ``edgpu_udp_sources`` with the batch; the receiver reports each ``edgpu_fanout`` queues
 (``edgpu_source_reports``) form the capture's EDRR trailer.  Each track's report identity is
@@ -35,8 +40,8 @@ import struct
 import numpy as np
 
 from . import edgpu
-from .trace import (BLOCK, JOIN, LEAVE, PKT, PUBLISH, TICK, UNPUBLISH, UPKT, Trace, pack_source_reports,
-                    rr_ssrc)
+from .trace import (BLOCK, JOIN, LEAVE, PKT, PREFS, PUBLISH, TICK, UNPUBLISH, UPKT, Trace, pack_source_reports,
+                    pref_bool, pref_values, rr_ssrc, rtp_info_player)
 
 
 def _wire_images(subs, desc, arena, images, budgets=None):
@@ -155,7 +160,10 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
     the indices of the batches a PUBLISH / UNPUBLISH ends (no frame is carried past them)."""
     out, cur, any_pkt, barriers = [], [], False, set()
     published = [True] * len(trace.sdps)
+    prefs = trace.prefs
     for ev in trace.events:
+        if ev[0] == PREFS:
+            prefs = ev[2]
         if ev[0] == PKT:
             _, t, s, ch, data = ev
             if not published[s]:
@@ -165,7 +173,7 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
         elif ev[0] == UPKT:
             if published[ev[2]]:
                 any_pkt = True
-        elif (ev[0] == JOIN and ev[5] & 1 and flush_on_rtpinfo) or ev[0] in (TICK, PUBLISH, UNPUBLISH):
+        elif (ev[0] == JOIN and rtp_info_player(prefs, ev[5]) and flush_on_rtpinfo) or ev[0] in (TICK, PUBLISH, UNPUBLISH):
             if any_pkt:
                 out.append(cur)
                 cur, any_pkt = [], False
@@ -178,7 +186,7 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
            interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None,
-           pinned: bool = False, **cfg):
+           pinned: bool = False, tick_info: list | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -200,9 +208,19 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     (edgpu_subscriber_rewrite) on every track of those subscribers, set at their join.
 
     pinned=True: every ingest batch is written into pinned host buffers (edgpu_host_alloc,
-    two sets used alternately) and handed over as EDGPU_PTR_PINNED (asynchronous copy)."""
+    two sets used alternately) and handed over as EDGPU_PTR_PINNED (asynchronous copy).
+
+    tick_info=[]: receives, per tick read back, (copy passes, largest sub-stream's arena bytes,
+    largest sub-stream's descriptors, the tick's arena bytes, its relayed packets) -- more than
+    one pass when a tick exceeds out_arena_bytes or max_out_packets (edgpu_fanout_next)."""
     if replica is not None and trace.has_lifecycle:
         raise ValueError("replica replays take no PUBLISH / UNPUBLISH events")
+    pv = pref_values(trace.prefs)           # the stream prefs: read once (ReflectorStream::Initialize)
+    cfg = dict(cfg)
+    cfg.setdefault("reflector_buffer_size_sec", int(pv["reflector_buffer_size_sec"]))
+    cfg.setdefault("rtp_reflector_threshold_msec", max(1000, int(pv["rtp_reflector_threshold_msec"])))   # :101-102
+    cfg.setdefault("reflector_rtp_info_offset_msec", int(pv["reflector_rtp_info_offset_msec"]) or edgpu.FALSE)
+    mod = {"prefs": dict(trace.prefs)}      # the module prefs (RereadPrefs at PREFS events)
     own = ctx is None
     if own:
         ctx = edgpu.Context(**cfg)
@@ -221,11 +239,15 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         # the trace session of each engine session (receiver reports name the trace's)
         gen = [None] * len(trace.sdps)
         published = [True] * len(trace.sdps)
+        kill_attr = [pref_bool(pref_values(mod["prefs"])["kill_clients_when_broadcast_stops"])] * len(trace.sdps)
         trace_of = {}
 
         def publish_fresh(i, now_s):
             nonlocal rand_calls
             sid = ctx.session_add(trace.sdps[i], udp_push=trace.udp_push(i))
+            p = pref_values(mod["prefs"])       # SetupReflectorSession's SSRC filter: the prefs now
+            ctx.session_ssrc_prefs(sid, pref_bool(p["use_one_SSRC_per_stream"]), int(p["timeout_stream_SSRC_secs"]))
+            kill_attr[i] = pref_bool(p["kill_clients_when_broadcast_stops"])     # the RECORD
             gen[i] = sid
             trace_of[sid] = i
             for tr in range(ctx.session_tracks(sid)):
@@ -244,6 +266,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         subs_meta = {}          # handle -> (sub_id, session, tcp)
         images = {}
         pending, joins, stats = [], [], []
+        tick_info = tick_info if tick_info is not None else []
         lag = bool(cfg.get("overlap_ticks")) and replica is None
         unread = None                       # (ctx, result) of a tick not read back yet
 
@@ -257,12 +280,20 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 unread = None
             if unread is not None:
                 c, r, tt, budgets = unread
-                st, subs, desc, arena = c.read_tick(r)
-                reports = _wire_images(subs, desc, arena, images, budgets)
+                reports, big = [], [0, 0]
+
+                def consume(st, subs, desc, arena):
+                    reports.extend(_wire_images(subs, desc, arena, images, budgets))
+                    if len(subs):
+                        big[0] = max(big[0], int(subs["out_bytes"].max()))
+                        big[1] = max(big[1], int(subs["desc_count"].max()))
+                # every copy pass of the tick (more than one when it exceeds the arena)
+                npass = c.read_passes(r, consume)
                 if reports:
                     c.fanout_blocked(reports)
-                    st = c.stats()
+                st = c.stats()
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
+                tick_info.append((npass, big[0], big[1], int(st.arena_bytes), int(st.relayed_packets)))
                 unread = None
 
         pin_sets = [{}, {}]                 # pinned host batch buffers, used alternately
@@ -327,7 +358,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             try:
                 h, _info = out.subscriber_play(gen[s] if rep is None else rsess[s],
                                                edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
-                                               rtp_info=bool(ua & 1), now_ms=now_j)
+                                               rtp_info=rtp_info_player(mod["prefs"], ua), now_ms=now_j)
             except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
                 if e.code != edgpu.WOULD_BLOCK:
                     raise
@@ -372,7 +403,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             elif ev[0] == JOIN:
                 # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):
                 # ingest what precedes it first
-                if ev[5] & 1 and rep is None:
+                if rtp_info_player(mod["prefs"], ev[5]) and rep is None:
                     flush()
                 if rep is None:
                     if gen[ev[2]] is not None:          # else no session: the SETUP fails
@@ -384,6 +415,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 flush()
                 if published[s]:
                     published[s] = False
+                    # RemoveOutput's kill: the pusher's attribute or the pref now (:2156)
+                    kill = kill or kill_attr[s] or pref_bool(pref_values(mod["prefs"])["kill_clients_when_broadcast_stops"])
                     if kill:                            # TearDownAllOutputs
                         for h in outputs_of(s):
                             gone.add(h)
@@ -398,6 +431,10 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     published[s] = True
                     if gen[s] is None:
                         publish_fresh(s, clock // 1000)
+                    else:                               # the surviving session's new RECORD
+                        kill_attr[s] = pref_bool(pref_values(mod["prefs"])["kill_clients_when_broadcast_stops"])
+            elif ev[0] == PREFS:
+                mod["prefs"] = dict(ev[2])              # RereadPrefs
             elif ev[0] == LEAVE:
                 # RemoveOutput applies at once: a join still waiting for its tick is made now
                 # (the output existed, with nothing sent yet), and the output stops at the next

@@ -33,9 +33,11 @@ ReflectorStream.cpp:1676-1714).
 Binary layout (little endian)::
 
     trace   := "EDTR" u32 version u32 n_sessions { u32 sdp_len sdp_bytes [u8 flags] }*
+               [ u32 prefs_len prefs_bytes ]                                 (version 4)
                event* u8 0
                (version 1: no flags byte; version 2: flags bit 0 = UDP push;
-                version 3: as 2, with PUBLISH / UNPUBLISH events)
+                version 3: as 2, with PUBLISH / UNPUBLISH events;
+                version 4: as 3, with the server's preferences and PREFS events)
     event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
              | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
              | u8 3 i64 t                                                    (TICK)
@@ -45,10 +47,23 @@ Binary layout (little endian)::
              | u8 6 i64 t u32 sub_id                                         (LEAVE)
              | u8 7 i64 t u32 session u8 kill                                (UNPUBLISH, v3)
              | u8 8 i64 t u32 session                                        (PUBLISH, v3)
+             | u8 9 i64 t u32 len bytes[len]                                 (PREFS, v4)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
                [ "EDRR" u32 m { i64 t u32 session u16 track u32 addr u16 port u32 len
                                bytes[len] }* ]
+
+``prefs_bytes`` (and a PREFS event's bytes) are ``name=value`` lines: the preferences the
+server's prefs objects hold (WinNTSupport/easydarwin.xml), every unnamed one at the reference's
+default (:data:`PREF_DEFAULTS`).  They are the QTSSReflectorModule prefs ReflectorStream::
+Initialize reads once (ReflectorStream.cpp:87-117) and the ones RereadPrefs reads
+(QTSSReflectorModule.cpp:454-537), plus the server pref ``player_requires_rtp_header_info``
+(comma-separated; QTSServerPrefs, read at every PLAY by HavePlayerProfile, QTSSModuleUtils.cpp:
+1012-1046).  A PREFS event is the server rewriting its prefs file and sending the
+QTSS_RereadPrefs_Role: the module prefs take the new values (new sessions get the SSRC ones,
+QTSSReflectorModule.cpp:1457); ReflectorStream's are not re-read.  A JOIN's ``ua_flags`` bit 0
+picks the player's user agent: "vlc/3.0.8 LibVLC/3.0.8" (else "EasyPlayer/1.0"); whether it
+is an RTP-Info player follows from the prefs (:func:`rtp_info_player`).
 
 ``kind`` is 0 for the RTP sub-stream, 1 for RTCP.  The capture bytes are the sub-stream's
 *wire image*: UDP = ``BE16(len) + datagram`` per packet; TCP = the exact interleaved byte
@@ -69,8 +84,68 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK, BLOCK, UPKT, LEAVE, UNPUBLISH, PUBLISH = 1, 2, 3, 4, 5, 6, 7, 8
+PKT, JOIN, TICK, BLOCK, UPKT, LEAVE, UNPUBLISH, PUBLISH, PREFS = 1, 2, 3, 4, 5, 6, 7, 8, 9
 UDP, TCP = 0, 1
+
+# The reference's defaults of the prefs a trace may set (ReflectorStream.cpp:53-59,
+# QTSSReflectorModule.cpp:100-166, and the shipped easydarwin.xml's player list, :98-101).
+PREF_DEFAULTS = {
+    "reflector_bucket_offset_delay_msec": "73",
+    "reflector_buffer_size_sec": "1",
+    "rtp_reflector_threshold_msec": "2000",
+    "reflector_rtp_info_offset_msec": "500",
+    "kill_clients_when_broadcast_stops": "false",
+    "use_one_SSRC_per_stream": "true",
+    "timeout_stream_SSRC_secs": "30",
+    "disable_rtp_play_info": "false",
+    "enable_player_compatibility": "true",
+    "force_rtp_info_sequence_and_time": "false",
+    "player_requires_rtp_header_info": "Android,vlc",
+}
+USER_AGENTS = ("EasyPlayer/1.0", "vlc/3.0.8 LibVLC/3.0.8")    # by JOIN ua_flags bit 0
+
+
+def pref_values(prefs: dict) -> dict:
+    """Every pref of PREF_DEFAULTS with the trace's overrides applied."""
+    unknown = set(prefs) - set(PREF_DEFAULTS)
+    assert not unknown, f"unknown prefs {sorted(unknown)}"
+    out = dict(PREF_DEFAULTS)
+    out.update({k: str(v) for k, v in prefs.items()})
+    return out
+
+
+def pref_bool(v: str) -> bool:
+    return v.strip().lower() == "true"
+
+
+def rtp_info_player(prefs: dict, ua_flags: int) -> bool:
+    """DoPlay's rtpInfoEnabled (QTSSReflectorModule.cpp:1962-1969): the player profile (a
+    case-sensitive substring of the user agent in player_requires_rtp_header_info, "*" = any,
+    QTSSModuleUtils.cpp:983-1010) when enable_player_compatibility, forced on by
+    force_rtp_info_sequence_and_time, off with disable_rtp_play_info."""
+    p = pref_values(prefs)
+    ua = USER_AGENTS[ua_flags & 1]
+    on = False
+    if pref_bool(p["enable_player_compatibility"]):
+        on = any(x == "*" or (x and x in ua) for x in p["player_requires_rtp_header_info"].split(","))
+    if pref_bool(p["force_rtp_info_sequence_and_time"]):
+        on = True
+    if pref_bool(p["disable_rtp_play_info"]):
+        on = False
+    return on
+
+
+def pack_prefs(prefs: dict) -> bytes:
+    return "".join(f"{k}={v}\n" for k, v in sorted(prefs.items())).encode()
+
+
+def unpack_prefs(b: bytes) -> dict:
+    out = {}
+    for line in b.decode().splitlines():
+        if line:
+            k, v = line.split("=", 1)
+            out[k] = v
+    return out
 
 
 @dataclass
@@ -78,6 +153,7 @@ class Trace:
     sdps: list[str] = field(default_factory=list)
     events: list[tuple] = field(default_factory=list)   # (type, t, ...) in file order
     flags: list[int] = field(default_factory=list)      # per session: bit 0 = UDP push
+    prefs: dict = field(default_factory=dict)           # the server's pref overrides (version 4)
 
     def add_session(self, sdp: str, udp_push: bool = False) -> int:
         self.sdps.append(sdp)
@@ -89,6 +165,8 @@ class Trace:
 
     @property
     def version(self) -> int:
+        if self.prefs or any(ev[0] == PREFS for ev in self.events):
+            return 4
         if any(ev[0] in (PUBLISH, UNPUBLISH) for ev in self.events):
             return 3
         return 2 if any(self.flags) or any(ev[0] == UPKT for ev in self.events) else 1
@@ -121,6 +199,12 @@ class Trace:
     def publish(self, t: int, session: int):
         self.events.append((PUBLISH, int(t), session))
 
+    def reprefs(self, t: int, prefs: dict):
+        """The server rewrites its prefs (these overrides replace the previous ones) and sends
+        QTSS_RereadPrefs_Role."""
+        pref_values(prefs)
+        self.events.append((PREFS, int(t), dict(prefs)))
+
     # -- serialisation ------------------------------------------------------------------
     def to_bytes(self) -> bytes:
         # PKT and TICK times drive the virtual clock and must not go back; a JOIN's time is
@@ -136,6 +220,9 @@ class Trace:
             out.append(b)
             if ver >= 2:
                 out.append(struct.pack("<B", self.flags[i] if i < len(self.flags) else 0))
+        if ver >= 4:
+            pb = pack_prefs(self.prefs)
+            out.append(struct.pack("<I", len(pb)) + pb)
         for ev in self.events:
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
@@ -157,6 +244,9 @@ class Trace:
                 out.append(struct.pack("<BqIB", UNPUBLISH, ev[1], ev[2], ev[3]))
             elif ev[0] == PUBLISH:
                 out.append(struct.pack("<BqI", PUBLISH, ev[1], ev[2]))
+            elif ev[0] == PREFS:
+                pb = pack_prefs(ev[2])
+                out.append(struct.pack("<BqI", PREFS, ev[1], len(pb)) + pb)
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -170,7 +260,7 @@ class Trace:
     def from_bytes(buf: bytes) -> "Trace":
         assert buf[:4] == b"EDTR"
         ver, n = struct.unpack_from("<II", buf, 4)
-        assert ver in (1, 2, 3)
+        assert ver in (1, 2, 3, 4)
         p = 12
         tr = Trace()
         for _ in range(n):
@@ -183,6 +273,10 @@ class Trace:
                 fl = buf[p]
                 p += 1
             tr.flags.append(fl)
+        if ver >= 4:
+            (ln,) = struct.unpack_from("<I", buf, p)
+            tr.prefs = unpack_prefs(buf[p + 4:p + 4 + ln])
+            p += 4 + ln
         while p < len(buf):
             typ = buf[p]
             if typ == 0:
@@ -216,6 +310,10 @@ class Trace:
                 _, t, s = struct.unpack_from("<BqI", buf, p)
                 p += 13
                 tr.events.append((PUBLISH, t, s))
+            elif typ == PREFS:
+                _, t, ln = struct.unpack_from("<BqI", buf, p)
+                tr.events.append((PREFS, t, unpack_prefs(buf[p + 13:p + 13 + ln])))
+                p += 13 + ln
             elif typ == UPKT:
                 _, t, s, ch, addr, port, ln = struct.unpack_from("<BqIBIHI", buf, p)
                 p += 24

@@ -71,7 +71,8 @@ extern "C" {
 #define EDGPU_NO_DEVICE       -101     /* no usable gfx950 device / HIP failure */
 #define EDGPU_OUT_OF_MEMORY   -102
 #define EDGPU_RING_OVERFLOW   -103     /* a needed packet fell out of a sender ring */
-#define EDGPU_OUT_OVERFLOW    -104     /* fan-out arena too small for this tick */
+#define EDGPU_OUT_OVERFLOW    -104     /* a buffer too small (a fan-out sub-stream larger than the
+                                          arena, a batch, a gather destination, ...) */
 
 /* transport of a subscriber (qtssRTPTransportType, QTSS.h:219-221) */
 #define EDGPU_TRANSPORT_UDP      0
@@ -109,9 +110,10 @@ typedef struct edgpu_config {
      * plus one ingest batch, else EDGPU_RING_OVERFLOW.  0 (default): one stream. */
     uint32_t overlap_ticks;
     uint32_t reflector_rtp_info_offset_msec; /* RTP-Info first packet: within over-buffer minus
-                                               this (ReflectorStream.cpp:109-110); default 500 */
+                                               this (ReflectorStream.cpp:109-110); default 500,
+                                               EDGPU_FALSE for an offset of 0 */
 } edgpu_config;
-#define EDGPU_FALSE 0xFFFFFFFFu
+#define EDGPU_FALSE 0xFFFFFFFFu   /* a flag off / a value of 0 where 0 would select the default */
 
 /* One ingested packet.  The batch blob is a sequence of 16-byte-aligned slots; a packet's
  * bytes start 4 bytes into its slot (the 4 bytes before it are the RTSP-interleaved header
@@ -175,13 +177,21 @@ typedef struct edgpu_fanout_result {
 /* Per-tick totals, read back by edgpu_tick_stats_get (which syncs). */
 typedef struct edgpu_tick_stats {
     uint64_t relayed_packets;   /* IncrementTotalPackets semantics (RTPStream.cpp:1213-1216) */
-    uint64_t relayed_bytes;     /* wire bytes incl. '$' framing */
-    uint64_t arena_bytes;
+    uint64_t relayed_bytes;     /* wire bytes incl. '$' framing (of the passes copied so far) */
+    uint64_t arena_bytes;       /* slot bytes of the whole tick (every pass) */
     uint64_t ingested_packets;  /* the batch the last edgpu_keyframe_index indexed (the counters
                                    move at the index, not at edgpu_ingest) */
     uint64_t ingested_bytes;
     int32_t  status;            /* sticky device-side error (EDGPU_RING_OVERFLOW, ...) */
     uint32_t _pad;
+    /* the current copy pass (edgpu_fanout_next): arena bytes and descriptors the result's
+     * sub-streams span, its ordinal (0 = the pass edgpu_fanout launched) and whether another
+     * pass follows */
+    uint64_t pass_arena_bytes;
+    uint32_t pass_packets;
+    uint32_t pass;
+    uint32_t more_passes;
+    uint32_t _pad2;
 } edgpu_tick_stats;
 
 typedef struct edgpu_ctx edgpu_ctx;
@@ -199,6 +209,14 @@ int  edgpu_sync(edgpu_ctx* ctx);
 int  edgpu_session_add(edgpu_ctx* ctx, const char* sdp, uint32_t sdp_len, int udp_push,
                        uint32_t* out_session);
 int  edgpu_session_tracks(edgpu_ctx* ctx, uint32_t session, uint32_t* out_tracks);
+/* The session's SSRC filter settings: SetupReflectorSession takes use_one_SSRC_per_stream and
+ * timeout_stream_SSRC_secs per session, from the module prefs as they are when the session is set
+ * up (QTSSReflectorModule.cpp:1457, RereadPrefs :478-481 -> FilterInvalidSSRCs,
+ * ReflectorStream.cpp:1732-1767).  edgpu_session_add gives a session the context's
+ * edgpu_config values; this changes them (before its first packet, for a session a module set up
+ * after a RereadPrefs).  Both are taken as given (a timeout of 0 s is the reference's too). */
+int  edgpu_session_ssrc_prefs(edgpu_ctx* ctx, uint32_t session, uint32_t use_one_SSRC_per_stream,
+                              uint32_t timeout_stream_SSRC_secs);
 
 /* Destroys a push session -- what the reference does when a ReflectorSession's reference
  * count reaches 0 (its pusher gone, every output removed: RemoveOutput, QTSSReflectorModule.cpp:
@@ -310,7 +328,9 @@ int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
  * remainder.  Ranges must extend the prefix staged so far (offset == bytes already staged) and
  * those bytes must not change before the ingest (a blob moved to a larger buffer keeps them).
  * May be called from another thread than the context's other calls.  A pinned batch that
- * edgpu_ingest refuses for its size or structure drops what was copied ahead of it. */
+ * edgpu_ingest refuses for its size or structure drops what was copied ahead of it; offset 0 with
+ * bytes 0 drops it explicitly (a host whose batch came to nothing, e.g. every packet of it belonged
+ * to a session removed since: the next pinned batch is then copied whole). */
 int  edgpu_ingest_prestage(edgpu_ctx* ctx, const uint8_t* blob, uint64_t offset, uint64_t bytes);
 /* RTSP-interleaved push ingest: the pusher connections' raw TCP reads, deframed on the GPU.
  * Replaces RTSPRequestStream::ReadRequest's '$' branch (Server.tproj/RTSPRequestStream.cpp:
@@ -360,6 +380,24 @@ int  edgpu_ingest_interleaved(edgpu_ctx* ctx, const edgpu_tcp_read* reads, uint3
 
 int  edgpu_keyframe_index(edgpu_ctx* ctx);
 int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
+
+/* Over-capacity ticks.  A tick whose outputs exceed out_arena_bytes or max_out_packets is not
+ * dropped: it is delivered in copy passes over consecutive rows of the sub-stream table, each
+ * within the arena and the descriptor array (the reference walks every output of every sender in
+ * each ReflectPackets, ReflectorStream.cpp:1088-1120, so no output may lose a tick).  edgpu_fanout
+ * launches pass 0; the result then shows only that pass's sub-streams (the other rows have
+ * desc_count 0 and out_bytes 0; flags are set on every row), their out_base / desc_base relative to
+ * the pass's arena and descriptors.  After consuming a pass the host calls edgpu_fanout_next:
+ * *launched = 1 when it launched the next pass (`out` as above), 0 when the tick is complete.
+ * edgpu_tick_stats_get reports the current pass (pass_arena_bytes, pass_packets, more_passes).
+ * Every pass of a tick must be consumed before the next edgpu_ingest / edgpu_ingest_interleaved
+ * / edgpu_fanout / edgpu_session_remove: those fail with EDGPU_ERR while the context knows of an
+ * outstanding pass (edgpu_counters.lost_passes counts passes a tick still owed when the next
+ * tick was planned).  Backpressure reports (edgpu_fanout_blocked) take tick-wide sub-stream rows
+ * and may follow any pass.  A tick fits one pass whenever its bytes and descriptors do; a single
+ * sub-stream larger than the arena (out_arena_bytes below a sender ring) still fails the tick
+ * with EDGPU_OUT_OVERFLOW. */
+int  edgpu_fanout_next(edgpu_ctx* ctx, edgpu_fanout_result* out, uint32_t* launched);
 
 /* Egress backpressure.  The host writes a tick's sub-streams to their sockets; when a socket
  * stops accepting (EAGAIN -> QTSS_WouldBlock, RTPStream::Write -> RTPSessionOutput::
@@ -443,7 +481,8 @@ int  edgpu_session_eyes_add(edgpu_ctx* ctx, uint32_t session, int32_t delta);
  * blocks).  Blocked TCP sub-streams are reported with edgpu_fanout_blocked before returning.
  * The tick's distinct bytes come over PCIe in one copy (identity UDP sub-streams of a sender share
  * one region, edgpu_arena_gather), with the descriptors and sub-stream table; `threads` workers
- * own disjoint subscribers and send with sendmmsg / sendmsg.
+ * own disjoint subscribers and send with sendmmsg / sendmsg.  An over-capacity tick is sent pass
+ * by pass (the call runs edgpu_fanout_next itself), so `r` is the result of edgpu_fanout.
  *
  * UDP loss granularity.  By default (EDGPU_EGRESS_GSO unset or 1) runs of equal-length
  * datagrams of a sub-stream (FU-A fragments of a frame) leave as UDP GSO messages (UDP_SEGMENT,
@@ -487,12 +526,13 @@ int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs; ED
                                                                        ingest awaits its index */
 
 /* The arrival time (fTimeArrived, OS::Milliseconds() at PushPacket) of each descriptor of
- * the last edgpu_fanout: out[i] for desc[i], i < the tick's relayed packets (serial ticks;
- * call before the next edgpu_fanout).  RTPSessionOutput::WritePacket derives the
+ * the current copy pass of the last edgpu_fanout: out[i] for desc[i], i < the pass's
+ * pass_packets (serial ticks; call before the next edgpu_fanout / edgpu_fanout_next).
+ * RTPSessionOutput::WritePacket derives the
  * QTSS_PacketStruct transmit time from it (RTPSessionOutput.cpp:604-608), which the server's
  * RTPStream::Write hands to its thinning and over-buffer logic (RTPStream.cpp:1062,1119-1137).
  * `out` is host memory (ptr_kind EDGPU_PTR_HOST) or device memory (EDGPU_PTR_DEVICE); `n`
- * must be at least the tick's relayed packets. */
+ * must be at least the pass's descriptors. */
 int  edgpu_fanout_arrivals(edgpu_ctx* ctx, int64_t* out, uint32_t n, int ptr_kind);
 
 /* Packs regions of a fan-out arena (16-B aligned offsets and lengths; in the order given)
@@ -522,6 +562,8 @@ typedef struct edgpu_counters {
     uint64_t fanout_launches;
     uint64_t ingested_packets;
     uint64_t ingested_bytes;
+    uint64_t fanout_passes;     /* copy passes launched (> fanout_launches: over-capacity ticks) */
+    uint64_t lost_passes;       /* passes a tick still owed when the next tick was planned */
 } edgpu_counters;
 int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 

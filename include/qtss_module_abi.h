@@ -91,8 +91,8 @@ enum : uint32_t {
 
 // attribute data types (QTSS.h:358-378)
 enum : uint32_t {
-    qtssAttrDataTypeCharArray = 1, qtssAttrDataTypeBool16 = 2, qtssAttrDataTypeSInt32 = 5,
-    qtssAttrDataTypeUInt32 = 6, qtssAttrDataTypeVoidPointer = 13,
+    qtssAttrDataTypeUnknown = 0, qtssAttrDataTypeCharArray = 1, qtssAttrDataTypeBool16 = 2,
+    qtssAttrDataTypeSInt32 = 5, qtssAttrDataTypeUInt32 = 6, qtssAttrDataTypeVoidPointer = 13,
 };
 
 // object types (QTSS.h:266-282)
@@ -103,6 +103,9 @@ enum : uint32_t {
     qtssRTSPRequestObjectType = four_cc('s', 'r', 'q', 'o'),
     qtssTextMessagesObjectType = four_cc('t', 'x', 't', 'o'),
     qtssModulePrefsObjectType = four_cc('m', 'o', 'd', 'p'),
+    qtssPrefsObjectType = four_cc('p', 'r', 'f', 'o'),
+    qtssModuleObjectType = four_cc('m', 'o', 'd', 'o'),
+    qtssAttrInfoObjectType = four_cc('a', 't', 't', 'r'),
 };
 
 // attribute ids read or written by the reflector module
@@ -113,7 +116,10 @@ enum : uint32_t {
     qtssRTPStrTransportType = 31,
     // client session object (QTSS.h:473-512)
     qtssCliSesStreamObjects = 0, qtssCliSesState = 7, qtssCliSesFirstUserAgent = 9,
-    qtssCliTeardownReason = 23,
+    qtssCliTeardownReason = 23, qtssCliSesOverBufferEnabled = 33,
+    // module object (QTSS.h:894-905), attribute-info object (:911-918), server prefs (:718-800)
+    qtssModPrefs = 4, qtssAttrName = 0, qtssAttrID = 1, qtssAttrDataType = 2,
+    qtssPrefsPlayersReqRTPHeader = 70,
     // RTSP request object (QTSS.h:588-623)
     qtssRTSPReqFilePath = 2, qtssRTSPReqFileName = 5, qtssRTSPReqFileDigit = 6,
     qtssRTSPReqMethod = 9, qtssRTSPReqRespKeepAlive = 13, qtssRTSPReqQueryString = 23,
@@ -191,7 +197,8 @@ enum : uint32_t {
     kWriteCallback = 10, kAppendRTSPHeadersCallback = 17, kSendStandardRTSPCallback = 18,
     kAddRTPStreamCallback = 19, kPlayCallback = 20, kPauseCallback = 21, kTeardownCallback = 22,
     kRequestEventCallback = 23, kSetIdleTimerCallback = 24, kReadCallback = 27,
-    kGetNumValuesCallback = 30, kAddStaticAttributeCallback = 35, kRemoveValueCallback = 46,
+    kGetNumValuesCallback = 30, kAddStaticAttributeCallback = 35, kAddInstanceAttributeCallback = 36,
+    kGetAttrInfoByNameCallback = 39, kGetValueAsStringCallback = 41, kRemoveValueCallback = 46,
     kLastCallback = 62,
 };
 struct QTSS_Callbacks {
@@ -237,6 +244,8 @@ typedef struct EDGPU_QTSSTickInfo {
     uint64_t ticks, failed_ticks;       /* since Initialize */
     int64_t  last_error;                /* the engine's code of the newest failed tick, or 0 */
     uint64_t prestaged_bytes;           /* of the tick's batch, copied to the device while it filled */
+    uint64_t passes;                    /* copy passes of the tick (> 1: it exceeded the arena) */
+    uint64_t rereads;                   /* RereadPrefs calls handled since Initialize */
 } EDGPU_QTSSTickInfo;
 edqtss::QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out);
 }

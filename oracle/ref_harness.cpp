@@ -50,6 +50,15 @@
 //     still exists (Resolve, not set up again, :1479-1536) or builds a fresh one (:1391-1478).
 //     PKT / UPKT of a session without a pusher are dropped; a JOIN of a session that no longer
 //     exists fails (FindOrCreateSession returns NULL for a player, :1391-1396).
+//   * preferences (trace v4): the trace's overrides are values of a module prefs object and of
+//     the server prefs object, read through the reference's own QTSSModuleUtils::GetAttribute /
+//     HavePlayerProfile over this fake server's dictionary callbacks (GetAttrInfoByName,
+//     GetNumValues, GetValueAsString); a pref the trace does not name is missing, so the
+//     reference falls back to its default.  ReflectorStream::Initialize reads its prefs once
+//     (ReflectorStream.cpp:87-117); the module prefs are read as RereadPrefs reads them
+//     (QTSSReflectorModule.cpp:454-537) at start and at every PREFS event, and used where the
+//     module uses them: SetupReflectorSession's SSRC filter (:1457), RECORD's kill-clients
+//     attribute (:1884) and RemoveOutput's kill (:2156), DoPlay's rtpInfoEnabled (:1962-1969).
 //
 // Usage: ref_harness <trace.edtr> <capture.edcp>
 //        ref_harness --bench <trace.edtr>    (memcpy sinks, no capture; prints the replay's
@@ -87,6 +96,7 @@
 #include "ReflectorStream.h"
 #include "RTPSessionOutput.h"
 #include "QTSServerInterface.h"
+#include "QTSSModuleUtils.h"
 #include "OSRef.h"
 
 // ---------------------------------------------------------------------------------------
@@ -130,6 +140,7 @@ extern "C" OS_Error __wrap__ZN9UDPSocket6SendToEjtPvj(void* self, UInt32 addr, U
 struct Value { std::vector<char> buf; UInt32 len = 0; };
 struct FakeObj {
     std::map<UInt32, std::vector<std::unique_ptr<Value>>> attrs;
+    std::map<std::string, std::pair<UInt32, UInt32>> named;   // attribute name -> (id, data type)
     // capture side (RTP stream objects only)
     bool is_stream = false;
     UInt32 sub_id = 0, session = 0, track = 0, transport = 0;
@@ -158,6 +169,76 @@ static Value* get_value(FakeObj* o, UInt32 id, UInt32 idx) {
 }
 
 static std::map<std::string, UInt32> g_attr_ids;
+
+// Preferences: the module prefs object and the server prefs object (trace v4).
+static const char* const kPrefDefaults[][2] = {            // easydarwin_amd/trace.py PREF_DEFAULTS
+    {"reflector_bucket_offset_delay_msec", "73"}, {"reflector_buffer_size_sec", "1"},
+    {"rtp_reflector_threshold_msec", "2000"}, {"reflector_rtp_info_offset_msec", "500"},
+    {"kill_clients_when_broadcast_stops", "false"}, {"use_one_SSRC_per_stream", "true"},
+    {"timeout_stream_SSRC_secs", "30"}, {"disable_rtp_play_info", "false"},
+    {"enable_player_compatibility", "true"}, {"force_rtp_info_sequence_and_time", "false"},
+    {"player_requires_rtp_header_info", "Android,vlc"},
+};
+static FakeObj* g_mod_prefs = nullptr;      // QTSSReflectorModule's prefs object
+static FakeObj* g_srv_prefs = nullptr;      // the server's prefs object
+// the trace's overrides (name -> value); a named pref becomes an attribute of the right type
+static void load_prefs(const std::map<std::string, std::string>& over) {
+    for (FakeObj* o : {g_mod_prefs, g_srv_prefs}) { o->attrs.clear(); o->named.clear(); }
+    UInt32 next = 0x20000000u;
+    for (const auto& kv : over) {
+        const std::string& k = kv.first;
+        const std::string& v = kv.second;
+        if (k == "player_requires_rtp_header_info") {          // a LIST-PREF, one value per entry
+            size_t p = 0, idx = 0;
+            while (p <= v.size()) {
+                size_t e = v.find(',', p);
+                if (e == std::string::npos) e = v.size();
+                std::string one = v.substr(p, e - p);
+                set_value(g_srv_prefs, qtssPrefsPlayersReqRTPHeader, (UInt32)idx++, one.data(), (UInt32)one.size());
+                p = e + 1;
+            }
+            continue;
+        }
+        const bool isBool = v == "true" || v == "false";
+        const UInt32 id = next++;
+        g_mod_prefs->named[k] = std::make_pair(id, (UInt32)(isBool ? qtssAttrDataTypeBool16 : qtssAttrDataTypeUInt32));
+        if (isBool) { bool b = v == "true"; set_value(g_mod_prefs, id, 0, &b, sizeof(b)); }
+        else { UInt32 u = (UInt32)strtoul(v.c_str(), nullptr, 10); set_value(g_mod_prefs, id, 0, &u, sizeof(u)); }
+    }
+}
+// RereadPrefs' module prefs used on this path (QTSSReflectorModule.cpp:454-537: same names,
+// types and defaults, :100-166), read through the reference's QTSSModuleUtils::GetAttribute
+struct ModulePrefs {
+    bool killClients = false, oneSSRC = true, rtpInfoDisabled = false, playerCompat = true, forceRTPInfo = false;
+    UInt32 timeoutSSRC = 30;
+};
+static ModulePrefs g_mp;
+static void reread_prefs() {
+    static bool dFalse = false, dTrue = true;
+    static UInt32 d30 = 30;
+    QTSS_ModulePrefsObject o = (QTSS_ModulePrefsObject)g_mod_prefs;
+    QTSSModuleUtils::GetAttribute(o, (char*)"disable_rtp_play_info", qtssAttrDataTypeBool16, &g_mp.rtpInfoDisabled, &dFalse, sizeof(dFalse));
+    QTSSModuleUtils::GetAttribute(o, (char*)"kill_clients_when_broadcast_stops", qtssAttrDataTypeBool16, &g_mp.killClients, &dFalse, sizeof(dFalse));
+    QTSSModuleUtils::GetAttribute(o, (char*)"use_one_SSRC_per_stream", qtssAttrDataTypeBool16, &g_mp.oneSSRC, &dTrue, sizeof(dTrue));
+    QTSSModuleUtils::GetAttribute(o, (char*)"timeout_stream_SSRC_secs", qtssAttrDataTypeUInt32, &g_mp.timeoutSSRC, &d30, sizeof(d30));
+    QTSSModuleUtils::GetAttribute(o, (char*)"enable_player_compatibility", qtssAttrDataTypeBool16, &g_mp.playerCompat, &dTrue, sizeof(dTrue));
+    QTSSModuleUtils::GetAttribute(o, (char*)"force_rtp_info_sequence_and_time", qtssAttrDataTypeBool16, &g_mp.forceRTPInfo, &dFalse, sizeof(dFalse));
+}
+static std::map<std::string, std::string> parse_prefs(const std::string& b) {
+    std::map<std::string, std::string> m;
+    size_t p = 0;
+    while (p < b.size()) {
+        size_t e = b.find('\n', p);
+        if (e == std::string::npos) e = b.size();
+        const std::string line = b.substr(p, e - p);
+        const size_t q = line.find('=');
+        if (q != std::string::npos) m[line.substr(0, q)] = line.substr(q + 1);
+        p = e + 1;
+    }
+    return m;
+}
+// a user agent of the trace (easydarwin_amd/trace.py USER_AGENTS: JOIN ua_flags bit 0)
+static const char* kUserAgents[2] = {"EasyPlayer/1.0", "vlc/3.0.8 LibVLC/3.0.8"};
 static UInt32 g_cookie_attr = 0;
 
 // ---------------------------------------------------------------------------------------
@@ -197,6 +278,36 @@ static QTSS_Error cb_get_value(void* obj, UInt32 id, UInt32 idx, void* buf, UInt
     if (*len < v->len) { *len = v->len; return QTSS_NotEnoughSpace; }
     memcpy(buf, v->buf.data(), v->len);
     *len = v->len;
+    return QTSS_NoErr;
+}
+// QTSS_GetAttrInfoByName: an attribute-info object with qtssAttrID / qtssAttrDataType
+static QTSS_Error cb_attr_info_by_name(void* obj, const char* name, void** out, ...) {
+    FakeObj* o = (FakeObj*)obj;
+    if (!o || !name) return QTSS_BadArgument;
+    auto it = o->named.find(name);
+    if (it == o->named.end()) return QTSS_AttrDoesntExist;
+    FakeObj* info = new_obj();
+    set_value(info, qtssAttrID, 0, &it->second.first, sizeof(UInt32));
+    set_value(info, qtssAttrDataType, 0, &it->second.second, sizeof(UInt32));
+    *out = info;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_num_values(void* obj, UInt32 id, UInt32* n, ...) {
+    if (!obj || !n) return QTSS_BadArgument;
+    auto it = ((FakeObj*)obj)->attrs.find(id);
+    *n = it == ((FakeObj*)obj)->attrs.end() ? 0 : (UInt32)it->second.size();
+    return QTSS_NoErr;
+}
+// QTSS_GetValueAsString of a char-array value: a new[] copy the caller deletes
+static QTSS_Error cb_value_as_string(void* obj, UInt32 id, UInt32 idx, char** out, ...) {
+    if (!obj || !out) return QTSS_BadArgument;
+    *out = nullptr;
+    Value* v = get_value((FakeObj*)obj, id, idx);
+    if (!v) return QTSS_ValueNotFound;
+    char* c = new char[v->len + 1];
+    memcpy(c, v->buf.data(), v->len);
+    c[v->len] = 0;
+    *out = c;
     return QTSS_NoErr;
 }
 static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf, UInt32 len, ...) {
@@ -274,6 +385,7 @@ struct Live {
     ReflectorSession* sess = nullptr;
     FakeObj* bcast = nullptr;       // the pusher's client session
     bool published = false;
+    bool killAttr = false;          // its QTSSReflectorModuleTearDownClients, set at RECORD (:1884)
 };
 
 int main(int argc, char** argv) {
@@ -311,7 +423,7 @@ int main(int argc, char** argv) {
     if (memcmp(&r.d[0], "EDTR", 4) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
     r.p = 4;
     UInt32 version = r.get<UInt32>();
-    if (version < 1 || version > 3) { fprintf(stderr, "bad version\n"); return 2; }
+    if (version < 1 || version > 4) { fprintf(stderr, "bad version\n"); return 2; }
 
     static NoopAssert logger;
     SetAssertLogger(&logger);
@@ -329,6 +441,9 @@ int main(int argc, char** argv) {
     cbs.addr[kLockObjectCallback]          = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kUnlockObjectCallback]        = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kTeardownCallback]            = (QTSS_CallbackProcPtr)cb_teardown;
+    cbs.addr[kGetAttrInfoByNameCallback]   = (QTSS_CallbackProcPtr)cb_attr_info_by_name;
+    cbs.addr[kGetNumValuesCallback]        = (QTSS_CallbackProcPtr)cb_num_values;
+    cbs.addr[kGetValueAsStringCallback]    = (QTSS_CallbackProcPtr)cb_value_as_string;
     QTSS_PrivateArgs args;
     memset(&args, 0, sizeof(args));
     args.inServerAPIVersion = QTSS_API_VERSION;
@@ -340,12 +455,30 @@ int main(int argc, char** argv) {
     ReflectorStream::Register();
     RTPSessionOutput::Register();
     (void)QTSS_IDForAttr(qtssRTPStreamObjectType, "qtssReflectorModuleStreamCookie", &g_cookie_attr);
-    FakeObj* prefs = new_obj();
-    ReflectorStream::Initialize((QTSS_ModulePrefsObject)prefs);   // every pref -> its default
-    if (ReflectorStream::sOverBufferInMsec != 1000) {      // pinned prefs: SURVEY.md §5 defaults
-        fprintf(stderr, "unexpected reflector prefs (overbuffer %u ms)\n", (unsigned)ReflectorStream::sOverBufferInMsec);
-        return 3;
+    g_mod_prefs = new_obj();
+    g_srv_prefs = new_obj();
+    // the trace's prefs (version 4: after the sessions); peek past the sessions for them
+    std::map<std::string, std::string> trace_prefs;
+    {
+        size_t q = r.p;
+        UInt32 ns; memcpy(&ns, &r.d[q], 4); q += 4;
+        for (UInt32 s = 0; s < ns; s++) { UInt32 l; memcpy(&l, &r.d[q], 4); q += 4 + l + (version >= 2 ? 1 : 0); }
+        if (version >= 4) {
+            UInt32 l; memcpy(&l, &r.d[q], 4);
+            trace_prefs = parse_prefs(std::string((const char*)&r.d[q + 4], l));
+        }
     }
+    std::map<std::string, std::string> eff;
+    for (auto& d : kPrefDefaults) eff[d[0]] = d[1];
+    for (auto& kv : trace_prefs) {
+        if (!eff.count(kv.first)) { fprintf(stderr, "unknown pref %s\n", kv.first.c_str()); return 2; }
+    }
+    // the server's player list is always present (the shipped easydarwin.xml's LIST-PREF);
+    // module prefs the trace does not name are missing from the prefs object
+    trace_prefs.emplace("player_requires_rtp_header_info", eff["player_requires_rtp_header_info"]);
+    load_prefs(trace_prefs);
+    ReflectorStream::Initialize((QTSS_ModulePrefsObject)g_mod_prefs);   // ReflectorStream.cpp:87-117
+    reread_prefs();
 
     // The replay; bench mode repeats it with fresh sessions, subscribers and clock each pass.
     const size_t p0 = r.p;
@@ -368,6 +501,7 @@ int main(int argc, char** argv) {
         r.p += sdplen;
         sflags[s] = version >= 2 ? r.get<UInt8>() : 0;
     }
+    if (version >= 4) { const UInt32 l = r.get<UInt32>(); r.p += l; }   // the prefs, read above
     OSRefTable sessionMap;                         // sSessionMap (QTSSReflectorModule.cpp:89)
     std::vector<Live> live(nsess);
     // FindOrCreateSession's create branch for a push (QTSSReflectorModule.cpp:1391-1478):
@@ -392,7 +526,7 @@ int main(int argc, char** argv) {
         params.inRTSPRequest = (QTSS_RTSPRequestObject)req;
         params.inClientSession = (QTSS_ClientSessionObject)bcast;
         QTSS_Error err = sess->SetupReflectorSession(info, &params,
-            ReflectorSession::kMarkSetup | ReflectorSession::kIsPushSession, true, 30);
+            ReflectorSession::kMarkSetup | ReflectorSession::kIsPushSession, g_mp.oneSSRC, g_mp.timeoutSSRC);
         if (err != QTSS_NoErr) { fprintf(stderr, "setup failed %d\n", (int)err); return false; }
         if (sessionMap.Register(sess->GetRef()) != OS_NoErr) { fprintf(stderr, "register failed\n"); return false; }
         if (sessionMap.Resolve(sess->GetRef()->GetString()) != sess->GetRef()) { fprintf(stderr, "resolve failed\n"); return false; }
@@ -414,6 +548,7 @@ int main(int argc, char** argv) {
         live[s].sess = sess;
         live[s].bcast = bcast;
         live[s].published = true;
+        live[s].killAttr = g_mp.killClients;       // the pusher's RECORD (:1884)
         return true;
     };
     for (UInt32 s = 0; s < nsess; s++)
@@ -472,7 +607,20 @@ int main(int argc, char** argv) {
             // HasFirstRTP / GetFirstPacketInfo; when a stream has nothing buffered the PLAY
             // is deferred (idle-timer retry), which this trace model drops as a join.
             std::vector<UInt16> firstSeq(sess->GetNumStreams(), 0);
-            if (uaflags & 1) {
+            // DoPlay's rtpInfoEnabled (QTSSReflectorModule.cpp:1962-1969) for the player's user agent
+            FakeObj* client = new_obj();
+            const char* ua = kUserAgents[uaflags & 1];
+            set_value(client, qtssCliSesFirstUserAgent, 0, ua, (UInt32)strlen(ua));
+            QTSS_StandardRTSP_Params pp;
+            memset(&pp, 0, sizeof(pp));
+            pp.inClientSession = (QTSS_ClientSessionObject)client;
+            bool rtpInfo = false;
+            if (g_mp.playerCompat)
+                rtpInfo = QTSSModuleUtils::HavePlayerProfile((QTSS_PrefsObject)g_srv_prefs, &pp,
+                                                             QTSSModuleUtils::kRequiresRTPInfoSeqAndTime);
+            if (g_mp.forceRTPInfo) rtpInfo = true;
+            if (g_mp.rtpInfoDisabled) rtpInfo = false;
+            if (rtpInfo) {
                 bool have = true;
                 for (UInt32 x = 0; x < sess->GetNumStreams() && have; x++) {
                     ReflectorStream* rs = sess->GetStreamByIndex(x);
@@ -488,7 +636,7 @@ int main(int argc, char** argv) {
             }
             Sub sb;
             sb.id = sub_id; sb.session = s; sb.rsess = sess;
-            sb.client = new_obj();
+            sb.client = client;
             UInt32 nstreams = sess->GetNumStreams();
             for (UInt32 x = 0; x < nstreams; x++) {
                 FakeObj* st = new_obj();
@@ -570,7 +718,7 @@ int main(int argc, char** argv) {
             sess->RemoveSessionFromOutput((QTSS_ClientSessionObject)live[s].bcast);
             // RemoveOutput(NULL, session, kill) (:2133-2196)
             g_torn_down.clear();
-            if (kill) sess->TearDownAllOutputs();
+            if (kill || live[s].killAttr || g_mp.killClients) sess->TearDownAllOutputs();
             std::vector<void*> closing = g_torn_down;
             release(sess);
             // the server closes every torn-down client session: ClientSessionClosing
@@ -588,9 +736,17 @@ int main(int argc, char** argv) {
                     fprintf(stderr, "resolve failed\n"); return 3;
                 }
                 live[s].published = true;
+                live[s].killAttr = g_mp.killClients;
             } else if (!create(s)) {
                 return 3;
             }
+        } else if (type == 9) {     // PREFS: the server's prefs rewritten, QTSS_RereadPrefs_Role
+            const UInt32 l = r.get<UInt32>();
+            std::map<std::string, std::string> over = parse_prefs(std::string((const char*)&r.d[r.p], l));
+            r.p += l;
+            over.emplace("player_requires_rtp_header_info", "Android,vlc");
+            load_prefs(over);
+            reread_prefs();             // RereadPrefs (ReflectorStream's prefs are not re-read)
         } else if (type == 4) {     // BLOCK
             UInt32 sub_id = r.get<UInt32>();
             UInt16 track = r.get<UInt16>();

@@ -34,6 +34,12 @@
 //             kRRInterval timer (RTCP sender)       ReflectorStream.cpp:1039-1047, h:343
 //             GetACName                             RTCPUtilitiesLib/RTCPSRPacket.cpp:87-117
 //             eye count (AddOutput isClient)        ReflectorSession.cpp:215-268
+//   prefs     ReflectorStream::Initialize           ReflectorStream.cpp:53-59, 87-117
+//             RereadPrefs (module prefs)            QTSSReflectorModule.cpp:100-166, 454-537
+//             per-session SSRC filter settings      QTSSReflectorModule.cpp:1457
+//             kill-clients attribute / RemoveOutput QTSSReflectorModule.cpp:1884, 2156
+//             rtpInfoEnabled + HavePlayerProfile    QTSSReflectorModule.cpp:1962-1969,
+//                                                   APICommonCode/QTSSModuleUtils.cpp:983-1046
 //   lifecycle pusher leave: DestroySession           QTSSReflectorModule.cpp:2082-2109
 //             RemoveOutput / refcount / kill         QTSSReflectorModule.cpp:2133-2196
 //             re-push: FindOrCreateSession           QTSSReflectorModule.cpp:1379-1545
@@ -72,9 +78,68 @@ struct Prefs {                                   // ReflectorStream::Initialize 
     int64_t max_packet_age_ms = 10000;           // 10 x over buffer
     int64_t relocate_age_ms = 2000;              // rtp_reflector_threshold_msec
     int64_t first_packet_offset_ms = 500;        // ReflectorStream::sFirstPacketOffsetMsec (:70)
+    // module prefs (RereadPrefs): new sessions take the SSRC ones
     uint32_t ssrc_timeout_s = 30;                // timeout_stream_SSRC_secs
     bool filter_ssrcs = true;                    // use_one_SSRC_per_stream
+    bool kill_clients = false;                   // kill_clients_when_broadcast_stops
+    bool rtp_info_disabled = false, player_compat = true, force_rtp_info = false;
+    std::vector<std::string> rtp_info_players{"Android", "vlc"};   // the server's player list
+
+    // a trace's pref overrides (easydarwin_amd/trace.py): the stream prefs only at start
+    // (ReflectorStream::Initialize), the module prefs at start and at every PREFS event, each
+    // unnamed one at its default
+    void apply(const std::map<std::string, std::string>& over, bool initial) {
+        auto get = [&](const char* k, const char* d) { auto it = over.find(k); return it == over.end() ? std::string(d) : it->second; };
+        auto u32 = [&](const char* k, const char* d) { return (uint32_t)strtoul(get(k, d).c_str(), nullptr, 10); };
+        auto flag = [&](const char* k, const char* d) { return get(k, d) == "true"; };
+        if (initial) {
+            over_buffer_ms = (int64_t)u32("reflector_buffer_size_sec", "1") * 1000;
+            max_packet_age_ms = over_buffer_ms != 0 ? over_buffer_ms * 10 : 10000;
+            relocate_age_ms = std::max<int64_t>(u32("rtp_reflector_threshold_msec", "2000"), 1000);
+            first_packet_offset_ms = u32("reflector_rtp_info_offset_msec", "500");
+        }
+        ssrc_timeout_s = u32("timeout_stream_SSRC_secs", "30");
+        filter_ssrcs = flag("use_one_SSRC_per_stream", "true");
+        kill_clients = flag("kill_clients_when_broadcast_stops", "false");
+        rtp_info_disabled = flag("disable_rtp_play_info", "false");
+        player_compat = flag("enable_player_compatibility", "true");
+        force_rtp_info = flag("force_rtp_info_sequence_and_time", "false");
+        rtp_info_players.clear();
+        const std::string l = get("player_requires_rtp_header_info", "Android,vlc");
+        for (size_t p = 0; p <= l.size();) {
+            size_t e = l.find(',', p);
+            if (e == std::string::npos) e = l.size();
+            rtp_info_players.push_back(l.substr(p, e - p));
+            p = e + 1;
+        }
+    }
+    // DoPlay's rtpInfoEnabled for a player's user agent (trace.py USER_AGENTS by ua_flags bit 0)
+    bool rtp_info_player(uint8_t ua_flags) const {
+        const std::string ua = (ua_flags & 1) ? "vlc/3.0.8 LibVLC/3.0.8" : "EasyPlayer/1.0";
+        bool on = false;
+        if (player_compat)
+            for (const std::string& x : rtp_info_players) {
+                if (x == "*" || ua.find(x) != std::string::npos) { on = true; break; }
+            }
+        if (force_rtp_info) on = true;
+        if (rtp_info_disabled) on = false;
+        return on;
+    }
 };
+
+static std::map<std::string, std::string> parse_prefs(const uint8_t* b, uint32_t n) {
+    std::map<std::string, std::string> m;
+    std::string s((const char*)b, n);
+    for (size_t p = 0; p < s.size();) {
+        size_t e = s.find('\n', p);
+        if (e == std::string::npos) e = s.size();
+        const std::string line = s.substr(p, e - p);
+        const size_t q = line.find('=');
+        if (q != std::string::npos) m[line.substr(0, q)] = line.substr(q + 1);
+        p = e + 1;
+    }
+    return m;
+}
 
 struct TrackInfo { PayloadType type = kUnknown; std::string name; };
 
@@ -211,6 +276,9 @@ struct Session {
     std::vector<std::unique_ptr<Output>> outputs;   // bucket order == join order here
     std::vector<std::unique_ptr<Output>> left;      // removed outputs (their captures stay)
     bool udp_push = false;
+    bool filter_ssrcs = true;         // SetupReflectorSession's SSRC filter (the prefs then)
+    uint32_t ssrc_timeout_s = 30;
+    bool kill_attr = false;           // the pusher's kill-clients attribute, set at RECORD
 };
 
 struct Model {
@@ -233,6 +301,9 @@ struct Model {
         auto s = std::make_unique<Session>();
         s->idx = idx;
         s->udp_push = udp_push;
+        s->filter_ssrcs = prefs.filter_ssrcs;
+        s->ssrc_timeout_s = prefs.ssrc_timeout_s;
+        s->kill_attr = prefs.kill_clients;
         for (auto& ti : parse_sdp(sdp)) {
             Stream st;
             st.info = ti;
@@ -263,7 +334,7 @@ struct Model {
         Session* se = s < sessions.size() ? sessions[s].get() : nullptr;
         if (!se || !se->published) return;
         se->published = false;
-        if (kill) {
+        if (kill || se->kill_attr || prefs.kill_clients) {
             for (auto& o : se->outputs) se->left.push_back(std::move(o));
             se->outputs.clear();
         }
@@ -273,7 +344,7 @@ struct Model {
     // pusher of a published session is refused
     void publish(uint32_t s) {
         if (s >= sessions.size()) return;
-        if (sessions[s]) { sessions[s]->published = true; return; }
+        if (sessions[s]) { sessions[s]->published = true; sessions[s]->kill_attr = prefs.kill_clients; return; }
         sessions[s] = build(sdps[s].first, sdps[s].second, s);
     }
 
@@ -285,7 +356,7 @@ struct Model {
         return be32(&p.data[8]);
     }
 
-    void filter_ssrc(Sender& s, Packet& p) {
+    void filter_ssrc(Sender& s, Packet& p, uint32_t timeout_s) {
         if (p.len == 0) return;
         int64_t now_s = now / 1000;
         if (s.valid_ssrc == 0) { s.valid_ssrc = get_ssrc(p, s.rtcp_port); s.last_valid_s = now_s; return; }
@@ -294,7 +365,7 @@ struct Model {
             if (ssrc == s.valid_ssrc) { s.last_valid_s = now_s; return; }
             p.len = 0;
         }
-        if (s.last_valid_s + (int64_t)prefs.ssrc_timeout_s < now_s) s.valid_ssrc = 0;
+        if (s.last_valid_s + (int64_t)timeout_s < now_s) s.valid_ssrc = 0;
     }
 
     static bool is_rtcp_sr(const Packet& p) {
@@ -318,7 +389,7 @@ struct Model {
         p.data.assign(data, data + n);
         p.len = n;
         if (snd.rtcp_port && !is_rtcp_sr(p)) return;          // UDP RTCP: SR-first only (Q14)
-        if (prefs.filter_ssrcs) filter_ssrc(snd, p);
+        if (se.filter_ssrcs) filter_ssrc(snd, p, se.ssrc_timeout_s);
         // the pusher's RTCP address (NAT_WORKAROUND): the first datagram sets it, RTCP ones
         // (SRs, by port) move it; an RTP source port that is even is followed by +1
         if (addr != 0 && (st.dest_addr == 0 || snd.rtcp_port)) {
@@ -560,20 +631,29 @@ static bool load(const char* path, Reader& r) {
     r.p = 4;
     const uint32_t v = r.get<uint32_t>();
     r.version = v;
-    return v >= 1 && v <= 3;
+    return v >= 1 && v <= 4;
 }
 
 // Replays a trace into `m`.  `sink_for` (bench mode) routes output bytes to memcpy sinks.
 template <class OnJoin>
 static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 0, uint32_t nshards = 1) {
     uint32_t nsess = r.get<uint32_t>();
+    std::vector<std::pair<std::string, bool>> sess;
     for (uint32_t s = 0; s < nsess; s++) {
         uint32_t n = r.get<uint32_t>();
         std::string sdp((const char*)&r.d[r.p], n);
         r.p += n;
         const uint8_t fl = r.version >= 2 ? r.get<uint8_t>() : 0;
-        m.add_session(sdp, (fl & 1) != 0);
+        sess.emplace_back(sdp, (fl & 1) != 0);
     }
+    std::map<std::string, std::string> over;
+    if (r.version >= 4) {                       // the server's prefs, before any session is set up
+        const uint32_t n = r.get<uint32_t>();
+        over = relay::parse_prefs(&r.d[r.p], n);
+        r.p += n;
+    }
+    m.prefs.apply(over, true);
+    for (auto& se : sess) m.add_session(se.first, se.second);
     while (r.p < r.d.size()) {
         uint8_t type = r.get<uint8_t>();
         if (type == 0) break;
@@ -590,7 +670,7 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
             uint32_t sub = r.get<uint32_t>();
             uint8_t tr = r.get<uint8_t>();
             uint8_t ua = r.get<uint8_t>();
-            if (s % nshards == shard) on_join(s, sub, tr != 0, (ua & 1) != 0);
+            if (s % nshards == shard) on_join(s, sub, tr != 0, m.prefs.rtp_info_player(ua));
         } else if (type == 3) {
             m.tick();
         } else if (type == 4) {
@@ -608,6 +688,10 @@ static void replay(relay::Model& m, Reader& r, OnJoin on_join, uint32_t shard = 
         } else if (type == 8) {                 // PUBLISH
             uint32_t s = r.get<uint32_t>();
             if (s % nshards == shard) m.publish(s);
+        } else if (type == 9) {                 // PREFS: RereadPrefs
+            const uint32_t n = r.get<uint32_t>();
+            m.prefs.apply(relay::parse_prefs(&r.d[r.p], n), false);
+            r.p += n;
         } else if (type == 5) {                 // UPKT: a datagram from the pusher's address
             uint32_t s = r.get<uint32_t>();
             uint8_t ch = r.get<uint8_t>();
@@ -686,6 +770,12 @@ static int run_bench(const char* in, int threads, int repeat) {
         r.p += n;
         udp.push_back(r.version >= 2 && (r.get<uint8_t>() & 1));
     }
+    std::map<std::string, std::string> over;
+    if (r.version >= 4) {
+        const uint32_t n = r.get<uint32_t>();
+        over = relay::parse_prefs(&r.d[r.p], n);
+        r.p += n;
+    }
     std::vector<std::vector<Ev>> lists(threads);
     while (r.p < r.d.size()) {
         Ev e{};
@@ -709,8 +799,8 @@ static int run_bench(const char* in, int threads, int repeat) {
         } else if (e.type == 6) {
             e.sub = r.get<uint32_t>();
             for (auto& l : lists) l.push_back(e);
-        } else if (e.type == 7 || e.type == 8) {
-            fprintf(stderr, "--bench models no session lifecycle (PUBLISH / UNPUBLISH events)\n");
+        } else if (e.type == 7 || e.type == 8 || e.type == 9) {
+            fprintf(stderr, "--bench models no session lifecycle or pref changes (PUBLISH / UNPUBLISH / PREFS)\n");
             return 2;
         } else {
             for (auto& l : lists) l.push_back(e);
@@ -729,6 +819,7 @@ static int run_bench(const char* in, int threads, int repeat) {
             auto a = std::chrono::steady_clock::now();
             for (int rep = 0; rep < repeat; rep++) {
             relay::Model m;
+            m.prefs.apply(over, true);
             for (uint32_t s = 0; s < nsess; s++) m.add_session(sdps[s], udp[s]);   // ids stay global
             std::vector<std::unique_ptr<std::vector<uint8_t>>> sinks;
             for (const Ev& e : lists[t]) {
@@ -738,7 +829,7 @@ static int run_bench(const char* in, int threads, int repeat) {
                 else if (e.type == 2) {
                     sinks.emplace_back(new std::vector<uint8_t>());
                     sinks.back()->reserve(1 << 20);
-                    m.join(e.s, e.sub, e.tcp, sinks.back().get(), (e.ua & 1) != 0);
+                    m.join(e.s, e.sub, e.tcp, sinks.back().get(), m.prefs.rtp_info_player(e.ua));
                 } else if (e.type == 6) {
                     m.leave(e.sub);
                 } else m.tick();

@@ -30,7 +30,11 @@ SAME(qtssCliSesCloseClientTeardown); SAME(qtssCliSesTearDownBroadcastEnded); SAM
 SAME(qtssDescribeMethod); SAME(qtssSetupMethod); SAME(qtssTeardownMethod); SAME(qtssPlayMethod);
 SAME(qtssPauseMethod); SAME(qtssOptionsMethod); SAME(qtssAnnounceMethod); SAME(qtssRecordMethod);
 SAME(qtssAttrDataTypeCharArray); SAME(qtssAttrDataTypeSInt32); SAME(qtssAttrDataTypeUInt32);
-SAME(qtssAttrDataTypeVoidPointer); SAME(qtssAttrDataTypeBool16);
+SAME(qtssAttrDataTypeVoidPointer); SAME(qtssAttrDataTypeBool16); SAME(qtssAttrDataTypeUnknown);
+SAME(qtssPrefsObjectType); SAME(qtssModuleObjectType); SAME(qtssAttrInfoObjectType);
+SAME(qtssCliSesOverBufferEnabled); SAME(qtssModPrefs); SAME(qtssAttrName); SAME(qtssAttrID); SAME(qtssAttrDataType);
+SAME(qtssPrefsPlayersReqRTPHeader);
+SAME(kAddInstanceAttributeCallback); SAME(kGetAttrInfoByNameCallback); SAME(kGetValueAsStringCallback);
 SAME(qtssRTPStreamObjectType); SAME(qtssClientSessionObjectType); SAME(qtssRTSPSessionObjectType);
 SAME(qtssRTSPRequestObjectType); SAME(qtssTextMessagesObjectType); SAME(qtssModulePrefsObjectType);
 SAME(qtssRTPStrTrackID); SAME(qtssRTPStrPayloadName); SAME(qtssRTPStrPayloadType);

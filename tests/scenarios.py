@@ -44,6 +44,12 @@ parity consequence:
                     dropped, duplicate PUBLISH / UNPUBLISH ignored.
 * ``threaded``      tick-invariant streams for the module's default (threaded) mode: players
                     joined before the first packet, no H.264 key frames, TCP and UDP pushers.
+* ``prefs_buffer``  non-default ReflectorStream prefs (read once): a 3-s buffer window, the
+                    RTP-Info offset, the 1000-ms relocation floor, the bucket delay.
+* ``prefs_reread``  non-default module prefs and RereadPrefs (PREFS events): SSRC filtering off,
+                    then a 5-s SSRC timeout for a session set up later; kill_clients by pref; the
+                    RTP-Info player list, forcing and disabling RTP-Info; a 5000-ms relocation
+                    threshold.
 """
 from __future__ import annotations
 
@@ -57,11 +63,13 @@ from easydarwin_amd.trace import TCP, UDP, Trace
 
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
-              joins: list[tuple], tick_times=None, blocks=None, leaves=None, pubs=None):
+              joins: list[tuple], tick_times=None, blocks=None, leaves=None, pubs=None, prefs=None):
     # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
     # blocks: {tick time: [(sub, track, kind, budget)]}
     # leaves: [(t, sub)]
     # pubs: [(t, "publish", session)] / [(t, "unpublish", session, kill)]
+    # prefs: [(t, {pref overrides})] -- the server rewrites its prefs (RereadPrefs), before
+    #        any PUBLISH or packet of the same time
     """Merge per-session packet lists (t, ch, bytes) with joins (t, sess, sub, transport)
     and ticks.  Within one tick interval the order is: packets and pusher PUBLISH / UNPUBLISH
     events (time order: a PUBLISH before and an UNPUBLISH after the packets of its time), then
@@ -77,6 +85,8 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
             pkts.append((p[0], -1, 0, "P", p[2]))
         else:
             pkts.append((p[0], 1 << 30, 0, "U", p[2], p[3]))
+    for k, (t, pr) in enumerate(prefs or []):
+        pkts.append((t, -2, k, "R", pr))
     pkts.sort(key=lambda x: (x[0], x[1], x[2]))
     joins = sorted([(j[0], 0) + tuple(j[1:]) for j in joins] + [(t, 1, sub) for t, sub in (leaves or [])])
     ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
@@ -84,7 +94,9 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
     for tt in ticks:
         while i < len(pkts) and pkts[i][0] <= tt:
             t, s, _, ch, data = pkts[i][:5]
-            if ch == "P":
+            if ch == "R":
+                tr.reprefs(t, data)
+            elif ch == "P":
                 tr.publish(t, data)
             elif ch == "U":
                 tr.unpublish(t, data, pkts[i][5])
@@ -552,11 +564,98 @@ def threaded() -> Trace:
     return _assemble(tr, pk, 100, dur + 200, joins)
 
 
+def prefs_buffer() -> Trace:
+    """ReflectorStream's prefs at non-default values (read once, ReflectorStream::Initialize,
+    ReflectorStream.cpp:87-117):
+
+    * reflector_buffer_size_sec 3: a new output of a stream without a key frame (session 1,
+      MPEG-4) starts 3 s back instead of 1 (GetClientBufferStartPacketOffset, :1201-1231), the
+      packet age limit becomes 30 s (:115) and a new RTP-Info window 3 s;
+    * reflector_rtp_info_offset_msec 1000: an RTP-Info player starts at the oldest packet no older
+      than 3000 - 1000 ms (GetFirstPacketInfo, :728-753);
+    * rtp_reflector_threshold_msec 700 -> the 1000-ms floor (:101-102): a TCP player blocked for
+      1.7 s has its bookmark moved to the newest key frame after 1 s (NeedRelocateBookMark,
+      :1293-1322); another blocked for 0.8 s is not relocated;
+    * reflector_bucket_offset_delay_msec 40: 19 outputs on session 0, three of them in the second
+      bucket of 16, whose writes' transmit times are 40 ms earlier (RTPSessionOutput.cpp:603-608)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 80))
+    s0 = [TrackSpec("video", "H264/90000", 96, bitrate=500_000, gop=45, idr_bytes=6_000, rtcp_every_ms=700),
+          TrackSpec("audio", "PCMA/8000", 8)]
+    s1 = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=300_000), TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    tr.prefs = {"reflector_buffer_size_sec": "3", "reflector_rtp_info_offset_msec": "1000",
+                "rtp_reflector_threshold_msec": "700", "reflector_bucket_offset_delay_msec": "40"}
+    tr.add_session(make_sdp(s0))
+    tr.add_session(make_sdp(s1))
+    pk0 = session_packets(s0, 6000, SEED_BASE + 81)
+    pk1 = session_packets(s1, 6000, SEED_BASE + 82)
+    joins = [(0, 0, k, UDP) for k in range(1, 19)] + [(0, 0, 20, TCP)]
+    joins += [(2500, 0, 21, UDP, VLC), (4100, 0, 22, TCP, VLC), (1500, 1, 30, UDP), (3700, 1, 31, TCP),
+              (4600, 1, 32, UDP, VLC), (5000, 1, 33, TCP, VLC)]
+    ticks = list(range(0, 6001, 100))
+    blocks = {}
+    for t in ticks:
+        if 1000 <= t < 2700:
+            blocks.setdefault(t, []).append((20, 0, 0, 0))          # TCP video: 1.7 s > 1 s floor
+        if 3000 <= t < 3800:
+            blocks.setdefault(t, []).append((5, 0, 0, 0))           # UDP video: 0.8 s, kept
+        if t % 500 == 0 and t > 0:
+            blocks.setdefault(t, []).append((31, 0, 0, int(rng.integers(0, 4))))
+    return _assemble(tr, [pk0, pk1], 100, 6000, joins, tick_times=ticks, blocks=blocks)
+
+
+def prefs_reread() -> Trace:
+    """The module's prefs at non-default values and RereadPrefs (QTSSReflectorModule.cpp:
+    454-537; a PREFS event is the server rewriting its prefs and sending QTSS_RereadPrefs_Role):
+
+    * at start: use_one_SSRC_per_stream false (session 0's pusher switching SSRCs passes whole,
+      FilterInvalidSSRCs off, ReflectorStream.cpp:1819-1820), kill_clients_when_broadcast_stops
+      true (the pusher's leave at 3 s tears its players down although its own flag is off, :1884,
+      2156; the session dies), rtp_reflector_threshold_msec 5000 (read once: a TCP player of
+      session 1 blocked for 3.5 s keeps its bookmark);
+    * 3.2 s: timeout_stream_SSRC_secs 5 and player_requires_rtp_header_info "EasyPlayer"; the
+      SSRC filter is back on by default; kill_clients back off.  Session 0 re-pushed at 3.5 s is a
+      fresh session set up with these: its pusher's new SSRC at 4.5 s is zero-length until 5 s
+      after the old SSRC's last packet; an "EasyPlayer" joiner now takes the RTP-Info PLAY, a
+      "vlc" one does not;
+    * 7 s: force_rtp_info_sequence_and_time (every player RTP-Info); 8.5 s:
+      disable_rtp_play_info (none); session 1's pusher leaves at 9.5 s without kill (players keep
+      it) and returns at 9.8 s."""
+    tr = Trace()
+    tr.prefs = {"use_one_SSRC_per_stream": "false", "kill_clients_when_broadcast_stops": "true",
+                "rtp_reflector_threshold_msec": "5000"}
+    v0 = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=20, idr_bytes=3_000, ssrc=0x0C0C0001)]
+    v0b = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=20, idr_bytes=3_000, ssrc=0x0C0C00BB)]
+    s1 = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=30, idr_bytes=4_000, rtcp_every_ms=800),
+          TrackSpec("audio", "PCMA/8000", 8)]
+    tr.add_session(make_sdp(v0))
+    tr.add_session(make_sdp(s1))
+    dur = 11_000
+    pk0 = [p for p in session_packets(v0, 1000, SEED_BASE + 90)]
+    pk0 += session_packets(v0b, 1000, SEED_BASE + 91, t0=1000)            # SSRC switch: passes (filter off)
+    pk0 += session_packets(v0, 800, SEED_BASE + 92, t0=2000)
+    pk0 += session_packets(v0, 1000, SEED_BASE + 93, t0=3500)             # the fresh session latches ...
+    pk0 += session_packets(v0b, dur - 4600, SEED_BASE + 94, t0=4500)      # ... then a new SSRC: held 5 s
+    pk1 = session_packets(s1, dur, SEED_BASE + 95)
+    joins = [(0, 0, 1, UDP), (500, 0, 2, TCP, VLC), (1500, 0, 3, UDP),
+             (3600, 0, 4, UDP), (3700, 0, 5, TCP, VLC), (6000, 0, 6, UDP), (10_500, 0, 7, TCP),
+             (0, 1, 10, UDP), (0, 1, 11, TCP), (1200, 1, 12, UDP, VLC), (4000, 1, 13, UDP),
+             (7200, 1, 14, UDP), (7300, 1, 15, TCP, VLC), (8700, 1, 16, UDP, VLC), (8800, 1, 17, TCP),
+             (9600, 1, 18, UDP)]
+    ticks = list(range(0, dur + 1, 100))
+    blocks = {t: [(11, 0, 0, 0)] for t in ticks if 3000 <= t < 6500}
+    pubs = [(3000, "unpublish", 0, 0), (3500, "publish", 0), (9500, "unpublish", 1, 0), (9800, "publish", 1)]
+    prefs = [(3200, {"timeout_stream_SSRC_secs": "5", "player_requires_rtp_header_info": "EasyPlayer"}),
+             (7000, {"force_rtp_info_sequence_and_time": "true", "timeout_stream_SSRC_secs": "5"}),
+             (8500, {"disable_rtp_play_info": "true", "force_rtp_info_sequence_and_time": "true"})]
+    return _assemble(tr, [pk0, pk1], 100, dur, joins, tick_times=ticks, blocks=blocks, pubs=pubs, prefs=prefs)
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
     "backpressure": backpressure, "udppush": udppush, "leave": leave, "repush": repush,
-    "threaded": threaded,
+    "threaded": threaded, "prefs_buffer": prefs_buffer, "prefs_reread": prefs_reread,
 }
 
 
@@ -566,7 +665,8 @@ def random_scenario(seed: int, lifecycle: bool = True) -> Trace:
     RTSP-interleaved or a UDP push of H.264 / MPEG-4 / MJPEG video and/or AAC / G.711 audio,
     pusher SRs, jittered sizes; UDP, TCP and RTP-Info players joining at random times; random
     leaves; random socket budgets (BLOCK) on TCP and UDP sub-streams; ticks every 50-200 ms;
-    pushers leaving and returning (PUBLISH / UNPUBLISH, with and without kill_clients).
+    pushers leaving and returning (PUBLISH / UNPUBLISH, with and without kill_clients); the
+    server's prefs at random values and rewritten mid-trace (PREFS: RereadPrefs).
     Kept inside the parity scope of DESIGN.md §4.4 (no lag past the 10-s retention)."""
     rng = np.random.Generator(np.random.PCG64(SEED_BASE + 1000 + seed))
     vids = ["H264/90000", "H264/90000", "MP4V-ES/90000", "JPEG/90000"]
@@ -633,4 +733,36 @@ def random_scenario(seed: int, lifecycle: bool = True) -> Trace:
                     pubs.append((t2, "publish", s))
                     if lrng.random() < 0.2:
                         pubs.append((t2 + 10, "publish", s))            # duplicate: refused
-    return _assemble(tr, per, tick, dur, joins, blocks=blocks, leaves=leaves, pubs=pubs)
+    # preferences, from a third generator: random overrides at start, sometimes a rewrite
+    prefs = []
+    if lifecycle:
+        prng = np.random.Generator(np.random.PCG64(SEED_BASE + 4000 + seed))
+        if prng.random() < 0.4:
+            tr.prefs = _random_prefs(prng, stream=True)
+        if prng.random() < 0.3:
+            prefs.append((int(prng.integers(100, dur)), _random_prefs(prng, stream=False)))
+    return _assemble(tr, per, tick, dur, joins, blocks=blocks, leaves=leaves, pubs=pubs, prefs=prefs)
+
+
+def _random_prefs(rng, stream: bool) -> dict:
+    """A random subset of the prefs a trace may set (easydarwin_amd/trace.py PREF_DEFAULTS)."""
+    choices = {
+        "kill_clients_when_broadcast_stops": lambda: str(bool(rng.random() < 0.5)).lower(),
+        "use_one_SSRC_per_stream": lambda: str(bool(rng.random() < 0.5)).lower(),
+        "timeout_stream_SSRC_secs": lambda: str(int(rng.integers(1, 40))),
+        "disable_rtp_play_info": lambda: str(bool(rng.random() < 0.3)).lower(),
+        "enable_player_compatibility": lambda: str(bool(rng.random() < 0.7)).lower(),
+        "force_rtp_info_sequence_and_time": lambda: str(bool(rng.random() < 0.3)).lower(),
+        "player_requires_rtp_header_info": lambda: str(rng.choice(["Android,vlc", "EasyPlayer", "*", "LibVLC",
+                                                                   "nobody"])),
+    }
+    if stream:
+        choices.update({
+            "reflector_buffer_size_sec": lambda: str(int(rng.integers(1, 5))),
+            "reflector_rtp_info_offset_msec": lambda: str(int(rng.integers(0, 2000))),
+            "rtp_reflector_threshold_msec": lambda: str(int(rng.integers(0, 6000))),
+            "reflector_bucket_offset_delay_msec": lambda: str(int(rng.integers(0, 150))),
+        })
+    keys = sorted(choices)
+    pick = [k for k in keys if rng.random() < 0.4]
+    return {k: choices[k]() for k in pick}

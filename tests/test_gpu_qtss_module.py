@@ -35,11 +35,12 @@ MODULE = os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so")
 REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
 TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "anchor", "rtpinfo", "backpressure"]
 UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones beside them)
+PREFS = ["prefs_buffer", "prefs_reread"]      # the server's prefs objects, RereadPrefs
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["whole", "parts"])
-@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH)
+@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS)
 def test_module_matches_reference(name, gather, tmp_path):
     """`parts`: every tick's readback gathered in parts, overlapped with the write threads
     (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split)."""

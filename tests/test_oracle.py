@@ -55,7 +55,8 @@ def test_port_matches_golden_digests(name, oracle_bins, tmp_path):
     assert hashlib.sha256(cap).hexdigest() == fix["capture_sha256"]
 
 
-@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor", "rtpinfo", "backpressure", "udppush", "leave"])
+@pytest.mark.parametrize("name", ["tiny", "nal", "ssrc", "anchor", "rtpinfo", "backpressure", "udppush", "leave",
+                                  "prefs_buffer", "prefs_reread"])
 def test_reference_harness_reproduces_fixture(name, oracle_bins, tmp_path):
     if oracle_bins["ref"] is None:
         pytest.skip("oracle/_ref/ref_harness not built (reference tree absent)")

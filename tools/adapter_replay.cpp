@@ -10,7 +10,11 @@
 // receiver reports reach the sink's SendReceiverReport.  Writes the capture format of
 // easydarwin_amd/trace.py so tests compare it with the reference harness byte for byte.
 // Usage: adapter_replay <trace.edtr> <capture.edcp>
+// EDGPU_ARENA_BYTES / EDGPU_MAX_OUT_PACKETS set the engine's fan-out capacities (a small arena
+// splits ticks into copy passes); the copy passes are counted on stderr.
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -18,6 +22,7 @@
 #include <vector>
 
 #include "reflector_adapter.h"
+#include "trace_prefs.h"
 
 using namespace edgpu_reflector;
 
@@ -63,17 +68,43 @@ int main(int argc, char** argv) {
     auto get = [&](auto& v) { memcpy(&v, &d[p], sizeof(v)); p += sizeof(v); };
     uint32_t ver, nsess;
     get(ver); get(nsess);
-    Reflector R;
-    if (R.Status()) { fprintf(stderr, "edgpu: %s\n", edgpu_last_error()); return 3; }
-    uint32_t rand_calls = 0;                  // the harness's deterministic rand() (trace.py rr_ssrc)
     std::vector<std::string> sdps(nsess);
     std::vector<uint8_t> udp(nsess, 0);
+    for (uint32_t s = 0; s < nsess; s++) {
+        uint32_t n; get(n);
+        sdps[s].assign((const char*)&d[p], n);
+        p += n;
+        if (ver >= 2) get(udp[s]);
+    }
+    // the server's prefs (trace v4): the stream prefs configure the engine, the module prefs
+    // are kept as the module keeps them (PREFS events: RereadPrefs)
+    trace_prefs::Prefs prefs;
+    if (ver >= 4) {
+        uint32_t n; get(n);
+        prefs = trace_prefs::Prefs::parse(&d[p], n);
+        p += n;
+    }
+    edgpu_config cfg;
+    edgpu_config_default(&cfg);
+    cfg.reflector_buffer_size_sec = prefs.u32("reflector_buffer_size_sec");
+    cfg.rtp_reflector_threshold_msec = std::max<uint32_t>(1000, prefs.u32("rtp_reflector_threshold_msec"));   // :101-102
+    cfg.reflector_rtp_info_offset_msec = prefs.u32("reflector_rtp_info_offset_msec") ? prefs.u32("reflector_rtp_info_offset_msec")
+                                                                                     : EDGPU_FALSE;
+    if (const char* v = getenv("EDGPU_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
+    if (const char* v = getenv("EDGPU_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)strtoul(v, nullptr, 0);
+    Reflector R(&cfg);
+    uint64_t ticks = 0, passes = 0;
+    if (R.Status()) { fprintf(stderr, "edgpu: %s\n", edgpu_last_error()); return 3; }
+    uint32_t rand_calls = 0;                  // the harness's deterministic rand() (trace.py rr_ssrc)
     std::vector<int64_t> sid_of(nsess, -1);   // engine session of each trace session (-1: removed)
+    std::vector<bool> killAttr(nsess, false); // the pusher's kill-clients attribute (its RECORD)
     std::vector<bool> published(nsess, true);
     std::map<uint32_t, uint32_t> trace_of;    // engine session -> trace session
     auto create = [&](uint32_t s, int64_t cnameSecs) -> bool {
         uint32_t sid;
         if (R.SetupReflectorSession(sdps[s], (udp[s] & 1) != 0, &sid)) return false;
+        if (R.SetSSRCFilter(sid, prefs.flag("use_one_SSRC_per_stream"), prefs.u32("timeout_stream_SSRC_secs"))) return false;
+        killAttr[s] = prefs.flag("kill_clients_when_broadcast_stops");
         for (uint32_t x = 0; x < R.GetNumStreams(sid); x++) {
             const uint32_t k = rand_calls++;
             if (R.SetSourceIdentity(sid, x, ((k + 1) * 0x9E3779B1u + 0x7F4A7C15u) & 0x7FFFFFFFu, cnameSecs)) return false;
@@ -82,13 +113,8 @@ int main(int argc, char** argv) {
         trace_of[sid] = s;
         return true;
     };
-    for (uint32_t s = 0; s < nsess; s++) {
-        uint32_t n; get(n);
-        sdps[s].assign((const char*)&d[p], n);
-        p += n;
-        if (ver >= 2) get(udp[s]);
+    for (uint32_t s = 0; s < nsess; s++)
         if (!create(s, 0)) return 3;
-    }
     std::map<std::pair<uint32_t, uint16_t>, Rec> recs;
     std::map<uint32_t, std::tuple<uint32_t, uint32_t, bool>> handles;   // handle -> (sub, trace session, tcp)
     std::map<uint32_t, bool> live;                                      // handle -> still an output
@@ -120,7 +146,7 @@ int main(int argc, char** argv) {
             if (sid_of[s] < 0) continue;      // no such session: the player's SETUP fails
             const uint32_t sid = (uint32_t)sid_of[s];
             uint32_t h;
-            if (ua & 1) {                     // RTP-Info player: PLAY now, or deferred
+            if (prefs.rtp_info_player(ua)) {  // RTP-Info player: PLAY now, or deferred
                 const int err = R.PlayRTPInfo(sid, tr != 0, now, &h, nullptr);
                 if (err == kWouldBlock) continue;
                 if (err) return 3;
@@ -140,6 +166,7 @@ int main(int argc, char** argv) {
             get(s); get(kill);
             if (!published[s]) continue;
             published[s] = false;
+            kill = kill || killAttr[s] || prefs.flag("kill_clients_when_broadcast_stops");   // :2156
             if (kill && sid_of[s] >= 0) {     // TearDownAllOutputs: the session ends with them
                 for (auto& kv : live)
                     if (kv.second && std::get<1>(handles[kv.first]) == s) kv.second = false;
@@ -152,12 +179,19 @@ int main(int argc, char** argv) {
             if (published[s]) continue;
             published[s] = true;
             if (sid_of[s] < 0 && !create(s, now / 1000)) return 3;
+            killAttr[s] = prefs.flag("kill_clients_when_broadcast_stops");
+        } else if (type == 9) {               // PREFS: the server's prefs rewritten (RereadPrefs)
+            uint32_t n; get(n);
+            prefs = trace_prefs::Prefs::parse(&d[p], n);
+            p += n;
         } else if (type == 3) {
             sink.now = t;
             const size_t before = sink.reports.size();
             int err = R.ReflectPackets(t, &sink);
             for (size_t i = before; i < sink.reports.size(); i++) sink.reports[i].session = trace_of[sink.reports[i].session];
             if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
+            ticks++;
+            passes += R.LastTick().passes;
             sink.budget.clear();
         } else if (type == 6) {               // LEAVE: ReflectorSession::RemoveOutput
             uint32_t sub; get(sub);
@@ -210,5 +244,6 @@ int main(int argc, char** argv) {
         }
     }
     fclose(o);
+    fprintf(stderr, "adapter_replay: %llu ticks, %llu copy passes\n", (unsigned long long)ticks, (unsigned long long)passes);
     return 0;
 }

@@ -29,6 +29,13 @@
 //     reference's reference counts itself and fails if the module disagrees: a player's SETUP
 //     must fail exactly when the session has ended;
 //   * TICK -> EDGPU_QTSSReflectorModule_Tick at the virtual clock (manual-tick mode);
+//   * preferences (trace v4): the module object's qtssModPrefs is a prefs object holding the
+//     trace's overrides of the QTSSReflectorModule prefs (typed as easydarwin.xml types them),
+//     and Initialize's inPrefs the server prefs object with player_requires_rtp_header_info;
+//     both are dictionaries with attribute-info lookup by name (QTSS_GetAttrInfoByName),
+//     instance attributes, value counts and string values -- what QTSSModuleUtils::
+//     GetAttribute / HavePlayerProfile use.  A PREFS event rewrites them and sends
+//     QTSS_RereadPrefs_Role;
 //   * BLOCK -> the player's RTP stream object accepts `budget` QTSS_Writes in the next tick,
 //     then returns QTSS_WouldBlock (the EAGAIN path of RTPStream::Write).
 // QTSS_Write on an RTP stream object frames the packet as RTPStream::Write does (UDP: the
@@ -84,6 +91,7 @@
 #include <vector>
 
 #include "qtss_module_abi.h"
+#include "trace_prefs.h"
 
 using namespace edqtss;
 
@@ -104,6 +112,8 @@ struct Obj {
     size_t body_off = 0;
     // client sessions
     bool played = false, idle_timer = false, torn_down = false;
+    // dictionaries with named (instance) attributes: the prefs objects
+    std::map<std::string, std::pair<uint32_t, uint32_t>> named;   // name -> (id, data type)
 };
 static std::vector<std::unique_ptr<Obj>> g_objs;
 static Obj* new_obj(uint32_t type) { g_objs.emplace_back(new Obj()); g_objs.back()->type = type; return g_objs.back().get(); }
@@ -168,6 +178,63 @@ static QTSS_Error cb_get_value(Obj* o, uint32_t id, uint32_t idx, void* buf, uin
     *len = (uint32_t)v.size();
     return QTSS_NoErr;
 }
+// attribute info by name / instance attributes / value counts / string values (prefs objects)
+static uint32_t g_next_named = 0x20000000u;
+static QTSS_Error cb_attr_info_by_name(Obj* o, const char* name, Obj** out, ...) {
+    if (!o || !name || !out) return QTSS_BadArgument;
+    auto it = o->named.find(name);
+    if (it == o->named.end()) return QTSS_AttrDoesntExist;
+    Obj* info = new_obj(qtssAttrInfoObjectType);
+    set_pod(info, qtssAttrID, it->second.first);
+    set_pod(info, qtssAttrDataType, it->second.second);
+    set_attr(info, qtssAttrName, 0, name, (uint32_t)strlen(name));
+    *out = info;
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_add_instance_attr(Obj* o, const char* name, void*, uint32_t type, ...) {
+    if (!o || !name) return QTSS_BadArgument;
+    if (o->named.count(name)) return QTSS_AttrNameExists;
+    o->named[name] = std::make_pair(g_next_named++, type);
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_num_values(Obj* o, uint32_t id, uint32_t* n, ...) {
+    if (!o || !n) return QTSS_BadArgument;
+    auto it = o->attrs.find(id);
+    *n = it == o->attrs.end() ? 0 : (uint32_t)it->second.size();
+    return QTSS_NoErr;
+}
+static QTSS_Error cb_value_as_string(Obj* o, uint32_t id, uint32_t idx, char** out, ...) {
+    if (!o || !out) return QTSS_BadArgument;
+    *out = nullptr;
+    auto it = o->attrs.find(id);
+    if (it == o->attrs.end() || idx >= it->second.size()) return QTSS_ValueNotFound;
+    const std::string& v = it->second[idx];
+    char* c = new char[v.size() + 1];          // QTSS_GetValueAsString: the caller delete[]s it
+    memcpy(c, v.data(), v.size());
+    c[v.size()] = 0;
+    *out = c;
+    return QTSS_NoErr;
+}
+// the trace's prefs into the module's prefs object and the server's (trace_prefs.h: only the
+// overridden module prefs exist; the player list always does, as in the shipped easydarwin.xml)
+static Obj* g_mod_prefs = nullptr;
+static Obj* g_srv_prefs = nullptr;
+static void load_prefs(const trace_prefs::Prefs& p) {
+    g_mod_prefs->attrs.clear();
+    g_mod_prefs->named.clear();
+    for (const auto& kv : p.over) {
+        if (kv.first == "player_requires_rtp_header_info") continue;
+        const bool isBool = kv.second == "true" || kv.second == "false";
+        const uint32_t id = g_next_named++;
+        g_mod_prefs->named[kv.first] = std::make_pair(id, (uint32_t)(isBool ? qtssAttrDataTypeBool16 : qtssAttrDataTypeUInt32));
+        if (isBool) set_pod<bool>(g_mod_prefs, id, kv.second == "true");
+        else set_pod<uint32_t>(g_mod_prefs, id, (uint32_t)strtoul(kv.second.c_str(), nullptr, 10));
+    }
+    g_srv_prefs->attrs.erase(qtssPrefsPlayersReqRTPHeader);
+    uint32_t i = 0;
+    for (const std::string& v : p.list("player_requires_rtp_header_info"))
+        set_attr(g_srv_prefs, qtssPrefsPlayersReqRTPHeader, i++, v.data(), (uint32_t)v.size());
+}
 static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* buf, uint32_t len, ...) {
     if (!o) return QTSS_BadArgument;
     set_attr(o, id, idx, buf, len);
@@ -176,6 +243,7 @@ static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* bu
 // QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
 static uint64_t g_writes = 0;
 static uint64_t g_prestaged = 0;                      // batch bytes the module copied ahead (trace mode)
+static uint64_t g_passes = 0, g_ticks = 0;            // copy passes of the manual ticks (trace mode)
 static bool g_count_only = false;                    // --bench: sinks count, no capture
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
@@ -531,6 +599,10 @@ int main(int argc, char** argv) {
     cbs.addr[kSendStandardRTSPCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kAppendRTSPHeadersCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kRequestEventCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kGetAttrInfoByNameCallback] = (QTSS_CallbackProcPtr)cb_attr_info_by_name;
+    cbs.addr[kAddInstanceAttributeCallback] = (QTSS_CallbackProcPtr)cb_add_instance_attr;
+    cbs.addr[kGetNumValuesCallback] = (QTSS_CallbackProcPtr)cb_num_values;
+    cbs.addr[kGetValueAsStringCallback] = (QTSS_CallbackProcPtr)cb_value_as_string;
     QTSS_PrivateArgs args;
     memset(&args, 0, sizeof(args));
     args.inServerAPIVersion = kApiVersion;
@@ -560,7 +632,29 @@ int main(int argc, char** argv) {
         setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
     }
     if (bench) setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
+    // the trace's prefs (version 4, after the sessions) are the prefs objects' values at Initialize
+    Reader r;
+    trace_prefs::Prefs prefs;
+    if (!bench) {
+        FILE* f = fopen(argv[2], "rb");
+        if (!f) { perror(argv[2]); return 2; }
+        fseek(f, 0, SEEK_END); r.d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
+        if (fread(r.d.data(), 1, r.d.size(), f) != r.d.size()) return 2;
+        fclose(f);
+        uint32_t v, ns;
+        memcpy(&v, &r.d[4], 4); memcpy(&ns, &r.d[8], 4);
+        size_t q = 12;
+        for (uint32_t s = 0; s < ns; s++) { uint32_t l; memcpy(&l, &r.d[q], 4); q += 4 + l + (v >= 2 ? 1 : 0); }
+        if (v >= 4) { uint32_t l; memcpy(&l, &r.d[q], 4); prefs = trace_prefs::Prefs::parse(&r.d[q + 4], l); }
+    }
+    g_mod_prefs = new_obj(qtssModulePrefsObjectType);
+    g_srv_prefs = new_obj(qtssPrefsObjectType);
+    load_prefs(prefs);
+    Obj* module = new_obj(qtssModuleObjectType);
+    set_pod<Obj*>(module, qtssModPrefs, g_mod_prefs);
     memset(&rp, 0, sizeof(rp));
+    rp.initParams.inPrefs = g_srv_prefs;
+    rp.initParams.inModule = module;
     if (g_dispatch(QTSS_Initialize_Role, &rp) != QTSS_NoErr) { fprintf(stderr, "Initialize failed (no GPU?)\n"); return 3; }
     if (bench) {
         auto last_fn = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
@@ -571,12 +665,6 @@ int main(int argc, char** argv) {
         return rc;
     }
 
-    Reader r;
-    FILE* f = fopen(argv[2], "rb");
-    if (!f) { perror(argv[2]); return 2; }
-    fseek(f, 0, SEEK_END); r.d.resize(ftell(f)); fseek(f, 0, SEEK_SET);
-    if (fread(r.d.data(), 1, r.d.size(), f) != r.d.size()) return 2;
-    fclose(f);
     r.p = 4;
     const uint32_t ver = r.get<uint32_t>();
     const uint32_t nsess = r.get<uint32_t>();
@@ -634,6 +722,7 @@ int main(int argc, char** argv) {
         paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
         if (!publish(s)) { fprintf(stderr, "push SETUP failed\n"); return 3; }
     }
+    if (ver >= 4) { const uint32_t l = r.get<uint32_t>(); r.p += l; }   // the prefs (read before Initialize)
     auto close_client = [&](Obj* client) {
         QTSS_RoleParams p;
         memset(&p, 0, sizeof(p));
@@ -701,7 +790,7 @@ int main(int argc, char** argv) {
             if (e) { fprintf(stderr, "tick failed %d\n", (int)e); return 3; }
             static auto last_tick = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
             EDGPU_QTSSTickInfo ti;
-            if (last_tick && last_tick(&ti) == QTSS_NoErr) g_prestaged += ti.prestaged_bytes;
+            if (last_tick && last_tick(&ti) == QTSS_NoErr) { g_prestaged += ti.prestaged_bytes; g_passes += ti.passes; g_ticks++; }
             read_reports();
             for (Obj* st : g_streams) st->budget[0] = st->budget[1] = -1;
         } else if (type == 4) {                                  // BLOCK
@@ -748,8 +837,8 @@ int main(int argc, char** argv) {
             if (!push_rtsp[s]) continue;
             auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleTearDownClients");
             if (it == g_attr_ids.end()) { fprintf(stderr, "kill-clients attribute not registered\n"); return 3; }
-            const uint16_t k16 = kill;
-            set_attr(push_client[s], it->second, 0, &k16, sizeof(k16));
+            // the event's kill flag is the attribute set at RECORD (the module sets it from its pref)
+            if (kill) { const uint16_t k16 = kill; set_attr(push_client[s], it->second, 0, &k16, sizeof(k16)); }
             close_client(push_client[s]);
             push_rtsp[s] = push_client[s] = nullptr;
             // the server closes the client sessions the module tore down (QTSS_Teardown)
@@ -763,6 +852,13 @@ int main(int argc, char** argv) {
                 }
             if (kill && torn == 0 && holders[s] != 0) { fprintf(stderr, "kill_clients tore nothing down\n"); return 3; }
             release_check(s);
+        } else if (type == 9) {                                  // PREFS -> QTSS_RereadPrefs_Role
+            const uint32_t n = r.get<uint32_t>();
+            load_prefs(trace_prefs::Prefs::parse(&r.d[r.p], n));
+            r.p += n;
+            QTSS_RoleParams p;
+            memset(&p, 0, sizeof(p));
+            if (g_dispatch(QTSS_RereadPrefs_Role, &p) != QTSS_NoErr) { fprintf(stderr, "RereadPrefs failed\n"); return 3; }
         } else if (type == 8) {                                  // PUBLISH -> a new pusher connection
             const uint32_t s = r.get<uint32_t>();
             if (push_rtsp[s]) {                                  // a duplicate broadcast must be refused
@@ -939,7 +1035,8 @@ int main(int argc, char** argv) {
             }
         fclose(t);
     }
-    fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes, %llu bytes copied ahead of their ticks\n", players.size(),
-            (unsigned long long)g_writes, (unsigned long long)g_prestaged);
+    fprintf(stderr, "qtss_replay: %zu players, %llu QTSS_Writes, %llu bytes copied ahead of their ticks, "
+            "%llu copy passes in %llu ticks\n", players.size(), (unsigned long long)g_writes, (unsigned long long)g_prestaged,
+            (unsigned long long)g_passes, (unsigned long long)g_ticks);
     return 0;
 }
