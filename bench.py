@@ -422,6 +422,10 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
+    if rank == 0:
+        log(f"[bench] C3 (BASELINE configs[2], 8192 streams x 64 subscribers over 8 GPUs): "
+            f"python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 "
+            f"bench.py --gpus 8 --subs 64   (this run: --subs {args.subs}, {world} rank(s))")
     # every rank owns exactly args.sessions streams of the hash-sharded population (weak scaling)
     gids = owned_sessions(args.sessions, rank, world) if world > 1 else np.arange(args.sessions)
     fleet = H264Fleet(gids, tick_ms=args.tick_ms)

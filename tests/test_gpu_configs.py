@@ -123,7 +123,10 @@ def test_c4_burst_joins_match_owner_gop():
     cfg = dict(video_ring_packets=8192, video_ring_bytes=16 << 20, other_ring_packets=256,
                other_ring_bytes=64 << 10, out_arena_bytes=12 << 30, max_out_packets=joins * 1200,
                max_batch_packets=max_pk + 1, max_batch_bytes=max_bytes + 16)
-    with edgpu.Context(**cfg) as owner, edgpu.Context(**cfg) as replica:
+    # the replica on a second GPU when there is one: the image crosses devices over xGMI
+    import torch
+    rdev = 1 if torch.cuda.device_count() > 1 else 0
+    with edgpu.Context(**cfg) as owner, edgpu.Context(device=rdev, **cfg) as replica:
         sdp = fleet.sdp()
         osess = [owner.session_add(sdp) for _ in range(n_sess)]
         rsess = [replica.session_add(sdp) for _ in range(n_sess)]
@@ -157,7 +160,7 @@ def test_c4_burst_joins_match_owner_gop():
         img_dst = replica.device_alloc(total)
         offs2, _ = owner.session_export([osess[g] for g in need], now, img_src.ptr, img_src.nbytes)
         assert np.array_equal(offs, offs2)
-        replica.memcpy_peer(img_dst.ptr, 0, img_src.ptr, total)
+        replica.memcpy_peer(img_dst.ptr, 0, img_src.ptr, total)          # owner GPU 0 -> replica GPU
         replica.session_import(img_dst.ptr, offs, [rsess[g] for g in need])
         h_own = owner.subscribers_add([osess[g] for g in sess_of[~remote]], edgpu.TRANSPORT_UDP)
         h_rep = replica.subscribers_add([rsess[g] for g in sess_of[remote]], edgpu.TRANSPORT_UDP)

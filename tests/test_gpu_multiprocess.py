@@ -8,7 +8,9 @@ multi-GPU path of SURVEY.md §8.e executed by libedgpu in separate processes, as
 * Exchange: one process owns every session (ingest + owner ticks), the other serves every
   subscriber from replica sessions kept in step by session images that dist.exchange_images
   moves between the processes each tick (DistReplicaLink: full image first, deltas after); the
-  subscribers' bytes equal the reference reflector's capture.
+  subscribers' bytes equal the reference reflector's capture.  With two or more GPUs visible
+  the processes take GPUs 0 and 1 and the images cross devices over RCCL (nccl backend, device
+  buffers); on a one-GPU box both share GPU 0 and the images go over gloo through host memory.
 """
 import hashlib
 import json
@@ -32,14 +34,24 @@ def _free_port():
     return p
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     return dist
+
+
+def _gpus():
+    import torch
+    return torch.cuda.device_count()          # counts devices without initialising the GPU
 
 
 def _shard_worker(rank, world, port, n_sess, out_q):
@@ -86,9 +98,11 @@ def test_two_engine_processes_shard_sessions(oracle_bins):
 
 
 def _exchange_worker(rank, world, port, name, out_q):
-    """rank 0: owner of every session of the scenario; rank 1: every subscriber, on replicas."""
+    """rank 0: owner of every session of the scenario; rank 1: every subscriber, on replicas.
+    Two GPUs: rank r on GPU r, images over RCCL; one GPU: both on GPU 0, images over gloo."""
     try:
-        dist = _init(rank, world, port)
+        cross = _gpus() >= world
+        dist = _init(rank, world, port, "nccl" if cross else "gloo")
         import numpy as np
         from easydarwin_amd import edgpu
         from easydarwin_amd.dist import owner
@@ -99,8 +113,8 @@ def _exchange_worker(rank, world, port, name, out_q):
         tr = _trace(name)
         # global ids whose FNV-1a owner is rank 0, one per trace session
         gid = [g for g in range(10_000) if owner(g, world) == 0][:len(tr.sdps)]
-        with edgpu.Context(device=0) as ctx:
-            link = DistReplicaLink(ctx, world, rank, comm="cpu")
+        with edgpu.Context(device=rank if cross else 0) as ctx:
+            link = DistReplicaLink(ctx, world, rank, comm="cuda" if cross else "cpu")
             local = {}
             if rank == 0:
                 for s, sdp in enumerate(tr.sdps):
@@ -151,7 +165,7 @@ def _exchange_worker(rank, world, port, name, out_q):
             else:
                 result = link.bytes_sent
             got = [None] * world
-            dist.all_gather_object(got, result)
+            dist.all_gather_object(got, (result, cross))
             if rank == 0:
                 out_q.put(got)
         dist.destroy_process_group()
@@ -176,6 +190,7 @@ def test_session_images_move_between_engine_processes(name):
         p.join(timeout=120)
     assert got[0] != "error", got
     assert all(p.exitcode == 0 for p in procs)
-    sent, (digest, received) = got[0], got[1]
+    (sent, cross), ((digest, received), _) = got[0], got[1]
+    assert cross == (_gpus() >= 2)
     assert sent == received > 0
     assert digest == fix["capture_sha256"]
