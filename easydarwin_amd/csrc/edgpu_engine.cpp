@@ -1170,7 +1170,13 @@ int edgpu_host_free(edgpu_ctx* x, void* p) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!p) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
-    if (x->h2d) HIP_CHECK(hipStreamSynchronize(x->h2d));
+    // any thread may free (a pusher growing its blob): the copy stream is created under pin_mu
+    hipStream_t h2d;
+    {
+        std::lock_guard<std::mutex> g(x->pin_mu);
+        h2d = x->h2d;
+    }
+    if (h2d) HIP_CHECK(hipStreamSynchronize(h2d));
     HIP_CHECK(hipHostFree(p));
     return EDGPU_OK;
 }

@@ -203,7 +203,8 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
         Batch& b = fBatch[fFill];
         Stripe& st = b.st[k];
         if (st.used + slot > st.cap) {                       // a new slab
-            if (b.next + kSlab > b.cap) {
+            // b.next moves by CAS under other stripes' locks: read it atomically
+            if (__atomic_load_n(&b.next, __ATOMIC_RELAXED) + kSlab > b.cap) {
                 // grow under every stripe lock (taken in order: release ours first), then retry
                 g.unlock();
                 LockAllStripes();

@@ -316,9 +316,12 @@ int  edgpu_ingest(edgpu_ctx* ctx, const edgpu_pkt_desc* desc, uint32_t n_packets
  * of two device staging sets on a dedicated copy stream, and k_ingest waits for that copy on
  * the context stream -- so the PCIe transfer of batch t+1 overlaps the fan-out of batch t, and
  * the call returns without waiting for the GPU.  Buffer reuse: a pinned batch may be rewritten
- * once the NEXT ingest call (edgpu_ingest of any pointer kind, or edgpu_ingest_interleaved) has
- * returned -- every ingest entry point waits for the previous pinned batch's copy -- so two host
- * batches used alternately never stall the reader on the GPU. */
+ * once the NEXT ingest call (edgpu_ingest of any pointer kind, or edgpu_ingest_interleaved), or
+ * any call that synchronises the context (edgpu_sync, edgpu_tick_stats_get), has returned --
+ * every ingest entry point waits for the previous pinned batch's copy, and the context stream
+ * waits for it before its ingest kernel -- so two host batches used alternately never stall the
+ * reader on the GPU.  edgpu_host_alloc / edgpu_host_free
+ * may be called from any thread (a pusher growing its blob); a free waits for the copy stream. */
 int  edgpu_host_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_host_free(edgpu_ctx* ctx, void* ptr);
 /* Copies bytes [offset, offset + bytes) of the NEXT pinned batch's blob to the device ahead of
