@@ -242,18 +242,57 @@ struct Module {
 };
 Module* M = nullptr;
 
-// "<file path without /trackID=N and leading '/'>-<channel>", the stream ID of the reference
-// (theStreamName, QRM:923-925 / 1384), channel from the query's "channel=" (EASY_TAG_CHANNEL)
+// The channel of a request: the first "channel" parameter (any case) of the URL-decoded query
+// string, 1 without one (DoSessionSetup / DoAnnounce, QRM:740-756 / 919-935: EasyUtil::Urldecode,
+// '%XX' and '+' -> ' ', then QueryParamList::BulidList's name=value parse, QueryParamList.cpp:64-103,
+// and DoFindCGIValueForParam's case-insensitive lookup of EASY_TAG_CHANNEL "Channel")
+uint32_t ChannelOf(const std::string& query) {
+    std::string q;
+    for (size_t i = 0; i < query.size(); i++) {
+        if (query[i] == '%' && i + 2 < query.size()) {
+            auto hex = [](char c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; };
+            q += (char)((hex(query[i + 1]) << 4) | hex(query[i + 2]));
+            i += 2;
+        } else {
+            q += query[i] == '+' ? ' ' : query[i];
+        }
+    }
+    for (size_t i = 0; i < q.size();) {
+        const size_t eq = q.find('=', i);
+        if (eq == std::string::npos) break;                     // a name with no '=': the parse ends
+        std::string name = q.substr(i, eq - i), value;
+        size_t j = eq + 1;
+        if (j < q.size() && q[j] == '"') {                      // a quoted value
+            const size_t close = q.find('"', j + 1);
+            value = q.substr(j + 1, (close == std::string::npos ? q.size() : close) - j - 1);
+            j = close == std::string::npos ? q.size() : q.find('&', close + 1);
+        } else {
+            const size_t amp = q.find('&', j);
+            value = q.substr(j, (amp == std::string::npos ? q.size() : amp) - j);
+            j = amp;
+        }
+        std::string lower = name;
+        for (char& c : lower) c = (char)tolower((unsigned char)c);
+        if (lower == "channel") return (uint32_t)atoi(value.c_str());
+        if (j == std::string::npos) break;
+        i = j + 1;
+    }
+    return 1;
+}
+
+// "<file name>-<channel>", the reference's stream name (theStreamName, QRM:937-938 / 1383-1384):
+// the server's qtssRTSPReqFileName is the path's FIRST component (RTSPRequestInterface::GetFileName,
+// RTSPRequestInterface.cpp:681-711), and the player's lookup path is the same name (GetFullPath with
+// EasyDarwin's empty root directory, RTSPRequestInterface.cpp:219-224)
 std::string StreamName(QTSS_Object req) {
-    std::string path = GetString(req, qtssRTSPReqFilePath);
-    const size_t tr = path.find("/trackID=");
-    if (tr != std::string::npos) path.resize(tr);
-    while (!path.empty() && path[0] == '/') path.erase(0, 1);
-    uint32_t channel = 1;
-    const std::string q = GetString(req, qtssRTSPReqQueryString);
-    const size_t c = q.find("channel=");
-    if (c != std::string::npos && (c == 0 || q[c - 1] == '&')) channel = (uint32_t)strtoul(q.c_str() + c + 8, nullptr, 10);
-    return path + "-" + std::to_string(channel);
+    return GetString(req, qtssRTSPReqFileName) + "-" + std::to_string(ChannelOf(GetString(req, qtssRTSPReqQueryString)));
+}
+
+// a first SETUP the reflector does not take: an empty file name, or a ".mov" (DoSessionSetup,
+// QRM:758-767, 805-818)
+bool NotReflected(QTSS_Object req) {
+    const std::string n = GetString(req, qtssRTSPReqFileName);
+    return n.empty() || (n.size() > 4 && n.compare(n.size() - 4, 4, ".mov") == 0);
 }
 
 uint32_t TrackFromRequest(QTSS_Object req, bool* ok) {
@@ -637,8 +676,11 @@ QTSS_Error Shutdown() {
 // ANNOUNCE (DoAnnounce, QRM:898-1174): read the request body (QTSS_Read, resumable), keep the
 // SDP under the stream name for the pusher's SETUPs and the players' DESCRIBE
 QTSS_Error DoAnnounce(QTSS_StandardRTSP_Params* p) {
-    const std::string path = GetString(p->inRTSPRequest, qtssRTSPReqFilePath);
-    if (path.size() < 4 || path.compare(path.size() - 4, 4, ".sdp") != 0) return QTSS_RequestFailed;
+    // any name will do (the reference's SDP suffix is empty, QRM:183, 953-962); an announced
+    // "<name>.kill" only looks a session up to kill it (QRM:940-951, 1052-1059) -- by the bare name,
+    // which never carries the "-<channel>" every session name has, so here it is refused outright
+    const std::string name = GetString(p->inRTSPRequest, qtssRTSPReqFileName);
+    if (name.size() > 5 && name.compare(name.size() - 5, 5, ".kill") == 0) return QTSS_RequestFailed;
     uint32_t clen = 0;
     if (!GetPOD(p->inRTSPRequest, qtssRTSPReqContentLen, &clen)) return QTSS_RequestFailed;
     std::string* body = nullptr;
@@ -778,7 +820,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         Session* s = nullptr;
         if (GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &held) && held) s = FindSession((uint32_t)held);
         const bool first = s == nullptr;
-        if (first) s = FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
+        if (first) s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
         if (!s) return QTSS_RequestFailed;
         if (first) DisableOverbufferingIfPref(p->inClientSession);
         // the reference sets the session up for one transport; a pusher of the other cannot join it
@@ -817,7 +859,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     // a player: the first SETUP creates its output and takes a reference (QRM:1614-1622)
     Output* o = nullptr;
     if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {
-        Session* s = FindOrCreateSession(StreamName(p->inRTSPRequest), false);
+        Session* s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), false);
         if (!s) return QTSS_RequestFailed;
         DisableOverbufferingIfPref(p->inClientSession);
         M->outputs.emplace_back(new Output());
@@ -883,7 +925,7 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
         uintptr_t sid = 0;
         if (!GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &sid) || !sid) return QTSS_RequestFailed;
         // the pref decides, per pusher, whether its leaving tears the players down (QRM:1884)
-        const uint16_t kill = M->killClients ? 1 : 0;
+        const bool kill = M->killClients;                 // a C++ bool, as the reference writes it
         (void)SetValue(p->inClientSession, sKillClientsEnabledAttr, 0, &kill, sizeof(kill));
         (void)SetValue(p->inRTSPSession, sRTSPBroadcastSessionAttr, 0, &sid, sizeof(sid));
         const bool keep = true;
@@ -1033,9 +1075,9 @@ QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
         // the pusher left (DestroySession's broadcaster branch, QRM:2082-2109)
         const uintptr_t none = 0;
         (void)SetValue(p->inClientSession, sClientBroadcastSessionAttr, 0, &none, sizeof(none));
-        uint16_t kill = 0;
+        bool kill = false;                                // (QRM:2101-2103: a bool, sizeof 1)
         uint32_t n = sizeof(kill);
-        if (GetValue(p->inClientSession, sKillClientsEnabledAttr, 0, &kill, &n) != QTSS_NoErr) kill = 0;
+        if (GetValue(p->inClientSession, sKillClientsEnabledAttr, 0, &kill, &n) != QTSS_NoErr) kill = false;
         std::vector<QTSS_Object> teardown;
         {
             std::lock_guard<std::mutex> g(M->mu);

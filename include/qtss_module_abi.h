@@ -92,7 +92,7 @@ enum : uint32_t {
 // attribute data types (QTSS.h:358-378)
 enum : uint32_t {
     qtssAttrDataTypeUnknown = 0, qtssAttrDataTypeCharArray = 1, qtssAttrDataTypeBool16 = 2,
-    qtssAttrDataTypeSInt32 = 5, qtssAttrDataTypeUInt32 = 6, qtssAttrDataTypeVoidPointer = 13,
+    qtssAttrDataTypeUInt16 = 4, qtssAttrDataTypeSInt32 = 5, qtssAttrDataTypeUInt32 = 6, qtssAttrDataTypeVoidPointer = 13,
 };
 
 // object types (QTSS.h:266-282)
@@ -119,11 +119,12 @@ enum : uint32_t {
     qtssCliTeardownReason = 23, qtssCliSesOverBufferEnabled = 33,
     // module object (QTSS.h:894-905), attribute-info object (:911-918), server prefs (:718-800)
     qtssModPrefs = 4, qtssAttrName = 0, qtssAttrID = 1, qtssAttrDataType = 2,
-    qtssPrefsPlayersReqRTPHeader = 70,
+    qtssPrefsMovieFolder = 5, qtssPrefsPlayersReqRTPHeader = 70,
     // RTSP request object (QTSS.h:588-623)
     qtssRTSPReqFilePath = 2, qtssRTSPReqFileName = 5, qtssRTSPReqFileDigit = 6,
     qtssRTSPReqMethod = 9, qtssRTSPReqRespKeepAlive = 13, qtssRTSPReqQueryString = 23,
     qtssRTSPReqContentLen = 25, qtssRTSPReqTransportType = 28, qtssRTSPReqTransportMode = 29,
+    qtssRTSPReqRootDir = 14,
     qtssRTSPReqSetUpServerPort = 30,                 // UInt16: server_port of a push SETUP's response
 };
 
@@ -198,7 +199,8 @@ enum : uint32_t {
     kAddRTPStreamCallback = 19, kPlayCallback = 20, kPauseCallback = 21, kTeardownCallback = 22,
     kRequestEventCallback = 23, kSetIdleTimerCallback = 24, kReadCallback = 27,
     kGetNumValuesCallback = 30, kAddStaticAttributeCallback = 35, kAddInstanceAttributeCallback = 36,
-    kGetAttrInfoByNameCallback = 39, kGetValueAsStringCallback = 41, kRemoveValueCallback = 46,
+    kGetAttrInfoByNameCallback = 39, kGetValueAsStringCallback = 41, kValueToStringCallback = 45,
+    kRemoveValueCallback = 46, kRefreshTimeOutCallback = 52, kLockObjectCallback = 55, kUnlockObjectCallback = 56,
     kLastCallback = 62,
 };
 struct QTSS_Callbacks {

@@ -1,0 +1,167 @@
+// oracle/ref_module_host.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as the
+// product).  What the EasyDarwin server process gives the REFERENCE QTSSReflectorModule when the
+// module, compiled from the read-only reference sources, is loaded as a QTSS module by the fake
+// server tools/qtss_replay (oracle/_ref/Makefile: libQTSSReflectorModule_ref.so):
+//
+//   * the server object behind QTSServerInterface::GetServer(), of which the module only reads
+//     the reflector session map (QTSSReflectorModule.cpp:373 -> QTSServerInterface.h:232), and the
+//     server's module tables with zero modules in any role (QTSServerInterface.h:356-357; the
+//     Redis roles ReflectorSession calls then do nothing -- as in oracle/ref_harness.cpp);
+//   * the socket event machinery the server sets up before loading modules (Socket::Initialize,
+//     epollInit): the UDP-push sockets BindSockets binds register with it (RequestEvent); the
+//     event thread is not started;
+//   * the clock: OS::Milliseconds is link-wrapped onto QTSS_Milliseconds, the fake server's
+//     virtual clock (the reference server's OS::Milliseconds is the same clock the callback
+//     reads);
+//   * the work the server's task threads would do, as manual entry points with the names the
+//     drop-in exports (include/qtss_module_abi.h), so one fake server drives both:
+//       EDGPU_QTSSReflectorModule_Tick    -- ReflectPackets on every sender of every registered
+//                                            session (RTP then RTCP, track order), as
+//                                            ReflectorSocket::Run does (ReflectorStream.cpp:
+//                                            1709-1714) and oracle/ref_harness.cpp's TICK does;
+//       EDGPU_QTSSReflectorModule_PollUDP -- the datagrams waiting on the UDP-push sockets the
+//                                            module bound (UDPSocketPool, BindSockets :388-506),
+//                                            each clamped to the 2060-byte packet buffer and
+//                                            handed to ReflectorSocket::ProcessPacket(now,
+//                                            packet, remote addr, remote port), as
+//                                            GetIncomingData does (:2013-2060) and the harness's
+//                                            UPKT does; returns the datagrams read.
+// Everything else -- ANNOUNCE / SETUP / PLAY / RECORD, the session map and reference counts,
+// RTPSessionOutput, prefs, teardown -- is the reference module's own code.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "QTSS.h"
+#include "QTSS_Private.h"
+#include "OS.h"
+#include "OSQueue.h"
+#include "OSRef.h"
+#include "ReflectorSession.h"
+#include "ReflectorStream.h"
+#include "QTSServerInterface.h"
+#include "MyAssert.h"
+#include "Socket.h"
+#include "epollEvent.h"
+
+// The server's module tables (no module in any role) and the server object.
+QTSSModule** QTSServerInterface::sModuleArray[QTSSModule::kNumRoles];
+UInt32       QTSServerInterface::sNumModulesInRole[QTSSModule::kNumRoles];
+QTSServerInterface* QTSServerInterface::sServer = NULL;
+
+// fReflectorSessionMap is the one member of the server object the module reads; it (and sServer)
+// is reached through a pointer taken by explicit instantiation (which the language exempts from
+// access checks) -- the server object here is storage with that member set, its constructor
+// (QTSServerInterface.cpp, the whole server) is not run.
+namespace {
+template <typename Tag, typename Tag::type M> struct Steal { friend typename Tag::type get(Tag) { return M; } };
+struct SessionMapMember { typedef OSRefTable* QTSServerInterface::*type; friend type get(SessionMapMember); };
+template struct Steal<SessionMapMember, &QTSServerInterface::fReflectorSessionMap>;
+struct ServerStatic { typedef QTSServerInterface** type; friend type get(ServerStatic); };
+template struct Steal<ServerStatic, &QTSServerInterface::sServer>;
+
+alignas(QTSServerInterface) unsigned char g_server[sizeof(QTSServerInterface)];
+OSRefTable* g_sessions = NULL;
+bool g_callbacks = false;                 // the stub library has the server's callback table
+
+OSRefTable* session_map() {
+    if (g_sessions == NULL) {
+        g_sessions = new OSRefTable();
+        QTSServerInterface* s = reinterpret_cast<QTSServerInterface*>(g_server);
+        s->*get(SessionMapMember()) = g_sessions;
+        *get(ServerStatic()) = s;
+    }
+    return g_sessions;
+}
+
+// the registered sessions, in name order (a deterministic tick order)
+std::vector<ReflectorSession*> live_sessions() {
+    std::vector<std::pair<std::string, ReflectorSession*>> v;
+    for (OSRefHashTableIter it(session_map()->GetHashTable()); !it.IsDone(); it.Next()) {
+        OSRef* ref = it.GetCurrent();
+        if (ref == NULL || ref->GetObject() == NULL) continue;
+        v.push_back(std::make_pair(std::string(ref->GetString()->Ptr, ref->GetString()->Len),
+                                   (ReflectorSession*)ref->GetObject()));
+    }
+    std::sort(v.begin(), v.end(), [](const std::pair<std::string, ReflectorSession*>& a,
+                                     const std::pair<std::string, ReflectorSession*>& b) { return a.first < b.first; });
+    std::vector<ReflectorSession*> out;
+    for (auto& e : v) out.push_back(e.second);
+    return out;
+}
+}  // namespace
+
+// The server's assert logger (the reference's MyAssert writes through a null pointer without
+// one): asserts are counted, and printed with EDTR_SHOW_ASSERTS, as the reference harness does.
+struct HostAssert : public AssertLogger {
+    unsigned long count = 0;
+    void LogAssert(char* m) override { if (getenv("EDTR_SHOW_ASSERTS")) fprintf(stderr, "assert: %s\n", m); ++count; }
+};
+
+// QTSSReflectorModule_Main -> _stublibrary_main: from here on the callbacks are set
+extern "C" QTSS_Error __real__stublibrary_main(void*, QTSS_DispatchFuncPtr);
+extern "C" QTSS_Error __wrap__stublibrary_main(void* args, QTSS_DispatchFuncPtr fn) {
+    static HostAssert logger;
+    SetAssertLogger(&logger);
+    // the server's socket event machinery, set up before modules load (RunServer): the event
+    // thread object the sockets register with and the epoll set; the thread itself is not started --
+    // PollUDP reads the sockets
+    Socket::Initialize();
+    (void)epollInit();
+    (void)session_map();
+    const QTSS_Error e = __real__stublibrary_main(args, fn);
+    g_callbacks = e == QTSS_NoErr;
+    return e;
+}
+
+extern "C" SInt64 __wrap__ZN2OS12MillisecondsEv() { return g_callbacks ? QTSS_Milliseconds() : 0; }
+
+extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
+    OSMutexLocker locker(session_map()->GetMutex());
+    static OSQueue sFree;                 // ReflectPackets only EnQueues freed packets onto it
+    for (ReflectorSession* sess : live_sessions())
+        for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+            ReflectorStream* st = sess->GetStreamByIndex(x);
+            if (st == NULL) continue;
+            SInt64 wake = 0;
+            st->GetRTPSender()->ReflectPackets(&wake, &sFree);
+            wake = 0;
+            st->GetRTCPSender()->ReflectPackets(&wake, &sFree);
+        }
+    return QTSS_NoErr;
+}
+
+extern "C" UInt32 EDGPU_QTSSReflectorModule_PollUDP(void) {
+    OSMutexLocker locker(session_map()->GetMutex());
+    UInt32 n = 0;
+    char buf[65536];
+    for (ReflectorSession* sess : live_sessions())
+        for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+            ReflectorStream* st = sess->GetStreamByIndex(x);
+            UDPSocketPair* pr = st == NULL ? NULL : st->GetSocketPair();
+            if (pr == NULL) continue;
+            for (int k = 0; k < 2; k++) {
+                ReflectorSocket* so = (ReflectorSocket*)(k ? pr->GetSocketB() : pr->GetSocketA());
+                if (so == NULL || so->GetSocketFD() < 0) continue;
+                for (;;) {
+                    sockaddr_in from;
+                    socklen_t fl = sizeof(from);
+                    const ssize_t got = recvfrom(so->GetSocketFD(), buf, sizeof(buf), MSG_DONTWAIT, (sockaddr*)&from, &fl);
+                    if (got <= 0) break;
+                    ReflectorPacket* pk = so->GetPacket();
+                    if (pk == NULL) break;
+                    pk->SetPacketData(buf, std::min<UInt32>((UInt32)got, 2060u));
+                    OSMutexLocker dl(so->GetDemuxer()->GetMutex());
+                    so->ProcessPacket(OS::Milliseconds(), pk, ntohl(from.sin_addr.s_addr), ntohs(from.sin_port));
+                    n++;
+                }
+            }
+        }
+    return n;
+}

@@ -29,11 +29,11 @@ SAME(qtssUnknownPayloadType); SAME(qtssVideoPayloadType); SAME(qtssAudioPayloadT
 SAME(qtssCliSesCloseClientTeardown); SAME(qtssCliSesTearDownBroadcastEnded); SAME(qtssCliTeardownReason);
 SAME(qtssDescribeMethod); SAME(qtssSetupMethod); SAME(qtssTeardownMethod); SAME(qtssPlayMethod);
 SAME(qtssPauseMethod); SAME(qtssOptionsMethod); SAME(qtssAnnounceMethod); SAME(qtssRecordMethod);
-SAME(qtssAttrDataTypeCharArray); SAME(qtssAttrDataTypeSInt32); SAME(qtssAttrDataTypeUInt32);
+SAME(qtssAttrDataTypeCharArray); SAME(qtssAttrDataTypeSInt32); SAME(qtssAttrDataTypeUInt16); SAME(qtssAttrDataTypeUInt32);
 SAME(qtssAttrDataTypeVoidPointer); SAME(qtssAttrDataTypeBool16); SAME(qtssAttrDataTypeUnknown);
 SAME(qtssPrefsObjectType); SAME(qtssModuleObjectType); SAME(qtssAttrInfoObjectType);
 SAME(qtssCliSesOverBufferEnabled); SAME(qtssModPrefs); SAME(qtssAttrName); SAME(qtssAttrID); SAME(qtssAttrDataType);
-SAME(qtssPrefsPlayersReqRTPHeader);
+SAME(qtssPrefsPlayersReqRTPHeader); SAME(qtssPrefsMovieFolder); SAME(qtssRTSPReqRootDir);
 SAME(kAddInstanceAttributeCallback); SAME(kGetAttrInfoByNameCallback); SAME(kGetValueAsStringCallback);
 SAME(qtssRTPStreamObjectType); SAME(qtssClientSessionObjectType); SAME(qtssRTSPSessionObjectType);
 SAME(qtssRTSPRequestObjectType); SAME(qtssTextMessagesObjectType); SAME(qtssModulePrefsObjectType);
@@ -53,6 +53,7 @@ SAME(kWriteCallback); SAME(kAppendRTSPHeadersCallback); SAME(kSendStandardRTSPCa
 SAME(kAddRTPStreamCallback); SAME(kPlayCallback); SAME(kPauseCallback); SAME(kTeardownCallback);
 SAME(kRequestEventCallback); SAME(kSetIdleTimerCallback); SAME(kReadCallback); SAME(kGetNumValuesCallback);
 SAME(kAddStaticAttributeCallback); SAME(kRemoveValueCallback); SAME(kLastCallback);
+SAME(kValueToStringCallback); SAME(kRefreshTimeOutCallback); SAME(kLockObjectCallback); SAME(kUnlockObjectCallback);
 
 static_assert(sizeof(E::QTSS_Error) == sizeof(::QTSS_Error), "QTSS_Error");
 static_assert(sizeof(E::QTSS_Role) == sizeof(::QTSS_Role), "QTSS_Role");

@@ -20,4 +20,6 @@ def oracle_bins():
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(port) or os.path.exists("/root/reference/EasyDarwin"):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    return {"port": port, "ref": ref if os.path.exists(ref) else None}
+    refmod = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
+    return {"port": port, "ref": ref if os.path.exists(ref) else None,
+            "refmod": refmod if os.path.exists(refmod) else None}

@@ -1,0 +1,60 @@
+"""CPU: the REFERENCE QTSSReflectorModule itself, hosted by the fake server.
+
+oracle/_ref/Makefile compiles QTSSReflectorModule.cpp with everything the reflector links, from the
+read-only reference sources, into a loadable QTSS module (libQTSSReflectorModule_ref.so); what the
+server process gives it -- the server object's session map, the socket event set-up, the clock,
+the reflect tick and UDP reads its task threads would run -- is oracle/ref_module_host.cpp.
+tools/qtss_replay, the fake server the GPU drop-in is tested with (tests/test_gpu_qtss_module.py),
+loads it and replays every golden trace through its roles: ANNOUNCE / SETUP / RECORD / PLAY,
+RTSPIncomingData, loopback UDP pushes, ClientSessionClosing, RereadPrefs.
+
+Its captures and transmit times must equal the golden fixtures byte for byte.  The fixtures come
+from oracle/ref_harness, which restates the module's role logic around the same reference runtime;
+so this pins that restatement to the module's own code, and pins the fake server's emulation of
+the server (request attributes, stream dictionaries, callbacks) to what the reference module
+expects of it.  The GPU drop-in, driven by the same fake server, must reproduce the same fixtures,
+so the two modules agree with each other.
+"""
+import hashlib
+import json
+import os
+import subprocess
+
+import pytest
+
+from scenarios import SCENARIOS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
+
+
+def _fix(name):
+    with open(os.path.join(GOLD, name + ".json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def refmod(oracle_bins):
+    if oracle_bins["refmod"] is None:
+        pytest.skip("oracle/_ref/libQTSSReflectorModule_ref.so not built (reference tree absent)")
+    if not os.path.exists(REPLAY):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "easydarwin_amd", "csrc"), REPLAY], check=True)
+    return oracle_bins["refmod"]
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_reference_module_reproduces_fixture(name, refmod, tmp_path):
+    t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
+    t.write_bytes(SCENARIOS[name]().to_bytes())
+    r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert hashlib.sha256(c.read_bytes()).hexdigest() == _fix(name)["capture_sha256"]
+    assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fix(name)["transmit_sha256"]
+
+
+def test_reference_module_registers_its_roles(refmod):
+    r = subprocess.run([REPLAY, refmod, "--register"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip().splitlines()[-1])["module"] == "QTSSReflectorModule"

@@ -215,6 +215,20 @@ static QTSS_Error cb_value_as_string(Obj* o, uint32_t id, uint32_t idx, char** o
     *out = c;
     return QTSS_NoErr;
 }
+// QTSS_ValueToString (QTSSDataConverter::ValueToString): a value's text, for the module's logs
+static QTSS_Error cb_value_to_string(const void* v, uint32_t len, uint32_t type, char** out, ...) {
+    if (!out) return QTSS_BadArgument;
+    std::string t;
+    if (type == qtssAttrDataTypeBool16 && len >= 1) t = *(const uint8_t*)v ? "true" : "false";
+    else if (type == qtssAttrDataTypeUInt32 && len == 4) t = std::to_string(*(const uint32_t*)v);
+    else if (type == qtssAttrDataTypeUInt16 && len == 2) t = std::to_string(*(const uint16_t*)v);
+    else if (type == qtssAttrDataTypeSInt32 && len == 4) t = std::to_string(*(const int32_t*)v);
+    else t.assign((const char*)v, len);
+    char* c = new char[t.size() + 1];
+    memcpy(c, t.c_str(), t.size() + 1);
+    *out = c;
+    return QTSS_NoErr;
+}
 // the trace's prefs into the module's prefs object and the server's (trace_prefs.h: only the
 // overridden module prefs exist; the player list always does, as in the shipped easydarwin.xml)
 static Obj* g_mod_prefs = nullptr;
@@ -231,6 +245,8 @@ static void load_prefs(const trace_prefs::Prefs& p) {
         else set_pod<uint32_t>(g_mod_prefs, id, (uint32_t)strtoul(kv.second.c_str(), nullptr, 10));
     }
     g_srv_prefs->attrs.erase(qtssPrefsPlayersReqRTPHeader);
+    const std::string movies = "./Movies/";             // the shipped easydarwin.xml's movie_folder
+    set_attr(g_srv_prefs, qtssPrefsMovieFolder, 0, movies.data(), (uint32_t)movies.size());
     uint32_t i = 0;
     for (const std::string& v : p.list("player_requires_rtp_header_info"))
         set_attr(g_srv_prefs, qtssPrefsPlayersReqRTPHeader, i++, v.data(), (uint32_t)v.size());
@@ -293,6 +309,10 @@ static QTSS_Error cb_add_rtp_stream(Obj* client, Obj* req, Obj** out, uint32_t, 
     if (it != req->attrs.end() && !it->second.empty()) memcpy(&tt, it->second[0].data(), 4);
     s->tcp = tt == qtssRTPTransportTypeTCP;
     set_pod(s, qtssRTPStrTransportType, tt);
+    // the RTPStream dictionary's own values, 0 until a module sets them (RTPStream.cpp:174-175,
+    // 279-280): RTPSessionOutput::FilterPacket reads the first sequence number of every stream
+    set_pod<int16_t>(s, qtssRTPStrFirstSeqNumber, 0);
+    set_pod<int32_t>(s, qtssRTPStrFirstTimestamp, 0);
     uint32_t& ch = g_next_channel[g_rtsp_of_client[client]];
     s->channel[0] = (uint8_t)ch; s->channel[1] = (uint8_t)(ch + 1);
     ch += 2;
@@ -389,6 +409,14 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     if (outReq) *outReq = req;
     set_pod<uint32_t>(req, qtssRTSPReqMethod, method);
     set_attr(req, qtssRTSPReqFilePath, 0, path.data(), (uint32_t)path.size());
+    // the server's qtssRTSPReqFileName: the path's first component (RTSPRequestInterface::
+    // GetFileName, RTSPRequestInterface.cpp:681-711) -- the reflector's stream name
+    std::string fname = path;
+    if (!fname.empty() && fname[0] == '/') fname.erase(0, 1);
+    if (fname.find('/') != std::string::npos) fname.resize(fname.find('/'));
+    set_attr(req, qtssRTSPReqFileName, 0, fname.data(), (uint32_t)fname.size());
+    // (no qtssRTSPReqRootDir: EasyDarwin's request never sets it, RTSPRequestInterface.cpp:219-224,
+    // so QTSSModuleUtils::GetFullPath yields the file name alone)
     if (!digit.empty()) set_attr(req, qtssRTSPReqFileDigit, 0, digit.data(), (uint32_t)digit.size());
     set_pod<uint32_t>(req, qtssRTSPReqTransportMode, mode);
     set_pod<uint32_t>(req, qtssRTSPReqTransportType, transport);
@@ -431,7 +459,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
     std::vector<Obj*> rtsp(nsess), client(nsess);
     const auto s0 = std::chrono::steady_clock::now();
     for (uint32_t s = 0; s < nsess; s++) {
-        const std::string path = "/live/bench" + std::to_string(s) + ".sdp";
+        const std::string path = "/bench" + std::to_string(s) + ".sdp";      // one component: the stream name
         rtsp[s] = new_obj(qtssRTSPSessionObjectType);
         client[s] = new_obj(qtssClientSessionObjectType);
         g_rtsp_of_client[client[s]] = rtsp[s];
@@ -603,6 +631,10 @@ int main(int argc, char** argv) {
     cbs.addr[kAddInstanceAttributeCallback] = (QTSS_CallbackProcPtr)cb_add_instance_attr;
     cbs.addr[kGetNumValuesCallback] = (QTSS_CallbackProcPtr)cb_num_values;
     cbs.addr[kGetValueAsStringCallback] = (QTSS_CallbackProcPtr)cb_value_as_string;
+    cbs.addr[kValueToStringCallback] = (QTSS_CallbackProcPtr)cb_value_to_string;
+    cbs.addr[kRefreshTimeOutCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kLockObjectCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kUnlockObjectCallback] = (QTSS_CallbackProcPtr)cb_ok;
     QTSS_PrivateArgs args;
     memset(&args, 0, sizeof(args));
     args.inServerAPIVersion = kApiVersion;
@@ -719,7 +751,7 @@ int main(int argc, char** argv) {
         r.p += n;
         flags[s] = ver >= 2 ? r.get<uint8_t>() : 0;
         for (size_t k = sdps[s].find("m="); k != std::string::npos; k = sdps[s].find("\nm=", k + 1)) ntracks[s]++;
-        paths[s] = "/live/stream" + std::to_string(s) + ".sdp";
+        paths[s] = "/stream" + std::to_string(s) + ".sdp";    // one component: the stream name
         if (!publish(s)) { fprintf(stderr, "push SETUP failed\n"); return 3; }
     }
     if (ver >= 4) { const uint32_t l = r.get<uint32_t>(); r.p += l; }   // the prefs (read before Initialize)
@@ -838,7 +870,7 @@ int main(int argc, char** argv) {
             auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleTearDownClients");
             if (it == g_attr_ids.end()) { fprintf(stderr, "kill-clients attribute not registered\n"); return 3; }
             // the event's kill flag is the attribute set at RECORD (the module sets it from its pref)
-            if (kill) { const uint16_t k16 = kill; set_attr(push_client[s], it->second, 0, &k16, sizeof(k16)); }
+            if (kill) { const bool k = true; set_attr(push_client[s], it->second, 0, &k, sizeof(k)); }   // a bool, as the module writes it
             close_client(push_client[s]);
             push_rtsp[s] = push_client[s] = nullptr;
             // the server closes the client sessions the module tore down (QTSS_Teardown)
