@@ -33,6 +33,8 @@
 #include <sys/socket.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -122,18 +124,61 @@ extern "C" QTSS_Error __wrap__stublibrary_main(void* args, QTSS_DispatchFuncPtr 
 
 extern "C" SInt64 __wrap__ZN2OS12MillisecondsEv() { return g_callbacks ? QTSS_Milliseconds() : 0; }
 
+// EDGPU_QTSSReflectorModule_LastTick's block (include/qtss_module_abi.h EDGPU_QTSSTickInfo, same
+// layout): for the fake server's --bench mode, the tick count and each tick's wall time, all of which
+// is spent holding the session map's mutex
+struct TickInfo {
+    uint64_t ingested_packets, ingested_bytes, readback_bytes, arena_bytes, writes;
+    double ingest_ms, fanout_ms, readback_ms, write_ms, hold_ms;
+    uint64_t ticks, failed_ticks;
+    int64_t last_error;
+    uint64_t prestaged_bytes, passes, rereads;
+};
+static TickInfo g_tick;
+extern "C" QTSS_Error EDGPU_QTSSReflectorModule_LastTick(TickInfo* out) {
+    *out = g_tick;
+    return QTSS_NoErr;
+}
+
 extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
-    OSMutexLocker locker(session_map()->GetMutex());
-    static OSQueue sFree;                 // ReflectPackets only EnQueues freed packets onto it
-    for (ReflectorSession* sess : live_sessions())
-        for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
-            ReflectorStream* st = sess->GetStreamByIndex(x);
-            if (st == NULL) continue;
-            SInt64 wake = 0;
-            st->GetRTPSender()->ReflectPackets(&wake, &sFree);
-            wake = 0;
-            st->GetRTCPSender()->ReflectPackets(&wake, &sFree);
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Done {
+        std::chrono::steady_clock::time_point t0;
+        ~Done() {
+            g_tick.ticks++;
+            g_tick.passes = 1;
+            g_tick.hold_ms = g_tick.write_ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         }
+    } done{t0};
+    OSMutexLocker locker(session_map()->GetMutex());
+    // EDGPU_REF_TICK_THREADS=N (default 1): the sessions' senders reflect on N threads, as the
+    // server's task threads run the ReflectorSocket tasks (one socket's senders on one thread at a
+    // time, ReflectorStream.cpp:1676-1714); each thread frees packets onto its own queue
+    static const unsigned nthreads = getenv("EDGPU_REF_TICK_THREADS") ? (unsigned)atoi(getenv("EDGPU_REF_TICK_THREADS")) : 1;
+    static std::vector<OSQueue> sFree(std::max(1u, nthreads));   // ReflectPackets only EnQueues onto it
+    const std::vector<ReflectorSession*> sessions = live_sessions();
+    auto reflect = [&](unsigned w, unsigned nw) {
+        for (size_t k = w; k < sessions.size(); k += nw) {
+            ReflectorSession* sess = sessions[k];
+            for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+                ReflectorStream* st = sess->GetStreamByIndex(x);
+                if (st == NULL) continue;
+                SInt64 wake = 0;
+                st->GetRTPSender()->ReflectPackets(&wake, &sFree[w]);
+                wake = 0;
+                st->GetRTCPSender()->ReflectPackets(&wake, &sFree[w]);
+            }
+        }
+    };
+    if (nthreads <= 1) {
+        reflect(0, 1);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned w = 1; w < nthreads; w++) th.emplace_back(reflect, w, nthreads);
+        reflect(0, nthreads);
+        for (std::thread& t : th) t.join();
+    }
     return QTSS_NoErr;
 }
 

@@ -60,6 +60,31 @@ def test_module_matches_reference(name, gather, tmp_path):
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]
 
 
+REF_MODULE = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["repush", "rtpinfo", "leave", "threaded", "udppush", "prefs_reread", "backpressure"])
+def test_module_equals_reference_module(name, tmp_path):
+    """The drop-in and the REFERENCE QTSSReflectorModule (compiled from its own sources,
+    oracle/_ref/Makefile; tests/test_ref_module.py) driven by the same fake server through the same
+    roles: equal QTSS_Write streams and transmit times (QTSSReflectorModule.cpp:604-678,
+    1379-1545, 1597-2023, 2070-2196)."""
+    if not os.path.exists(REF_MODULE):
+        pytest.skip("oracle/_ref/libQTSSReflectorModule_ref.so not built")
+    t = tmp_path / "t.edtr"
+    t.write_bytes(_trace(name).to_bytes())
+    out = {}
+    for tag, so in (("gpu", MODULE), ("ref", REF_MODULE)):
+        c, tt = tmp_path / f"{tag}.edcp", tmp_path / f"{tag}.edtt"
+        r = subprocess.run([REPLAY, so, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+        assert r.returncode == 0, (tag, r.stderr[-2000:])
+        out[tag] = (c.read_bytes(), tt.read_bytes())
+    assert out["gpu"][0] == out["ref"][0]
+    assert out["gpu"][1] == out["ref"][1]
+
+
 @pytest.mark.gpu
 def test_module_threaded_default_mode_matches_reference(tmp_path):
     """Tick thread + UDP reader thread + two pusher threads: the per-sub-stream bytes (tick
