@@ -195,6 +195,10 @@ struct edgpu_ctx {
     std::vector<void*> snd_meta, snd_ring;   // per sender: its rings (null once its session is removed)
     std::vector<uint32_t> dead_sessions;     // removed session ids, reused by edgpu_session_add
     std::map<uint32_t, std::vector<uint32_t>> free_subs;   // SubDev ranges of removed subscribers, by size
+    // ranges freed since the last edgpu_fanout: their rows still hold that tick's plan (its later
+    // copy passes and backpressure reports read them), so they are reused only from the next tick
+    std::vector<std::pair<uint32_t, uint32_t>> free_pending;   // (size, first row)
+    uint32_t tick_nsubs = 0;                     // sub-stream rows of the last edgpu_fanout's table
     uint64_t work_cap_needed = 0;
     void* d_null = nullptr;                  // zeroed 4 KiB: the rings of a removed session's senders
 
@@ -295,6 +299,17 @@ static int owed_pass(const edgpu_ctx* x, const char* what) {
         return fail(EDGPU_ERR, std::string(what) + ": the last fan-out tick has a copy pass not yet delivered "
                                                    "(edgpu_fanout_next)");
     return EDGPU_OK;
+}
+static int read_totals(edgpu_ctx* x, TickTotals* t);
+// The same for calls that free what a later copy pass reads (a session's rings and rows): when the
+// host has not read the last tick's stats yet, whether a pass is owed is read from the device.
+static int owed_pass_known(edgpu_ctx* x, const char* what) {
+    if (x->passes_more == -1 && x->fanout_launches) {
+        TickTotals t;
+        if (int r = read_totals(x, &t)) return r;
+        x->passes_more = t.pass_next[x->pass_ord & 1u] != kNoPass ? 1 : 0;
+    }
+    return owed_pass(x, what);
 }
 
 extern "C" {
@@ -488,6 +503,16 @@ struct Readback {
         return hipSuccess;
     }
 };
+
+// The tick totals, after every stream of the context has drained.
+static int read_totals(edgpu_ctx* x, TickTotals* t) {
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(sync_all(x));
+    Readback rb(x);
+    HIP_CHECK(rb.add(t, x->d_totals, sizeof(*t)));
+    HIP_CHECK(rb.run());
+    return EDGPU_OK;
+}
 
 int edgpu_sync(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
@@ -686,7 +711,7 @@ static int detach_subscriber(edgpu_ctx* x, uint32_t handle) {
     SessionHost& sh = x->sessions[s.session];
     sh.eyes--;                                   // RemoveOutput(..., isClient) -> DecEyeCount
     sh.subs.erase(std::find(sh.subs.begin(), sh.subs.end(), handle));
-    x->free_subs[s.nsub].push_back(s.first_sub);
+    x->free_pending.emplace_back(s.nsub, s.first_sub);
     x->index_dirty = true;
     return EDGPU_OK;
 }
@@ -695,7 +720,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (flags & ~EDGPU_SESSION_KILL_OUTPUTS) return fail(EDGPU_BAD_ARGUMENT, "bad flags");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    if (int r = owed_pass(x, "edgpu_session_remove")) return r;
+    if (int r = owed_pass_known(x, "edgpu_session_remove")) return r;
     SessionHost& sh = x->sessions[session];
     if (!sh.subs.empty() && !(flags & EDGPU_SESSION_KILL_OUTPUTS))
         return fail(EDGPU_ERR, "session still has outputs (the reference keeps a ReflectorSession while outputs "
@@ -1261,6 +1286,8 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
                  const uint32_t* seg_sess, uint32_t nseg, const uint8_t* blob, uint64_t blob_bytes, int where) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    // (a pass the host has not learnt of yet is guarded on the device: k_ingest checks the batch
+    // against the tick's window while one is owed)
     const int owed = owed_pass(x, "edgpu_ingest");
     if (owed || n > x->cfg.max_batch_packets || nseg > x->cfg.max_batch_packets ||
         (where != EDGPU_PTR_DEVICE && blob_bytes > x->cfg.max_batch_bytes)) {
@@ -1424,7 +1451,7 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n)
     if (!n) return EDGPU_OK;
     if (x->fanout_launches == 0) return fail(EDGPU_ERR, "no fan-out tick to report on");
     if (x->pending) return fail(EDGPU_ERR, "backpressure reports must precede the next edgpu_ingest");
-    const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    const uint32_t nsub = x->tick_nsubs;             // rows of the tick reported on
     for (uint32_t i = 0; i < n; i++)
         if (reports[i].substream >= nsub) return fail(EDGPU_BAD_ARGUMENT, "bad sub-stream index");
     HIP_CHECK(hipSetDevice(x->device));
@@ -1481,7 +1508,7 @@ static int pick_fanout_variant(const edgpu_ctx* x) {
 
 // The plan parameters of the context's current tick (arena / descriptor buffers of x->cur).
 static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
-    const uint32_t nsub = (uint32_t)x->sub_sender.size();
+    const uint32_t nsub = x->tick_nsubs;            // rows added since are not the tick's
     PlanParams p;
     p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
     p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
@@ -1529,7 +1556,7 @@ static int launch_copy_pass(edgpu_ctx* x, edgpu_fanout_result* out) {
         out->arena = f.arena;
         out->desc = f.desc;
         out->substreams = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
-        out->n_substreams = (uint32_t)x->sub_sender.size();
+        out->n_substreams = x->tick_nsubs;
     }
     return EDGPU_OK;
 }
@@ -1546,7 +1573,11 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
         HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
         x->cur ^= 1;
     }
+    // rows freed during the last tick may be reused from now on (its passes are delivered)
+    for (const auto& f : x->free_pending) x->free_subs[f.first].push_back(f.second);
+    x->free_pending.clear();
     if (x->index_dirty) { int r = rebuild_index(x); if (r) return r; }
+    x->tick_nsubs = (uint32_t)x->sub_sender.size();     // this tick's table: later passes keep it
     x->last_now = now_ms;
     queue_source_reports(x, now_ms);
     x->tick_variant = pick_fanout_variant(x);
@@ -1655,7 +1686,7 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
         HIP_CHECK(x->d_arrivals.reserve(npass, x->stream));
         dst = x->d_arrivals.ptr;
     }
-    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, (uint32_t)x->sub_sender.size(), x->pass_id, dst,
+    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, x->tick_nsubs, x->pass_id, dst,
                                   x->stream));
     Readback rb(x);
     if (kind == EDGPU_PTR_HOST) HIP_CHECK(rb.add(out, dst, (size_t)npass * sizeof(int64_t)));

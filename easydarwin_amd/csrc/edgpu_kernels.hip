@@ -659,10 +659,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         SenderDev& D = P.senders[S.first_sender + tid];
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
-        // tick pipelining: this batch must not lap what the previous tick's fan-out (possibly
-        // still running on the other stream) reads
-        if (P.overlap && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
-                          s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
+        // tick pipelining, or a copy pass the last tick still owes (edgpu_fanout_next): this batch
+        // must not lap what that tick's fan-out (possibly still running on the other stream) reads
+        const bool guard = P.overlap || P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
+        if (guard && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
+                      s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
             atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);
     }
     if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];

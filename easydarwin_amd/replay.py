@@ -383,6 +383,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         def release_check(s):
             """A session without pusher or outputs dies (RemoveOutput's refcount-0 branch)."""
             if gen[s] is not None and not published[s] and not outputs_of(s):
+                drain()                     # (overlap_ticks: a session goes only after its last tick is read)
                 ctx.session_remove(gen[s])
                 gen[s] = None
 
@@ -421,6 +422,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                         for h in outputs_of(s):
                             gone.add(h)
                         if gen[s] is not None:
+                            drain()
                             ctx.session_remove(gen[s], kill_outputs=True)
                             gen[s] = None
                     release_check(s)

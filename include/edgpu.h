@@ -393,11 +393,16 @@ int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
  * the pass's arena and descriptors.  After consuming a pass the host calls edgpu_fanout_next:
  * *launched = 1 when it launched the next pass (`out` as above), 0 when the tick is complete.
  * edgpu_tick_stats_get reports the current pass (pass_arena_bytes, pass_packets, more_passes).
- * Every pass of a tick must be consumed before the next edgpu_ingest / edgpu_ingest_interleaved
- * / edgpu_fanout / edgpu_session_remove: those fail with EDGPU_ERR while the context knows of an
- * outstanding pass (edgpu_counters.lost_passes counts passes a tick still owed when the next
- * tick was planned).  Backpressure reports (edgpu_fanout_blocked) take tick-wide sub-stream rows
- * and may follow any pass.  A tick fits one pass whenever its bytes and descriptors do; a single
+ * Every pass of a tick must be consumed before the next edgpu_fanout and edgpu_session_remove:
+ * those fail with EDGPU_ERR while a pass is owed (session removal reads that from the device when
+ * the host has not read the tick's stats; edgpu_counters.lost_passes counts passes a tick still
+ * owed when the next tick was planned).  edgpu_ingest / edgpu_ingest_interleaved fail the same
+ * way while the host knows of an owed pass; before it has read the stats an ingest may run (the
+ * overlap_ticks pattern), and a batch that would lap the tick's window in a ring while a pass is
+ * owed fails the ring (EDGPU_RING_OVERFLOW) instead of corrupting the pass.  Subscribers may come and go between passes: the passes keep the tick's table (rows
+ * added since are not in it, rows of removed subscribers still deliver the tick, and their rows
+ * are reused only from the next tick).  Backpressure reports (edgpu_fanout_blocked) take
+ * tick-wide sub-stream rows and may follow any pass.  A tick fits one pass whenever its bytes and descriptors do; a single
  * sub-stream larger than the arena (out_arena_bytes below a sender ring) still fails the tick
  * with EDGPU_OUT_OVERFLOW. */
 int  edgpu_fanout_next(edgpu_ctx* ctx, edgpu_fanout_result* out, uint32_t* launched);
