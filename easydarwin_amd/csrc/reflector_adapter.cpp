@@ -28,9 +28,9 @@ Reflector::Reflector(const edgpu_config* cfg) {
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;      // 0: the engine's default (edgpu_ctx_create)
     for (Batch& b : fBatch) {
         b.nslabs = c.max_batch_bytes / kSlab + 1;
-        b.slabPend.reset(new std::atomic<uint32_t>[b.nslabs]);
+        b.slabPend.reset(new Batch::Pend[b.nslabs]);
         b.slabSealed.reset(new std::atomic<uint8_t>[b.nslabs]);
-        for (uint64_t i = 0; i < b.nslabs; i++) { b.slabPend[i].store(0); b.slabSealed[i].store(0); }
+        for (uint64_t i = 0; i < b.nslabs; i++) { b.slabPend[i].n.store(0); b.slabSealed[i].store(0); }
     }
     if (fPrestageBytes) {
         fStageArmed = fFill;
@@ -128,7 +128,7 @@ void Reflector::StagerLoop() {
         const uint64_t lim = std::min<uint64_t>(__atomic_load_n(&b.next, __ATOMIC_ACQUIRE) / kSlab, b.nslabs);
         uint64_t e = b.staged;
         while (e < lim && b.slabSealed[e].load(std::memory_order_acquire) &&
-               b.slabPend[e].load(std::memory_order_acquire) == 0)
+               b.slabPend[e].n.load(std::memory_order_acquire) == 0)
             e++;
         if ((e - b.staged) * kSlab < fPrestageBytes) continue;
         if (edgpu_ingest_prestage(fCtx, b.blob, b.staged * kSlab, (e - b.staged) * kSlab) != 0) {
@@ -225,7 +225,7 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
         }
         d = b.blob + st.slab + st.used;
         if (st.slab / kSlab < b.nslabs) {
-            pend = &b.slabPend[st.slab / kSlab];
+            pend = &b.slabPend[st.slab / kSlab].n;
             pend->fetch_add(1, std::memory_order_relaxed);
         }
         st.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, st.slab + st.used, packetLen});

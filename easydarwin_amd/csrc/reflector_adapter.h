@@ -197,7 +197,8 @@ private:
         // copies still in flight and whether its stripe has moved on to another slab.  A sealed
         // slab with none in flight is final; the stager thread copies the prefix of final slabs
         // ahead, and the flush copies only the rest.
-        std::unique_ptr<std::atomic<uint32_t>[]> slabPend;
+        struct alignas(64) Pend { std::atomic<uint32_t> n{0}; };   // own line: pushers of different
+        std::unique_ptr<Pend[]> slabPend;                   // stripes count on neighbouring slabs
         std::unique_ptr<std::atomic<uint8_t>[]> slabSealed;
         uint64_t nslabs = 0;                                // slabs tracked (max_batch_bytes / kSlab)
         uint64_t staged = 0;                                // slabs copied ahead (under fStageMu)

@@ -9,6 +9,10 @@ sink counts.  Reported: relayed packets/s over push + tick wall time, per-tick m
 hold, engine ingest / fan-out / readback / QTSS_Write time, readback (PCIe) bytes per tick
 against the fan-out arena bytes per tick (what a whole-arena readback would move).
 
+Reference module: the REFERENCE QTSSReflectorModule (oracle/_ref/libQTSSReflectorModule_ref.so) in
+the same fake server at the same load and tick, its senders reflected on as many threads as the
+drop-in has write threads -- the like-for-like comparison (module_vs_reference_module).
+
 Reference side: oracle/_ref/ref_harness --bench (EasyDarwin's reflector compiled from its
 sources, memcpy sinks) on bench.py's bounded sample (64 sessions x <subs> x 3 s at the same
 tick), sessions sharded over one process per core (bench.py _reference_replay).
@@ -38,6 +42,27 @@ def module_run(args) -> dict:
     if r.returncode:
         raise SystemExit(f"qtss_replay --bench failed ({r.returncode}): {r.stderr.strip()[-400:]}")
     return json.loads(r.stdout)
+
+
+def reference_module_run(args) -> dict | None:
+    """The REFERENCE QTSSReflectorModule (oracle/_ref/libQTSSReflectorModule_ref.so, compiled from its
+    sources) in the same fake server, same load, same pusher threads; its senders reflect on as many
+    threads as the drop-in has write threads (EDGPU_REF_TICK_THREADS: the server's task threads)."""
+    so = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
+    if not os.path.exists(so):
+        return None
+    env = dict(os.environ, EDGPU_REF_TICK_THREADS=str(int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads))))
+    if args.concurrent_push:
+        env["EDGPU_BENCH_CONCURRENT_PUSH"] = "1"
+    cmd = [os.path.join(ROOT, "tools", "qtss_replay"), so, "--bench", str(args.sessions), str(args.subs),
+           str(args.seconds), str(args.tick_ms), str(args.threads)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
+    if r.returncode:
+        raise SystemExit(f"qtss_replay --bench (reference module) failed ({r.returncode}): {r.stderr.strip()[-400:]}")
+    line = [ln for ln in r.stdout.splitlines() if '"relayed_per_s"' in ln][-1]   # (the module prints debug lines)
+    d = json.loads(line)
+    d["reflect_threads"] = int(env["EDGPU_REF_TICK_THREADS"])
+    return d
 
 
 def reference_run(args) -> dict | None:
@@ -79,6 +104,9 @@ def main():
     pt = m["per_tick_bytes"]
     out["readback_vs_arena"] = round(pt["readback"] / pt["arena"], 4) if pt["arena"] else None
     if not args.no_reference:
+        out["reference_module"] = reference_module_run(args)
+        if out["reference_module"]:
+            out["module_vs_reference_module"] = round(m["relayed_per_s"] / out["reference_module"]["relayed_per_s"], 2)
         out["reference"] = reference_run(args)
         if out["reference"]:
             out["module_vs_reference"] = round(m["relayed_per_s"] / out["reference"]["relayed_per_s"], 2)
