@@ -110,6 +110,7 @@ struct SourceHost {
 struct SessionHost {
     uint32_t first_sender, ntracks, first_stream;
     bool udp_push;
+    uint32_t span = 0;              // tracks' worth of rows it holds (>= ntracks after a reuse)
     uint32_t eyes = 0;              // client outputs (ReflectorStream::fEyeCount, every track)
     std::vector<SourceHost> src;    // per track
     bool alive = true;              // false after edgpu_session_remove (its id may be reused)
@@ -136,6 +137,7 @@ struct SubscriberHost {
     uint32_t nsub;
     bool active;
     int transport;
+    uint32_t span;              // SubDev rows it holds (>= nsub in a larger free range)
 };
 
 struct edgpu_ctx {
@@ -606,20 +608,29 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
     std::vector<TrackHost> tracks = parse_sdp(sdp, sdp_len);
     if (tracks.empty() || tracks.size() > kMaxTracks)
         return fail(EDGPU_BAD_ARGUMENT, "SDP must describe 1..16 tracks");
-    // a removed session with as many tracks gives its id and table rows (senders, streams)
+    // a removed session whose rows fit gives its id and table rows (senders, streams): the
+    // smallest such, so the tables stay as large as the most sessions / tracks live at once under
+    // churn with mixed track counts (rows it does not use stay dead senders)
     uint32_t sid = (uint32_t)x->sessions.size();
     bool reuse = false;
-    for (size_t k = 0; k < x->dead_sessions.size(); k++)
-        if (x->sessions[x->dead_sessions[k]].ntracks == tracks.size()) {
-            sid = x->dead_sessions[k];
-            x->dead_sessions.erase(x->dead_sessions.begin() + (long)k);
-            reuse = true;
-            break;
-        }
+    size_t best = x->dead_sessions.size();
+    for (size_t k = 0; k < x->dead_sessions.size(); k++) {
+        const uint32_t sp = x->sessions[x->dead_sessions[k]].span;
+        if (sp >= tracks.size() && (best == x->dead_sessions.size() || sp < x->sessions[x->dead_sessions[best]].span))
+            best = k;
+    }
+    uint32_t span = (uint32_t)tracks.size();
+    if (best < x->dead_sessions.size()) {
+        sid = x->dead_sessions[best];
+        span = x->sessions[sid].span;
+        x->dead_sessions.erase(x->dead_sessions.begin() + (long)best);
+        reuse = true;
+    }
     const uint32_t ntracks = (uint32_t)tracks.size();
     const uint32_t first_sender = reuse ? x->sessions[sid].first_sender : x->nsenders;
     const uint32_t first_stream = reuse ? x->sessions[sid].first_stream : x->nstreams;
     SessionHost sh{first_sender, ntracks, first_stream, udp_push != 0};
+    sh.span = span;
     // receiver-report identity, as the ReflectorStream constructor draws it (:164-201)
     const int64_t wall_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
         std::chrono::system_clock::now().time_since_epoch()).count();
@@ -711,7 +722,7 @@ static int detach_subscriber(edgpu_ctx* x, uint32_t handle) {
     SessionHost& sh = x->sessions[s.session];
     sh.eyes--;                                   // RemoveOutput(..., isClient) -> DecEyeCount
     sh.subs.erase(std::find(sh.subs.begin(), sh.subs.end(), handle));
-    x->free_pending.emplace_back(s.nsub, s.first_sub);
+    x->free_pending.emplace_back(s.span, s.first_sub);
     x->index_dirty = true;
     return EDGPU_OK;
 }
@@ -792,10 +803,12 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
     SessionHost& sh = x->sessions[session];
     const uint32_t handle = (uint32_t)x->subscribers.size();
     const uint32_t nsub = 2 * sh.ntracks;
-    uint32_t first = (uint32_t)x->sub_sender.size();
-    auto fr = x->free_subs.find(nsub);
-    if (fr != x->free_subs.end() && !fr->second.empty()) {
+    uint32_t first = (uint32_t)x->sub_sender.size(), span = nsub;
+    auto fr = x->free_subs.lower_bound(nsub);      // the smallest free range that fits
+    while (fr != x->free_subs.end() && fr->second.empty()) ++fr;
+    if (fr != x->free_subs.end()) {
         first = fr->second.back();
+        span = fr->first;                          // rows past nsub stay inactive
         fr->second.pop_back();
     } else {
         x->sub_sender.resize(first + nsub, 0);
@@ -822,7 +835,7 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             x->sub_rw[q] = 0;
             v.emplace_back(q, Q);
         }
-    x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport});
+    x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport, span});
     if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += nsub;
     sh.eyes++;                                   // AddOutput(..., isClient) -> IncEyeCount
     sh.subs.push_back(handle);
@@ -1736,6 +1749,8 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     out->ingested_bytes = t.cum_ingested_bytes;
     out->fanout_passes = x->fanout_passes;
     out->lost_passes = t.cum_lost_passes;
+    out->senders = x->nsenders;
+    out->substream_rows = (uint32_t)x->sub_sender.size();
     return EDGPU_OK;
 }
 

@@ -837,8 +837,14 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
                 u.engine = s->engine;
                 u.track = (uint32_t)t;
                 std::lock_guard<std::mutex> ug(M->udpMu);
-                M->udp.push_back(u);
-                s->pair[t] = (int)M->udp.size() - 1;
+                // a slot an ended session left (both sockets closed) is reused: the table and the
+                // reader's poll set stay as large as the live UDP tracks under churn
+                int slot = -1;
+                for (size_t i = 0; i < M->udp.size() && slot < 0; i++)
+                    if (M->udp[i].fd[0] < 0 && M->udp[i].fd[1] < 0) slot = (int)i;
+                if (slot < 0) { M->udp.push_back(u); slot = (int)M->udp.size() - 1; }
+                else M->udp[slot] = u;
+                s->pair[t] = slot;
             }
             const uint16_t port = M->udp[s->pair[t]].port;
             (void)SetValue(p->inRTSPRequest, qtssRTSPReqSetUpServerPort, 0, &port, sizeof(port));

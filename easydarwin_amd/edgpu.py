@@ -119,7 +119,8 @@ class Counters(C.Structure):
     _fields_ = [("relayed_packets", C.c_uint64), ("relayed_bytes", C.c_uint64),
                 ("fanout_in_bytes", C.c_uint64), ("fanout_launches", C.c_uint64),
                 ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64),
-                ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64)]
+                ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64),
+                ("senders", C.c_uint32), ("substream_rows", C.c_uint32)]
 
 
 # numpy mirrors (same layout as the C structs)

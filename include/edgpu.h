@@ -572,6 +572,8 @@ typedef struct edgpu_counters {
     uint64_t ingested_bytes;
     uint64_t fanout_passes;     /* copy passes launched (> fanout_launches: over-capacity ticks) */
     uint64_t lost_passes;       /* passes a tick still owed when the next tick was planned */
+    uint32_t senders;           /* sender rows (2 per track) and sub-stream rows of the tables: */
+    uint32_t substream_rows;    /* removed sessions' / subscribers' rows are reused, best fit */
 } edgpu_counters;
 int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 

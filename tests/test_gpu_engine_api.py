@@ -256,3 +256,32 @@ def test_fanout_kernel_follows_patching_substreams():
         tick(patching, 5)
         ctx.subscriber_rewrite(u, 0)         # identity again
         tick(plain, 5)
+
+
+@pytest.mark.gpu
+def test_churn_keeps_the_tables_bounded():
+    """Sessions of mixed track counts and their subscribers come and go: a removed session's
+    sender rows and a removed subscriber's sub-stream rows are reused, best fit, by any later one
+    that fits, so the tables stay at the size of the most that were live at once."""
+    def sdp(n):
+        return "v=0\r\n" + "".join(f"m=video 0 RTP/AVP 96\r\na=rtpmap:96 H264/90000\r\na=control:trackID={i + 1}\r\n"
+                                   for i in range(n))
+    sizes = []
+    with edgpu.Context() as ctx:
+        for cycle in range(6):
+            live = []
+            for n in ((3, 1, 2) if cycle % 2 == 0 else (2, 2, 1)):
+                s = ctx.session_add(sdp(n))
+                live.append((s, [ctx.subscriber_add(s, edgpu.TRANSPORT_UDP) for _ in range(2)]))
+            ctx.fanout(1000 * cycle)
+            ctx.stats()
+            for s, subs in live:
+                for h in subs:
+                    ctx.subscriber_remove(h)
+                ctx.session_remove(s)
+            ctx.fanout(1000 * cycle + 500)         # freed sub-stream rows are reusable from this tick
+            ctx.stats()
+            c = ctx.counters()
+            sizes.append((c["senders"], c["substream_rows"]))
+    # 6 tracks live at most: 12 senders; 2 subscribers x 2 sub-streams per track: 24 rows
+    assert sizes == [(12, 24)] * 6
