@@ -280,10 +280,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 unread = None
             if unread is not None:
                 c, r, tt, budgets = unread
-                reports, big = [], [0, 0]
+                reports, big = [], [0, 0, 0]
 
                 def consume(st, subs, desc, arena):
                     reports.extend(_wire_images(subs, desc, arena, images, budgets))
+                    big[2] = max(big[2], int(st.relayed_packets))     # the tick's planned packets
                     if len(subs):
                         big[0] = max(big[0], int(subs["out_bytes"].max()))
                         big[1] = max(big[1], int(subs["desc_count"].max()))
@@ -293,7 +294,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     c.fanout_blocked(reports)
                 st = c.stats()
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
-                tick_info.append((npass, big[0], big[1], int(st.arena_bytes), int(st.relayed_packets)))
+                # (relayed_packets before the backpressure reports take the unsent ones off)
+                tick_info.append((npass, big[0], big[1], int(st.arena_bytes), big[2]))
                 unread = None
 
         pin_sets = [{}, {}]                 # pinned host batch buffers, used alternately
