@@ -95,6 +95,7 @@
 #include "ReflectorSession.h"
 #include "ReflectorStream.h"
 #include "RTPSessionOutput.h"
+#include "RTPOverbufferWindow.h"
 #include "QTSServerInterface.h"
 #include "QTSSModuleUtils.h"
 #include "OSRef.h"
@@ -149,6 +150,15 @@ struct FakeObj {
     UInt64 npk[2] = {0, 0};
     SInt64 budget[2] = {-1, -1}; // writes the socket accepts this tick (-1: unlimited)
     std::vector<SInt64> tt[2];   // QTSS_PacketStruct.packetTransmitTime of each accepted write
+    // EDTR_SERVER_GATE: the server's RTPStream::Write gate (below)
+    FakeObj* client = nullptr;   // the stream's client session
+    bool video = false;          // qtssRTPStrPayloadType is video (the SDP's m= media)
+    SInt64 last_delay = 0;       // RTPStream::fLastCurrentPacketDelay
+    UInt64 stale_dropped = 0;    // fStalePacketsDropped
+    // the client session's RTPSession part (on the client object)
+    RTPOverbufferWindow* window = nullptr;
+    SInt64 play_time = 0, last_check = 0, last_check_media = 0;
+    bool started_thinning = false;
 };
 static std::vector<std::unique_ptr<FakeObj>> g_objs;
 static FakeObj* new_obj() { g_objs.emplace_back(new FakeObj()); return g_objs.back().get(); }
@@ -326,11 +336,64 @@ static UInt64 g_bench_pkts = 0, g_bench_bytes = 0;
 static char g_scratch[70000];
 static int g_udp_fd = -1;                      // --bench-udp: the subscribers' UDP socket
 static sockaddr_in g_udp_dst;                  // an unread loopback socket (drops when full)
+//
+// EDTR_SERVER_GATE=1: QTSS_Write also applies what the server's RTPStream::Write does before its
+// socket write (Server.tproj/RTPStream.cpp:1048-1147) -- Q20, for the engine's own egress
+// (edgpu_egress pacing): the session's over-buffer window, the REFERENCE's RTPOverbufferWindow
+// (RTPOverbufferWindow.cpp, compiled in) built as RTPSessionInterface builds it (send_interval
+// 50 ms, window kUInt32_Max, max_send_ahead_time 25 s, overbuffer_rate 2.0: RTPSessionInterface.cpp:
+// 131, QTSServerPrefs.cpp:132-160) with overbuffering off -- DoSetup turns it off for every
+// player without a dynamic-rate header (QTSSReflectorModule.cpp:1772-1777), which is every player
+// here -- gates RTP and (overbuffering off) RTCP writes: a packet whose transmit time is past
+// now + the send interval waits (QTSS_WouldBlock); then RTP packets of TCP non-video streams go
+// through RTPStream::UpdateQualityLevel (:936-1045) with SetThinningParams' defaults (:897-918:
+// late tolerance 1.5 s -> no adjustment; drop_all_packets_delay 2500, thin_all_the_way 1500,
+// start_thinning 0, start_thicking 250 ms, QTSServerPrefs.cpp:110-148), restated below: with the
+// reflector's two quality levels (ReflectorSession.h:152-154) only its stale-packet drop can
+// change what is written.  A dropped packet is written nowhere but counts as written.  Only then
+// does the socket budget apply, and an accepted RTP write enters the window (:1208-1213).
+static bool g_gate = false;
+static bool update_quality_level(FakeObj* st, FakeObj* cs, SInt64 tt, SInt64 delay, SInt64 now) {
+    if (tt <= cs->play_time) return true;
+    if (st->video) return true;                            // no thinning for video (:946-951)
+    if (st->transport != qtssRTPTransportTypeTCP) return true;
+    if (cs->last_check == 0) {
+        cs->last_check = now; cs->last_check_media = tt; st->last_delay = delay;
+        return true;
+    }
+    if (!cs->started_thinning) {
+        if (delay > 0 && delay - st->last_delay < 250) {   // fStartThinningDelay 0
+            if (delay < st->last_delay) st->last_delay = delay;
+            return true;
+        }
+        cs->started_thinning = true;
+    }
+    if (cs->last_check == 0 || delay > 1500) {             // fThinAllTheWayDelay
+        cs->last_check = now; cs->last_check_media = tt; st->last_delay = delay;
+        if (delay > 1500 && delay > 2500) {                // SetMinQuality; fDropAllPacketsForThisStreamDelay
+            st->stale_dropped++;
+            return false;
+        }
+    }
+    return true;                                           // two quality levels: nothing else drops
+}
+
 static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* outLen, UInt32 flags, ...) {
     FakeObj* s = (FakeObj*)stream;
     const QTSS_PacketStruct* pkt = (const QTSS_PacketStruct*)buf;
     int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (len == 0) return QTSS_NoErr;
+    if (g_gate && s->client) {
+        FakeObj* cs = s->client;
+        const SInt64 now = g_now;
+        const SInt64 delay = now - pkt->packetTransmitTime;
+        // overbuffering is off: RTCP is gated too (:1085-1096)
+        if (cs->window->CheckTransmitTime(pkt->packetTransmitTime, now, (SInt32)len) > now) return QTSS_WouldBlock;
+        if (!k && !update_quality_level(s, cs, pkt->packetTransmitTime, delay, now)) {
+            if (outLen) *outLen = len;
+            return QTSS_NoErr;                             // stale: not written, counted as written
+        }
+    }
     if (s->budget[k] == 0) return QTSS_WouldBlock;
     if (s->budget[k] > 0) s->budget[k]--;
     if (g_bench) {
@@ -344,6 +407,7 @@ static QTSS_Error cb_write(void* stream, const void* buf, UInt32 len, UInt32* ou
         if (outLen) *outLen = len;
         return QTSS_NoErr;
     }
+    if (g_gate && s->client && !k) s->client->window->AddPacketToWindow((SInt32)len);
     std::string& c = s->cap[k];
     if (s->transport == qtssRTPTransportTypeTCP) {
         c.push_back('$');
@@ -427,6 +491,7 @@ int main(int argc, char** argv) {
 
     static NoopAssert logger;
     SetAssertLogger(&logger);
+    g_gate = getenv("EDTR_SERVER_GATE") && atoi(getenv("EDTR_SERVER_GATE")) != 0;
 
     static QTSS_Callbacks cbs;
     for (int i = 0; i < kLastCallback; i++) cbs.addr[i] = (QTSS_CallbackProcPtr)cb_fail;
@@ -502,6 +567,11 @@ int main(int argc, char** argv) {
         sflags[s] = version >= 2 ? r.get<UInt8>() : 0;
     }
     if (version >= 4) { const UInt32 l = r.get<UInt32>(); r.p += l; }   // the prefs, read above
+    // each track's media (SDPSourceInfo: m= lines in order; qtssRTPStrPayloadType, QRM:1732-1765)
+    std::vector<std::vector<bool>> media_video(nsess);
+    for (UInt32 s = 0; s < nsess; s++)
+        for (size_t q = 0; (q = sdps[s].find("m=", q)) != std::string::npos; q += 2)
+            if (q == 0 || sdps[s][q - 1] == '\n') media_video[s].push_back(sdps[s].compare(q, 7, "m=video") == 0);
     OSRefTable sessionMap;                         // sSessionMap (QTSSReflectorModule.cpp:89)
     std::vector<Live> live(nsess);
     // FindOrCreateSession's create branch for a push (QTSSReflectorModule.cpp:1391-1478):
@@ -611,6 +681,15 @@ int main(int argc, char** argv) {
             FakeObj* client = new_obj();
             const char* ua = kUserAgents[uaflags & 1];
             set_value(client, qtssCliSesFirstUserAgent, 0, ua, (UInt32)strlen(ua));
+            if (g_gate) {
+                // the RTPSession's window (RTPSessionInterface.cpp:131), overbuffering off for a
+                // player without x-dynamic-rate (QTSSReflectorModule.cpp:1772-1777), the TCP
+                // streams' SetWindowSize(kUInt32_Max) (RTPStream.cpp:466-469); PLAY now (RTPSession::Play)
+                client->window = new RTPOverbufferWindow(50, kUInt32_Max, 25, 2.0f);
+                client->window->TurnOffOverbuffering();
+                if (transport) client->window->SetWindowSize(kUInt32_Max);
+                client->play_time = g_now;
+            }
             QTSS_StandardRTSP_Params pp;
             memset(&pp, 0, sizeof(pp));
             pp.inClientSession = (QTSS_ClientSessionObject)client;
@@ -644,6 +723,8 @@ int main(int argc, char** argv) {
                 st->sub_id = sub_id; st->session = s; st->track = x;
                 st->transport = transport ? qtssRTPTransportTypeTCP : qtssRTPTransportTypeUDP;
                 st->rtp_channel = 2 * x; st->rtcp_channel = 2 * x + 1;   // RTPStream.cpp:472-473
+                st->client = client;
+                st->video = x < media_video[s].size() && media_video[s][x];
                 void* cookie = sess->GetStreamByIndex(x)->GetStreamCookie();
                 set_value(st, g_cookie_attr, 0, &cookie, sizeof(cookie));
                 set_value(st, qtssRTPStrTransportType, 0, &st->transport, sizeof(UInt32));

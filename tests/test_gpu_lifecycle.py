@@ -103,11 +103,15 @@ def test_remove_with_outputs_needs_kill_and_invalidates_everything():
         ctx.session_remove(s2, kill_outputs=True)
         with pytest.raises(edgpu.EdgpuError):
             ctx.subscriber_remove(h2)                    # torn down with its session
-        # a session with another track count does not take the removed id
-        s3 = ctx.session_add(make_sdp(AV[:1]))
+        # a session with more tracks does not fit the removed one's rows; one with fewer takes them
+        # (best fit: the tables do not grow under churn with mixed track counts)
+        s3 = ctx.session_add(make_sdp(AV + AV[:1]))
         assert s3 != s2
         s4 = ctx.session_add(make_sdp(AV))
         assert s4 == s2
+        ctx.session_remove(s4)
+        s5 = ctx.session_add(make_sdp(AV[:1]))
+        assert s5 == s2
 
 
 @pytest.mark.gpu
