@@ -112,6 +112,7 @@ struct SessionHost {
     bool udp_push;
     uint32_t span = 0;              // tracks' worth of rows it holds (>= ntracks after a reuse)
     uint32_t eyes = 0;              // client outputs (ReflectorStream::fEyeCount, every track)
+    std::vector<int32_t> slots;     // the streams' bucket arrays: subscriber per slot, -1 empty
     std::vector<SourceHost> src;    // per track
     bool alive = true;              // false after edgpu_session_remove (its id may be reused)
     std::vector<uint32_t> subs;     // attached subscriber handles
@@ -138,6 +139,7 @@ struct SubscriberHost {
     bool active;
     int transport;
     uint32_t span;              // SubDev rows it holds (>= nsub in a larger free range)
+    int32_t slot;               // its place in the session's bucket arrays
 };
 
 struct edgpu_ctx {
@@ -722,6 +724,7 @@ static int detach_subscriber(edgpu_ctx* x, uint32_t handle) {
     SessionHost& sh = x->sessions[s.session];
     sh.eyes--;                                   // RemoveOutput(..., isClient) -> DecEyeCount
     sh.subs.erase(std::find(sh.subs.begin(), sh.subs.end(), handle));
+    if (s.slot >= 0 && (size_t)s.slot < sh.slots.size()) sh.slots[s.slot] = -1;   // ReflectorStream::RemoveOutput
     x->free_pending.emplace_back(s.span, s.first_sub);
     x->index_dirty = true;
     return EDGPU_OK;
@@ -835,7 +838,13 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
             x->sub_rw[q] = 0;
             v.emplace_back(q, Q);
         }
-    x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport, span});
+    // ReflectorStream::AddOutput + FindBucket (RS.cpp:281-334): the first empty place in bucket
+    // order (bucket = slot / 16, each holding 16); every track's array holds the output there
+    int32_t slot = 0;
+    while ((size_t)slot < sh.slots.size() && sh.slots[slot] >= 0) slot++;
+    if ((size_t)slot == sh.slots.size()) sh.slots.push_back(-1);
+    sh.slots[slot] = (int32_t)handle;
+    x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport, span, slot});
     if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += nsub;
     sh.eyes++;                                   // AddOutput(..., isClient) -> IncEyeCount
     sh.subs.push_back(handle);
@@ -952,6 +961,13 @@ int edgpu_subscribers_add(edgpu_ctx* x, uint32_t n, const uint32_t* sessions, co
         if (out_handles) out_handles[i] = h;
     }
     return upload_subs(x, v);
+}
+
+int edgpu_subscriber_slot(edgpu_ctx* x, uint32_t handle, int32_t* out_slot) {
+    if (!x || !out_slot || handle >= x->subscribers.size() || !x->subscribers[handle].active)
+        return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
+    *out_slot = x->subscribers[handle].slot;
+    return EDGPU_OK;
 }
 
 int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {

@@ -255,6 +255,13 @@ int  edgpu_sdp_parse(const char* sdp, uint32_t sdp_len, edgpu_sdp_track* out, ui
 int  edgpu_subscriber_add(edgpu_ctx* ctx, uint32_t session, int transport,
                           uint32_t* out_handle);
 int  edgpu_subscriber_remove(edgpu_ctx* ctx, uint32_t handle);
+/* The subscriber's place in its session's bucket arrays, as ReflectorStream::AddOutput /
+ * FindBucket give it (ReflectorStream.cpp:281-334: the first empty place, 16 per bucket, a
+ * removed output's place reused): its writes' transmit times are bucket x
+ * reflector_bucket_offset_delay_msec early (ReflectorStream.cpp:1107, RTPSessionOutput.cpp:
+ * 603-608), and a new output's first write decides for every output after it in this order
+ * (ReflectorStream.cpp:1088-1104).  Used by the egress's write gate (edgpu_egress_pacing). */
+int  edgpu_subscriber_slot(edgpu_ctx* ctx, uint32_t handle, int32_t* out_slot);
 /* A burst of joins (e.g. BASELINE config C4's 10k mid-GOP joins) in one call: subscriber i
  * joins sessions[i] with transports[i]; handles as edgpu_subscriber_add would return them. */
 int  edgpu_subscribers_add(edgpu_ctx* ctx, uint32_t n, const uint32_t* sessions,
