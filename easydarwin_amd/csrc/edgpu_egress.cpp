@@ -41,6 +41,7 @@
 #include <unistd.h>
 
 #include "edgpu.h"
+#include "edgpu_pacing.h"
 #include "tick_regions.h"
 
 namespace {
@@ -65,7 +66,26 @@ struct Worker {
     int udp_fd = -1;
     bool gso = true;                    // UDP generic segmentation offload still usable
     std::vector<edgpu_blocked> blocked;
-    uint64_t udp_datagrams = 0, udp_bytes = 0, udp_dropped = 0, tcp_frames = 0, tcp_bytes = 0;
+    std::vector<edgpu_egress_block> why;   // per blocked sub-stream: writes that went, the cause
+    std::vector<edgpu_out_desc> sel;       // a paced UDP sub-stream's packets that pass the gate
+    uint64_t udp_datagrams = 0, udp_bytes = 0, udp_dropped = 0, tcp_frames = 0, tcp_bytes = 0, stale = 0;
+    void block(uint32_t q, uint32_t sent, uint32_t written, uint32_t cause) {
+        blocked.push_back(edgpu_blocked{q, sent});
+        why.push_back(edgpu_egress_block{q, sent, written, cause});
+    }
+};
+
+// A subscriber with the server's write gate (edgpu_egress_pacing).
+struct Paced {
+    Paced(const edpace::Config& c, bool tcp, const edgpu_pacing& p)
+        : player(c, tcp, (p.flags & EDGPU_PACE_OVERBUFFER) != 0), video(p.video_tracks),
+          overbuffer((p.flags & EDGPU_PACE_OVERBUFFER) != 0) {
+        player.play_time_ms = p.play_time_ms;
+    }
+    edpace::Player player;
+    uint32_t video;
+    bool overbuffer;
+    int32_t slot = 0;
 };
 
 }  // namespace
@@ -85,7 +105,15 @@ struct edgpu_egress {
     std::vector<const uint8_t*> base;   // per sub-stream: host address of its arena region's start
     std::vector<Worker> workers;
     std::vector<edgpu_blocked> last_blocked;
+    std::vector<edgpu_egress_block> last_why;
     std::vector<uint32_t> disconnected;
+    // the write gate (Q20): config, paced subscribers, the tick's clock, the current pass's
+    // arrivals and, per sender, the first bucket place of a new output this tick
+    edpace::Config pcfg;
+    std::map<uint32_t, Paced> paced;
+    int64_t now = 0;
+    std::vector<int64_t> arrival;
+    std::map<uint32_t, int32_t> first_new;
     uint64_t copied_bytes = 0;
     std::string err;
 };
@@ -140,12 +168,18 @@ static void send_udp_plain(Worker& w, int fd, const sockaddr_in* to, const uint8
     }
 }
 
+static void send_udp_list(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d,
+                          const edgpu_out_desc* ds, uint32_t count);
 static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d) {
+    send_udp_list(e, w, q, s, d, e->desc + s.desc_base, s.desc_count);
+}
+// `count` datagrams ds[0..count) of sub-stream q
+static void send_udp_list(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, const UdpDest& d,
+                          const edgpu_out_desc* ds, uint32_t count) {
     const int k = s.kind ? 1 : 0;
     const uint8_t* base = e->base[q] - s.out_base;
     const int fd = d.fd[k] >= 0 ? d.fd[k] : w.udp_fd;
-    const edgpu_out_desc* ds = e->desc + s.desc_base;
-    if (!e->gso || !w.gso) { send_udp_plain(w, fd, &d.addr[k], base, ds, s.desc_count); return; }
+    if (!e->gso || !w.gso) { send_udp_plain(w, fd, &d.addr[k], base, ds, count); return; }
     constexpr uint32_t kMsgs = 64, kSegs = 64, kMaxPayload = 65507, kMaxSeg = 1472;
     struct Msg { uint32_t first, n, seg; };
     mmsghdr msgs[kMsgs];
@@ -153,16 +187,16 @@ static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
     iovec iov[kMsgs * kSegs];
     alignas(cmsghdr) char ctl[kMsgs][CMSG_SPACE(sizeof(uint16_t))];
     uint32_t i = 0;
-    while (i < s.desc_count) {
+    while (i < count) {
         // build up to kMsgs messages: runs of equal-length datagrams (+ one shorter tail)
         uint32_t nm = 0, niov = 0;
-        while (nm < kMsgs && i < s.desc_count) {
+        while (nm < kMsgs && i < count) {
             const uint32_t L = ds[i].len;
             // a segment must fit the path MTU: only datagrams that fit a 1500-B Ethernet frame
             const uint32_t cap = (L && L <= kMaxSeg) ? std::min(kSegs, kMaxPayload / L) : 1;
             uint32_t n = 1;
-            while (n < cap && i + n < s.desc_count && ds[i + n].len == L) n++;
-            if (n < cap && i + n < s.desc_count && ds[i + n].len < L && ds[i + n].len > 0) n++;   // shorter last segment
+            while (n < cap && i + n < count && ds[i + n].len == L) n++;
+            if (n < cap && i + n < count && ds[i + n].len < L && ds[i + n].len > 0) n++;   // shorter last segment
             Msg& m = mi[nm];
             m.first = i; m.n = n; m.seg = L;
             mmsghdr& h = msgs[nm];
@@ -211,7 +245,7 @@ static void send_udp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
             }
             done++;
         }
-        if (!w.gso && i < s.desc_count) { send_udp_plain(w, fd, &d.addr[k], base, ds + i, s.desc_count - i); return; }
+        if (!w.gso && i < count) { send_udp_plain(w, fd, &d.addr[k], base, ds + i, count - i); return; }
     }
 }
 
@@ -251,7 +285,7 @@ static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
         size_t wrote = r > 0 ? (size_t)r : 0;
         if (wrote < plen) {                               // the old tail is still not out
             c.pending.erase(0, wrote);
-            w.blocked.push_back(edgpu_blocked{q, i});
+            w.block(q, i, i, 0);
             return;
         }
         c.pending.clear();
@@ -266,15 +300,95 @@ static void send_tcp(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substre
             w.tcp_frames++;
             j++;
             i += j;
-            if (i < s.desc_count) w.blocked.push_back(edgpu_blocked{q, i});
+            if (i < s.desc_count) w.block(q, i, i, 0);
             return;
         }
         i += j;
         if (j < n || (size_t)r < total) {                 // no byte of frame i went out
-            w.blocked.push_back(edgpu_blocked{q, i});
+            w.block(q, i, i, 0);
             return;
         }
     }
+}
+
+// One frame of a paced TCP sub-stream, RTSPResponseStream::WriteV(kAllOrNothing): 1 = it went
+// (a partial frame counts, its tail buffered, 2), 0 = no byte of it went (EAGAIN), -1 = dead peer.
+static int tcp_frame(Worker& w, TcpConn& c, const uint8_t* p, uint32_t len) {
+    for (;;) {
+        iovec iov[2];
+        uint32_t nv = 0;
+        const size_t plen = c.pending.size();
+        if (plen) { iov[nv].iov_base = &c.pending[0]; iov[nv].iov_len = plen; nv++; }
+        iov[nv].iov_base = const_cast<uint8_t*>(p); iov[nv].iov_len = len; nv++;
+        msghdr mh;
+        memset(&mh, 0, sizeof(mh));
+        mh.msg_iov = iov;
+        mh.msg_iovlen = nv;
+        const ssize_t r = sendmsg(c.fd, &mh, MSG_NOSIGNAL);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) { c.dead = errno; c.pending.clear(); return -1; }
+        size_t wrote = r > 0 ? (size_t)r : 0;
+        if (wrote < plen) { c.pending.erase(0, wrote); return 0; }
+        c.pending.clear();
+        wrote -= plen;
+        if (wrote == 0) return 0;
+        w.tcp_frames++;
+        w.tcp_bytes += len;
+        if (wrote < len) { c.pending.assign(reinterpret_cast<const char*>(p) + wrote, len - wrote); return 2; }
+        return 1;
+    }
+}
+
+// A paced sub-stream: RTPSessionOutput::WritePacket's transmit time, then RTPStream::Write's gate
+// before each socket write (edgpu_pacing.h): the over-buffer window (RTP, and RTCP while
+// overbuffering is off) holds the packet -> the sub-stream stops here (and a new output's first
+// pass takes the packet's age as its buffer delay, RTPSessionOutput.cpp:612-622); a stale RTP
+// packet of a TCP non-video stream is dropped (counted as written); a written RTP packet enters
+// the window.
+static void send_paced(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_substream_out& s, Paced& P,
+                       const UdpDest* ud, TcpConn* tc) {
+    const edgpu_out_desc* ds = e->desc + s.desc_base;
+    const uint8_t* base = e->base[q] - s.out_base;
+    const int64_t* arr = e->arrival.data() + s.desc_base;
+    const bool rtcp = s.kind != 0, tcp = s.transport == EDGPU_TRANSPORT_TCP;
+    const bool video = s.track < 32 && ((P.video >> s.track) & 1u);
+    const int64_t now = e->now;
+    const int64_t lateness = e->pcfg.bucket_delay_ms * (int64_t)(P.slot / (int32_t)e->pcfg.bucket_size);
+    auto fn = e->first_new.find(s.sender);
+    const bool first = fn != e->first_new.end() && P.slot >= fn->second;   // ReflectPackets' firstPacket
+    edpace::Player& pl = P.player;
+    if (tcp && tc->dead) return;
+    w.sel.clear();
+    uint32_t written = 0;
+    bool socket_full = false;                   // a frame went out in part: the next one waits
+    for (uint32_t i = 0; i < s.desc_count; i++) {
+        const uint32_t len = ds[i].len - (tcp ? 4u : 0u);           // the packet RTPStream::Write gets
+        const int64_t tt = edpace::transmit_time(now, lateness, pl.buffer_delay_ms, arr[i]);
+        if ((!rtcp || !P.overbuffer) && pl.win.CheckTransmitTime(tt, now, (int32_t)len) > now) {
+            if (first) pl.buffer_delay_ms = now - arr[i];
+            w.block(q, i, written, 1);
+            break;
+        }
+        if (!rtcp && !edpace::keep_packet(pl, s.track, video, tcp, tt, now - tt, now, e->pcfg)) {
+            w.stale++;
+            continue;
+        }
+        if (tcp) {
+            const int r = socket_full ? 0 : tcp_frame(w, *tc, base + ds[i].offset, ds[i].len);
+            if (r < 0) break;                                         // dead peer: counted as written
+            if (r == 0) {
+                if (first) pl.buffer_delay_ms = now - arr[i];
+                w.block(q, i, written, 0);
+                break;
+            }
+            if (r == 2) socket_full = true;
+        } else {
+            w.sel.push_back(ds[i]);
+        }
+        written++;
+        if (!rtcp) pl.win.AddPacketToWindow((int32_t)len);
+    }
+    if (!tcp && !w.sel.empty()) send_udp_list(e, w, q, s, *ud, w.sel.data(), (uint32_t)w.sel.size());
 }
 
 extern "C" {
@@ -377,13 +491,52 @@ static int send_pass(edgpu_egress* e, const edgpu_fanout_result* r, const edgpu_
         for (uint32_t q = 0; q < nq; q++) e->base[q] = e->h_arena + e->subs[q].out_base;
     }
     e->copied_bytes += need;
+    if (!e->paced.empty()) {
+        // the write gate's inputs: every descriptor's arrival, and (at the tick's first pass, whose
+        // table flags every new output) the first bucket place of a new output per sender
+        e->arrival.resize(std::max<uint64_t>(st.pass_packets, 1));
+        if (st.pass_packets &&
+            (rc = edgpu_fanout_arrivals(e->ctx, e->arrival.data(), st.pass_packets, EDGPU_PTR_HOST)))
+            return eg_fail(e, rc, "arrivals (pacing needs serial ticks)");
+        if (st.pass == 0) {
+            e->first_new.clear();
+            std::map<uint32_t, int32_t> slot_of;
+            for (uint32_t q = 0; q < nq; q++) {
+                const edgpu_substream_out& o = e->subs[q];
+                if (!(o.flags & EDGPU_SUB_NEW)) continue;
+                auto it = slot_of.find(o.subscriber);
+                if (it == slot_of.end()) {
+                    int32_t sl = -1;
+                    if (edgpu_subscriber_slot(e->ctx, o.subscriber, &sl) != EDGPU_OK) sl = -1;
+                    it = slot_of.emplace(o.subscriber, sl).first;
+                }
+                if (it->second < 0) continue;
+                auto f = e->first_new.find(o.sender);
+                if (f == e->first_new.end() || it->second < f->second) e->first_new[o.sender] = it->second;
+            }
+        }
+    }
     auto t1 = std::chrono::steady_clock::now();
-    for (Worker& w : e->workers) { w.blocked.clear(); w.udp_datagrams = w.udp_bytes = w.udp_dropped = w.tcp_frames = w.tcp_bytes = 0; }
+    for (Worker& w : e->workers) {
+        w.blocked.clear(); w.why.clear();
+        w.udp_datagrams = w.udp_bytes = w.udp_dropped = w.tcp_frames = w.tcp_bytes = w.stale = 0;
+    }
     auto run = [&](uint32_t k) {
         Worker& w = e->workers[k];
         for (uint32_t q = 0; q < (uint32_t)e->subs.size(); q++) {
             const edgpu_substream_out& s = e->subs[q];
             if (s.desc_count == 0 || s.subscriber % e->nthreads != k) continue;
+            auto pc = e->paced.find(s.subscriber);
+            if (pc != e->paced.end()) {                  // (one worker owns a subscriber: no lock)
+                if (s.transport == EDGPU_TRANSPORT_TCP) {
+                    auto it = e->tcp.find(s.subscriber);
+                    if (it != e->tcp.end()) send_paced(e, w, q, s, pc->second, nullptr, &it->second);
+                } else {
+                    auto it = e->udp.find((uint64_t)s.subscriber << 16 | s.track);
+                    if (it != e->udp.end()) send_paced(e, w, q, s, pc->second, &it->second, nullptr);
+                }
+                continue;
+            }
             if (s.transport == EDGPU_TRANSPORT_TCP) {
                 auto it = e->tcp.find(s.subscriber);
                 if (it != e->tcp.end()) send_tcp(e, w, q, s, it->second);
@@ -403,6 +556,8 @@ static int send_pass(edgpu_egress* e, const edgpu_fanout_result* r, const edgpu_
     s.send_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     for (Worker& w : e->workers) {
         blocked.insert(blocked.end(), w.blocked.begin(), w.blocked.end());
+        e->last_why.insert(e->last_why.end(), w.why.begin(), w.why.end());
+        s.stale_dropped += w.stale;
         s.udp_datagrams += w.udp_datagrams; s.udp_bytes += w.udp_bytes; s.udp_dropped += w.udp_dropped;
         s.tcp_frames += w.tcp_frames; s.tcp_bytes += w.tcp_bytes;
     }
@@ -415,6 +570,7 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     edgpu_egress_stats s;
     memset(&s, 0, sizeof(s));
     e->copied_bytes = 0;
+    e->last_why.clear();
     std::vector<edgpu_blocked> blocked;
     // every copy pass of the tick, in sub-stream row order: a connection's frames keep their order
     edgpu_fanout_result cur = *r;
@@ -433,6 +589,8 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     s.blocked_substreams = (uint32_t)blocked.size();
     s.copy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - s.send_ms;
     e->last_blocked = blocked;
+    std::sort(e->last_why.begin(), e->last_why.end(),
+              [](const edgpu_egress_block& a, const edgpu_egress_block& b) { return a.substream < b.substream; });
     for (auto& kv : e->tcp)
         if (kv.second.dead && !kv.second.reported) { e->disconnected.push_back(kv.first); kv.second.reported = true; }
     s.copied_bytes = e->copied_bytes;
@@ -457,6 +615,46 @@ int edgpu_egress_disconnected(edgpu_egress* e, uint32_t* out, uint32_t cap, uint
     std::copy(e->disconnected.begin(), e->disconnected.begin() + k, out);
     *n = (uint32_t)e->disconnected.size();
     e->disconnected.erase(e->disconnected.begin(), e->disconnected.begin() + k);
+    return EDGPU_OK;
+}
+
+int edgpu_egress_pacing_config(edgpu_egress* e, const edgpu_pacing_config* c) {
+    if (!e || !c || c->bucket_size == 0) return EDGPU_BAD_ARGUMENT;
+    e->pcfg.bucket_delay_ms = c->bucket_delay_ms;
+    e->pcfg.over_buffer_ms = c->over_buffer_ms;
+    e->pcfg.drop_all_packets_ms = c->drop_all_packets_ms;
+    e->pcfg.thin_all_the_way_ms = c->thin_all_the_way_ms;
+    e->pcfg.start_thinning_ms = c->start_thinning_ms;
+    e->pcfg.bucket_size = c->bucket_size;
+    e->pcfg.send_interval_ms = c->send_interval_ms;
+    e->pcfg.max_send_ahead_s = c->max_send_ahead_s;
+    e->pcfg.overbuffer_rate = c->overbuffer_rate;
+    return EDGPU_OK;
+}
+
+int edgpu_egress_pacing(edgpu_egress* e, uint32_t subscriber, const edgpu_pacing* p) {
+    if (!e) return EDGPU_BAD_ARGUMENT;
+    if (!p) { e->paced.erase(subscriber); return EDGPU_OK; }
+    int32_t slot = -1;
+    if (edgpu_subscriber_slot(e->ctx, subscriber, &slot) != EDGPU_OK) return eg_fail(e, EDGPU_BAD_ARGUMENT, "bad subscriber");
+    const bool tcp = e->tcp.count(subscriber) != 0;
+    e->paced.erase(subscriber);
+    Paced& P = e->paced.emplace(subscriber, Paced(e->pcfg, tcp, *p)).first->second;
+    P.slot = slot;
+    return EDGPU_OK;
+}
+
+int edgpu_egress_clock(edgpu_egress* e, int64_t now_ms) {
+    if (!e) return EDGPU_BAD_ARGUMENT;
+    e->now = now_ms;
+    return EDGPU_OK;
+}
+
+int edgpu_egress_block_info(edgpu_egress* e, edgpu_egress_block* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n || (cap && !out)) return EDGPU_BAD_ARGUMENT;
+    const uint32_t k = (uint32_t)std::min<size_t>(cap, e->last_why.size());
+    std::copy(e->last_why.begin(), e->last_why.begin() + k, out);
+    *n = (uint32_t)e->last_why.size();
     return EDGPU_OK;
 }
 

@@ -17,7 +17,7 @@
 #include <cstdint>
 #include <vector>
 
-namespace edgpu_pacing {
+namespace edpace {
 
 // The server prefs the gate reads (QTSServerPrefs.cpp defaults) and the reflector's own
 // (ReflectorStream::Initialize prefs, ReflectorStream.cpp:87-117).
@@ -172,4 +172,4 @@ inline bool keep_packet(Player& p, uint32_t track, bool video, bool tcp, int64_t
     return true;
 }
 
-}  // namespace edgpu_pacing
+}  // namespace edpace

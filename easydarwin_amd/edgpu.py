@@ -38,6 +38,8 @@ EXPORTED = [
     "edgpu_subscriber_rewrite", "edgpu_sdp_parse", "edgpu_host_alloc", "edgpu_host_free",
     "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
     "edgpu_set_timing", "edgpu_ingest_prestage", "edgpu_fanout_next", "edgpu_session_ssrc_prefs",
+    "edgpu_subscriber_slot", "edgpu_egress_pacing_config", "edgpu_egress_pacing", "edgpu_egress_clock",
+    "edgpu_egress_block_info",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -112,7 +114,20 @@ class EgressStats(C.Structure):
     _fields_ = [("udp_datagrams", C.c_uint64), ("udp_bytes", C.c_uint64), ("udp_dropped", C.c_uint64),
                 ("tcp_frames", C.c_uint64), ("tcp_bytes", C.c_uint64), ("blocked_substreams", C.c_uint32),
                 ("_pad", C.c_uint32), ("copy_ms", C.c_double), ("send_ms", C.c_double),
-                ("copied_bytes", C.c_uint64)]
+                ("copied_bytes", C.c_uint64), ("stale_dropped", C.c_uint64)]
+
+
+PACE_OVERBUFFER = 1
+
+
+class Pacing(C.Structure):
+    _fields_ = [("play_time_ms", C.c_int64), ("video_tracks", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class PacingConfig(C.Structure):
+    _fields_ = [("bucket_delay_ms", C.c_int64), ("over_buffer_ms", C.c_int64), ("drop_all_packets_ms", C.c_int64),
+                ("thin_all_the_way_ms", C.c_int64), ("start_thinning_ms", C.c_int64), ("bucket_size", C.c_uint32),
+                ("send_interval_ms", C.c_uint32), ("max_send_ahead_s", C.c_uint32), ("overbuffer_rate", C.c_float)]
 
 
 class Counters(C.Structure):
@@ -219,6 +234,11 @@ def load(path: str = LIB_PATH):
         "edgpu_host_free": (I32, [P, P]),
         "edgpu_arena_gather": (I32, [P, C.POINTER(FanoutResult), P, U32, P, U64]),
         "edgpu_egress_disconnected": (I32, [P, P, U32, C.POINTER(U32)]),
+        "edgpu_subscriber_slot": (I32, [P, U32, C.POINTER(C.c_int32)]),
+        "edgpu_egress_pacing_config": (I32, [P, C.POINTER(PacingConfig)]),
+        "edgpu_egress_pacing": (I32, [P, U32, C.POINTER(Pacing)]),
+        "edgpu_egress_clock": (I32, [P, C.c_int64]),
+        "edgpu_egress_block_info": (I32, [P, P, U32, C.POINTER(U32)]),
         "edgpu_fanout_arrivals": (I32, [P, P, U32, I32]),
     }
     for name, (res, args) in sig.items():
@@ -331,6 +351,12 @@ class Context:
 
     def subscriber_remove(self, handle: int):
         _check(self.lib.edgpu_subscriber_remove(self.h, handle))
+
+    def subscriber_slot(self, handle: int) -> int:
+        """Its place in the session's bucket arrays (ReflectorStream::AddOutput / FindBucket)."""
+        v = C.c_int32()
+        _check(self.lib.edgpu_subscriber_slot(self.h, handle, C.byref(v)))
+        return v.value
 
     def ingest_host(self, desc: np.ndarray, seg_off: np.ndarray, seg_sess: np.ndarray, blob: np.ndarray):
         desc = np.ascontiguousarray(desc, dtype=PKT_DTYPE)
@@ -581,6 +607,33 @@ class Egress:
         buf = np.zeros((cap, 2), dtype=np.uint32)
         n = C.c_uint32()
         self._chk(self.lib.edgpu_egress_blocked(self.h, _ptr(buf), cap, C.byref(n)))
+        return [tuple(map(int, x)) for x in buf[:min(n.value, cap)]]
+
+    def pacing_config(self, bucket_delay_ms=73, over_buffer_ms=1000, drop_all_packets_ms=2500,
+                      thin_all_the_way_ms=1500, start_thinning_ms=0, bucket_size=16, send_interval_ms=50,
+                      max_send_ahead_s=25, overbuffer_rate=2.0):
+        c = PacingConfig(bucket_delay_ms, over_buffer_ms, drop_all_packets_ms, thin_all_the_way_ms,
+                         start_thinning_ms, bucket_size, send_interval_ms, max_send_ahead_s, overbuffer_rate)
+        self._chk(self.lib.edgpu_egress_pacing_config(self.h, C.byref(c)))
+
+    def pacing(self, subscriber: int, play_time_ms: int | None, video_tracks: int = 0, flags: int = 0):
+        """The server's write gate for this subscriber (None: off): edgpu_egress_pacing."""
+        if play_time_ms is None:
+            self._chk(self.lib.edgpu_egress_pacing(self.h, subscriber, None))
+        else:
+            p = Pacing(play_time_ms, video_tracks, flags)
+            self._chk(self.lib.edgpu_egress_pacing(self.h, subscriber, C.byref(p)))
+
+    def clock(self, now_ms: int):
+        self._chk(self.lib.edgpu_egress_clock(self.h, int(now_ms)))
+
+    def block_info(self):
+        """(sub-stream, sent, written, cause) of the last send's stopped sub-streams; cause 0 = the
+        socket, 1 = the write gate."""
+        cap = 1 << 16
+        buf = np.zeros((cap, 4), dtype=np.uint32)
+        n = C.c_uint32()
+        self._chk(self.lib.edgpu_egress_block_info(self.h, _ptr(buf), cap, C.byref(n)))
         return [tuple(map(int, x)) for x in buf[:min(n.value, cap)]]
 
     def disconnected(self) -> list:

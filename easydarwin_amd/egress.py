@@ -10,6 +10,12 @@ TCP backpressure: ``hold`` (tick time -> set of subscriber ids) leaves a subscri
 undrained at that tick, so its small send buffer fills and the egress sees EAGAIN; the reports
 the egress filed with the engine are kept per tick (``blocked``, as BLOCK events) so the same
 budgets can be replayed through the reference harness.
+
+Q20: ``pacing`` (a dict of edgpu_pacing_config fields, {} for the defaults) turns the server's
+write gate on for every subscriber (edgpu_egress_pacing: over-buffer window, TCP-audio thinning),
+with the PLAY time and the video tracks ``join`` is given and the tick's clock; then ``blocked``
+keeps only the writes the socket refused (with the writes it took), since the reference harness
+applies the gate itself (EDTR_SERVER_GATE=1).
 """
 from __future__ import annotations
 
@@ -21,8 +27,11 @@ from . import edgpu
 
 class SocketSink:
     def __init__(self, ctx: edgpu.Context, threads: int = 2, tcp_sndbuf: int | None = None,
-                 hold: dict | None = None):
+                 hold: dict | None = None, pacing: dict | None = None):
         self.eg = edgpu.Egress(ctx, threads)
+        self.pacing = pacing
+        if pacing is not None:
+            self.eg.pacing_config(**pacing)
         self.tcp_sndbuf = tcp_sndbuf
         self.hold = hold or {}
         self.udp = {}           # (handle, track, kind) -> receiver socket
@@ -33,7 +42,7 @@ class SocketSink:
         self.blocked = []       # (tick time, sub_id, track, kind, sent)
         self.stats = []
 
-    def join(self, handle: int, sub_id: int, ntracks: int, tcp: bool):
+    def join(self, handle: int, sub_id: int, ntracks: int, tcp: bool, play_time: int = 0, video_tracks: int = 0):
         self.sub_id[handle] = sub_id
         for t in range(ntracks):
             for k in (0, 1):
@@ -59,13 +68,19 @@ class SocketSink:
                     self.udp[(handle, t, k)] = r
                     ports.append(r.getsockname()[1])
                 self.eg.udp(handle, t, "127.0.0.1", ports[0], ports[1])
+        if self.pacing is not None:
+            self.eg.pacing(handle, play_time, video_tracks)
 
     def tick(self, result, t: int):
+        if self.pacing is not None:
+            self.eg.clock(t)
         st = self.eg.send(result)
         self.stats.append(st)
-        for q, sent in self.eg.blocked():
+        for q, _sent, written, cause in self.eg.block_info():
+            if cause != 0:                          # the write gate held it, not the socket
+                continue
             h, trk, kind = self.q_of[q]
-            self.blocked.append((t, self.sub_id[h], trk, kind, sent))
+            self.blocked.append((t, self.sub_id[h], trk, kind, written))
         held = self.hold.get(t, set())
         self.drain(skip={h for h, sid in self.sub_id.items() if sid in held})
         return st

@@ -35,6 +35,7 @@ RTSP stack (consume the request through its blank line, resubmit the rest).
 from __future__ import annotations
 
 import random
+import re
 import struct
 
 import numpy as np
@@ -350,7 +351,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             from .egress import SocketSink
             if any(ev[0] == BLOCK for ev in trace.events) or lag:
                 raise ValueError("socket egress replays take neither BLOCK events nor overlap_ticks")
-            sink = SocketSink(ctx if rep is None else rep, **{k: v for k, v in sockets.items() if k != "report"})
+            kw = {k: v for k, v in sockets.items() if k not in ("report", "stats")}
+            if kw.get("pacing") is not None:        # the gate's reflector prefs are the trace's
+                kw["pacing"] = dict({"bucket_delay_ms": int(pv["reflector_bucket_offset_delay_msec"]),
+                                     "over_buffer_ms": 1000 * int(cfg["reflector_buffer_size_sec"])}, **kw["pacing"])
+            sink = SocketSink(ctx if rep is None else rep, **kw)
         blocks = {}                         # (sub_id, track, kind) -> budget for the next TICK
         gone = set()                        # handles removed by LEAVE
 
@@ -372,7 +377,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             if rep is not None:
                 ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
             if sink is not None:
-                sink.join(h, sub_id, sess_tracks[s], bool(transport))
+                vid = sum(1 << t for t, m in enumerate(re.findall(r"(?m)^m=(\w+)", trace.sdps[s])) if m == "video")
+                sink.join(h, sub_id, sess_tracks[s], bool(transport), play_time=now_j, video_tracks=vid)
             for tr in range(sess_tracks[s]):
                 for k in (0, 1):
                     images[(h, tr, k)] = []
@@ -492,6 +498,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             sink.close()
             if isinstance(sockets, dict) and "report" in sockets:
                 sockets["report"].extend(sink.blocked)
+            if isinstance(sockets, dict) and "stats" in sockets:
+                sockets["stats"].extend(sink.stats)
         # capture: one record per (subscriber, track, kind), sorted by subscriber id
         recs = []
         for (h, tr, k), parts in images.items():

@@ -516,6 +516,7 @@ typedef struct edgpu_egress_stats {
     uint32_t _pad;
     double   copy_ms, send_ms;  /* device -> pinned host copy; socket writes */
     uint64_t copied_bytes;      /* bytes brought over PCIe for this tick */
+    uint64_t stale_dropped;     /* paced subscribers: stale TCP non-video RTP packets dropped (Q20) */
 } edgpu_egress_stats;
 int  edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out);
 int  edgpu_egress_destroy(edgpu_egress* eg);
@@ -536,6 +537,53 @@ int  edgpu_egress_flush(edgpu_egress* eg, uint64_t* pending);
  * write as done, RTPSessionOutput.cpp:612-653); the host tears the session down
  * (ClientSessionClosing -> edgpu_subscriber_remove).  Sockets are written with MSG_NOSIGNAL. */
 int  edgpu_egress_disconnected(edgpu_egress* eg, uint32_t* out, uint32_t cap, uint32_t* n);
+
+/* ---- The server's write gate (Q20): over-buffer window and TCP-audio thinning ----
+ * Behind the reference module, each relayed packet goes through the server's RTPStream::Write
+ * (Server.tproj/RTPStream.cpp:1048-1147) with the transmit time RTPSessionOutput::WritePacket gave
+ * it (RTPSessionOutput.cpp:603-608: now - bucket lateness, + the output's buffer delay left for the
+ * packet).  There the session's over-buffer window (RTPOverbufferWindow::CheckTransmitTime) holds a
+ * packet whose time has not come -- QTSS_WouldBlock: the output stops for this reflect, and on a new
+ * output's first pass the packet's age becomes its buffer delay (RTPSessionOutput.cpp:612-622) --
+ * and RTPStream::UpdateQualityLevel (:936-1045) drops RTP packets of a TCP non-video stream that have
+ * fallen more than drop_all_packets_delay behind.  With pacing on for a subscriber the egress does
+ * the same before its socket writes: held packets are reported to the engine like a blocked socket
+ * (edgpu_fanout_blocked), dropped ones count as written.  It needs each packet's arrival (so serial
+ * ticks: edgpu_fanout_arrivals) and the tick's clock (edgpu_egress_clock), the subscriber's bucket
+ * place comes from the engine (edgpu_subscriber_slot). */
+#define EDGPU_PACE_OVERBUFFER 1u   /* the client asked for dynamic rate (x-dynamic-rate: 1): the
+                                      reflector otherwise turns overbuffering off, QRM:1772-1777 */
+typedef struct edgpu_pacing {
+    int64_t  play_time_ms;         /* the PLAY's time (RTPSession::fPlayTime): packets due before it
+                                      are never thinned (RTPStream.cpp:941-942) */
+    uint32_t video_tracks;         /* bit t: track t is video (never thinned, :946-948) */
+    uint32_t flags;                /* EDGPU_PACE_* */
+} edgpu_pacing;
+/* Server and reflector prefs the gate reads; edgpu_egress_create sets the reference defaults
+ * (QTSServerPrefs.cpp: send_interval 50, max_send_ahead_time 25, overbuffer_rate 2.0,
+ * drop_all_packets_delay 2500, thin_all_the_way_delay 1500, start_thinning_delay 0; the late
+ * tolerance's 1.5-s default adjusts none, RTPStream.cpp:897-918; the reflector's bucket offset
+ * delay 73 ms, 16 outputs a bucket, buffer 1000 ms, ReflectorStream.cpp:53-117). */
+typedef struct edgpu_pacing_config {
+    int64_t  bucket_delay_ms;      /* reflector_bucket_offset_delay_msec */
+    int64_t  over_buffer_ms;       /* reflector_buffer_size_sec x 1000: a new output's buffer delay */
+    int64_t  drop_all_packets_ms, thin_all_the_way_ms, start_thinning_ms;
+    uint32_t bucket_size;          /* outputs per bucket (16) */
+    uint32_t send_interval_ms, max_send_ahead_s;
+    float    overbuffer_rate;
+} edgpu_pacing_config;
+int  edgpu_egress_pacing_config(edgpu_egress* eg, const edgpu_pacing_config* cfg);
+/* Turns the gate on for `subscriber` (NULL: off).  Call after its edgpu_egress_udp / _tcp. */
+int  edgpu_egress_pacing(edgpu_egress* eg, uint32_t subscriber, const edgpu_pacing* p);
+/* The tick's clock (OS::Milliseconds at the reflect), for the next edgpu_egress_send. */
+int  edgpu_egress_clock(edgpu_egress* eg, int64_t now_ms);
+/* Why each sub-stream of the last edgpu_egress_send stopped: `sent` descriptors went (written,
+ * or dropped as stale), `written` of them reached the socket; cause 0 = the socket would block,
+ * 1 = the write gate held the next packet. */
+typedef struct edgpu_egress_block {
+    uint32_t substream, sent, written, cause;
+} edgpu_egress_block;
+int  edgpu_egress_block_info(edgpu_egress* eg, edgpu_egress_block* out, uint32_t cap, uint32_t* n);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs; EDGPU_ERR while an
                                                                        ingest awaits its index */

@@ -7,13 +7,13 @@
 #include "edgpu_pacing.h"
 
 int main() {
-    std::unique_ptr<edgpu_pacing::OverbufferWindow> w;
+    std::unique_ptr<edpace::OverbufferWindow> w;
     char op[8];
     while (scanf("%7s", op) == 1) {
         if (!strcmp(op, "N")) {
             unsigned si, ws, sa; float r;
             if (scanf("%u %u %u %f", &si, &ws, &sa, &r) != 4) return 2;
-            w.reset(new edgpu_pacing::OverbufferWindow(si, ws, sa, r));
+            w.reset(new edpace::OverbufferWindow(si, ws, sa, r));
         } else if (!w) {
             return 2;
         } else if (!strcmp(op, "C")) {

@@ -181,3 +181,59 @@ def test_udp_overload_loses_datagrams_without_reordering(gso, monkeypatch):
                 lost += len(want) - len(got)
         assert lost > 0, "the receivers kept up: the test did not overload them"
         sink.close()
+
+
+def _gate_reference(tr: Trace, report, exe, tmp_path):
+    """The reference harness with the server's write gate (EDTR_SERVER_GATE=1) and the socket
+    budgets the egress met."""
+    p = tmp_path / "gate.edtr"
+    _with_blocks(tr, report).write(str(p))
+    c = tmp_path / "gate.edcp"
+    subprocess.run([exe, str(p), str(c)], check=True, stderr=subprocess.DEVNULL,
+                   env=dict(os.environ, EDTR_SERVER_GATE="1"))
+    return capture_summary(read_capture(c.read_bytes()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in SCENARIOS
+                                  if not any(ev[0] == BLOCK for ev in SCENARIOS[n]().events)])
+def test_paced_egress_matches_the_reference_server_gate(name, oracle_bins, tmp_path):
+    """Q20: with pacing on (edgpu_egress_pacing) the egress applies the server's RTPStream::Write
+    gate -- the over-buffer window holds a new output's first packets until their transmit time
+    (its buffer delay then becomes their age, RTPSessionOutput.cpp:612-622), and relocation,
+    bookmarks and the next ticks follow from that -- and its sockets carry exactly what the
+    reference harness writes through the same gate (compiled RTPOverbufferWindow)."""
+    if oracle_bins["ref"] is None:
+        pytest.skip("oracle/_ref/ref_harness not built")
+    tr = SCENARIOS[name]()
+    report = []
+    cap, _ = replay(tr, sockets={"threads": 2, "pacing": {}, "report": report})
+    want = _gate_reference(tr, report, oracle_bins["ref"], tmp_path)
+    got = capture_summary(read_capture(cap))
+    bad = [k for k in want if got.get(k) != want[k]]
+    assert not bad, f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mixed", "anchor"])
+def test_paced_egress_thins_congested_tcp_audio_like_the_reference(name, oracle_bins, tmp_path):
+    """Q20: TCP readers held for most of the run -- the interleaved connections stall, packets
+    queue in the rings, and once an audio packet is more than drop_all_packets_delay (2.5 s) late
+    RTPStream::UpdateQualityLevel drops it (RTPStream.cpp:936-1045).  The egress drops exactly the
+    packets the reference harness's gate drops."""
+    if oracle_bins["ref"] is None:
+        pytest.skip("oracle/_ref/ref_harness not built")
+    tr = SCENARIOS[name]()
+    tcp_subs = {ev[3] for ev in tr.events if ev[0] == 2 and ev[4] == TCP}
+    ticks = [ev[1] for ev in tr.events if ev[0] == TICK]
+    lo, hi = ticks[len(ticks) // 6], ticks[5 * len(ticks) // 6]
+    hold = {t: tcp_subs for t in ticks if lo <= t < hi}
+    report, stats = [], []
+    cap, _ = replay(tr, sockets={"threads": 2, "tcp_sndbuf": 4096, "hold": hold, "pacing": {}, "report": report,
+                                 "stats": stats})
+    assert report, "no write blocked: the test did not congest the connections"
+    assert sum(s.stale_dropped for s in stats) > 0, "no packet went stale: thinning was not exercised"
+    want = _gate_reference(tr, report, oracle_bins["ref"], tmp_path)
+    got = capture_summary(read_capture(cap))
+    bad = [k for k in want if got.get(k) != want[k]]
+    assert not bad, f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}"
