@@ -412,10 +412,16 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             elif ev[0] == JOIN:
                 # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):
                 # ingest what precedes it first
-                if rtp_info_player(mod["prefs"], ev[5]) and rep is None:
+                # (on a replica too: its session is brought up to the owner's queues first)
+                rtpi = rtp_info_player(mod["prefs"], ev[5])
+                if rtpi:
                     flush()
-                if rep is None:
+                if rep is None or rtpi:
                     if gen[ev[2]] is not None:          # else no session: the SETUP fails
+                        if link is not None:
+                            if replica == "late" or ev[2] not in rsess:
+                                rsess[ev[2]] = link.add(ev[2], trace.sdps[ev[2]])
+                            link.sync(clock)
                         do_join(ev + (clock,))
                 else:
                     joins.append(ev + (clock,))     # replicas: made at the tick

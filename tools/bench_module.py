@@ -103,6 +103,12 @@ def main():
     m = out["module"]
     pt = m["per_tick_bytes"]
     out["readback_vs_arena"] = round(pt["readback"] / pt["arena"], 4) if pt["arena"] else None
+    # The latency the tick adds over the reference's reflect on arrival (ReflectorStream.cpp:573 signals
+    # the sender's socket task, :603-618 / :1676-1714 reflect at once): a packet waits for the next
+    # tick (uniform over the tick period) and then for the tick's own wall time before its write.
+    wall = 1000.0 * m["tick_s"] / max(m["ticks_timed"], 1)
+    out["added_latency_ms"] = {"mean": round(args.tick_ms / 2 + wall, 3), "max": round(args.tick_ms + wall, 3),
+                               "tick_wall_ms": round(wall, 3), "lock_hold_max_ms": m["per_tick_ms"]["hold_max"]}
     if not args.no_reference:
         out["reference_module"] = reference_module_run(args)
         if out["reference_module"]:
