@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cerrno>
 #include <cstring>
@@ -115,6 +116,7 @@ struct edgpu_egress {
     std::vector<int64_t> arrival;
     std::map<uint32_t, int32_t> first_new;
     uint64_t copied_bytes = 0;
+    std::atomic<int64_t> trace_left{0};     // EDGPU_PACE_TRACE=n: the first n gate decisions to stderr (debug)
     std::string err;
 };
 
@@ -369,6 +371,12 @@ static void send_paced(edgpu_egress* e, Worker& w, uint32_t q, const edgpu_subst
             w.block(q, i, written, 1);
             break;
         }
+        if (e->trace_left > 0 && tcp && !video && !rtcp && (now - tt > 800 || first)) {
+            e->trace_left--;
+            fprintf(stderr, "pace sub=%u tr=%u now=%lld arr=%lld bd=%lld tt=%lld first=%d slot=%d st=%d lc=%lld\n", s.subscriber,
+                    s.track, (long long)now, (long long)arr[i], (long long)pl.buffer_delay_ms, (long long)tt, (int)first,
+                    P.slot, (int)pl.started_thinning, (long long)pl.last_check);
+        }
         if (!rtcp && !edpace::keep_packet(pl, s.track, video, tcp, tt, now - tt, now, e->pcfg)) {
             w.stale++;
             continue;
@@ -400,6 +408,7 @@ int edgpu_egress_create(edgpu_ctx* ctx, uint32_t threads, edgpu_egress** out) {
     e->nthreads = std::max(1u, std::min(threads, 64u));
     if (const char* v = getenv("EDGPU_EGRESS_DEDUP")) e->dedup = atoi(v) != 0;
     if (const char* v = getenv("EDGPU_EGRESS_GSO")) e->gso = atoi(v) != 0;
+    if (const char* v = getenv("EDGPU_PACE_TRACE")) e->trace_left = atoll(v);
     e->workers.resize(e->nthreads);
     for (Worker& w : e->workers) {
         w.udp_fd = socket(AF_INET, SOCK_DGRAM, 0);

@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <emmintrin.h>
 
 namespace edgpu_reflector {
 
@@ -183,6 +184,28 @@ int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
     return kNoErr;
 }
 
+// Writes one packet's slot ([4 zero bytes][packet][zero pad to 16], `slot` bytes at the 16-B
+// aligned `d`) with streaming stores: the batch leaves by DMA and is never read back by this core,
+// so the stores skip the read-for-ownership a cached copy pays per line (about half the push
+// path's per-packet time at C2).  The caller fences before publishing the slot.
+static void stream_slot(uint8_t* d, const char* p, uint32_t n, uint64_t slot) {
+    alignas(16) uint8_t t[16];
+    memset(t, 0, sizeof(t));
+    const uint32_t h = std::min<uint32_t>(n, 12);
+    memcpy(t + 4, p, h);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d), _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
+    uint64_t off = 16;
+    const char* s = p + h;
+    uint32_t left = n - h;
+    for (; left >= 16; left -= 16, s += 16, off += 16)
+        _mm_stream_si128(reinterpret_cast<__m128i*>(d + off), _mm_loadu_si128(reinterpret_cast<const __m128i*>(s)));
+    if (off < slot) {                                      // the last bytes and the zero pad
+        memset(t, 0, sizeof(t));
+        memcpy(t, s, left);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(d + off), _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
+    }
+}
+
 // Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
 // filled: the only host copy of the packet.  Under its stripe's lock the pusher reserves the slot
 // in the stripe's slab (a new 64-KiB slab from the blob when it is full); it copies the packet
@@ -235,9 +258,8 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
         sp = &st;
         break;
     }
-    memset(d, 0, 4);
-    memcpy(d + 4, packet, clamped);
-    if (slot > clamped + 4) memset(d + 4 + clamped, 0, slot - clamped - 4);
+    stream_slot(d, packet, clamped, slot);
+    _mm_sfence();                                        // the slot is complete before it is published
     if (pend) pend->fetch_sub(1, std::memory_order_release);
     sp->copying.fetch_sub(1, std::memory_order_release);
 }

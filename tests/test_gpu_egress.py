@@ -212,7 +212,8 @@ def test_paced_egress_matches_the_reference_server_gate(name, oracle_bins, tmp_p
     want = _gate_reference(tr, report, oracle_bins["ref"], tmp_path)
     got = capture_summary(read_capture(cap))
     bad = [k for k in want if got.get(k) != want[k]]
-    assert not bad, f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}"
+    assert not bad, (f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}; "
+                     f"{len(report)} socket blocks, e.g. {report[:12]}")
 
 
 @pytest.mark.gpu
@@ -233,10 +234,15 @@ def test_paced_egress_thins_congested_tcp_audio_like_the_reference(seconds, orac
     lo, hi = ticks[len(ticks) // 6], ticks[5 * len(ticks) // 6]
     hold = {t: tcp_subs for t in ticks if lo <= t < hi}
     report, stats = [], []
-    cap, _ = replay(tr, sockets={"threads": 2, "tcp_sndbuf": 4096, "hold": hold, "pacing": {}, "report": report,
-                                 "stats": stats})
+    os.environ["EDGPU_PACE_TRACE"] = "400"
+    try:
+        cap, _ = replay(tr, sockets={"threads": 2, "tcp_sndbuf": 4096, "hold": hold, "pacing": {}, "report": report,
+                                     "stats": stats})
+    finally:
+        del os.environ["EDGPU_PACE_TRACE"]
     assert report, "no write blocked: the test did not congest the connections"
-    assert sum(s.stale_dropped for s in stats) > 0, "no packet went stale: thinning was not exercised"
+    assert sum(s.stale_dropped for s in stats) > 0, \
+        f"no packet went stale: thinning was not exercised ({len(report)} socket blocks, e.g. {report[:8]})"
     want = _gate_reference(tr, report, oracle_bins["ref"], tmp_path)
     got = capture_summary(read_capture(cap))
     bad = [k for k in want if got.get(k) != want[k]]
