@@ -904,5 +904,11 @@ int main(int argc, char** argv) {
         fclose(t);
     }
     fprintf(stderr, "ref_harness: %zu subs, %lu asserts logged\n", subs.size(), logger.count);
+    if (g_gate) {                              // the write gate's stale drops (fStalePacketsDropped)
+        unsigned long long stale = 0;
+        for (auto& sb : subs)
+            for (FakeObj* st : sb.streams) stale += st->stale_dropped;
+        fprintf(stderr, "ref_harness: gate stale_dropped %llu\n", stale);
+    }
     return 0;
 }
