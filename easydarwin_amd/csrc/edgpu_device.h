@@ -142,6 +142,9 @@ struct SessionDev {
     // inFilterSSRCs / inTimeout, QTSSReflectorModule.cpp:1457 -> ReflectorStream.cpp:1732-1767)
     uint32_t ssrc_filter;           // use_one_SSRC_per_stream
     uint32_t ssrc_timeout_s;        // timeout_stream_SSRC_secs
+    // a backpressure report relocated an output (Q9) since edgpu_session_relocations last read
+    // it: on a replica, the owner's next audio packet must become the audio anchor
+    uint32_t relocated;
 };
 
 struct SubDev {                     // one sub-stream: subscriber x sender

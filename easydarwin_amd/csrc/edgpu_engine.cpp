@@ -904,9 +904,10 @@ static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms
             Readback rb(x);
             HIP_CHECK(rb.add(d, x->d_senders.ptr + q[t].rtp_sender, 2 * sizeof(SenderDev)));
             HIP_CHECK(rb.run());
-            fprintf(stderr, "play now=%lld track=%u cutoff=%lld head=%llu/%llu found=%u seq=%u\n", (long long)now_ms, t,
-                    (long long)q[t].cutoff, (unsigned long long)d[0].head, (unsigned long long)d[1].head, r[t].found,
-                    r[t].seq);
+            fprintf(stderr, "play now=%lld track=%u cutoff=%lld head=%llu/%llu found=%u seq=%u key=%lld new_start=%lld "
+                    "tail=%llu floor=%llu\n", (long long)now_ms, t, (long long)q[t].cutoff, (unsigned long long)d[0].head,
+                    (unsigned long long)d[1].head, r[t].found, r[t].seq, (long long)d[0].key, (long long)d[0].new_start,
+                    (unsigned long long)d[0].tail, (unsigned long long)d[0].floor);
         }
     }
     for (uint32_t t = 0; t < sh.ntracks; t++) {
@@ -1964,7 +1965,19 @@ int edgpu_session_export(edgpu_ctx* x, const uint32_t* sessions, uint32_t n, int
     offsets[n] = base;
     if (!dst) return EDGPU_OK;                         // size query
     if (base > cap) return fail(EDGPU_OUT_OVERFLOW, "image buffer too small");
-    return image_launch(x, plan, now_ms, (uint8_t*)dst, 1);
+    r = image_launch(x, plan, now_ms, (uint8_t*)dst, 1);
+    if (!r && getenv("EDGPU_DEBUG_PLAY")) {              // debugging: the exported senders' key pointers
+        for (const ImgPlan& E : plan) {
+            SenderDev d;
+            Readback rb(x);
+            HIP_CHECK(rb.add(&d, x->d_senders.ptr + E.sender, sizeof(SenderDev)));
+            HIP_CHECK(rb.run());
+            fprintf(stderr, "export now=%lld session=%u ls=%u from=%lld floor=%llu head=%llu key=%lld\n", (long long)now_ms,
+                    E.session, E.ls, (long long)E.from, (unsigned long long)E.floor, (unsigned long long)d.head,
+                    (long long)d.key);
+        }
+    }
+    return r;
 }
 
 int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offsets, uint32_t n,
@@ -1989,6 +2002,44 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     if (plan.empty()) return EDGPU_OK;
     if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
     return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);
+}
+
+// Replica feedback: relocations made on this context's sessions since the last call (read and
+// cleared), and the owner's side, ReflectorSession::SetHasVideoKeyFrameUpdate(true).
+int edgpu_session_relocations(edgpu_ctx* x, const uint32_t* sessions, uint32_t n, uint8_t* out) {
+    if (!x || (n && (!sessions || !out))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    for (uint32_t i = 0; i < n; i++)
+        if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (!n) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    std::vector<uint32_t> v(n, 0);
+    {
+        Readback rb(x);                               // after the backpressure reports (same stream)
+        for (uint32_t i = 0; i < n; i++) HIP_CHECK(rb.add(&v[i], &x->d_sessions.ptr[sessions[i]].relocated, sizeof(uint32_t)));
+        HIP_CHECK(rb.run());
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        out[i] = v[i] ? 1 : 0;
+        if (v[i]) HIP_CHECK(hipMemsetAsync(&x->d_sessions.ptr[sessions[i]].relocated, 0, sizeof(uint32_t), x->stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    return EDGPU_OK;
+}
+
+int edgpu_session_key_update(edgpu_ctx* x, const uint32_t* sessions, uint32_t n) {
+    if (!x || (n && !sessions)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
+    for (uint32_t i = 0; i < n; i++)
+        if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    if (!n) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    static const uint32_t one = 1;
+    // on the stream the keyframe index runs on: the next batch's k_keyframe reads it
+    for (uint32_t i = 0; i < n; i++)
+        HIP_CHECK(hipMemcpyAsync(&x->d_sessions.ptr[sessions[i]].video_key_flag, &one, sizeof(one), hipMemcpyHostToDevice,
+                                 x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    return EDGPU_OK;
 }
 
 int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {

@@ -1222,6 +1222,7 @@ __global__ void k_blocked(BlockedParams P) {
     if (P.now - mx.arrival > P.relocate_ms && D.key >= 0 && meta[(uint64_t)D.key & D.pk_mask].arrival > mx.arrival) {
         bm = D.key;
         atomicExch(&P.sessions[D.session].video_key_flag, 1u);
+        atomicExch(&P.sessions[D.session].relocated, 1u);
     }
     Q.bookmark = bm;
     Q.resume_at = 1;

@@ -84,3 +84,21 @@ def exchange_images(requests, export_fn, import_fn, make_buf, world: int, rank: 
     sent = sum(o[-1] for _, _, o in outgoing.values())
     recv = sum(o[-1] for _, o, _ in incoming.values())
     return sent, recv
+
+
+def route_relocations(relocated, key_update_fn, world: int, rank: int):
+    """The replicas' feedback to the owners: a relocation on a replica (Q9,
+    ReflectorSender::NeedRelocateBookMark -> ReflectorSession::SetHasVideoKeyFrameUpdate,
+    ReflectorStream.cpp:1311-1317) must set the owner's flag before the owner's next keyframe
+    index, so the session's next audio packet becomes its audio key pointer (:1913-1930).
+
+    relocated      global sessions this rank's replicas relocated an output of (since the last call)
+    key_update_fn  (global sessions owned here) -> None; sets their flag (edgpu_session_key_update)
+
+    Collective (all_gather_object of a few integers).  Returns the owned sessions updated."""
+    lists = [None] * world
+    dist.all_gather_object(lists, sorted(int(g) for g in relocated))
+    mine = sorted({g for lst in lists for g in lst if owner(g, world) == rank})
+    if mine:
+        key_update_fn(mine)
+    return mine

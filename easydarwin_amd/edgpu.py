@@ -29,7 +29,8 @@ EXPORTED = [
     "edgpu_subscriber_add", "edgpu_subscriber_remove", "edgpu_ingest", "edgpu_keyframe_index",
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
-    "edgpu_session_export", "edgpu_session_import", "edgpu_memcpy_peer", "edgpu_device_alloc",
+    "edgpu_session_export", "edgpu_session_import", "edgpu_session_relocations", "edgpu_session_key_update",
+    "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
     "edgpu_egress_create", "edgpu_egress_destroy", "edgpu_egress_last_error", "edgpu_egress_udp",
@@ -208,6 +209,8 @@ def load(path: str = LIB_PATH):
         "edgpu_gop_copy": (I32, [P, U32, U32, P, U64, C.POINTER(U64), C.POINTER(U32)]),
         "edgpu_session_export": (I32, [P, P, U32, I64, P, P, U64, P, P]),
         "edgpu_session_import": (I32, [P, P, P, U32, P]),
+        "edgpu_session_relocations": (I32, [P, P, U32, P]),
+        "edgpu_session_key_update": (I32, [P, P, U32]),
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
@@ -529,6 +532,19 @@ class Context:
         if len(offsets) != len(sess) + 1:
             raise ValueError("offsets must have len(sessions) + 1 entries")
         _check(self.lib.edgpu_session_import(self.h, C.c_void_p(images_ptr), _ptr(offsets), len(sess), _ptr(sess)))
+
+    def session_relocations(self, sessions) -> list:
+        """Sessions (of `sessions`, on this context) whose outputs a backpressure report relocated
+        since the last call (a replica's feedback for its owner); the indication is cleared."""
+        sess = np.ascontiguousarray(sessions, dtype=np.uint32)
+        out = np.zeros(max(len(sess), 1), dtype=np.uint8)
+        _check(self.lib.edgpu_session_relocations(self.h, _ptr(sess), len(sess), _ptr(out)))
+        return [int(x) for x, f in zip(sess, out) if f]
+
+    def session_key_update(self, sessions):
+        """The owner's side: ReflectorSession::SetHasVideoKeyFrameUpdate(true) on `sessions`."""
+        sess = np.ascontiguousarray(sessions, dtype=np.uint32)
+        _check(self.lib.edgpu_session_key_update(self.h, _ptr(sess), len(sess)))
 
     def memcpy_peer(self, dst_ptr: int, src_device: int, src_ptr: int, nbytes: int):
         _check(self.lib.edgpu_memcpy_peer(self.h, C.c_void_p(dst_ptr), int(src_device), C.c_void_p(src_ptr), int(nbytes)))

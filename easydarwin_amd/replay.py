@@ -276,6 +276,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             if unread is not None and sink is not None:
                 c, r, tt, _ = unread
                 sink.tick(r, tt)
+                if link is not None and c is rep:
+                    link.feedback()
                 st = c.stats()
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
                 unread = None
@@ -293,6 +295,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 npass = c.read_passes(r, consume)
                 if reports:
                     c.fanout_blocked(reports)
+                if link is not None and c is rep:
+                    link.feedback()                 # the replica's relocations reach the owner
                 st = c.stats()
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
                 # (relayed_packets before the backpressure reports take the unsent ones off)
@@ -319,7 +323,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         clock = 0                           # the harness's virtual clock: max event time so far
         plan = None
         if interleaved is not None:
-            bl, barriers = _batches(trace, rep is None)
+            bl, barriers = _batches(trace, True)
             plan = tcp_plan(bl, interleaved, barriers=barriers)
         nflush = 0
 

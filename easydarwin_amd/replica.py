@@ -81,6 +81,21 @@ class ReplicaLink:
         self.bytes_shipped += total
         return total
 
+    def feedback(self) -> list:
+        """Relocations on the replica sessions since the last call (a backpressure report moved an
+        output to the newest key frame) set the owners' video-key-update flag, so the owner's next
+        audio packet becomes the session's audio key pointer as in the reference
+        (edgpu_session_relocations -> edgpu_session_key_update).  Call it after the replica's
+        backpressure reports and before the owner's next keyframe index.  Returns the owner
+        sessions updated."""
+        if not self.pairs:
+            return []
+        hit = set(self.replica.session_relocations([r for _, r in self.pairs]))
+        upd = sorted({o for o, r in self.pairs if r in hit})
+        if upd:
+            self.owner.session_key_update(upd)
+        return upd
+
 
 class DistReplicaLink:
     """The one-process-per-GPU form of ReplicaLink: the owner of global session g is rank
@@ -139,3 +154,15 @@ class DistReplicaLink:
         self.bytes_sent += sent
         self.bytes_received += recv
         return sent, recv
+
+    def feedback(self) -> list:
+        """ReplicaLink.feedback across ranks (dist.route_relocations): this rank's replicas'
+        relocations go to the owners, and the owned sessions other ranks relocated get their
+        flag set here.  Collective; call it after the replicas' backpressure reports and before
+        the owners' next keyframe index.  Returns the owned global sessions updated."""
+        from .dist import route_relocations
+        g_of = {v: g for g, v in self.replica_of.items()}
+        hit = self.ctx.session_relocations(sorted(g_of)) if g_of else []
+        return route_relocations([g_of[s] for s in hit],
+                                 lambda gs: self.ctx.session_key_update([self.local_of[g] for g in gs]),
+                                 self.world, self.rank)

@@ -708,6 +708,17 @@ int  edgpu_session_export(edgpu_ctx* ctx, const uint32_t* sessions, uint32_t n, 
  * or out-of-order image, EDGPU_RING_OVERFLOW if the replica's rings are too small.  Syncs. */
 int  edgpu_session_import(edgpu_ctx* ctx, const void* images, const uint64_t* offsets, uint32_t n,
                           const uint32_t* sessions);
+/* Replica feedback (Q9 on a replica).  A backpressure report that relocates an output's bookmark
+ * to the newest key frame sets the session's video-key-update flag
+ * (ReflectorSender::NeedRelocateBookMark -> ReflectorSession::SetHasVideoKeyFrameUpdate(true),
+ * ReflectorStream.cpp:1311-1317), and the session's next audio packet becomes the audio key
+ * pointer (:1913-1930).  A replica session does not ingest: its relocations must reach the owner
+ * before the owner's next edgpu_keyframe_index.  edgpu_session_relocations: out[i] = 1 when a
+ * relocation happened on sessions[i] (of this context) since the last call; the indication is
+ * cleared.  edgpu_session_key_update: sets the flag on the owner's sessions (not while an ingest
+ * awaits its keyframe index). */
+int  edgpu_session_relocations(edgpu_ctx* ctx, const uint32_t* sessions, uint32_t n, uint8_t* out);
+int  edgpu_session_key_update(edgpu_ctx* ctx, const uint32_t* sessions, uint32_t n);
 
 /* Enqueues a device-to-device copy from GPU `src_device` into this context's GPU on the
  * context stream (hipMemcpyPeerAsync over xGMI; a plain device copy when the devices are

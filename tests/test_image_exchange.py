@@ -88,3 +88,35 @@ def test_exchange_routes_images(world):
             total_sent += sent
             total_recv += recv
     assert total_sent == total_recv > 0
+
+
+def _reloc_worker(rank, world, port, out_q):
+    import torch.distributed as dist
+    from easydarwin_amd.dist import route_relocations
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = []
+    # rank r's replicas relocated outputs of the sessions g with g % (r + 2) == 0 it does not own
+    mine = [g for g in range(N_SESS) if g % (rank + 2) == 0 and owner(g, world) != rank]
+    upd = route_relocations(mine, got.extend, world, rank)
+    out_q.put((rank, mine, upd, sorted(got)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_relocations_reach_the_owners(world):
+    """Replica feedback (dist.route_relocations): every relocation a rank's replica reports
+    reaches the session's owner once, and nothing else is updated."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reloc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (m, u, g) for r, m, u, g in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    reported = {g for m, _, _ in res.values() for g in m}
+    for r, (_, upd, got) in res.items():
+        want = sorted(g for g in reported if owner(g, world) == r)
+        assert upd == want and got == want

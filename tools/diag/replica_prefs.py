@@ -11,7 +11,7 @@ from test_gpu_parity import _fixture
 
 tr = SCENARIOS["prefs_buffer"]()
 gold = _fixture("prefs_buffer")["substreams"]
-for mode in (None, "all", "late"):
+for mode in (None, "all"):
     print("=== mode", mode, flush=True)
     cap, _ = replay(tr, replica=mode)
     g = capture_summary(read_capture(cap))
