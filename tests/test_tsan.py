@@ -10,6 +10,10 @@ edgpu_ingest_prestage, the gather thread and four write threads (``--bench`` wit
 pushes), and session teardown / prefs rereads / backpressure with manual ticks.  The relayed bytes
 are the stand-in's and are not compared (the GPU tests pin them); any ThreadSanitizer report, or a
 non-zero exit, fails.
+
+The same runs also go through an AddressSanitizer + UndefinedBehaviorSanitizer build (``make
+SAN=address``, leak checking on): out-of-bounds and use-after-free in the striped push path, the
+pinned blob's growth, the gather parts and the teardown paths, and undefined behaviour.
 """
 import os
 import shutil
@@ -27,18 +31,24 @@ pytestmark = pytest.mark.skipif(not os.path.exists(CLANG) or not shutil.which("m
                                 reason="LLVM clang++ (TSan runtime) not in this image")
 
 
-@pytest.fixture(scope="module")
-def tsan_build():
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tsan"), "-j4"], capture_output=True, text=True,
-                       timeout=600)
+@pytest.fixture(scope="module", params=["thread", "address"])
+def tsan_build(request):
+    san = request.param
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tsan"), "-j4", f"SAN={san}"], capture_output=True,
+                       text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    return os.path.join(BUILD, "qtss_replay"), os.path.join(BUILD, "libQTSSReflectorModule.so")
+    b = BUILD if san == "thread" else f"{BUILD}_{san}"
+    return os.path.join(b, "qtss_replay"), os.path.join(b, "libQTSSReflectorModule.so")
 
 
 def _run(args, env_extra, tmp_path):
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=66 second_deadlock_stack=1", **env_extra)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=66 second_deadlock_stack=1",
+               # (verify_asan_link_order=0: a preloaded library may come before the ASan runtime)
+               ASAN_OPTIONS="detect_leaks=1 exitcode=67 verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1 halt_on_error=1", **env_extra)
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env, cwd=tmp_path)
-    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    for tool in ("ThreadSanitizer", "AddressSanitizer", "LeakSanitizer", "runtime error:"):
+        assert tool not in r.stderr, r.stderr[-6000:]
     assert r.returncode == 0, r.stderr[-3000:]
     return r
 
