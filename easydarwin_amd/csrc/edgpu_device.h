@@ -145,7 +145,12 @@ struct SessionDev {
     // a backpressure report relocated an output (Q9) since edgpu_session_relocations last read
     // it: on a replica, the owner's next audio packet must become the audio anchor
     uint32_t relocated;
+    // sticky stream errors (kStreamRingOverflow: a packet an output still needed, or the key frame
+    // a new output starts at, fell out of a sender ring); the session's own outputs lose packets,
+    // the tick goes on for every other session.  Read and cleared by edgpu_stream_errors.
+    uint32_t errors;
 };
+constexpr uint32_t kStreamRingOverflow = 1u;
 
 struct SubDev {                     // one sub-stream: subscriber x sender
     uint32_t handle;                // subscriber handle
@@ -276,7 +281,7 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned int pass_desc[2];
     unsigned int pass_next[2];
     unsigned int pass_slot;         // slot of the last launched pass
-    unsigned int _pad3;
+    unsigned int stream_errors;     // sessions newly marked with a stream error by this tick
     unsigned long long cum_lost_passes;   // passes a tick still owed when the next tick was planned
 };
 constexpr uint32_t kNoPass = 0xFFFFFFFFu;

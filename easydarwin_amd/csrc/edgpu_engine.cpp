@@ -1546,6 +1546,7 @@ static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
     p.blk_maxb = x->d_blk_maxb.ptr; p.blk_maxc = x->d_blk_maxc.ptr;
+    p.sessions = x->d_sessions.ptr;
     p.totals = x->d_totals;
     p.T.now = now_ms;
     p.T.over_buffer_ms = (int64_t)x->cfg.reflector_buffer_size_sec * 1000;
@@ -1684,7 +1685,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->pass_packets = t.pass_desc[slot];
     out->pass = x->pass_ord;
     out->more_passes = (x->fanout_launches && t.pass_next[slot] != kNoPass) ? 1u : 0u;
-    out->_pad2 = 0;
+    out->stream_errors = t.stream_errors;
     if (x->fanout_launches) x->passes_more = (int)out->more_passes;
 #ifdef EDGPU_AB_VARIANTS
     if (getenv("EDGPU_FAN_TAIL") && t.fan_done_max > t.fan_t0_min)   // 100-MHz s_memrealtime ticks
@@ -2002,6 +2003,35 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     if (plan.empty()) return EDGPU_OK;
     if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
     return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);
+}
+
+// Per-stream isolation: the sessions a tick marked, read and cleared.
+int edgpu_stream_errors(edgpu_ctx* x, uint32_t* sessions, int32_t* codes, uint32_t cap, uint32_t* n) {
+    if (!x || !n || (cap && (!sessions || !codes))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    *n = 0;
+    const uint32_t ns = (uint32_t)x->sessions.size();
+    if (!ns) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    HIP_CHECK(sync_all(x));
+    std::vector<SessionDev> sd(ns);
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(sd.data(), x->d_sessions.ptr, ns * sizeof(SessionDev)));
+        HIP_CHECK(rb.run());
+    }
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        if (!sd[s].errors || !x->sessions[s].alive) continue;
+        if (k < cap) {
+            sessions[k] = s;
+            codes[k] = EDGPU_RING_OVERFLOW;
+            HIP_CHECK(hipMemsetAsync(&x->d_sessions.ptr[s].errors, 0, sizeof(uint32_t), x->stream));
+        }
+        k++;
+    }
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    *n = k;
+    return EDGPU_OK;
 }
 
 // Replica feedback: relocations made on this context's sessions since the last call (read and

@@ -816,7 +816,7 @@ __device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, ui
 // (ReflectorStream.cpp:1058-1069).
 __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
-    t->status = 0; t->nwork = 0; t->fan_next = 0;
+    t->status = 0; t->nwork = 0; t->fan_next = 0; t->stream_errors = 0;
     t->fan_t0_min = ~0ull; t->fan_done_min = ~0ull; t->fan_done_max = 0;
     // a pass the previous tick still owed is lost now (its host never called edgpu_fanout_next)
     if (t->pass_next[t->pass_slot & 1u] != kNoPass) t->cum_lost_passes++;
@@ -831,6 +831,12 @@ __global__ void k_totals_reset(TickTotals* t, int which) {
     if (threadIdx.x != 0) return;
     if (which == 0) reset_tick_totals(t);
     else mark_ingest_totals(t);
+}
+
+// A sender ring lost a packet an output of its session needed (per-stream isolation: the
+// session is marked, the tick goes on).
+__device__ __forceinline__ void mark_stream_error(const PlanParams& P, uint32_t session) {
+    if (atomicOr(&P.sessions[session].errors, kStreamRingOverflow) == 0u) atomicAdd(&P.totals->stream_errors, 1u);
 }
 
 __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
@@ -894,15 +900,15 @@ __global__ __launch_bounds__(256) void k_plan_subs(PlanParams P) {
                 if (Q.rtp_info && Q.kind == 0 && !Q.has_last && (Q.sent_any || P.subs[q + 1].sent_any))
                     a = (uint64_t)Q.bookmark;
                 have = true;
-                if (a < D.tail && a < head) { atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW); a = D.tail; }
+                if (a < D.tail && a < head) { mark_stream_error(P, D.session); a = D.tail; }
             } else if (D.new_start >= 0) {             // new output: key pointer / buffer start
                 a = (uint64_t)D.new_start;
                 have = true;
                 if (Q.has_last)                        // PacketAlreadySent for a re-joined output
                     a = lower_bound_meta(meta, D.pk_mask, a, head,
                                          [&](const PktMeta& m) { return m.id > Q.last_id; });
-            } else if (D.new_start == -2) {
-                atomicExch(&P.totals->status, EDGPU_RING_OVERFLOW);
+            } else if (D.new_start == -2) {               // retried next tick (still a new output)
+                mark_stream_error(P, D.session);
             }
             if (have) {
                 // FilterPacket (RTPSessionOutput.cpp:249-280, Q10): until the client stream's

@@ -92,6 +92,7 @@ struct PlanParams {
     uint32_t* blk_count;
     uint64_t* blk_maxb;         // per K2 block: the largest sub-stream (bytes, descriptors)
     uint32_t* blk_maxc;
+    SessionDev* sessions;       // stream errors (per-session isolation)
     TickTotals* totals;
     TickParams T;
 };

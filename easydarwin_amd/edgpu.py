@@ -30,6 +30,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_session_relocations", "edgpu_session_key_update",
+    "edgpu_stream_errors",
     "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
@@ -108,7 +109,7 @@ class TickStats(C.Structure):
                 ("arena_bytes", C.c_uint64), ("ingested_packets", C.c_uint64),
                 ("ingested_bytes", C.c_uint64), ("status", C.c_int32), ("nwork", C.c_uint32),
                 ("pass_arena_bytes", C.c_uint64), ("pass_packets", C.c_uint32), ("pass_", C.c_uint32),
-                ("more_passes", C.c_uint32), ("_pad2", C.c_uint32)]
+                ("more_passes", C.c_uint32), ("stream_errors", C.c_uint32)]
 
 
 class EgressStats(C.Structure):
@@ -211,6 +212,7 @@ def load(path: str = LIB_PATH):
         "edgpu_session_import": (I32, [P, P, P, U32, P]),
         "edgpu_session_relocations": (I32, [P, P, U32, P]),
         "edgpu_session_key_update": (I32, [P, P, U32]),
+        "edgpu_stream_errors": (I32, [P, P, P, U32, P]),
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
@@ -540,6 +542,16 @@ class Context:
         out = np.zeros(max(len(sess), 1), dtype=np.uint8)
         _check(self.lib.edgpu_session_relocations(self.h, _ptr(sess), len(sess), _ptr(out)))
         return [int(x) for x, f in zip(sess, out) if f]
+
+    def stream_errors(self) -> list:
+        """[(session, code)] the ticks marked since the last call (edgpu_stream_errors); clears them."""
+        n = C.c_uint32()
+        _check(self.lib.edgpu_stream_errors(self.h, None, None, 0, C.byref(n)))      # how many
+        cap = max(n.value, 1)
+        ss = np.zeros(cap, dtype=np.uint32)
+        cs = np.zeros(cap, dtype=np.int32)
+        _check(self.lib.edgpu_stream_errors(self.h, _ptr(ss), _ptr(cs), cap, C.byref(n)))
+        return [(int(a), int(b)) for a, b in zip(ss[:min(n.value, cap)], cs[:min(n.value, cap)])]
 
     def session_key_update(self, sessions):
         """The owner's side: ReflectorSession::SetHasVideoKeyFrameUpdate(true) on `sessions`."""

@@ -182,7 +182,9 @@ typedef struct edgpu_tick_stats {
     uint64_t ingested_packets;  /* the batch the last edgpu_keyframe_index indexed (the counters
                                    move at the index, not at edgpu_ingest) */
     uint64_t ingested_bytes;
-    int32_t  status;            /* sticky device-side error (EDGPU_RING_OVERFLOW, ...) */
+    int32_t  status;            /* device-side error of the whole tick (EDGPU_OUT_OVERFLOW, ...); a
+                                   ring that lost a packet one session needed marks that session
+                                   instead (stream_errors) */
     uint32_t _pad;
     /* the current copy pass (edgpu_fanout_next): arena bytes and descriptors the result's
      * sub-streams span, its ordinal (0 = the pass edgpu_fanout launched) and whether another
@@ -191,7 +193,9 @@ typedef struct edgpu_tick_stats {
     uint32_t pass_packets;
     uint32_t pass;
     uint32_t more_passes;
-    uint32_t _pad2;
+    /* sessions the tick newly marked with a stream error (edgpu_stream_errors): their outputs
+     * lost packets, every other session's went out as usual */
+    uint32_t stream_errors;
 } edgpu_tick_stats;
 
 typedef struct edgpu_ctx edgpu_ctx;
@@ -584,6 +588,15 @@ typedef struct edgpu_egress_block {
     uint32_t substream, sent, written, cause;
 } edgpu_egress_block;
 int  edgpu_egress_block_info(edgpu_egress* eg, edgpu_egress_block* out, uint32_t cap, uint32_t* n);
+
+/* Per-stream error isolation (a bad stream marks that stream, not the batch).  A
+ * sender ring too small for what a session's outputs still need -- a blocked output's bookmark
+ * or a new output's key frame overwritten by newer packets (the reference's queue is unbounded,
+ * ReflectorStream.cpp:1088-1120) -- marks the session; its outputs resume at the oldest packet
+ * still held (a new output waits for the next tick), and every other session's tick is
+ * unaffected.  Lists the marked live sessions (code EDGPU_RING_OVERFLOW) and clears the marks of
+ * those returned; *n = how many are marked.  Syncs. */
+int  edgpu_stream_errors(edgpu_ctx* ctx, uint32_t* sessions, int32_t* codes, uint32_t cap, uint32_t* n);
 
 int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs; EDGPU_ERR while an
                                                                        ingest awaits its index */

@@ -1,0 +1,68 @@
+"""GPU: per-stream error isolation (a bad stream marks that stream, not the batch).
+
+The reference's sender queues are unbounded lists (ReflectorStream.cpp:1088-1120); the engine's
+sender rings are sized by edgpu_config.  A session whose ring is too small for what one of its
+outputs still needs -- here a TCP player held for 3 s on a 2-Mb/s stream whose video ring holds
+256 packets (~1.2 s), under a relocation threshold that does not move it first -- loses packets
+on that output.  That marks the session (edgpu_stream_errors, edgpu_tick_stats.stream_errors),
+and nothing else: every tick goes on, and every other output, of that session and of the other
+session, is byte-identical to the reference reflector's (oracle/_ref/ref_harness) on the same
+trace and budgets.
+"""
+import os
+import subprocess
+
+import pytest
+
+from easydarwin_amd import edgpu
+from easydarwin_amd.replay import replay
+from easydarwin_amd.synth import SEED_BASE, TrackSpec, make_sdp, session_packets
+from easydarwin_amd.trace import TCP, UDP, Trace, capture_summary, pref_values, read_capture
+from scenarios import _assemble
+
+HELD = 2                                   # the TCP player of session 0 the test holds
+
+
+def _trace() -> Trace:
+    s0 = [TrackSpec("video", "H264/90000", 96, bitrate=2_000_000, gop=30, idr_bytes=20_000),
+          TrackSpec("audio", "PCMA/8000", 8)]
+    s1 = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=30, idr_bytes=4_000),
+          TrackSpec("audio", "PCMU/8000", 0)]
+    tr = Trace()
+    # relocation only after 5 s (ReflectorStream.cpp:101-102): the held output falls behind the ring first
+    tr.prefs = {"rtp_reflector_threshold_msec": "5000"}
+    tr.add_session(make_sdp(s0))
+    tr.add_session(make_sdp(s1))
+    pk0 = session_packets(s0, 6000, SEED_BASE + 90)
+    pk1 = session_packets(s1, 6000, SEED_BASE + 91)
+    joins = [(0, 0, 1, UDP), (0, 0, HELD, TCP), (0, 1, 3, UDP), (0, 1, 4, TCP), (2500, 0, 5, UDP)]
+    blocks = {t: [(HELD, 0, 0, 0), (HELD, 1, 0, 0)] for t in range(1000, 4000, 100)}
+    return _assemble(tr, [pk0, pk1], 100, 6000, joins, blocks=blocks)
+
+
+@pytest.mark.gpu
+def test_ring_overflow_marks_one_session_and_the_tick_goes_on(oracle_bins, tmp_path):
+    if oracle_bins["ref"] is None:
+        pytest.skip("oracle/_ref/ref_harness not built")
+    tr = _trace()
+    pv = pref_values(tr.prefs)
+    ctx = edgpu.Context(video_ring_packets=256, video_ring_bytes=1 << 20,
+                        reflector_buffer_size_sec=int(pv["reflector_buffer_size_sec"]),
+                        rtp_reflector_threshold_msec=max(1000, int(pv["rtp_reflector_threshold_msec"])),
+                        reflector_rtp_info_offset_msec=int(pv["reflector_rtp_info_offset_msec"]) or edgpu.FALSE)
+    try:
+        cap, _ = replay(tr, ctx=ctx)                      # no tick fails
+        marked = ctx.stream_errors()
+        assert marked == [(0, edgpu.RING_OVERFLOW)], marked
+        assert ctx.stream_errors() == []                  # read and cleared
+    finally:
+        ctx.close()
+    p, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    tr.write(str(p))
+    subprocess.run([oracle_bins["ref"], str(p), str(c)], check=True, stderr=subprocess.DEVNULL, env=dict(os.environ))
+    want = capture_summary(read_capture(c.read_bytes()))
+    got = capture_summary(read_capture(cap))
+    held = [k for k in want if k.startswith(f"{HELD}/")]
+    assert held and any(got.get(k) != want[k] for k in held), "the held output lost nothing: no overflow"
+    bad = [k for k in want if not k.startswith(f"{HELD}/") and got.get(k) != want[k]]
+    assert not bad, f"{len(bad)} other sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}"
