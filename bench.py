@@ -620,6 +620,12 @@ def main():
                           f"from {extra} steps after them"),
         "ingest": ingest,
         "cpu_baseline": cpu,
+        # the metric counts packets made send-ready in HBM; what reaches sockets is host-bound
+        # (sendmmsg / writev over PCIe-copied bytes): tools/bench_egress.py, DESIGN.md §5.6
+        "wire_note": ("value counts relayed packets made send-ready in HBM (the north_star metric); on sockets "
+                      "the engine's egress is host-bound: tools/bench_egress.py, 41 M datagrams/s with UDP GSO "
+                      "and ~7 M in reference-exact one-datagram-per-send mode vs the reference's ~7.7 M "
+                      "(profiles/r04_bench/bench_egress.json, DESIGN.md 5.6)"),
     }
     print(json.dumps(res), flush=True)
     if dist:

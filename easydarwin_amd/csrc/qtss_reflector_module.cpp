@@ -78,6 +78,7 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -219,6 +220,14 @@ struct Module {
     std::vector<std::unique_ptr<Output>> outputs;
     int32_t rtpInfoWaitLoops = 10;      // sWaitTimeLoopCount: 100-ms PLAY retries before 404
     uint32_t tickMs = 20;
+    // EDGPU_QTSS_REFLECT_ON_ARRIVAL=<ms>: reflect as soon as packets are waiting, at most every
+    // <ms> (the reference reflects a sender when its socket task wakes on new packets,
+    // ReflectorStream.cpp:573, 603-618, 1676-1714); tickMs stays the longest interval.  0: a tick
+    // every tickMs.
+    uint32_t arrivalMinMs = 0;
+    std::atomic<bool> pending{false};   // a packet arrived since the last tick took the batch
+    std::mutex wakeMu;
+    std::condition_variable wake;
     // ReflectorStream::Initialize's prefs (read once, at Initialize)
     int64_t overBufferMs = 1000;        // sOverBufferInMsec (reflector_buffer_size_sec x 1000)
     int64_t bucketDelayMs = 73;         // sBucketDelayInMsec (reflector_bucket_offset_delay_msec)
@@ -468,6 +477,16 @@ bool BindPair(uint16_t port, UdpPair* out) {
     return false;
 }
 
+// A packet reached the batch: in reflect-on-arrival mode the first one after a tick wakes the
+// ticker (later ones only read the flag: no shared-line writes per packet).
+inline void NotifyArrival() {
+    if (!M->arrivalMinMs || M->pending.load(std::memory_order_relaxed)) return;
+    if (!M->pending.exchange(true, std::memory_order_acq_rel)) {
+        std::lock_guard<std::mutex> g(M->wakeMu);
+        M->wake.notify_one();
+    }
+}
+
 // ReflectorSocket::GetIncomingData (ReflectorStream.cpp:1716-1735): every datagram waiting on a
 // UDP push socket, read like RecvFrom into a kMaxReflectorPacketSize (2060) buffer -- a longer
 // datagram is truncated there -- and handed to the engine with its source address (the UDP RTCP
@@ -492,6 +511,7 @@ uint32_t DrainUDP() {
                 if (r == 0) continue;
                 M->R->ProcessUDPPacket(u.engine, u.track, k == 1, buf, (uint32_t)r, ntohl(from.sin_addr.s_addr),
                                        ntohs(from.sin_port), Milliseconds());
+                NotifyArrival();
                 n++;
             }
         }
@@ -519,6 +539,7 @@ QTSS_Error Tick() {
     const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(M->mu);
     if (!M->R) return QTSS_RequestFailed;
+    M->pending.store(false, std::memory_order_release);   // this tick takes what arrived so far
     QTSSSink sink;
     sink.now = Milliseconds();
     const int err = M->R->ReflectPackets(sink.now, &sink);
@@ -584,6 +605,7 @@ void ReadModulePrefsLocked() {
 QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     std::lock_guard<std::mutex> g(M->mu);
     if (const char* v = getenv("EDGPU_QTSS_TICK_MSEC")) M->tickMs = (uint32_t)std::max(1, atoi(v));
+    if (const char* v = getenv("EDGPU_QTSS_REFLECT_ON_ARRIVAL")) M->arrivalMinMs = (uint32_t)std::max(0, atoi(v));
     if (const char* v = getenv("EDGPU_QTSS_MANUAL_TICK")) M->manualTick = atoi(v) != 0;
     // the prefs objects: the server's (inPrefs) and this module's (GetModulePrefsObject:
     // qtssModPrefs of the module object, QTSSModuleUtils.cpp:634-642)
@@ -633,9 +655,22 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
         M->stop = false;
         M->reader = std::thread(ReaderLoop);
         M->ticker = std::thread([] {
+            // a tick every tickMs from the previous tick's start (not tickMs after its end); in
+            // reflect-on-arrival mode as soon as a packet waits, at most every arrivalMinMs
+            using Clk = std::chrono::steady_clock;
+            Clk::time_point last = Clk::now();
             while (!M->stop.load()) {
-                std::this_thread::sleep_for(std::chrono::milliseconds(M->tickMs));
+                const Clk::time_point longest = last + std::chrono::milliseconds(M->tickMs);
+                if (M->arrivalMinMs) {
+                    std::unique_lock<std::mutex> lk(M->wakeMu);
+                    M->wake.wait_until(lk, longest, [] { return M->stop.load() || M->pending.load(); });
+                    lk.unlock();
+                    std::this_thread::sleep_until(last + std::chrono::milliseconds(M->arrivalMinMs));
+                } else {
+                    std::this_thread::sleep_until(longest);
+                }
                 if (M->stop.load()) break;
+                last = Clk::now();
                 const QTSS_Error e = Tick();
                 if (e) M->tickErr = e;
             }
@@ -655,6 +690,10 @@ QTSS_Error RereadPrefs() {
 
 QTSS_Error Shutdown() {
     M->stop = true;
+    {
+        std::lock_guard<std::mutex> w(M->wakeMu);
+        M->wake.notify_all();
+    }
     if (M->ticker.joinable()) M->ticker.join();
     if (M->reader.joinable()) M->reader.join();
     std::lock_guard<std::mutex> g(M->mu);
@@ -1063,6 +1102,7 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     const uint32_t track = channel / 2;
     if (track >= it->second.second) return QTSS_NoErr;
     M->R->PushPacket(it->second.first, track, (const char*)d + 4, len, (channel & 1) != 0, now);
+    NotifyArrival();
     return QTSS_NoErr;
 }
 

@@ -86,16 +86,19 @@ def test_module_equals_reference_module(name, tmp_path):
 
 
 @pytest.mark.gpu
-def test_module_threaded_default_mode_matches_reference(tmp_path):
+@pytest.mark.parametrize("arrival", ["", "1"])
+def test_module_threaded_default_mode_matches_reference(tmp_path, arrival):
     """Tick thread + UDP reader thread + two pusher threads: the per-sub-stream bytes (tick
     invariant for this trace) equal the reference capture's.  Transmit times and receiver-report
-    times depend on when the ticks ran and are not compared."""
+    times depend on when the ticks ran and are not compared.  arrival="1": the ticker reflects as
+    soon as a packet waits, at most every 1 ms (EDGPU_QTSS_REFLECT_ON_ARRIVAL)."""
     from easydarwin_amd.trace import capture_summary, read_capture
     t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
     t.write_bytes(_trace("threaded").to_bytes())
+    env = dict(os.environ, **({"EDGPU_QTSS_REFLECT_ON_ARRIVAL": arrival} if arrival else {}))
     for attempt in range(2):             # the same bytes whatever the tick timing: run it twice
         r = subprocess.run([REPLAY, MODULE, str(t), str(c), "--threaded"], capture_output=True, text=True,
-                           timeout=120)
+                           timeout=120, env=env)
         assert r.returncode == 0, r.stderr[-2000:]
         got = capture_summary(read_capture(c.read_bytes()))
         want = _fixture("threaded")["substreams"]

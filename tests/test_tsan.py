@@ -53,12 +53,15 @@ def _run(args, env_extra, tmp_path):
     return r
 
 
+@pytest.mark.parametrize("arrival", ["", "1"])
 @pytest.mark.parametrize("name", ["threaded"])
-def test_tsan_threaded_default_mode(tsan_build, name, tmp_path):
-    """The module's own 5-ms tick thread and UDP reader, two pusher threads of the fake server."""
+def test_tsan_threaded_default_mode(tsan_build, name, arrival, tmp_path):
+    """The module's own 5-ms tick thread and UDP reader, two pusher threads of the fake server;
+    and the reflect-on-arrival ticker (woken by the pushes, at most every 1 ms)."""
     replay, module = tsan_build
     (tmp_path / "t.edtr").write_bytes(_trace(name).to_bytes())
-    _run([replay, module, "t.edtr", "c.edcp", "--threaded"], {}, tmp_path)
+    _run([replay, module, "t.edtr", "c.edcp", "--threaded"],
+         {"EDGPU_QTSS_REFLECT_ON_ARRIVAL": arrival} if arrival else {}, tmp_path)
 
 
 @pytest.mark.parametrize("sessions,subs,tick_ms", [(16, 8, 20), (64, 2, 200)])

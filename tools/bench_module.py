@@ -44,6 +44,27 @@ def module_run(args) -> dict:
     return json.loads(r.stdout)
 
 
+def realtime_runs(args) -> list:
+    """The module on its own ticker at the stream's real rate (qtss_replay --bench with
+    EDGPU_BENCH_REALTIME=1): every frame pushed at its time, the latency from RTSPIncomingData to
+    QTSS_Write of every RTP packet; a fixed tick every <tick_ms> and reflect-on-arrival at 1 and
+    2 ms (EDGPU_QTSS_REFLECT_ON_ARRIVAL)."""
+    out = []
+    for arrival in ("0", "2", "1"):
+        env = dict(os.environ, EDGPU_BENCH_REALTIME="1", EDGPU_QTSS_TICK_MSEC=str(args.tick_ms),
+                   EDGPU_QTSS_REFLECT_ON_ARRIVAL=arrival)
+        env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
+        env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
+        env.setdefault("EDGPU_QTSS_WRITE_THREADS", str(args.write_threads))
+        cmd = [os.path.join(ROOT, "tools", "qtss_replay"), os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"),
+               "--bench", str(args.sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
+        if r.returncode:
+            raise SystemExit(f"qtss_replay --bench realtime failed ({r.returncode}): {r.stderr.strip()[-400:]}")
+        out.append(json.loads([ln for ln in r.stdout.splitlines() if '"mode": "realtime"' in ln][-1]))
+    return out
+
+
 def reference_module_run(args) -> dict | None:
     """The REFERENCE QTSSReflectorModule (oracle/_ref/libQTSSReflectorModule_ref.so, compiled from its
     sources) in the same fake server, same load, same pusher threads; its senders reflect on as many
@@ -94,7 +115,15 @@ def main():
     # the pushers push the next tick's packets while a tick runs, as a server's RTSP threads do
     # (default: pushing and ticking alternate, the conservative measure)
     ap.add_argument("--concurrent-push", action="store_true")
+    # the module on its own ticker at the streams' real rate: throughput = the offered load,
+    # plus the latency it adds (fixed tick vs reflect-on-arrival)
+    ap.add_argument("--realtime", action="store_true")
     args = ap.parse_args()
+    if args.realtime:
+        print(json.dumps({"workload": f"C2 at its real rate through the QTSS module: {args.sessions} RTSP-interleaved "
+                                      f"H.264 30-fps pushers x {args.subs} UDP players, {args.threads} pusher threads, "
+                                      f"the module's own ticker", "runs": realtime_runs(args)}))
+        return
     out = {"workload": f"C2 through the QTSS module: {args.sessions} RTSP-interleaved H.264 pushers x {args.subs} "
                        f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads "
                        f"({'concurrent with' if args.concurrent_push else 'alternating with'} the ticks)",

@@ -85,6 +85,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
 #include <thread>
@@ -261,6 +262,23 @@ static uint64_t g_writes = 0;
 static uint64_t g_prestaged = 0;                      // batch bytes the module copied ahead (trace mode)
 static uint64_t g_passes = 0, g_ticks = 0;            // copy passes of the manual ticks (trace mode)
 static bool g_count_only = false;                    // --bench: sinks count, no capture
+// --bench with EDGPU_BENCH_REALTIME=1: every pushed packet carries its push time (steady clock, ns)
+// in its last 8 bytes; the sinks histogram write time - push time (50-us bins, last bin = more)
+static bool g_realtime = false;
+static std::atomic<bool> g_lat_on{false};
+constexpr uint32_t kLatBins = 20000;                 // 50 us x 20000 = 1 s
+struct LatHist { std::vector<uint64_t> bins = std::vector<uint64_t>(kLatBins + 1, 0); double sum_us = 0; uint64_t n = 0; };
+static std::mutex g_lat_mu;
+static std::vector<LatHist*> g_lat_all;
+static LatHist* lat_hist() {
+    thread_local LatHist* h = nullptr;
+    if (!h) {
+        h = new LatHist();
+        std::lock_guard<std::mutex> g(g_lat_mu);
+        g_lat_all.push_back(h);
+    }
+    return h;
+}
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
     const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
@@ -269,6 +287,17 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
         // write threads call this concurrently for different players: per-stream counts)
         thread_local static char scratch[70000];
         memcpy(scratch, ((const QTSS_PacketStruct*)buf)->packetData, std::min<uint32_t>(len, sizeof(scratch)));
+        if (g_realtime && k == 0 && len >= 28 && g_lat_on.load(std::memory_order_relaxed)) {
+            int64_t stamp;
+            memcpy(&stamp, scratch + len - 8, 8);
+            const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                std::chrono::steady_clock::now().time_since_epoch()).count();
+            const double us = (double)(now - stamp) / 1000.0;
+            LatHist* h = lat_hist();
+            h->bins[std::min<uint64_t>((uint64_t)std::max(0.0, us) / 50, kLatBins)]++;
+            h->sum_us += us;
+            h->n++;
+        }
         o->npk[k]++;
         if (outLen) *outLen = len;
         return QTSS_NoErr;
@@ -497,6 +526,11 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             p[8] = (uint8_t)(P.ssrc >> 24); p[9] = (uint8_t)(P.ssrc >> 16); p[10] = (uint8_t)(P.ssrc >> 8); p[11] = (uint8_t)P.ssrc;
             memcpy(p + 12, hdr, nh);
             memcpy(p + 12 + nh, &pool[(P.seq * 1031u) % (pool.size() - 2048)], body);
+            if (g_realtime && len >= 28) {                    // the push time, for the sinks' latency
+                const int64_t stamp = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now().time_since_epoch()).count();
+                memcpy(p + len - 8, &stamp, 8);
+            }
             P.seq++;
             QTSS_RoleParams rp;
             memset(&rp, 0, sizeof(rp));
@@ -523,6 +557,65 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         P.frame++;
         P.ts += 90000 / fps;
     };
+    if (g_realtime) {
+        // Real time: the pushers push each frame at its time (1024 x 30 fps sessions, as a server's
+        // RTSP threads receive them); the module reflects on its own ticker (EDGPU_QTSS_TICK_MSEC,
+        // EDGPU_QTSS_REFLECT_ON_ARRIVAL).  Measured after a 1-s warm-up: relayed packets/s and the
+        // latency from RTSPIncomingData to QTSS_Write of every RTP packet.
+        using Clk = std::chrono::steady_clock;
+        const auto t0 = Clk::now();
+        std::atomic<bool> done{false};
+        std::vector<std::thread> th;
+        for (uint32_t w = 0; w < nthreads; w++)
+            th.emplace_back([&, w]() {
+                std::vector<char> fr(2100);
+                while (!done.load()) {
+                    const int64_t el = std::chrono::duration_cast<std::chrono::milliseconds>(Clk::now() - t0).count();
+                    advance_clock(el);
+                    for (uint32_t s = w; s < nsess; s += nthreads)
+                        while ((int64_t)ps[s].frame * 1000 / fps <= el) push_frame(s, fr, el);
+                    std::this_thread::sleep_for(std::chrono::microseconds(500));
+                }
+            });
+        std::this_thread::sleep_for(std::chrono::milliseconds(1000));
+        g_lat_on = true;
+        const uint64_t w0 = stream_writes();
+        const auto m0 = Clk::now();
+        std::this_thread::sleep_for(std::chrono::milliseconds((int64_t)(seconds * 1000)));
+        const uint64_t w1 = stream_writes();
+        const double secs = std::chrono::duration<double>(Clk::now() - m0).count();
+        g_lat_on = false;
+        done = true;
+        for (auto& t : th) t.join();
+        LatHist all;
+        {
+            std::lock_guard<std::mutex> g(g_lat_mu);
+            for (LatHist* h : g_lat_all) {
+                for (uint32_t b = 0; b <= kLatBins; b++) all.bins[b] += h->bins[b];
+                all.sum_us += h->sum_us;
+                all.n += h->n;
+            }
+        }
+        auto pct = [&](double q) {
+            const uint64_t want = (uint64_t)(q * (double)all.n);
+            uint64_t c = 0;
+            for (uint32_t b = 0; b <= kLatBins; b++)
+                if ((c += all.bins[b]) > want) return (b + 1) * 0.05;
+            return kLatBins * 0.05;
+        };
+        EDGPU_QTSSTickInfo ti;
+        if (last_fn(&ti)) return 3;
+        const char* tm = getenv("EDGPU_QTSS_TICK_MSEC");
+        const char* ar = getenv("EDGPU_QTSS_REFLECT_ON_ARRIVAL");
+        printf("{\"mode\": \"realtime\", \"sessions\": %u, \"subs\": %u, \"pusher_threads\": %u, \"tick_ms\": %s, "
+               "\"reflect_on_arrival_ms\": %s, \"seconds\": %.3f, \"relayed_per_s\": %.1f, \"ticks\": %llu, "
+               "\"failed_ticks\": %llu, \"latency_ms\": {\"packets\": %llu, \"mean\": %.3f, \"p50\": %.2f, "
+               "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}}\n",
+               nsess, nsub, nthreads, tm ? tm : "20", ar ? ar : "0", secs, (double)(w1 - w0) / secs,
+               (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks, (unsigned long long)all.n,
+               all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12));
+        return 0;
+    }
     const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
     double push_s = 0, tick_s = 0, wall_s = 0, hold = 0, hold_max = 0, gpu = 0, rb = 0, wr = 0, ing = 0;
     uint64_t rb_bytes = 0, arena = 0, ingested = 0, writes0 = 0, timed_ticks = 0, prestaged = 0, ingested_b = 0;
@@ -663,7 +756,10 @@ int main(int argc, char** argv) {
     } else {
         setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
     }
-    if (bench) setenv("EDGPU_QTSS_MANUAL_TICK", "1", 1);
+    if (bench) {
+        g_realtime = getenv("EDGPU_BENCH_REALTIME") && atoi(getenv("EDGPU_BENCH_REALTIME")) != 0;
+        setenv("EDGPU_QTSS_MANUAL_TICK", g_realtime ? "0" : "1", 1);     // realtime: the module's own ticker
+    }
     // the trace's prefs (version 4, after the sessions) are the prefs objects' values at Initialize
     Reader r;
     trace_prefs::Prefs prefs;
