@@ -247,3 +247,23 @@ def test_paced_egress_thins_congested_tcp_audio_like_the_reference(seconds, orac
     assert not bad, (f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}; "
                      f"stale {stale} vs the reference's {ref_stale}")
     assert stale == ref_stale
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_paced_egress_matches_the_reference_server_gate_on_random_traces(seed, oracle_bins, tmp_path):
+    """Q20 on fresh random traces (random sessions, codecs, UDP / interleaved pushers, UDP / TCP /
+    RTP-Info players, leaves, pusher lifecycle, random prefs; their socket budgets dropped -- the
+    sockets' own take their place): the paced egress against the reference harness's gate."""
+    from scenarios import random_scenario
+    if oracle_bins["ref"] is None:
+        pytest.skip("oracle/_ref/ref_harness not built")
+    r0 = random_scenario(seed)
+    tr = Trace(sdps=list(r0.sdps), events=[ev for ev in r0.events if ev[0] != BLOCK], flags=list(r0.flags),
+               prefs=dict(r0.prefs))
+    report = []
+    cap, _ = replay(tr, sockets={"threads": 2, "pacing": {}, "report": report})
+    want, _ = _gate_reference(tr, report, oracle_bins["ref"], tmp_path)
+    got = capture_summary(read_capture(cap))
+    bad = [k for k in want if got.get(k) != want[k]]
+    assert not bad, (f"{len(bad)} sub-streams differ, e.g. {[(k, got.get(k), want[k]) for k in bad[:3]]}; "
+                     f"{len(report)} socket blocks")
