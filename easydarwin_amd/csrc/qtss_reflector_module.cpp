@@ -551,6 +551,18 @@ QTSS_Error Tick() {
     o.prestaged_bytes = t.prestaged_bytes;
     o.passes = t.passes;
     o.rereads = M->rereads;
+    if (t.stream_errors) {
+        // per-stream isolation: name the sessions whose outputs lost packets, and go on
+        std::vector<uint32_t> marked;
+        if (M->R->StreamErrors(&marked) == 0)
+            for (uint32_t e : marked) {
+                o.stream_errors++;
+                for (const auto& kv : M->sessions)
+                    if (kv.second.engine == e)
+                        fprintf(stderr, "QTSSReflectorModule: stream %s lost packets its outputs needed (sender ring "
+                                        "too small for them: raise the ring capacity)\n", kv.second.name.c_str());
+            }
+    }
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     o.ticks++;
     if (err) {

@@ -387,6 +387,19 @@ int Reflector::FlushIngest() {
     return kNoErr;
 }
 
+int Reflector::StreamErrors(std::vector<uint32_t>* sessions) {
+    if (!fCtx || !sessions) return kBadArgument;
+    sessions->clear();
+    uint32_t n = 0;
+    int err = edgpu_stream_errors(fCtx, nullptr, nullptr, 0, &n);
+    if (err || !n) return err;
+    std::vector<int32_t> codes(n);
+    sessions->resize(n);
+    if ((err = edgpu_stream_errors(fCtx, sessions->data(), codes.data(), n, &n))) return err;
+    sessions->resize(std::min<size_t>(n, sessions->size()));
+    return kNoErr;
+}
+
 int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if (!fCtx) return kRequestFailed;
     fLastErr.clear();
@@ -396,6 +409,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     fTick.readback_bytes = fTick.arena_bytes = fTick.writes = 0;
     fTick.fanout_ms = fTick.readback_ms = fTick.write_ms = 0;
     fTick.passes = 0;
+    fTick.stream_errors = 0;
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
     uint32_t nrr = 0;
@@ -410,6 +424,7 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
     fTick.fanout_ms = ms_since(t0);
     if (st.status) return st.status;
+    fTick.stream_errors = st.stream_errors;             // the tick went on for every other session
     fTick.arena_bytes = st.arena_bytes;
     // A tick over the arena comes in copy passes of consecutive sub-stream rows (edgpu_fanout_next):
     // each is delivered before the next is copied, so every output gets the whole tick, in the order

@@ -157,9 +157,13 @@ public:
         uint64_t writes = 0;                                // OutputSink::Write calls
         uint64_t prestaged_bytes = 0;                       // of the batch, copied ahead while it filled
         uint32_t passes = 0;                                // copy passes (> 1: the tick exceeded the arena)
+        uint32_t stream_errors = 0;                         // sessions the tick marked (edgpu_stream_errors)
         double ingest_ms = 0, fanout_ms = 0, readback_ms = 0, write_ms = 0;
     };
     const TickInfo& LastTick() const { return fTick; }
+    // the sessions marked with a stream error (a sender ring lost a packet one of their outputs
+    // needed) since the last call, and clears them: edgpu_stream_errors
+    int StreamErrors(std::vector<uint32_t>* sessions);
     // the message of the last ReflectPackets failure that happened on another thread than the
     // caller's (edgpu_last_error() is per thread); empty otherwise
     const std::string& LastError() const { return fLastErr; }
