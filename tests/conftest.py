@@ -1,6 +1,8 @@
+import contextlib
 import os
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -23,3 +25,13 @@ def oracle_bins():
     refmod = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
     return {"port": port, "ref": ref if os.path.exists(ref) else None,
             "refmod": refmod if os.path.exists(refmod) else None}
+
+
+@contextlib.contextmanager
+def udp_port_lock():
+    """tools/qtss_replay binds the traces' fixed loopback source ports for UDP pushers: runs of it
+    on the CPU take turns under pytest -n (one machine-wide lock file)."""
+    import fcntl
+    with open(os.path.join(tempfile.gettempdir(), "edgpu_udp_ports.lock"), "a+") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        yield

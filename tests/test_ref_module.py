@@ -47,8 +47,10 @@ def refmod(oracle_bins):
 def test_reference_module_reproduces_fixture(name, refmod, tmp_path):
     t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
     t.write_bytes(SCENARIOS[name]().to_bytes())
-    r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+    from conftest import udp_port_lock
+    with udp_port_lock():                # UDP pushers bind fixed loopback source ports
+        r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
     assert r.returncode == 0, r.stderr[-3000:]
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fix(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fix(name)["transmit_sha256"]

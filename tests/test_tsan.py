@@ -42,6 +42,12 @@ def tsan_build(request):
 
 
 def _run(args, env_extra, tmp_path):
+    from conftest import udp_port_lock
+    with udp_port_lock():                  # traces with UDP pushers bind fixed loopback source ports
+        return _run_locked(args, env_extra, tmp_path)
+
+
+def _run_locked(args, env_extra, tmp_path):
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=66 second_deadlock_stack=1",
                # (verify_asan_link_order=0: a preloaded library may come before the ASan runtime)
                ASAN_OPTIONS="detect_leaks=1 exitcode=67 verify_asan_link_order=0",
