@@ -552,7 +552,9 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             }
         };
         advance_clock(t);           // once per frame: the shared clock is one contended line
-        if (P.frame % gop == 0) { nal(0x67, 24, false); nal(0x68, 8, false); nal(0x65, idr, true); }
+        // (real time: the sessions' GOPs are staggered, as independent pushers' are; the tick-paced
+        // bench keeps them aligned, its worst case)
+        if ((P.frame + (g_realtime ? s * gop / nsess : 0)) % gop == 0) { nal(0x67, 24, false); nal(0x68, 8, false); nal(0x65, idr, true); }
         else nal(0x41, p_frame, true);
         P.frame++;
         P.ts += 90000 / fps;
