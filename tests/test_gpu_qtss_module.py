@@ -86,16 +86,17 @@ def test_module_equals_reference_module(name, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arrival", ["", "1"])
+@pytest.mark.parametrize("arrival", ["0", "1", "2"])
 def test_module_threaded_default_mode_matches_reference(tmp_path, arrival):
     """Tick thread + UDP reader thread + two pusher threads: the per-sub-stream bytes (tick
     invariant for this trace) equal the reference capture's.  Transmit times and receiver-report
-    times depend on when the ticks ran and are not compared.  arrival="1": the ticker reflects as
-    soon as a packet waits, at most every 1 ms (EDGPU_QTSS_REFLECT_ON_ARRIVAL)."""
+    times depend on when the ticks ran and are not compared.  arrival: "0" a tick every 5 ms; "1"
+    and "2" (the default) the ticker reflects as soon as a packet waits, at most every 1 / 2 ms
+    (EDGPU_QTSS_REFLECT_ON_ARRIVAL)."""
     from easydarwin_amd.trace import capture_summary, read_capture
     t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
     t.write_bytes(_trace("threaded").to_bytes())
-    env = dict(os.environ, **({"EDGPU_QTSS_REFLECT_ON_ARRIVAL": arrival} if arrival else {}))
+    env = dict(os.environ, EDGPU_QTSS_REFLECT_ON_ARRIVAL=arrival)
     for attempt in range(2):             # the same bytes whatever the tick timing: run it twice
         r = subprocess.run([REPLAY, MODULE, str(t), str(c), "--threaded"], capture_output=True, text=True,
                            timeout=120, env=env)

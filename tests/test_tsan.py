@@ -59,15 +59,14 @@ def _run_locked(args, env_extra, tmp_path):
     return r
 
 
-@pytest.mark.parametrize("arrival", ["", "1"])
+@pytest.mark.parametrize("arrival", ["0", "2"])
 @pytest.mark.parametrize("name", ["threaded"])
 def test_tsan_threaded_default_mode(tsan_build, name, arrival, tmp_path):
-    """The module's own 5-ms tick thread and UDP reader, two pusher threads of the fake server;
-    and the reflect-on-arrival ticker (woken by the pushes, at most every 1 ms)."""
+    """The module's own tick thread and UDP reader, two pusher threads of the fake server: a tick
+    every 5 ms, and the reflect-on-arrival ticker (woken by the pushes, at most every 2 ms)."""
     replay, module = tsan_build
     (tmp_path / "t.edtr").write_bytes(_trace(name).to_bytes())
-    _run([replay, module, "t.edtr", "c.edcp", "--threaded"],
-         {"EDGPU_QTSS_REFLECT_ON_ARRIVAL": arrival} if arrival else {}, tmp_path)
+    _run([replay, module, "t.edtr", "c.edcp", "--threaded"], {"EDGPU_QTSS_REFLECT_ON_ARRIVAL": arrival}, tmp_path)
 
 
 @pytest.mark.parametrize("sessions,subs,tick_ms", [(16, 8, 20), (64, 2, 200)])
