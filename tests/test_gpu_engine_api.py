@@ -119,8 +119,8 @@ def test_timing_levels_select_the_recorded_pairs():
 def test_prestaged_pinned_batches_relay_the_same_bytes():
     """edgpu_ingest_prestage: a pinned batch's blob prefix copied ahead in pieces, then the
     ingest copies the rest -- every tick's arena equals the one of a plain pinned ingest; a piece
-    that does not extend the staged prefix, or runs past max_batch_bytes, is refused, and a
-    batch refused by validation drops what was copied ahead of it."""
+    that does not extend the staged prefix, or runs past max_batch_bytes, is refused; a batch
+    refused by validation drops what was copied ahead of it, and so does an explicit discard."""
     rng = np.random.default_rng(7)
     ticks = []
     seq = 0
@@ -146,7 +146,17 @@ def test_prestaged_pinned_batches_relay_the_same_bytes():
                 for name, a in (("desc", desc), ("seg", seg), ("sess", sess), ("blob", blob)):
                     v = np.ascontiguousarray(a).view(np.uint8).ravel()
                     B[name].array[:v.nbytes] = v
-                if prestage:
+                if prestage and t == 9:
+                    # a prefix copied ahead and then discarded (edgpu_ingest_prestage(NULL, 0, 0): the
+                    # host dropped the batch it belonged to) must not reach the next ingest: stage other
+                    # bytes, discard, then write the batch and ingest it with nothing staged
+                    v = np.ascontiguousarray(blob).view(np.uint8).ravel()
+                    B["blob"].array[:v.nbytes] = v[::-1]
+                    _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(B["blob"].ptr), 0, blob.nbytes // 2 // 16 * 16))
+                    _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, None, 0, 0))
+                    _check_ok(ctx.lib.edgpu_sync(ctx.h))       # (the discarded copy has read the buffer)
+                    B["blob"].array[:v.nbytes] = v
+                elif prestage:
                     cut = [0, blob.nbytes // 3, (2 * blob.nbytes) // 3]
                     for a, b in zip(cut, cut[1:]):
                         _check_ok(ctx.lib.edgpu_ingest_prestage(ctx.h, C.c_void_p(B["blob"].ptr), a, b - a))
