@@ -565,6 +565,8 @@ QTSS_Error Tick() {
             }
     }
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    o.hold_max_ms = std::max(o.hold_max_ms, o.hold_ms);
+    o.hold_sum_ms += o.hold_ms;
     o.ticks++;
     if (err) {
         // the first failure is logged with the engine's message; later ones are counted

@@ -248,6 +248,8 @@ typedef struct EDGPU_QTSSTickInfo {
     uint64_t prestaged_bytes;           /* of the tick's batch, copied to the device while it filled */
     uint64_t passes;                    /* copy passes of the tick (> 1: it exceeded the arena) */
     uint64_t rereads;                   /* RereadPrefs calls handled since Initialize */
+    double   hold_max_ms, hold_sum_ms;  /* the longest lock hold of any tick / the sum of all, since
+                                           Initialize (RTSP roles wait behind a tick) */
     uint64_t stream_errors;             /* sessions a tick marked since Initialize: a sender ring lost
                                            a packet one of their outputs needed (logged by name;
                                            the ticks went on for every other session) */

@@ -611,10 +611,12 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         const char* ar = getenv("EDGPU_QTSS_REFLECT_ON_ARRIVAL");
         printf("{\"mode\": \"realtime\", \"sessions\": %u, \"subs\": %u, \"pusher_threads\": %u, \"tick_ms\": %s, "
                "\"reflect_on_arrival_ms\": %s, \"seconds\": %.3f, \"relayed_per_s\": %.1f, \"ticks\": %llu, "
-               "\"failed_ticks\": %llu, \"latency_ms\": {\"packets\": %llu, \"mean\": %.3f, \"p50\": %.2f, "
+               "\"failed_ticks\": %llu, \"lock_hold_ms\": {\"mean\": %.3f, \"max\": %.3f}, "
+               "\"latency_ms\": {\"packets\": %llu, \"mean\": %.3f, \"p50\": %.2f, "
                "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}}\n",
                nsess, nsub, nthreads, tm ? tm : "20", ar ? ar : "0", secs, (double)(w1 - w0) / secs,
-               (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks, (unsigned long long)all.n,
+               (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks,
+               ti.ticks ? ti.hold_sum_ms / (double)ti.ticks : 0.0, ti.hold_max_ms, (unsigned long long)all.n,
                all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12));
         return 0;
     }
