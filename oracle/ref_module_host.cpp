@@ -133,6 +133,8 @@ struct TickInfo {
     uint64_t ticks, failed_ticks;
     int64_t last_error;
     uint64_t prestaged_bytes, passes, rereads;
+    double hold_max_ms, hold_sum_ms;
+    uint64_t stream_errors;
 };
 static TickInfo g_tick;
 extern "C" QTSS_Error EDGPU_QTSSReflectorModule_LastTick(TickInfo* out) {
@@ -149,6 +151,8 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
             g_tick.passes = 1;
             g_tick.hold_ms = g_tick.write_ms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            g_tick.hold_max_ms = std::max(g_tick.hold_max_ms, g_tick.hold_ms);
+            g_tick.hold_sum_ms += g_tick.hold_ms;
         }
     } done{t0};
     OSMutexLocker locker(session_map()->GetMutex());
