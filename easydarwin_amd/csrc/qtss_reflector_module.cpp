@@ -223,8 +223,8 @@ struct Module {
     // EDGPU_QTSS_REFLECT_ON_ARRIVAL=<ms> (default 2): reflect as soon as packets are waiting, at
     // most every <ms> (the reference reflects a sender when its socket task wakes on new packets,
     // ReflectorStream.cpp:573, 603-618, 1676-1714); tickMs stays the longest interval.  0: a tick
-    // every tickMs.  At C2's real rate: 4.0 ms mean RTSPIncomingData -> QTSS_Write latency against
-    // 12.8 ms with 20-ms ticks, the same throughput.
+    // every tickMs.  At C2's real rate: 4.3 ms mean RTSPIncomingData -> QTSS_Write latency against
+    // 12.9 ms with 20-ms ticks, the same throughput.
     uint32_t arrivalMinMs = 2;
     std::atomic<bool> pending{false};   // a packet arrived since the last tick took the batch
     std::mutex wakeMu;
