@@ -79,6 +79,11 @@ struct SenderDev {
     uint64_t umin;                  // min range start over this sender's sub-streams
     uint32_t _pad_items[2];
     uint64_t fan_lo, fan_vlo;       // oldest packet index / vbyte the last fan-out reads
+    // the last host batch (edgpu_fanout_sources): packets [batch_lo, head) came from the blob of
+    // the ingest whose epoch is batch_epoch; their blob slots follow the meta ring (uint32 per
+    // ring entry, same index), written by k_ingest
+    uint64_t batch_lo;
+    uint32_t batch_epoch, _pad_b;
 };
 
 // ---- Session images (cross-GPU keyframe fast start) ----

@@ -32,6 +32,8 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st);
 hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
+hipError_t launch_desc_source(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
+                              uint32_t epoch, uint32_t* out, hipStream_t st);
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                                int64_t* out, hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
@@ -287,6 +289,9 @@ struct edgpu_ctx {
     DevVec<edgpu_blocked> d_blocked;
     DevVec<edgpu_region> d_gather_reg;          // edgpu_arena_gather
     DevVec<int64_t> d_arrivals;                 // edgpu_fanout_arrivals
+    DevVec<uint32_t> d_sources;                 // edgpu_fanout_packet_info
+    uint32_t ingest_epoch = 0;                  // ingests so far
+    uint32_t host_epoch_last = 0;               // the last ingest's epoch if it was a host batch, else 0
     DevVec<uint64_t> d_gather_off;
     // session images
     DevVec<ImgPlan> d_img_plan;
@@ -420,7 +425,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
-    x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release();
+    x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release(); x->d_sources.release();
     if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
@@ -670,7 +675,8 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             const uint64_t by = big ? x->cfg.video_ring_bytes : x->cfg.other_ring_bytes;
             void* meta = nullptr; void* ring = nullptr;
             const uint32_t gs = first_sender + 2 * t + k;
-            if (dmalloc(&meta, pk * sizeof(PktMeta)) != hipSuccess) { undo(2 * t + k); return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring"); }
+            // the meta ring, then a uint32 blob slot per entry (edgpu_fanout_packet_info)
+            if (dmalloc(&meta, pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess) { undo(2 * t + k); return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring"); }
             x->snd_meta[gs] = meta;
             if (dmalloc(&ring, by) != hipSuccess) { undo(2 * t + k + 1); return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring"); }
             x->snd_ring[gs] = ring;
@@ -1170,9 +1176,13 @@ static int rebuild_index(edgpu_ctx* x) {
 // edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
 // inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
-                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, const TcpParams* tcp = nullptr,
+                          uint32_t nseg, const uint8_t* db, uint32_t copy_mode, bool host_src, const TcpParams* tcp = nullptr,
                           hipEvent_t deframed = nullptr) {
     IngestParams p;
+    // a host batch: k_ingest records each packet's blob slot (edgpu_fanout_packet_info)
+    p.host_epoch = host_src ? ++x->ingest_epoch : 0u;
+    if (!host_src) ++x->ingest_epoch;
+    x->host_epoch_last = p.host_epoch;
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
@@ -1343,7 +1353,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         int k = 0;
         if ((r = stage_pinned(x, desc, n, seg_off, seg_sess, nseg, blob, blob_bytes, &k))) return r;
         const edgpu_ctx::PinStage& S = x->pin[k];
-        r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, x->ingest_mode);
+        r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, x->ingest_mode, true);
         if (!r) x->pend_stage = k;
         else (void)hipEventRecord(S.consumed, x->stream);   // nothing will read the set: free it
         return r;
@@ -1366,7 +1376,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
     }
-    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode);
+    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode, where == EDGPU_PTR_HOST);
 }
 
 int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t n, const uint8_t* bytes,
@@ -1461,7 +1471,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
     HIP_CHECK(launch_deframe(p, x->aux));
     HIP_CHECK(hipEventRecord(x->ev_deframe, x->aux));
-    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, &p, x->ev_deframe);
+    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, false, &p, x->ev_deframe);
     if (r) return r;
     TcpTotals tot;
     Readback rb(x);
@@ -1698,8 +1708,15 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
 
 int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    return edgpu_fanout_packet_info(x, out, nullptr, n, kind);
+}
+
+// Per descriptor of the current pass: its packet's arrival and/or its blob slot in the last host
+// batch (kNoSource when it came with an earlier batch, or the last one was not a host batch).
+int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources, uint32_t n, int kind) {
+    if (!x || (!arrivals && !sources)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
-    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_arrivals needs serial ticks");
+    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_arrivals / _sources need serial ticks");
     HIP_CHECK(hipSetDevice(x->device));
     TickTotals t;
     HIP_CHECK(sync_all(x));
@@ -1710,17 +1727,26 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
     }
     if (t.status) return fail(t.status, "the last tick failed");
     const uint32_t npass = t.pass_desc[x->pass_ord & 1u];      // the current copy pass's descriptors
-    if (n < npass) return fail(EDGPU_OUT_OVERFLOW, "arrival array smaller than the pass's descriptors");
+    if (n < npass) return fail(EDGPU_OUT_OVERFLOW, "array smaller than the pass's descriptors");
     if (!npass) return EDGPU_OK;
-    int64_t* dst = out;
+    int64_t* da = arrivals;
+    uint32_t* dsrc = sources;
     if (kind == EDGPU_PTR_HOST) {
-        HIP_CHECK(x->d_arrivals.reserve(npass, x->stream));
-        dst = x->d_arrivals.ptr;
+        if (arrivals) { HIP_CHECK(x->d_arrivals.reserve(npass, x->stream)); da = x->d_arrivals.ptr; }
+        if (sources) { HIP_CHECK(x->d_sources.reserve(npass, x->stream)); dsrc = x->d_sources.ptr; }
     }
-    HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, x->tick_nsubs, x->pass_id, dst,
-                                  x->stream));
+    if (arrivals) HIP_CHECK(launch_desc_arrival(x->d_subs.ptr, x->d_senders.ptr, x->tick_nsubs, x->pass_id, da, x->stream));
+    if (sources) {
+        HIP_CHECK(hipMemsetAsync(dsrc, 0xFF, (size_t)npass * sizeof(uint32_t), x->stream));
+        if (x->host_epoch_last)
+            HIP_CHECK(launch_desc_source(x->d_subs.ptr, x->d_senders.ptr, x->tick_nsubs, x->pass_id, x->host_epoch_last,
+                                         dsrc, x->stream));
+    }
     Readback rb(x);
-    if (kind == EDGPU_PTR_HOST) HIP_CHECK(rb.add(out, dst, (size_t)npass * sizeof(int64_t)));
+    if (kind == EDGPU_PTR_HOST) {
+        if (arrivals) HIP_CHECK(rb.add(arrivals, da, (size_t)npass * sizeof(int64_t)));
+        if (sources) HIP_CHECK(rb.add(sources, dsrc, (size_t)npass * sizeof(uint32_t)));
+    }
     HIP_CHECK(rb.run());
     return EDGPU_OK;
 }

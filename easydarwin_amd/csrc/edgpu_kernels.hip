@@ -553,6 +553,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             m.seq = len >= 4 ? (uint16_t)hbe16(hdr, 2) : (uint16_t)0;
             m.vcount = s_vcount[ls] + my_nzpre;
             reinterpret_cast<PktMeta*>(s_meta[ls])[idx & s_pkmask[ls]] = m;
+            if (P.host_epoch)                            // its blob slot, for edgpu_fanout_sources
+                reinterpret_cast<uint32_t*>(s_meta[ls] + ((uint64_t)s_pkmask[ls] + 1) * sizeof(PktMeta))[idx & s_pkmask[ls]] = slot;
             const bool by_port_rtp = !(fl & kSndRtcpPort);
             const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len >= 20 &&
                              ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len)
@@ -657,6 +659,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 
     if (tid < (int)nsnd) {
         SenderDev& D = P.senders[S.first_sender + tid];
+        if (P.host_epoch) { D.batch_lo = D.head; D.batch_epoch = P.host_epoch; }   // (the head before the batch)
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
         // tick pipelining, or a copy pass the last tick still owes (edgpu_fanout_next): this batch
@@ -2439,6 +2442,33 @@ __global__ __launch_bounds__(256) void k_desc_arrival(const SubDev* subs, const 
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                                int64_t* out, hipStream_t st) {
     if (nsubs) hipLaunchKernelGGL(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass, out);
+    return hipGetLastError();
+}
+
+// edgpu_fanout_sources: per descriptor of the current pass, the blob slot of its packet when the
+// packet came with the last host batch (ingest epoch `epoch`), else kNoSource.  Numbered as
+// k_desc_arrival numbers them; out[] was filled with kNoSource first.
+__global__ __launch_bounds__(256) void k_desc_source(const SubDev* subs, const SenderDev* senders, uint32_t nsubs,
+                                                     uint32_t pass, uint32_t epoch, uint32_t* out) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (q >= nsubs) return;
+    const SubDev& Q = subs[q];
+    if (!Q.active || !Q.nonempty || Q.count == 0 || Q.pass != pass) return;
+    const SenderDev& D = senders[Q.sender];
+    if (D.batch_epoch != epoch) return;
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(D.meta + ((uint64_t)D.pk_mask + 1) * sizeof(PktMeta));
+    for (uint64_t p = max(Q.a, D.batch_lo) + lane; p < D.head; p += 64) {
+        const PktMeta m = meta[p & D.pk_mask];
+        const uint32_t i = m.vcount - Q.vcstart;
+        if (m.len != 0 && i < Q.count) out[Q.desc_base + i] = src[p & D.pk_mask];
+    }
+}
+hipError_t launch_desc_source(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
+                              uint32_t epoch, uint32_t* out, hipStream_t st) {
+    if (nsubs) hipLaunchKernelGGL(k_desc_source, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass,
+                                  epoch, out);
     return hipGetLastError();
 }
 

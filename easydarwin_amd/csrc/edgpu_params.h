@@ -54,6 +54,8 @@ struct IngestParams {
     uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7: 16 no totals, 32 no slot
                             // copy, 64 no per-sender scans)
     uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
+    uint32_t host_epoch;    // != 0: the blob is a host batch the host keeps for the tick; record each
+                            // packet's slot and the batch (edgpu_fanout_sources)
     TickTotals* totals;
     // Interleaved ingest (null otherwise): segment g is deframe group g, and k_ingest finds each
     // frame itself -- its chunk from the per-chunk results, its start from the walk's recorded

@@ -23,6 +23,7 @@ Reflector::Reflector(const edgpu_config* cfg) {
     if (const char* v = getenv("EDGPU_GATHER_PARTS"))
         fGatherParts = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)atoi(v), edgpu_host::TickParts::kMax));
     if (const char* v = getenv("EDGPU_PRESTAGE_BYTES")) fPrestageBytes = strtoull(v, nullptr, 0);
+    if (const char* v = getenv("EDGPU_BATCH_SOURCES")) fBatchSources = atoi(v) != 0;
     if (fStatus || !fCtx) return;
     edgpu_config c;
     if (cfg) c = *cfg; else edgpu_config_default(&c);
@@ -52,7 +53,7 @@ Reflector::~Reflector() {
         for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
             if (p) (void)edgpu_host_free(fCtx, p);
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
-    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinArr})
+    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinArr, &fPinSrc})
         if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
     edgpu_ctx_destroy(fCtx);
 }
@@ -294,6 +295,7 @@ int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc
 int Reflector::FlushIngest() {
     const auto t0 = Clock::now();
     fTick.ingested_packets = fTick.ingested_bytes = 0;
+    fIngestedBlob = nullptr;
     // The batch to become the fill buffer was handed to edgpu_ingest two flushes ago; every call
     // that flushed has synchronised the stream since (fan-out stats, PLAY, session removal), so its
     // DMA is done -- this sync is the guarantee for error paths (idle stream: microseconds).
@@ -367,6 +369,7 @@ int Reflector::FlushIngest() {
         fTick.ingested_packets = n;
         err = edgpu_ingest(fCtx, b.desc, n, b.seg, b.segSess, nseg, b.blob, b.next, EDGPU_PTR_PINNED);
         ingested = true;                                     // (a refused batch drops the prestage itself)
+        if (!err) fIngestedBlob = b.blob;                    // intact until the next flush swaps it back in
         if (!err) err = edgpu_keyframe_index(fCtx);
     }
     drop_prestage();
@@ -464,8 +467,34 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
     if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
     if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
+    // Packets that came with the batch this tick ingested are still in its pinned blob: an identity
+    // UDP sub-stream made only of them is written from there (its wire bytes are the packets') and
+    // needs no readback.  The rest -- GOP replays of new outputs, earlier batches, interleaved or
+    // rewritten sub-streams -- is gathered.
+    const int64_t* arrival = nullptr;
+    const uint32_t* source = nullptr;
+    const bool useSrc = fBatchSources && fIngestedBlob != nullptr;
+    if (sink->WantsArrivals() || useSrc) {
+        if ((sink->WantsArrivals() && (err = EnsurePinned(fPinArr, nd * sizeof(int64_t)))) ||
+            (useSrc && (err = EnsurePinned(fPinSrc, nd * sizeof(uint32_t)))))
+            return err;
+        if ((err = edgpu_fanout_packet_info(fCtx, sink->WantsArrivals() ? (int64_t*)fPinArr.p : nullptr,
+                                            useSrc ? (uint32_t*)fPinSrc.p : nullptr, (uint32_t)nd, EDGPU_PTR_HOST)))
+            return err == EDGPU_BAD_ARGUMENT ? kBadArgument : err;   // overlap_ticks: no arrivals
+        if (sink->WantsArrivals()) arrival = (const int64_t*)fPinArr.p;
+        if (useSrc) source = (const uint32_t*)fPinSrc.p;
+    }
+    fSkip.assign(source ? nq : 0, 0);
+    if (source)
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = subs[q];
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || s.transport == EDGPU_TRANSPORT_TCP) continue;
+            bool all = true;
+            for (uint32_t i = 0; i < s.desc_count && all; i++) all = source[s.desc_base + i] != EDGPU_NO_SOURCE;
+            fSkip[q] = all ? 1 : 0;
+        }
     // the pass's distinct bytes only: one region per identity sender + the other sub-streams
-    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq);
+    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq, source ? fSkip.data() : nullptr);
     if (tr.bytes > fHostOutCap) {            // grown geometrically: pinning costs ~40 ms per call
         if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
         fHostOut = nullptr; fHostOutCap = 0;
@@ -475,15 +504,8 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         fHostOut = (uint8_t*)h;
         fHostOutCap = cap;
     }
-    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc);
-    const int64_t* arrival = nullptr;
-    if (sink->WantsArrivals()) {
-        if ((err = EnsurePinned(fPinArr, nd * sizeof(int64_t)))) return err;
-        if ((err = edgpu_fanout_arrivals(fCtx, (int64_t*)fPinArr.p, (uint32_t)nd, EDGPU_PTR_HOST))) {
-            return err == EDGPU_BAD_ARGUMENT ? kBadArgument : err;   // overlap_ticks: no arrivals
-        }
-        arrival = (const int64_t*)fPinArr.p;
-    }
+    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc) +
+                            (arrival ? nd * sizeof(int64_t) : 0) + (source ? nd * sizeof(uint32_t) : 0);
     // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
     // PCIe, one pass) in up to TickParts::kMax parts of the sub-stream table, each part's regions after the
     // previous part's: with several write threads a gather thread brings part k + 1 over while the
@@ -523,6 +545,7 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     WriteJob job;
     job.subs = subs; job.nsubs = nq;
     job.desc = d; job.arrival = arrival;
+    job.batch = fIngestedBlob; job.source = source;
     job.sink = sink;
     job.host = fHostOut;
     job.regions = &tr;
@@ -577,11 +600,15 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
         const edgpu_substream_out& q = j.subs[s];
         if (!q.desc_count || (nworkers > 1 && writer_of(q, nworkers) != worker)) continue;
         while (part + 1 < j.nparts && s >= j.part_q[part]) part++;
-        // this sub-stream's bytes are in part `part` of the gather: wait for it (a failed
-        // gather also ends the wait; the tick then returns its error)
-        while (j.ready->load(std::memory_order_acquire) <= part) std::this_thread::yield();
-        if (j.failed->load(std::memory_order_relaxed)) { r.writes = writes; return; }
-        const uint8_t* base = j.regions->at(j.host, s);
+        // its packets all in the ingested batch: read them there; else its bytes are in part
+        // `part` of the gather: wait for it (a failed gather also ends the wait; the tick then
+        // returns its error)
+        const bool fromBatch = j.regions->src[s].first == edgpu_host::TickRegions::kNone;
+        if (!fromBatch) {
+            while (j.ready->load(std::memory_order_acquire) <= part) std::this_thread::yield();
+            if (j.failed->load(std::memory_order_relaxed)) { r.writes = writes; return; }
+        }
+        const uint8_t* base = fromBatch ? nullptr : j.regions->at(j.host, s);
         for (uint32_t i = 0; i < q.desc_count; i++) {
             const edgpu_out_desc& o = j.desc[q.desc_base + i];
             PacketWrite w;
@@ -589,7 +616,8 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
             w.track = q.track;
             w.isRTCP = q.kind != 0;
             w.interleaved = q.transport == EDGPU_TRANSPORT_TCP;
-            w.wire = base + (o.offset - q.out_base);
+            // (a batch slot holds 4 bytes of interleave-header room, then the packet)
+            w.wire = fromBatch ? j.batch + (uint64_t)j.source[q.desc_base + i] * 16 + 4 : base + (o.offset - q.out_base);
             w.wireLen = o.len;
             w.packetID = o.packet_id;
             w.arrivalMs = j.arrival ? j.arrival[q.desc_base + i] : -1;

@@ -218,6 +218,9 @@ private:
         const edgpu_substream_out* subs; uint32_t nsubs;
         const edgpu_out_desc* desc; const int64_t* arrival;
         const uint8_t* host; const edgpu_host::TickRegions* regions;   // the tick's bytes
+        // identity UDP sub-streams without a region: every packet came with the batch this tick
+        // ingested, still in `batch` (the pinned blob); source[d] = its slot (edgpu_fanout_packet_info)
+        const uint8_t* batch = nullptr; const uint32_t* source = nullptr;
         OutputSink* sink;
         // the gather's parts: sub-streams [part_q[k-1], part_q[k]) need part k; `ready` counts the
         // parts in the pinned buffer; `failed`: a gather failed (the writers stop)
@@ -255,7 +258,11 @@ private:
     // readback buffers
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
-    PinBuf fPinSubs, fPinDesc, fPinArr;                     // sub-stream table, descriptors, arrivals
+    PinBuf fPinSubs, fPinDesc, fPinArr, fPinSrc;            // sub-stream table, descriptors, arrivals, sources
+    const uint8_t* fIngestedBlob = nullptr;                 // the blob the last FlushIngest ingested (intact
+                                                            // until the next one swaps it back in)
+    bool fBatchSources = true;                              // EDGPU_BATCH_SOURCES=0: read every byte back
+    std::vector<uint8_t> fSkip;                             // per sub-stream: written from the batch
     uint64_t fGatherSplitBytes = 8ull << 20;               // see ReflectPackets
     uint32_t fGatherParts = 4;                              // EDGPU_GATHER_PARTS (<= TickParts::kMax)
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes (edgpu_arena_gather target)

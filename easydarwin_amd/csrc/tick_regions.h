@@ -28,7 +28,9 @@ struct TickRegions {
     const uint8_t* at(const uint8_t* base, uint32_t q) const { return base + reg_off[src[q].first] + src[q].second; }
 };
 
-inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
+// `skip` (optional, per sub-stream): it needs no region (the host has its bytes elsewhere: an
+// identity sub-stream whose packets all came with the batch the host still holds); its src is kNone.
+inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq, const uint8_t* skip = nullptr) {
     TickRegions t;
     t.src.assign(nq, {TickRegions::kNone, 0});
     // per sender (engine sender ids are dense): its longest identity sub-stream, its region
@@ -38,14 +40,14 @@ inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq) {
     std::vector<uint32_t> rep(nsend, TickRegions::kNone), rep_reg(nsend, TickRegions::kNone);
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];
-        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
+        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || (skip && skip[q])) continue;
         uint32_t& r = rep[s.sender];
         if (r == TickRegions::kNone || subs[r].out_bytes < s.out_bytes) r = q;
     }
     t.reg.reserve(nq);
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];
-        if (!s.desc_count) continue;
+        if (!s.desc_count || (skip && skip[q])) continue;
         if (s.flags & EDGPU_SUB_IDENTITY) {
             const edgpu_substream_out& R = subs[rep[s.sender]];
             uint32_t& g = rep_reg[s.sender];

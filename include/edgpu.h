@@ -610,6 +610,15 @@ int  edgpu_tick_stats_get(edgpu_ctx* ctx, edgpu_tick_stats* out);   /* syncs; ED
  * `out` is host memory (ptr_kind EDGPU_PTR_HOST) or device memory (EDGPU_PTR_DEVICE); `n`
  * must be at least the pass's descriptors. */
 int  edgpu_fanout_arrivals(edgpu_ctx* ctx, int64_t* out, uint32_t n, int ptr_kind);
+/* edgpu_fanout_arrivals and / or, per descriptor of the current pass, the blob slot (byte offset /
+ * 16) of its packet in the batch of the LAST edgpu_ingest -- when that was a host batch
+ * (EDGPU_PTR_PINNED or EDGPU_PTR_HOST) and the packet came with it -- else EDGPU_NO_SOURCE.  A host
+ * that still holds that blob can read an identity UDP descriptor's bytes (the packet, `len` bytes)
+ * at blob + slot * 16 + 4 instead of reading the arena back (the module adapter does); for other
+ * sub-streams the arena's bytes differ (framing, rewrite).  Either output may be NULL; serial
+ * ticks; syncs. */
+#define EDGPU_NO_SOURCE 0xFFFFFFFFu
+int  edgpu_fanout_packet_info(edgpu_ctx* ctx, int64_t* arrivals, uint32_t* sources, uint32_t n, int ptr_kind);
 
 /* Packs regions of a fan-out arena (16-B aligned offsets and lengths; in the order given)
  * back to back into `dst` on the context stream -- so a host egress brings only the distinct

@@ -27,13 +27,14 @@ namespace {
 thread_local std::string g_err;
 int fail(int code, const char* m) { g_err = m; return code; }
 
-struct Pkt { std::string data; int64_t arrival; };
+struct Pkt { std::string data; int64_t arrival; uint32_t slot, epoch; };   // epoch: its host ingest (0: none)
 struct Sub { uint32_t handle, session, track; uint8_t kind, transport; size_t cursor; bool active, fresh; };
 struct Sess { uint32_t ntracks; bool alive; std::vector<std::vector<Pkt>> q; };   // per sender (2 x track)
 
 }  // namespace
 
 struct edgpu_ctx {
+    uint32_t ingest_epoch = 0, host_epoch_last = 0;   // edgpu_fanout_packet_info's batch sources
     uint64_t calls = 0;                     // written by every context call (unlocked, on purpose)
     std::mutex stage_mu;                    // prestage + host buffers, from any thread
     std::vector<uint8_t> staged;            // a copy of the prefix the stager pushed ahead
@@ -49,6 +50,7 @@ struct edgpu_ctx {
     std::vector<uint8_t> arena;
     std::vector<edgpu_out_desc> desc;
     std::vector<int64_t> arrivals;
+    std::vector<uint32_t> sources;
     std::vector<edgpu_substream_out> table;
     uint64_t relayed = 0, relayed_bytes = 0;
 };
@@ -202,6 +204,9 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* d, uint32_t n, const uint32
         x->staged.clear();
     }
     if (x->pending) return fail(EDGPU_ERR, "keyframe index pending");
+    const uint32_t epoch = where == EDGPU_PTR_DEVICE ? 0u : ++x->ingest_epoch;
+    if (!epoch) ++x->ingest_epoch;
+    x->host_epoch_last = epoch;
     for (uint32_t k = 0; k < nseg; k++) {
         if (sess[k] >= x->sessions.size() || !x->sessions[sess[k]].alive) continue;
         Sess& S = x->sessions[sess[k]];
@@ -209,7 +214,8 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* d, uint32_t n, const uint32
             const uint32_t len = std::min<uint32_t>(d[i].len, 2060);
             const uint32_t snd = d[i].channel;
             if (snd >= S.q.size()) continue;
-            S.q[snd].push_back(Pkt{std::string((const char*)blob + (size_t)d[i].slot * 16 + 4, len), d[i].arrival_ms});
+            S.q[snd].push_back(Pkt{std::string((const char*)blob + (size_t)d[i].slot * 16 + 4, len), d[i].arrival_ms, d[i].slot,
+                                   epoch});
         }
     }
     x->pending = true;
@@ -219,7 +225,7 @@ int edgpu_keyframe_index(edgpu_ctx* x) { touch(x); x->pending = false; return ED
 
 int edgpu_fanout(edgpu_ctx* x, int64_t, edgpu_fanout_result* out) {
     touch(x);
-    x->arena.clear(); x->desc.clear(); x->arrivals.clear(); x->table.clear();
+    x->arena.clear(); x->desc.clear(); x->arrivals.clear(); x->sources.clear(); x->table.clear();
     x->relayed = x->relayed_bytes = 0;
     for (Sub& q : x->subs) {
         edgpu_substream_out o;
@@ -227,7 +233,9 @@ int edgpu_fanout(edgpu_ctx* x, int64_t, edgpu_fanout_result* out) {
         o.subscriber = q.handle; o.track = (uint16_t)q.track; o.kind = q.kind; o.transport = q.transport;
         o.sender = 2 * q.track + q.kind;            // sessions' senders as distinct ids
         o.sender += 64 * q.session;
-        o.flags = q.fresh ? EDGPU_SUB_NEW : 0u;    // every sub-stream has its own bytes here
+        // (every sub-stream has its own bytes here; UDP ones are identity: each a suffix of its
+        // sender's longest, as the engine's)
+        o.flags = (q.fresh ? EDGPU_SUB_NEW : 0u) | (q.transport ? 0u : EDGPU_SUB_IDENTITY);
         q.fresh = false;
         o.desc_base = (uint32_t)x->desc.size();
         o.out_base = x->arena.size();
@@ -244,6 +252,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t, edgpu_fanout_result* out) {
                 memcpy(&x->arena[slot + 4], pk[i].data.data(), len);
                 x->desc.push_back(edgpu_out_desc{slot + (q.transport ? 0 : 4), len + (q.transport ? 4u : 0u), (uint32_t)i + 1});
                 x->arrivals.push_back(pk[i].arrival);
+                x->sources.push_back(x->host_epoch_last && pk[i].epoch == x->host_epoch_last ? pk[i].slot : EDGPU_NO_SOURCE);
                 x->relayed++;
                 x->relayed_bytes += len;
             }
@@ -277,6 +286,13 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int) {
     touch(x);
     if (n < x->arrivals.size()) return EDGPU_OUT_OVERFLOW;
     if (!x->arrivals.empty()) memcpy(out, x->arrivals.data(), x->arrivals.size() * sizeof(int64_t));
+    return EDGPU_OK;
+}
+int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources, uint32_t n, int) {
+    touch(x);
+    if (n < x->arrivals.size()) return EDGPU_OUT_OVERFLOW;
+    if (arrivals && !x->arrivals.empty()) memcpy(arrivals, x->arrivals.data(), x->arrivals.size() * sizeof(int64_t));
+    if (sources && !x->sources.empty()) memcpy(sources, x->sources.data(), x->sources.size() * sizeof(uint32_t));
     return EDGPU_OK;
 }
 int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* r, uint32_t n) {
