@@ -30,7 +30,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_session_relocations", "edgpu_session_key_update",
-    "edgpu_stream_errors",
+    "edgpu_stream_errors", "edgpu_fanout_packet_info",
     "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
@@ -45,6 +45,7 @@ EXPORTED = [
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
+NO_SOURCE = 0xFFFFFFFF
 
 
 class Config(C.Structure):
@@ -213,6 +214,7 @@ def load(path: str = LIB_PATH):
         "edgpu_session_relocations": (I32, [P, P, U32, P]),
         "edgpu_session_key_update": (I32, [P, P, U32]),
         "edgpu_stream_errors": (I32, [P, P, P, U32, P]),
+        "edgpu_fanout_packet_info": (I32, [P, P, P, U32, I32]),
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
@@ -574,6 +576,13 @@ class Context:
         """Arrival time (ms) of each of the last tick's `n` descriptors (edgpu_fanout_arrivals)."""
         out = np.zeros(max(int(n), 1), dtype=np.int64)
         _check(self.lib.edgpu_fanout_arrivals(self.h, _ptr(out), out.size, PTR_HOST))
+        return out[:n]
+
+    def fanout_sources(self, n: int) -> np.ndarray:
+        """Per descriptor of the current pass: its packet's blob slot in the last host batch, or
+        NO_SOURCE (edgpu_fanout_packet_info)."""
+        out = np.zeros(max(int(n), 1), dtype=np.uint32)
+        _check(self.lib.edgpu_fanout_packet_info(self.h, None, _ptr(out), out.size, PTR_HOST))
         return out[:n]
 
     def read_tick(self, r: FanoutResult):

@@ -295,3 +295,46 @@ def test_churn_keeps_the_tables_bounded():
             sizes.append((c["senders"], c["substream_rows"]))
     # 6 tracks live at most: 12 senders; 2 subscribers x 2 sub-streams per track: 24 rows
     assert sizes == [(12, 24)] * 6
+
+
+@pytest.mark.gpu
+def test_fanout_sources_point_into_the_last_host_batch():
+    """edgpu_fanout_packet_info's sources: a descriptor whose packet came with the last host batch
+    names its blob slot, and the packet bytes there are the identity UDP wire bytes in the arena;
+    packets of an earlier batch (a new output's GOP replay) and of a device batch have none."""
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(H264))
+        ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+        rng = np.random.default_rng(3)
+
+        def batch(t, seq0, n):
+            return edgpu.build_batch([(s, 0, t, _rtp(seq0 + k, 90 * t, payload=bytes([0x65 if k == 0 else 0x41])
+                                                     + rng.bytes(int(rng.integers(20, 1300))))) for k in range(n)])
+
+        def check(b, want_sources):
+            desc, seg_off, seg_sess, blob = b
+            r = ctx.fanout(0)
+            st, subs, d, arena = ctx.read_tick(r)
+            src = ctx.fanout_sources(st.pass_packets)
+            got = 0
+            for q in subs:
+                for i in range(int(q["desc_count"])):
+                    k = int(q["desc_base"]) + i
+                    off, ln = int(d["offset"][k]), int(d["len"][k])
+                    if src[k] == edgpu.NO_SOURCE:
+                        continue
+                    got += 1
+                    assert bytes(blob[int(src[k]) * 16 + 4:int(src[k]) * 16 + 4 + ln]) == bytes(arena[off:off + ln])
+            assert got == want_sources, (got, want_sources)
+            return int(st.pass_packets)
+
+        b1 = batch(10, 100, 12)
+        ctx.ingest_host(*b1)
+        ctx.keyframe_index()
+        assert check(b1, 12) == 12                 # every packet came with this batch
+        b2 = batch(20, 200, 5)
+        ctx.ingest_host(*b2)
+        ctx.keyframe_index()
+        ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)  # a new output: the GOP from batch 1 + batch 2
+        n = check(b2, 10)                           # 5 new packets x 2 outputs have sources
+        assert n == 5 + 12 + 5
