@@ -307,8 +307,8 @@ def test_fanout_sources_point_into_the_last_host_batch():
         ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
         rng = np.random.default_rng(3)
 
-        def batch(t, seq0, n):
-            return edgpu.build_batch([(s, 0, t, _rtp(seq0 + k, 90 * t, payload=bytes([0x65 if k == 0 else 0x41])
+        def batch(t, seq0, n, key):
+            return edgpu.build_batch([(s, 0, t, _rtp(seq0 + k, 90 * t, payload=bytes([0x65 if k == 0 and key else 0x41])
                                                      + rng.bytes(int(rng.integers(20, 1300))))) for k in range(n)])
 
         def check(b, want_sources):
@@ -328,11 +328,11 @@ def test_fanout_sources_point_into_the_last_host_batch():
             assert got == want_sources, (got, want_sources)
             return int(st.pass_packets)
 
-        b1 = batch(10, 100, 12)
+        b1 = batch(10, 100, 12, True)
         ctx.ingest_host(*b1)
         ctx.keyframe_index()
         assert check(b1, 12) == 12                 # every packet came with this batch
-        b2 = batch(20, 200, 5)
+        b2 = batch(20, 200, 5, False)              # no key frame: the key stays in batch 1
         ctx.ingest_host(*b2)
         ctx.keyframe_index()
         ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)  # a new output: the GOP from batch 1 + batch 2
