@@ -28,6 +28,7 @@ Reflector::Reflector(const edgpu_config* cfg) {
     edgpu_config c;
     if (cfg) c = *cfg; else edgpu_config_default(&c);
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;      // 0: the engine's default (edgpu_ctx_create)
+    if (c.overlap_ticks) fBatchSources = false;                   // (per-descriptor sources need serial ticks)
     for (Batch& b : fBatch) {
         b.nslabs = c.max_batch_bytes / kSlab + 1;
         b.slabPend.reset(new Batch::Pend[b.nslabs]);
