@@ -576,6 +576,9 @@ typedef struct edgpu_pacing_config {
     uint32_t send_interval_ms, max_send_ahead_s;
     float    overbuffer_rate;
 } edgpu_pacing_config;
+/* (A subscriber's over-buffer window takes send_interval_ms, max_send_ahead_s, overbuffer_rate and
+ * over_buffer_ms when edgpu_egress_pacing turns its gate on, as an RTPSession builds its window at
+ * SETUP; the other fields apply at every send.) */
 int  edgpu_egress_pacing_config(edgpu_egress* eg, const edgpu_pacing_config* cfg);
 /* Turns the gate on for `subscriber` (NULL: off).  Call after its edgpu_egress_udp / _tcp. */
 int  edgpu_egress_pacing(edgpu_egress* eg, uint32_t subscriber, const edgpu_pacing* p);
