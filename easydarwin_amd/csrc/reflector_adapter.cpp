@@ -490,9 +490,9 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         for (uint32_t q = 0; q < nq; q++) {
             const edgpu_substream_out& s = subs[q];
             if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || s.transport == EDGPU_TRANSPORT_TCP) continue;
-            bool all = true;
-            for (uint32_t i = 0; i < s.desc_count && all; i++) all = source[s.desc_base + i] != EDGPU_NO_SOURCE;
-            fSkip[q] = all ? 1 : 0;
+            // a sub-stream is a range of its sender's queue and the batch is the queue's newest
+            // part: all its packets came with the batch iff its first one did
+            fSkip[q] = source[s.desc_base] != EDGPU_NO_SOURCE ? 1 : 0;
         }
     // the pass's distinct bytes only: one region per identity sender + the other sub-streams
     const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq, source ? fSkip.data() : nullptr);
