@@ -34,6 +34,9 @@ hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStr
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
 hipError_t launch_desc_source(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                               uint32_t epoch, uint32_t* out, hipStream_t st);
+hipError_t launch_sub_rows(const SubDev* subs, const SenderDev* senders, const edgpu_out_desc* desc, const uint32_t* sel,
+                           uint32_t nsel, uint32_t nsubs, uint32_t pass, uint32_t epoch, edgpu_packet_row* rows,
+                           uint64_t nrows, hipStream_t st);
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                                int64_t* out, hipStream_t st);
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
@@ -290,6 +293,8 @@ struct edgpu_ctx {
     DevVec<edgpu_region> d_gather_reg;          // edgpu_arena_gather
     DevVec<int64_t> d_arrivals;                 // edgpu_fanout_arrivals
     DevVec<uint32_t> d_sources;                 // edgpu_fanout_packet_info
+    DevVec<uint32_t> d_row_sel;                 // edgpu_fanout_rows
+    DevVec<edgpu_packet_row> d_rows;
     uint32_t ingest_epoch = 0;                  // ingests so far
     uint32_t host_epoch_last = 0;               // the last ingest's epoch if it was a host batch, else 0
     DevVec<uint64_t> d_gather_off;
@@ -425,7 +430,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
-    x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release(); x->d_sources.release();
+    x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release(); x->d_sources.release(); x->d_row_sel.release(); x->d_rows.release();
     if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
@@ -1748,6 +1753,36 @@ int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources,
         if (sources) HIP_CHECK(rb.add(sources, dsrc, (size_t)npass * sizeof(uint32_t)));
     }
     HIP_CHECK(rb.run());
+    return EDGPU_OK;
+}
+
+int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_packet_row* rows, uint64_t nrows, int kind) {
+    if (!x || (nsel && (!sel || !rows))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
+    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_rows needs serial ticks");
+    if (!nsel || !nrows) return EDGPU_OK;
+    HIP_CHECK(hipSetDevice(x->device));
+    TickTotals t;
+    HIP_CHECK(sync_all(x));
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
+        HIP_CHECK(rb.run());
+    }
+    if (t.status) return fail(t.status, "the last tick failed");
+    edgpu_packet_row* dr = rows;
+    if (kind == EDGPU_PTR_HOST) { HIP_CHECK(x->d_rows.reserve(nrows, x->stream)); dr = x->d_rows.ptr; }
+    HIP_CHECK(x->d_row_sel.reserve(2 * (uint64_t)nsel, x->stream));
+    HIP_CHECK(hipMemcpyAsync(x->d_row_sel.ptr, sel, 2 * (size_t)nsel * sizeof(uint32_t), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(launch_sub_rows(x->d_subs.ptr, x->d_senders.ptr, x->d_out_desc_buf[x->cur], x->d_row_sel.ptr, nsel,
+                              x->tick_nsubs, x->pass_id, x->host_epoch_last, dr, nrows, x->stream));
+    if (kind == EDGPU_PTR_HOST) {
+        Readback rb(x);
+        HIP_CHECK(rb.add(rows, dr, (size_t)nrows * sizeof(edgpu_packet_row)));
+        HIP_CHECK(rb.run());
+    } else {
+        HIP_CHECK(hipStreamSynchronize(x->stream));      // `sel` is host memory
+    }
     return EDGPU_OK;
 }
 

@@ -2472,6 +2472,47 @@ hipError_t launch_desc_source(const SubDev* subs, const SenderDev* senders, uint
     return hipGetLastError();
 }
 
+// edgpu_fanout_rows: one wave per selected sub-stream (sel[2k] its row, sel[2k + 1] its first
+// output row); each of its descriptors with the packet's arrival and batch slot, numbered as
+// k_desc_arrival numbers them.  Rows past `nrows` are not written.
+__global__ __launch_bounds__(256) void k_sub_rows(const SubDev* subs, const SenderDev* senders, const edgpu_out_desc* desc,
+                                                  const uint32_t* sel, uint32_t nsel, uint32_t nsubs, uint32_t pass,
+                                                  uint32_t epoch, edgpu_packet_row* rows, uint64_t nrows) {
+    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (k >= nsel) return;
+    const uint32_t q = sel[2 * k];
+    const uint64_t base = sel[2 * k + 1];
+    if (q >= nsubs) return;
+    const SubDev& Q = subs[q];
+    if (!Q.active || !Q.nonempty || Q.count == 0 || Q.pass != pass) return;
+    const SenderDev& D = senders[Q.sender];
+    const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(D.meta + ((uint64_t)D.pk_mask + 1) * sizeof(PktMeta));
+    const uint64_t from_batch = (epoch && D.batch_epoch == epoch) ? D.batch_lo : ~0ull;
+    for (uint64_t p = Q.a + lane; p < D.head; p += 64) {
+        const PktMeta m = meta[p & D.pk_mask];
+        const uint32_t i = m.vcount - Q.vcstart;
+        if (m.len == 0 || i >= Q.count || base + i >= nrows) continue;
+        const edgpu_out_desc o = desc[Q.desc_base + i];
+        edgpu_packet_row r;
+        r.offset = o.offset;
+        r.len = o.len;
+        r.packet_id = o.packet_id;
+        r.arrival = m.arrival;
+        r.source = p >= from_batch ? src[p & D.pk_mask] : EDGPU_NO_SOURCE;
+        r._pad = 0;
+        rows[base + i] = r;
+    }
+}
+hipError_t launch_sub_rows(const SubDev* subs, const SenderDev* senders, const edgpu_out_desc* desc, const uint32_t* sel,
+                           uint32_t nsel, uint32_t nsubs, uint32_t pass, uint32_t epoch, edgpu_packet_row* rows,
+                           uint64_t nrows, hipStream_t st) {
+    if (nsel) hipLaunchKernelGGL(k_sub_rows, dim3((nsel + 3) / 4), dim3(256), 0, st, subs, senders, desc, sel, nsel,
+                                 nsubs, pass, epoch, rows, nrows);
+    return hipGetLastError();
+}
+
 
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (nseg == 0) return hipSuccess;

@@ -28,6 +28,7 @@ Reflector::Reflector(const edgpu_config* cfg) {
     edgpu_config c;
     if (cfg) c = *cfg; else edgpu_config_default(&c);
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;      // 0: the engine's default (edgpu_ctx_create)
+    fOverlap = c.overlap_ticks != 0;
     if (c.overlap_ticks) fBatchSources = false;                   // (per-descriptor sources need serial ticks)
     for (Batch& b : fBatch) {
         b.nslabs = c.max_batch_bytes / kSlab + 1;
@@ -54,7 +55,7 @@ Reflector::~Reflector() {
         for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
             if (p) (void)edgpu_host_free(fCtx, p);
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
-    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinArr, &fPinSrc})
+    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinRows})
         if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
     edgpu_ctx_destroy(fCtx);
 }
@@ -458,44 +459,80 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
                            bool firstPass, std::vector<edgpu_blocked>* blockedOut) {
     int err;
     auto t0 = Clock::now();
-    // the sub-stream table, descriptors (and arrivals) land in pinned buffers: one DMA each
+    // the sub-stream table lands in a pinned buffer, then the rows of the writes: one per
+    // descriptor of a sub-stream that is not an identity one, one per packet of each sender's
+    // identity sub-streams (its longest one's rows serve the others, edgpu_fanout_rows)
     const uint32_t nq = res.n_substreams;
     const uint64_t nd = st.pass_packets;
-    if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out))) ||
-        (err = EnsurePinned(fPinDesc, nd * sizeof(edgpu_out_desc))))
-        return err;
+    if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
     const edgpu_substream_out* subs = (const edgpu_substream_out*)fPinSubs.p;
-    const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
     if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
-    if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
+    fRowOf.assign(nq, 0);
+    fRowDelta.assign(nq, 0);
+    uint64_t nrows = 0;
+    if (fOverlap) {
+        // tick pipelining: the descriptors themselves (no arrivals, no batch sources)
+        if (sink->WantsArrivals()) return fail_with(kBadArgument, "packet arrivals need serial ticks");
+        if ((err = EnsurePinned(fPinDesc, nd * sizeof(edgpu_out_desc))) ||
+            (err = EnsurePinned(fPinRows, nd * sizeof(edgpu_packet_row))))
+            return err;
+        if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
+        const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
+        edgpu_packet_row* rw = (edgpu_packet_row*)fPinRows.p;
+        for (uint64_t i = 0; i < nd; i++) rw[i] = edgpu_packet_row{d[i].offset, d[i].len, d[i].packet_id, -1, EDGPU_NO_SOURCE, 0};
+        for (uint32_t q = 0; q < nq; q++) { fRowOf[q] = subs[q].desc_base; fRowDelta[q] = -(int64_t)subs[q].out_base; }
+        nrows = nd;
+    } else {
+        uint32_t nsend = 0;
+        for (uint32_t q = 0; q < nq; q++)
+            if (subs[q].desc_count && (subs[q].flags & EDGPU_SUB_IDENTITY)) nsend = std::max(nsend, subs[q].sender + 1);
+        fRowRep.assign(nsend, 0xFFFFFFFFu);
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = subs[q];
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
+            uint32_t& r = fRowRep[s.sender];
+            if (r == 0xFFFFFFFFu || subs[r].desc_count < s.desc_count) r = q;
+        }
+        fRowSel.clear();
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = subs[q];
+            if (!s.desc_count || ((s.flags & EDGPU_SUB_IDENTITY) && fRowRep[s.sender] != q)) continue;
+            fRowSel.push_back(q);
+            fRowSel.push_back((uint32_t)nrows);
+            fRowOf[q] = (uint32_t)nrows;
+            fRowDelta[q] = -(int64_t)s.out_base;
+            nrows += s.desc_count;
+        }
+        for (uint32_t q = 0; q < nq; q++) {             // the others of a sender: a suffix of its rows
+            const edgpu_substream_out& s = subs[q];
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
+            const edgpu_substream_out& R = subs[fRowRep[s.sender]];
+            fRowOf[q] = fRowOf[fRowRep[s.sender]] + (R.desc_count - s.desc_count);
+            fRowDelta[q] = -(int64_t)R.out_base - (int64_t)(R.out_bytes - s.out_bytes);
+        }
+        if (nrows > 0xFFFFFFFFull) return fail_with(kRequestFailed, "tick rows exceed 2^32");
+        if ((err = EnsurePinned(fPinRows, nrows * sizeof(edgpu_packet_row)))) return err;
+        if ((err = edgpu_fanout_rows(fCtx, fRowSel.data(), (uint32_t)(fRowSel.size() / 2), (edgpu_packet_row*)fPinRows.p,
+                                     nrows, EDGPU_PTR_HOST)))
+            return err;
+    }
+    const edgpu_packet_row* rows = (const edgpu_packet_row*)fPinRows.p;
     // Packets that came with the batch this tick ingested are still in its pinned blob: an identity
     // UDP sub-stream made only of them is written from there (its wire bytes are the packets') and
     // needs no readback.  The rest -- GOP replays of new outputs, earlier batches, interleaved or
     // rewritten sub-streams -- is gathered.
-    const int64_t* arrival = nullptr;
-    const uint32_t* source = nullptr;
-    const bool useSrc = fBatchSources && fIngestedBlob != nullptr;
-    if (sink->WantsArrivals() || useSrc) {
-        if ((sink->WantsArrivals() && (err = EnsurePinned(fPinArr, nd * sizeof(int64_t)))) ||
-            (useSrc && (err = EnsurePinned(fPinSrc, nd * sizeof(uint32_t)))))
-            return err;
-        if ((err = edgpu_fanout_packet_info(fCtx, sink->WantsArrivals() ? (int64_t*)fPinArr.p : nullptr,
-                                            useSrc ? (uint32_t*)fPinSrc.p : nullptr, (uint32_t)nd, EDGPU_PTR_HOST)))
-            return err == EDGPU_BAD_ARGUMENT ? kBadArgument : err;   // overlap_ticks: no arrivals
-        if (sink->WantsArrivals()) arrival = (const int64_t*)fPinArr.p;
-        if (useSrc) source = (const uint32_t*)fPinSrc.p;
-    }
-    fSkip.assign(source ? nq : 0, 0);
-    if (source)
+    const bool useSrc = fBatchSources && fIngestedBlob != nullptr && !fOverlap;
+    fSkip.assign(useSrc ? nq : 0, 0);
+    if (useSrc)
         for (uint32_t q = 0; q < nq; q++) {
             const edgpu_substream_out& s = subs[q];
-            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || s.transport == EDGPU_TRANSPORT_TCP) continue;
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
             // a sub-stream is a range of its sender's queue and the batch is the queue's newest
             // part: all its packets came with the batch iff its first one did
-            fSkip[q] = source[s.desc_base] != EDGPU_NO_SOURCE ? 1 : 0;
+            fSkip[q] = rows[fRowOf[q]].source != EDGPU_NO_SOURCE ? 1 : 0;
         }
     // the pass's distinct bytes only: one region per identity sender + the other sub-streams
-    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq, source ? fSkip.data() : nullptr);
+    const edgpu_host::TickRegions tr = edgpu_host::tick_regions(subs, nq, useSrc ? fSkip.data() : nullptr);
     if (tr.bytes > fHostOutCap) {            // grown geometrically: pinning costs ~40 ms per call
         if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
         fHostOut = nullptr; fHostOutCap = 0;
@@ -505,8 +542,8 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         fHostOut = (uint8_t*)h;
         fHostOutCap = cap;
     }
-    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) + nd * sizeof(edgpu_out_desc) +
-                            (arrival ? nd * sizeof(int64_t) : 0) + (source ? nd * sizeof(uint32_t) : 0);
+    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) +
+                            (fOverlap ? nd * sizeof(edgpu_out_desc) : nrows * sizeof(edgpu_packet_row));
     // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
     // PCIe, one pass) in up to TickParts::kMax parts of the sub-stream table, each part's regions after the
     // previous part's: with several write threads a gather thread brings part k + 1 over while the
@@ -545,8 +582,9 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     if (firstPass) sink->BeginTick(subs, nq);               // every row carries its flags in every pass
     WriteJob job;
     job.subs = subs; job.nsubs = nq;
-    job.desc = d; job.arrival = arrival;
-    job.batch = fIngestedBlob; job.source = source;
+    job.rows = rows; job.row_of = fRowOf.data(); job.delta = fRowDelta.data();
+    job.arrivals = sink->WantsArrivals();
+    job.batch = useSrc ? fIngestedBlob : nullptr;
     job.sink = sink;
     job.host = fHostOut;
     job.regions = &tr;
@@ -610,18 +648,20 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
             if (j.failed->load(std::memory_order_relaxed)) { r.writes = writes; return; }
         }
         const uint8_t* base = fromBatch ? nullptr : j.regions->at(j.host, s);
+        const int64_t delta = j.delta[s];
+        const edgpu_packet_row* row = j.rows + j.row_of[s];
         for (uint32_t i = 0; i < q.desc_count; i++) {
-            const edgpu_out_desc& o = j.desc[q.desc_base + i];
+            const edgpu_packet_row& o = row[i];
             PacketWrite w;
             w.subscriber = q.subscriber;
             w.track = q.track;
             w.isRTCP = q.kind != 0;
             w.interleaved = q.transport == EDGPU_TRANSPORT_TCP;
             // (a batch slot holds 4 bytes of interleave-header room, then the packet)
-            w.wire = fromBatch ? j.batch + (uint64_t)j.source[q.desc_base + i] * 16 + 4 : base + (o.offset - q.out_base);
+            w.wire = fromBatch ? j.batch + (uint64_t)o.source * 16 + 4 : base + ((int64_t)o.offset + delta);
             w.wireLen = o.len;
             w.packetID = o.packet_id;
-            w.arrivalMs = j.arrival ? j.arrival[q.desc_base + i] : -1;
+            w.arrivalMs = j.arrivals ? o.arrival : -1;
             w.sender = q.sender;
             w.newOutput = (q.flags & EDGPU_SUB_NEW) != 0;
             w.worker = worker;

@@ -216,11 +216,15 @@ private:
     // the write phase of a tick, for the subscribers of one worker
     struct WriteJob {
         const edgpu_substream_out* subs; uint32_t nsubs;
-        const edgpu_out_desc* desc; const int64_t* arrival;
+        // sub-stream s's i-th write is rows[row_of[s] + i] (edgpu_fanout_rows: identity sub-streams
+        // of one sender share their longest one's rows); its bytes are at regions->at(host, s) +
+        // row.offset + delta[s]
+        const edgpu_packet_row* rows; const uint32_t* row_of; const int64_t* delta;
+        bool arrivals = false;                                          // the sink wants row.arrival
         const uint8_t* host; const edgpu_host::TickRegions* regions;   // the tick's bytes
         // identity UDP sub-streams without a region: every packet came with the batch this tick
-        // ingested, still in `batch` (the pinned blob); source[d] = its slot (edgpu_fanout_packet_info)
-        const uint8_t* batch = nullptr; const uint32_t* source = nullptr;
+        // ingested, still in `batch` (the pinned blob), at its row's source slot
+        const uint8_t* batch = nullptr;
         OutputSink* sink;
         // the gather's parts: sub-streams [part_q[k-1], part_q[k]) need part k; `ready` counts the
         // parts in the pinned buffer; `failed`: a gather failed (the writers stop)
@@ -258,7 +262,10 @@ private:
     // readback buffers
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
-    PinBuf fPinSubs, fPinDesc, fPinArr, fPinSrc;            // sub-stream table, descriptors, arrivals, sources
+    PinBuf fPinSubs, fPinDesc, fPinRows;                    // sub-stream table, descriptors (overlap_ticks), rows
+    std::vector<uint32_t> fRowSel, fRowOf, fRowRep;         // edgpu_fanout_rows' selection, per sub-stream row start
+    std::vector<int64_t> fRowDelta;
+    bool fOverlap = false;                                  // edgpu_config.overlap_ticks: no edgpu_fanout_rows
     const uint8_t* fIngestedBlob = nullptr;                 // the blob the last FlushIngest ingested (intact
                                                             // until the next one swaps it back in)
     bool fBatchSources = true;                              // EDGPU_BATCH_SOURCES=0: read every byte back

@@ -30,7 +30,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_session_relocations", "edgpu_session_key_update",
-    "edgpu_stream_errors", "edgpu_fanout_packet_info",
+    "edgpu_stream_errors", "edgpu_fanout_packet_info", "edgpu_fanout_rows",
     "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
@@ -215,6 +215,7 @@ def load(path: str = LIB_PATH):
         "edgpu_session_key_update": (I32, [P, P, U32]),
         "edgpu_stream_errors": (I32, [P, P, P, U32, P]),
         "edgpu_fanout_packet_info": (I32, [P, P, P, U32, I32]),
+        "edgpu_fanout_rows": (I32, [P, P, U32, P, U64, I32]),
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
@@ -584,6 +585,25 @@ class Context:
         out = np.zeros(max(int(n), 1), dtype=np.uint32)
         _check(self.lib.edgpu_fanout_packet_info(self.h, None, _ptr(out), out.size, PTR_HOST))
         return out[:n]
+
+    ROW_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("packet_id", "<u4"), ("arrival", "<i8"),
+                          ("source", "<u4"), ("_pad", "<u4")])
+
+    def fanout_rows(self, sel) -> np.ndarray:
+        """edgpu_fanout_rows: `sel` = [(substream row, first output row), ...]; returns the rows
+        (offset, len, packet_id, arrival, source) of those sub-streams' descriptors."""
+        sel = np.ascontiguousarray(np.asarray(sel, dtype=np.uint32).reshape(-1, 2))
+        nrows = int(sel[:, 1].max()) + 1 if sel.size else 0
+        return self._rows(sel, nrows)
+
+    def fanout_rows_n(self, sel, nrows: int) -> np.ndarray:
+        sel = np.ascontiguousarray(np.asarray(sel, dtype=np.uint32).reshape(-1, 2))
+        return self._rows(sel, int(nrows))
+
+    def _rows(self, sel, nrows):
+        out = np.zeros(max(nrows, 1), dtype=self.ROW_DTYPE)
+        _check(self.lib.edgpu_fanout_rows(self.h, _ptr(sel), len(sel), _ptr(out), nrows, PTR_HOST))
+        return out[:nrows]
 
     def read_tick(self, r: FanoutResult):
         """(stats, substream table, descriptors, arena) of the current copy pass of the last

@@ -623,6 +623,26 @@ int  edgpu_fanout_arrivals(edgpu_ctx* ctx, int64_t* out, uint32_t n, int ptr_kin
 #define EDGPU_NO_SOURCE 0xFFFFFFFFu
 int  edgpu_fanout_packet_info(edgpu_ctx* ctx, int64_t* arrivals, uint32_t* sources, uint32_t n, int ptr_kind);
 
+/* What a host write loop needs of one descriptor, in one row: the descriptor, its packet's
+ * arrival (edgpu_fanout_arrivals) and batch slot (edgpu_fanout_packet_info's sources). */
+typedef struct edgpu_packet_row {
+    uint64_t offset;        /* edgpu_out_desc.offset */
+    uint32_t len;           /* edgpu_out_desc.len */
+    uint32_t packet_id;     /* edgpu_out_desc.packet_id */
+    int64_t  arrival;       /* fTimeArrived */
+    uint32_t source;        /* blob slot in the last host batch, or EDGPU_NO_SOURCE */
+    uint32_t _pad;
+} edgpu_packet_row;
+/* The rows of SELECTED sub-streams of the current copy pass only: sel[2k] is a row of the
+ * sub-stream table, sel[2k + 1] where its rows start in `rows`: rows[sel[2k + 1] + i] for its
+ * descriptor desc_base + i, i < desc_count (rows at or past `nrows` are not written).  Two
+ * EDGPU_SUB_IDENTITY sub-streams of one sender share their packets (the shorter a suffix of the
+ * longer), so a host reads one sender's rows once for all of them -- at C2 the module's
+ * readback falls from 28 B per write to 32 B per relayed packet.  `sel` is host
+ * memory; `rows` host (EDGPU_PTR_HOST) or device (EDGPU_PTR_DEVICE).  Serial ticks; syncs. */
+int  edgpu_fanout_rows(edgpu_ctx* ctx, const uint32_t* sel, uint32_t nsel, edgpu_packet_row* rows, uint64_t nrows,
+                       int ptr_kind);
+
 /* Packs regions of a fan-out arena (16-B aligned offsets and lengths; in the order given)
  * back to back into `dst` on the context stream -- so a host egress brings only the distinct
  * bytes of a tick over PCIe instead of the whole write-many arena.  `dst` is device memory, or

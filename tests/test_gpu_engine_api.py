@@ -298,6 +298,60 @@ def test_churn_keeps_the_tables_bounded():
 
 
 @pytest.mark.gpu
+def test_fanout_rows_equal_descriptors_arrivals_and_sources():
+    """edgpu_fanout_rows: for each selected sub-stream, its descriptors with their arrivals and batch
+    slots (edgpu_fanout_packet_info) at the rows asked for; identity sub-streams of one sender are
+    suffixes of the longest one's rows (what the module adapter reads back instead of every
+    descriptor)."""
+    with edgpu.Context() as ctx:
+        s = ctx.session_add(make_sdp(H264))
+        ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+        ctx.subscriber_add(s, edgpu.TRANSPORT_TCP)
+        rng = np.random.default_rng(5)
+
+        def batch(t, seq0, n, key):
+            return edgpu.build_batch([(s, 0, t + k, _rtp(seq0 + k, 90 * t, payload=bytes([0x65 if k == 0 and key else 0x41])
+                                                         + rng.bytes(int(rng.integers(20, 1300))))) for k in range(n)])
+
+        for t, seq0, n, key, join in ((10, 100, 12, True, False), (40, 200, 7, False, True)):
+            ctx.ingest_host(*batch(t, seq0, n, key))
+            ctx.keyframe_index()
+            if join:
+                ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)     # a GOP replay: longer than the others
+            r = ctx.fanout(0)
+            st, subs, d, arena = ctx.read_tick(r)
+            arr = ctx.fanout_arrivals(st.pass_packets)
+            src = ctx.fanout_sources(st.pass_packets)
+            live = [q for q in range(len(subs)) if subs[q]["desc_count"]]
+            sel, base = [], 0
+            for q in live:
+                sel.append((q, base))
+                base += int(subs[q]["desc_count"])
+            rows = ctx.fanout_rows_n(sel, base)
+            for q, b in sel:
+                n_q, db = int(subs[q]["desc_count"]), int(subs[q]["desc_base"])
+                got = rows[b:b + n_q]
+                assert (got["offset"] == d["offset"][db:db + n_q]).all()
+                assert (got["len"] == d["len"][db:db + n_q]).all()
+                assert (got["packet_id"] == d["packet_id"][db:db + n_q]).all()
+                assert (got["arrival"] == arr[db:db + n_q]).all()
+                assert (got["source"] == src[db:db + n_q]).all()
+            ident = [q for q in live if subs[q]["flags"] & edgpu.SUB_IDENTITY and subs[q]["kind"] == 0]
+            if join:
+                assert len({int(subs[q]["desc_count"]) for q in ident}) == 2
+            longest = max(ident, key=lambda q: int(subs[q]["desc_count"]))
+            lb = dict(sel)[longest]
+            for q in ident:                      # a suffix of the longest one's rows
+                n_q, b = int(subs[q]["desc_count"]), dict(sel)[q]
+                tail = rows[lb + int(subs[longest]["desc_count"]) - n_q:lb + int(subs[longest]["desc_count"])]
+                for f in ("len", "packet_id", "arrival", "source"):
+                    assert (tail[f] == rows[b:b + n_q][f]).all()
+            # rows past nrows are not written
+            short = ctx.fanout_rows_n(sel[:1], 1)
+            assert len(short) == 1 and short[0]["packet_id"] == rows[0]["packet_id"]
+
+
+@pytest.mark.gpu
 def test_fanout_sources_point_into_the_last_host_batch():
     """edgpu_fanout_packet_info's sources: a descriptor whose packet came with the last host batch
     names its blob slot, and the packet bytes there are the identity UDP wire bytes in the arena;

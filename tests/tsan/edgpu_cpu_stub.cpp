@@ -295,6 +295,20 @@ int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources,
     if (sources && !x->sources.empty()) memcpy(sources, x->sources.data(), x->sources.size() * sizeof(uint32_t));
     return EDGPU_OK;
 }
+int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_packet_row* rows, uint64_t nrows, int) {
+    touch(x);
+    for (uint32_t k = 0; k < nsel; k++) {
+        if (sel[2 * k] >= x->table.size()) continue;
+        const edgpu_substream_out& o = x->table[sel[2 * k]];
+        for (uint32_t i = 0; i < o.desc_count && sel[2 * k + 1] + (uint64_t)i < nrows; i++) {
+            const size_t d = (size_t)o.desc_base + i;
+            rows[sel[2 * k + 1] + i] = edgpu_packet_row{x->desc[d].offset, x->desc[d].len, x->desc[d].packet_id,
+                                                        d < x->arrivals.size() ? x->arrivals[d] : -1,
+                                                        d < x->sources.size() ? x->sources[d] : EDGPU_NO_SOURCE, 0};
+        }
+    }
+    return EDGPU_OK;
+}
 int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* r, uint32_t n) {
     touch(x);
     for (uint32_t i = 0; i < n; i++) {
