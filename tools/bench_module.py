@@ -36,7 +36,7 @@ def module_run(args) -> dict:
     env.setdefault("EDGPU_QTSS_WRITE_THREADS", str(args.write_threads))
     if args.concurrent_push:
         env["EDGPU_BENCH_CONCURRENT_PUSH"] = "1"
-    cmd = [os.path.join(ROOT, "tools", "qtss_replay"), os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"),
+    cmd = [os.path.join(ROOT, "tools", "qtss_replay"), args.module,
            "--bench", str(args.sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
     if r.returncode:
@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--max-out-packets", type=int, default=4 << 20)
     ap.add_argument("--timeout", type=int, default=300)
     ap.add_argument("--no-reference", action="store_true")
+    # another build of the module (A/Bs)
+    ap.add_argument("--module", default=os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so"))
     # the pushers push the next tick's packets while a tick runs, as a server's RTSP threads do
     # (default: pushing and ticking alternate, the conservative measure)
     ap.add_argument("--concurrent-push", action="store_true")
