@@ -583,16 +583,32 @@ int edgpu_egress_send(edgpu_egress* e, const edgpu_fanout_result* r, edgpu_egres
     std::vector<edgpu_blocked> blocked;
     // every copy pass of the tick, in sub-stream row order: a connection's frames keep their order
     edgpu_fanout_result cur = *r;
+    int failed = EDGPU_OK;
     for (;;) {
         edgpu_tick_stats st;
         int rc = edgpu_tick_stats_get(e->ctx, &st);
-        if (rc) return eg_fail(e, rc, "tick stats");
-        if (st.status) return eg_fail(e, st.status, "device-side status after fan-out");
-        if ((rc = send_pass(e, &cur, st, blocked, s))) return rc;
+        if (rc) { failed = eg_fail(e, rc, "tick stats"); break; }
+        if (st.status) { failed = eg_fail(e, st.status, "device-side status after fan-out"); break; }
+        if ((rc = send_pass(e, &cur, st, blocked, s))) { failed = rc; break; }
         if (!st.more_passes) break;
         uint32_t launched = 0;
-        if ((rc = edgpu_fanout_next(e->ctx, &cur, &launched))) return eg_fail(e, rc, "next copy pass");
+        if ((rc = edgpu_fanout_next(e->ctx, &cur, &launched))) { failed = eg_fail(e, rc, "next copy pass"); break; }
         if (!launched) break;
+    }
+    if (failed) {
+        // the context must not stay owing the rest of the tick (every later ingest / fan-out would
+        // be refused): the remaining passes are launched unsent (counted in lost_passes), and the
+        // blocked sub-streams of the passes already sent are still reported
+        for (uint32_t guard = 0; guard < (1u << 20); guard++) {
+            uint32_t launched = 0;
+            if (edgpu_fanout_next(e->ctx, &cur, &launched) != EDGPU_OK || !launched) break;
+        }
+        if (!blocked.empty()) {
+            std::sort(blocked.begin(), blocked.end(),
+                      [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
+            (void)edgpu_fanout_blocked(e->ctx, blocked.data(), (uint32_t)blocked.size());
+        }
+        return failed;
     }
     std::sort(blocked.begin(), blocked.end(), [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
     s.blocked_substreams = (uint32_t)blocked.size();

@@ -1657,7 +1657,12 @@ int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched
         HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
         HIP_CHECK(rb.run());
     }
-    if (t.status) return fail(t.status, "the tick failed");
+    if (t.status) {
+        // a failed tick owes nothing: its remaining passes are dropped (the next fan-out counts
+        // them in lost_passes), so the context does not refuse every later call
+        x->passes_more = 0;
+        return fail(t.status, "the tick failed");
+    }
     const uint32_t next = t.pass_next[x->pass_ord & 1u];
     if (next == kNoPass) {
         x->passes_more = 0;
@@ -1701,7 +1706,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->pass = x->pass_ord;
     out->more_passes = (x->fanout_launches && t.pass_next[slot] != kNoPass) ? 1u : 0u;
     out->stream_errors = t.stream_errors;
-    if (x->fanout_launches) x->passes_more = (int)out->more_passes;
+    if (x->fanout_launches) x->passes_more = t.status ? 0 : (int)out->more_passes;
 #ifdef EDGPU_AB_VARIANTS
     if (getenv("EDGPU_FAN_TAIL") && t.fan_done_max > t.fan_t0_min)   // 100-MHz s_memrealtime ticks
         fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u; ingest span %.1f us, first exit at %.1f us\n",

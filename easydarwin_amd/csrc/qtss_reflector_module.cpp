@@ -165,13 +165,32 @@ void GetPref(QTSS_Object prefs, const char* name, uint32_t type, T* out, T def) 
 QTSS_AttributeID sOutputAttr, sClientBroadcastSessionAttr, sRTSPBroadcastSessionAttr, sStreamCookieAttr,
     sRequestBodyAttr, sBufferOffsetAttr, sRTPInfoWaitTimeAttr, sKillClientsEnabledAttr;
 
+// The broadcaster keep-alive of one session's sockets (ReflectorSocket::fBroadcasterClientSession /
+// fLastBroadcasterTimeOutRefresh, ReflectorStream.h:216-239): every push SETUP names the pusher's
+// client session on all of the session's sockets (AddBroadcasterClientSession, ReflectorSession.cpp:
+// 193-206), its leaving clears it (RemoveSessionFromOutput, :285-293), and every pushed packet --
+// interleaved or a UDP datagram -- calls QTSS_RefreshTimeOut on it when its socket last did so more
+// than 10 s ago (ReflectorSocket::ProcessPacket, ReflectorStream.cpp:1779-1786).  The server refreshes
+// an RTSP-interleaved pusher itself on every '$' frame (RTSPSession.cpp:2157); a UDP pusher's packets
+// land on the module's sockets, so without this the server times its session out.  One socket per
+// track x {RTP, RTCP}; `last` is read and written under the lock of the path that carries the packet
+// (the route stripe or udpMu), `client` is set under `mu`.
+struct Keepalive {
+    static constexpr int64_t kIntervalMs = 10000;       // kRefreshBroadcastSessionIntervalMilliSecs
+    std::atomic<QTSS_Object> client{nullptr};
+    std::vector<std::atomic<int64_t>> last;
+    explicit Keepalive(size_t sockets) : last(sockets) { for (auto& l : last) l.store(0); }
+};
+
 struct Output;
 struct Session {                        // a pushed stream ("<path>-<channel>", QRM:1384)
     uint32_t id = 0;                    // module session id (never reused; client attributes hold it)
     std::string name;
     uint32_t engine = 0;                // edgpu session
     bool udpPush = false;               // pushed over UDP: RTCP on the odd port (Q12/Q14)
-    bool pusher = false;                // a pusher is attached (its reference)
+    uint32_t pushers = 0;               // pushers attached (each holds a reference; > 1 only with
+                                        // allow_duplicate_broadcasts)
+    std::shared_ptr<Keepalive> ka;      // the sockets' broadcaster refresh
     uint32_t refs = 0;                  // the session map's reference count: pusher + outputs
     std::vector<uint32_t> trackIDs;     // a=control:trackID=N per m= line, SDP order
     std::vector<uint16_t> sdpPorts;     // the m= lines' ports (StreamInfo::fPort)
@@ -186,6 +205,7 @@ struct UdpPair {
     int fd[2] = {-1, -1};               // -1 once its session ended
     uint16_t port = 0;
     uint32_t engine = 0, track = 0;     // engine session, track index
+    std::shared_ptr<Keepalive> ka;      // its session's (guarded by udpMu)
 };
 
 struct Output {                         // one player (RTPSessionOutput)
@@ -211,9 +231,10 @@ struct Module {
     // the pushers' path (RTSPIncomingData): module session id -> (engine session, tracks) while a
     // pusher is attached; stripe id % kRouteStripes guards its part alone
     static constexpr uint32_t kRouteStripes = 16;
+    struct Route { uint32_t engine, tracks; Keepalive* ka; };
     struct alignas(64) RouteStripe {
         std::mutex mu;
-        std::map<uint32_t, std::pair<uint32_t, uint32_t>> route;
+        std::map<uint32_t, Route> route;
     } routes[kRouteStripes];
     std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
     std::map<uint32_t, Output*> byHandle;
@@ -240,6 +261,10 @@ struct Module {
     bool playerCompat = true;           // enable_player_compatibility
     bool forceRTPInfo = false;          // force_rtp_info_sequence_and_time
     bool disableOverbuffering = false;  // disable_overbuffering
+    bool announceEnabled = true;        // enable_broadcast_announce (DoAnnounce, QRM:900)
+    std::atomic<bool> pushEnabled{true};   // enable_broadcast_push (ProcessRTPData, QRM:606; read without mu)
+    bool allowDuplicates = false;       // allow_duplicate_broadcasts (DoSetup, QRM:1682)
+    uint32_t broadcasterTimeoutMs = 30000;  // max(30, timeout_broadcaster_session_secs) x 1000 (QRM:483-487, 541)
     QTSS_Object modPrefs = nullptr;     // this module's prefs object
     QTSS_Object serverPrefs = nullptr;  // the server's prefs object (player_requires_rtp_header_info)
     uint64_t rereads = 0;
@@ -249,6 +274,7 @@ struct Module {
     std::atomic<bool> stop{false};
     QTSS_Error tickErr = QTSS_NoErr;
     EDGPU_QTSSTickInfo lastTick{};      // guarded by mu
+    std::vector<uint32_t> orphans;      // engine sessions whose removal the engine refused: retried per tick
 };
 Module* M = nullptr;
 
@@ -488,6 +514,19 @@ inline void NotifyArrival() {
     }
 }
 
+// ReflectorSocket::ProcessPacket's broadcaster refresh (ReflectorStream.cpp:1779-1786) for socket
+// `sock` (2 x track + RTCP) of a session at `now`; the caller holds the lock of the packet's path.
+inline void RefreshBroadcaster(Keepalive* ka, uint32_t sock, int64_t now) {
+    if (!ka || sock >= ka->last.size()) return;
+    QTSS_Object c = ka->client.load(std::memory_order_acquire);
+    if (!c) return;
+    std::atomic<int64_t>& last = ka->last[sock];
+    if (now - last.load(std::memory_order_relaxed) > Keepalive::kIntervalMs) {
+        (void)cb(kRefreshTimeOutCallback, c);
+        last.store(now, std::memory_order_relaxed);
+    }
+}
+
 // ReflectorSocket::GetIncomingData (ReflectorStream.cpp:1716-1735): every datagram waiting on a
 // UDP push socket, read like RecvFrom into a kMaxReflectorPacketSize (2060) buffer -- a longer
 // datagram is truncated there -- and handed to the engine with its source address (the UDP RTCP
@@ -510,8 +549,10 @@ uint32_t DrainUDP() {
                     break;                                            // EAGAIN: drained
                 }
                 if (r == 0) continue;
+                const int64_t now = Milliseconds();
+                RefreshBroadcaster(u.ka.get(), 2 * u.track + (uint32_t)k, now);
                 M->R->ProcessUDPPacket(u.engine, u.track, k == 1, buf, (uint32_t)r, ntohl(from.sin_addr.s_addr),
-                                       ntohs(from.sin_port), Milliseconds());
+                                       ntohs(from.sin_port), now);
                 NotifyArrival();
                 n++;
             }
@@ -544,6 +585,9 @@ QTSS_Error Tick() {
     QTSSSink sink;
     sink.now = Milliseconds();
     const int err = M->R->ReflectPackets(sink.now, &sink);
+    for (size_t i = 0; i < M->orphans.size();)
+        if (M->R->RemoveSession(M->orphans[i], true) == 0) M->orphans.erase(M->orphans.begin() + i);
+        else i++;
     const edgpu_reflector::Reflector::TickInfo& t = M->R->LastTick();
     EDGPU_QTSSTickInfo& o = M->lastTick;
     o.ingested_packets = t.ingested_packets; o.ingested_bytes = t.ingested_bytes;
@@ -615,6 +659,14 @@ void ReadModulePrefsLocked() {
     GetPref<bool>(o, "disable_overbuffering", qtssAttrDataTypeBool16, &M->disableOverbuffering, false);
     GetPref<bool>(o, "enable_player_compatibility", qtssAttrDataTypeBool16, &M->playerCompat, true);
     GetPref<bool>(o, "force_rtp_info_sequence_and_time", qtssAttrDataTypeBool16, &M->forceRTPInfo, false);
+    GetPref<bool>(o, "enable_broadcast_announce", qtssAttrDataTypeBool16, &M->announceEnabled, true);
+    bool push = true;
+    GetPref<bool>(o, "enable_broadcast_push", qtssAttrDataTypeBool16, &push, true);
+    M->pushEnabled.store(push, std::memory_order_relaxed);
+    GetPref<bool>(o, "allow_duplicate_broadcasts", qtssAttrDataTypeBool16, &M->allowDuplicates, false);
+    uint32_t bsecs = 30;
+    GetPref<uint32_t>(o, "timeout_broadcaster_session_secs", qtssAttrDataTypeUInt32, &bsecs, 30u);
+    M->broadcasterTimeoutMs = std::max<uint32_t>(bsecs, 30) * 1000;
 }
 
 QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
@@ -734,6 +786,10 @@ QTSS_Error DoAnnounce(QTSS_StandardRTSP_Params* p) {
     // any name will do (the reference's SDP suffix is empty, QRM:183, 953-962); an announced
     // "<name>.kill" only looks a session up to kill it (QRM:940-951, 1052-1059) -- by the bare name,
     // which never carries the "-<channel>" every session name has, so here it is refused outright
+    {   // enable_broadcast_announce (QRM:900: 412 Precondition Failed, nothing cached)
+        std::lock_guard<std::mutex> g(M->mu);
+        if (!M->announceEnabled) return QTSS_RequestFailed;
+    }
     const std::string name = GetString(p->inRTSPRequest, qtssRTSPReqFileName);
     if (name.size() > 5 && name.compare(name.size() - 5, 5, ".kill") == 0) return QTSS_RequestFailed;
     uint32_t clen = 0;
@@ -790,7 +846,7 @@ Session* FindSession(uint32_t id) {
 void SetRoute(const Session& s, bool on) {
     Module::RouteStripe& r = M->routes[s.id % Module::kRouteStripes];
     std::lock_guard<std::mutex> g(r.mu);
-    if (on) r.route[s.id] = std::make_pair(s.engine, (uint32_t)s.trackIDs.size());
+    if (on) r.route[s.id] = Module::Route{s.engine, (uint32_t)s.trackIDs.size(), s.ka.get()};
     else r.route.erase(s.id);
 }
 
@@ -820,6 +876,7 @@ Session* FindOrCreateSession(const std::string& name, bool isPush, bool udpPush 
     s.sdpPorts.resize(s.trackIDs.size(), 0);
     s.pair.assign(s.trackIDs.size(), -1);
     s.setupToReceive.assign(s.trackIDs.size(), false);
+    s.ka = std::make_shared<Keepalive>(2 * s.trackIDs.size());
     // each ReflectorStream draws its receiver-report SSRC from rand() and its CNAME from
     // OS::Milliseconds()/1000 when it is built (ReflectorStream.cpp:164-201, RTCPSRPacket.cpp:87-117)
     for (uint32_t t = 0; t < s.trackIDs.size(); t++)
@@ -836,13 +893,20 @@ void ReleaseLocked(Session* s) {
     if (s->refs > 0) s->refs--;
     if (s->refs > 0) return;
     SetRoute(*s, false);
-    if (M->R) (void)M->R->RemoveSession(s->engine, false);
+    // the engine may refuse (a device error): the session is gone from the module either way, and
+    // its engine session -- rings and all -- is removed at a later tick instead of leaking
+    if (M->R && M->R->RemoveSession(s->engine, false) != 0) {
+        fprintf(stderr, "QTSSReflectorModule: session %s: engine removal deferred (%s)\n", s->name.c_str(), edgpu_last_error());
+        M->orphans.push_back(s->engine);
+    }
     {
         std::lock_guard<std::mutex> g(M->udpMu);
         for (int pi : s->pair)
-            if (pi >= 0)
+            if (pi >= 0) {
                 for (int& fd : M->udp[pi].fd)
                     if (fd >= 0) { close(fd); fd = -1; }
+                M->udp[pi].ka.reset();
+            }
     }
     M->byName.erase(s->name);
     M->announced.erase(s->name);
@@ -878,12 +942,17 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         if (first) s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
         if (!s) return QTSS_RequestFailed;
         if (first) DisableOverbufferingIfPref(p->inClientSession);
+        // the pusher's client session times out after timeout_broadcaster_session_secs (at least
+        // 30 s) without a refresh; set at every push SETUP once the session resolved (QRM:1644)
+        const uint32_t tmo = M->broadcasterTimeoutMs;
+        (void)SetValue(p->inClientSession, qtssCliSesTimeoutMsec, 0, &tmo, sizeof(tmo));
         // the reference sets the session up for one transport; a pusher of the other cannot join it
         // (DeleteReflectorPushSession: the reference it took goes back, :1548-1570)
         auto refuse = [&]() { if (first && s->refs == 0) ReleaseLocked(s); return QTSS_RequestFailed; };
         if (!digitOK || s->udpPush != udp) return refuse();
         const int t = TrackIndex(*s, trackID);
-        if (t < 0 || s->setupToReceive[t]) return refuse();              // bad / duplicate track
+        // a bad track, or one another pusher set up: refused unless allow_duplicate_broadcasts (QRM:1682)
+        if (t < 0 || (s->setupToReceive[t] && !M->allowDuplicates)) return refuse();
         if (udp) {
             // the track's socket pair (BindSockets) and its port in the SETUP response
             if (s->pair[t] < 0) {
@@ -891,6 +960,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
                 if (!BindPair(s->sdpPorts[t], &u)) return refuse();        // sCantBindReflectorSocketErr
                 u.engine = s->engine;
                 u.track = (uint32_t)t;
+                u.ka = s->ka;
                 std::lock_guard<std::mutex> ug(M->udpMu);
                 // a slot an ended session left (both sockets closed) is reused: the table and the
                 // reader's poll set stay as large as the live UDP tracks under churn
@@ -910,9 +980,11 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         s->setupToReceive[t] = true;
         if (first) {                                     // the pusher's reference
             s->refs++;
-            s->pusher = true;
+            s->pushers++;
             SetRoute(*s, true);
         }
+        // AddBroadcasterClientSession (QRM:1715): this pusher is the one every socket refreshes
+        s->ka->client.store(p->inClientSession, std::memory_order_release);
         const uintptr_t sid = s->id;
         (void)SetValue(p->inClientSession, sClientBroadcastSessionAttr, 0, &sid, sizeof(sid));
         return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)0);
@@ -1103,6 +1175,7 @@ QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
 // RTSPIncomingData (ProcessRTPData, QRM:604-678): one '$' ch BE16(len) frame of a pusher.  Never
 // takes `mu`: one stripe of the route table and one of the Reflector's push path, so it never waits for a tick.
 QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
+    if (!M->pushEnabled.load(std::memory_order_relaxed)) return QTSS_NoErr;      // enable_broadcast_push (QRM:606)
     uintptr_t sid = 0;
     if (!GetPOD(p->inRTSPSession, sRTSPBroadcastSessionAttr, &sid) || !sid) return QTSS_NoErr;
     if (!p->inPacketData || p->inPacketLen < 4) return QTSS_NoErr;
@@ -1116,8 +1189,11 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
     auto it = r.route.find((uint32_t)sid);
     if (!M->R || it == r.route.end()) return QTSS_NoErr;       // no pusher attached any more
     const uint32_t track = channel / 2;
-    if (track >= it->second.second) return QTSS_NoErr;
-    M->R->PushPacket(it->second.first, track, (const char*)d + 4, len, (channel & 1) != 0, now);
+    if (track >= it->second.tracks) return QTSS_NoErr;
+    // ReflectorStream::PushPacket takes only non-empty packets to ProcessPacket (RS.cpp:533), whose
+    // first step is the broadcaster refresh
+    if (len) RefreshBroadcaster(it->second.ka, channel, now);
+    M->R->PushPacket(it->second.engine, track, (const char*)d + 4, len, (channel & 1) != 0, now);
     NotifyArrival();
     return QTSS_NoErr;
 }
@@ -1144,10 +1220,13 @@ QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
         {
             std::lock_guard<std::mutex> g(M->mu);
             Session* s = FindSession((uint32_t)sid);
-            if (!s || !s->pusher) return QTSS_NoErr;
+            if (!s || !s->pushers) return QTSS_NoErr;
             s->setupToReceive.assign(s->setupToReceive.size(), false);   // a new pusher may set up
-            s->pusher = false;
-            SetRoute(*s, false);
+            // RemoveSessionFromOutput: the sockets stop refreshing this pusher (another one keeps
+            // its own place only if it set up last, ReflectorStream.h:217)
+            QTSS_Object me = p->inClientSession;
+            s->ka->client.compare_exchange_strong(me, nullptr, std::memory_order_acq_rel);
+            if (--s->pushers == 0) SetRoute(*s, false);
             // RemoveOutput(NULL, session, kill): TearDownAllOutputs asks the server to close every
             // output's client session (RTPSessionOutput::TearDown); each then comes back through
             // ClientSessionClosing and releases its reference

@@ -418,39 +418,60 @@ int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     edgpu_fanout_result res;
     if ((err = edgpu_fanout(fCtx, nowMs, &res))) return err;
     uint32_t nrr = 0;
-    if ((err = edgpu_source_reports(fCtx, nullptr, 0, &nrr)) && nrr == 0) return err;
-    if (nrr && sink) {
+    err = edgpu_source_reports(fCtx, nullptr, 0, &nrr);
+    if (err && nrr) err = kNoErr;
+    if (!err && nrr && sink) {
         std::vector<edgpu_source_report> rr(nrr);
-        if ((err = edgpu_source_reports(fCtx, rr.data(), nrr, &nrr))) return err;
-        for (const edgpu_source_report& r : rr)
-            sink->SendReceiverReport(r.session, r.track, r.addr, r.port, r.bytes, r.len);
+        if (!(err = edgpu_source_reports(fCtx, rr.data(), nrr, &nrr)))
+            for (const edgpu_source_report& r : rr)
+                sink->SendReceiverReport(r.session, r.track, r.addr, r.port, r.bytes, r.len);
     }
     edgpu_tick_stats st;
+    std::vector<edgpu_blocked> blocked;
+    if (!err) err = DeliverTick(&res, &st, sink, &blocked, t0);
+    if (err) {
+        // A pass that failed must not leave the context owing the rest of the tick: every later
+        // ingest, fan-out and session removal would be refused for good.  The remaining passes are
+        // launched without delivery (the engine counts them in lost_passes) and the blocked
+        // sub-streams of the passes delivered so far are still reported; the first error stands.
+        for (uint32_t guard = 0; guard < (1u << 20); guard++) {
+            uint32_t launched = 0;
+            if (edgpu_fanout_next(fCtx, &res, &launched) != 0 || !launched) break;
+        }
+    }
+    if (blocked.empty()) return err;
+    std::sort(blocked.begin(), blocked.end(),
+              [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
+    const int berr = edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
+    return err ? err : berr;
+}
+
+// Every copy pass of the tick fan-out launched (its first pass): a tick over the arena comes in
+// copy passes of consecutive sub-stream rows (edgpu_fanout_next), each delivered before the next is
+// copied, so every output gets the whole tick, in the order one pass would have written it.
+// Backpressure reports cover the whole tick (appended to *blocked, reported by the caller).
+int Reflector::DeliverTick(edgpu_fanout_result* res, edgpu_tick_stats* stp, OutputSink* sink,
+                           std::vector<edgpu_blocked>* blocked, Clock::time_point t0) {
+    edgpu_tick_stats& st = *stp;
+    int err;
     if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
     fTick.fanout_ms = ms_since(t0);
     if (st.status) return st.status;
     fTick.stream_errors = st.stream_errors;             // the tick went on for every other session
     fTick.arena_bytes = st.arena_bytes;
-    // A tick over the arena comes in copy passes of consecutive sub-stream rows (edgpu_fanout_next):
-    // each is delivered before the next is copied, so every output gets the whole tick, in the order
-    // one pass would have written it.  Backpressure reports cover the whole tick.
-    std::vector<edgpu_blocked> blocked;
     for (uint32_t pass = 0;; pass++) {
         fTick.passes++;
         if (sink && st.pass_packets) {
-            if ((err = DeliverPass(res, st, sink, pass == 0, &blocked))) return err;
+            if ((err = DeliverPass(*res, st, sink, pass == 0, blocked))) return err;
         }
         if (!st.more_passes) break;
         uint32_t launched = 0;
-        if ((err = edgpu_fanout_next(fCtx, &res, &launched))) return err;
+        if ((err = edgpu_fanout_next(fCtx, res, &launched))) return err;
         if (!launched) break;
         if ((err = edgpu_tick_stats_get(fCtx, &st))) return err;
         if (st.status) return st.status;
     }
-    if (blocked.empty()) return kNoErr;
-    std::sort(blocked.begin(), blocked.end(),
-              [](const edgpu_blocked& a, const edgpu_blocked& b) { return a.substream < b.substream; });
-    return edgpu_fanout_blocked(fCtx, blocked.data(), (uint32_t)blocked.size());
+    return kNoErr;
 }
 
 // One copy pass: its sub-stream table, descriptors (and arrivals) and distinct bytes come to pinned
@@ -483,16 +504,9 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         for (uint32_t q = 0; q < nq; q++) { fRowOf[q] = subs[q].desc_base; fRowDelta[q] = -(int64_t)subs[q].out_base; }
         nrows = nd;
     } else {
-        uint32_t nsend = 0;
-        for (uint32_t q = 0; q < nq; q++)
-            if (subs[q].desc_count && (subs[q].flags & EDGPU_SUB_IDENTITY)) nsend = std::max(nsend, subs[q].sender + 1);
-        fRowRep.assign(nsend, 0xFFFFFFFFu);
-        for (uint32_t q = 0; q < nq; q++) {
-            const edgpu_substream_out& s = subs[q];
-            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY)) continue;
-            uint32_t& r = fRowRep[s.sender];
-            if (r == 0xFFFFFFFFu || subs[r].desc_count < s.desc_count) r = q;
-        }
+        // the representative tick_regions gathers (the longest by bytes): its rows serve the
+        // sender's other identity sub-streams, each a suffix of it in bytes and in packets
+        fRowRep = edgpu_host::identity_reps(subs, nq);
         fRowSel.clear();
         for (uint32_t q = 0; q < nq; q++) {
             const edgpu_substream_out& s = subs[q];
@@ -515,6 +529,19 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         if ((err = edgpu_fanout_rows(fCtx, fRowSel.data(), (uint32_t)(fRowSel.size() / 2), (edgpu_packet_row*)fPinRows.p,
                                      nrows, EDGPU_PTR_HOST)))
             return err;
+        // the suffix sharing holds only if every sub-stream's first row is where its bytes start in
+        // the representative's region (a UDP datagram 4 bytes into its slot, after the interleave
+        // header room); a plan that broke it would write wrong bytes silently
+        const edgpu_packet_row* rw = (const edgpu_packet_row*)fPinRows.p;
+        for (uint32_t q = 0; q < nq; q++) {
+            const edgpu_substream_out& s = subs[q];
+            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
+            const edgpu_substream_out& R = subs[fRowRep[s.sender]];
+            if (R.desc_count < s.desc_count || R.out_bytes < s.out_bytes ||
+                rw[fRowOf[q]].offset != R.out_base + (R.out_bytes - s.out_bytes) +
+                                            (s.transport == EDGPU_TRANSPORT_TCP ? 0u : 4u))
+                return fail_with(kRequestFailed, "identity sub-stream is not a suffix of its sender's longest");
+        }
     }
     const edgpu_packet_row* rows = (const edgpu_packet_row*)fPinRows.p;
     // Packets that came with the batch this tick ingested are still in its pinned blob: an identity

@@ -44,6 +44,7 @@
 #pragma once
 #include <stdint.h>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <condition_variable>
 #include <mutex>
@@ -173,6 +174,9 @@ private:
     // one copy pass of a tick to the sink (ReflectPackets)
     int  DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stats& st, OutputSink* sink, bool firstPass,
                      std::vector<edgpu_blocked>* blockedOut);
+    // every copy pass of a launched fan-out (ReflectPackets; on failure the caller drains the rest)
+    int  DeliverTick(edgpu_fanout_result* res, edgpu_tick_stats* st, OutputSink* sink,
+                     std::vector<edgpu_blocked>* blocked, std::chrono::steady_clock::time_point t0);
     int  fail_with(int code, const std::string& msg) { fLastErr = msg; return code; }
     std::string fLastErr;
     // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob

@@ -28,22 +28,32 @@ struct TickRegions {
     const uint8_t* at(const uint8_t* base, uint32_t q) const { return base + reg_off[src[q].first] + src[q].second; }
 };
 
+// Per sender (engine sender ids are dense): the representative of its identity sub-streams -- the
+// longest by bytes -- whose bytes and packet rows serve every other one of them as a suffix.  Both
+// the gather (tick_regions) and the adapter's row sharing pick it here, so they agree; `skip` as
+// below.  Senders without an identity sub-stream map to TickRegions::kNone.
+inline std::vector<uint32_t> identity_reps(const edgpu_substream_out* subs, uint32_t nq, const uint8_t* skip = nullptr) {
+    uint32_t nsend = 0;
+    for (uint32_t q = 0; q < nq; q++)
+        if (subs[q].desc_count && (subs[q].flags & EDGPU_SUB_IDENTITY)) nsend = std::max(nsend, subs[q].sender + 1);
+    std::vector<uint32_t> rep(nsend, 0xFFFFFFFFu);
+    for (uint32_t q = 0; q < nq; q++) {
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || (skip && skip[q])) continue;
+        uint32_t& r = rep[s.sender];
+        if (r == 0xFFFFFFFFu || subs[r].out_bytes < s.out_bytes) r = q;
+    }
+    return rep;
+}
+
 // `skip` (optional, per sub-stream): it needs no region (the host has its bytes elsewhere: an
 // identity sub-stream whose packets all came with the batch the host still holds); its src is kNone.
 inline TickRegions tick_regions(const edgpu_substream_out* subs, uint32_t nq, const uint8_t* skip = nullptr) {
     TickRegions t;
     t.src.assign(nq, {TickRegions::kNone, 0});
-    // per sender (engine sender ids are dense): its longest identity sub-stream, its region
-    uint32_t nsend = 0;
-    for (uint32_t q = 0; q < nq; q++)
-        if (subs[q].desc_count && (subs[q].flags & EDGPU_SUB_IDENTITY)) nsend = std::max(nsend, subs[q].sender + 1);
-    std::vector<uint32_t> rep(nsend, TickRegions::kNone), rep_reg(nsend, TickRegions::kNone);
-    for (uint32_t q = 0; q < nq; q++) {
-        const edgpu_substream_out& s = subs[q];
-        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || (skip && skip[q])) continue;
-        uint32_t& r = rep[s.sender];
-        if (r == TickRegions::kNone || subs[r].out_bytes < s.out_bytes) r = q;
-    }
+    // per sender: its longest identity sub-stream, its region
+    const std::vector<uint32_t> rep = identity_reps(subs, nq, skip);
+    std::vector<uint32_t> rep_reg(rep.size(), TickRegions::kNone);
     t.reg.reserve(nq);
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];

@@ -101,6 +101,10 @@ PREF_DEFAULTS = {
     "enable_player_compatibility": "true",
     "force_rtp_info_sequence_and_time": "false",
     "player_requires_rtp_header_info": "Android,vlc",
+    "enable_broadcast_announce": "true",
+    "enable_broadcast_push": "true",
+    "allow_duplicate_broadcasts": "false",
+    "timeout_broadcaster_session_secs": "30",
 }
 USER_AGENTS = ("EasyPlayer/1.0", "vlc/3.0.8 LibVLC/3.0.8")    # by JOIN ua_flags bit 0
 

@@ -116,7 +116,7 @@ enum : uint32_t {
     qtssRTPStrTransportType = 31,
     // client session object (QTSS.h:473-512)
     qtssCliSesStreamObjects = 0, qtssCliSesState = 7, qtssCliSesFirstUserAgent = 9,
-    qtssCliTeardownReason = 23, qtssCliSesOverBufferEnabled = 33,
+    qtssCliTeardownReason = 23, qtssCliSesTimeoutMsec = 32, qtssCliSesOverBufferEnabled = 33,
     // module object (QTSS.h:894-905), attribute-info object (:911-918), server prefs (:718-800)
     qtssModPrefs = 4, qtssAttrName = 0, qtssAttrID = 1, qtssAttrDataType = 2,
     qtssPrefsMovieFolder = 5, qtssPrefsPlayersReqRTPHeader = 70,

@@ -26,7 +26,7 @@ SAME(qtssPlayRespWriteTrackInfo); SAME(qtssSetupRespDontWriteSSRC);
 SAME(qtssPausedState); SAME(qtssPlayingState); SAME(qtssRTPTransportTypeUDP); SAME(qtssRTPTransportTypeTCP);
 SAME(qtssRTPTransportModePlay); SAME(qtssRTPTransportModeRecord);
 SAME(qtssUnknownPayloadType); SAME(qtssVideoPayloadType); SAME(qtssAudioPayloadType);
-SAME(qtssCliSesCloseClientTeardown); SAME(qtssCliSesTearDownBroadcastEnded); SAME(qtssCliTeardownReason);
+SAME(qtssCliSesCloseClientTeardown); SAME(qtssCliSesTearDownBroadcastEnded); SAME(qtssCliTeardownReason); SAME(qtssCliSesTimeoutMsec);
 SAME(qtssDescribeMethod); SAME(qtssSetupMethod); SAME(qtssTeardownMethod); SAME(qtssPlayMethod);
 SAME(qtssPauseMethod); SAME(qtssOptionsMethod); SAME(qtssAnnounceMethod); SAME(qtssRecordMethod);
 SAME(qtssAttrDataTypeCharArray); SAME(qtssAttrDataTypeSInt32); SAME(qtssAttrDataTypeUInt16); SAME(qtssAttrDataTypeUInt32);

@@ -651,11 +651,89 @@ def prefs_reread() -> Trace:
     return _assemble(tr, [pk0, pk1], 100, dur, joins, tick_times=ticks, blocks=blocks, pubs=pubs, prefs=prefs)
 
 
+def keepalive() -> Trace:
+    """The pushers' client-session timeouts over 70 s (SURVEY §5 broadcaster keep-alive; the
+    server closes a client session whose timeout passes without a refresh, TimeoutTask.cpp,
+    RTPSession.cpp:496-501).  The module sets each pusher's timeout to max(30 s,
+    timeout_broadcaster_session_secs) at its SETUPs (QTSSReflectorModule.cpp:1644, 483-487), and
+    every socket refreshes it on a packet when it last did more than 10 s before
+    (ReflectorSocket::ProcessPacket, ReflectorStream.cpp:1779-1786) -- each socket on its own
+    clock, so the video RTP socket refreshes at the first packet after 10 s and its RTCP socket,
+    with SRs every 5 s, only at 15 s.
+
+    * session 0: a UDP push (video + SRs every 5 s).  Nothing but those refreshes keeps its pusher:
+      its datagrams land on the module's sockets, the server never sees them.  kill_clients is on,
+      so were the pusher to time out (the replay tools' EDGPU_REPLAY_NO_REFRESH) its players 1 and
+      2 would be torn down at 30 s, the session would end and player 3 joining at 35 s would find
+      none;
+    * session 1: an RTSP-interleaved push, which the server refreshes on every '$' frame
+      (RTSPSession.cpp:2157) besides the module's refreshes; player 10."""
+    u = [TrackSpec("video", "H264/90000", 96, bitrate=100_000, gop=60, idr_bytes=2_000, rtcp_every_ms=5000)]
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=40_000, fps=10, gop=20, idr_bytes=1_500)]
+    tr = Trace()
+    tr.prefs = {"kill_clients_when_broadcast_stops": "true"}
+    tr.add_session(make_sdp(u), udp_push=True)
+    tr.add_session(make_sdp(v))
+    dur = 70_000
+    src = _ip(10, 3, 0, 9)
+    pk0 = [(t, ch, d, src, 6100 + (ch & 1)) for t, ch, d in session_packets(u, dur, SEED_BASE + 120)]
+    pk1 = session_packets(v, dur, SEED_BASE + 121)
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (35_000, 0, 3, UDP), (0, 1, 10, UDP)]
+    return _assemble(tr, [pk0, pk1], 250, dur, joins)
+
+
+def prefs_push() -> Trace:
+    """The module prefs that gate the push path, toggled by PREFS events (RereadPrefs,
+    QTSSReflectorModule.cpp:454-541).  A scenario for the QTSS module only (tools/qtss_replay):
+    its fixture comes from the REFERENCE module itself (oracle/_ref/libQTSSReflectorModule_ref.so)
+    in the same fake server, since the harness and the engine-level replays have no ANNOUNCE or
+    second pusher to model.
+
+    * timeout_broadcaster_session_secs 45 at start (every push SETUP sets 45 s, :1644), 20 from
+      5 s (clamped to 30, :486-487);
+    * enable_broadcast_push off from 1 s to 2 s: session 0's RTSP-interleaved packets are dropped
+      at RTSPIncomingData (:606) -- no refresh either; session 1's UDP datagrams are not;
+    * enable_broadcast_announce off from 3 s to 4 s: session 0's pusher leaves at 3.1 s (its
+      players keep the session), a new one is refused at ANNOUNCE at 3.2 s (:900), so nothing is
+      pushed until the next one at 4.1 s;
+    * allow_duplicate_broadcasts on from 5 s: a second pusher sets up session 0's live tracks at
+      5.1 s and carries its packets (:1682), a second UDP pusher joins session 1 at 5.2 s; the
+      second of session 0 leaves at 6 s, which clears every track's fSetupToReceive (:2089-2096),
+      so with duplicates off again (6.1 s) a third pusher still sets up at 6.2 s; session 1's
+      newest pusher leaves at 7 s, its first one keeps pushing."""
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=30, idr_bytes=4_000, rtcp_every_ms=700),
+         TrackSpec("audio", "PCMA/8000", 8)]
+    u = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=30, idr_bytes=3_000, rtcp_every_ms=900)]
+    tr = Trace()
+    t45 = {"timeout_broadcaster_session_secs": "45"}
+    tr.prefs = dict(t45)
+    tr.add_session(make_sdp(v))
+    tr.add_session(make_sdp(u), udp_push=True)
+    dur = 9_000
+    pk0 = session_packets(v, dur, SEED_BASE + 130)
+    src = _ip(10, 4, 0, 2)
+    pk1 = [(t, ch, d, src, 6200 + (ch & 1)) for t, ch, d in session_packets(u, dur, SEED_BASE + 131)]
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (1500, 0, 3, UDP), (3500, 0, 4, TCP), (5500, 0, 5, UDP),
+             (0, 1, 10, UDP), (2500, 1, 11, TCP), (7500, 1, 12, UDP)]
+    pubs = [(3100, "unpublish", 0, 0), (3200, "publish", 0), (4100, "publish", 0), (5100, "publish", 0),
+            (5200, "publish", 1), (6000, "unpublish", 0, 0), (6200, "publish", 0), (7000, "unpublish", 1, 0)]
+    prefs = [(1000, dict(t45, enable_broadcast_push="false")), (2000, dict(t45)),
+             (3000, dict(t45, enable_broadcast_announce="false")), (4000, dict(t45)),
+             (5000, {"allow_duplicate_broadcasts": "true", "timeout_broadcaster_session_secs": "20"}),
+             (6100, {"timeout_broadcaster_session_secs": "20"})]
+    return _assemble(tr, [pk0, pk1], 100, dur, joins, pubs=pubs, prefs=prefs)
+
+
+# Scenarios for the QTSS module alone: fixtures from the reference module in tools/qtss_replay
+MODULE_SCENARIOS = {"prefs_push": prefs_push}
+
+
 SCENARIOS = {
     "tiny": tiny, "c1": c1, "mixed": mixed, "clamp": clamp, "ssrc": ssrc, "nal": nal,
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
     "backpressure": backpressure, "udppush": udppush, "leave": leave, "repush": repush,
     "threaded": threaded, "prefs_buffer": prefs_buffer, "prefs_reread": prefs_reread,
+    "keepalive": keepalive,
 }
 
 

@@ -8,7 +8,7 @@ import pytest
 
 from easydarwin_amd.replay import replay
 from easydarwin_amd.trace import BLOCK, Trace, capture_summary, read_capture
-from scenarios import SCENARIOS
+from scenarios import MODULE_SCENARIOS, SCENARIOS
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -23,7 +23,7 @@ def _trace(name):
     if os.path.exists(p):
         with open(p, "rb") as f:
             return Trace.from_bytes(f.read())
-    tr = SCENARIOS[name]()
+    tr = SCENARIOS[name]() if name in SCENARIOS else MODULE_SCENARIOS[name]()
     assert hashlib.sha256(tr.to_bytes()).hexdigest() == _fixture(name)["trace_sha256"], \
         "trace generator drifted from the golden fixture"
     return tr

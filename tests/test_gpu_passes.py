@@ -261,3 +261,23 @@ def test_c4_burst_through_the_module_at_the_default_arena(oracle_bins, tmp_path)
     for ss in joiners:
         first = ss.data[4:] if ss.tcp else ss.data[2:]
         assert first[12] & 0x1F == 7 or (first[12] & 0x1F == 28 and first[13] & 0x1F == 5), "not a key-frame start"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["leave", "repush"])
+def test_failed_pass_leaves_the_context_usable(name, tmp_path):
+    """A sink error in the second copy pass of an over-capacity tick fails that tick only: the
+    adapter drains the passes it still owed (edgpu_fanout_next, counted as lost) and reports the
+    blocked sub-streams it had, so every later tick, output removal and session removal of the
+    trace succeeds (a failed pass used to leave the context refusing all of them)."""
+    info = []
+    replay(_trace(name), tick_info=info)
+    arena, desc = _small(info)
+    t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
+    t.write_bytes(_trace(name).to_bytes())
+    r = subprocess.run([ADAPTER, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, EDGPU_ARENA_BYTES=str(arena), EDGPU_MAX_OUT_PACKETS=str(desc),
+                                EDGPU_REPLAY_FAIL_PASS="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    failed, after = map(int, re.search(r"(\d+) failed ticks, (\d+) good ticks after", r.stderr).groups())
+    assert failed == 1 and after > 0, r.stderr[-2000:]

@@ -35,18 +35,22 @@ MODULE = os.path.join(ROOT, "easydarwin_amd", "libQTSSReflectorModule.so")
 REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
 TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "anchor", "rtpinfo", "backpressure"]
 UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones beside them)
-PREFS = ["prefs_buffer", "prefs_reread"]      # the server's prefs objects, RereadPrefs
+PREFS = ["prefs_buffer", "prefs_reread", "prefs_push"]   # the server's prefs objects, RereadPrefs
+KEEPALIVE = ["keepalive"]                     # 70 s: the pushers' timeouts and the module's refreshes
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["whole", "parts"])
-@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS)
+@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE)
 def test_module_matches_reference(name, gather, tmp_path):
     """`parts`: every tick's readback gathered in parts, overlapped with the write threads
-    (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split)."""
-    t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
+    (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split).  The
+    keep-alive log -- the timeout set at every push SETUP, every QTSS_RefreshTimeOut, the server's
+    timeouts -- is the reference's too (QTSSReflectorModule.cpp:1644, ReflectorStream.cpp:
+    1779-1786).  `prefs_push`'s fixture is the reference module's own output."""
+    t, c, tt, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log"
     t.write_bytes(_trace(name).to_bytes())
-    env = dict(os.environ, EDGPU_TT_OUT=str(tt))
+    env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka))
     if gather == "parts":
         env["EDGPU_GATHER_SPLIT_BYTES"] = "0"
     r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
@@ -58,29 +62,52 @@ def test_module_matches_reference(name, gather, tmp_path):
         assert len(read_source_reports(c.read_bytes())) == len(fx["source_reports"])
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]
+    assert hashlib.sha256(ka.read_bytes()).hexdigest() == _fixture(name)["keepalive_log_sha256"]
+
+
+@pytest.mark.gpu
+def test_module_udp_pusher_times_out_without_refresh(tmp_path):
+    """The same 70-s trace with the server ignoring QTSS_RefreshTimeOut: the UDP pusher times out
+    at 30 s and kill_clients tears its players down -- exactly as the reference does (the
+    fixture's no-refresh capture and log); with the refreshes it is fed for 70 s."""
+    t, c, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "ka.log"
+    t.write_bytes(_trace("keepalive").to_bytes())
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, EDGPU_REPLAY_NO_REFRESH="1", EDGPU_KEEPALIVE_LOG=str(ka)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    fx = _fixture("keepalive")["no_refresh"]
+    assert ka.read_text().splitlines() == fx["keepalive_log"]
+    assert hashlib.sha256(c.read_bytes()).hexdigest() == fx["capture_sha256"]
 
 
 REF_MODULE = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["repush", "rtpinfo", "leave", "threaded", "udppush", "prefs_reread", "backpressure"])
-def test_module_equals_reference_module(name, tmp_path):
+@pytest.mark.parametrize("name", ["repush", "rtpinfo", "leave", "threaded", "udppush", "prefs_reread", "backpressure",
+                                  "keepalive", "prefs_push"])
+@pytest.mark.parametrize("refresh", ["on", "off"])
+def test_module_equals_reference_module(name, refresh, tmp_path):
     """The drop-in and the REFERENCE QTSSReflectorModule (compiled from its own sources,
     oracle/_ref/Makefile; tests/test_ref_module.py) driven by the same fake server through the same
     roles: equal QTSS_Write streams and transmit times (QTSSReflectorModule.cpp:604-678,
     1379-1545, 1597-2023, 2070-2196)."""
     if not os.path.exists(REF_MODULE):
         pytest.skip("oracle/_ref/libQTSSReflectorModule_ref.so not built")
+    if refresh == "off" and name not in ("keepalive", "prefs_push", "udppush"):
+        pytest.skip("no pusher outlives its timeout in this trace either way")
     t = tmp_path / "t.edtr"
     t.write_bytes(_trace(name).to_bytes())
     out = {}
     for tag, so in (("gpu", MODULE), ("ref", REF_MODULE)):
-        c, tt = tmp_path / f"{tag}.edcp", tmp_path / f"{tag}.edtt"
-        r = subprocess.run([REPLAY, so, str(t), str(c)], capture_output=True, text=True, timeout=120,
-                           env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+        c, tt, ka = tmp_path / f"{tag}.edcp", tmp_path / f"{tag}.edtt", tmp_path / f"{tag}.ka"
+        env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka))
+        if refresh == "off":
+            env["EDGPU_REPLAY_NO_REFRESH"] = "1"
+        r = subprocess.run([REPLAY, so, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
         assert r.returncode == 0, (tag, r.stderr[-2000:])
-        out[tag] = (c.read_bytes(), tt.read_bytes())
+        out[tag] = (c.read_bytes(), tt.read_bytes(), ka.read_text())
+    assert out["gpu"][2] == out["ref"][2], "keep-alive logs differ"
     assert out["gpu"][0] == out["ref"][0]
     assert out["gpu"][1] == out["ref"][1]
 

@@ -22,7 +22,7 @@ import subprocess
 
 import pytest
 
-from scenarios import SCENARIOS
+from scenarios import MODULE_SCENARIOS, SCENARIOS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -43,17 +43,42 @@ def refmod(oracle_bins):
     return oracle_bins["refmod"]
 
 
-@pytest.mark.parametrize("name", sorted(SCENARIOS))
+@pytest.mark.parametrize("name", sorted(SCENARIOS) + sorted(MODULE_SCENARIOS))
 def test_reference_module_reproduces_fixture(name, refmod, tmp_path):
-    t, c, tt = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt"
-    t.write_bytes(SCENARIOS[name]().to_bytes())
+    """Captures, transmit times and the keep-alive log (the pushers' timeouts the module set,
+    its QTSS_RefreshTimeOut calls, the server's timeouts: ReflectorStream.cpp:1779-1786,
+    QTSSReflectorModule.cpp:1644) as the harness restated them -- or, for the module-only
+    scenarios, as this same module produced them when the fixture was made."""
+    t, c, tt, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log"
+    fn = SCENARIOS.get(name) or MODULE_SCENARIOS[name]
+    t.write_bytes(fn().to_bytes())
     from conftest import udp_port_lock
     with udp_port_lock():                # UDP pushers bind fixed loopback source ports
         r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
-                           env=dict(os.environ, EDGPU_TT_OUT=str(tt)))
+                           env=dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka)))
     assert r.returncode == 0, r.stderr[-3000:]
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fix(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fix(name)["transmit_sha256"]
+    assert hashlib.sha256(ka.read_bytes()).hexdigest() == _fix(name)["keepalive_log_sha256"]
+
+
+def test_reference_module_udp_pusher_times_out_without_refresh(refmod, tmp_path):
+    """The keepalive trace with the server ignoring the module's QTSS_RefreshTimeOut calls
+    (EDGPU_REPLAY_NO_REFRESH): the UDP pusher's session times out at 30 s, its players are torn
+    down (kill_clients) and the session ends -- the outcome the refreshes prevent."""
+    t, c, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "ka.log"
+    t.write_bytes(SCENARIOS["keepalive"]().to_bytes())
+    from conftest import udp_port_lock
+    with udp_port_lock():
+        r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, EDGPU_REPLAY_NO_REFRESH="1", EDGPU_KEEPALIVE_LOG=str(ka)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    fx = _fix("keepalive")
+    assert hashlib.sha256(c.read_bytes()).hexdigest() == fx["no_refresh"]["capture_sha256"]
+    assert ka.read_text().splitlines() == fx["no_refresh"]["keepalive_log"]
+    assert "X 30000 push 0.0" in fx["no_refresh"]["keepalive_log"]
+    fed, starved = fx["substreams"]["1/0/0"][0], fx["no_refresh"]["substreams"]["1/0/0"][0]
+    assert starved < fed / 2
 
 
 def test_reference_module_registers_its_roles(refmod):

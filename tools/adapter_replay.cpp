@@ -40,8 +40,13 @@ public:
     }
     std::map<std::pair<uint32_t, uint16_t>, Rec>* recs;      // (handle, track)
     std::map<std::tuple<uint32_t, uint16_t, int>, int64_t> budget;   // BLOCK: writes left this tick
+    // EDGPU_REPLAY_FAIL_PASS=1: the first write of a tick's second copy pass fails once (a sink
+    // error), to check that the failed tick leaves the context usable (no owed pass)
+    const Reflector* R = nullptr;
+    bool failPass = false, failed = false;
     int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved, const uint8_t* wire,
                     uint32_t wireLen, uint32_t) override {
+        if (failPass && !failed && R && R->LastTick().passes >= 2) { failed = true; return kRequestFailed; }
         auto b = budget.find(std::make_tuple(subscriber, track, isRTCP ? 1 : 0));
         if (b != budget.end()) {
             if (b->second == 0) return kWouldBlock;
@@ -120,6 +125,9 @@ int main(int argc, char** argv) {
     std::map<uint32_t, bool> live;                                      // handle -> still an output
     CaptureSink sink;
     sink.recs = &recs;
+    sink.R = &R;
+    sink.failPass = getenv("EDGPU_REPLAY_FAIL_PASS") && atoi(getenv("EDGPU_REPLAY_FAIL_PASS")) != 0;
+    uint64_t failedTicks = 0, ticksAfterFailure = 0;
     int64_t now = 0;
     // a session without pusher or outputs ends (RemoveOutput's refcount-0 branch)
     auto release_check = [&](uint32_t s) -> bool {
@@ -189,7 +197,15 @@ int main(int argc, char** argv) {
             const size_t before = sink.reports.size();
             int err = R.ReflectPackets(t, &sink);
             for (size_t i = before; i < sink.reports.size(); i++) sink.reports[i].session = trace_of[sink.reports[i].session];
-            if (err) { fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error()); return 3; }
+            if (err && sink.failed && failedTicks == 0) {
+                fprintf(stderr, "adapter_replay: injected sink failure at tick %llu (%d)\n", (unsigned long long)ticks, err);
+                failedTicks++;
+            } else if (err) {
+                fprintf(stderr, "ReflectPackets: %d %s\n", err, edgpu_last_error());
+                return 3;
+            } else if (failedTicks) {
+                ticksAfterFailure++;
+            }
             ticks++;
             passes += R.LastTick().passes;
             sink.budget.clear();
@@ -245,5 +261,8 @@ int main(int argc, char** argv) {
     }
     fclose(o);
     fprintf(stderr, "adapter_replay: %llu ticks, %llu copy passes\n", (unsigned long long)ticks, (unsigned long long)passes);
+    if (sink.failPass)
+        fprintf(stderr, "adapter_replay: %llu failed ticks, %llu good ticks after the failure\n",
+                (unsigned long long)failedTicks, (unsigned long long)ticksAfterFailure);
     return 0;
 }

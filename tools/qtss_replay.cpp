@@ -79,6 +79,7 @@
 #include <atomic>
 #include <chrono>
 #include <cerrno>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -113,6 +114,12 @@ struct Obj {
     size_t body_off = 0;
     // client sessions
     bool played = false, idle_timer = false, torn_down = false;
+    // the client session's timeout (RTPSessionInterface's fTimeoutTask, TimeoutTask.h:97): the server
+    // pref rtp_session_timeout (120 s, QTSServerPrefs.cpp:91) until a module sets qtssCliSesTimeoutMsec
+    bool is_client = false, closed = false;
+    int64_t to_ms = 120000, deadline = 0;
+    int push_s = -1, push_k = -1, player_sub = -1;        // who it is, for the keep-alive log
+    Obj* owner = nullptr;                                 // RTP stream objects: their client session
     // dictionaries with named (instance) attributes: the prefs objects
     std::map<std::string, std::pair<uint32_t, uint32_t>> named;   // name -> (id, data type)
 };
@@ -130,6 +137,36 @@ static std::atomic<int64_t> g_now{0};
 static void advance_clock(int64_t t) {
     int64_t c = g_now.load();
     while (t > c && !g_now.compare_exchange_weak(c, t)) {}
+}
+
+// ---- client-session timeouts and the keep-alive log ---------------------------------------------
+// The server's timeouts for the pushers' client sessions, as RTPSessionInterface keeps them: a
+// deadline now + timeout, moved on by every RTSP request of the session (RTSPSession.cpp:1669),
+// every '$' frame an RTSP-interleaved pusher sends (RTSPSession.cpp:2157), QTSS_RefreshTimeOut
+// (QTSSCallbacks.cpp:645) and a module's qtssCliSesTimeoutMsec (SetTimeout, RTPSessionInterface.cpp:
+// 202-206); when the clock reaches it, the session is closed (TimeoutTaskThread::Run -> kTimeoutEvent,
+// RTPSession.cpp:496-501): ClientSessionClosing, as for a pusher that hung up.  Players are kept alive
+// by their receiver reports (RTPStream.cpp:1486) and by TCP writes (:805) and never time out here.
+// EDGPU_KEEPALIVE_LOG=<path>: every module SetTimeout ("S"), QTSS_RefreshTimeOut ("R") and timeout
+// ("X"), with the virtual time and "push <session>.<pusher ordinal>"; EDGPU_REPLAY_NO_REFRESH=1: the
+// refreshes are logged but ignored (the pusher then times out).
+static FILE* g_ka_log = nullptr;
+static bool g_no_refresh = false;
+static bool g_enforce_timeouts = false;               // trace mode (not --threaded, not --bench)
+static std::string who(const Obj* c) {
+    if (c && c->push_s >= 0) return "push " + std::to_string(c->push_s) + "." + std::to_string(c->push_k);
+    if (c && c->player_sub >= 0) return "player " + std::to_string(c->player_sub);
+    return "client ?";
+}
+static void ka_log(char kind, int64_t t, const Obj* c, const char* extra = "") {
+    if (g_ka_log) fprintf(g_ka_log, "%c %lld %s%s\n", kind, (long long)t, who(c).c_str(), extra);
+}
+static void refresh(Obj* c) { if (c && c->is_client && !c->closed) c->deadline = g_now.load() + c->to_ms; }
+static Obj* new_client() {
+    Obj* c = new_obj(qtssClientSessionObjectType);
+    c->is_client = true;
+    c->deadline = g_now.load() + c->to_ms;
+    return c;
 }
 
 // the reference harness's deterministic rand() (trace.py rr_ssrc), for the module's own calls;
@@ -255,6 +292,20 @@ static void load_prefs(const trace_prefs::Prefs& p) {
 static QTSS_Error cb_set_value(Obj* o, uint32_t id, uint32_t idx, const void* buf, uint32_t len, ...) {
     if (!o) return QTSS_BadArgument;
     set_attr(o, id, idx, buf, len);
+    if (o->is_client && id == qtssCliSesTimeoutMsec && len == 4) {        // SetTimeout
+        uint32_t v;
+        memcpy(&v, buf, 4);
+        o->to_ms = v;
+        o->deadline = v ? g_now.load() + v : 0;
+        ka_log('S', g_now.load(), o, (" " + std::to_string(v)).c_str());
+    }
+    return QTSS_NoErr;
+}
+// QTSS_RefreshTimeOut(client session)
+static QTSS_Error cb_refresh_timeout(Obj* c, ...) {
+    if (!c || !c->is_client) return QTSS_BadArgument;
+    ka_log('R', g_now.load(), c);
+    if (!g_no_refresh) refresh(c);
     return QTSS_NoErr;
 }
 // QTSS_Write: on an RTP stream object, RTPStream::Write's framing; on a request (DESCRIBE), ignored
@@ -317,6 +368,7 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
     __atomic_add_fetch(&o->npk[k], 1, __ATOMIC_RELEASE);
     o->tt[k].push_back(ps->packetTransmitTime);
     __atomic_add_fetch(&g_writes, 1, __ATOMIC_RELEASE);
+    if (g_enforce_timeouts) refresh(o->owner);
     if (outLen) *outLen = len;
     return QTSS_NoErr;
 }
@@ -333,6 +385,7 @@ static std::map<Obj*, Obj*> g_rtsp_of_client;
 static std::map<Obj*, uint32_t> g_next_channel;
 static QTSS_Error cb_add_rtp_stream(Obj* client, Obj* req, Obj** out, uint32_t, ...) {
     Obj* s = new_obj(qtssRTPStreamObjectType);
+    s->owner = client;
     uint32_t tt = qtssRTPTransportTypeUDP;
     auto it = req->attrs.find(qtssRTSPReqTransportType);
     if (it != req->attrs.end() && !it->second.empty()) memcpy(&tt, it->second[0].data(), 4);
@@ -455,6 +508,7 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     p.rtspRequestParams.inRTSPSession = rtsp;
     p.rtspRequestParams.inRTSPRequest = req;
     p.rtspRequestParams.inClientSession = client;
+    refresh(client);                                   // RTSPSession.cpp:1669
     g_current_client = client;
     const QTSS_Error e = g_dispatch(QTSS_RTSPPreProcessor_Role, &p);
     g_current_client = nullptr;
@@ -490,7 +544,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
     for (uint32_t s = 0; s < nsess; s++) {
         const std::string path = "/bench" + std::to_string(s) + ".sdp";      // one component: the stream name
         rtsp[s] = new_obj(qtssRTSPSessionObjectType);
-        client[s] = new_obj(qtssClientSessionObjectType);
+        client[s] = new_client();
         g_rtsp_of_client[client[s]] = rtsp[s];
         if (request(rtsp[s], client[s], qtssAnnounceMethod, path, "", 0, qtssRTPTransportTypeTCP, sdp) ||
             request(rtsp[s], client[s], qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModeRecord,
@@ -499,7 +553,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             { fprintf(stderr, "bench: push setup failed\n"); return 3; }
         for (uint32_t k = 0; k < nsub; k++) {
             Obj* pr = new_obj(qtssRTSPSessionObjectType);
-            Obj* pc = new_obj(qtssClientSessionObjectType);
+            Obj* pc = new_client();
             g_rtsp_of_client[pc] = pr;
             if (request(pr, pc, qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModePlay, qtssRTPTransportTypeUDP) ||
                 request(pr, pc, qtssPlayMethod, path, "", qtssRTPTransportModePlay, qtssRTPTransportTypeUDP))
@@ -729,7 +783,7 @@ int main(int argc, char** argv) {
     cbs.addr[kGetNumValuesCallback] = (QTSS_CallbackProcPtr)cb_num_values;
     cbs.addr[kGetValueAsStringCallback] = (QTSS_CallbackProcPtr)cb_value_as_string;
     cbs.addr[kValueToStringCallback] = (QTSS_CallbackProcPtr)cb_value_to_string;
-    cbs.addr[kRefreshTimeOutCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kRefreshTimeOutCallback] = (QTSS_CallbackProcPtr)cb_refresh_timeout;
     cbs.addr[kLockObjectCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kUnlockObjectCallback] = (QTSS_CallbackProcPtr)cb_ok;
     QTSS_PrivateArgs args;
@@ -797,26 +851,43 @@ int main(int argc, char** argv) {
         return rc;
     }
 
+    g_enforce_timeouts = !threaded;
+    g_no_refresh = getenv("EDGPU_REPLAY_NO_REFRESH") && atoi(getenv("EDGPU_REPLAY_NO_REFRESH")) != 0;
+    if (const char* lp = getenv("EDGPU_KEEPALIVE_LOG")) {
+        g_ka_log = fopen(lp, "w");
+        if (!g_ka_log) { perror(lp); return 2; }
+    }
     r.p = 4;
     const uint32_t ver = r.get<uint32_t>();
     const uint32_t nsess = r.get<uint32_t>();
     std::vector<std::string> paths(nsess), sdps(nsess);
     std::vector<uint32_t> ntracks(nsess, 0);
     std::vector<uint8_t> flags(nsess, 0);
-    std::vector<Obj*> push_rtsp(nsess, nullptr), push_client(nsess, nullptr);
+    // the pusher connections of each session, oldest first: the newest carries the session's
+    // packets (more than one only while allow_duplicate_broadcasts lets a second pusher set up a
+    // live session's tracks, QTSSReflectorModule.cpp:1682); an UNPUBLISH closes the newest
+    struct PushConn { Obj* rtsp; Obj* client; };
+    std::vector<std::vector<PushConn>> pushers(nsess);
+    std::vector<uint32_t> pub_count(nsess, 0);                 // pusher ordinals (the keep-alive log)
     std::vector<std::vector<uint16_t>> server_port(nsess);     // UDP push: the module's RTP port per track
     // the reference's reference counting, kept here to check the module's: does the session
-    // exist, and how many players hold it (the pusher's reference is push_rtsp[s] != nullptr)
+    // exist, and how many players hold it (each pusher connection holds one more)
     std::vector<bool> alive(nsess, false);
     std::vector<uint32_t> holders(nsess, 0);
+    // the tracks' fSetupToReceive: set by a pusher's SETUPs, cleared when any pusher of the session
+    // leaves (DestroySession, QTSSReflectorModule.cpp:2089-2096)
+    std::vector<bool> receiving(nsess, false);
+    trace_prefs::Prefs cur = prefs;                            // the prefs of now (PREFS events)
     // a pusher connection: ANNOUNCE, a record-mode SETUP per track, RECORD (false: refused)
     auto publish = [&](uint32_t s) -> bool {
         const uint32_t tt = (flags[s] & 1) ? qtssRTPTransportTypeUDP : qtssRTPTransportTypeTCP;
         Obj* rtsp = new_obj(qtssRTSPSessionObjectType);
-        Obj* client = new_obj(qtssClientSessionObjectType);
+        Obj* client = new_client();
+        client->push_s = (int)s;
+        client->push_k = (int)pub_count[s]++;
         g_rtsp_of_client[client] = rtsp;
-        if (request(rtsp, client, qtssAnnounceMethod, paths[s], "", 0, tt, sdps[s]))
-            { fprintf(stderr, "ANNOUNCE failed\n"); exit(3); }
+        // refused with enable_broadcast_announce off (QRM:900): the pusher gives up, no SETUP
+        if (request(rtsp, client, qtssAnnounceMethod, paths[s], "", 0, tt, sdps[s])) { client->closed = true; return false; }
         std::vector<uint16_t> ports;
         for (uint32_t t = 0; t < ntracks[s]; t++) {
             Obj* req = nullptr;
@@ -826,6 +897,7 @@ int main(int argc, char** argv) {
                 memset(&p, 0, sizeof(p));
                 p.clientSessionClosingParams.inClientSession = client;
                 (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
+                client->closed = true;
                 return false;
             }
             if (flags[s] & 1) {
@@ -839,10 +911,10 @@ int main(int argc, char** argv) {
         }
         if (request(rtsp, client, qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, tt))
             { fprintf(stderr, "RECORD failed\n"); exit(3); }
-        push_rtsp[s] = rtsp;
-        push_client[s] = client;
+        pushers[s].push_back(PushConn{rtsp, client});
         server_port[s] = ports;
         alive[s] = true;
+        receiving[s] = true;
         return true;
     };
     for (uint32_t s = 0; s < nsess; s++) {
@@ -861,8 +933,50 @@ int main(int argc, char** argv) {
         p.clientSessionClosingParams.inClientSession = client;
         (void)g_dispatch(QTSS_ClientSessionClosing_Role, &p);
     };
-    auto release_check = [&](uint32_t s) { if (!push_rtsp[s] && holders[s] == 0) alive[s] = false; };
+    auto release_check = [&](uint32_t s) { if (pushers[s].empty() && holders[s] == 0) alive[s] = false; };
     std::vector<Player> players;
+    // pusher connection `i` of session s closes (an UNPUBLISH with its kill flag, or a timeout):
+    // ClientSessionClosing, then, as the server does after QTSS_Teardown, ClientSessionClosing for
+    // every player the module tore down
+    auto close_pusher = [&](uint32_t s, size_t i, bool kill) -> bool {
+        Obj* client = pushers[s][i].client;
+        auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleTearDownClients");
+        if (it == g_attr_ids.end()) { fprintf(stderr, "kill-clients attribute not registered\n"); return false; }
+        // the event's kill flag is the attribute set at RECORD (the module sets it from its pref)
+        if (kill) { const bool k = true; set_attr(client, it->second, 0, &k, sizeof(k)); }   // a bool, as the module writes it
+        close_client(client);
+        client->closed = true;
+        pushers[s].erase(pushers[s].begin() + (long)i);
+        receiving[s] = false;
+        uint32_t torn = 0;
+        for (auto& pl : players)
+            if (!pl.left && pl.client->torn_down) {
+                close_client(pl.client);
+                pl.left = true;
+                holders[pl.session]--;
+                torn++;
+            }
+        if (kill && torn == 0 && holders[s] != 0) { fprintf(stderr, "kill_clients tore nothing down\n"); return false; }
+        release_check(s);
+        return true;
+    };
+    // every pusher whose deadline the clock reached by `t` times out, earliest first, at its deadline
+    auto fire_timeouts = [&](int64_t t) -> bool {
+        for (;;) {
+            int64_t best = INT64_MAX;
+            uint32_t bs = 0;
+            size_t bi = 0;
+            for (uint32_t s = 0; s < nsess; s++)
+                for (size_t i = 0; i < pushers[s].size(); i++) {
+                    const Obj* c = pushers[s][i].client;
+                    if (c->deadline > 0 && c->deadline <= t && c->deadline < best) { best = c->deadline; bs = s; bi = i; }
+                }
+            if (best == INT64_MAX) return true;
+            advance_clock(best);
+            ka_log('X', best, pushers[bs][bi].client);
+            if (!close_pusher(bs, bi, false)) return false;
+        }
+    };
     std::vector<char> frame(70000);
     while (r.p < r.d.size()) {
         const size_t at = r.p;
@@ -871,6 +985,7 @@ int main(int argc, char** argv) {
         const int64_t t = r.get<int64_t>();
         if (threaded && (type == 1 || type == 5)) { r.p = at; break; }     // the pusher threads' part
         if (threaded && type == 3) continue;                               // the module ticks itself
+        if (g_enforce_timeouts && !fire_timeouts(t)) return 3;
         advance_clock(t);
         if (type == 1) {                                         // PKT -> RTSPIncomingData
             const uint32_t s = r.get<uint32_t>();
@@ -879,18 +994,21 @@ int main(int argc, char** argv) {
             frame[0] = '$'; frame[1] = (char)ch; frame[2] = (char)(len >> 8); frame[3] = (char)len;
             memcpy(&frame[4], &r.d[r.p], len);
             r.p += len;
-            if (!push_rtsp[s]) continue;
+            if (pushers[s].empty()) continue;
+            const PushConn& pc = pushers[s].back();
+            refresh(pc.client);                                  // RTSPSession.cpp:2157
             QTSS_RoleParams p;
             memset(&p, 0, sizeof(p));
-            p.rtspIncomingDataParams.inRTSPSession = push_rtsp[s];
-            p.rtspIncomingDataParams.inClientSession = push_client[s];
+            p.rtspIncomingDataParams.inRTSPSession = pc.rtsp;
+            p.rtspIncomingDataParams.inClientSession = pc.client;
             p.rtspIncomingDataParams.inPacketData = frame.data();
             p.rtspIncomingDataParams.inPacketLen = len + 4;
             (void)g_dispatch(QTSS_RTSPIncomingData_Role, &p);
         } else if (type == 2) {                                  // JOIN -> SETUP x tracks + PLAY
             const uint32_t s = r.get<uint32_t>(), sub = r.get<uint32_t>();
             const uint8_t tr = r.get<uint8_t>(), ua = r.get<uint8_t>();
-            Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_obj(qtssClientSessionObjectType), {}};
+            Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_client(), {}};
+            pl.client->player_sub = (int)sub;
             g_rtsp_of_client[pl.client] = pl.rtsp;
             const std::string agent = (ua & 1) ? "vlc/3.0.8 LibVLC/3.0.8" : "EasyPlayer/1.0";   // case-sensitive match
             set_attr(pl.client, qtssCliSesFirstUserAgent, 0, agent.data(), (uint32_t)agent.size());
@@ -940,7 +1058,7 @@ int main(int argc, char** argv) {
             const uint32_t len = r.get<uint32_t>();
             const uint8_t* data = &r.d[r.p];
             r.p += len;
-            if (!push_rtsp[s] || len == 0 || ch / 2 >= server_port[s].size()) continue;
+            if (pushers[s].empty() || len == 0 || ch / 2 >= server_port[s].size()) continue;
             const int fd = source_socket(addr, port);
             (void)source_socket(addr, (uint16_t)(port | 1));        // where the receiver reports may go
             sockaddr_in to;
@@ -966,41 +1084,25 @@ int main(int argc, char** argv) {
         } else if (type == 7) {                                  // UNPUBLISH -> the pusher's session closes
             const uint32_t s = r.get<uint32_t>();
             const uint8_t kill = r.get<uint8_t>();
-            if (!push_rtsp[s]) continue;
-            auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleTearDownClients");
-            if (it == g_attr_ids.end()) { fprintf(stderr, "kill-clients attribute not registered\n"); return 3; }
-            // the event's kill flag is the attribute set at RECORD (the module sets it from its pref)
-            if (kill) { const bool k = true; set_attr(push_client[s], it->second, 0, &k, sizeof(k)); }   // a bool, as the module writes it
-            close_client(push_client[s]);
-            push_rtsp[s] = push_client[s] = nullptr;
-            // the server closes the client sessions the module tore down (QTSS_Teardown)
-            uint32_t torn = 0;
-            for (auto& pl : players)
-                if (!pl.left && pl.client->torn_down) {
-                    close_client(pl.client);
-                    pl.left = true;
-                    holders[pl.session]--;
-                    torn++;
-                }
-            if (kill && torn == 0 && holders[s] != 0) { fprintf(stderr, "kill_clients tore nothing down\n"); return 3; }
-            release_check(s);
+            if (pushers[s].empty()) continue;
+            if (!close_pusher(s, pushers[s].size() - 1, kill != 0)) return 3;
         } else if (type == 9) {                                  // PREFS -> QTSS_RereadPrefs_Role
             const uint32_t n = r.get<uint32_t>();
-            load_prefs(trace_prefs::Prefs::parse(&r.d[r.p], n));
+            cur = trace_prefs::Prefs::parse(&r.d[r.p], n);
+            load_prefs(cur);
             r.p += n;
             QTSS_RoleParams p;
             memset(&p, 0, sizeof(p));
             if (g_dispatch(QTSS_RereadPrefs_Role, &p) != QTSS_NoErr) { fprintf(stderr, "RereadPrefs failed\n"); return 3; }
         } else if (type == 8) {                                  // PUBLISH -> a new pusher connection
             const uint32_t s = r.get<uint32_t>();
-            if (push_rtsp[s]) {                                  // a duplicate broadcast must be refused
-                const std::vector<uint16_t> keep = server_port[s];
-                Obj* kr = push_rtsp[s]; Obj* kc = push_client[s];
-                if (publish(s)) { fprintf(stderr, "duplicate PUBLISH accepted\n"); return 3; }
-                push_rtsp[s] = kr; push_client[s] = kc; server_port[s] = keep;
-                continue;
-            }
-            if (!publish(s)) { fprintf(stderr, "PUBLISH refused\n"); return 3; }
+            // refused when ANNOUNCE is disabled, and on tracks another pusher set up unless
+            // allow_duplicate_broadcasts (QRM:900, 1682); the module must agree
+            const bool want = cur.flag("enable_broadcast_announce") && (!receiving[s] || cur.flag("allow_duplicate_broadcasts"));
+            const std::vector<uint16_t> keep = server_port[s];
+            const bool got = publish(s);
+            if (!got) server_port[s] = keep;
+            if (got != want) { fprintf(stderr, "PUBLISH of session %u %s\n", s, got ? "accepted" : "refused"); return 3; }
         } else {
             fprintf(stderr, "bad event %u\n", type);
             return 3;
@@ -1073,8 +1175,8 @@ int main(int argc, char** argv) {
                     memcpy(&fr[4], e.data, e.len);
                     QTSS_RoleParams p;
                     memset(&p, 0, sizeof(p));
-                    p.rtspIncomingDataParams.inRTSPSession = push_rtsp[e.s];
-                    p.rtspIncomingDataParams.inClientSession = push_client[e.s];
+                    p.rtspIncomingDataParams.inRTSPSession = pushers[e.s].back().rtsp;
+                    p.rtspIncomingDataParams.inClientSession = pushers[e.s].back().client;
                     p.rtspIncomingDataParams.inPacketData = fr.data();
                     p.rtspIncomingDataParams.inPacketLen = e.len + 4;
                     (void)g_dispatch(QTSS_RTSPIncomingData_Role, &p);
@@ -1122,6 +1224,7 @@ int main(int argc, char** argv) {
     }
     memset(&rp, 0, sizeof(rp));
     (void)g_dispatch(QTSS_Shutdown_Role, &rp);
+    if (g_ka_log) fclose(g_ka_log);
 
     // capture: (sub, track, kind) records, subscriber order
     std::vector<Obj*> st;

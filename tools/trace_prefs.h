@@ -21,6 +21,8 @@ inline const std::vector<std::pair<std::string, std::string>>& defaults() {
         {"timeout_stream_SSRC_secs", "30"}, {"disable_rtp_play_info", "false"},
         {"enable_player_compatibility", "true"}, {"force_rtp_info_sequence_and_time", "false"},
         {"player_requires_rtp_header_info", "Android,vlc"},
+        {"enable_broadcast_announce", "true"}, {"enable_broadcast_push", "true"},
+        {"allow_duplicate_broadcasts", "false"}, {"timeout_broadcaster_session_secs", "30"},
     };
     return d;
 }
