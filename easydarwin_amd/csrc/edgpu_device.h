@@ -288,7 +288,20 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned int pass_slot;         // slot of the last launched pass
     unsigned int stream_errors;     // sessions newly marked with a stream error by this tick
     unsigned long long cum_lost_passes;   // passes a tick still owed when the next tick was planned
+    unsigned int grow_count;        // senders this tick's plan asked to grow (GrowReq list, kMaxGrow)
+    unsigned int _pad_g;
 };
+
+// A sender ring the plan found too small for the span the reference would retain (edgpu_config.
+// ring_growth): the capacities it should have, as powers of two.
+struct GrowReq {                    // 32 B
+    uint32_t sender;
+    uint32_t pk_log2;               // packets
+    uint32_t bytes_log2;            // bytes
+    uint32_t _pad;
+    uint64_t tail, head;            // the sender's intact range when the plan measured it
+};
+constexpr uint32_t kMaxGrow = 1024;     // requests per tick (the rest are made again next tick)
 constexpr uint32_t kNoPass = 0xFFFFFFFFu;
 
 struct TickParams {
@@ -302,6 +315,9 @@ struct TickParams {
     uint32_t chunk;                 // packets per fan-out work item (per kernel variant)
     uint32_t pass_ord;              // k_plan_pass: ordinal of the pass (1, 2, ...) and its id
     uint32_t pass_id;
+    uint32_t grow_on;               // ring growth: on, and its per-sender bounds
+    uint32_t grow_max_pk;
+    uint64_t grow_max_bytes;
 };
 
 }  // namespace edgpu

@@ -29,6 +29,8 @@ hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r,
                                     uint32_t n, hipStream_t st);
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st);
 hipError_t launch_plan(const PlanParams& p, hipStream_t st);
+hipError_t launch_ring_move(int kind, const void* src, uint64_t smask, void* dst, uint64_t dmask, uint64_t lo, uint64_t n,
+                            hipStream_t st);
 hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st);
 hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStream_t st);
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st);
@@ -302,6 +304,13 @@ struct edgpu_ctx {
     DevVec<ImgPlan> d_img_plan;
     int* d_img_status = nullptr;
     TickTotals* d_totals = nullptr;
+    // ring growth (edgpu_config.ring_growth): the plan's requests, how many the host has learnt
+    // of since (grown before the next ingest), which fan-out launch they were read for
+    GrowReq* d_grow = nullptr;
+    uint32_t grow_pending = 0;
+    uint64_t grow_seen_launch = 0;
+    uint64_t ring_grows = 0;
+    uint64_t ring_bytes = 0;                    // device bytes of the live senders' rings
 };
 
 static bool live_session(const edgpu_ctx* x, uint32_t s) { return s < x->sessions.size() && x->sessions[s].alive; }
@@ -351,6 +360,9 @@ static void fill_defaults(edgpu_config& c) {
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;
     if (!c.reflector_rtp_info_offset_msec) c.reflector_rtp_info_offset_msec = 500;
     else if (c.reflector_rtp_info_offset_msec == EDGPU_FALSE) c.reflector_rtp_info_offset_msec = 0;
+    c.ring_growth = (c.ring_growth == EDGPU_FALSE) ? 0 : 1;
+    if (!c.max_ring_packets) c.max_ring_packets = 1u << 20;
+    if (!c.max_ring_bytes) c.max_ring_bytes = 1ull << 30;
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -362,7 +374,8 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (cfg_in) c = *cfg_in; else edgpu_config_default(&c);
     fill_defaults(c);
     if (!pow2(c.video_ring_packets) || !pow2(c.other_ring_packets) || !pow2(c.video_ring_bytes) ||
-        !pow2(c.other_ring_bytes) || c.video_ring_bytes < 4096 || c.other_ring_bytes < 4096)
+        !pow2(c.other_ring_bytes) || c.video_ring_bytes < 4096 || c.other_ring_bytes < 4096 ||
+        !pow2(c.max_ring_packets) || !pow2(c.max_ring_bytes))
         return fail(EDGPU_BAD_ARGUMENT, "ring capacities must be powers of two (bytes >= 4096)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -398,6 +411,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
         if (hipEventCreateWithFlags(&x->ev_copy, hipEventDisableTiming) != hipSuccess) return bad("event");
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
+    if (dmalloc(&x->d_grow, sizeof(GrowReq) * kMaxGrow) != hipSuccess) return bad("ring growth requests");
     if (hipMalloc(&x->d_null, 4096) != hipSuccess || hipMemset(x->d_null, 0, 4096) != hipSuccess) return bad("null ring");
     {
         TickTotals t0;
@@ -442,7 +456,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
-                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals})
+                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals, (void*)x->d_grow})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->h2d) (void)hipStreamSynchronize(x->h2d);
@@ -525,6 +539,87 @@ static int read_totals(edgpu_ctx* x, TickTotals* t) {
     Readback rb(x);
     HIP_CHECK(rb.add(t, x->d_totals, sizeof(*t)));
     HIP_CHECK(rb.run());
+    return EDGPU_OK;
+}
+
+// The plan's ring-growth requests of the tick read back in `t` (once per fan-out launch): grown
+// before the next ingest (grow_rings).
+static void note_grow(edgpu_ctx* x, const TickTotals& t) {
+    if (!x->fanout_launches || x->grow_seen_launch == x->fanout_launches) return;
+    x->grow_seen_launch = x->fanout_launches;
+    if (t.grow_count) x->grow_pending = std::min<uint32_t>(t.grow_count, kMaxGrow);
+}
+
+// Ring growth (edgpu_config.ring_growth), at a tick boundary -- before an ingest, nothing in
+// flight: every sender the last plan found holding more than half of a ring's capacity of what the
+// reference would retain gets that ring replaced by one of the requested power-of-two size, its
+// entries moved to their places under the new mask (the rings are addressed by monotonic index /
+// virtual byte, so an entry's new place is its index & new mask).  The sender's floor becomes the
+// tail the plan measured: entries older than it were already lost and must not look intact in
+// the larger ring.  A request made before the sender's head moved on (a replica's image apply in
+// between) is dropped; the next plan makes it again.
+static int grow_rings(edgpu_ctx* x) {
+    const uint32_t n = x->grow_pending;
+    x->grow_pending = 0;
+    if (!n) return EDGPU_OK;
+    HIP_CHECK(sync_all(x));
+    std::vector<GrowReq> req(n);
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(req.data(), x->d_grow, n * sizeof(GrowReq)));
+        HIP_CHECK(rb.run());
+    }
+    std::sort(req.begin(), req.end(), [](const GrowReq& a, const GrowReq& b) { return a.sender < b.sender; });
+    for (size_t k = 0; k < req.size(); k++) {
+        const GrowReq& R = req[k];
+        if ((k && req[k - 1].sender == R.sender) || R.sender >= x->nsenders || !x->snd_meta[R.sender]) continue;
+        SenderDev D;
+        {
+            Readback rb(x);
+            HIP_CHECK(rb.add(&D, x->d_senders.ptr + R.sender, sizeof(D)));
+            HIP_CHECK(rb.run());
+        }
+        if (D.head != R.head || D.meta != (uint64_t)(uintptr_t)x->snd_meta[R.sender]) continue;
+        const uint64_t old_pk = (uint64_t)D.pk_mask + 1, old_by = ((uint64_t)D.word_mask + 1) * 16;
+        const uint64_t new_pk = std::min<uint64_t>(std::max<uint64_t>(old_pk, 1ull << R.pk_log2), x->cfg.max_ring_packets);
+        const uint64_t new_by = std::min<uint64_t>(std::max<uint64_t>(old_by, 1ull << R.bytes_log2), x->cfg.max_ring_bytes);
+        if (new_pk == old_pk && new_by == old_by) continue;
+        void* meta = x->snd_meta[R.sender];
+        void* ring = x->snd_ring[R.sender];
+        void* nmeta = meta;
+        void* nring = ring;
+        if (new_pk > old_pk) {
+            if (dmalloc(&nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess)
+                return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender meta ring");
+            const uint64_t lo = D.head > old_pk ? D.head - old_pk : 0;
+            HIP_CHECK(launch_ring_move(0, meta, old_pk - 1, nmeta, new_pk - 1, lo, D.head - lo, x->stream));
+            HIP_CHECK(launch_ring_move(1, (const uint8_t*)meta + old_pk * sizeof(PktMeta), old_pk - 1,
+                                       (uint8_t*)nmeta + new_pk * sizeof(PktMeta), new_pk - 1, lo, D.head - lo, x->stream));
+        }
+        if (new_by > old_by) {
+            if (dmalloc(&nring, new_by) != hipSuccess) {
+                if (nmeta != meta) (void)hipFree(nmeta);
+                return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender byte ring");
+            }
+            const uint64_t wend = D.vbyte_end / 16, wlo = wend > old_by / 16 ? wend - old_by / 16 : 0;
+            HIP_CHECK(launch_ring_move(2, ring, old_by / 16 - 1, nring, new_by / 16 - 1, wlo, wend - wlo, x->stream));
+        }
+        D.meta = (uint64_t)(uintptr_t)nmeta;
+        D.ring = (uint64_t)(uintptr_t)nring;
+        D.pk_mask = (uint32_t)(new_pk - 1);
+        D.word_mask = (uint32_t)(new_by / 16 - 1);
+        D.floor = std::max(D.floor, R.tail);
+        HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + R.sender, &D, sizeof(D), hipMemcpyHostToDevice, x->stream));
+        HIP_CHECK(hipStreamSynchronize(x->stream));
+        if (nmeta != meta) HIP_CHECK(hipFree(meta));
+        if (nring != ring) HIP_CHECK(hipFree(ring));
+        x->snd_meta[R.sender] = nmeta;
+        x->snd_ring[R.sender] = nring;
+        x->work_cap_needed += new_pk / 16 - old_pk / 16;
+        x->ring_bytes += (new_pk - old_pk) * (sizeof(PktMeta) + sizeof(uint32_t)) + (new_by - old_by);
+        x->ring_grows++;
+        x->index_dirty = true;                  // the work list is sized from the rings
+    }
     return EDGPU_OK;
 }
 
@@ -697,6 +792,7 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             D.last_nonzero = -1;
             D.new_start = -1;
             x->work_cap_needed += pk / 16 + 1;          // smallest chunk of any variant
+            x->ring_bytes += pk * (sizeof(PktMeta) + sizeof(uint32_t)) + by;
         }
         str[t].packet_count = 0;
     }
@@ -766,6 +862,8 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     for (uint32_t i = 0; i < nsnd; i++) {
         const uint32_t gs = sh.first_sender + i;
         x->work_cap_needed -= ((uint64_t)old[i].pk_mask + 1) / 16 + 1;
+        x->ring_bytes -= ((uint64_t)old[i].pk_mask + 1) * (sizeof(PktMeta) + sizeof(uint32_t)) +
+                         ((uint64_t)old[i].word_mask + 1) * 16;
         snd[i].stream = old[i].stream;
         snd[i].track = old[i].track;
         for (auto* v : {&x->snd_meta, &x->snd_ring}) {
@@ -1344,6 +1442,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     }
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
+    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
     const edgpu_pkt_desc* dd = desc;
     const uint32_t* ds = seg_off;
     const uint32_t* dss = seg_sess;
@@ -1395,6 +1494,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (int r = owed_pass(x, "edgpu_ingest_interleaved")) return r;
     if (!n) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
+    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
     { int r = wait_pinned_copies(x); if (r) return r; }
     x->carry_len.resize(x->sessions.size(), 0);
     // one group per session: its reads are a run of consecutive entries, contiguous in `bytes`
@@ -1573,6 +1673,10 @@ static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     p.T.chunk = (uint32_t)fanout_chunk(x->tick_variant);
     p.T.pass_ord = x->pass_ord;
     p.T.pass_id = x->pass_id;
+    p.grow = x->d_grow;
+    p.T.grow_on = x->cfg.ring_growth;
+    p.T.grow_max_pk = x->cfg.max_ring_packets;
+    p.T.grow_max_bytes = x->cfg.max_ring_bytes;
     return p;
 }
 
@@ -1657,6 +1761,7 @@ int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched
         HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
         HIP_CHECK(rb.run());
     }
+    note_grow(x, t);
     if (t.status) {
         // a failed tick owes nothing: its remaining passes are dropped (the next fan-out counts
         // them in lost_passes), so the context does not refuse every later call
@@ -1693,6 +1798,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
         HIP_CHECK(rb.add(&t, x->d_totals, sizeof(t)));
         HIP_CHECK(rb.run());
     }
+    note_grow(x, t);
     out->relayed_packets = t.relayed_packets;
     out->relayed_bytes = t.relayed_bytes;
     out->arena_bytes = t.arena_bytes;
@@ -1833,6 +1939,8 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     out->ingested_bytes = t.cum_ingested_bytes;
     out->fanout_passes = x->fanout_passes;
     out->lost_passes = t.cum_lost_passes;
+    out->ring_grows = x->ring_grows;
+    out->ring_bytes = x->ring_bytes;
     out->senders = x->nsenders;
     out->substream_rows = (uint32_t)x->sub_sender.size();
     return EDGPU_OK;

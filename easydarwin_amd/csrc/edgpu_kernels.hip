@@ -825,6 +825,7 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     if (t->pass_next[t->pass_slot & 1u] != kNoPass) t->cum_lost_passes++;
     t->pass_slot = 0;
     for (int k = 0; k < 2; k++) { t->pass_bytes[k] = 0; t->pass_desc[k] = 0; t->pass_next[k] = kNoPass; }
+    t->grow_count = 0;
 }
 
 // Per-tick counter updates as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
@@ -867,10 +868,48 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
                                                  [&](const PktMeta& m) { return m.arrival >= cutoff; });
         if (f < head) ns = (f == tail && tail > D.floor) ? -2 : (int64_t)f;   // -2: window exceeds ring
     }
+    // Ring growth: the span the reference would still hold in its unbounded queue -- every packet
+    // younger than sMaxPacketAgeMSec = 10 x the buffer (ReflectorStream.cpp:112-114), the key
+    // packet and everything after it, and what last tick's outputs still read from (a blocked
+    // output's bookmark keeps its packet, fNeededByOutput, RemoveOldPackets :1233-1289).  Measured
+    // only once the ring holds more than half of either capacity; a span over half of one asks
+    // the host to double that ring before the next ingest (GrowReq).
+    if (P.T.grow_on && head > tail) {
+        const uint64_t held_b = vend - meta[tail & D.pk_mask].vbyte;
+        if (2 * (head - tail) > pk_cap || 2 * held_b > byte_cap) {
+            const int64_t age_cut = P.T.now - 10 * P.T.over_buffer_ms;
+            uint64_t r = wave_lower_bound_meta(meta, D.pk_mask, tail, head,
+                                               [&](const PktMeta& m) { return m.arrival >= age_cut; });
+            if (D.key >= 0 && (uint64_t)D.key >= tail) r = min(r, (uint64_t)D.key);
+            if (D.umin >= tail) r = min(r, D.umin);              // last tick's reads (before the reset below)
+            const uint64_t need_pk = head - r;
+            const uint64_t need_b = r < head ? vend - meta[r & D.pk_mask].vbyte : 0;
+            uint64_t want_pk = pk_cap, want_b = byte_cap;
+            while (2 * need_pk > want_pk && want_pk < P.T.grow_max_pk) want_pk *= 2;
+            while (2 * need_b > want_b && want_b < P.T.grow_max_bytes) want_b *= 2;
+            if ((threadIdx.x & 63) == 0 && (want_pk > pk_cap || want_b > byte_cap)) {
+                const uint32_t k = atomicAdd(&P.totals->grow_count, 1u);
+                if (k < kMaxGrow)
+                    P.grow[k] = GrowReq{s, (uint32_t)(63 - __clzll((long long)want_pk)),
+                                        (uint32_t)(63 - __clzll((long long)want_b)), 0u, tail, head};
+            }
+        }
+    }
     if ((threadIdx.x & 63) == 0) {
         D.tail = tail;
         D.new_start = ns;
         D.umin = head;
+    }
+}
+
+// Ring growth: a sender's ring entries [lo, lo + n) (monotonic indices) from a ring of mask
+// `smask` to one of mask `dmask` (both powers of two minus one), entry v at v & mask in each.
+template <typename T>
+__global__ __launch_bounds__(256) void k_ring_move(const T* __restrict__ src, uint64_t smask, T* __restrict__ dst,
+                                                   uint64_t dmask, uint64_t lo, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t v = lo + i;
+        dst[v & dmask] = src[v & smask];
     }
 }
 
@@ -2564,6 +2603,21 @@ hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
     if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+// A sender ring moved into a larger one (ring growth): kind 0 the PktMeta ring, 1 its blob-slot
+// array (uint32 per entry), 2 the byte ring (16-B words); entries [lo, lo + n).
+hipError_t launch_ring_move(int kind, const void* src, uint64_t smask, void* dst, uint64_t dmask, uint64_t lo, uint64_t n,
+                            hipStream_t st) {
+    if (!n) return hipSuccess;
+    const uint64_t nb = (n + 255) / 256;
+    const uint32_t blocks = (uint32_t)(nb < 4096 ? nb : 4096);
+    if (kind == 0)
+        hipLaunchKernelGGL(k_ring_move<PktMeta>, dim3(blocks), dim3(256), 0, st, (const PktMeta*)src, smask, (PktMeta*)dst, dmask, lo, n);
+    else if (kind == 1)
+        hipLaunchKernelGGL(k_ring_move<uint32_t>, dim3(blocks), dim3(256), 0, st, (const uint32_t*)src, smask, (uint32_t*)dst, dmask, lo, n);
+    else
+        hipLaunchKernelGGL(k_ring_move<u32x4>, dim3(blocks), dim3(256), 0, st, (const u32x4*)src, smask, (u32x4*)dst, dmask, lo, n);
     return hipGetLastError();
 }
 hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st) {

@@ -96,6 +96,7 @@ struct PlanParams {
     uint32_t* blk_maxc;
     SessionDev* sessions;       // stream errors (per-session isolation)
     TickTotals* totals;
+    GrowReq* grow;              // ring growth requests (kMaxGrow)
     TickParams T;
 };
 

@@ -605,7 +605,7 @@ QTSS_Error Tick() {
                 for (const auto& kv : M->sessions)
                     if (kv.second.engine == e)
                         fprintf(stderr, "QTSSReflectorModule: stream %s lost packets its outputs needed (sender ring "
-                                        "too small for them: raise the ring capacity)\n", kv.second.name.c_str());
+                                        "at its bound: raise EDGPU_QTSS_MAX_RING_MB / _PACKETS)\n", kv.second.name.c_str());
             }
     }
     o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -709,6 +709,13 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     if (const char* v = getenv("EDGPU_QTSS_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_QTSS_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)atoll(v);
     if (const char* v = getenv("EDGPU_QTSS_MAX_BATCH_PACKETS")) cfg.max_batch_packets = (uint32_t)atoll(v);
+    // sender rings: their starting capacities and the bound of their growth (powers of two; the
+    // rings grow to hold what the reference retains, RemoveOldPackets, ReflectorStream.cpp:1233-1289)
+    if (const char* v = getenv("EDGPU_QTSS_VIDEO_RING_MB")) cfg.video_ring_bytes = (uint64_t)atoll(v) << 20;
+    if (const char* v = getenv("EDGPU_QTSS_VIDEO_RING_PACKETS")) cfg.video_ring_packets = (uint32_t)atoll(v);
+    if (const char* v = getenv("EDGPU_QTSS_MAX_RING_MB")) cfg.max_ring_bytes = (uint64_t)atoll(v) << 20;
+    if (const char* v = getenv("EDGPU_QTSS_MAX_RING_PACKETS")) cfg.max_ring_packets = (uint32_t)atoll(v);
+    if (const char* v = getenv("EDGPU_QTSS_RING_GROWTH")) cfg.ring_growth = atoi(v) ? 0u : EDGPU_FALSE;
     M->R.reset(new edgpu_reflector::Reflector(&cfg));
     if (M->R->Status() != 0) {
         fprintf(stderr, "QTSSReflectorModule: edgpu context: %s\n", edgpu_last_error());

@@ -65,6 +65,9 @@ class Config(C.Structure):
         ("max_batch_bytes", C.c_uint64),
         ("overlap_ticks", C.c_uint32),
         ("reflector_rtp_info_offset_msec", C.c_uint32),
+        ("ring_growth", C.c_uint32),
+        ("max_ring_packets", C.c_uint32),
+        ("max_ring_bytes", C.c_uint64),
     ]
 
 
@@ -138,7 +141,8 @@ class Counters(C.Structure):
                 ("fanout_in_bytes", C.c_uint64), ("fanout_launches", C.c_uint64),
                 ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64),
                 ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64),
-                ("senders", C.c_uint32), ("substream_rows", C.c_uint32)]
+                ("senders", C.c_uint32), ("substream_rows", C.c_uint32),
+                ("ring_grows", C.c_uint64), ("ring_bytes", C.c_uint64)]
 
 
 # numpy mirrors (same layout as the C structs)

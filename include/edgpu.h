@@ -112,6 +112,17 @@ typedef struct edgpu_config {
     uint32_t reflector_rtp_info_offset_msec; /* RTP-Info first packet: within over-buffer minus
                                                this (ReflectorStream.cpp:109-110); default 500,
                                                EDGPU_FALSE for an offset of 0 */
+    /* Ring growth (default on; EDGPU_FALSE: the rings keep their configured capacities).  The
+     * reference keeps every packet younger than 10 x reflector_buffer_size_sec, the key packet
+     * and everything after it, and whatever a blocked output still needs, in an unbounded queue
+     * (RemoveOldPackets, ReflectorStream.cpp:1233-1289, 112-114).  Each fan-out's plan measures
+     * that span per sender; a sender whose span passes half of either of its rings has that ring
+     * doubled (powers of two, up to the bounds below) before the next edgpu_ingest, its packets
+     * moved over.  The request is noticed when the host reads the tick (edgpu_tick_stats_get /
+     * edgpu_fanout_next), as every tick driver does. */
+    uint32_t ring_growth;
+    uint32_t max_ring_packets;              /* per sender bound of growth (1 Mi), power of two */
+    uint64_t max_ring_bytes;                /* per sender bound of growth (1 GiB), power of two */
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu   /* a flag off / a value of 0 where 0 would select the default */
 
@@ -674,6 +685,8 @@ typedef struct edgpu_counters {
     uint64_t lost_passes;       /* passes a tick still owed when the next tick was planned */
     uint32_t senders;           /* sender rows (2 per track) and sub-stream rows of the tables: */
     uint32_t substream_rows;    /* removed sessions' / subscribers' rows are reused, best fit */
+    uint64_t ring_grows;        /* sender rings grown so far (edgpu_config.ring_growth) */
+    uint64_t ring_bytes;        /* device bytes of every live sender's two rings now */
 } edgpu_counters;
 int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 

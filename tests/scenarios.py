@@ -682,6 +682,40 @@ def keepalive() -> Trace:
     return _assemble(tr, [pk0, pk1], 250, dur, joins)
 
 
+def highrate() -> Trace:
+    """A stream the engine's default rings cannot hold: 1080p at 12 Mb/s
+    with a 10-s GOP.  The reference keeps every packet younger than 10 x the buffer and the key
+    packet with everything after it in an unbounded queue (RemoveOldPackets, ReflectorStream.cpp:
+    1233-1289), so players joining at 9 s are replayed the GOP from its key packet at 0 s: ~9,600
+    packets / 13.5 MB, past the default 8,192-packet / 8-MiB video ring.  The engine grows that
+    sender's rings before they lose what the reference retains (edgpu_config.ring_growth)."""
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=12_000_000, gop=300, idr_bytes=150_000, rtcp_every_ms=1000)]
+    tr = Trace()
+    tr.add_session(make_sdp(v))
+    dur = 11_000
+    pk = session_packets(v, dur, SEED_BASE + 140)
+    joins = [(0, 0, 1, UDP), (9000, 0, 2, UDP), (9000, 0, 3, TCP), (10_500, 0, 4, UDP)]
+    return _assemble(tr, [pk], 100, dur, joins)
+
+
+def longbuffer() -> Trace:
+    """reflector_buffer_size_sec = 3 (ReflectorStream.cpp:87-117: a 3-s new-output window and a 30-s
+    packet age, sMaxPacketAgeMSec) on a 4 Mb/s stream with a 2-s GOP, and a TCP player held by
+    backpressure for 8 s (BLOCK from 3 s to 11 s: its bookmark holds its packet, fNeededByOutput, until
+    the relocation threshold moves it, Q9) -- at the engine's default ring capacities."""
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=4_000_000, gop=60, idr_bytes=60_000, rtcp_every_ms=1000),
+         TrackSpec("audio", "PCMA/8000", 8)]
+    tr = Trace()
+    tr.prefs = {"reflector_buffer_size_sec": "3"}
+    tr.add_session(make_sdp(v))
+    dur = 14_000
+    pk = session_packets(v, dur, SEED_BASE + 141)
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (5000, 0, 3, UDP), (12_000, 0, 4, TCP)]
+    ticks = list(range(0, dur + 1, 100))
+    blocks = {t: [(2, 0, 0, 0), (2, 1, 0, 0)] for t in ticks if 3000 <= t < 11_000}
+    return _assemble(tr, [pk], 100, dur, joins, tick_times=ticks, blocks=blocks)
+
+
 def prefs_push() -> Trace:
     """The module prefs that gate the push path, toggled by PREFS events (RereadPrefs,
     QTSSReflectorModule.cpp:454-541).  A scenario for the QTSS module only (tools/qtss_replay):
@@ -733,7 +767,7 @@ SCENARIOS = {
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
     "backpressure": backpressure, "udppush": udppush, "leave": leave, "repush": repush,
     "threaded": threaded, "prefs_buffer": prefs_buffer, "prefs_reread": prefs_reread,
-    "keepalive": keepalive,
+    "keepalive": keepalive, "highrate": highrate, "longbuffer": longbuffer,
 }
 
 

@@ -20,12 +20,14 @@ TOOL = os.path.join(ROOT, "tools", "adapter_replay")
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["tiny", "mixed", "nal", "ssrc", "anchor", "c1", "rtpinfo", "backpressure", "leave",
-                                  "udppush", "repush", "prefs_buffer", "prefs_reread"])
+                                  "udppush", "repush", "prefs_buffer", "prefs_reread", "keepalive", "highrate",
+                                  "longbuffer"])
 def test_adapter_replay_matches_reference(name, tmp_path):
     fix = json.load(open(os.path.join(GOLD, name + ".json")))
     t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"
     t.write_bytes(SCENARIOS[name]().to_bytes())
-    subprocess.run([TOOL, str(t), str(c)], check=True)
+    r = subprocess.run([TOOL, str(t), str(c)], check=True, capture_output=True, text=True)
+    assert "0 stream errors" in r.stderr, r.stderr[-2000:]
     cap = c.read_bytes()
     if hashlib.sha256(cap).hexdigest() != fix["capture_sha256"]:
         got = capture_summary(read_capture(cap))

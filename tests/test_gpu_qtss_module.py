@@ -37,11 +37,12 @@ TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "an
 UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones beside them)
 PREFS = ["prefs_buffer", "prefs_reread", "prefs_push"]   # the server's prefs objects, RereadPrefs
 KEEPALIVE = ["keepalive"]                     # 70 s: the pushers' timeouts and the module's refreshes
+RETENTION = ["highrate", "longbuffer"]        # retention past the default ring capacities (ring growth)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["whole", "parts"])
-@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE)
+@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE + RETENTION)
 def test_module_matches_reference(name, gather, tmp_path):
     """`parts`: every tick's readback gathered in parts, overlapped with the write threads
     (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split).  The
@@ -55,6 +56,7 @@ def test_module_matches_reference(name, gather, tmp_path):
         env["EDGPU_GATHER_SPLIT_BYTES"] = "0"
     r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
+    assert "lost packets" not in r.stderr, r.stderr[-2000:]          # no stream error at default capacities
     if name in UDP_PUSH:                 # name the part that differs before the whole-file hash
         from easydarwin_amd.trace import capture_summary, read_capture, read_source_reports
         fx = _fixture(name)

@@ -98,7 +98,7 @@ int main(int argc, char** argv) {
     if (const char* v = getenv("EDGPU_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)strtoul(v, nullptr, 0);
     Reflector R(&cfg);
-    uint64_t ticks = 0, passes = 0;
+    uint64_t ticks = 0, passes = 0, stream_errors = 0;
     if (R.Status()) { fprintf(stderr, "edgpu: %s\n", edgpu_last_error()); return 3; }
     uint32_t rand_calls = 0;                  // the harness's deterministic rand() (trace.py rr_ssrc)
     std::vector<int64_t> sid_of(nsess, -1);   // engine session of each trace session (-1: removed)
@@ -208,6 +208,7 @@ int main(int argc, char** argv) {
             }
             ticks++;
             passes += R.LastTick().passes;
+            stream_errors += R.LastTick().stream_errors;
             sink.budget.clear();
         } else if (type == 6) {               // LEAVE: ReflectorSession::RemoveOutput
             uint32_t sub; get(sub);
@@ -260,7 +261,8 @@ int main(int argc, char** argv) {
         }
     }
     fclose(o);
-    fprintf(stderr, "adapter_replay: %llu ticks, %llu copy passes\n", (unsigned long long)ticks, (unsigned long long)passes);
+    fprintf(stderr, "adapter_replay: %llu ticks, %llu copy passes, %llu stream errors\n", (unsigned long long)ticks,
+            (unsigned long long)passes, (unsigned long long)stream_errors);
     if (sink.failPass)
         fprintf(stderr, "adapter_replay: %llu failed ticks, %llu good ticks after the failure\n",
                 (unsigned long long)failedTicks, (unsigned long long)ticksAfterFailure);
