@@ -212,12 +212,18 @@ struct Output {                         // one player (RTPSessionOutput)
     QTSS_Object client = nullptr;
     uint32_t session = 0;
     bool tcp = false;
-    bool joined = false;                // engine subscriber exists
-    bool paused = false;
+    bool joined = false;                // engine subscriber exists (guarded by mu)
+    std::atomic<bool> paused{false};
     uint32_t handle = 0;
-    std::vector<QTSS_Object> streams;   // per track: the RTP stream object SETUP created (or null)
+    // per track: the RTP stream object SETUP created (or null); read by the write threads
+    std::unique_ptr<std::atomic<QTSS_Object>[]> streams;
+    uint32_t nstreams = 0;
     int32_t slot = -1;                  // position in the session's buckets (sBucketSize members each)
-    int64_t bufferDelayMs = 0;          // RTPSessionOutput::fBufferDelayMSecs
+    int64_t bufferDelayMs = 0;          // RTPSessionOutput::fBufferDelayMSecs (its write thread's, once joined)
+    // a teardown while a tick writes (ClientSessionClosing): `closed` stops new writes to it,
+    // `writing` is held by the one write thread delivering to it (the reference's RemoveOutput
+    // waits for the stream's fBucketMutex, ReflectorStream.cpp:338-362, 1051)
+    std::atomic<bool> closed{false}, writing{false};
 };
 
 struct Module {
@@ -237,8 +243,16 @@ struct Module {
         std::map<uint32_t, Route> route;
     } routes[kRouteStripes];
     std::mutex udpMu;                   // guards `udp` (the reader thread takes only this)
-    std::map<uint32_t, Output*> byHandle;
     std::vector<std::unique_ptr<Output>> outputs;
+    // The tick's writes run without `mu` (and without the engine lock, SetConcurrentDelivery): they
+    // find an output by its engine handle in a table read without a lock -- chunks of 4096 entries,
+    // set under `mu` -- and an output removed meanwhile stays allocated until every tick that may
+    // have read it has ended (graveyard, by the tick sequence at removal).
+    static constexpr uint32_t kChunkBits = 12, kChunk = 1u << kChunkBits, kChunks = 1u << 16;
+    std::unique_ptr<std::atomic<std::atomic<Output*>*>[]> handleChunks{new std::atomic<std::atomic<Output*>*>[kChunks]};
+    uint64_t tickSeq = 0;                                              // ticks started (under mu)
+    std::vector<std::pair<uint64_t, std::unique_ptr<Output>>> graveyard;
+    std::mutex tickMu;                  // one tick at a time (the ticker and EDGPU_QTSSReflectorModule_Tick)
     int32_t rtpInfoWaitLoops = 10;      // sWaitTimeLoopCount: 100-ms PLAY retries before 404
     uint32_t tickMs = 20;
     // EDGPU_QTSS_REFLECT_ON_ARRIVAL=<ms> (default 2): reflect as soon as packets are waiting, at
@@ -277,6 +291,27 @@ struct Module {
     std::vector<uint32_t> orphans;      // engine sessions whose removal the engine refused: retried per tick
 };
 Module* M = nullptr;
+
+Output* OutputOf(uint32_t h) {
+    if ((h >> Module::kChunkBits) >= Module::kChunks) return nullptr;
+    std::atomic<Output*>* c = M->handleChunks[h >> Module::kChunkBits].load(std::memory_order_acquire);
+    return c ? c[h & (Module::kChunk - 1)].load(std::memory_order_acquire) : nullptr;
+}
+// Caller holds mu.
+void SetOutputOf(uint32_t h, Output* o) {
+    if ((h >> Module::kChunkBits) >= Module::kChunks) {
+        fprintf(stderr, "QTSSReflectorModule: subscriber handle %u past the handle table\n", h);
+        return;
+    }
+    std::atomic<std::atomic<Output*>*>& slot = M->handleChunks[h >> Module::kChunkBits];
+    std::atomic<Output*>* c = slot.load(std::memory_order_acquire);
+    if (!c) {
+        c = new std::atomic<Output*>[Module::kChunk];
+        for (uint32_t i = 0; i < Module::kChunk; i++) c[i].store(nullptr, std::memory_order_relaxed);
+        slot.store(c, std::memory_order_release);
+    }
+    c[h & (Module::kChunk - 1)].store(o, std::memory_order_release);
+}
 
 // The channel of a request: the first "channel" parameter (any case) of the URL-decoded query
 // string, 1 without one (DoSessionSetup / DoAnnounce, QRM:740-756 / 919-935: EasyUtil::Urldecode,
@@ -381,10 +416,10 @@ public:
         firstNewSlot.clear();
         for (uint32_t i = 0; i < n; i++) {
             if (!(subs[i].flags & EDGPU_SUB_NEW)) continue;
-            auto it = M->byHandle.find(subs[i].subscriber);
-            if (it == M->byHandle.end() || it->second->slot < 0) continue;
+            const Output* o = OutputOf(subs[i].subscriber);
+            if (!o || o->slot < 0) continue;
             auto f = firstNewSlot.find(subs[i].sender);
-            if (f == firstNewSlot.end() || it->second->slot < f->second) firstNewSlot[subs[i].sender] = it->second->slot;
+            if (f == firstNewSlot.end() || o->slot < f->second) firstNewSlot[subs[i].sender] = o->slot;
         }
     }
     int WritePacket(uint32_t, uint16_t, bool, bool, const uint8_t*, uint32_t, uint32_t) override {
@@ -400,26 +435,39 @@ public:
         bool lastHasFirst = false;
     };
     Cache cache[64];
+    // The write thread moves on from output `c.lastOut` (or ends its writes): the output's teardown
+    // may proceed (it waits for `writing` to drop).
+    static void Leave(Cache& c) {
+        if (c.lastOut) c.lastOut->writing.store(false, std::memory_order_release);
+        c.lastOut = nullptr;
+        c.lastHandle = 0xFFFFFFFFu;
+    }
+    void EndWrites(uint32_t worker) override { Leave(cache[worker & 63]); }
     int Write(const edgpu_reflector::PacketWrite& w) override {
         Cache& c = cache[w.worker & 63];
-        uint32_t& lastHandle = c.lastHandle;
         uint32_t& lastSender = c.lastSender;
-        Output*& lastOut = c.lastOut;
         int32_t& lastFirst = c.lastFirst;
         bool& lastHasFirst = c.lastHasFirst;
-        if (w.subscriber != lastHandle) {
-            auto it = M->byHandle.find(w.subscriber);
-            lastHandle = w.subscriber;
-            lastOut = it == M->byHandle.end() ? nullptr : it->second;
+        if (w.subscriber != c.lastHandle) {
+            Leave(c);
+            c.lastHandle = w.subscriber;
+            Output* o = OutputOf(w.subscriber);
+            if (o) {
+                // hold it, then check it is still an output (a teardown sets `closed`, then waits)
+                o->writing.store(true, std::memory_order_seq_cst);
+                if (o->closed.load(std::memory_order_seq_cst)) o->writing.store(false, std::memory_order_release);
+                else c.lastOut = o;
+            }
         }
-        if (!lastOut) {
+        if (!c.lastOut) {
             if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: write for unknown handle %u\n", w.subscriber);
             return edgpu_reflector::kNoErr;
         }
-        Output& o = *lastOut;
+        Output& o = *c.lastOut;
         // not playing (paused): WritePacket returns QTSS_WouldBlock (RTPSessionOutput.cpp:575-579)
-        if (o.paused) return edgpu_reflector::kWouldBlock;
-        if (w.track >= o.streams.size() || !o.streams[w.track]) {                               // track not SETUP
+        if (o.paused.load(std::memory_order_relaxed)) return edgpu_reflector::kWouldBlock;
+        QTSS_Object stream = w.track < o.nstreams ? o.streams[w.track].load(std::memory_order_acquire) : nullptr;
+        if (!stream) {                                                                           // track not SETUP
             if (getenv("EDGPU_QTSS_DEBUG")) fprintf(stderr, "QTSSReflectorModule: handle %u track %u not set up\n", w.subscriber, w.track);
             return edgpu_reflector::kNoErr;
         }
@@ -442,7 +490,7 @@ public:
         if (o.bufferDelayMs > 0) ps.packetTransmitTime += o.bufferDelayMs - (now - w.arrivalMs);
         ps.suggestedWakeupTime = -1;
         const uint32_t flags = (w.isRTCP ? qtssWriteFlagsIsRTCP : qtssWriteFlagsIsRTP) | qtssWriteFlagsWriteBurstBegin;
-        const QTSS_Error err = cb(kWriteCallback, o.streams[w.track], (const void*)&ps, len, (uint32_t*)nullptr, flags);
+        const QTSS_Error err = cb(kWriteCallback, stream, (const void*)&ps, len, (uint32_t*)nullptr, flags);
         // only QTSS_WouldBlock stops SendPacketsToOutput (ReflectorStream.cpp:1158-1190); blocked
         // on a first-packet pass, the output's buffer delay becomes this packet's age (:617-622)
         if (err == QTSS_WouldBlock) {
@@ -451,23 +499,32 @@ public:
         }
         return edgpu_reflector::kNoErr;
     }
-    // ReflectorStream::SendReceiverReport (ReflectorStream.cpp:510-527): from the track's RTCP
-    // socket to the pusher's RTCP address; the send result is ignored, as there
+    // ReflectorStream::SendReceiverReport (ReflectorStream.cpp:510-527): kept until the tick's
+    // engine part is over, then sent by SendReports
+    struct RR { uint32_t session; uint16_t track; uint32_t addr; uint16_t port; std::string bytes; };
+    std::vector<RR> reports;
     void SendReceiverReport(uint32_t session, uint16_t track, uint32_t addr, uint16_t port, const uint8_t* rr,
                             uint32_t len) override {
-        for (const auto& kv : M->sessions) {
-            const Session& s = kv.second;
-            if (s.engine != session || track >= s.pair.size() || s.pair[track] < 0) continue;
-            sockaddr_in to;
-            memset(&to, 0, sizeof(to));
-            to.sin_family = AF_INET;
-            to.sin_addr.s_addr = htonl(addr);
-            to.sin_port = htons(port);
-            std::lock_guard<std::mutex> g(M->udpMu);
-            const int fd = M->udp[s.pair[track]].fd[1];
-            if (fd >= 0) (void)sendto(fd, rr, len, MSG_NOSIGNAL, (const sockaddr*)&to, sizeof(to));
-            return;
-        }
+        reports.push_back(RR{session, track, addr, port, std::string((const char*)rr, len)});
+    }
+    // from the track's RTCP socket to the pusher's RTCP address; the send result is ignored, as
+    // there.  Caller holds mu.
+    void SendReports() {
+        for (const RR& r : reports)
+            for (const auto& kv : M->sessions) {
+                const Session& s = kv.second;
+                if (s.engine != r.session || r.track >= s.pair.size() || s.pair[r.track] < 0) continue;
+                sockaddr_in to;
+                memset(&to, 0, sizeof(to));
+                to.sin_family = AF_INET;
+                to.sin_addr.s_addr = htonl(r.addr);
+                to.sin_port = htons(r.port);
+                std::lock_guard<std::mutex> g(M->udpMu);
+                const int fd = M->udp[s.pair[r.track]].fd[1];
+                if (fd >= 0) (void)sendto(fd, r.bytes.data(), r.bytes.size(), MSG_NOSIGNAL, (const sockaddr*)&to, sizeof(to));
+                break;
+            }
+        reports.clear();
     }
 };
 
@@ -577,14 +634,32 @@ void ReaderLoop() {
     }
 }
 
+// One reflect tick.  `mu` is held only to start and to end it: the engine part (ingest, fan-out,
+// readback) holds the Reflector's engine lock, and the QTSS_Writes hold neither (SetConcurrentDelivery),
+// so SETUP / PLAY / TEARDOWN proceed while a tick writes -- as the reference's per-stream
+// fBucketMutex lets them (ReflectorStream.cpp:1051); a TEARDOWN waits only for the output it removes.
 QTSS_Error Tick() {
+    std::lock_guard<std::mutex> tg(M->tickMu);
     const auto t0 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> g(M->mu);
-    if (!M->R) return QTSS_RequestFailed;
+    uint64_t seq;
+    double held = 0;                                      // ms this tick held `mu`
+    {
+        std::lock_guard<std::mutex> g(M->mu);
+        if (!M->R) return QTSS_RequestFailed;
+        seq = ++M->tickSeq;
+        held += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     M->pending.store(false, std::memory_order_release);   // this tick takes what arrived so far
     QTSSSink sink;
     sink.now = Milliseconds();
     const int err = M->R->ReflectPackets(sink.now, &sink);
+    std::lock_guard<std::mutex> g(M->mu);
+    const auto t1 = std::chrono::steady_clock::now();
+    sink.SendReports();
+    // outputs removed before or during this tick: no tick can reach them any more
+    M->graveyard.erase(std::remove_if(M->graveyard.begin(), M->graveyard.end(),
+                                      [&](const std::pair<uint64_t, std::unique_ptr<Output>>& e) { return e.first <= seq; }),
+                       M->graveyard.end());
     for (size_t i = 0; i < M->orphans.size();)
         if (M->R->RemoveSession(M->orphans[i], true) == 0) M->orphans.erase(M->orphans.begin() + i);
         else i++;
@@ -608,7 +683,9 @@ QTSS_Error Tick() {
                                         "at its bound: raise EDGPU_QTSS_MAX_RING_MB / _PACKETS)\n", kv.second.name.c_str());
             }
     }
-    o.hold_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // the session lock's hold: what SETUP / PLAY / TEARDOWN may wait for (the tick's wall time is
+    // ingest + fan-out + readback + writes)
+    o.hold_ms = held + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     o.hold_max_ms = std::max(o.hold_max_ms, o.hold_ms);
     o.hold_sum_ms += o.hold_ms;
     o.ticks++;
@@ -726,6 +803,10 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     uint32_t writers = 4;
     if (const char* v = getenv("EDGPU_QTSS_WRITE_THREADS")) writers = (uint32_t)std::max(1, atoi(v));
     M->R->SetWriteThreads(writers);
+    // the tick's writes run without the engine lock (EDGPU_QTSS_CONCURRENT_DELIVERY=0: held throughout)
+    bool concurrent = true;
+    if (const char* v = getenv("EDGPU_QTSS_CONCURRENT_DELIVERY")) concurrent = atoi(v) != 0;
+    M->R->SetConcurrentDelivery(concurrent);
     if (!M->manualTick) {
         M->stop = false;
         M->reader = std::thread(ReaderLoop);
@@ -1007,7 +1088,9 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         o->client = p->inClientSession;
         o->session = s->id;
         o->tcp = transport == qtssRTPTransportTypeTCP;
-        o->streams.assign(s->trackIDs.size(), nullptr);
+        o->nstreams = (uint32_t)s->trackIDs.size();
+        o->streams.reset(new std::atomic<QTSS_Object>[o->nstreams]);
+        for (uint32_t k = 0; k < o->nstreams; k++) o->streams[k].store(nullptr, std::memory_order_relaxed);
         s->refs++;
         (void)SetValue(p->inClientSession, sOutputAttr, 0, &o, sizeof(o));
     }
@@ -1021,7 +1104,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     (void)SetValue(stream, qtssRTPStrTrackID, 0, &trackID, sizeof(trackID));
     const uintptr_t cookie = ((uintptr_t)o->session << 16) | (uint32_t)t;          // the stream cookie
     (void)SetValue(stream, sStreamCookieAttr, 0, &cookie, sizeof(cookie));
-    o->streams[t] = stream;
+    if ((uint32_t)t < o->nstreams) o->streams[t].store(stream, std::memory_order_release);
     return cb(kSendStandardRTSPCallback, p->inRTSPRequest, stream, (uint32_t)qtssSetupRespDontWriteSSRC);
 }
 
@@ -1074,8 +1157,8 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
         std::unique_lock<std::mutex> g(M->mu);
         Session* s = FindSession(o->session);
         if (!s) return QTSS_RequestFailed;
-        if (o->joined && o->paused) {                     // resume after PAUSE
-            o->paused = false;
+        if (o->joined && o->paused.load()) {              // resume after PAUSE
+            o->paused.store(false);
         } else if (!o->joined) {
             const bool tcp = o->tcp;
             uint32_t h = 0;
@@ -1102,17 +1185,17 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
                     return cb(kSetIdleTimerCallback, (int64_t)100);
                 }
                 if (err) return QTSS_RequestFailed;
-                for (size_t t = 0; t < o->streams.size() && t < info.size(); t++) {
-                    if (!o->streams[t]) continue;
-                    (void)SetValue(o->streams[t], qtssRTPStrFirstSeqNumber, 0, &info[t].seq, sizeof(info[t].seq));
-                    (void)SetValue(o->streams[t], qtssRTPStrFirstTimestamp, 0, &info[t].rtptime, sizeof(info[t].rtptime));
+                for (size_t t = 0; t < o->nstreams && t < info.size(); t++) {
+                    QTSS_Object st = o->streams[t].load();
+                    if (!st) continue;
+                    (void)SetValue(st, qtssRTPStrFirstSeqNumber, 0, &info[t].seq, sizeof(info[t].seq));
+                    (void)SetValue(st, qtssRTPStrFirstTimestamp, 0, &info[t].rtptime, sizeof(info[t].rtptime));
                 }
             } else if ((err = M->R->AddOutput(s->engine, tcp, &h)) != 0) {
                 return QTSS_RequestFailed;
             }
             o->handle = h;
             o->joined = true;
-            M->byHandle[h] = o;
             // ReflectorSession::AddOutput: the first free bucket member (ReflectorStream.cpp:281-336)
             std::vector<Output*>& slots = s->slots;
             size_t k = 0;
@@ -1123,6 +1206,7 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
             if (getenv("EDGPU_QTSS_DEBUG"))
                 fprintf(stderr, "QTSSReflectorModule: output joined session=%u handle=%u slot=%zu tcp=%d\n", o->session, h, k, (int)tcp);
             o->bufferDelayMs = M->overBufferMs;         // RTPSessionOutput(): fBufferDelayMSecs
+            SetOutputOf(h, o);                          // the write threads find it from now on
         }
         g.unlock();
         const QTSS_Error e = cb(kPlayCallback, p->inClientSession, p->inRTSPRequest,
@@ -1134,15 +1218,27 @@ QTSS_Error DoPlay(QTSS_StandardRTSP_Params* p, Output* o) {
 
 // RemoveOutput(output, session, false) (QRM:2133-2196): out of the buckets, delete, and the
 // output's reference on the session goes
+// A tick writing to `o` finishes the write it is in; later ones skip it (Output::closed).
+void StopWrites(Output* o) {
+    o->closed.store(true, std::memory_order_seq_cst);
+    while (o->writing.load(std::memory_order_seq_cst)) std::this_thread::yield();
+}
+
 void RemoveOutputLocked(Output* o) {
+    StopWrites(o);                      // (callers outside a tick's writes find it idle)
     if (o->joined) {                    // an output whose PLAY never succeeded has no handle
         if (M->R) (void)M->R->RemoveOutput(o->handle);
-        M->byHandle.erase(o->handle);
+        SetOutputOf(o->handle, nullptr);
     }
     Session* s = FindSession(o->session);
     if (s && o->slot >= 0) s->slots[o->slot] = nullptr;
     for (auto it = M->outputs.begin(); it != M->outputs.end(); ++it)
-        if (it->get() == o) { M->outputs.erase(it); break; }
+        if (it->get() == o) {
+            // a tick that started before now may still hold it: freed once that tick has ended
+            M->graveyard.emplace_back(M->tickSeq, std::move(*it));
+            M->outputs.erase(it);
+            break;
+        }
     if (s) ReleaseLocked(s);
 }
 
@@ -1165,10 +1261,7 @@ QTSS_Error ProcessRTSPRequest(QTSS_StandardRTSP_Params* p) {
         (void)cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
         break;
     case qtssPauseMethod: {
-        {
-            std::lock_guard<std::mutex> g(M->mu);
-            o->paused = true;
-        }
+        o->paused.store(true);
         (void)cb(kPauseCallback, p->inClientSession);
         (void)cb(kSendStandardRTSPCallback, p->inRTSPRequest, p->inClientSession, (uint32_t)0);
         break;
@@ -1209,6 +1302,7 @@ QTSS_Error ProcessRTPData(QTSS_IncomingData_Params* p) {
 QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
     Output* o = nullptr;
     if (GetPOD(p->inClientSession, sOutputAttr, &o) && o) {
+        StopWrites(o);                  // waits for a tick's write to it only, not for `mu`
         std::lock_guard<std::mutex> g(M->mu);
         RemoveOutputLocked(o);
         Output* none = nullptr;
@@ -1274,7 +1368,10 @@ extern "C" QTSS_Error QTSSReflectorModule_Main(void* inPrivateArgs) {
     sCallbacks = a->inCallbacks;
     a->outStubLibraryVersion = kApiVersion;
     a->outDispatchFunction = Dispatch;
-    if (!M) M = new Module();
+    if (!M) {
+        M = new Module();
+        for (uint32_t k = 0; k < Module::kChunks; k++) M->handleChunks[k].store(nullptr, std::memory_order_relaxed);
+    }
     return QTSS_NoErr;
 }
 

@@ -72,6 +72,7 @@ int Reflector::EnsurePinned(PinBuf& b, uint64_t bytes) {
 
 int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint32_t* outSession) {
     if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     uint32_t s = 0, n = 0;
     int err = edgpu_session_add(fCtx, sdp.data(), (uint32_t)sdp.size(), udpPush ? 1 : 0, &s);
     if (err) return err;
@@ -86,6 +87,7 @@ int Reflector::SetupReflectorSession(const std::string& sdp, bool udpPush, uint3
 
 int Reflector::SetSSRCFilter(uint32_t session, bool oneSSRCPerStream, uint32_t timeoutSecs) {
     if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     return edgpu_session_ssrc_prefs(fCtx, session, oneSSRCPerStream ? 1 : 0, timeoutSecs);
 }
 
@@ -145,12 +147,15 @@ void Reflector::StagerLoop() {
 
 int Reflector::AddOutput(uint32_t session, bool interleaved, uint32_t* outHandle) {
     if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     return edgpu_subscriber_add(fCtx, session, interleaved ? EDGPU_TRANSPORT_TCP : EDGPU_TRANSPORT_UDP, outHandle);
 }
 
 int Reflector::PlayRTPInfo(uint32_t session, bool interleaved, int64_t nowMs, uint32_t* outHandle,
                            std::vector<edgpu_rtp_info>* outInfo) {
     if (!fCtx) return kRequestFailed;
+    std::unique_lock<std::mutex> eg(fEngineMu);
+    WaitIdle(eg);                                           // a tick's writes may read the batch
     int err = FlushIngest();
     if (err) return err;
     std::vector<edgpu_rtp_info> info(std::max<uint32_t>(GetNumStreams(session), 1));
@@ -162,11 +167,14 @@ int Reflector::PlayRTPInfo(uint32_t session, bool interleaved, int64_t nowMs, ui
 
 int Reflector::RemoveOutput(uint32_t handle) {
     if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     return edgpu_subscriber_remove(fCtx, handle);
 }
 
 int Reflector::RemoveSession(uint32_t session, bool killOutputs) {
     if (!fCtx) return kRequestFailed;
+    std::unique_lock<std::mutex> eg(fEngineMu);
+    WaitIdle(eg);                                           // a tick's writes may read the batch
     // what was pushed to it before the end is ingested (the reference had queued it)
     int err = FlushIngest();
     if (err) return err;
@@ -291,6 +299,7 @@ void Reflector::ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort
 
 int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs) {
     if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     return edgpu_source_identity(fCtx, session, track, ssrc, cnameSecs);
 }
 
@@ -394,6 +403,7 @@ int Reflector::FlushIngest() {
 
 int Reflector::StreamErrors(std::vector<uint32_t>* sessions) {
     if (!fCtx || !sessions) return kBadArgument;
+    std::lock_guard<std::mutex> eg(fEngineMu);
     sessions->clear();
     uint32_t n = 0;
     int err = edgpu_stream_errors(fCtx, nullptr, nullptr, 0, &n);
@@ -407,6 +417,24 @@ int Reflector::StreamErrors(std::vector<uint32_t>* sessions) {
 
 int Reflector::ReflectPackets(int64_t nowMs, OutputSink* sink) {
     if (!fCtx) return kRequestFailed;
+    std::unique_lock<std::mutex> eg(fEngineMu);
+    fTickLock = &eg;
+    const int err = ReflectPacketsLocked(nowMs, sink);
+    fTickLock = nullptr;
+    if (fDelivering) {                                      // the tick is over: waiters may ingest
+        fDelivering = false;
+        fIdleCv.notify_all();
+    }
+    return err;
+}
+
+void Reflector::SetConcurrentDelivery(bool on) {
+    std::unique_lock<std::mutex> eg(fEngineMu);
+    WaitIdle(eg);
+    fConcurrent = on;
+}
+
+int Reflector::ReflectPacketsLocked(int64_t nowMs, OutputSink* sink) {
     fLastErr.clear();
     int err = FlushIngest();
     if (err) return err;
@@ -580,9 +608,14 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     const uint32_t nparts = parts.n;
     const uint32_t* part_q = parts.q;
     const uint32_t* part_r = parts.r;
+    // with concurrent delivery the engine lock is given up while the writes run: the gatherer's
+    // later parts then take it per part, as any other engine call does
+    const bool release = fConcurrent && fTickLock != nullptr;
     auto gather = [&](uint32_t k) -> int {
         const uint32_t r0 = part_r[k], r1 = part_r[k + 1];
         if (r1 <= r0) return kNoErr;
+        std::unique_lock<std::mutex> gl(fEngineMu, std::defer_lock);
+        if (release && k > 0) gl.lock();
         return edgpu_arena_gather(fCtx, &res, tr.reg.data() + r0, r1 - r0, fHostOut + tr.reg_off[r0],
                                   fHostOutCap - tr.reg_off[r0]);
     };
@@ -606,6 +639,12 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         });
     fTick.readback_ms += ms_since(t0);
     t0 = Clock::now();
+    fDelivering = true;                                     // until the tick's end (ReflectPackets)
+    if (release) fTickLock->unlock();
+    struct Relock {                                         // the engine lock back for what follows
+        std::unique_lock<std::mutex>* l;
+        ~Relock() { if (l) l->lock(); }
+    } relock{release ? fTickLock : nullptr};
     if (firstPass) sink->BeginTick(subs, nq);               // every row carries its flags in every pass
     WriteJob job;
     job.subs = subs; job.nsubs = nq;
@@ -657,6 +696,10 @@ static inline uint32_t writer_of(const edgpu_substream_out& q, uint32_t nworkers
 // The writes of the subscribers of one worker, sub-stream by sub-stream in table order (the order
 // one thread takes): a write that would block stops that sub-stream.
 void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers) {
+    struct End {
+        OutputSink* s; uint32_t w;
+        ~End() { s->EndWrites(w); }
+    } end{j.sink, worker};
     WriteJob::Result& r = j.out[worker];
     r.err = kNoErr;
     r.blocked.clear();
@@ -723,6 +766,8 @@ void Reflector::WorkerLoop(uint32_t worker) {
 }
 
 void Reflector::SetWriteThreads(uint32_t n) {
+    std::unique_lock<std::mutex> eg(fEngineMu);
+    WaitIdle(eg);
     n = std::max<uint32_t>(1, std::min<uint32_t>(n, 64));
     if (n == fNumWriters && fWorkers.size() + 1 == n) return;
     {
@@ -794,6 +839,7 @@ bool CKeyFrameCache::SetBuf(char* frameBuf, int len) {
 int CKeyFrameCache::LoadGOP(Reflector& r, uint32_t session, uint32_t track, uint32_t* outPackets) {
     uint64_t n = 0;
     uint32_t k = 0;
+    std::lock_guard<std::mutex> eg(r.EngineMutex());
     const int err = edgpu_gop_copy(r.Context(), session, track, (uint8_t*)_memory, (uint64_t)mem_size, &n, &k);
     if (err) return err;
     curdatalen = (int)n;

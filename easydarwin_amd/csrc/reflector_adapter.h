@@ -27,9 +27,14 @@
 // reserves its slot in the pending batch under a short lock (one of 16 stripes, by session) and
 // copies the packet outside it,
 // and never waits for a tick (the reference takes only the demuxer / stream mutex per packet,
-// ReflectorStream.cpp:529-576, 1769-1875).  Every other call is serialised by the caller (the
-// reference's session-map and per-stream fBucketMutex), and ReflectPackets runs the tick
-// without holding the push lock except for swapping the pending batch.  With
+// ReflectorStream.cpp:529-576, 1769-1875).  Every other call takes the Reflector's engine lock
+// (the edgpu context is one device queue and its host tables), so callers on different threads are
+// serialised here; ReflectPackets holds it for the tick and takes the push lock only to swap the
+// pending batch.  SetConcurrentDelivery(true): the tick gives the engine lock up while its writes
+// run (the QTSS_Write half of a tick, most of its time at fleet scale), so AddOutput, RemoveOutput
+// and session set-up proceed meanwhile -- the reference serialises only per stream (fBucketMutex,
+// ReflectorStream.cpp:1051); PlayRTPInfo and RemoveSession, which ingest what is pending, wait for
+// the tick's writes to end (the batch being written from is the one they would refill).  With
 // SetWriteThreads(n > 1) ReflectPackets delivers a tick's packets from n threads, split by
 // session: all of one subscriber's writes come from one thread, in the order one thread would
 // make them, and a session's subscribers -- the same packet bytes -- share that thread's caches
@@ -105,6 +110,8 @@ public:
                                     const uint8_t* rr, uint32_t len) {
         (void)session; (void)track; (void)addr; (void)port; (void)rr; (void)len;
     }
+    // A write thread has made the last write of a copy pass (on that thread).
+    virtual void EndWrites(uint32_t worker) { (void)worker; }
 };
 
 class Reflector {
@@ -148,6 +155,10 @@ public:
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
     // threads that deliver a tick's writes (default 1; at most 64); call between ticks
     void SetWriteThreads(uint32_t n);
+    // the tick's writes run without the engine lock (see Threading above); default off
+    void SetConcurrentDelivery(bool on);
+    // the engine lock, for code that calls the edgpu ABI on Context() itself (CKeyFrameCache::LoadGOP)
+    std::mutex& EngineMutex() { return fEngineMu; }
     uint32_t WriteThreads() const { return fNumWriters; }
     edgpu_ctx* Context() { return fCtx; }
 
@@ -179,6 +190,16 @@ private:
                      std::vector<edgpu_blocked>* blocked, std::chrono::steady_clock::time_point t0);
     int  fail_with(int code, const std::string& msg) { fLastErr = msg; return code; }
     std::string fLastErr;
+    // the engine lock and the tick's write phase (SetConcurrentDelivery): fTickLock is the ticking
+    // thread's hold of fEngineMu, given up during writes when fConcurrent; fDelivering is true from
+    // a tick's first write to its backpressure report (waiters: fIdleCv on fEngineMu)
+    std::mutex fEngineMu;
+    std::condition_variable fIdleCv;
+    bool fDelivering = false;
+    bool fConcurrent = false;
+    std::unique_lock<std::mutex>* fTickLock = nullptr;
+    void WaitIdle(std::unique_lock<std::mutex>& lk) { fIdleCv.wait(lk, [&] { return !fDelivering; }); }
+    int  ReflectPacketsLocked(int64_t nowMs, OutputSink* sink);
     // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob
     struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint64_t slot; uint32_t len; };
     // The push path is striped by session (session % kStripes): a pusher takes only its stripe's

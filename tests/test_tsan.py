@@ -92,3 +92,19 @@ def test_tsan_manual_ticks(tsan_build, name, tmp_path):
     (tmp_path / "t.edtr").write_bytes(_trace(name).to_bytes())
     _run([replay, module, "t.edtr", "c.edcp"], {"EDGPU_GATHER_SPLIT_BYTES": "0", "EDGPU_QTSS_WRITE_THREADS": "4"},
          tmp_path)
+
+
+@pytest.mark.parametrize("writers", ["1", "4"])
+def test_tsan_rtsp_churn_during_concurrent_writes(tsan_build, writers, tmp_path):
+    """The module's own ticker reflecting a real-time push load while a churn thread SETs UP, PLAYs
+    and TEARs DOWN a player every 5 ms: the tick's writes run without `mu` and without the engine
+    lock (SetConcurrentDelivery), so AddOutput / RemoveOutput meet the write threads, the gather
+    thread and the handle table's readers; a teardown waits only for its own output's write."""
+    replay, module = tsan_build
+    r = _run([replay, module, "--bench", "16", "4", "2.0", "20", "2"],
+             {"EDGPU_BENCH_REALTIME": "1", "EDGPU_QTSS_TICK_MSEC": "5", "EDGPU_GATHER_SPLIT_BYTES": "0",
+              "EDGPU_QTSS_WRITE_THREADS": writers}, tmp_path)
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["relayed_per_s"] > 0
+    assert line["rtsp_ms"]["setup_play"]["n"] > 50 and line["rtsp_ms"]["teardown"]["n"] > 50, line

@@ -119,12 +119,19 @@ struct Obj {
     bool is_client = false, closed = false;
     int64_t to_ms = 120000, deadline = 0;
     int push_s = -1, push_k = -1, player_sub = -1;        // who it is, for the keep-alive log
+    bool churn = false;                                   // --bench realtime: a churn thread's player
     Obj* owner = nullptr;                                 // RTP stream objects: their client session
     // dictionaries with named (instance) attributes: the prefs objects
     std::map<std::string, std::pair<uint32_t, uint32_t>> named;   // name -> (id, data type)
 };
 static std::vector<std::unique_ptr<Obj>> g_objs;
-static Obj* new_obj(uint32_t type) { g_objs.emplace_back(new Obj()); g_objs.back()->type = type; return g_objs.back().get(); }
+static std::mutex g_objs_mu;                          // --bench realtime: the churn thread creates objects
+static Obj* new_obj(uint32_t type) {
+    std::lock_guard<std::mutex> g(g_objs_mu);
+    g_objs.emplace_back(new Obj());
+    g_objs.back()->type = type;
+    return g_objs.back().get();
+}
 
 static void set_attr(Obj* o, uint32_t id, uint32_t idx, const void* p, uint32_t len) {
     auto& v = o->attrs[id];
@@ -183,6 +190,7 @@ extern "C" int rand(void) {
 static std::set<uint32_t> g_roles;
 static std::map<std::string, uint32_t> g_attr_ids;
 static std::vector<Obj*> g_streams;                  // every RTP stream object, creation order
+static std::mutex g_streams_mu;
 
 // ---- callbacks (QTSS_Private.h indices; signatures of the QTSS_Private.cpp stubs) -----------
 static QTSS_Error cb_milliseconds(int64_t* out, ...) { *out = g_now.load(); return QTSS_NoErr; }
@@ -338,7 +346,8 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
         // write threads call this concurrently for different players: per-stream counts)
         thread_local static char scratch[70000];
         memcpy(scratch, ((const QTSS_PacketStruct*)buf)->packetData, std::min<uint32_t>(len, sizeof(scratch)));
-        if (g_realtime && k == 0 && len >= 28 && g_lat_on.load(std::memory_order_relaxed)) {
+        // (a churn player's first writes replay the GOP: packets pushed up to a GOP ago, not latency)
+        if (g_realtime && k == 0 && len >= 28 && g_lat_on.load(std::memory_order_relaxed) && !(o->owner && o->owner->churn)) {
             int64_t stamp;
             memcpy(&stamp, scratch + len - 8, 8);
             const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -349,7 +358,7 @@ static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outL
             h->sum_us += us;
             h->n++;
         }
-        o->npk[k]++;
+        __atomic_add_fetch(&o->npk[k], 1, __ATOMIC_RELAXED);
         if (outLen) *outLen = len;
         return QTSS_NoErr;
     }
@@ -401,6 +410,7 @@ static QTSS_Error cb_add_rtp_stream(Obj* client, Obj* req, Obj** out, uint32_t, 
     auto& v = client->attrs[qtssCliSesStreamObjects];
     const std::string ref((const char*)&s, sizeof(s));
     v.push_back(ref);
+    std::lock_guard<std::mutex> g(g_streams_mu);
     g_streams.push_back(s);
     *out = s;
     return QTSS_NoErr;
@@ -517,8 +527,9 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
 
 static void* g_so = nullptr;
 static uint64_t stream_writes() {                     // --bench: writes so far, over every stream
+    std::lock_guard<std::mutex> g(g_streams_mu);
     uint64_t n = 0;
-    for (const Obj* o : g_streams) n += o->npk[0] + o->npk[1];
+    for (const Obj* o : g_streams) n += __atomic_load_n(&o->npk[0], __ATOMIC_RELAXED) + __atomic_load_n(&o->npk[1], __ATOMIC_RELAXED);
     return n;
 }                         // the module (and, through it, libedgpu)
 
@@ -633,6 +644,51 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                     std::this_thread::sleep_for(std::chrono::microseconds(500));
                 }
             });
+        // EDGPU_BENCH_CHURN (default 1): a thread plays a player's life every 5 ms -- SETUP + PLAY on
+        // a random session, TEARDOWN (ClientSessionClosing) 200 ms later -- and times each RTSP
+        // request's module call: what a viewer waits on while the module reflects C2's load
+        const bool churn = !getenv("EDGPU_BENCH_CHURN") || atoi(getenv("EDGPU_BENCH_CHURN")) != 0;
+        std::vector<double> lat_play, lat_down;
+        std::thread churner;
+        if (churn)
+            churner = std::thread([&]() {
+                struct Live { Obj* client; Clk::time_point born; };
+                std::vector<Live> live;
+                uint64_t rng = 0x2545F4914F6CDD1Dull;
+                auto close_one = [&](const Live& l) {
+                    QTSS_RoleParams cp;
+                    memset(&cp, 0, sizeof(cp));
+                    cp.clientSessionClosingParams.inClientSession = l.client;
+                    const auto a = Clk::now();
+                    (void)g_dispatch(QTSS_ClientSessionClosing_Role, &cp);
+                    if (g_lat_on.load()) lat_down.push_back(std::chrono::duration<double, std::milli>(Clk::now() - a).count());
+                };
+                while (!done.load()) {
+                    rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+                    const uint32_t s = (uint32_t)(rng % nsess);
+                    const std::string path = "/bench" + std::to_string(s) + ".sdp";
+                    Obj* pr = new_obj(qtssRTSPSessionObjectType);
+                    Obj* pc = new_client();
+                    pc->churn = true;
+                    {
+                        std::lock_guard<std::mutex> g(g_objs_mu);
+                        g_rtsp_of_client[pc] = pr;
+                    }
+                    const auto a = Clk::now();
+                    const bool ok = request(pr, pc, qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModePlay,
+                                            qtssRTPTransportTypeUDP) == QTSS_NoErr &&
+                                    request(pr, pc, qtssPlayMethod, path, "", qtssRTPTransportModePlay,
+                                            qtssRTPTransportTypeUDP) == QTSS_NoErr;
+                    if (ok && g_lat_on.load()) lat_play.push_back(std::chrono::duration<double, std::milli>(Clk::now() - a).count());
+                    live.push_back(Live{pc, Clk::now()});
+                    while (!live.empty() && Clk::now() - live.front().born > std::chrono::milliseconds(200)) {
+                        close_one(live.front());
+                        live.erase(live.begin());
+                    }
+                    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+                }
+                for (const Live& l : live) close_one(l);
+            });
         std::this_thread::sleep_for(std::chrono::milliseconds(1000));
         g_lat_on = true;
         const uint64_t w0 = stream_writes();
@@ -643,6 +699,17 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         g_lat_on = false;
         done = true;
         for (auto& t : th) t.join();
+        if (churner.joinable()) churner.join();
+        auto stats = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            char b[160];
+            if (v.empty()) return std::string("{\"n\": 0}");
+            auto q = [&](double f) { return v[std::min(v.size() - 1, (size_t)(f * (double)v.size()))]; };
+            snprintf(b, sizeof(b), "{\"n\": %zu, \"p50\": %.3f, \"p99\": %.3f, \"max\": %.3f}", v.size(), q(0.5), q(0.99),
+                     v.back());
+            return std::string(b);
+        };
+        const std::string rtsp = "{\"setup_play\": " + stats(lat_play) + ", \"teardown\": " + stats(lat_down) + "}";
         LatHist all;
         {
             std::lock_guard<std::mutex> g(g_lat_mu);
@@ -651,6 +718,10 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                 all.sum_us += h->sum_us;
                 all.n += h->n;
             }
+            // the module's write threads are idle now (no pusher, every churn player gone) and
+            // their thread_local pointers are not used again: free the histograms
+            for (LatHist* h : g_lat_all) delete h;
+            g_lat_all.clear();
         }
         auto pct = [&](double q) {
             const uint64_t want = (uint64_t)(q * (double)all.n);
@@ -667,11 +738,11 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                "\"reflect_on_arrival_ms\": %s, \"seconds\": %.3f, \"relayed_per_s\": %.1f, \"ticks\": %llu, "
                "\"failed_ticks\": %llu, \"lock_hold_ms\": {\"mean\": %.3f, \"max\": %.3f}, "
                "\"latency_ms\": {\"packets\": %llu, \"mean\": %.3f, \"p50\": %.2f, "
-               "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}}\n",
+               "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}, \"rtsp_ms\": %s}\n",
                nsess, nsub, nthreads, tm ? tm : "20", ar ? ar : "0", secs, (double)(w1 - w0) / secs,
                (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks,
                ti.ticks ? ti.hold_sum_ms / (double)ti.ticks : 0.0, ti.hold_max_ms, (unsigned long long)all.n,
-               all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12));
+               all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12), rtsp.c_str());
         return 0;
     }
     const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
