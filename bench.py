@@ -35,7 +35,9 @@ from easydarwin_amd.dist import reduce_run  # noqa: E402
 from easydarwin_amd.workload import H264Fleet, owned_sessions  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
-C2_SECONDS = 5                 # stream seconds of the CPU baseline's C2 replay (2.6 GB of packets)
+C2_SECONDS = 5                 # stream seconds of the CPU baseline's C2 trace (2.6 GB of packets) ...
+C2_LOOPS = 4                   # ... replayed back to back on the same sessions: 20 s of stream, of which
+C2_WARM_MS = 10_000            # the window after the reference's 10-s packet age counts (steady state)
 
 
 def log(*a):
@@ -255,6 +257,18 @@ def _parallel_bench(exe: str, mode: str, paths: list[str], target_s: float, extr
             max(o["seconds"] for o in outs), rep)
 
 
+def _parallel_steady(exe: str, paths: list[str], loops: int = C2_LOOPS, warm_ms: int = C2_WARM_MS):
+    """Every shard replayed by its own process at once in the harness's steady-state mode
+    (ref_harness --bench-steady): `loops` back-to-back replays on the same sessions, counted from
+    virtual time warm_ms.  Returns the per-process results, or None."""
+    procs = [subprocess.Popen([exe, "--bench-steady", p, str(loops), str(warm_ms)], stdout=subprocess.PIPE,
+                              stderr=subprocess.DEVNULL, text=True) for p in paths]
+    outs = [pr.communicate()[0] for pr in procs]
+    if any(pr.returncode for pr in procs):
+        return None
+    return [json.loads(o) for o in outs]
+
+
 def _reference_replay(args, tick: int, procs_n: int, mode: str = "--bench"):
     """The cache-resident extra line (round 3's sample): 64 sessions x 3 s at `tick`-ms ticks,
     sharded over procs_n processes: (relayed packets, relayed bytes, longest seconds, repeats)."""
@@ -269,15 +283,52 @@ def _reference_replay(args, tick: int, procs_n: int, mode: str = "--bench"):
         return _parallel_bench(exe, mode, paths, 1.5)
 
 
+def _steady_summary(outs: list[dict]) -> dict:
+    """Aggregate of the processes of one --bench-steady run (all ran at once): the reflect loop's
+    rate is the sum of each process's relayed packets over its own reflect time, the ingest's the
+    sum of its pushes over its PushPacket time."""
+    return {"reflect_per_s": sum(o["relayed_packets"] / max(o["reflect_seconds"], 1e-9) for o in outs),
+            "reflect_GBps": sum(o["relayed_bytes"] / max(o["reflect_seconds"], 1e-9) for o in outs) / 1e9,
+            "ingest_per_s": sum(o["pushed_packets"] / max(o["push_seconds"], 1e-9) for o in outs),
+            "relayed_packets": sum(o["relayed_packets"] for o in outs),
+            "pushed_packets": sum(o["pushed_packets"] for o in outs),
+            "reflect_seconds_max": max(o["reflect_seconds"] for o in outs),
+            "push_seconds_max": max(o["push_seconds"] for o in outs),
+            "both_per_s": sum(o["relayed_packets"] / max(o["reflect_seconds"] + o["push_seconds"], 1e-9) for o in outs)}
+
+
+def c2_reference_steady(sessions: int, subs: int, tick_ms: int, procs_n: int) -> dict | None:
+    """EasyDarwin's reflector (ref_harness --bench-steady) on the C2 fleet at `tick_ms` ticks, in its
+    steady state, sessions sharded over procs_n processes running at once (also tools/bench_module.py's
+    reference)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory(dir=os.environ.get("EDGPU_BASELINE_TMP")) as td:
+        t0 = time.time()
+        paths = _fleet_shards(sessions, subs, C2_SECONDS * 1000, tick_ms, procs_n, td)
+        gen_s = time.time() - t0
+        trace_gb = sum(os.path.getsize(p) for p in paths) / 1e9
+        outs = _parallel_steady(exe, paths)
+    if outs is None:
+        return None
+    d = _steady_summary(outs)
+    d.update(gen_s=gen_s, trace_gb=trace_gb, procs=procs_n, tick_ms=tick_ms)
+    return d
+
+
 def cpu_baseline_reference(args) -> dict | None:
-    """The REFERENCE reflector itself (oracle/_ref/ref_harness --bench: EasyDarwin's
-    ReflectorStream / ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS
-    server, memcpy sinks) on the bench's own C2 workload: all args.sessions sessions x args.subs
-    UDP players for C2_SECONDS of stream at 100-ms ticks (the reflector's own wakeup scale,
-    RS.cpp:1125-1131), sessions sharded over one process per leased core, all running at once;
-    value = relayed packets / the longest process's replay time.  Extra lines: the same at the GPU
-    step's 1000-ms tick, with a real sendto() per subscriber packet, and round 3's cache-resident
-    64-session sample."""
+    """The REFERENCE reflector itself (oracle/_ref/ref_harness: EasyDarwin's ReflectorStream /
+    ReflectorSender / RTPSessionOutput compiled from its sources, fake QTSS server, memcpy sinks) on
+    the bench's own C2 workload -- all args.sessions sessions x args.subs UDP players, sessions sharded
+    over one process per leased core, all running at once -- in its STEADY STATE (--bench-steady): the
+    C2_SECONDS-s trace replayed C2_LOOPS times back to back on the same sessions and players, only
+    what happens after C2_WARM_MS counted (the reference's queues have reached their 10-s packet age,
+    ReflectorStream.cpp:112-114, and recycle packets through each socket's free queue, :1713,
+    2039-2047), at 100-ms ticks (the reflector's own wakeup scale, RS.cpp:1125-1131).  value = the
+    reflect loop's rate (ReflectPackets alone); the ingest (PushPacket) is timed apart
+    and reported beside it.  Extra lines: the same at the GPU step's 1000-ms tick, a real sendto() per
+    subscriber packet, and the clean-room restatement."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(exe):
         return None
@@ -288,28 +339,32 @@ def cpu_baseline_reference(args) -> dict | None:
         paths = _fleet_shards(args.sessions, args.subs, dur, 100, procs_n, td)
         gen_s = time.time() - t0
         trace_gb = sum(os.path.getsize(p) for p in paths) / 1e9
-        r100 = _parallel_bench(exe, "--bench", paths, 5.0)
+        s100 = _parallel_steady(exe, paths)
         rudp = _parallel_bench(exe, "--bench-udp", paths, 3.0)
         port = os.path.join(ROOT, "oracle", "relay_model")
         rport = _parallel_bench(port, "--bench", paths, 5.0, extra=("1",)) if os.path.exists(port) else None
         for p in paths:
             os.remove(p)
         paths1 = _fleet_shards(args.sessions, args.subs, dur, 1000, procs_n, td)
-        r1000 = _parallel_bench(exe, "--bench", paths1, 5.0)
-    if r100 is None:
+        s1000 = _parallel_steady(exe, paths1)
+    if s100 is None:
         return None
-    pk, by, secs, rep = r100
-    out = {"value": round(pk / secs, 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
-           "cpu_model": cpu_model(), "cores_note": why, "GBps": round(by / secs / 1e9, 3), "tick_ms": 100,
-           "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench, compiled from the reference "
+    d = _steady_summary(s100)
+    out = {"value": round(d["reflect_per_s"], 1), "unit": "relayed RTP packets/s", "cores": procs_n, "kind": "reference",
+           "cpu_model": cpu_model(), "cores_note": why, "GBps": round(d["reflect_GBps"], 3), "tick_ms": 100,
+           "ingest_per_s": round(d["ingest_per_s"], 1), "with_ingest_per_s": round(d["both_per_s"], 1),
+           "sample": f"EasyDarwin's reflector (oracle/_ref/ref_harness --bench-steady, compiled from the reference "
                      f"sources) on the bench's C2 workload itself: {args.sessions} H.264 1080p 4 Mb/s sessions x "
-                     f"{args.subs} UDP subs x {C2_SECONDS} s of stream ({trace_gb:.2f} GB of trace, generated in "
-                     f"{gen_s:.0f} s) at 100-ms ticks, sessions sharded over {procs_n} processes, each replaying its "
-                     f"shard {rep} times; {pk} relayed packets, longest process {secs:.2f} s (memcpy sinks)"}
-    if r1000 is not None:
-        pk1, by1, secs1, rep1 = r1000
-        out["tick_1000ms"] = {"value": round(pk1 / secs1, 1), "GBps": round(by1 / secs1 / 1e9, 3),
-                              "relayed_packets": pk1, "seconds": round(secs1, 3), "repeat": rep1}
+                     f"{args.subs} UDP subs, a {C2_SECONDS}-s trace ({trace_gb:.2f} GB, generated in {gen_s:.0f} s) "
+                     f"replayed {C2_LOOPS} times back to back on the same sessions at 100-ms ticks, counted after "
+                     f"{C2_WARM_MS // 1000} s of stream (steady state: packets recycled through each socket's free "
+                     f"queue), sessions sharded over {procs_n} processes at once; value = ReflectPackets alone "
+                     f"({d['relayed_packets']} relayed packets), PushPacket timed apart (ingest_per_s; "
+                     f"with_ingest_per_s: both) (memcpy sinks)"}
+    if s1000 is not None:
+        d1 = _steady_summary(s1000)
+        out["tick_1000ms"] = {"value": round(d1["reflect_per_s"], 1), "GBps": round(d1["reflect_GBps"], 3),
+                              "ingest_per_s": round(d1["ingest_per_s"], 1), "relayed_packets": d1["relayed_packets"]}
     if rudp is not None:            # the full write path: one sendto() per subscriber packet
         pku, byu, secsu, repu = rudp
         out["with_udp_sockets"] = {"value": round(pku / secsu, 1), "unit": "datagrams/s",
@@ -321,11 +376,6 @@ def cpu_baseline_reference(args) -> dict | None:
         out["restatement"] = {"value": round(pkp / secsp, 1), "cores": procs_n, "kind": "port",
                               "sample": f"oracle/relay_model --bench, one thread per process, the same shards, "
                                         f"{repp} replays each"}
-    small = _reference_replay(args, 100, procs_n)
-    if small is not None:          # round 3's line: a 64-session sample that stays in cache
-        pks, bys, secss, reps = small
-        out["cache_resident_64_sessions"] = {"value": round(pks / secss, 1), "relayed_packets": pks,
-                                             "seconds": round(secss, 3), "repeat": reps, "tick_ms": 100}
     return out
 
 
@@ -615,6 +665,10 @@ def main():
                       "tick_plan_plus_fanout": round(float(np.mean(k_tick)), 4) if k_tick else None,
                       "ingest": round(float(np.mean(k_ing)), 4) if k_ing else None,
                       "keyframe_index": round(float(np.mean(k_key)), 4) if k_key else None},
+        # the fan-out alone (plan + copy: the reflect loop), like-for-like with cpu_baseline.value,
+        # which times the reference's ReflectPackets apart from its PushPacket
+        "reflect_loop": ({"relayed_per_s": round(relayed / max(launches, 1) / (float(np.mean(k_tick)) / 1e3), 1),
+                          "timing": "tick_plan_plus_fanout kernel time per step"} if k_tick else None),
         "timing_events": ("every kernel's, inside the timed steps" if args.all_timing_events else
                           f"the fan-out copy kernel's pair inside the timed steps; ingest, keyframe and plan "
                           f"from {extra} steps after them"),

@@ -109,6 +109,34 @@ QTSSModule** QTSServerInterface::sModuleArray[QTSSModule::kNumRoles];
 UInt32       QTSServerInterface::sNumModulesInRole[QTSSModule::kNumRoles];
 
 // ---------------------------------------------------------------------------------------
+// A ReflectorSocket's own free-packet queue (private; reached by explicit instantiation, which
+// the language exempts from access checks, as oracle/ref_module_host.cpp reaches the session
+// map): ReflectorSocket::Run hands it to ReflectPackets (ReflectorStream.cpp:1713), so the
+// packets RemoveOldPackets frees go back to the socket and GetPacket reuses them (:2039-2047).
+namespace {
+template <typename Tag, typename Tag::type M> struct Steal { friend typename Tag::type get(Tag) { return M; } };
+struct FreeQueueMember { typedef OSQueue ReflectorSocket::*type; friend type get(FreeQueueMember); };
+template struct Steal<FreeQueueMember, &ReflectorSocket::fFreeQueue>;
+}
+// ReflectorSocket::Run's reflect step for one stream: each sender under its socket's demuxer
+// mutex, with that socket's free queue (ReflectorStream.cpp:1687, 1709-1714)
+static void reflect_stream(ReflectorStream* st) {
+    UDPSocketPair* pr = st->GetSocketPair();
+    ReflectorSocket* a = (ReflectorSocket*)pr->GetSocketA();
+    ReflectorSocket* b = (ReflectorSocket*)pr->GetSocketB();
+    SInt64 wake = 0;
+    {
+        OSMutexLocker l(a->GetDemuxer()->GetMutex());
+        st->GetRTPSender()->ReflectPackets(&wake, &(a->*get(FreeQueueMember())));
+    }
+    wake = 0;
+    {
+        OSMutexLocker l(b->GetDemuxer()->GetMutex());
+        st->GetRTCPSender()->ReflectPackets(&wake, &(b->*get(FreeQueueMember())));
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Virtual clock.
 static SInt64 g_now = 0;
 extern "C" SInt64 __wrap__ZN2OS12MillisecondsEv() { return g_now; }
@@ -365,6 +393,9 @@ static QTSS_Error cb_set_value(void* obj, UInt32 id, UInt32 idx, const void* buf
 // Bench mode (--bench): the sink is a memcpy into a scratch buffer (no capture), counted.
 static bool g_bench = false;
 static UInt64 g_bench_pkts = 0, g_bench_bytes = 0;
+// --bench-steady: the reflect loop's own time (TICKs) apart from the ingest's (PKTs)
+static double g_reflect_s = 0, g_push_s = 0;
+static UInt64 g_ticks = 0, g_pushed = 0;
 static char g_scratch[70000];
 static int g_udp_fd = -1;                      // --bench-udp: the subscribers' UDP socket
 static sockaddr_in g_udp_dst;                  // an unread loopback socket (drops when full)
@@ -487,6 +518,22 @@ struct Live {
 
 int main(int argc, char** argv) {
     int reps = 1;
+    // --bench-steady <trace> <loops> <warm_ms>: the trace's packets and ticks replayed `loops` times
+    // back to back on the same sessions and players, the clock running on (loop k at k x the last
+    // TICK's time), so the queues reach the reference's steady state -- packets older than
+    // sMaxPacketAgeMSec freed to their socket's queue and reused (RemoveOldPackets,
+    // ReflectorStream.cpp:1233-1289; GetPacket :2039-2047) -- and only what happens at or after
+    // virtual time warm_ms is counted: relayed packets, the TICKs' reflect time and, apart from it,
+    // the PKTs' PushPacket time (the steady-state reflect loop, ingest timed separately).
+    int steady_loops = 0;
+    SInt64 steady_warm = 0;
+    if (argc == 5 && strcmp(argv[1], "--bench-steady") == 0) {
+        steady_loops = atoi(argv[3]);
+        steady_warm = atoll(argv[4]);
+        if (steady_loops < 1) return 2;
+        argv[1] = (char*)"--bench";
+        argc = 3;
+    }
     const bool udp = argc >= 3 && strcmp(argv[1], "--bench-udp") == 0;
     if (argc >= 3 && (strcmp(argv[1], "--bench") == 0 || udp)) {
         g_bench = true;
@@ -586,6 +633,7 @@ int main(int argc, char** argv) {
     const size_t p0 = r.p;
     std::vector<Sub> subs;
     double bench_secs = 0;
+    UInt64 pkts_at_warm = 0, bytes_at_warm = 0;        // --bench-steady: the counters when the window began
     for (int rep = 0; rep < reps; rep++) {
     r.p = p0;
     g_now = 0;
@@ -725,10 +773,28 @@ int main(int argc, char** argv) {
 
     std::vector<char> pktbuf(70000);
     const auto t_start = std::chrono::steady_clock::now();
+    const size_t ev0 = r.p;
+    SInt64 loop_dur = 0, loop_off = 0;                 // --bench-steady: the trace's span, this loop's offset
+    bool warm = steady_loops == 0;
+    for (int loop = 0; loop < std::max(1, steady_loops); loop++) {
+    r.p = ev0;
+    loop_off = (SInt64)loop * loop_dur;
     while (!r.done()) {
         UInt8 type = r.get<UInt8>();
         if (type == 0) break;
-        SInt64 t = r.get<SInt64>();
+        SInt64 t = r.get<SInt64>() + loop_off;
+        if (steady_loops) {
+            if (loop == 0 && type == 3) loop_dur = std::max(loop_dur, t);
+            if (!warm && t >= steady_warm) {
+                warm = true;
+                pkts_at_warm = g_bench_pkts; bytes_at_warm = g_bench_bytes;
+                g_reflect_s = g_push_s = 0; g_ticks = g_pushed = 0;
+            }
+            if (type != 1 && type != 2 && type != 3) {
+                fprintf(stderr, "--bench-steady takes PKT / JOIN / TICK traces only\n");
+                return 2;
+            }
+        }
         // pushers whose deadline the clock reached time out first, earliest first, at their deadline
         for (;;) {
             SInt64 best = INT64_MAX;
@@ -752,13 +818,20 @@ int main(int argc, char** argv) {
             ReflectorSession* sess = live[s].sess;
             if (live[s].bcast->deadline) live[s].bcast->deadline = g_now + live[s].bcast->to_ms;   // RTSPSession.cpp:2157
             UInt32 idx = ch / 2;
-            if (idx < sess->GetNumStreams())
+            if (idx < sess->GetNumStreams()) {
+                const auto a = g_bench ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
                 sess->GetStreamByIndex(idx)->PushPacket(pktbuf.data(), len, (ch & 1) != 0);
+                if (g_bench) {
+                    g_push_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+                    g_pushed++;
+                }
+            }
         } else if (type == 2) {     // JOIN
             UInt32 s = r.get<UInt32>();
             UInt32 sub_id = r.get<UInt32>();
             UInt8 transport = r.get<UInt8>();
             UInt8 uaflags = r.get<UInt8>();
+            if (steady_loops && loop > 0) continue;       // the players joined once, in the first loop
             ReflectorSession* sess = live[s].sess;
             if (sess == nullptr) continue;                // no such session: the player's SETUP fails
             // RTP-Info player (ua_flags bit 0: the kRequiresRTPInfoSeqAndTime profile, UA
@@ -830,23 +903,19 @@ int main(int argc, char** argv) {
             set_value(sb.client, qtssCliSesState, 0, &playing, sizeof(playing));
             subs.push_back(sb);
         } else if (type == 3) {     // TICK
+            const auto a = std::chrono::steady_clock::now();
+            const UInt64 before = g_bench_pkts;
             for (UInt32 s = 0; s < nsess; s++) {
                 ReflectorSession* sess = live[s].sess;
                 if (sess == nullptr) continue;
-                for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
-                    ReflectorStream* st = sess->GetStreamByIndex(x);
-                    OSQueue* freeA = NULL;
-                    // The socket's free queue is private; ReflectPackets only EnQueues
-                    // freed packets onto it, so a harness-owned queue is equivalent.
-                    static OSQueue sFree;
-                    freeA = &sFree;
-                    SInt64 wake = 0;
-                    st->GetRTPSender()->ReflectPackets(&wake, freeA);
-                    wake = 0;
-                    st->GetRTCPSender()->ReflectPackets(&wake, freeA);
-                }
+                for (UInt32 x = 0; x < sess->GetNumStreams(); x++) reflect_stream(sess->GetStreamByIndex(x));
             }
-            for (auto& o : g_objs) o->budget[0] = o->budget[1] = -1;
+            if (g_bench) {
+                g_reflect_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+                g_ticks++;
+                (void)before;
+            }
+            if (!g_bench) for (auto& o : g_objs) o->budget[0] = o->budget[1] = -1;
         } else if (type == 5) {     // UPKT: a datagram read by ReflectorSocket::GetIncomingData
             UInt32 s = r.get<UInt32>();
             UInt8 ch = r.get<UInt8>();
@@ -920,10 +989,19 @@ int main(int argc, char** argv) {
         }
     }
 
+    }   // steady loop
     bench_secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     }   // rep
     if (g_ka_log) fclose(g_ka_log);
 
+    if (steady_loops) {             // the counted window only
+        printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"reflect_seconds\": %.6f, \"push_seconds\": %.6f, "
+               "\"pushed_packets\": %llu, \"ticks\": %llu, \"window_ms\": [%lld, %lld], \"loops\": %d}\n",
+               (unsigned long long)(g_bench_pkts - pkts_at_warm), (unsigned long long)(g_bench_bytes - bytes_at_warm),
+               g_reflect_s, g_push_s, (unsigned long long)g_pushed, (unsigned long long)g_ticks, (long long)steady_warm,
+               (long long)g_now, steady_loops);
+        return 0;
+    }
     if (g_bench) {                  // the replays only: PushPacket + ReflectPackets + joins
         printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"repeat\": %d}\n",
                (unsigned long long)g_bench_pkts, (unsigned long long)g_bench_bytes, bench_secs, reps);

@@ -67,6 +67,11 @@ struct SessionMapMember { typedef OSRefTable* QTSServerInterface::*type; friend 
 template struct Steal<SessionMapMember, &QTSServerInterface::fReflectorSessionMap>;
 struct ServerStatic { typedef QTSServerInterface** type; friend type get(ServerStatic); };
 template struct Steal<ServerStatic, &QTSServerInterface::sServer>;
+// each ReflectorSocket's own free-packet queue, which ReflectorSocket::Run hands to ReflectPackets
+// (ReflectorStream.cpp:1713): the packets RemoveOldPackets frees go back to the socket that GetPacket
+// takes them from (:2039-2047), so a long run recycles them as the server does
+struct FreeQueueMember { typedef OSQueue ReflectorSocket::*type; friend type get(FreeQueueMember); };
+template struct Steal<FreeQueueMember, &ReflectorSocket::fFreeQueue>;
 
 alignas(QTSServerInterface) unsigned char g_server[sizeof(QTSServerInterface)];
 OSRefTable* g_sessions = NULL;
@@ -158,20 +163,27 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
     OSMutexLocker locker(session_map()->GetMutex());
     // EDGPU_REF_TICK_THREADS=N (default 1): the sessions' senders reflect on N threads, as the
     // server's task threads run the ReflectorSocket tasks (one socket's senders on one thread at a
-    // time, ReflectorStream.cpp:1676-1714); each thread frees packets onto its own queue
+    // time, under its demuxer mutex, with its free queue: ReflectorStream.cpp:1676-1714)
     static const unsigned nthreads = getenv("EDGPU_REF_TICK_THREADS") ? (unsigned)atoi(getenv("EDGPU_REF_TICK_THREADS")) : 1;
-    static std::vector<OSQueue> sFree(std::max(1u, nthreads));   // ReflectPackets only EnQueues onto it
     const std::vector<ReflectorSession*> sessions = live_sessions();
     auto reflect = [&](unsigned w, unsigned nw) {
         for (size_t k = w; k < sessions.size(); k += nw) {
             ReflectorSession* sess = sessions[k];
             for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
                 ReflectorStream* st = sess->GetStreamByIndex(x);
-                if (st == NULL) continue;
+                if (st == NULL || st->GetSocketPair() == NULL) continue;
+                ReflectorSocket* a = (ReflectorSocket*)st->GetSocketPair()->GetSocketA();
+                ReflectorSocket* b = (ReflectorSocket*)st->GetSocketPair()->GetSocketB();
                 SInt64 wake = 0;
-                st->GetRTPSender()->ReflectPackets(&wake, &sFree[w]);
+                {
+                    OSMutexLocker l(a->GetDemuxer()->GetMutex());
+                    st->GetRTPSender()->ReflectPackets(&wake, &(a->*get(FreeQueueMember())));
+                }
                 wake = 0;
-                st->GetRTCPSender()->ReflectPackets(&wake, &sFree[w]);
+                {
+                    OSMutexLocker l(b->GetDemuxer()->GetMutex());
+                    st->GetRTCPSender()->ReflectPackets(&wake, &(b->*get(FreeQueueMember())));
+                }
             }
         }
     };

@@ -13,9 +13,14 @@ Reference module: the REFERENCE QTSSReflectorModule (oracle/_ref/libQTSSReflecto
 the same fake server at the same load and tick, its senders reflected on as many threads as the
 drop-in has write threads -- the like-for-like comparison (module_vs_reference_module).
 
-Reference side: oracle/_ref/ref_harness --bench (EasyDarwin's reflector compiled from its
-sources, memcpy sinks) on bench.py's bounded sample (64 sessions x <subs> x 3 s at the same
-tick), sessions sharded over one process per core (bench.py _reference_replay).
+Both modules run <seconds> (default 15) of stream and are timed only after <warm-ms> (default
+10 s: the reference's queues reach their 10-s packet age and recycle packets through each
+socket's free queue, ReflectorStream.cpp:112-114, 1713, 2039-2047).
+
+Reference side: oracle/_ref/ref_harness --bench-steady (EasyDarwin's reflector compiled from its
+sources, memcpy sinks) on the same C2 fleet -- all <sessions> x <subs> -- at the same tick, in its
+steady state, sessions sharded over one process per core (bench.py c2_reference_steady); compared
+on push + reflect (with_ingest_per_s), as the module's rate counts both.
 
 Prints one JSON object.  Needs a GPU (the module initialises an edgpu context).
 """
@@ -29,7 +34,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def module_run(args) -> dict:
-    env = dict(os.environ)
+    env = dict(os.environ, EDGPU_BENCH_WARM_MS=str(args.warm_ms))
     # one tick carries every session's IDR at once (all GOPs start together): 1024 x 16 x ~150 KB
     env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
     env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
@@ -72,7 +77,8 @@ def reference_module_run(args) -> dict | None:
     so = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
     if not os.path.exists(so):
         return None
-    env = dict(os.environ, EDGPU_REF_TICK_THREADS=str(int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads))))
+    env = dict(os.environ, EDGPU_REF_TICK_THREADS=str(int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads))),
+               EDGPU_BENCH_WARM_MS=str(args.warm_ms))
     if args.concurrent_push:
         env["EDGPU_BENCH_CONCURRENT_PUSH"] = "1"
     cmd = [os.path.join(ROOT, "tools", "qtss_replay"), so, "--bench", str(args.sessions), str(args.subs),
@@ -89,21 +95,25 @@ def reference_module_run(args) -> dict | None:
 def reference_run(args) -> dict | None:
     sys.path.insert(0, ROOT)
     import bench
-    procs_n = min(16, os.cpu_count() or 1)
-    r = bench._reference_replay(argparse.Namespace(subs=args.subs), args.tick_ms, procs_n)
-    if r is None:
+    procs_n, why = bench.baseline_cores()
+    d = bench.c2_reference_steady(args.sessions, args.subs, args.tick_ms, procs_n)
+    if d is None:
         return None
-    pk, by, secs, rep = r
-    return {"relayed_per_s": round(pk / secs, 1), "cores": procs_n, "relayed_packets": pk, "seconds": round(secs, 3),
-            "sample": f"oracle/_ref/ref_harness --bench: 64 sessions x {args.subs} UDP subs x 3 s at {args.tick_ms}-ms "
-                      f"ticks, sharded over {procs_n} processes, {rep} replays each (memcpy sinks)"}
+    return {"relayed_per_s": round(d["both_per_s"], 1), "reflect_per_s": round(d["reflect_per_s"], 1),
+            "ingest_per_s": round(d["ingest_per_s"], 1), "cores": procs_n, "cores_note": why,
+            "relayed_packets": d["relayed_packets"],
+            "sample": f"oracle/_ref/ref_harness --bench-steady: the C2 fleet, {args.sessions} sessions x {args.subs} UDP "
+                      f"subs, a {bench.C2_SECONDS}-s trace replayed {bench.C2_LOOPS} times at {args.tick_ms}-ms ticks, "
+                      f"counted after {bench.C2_WARM_MS // 1000} s, sharded over {procs_n} processes at once "
+                      f"(memcpy sinks); relayed_per_s counts push + reflect time, as the module's does"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sessions", type=int, default=1024)
     ap.add_argument("--subs", type=int, default=16)
-    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--seconds", type=float, default=15.0)
+    ap.add_argument("--warm-ms", type=int, default=10_000)
     ap.add_argument("--tick-ms", type=int, default=100)
     ap.add_argument("--threads", type=int, default=8)
     # QTSS_Write threads: the box's CPU share is 16 (the reference baseline runs 16 processes)

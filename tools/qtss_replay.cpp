@@ -537,6 +537,7 @@ static uint64_t stream_writes() {                     // --bench: writes so far,
 struct Pusher {                                        // one synthetic H.264 push (one track)
     uint32_t seq = 0, ts = 0, ssrc = 0, frame = 0;
 };
+static std::atomic<uint64_t> g_pushed{0};             // --bench: RTSPIncomingData calls made
 static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
                      QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
     (void)poll_fn;
@@ -604,6 +605,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             rp.rtspIncomingDataParams.inPacketData = fr.data();
             rp.rtspIncomingDataParams.inPacketLen = len + 4;
             (void)g_dispatch(QTSS_RTSPIncomingData_Role, &rp);
+            g_pushed.fetch_add(1, std::memory_order_relaxed);
         };
         auto nal = [&](uint8_t h, uint32_t n, bool last) {     // single NAL or FU-A fragments
             if (12 + n <= mtu) { one(&h, 1, n - 1, last); return; }
@@ -748,7 +750,11 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
     const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
     double push_s = 0, tick_s = 0, wall_s = 0, hold = 0, hold_max = 0, gpu = 0, rb = 0, wr = 0, ing = 0;
     uint64_t rb_bytes = 0, arena = 0, ingested = 0, writes0 = 0, timed_ticks = 0, prestaged = 0, ingested_b = 0;
-    const uint32_t warm = std::min<uint32_t>(3, nticks / 4);
+    // EDGPU_BENCH_WARM_MS=<ms>: the ticks before that much stream time are not timed (the reference's
+    // queues reach their steady state after the 10-s packet age, ReflectorStream.cpp:112-114);
+    // default: the first min(3, ticks / 4)
+    uint32_t warm = std::min<uint32_t>(3, nticks / 4);
+    if (const char* v = getenv("EDGPU_BENCH_WARM_MS")) warm = std::min<uint32_t>((uint32_t)(atoll(v) / tick_ms), nticks - 1);
     // EDGPU_BENCH_CONCURRENT_PUSH=1: the pushers push the next tick's packets while a tick runs
     // (as a server's RTSP threads do; the push path never waits on a tick); default: pushing and
     // ticking alternate.  Either way a tick relays what was pushed before it started.
@@ -764,8 +770,10 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         for (auto& t : th) t.join();
     };
     if (concurrent) push_until(tick_ms);
+    uint64_t pushed = 0;                                  // pushes in the timed window
     for (uint32_t k = 0; k < nticks; k++) {
         const int64_t t_end = (int64_t)(k + 1) * tick_ms;
+        const uint64_t p0 = g_pushed.load();
         auto a = std::chrono::steady_clock::now();
         if (!concurrent) push_until(t_end);
         advance_clock(t_end);
@@ -792,6 +800,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         EDGPU_QTSSTickInfo ti;
         if (last_fn(&ti)) return 3;
         if (k == warm) writes0 = stream_writes();
+        if (k >= warm) pushed += g_pushed.load() - p0;
         if (k >= warm) {
             timed_ticks++;
             wall_s += std::chrono::duration<double>(d - a).count();
@@ -811,12 +820,13 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
            "\"relayed_per_s\": %.1f, \"ingested_per_s\": %.1f, \"per_tick_ms\": {\"hold\": %.3f, \"hold_max\": %.3f, "
            "\"ingest\": %.3f, \"gpu_fanout\": %.3f, \"readback\": %.3f, \"writes\": %.3f}, "
            "\"per_tick_bytes\": {\"readback\": %.0f, \"arena\": %.0f, \"ingested\": %.0f, \"prestaged\": %.0f}, "
-           "\"virtual_s\": %.3f}\n",
+           "\"virtual_s\": %.3f, \"warm_ticks\": %u, \"push_us_per_packet\": %.4f}\n",
            nsess, nsub, tick_ms, nthreads, wt ? wt : "4", (unsigned long long)timed_ticks,
            concurrent ? "concurrent with the ticks" : "alternating with the ticks", setup_s, (unsigned long long)relayed,
            (unsigned long long)ingested, push_s, tick_s, wall_s, relayed / std::max(wall_s, 1e-9),
            ingested / std::max(wall_s, 1e-9), hold / n, hold_max, ing / n, gpu / n, rb / n, wr / n,
-           rb_bytes / n, arena / n, ingested_b / n, prestaged / n, timed_ticks * tick_ms / 1000.0);
+           rb_bytes / n, arena / n, ingested_b / n, prestaged / n, timed_ticks * tick_ms / 1000.0, warm,
+           pushed ? push_s * 1e6 / (double)pushed : 0.0);
     return 0;
 }
 
