@@ -220,6 +220,8 @@ def _fleet_shards(n_sess: int, subs: int, dur_ms: int, tick_ms: int, nshards: in
             for k in range(nshards):
                 sel = order[(sess[order] % nshards) == k]
                 n = len(sel)
+                if n == 0:                            # (short ticks: a shard may push nothing in one)
+                    continue
                 hdr = np.zeros(n, dtype=rec)
                 hdr["type"] = 1
                 hdr["t"] = prev["arrival"][sel]

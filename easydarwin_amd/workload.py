@@ -86,7 +86,9 @@ class H264Fleet:
         ``fu`` (n x 2: bytes 16-17 of the slot = FU indicator/header or NAL header + 1 byte),
         ``slot_bytes`` (n), ``t_end`` (tick time)."""
         f0 = self.frame
-        nf = self.tick_ms * FPS // 1000
+        # the frames due by the end of this tick (a tick shorter than a frame interval may carry none)
+        self.t_ms = getattr(self, "t_ms", 0) + self.tick_ms
+        nf = self.t_ms * FPS // 1000 - f0
         self.frame += nf
         n = self.n
         fidx = f0 + np.arange(nf)                                    # frames of this tick
