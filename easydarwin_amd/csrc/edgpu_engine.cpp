@@ -550,14 +550,71 @@ static void note_grow(edgpu_ctx* x, const TickTotals& t) {
     if (t.grow_count) x->grow_pending = std::min<uint32_t>(t.grow_count, kMaxGrow);
 }
 
-// Ring growth (edgpu_config.ring_growth), at a tick boundary -- before an ingest, nothing in
-// flight: every sender the last plan found holding more than half of a ring's capacity of what the
-// reference would retain gets that ring replaced by one of the requested power-of-two size, its
-// entries moved to their places under the new mask (the rings are addressed by monotonic index /
-// virtual byte, so an entry's new place is its index & new mask).  The sender's floor becomes the
-// tail the plan measured: entries older than it were already lost and must not look intact in
-// the larger ring.  A request made before the sender's head moved on (a replica's image apply in
-// between) is dropped; the next plan makes it again.
+// One sender's rings replaced by ones of (at least) `want_pk` packets / `want_by` bytes, powers of
+// two within the configured bounds; its entries move to their places under the new masks (the rings
+// are addressed by monotonic index / virtual byte, so an entry's new place is its index & new mask).
+// The sender's floor becomes `tail`, the oldest entry intact in the old rings: older ones were lost
+// already and must not look intact in the larger rings.  Nothing may be in flight (the caller synced).
+static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t want_by, uint64_t tail,
+                       const uint64_t* expect_head, bool* grown) {
+    *grown = false;
+    if (sender >= x->nsenders || !x->snd_meta[sender]) return EDGPU_OK;
+    SenderDev D;
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&D, x->d_senders.ptr + sender, sizeof(D)));
+        HIP_CHECK(rb.run());
+    }
+    if ((expect_head && D.head != *expect_head) || D.meta != (uint64_t)(uintptr_t)x->snd_meta[sender]) return EDGPU_OK;
+    const uint64_t old_pk = (uint64_t)D.pk_mask + 1, old_by = ((uint64_t)D.word_mask + 1) * 16;
+    auto pow2_at_least = [](uint64_t v) { uint64_t p = 1; while (p < v) p <<= 1; return p; };
+    const uint64_t new_pk = std::min<uint64_t>(std::max(old_pk, pow2_at_least(want_pk)), x->cfg.max_ring_packets);
+    const uint64_t new_by = std::min<uint64_t>(std::max(old_by, pow2_at_least(want_by)), x->cfg.max_ring_bytes);
+    if (new_pk <= old_pk && new_by <= old_by) return EDGPU_OK;
+    void* meta = x->snd_meta[sender];
+    void* ring = x->snd_ring[sender];
+    void* nmeta = meta;
+    void* nring = ring;
+    if (new_pk > old_pk) {
+        if (dmalloc(&nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess)
+            return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender meta ring");
+        const uint64_t lo = D.head > old_pk ? D.head - old_pk : 0;
+        HIP_CHECK(launch_ring_move(0, meta, old_pk - 1, nmeta, new_pk - 1, lo, D.head - lo, x->stream));
+        HIP_CHECK(launch_ring_move(1, (const uint8_t*)meta + old_pk * sizeof(PktMeta), old_pk - 1,
+                                   (uint8_t*)nmeta + new_pk * sizeof(PktMeta), new_pk - 1, lo, D.head - lo, x->stream));
+    }
+    if (new_by > old_by) {
+        if (dmalloc(&nring, new_by) != hipSuccess) {
+            if (nmeta != meta) (void)hipFree(nmeta);
+            return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender byte ring");
+        }
+        const uint64_t wend = D.vbyte_end / 16, wlo = wend > old_by / 16 ? wend - old_by / 16 : 0;
+        HIP_CHECK(launch_ring_move(2, ring, old_by / 16 - 1, nring, new_by / 16 - 1, wlo, wend - wlo, x->stream));
+    }
+    D.meta = (uint64_t)(uintptr_t)nmeta;
+    D.ring = (uint64_t)(uintptr_t)nring;
+    D.pk_mask = (uint32_t)(new_pk - 1);
+    D.word_mask = (uint32_t)(new_by / 16 - 1);
+    D.floor = std::max(D.floor, tail);
+    HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sender, &D, sizeof(D), hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(hipStreamSynchronize(x->stream));
+    if (nmeta != meta) HIP_CHECK(hipFree(meta));
+    if (nring != ring) HIP_CHECK(hipFree(ring));
+    x->snd_meta[sender] = nmeta;
+    x->snd_ring[sender] = nring;
+    x->work_cap_needed += new_pk / 16 - old_pk / 16;
+    x->ring_bytes += (new_pk - old_pk) * (sizeof(PktMeta) + sizeof(uint32_t)) + (new_by - old_by);
+    x->ring_grows++;
+    x->index_dirty = true;                      // the work list is sized from the rings
+    *grown = true;
+    return EDGPU_OK;
+}
+
+// Ring growth (edgpu_config.ring_growth), at a tick boundary -- before an ingest or an image import,
+// nothing in flight: every sender the last plan found holding more than half of a ring's capacity
+// of what the reference would retain gets that ring grown to the requested size (grow_sender), its
+// floor raised to the tail the plan measured.  A request made before the sender's head moved on (a
+// replica's image apply in between) is dropped; the next plan makes it again.
 static int grow_rings(edgpu_ctx* x) {
     const uint32_t n = x->grow_pending;
     x->grow_pending = 0;
@@ -572,53 +629,9 @@ static int grow_rings(edgpu_ctx* x) {
     std::sort(req.begin(), req.end(), [](const GrowReq& a, const GrowReq& b) { return a.sender < b.sender; });
     for (size_t k = 0; k < req.size(); k++) {
         const GrowReq& R = req[k];
-        if ((k && req[k - 1].sender == R.sender) || R.sender >= x->nsenders || !x->snd_meta[R.sender]) continue;
-        SenderDev D;
-        {
-            Readback rb(x);
-            HIP_CHECK(rb.add(&D, x->d_senders.ptr + R.sender, sizeof(D)));
-            HIP_CHECK(rb.run());
-        }
-        if (D.head != R.head || D.meta != (uint64_t)(uintptr_t)x->snd_meta[R.sender]) continue;
-        const uint64_t old_pk = (uint64_t)D.pk_mask + 1, old_by = ((uint64_t)D.word_mask + 1) * 16;
-        const uint64_t new_pk = std::min<uint64_t>(std::max<uint64_t>(old_pk, 1ull << R.pk_log2), x->cfg.max_ring_packets);
-        const uint64_t new_by = std::min<uint64_t>(std::max<uint64_t>(old_by, 1ull << R.bytes_log2), x->cfg.max_ring_bytes);
-        if (new_pk == old_pk && new_by == old_by) continue;
-        void* meta = x->snd_meta[R.sender];
-        void* ring = x->snd_ring[R.sender];
-        void* nmeta = meta;
-        void* nring = ring;
-        if (new_pk > old_pk) {
-            if (dmalloc(&nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess)
-                return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender meta ring");
-            const uint64_t lo = D.head > old_pk ? D.head - old_pk : 0;
-            HIP_CHECK(launch_ring_move(0, meta, old_pk - 1, nmeta, new_pk - 1, lo, D.head - lo, x->stream));
-            HIP_CHECK(launch_ring_move(1, (const uint8_t*)meta + old_pk * sizeof(PktMeta), old_pk - 1,
-                                       (uint8_t*)nmeta + new_pk * sizeof(PktMeta), new_pk - 1, lo, D.head - lo, x->stream));
-        }
-        if (new_by > old_by) {
-            if (dmalloc(&nring, new_by) != hipSuccess) {
-                if (nmeta != meta) (void)hipFree(nmeta);
-                return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender byte ring");
-            }
-            const uint64_t wend = D.vbyte_end / 16, wlo = wend > old_by / 16 ? wend - old_by / 16 : 0;
-            HIP_CHECK(launch_ring_move(2, ring, old_by / 16 - 1, nring, new_by / 16 - 1, wlo, wend - wlo, x->stream));
-        }
-        D.meta = (uint64_t)(uintptr_t)nmeta;
-        D.ring = (uint64_t)(uintptr_t)nring;
-        D.pk_mask = (uint32_t)(new_pk - 1);
-        D.word_mask = (uint32_t)(new_by / 16 - 1);
-        D.floor = std::max(D.floor, R.tail);
-        HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + R.sender, &D, sizeof(D), hipMemcpyHostToDevice, x->stream));
-        HIP_CHECK(hipStreamSynchronize(x->stream));
-        if (nmeta != meta) HIP_CHECK(hipFree(meta));
-        if (nring != ring) HIP_CHECK(hipFree(ring));
-        x->snd_meta[R.sender] = nmeta;
-        x->snd_ring[R.sender] = nring;
-        x->work_cap_needed += new_pk / 16 - old_pk / 16;
-        x->ring_bytes += (new_pk - old_pk) * (sizeof(PktMeta) + sizeof(uint32_t)) + (new_by - old_by);
-        x->ring_grows++;
-        x->index_dirty = true;                  // the work list is sized from the rings
+        if (k && req[k - 1].sender == R.sender) continue;
+        bool grown = false;
+        if (int r = grow_sender(x, R.sender, 1ull << R.pk_log2, 1ull << R.bytes_log2, R.tail, &R.head, &grown)) return r;
     }
     return EDGPU_OK;
 }
@@ -2176,6 +2189,37 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     }
     if (plan.empty()) return EDGPU_OK;
     if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
+    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
+    if (x->cfg.ring_growth) {
+        // a replica's rings must hold what its owner's image carries (a full image: the key packet's
+        // GOP, say): a sender whose image part exceeds a ring gets it grown first
+        HIP_CHECK(sync_all(x));
+        std::vector<ImgSender> isnd(plan.size());
+        {
+            Readback rb(x);
+            for (size_t k = 0; k < plan.size(); k++) {
+                const uint32_t nt = x->sessions[plan[k].session].ntracks;
+                const uint8_t* hdr = (const uint8_t*)images + plan[k].image_base + sizeof(ImgHeader) + nt * sizeof(ImgStream);
+                HIP_CHECK(rb.add(&isnd[k], hdr + plan[k].ls * sizeof(ImgSender), sizeof(ImgSender)));
+            }
+            HIP_CHECK(rb.run());
+        }
+        std::vector<SenderDev> cur(plan.size());
+        {
+            Readback rb(x);
+            for (size_t k = 0; k < plan.size(); k++) HIP_CHECK(rb.add(&cur[k], x->d_senders.ptr + plan[k].sender, sizeof(SenderDev)));
+            HIP_CHECK(rb.run());
+        }
+        for (size_t k = 0; k < plan.size(); k++) {
+            const ImgSender& r = isnd[k];
+            const SenderDev& D = cur[k];
+            // (what the ring keeps beyond the image is the replica plan's growth requests' concern)
+            const uint64_t nmeta = r.head - r.floor, nbytes = r.vbyte_end - r.vbyte_floor;
+            if (nmeta <= (uint64_t)D.pk_mask + 1 && nbytes <= ((uint64_t)D.word_mask + 1) * 16) continue;
+            bool grown = false;
+            if (int e = grow_sender(x, plan[k].sender, 2 * nmeta, 2 * nbytes, std::max(D.tail, D.floor), nullptr, &grown)) return e;
+        }
+    }
     return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);
 }
 
