@@ -567,9 +567,10 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
     }
     if ((expect_head && D.head != *expect_head) || D.meta != (uint64_t)(uintptr_t)x->snd_meta[sender]) return EDGPU_OK;
     const uint64_t old_pk = (uint64_t)D.pk_mask + 1, old_by = ((uint64_t)D.word_mask + 1) * 16;
-    auto pow2_at_least = [](uint64_t v) { uint64_t p = 1; while (p < v) p <<= 1; return p; };
-    const uint64_t new_pk = std::min<uint64_t>(std::max(old_pk, pow2_at_least(want_pk)), x->cfg.max_ring_packets);
-    const uint64_t new_by = std::min<uint64_t>(std::max(old_by, pow2_at_least(want_by)), x->cfg.max_ring_bytes);
+    // the power of two at least v, capped at the bound (itself a power of two)
+    auto pow2_at_least = [](uint64_t v, uint64_t bound) { uint64_t p = 1; while (p < v && p < bound) p <<= 1; return p; };
+    const uint64_t new_pk = std::max(old_pk, pow2_at_least(want_pk, x->cfg.max_ring_packets));
+    const uint64_t new_by = std::max(old_by, pow2_at_least(want_by, x->cfg.max_ring_bytes));
     if (new_pk <= old_pk && new_by <= old_by) return EDGPU_OK;
     void* meta = x->snd_meta[sender];
     void* ring = x->snd_ring[sender];
@@ -2194,11 +2195,25 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
         // a replica's rings must hold what its owner's image carries (a full image: the key packet's
         // GOP, say): a sender whose image part exceeds a ring gets it grown first
         HIP_CHECK(sync_all(x));
-        std::vector<ImgSender> isnd(plan.size());
+        std::vector<ImgHeader> ih(n);
         {
             Readback rb(x);
-            for (size_t k = 0; k < plan.size(); k++) {
+            for (uint32_t i = 0; i < n; i++) HIP_CHECK(rb.add(&ih[i], (const uint8_t*)images + offsets[i], sizeof(ImgHeader)));
+            HIP_CHECK(rb.run());
+        }
+        std::vector<ImgSender> isnd(plan.size());
+        std::vector<uint8_t> ok(plan.size(), 0);
+        {
+            Readback rb(x);
+            for (size_t k = 0, i = 0; k < plan.size(); k++) {
+                while (i + 1 < n && plan[k].image_base != offsets[i]) i++;
                 const uint32_t nt = x->sessions[plan[k].session].ntracks;
+                const ImgHeader& h = ih[i];
+                // an image that does not match its replica is left to the apply kernel to reject
+                if (h.magic != kImageMagic || h.version != kImageVersion || h.ntracks != nt || h.nsenders != 2 * nt ||
+                    offsets[i] + sizeof(ImgHeader) + nt * sizeof(ImgStream) + 2 * nt * sizeof(ImgSender) > offsets[i + 1])
+                    continue;
+                ok[k] = 1;
                 const uint8_t* hdr = (const uint8_t*)images + plan[k].image_base + sizeof(ImgHeader) + nt * sizeof(ImgStream);
                 HIP_CHECK(rb.add(&isnd[k], hdr + plan[k].ls * sizeof(ImgSender), sizeof(ImgSender)));
             }
@@ -2211,8 +2226,10 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
             HIP_CHECK(rb.run());
         }
         for (size_t k = 0; k < plan.size(); k++) {
+            if (!ok[k]) continue;
             const ImgSender& r = isnd[k];
             const SenderDev& D = cur[k];
+            if (r.head < r.floor || r.vbyte_end < r.vbyte_floor) continue;
             // (what the ring keeps beyond the image is the replica plan's growth requests' concern)
             const uint64_t nmeta = r.head - r.floor, nbytes = r.vbyte_end - r.vbyte_floor;
             if (nmeta <= (uint64_t)D.pk_mask + 1 && nbytes <= ((uint64_t)D.word_mask + 1) * 16) continue;

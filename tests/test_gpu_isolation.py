@@ -1,9 +1,11 @@
 """GPU: per-stream error isolation (a bad stream marks that stream, not the batch).
 
 The reference's sender queues are unbounded lists (ReflectorStream.cpp:1088-1120); the engine's
-sender rings are sized by edgpu_config.  A session whose ring is too small for what one of its
-outputs still needs -- here a TCP player held for 3 s on a 2-Mb/s stream whose video ring holds
-256 packets (~1.2 s), under a relocation threshold that does not move it first -- loses packets
+sender rings are sized by edgpu_config and grow to the reference's retention (ring_growth, the
+default; tests/test_gpu_ring_growth.py) up to a bound.  A session whose ring is too small for
+what one of its outputs still needs -- here, with growth off, a TCP player held for 3 s on a
+2-Mb/s stream whose video ring holds 256 packets (~1.2 s), under a relocation threshold that does
+not move it first; in production, a ring at its growth bound -- loses packets
 on that output.  That marks the session (edgpu_stream_errors, edgpu_tick_stats.stream_errors),
 and nothing else: every tick goes on, and every other output, of that session and of the other
 session, is byte-identical to the reference reflector's (oracle/_ref/ref_harness) on the same
@@ -46,7 +48,7 @@ def test_ring_overflow_marks_one_session_and_the_tick_goes_on(oracle_bins, tmp_p
         pytest.skip("oracle/_ref/ref_harness not built")
     tr = _trace()
     pv = pref_values(tr.prefs)
-    ctx = edgpu.Context(video_ring_packets=256, video_ring_bytes=1 << 20,
+    ctx = edgpu.Context(video_ring_packets=256, video_ring_bytes=1 << 20, ring_growth=edgpu.FALSE,
                         reflector_buffer_size_sec=int(pv["reflector_buffer_size_sec"]),
                         rtp_reflector_threshold_msec=max(1000, int(pv["rtp_reflector_threshold_msec"])),
                         reflector_rtp_info_offset_msec=int(pv["reflector_rtp_info_offset_msec"]) or edgpu.FALSE)
