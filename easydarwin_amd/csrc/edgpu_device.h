@@ -318,6 +318,8 @@ struct TickParams {
     uint32_t grow_on;               // ring growth: on, and its per-sender bounds
     uint32_t grow_max_pk;
     uint64_t grow_max_bytes;
+    uint32_t* grow_flag;            // pinned host word (mapped): set when a request is made, so the
+                                    // host learns of it without reading the tick back
 };
 
 }  // namespace edgpu

@@ -307,6 +307,8 @@ struct edgpu_ctx {
     // ring growth (edgpu_config.ring_growth): the plan's requests, how many the host has learnt
     // of since (grown before the next ingest), which fan-out launch they were read for
     GrowReq* d_grow = nullptr;
+    uint32_t* h_grow_flag = nullptr;            // pinned, mapped: the plan sets it with a request
+    uint32_t* d_grow_flag = nullptr;            // its device address
     uint32_t grow_pending = 0;
     uint64_t grow_seen_launch = 0;
     uint64_t ring_grows = 0;
@@ -412,6 +414,10 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     }
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (dmalloc(&x->d_grow, sizeof(GrowReq) * kMaxGrow) != hipSuccess) return bad("ring growth requests");
+    if (hipHostMalloc((void**)&x->h_grow_flag, 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&x->d_grow_flag, x->h_grow_flag, 0) != hipSuccess)
+        return bad("ring growth flag");
+    *x->h_grow_flag = 0;
     if (hipMalloc(&x->d_null, 4096) != hipSuccess || hipMemset(x->d_null, 0, 4096) != hipSuccess) return bad("null ring");
     {
         TickTotals t0;
@@ -450,6 +456,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
     if (x->h_fpi_r) (void)hipHostFree(x->h_fpi_r);
     if (x->h_stage) (void)hipHostFree(x->h_stage);
+    if (x->h_grow_flag) (void)hipHostFree(x->h_grow_flag);
     if (x->d_tcp_src) (void)hipFree(x->d_tcp_src);
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
@@ -548,6 +555,7 @@ static void note_grow(edgpu_ctx* x, const TickTotals& t) {
     if (!x->fanout_launches || x->grow_seen_launch == x->fanout_launches) return;
     x->grow_seen_launch = x->fanout_launches;
     if (t.grow_count) x->grow_pending = std::min<uint32_t>(t.grow_count, kMaxGrow);
+    if (x->h_grow_flag) __atomic_store_n(x->h_grow_flag, 0u, __ATOMIC_RELEASE);
 }
 
 // One sender's rings replaced by ones of (at least) `want_pk` packets / `want_by` bytes, powers of
@@ -617,8 +625,16 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
 // floor raised to the tail the plan measured.  A request made before the sender's head moved on (a
 // replica's image apply in between) is dropped; the next plan makes it again.
 static int grow_rings(edgpu_ctx* x) {
-    const uint32_t n = x->grow_pending;
+    uint32_t n = x->grow_pending;
     x->grow_pending = 0;
+    if (x->h_grow_flag && __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) {
+        // a plan asked (the host did not read that tick's stats): its request count
+        __atomic_store_n(x->h_grow_flag, 0u, __ATOMIC_RELEASE);
+        HIP_CHECK(sync_all(x));
+        TickTotals t;
+        if (int r = read_totals(x, &t)) return r;
+        n = std::max(n, std::min<uint32_t>(t.grow_count, kMaxGrow));
+    }
     if (!n) return EDGPU_OK;
     HIP_CHECK(sync_all(x));
     std::vector<GrowReq> req(n);
@@ -1456,7 +1472,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     }
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
     HIP_CHECK(hipSetDevice(x->device));
-    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
+    if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     const edgpu_pkt_desc* dd = desc;
     const uint32_t* ds = seg_off;
     const uint32_t* dss = seg_sess;
@@ -1508,7 +1524,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (int r = owed_pass(x, "edgpu_ingest_interleaved")) return r;
     if (!n) return EDGPU_OK;
     HIP_CHECK(hipSetDevice(x->device));
-    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
+    if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     { int r = wait_pinned_copies(x); if (r) return r; }
     x->carry_len.resize(x->sessions.size(), 0);
     // one group per session: its reads are a run of consecutive entries, contiguous in `bytes`
@@ -1691,6 +1707,7 @@ static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     p.T.grow_on = x->cfg.ring_growth;
     p.T.grow_max_pk = x->cfg.max_ring_packets;
     p.T.grow_max_bytes = x->cfg.max_ring_bytes;
+    p.T.grow_flag = x->d_grow_flag;
     return p;
 }
 
@@ -2190,7 +2207,7 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     }
     if (plan.empty()) return EDGPU_OK;
     if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
-    if (x->grow_pending) { int r = grow_rings(x); if (r) return r; }
+    if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     if (x->cfg.ring_growth) {
         // a replica's rings must hold what its owner's image carries (a full image: the key packet's
         // GOP, say): a sender whose image part exceeds a ring gets it grown first

@@ -892,6 +892,7 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
                 if (k < kMaxGrow)
                     P.grow[k] = GrowReq{s, (uint32_t)(63 - __clzll((long long)want_pk)),
                                         (uint32_t)(63 - __clzll((long long)want_b)), 0u, tail, head};
+                if (k == 0 && P.T.grow_flag) *(volatile uint32_t*)P.T.grow_flag = 1u;   // (a vector store)
             }
         }
     }
