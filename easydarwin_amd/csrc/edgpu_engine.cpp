@@ -114,12 +114,17 @@ struct SourceHost {
     int64_t last_rr = 0;
 };
 
+// Bucket-array entries besides a subscriber handle (SessionHost::slots)
+constexpr int32_t kPlaceFree = -1, kPlaceRemote = -2;
+constexpr uint32_t kMaxPlaces = 1u << 20;
+
 struct SessionHost {
     uint32_t first_sender, ntracks, first_stream;
     bool udp_push;
     uint32_t span = 0;              // tracks' worth of rows it holds (>= ntracks after a reuse)
     uint32_t eyes = 0;              // client outputs (ReflectorStream::fEyeCount, every track)
-    std::vector<int32_t> slots;     // the streams' bucket arrays: subscriber per slot, -1 empty
+    std::vector<int32_t> slots;     // the streams' bucket arrays: subscriber per slot, kPlaceFree
+                                    // empty, kPlaceRemote a replica's output (remote_join)
     std::vector<SourceHost> src;    // per track
     bool alive = true;              // false after edgpu_session_remove (its id may be reused)
     std::vector<uint32_t> subs;     // attached subscriber handles
@@ -861,7 +866,8 @@ static int detach_subscriber(edgpu_ctx* x, uint32_t handle) {
     SessionHost& sh = x->sessions[s.session];
     sh.eyes--;                                   // RemoveOutput(..., isClient) -> DecEyeCount
     sh.subs.erase(std::find(sh.subs.begin(), sh.subs.end(), handle));
-    if (s.slot >= 0 && (size_t)s.slot < sh.slots.size()) sh.slots[s.slot] = -1;   // ReflectorStream::RemoveOutput
+    if (s.slot >= 0 && (size_t)s.slot < sh.slots.size() && sh.slots[s.slot] == (int32_t)handle)
+        sh.slots[s.slot] = kPlaceFree;           // ReflectorStream::RemoveOutput
     x->free_pending.emplace_back(s.span, s.first_sub);
     x->index_dirty = true;
     return EDGPU_OK;
@@ -911,6 +917,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     HIP_CHECK(hipStreamSynchronize(x->stream));
     sh.alive = false;
     sh.eyes = 0;
+    sh.slots.clear();                            // (remote places too)
     for (auto& h : sh.src) h = SourceHost();
     if (session < x->carry_len.size()) x->carry_len[session] = 0;
     x->dead_sessions.push_back(session);
@@ -980,8 +987,8 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
     // ReflectorStream::AddOutput + FindBucket (RS.cpp:281-334): the first empty place in bucket
     // order (bucket = slot / 16, each holding 16); every track's array holds the output there
     int32_t slot = 0;
-    while ((size_t)slot < sh.slots.size() && sh.slots[slot] >= 0) slot++;
-    if ((size_t)slot == sh.slots.size()) sh.slots.push_back(-1);
+    while ((size_t)slot < sh.slots.size() && sh.slots[slot] != kPlaceFree) slot++;
+    if ((size_t)slot == sh.slots.size()) sh.slots.push_back(kPlaceFree);
     sh.slots[slot] = (int32_t)handle;
     x->subscribers.push_back(SubscriberHost{session, first, nsub, true, transport, span, slot});
     if (transport == EDGPU_TRANSPORT_TCP) x->n_tcp += nsub;
@@ -1225,6 +1232,49 @@ int edgpu_session_eyes_add(edgpu_ctx* x, uint32_t session, int32_t delta) {
     SessionHost& sh = x->sessions[session];
     if (delta < 0 && (uint32_t)(-(int64_t)delta) > sh.eyes) return fail(EDGPU_BAD_ARGUMENT, "eye count below zero");
     sh.eyes = (uint32_t)((int64_t)sh.eyes + delta);
+    return EDGPU_OK;
+}
+
+// A remote output (a replica session's subscriber on another context) in the owner's bucket
+// arrays: ReflectorStream::AddOutput's first empty place (RS.cpp:281-334) and its eye
+// (IncEyeCount), so that owner and replica subscribers of one session are numbered in one
+// array, as the reference's one process numbers them.
+int edgpu_session_remote_join(edgpu_ctx* x, uint32_t session, int32_t* out_place) {
+    if (!x || !out_place || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    SessionHost& sh = x->sessions[session];
+    int32_t slot = 0;
+    while ((size_t)slot < sh.slots.size() && sh.slots[slot] != kPlaceFree) slot++;
+    if ((size_t)slot == sh.slots.size()) sh.slots.push_back(kPlaceFree);
+    sh.slots[slot] = kPlaceRemote;
+    sh.eyes++;
+    *out_place = slot;
+    return EDGPU_OK;
+}
+
+int edgpu_session_remote_leave(edgpu_ctx* x, uint32_t session, int32_t place) {
+    if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
+    SessionHost& sh = x->sessions[session];
+    if (place < 0 || (size_t)place >= sh.slots.size() || sh.slots[place] != kPlaceRemote)
+        return fail(EDGPU_BAD_ARGUMENT, "no remote output at that place");
+    if (sh.eyes == 0) return fail(EDGPU_BAD_ARGUMENT, "eye count below zero");
+    sh.slots[place] = kPlaceFree;
+    sh.eyes--;
+    return EDGPU_OK;
+}
+
+int edgpu_subscriber_set_slot(edgpu_ctx* x, uint32_t handle, int32_t slot) {
+    if (!x || handle >= x->subscribers.size() || !x->subscribers[handle].active)
+        return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
+    if (slot < 0 || slot >= (int32_t)kMaxPlaces) return fail(EDGPU_BAD_ARGUMENT, "bad place");
+    SubscriberHost& s = x->subscribers[handle];
+    SessionHost& sh = x->sessions[s.session];
+    if ((size_t)slot < sh.slots.size() && sh.slots[slot] != kPlaceFree && sh.slots[slot] != (int32_t)handle)
+        return fail(EDGPU_BAD_ARGUMENT, "place taken by another output of the session");
+    if (s.slot >= 0 && (size_t)s.slot < sh.slots.size() && sh.slots[s.slot] == (int32_t)handle)
+        sh.slots[s.slot] = kPlaceFree;
+    if ((size_t)slot >= sh.slots.size()) sh.slots.resize((size_t)slot + 1, kPlaceFree);
+    sh.slots[slot] = (int32_t)handle;
+    s.slot = slot;
     return EDGPU_OK;
 }
 

@@ -102,3 +102,35 @@ def route_relocations(relocated, key_update_fn, world: int, rank: int):
     if mine:
         key_update_fn(mine)
     return mine
+
+
+def route_places(events, join_fn, leave_fn, world: int, rank: int):
+    """Bucket places of replica subscribers, taken in their owners' bucket arrays
+    (ReflectorStream::AddOutput / RemoveOutput, ReflectorStream.cpp:281-336), so that a session's
+    subscribers on every GPU are numbered in one array as the reference's one process numbers
+    them (edgpu_session_remote_join / _leave).
+
+    events    this rank's replica joins and leaves since the last round, in order:
+              ("join", t_ms, global session, key) / ("leave", t_ms, global session, place)
+    join_fn   (global session owned here) -> place
+    leave_fn  (global session owned here, place) -> None
+
+    Every owner applies all ranks' events on its sessions in (time, rank, order) -- the order a
+    single server would have seen them in.  Collective (two all_gather_object rounds of a few
+    integers).  Returns {key: place} for this rank's joins."""
+    lists = [None] * world
+    dist.all_gather_object(lists, [tuple(e) for e in events])
+    merged = sorted((e[1], r, i, e) for r, lst in enumerate(lists) for i, e in enumerate(lst)
+                    if owner(e[2], world) == rank)
+    given = {}
+    for _t, r, _i, e in merged:
+        if e[0] == "join":
+            given.setdefault(r, {})[e[3]] = int(join_fn(e[2]))
+        else:
+            leave_fn(e[2], int(e[3]))
+    answers = [None] * world
+    dist.all_gather_object(answers, given)
+    out = {}
+    for a in answers:
+        out.update(a.get(rank, {}))
+    return out

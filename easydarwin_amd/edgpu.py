@@ -41,7 +41,8 @@ EXPORTED = [
     "edgpu_arena_gather", "edgpu_egress_disconnected", "edgpu_fanout_arrivals", "edgpu_session_remove",
     "edgpu_set_timing", "edgpu_ingest_prestage", "edgpu_fanout_next", "edgpu_session_ssrc_prefs",
     "edgpu_subscriber_slot", "edgpu_egress_pacing_config", "edgpu_egress_pacing", "edgpu_egress_clock",
-    "edgpu_egress_block_info",
+    "edgpu_egress_block_info", "edgpu_session_remote_join", "edgpu_session_remote_leave",
+    "edgpu_subscriber_set_slot",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -247,6 +248,9 @@ def load(path: str = LIB_PATH):
         "edgpu_arena_gather": (I32, [P, C.POINTER(FanoutResult), P, U32, P, U64]),
         "edgpu_egress_disconnected": (I32, [P, P, U32, C.POINTER(U32)]),
         "edgpu_subscriber_slot": (I32, [P, U32, C.POINTER(C.c_int32)]),
+        "edgpu_session_remote_join": (I32, [P, U32, C.POINTER(C.c_int32)]),
+        "edgpu_session_remote_leave": (I32, [P, U32, C.c_int32]),
+        "edgpu_subscriber_set_slot": (I32, [P, U32, C.c_int32]),
         "edgpu_egress_pacing_config": (I32, [P, C.POINTER(PacingConfig)]),
         "edgpu_egress_pacing": (I32, [P, U32, C.POINTER(Pacing)]),
         "edgpu_egress_clock": (I32, [P, C.c_int64]),
@@ -370,6 +374,10 @@ class Context:
         _check(self.lib.edgpu_subscriber_slot(self.h, handle, C.byref(v)))
         return v.value
 
+    def subscriber_set_slot(self, handle: int, slot: int):
+        """Moves the subscriber to bucket place `slot` (the place its owner gave a replica's output)."""
+        _check(self.lib.edgpu_subscriber_set_slot(self.h, handle, int(slot)))
+
     def ingest_host(self, desc: np.ndarray, seg_off: np.ndarray, seg_sess: np.ndarray, blob: np.ndarray):
         desc = np.ascontiguousarray(desc, dtype=PKT_DTYPE)
         seg_off = np.ascontiguousarray(seg_off, dtype=np.uint32)
@@ -452,6 +460,16 @@ class Context:
     def session_eyes_add(self, session: int, delta: int):
         """Subscribers of an owned session joined (+) or left (-) on another context."""
         _check(self.lib.edgpu_session_eyes_add(self.h, session, int(delta)))
+
+    def session_remote_join(self, session: int) -> int:
+        """A subscriber of this owned session joined on another context: its eye and its place in
+        the session's bucket arrays (returned)."""
+        v = C.c_int32()
+        _check(self.lib.edgpu_session_remote_join(self.h, session, C.byref(v)))
+        return v.value
+
+    def session_remote_leave(self, session: int, place: int):
+        _check(self.lib.edgpu_session_remote_leave(self.h, session, int(place)))
 
     def fanout(self, now_ms: int) -> FanoutResult:
         r = FanoutResult()

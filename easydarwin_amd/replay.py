@@ -45,16 +45,17 @@ from .trace import (BLOCK, JOIN, LEAVE, PKT, PREFS, PUBLISH, TICK, UNPUBLISH, UP
                     pref_bool, pref_values, rr_ssrc, rtp_info_player)
 
 
-def _wire_images(subs, desc, arena, images, budgets=None):
+def _wire_images(subs, desc, arena, images, budgets=None, tag=0):
     """Appends each sub-stream's packets of the tick to its wire image.  `budgets` maps
-    (handle, track, kind) -> the writes its socket accepted this tick (BLOCK events); the
-    rest would have blocked.  Returns the edgpu_fanout_blocked reports."""
+    (tag, handle, track, kind) -> the writes its socket accepted this tick (BLOCK events); the
+    rest would have blocked.  `tag` names the context (0 owner, 1 replica).  Returns the
+    edgpu_fanout_blocked reports."""
     reports = []
     for q, s in enumerate(subs):
         n = int(s["desc_count"])
         if n == 0:
             continue
-        key = (int(s["subscriber"]), int(s["track"]), int(s["kind"]))
+        key = (tag, int(s["subscriber"]), int(s["track"]), int(s["kind"]))
         if budgets and key in budgets and budgets[key] < n:
             n = budgets[key]
             reports.append((q, n))
@@ -187,7 +188,7 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
            interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None,
-           pinned: bool = False, tick_info: list | None = None, **cfg):
+           pinned: bool = False, tick_info: list | None = None, slots: dict | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
@@ -195,11 +196,16 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     still be in flight (the pipelined mode's contract: results stay valid one extra tick).
 
     replica=None: subscribers join the context that ingests (the owner).
-    replica="all" / "late": every subscriber joins a replica session on a second context,
+    replica="all" / "late" / "split": subscribers join a replica session on a second context,
     kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
     every replica before the first packet; "late" creates a fresh replica for every joining
     subscriber at its join tick, from a full image taken mid-stream (the C4 fast-start
-    path).
+    path); "split" sends the odd subscriber ids to one replica per session and keeps the even
+    ones on the owner, so a session's outputs are served by two contexts at once.  A replica
+    subscriber takes its bucket place from the owner (edgpu_session_remote_join, at its JOIN);
+    `slots` (a dict) receives every subscriber's place by sub id.  The session lifecycle
+    (PUBLISH / UNPUBLISH) reaches the replicas: a session that ends on the owner ends on them
+    (its replica subscribers torn down with it by a kill), a fresh re-push gets fresh replicas.
 
     sockets={...}: every tick leaves through the engine's socket egress to loopback receivers
     (easydarwin_amd/egress.py SocketSink, constructed with these keyword arguments) and the
@@ -214,8 +220,6 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     tick_info=[]: receives, per tick read back, (copy passes, largest sub-stream's arena bytes,
     largest sub-stream's descriptors, the tick's arena bytes, its relayed packets) -- more than
     one pass when a tick exceeds out_arena_bytes or max_out_packets (edgpu_fanout_next)."""
-    if replica is not None and trace.has_lifecycle:
-        raise ValueError("replica replays take no PUBLISH / UNPUBLISH events")
     pv = pref_values(trace.prefs)           # the stream prefs: read once (ReflectorStream::Initialize)
     cfg = dict(cfg)
     cfg.setdefault("reflector_buffer_size_sec", int(pv["reflector_buffer_size_sec"]))
@@ -228,7 +232,9 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     rep = link = None
     if replica is not None:
         from .replica import ReplicaLink
-        assert replica in ("all", "late")
+        assert replica in ("all", "late", "split")
+        if sockets is not None and replica == "split":
+            raise ValueError("socket egress replays serve one context")
         dev = int(cfg.get("device", 0))
         rep = edgpu.Context(**cfg)
         link = ReplicaLink(ctx, dev, rep, dev)
@@ -261,32 +267,31 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             assert sid == len(sess_tracks)
             sess_tracks.append(ctx.session_tracks(sid))
             if replica == "all":
-                rsess[sid] = link.add(sid, sdp)
+                rsess[i] = link.add(sid, sdp, trace.udp_push(i))
         reports = []                        # (t, session, track, addr, port, bytes)
         sources = []                        # this batch's UDP datagram sources
-        subs_meta = {}          # handle -> (sub_id, session, tcp)
+        subs_meta = {}          # (tag, handle) -> (sub_id, session, tcp, place); tag 0 owner, 1 replica
         images = {}
         pending, joins, stats = [], [], []
         tick_info = tick_info if tick_info is not None else []
         lag = bool(cfg.get("overlap_ticks")) and replica is None
-        unread = None                       # (ctx, result) of a tick not read back yet
+        unread = []                         # (ctx, tag, result, t, budgets) of ticks not read back yet
 
         def drain():
             nonlocal unread
-            if unread is not None and sink is not None:
-                c, r, tt, _ = unread
-                sink.tick(r, tt)
-                if link is not None and c is rep:
-                    link.feedback()
-                st = c.stats()
-                stats.append((tt, st.relayed_packets, st.relayed_bytes))
-                unread = None
-            if unread is not None:
-                c, r, tt, budgets = unread
+            todo, unread = unread, []
+            for c, tag, r, tt, budgets in todo:
+                if sink is not None:
+                    sink.tick(r, tt)
+                    if link is not None and c is rep:
+                        link.feedback()
+                    st = c.stats()
+                    stats.append((tt, st.relayed_packets, st.relayed_bytes))
+                    continue
                 reports, big = [], [0, 0, 0]
 
                 def consume(st, subs, desc, arena):
-                    reports.extend(_wire_images(subs, desc, arena, images, budgets))
+                    reports.extend(_wire_images(subs, desc, arena, images, budgets, tag))
                     big[2] = max(big[2], int(st.relayed_packets))     # the tick's planned packets
                     if len(subs):
                         big[0] = max(big[0], int(subs["out_bytes"].max()))
@@ -301,7 +306,6 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 stats.append((tt, st.relayed_packets, st.relayed_bytes))
                 # (relayed_packets before the backpressure reports take the unsent ones off)
                 tick_info.append((npass, big[0], big[1], int(st.arena_bytes), big[2]))
-                unread = None
 
         pin_sets = [{}, {}]                 # pinned host batch buffers, used alternately
         pin_next = [0]
@@ -361,43 +365,59 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                                      "over_buffer_ms": 1000 * int(cfg["reflector_buffer_size_sec"])}, **kw["pacing"])
             sink = SocketSink(ctx if rep is None else rep, **kw)
         blocks = {}                         # (sub_id, track, kind) -> budget for the next TICK
-        gone = set()                        # handles removed by LEAVE
+        gone = set()                        # (tag, handle)s removed by LEAVE or a kill
+
+        def remote(sub_id):
+            """Does this subscriber join a replica session?"""
+            return rep is not None and (replica != "split" or sub_id % 2 == 1)
 
         def do_join(j):
-            (_, jt, s, sub_id, transport, ua, now_j) = j
-            out = ctx if rep is None else rep
+            (_, jt, s, sub_id, transport, ua, now_j, place) = j
+            tport = edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP
+            rtpi = rtp_info_player(mod["prefs"], ua)
             try:
-                h, _info = out.subscriber_play(gen[s] if rep is None else rsess[s],
-                                               edgpu.TRANSPORT_TCP if transport else edgpu.TRANSPORT_UDP,
-                                               rtp_info=rtp_info_player(mod["prefs"], ua), now_ms=now_j)
+                if remote(sub_id):
+                    out, tag = rep, 1
+                    h, _info, place = link.join(gen[s], rsess[s], tport, rtp_info=rtpi, now_ms=now_j, place=place)
+                else:
+                    out, tag = ctx, 0
+                    h, _info = ctx.subscriber_play(gen[s], tport, rtp_info=rtpi, now_ms=now_j)
+                    place = ctx.subscriber_slot(h)
             except edgpu.EdgpuError as e:      # deferred RTP-Info PLAY: not a subscriber
                 if e.code != edgpu.WOULD_BLOCK:
                     raise
                 return
-            subs_meta[h] = (sub_id, s, transport)
+            subs_meta[(tag, h)] = (sub_id, s, transport, place)
+            if slots is not None:
+                slots[sub_id] = place
             if rewrite and sub_id in rewrite:
                 for tr in range(sess_tracks[s]):
                     out.subscriber_rewrite(h, tr, *rewrite[sub_id])
-            if rep is not None:
-                ctx.session_eyes_add(s, 1)     # the owner counts remote subscribers
             if sink is not None:
                 vid = sum(1 << t for t, m in enumerate(re.findall(r"(?m)^m=(\w+)", trace.sdps[s])) if m == "video")
                 sink.join(h, sub_id, sess_tracks[s], bool(transport), play_time=now_j, video_tracks=vid)
             for tr in range(sess_tracks[s]):
                 for k in (0, 1):
-                    images[(h, tr, k)] = []
+                    images[(tag, h, tr, k)] = []
         if lag and any(ev[0] == BLOCK for ev in trace.events):
             raise ValueError("backpressure reports need each tick read before the next ingest")
 
         def outputs_of(s):
-            return [h for h, meta in subs_meta.items() if meta[1] == s and h not in gone]
+            return [th for th, meta in subs_meta.items() if meta[1] == s and th not in gone]
+
+        def end_session(s, kill=False):
+            """The owner session ends; its replicas with it (their subscribers too with a kill)."""
+            drain()                         # (overlap_ticks: a session goes only after its last tick is read)
+            if link is not None:
+                link.remove(gen[s], kill_outputs=kill)
+                rsess.pop(s, None)
+            ctx.session_remove(gen[s], kill_outputs=kill)
+            gen[s] = None
 
         def release_check(s):
             """A session without pusher or outputs dies (RemoveOutput's refcount-0 branch)."""
-            if gen[s] is not None and not published[s] and not outputs_of(s):
-                drain()                     # (overlap_ticks: a session goes only after its last tick is read)
-                ctx.session_remove(gen[s])
-                gen[s] = None
+            if gen[s] is not None and not published[s] and not outputs_of(s) and not any(j[2] == s for j in joins):
+                end_session(s)          # (a replica join waiting for its tick is an output already)
 
         for ev in trace.events:
             if ev[0] == BLOCK:
@@ -420,15 +440,18 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 rtpi = rtp_info_player(mod["prefs"], ev[5])
                 if rtpi:
                     flush()
-                if rep is None or rtpi:
-                    if gen[ev[2]] is not None:          # else no session: the SETUP fails
-                        if link is not None:
-                            if replica == "late" or ev[2] not in rsess:
-                                rsess[ev[2]] = link.add(ev[2], trace.sdps[ev[2]])
-                            link.sync(clock)
-                        do_join(ev + (clock,))
+                s = ev[2]
+                if gen[s] is None:                      # no session: the SETUP fails
+                    continue
+                if not remote(ev[3]) or rtpi:
+                    if remote(ev[3]):
+                        if replica == "late" or s not in rsess:
+                            rsess[s] = link.add(gen[s], trace.sdps[s], trace.udp_push(s))
+                        link.sync(clock)
+                    do_join(ev + (clock, None))
                 else:
-                    joins.append(ev + (clock,))     # replicas: made at the tick
+                    # replicas: made at the tick, the place taken on the owner now (AddOutput order)
+                    joins.append(ev + (clock, ctx.session_remote_join(gen[s])))
             elif ev[0] == UNPUBLISH:
                 _, t, s, kill = ev
                 flush()
@@ -437,12 +460,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     # RemoveOutput's kill: the pusher's attribute or the pref now (:2156)
                     kill = kill or kill_attr[s] or pref_bool(pref_values(mod["prefs"])["kill_clients_when_broadcast_stops"])
                     if kill:                            # TearDownAllOutputs
-                        for h in outputs_of(s):
-                            gone.add(h)
+                        for th in outputs_of(s):
+                            gone.add(th)
+                        joins = [j for j in joins if j[2] != s]   # (their places go with the session)
                         if gen[s] is not None:
-                            drain()
-                            ctx.session_remove(gen[s], kill_outputs=True)
-                            gen[s] = None
+                            end_session(s, kill=True)
                     release_check(s)
             elif ev[0] == PUBLISH:
                 _, t, s = ev
@@ -451,6 +473,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     published[s] = True
                     if gen[s] is None:
                         publish_fresh(s, clock // 1000)
+                        if replica == "all":
+                            rsess[s] = link.add(gen[s], trace.sdps[s], trace.udp_push(s))
                     else:                               # the surviving session's new RECORD
                         kill_attr[s] = pref_bool(pref_values(mod["prefs"])["kill_clients_when_broadcast_stops"])
             elif ev[0] == PREFS:
@@ -461,44 +485,44 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 # tick (edgpu_subscriber_remove)
                 sub_id = ev[2]
                 for j in [j for j in joins if j[3] == sub_id]:
-                    if link is not None and (replica == "late" or j[2] not in rsess):
-                        rsess[j[2]] = link.add(j[2], trace.sdps[j[2]])
+                    if replica == "late" or j[2] not in rsess:
+                        rsess[j[2]] = link.add(gen[j[2]], trace.sdps[j[2]], trace.udp_push(j[2]))
                     do_join(j)
                 joins = [j for j in joins if j[3] != sub_id]
-                for h, meta in subs_meta.items():
-                    if meta[0] == sub_id and h not in gone:
-                        (ctx if rep is None else rep).subscriber_remove(h)
-                        gone.add(h)
-                        if rep is not None:
-                            ctx.session_eyes_add(meta[1], -1)
+                for (tag, h), meta in subs_meta.items():
+                    if meta[0] == sub_id and (tag, h) not in gone:
+                        if tag:
+                            link.leave(gen[meta[1]], h, meta[3])
                         else:
-                            release_check(meta[1])
+                            ctx.subscriber_remove(h)
+                        gone.add((tag, h))
+                        release_check(meta[1])
                         break
             elif ev[0] == TICK:
                 t = ev[1]
                 flush()
                 if link is not None:
-                    for (_, jt, s, sub_id, transport, _ua, _now) in joins:
+                    for (_, jt, s, sub_id, transport, _ua, _now, _place) in joins:
                         if replica == "late" or s not in rsess:
-                            rsess[s] = link.add(s, trace.sdps[s])     # "late": a fresh replica per join
+                            rsess[s] = link.add(gen[s], trace.sdps[s], trace.udp_push(s))   # "late": a fresh replica per join
                     link.sync(t)
-                out = ctx if rep is None else rep
                 for j in joins:
                     do_join(j)
                 joins = []
-                if rep is not None:
-                    ctx.fanout(t)                      # the owner ticks too (no subscribers here)
-                    reports.extend((t, trace_of[r[0]]) + tuple(r[1:]) for r in ctx.source_reports())
                 drain()                              # the previous tick, after this batch's ingest
                 by_handle = {}
                 for (sub_id, trk, kind), b in blocks.items():
-                    for h, meta in subs_meta.items():
-                        if meta[0] == sub_id and h not in gone:
-                            by_handle[(h, trk, kind)] = b
+                    for (tag, h), meta in subs_meta.items():
+                        if meta[0] == sub_id and (tag, h) not in gone:
+                            by_handle[(tag, h, trk, kind)] = b
                 blocks = {}
-                unread = (out, out.fanout(t), t, by_handle)
-                if rep is None:
-                    reports.extend((t, trace_of[r[0]]) + tuple(r[1:]) for r in ctx.source_reports())
+                # the owner ticks (with subscribers of its own in "split"), then the replica
+                unread.append((ctx, 0, ctx.fanout(t), t, by_handle))
+                reports.extend((t, trace_of[r[0]]) + tuple(r[1:]) for r in ctx.source_reports())
+                if rep is not None:
+                    if replica != "split":
+                        unread.pop()                 # (no subscribers on the owner)
+                    unread.append((rep, 1, rep.fanout(t), t, by_handle))
                 if not lag:
                     drain()
         drain()
@@ -512,8 +536,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 sockets["stats"].extend(sink.stats)
         # capture: one record per (subscriber, track, kind), sorted by subscriber id
         recs = []
-        for (h, tr, k), parts in images.items():
-            sub_id, s, transport = subs_meta[h]
+        for (tag, h, tr, k), parts in images.items():
+            sub_id, s, transport, _place = subs_meta[(tag, h)]
             if wire is not None:
                 n, data = wire.get((h, tr, k), (0, b""))
             else:

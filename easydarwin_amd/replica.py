@@ -32,7 +32,7 @@ class ReplicaLink:
         self.owner, self.replica = owner, replica
         self.odev, self.rdev = owner_device, replica_device
         self.pairs: list[tuple[int, int]] = []      # (owner session, replica session)
-        self.heads: dict[int, np.ndarray] = {}      # pair index -> heads after its last export
+        self.heads: dict[tuple[int, int], np.ndarray] = {}   # pair -> heads after its last export
         self.bytes_shipped = 0
         self._src = None
         self._dst = None
@@ -42,6 +42,35 @@ class ReplicaLink:
         rs = self.replica.session_add(sdp, udp_push)
         self.pairs.append((owner_session, rs))
         return rs
+
+    def join(self, owner_session: int, replica_session: int, transport: int, rtp_info: bool = False,
+             now_ms: int = 0, place: int | None = None):
+        """A subscriber of the replica session: (handle, rtp-info, place).  Its place in the session's
+        bucket arrays is taken on the owner (edgpu_session_remote_join, which counts its eye there)
+        unless `place` was reserved already, so that the owner's and every replica's subscribers are
+        numbered in one array as the reference's AddOutput numbers them (ReflectorStream.cpp:281-334)."""
+        h, info = self.replica.subscriber_play(replica_session, transport, rtp_info=rtp_info, now_ms=now_ms)
+        if place is None:
+            place = self.owner.session_remote_join(owner_session)
+        self.replica.subscriber_set_slot(h, place)
+        return h, info, place
+
+    def leave(self, owner_session: int, handle: int, place: int):
+        """RemoveOutput of a replica subscriber: gone from the replica, its place and eye from the owner."""
+        self.replica.subscriber_remove(handle)
+        self.owner.session_remote_leave(owner_session, place)
+
+    def remove(self, owner_session: int, kill_outputs: bool = False):
+        """The owner session ends (edgpu_session_remove on the owner follows): its replica sessions go
+        with it, their subscribers too with kill_outputs (TearDownAllOutputs)."""
+        keep = []
+        for pr in self.pairs:
+            if pr[0] == owner_session:
+                self.replica.session_remove(pr[1], kill_outputs=kill_outputs)
+                self.heads.pop(pr, None)
+            else:
+                keep.append(pr)
+        self.pairs = keep
 
     def _buffers(self, nbytes: int):
         if self._src is None or self._src.nbytes < nbytes:
@@ -65,9 +94,9 @@ class ReplicaLink:
             return 0
         osess = [o for o, _ in self.pairs]
         nsnd = [self.owner.senders_of([o]) for o in osess]
-        since = np.concatenate([self.heads[i] if i in self.heads
+        since = np.concatenate([self.heads[pr] if pr in self.heads
                                 else np.full(n, edgpu.IMAGE_FULL, dtype=np.uint64)
-                                for i, n in enumerate(nsnd)])
+                                for pr, n in zip(self.pairs, nsnd)])
         offsets, heads = self.owner.session_export(osess, now_ms, since=since)     # size query
         total = int(offsets[-1])
         src, dst = self._buffers(total)
@@ -75,8 +104,8 @@ class ReplicaLink:
         self.replica.memcpy_peer(dst.ptr, self.odev, src.ptr, total)
         self.replica.session_import(dst.ptr, offsets, [r for _, r in self.pairs])
         k = 0
-        for i, n in enumerate(nsnd):
-            self.heads[i] = heads[k:k + n].copy()
+        for pr, n in zip(self.pairs, nsnd):
+            self.heads[pr] = heads[k:k + n].copy()
             k += n
         self.bytes_shipped += total
         return total
@@ -123,6 +152,15 @@ class DistReplicaLink:
         rs = self.ctx.session_add(sdp, udp_push)
         self.replica_of[int(g)] = rs
         return rs
+
+    def places(self, events):
+        """dist.route_places over this context: the owners here take / free the places of every
+        rank's replica joins / leaves (events as route_places takes them); returns {key: place}
+        for this rank's joins, each to be given to its subscriber with subscriber_set_slot."""
+        from .dist import route_places
+        return route_places(events, lambda g: self.ctx.session_remote_join(self.local_of[g]),
+                            lambda g, p: self.ctx.session_remote_leave(self.local_of[g], p),
+                            self.world, self.rank)
 
     def _export(self, sessions, dst_rank, now_ms):
         local = [self.local_of[g] for g in sessions]

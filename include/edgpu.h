@@ -500,6 +500,18 @@ int  edgpu_source_identity(edgpu_ctx* ctx, uint32_t session, uint32_t track, uin
  * counts every output (IncEyeCount / DecEyeCount).  `delta` is +1 per remote join, -1 per
  * remote leave. */
 int  edgpu_session_eyes_add(edgpu_ctx* ctx, uint32_t session, int32_t delta);
+/* The same for a remote subscriber that also takes its place in the owner's bucket arrays
+ * (ReflectorStream::AddOutput / RemoveOutput, ReflectorStream.cpp:281-336: the first empty place,
+ * 16 a bucket), so that the owner's and its replicas' subscribers of one session are numbered
+ * in one array, as the reference numbers them in one process: a subscriber past the first
+ * bucket then gets the reference's bucket lateness in its transmit times on whichever GPU serves
+ * it.  edgpu_session_remote_join counts the eye and returns the place; the replica passes it to
+ * edgpu_subscriber_set_slot for its subscriber.  edgpu_session_remote_leave frees it. */
+int  edgpu_session_remote_join(edgpu_ctx* ctx, uint32_t session, int32_t* out_place);
+int  edgpu_session_remote_leave(edgpu_ctx* ctx, uint32_t session, int32_t place);
+/* Moves a subscriber to bucket place `slot` of its session (a replica session's subscriber takes
+ * the place its owner gave it, edgpu_session_remote_join).  Fails if another output holds it. */
+int  edgpu_subscriber_set_slot(edgpu_ctx* ctx, uint32_t handle, int32_t slot);
 
 /* ---- Socket egress (host side) ----
  * Sends a fan-out tick to the subscribers' sockets as RTPStream::Write does

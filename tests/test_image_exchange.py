@@ -120,3 +120,80 @@ def test_relocations_reach_the_owners(world):
     for r, (_, upd, got) in res.items():
         want = sorted(g for g in reported if owner(g, world) == r)
         assert upd == want and got == want
+
+
+def _first_empty(arr):
+    p = next((i for i, v in enumerate(arr) if v is None), len(arr))
+    if p == len(arr):
+        arr.append(None)
+    return p
+
+
+def _places_worker(rank, world, port, out_q):
+    import random
+
+    import torch.distributed as dist
+    from easydarwin_amd.dist import route_places
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    arrays = {}                                  # owned session -> bucket array (None = empty)
+
+    def join(g):
+        a = arrays.setdefault(g, [])
+        p = _first_empty(a)
+        a[p] = "remote"
+        return p
+
+    def leave(g, p):
+        assert arrays[g][p] == "remote"
+        arrays[g][p] = None
+
+    rng = random.Random(100 + rank)
+    held, rounds = [], []
+    for rnd in range(4):
+        ev = []
+        for i in range(12):
+            t = 1000 * rnd + rng.randint(0, 999)
+            if held and rng.random() < 0.3:
+                g, p = held.pop(rng.randrange(len(held)))
+                ev.append(("leave", t, g, p))
+            else:
+                ev.append(("join", t, rng.randrange(N_SESS), (rank, rnd, i)))
+        ev.sort(key=lambda e: e[1])
+        got = route_places(ev, join, leave, world, rank)
+        held += [(e[2], got[e[3]]) for e in ev if e[0] == "join"]
+        rounds.append((ev, got))
+    out_q.put((rank, rounds))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_remote_places_follow_one_array(world):
+    """dist.route_places: replica joins and leaves from every rank, over several rounds, get the places
+    one bucket array per session would give them when the events are applied in (time, rank, order)
+    -- a single server's AddOutput / RemoveOutput order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_places_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    arrays, want = {}, {}
+    for rnd in range(4):
+        merged = sorted((e[1], r, i, e) for r in range(world) for i, e in enumerate(res[r][rnd][0]))
+        for _t, r, _i, e in merged:
+            a = arrays.setdefault(e[2], [])
+            if e[0] == "join":
+                p = _first_empty(a)
+                a[p] = e[3]
+                want[e[3]] = p
+            else:
+                a[e[3]] = None
+    for r in range(world):
+        for ev, got in res[r]:
+            for e in ev:
+                if e[0] == "join":
+                    assert got[e[3]] == want[e[3]]
