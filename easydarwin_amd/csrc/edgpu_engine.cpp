@@ -2174,7 +2174,7 @@ static int image_launch(edgpu_ctx* x, std::vector<ImgPlan>& plan, int64_t now_ms
     int status = 0;
     Readback rb(x);
     HIP_CHECK(rb.add(&status, x->d_img_status, sizeof(int)));
-    if (phase == 0) HIP_CHECK(rb.add(plan.data(), x->d_img_plan.ptr, plan.size() * sizeof(ImgPlan)));
+    if (phase == 0 || phase == 3) HIP_CHECK(rb.add(plan.data(), x->d_img_plan.ptr, plan.size() * sizeof(ImgPlan)));
     HIP_CHECK(rb.run());
     if (status) return fail(status, phase == 2 ? "session image rejected by the replica" : "session image export");
     return EDGPU_OK;
@@ -2260,48 +2260,20 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
     if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     if (x->cfg.ring_growth) {
         // a replica's rings must hold what its owner's image carries (a full image: the key packet's
-        // GOP, say): a sender whose image part exceeds a ring gets it grown first
+        // GOP, say): a sender whose image part exceeds a ring gets it grown first (k_image_fit
+        // measures every sender at once; one readback)
         HIP_CHECK(sync_all(x));
-        std::vector<ImgHeader> ih(n);
-        {
-            Readback rb(x);
-            for (uint32_t i = 0; i < n; i++) HIP_CHECK(rb.add(&ih[i], (const uint8_t*)images + offsets[i], sizeof(ImgHeader)));
-            HIP_CHECK(rb.run());
+        std::vector<ImgPlan> fit(plan);
+        for (size_t k = 0, i = 0; k < fit.size(); k++) {
+            while (i + 1 < n && fit[k].image_base != offsets[i]) i++;
+            fit[k].image_bytes = offsets[i + 1] - offsets[i];
         }
-        std::vector<ImgSender> isnd(plan.size());
-        std::vector<uint8_t> ok(plan.size(), 0);
-        {
-            Readback rb(x);
-            for (size_t k = 0, i = 0; k < plan.size(); k++) {
-                while (i + 1 < n && plan[k].image_base != offsets[i]) i++;
-                const uint32_t nt = x->sessions[plan[k].session].ntracks;
-                const ImgHeader& h = ih[i];
-                // an image that does not match its replica is left to the apply kernel to reject
-                if (h.magic != kImageMagic || h.version != kImageVersion || h.ntracks != nt || h.nsenders != 2 * nt ||
-                    offsets[i] + sizeof(ImgHeader) + nt * sizeof(ImgStream) + 2 * nt * sizeof(ImgSender) > offsets[i + 1])
-                    continue;
-                ok[k] = 1;
-                const uint8_t* hdr = (const uint8_t*)images + plan[k].image_base + sizeof(ImgHeader) + nt * sizeof(ImgStream);
-                HIP_CHECK(rb.add(&isnd[k], hdr + plan[k].ls * sizeof(ImgSender), sizeof(ImgSender)));
-            }
-            HIP_CHECK(rb.run());
-        }
-        std::vector<SenderDev> cur(plan.size());
-        {
-            Readback rb(x);
-            for (size_t k = 0; k < plan.size(); k++) HIP_CHECK(rb.add(&cur[k], x->d_senders.ptr + plan[k].sender, sizeof(SenderDev)));
-            HIP_CHECK(rb.run());
-        }
-        for (size_t k = 0; k < plan.size(); k++) {
-            if (!ok[k]) continue;
-            const ImgSender& r = isnd[k];
-            const SenderDev& D = cur[k];
-            if (r.head < r.floor || r.vbyte_end < r.vbyte_floor) continue;
+        if (int r = image_launch(x, fit, 0, (uint8_t*)const_cast<void*>(images), 3)) return r;
+        for (const ImgPlan& f : fit) {
+            if (!f.nmeta && !f.nbytes) continue;
             // (what the ring keeps beyond the image is the replica plan's growth requests' concern)
-            const uint64_t nmeta = r.head - r.floor, nbytes = r.vbyte_end - r.vbyte_floor;
-            if (nmeta <= (uint64_t)D.pk_mask + 1 && nbytes <= ((uint64_t)D.word_mask + 1) * 16) continue;
             bool grown = false;
-            if (int e = grow_sender(x, plan[k].sender, 2 * nmeta, 2 * nbytes, std::max(D.tail, D.floor), nullptr, &grown)) return e;
+            if (int e = grow_sender(x, f.sender, 2 * f.nmeta, 2 * f.nbytes, f.floor, nullptr, &grown)) return e;
         }
     }
     return image_launch(x, plan, 0, (uint8_t*)const_cast<void*>(images), 2);

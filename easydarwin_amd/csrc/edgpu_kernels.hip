@@ -2422,6 +2422,32 @@ __global__ __launch_bounds__(256) void k_image_apply(ImageParams P) {
     }
 }
 
+// Import fit (ring growth), one thread per (image, sender): a replica's rings must hold what its
+// owner's image carries, so the image part's packets / bytes go back (nmeta / nbytes, with the
+// sender's oldest kept index in floor) when they exceed the rings, else 0.  An image that does not
+// match its replica (header, size) is left to k_image_apply to reject.  E.image_bytes: the image's
+// size in the buffer.
+__global__ void k_image_fit(ImageParams P) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.nplan) return;
+    ImgPlan& E = P.plan[j];
+    E.nmeta = 0;
+    E.nbytes = 0;
+    const SenderDev& D = P.senders[E.sender];
+    const uint32_t nt = P.sessions[E.session].ntracks;
+    const uint8_t* img = P.buf + E.image_base;
+    if (E.image_bytes < sizeof(ImgHeader) + nt * sizeof(ImgStream) + 2 * nt * sizeof(ImgSender)) return;
+    const ImgHeader h = *reinterpret_cast<const ImgHeader*>(img);
+    if (h.magic != kImageMagic || h.version != kImageVersion || h.ntracks != nt || h.nsenders != 2 * nt) return;
+    const ImgSender r = reinterpret_cast<const ImgSender*>(img + sizeof(ImgHeader) + nt * sizeof(ImgStream))[E.ls];
+    if (r.head < r.floor || r.vbyte_end < r.vbyte_floor) return;
+    const uint64_t nmeta = r.head - r.floor, nbytes = r.vbyte_end - r.vbyte_floor;
+    if (nmeta <= (uint64_t)D.pk_mask + 1 && nbytes <= ((uint64_t)D.word_mask + 1) * 16) return;
+    E.nmeta = nmeta;
+    E.nbytes = nbytes;
+    E.floor = D.tail > D.floor ? D.tail : D.floor;
+}
+
 }  // namespace edgpu
 
 // ---------------------------------------------------------------------------------------
@@ -2575,7 +2601,8 @@ hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
     if (p.nplan == 0) return hipSuccess;
     if (phase == 0) hipLaunchKernelGGL(k_image_plan, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
     else if (phase == 1) hipLaunchKernelGGL(k_image_pack, dim3(p.nplan), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
+    else if (phase == 2) hipLaunchKernelGGL(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_image_fit, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,

@@ -70,10 +70,11 @@ def realtime_runs(args) -> list:
     return out
 
 
-def reference_module_run(args) -> dict | None:
+def reference_module_run(args, threads: int | None = None) -> dict | None:
     """The REFERENCE QTSSReflectorModule (oracle/_ref/libQTSSReflectorModule_ref.so, compiled from its
-    sources) in the same fake server, same load, same pusher threads; its senders reflect on as many
-    threads as the drop-in has write threads (EDGPU_REF_TICK_THREADS: the server's task threads)."""
+    sources) in the same fake server, same load, same pusher threads (or `threads`); its senders reflect
+    on as many threads as the drop-in has write threads (EDGPU_REF_TICK_THREADS: the server's task
+    threads)."""
     so = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
     if not os.path.exists(so):
         return None
@@ -82,7 +83,7 @@ def reference_module_run(args) -> dict | None:
     if args.concurrent_push:
         env["EDGPU_BENCH_CONCURRENT_PUSH"] = "1"
     cmd = [os.path.join(ROOT, "tools", "qtss_replay"), so, "--bench", str(args.sessions), str(args.subs),
-           str(args.seconds), str(args.tick_ms), str(args.threads)]
+           str(args.seconds), str(args.tick_ms), str(threads or args.threads)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
     if r.returncode:
         raise SystemExit(f"qtss_replay --bench (reference module) failed ({r.returncode}): {r.stderr.strip()[-400:]}")
@@ -102,6 +103,8 @@ def reference_run(args) -> dict | None:
     return {"relayed_per_s": round(d["both_per_s"], 1), "reflect_per_s": round(d["reflect_per_s"], 1),
             "ingest_per_s": round(d["ingest_per_s"], 1), "cores": procs_n, "cores_note": why,
             "relayed_packets": d["relayed_packets"],
+            # one process's PushPacket time per packet (each process pushes on one thread)
+            "push_us_per_packet_per_process": round(1e6 * procs_n / max(d["ingest_per_s"], 1e-9), 4),
             "sample": f"oracle/_ref/ref_harness --bench-steady: the C2 fleet, {args.sessions} sessions x {args.subs} UDP "
                       f"subs, a {bench.C2_SECONDS}-s trace replayed {bench.C2_LOOPS} times at {args.tick_ms}-ms ticks, "
                       f"counted after {bench.C2_WARM_MS // 1000} s, sharded over {procs_n} processes at once "
@@ -154,9 +157,19 @@ def main():
         out["reference_module"] = reference_module_run(args)
         if out["reference_module"]:
             out["module_vs_reference_module"] = round(m["relayed_per_s"] / out["reference_module"]["relayed_per_s"], 2)
+            # its push path on one pusher thread: every pushed packet's Task::Signal takes the process-wide
+            # mutex of CommonUtilitiesLib/atomic.cpp (atomic_or), so pusher threads do not scale there
+            one = reference_module_run(args, threads=1)
+            out["reference_module_push_us_per_packet"] = {
+                f"{args.threads}_threads": out["reference_module"]["push_us_per_packet"],
+                "1_thread": one["push_us_per_packet"]}
         out["reference"] = reference_run(args)
         if out["reference"]:
             out["module_vs_reference"] = round(m["relayed_per_s"] / out["reference"]["relayed_per_s"], 2)
+            if out["reference"].get("push_us_per_packet_per_process"):
+                out["reference_module_push_vs_harness"] = round(
+                    out["reference_module_push_us_per_packet"]["1_thread"]
+                    / out["reference"]["push_us_per_packet_per_process"], 2) if out.get("reference_module") else None
     print(json.dumps(out))
 
 
