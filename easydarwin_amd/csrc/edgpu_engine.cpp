@@ -159,6 +159,7 @@ struct edgpu_ctx {
     int device = 0;
     int num_cus = 256;
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
+    bool deframe_serial = false;    // EDGPU_DEFRAME_SERIAL (measurement): no deframe / fan-out overlap
     uint32_t ablate = 0;
     int timing = EDGPU_TIMING_ALL;  // edgpu_set_timing: which per-launch event pairs are recorded
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
@@ -176,6 +177,7 @@ struct edgpu_ctx {
     // k_ingest waits for ev_deframe
     hipStream_t aux = nullptr;
     hipEvent_t ev_deframe = nullptr;
+    hipEvent_t ev_serial = nullptr;       // EDGPU_DEFRAME_SERIAL
     // the last keyframe index (it reads the segment tables the next deframe rewrites)
     hipEvent_t ev_kf = nullptr;
     bool kf_recorded = false;
@@ -435,6 +437,8 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);
     if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 3);
+    // measurement: the deframe waits for everything enqueued before it (no overlap with the last fan-out)
+    if (const char* v = getenv("EDGPU_DEFRAME_SERIAL")) x->deframe_serial = atoi(v) != 0;
 #endif
     *out = x;
     return EDGPU_OK;
@@ -483,6 +487,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->copy) (void)hipStreamDestroy(x->copy);
     if (x->aux) (void)hipStreamSynchronize(x->aux);
     if (x->ev_deframe) (void)hipEventDestroy(x->ev_deframe);
+    if (x->ev_serial) (void)hipEventDestroy(x->ev_serial);
     if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
     if (x->aux) (void)hipStreamDestroy(x->aux);
     if (x->stream) (void)hipStreamDestroy(x->stream);
@@ -1632,6 +1637,11 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     // the deframe rewrites the segment tables the last keyframe index reads (a reserve above that
     // grew has synchronised `stream`); the fan-out after that index keeps running
     if (x->kf_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_kf, 0));
+    if (x->deframe_serial) {
+        if (!x->ev_serial) HIP_CHECK(hipEventCreateWithFlags(&x->ev_serial, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(x->ev_serial, x->stream));
+        HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_serial, 0));
+    }
     const uint8_t* raw = bytes;
     if (where == EDGPU_PTR_HOST) {
         if (!x->d_tcp_raw && dmalloc(&x->d_tcp_raw, x->cfg.max_batch_bytes) != hipSuccess)
