@@ -122,7 +122,7 @@ def _exchange_worker(rank, world, port, name, out_q):
                     link.own(gid[s], local[s])
                     for t in range(ctx.session_tracks(local[s])):
                         ctx.source_identity(local[s], t, rr_ssrc(s * 16 + t), 0)
-            pending, joins, images, meta = [], [], {}, {}
+            pending, joins, images, meta, places = [], [], {}, {}, {}
             for ev in tr.events:
                 if ev[0] == PKT and rank == 0:
                     pending.append((local[ev[2]], ev[3], ev[1], ev[4]))
@@ -142,13 +142,17 @@ def _exchange_worker(rank, world, port, name, out_q):
                             if gid[j[2]] not in link.replica_of:
                                 local[j[2]] = link.want(gid[j[2]], tr.sdps[j[2]])
                     link.sync(t)                             # collective: images owner -> replica
+                    # collective: the joiners' bucket places, taken in the owner's arrays
+                    given = link.places([("join", j[1], gid[j[2]], int(j[3])) for j in joins] if rank == 1 else [])
                     if rank == 1:
                         for j in joins:
                             h = ctx.subscriber_add(local[j[2]], edgpu.TRANSPORT_TCP if j[4] else edgpu.TRANSPORT_UDP)
+                            ctx.subscriber_set_slot(h, given[int(j[3])])
+                            places[int(j[3])] = given[int(j[3])]
                             meta[h] = (j[3], j[2], j[4])
                             for tk in range(ctx.session_tracks(local[j[2]])):
                                 for k in (0, 1):
-                                    images[(h, tk, k)] = []
+                                    images[(0, h, tk, k)] = []
                         joins = []
                         st, subs, desc, arena = ctx.read_tick(ctx.fanout(t))
                         _wire_images(subs, desc, arena, images)
@@ -156,12 +160,12 @@ def _exchange_worker(rank, world, port, name, out_q):
             if rank == 1:
                 import struct
                 recs = sorted((meta[h][0], meta[h][1], tk, k, meta[h][2], len(p), b"".join(p))
-                              for (h, tk, k), p in images.items())
+                              for (_, h, tk, k), p in images.items())
                 out = [b"EDCP", struct.pack("<I", len(recs))]
                 for sub_id, s, tk, k, tcp, n, data in recs:
                     out.append(struct.pack("<IIHBBQQ", sub_id, s, tk, k, tcp, n, len(data)))
                     out.append(data)
-                result = (hashlib.sha256(b"".join(out)).hexdigest(), link.bytes_received)
+                result = (hashlib.sha256(b"".join(out)).hexdigest(), link.bytes_received, places)
             else:
                 result = link.bytes_sent
             got = [None] * world
@@ -190,7 +194,17 @@ def test_session_images_move_between_engine_processes(name):
         p.join(timeout=120)
     assert got[0] != "error", got
     assert all(p.exitcode == 0 for p in procs)
-    (sent, cross), ((digest, received), _) = got[0], got[1]
+    (sent, cross), ((digest, received, places), _) = got[0], got[1]
     assert cross == (_gpus() >= 2)
     assert sent == received > 0
     assert digest == fix["capture_sha256"]
+    # every join's bucket place came from the owner process: AddOutput's first empty place, in
+    # join order per session (no LEAVE in these traces)
+    from easydarwin_amd.trace import JOIN
+    from test_gpu_parity import _trace
+    n, want = {}, {}
+    for ev in _trace(name).events:
+        if ev[0] == JOIN:
+            want[ev[3]] = n.get(ev[2], 0)
+            n[ev[2]] = want[ev[3]] + 1
+    assert places == want
