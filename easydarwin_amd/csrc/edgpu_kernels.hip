@@ -359,17 +359,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __syncthreads();
 
     uint64_t in_pk = 0, in_bytes = 0;
-#ifdef EDGPU_AB_VARIANTS
-    // phase-stagger experiments (EDGPU_ABLATE bits 8-11: odd segments sleep k x ~3.4 us first;
-    // bit 12: odd segments take a half first round), so that some sessions' header phases meet
-    // other sessions' slot copies
-    if (seg & 1u) for (uint32_t k = 0; k < ((EDGPU_ABL(P) >> 8) & 15u); k++) __builtin_amdgcn_s_sleep(127);
-    uint32_t first_n = ((EDGPU_ABL(P) & 4096u) && (seg & 1u)) ? (uint32_t)THREADS / 2 : (uint32_t)THREADS;
-#else
-    constexpr uint32_t first_n = THREADS;
-#endif
-    for (uint32_t base = b, n = 0; base < e; base += n) {
-        n = min(base == b ? first_n : (uint32_t)THREADS, e - base);
+    for (uint32_t base = b; base < e; base += THREADS) {
+        const uint32_t n = min((uint32_t)THREADS, e - base);
         const uint32_t i = base + tid;
         const bool valid = (uint32_t)tid < n;
         if (tid < (int)nsnd) c_last[tid] = -1;
