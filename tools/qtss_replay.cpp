@@ -537,7 +537,7 @@ static uint64_t stream_writes() {                     // --bench: writes so far,
 struct Pusher {                                        // one synthetic H.264 push (one track)
     uint32_t seq = 0, ts = 0, ssrc = 0, frame = 0;
 };
-static std::atomic<uint64_t> g_pushed{0};             // --bench: RTSPIncomingData calls made
+static std::atomic<uint64_t> g_pushed{0};             // --bench: RTSPIncomingData calls made (per dispatch phase)
 static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
                      QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
     (void)poll_fn;
@@ -589,7 +589,6 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         rp.rtspIncomingDataParams.inPacketData = const_cast<char*>(frame);
         rp.rtspIncomingDataParams.inPacketLen = framelen;
         (void)g_dispatch(QTSS_RTSPIncomingData_Role, &rp);
-        g_pushed.fetch_add(1, std::memory_order_relaxed);
     };
     // The frames of one video frame of session s, built here; `out` (the tick bench: a buffer the
     // pusher thread dispatches from afterwards, so the synthesis is not timed as the module's push)
@@ -789,13 +788,15 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                     while ((int64_t)ps[s].frame * 1000 / fps < t_end) push_frame(s, fr, (int64_t)ps[s].frame * 1000 / fps, &b);
                 built.fetch_add(1);
                 while (!go.load()) std::this_thread::yield();
-                for (size_t at = 0; at < b.size();) {
+                uint64_t np = 0;                          // (counted per thread: no shared line per push)
+                for (size_t at = 0; at < b.size(); np++) {
                     uint32_t s;
                     memcpy(&s, &b[at], 4);
                     const uint32_t len = ((uint32_t)(uint8_t)b[at + 6] << 8) | (uint8_t)b[at + 7];
                     dispatch(s, &b[at + 4], len + 4);
                     at += 4 + len + 4;
                 }
+                g_pushed.fetch_add(np, std::memory_order_relaxed);
             });
         while (built.load() < nthreads) std::this_thread::yield();
         const auto d0 = std::chrono::steady_clock::now();
