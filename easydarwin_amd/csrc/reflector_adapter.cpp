@@ -24,6 +24,9 @@ Reflector::Reflector(const edgpu_config* cfg) {
         fGatherParts = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)atoi(v), edgpu_host::TickParts::kMax));
     if (const char* v = getenv("EDGPU_PRESTAGE_BYTES")) fPrestageBytes = strtoull(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_BATCH_SOURCES")) fBatchSources = atoi(v) != 0;
+    // EDGPU_PUSH_STREAMING=0: the push path copies a slot with cached stores (no fence) instead of
+    // streaming ones -- better when the batch being filled stays in the host's cache
+    if (const char* v = getenv("EDGPU_PUSH_STREAMING")) fPushStreaming = atoi(v) != 0;
     if (fStatus || !fCtx) return;
     edgpu_config c;
     if (cfg) c = *cfg; else edgpu_config_default(&c);
@@ -217,6 +220,13 @@ static void stream_slot(uint8_t* d, const char* p, uint32_t n, uint64_t slot) {
     }
 }
 
+// The same slot with ordinary (cached) stores: header room zeroed, packet, zero pad.
+static void cached_slot(uint8_t* d, const char* p, uint32_t n, uint64_t slot) {
+    memset(d, 0, 4);
+    memcpy(d + 4, p, n);
+    memset(d + 4 + n, 0, slot - 4 - n);
+}
+
 // Appends one packet's slot ([4-B interleave header room][packet][pad to 16]) to the batch being
 // filled: the only host copy of the packet.  Under its stripe's lock the pusher reserves the slot
 // in the stripe's slab (a new 64-KiB slab from the blob when it is full); it copies the packet
@@ -269,8 +279,12 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
         sp = &st;
         break;
     }
-    stream_slot(d, packet, clamped, slot);
-    _mm_sfence();                                        // the slot is complete before it is published
+    if (fPushStreaming) {
+        stream_slot(d, packet, clamped, slot);
+        _mm_sfence();                                    // the slot is complete before it is published
+    } else {
+        cached_slot(d, packet, clamped, slot);           // (ordinary stores: ordered by the release below)
+    }
     if (pend) pend->fetch_sub(1, std::memory_order_release);
     sp->copying.fetch_sub(1, std::memory_order_release);
 }

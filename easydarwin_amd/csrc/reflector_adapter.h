@@ -294,6 +294,7 @@ private:
     const uint8_t* fIngestedBlob = nullptr;                 // the blob the last FlushIngest ingested (intact
                                                             // until the next one swaps it back in)
     bool fBatchSources = true;                              // EDGPU_BATCH_SOURCES=0: read every byte back
+    bool fPushStreaming = true;                             // EDGPU_PUSH_STREAMING=0: cached stores in Append
     std::vector<uint8_t> fSkip;                             // per sub-stream: written from the batch
     uint64_t fGatherSplitBytes = 8ull << 20;               // see ReflectPackets
     uint32_t fGatherParts = 4;                              // EDGPU_GATHER_PARTS (<= TickParts::kMax)
