@@ -537,6 +537,7 @@ static uint64_t stream_writes() {                     // --bench: writes so far,
 struct Pusher {                                        // one synthetic H.264 push (one track)
     uint32_t seq = 0, ts = 0, ssrc = 0, frame = 0;
 };
+static const bool g_bench_trace = getenv("EDGPU_BENCH_TRACE") && atoi(getenv("EDGPU_BENCH_TRACE")) != 0;
 static std::atomic<uint64_t> g_pushed{0};             // --bench: RTSPIncomingData calls made (per dispatch phase)
 static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
                      QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
@@ -826,6 +827,9 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         }
         if (k >= warm) push_s += push_k;
         auto d = std::chrono::steady_clock::now();
+        if (g_bench_trace)                                // EDGPU_BENCH_TRACE=1: every tick's phases
+            fprintf(stderr, "bench tick %u: push %.3f ms (%llu frames), tick %.3f ms\n", k, push_k * 1e3,
+                    (unsigned long long)(g_pushed.load() - p0), std::chrono::duration<double>(c - b).count() * 1e3);
         if (e) {
             fprintf(stderr, "bench: tick %u failed (%d): %s\n", k, (int)e, last_error ? last_error() : "?");
             return 3;
