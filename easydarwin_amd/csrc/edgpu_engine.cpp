@@ -319,6 +319,7 @@ struct edgpu_ctx {
     uint32_t grow_pending = 0;
     uint64_t grow_seen_launch = 0;
     uint64_t ring_grows = 0;
+    uint64_t grow_deferred = 0;     // growth requests left to a later call (the per-call time budget)
     uint64_t ring_bytes = 0;                    // device bytes of the live senders' rings
 };
 
@@ -574,11 +575,13 @@ static void note_grow(edgpu_ctx* x, const TickTotals& t) {
 // The sender's floor becomes `tail`, the oldest entry intact in the old rings: older ones were lost
 // already and must not look intact in the larger rings.  Nothing may be in flight (the caller synced).
 static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t want_by, uint64_t tail,
-                       const uint64_t* expect_head, bool* grown) {
+                       const uint64_t* expect_head, bool* grown, const SenderDev* now = nullptr) {
     *grown = false;
     if (sender >= x->nsenders || !x->snd_meta[sender]) return EDGPU_OK;
     SenderDev D;
-    {
+    if (now) {
+        D = *now;                               // read by the caller, nothing ran since
+    } else {
         Readback rb(x);
         HIP_CHECK(rb.add(&D, x->d_senders.ptr + sender, sizeof(D)));
         HIP_CHECK(rb.run());
@@ -634,6 +637,7 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
 // of what the reference would retain gets that ring grown to the requested size (grow_sender), its
 // floor raised to the tail the plan measured.  A request made before the sender's head moved on (a
 // replica's image apply in between) is dropped; the next plan makes it again.
+static constexpr double kGrowBudgetUs = 4000;   // ring growth per call (grow_rings)
 static int grow_rings(edgpu_ctx* x) {
     uint32_t n = x->grow_pending;
     x->grow_pending = 0;
@@ -654,11 +658,28 @@ static int grow_rings(edgpu_ctx* x) {
         HIP_CHECK(rb.run());
     }
     std::sort(req.begin(), req.end(), [](const GrowReq& a, const GrowReq& b) { return a.sender < b.sender; });
+    req.erase(std::unique(req.begin(), req.end(), [](const GrowReq& a, const GrowReq& b) { return a.sender == b.sender; }),
+              req.end());
+    std::vector<SenderDev> cur(req.size());
+    {   // every requested sender's record in one round trip
+        Readback rb(x);
+        for (size_t k = 0; k < req.size(); k++)
+            if (req[k].sender < x->nsenders) HIP_CHECK(rb.add(&cur[k], x->d_senders.ptr + req[k].sender, sizeof(SenderDev)));
+        HIP_CHECK(rb.run());
+    }
+    // A burst of requests (every C2 video sender passes half its ring within a tick or two) is spread
+    // over ticks: each call grows senders for at most kGrowBudgetUs (at least one); the next plan
+    // re-measures the rest and asks again -- a request means the ring still has half its capacity left.
+    const auto t0 = std::chrono::steady_clock::now();
     for (size_t k = 0; k < req.size(); k++) {
+        if (k && std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kGrowBudgetUs) {
+            x->grow_deferred += req.size() - k;
+            break;
+        }
         const GrowReq& R = req[k];
-        if (k && req[k - 1].sender == R.sender) continue;
         bool grown = false;
-        if (int r = grow_sender(x, R.sender, 1ull << R.pk_log2, 1ull << R.bytes_log2, R.tail, &R.head, &grown)) return r;
+        if (int r = grow_sender(x, R.sender, 1ull << R.pk_log2, 1ull << R.bytes_log2, R.tail, &R.head, &grown, &cur[k]))
+            return r;
     }
     return EDGPU_OK;
 }
