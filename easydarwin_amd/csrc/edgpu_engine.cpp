@@ -114,6 +114,67 @@ struct SourceHost {
     int64_t last_rr = 0;
 };
 
+// Sender rings come from a pool: chunks from hipMalloc carved by a bump pointer, and a free list per
+// size (ring sizes are powers of two: meta rings packets x 36 B, byte rings 2^k B), so ring growth,
+// session add / remove and session churn allocate and free no device memory once the pool holds
+// enough (hipMalloc + hipFree of a ring cost ~0.2 ms: a burst of 1000 growths stalled a tick for
+// a quarter of a second).  Memory stays with the pool until the context is destroyed.
+struct RingPool {
+    static constexpr size_t kChunk = 512ull << 20, kAlign = 4096, kOwn = 128ull << 20;
+    std::vector<void*> chunks;                     // every device allocation (freed at destroy)
+    std::map<size_t, std::vector<void*>> freed;    // by (aligned) size
+    char* cur = nullptr;
+    size_t left = 0, held = 0;
+    static size_t align(size_t b) { return (b + kAlign - 1) & ~(kAlign - 1); }
+    hipError_t get(void** out, size_t bytes) {
+        bytes = align(bytes);
+        auto it = freed.find(bytes);
+        if (it != freed.end() && !it->second.empty()) {
+            *out = it->second.back();
+            it->second.pop_back();
+            return poison(*out, bytes);
+        }
+        void* p = nullptr;
+        if (bytes >= kOwn) {                       // a big ring: its own allocation
+            hipError_t e = dmalloc(&p, bytes);
+            if (e != hipSuccess) return e;
+            chunks.push_back(p);
+            held += bytes;
+            *out = p;
+            return hipSuccess;
+        }
+        if (bytes > left) {
+            hipError_t e = dmalloc(&p, kChunk);
+            if (e != hipSuccess) {                 // no room for a whole chunk: this ring alone
+                (void)hipGetLastError();
+                if ((e = dmalloc(&p, bytes)) != hipSuccess) return e;
+                chunks.push_back(p);
+                held += bytes;
+                *out = p;
+                return hipSuccess;
+            }
+            chunks.push_back(p);
+            held += kChunk;
+            cur = (char*)p;
+            left = kChunk;
+        }
+        *out = cur;
+        cur += bytes;
+        left -= bytes;
+        return poison(*out, bytes);
+    }
+    void put(void* p, size_t bytes) { if (p) freed[align(bytes)].push_back(p); }
+    static hipError_t poison(void* p, size_t n) {  // EDGPU_POISON: as a fresh allocation
+        if (!poison_on()) return hipSuccess;
+        hipError_t e = hipMemset(p, 0xA5, n);
+        return e == hipSuccess ? hipDeviceSynchronize() : e;
+    }
+    void release() {
+        for (void* p : chunks) (void)hipFree(p);
+        chunks.clear(); freed.clear(); cur = nullptr; left = held = 0;
+    }
+};
+
 // Bucket-array entries besides a subscriber handle (SessionHost::slots)
 constexpr int32_t kPlaceFree = -1, kPlaceRemote = -2;
 constexpr uint32_t kMaxPlaces = 1u << 20;
@@ -320,6 +381,7 @@ struct edgpu_ctx {
     uint64_t grow_seen_launch = 0;
     uint64_t ring_grows = 0;
     uint64_t grow_deferred = 0;     // growth requests left to a later call (the per-call time budget)
+    RingPool rings;                 // every sender's meta and byte rings
     uint64_t ring_bytes = 0;                    // device bytes of the live senders' rings
 };
 
@@ -450,8 +512,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     (void)hipSetDevice(x->device);
     if (x->stream) (void)hipStreamSynchronize(x->stream);
     if (x->copy) (void)hipStreamSynchronize(x->copy);
-    for (void* p : x->snd_meta) if (p) (void)hipFree(p);
-    for (void* p : x->snd_ring) if (p) (void)hipFree(p);
+    x->rings.release();                          // (every sender's rings)
     if (x->d_null) (void)hipFree(x->d_null);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
@@ -598,7 +659,7 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
     void* nmeta = meta;
     void* nring = ring;
     if (new_pk > old_pk) {
-        if (dmalloc(&nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess)
+        if (x->rings.get(&nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess)
             return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender meta ring");
         const uint64_t lo = D.head > old_pk ? D.head - old_pk : 0;
         HIP_CHECK(launch_ring_move(0, meta, old_pk - 1, nmeta, new_pk - 1, lo, D.head - lo, x->stream));
@@ -606,8 +667,8 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
                                    (uint8_t*)nmeta + new_pk * sizeof(PktMeta), new_pk - 1, lo, D.head - lo, x->stream));
     }
     if (new_by > old_by) {
-        if (dmalloc(&nring, new_by) != hipSuccess) {
-            if (nmeta != meta) (void)hipFree(nmeta);
+        if (x->rings.get(&nring, new_by) != hipSuccess) {
+            if (nmeta != meta) x->rings.put(nmeta, new_pk * (sizeof(PktMeta) + sizeof(uint32_t)));
             return fail(EDGPU_OUT_OF_MEMORY, "ring growth: sender byte ring");
         }
         const uint64_t wend = D.vbyte_end / 16, wlo = wend > old_by / 16 ? wend - old_by / 16 : 0;
@@ -620,8 +681,8 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
     D.floor = std::max(D.floor, tail);
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sender, &D, sizeof(D), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipStreamSynchronize(x->stream));
-    if (nmeta != meta) HIP_CHECK(hipFree(meta));
-    if (nring != ring) HIP_CHECK(hipFree(ring));
+    if (nmeta != meta) x->rings.put(meta, old_pk * (sizeof(PktMeta) + sizeof(uint32_t)));
+    if (nring != ring) x->rings.put(ring, old_by);
     x->snd_meta[sender] = nmeta;
     x->snd_ring[sender] = nring;
     x->work_cap_needed += new_pk / 16 - old_pk / 16;
@@ -661,17 +722,22 @@ static int grow_rings(edgpu_ctx* x) {
     req.erase(std::unique(req.begin(), req.end(), [](const GrowReq& a, const GrowReq& b) { return a.sender == b.sender; }),
               req.end());
     std::vector<SenderDev> cur(req.size());
-    {   // every requested sender's record in one round trip
+    const auto tr = std::chrono::steady_clock::now();
+    {   // the sender table in one copy (one small copy per sender costs ~10 us each)
+        std::vector<SenderDev> all(x->nsenders);
         Readback rb(x);
-        for (size_t k = 0; k < req.size(); k++)
-            if (req[k].sender < x->nsenders) HIP_CHECK(rb.add(&cur[k], x->d_senders.ptr + req[k].sender, sizeof(SenderDev)));
+        HIP_CHECK(rb.add(all.data(), x->d_senders.ptr, all.size() * sizeof(SenderDev)));
         HIP_CHECK(rb.run());
+        for (size_t k = 0; k < req.size(); k++)
+            if (req[k].sender < x->nsenders) cur[k] = all[req[k].sender];
     }
+    const double read_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
     // A burst of requests (every C2 video sender passes half its ring within a tick or two) is spread
     // over ticks: each call grows senders for at most kGrowBudgetUs (at least one); the next plan
     // re-measures the rest and asks again -- a request means the ring still has half its capacity left.
     const auto t0 = std::chrono::steady_clock::now();
-    for (size_t k = 0; k < req.size(); k++) {
+    size_t k = 0;
+    for (; k < req.size(); k++) {
         if (k && std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kGrowBudgetUs) {
             x->grow_deferred += req.size() - k;
             break;
@@ -681,6 +747,10 @@ static int grow_rings(edgpu_ctx* x) {
         if (int r = grow_sender(x, R.sender, 1ull << R.pk_log2, 1ull << R.bytes_log2, R.tail, &R.head, &grown, &cur[k]))
             return r;
     }
+    static const bool dbg = getenv("EDGPU_DEBUG_GROW") != nullptr;
+    if (dbg)
+        fprintf(stderr, "edgpu: ring growth: %zu of %zu requests in %.3f ms (read %.3f ms)\n", k, req.size(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), read_ms);
     return EDGPU_OK;
 }
 
@@ -815,13 +885,15 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
     }
     std::vector<SenderDev> snd(nsnd);
     std::vector<StreamDev> str(sh.ntracks);
-    auto undo = [&](uint32_t upto) {            // frees the rings allocated so far
-        for (uint32_t i = 0; i < upto; i++)
-            for (auto* v : {&x->snd_meta, &x->snd_ring}) {
-                void*& p = (*v)[first_sender + i];
-                if (p) (void)hipFree(p);
-                p = nullptr;
-            }
+    std::vector<std::pair<uint64_t, uint64_t>> sizes(nsnd);   // (packets, bytes) per sender
+    auto undo = [&](uint32_t upto) {            // returns the rings allocated so far
+        for (uint32_t i = 0; i < upto; i++) {
+            void*& m = x->snd_meta[first_sender + i];
+            void*& r = x->snd_ring[first_sender + i];
+            x->rings.put(m, sizes[i].first * (sizeof(PktMeta) + sizeof(uint32_t)));
+            x->rings.put(r, sizes[i].second);
+            m = r = nullptr;
+        }
     };
     for (uint32_t t = 0; t < sh.ntracks; t++) {
         uint32_t base = 0;
@@ -837,9 +909,10 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
             void* meta = nullptr; void* ring = nullptr;
             const uint32_t gs = first_sender + 2 * t + k;
             // the meta ring, then a uint32 blob slot per entry (edgpu_fanout_packet_info)
-            if (dmalloc(&meta, pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess) { undo(2 * t + k); return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring"); }
+            sizes[2 * t + k] = {pk, by};
+            if (x->rings.get(&meta, pk * (sizeof(PktMeta) + sizeof(uint32_t))) != hipSuccess) { undo(2 * t + k); return fail(EDGPU_OUT_OF_MEMORY, "sender meta ring"); }
             x->snd_meta[gs] = meta;
-            if (dmalloc(&ring, by) != hipSuccess) { undo(2 * t + k + 1); return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring"); }
+            if (x->rings.get(&ring, by) != hipSuccess) { undo(2 * t + k + 1); return fail(EDGPU_OUT_OF_MEMORY, "sender byte ring"); }
             x->snd_ring[gs] = ring;
             D.meta = (uint64_t)(uintptr_t)meta;
             D.ring = (uint64_t)(uintptr_t)ring;
@@ -928,11 +1001,10 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
                          ((uint64_t)old[i].word_mask + 1) * 16;
         snd[i].stream = old[i].stream;
         snd[i].track = old[i].track;
-        for (auto* v : {&x->snd_meta, &x->snd_ring}) {
-            void*& p = (*v)[gs];
-            if (p) HIP_CHECK(hipFree(p));
-            p = nullptr;
-        }
+        // the rings go back to the pool (a later session or growth takes them)
+        x->rings.put(x->snd_meta[gs], ((uint64_t)old[i].pk_mask + 1) * (sizeof(PktMeta) + sizeof(uint32_t)));
+        x->rings.put(x->snd_ring[gs], ((uint64_t)old[i].word_mask + 1) * 16);
+        x->snd_meta[gs] = x->snd_ring[gs] = nullptr;
     }
     std::vector<StreamDev> str(sh.ntracks);
     for (auto& st : str) st.packet_count = 0;

@@ -1,13 +1,12 @@
-# round 5: ring growth spread over ticks by a per-call time budget -- the growth tests, the module
-# suites, and the per-tick trace of a 15-s C2 module run (the growth burst at ~8 s of stream).
+# round 5: sender rings from a pool -- the full GPU suite, then the growth trace of a 15-s C2 module run.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${1:-r05p}
+O=$R/gpurun_out/${1:-r05r}
 mkdir -p $O
 cd $R
-[ -n "$SKIPTESTS" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_ring_growth.py tests/test_gpu_qtss_module.py tests/test_gpu_isolation.py tests/test_gpu_replica.py \
-    -q -x --timeout 150 --timeout-method thread -p no:cacheprovider > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
-tail -1 $O/gputest.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf --timeout 150 --timeout-method thread -p no:cacheprovider > $O/gputests.log 2>&1; rc=$?
+echo "gpu tests rc=$rc"; grep -E "FAILED|Timeout" $O/gputests.log | head -20; tail -1 $O/gputests.log
+[ $rc -ne 0 ] && exit $rc
 EDGPU_DEBUG_GROW=1 EDGPU_BENCH_TRACE=1 EDGPU_QTSS_WRITE_THREADS=16 EDGPU_QTSS_ARENA_MB=4096 EDGPU_QTSS_MAX_OUT_PACKETS=4194304 \
   timeout -k 10 200 $R/tools/qtss_replay $R/easydarwin_amd/libQTSSReflectorModule.so --bench 1024 16 15 100 8 > $O/trace.json 2> $O/trace.err || exit 1
 python3 - $O/trace.err <<'PY'
@@ -15,4 +14,6 @@ import re, sys
 rows = [(int(re.search(r"tick (\d+):", l).group(1)), float(re.search(r"tick ([\d.]+) ms", l).group(1))) for l in open(sys.argv[1]) if l.startswith("bench tick")]
 big = sorted(rows, key=lambda r: -r[1])[:8]
 print("slowest ticks", big, "median", sorted(r[1] for r in rows)[len(rows) // 2])
+g = [l.strip() for l in open(sys.argv[1]) if "ring growth" in l]
+print(len(g), "growth calls;", g[:4])
 PY
