@@ -64,3 +64,24 @@ def test_growth_stops_at_its_bound():
     with _ctx(tr, max_ring_bytes=8 << 20, max_ring_packets=8192) as ctx:
         replay(tr, ctx=ctx)
         assert ctx.counters()["ring_grows"] == 0
+
+
+@pytest.mark.gpu
+def test_pooled_rings_are_reused_clean():
+    """Rings come from a pool (edgpu_engine.cpp RingPool): a session that grew its rings and ended
+    returns them, and the next session of the context takes them -- with whatever bytes the last
+    owner left in them.  ``highrate`` replayed three times into one context, its session removed
+    in between, must match the reference byte for byte each time, and the counters must come back
+    to the empty context's rings."""
+    tr = _trace("highrate")
+    with _ctx(tr) as ctx:
+        c0 = ctx.counters()
+        for k in range(3):
+            cap, _ = replay(tr, ctx=ctx)
+            assert ctx.stream_errors() == []
+            assert hashlib.sha256(cap).hexdigest() == _fixture("highrate")["capture_sha256"], k
+            for s in range(len(tr.sdps)):            # (a removed session's id is reused by the next)
+                ctx.session_remove(s, kill_outputs=True)
+            c = ctx.counters()
+            assert c["ring_bytes"] == c0["ring_bytes"], k
+            assert c["ring_grows"] >= 2 * (k + 1)
