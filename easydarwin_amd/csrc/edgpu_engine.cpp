@@ -498,7 +498,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
 #ifdef EDGPU_AB_VARIANTS                         // measurement builds only (edgpu_params.h)
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);
-    if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
+    if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)std::min(std::max(atoi(v), 0), 2);
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 3);
     // measurement: the deframe waits for everything enqueued before it (no overlap with the last fan-out)
     if (const char* v = getenv("EDGPU_DEFRAME_SERIAL")) x->deframe_serial = atoi(v) != 0;

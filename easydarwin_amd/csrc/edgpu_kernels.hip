@@ -715,6 +715,37 @@ __global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
         if (j.vword + k >= live) ring[(j.vword + k) & j.wmask] = v;
     }
 }
+
+// The same flat copy with every lane's words loaded before its first store (EDGPU_INGEST=2): a
+// slot is at most 129 words, so 16 lanes hold it in <= 9 registers of 16 B each; low register use
+// keeps many waves -- and their loads -- in flight per CU.
+__global__ __launch_bounds__(kCopyThreads) void k_ingest_copy2(IngestParams P) {
+    const uint32_t g = blockIdx.x * (kCopyThreads / kCopyLanes) + threadIdx.x / kCopyLanes;
+    const uint32_t lane = threadIdx.x % kCopyLanes;
+    if (g >= P.npk) return;
+    const CopyJob j = P.jobs[g];
+    if (j.len == 0) return;
+    const uint32_t nw = (j.len + 4 + 15) >> 4;
+    const uint64_t vend = P.senders[j.sender].vbyte_end >> 4, cap = (uint64_t)j.wmask + 1;
+    const uint64_t live = vend > cap ? vend - cap : 0ull;
+    const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)j.src_slot * 16);
+    u32x4* ring = reinterpret_cast<u32x4*>(j.ring);
+    constexpr uint32_t kMaxW = (kSlotWordsMax + kCopyLanes - 1) / kCopyLanes;
+    u32x4 v[kMaxW];
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxW; i++) {
+        const uint32_t k = lane + i * kCopyLanes;
+        if (k < nw) v[i] = __builtin_nontemporal_load(src + k);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxW; i++) {
+        const uint32_t k = lane + i * kCopyLanes;
+        if (k < nw) {
+            if (k == 0) v[i].x = slot_header(j.len);
+            if (j.vword + k >= live) ring[(j.vword + k) & j.wmask] = v[i];
+        }
+    }
+}
 #endif  // EDGPU_AB_VARIANTS
 
 // =========================================================================================
@@ -2588,9 +2619,10 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
     else if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
-    if (p.npk && EDGPU_COPY_MODE(p) == 1) {
+    if (p.npk && EDGPU_COPY_MODE(p) != 0) {
         const uint32_t per = kCopyThreads / kCopyLanes;
-        hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+        if (EDGPU_COPY_MODE(p) == 2) hipLaunchKernelGGL(k_ingest_copy2, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+        else hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
 #else
     hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
