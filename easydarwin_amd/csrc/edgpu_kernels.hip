@@ -722,11 +722,18 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 // =========================================================================================
 constexpr int kCopyThreads = 256, kCopyLanes = 16;
 
-__device__ __forceinline__ u32x4 row_next16(u32x4 v) {          // lane l <- lane (l + 1) % 16 of its row
-    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x12F, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x12F, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x12F, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x12F, 0xF, 0xF, false)};
+// Lane l of a 16-lane row gets lane l + 1's value of `v` (DPP row_shl:1); lane 15 of the row keeps `v`
+// (the caller takes its word from the row's lane 0 instead).
+__device__ __forceinline__ u32x4 row_next16(u32x4 v) {
+    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp((int)v.x, (int)v.x, 0x101, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.y, (int)v.y, 0x101, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.z, (int)v.z, 0x101, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.w, (int)v.w, 0x101, 0xF, 0xF, false)};
+}
+// The row's lane 0 value of `v`, for every lane of the row
+__device__ __forceinline__ u32x4 row_first16(u32x4 v, int src) {
+    return u32x4{(uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
+                 (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64)};
 }
 
 __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
@@ -762,12 +769,13 @@ __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
         const uint64_t vend = D.vbyte_end >> 4, cap = (uint64_t)wm + 1;
         live = vend > cap ? vend - cap : 0ull;
     }
-    u32x4 nxt = row_next16(blk[0]);
+    const int row0 = (int)(threadIdx.x & 63u) & ~(kCopyLanes - 1);   // the row's lane 0 in the wave
 #pragma unroll
     for (uint32_t i = 0; i < kB; i++) {
-        const u32x4 nxt1 = row_next16(blk[i + 1]);
-        const u32x4 hi = lane == kCopyLanes - 1 ? nxt1 : nxt;    // block w + 1
-        nxt = nxt1;
+        // block w + 1: the next lane's block i, or for lane 15 the row's lane 0's block i + 1
+        const u32x4 nb = row_next16(blk[i]);
+        const u32x4 wrap = row_first16(blk[i + 1], row0);
+        const u32x4 hi = lane == kCopyLanes - 1 ? wrap : nb;
         const uint32_t w = lane + i * kCopyLanes;
         if (w < nw) {
             u32x4 v = funnel16(blk[i], hi, sh);
