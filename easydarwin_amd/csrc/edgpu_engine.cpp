@@ -23,7 +23,7 @@
 
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
-hipError_t launch_slot_copy(const IngestParams& p, hipStream_t st);
+hipError_t launch_slot_copy(const IngestParams& p, uint32_t max_packets, uint32_t num_cus, hipStream_t st);
 bool fanout_reads_senders(int variant);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
@@ -1491,7 +1491,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
+    p.jobs = x->d_jobs; p.npk = n; p.nseg = nseg; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.totals = x->d_totals;
     p.tcp_groups = tcp ? tcp->groups : nullptr;
@@ -1522,7 +1522,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
         q.copy_mode = kCopySerial;
         q.overlap = 0;
         HIP_CHECK(launch_ingest(q, nseg, x->stream));
-        HIP_CHECK(launch_slot_copy(p, x->stream));
+        HIP_CHECK(launch_slot_copy(p, n ? n : x->cfg.max_batch_packets, (uint32_t)x->num_cus, x->stream));
         HIP_CHECK(hist_mark(x, 2, 1));
     } else {
         HIP_CHECK(hist_mark(x, 2, 0));

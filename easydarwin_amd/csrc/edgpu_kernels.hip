@@ -739,10 +739,14 @@ __device__ __forceinline__ u32x4 row_first16(u32x4 v, int src) {
 __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
     static_assert(kCopyLanes == 16, "row_next16 works on DPP rows of 16 lanes");
     constexpr uint32_t kB = (kSlotWordsMax + kCopyLanes - 1) / kCopyLanes;   // blocks per lane (9)
-    const uint32_t g = blockIdx.x * (kCopyThreads / kCopyLanes) + threadIdx.x / kCopyLanes;
+    constexpr uint32_t kPer = kCopyThreads / kCopyLanes;
     const uint32_t lane = threadIdx.x % kCopyLanes;
-    // (no early return: every lane of a row takes part in the DPP exchange)
-    const bool live_pk = g < P.npk;
+    const uint32_t npk = P.seg_off[P.nseg];                        // (interleaved: found by the deframe)
+    // a grid-stride loop over packets (the interleaved batch's count is known on the device only);
+    // the bound is uniform per workgroup, and every lane of a row takes part in the exchanges
+    for (uint32_t g0 = blockIdx.x * kPer; g0 < npk; g0 += gridDim.x * kPer) {
+    const uint32_t g = g0 + threadIdx.x / kCopyLanes;
+    const bool live_pk = g < npk;
     CopyJob j;
     j.src = 0; j.vword = 0; j.sender = 0; j.len = 0;
     if (live_pk) j = P.jobs[g];
@@ -783,6 +787,7 @@ __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
             v = keep16(v, (int)fl - 16 * (int)w);
             if (j.vword + w >= live) reinterpret_cast<u32x4*>(ring)[(j.vword + w) & wm] = v;
         }
+    }
     }
 }
 
@@ -2663,10 +2668,11 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     return hipGetLastError();
 }
 // The split ingest's slot copy (after k_ingest kCopyHeader)
-hipError_t launch_slot_copy(const IngestParams& p, hipStream_t st) {
-    if (p.npk == 0) return hipSuccess;
+hipError_t launch_slot_copy(const IngestParams& p, uint32_t max_packets, uint32_t num_cus, hipStream_t st) {
+    if (p.nseg == 0) return hipSuccess;
     const uint32_t per = kCopyThreads / kCopyLanes;
-    hipLaunchKernelGGL(k_slot_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+    const uint32_t grid = std::max(1u, std::min((max_packets + per - 1) / per, num_cus * 8));
+    hipLaunchKernelGGL(k_slot_copy, dim3(grid), dim3(kCopyThreads), 0, st, p);
     return hipGetLastError();
 }
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {

@@ -49,7 +49,8 @@ struct IngestParams {
     uint64_t* pidx;         // per desc: sender queue index
     CopyJob* jobs;          // per desc: slot copy for k_slot_copy
     uint8_t* seg_serial;    // per segment (copy modes 1 / 2): the header pass left it to the serial pass
-    uint32_t npk;           // descriptors in the batch
+    uint32_t npk;           // descriptors in the batch (0 for interleaved reads: seg_off[nseg] counts the frames)
+    uint32_t nseg;          // segments (k_slot_copy reads the packet count at seg_off[nseg])
     uint32_t copy_mode;     // kCopyFused: header work and slot copy in k_ingest; kCopyHeader: the header
                             // pass (beside the last fan-out), jobs for k_slot_copy; kCopySerial: the
                             // fused ingest of the segments the header pass left (seg_serial)
