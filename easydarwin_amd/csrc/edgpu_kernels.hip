@@ -361,16 +361,60 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __syncthreads();
     // Split ingest.  The serial pass (after the fan-out) takes only the segments the header pass left.
     // The header pass may run beside the last tick's fan-out: a segment whose batch could lap the
-    // window that fan-out reads (fan_lo / fan_vlo, from its plan) -- counted as if every packet went
-    // to one sender, at the largest slot -- is left whole to the serial pass, its jobs emptied.
+    // window that fan-out reads (fan_lo / fan_vlo, from its plan) in any sender's ring -- its packets
+    // counted per sender, each at its slot size, before the SSRC filter -- is left whole to the
+    // serial pass, its jobs emptied.
     if (EDGPU_COPY_MODE(P) == kCopySerial && !P.seg_serial[seg]) return;          // uniform
     if (EDGPU_COPY_MODE(P) == kCopyHeader) {
-        if (P.overlap && tid < (int)nsnd) {
-            const SenderDev& D = P.senders[S.first_sender + tid];
-            const uint64_t np = e - b;
-            if (s_head[tid] + np > D.fan_lo + (uint64_t)s_pkmask[tid] + 1 ||
-                s_vbyte[tid] + np * (uint64_t)(kSlotWordsMax * 16) > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16)
-                s_risky = 1;
+        if (P.overlap) {
+            if (tid < (int)nsnd) { c_tot[tid] = 0; c_last[tid] = 0; }
+            __syncthreads();
+            for (uint32_t i = b + tid; i < e; i += THREADS) {
+                uint32_t ch = 0, ln = 0;
+                bool found = false;
+                if (P.tcp_groups) {                   // the frame's '$' ch BE16(len) header
+                    const uint32_t j = i - b;
+                    uint32_t lo = 0, hi = G.nchunks - 1;
+                    const bool lds = G.nchunks <= kLdsChunks;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        uint32_t ce;
+                        if (lds) ce = t_cend[mid];
+                        else { const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + mid]; ce = R.fbase + R.nframes; }
+                        if (ce > j) hi = mid; else lo = mid + 1;
+                    }
+                    uint32_t rec, fbase;
+                    if (lds) { rec = t_crec[lo]; fbase = lo ? t_cend[lo - 1] : 0u; }
+                    else {
+                        const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + lo];
+                        rec = R.entry != kTcpNone && R.nframes <= kTcpFrames ? R.cand : kTcpNone;
+                        fbase = R.fbase;
+                    }
+                    if (rec != kTcpNone) {
+                        const uint64_t pos = (uint64_t)lo * kTcpChunk +
+                                             P.tcp_offs[((size_t)(G.first_chunk + lo) * kTcpCands + rec) * kTcpFrames + (j - fbase)];
+                        const uint8_t* sp = pos >= G.carry_len ? P.tcp_raw + G.raw_off + (pos - G.carry_len)
+                                                               : P.tcp_stage + (uint64_t)seg * kTcpCarry;
+                        ch = sp[1];
+                        ln = (uint32_t)sp[2] << 8 | sp[3];
+                        found = true;
+                    }
+                }
+                if (!found) { const edgpu_pkt_desc d = P.desc[i]; ch = d.channel; ln = d.len; }
+                ln = min(ln, (uint32_t)kMaxPacket);
+                const uint32_t l = 2 * (ch >> 1) + (ch & 1);
+                if ((ch >> 1) < S.ntracks && ln > 0) {
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&c_tot[l]), (unsigned long long)((ln + 4 + 15) & ~15u));
+                    atomicAdd(reinterpret_cast<uint32_t*>(&c_last[l]), 1u);
+                }
+            }
+            __syncthreads();
+            if (tid < (int)nsnd) {
+                const SenderDev& D = P.senders[S.first_sender + tid];
+                if (s_head[tid] + (uint32_t)c_last[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1 ||
+                    s_vbyte[tid] + c_tot[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16)
+                    s_risky = 1;
+            }
         }
         __syncthreads();
         const bool risky = s_risky != 0;
