@@ -889,6 +889,8 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
     sh.src.resize(sh.ntracks);
     for (auto& h : sh.src) { h.rr_ssrc = (uint32_t)::rand(); h.cname = source_cname(wall_ms / 1000); }
     const uint32_t nsnd = 2 * sh.ntracks;
+    if (!reuse && x->nsenders + nsnd > (1u << 20))          // (CopyJob::sender is 20 bits)
+        return fail(EDGPU_OUT_OF_MEMORY, "more than 2^20 senders in one context");
     if (!reuse) {
         HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
         HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));

@@ -704,8 +704,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             CopyJob j;
             j.src = src;
             j.vword = vb >> 4;
-            j.sender = S.first_sender + ls;
+            j.ring = acc ? s_ring[ls] : 0ull;
+            j.wmask = acc ? s_wmask[ls] : 0u;
             j.len = slotb ? len : 0u;
+            j.sender = S.first_sender + ls;
             P.jobs[i] = j;
         }
         // ---- advance per-sender / per-stream state ----
@@ -766,22 +768,23 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 // =========================================================================================
 constexpr int kCopyThreads = 256, kCopyLanes = 16;
 
-// Lane l of a 16-lane row gets lane l + 1's value of `v` (DPP row_shl:1); lane 15 of the row keeps `v`
-// (the caller takes its word from the row's lane 0 instead).
+// Lane l of a 16-lane row gets lane l + 1's value of `v` (DPP row_shl:1); lane 15 of the row keeps `v`.
 __device__ __forceinline__ u32x4 row_next16(u32x4 v) {
     return u32x4{(uint32_t)__builtin_amdgcn_update_dpp((int)v.x, (int)v.x, 0x101, 0xF, 0xF, false),
                  (uint32_t)__builtin_amdgcn_update_dpp((int)v.y, (int)v.y, 0x101, 0xF, 0xF, false),
                  (uint32_t)__builtin_amdgcn_update_dpp((int)v.z, (int)v.z, 0x101, 0xF, 0xF, false),
                  (uint32_t)__builtin_amdgcn_update_dpp((int)v.w, (int)v.w, 0x101, 0xF, 0xF, false)};
 }
-// The row's lane 0 value of `v`, for every lane of the row
-__device__ __forceinline__ u32x4 row_first16(u32x4 v, int src) {
-    return u32x4{(uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
-                 (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64)};
+// Lane l of a 16-lane row gets lane 15 - l's value (DPP row_mirror): lane 15 gets the row's lane 0.
+__device__ __forceinline__ u32x4 row_mirror16(u32x4 v) {
+    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp((int)v.x, (int)v.x, 0x140, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.y, (int)v.y, 0x140, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.z, (int)v.z, 0x140, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.w, (int)v.w, 0x140, 0xF, 0xF, false)};
 }
 
 __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
-    static_assert(kCopyLanes == 16, "row_next16 works on DPP rows of 16 lanes");
+    static_assert(kCopyLanes == 16, "the DPP exchanges work on rows of 16 lanes");
     constexpr uint32_t kB = (kSlotWordsMax + kCopyLanes - 1) / kCopyLanes;   // blocks per lane (9)
     constexpr uint32_t kPer = kCopyThreads / kCopyLanes;
     const uint32_t lane = threadIdx.x % kCopyLanes;
@@ -789,49 +792,47 @@ __global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
     // a grid-stride loop over packets (the interleaved batch's count is known on the device only);
     // the bound is uniform per workgroup, and every lane of a row takes part in the exchanges
     for (uint32_t g0 = blockIdx.x * kPer; g0 < npk; g0 += gridDim.x * kPer) {
-    const uint32_t g = g0 + threadIdx.x / kCopyLanes;
-    const bool live_pk = g < npk;
-    CopyJob j;
-    j.src = 0; j.vword = 0; j.sender = 0; j.len = 0;
-    if (live_pk) j = P.jobs[g];
-    const uint32_t fl = j.len ? 4u + j.len : 0u;                 // frame bytes ('$'-header room + packet)
-    const uint32_t nw = (fl + 15) >> 4;
-    const uint64_t a0 = j.src & ~15ull;
-    const uint32_t sh = (uint32_t)(j.src & 15);
-    const uint32_t nblk = fl ? (uint32_t)((j.src + fl - 1 - a0) >> 4) + 1 : 0u;
-    const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
-    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-    u32x4 blk[kB + 1];
+        const uint32_t g = g0 + threadIdx.x / kCopyLanes;
+        CopyJob j;
+        j.src = 0; j.vword = 0; j.ring = 0; j.wmask = 0; j.len = 0; j.sender = 0;
+        if (g < npk) j = P.jobs[g];
+        const uint32_t fl = j.len ? 4u + j.len : 0u;               // frame bytes ('$'-header room + packet)
+        const uint32_t nw = (fl + 15) >> 4;
+        const uint64_t a0 = j.src & ~15ull;
+        const uint32_t sh = (uint32_t)(j.src & 15);
+        const uint32_t nblk = fl ? (uint32_t)((j.src + fl - 1 - a0) >> 4) + 1 : 0u;
+        const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
+        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+        u32x4 blk[kB + 1];
 #pragma unroll
-    for (uint32_t i = 0; i < kB; i++) {
-        const uint32_t w = lane + i * kCopyLanes;
-        blk[i] = w < nblk ? __builtin_nontemporal_load(ab + w) : z;
-    }
-    blk[kB] = z;
-    uint64_t ring = 0, live = 0;
-    uint32_t wm = 0;
-    if (nw) {
-        const SenderDev& D = P.senders[j.sender];
-        ring = D.ring;
-        wm = D.word_mask;
-        const uint64_t vend = D.vbyte_end >> 4, cap = (uint64_t)wm + 1;
-        live = vend > cap ? vend - cap : 0ull;
-    }
-    const int row0 = (int)(threadIdx.x & 63u) & ~(kCopyLanes - 1);   // the row's lane 0 in the wave
-#pragma unroll
-    for (uint32_t i = 0; i < kB; i++) {
-        // block w + 1: the next lane's block i, or for lane 15 the row's lane 0's block i + 1
-        const u32x4 nb = row_next16(blk[i]);
-        const u32x4 wrap = row_first16(blk[i + 1], row0);
-        const u32x4 hi = lane == kCopyLanes - 1 ? wrap : nb;
-        const uint32_t w = lane + i * kCopyLanes;
-        if (w < nw) {
-            u32x4 v = funnel16(blk[i], hi, sh);
-            if (w == 0) v.x = slot_header(j.len);
-            v = keep16(v, (int)fl - 16 * (int)w);
-            if (j.vword + w >= live) reinterpret_cast<u32x4*>(ring)[(j.vword + w) & wm] = v;
+        for (uint32_t i = 0; i < kB; i++) {
+            const uint32_t w = lane + i * kCopyLanes;
+            blk[i] = w < nblk ? __builtin_nontemporal_load(ab + w) : z;
         }
-    }
+        blk[kB] = z;
+        uint64_t live = 0;
+        if (nw) {
+            const uint64_t vend = P.senders[j.sender].vbyte_end >> 4, cap = (uint64_t)j.wmask + 1;
+            live = vend > cap ? vend - cap : 0ull;
+        }
+        u32x4* ring = reinterpret_cast<u32x4*>(j.ring);
+        const bool misaligned = __ballot(sh != 0) != 0;            // (descriptor batches: never)
+#pragma unroll
+        for (uint32_t i = 0; i < kB; i++) {
+            const uint32_t w = lane + i * kCopyLanes;
+            u32x4 v = blk[i];
+            if (misaligned) {
+                // block w + 1: the next lane's block i, or for lane 15 the row's lane 0's block i + 1
+                const u32x4 nb = row_next16(blk[i]);
+                const u32x4 wrap = row_mirror16(blk[i + 1]);
+                v = funnel16(blk[i], lane == kCopyLanes - 1 ? wrap : nb, sh);
+            }
+            if (w < nw) {
+                if (w == 0) v.x = slot_header(j.len);
+                v = keep16(v, (int)fl - 16 * (int)w);
+                if (j.vword + w >= live) ring[(j.vword + w) & j.wmask] = v;
+            }
+        }
     }
 }
 
