@@ -44,14 +44,13 @@ struct PktMeta {                    // 32 B
     uint32_t vcount;                // number of non-empty packets before this one (mod 2^32)
 };
 
-struct CopyJob {                    // 32 B: one enqueued packet's slot copy into its sender's byte ring
-    uint64_t src;                   // device address of the slot's first byte: the batch blob slot, or
-                                    // the frame's '$' in the TCP bytes (any alignment)
-    uint64_t vword;                 // virtual word index of the slot in the ring
-    uint64_t ring;                  // the sender's byte ring (16-B words)
+struct CopyJob {                    // 32 B: one enqueued packet's slot copy, blob -> byte ring
+    uint64_t ring;                  // device pointer of the sender's byte ring (16-B words)
+    uint64_t vword;                 // virtual word index of the slot
     uint32_t wmask;                 // ring words - 1
-    uint32_t len : 12;              // packet length, <= 2060 (0: nothing to copy)
-    uint32_t sender : 20;           // global sender index (its vbyte_end bounds the live words)
+    uint32_t src_slot;              // slot index in the batch blob
+    uint32_t len;                   // packet length (0: nothing to copy)
+    uint32_t sender;                // global sender index (its vbyte_end bounds the live words)
 };
 
 struct SenderDev {

@@ -23,8 +23,6 @@
 
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
-hipError_t launch_slot_copy(const IngestParams& p, uint32_t max_packets, uint32_t num_cus, hipStream_t st);
-bool fanout_reads_senders(int variant);
 hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
@@ -225,14 +223,7 @@ struct edgpu_ctx {
     bool deframe_serial = false;    // EDGPU_DEFRAME_SERIAL (measurement): no deframe / fan-out overlap
     uint32_t ablate = 0;
     int timing = EDGPU_TIMING_ALL;  // edgpu_set_timing: which per-launch event pairs are recorded
-    // The split ingest (default; EDGPU_INGEST_SPLIT=0 for the fused one): k_ingest's header pass on
-    // `aux` beside the last tick's fan-out, then k_slot_copy (and the serial pass of any segment
-    // the header pass left) on `stream` after it.  Not with overlap_ticks.
-    bool split_ingest = true;
-    uint8_t* d_seg_serial = nullptr;    // per segment: left to the serial pass
-    hipEvent_t ev_planned = nullptr;    // after the last tick's plan (the window it set, the heads it read)
-    bool plan_recorded = false;
-    hipEvent_t ev_hdr = nullptr;        // after the header pass
+    uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
     uint32_t tcp_copy = 3;          // EDGPU_INGEST_TCP: 3 frame state in SGPRs, DPP neighbour word, two
                                     // frames per wave round; 2 the same with per-lane frame state;
                                     // 1 one frame per round; 0 two loads per word
@@ -505,11 +496,9 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
         if (hipMemcpy(x->d_totals, &t0, sizeof(t0), hipMemcpyHostToDevice) != hipSuccess) return bad("totals");
     }
     if (const char* v = getenv("EDGPU_FANOUT")) x->fanout_variant = atoi(v);
-    if (const char* v = getenv("EDGPU_INGEST_SPLIT")) x->split_ingest = atoi(v) != 0;
-    if (dmalloc(&x->d_seg_serial, (size_t)c.max_batch_packets + 1) != hipSuccess) return bad("segment flags");
 #ifdef EDGPU_AB_VARIANTS                         // measurement builds only (edgpu_params.h)
     if (const char* v = getenv("EDGPU_ABLATE")) x->ablate = (uint32_t)atoi(v);
-
+    if (const char* v = getenv("EDGPU_INGEST")) x->ingest_mode = (uint32_t)atoi(v) == 1 ? 1u : 0u;
     if (const char* v = getenv("EDGPU_INGEST_TCP")) x->tcp_copy = (uint32_t)std::min(std::max(atoi(v), 0), 3);
     // measurement: the deframe waits for everything enqueued before it (no overlap with the last fan-out)
     if (const char* v = getenv("EDGPU_DEFRAME_SERIAL")) x->deframe_serial = atoi(v) != 0;
@@ -561,9 +550,6 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->aux) (void)hipStreamSynchronize(x->aux);
     if (x->ev_deframe) (void)hipEventDestroy(x->ev_deframe);
     if (x->ev_serial) (void)hipEventDestroy(x->ev_serial);
-    if (x->ev_hdr) (void)hipEventDestroy(x->ev_hdr);
-    if (x->ev_planned) (void)hipEventDestroy(x->ev_planned);
-    if (x->d_seg_serial) (void)hipFree(x->d_seg_serial);
     if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
     if (x->aux) (void)hipStreamDestroy(x->aux);
     if (x->stream) (void)hipStreamDestroy(x->stream);
@@ -889,8 +875,6 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
     sh.src.resize(sh.ntracks);
     for (auto& h : sh.src) { h.rr_ssrc = (uint32_t)::rand(); h.cname = source_cname(wall_ms / 1000); }
     const uint32_t nsnd = 2 * sh.ntracks;
-    if (!reuse && x->nsenders + nsnd > (1u << 20))          // (CopyJob::sender is 20 bits)
-        return fail(EDGPU_OUT_OF_MEMORY, "more than 2^20 senders in one context");
     if (!reuse) {
         HIP_CHECK(x->d_sessions.reserve(sid + 1, x->stream));
         HIP_CHECK(x->d_senders.reserve(x->nsenders + nsnd, x->stream));
@@ -1472,18 +1456,9 @@ static int rebuild_index(edgpu_ctx* x) {
 // Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
 // edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
 // inside the ingest timing events.
-// The side stream of the deframe and the split ingest's header pass, and its events.
-static int ensure_aux(edgpu_ctx* x) {
-    if (!x->aux) HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
-    if (!x->ev_deframe) HIP_CHECK(hipEventCreateWithFlags(&x->ev_deframe, hipEventDisableTiming));
-    if (!x->ev_hdr) HIP_CHECK(hipEventCreateWithFlags(&x->ev_hdr, hipEventDisableTiming));
-    if (!x->ev_planned) HIP_CHECK(hipEventCreateWithFlags(&x->ev_planned, hipEventDisableTiming));
-    return EDGPU_OK;
-}
-
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
                           uint32_t nseg, const uint8_t* db, uint32_t copy_mode, bool host_src, const TcpParams* tcp = nullptr,
-                          hipEvent_t deframed = nullptr, hipEvent_t inputs = nullptr) {
+                          hipEvent_t deframed = nullptr) {
     IngestParams p;
     // a host batch: k_ingest records each packet's blob slot (edgpu_fanout_packet_info)
     p.host_epoch = host_src ? ++x->ingest_epoch : 0u;
@@ -1493,7 +1468,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.jobs = x->d_jobs; p.npk = n; p.nseg = nseg; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
+    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.totals = x->d_totals;
     p.tcp_groups = tcp ? tcp->groups : nullptr;
@@ -1503,36 +1478,11 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.tcp_raw = tcp ? tcp->raw : nullptr;
     p.tcp_stage = tcp ? tcp->stage : nullptr;
     p.tcp_results = tcp ? tcp->results : nullptr;
-    p.seg_serial = x->d_seg_serial;
-    if (copy_mode == kCopyFused && x->split_ingest && !x->overlap && nseg) {
-        // The split ingest.  The header pass runs on `aux`, beside the last tick's fan-out if that is
-        // still running: after that tick's plan (which read the heads this pass moves and set the
-        // window it checks a segment against) and after the batch's inputs (a deframe before it on
-        // `aux` is already in order).  The slot copy -- the HBM-bound part -- follows the fan-out on
-        // `stream`, with the serial pass of any segment that could have lapped the fan-out's window.
-        if (int r = ensure_aux(x)) return r;
-        if (x->plan_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_planned, 0));
-        if (inputs) HIP_CHECK(hipStreamWaitEvent(x->aux, inputs, 0));
-        if (tcp && !deframed) HIP_CHECK(launch_deframe(*tcp, x->aux));
-        p.copy_mode = kCopyHeader;
-        p.overlap = x->plan_recorded ? 1u : 0u;
-        HIP_CHECK(launch_ingest(p, nseg, x->aux));
-        HIP_CHECK(hipEventRecord(x->ev_hdr, x->aux));
-        HIP_CHECK(hist_mark(x, 2, 0));
-        HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_hdr, 0));
-        IngestParams q = p;
-        q.copy_mode = kCopySerial;
-        q.overlap = 0;
-        HIP_CHECK(launch_ingest(q, nseg, x->stream));
-        HIP_CHECK(launch_slot_copy(p, n ? n : x->cfg.max_batch_packets, (uint32_t)x->num_cus, x->stream));
-        HIP_CHECK(hist_mark(x, 2, 1));
-    } else {
-        HIP_CHECK(hist_mark(x, 2, 0));
-        if (deframed) HIP_CHECK(hipStreamWaitEvent(x->stream, deframed, 0));    // the deframe ran on aux
-        else if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
-        HIP_CHECK(launch_ingest(p, nseg, x->stream));
-        HIP_CHECK(hist_mark(x, 2, 1));
-    }
+    HIP_CHECK(hist_mark(x, 2, 0));
+    if (deframed) HIP_CHECK(hipStreamWaitEvent(x->stream, deframed, 0));    // the deframe ran on aux
+    else if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
+    HIP_CHECK(launch_ingest(p, nseg, x->stream));
+    HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
     x->kf_share = tcp == nullptr;       // the interleaved path syncs and reads back results next
     x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
@@ -1685,7 +1635,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         int k = 0;
         if ((r = stage_pinned(x, desc, n, seg_off, seg_sess, nseg, blob, blob_bytes, &k))) return r;
         const edgpu_ctx::PinStage& S = x->pin[k];
-        r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, kCopyFused, true, nullptr, nullptr, S.copied);
+        r = enqueue_ingest(x, S.desc, n, S.seg, S.sess, nseg, S.blob, x->ingest_mode, true);
         if (!r) x->pend_stage = k;
         else (void)hipEventRecord(S.consumed, x->stream);   // nothing will read the set: free it
         return r;
@@ -1708,7 +1658,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
     }
-    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, kCopyFused, where == EDGPU_PTR_HOST);
+    return enqueue_ingest(x, dd, n, ds, dss, nseg, db, x->ingest_mode, where == EDGPU_PTR_HOST);
 }
 
 int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t n, const uint8_t* bytes,
@@ -1773,7 +1723,10 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
-    if (int r = ensure_aux(x)) return r;
+    if (!x->aux) {
+        HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&x->ev_deframe, hipEventDisableTiming));
+    }
     // the deframe rewrites the segment tables the last keyframe index reads (a reserve above that
     // grew has synchronised `stream`); the fan-out after that index keeps running
     if (x->kf_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_kf, 0));
@@ -1942,17 +1895,6 @@ static int launch_copy_pass(edgpu_ctx* x, edgpu_fanout_result* out) {
     return EDGPU_OK;
 }
 
-// The point the split ingest's next header pass waits for: after the plan, or -- for a copy kernel
-// that reads the sender records the header pass moves (the measurement build's k_fanout3) -- after
-// the copy.
-static int record_plan(edgpu_ctx* x, bool after_copy) {
-    if (!x->split_ingest || x->overlap || after_copy != fanout_reads_senders(x->tick_variant)) return EDGPU_OK;
-    if (int r = ensure_aux(x)) return r;
-    HIP_CHECK(hipEventRecord(x->ev_planned, x->stream));
-    x->plan_recorded = true;
-    return EDGPU_OK;
-}
-
 int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
@@ -1979,9 +1921,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     // the per-tick totals (relayed_*, arena, status, nwork, passes) are reset by the plan's first kernel
     HIP_CHECK(hist_mark(x, 1, 0));
     HIP_CHECK(launch_plan(p, x->stream));
-    if (int r = record_plan(x, false)) return r;
     if (int r = launch_copy_pass(x, out)) return r;
-    if (int r = record_plan(x, true)) return r;
     if (x->timing >= EDGPU_TIMING_ALL) {   // the whole-tick pair (ring 1) ends at this copy kernel's end event
         const uint32_t s1 = x->hist_n[1];
         x->tick_end[s1 % edgpu_ctx::kHist] = x->last_seq[0];
@@ -2021,9 +1961,7 @@ int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched
     x->pass_id = next;
     const PlanParams p = plan_params(x, x->last_now);
     HIP_CHECK(launch_plan_pass(p, x->stream));
-    if (int r = record_plan(x, false)) return r;
     if (int r = launch_copy_pass(x, out)) return r;
-    if (int r = record_plan(x, true)) return r;
     *launched = 1;
     return EDGPU_OK;
 }

@@ -324,7 +324,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint64_t p_vb[THREADS];
     __shared__ uint64_t scan64[NW];
     __shared__ uint32_t scan32[NW];
-    __shared__ int s_risky;
     // interleaved ingest: the session's chunk table (frame end of each chunk, the recorded
     // candidate or kTcpNone) and its reads, for every lane's frame lookup
     constexpr uint32_t kLdsChunks = 256, kLdsReads = 64;
@@ -357,73 +356,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #ifdef EDGPU_AB_VARIANTS
     if (tid == 0) atomicMin(&P.totals->ing_t0_min, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-    if (tid == 0) s_risky = 0;
     __syncthreads();
-    // Split ingest.  The serial pass (after the fan-out) takes only the segments the header pass left.
-    // The header pass may run beside the last tick's fan-out: a segment whose batch could lap the
-    // window that fan-out reads (fan_lo / fan_vlo, from its plan) in any sender's ring -- its packets
-    // counted per sender, each at its slot size, before the SSRC filter -- is left whole to the
-    // serial pass, its jobs emptied.
-    if (EDGPU_COPY_MODE(P) == kCopySerial && !P.seg_serial[seg]) return;          // uniform
-    if (EDGPU_COPY_MODE(P) == kCopyHeader) {
-        if (P.overlap) {
-            if (tid < (int)nsnd) { c_tot[tid] = 0; c_last[tid] = 0; }
-            __syncthreads();
-            for (uint32_t i = b + tid; i < e; i += THREADS) {
-                uint32_t ch = 0, ln = 0;
-                bool found = false;
-                if (P.tcp_groups) {                   // the frame's '$' ch BE16(len) header
-                    const uint32_t j = i - b;
-                    uint32_t lo = 0, hi = G.nchunks - 1;
-                    const bool lds = G.nchunks <= kLdsChunks;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        uint32_t ce;
-                        if (lds) ce = t_cend[mid];
-                        else { const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + mid]; ce = R.fbase + R.nframes; }
-                        if (ce > j) hi = mid; else lo = mid + 1;
-                    }
-                    uint32_t rec, fbase;
-                    if (lds) { rec = t_crec[lo]; fbase = lo ? t_cend[lo - 1] : 0u; }
-                    else {
-                        const TcpChunkRes R = P.tcp_chunkres[G.first_chunk + lo];
-                        rec = R.entry != kTcpNone && R.nframes <= kTcpFrames ? R.cand : kTcpNone;
-                        fbase = R.fbase;
-                    }
-                    if (rec != kTcpNone) {
-                        const uint64_t pos = (uint64_t)lo * kTcpChunk +
-                                             P.tcp_offs[((size_t)(G.first_chunk + lo) * kTcpCands + rec) * kTcpFrames + (j - fbase)];
-                        const uint8_t* sp = pos >= G.carry_len ? P.tcp_raw + G.raw_off + (pos - G.carry_len)
-                                                               : P.tcp_stage + (uint64_t)seg * kTcpCarry;
-                        ch = sp[1];
-                        ln = (uint32_t)sp[2] << 8 | sp[3];
-                        found = true;
-                    }
-                }
-                if (!found) { const edgpu_pkt_desc d = P.desc[i]; ch = d.channel; ln = d.len; }
-                ln = min(ln, (uint32_t)kMaxPacket);
-                const uint32_t l = 2 * (ch >> 1) + (ch & 1);
-                if ((ch >> 1) < S.ntracks && ln > 0) {
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&c_tot[l]), (unsigned long long)((ln + 4 + 15) & ~15u));
-                    atomicAdd(reinterpret_cast<uint32_t*>(&c_last[l]), 1u);
-                }
-            }
-            __syncthreads();
-            if (tid < (int)nsnd) {
-                const SenderDev& D = P.senders[S.first_sender + tid];
-                if (s_head[tid] + (uint32_t)c_last[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1 ||
-                    s_vbyte[tid] + c_tot[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16)
-                    s_risky = 1;
-            }
-        }
-        __syncthreads();
-        const bool risky = s_risky != 0;
-        if (tid == 0) P.seg_serial[seg] = risky ? 1 : 0;
-        if (risky) {
-            for (uint32_t i = b + tid; i < e; i += THREADS) P.jobs[i].len = 0;
-            return;
-        }
-    }
 
     uint64_t in_pk = 0, in_bytes = 0;
     for (uint32_t base = b; base < e; base += THREADS) {
@@ -640,11 +573,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
         if (EDGPU_ABL(P) & 32u) {
             // timing ablation only: no slot copy
-        } else if (EDGPU_COPY_MODE(P) != kCopyHeader && P.src_addr && EDGPU_TCP_COPY(P) >= 1) {   // frames inside the TCP byte stream
+        } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr && EDGPU_TCP_COPY(P) >= 1) {   // frames inside the TCP byte stream
             if (EDGPU_TCP_COPY(P) == 3) tcp_slot_copy_s<kTcpFramesPerRound, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else if (EDGPU_TCP_COPY(P) >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else tcp_slot_copy<1, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
-        } else if (EDGPU_COPY_MODE(P) != kCopyHeader && P.src_addr) {   // same, two aligned loads per word (A/B)
+        } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr) {   // same, two aligned loads per word (A/B)
             const int lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += THREADS / 64) {
                 const uint32_t sb = p_slotb[p];
@@ -666,7 +599,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 if (lane + 64 < nw) ring[(w0 + lane + 64) & wm] = v1;
                 if (lane + 128 < nw) ring[(w0 + lane + 128) & wm] = v2;
             }
-        } else if (EDGPU_COPY_MODE(P) != kCopyHeader) {
+        } else if (EDGPU_COPY_MODE(P) == 0) {
             // kDepth packets per wave per round, and a slot is at most 129 words (2060 + 4 B),
             // so every lane issues all of its loads (<= 3 x 16 B per packet) before its first
             // store: a wave keeps kDepth whole slots in flight instead of waiting out one load
@@ -700,12 +633,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                         if (lane + 64 * k < nw[d]) ring[(w0 + lane + 64 * k) & wm] = v[d][k];
                 }
             }
-        } else if (valid) {             // the header pass: the slot copy is k_slot_copy's job
+        } else if (valid) {
             CopyJob j;
-            j.src = src;
-            j.vword = vb >> 4;
             j.ring = acc ? s_ring[ls] : 0ull;
+            j.vword = vb >> 4;
             j.wmask = acc ? s_wmask[ls] : 0u;
+            j.src_slot = slot;
             j.len = slotb ? len : 0u;
             j.sender = S.first_sender + ls;
             P.jobs[i] = j;
@@ -756,85 +689,33 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 }
 
 // =========================================================================================
-// Slot copy of the split ingest (k_ingest kCopyHeader wrote one job per packet): a flat grid over
-// packets, kCopyLanes lanes per packet, every lane's words loaded before its first store (a slot is
-// at most 129 words, so <= 9 blocks per lane): few registers per wave, many waves and loads in
-// flight per CU, and no per-session workgroup's header work between them.  Slot word w is the
-// 16 bytes at src + 16 w -- two aligned blocks funnelled by src & 15 when the frame is misaligned
-// (frames inside the TCP bytes), the next block coming from the next lane of the 16-lane row by DPP
-// (row_ror:15) -- with word 0's first dword the slot header and the bytes past the frame cleared.
-// Words a later packet of the same batch laps are left to it (k_ingest has already advanced
-// vbyte_end), as in the fused copy.
+// Slot copy, blob -> byte rings.  Each group of kCopyLanes lanes copies one packet's slot as
+// 16-B words, rewriting word 0's 4-byte prefix to the '$' 0 BE16(len) frame header.  A flat
+// grid over packets keeps every CU busy regardless of how packets spread over sessions.
 // =========================================================================================
+#ifdef EDGPU_AB_VARIANTS
 constexpr int kCopyThreads = 256, kCopyLanes = 16;
 
-// Lane l of a 16-lane row gets lane l + 1's value of `v` (DPP row_shl:1); lane 15 of the row keeps `v`.
-__device__ __forceinline__ u32x4 row_next16(u32x4 v) {
-    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp((int)v.x, (int)v.x, 0x101, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.y, (int)v.y, 0x101, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.z, (int)v.z, 0x101, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.w, (int)v.w, 0x101, 0xF, 0xF, false)};
-}
-// Lane l of a 16-lane row gets lane 15 - l's value (DPP row_mirror): lane 15 gets the row's lane 0.
-__device__ __forceinline__ u32x4 row_mirror16(u32x4 v) {
-    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp((int)v.x, (int)v.x, 0x140, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.y, (int)v.y, 0x140, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.z, (int)v.z, 0x140, 0xF, 0xF, false),
-                 (uint32_t)__builtin_amdgcn_update_dpp((int)v.w, (int)v.w, 0x140, 0xF, 0xF, false)};
-}
-
-__global__ __launch_bounds__(kCopyThreads) void k_slot_copy(IngestParams P) {
-    static_assert(kCopyLanes == 16, "the DPP exchanges work on rows of 16 lanes");
-    constexpr uint32_t kB = (kSlotWordsMax + kCopyLanes - 1) / kCopyLanes;   // blocks per lane (9)
-    constexpr uint32_t kPer = kCopyThreads / kCopyLanes;
+__global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
+    const uint32_t g = blockIdx.x * (kCopyThreads / kCopyLanes) + threadIdx.x / kCopyLanes;
     const uint32_t lane = threadIdx.x % kCopyLanes;
-    const uint32_t npk = P.seg_off[P.nseg];                        // (interleaved: found by the deframe)
-    // a grid-stride loop over packets (the interleaved batch's count is known on the device only);
-    // the bound is uniform per workgroup, and every lane of a row takes part in the exchanges
-    for (uint32_t g0 = blockIdx.x * kPer; g0 < npk; g0 += gridDim.x * kPer) {
-        const uint32_t g = g0 + threadIdx.x / kCopyLanes;
-        CopyJob j;
-        j.src = 0; j.vword = 0; j.ring = 0; j.wmask = 0; j.len = 0; j.sender = 0;
-        if (g < npk) j = P.jobs[g];
-        const uint32_t fl = j.len ? 4u + j.len : 0u;               // frame bytes ('$'-header room + packet)
-        const uint32_t nw = (fl + 15) >> 4;
-        const uint64_t a0 = j.src & ~15ull;
-        const uint32_t sh = (uint32_t)(j.src & 15);
-        const uint32_t nblk = fl ? (uint32_t)((j.src + fl - 1 - a0) >> 4) + 1 : 0u;
-        const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
-        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-        u32x4 blk[kB + 1];
-#pragma unroll
-        for (uint32_t i = 0; i < kB; i++) {
-            const uint32_t w = lane + i * kCopyLanes;
-            blk[i] = w < nblk ? __builtin_nontemporal_load(ab + w) : z;
-        }
-        blk[kB] = z;
-        uint64_t live = 0;
-        if (nw) {
-            const uint64_t vend = P.senders[j.sender].vbyte_end >> 4, cap = (uint64_t)j.wmask + 1;
-            live = vend > cap ? vend - cap : 0ull;
-        }
-        u32x4* ring = reinterpret_cast<u32x4*>(j.ring);
-        const bool misaligned = __ballot(sh != 0) != 0;            // (descriptor batches: never)
-#pragma unroll
-        for (uint32_t i = 0; i < kB; i++) {
-            const uint32_t w = lane + i * kCopyLanes;
-            u32x4 v = blk[i];
-            if (misaligned) {
-                // block w + 1: the next lane's block i, or for lane 15 the row's lane 0's block i + 1
-                const u32x4 nb = row_next16(blk[i]);
-                const u32x4 wrap = row_mirror16(blk[i + 1]);
-                v = funnel16(blk[i], lane == kCopyLanes - 1 ? wrap : nb, sh);
-            }
-            if (w < nw) {
-                if (w == 0) v.x = slot_header(j.len);
-                v = keep16(v, (int)fl - 16 * (int)w);
-                if (j.vword + w >= live) ring[(j.vword + w) & j.wmask] = v;
-            }
-        }
+    if (g >= P.npk) return;
+    const CopyJob j = P.jobs[g];
+    if (j.len == 0) return;
+    const uint32_t nw = (j.len + 4 + 15) >> 4;
+    // words a later packet of the same batch laps are left to it (k_ingest has already
+    // advanced vbyte_end), so a batch larger than the ring stays deterministic
+    const uint64_t vend = P.senders[j.sender].vbyte_end >> 4, cap = (uint64_t)j.wmask + 1;
+    const uint64_t live = vend > cap ? vend - cap : 0ull;
+    const u32x4* src = reinterpret_cast<const u32x4*>(P.blob + (uint64_t)j.src_slot * 16);
+    u32x4* ring = reinterpret_cast<u32x4*>(j.ring);
+    for (uint32_t k = lane; k < nw; k += kCopyLanes) {
+        u32x4 v = src[k];
+        if (k == 0) v.x = slot_header(j.len);
+        if (j.vword + k >= live) ring[(j.vword + k) & j.wmask] = v;
     }
 }
+#endif  // EDGPU_AB_VARIANTS
 
 // =========================================================================================
 // Keyframe index + audio anchor: one wave per session segment.
@@ -2707,17 +2588,13 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
     else if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    if (p.npk && EDGPU_COPY_MODE(p) == 1) {
+        const uint32_t per = kCopyThreads / kCopyLanes;
+        hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+    }
 #else
     hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
 #endif
-    return hipGetLastError();
-}
-// The split ingest's slot copy (after k_ingest kCopyHeader)
-hipError_t launch_slot_copy(const IngestParams& p, uint32_t max_packets, uint32_t num_cus, hipStream_t st) {
-    if (p.nseg == 0) return hipSuccess;
-    const uint32_t per = kCopyThreads / kCopyLanes;
-    const uint32_t grid = std::max(1u, std::min((max_packets + per - 1) / per, num_cus * 8));
-    hipLaunchKernelGGL(k_slot_copy, dim3(grid), dim3(kCopyThreads), 0, st, p);
     return hipGetLastError();
 }
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
@@ -2905,16 +2782,6 @@ static const int kDefaultPlain = 1;
 static const int kFirstRewriting = 0;
 #endif
 int fanout_default(bool patching) { return patching ? kDefaultVariant : kDefaultPlain; }
-// k_fanout3 (the measurement build's variants 0 and 1) reads the sender records' heads while it copies
-bool fanout_reads_senders(int variant) {
-#ifdef EDGPU_AB_VARIANTS
-    if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;
-    return variant < 2;
-#else
-    (void)variant;
-    return false;
-#endif
-}
 // edgpu_subscriber_rewrite refuses a variant without a rewrite stage
 bool fanout_rewrites(int variant) {
     if (variant < 0 || variant >= kNumVariants) variant = kDefaultVariant;

@@ -11,12 +11,13 @@
 // kernels and no skip-work branch: these knobs are compile-time constants there.
 #ifdef EDGPU_AB_VARIANTS
 #define EDGPU_ABL(P) ((P).ablate)
+#define EDGPU_COPY_MODE(P) ((P).copy_mode)
 #define EDGPU_TCP_COPY(P) ((P).tcp_copy)
 #else
 #define EDGPU_ABL(P) 0u
+#define EDGPU_COPY_MODE(P) 0u
 #define EDGPU_TCP_COPY(P) 3u
 #endif
-#define EDGPU_COPY_MODE(P) ((P).copy_mode)
 
 namespace edgpu {
 
@@ -32,9 +33,6 @@ struct TcpGroup;
 struct TcpChunkRes;
 struct TcpRead;
 
-// k_ingest copy modes (IngestParams::copy_mode)
-constexpr uint32_t kCopyFused = 0, kCopyHeader = 1, kCopySerial = 2;
-
 struct IngestParams {
     const edgpu_pkt_desc* desc;
     const uint32_t* seg_off;
@@ -47,13 +45,9 @@ struct IngestParams {
     StreamDev* streams;
     uint32_t* pflags;       // per desc: bit0 enqueued, bit1 video key, bit2 audio event, bits 8-15 local sender
     uint64_t* pidx;         // per desc: sender queue index
-    CopyJob* jobs;          // per desc: slot copy for k_slot_copy
-    uint8_t* seg_serial;    // per segment (copy modes 1 / 2): the header pass left it to the serial pass
-    uint32_t npk;           // descriptors in the batch (0 for interleaved reads: seg_off[nseg] counts the frames)
-    uint32_t nseg;          // segments (k_slot_copy reads the packet count at seg_off[nseg])
-    uint32_t copy_mode;     // kCopyFused: header work and slot copy in k_ingest; kCopyHeader: the header
-                            // pass (beside the last fan-out), jobs for k_slot_copy; kCopySerial: the
-                            // fused ingest of the segments the header pass left (seg_serial)
+    CopyJob* jobs;          // per desc: slot copy for k_ingest_copy
+    uint32_t npk;           // descriptors in the batch
+    uint32_t copy_mode;     // 0: copy inside k_ingest, 1: k_ingest_copy (EDGPU_INGEST)
     uint32_t tcp_copy;      // frames in the TCP byte stream: 1 one aligned load per word + the
                             // neighbour word by DPP, 2 the same with two frames per wave round
                             // (default); 0 two aligned loads per word (EDGPU_INGEST_TCP)
