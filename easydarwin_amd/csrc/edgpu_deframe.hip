@@ -548,9 +548,11 @@ __global__ __launch_bounds__(kScanThreads) void k_tcp_scan(TcpParams P) {
 // k_ingest finds the frames of every chunk whose true walk was recorded itself (IngestParams.
 // tcp_groups).  This wave does the rest of the session: a descriptor and a source address per
 // frame of the chunks the walk did not record (re-walked here: a chunk entered by the sequential
-// fallback, or with more than kTcpFrames frames) and their per-read frame counts; the staging of
-// a frame that starts in the carried bytes (only the stream's first frame can), then the new
-// carry -- only this wave reads the carried bytes after the walk -- and the per-read report.
+// fallback, or with more than kTcpFrames frames); the staging of a frame that starts in the
+// carried bytes (only the stream's first frame can), then the new carry -- only this wave reads
+// the carried bytes after the walk -- and the whole per-read report, frame counts included: a
+// recorded chunk's frame ends are its next recorded start (its walk's exit for the last), so the
+// report needs no header and is complete when the deframe is, before k_ingest has run.
 // A session with no stream bytes has no chunk; its report is the zeros the host cleared.
 __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
     const uint32_t g = blockIdx.x;
@@ -567,9 +569,15 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
     __shared__ uint64_t s_rstart[64];
     __shared__ int64_t s_rarr[64];
     __shared__ uint8_t s_carry[kTcpCarry];
+    __shared__ uint32_t s_frames[64];                 // per read (up to 64 reads), else global atomics
     const bool lds_reads = G.nreads <= 64;
     if (lds_reads && (uint32_t)lane < G.nreads) { s_rstart[lane] = rd[lane].start; s_rarr[lane] = rd[lane].arrival; }
+    s_frames[lane] = 0;
     __syncthreads();
+    auto count_frame = [&](uint32_t r) {
+        if (lds_reads) atomicAdd(&s_frames[r], 1u);
+        else atomicAdd(&P.results[G.first_read + r].frames, 1u);
+    };
     for (uint32_t k0 = 0; !over && k0 < G.nchunks; k0 += 64) {
         // the chunks the walk did not record, 64 at a time
         const uint32_t k = k0 + (uint32_t)lane;
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
                     P.desc[fi] = d;
                     const uint8_t* a = p >= v.clen ? v.raw + (p - v.clen) : P.stage + (uint64_t)g * kTcpCarry;
                     P.src_addr[fi] = (uint64_t)(uintptr_t)a;
-                    atomicAdd(&P.results[G.first_read + lo].frames, 1u);
+                    count_frame((uint32_t)lo);
                 }
                 done += m;
                 __syncthreads();
@@ -631,6 +639,24 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
             }
         }
     }
+    // the recorded chunks' frames, counted per read: a lane per chunk walks its recorded starts;
+    // frame f ends where frame f + 1 starts (the walk's exit for the last), and reads are in
+    // stream order, so one cursor finds each frame's read (the one holding its last byte)
+    for (uint32_t k = (uint32_t)lane; !over && k < G.nchunks; k += 64) {
+        const TcpChunkRes R = P.chunkres[G.first_chunk + k];
+        if (R.entry == kTcpNone || R.cand == kTcpNone || R.nframes > kTcpFrames) continue;
+        const size_t ci = (size_t)(G.first_chunk + k) * kTcpCands + R.cand;
+        const uint16_t* fo = P.offs + ci * kTcpFrames;
+        const uint32_t ex = P.cands[ci].exit;
+        const uint64_t start = (uint64_t)k * kTcpChunk;
+        uint32_t r = 0;
+        for (uint32_t f = 0; f < R.nframes; f++) {
+            const uint64_t last = start + (f + 1 < R.nframes ? (uint32_t)fo[f + 1] : ex) - 1;
+            while (r + 1 < G.nreads && (lds_reads ? s_rstart[r + 1] : rd[r + 1].start) <= last) r++;
+            count_frame(r);
+        }
+    }
+    __syncthreads();
     // a frame that starts in the carried bytes -- the stream's first, at position 0 -- is staged
     // contiguously for k_ingest before the carry is overwritten
     if (!over && G.nchunks && v.clen) {
@@ -664,10 +690,13 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
         if (over) {
             consumed = 0;
             o.frames = 0;
-        } else if (code == kWalkMessage || code == kWalkDropped) {
-            consumed = stop <= r.start ? 0u : (uint32_t)min<uint64_t>(stop - r.start, r.len);
-            const uint64_t at = code == kWalkMessage ? stop : stop + kTcpMaxFrame - 1;
-            if (r.start + r.len > at) status = code == kWalkMessage ? EDGPU_TCP_MESSAGE : EDGPU_TCP_DROPPED;
+        } else {
+            if (lds_reads) o.frames = s_frames[i];
+            if (code == kWalkMessage || code == kWalkDropped) {
+                consumed = stop <= r.start ? 0u : (uint32_t)min<uint64_t>(stop - r.start, r.len);
+                const uint64_t at = code == kWalkMessage ? stop : stop + kTcpMaxFrame - 1;
+                if (r.start + r.len > at) status = code == kWalkMessage ? EDGPU_TCP_MESSAGE : EDGPU_TCP_DROPPED;
+            }
         }
         o.consumed = consumed;
         o.status = status;

@@ -574,10 +574,11 @@ static hipError_t sync_all(edgpu_ctx* x) {
 static constexpr size_t kStageBytes = 64 << 10;
 struct Readback {
     edgpu_ctx* x;
+    hipStream_t st;         // the stream the reads follow (the context stream unless given)
     struct Item { void* dst; size_t off, bytes; };
     std::vector<Item> staged;
     size_t used = 0;
-    explicit Readback(edgpu_ctx* c) : x(c) {}
+    explicit Readback(edgpu_ctx* c, hipStream_t s = nullptr) : x(c), st(s ? s : c->stream) {}
     hipError_t add(void* dst, const void* src, size_t bytes) {
         if (!bytes) return hipSuccess;
         if (!x->h_stage) {
@@ -586,14 +587,14 @@ struct Readback {
         }
         if (bytes <= kStageBytes - used) {
             staged.push_back({dst, used, bytes});
-            hipError_t e = hipMemcpyAsync(x->h_stage + used, src, bytes, hipMemcpyDeviceToHost, x->stream);
+            hipError_t e = hipMemcpyAsync(x->h_stage + used, src, bytes, hipMemcpyDeviceToHost, st);
             used += (bytes + 15) & ~size_t(15);
             return e;
         }
         // a large read into pinned memory: a copy kernel storing over PCIe beats the DMA copy
         if (bytes >= kKernelCopyBytes && !(((uintptr_t)dst | (uintptr_t)src) & 15) && is_pinned(dst))
-            return launch_copy_to_pinned(dst, src, bytes, x->stream);
-        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, x->stream);
+            return launch_copy_to_pinned(dst, src, bytes, st);
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     }
     static constexpr size_t kKernelCopyBytes = 256 << 10;
     static bool is_pinned(const void* p) {
@@ -602,7 +603,7 @@ struct Readback {
         return a.type == hipMemoryTypeHost;
     }
     hipError_t run() {
-        hipError_t e = hipStreamSynchronize(x->stream);
+        hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) return e;
         for (const Item& it : staged) memcpy(it.dst, x->h_stage + it.off, it.bytes);
         staged.clear();
@@ -1477,14 +1478,13 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.tcp_reads = tcp ? tcp->reads : nullptr;
     p.tcp_raw = tcp ? tcp->raw : nullptr;
     p.tcp_stage = tcp ? tcp->stage : nullptr;
-    p.tcp_results = tcp ? tcp->results : nullptr;
     HIP_CHECK(hist_mark(x, 2, 0));
     if (deframed) HIP_CHECK(hipStreamWaitEvent(x->stream, deframed, 0));    // the deframe ran on aux
     else if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
-    x->kf_share = tcp == nullptr;       // the interleaved path syncs and reads back results next
+    x->kf_share = true;                 // (the interleaved path reads its report on aux)
     x->pend_seg = ds; x->pend_seg_sess = dss; x->pend_nseg = nseg; x->pending = true;
     return EDGPU_OK;
 }
@@ -1761,8 +1761,12 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     HIP_CHECK(hipEventRecord(x->ev_deframe, x->aux));
     int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, false, &p, x->ev_deframe);
     if (r) return r;
+    // The report is the deframe's alone (k_tcp_finish counts the frames too): read on aux, it
+    // waits for the deframe only -- which ran beside the previous tick's fan-out -- and the call
+    // returns while k_ingest is still queued behind that fan-out, so the host enqueues the
+    // keyframe index and the next fan-out without leaving the device idle.
     TcpTotals tot;
-    Readback rb(x);
+    Readback rb(x, x->aux);
     HIP_CHECK(rb.add(&tot, x->d_tcp_tot, sizeof(tot)));
     HIP_CHECK(rb.add(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result)));
     HIP_CHECK(rb.run());

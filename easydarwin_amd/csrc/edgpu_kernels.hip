@@ -370,8 +370,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         bool acc = false;
         const uint8_t* pk = nullptr;
         uint32_t hdr[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};   // packet bytes 0..27, little-endian words
-        bool direct = false;            // interleaved frame found here (counted per read below)
-        uint32_t rd_idx = 0;
+        bool direct = false;            // an interleaved frame found here
         if (valid && P.tcp_groups) {
             // the frame's chunk: the first whose frame end passes the frame's session index
             const uint32_t j = i - b;
@@ -425,7 +424,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                     const uint64_t st = G.nreads <= kLdsReads ? t_rstart[mid] : P.tcp_reads[G.first_read + mid].start;
                     if (st <= last) rl = mid; else rh = mid - 1;
                 }
-                rd_idx = rl;
                 arrival = G.nreads <= kLdsReads ? t_rarr[rl] : P.tcp_reads[G.first_read + rl].arrival;
                 slot = 0;
                 acc = track < S.ntracks && len > 0;
@@ -443,17 +441,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                     acc = len >= 8 && len >= 4 * hbe16(hdr, 2) + 4 && (hbyte(hdr, 0) >> 6) == 2 && hbyte(hdr, 1) == 200;
                 in_pk += 1;
                 in_bytes += len;
-            }
-        }
-        // per read, the frames this round found here (one atomic per read and wave)
-        if (P.tcp_groups) {
-            uint64_t pend = __ballot(direct);
-            while (pend) {
-                const int leader = __ffsll((unsigned long long)pend) - 1;
-                const uint32_t key = (uint32_t)__shfl((int)rd_idx, leader, 64);
-                const uint64_t same = __ballot(direct && rd_idx == key);
-                if ((tid & 63) == leader) atomicAdd(&P.tcp_results[G.first_read + key].frames, (uint32_t)__popcll(same));
-                pend &= ~same;
             }
         }
         if (valid && !direct) {

@@ -68,7 +68,6 @@ struct IngestParams {
     const TcpRead* tcp_reads;
     const uint8_t* tcp_raw;
     const uint8_t* tcp_stage;
-    edgpu_tcp_result* tcp_results;
 };
 
 struct KeyframeParams {

@@ -384,7 +384,10 @@ int  edgpu_ingest_prestage(edgpu_ctx* ctx, const uint8_t* blob, uint64_t offset,
  * `carry` is the session's carried byte count after the call.  Returns EDGPU_OUT_OVERFLOW
  * (nothing ingested, no carry changed) when the frames exceed max_batch_packets.  Host reads
  * are staged in a max_batch_bytes buffer; device reads are read in place (the frames are
- * copied from them into the sender rings).  Syncs (the results are read back). */
+ * copied from them into the sender rings).  Returns once the frames are found and `results`
+ * written, which is before the copy into the rings has run (it is stream-ordered before the
+ * context's next work): device `bytes`, like every EDGPU_PTR_DEVICE pointer, stay valid until
+ * edgpu_sync (or a synchronising call) returns; host `bytes` are consumed on return. */
 #define EDGPU_TCP_MESSAGE  1
 #define EDGPU_TCP_DROPPED  2
 typedef struct edgpu_tcp_read {

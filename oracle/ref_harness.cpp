@@ -1003,8 +1003,10 @@ int main(int argc, char** argv) {
         return 0;
     }
     if (g_bench) {                  // the replays only: PushPacket + ReflectPackets + joins
-        printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"repeat\": %d}\n",
-               (unsigned long long)g_bench_pkts, (unsigned long long)g_bench_bytes, bench_secs, reps);
+        // reflect_seconds: the TICKs alone (ReflectPackets and, with --bench-udp, every sendto)
+        printf("{\"relayed_packets\": %llu, \"relayed_bytes\": %llu, \"seconds\": %.6f, \"reflect_seconds\": %.6f, "
+               "\"repeat\": %d}\n",
+               (unsigned long long)g_bench_pkts, (unsigned long long)g_bench_bytes, bench_secs, g_reflect_s, reps);
         return 0;
     }
 

@@ -16,6 +16,7 @@ import argparse
 import json
 import os
 import socket
+import subprocess
 import sys
 import time
 
@@ -45,6 +46,10 @@ def main():
     ap.add_argument("--gso", type=int, default=1,
                     help="1: runs of equal-length datagrams to one subscriber leave as one UDP GSO message; "
                          "0: one datagram per message")
+    ap.add_argument("--reference", action="store_true",
+                    help="also time the reference's own write path on this host: oracle/_ref/ref_harness "
+                         "--bench-udp (a sendto() per subscriber datagram) on the same C2 fleet, sharded over "
+                         "one process per leased core")
     args = ap.parse_args()
     os.environ["EDGPU_EGRESS_DEDUP"] = str(args.dedup)     # read by edgpu_egress_create
     os.environ["EDGPU_EGRESS_GSO"] = str(args.gso)
@@ -102,9 +107,42 @@ def main():
         "note": "loopback receivers are never read (receive-side drops); send errors are ignored as "
                 "RTPStream::Write's (void)SendTo does",
     }
-    print(json.dumps(res), flush=True)
     eg.close()
     ctx.close()
+    if args.reference:
+        res["reference"] = reference_udp(args)
+        if res["reference"]:
+            res["egress_vs_reference_sendto"] = round(res["egress_datagrams_per_s"]
+                                                      / res["reference"]["sendto_datagrams_per_s"], 3)
+    print(json.dumps(res), flush=True)
+
+
+def reference_udp(args) -> dict | None:
+    """EasyDarwin's reflector writing every UDP subscriber datagram with a sendto() of its own (the
+    reference's RTPStream::Write -> UDPSocket::SendTo, Server.tproj/RTPStream.cpp:1084-1147), each
+    process to one unread loopback socket: ref_harness --bench-udp over the same C2 fleet, one process
+    per leased core at once.  sendto_datagrams_per_s counts the ticks' time (ReflectPackets and the
+    sends); with_push_per_s adds PushPacket."""
+    import tempfile
+    import bench
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    procs_n, why = bench.baseline_cores()
+    with tempfile.TemporaryDirectory(dir=os.environ.get("EDGPU_BASELINE_TMP")) as td:
+        paths = bench._fleet_shards(args.sessions, args.subs, 3000, args.tick_ms, procs_n, td)
+        procs = [subprocess.Popen([exe, "--bench-udp", p, "1"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                  text=True) for p in paths]
+        outs = [json.loads(pr.communicate()[0]) for pr in procs]
+        if any(pr.returncode for pr in procs):
+            return None
+    pk = sum(o["relayed_packets"] for o in outs)
+    return {"sendto_datagrams_per_s": round(pk / max(o["reflect_seconds"] for o in outs), 1),
+            "with_push_per_s": round(pk / max(o["seconds"] for o in outs), 1),
+            "datagrams": pk, "processes": procs_n, "cores_note": why,
+            "sample": f"oracle/_ref/ref_harness --bench-udp: the C2 fleet ({args.sessions} x {args.subs} UDP subs), "
+                      f"3 s of stream at {args.tick_ms}-ms ticks, sharded over {procs_n} processes at once, "
+                      f"each sending to one unread 127.0.0.1 socket; time = the longest process's"}
 
 
 if __name__ == "__main__":
