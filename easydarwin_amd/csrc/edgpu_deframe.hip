@@ -639,22 +639,49 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
             }
         }
     }
-    // the recorded chunks' frames, counted per read: a lane per chunk walks its recorded starts;
-    // frame f ends where frame f + 1 starts (the walk's exit for the last), and reads are in
-    // stream order, so one cursor finds each frame's read (the one holding its last byte)
-    for (uint32_t k = (uint32_t)lane; !over && k < G.nchunks; k += 64) {
-        const TcpChunkRes R = P.chunkres[G.first_chunk + k];
-        if (R.entry == kTcpNone || R.cand == kTcpNone || R.nframes > kTcpFrames) continue;
-        const size_t ci = (size_t)(G.first_chunk + k) * kTcpCands + R.cand;
-        const uint16_t* fo = P.offs + ci * kTcpFrames;
-        const uint32_t ex = P.cands[ci].exit;
-        const uint64_t start = (uint64_t)k * kTcpChunk;
-        uint32_t r = 0;
-        for (uint32_t f = 0; f < R.nframes; f++) {
-            const uint64_t last = start + (f + 1 < R.nframes ? (uint32_t)fo[f + 1] : ex) - 1;
-            while (r + 1 < G.nreads && (lds_reads ? s_rstart[r + 1] : rd[r + 1].start) <= last) r++;
-            count_frame(r);
+    // the recorded chunks' frames, counted per read: frame f of a chunk ends where frame f + 1
+    // starts (the walk's exit for the last) and belongs to the read holding its last byte.  A lane
+    // per recorded frame (kTcpFrames = 32: two chunks per wave, eight per pass, their loads issued
+    // together); the chunk table comes through LDS 64 chunks at a time.
+    static_assert(kTcpFrames == 32, "two chunks per wave");
+    __shared__ uint32_t s_cnf[64], s_cci[64];         // recorded frames (0: none) / candidate row
+    for (uint32_t c0 = 0; !over && c0 < G.nchunks; c0 += 64) {
+        const uint32_t nc = min(64u, G.nchunks - c0);
+        if ((uint32_t)lane < nc) {
+            const TcpChunkRes R = P.chunkres[G.first_chunk + c0 + lane];
+            const bool rec = R.entry != kTcpNone && R.cand != kTcpNone && R.nframes <= kTcpFrames;
+            s_cnf[lane] = rec ? R.nframes : 0u;
+            s_cci[lane] = rec ? R.cand : 0u;
         }
+        __syncthreads();
+        for (uint32_t k0 = 0; k0 < nc; k0 += 8) {
+            uint32_t nxt[4];
+            bool on[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t k = k0 + 2 * u + (uint32_t)(lane >> 5), f = (uint32_t)lane & 31u;
+                const uint32_t nf = k < nc ? s_cnf[k] : 0u;
+                on[u] = f < nf;
+                nxt[u] = 0;
+                if (on[u]) {
+                    const size_t ci = (size_t)(G.first_chunk + c0 + k) * kTcpCands + s_cci[k];
+                    nxt[u] = f + 1 < nf ? (uint32_t)P.offs[ci * kTcpFrames + f + 1] : P.cands[ci].exit;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (!on[u]) continue;
+                const uint32_t k = k0 + 2 * u + (uint32_t)(lane >> 5);
+                const uint64_t last = (uint64_t)(c0 + k) * kTcpChunk + nxt[u] - 1;
+                int lo = 0, hi = (int)G.nreads - 1;       // last read starting at or before `last`
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((lds_reads ? s_rstart[mid] : rd[mid].start) <= last) lo = mid; else hi = mid - 1;
+                }
+                count_frame((uint32_t)lo);
+            }
+        }
+        __syncthreads();
     }
     __syncthreads();
     // a frame that starts in the carried bytes -- the stream's first, at position 0 -- is staged

@@ -235,9 +235,8 @@ struct edgpu_ctx {
     hipEvent_t ev_plan = nullptr, ev_copy = nullptr;
     // the RTSP-interleaved deframe (k_tcp_*) runs on `aux`: it reads only the call's TCP bytes
     // and writes deframe scratch, so it overlaps the previous tick's fan-out still on `stream`;
-    // k_ingest waits for ev_deframe
+    // the host reads its report, then enqueues k_ingest (no cross-stream wait left on `stream`)
     hipStream_t aux = nullptr;
-    hipEvent_t ev_deframe = nullptr;
     hipEvent_t ev_serial = nullptr;       // EDGPU_DEFRAME_SERIAL
     // the last keyframe index (it reads the segment tables the next deframe rewrites)
     hipEvent_t ev_kf = nullptr;
@@ -548,7 +547,6 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
     if (x->copy) (void)hipStreamDestroy(x->copy);
     if (x->aux) (void)hipStreamSynchronize(x->aux);
-    if (x->ev_deframe) (void)hipEventDestroy(x->ev_deframe);
     if (x->ev_serial) (void)hipEventDestroy(x->ev_serial);
     if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
     if (x->aux) (void)hipStreamDestroy(x->aux);
@@ -1455,11 +1453,11 @@ static int rebuild_index(edgpu_ctx* x) {
 }
 
 // Enqueues k_ingest over a staged batch (device pointers) and marks it pending for
-// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels run first,
-// inside the ingest timing events.
+// edgpu_keyframe_index.  With `tcp` (edgpu_ingest_interleaved) the deframe kernels have run
+// (`deframed`: on aux, observed by the host) or run first, inside the ingest timing events.
 static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, const uint32_t* ds, const uint32_t* dss,
                           uint32_t nseg, const uint8_t* db, uint32_t copy_mode, bool host_src, const TcpParams* tcp = nullptr,
-                          hipEvent_t deframed = nullptr) {
+                          bool deframed = false) {
     IngestParams p;
     // a host batch: k_ingest records each packet's blob slot (edgpu_fanout_packet_info)
     p.host_epoch = host_src ? ++x->ingest_epoch : 0u;
@@ -1479,8 +1477,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.tcp_raw = tcp ? tcp->raw : nullptr;
     p.tcp_stage = tcp ? tcp->stage : nullptr;
     HIP_CHECK(hist_mark(x, 2, 0));
-    if (deframed) HIP_CHECK(hipStreamWaitEvent(x->stream, deframed, 0));    // the deframe ran on aux
-    else if (tcp) HIP_CHECK(launch_deframe(*tcp, x->stream));
+    if (tcp && !deframed) HIP_CHECK(launch_deframe(*tcp, x->stream));
     HIP_CHECK(launch_ingest(p, nseg, x->stream));
     HIP_CHECK(hist_mark(x, 2, 1));
     x->timed_ingest = true;
@@ -1723,10 +1720,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
-    if (!x->aux) {
-        HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&x->ev_deframe, hipEventDisableTiming));
-    }
+    if (!x->aux) HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
     // the deframe rewrites the segment tables the last keyframe index reads (a reserve above that
     // grew has synchronised `stream`); the fan-out after that index keeps running
     if (x->kf_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_kf, 0));
@@ -1758,22 +1752,19 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
     HIP_CHECK(launch_deframe(p, x->aux));
-    HIP_CHECK(hipEventRecord(x->ev_deframe, x->aux));
-    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, false, &p, x->ev_deframe);
-    if (r) return r;
     // The report is the deframe's alone (k_tcp_finish counts the frames too): read on aux, it
-    // waits for the deframe only -- which ran beside the previous tick's fan-out -- and the call
-    // returns while k_ingest is still queued behind that fan-out, so the host enqueues the
-    // keyframe index and the next fan-out without leaving the device idle.
+    // waits for the deframe only, which runs beside the previous tick's fan-out.  k_ingest is
+    // enqueued after it, behind that fan-out on `stream`, with nothing to wait for there: the
+    // call returns while the fan-out still runs, and the host enqueues the keyframe index and
+    // the next fan-out without leaving the device idle.
     TcpTotals tot;
     Readback rb(x, x->aux);
     HIP_CHECK(rb.add(&tot, x->d_tcp_tot, sizeof(tot)));
     HIP_CHECK(rb.add(results, x->d_tcp_results.ptr, n * sizeof(edgpu_tcp_result)));
     HIP_CHECK(rb.run());
-    if (tot.status) {
-        x->pending = false;                 // the ingest ran over empty segments
-        return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets");
-    }
+    if (tot.status) return fail(EDGPU_OUT_OVERFLOW, "interleaved frames exceed max_batch_packets");
+    int r = enqueue_ingest(x, x->d_desc, 0, x->d_seg, x->d_seg_sess, ng, nullptr, 0, false, &p, true);
+    if (r) return r;
     for (const TcpGroup& G : groups) x->carry_len[G.session] = results[G.first_read + G.nreads - 1].carry;
     return EDGPU_OK;
 }
