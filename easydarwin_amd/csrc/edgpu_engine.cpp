@@ -1720,7 +1720,13 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (!x->d_tcp_tot && dmalloc(&x->d_tcp_tot, sizeof(TcpTotals)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "tcp totals");
     if (!x->d_tcp_src && dmalloc(&x->d_tcp_src, sizeof(uint64_t) * (size_t)x->cfg.max_batch_packets) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "frame addresses");
-    if (!x->aux) HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
+    if (!x->aux) {
+        HIP_CHECK(hipStreamCreateWithFlags(&x->aux, hipStreamNonBlocking));
+        // from now on every keyframe index records ev_kf; the first deframe follows all work so far
+        HIP_CHECK(hipEventCreateWithFlags(&x->ev_kf, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(x->ev_kf, x->stream));
+        x->kf_recorded = true;
+    }
     // the deframe rewrites the segment tables the last keyframe index reads (a reserve above that
     // grew has synchronised `stream`); the fan-out after that index keeps running
     if (x->kf_recorded) HIP_CHECK(hipStreamWaitEvent(x->aux, x->ev_kf, 0));
@@ -1811,9 +1817,10 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     x->kf_share = false;
     HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
     HIP_CHECK(hist_mark(x, 3, 1));
-    if (!x->ev_kf) HIP_CHECK(hipEventCreateWithFlags(&x->ev_kf, hipEventDisableTiming));
-    HIP_CHECK(hipEventRecord(x->ev_kf, x->stream));
-    x->kf_recorded = true;
+    if (x->aux) {       // the next deframe (on aux) rewrites the segment tables this index reads
+        HIP_CHECK(hipEventRecord(x->ev_kf, x->stream));
+        x->kf_recorded = true;
+    }
     if (x->pend_stage >= 0) {                   // the pinned staging set may be refilled now
         HIP_CHECK(hipEventRecord(x->pin[x->pend_stage].consumed, x->stream));
         x->pend_stage = -1;
