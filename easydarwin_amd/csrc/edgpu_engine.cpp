@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -15,6 +16,8 @@
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <sched.h>
 
 #include "edgpu.h"
 #include "edgpu_device.h"
@@ -2456,6 +2459,41 @@ int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
     HIP_CHECK(hipSetDevice(x->device));
     *out = nullptr;
     if (dmalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "device buffer");
+    return EDGPU_OK;
+}
+
+// The host CPUs of the device's NUMA node (its PCI function's sysfs local_cpulist) that the
+// calling thread may run on: where a server's host threads belong next to this GPU.
+int edgpu_device_local_cpus(int device, uint32_t* cpus, uint32_t cap, uint32_t* n_out) {
+    if (!n_out || (cap && !cpus)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    *n_out = 0;
+    char bdf[64] = {0};
+    HIP_CHECK(hipDeviceGetPCIBusId(bdf, (int)sizeof(bdf) - 1, device));
+    for (char* c = bdf; *c; c++) *c = (char)tolower((unsigned char)*c);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bdf + "/local_cpulist";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return fail(EDGPU_ERR, "no " + path);
+    char buf[4096];
+    const size_t len = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[len] = 0;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return fail(EDGPU_ERR, "sched_getaffinity");
+    uint32_t n = 0;
+    for (const char* q = buf; *q >= '0' && *q <= '9';) {          // "a-b,c,d-e\n"
+        char* e;
+        const long a = strtol(q, &e, 10);
+        long b = a;
+        if (*e == '-') b = strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            if (CPU_ISSET(c, &allowed)) {
+                if (n < cap) cpus[n] = (uint32_t)c;
+                n++;
+            }
+        q = *e == ',' ? e + 1 : e;
+    }
+    *n_out = n;
     return EDGPU_OK;
 }
 

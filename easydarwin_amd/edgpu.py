@@ -42,7 +42,7 @@ EXPORTED = [
     "edgpu_set_timing", "edgpu_ingest_prestage", "edgpu_fanout_next", "edgpu_session_ssrc_prefs",
     "edgpu_subscriber_slot", "edgpu_egress_pacing_config", "edgpu_egress_pacing", "edgpu_egress_clock",
     "edgpu_egress_block_info", "edgpu_session_remote_join", "edgpu_session_remote_leave",
-    "edgpu_subscriber_set_slot",
+    "edgpu_subscriber_set_slot", "edgpu_device_local_cpus",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -251,6 +251,7 @@ def load(path: str = LIB_PATH):
         "edgpu_session_remote_join": (I32, [P, U32, C.POINTER(C.c_int32)]),
         "edgpu_session_remote_leave": (I32, [P, U32, C.c_int32]),
         "edgpu_subscriber_set_slot": (I32, [P, U32, C.c_int32]),
+        "edgpu_device_local_cpus": (I32, [C.c_int, P, U32, P]),
         "edgpu_egress_pacing_config": (I32, [P, C.POINTER(PacingConfig)]),
         "edgpu_egress_pacing": (I32, [P, U32, C.POINTER(Pacing)]),
         "edgpu_egress_clock": (I32, [P, C.c_int64]),
@@ -282,6 +283,17 @@ def sdp_parse(sdp: bytes) -> list:
     buf = (SdpTrack * cap)()
     _check(lib.edgpu_sdp_parse(sdp, len(sdp), buf, cap, C.byref(n)))
     return [(buf[i].payload_type, bytes(buf[i].name[:buf[i].name_len]), buf[i].track_id) for i in range(n.value)]
+
+
+def device_local_cpus(device: int = 0) -> list:
+    """The host CPUs of the GPU's NUMA node this process may run on (edgpu_device_local_cpus;
+    initialises HIP)."""
+    lib = load()
+    cap = 4096
+    buf = (C.c_uint32 * cap)()
+    n = C.c_uint32()
+    _check(lib.edgpu_device_local_cpus(device, buf, cap, C.byref(n)))
+    return [int(buf[i]) for i in range(min(n.value, cap))]
 
 
 class Context:

@@ -318,6 +318,10 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* r, uint32_t n) {
     }
     return EDGPU_OK;
 }
+int edgpu_device_local_cpus(int, uint32_t*, uint32_t, uint32_t* n) {   // no GPU: no placement
+    if (n) *n = 0;
+    return EDGPU_ERR;
+}
 int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes) {
     touch(x);
     if (bytes) memcpy(dst, src, bytes);

@@ -22,6 +22,11 @@ sources, memcpy sinks) on the same C2 fleet -- all <sessions> x <subs> -- at the
 steady state, sessions sharded over one process per core (bench.py c2_reference_steady); compared
 on push + reflect (with_ingest_per_s), as the module's rate counts both.
 
+Placement (--affinity): by default every run -- the fake server with its pusher threads and either
+module, and the reference reflector's processes -- runs on the CPUs of the GPU's NUMA node, as a
+server is deployed next to its GPU; `none` leaves them to the scheduler (the box allows both
+sockets).  The drop-in also keeps its own threads on that node (EDGPU_QTSS_AFFINITY).
+
 Prints one JSON object.  Needs a GPU (the module initialises an edgpu context).
 """
 import argparse
@@ -31,6 +36,29 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def gpu_node_cpus() -> list:
+    """The CPUs of the GPU's NUMA node this process may use (edgpu_device_local_cpus), asked in a
+    child process so that this one never initialises the GPU (it only starts the runs)."""
+    r = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, sys.argv[1]); "
+                        "from easydarwin_amd import edgpu; print(','.join(map(str, edgpu.device_local_cpus(0))))", ROOT],
+                       capture_output=True, text=True, timeout=120)
+    if r.returncode or not r.stdout.strip():
+        raise SystemExit(f"edgpu_device_local_cpus failed: {r.stderr.strip()[-300:]}")
+    return [int(c) for c in r.stdout.strip().split(",")]
+
+
+def cpu_ranges(cpus: list) -> str:
+    out, i = [], 0
+    cpus = sorted(cpus)
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def module_run(args) -> dict:
@@ -133,16 +161,26 @@ def main():
     # the module on its own ticker at the streams' real rate: throughput = the offered load,
     # plus the latency it adds (fixed tick vs reflect-on-arrival)
     ap.add_argument("--realtime", action="store_true")
+    # gpu-node: every run (the fake server with its pusher threads and either module, and the
+    # reference reflector's processes) on the CPUs of the GPU's NUMA node, as a server is deployed
+    # next to its GPU; none: wherever the scheduler puts them (the box allows both sockets)
+    ap.add_argument("--affinity", choices=["gpu-node", "none"], default="gpu-node")
     args = ap.parse_args()
+    affinity = {"mode": args.affinity}
+    if args.affinity == "gpu-node":
+        cpus = gpu_node_cpus()
+        os.sched_setaffinity(0, cpus)                  # inherited by every run started below
+        affinity.update(cpus=cpu_ranges(cpus), n_cpus=len(cpus))
     if args.realtime:
         print(json.dumps({"workload": f"C2 at its real rate through the QTSS module: {args.sessions} RTSP-interleaved "
                                       f"H.264 30-fps pushers x {args.subs} UDP players, {args.threads} pusher threads, "
-                                      f"the module's own ticker", "runs": realtime_runs(args)}))
+                                      f"the module's own ticker", "affinity": affinity, "runs": realtime_runs(args)}))
         return
     out = {"workload": f"C2 through the QTSS module: {args.sessions} RTSP-interleaved H.264 pushers x {args.subs} "
                        f"UDP players, {args.tick_ms}-ms ticks, {args.threads} pusher threads "
                        f"({'concurrent with' if args.concurrent_push else 'alternating with'} the ticks)",
            "write_threads": int(os.environ.get("EDGPU_QTSS_WRITE_THREADS", args.write_threads)),
+           "affinity": affinity,
            "module": module_run(args)}
     m = out["module"]
     pt = m["per_tick_bytes"]
