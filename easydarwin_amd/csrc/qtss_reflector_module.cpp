@@ -71,8 +71,6 @@
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <poll.h>
-#include <pthread.h>
-#include <sched.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -287,7 +285,6 @@ struct Module {
     bool manualTick = false;
     std::vector<UdpPair> udp;
     std::thread ticker, reader;
-    std::vector<uint32_t> cpus;            // the GPU's NUMA node (EDGPU_QTSS_AFFINITY), or empty
     std::atomic<bool> stop{false};
     QTSS_Error tickErr = QTSS_NoErr;
     EDGPU_QTSSTickInfo lastTick{};      // guarded by mu
@@ -749,16 +746,6 @@ void ReadModulePrefsLocked() {
     M->broadcasterTimeoutMs = std::max<uint32_t>(bsecs, 30) * 1000;
 }
 
-// A module thread onto the GPU's NUMA node (M->cpus; best effort, nothing when empty).
-static void PinToGpuNode(std::thread& t) {
-    if (M->cpus.empty() || !t.joinable()) return;
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    for (uint32_t c : M->cpus)
-        if (c < CPU_SETSIZE) CPU_SET(c, &set);
-    (void)pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);
-}
-
 QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     std::lock_guard<std::mutex> g(M->mu);
     if (const char* v = getenv("EDGPU_QTSS_TICK_MSEC")) M->tickMs = (uint32_t)std::max(1, atoi(v));
@@ -815,21 +802,6 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     // threads that make a tick's QTSS_Write calls (each player's writes stay on one thread)
     uint32_t writers = 4;
     if (const char* v = getenv("EDGPU_QTSS_WRITE_THREADS")) writers = (uint32_t)std::max(1, atoi(v));
-    // the module's host threads stay on the GPU's NUMA node (EDGPU_QTSS_AFFINITY=0: where the
-    // scheduler puts them): the pinned batch and readback buffers and the tick's locks are then
-    // shared within one socket
-    bool pin = true;
-    if (const char* v = getenv("EDGPU_QTSS_AFFINITY")) pin = atoi(v) != 0;
-    M->cpus.clear();
-    if (pin) {
-        std::vector<uint32_t> cpus(4096);
-        uint32_t n = 0;
-        if (edgpu_device_local_cpus(cfg.device, cpus.data(), (uint32_t)cpus.size(), &n) == EDGPU_OK && n) {
-            cpus.resize(std::min<uint32_t>(n, (uint32_t)cpus.size()));
-            M->cpus = cpus;
-            M->R->SetAffinity(cpus.data(), (uint32_t)cpus.size());
-        }
-    }
     M->R->SetWriteThreads(writers);
     // the tick's writes run without the engine lock (EDGPU_QTSS_CONCURRENT_DELIVERY=0: held throughout)
     bool concurrent = true;
@@ -859,7 +831,6 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
                 if (e) M->tickErr = e;
             }
         });
-        for (std::thread* t : {&M->reader, &M->ticker}) PinToGpuNode(*t);
     }
     return QTSS_NoErr;
 }

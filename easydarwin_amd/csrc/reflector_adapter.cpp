@@ -7,8 +7,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <emmintrin.h>
-#include <pthread.h>
-#include <sched.h>
 
 namespace edgpu_reflector {
 
@@ -795,27 +793,7 @@ void Reflector::SetWriteThreads(uint32_t n) {
     fWorkers.clear();
     fPoolStop = false;
     fNumWriters = n;
-    for (uint32_t k = 1; k < n; k++) {
-        fWorkers.emplace_back([this, k] { WorkerLoop(k); });
-        PinThread(fWorkers.back());
-    }
-}
-
-void Reflector::PinThread(std::thread& t) const {
-    if (fCpus.empty() || !t.joinable()) return;
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    for (uint32_t c : fCpus)
-        if (c < CPU_SETSIZE) CPU_SET(c, &set);
-    (void)pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);   // best effort
-}
-
-void Reflector::SetAffinity(const uint32_t* cpus, uint32_t n) {
-    std::unique_lock<std::mutex> eg(fEngineMu);
-    WaitIdle(eg);
-    fCpus.assign(cpus, cpus + (cpus ? n : 0));
-    for (std::thread& t : fWorkers) PinThread(t);
-    PinThread(fStager);
+    for (uint32_t k = 1; k < n; k++) fWorkers.emplace_back([this, k] { WorkerLoop(k); });
 }
 
 // ---------------------------------------------------------------------------------------

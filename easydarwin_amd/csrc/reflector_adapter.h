@@ -155,9 +155,6 @@ public:
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
     // threads that deliver a tick's writes (default 1; at most 64); call between ticks
     void SetWriteThreads(uint32_t n);
-    // keep the adapter's own threads (write workers, the batch stager) on these CPUs -- the GPU's
-    // NUMA node (edgpu_device_local_cpus) -- from now on; an empty set leaves them where they are
-    void SetAffinity(const uint32_t* cpus, uint32_t n);
     // the tick's writes run without the engine lock (see Threading above); default off
     void SetConcurrentDelivery(bool on);
     // the engine lock, for code that calls the edgpu ABI on Context() itself (CKeyFrameCache::LoadGOP)
@@ -304,8 +301,6 @@ private:
     uint8_t* fHostOut = nullptr; uint64_t fHostOutCap = 0;  // pinned: the tick's gathered bytes (edgpu_arena_gather target)
     TickInfo fTick;
     // write threads (workers 1..n-1; the ticking thread is worker 0)
-    std::vector<uint32_t> fCpus;                            // SetAffinity
-    void PinThread(std::thread& t) const;
     uint32_t fNumWriters = 1;
     std::vector<std::thread> fWorkers;
     std::mutex fPoolMu;

@@ -803,9 +803,9 @@ int  edgpu_memcpy_peer(edgpu_ctx* ctx, void* dst, int src_device, const void* sr
 int  edgpu_device_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_device_free(edgpu_ctx* ctx, void* ptr);
 /* The host CPUs of device `device`'s NUMA node (the sysfs local_cpulist of its PCI function) that
- * the calling thread may run on: cpus[0 .. min(*n_out, cap)), *n_out = how many.  The drop-in
- * module keeps its write, tick and reader threads on them (EDGPU_QTSS_AFFINITY=0: it does not).
- * No reference counterpart (host placement next to the GPU). */
+ * the calling thread may run on: cpus[0 .. min(*n_out, cap)), *n_out = how many -- where a server
+ * hosting the module belongs (tools/bench_module.py --affinity gpu-node).  No
+ * reference counterpart (host placement next to the GPU). */
 int  edgpu_device_local_cpus(int device, uint32_t* cpus, uint32_t cap, uint32_t* n_out);
 
 #ifdef __cplusplus

@@ -25,7 +25,7 @@ on push + reflect (with_ingest_per_s), as the module's rate counts both.
 Placement (--affinity): by default every run -- the fake server with its pusher threads and either
 module, and the reference reflector's processes -- runs on the CPUs of the GPU's NUMA node, as a
 server is deployed next to its GPU; `none` leaves them to the scheduler (the box allows both
-sockets).  The drop-in also keeps its own threads on that node (EDGPU_QTSS_AFFINITY).
+sockets).
 
 Prints one JSON object.  Needs a GPU (the module initialises an edgpu context).
 """

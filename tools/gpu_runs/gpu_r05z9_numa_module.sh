@@ -1,6 +1,7 @@
 # round 5: the module with its threads on the GPU's NUMA node (EDGPU_QTSS_AFFINITY, default on) and
 # tools/bench_module.py --affinity gpu-node (every side on that node) against --affinity none and
 # the module's own pinning off.  Module tests first.  Logs under gpurun_out/$1.
+# (EDGPU_QTSS_AFFINITY was removed after this run: the module's own pinning measured no gain.)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
