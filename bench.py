@@ -129,6 +129,64 @@ def run_step(ctx: edgpu.Context, bt: dict):
     ctx.fanout(bt["t"])
 
 
+def cross_device_check(ctx, args, gids, world: int, rank: int, backend: str, local: int, sdp: str, now_ms: int,
+                       k: int = 16) -> dict:
+    """N > 1, after the timed steps (untimed): BASELINE C4's cross-GPU exchange on the node's own
+    devices.  Every rank takes replicas of the first k sessions of the next rank and brings their
+    session images over with dist.exchange_images (DistReplicaLink.sync: RCCL batch_isend_irecv
+    between the GPUs' device buffers under nccl, host buffers under gloo); then each replica's GOP
+    (the CKeyFrameCache image, key packet -> newest) must equal its owner's byte for byte."""
+    import hashlib
+    import torch.distributed as tdist
+    from easydarwin_amd.replica import DistReplicaLink
+    torch.cuda.set_device(local)                      # (a thread of its own: HIP's device is per thread)
+    link = DistReplicaLink(ctx, world, rank, comm="cuda" if backend == "nccl" else "cpu")
+    for si, g in enumerate(gids):
+        link.own(int(g), si)
+    want = [int(g) for g in owned_sessions(args.sessions, (rank + 1) % world, world)[:k]]
+    for g in want:
+        link.want(g, sdp)
+    tdist.barrier()
+    t0 = time.perf_counter()
+    sent, recv = link.sync(now_ms)
+    ms = (time.perf_counter() - t0) * 1e3
+
+    def digest(s):
+        return hashlib.sha256(ctx.gop_copy(s, 0)[0]).hexdigest()
+    mine = {int(g): digest(si) for si, g in enumerate(gids[:k])}
+    every = [None] * world
+    tdist.all_gather_object(every, mine)
+    owners = {g: d for m in every for g, d in m.items()}
+    ok = all(digest(link.replica_of[g]) == owners[g] for g in want)
+    res = [None] * world
+    tdist.all_gather_object(res, (ok, int(sent), int(recv), ms))
+    return {"ok": all(r[0] for r in res), "ranks": world, "sessions_per_rank": k,
+            "image_bytes": sum(r[1] for r in res), "received_bytes": sum(r[2] for r in res),
+            "ms_max": round(max(r[3] for r in res), 3),
+            "transport": ("RCCL batch_isend_irecv, device buffers on distinct GPUs" if backend == "nccl"
+                          else "gloo, host buffers (ranks may share a GPU)"),
+            "check": "each replica's GOP image (key packet -> newest) equals its owner's (sha256)"}
+
+
+def run_bounded(fn, seconds: float):
+    """fn() on a thread of its own, waited for at most `seconds`: (result, hung).  An exception is
+    a failed result; a hang leaves the thread behind (the caller then ends the process)."""
+    import threading
+    out = {}
+
+    def work():
+        try:
+            out["v"] = fn()
+        except Exception as e:                        # noqa: BLE001 -- reported in the line
+            out["v"] = {"ok": False, "error": f"{type(e).__name__}: {e}"}
+    th = threading.Thread(target=work, daemon=True)
+    th.start()
+    th.join(seconds)
+    if th.is_alive():
+        return {"ok": False, "error": f"timed out after {seconds:.0f} s"}, True
+    return out["v"], False
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -576,8 +634,17 @@ def main():
 
     dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None,
                                           force=force_pg)
+    # N > 1: the C4 session-image exchange across the devices, checked (after the timing; bounded:
+    # a hung exchange is reported and the process ends without waiting for it)
+    xdev, hung = None, False
+    if dist and world > 1:
+        now_ms = int(batches[warm + steps + extra - 1]["t"])
+        xdev, hung = run_bounded(lambda: cross_device_check(ctx, args, gids, world, rank, backend, local,
+                                                            fleet.sdp(), now_ms), 120.0)
 
     if rank != 0:
+        if hung:
+            os._exit(0)
         if dist:
             dist.destroy_process_group()
         return
@@ -683,7 +750,11 @@ def main():
                       "and 7.9 M in reference-exact one-datagram-per-send mode vs the reference's sendto() path "
                       "at 7.9 M on the same box (profiles/r05z_wire/, DESIGN.md 5.6)"),
     }
+    if xdev is not None:
+        res["cross_device"] = xdev
     print(json.dumps(res), flush=True)
+    if hung:
+        os._exit(0)
     if dist:
         dist.destroy_process_group()
 
