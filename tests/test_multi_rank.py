@@ -109,3 +109,18 @@ def test_owned_sessions_balance_a_hash_sharded_population():
         for r, p in enumerate(parts):
             assert all(fnv1a64(stream_id(int(g))) % world == r for g in p)
     assert owned_sessions(64, 0, 1).tolist() == list(range(64))
+
+
+def test_bench_bounded_check_reports_hangs_and_errors():
+    """bench.py's cross-device check runs bounded (run_bounded): a result passes through, an
+    exception becomes a failed result, and a hang is reported after the deadline instead of
+    holding up the line."""
+    import threading
+    import bench
+    assert bench.run_bounded(lambda: {"ok": True}, 5.0) == ({"ok": True}, False)
+    res, hung = bench.run_bounded(lambda: 1 / 0, 5.0)
+    assert not hung and res["ok"] is False and "ZeroDivisionError" in res["error"]
+    stop = threading.Event()
+    res, hung = bench.run_bounded(lambda: stop.wait(30), 0.2)
+    stop.set()
+    assert hung and res == {"ok": False, "error": "timed out after 0 s"}
