@@ -84,6 +84,29 @@ __device__ __forceinline__ uint32_t packet_ssrc(const uint8_t* p, uint32_t len, 
     return be32(p + 8);
 }
 
+// Inclusive scan of a 64-bit value across the wave, in registers: DPP row shifts (1, 2, 4, 8)
+// give each row of 16 lanes its own prefix, then every lane adds the totals of the rows before its
+// own (lanes 15, 31, 47, read as scalars).  Call with every lane active.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+__device__ __forceinline__ uint64_t wave_inclusive_scan_u64(uint64_t x) {
+    x += dpp_u64<0x111>(x);                 // row_shr:1 (a row's first lanes read 0)
+    x += dpp_u64<0x112>(x);                 // row_shr:2
+    x += dpp_u64<0x114>(x);                 // row_shr:4
+    x += dpp_u64<0x118>(x);                 // row_shr:8
+    const uint64_t r0 = readlane_u64(x, 15), r1 = readlane_u64(x, 31), r2 = readlane_u64(x, 47);
+    const int row = (threadIdx.x & 63) >> 4;
+    return x + (row >= 1 ? r0 : 0ull) + (row >= 2 ? r1 : 0ull) + (row >= 3 ? r2 : 0ull);
+}
+
 // Exclusive scan over a workgroup of NW waves of 64 (256 threads by default).  `scratch` holds
 // NW entries.
 template <typename T, int NW = 4>
@@ -310,7 +333,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint64_t s_meta[kMaxSendersPerSession], s_ring[kMaxSendersPerSession];
     __shared__ uint64_t s_count[kMaxTracks];
     __shared__ uint64_t c_tot[kMaxSendersPerSession];
-    __shared__ uint32_t c_ttot[kMaxTracks];
+    __shared__ uint64_t s_wsum[kMaxSendersPerSession][NW];    // per sender, each wave's total
     __shared__ int c_last[kMaxSendersPerSession];   // (tid << 10 | rank) of the chunk's newest non-empty packet
     __shared__ int c_lastacc[kMaxSendersPerSession];  // lane of the chunk's newest accepted packet, per socket
     // per packet of the current chunk
@@ -323,7 +346,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint32_t p_slotb[THREADS];
     __shared__ uint64_t p_vb[THREADS];
     __shared__ uint64_t scan64[NW];
-    __shared__ uint32_t scan32[NW];
     // interleaved ingest: the session's chunk table (frame end of each chunk, the recorded
     // candidate or kTcpNone) and its reads, for every lane's frame lookup
     constexpr uint32_t kLdsChunks = 256, kLdsReads = 64;
@@ -509,25 +531,38 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         const bool nz = acc && len > 0;
         const uint32_t slotb = nz ? ((len + 4 + 15) & ~15u) : 0;
         // ---- per-sender queue index / slot offset / non-empty count ----
-        uint32_t my_rank = 0, my_nzpre = 0;
+        // Every sender of the session in one pass: each wave scans (count | non-empty << 10 | slot
+        // bytes << 20) per sender in registers (wave_inclusive_scan_u64), the wave totals meet in
+        // LDS across one barrier.  A packet keeps the prefixes of its own sender and of its track's
+        // other one (RTP / RTCP, ls ^ 1): its rank in the track (fStreamCountID order) is their sum.
+        uint32_t my_rank = 0, my_nzpre = 0, my_trank = 0;
         uint64_t my_slotpre = 0;
-        for (uint32_t s = 0; s < ((EDGPU_ABL(P) & 64u) ? 0u : nsnd); s++) {
-            const bool mine = acc && ls == s;
-            const uint64_t x = mine ? (1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20) : 0ull;
-            uint64_t tot;
-            const uint64_t pre = block_exclusive_scan<uint64_t, NW>(x, scan64, tot);
-            if (mine) { my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20; }
-            if (tid == 0) c_tot[s] = tot;
+        {
+            const int lane = tid & 63, wid = tid >> 6;
+            const uint64_t mx = 1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20;
+            const uint32_t ns = (EDGPU_ABL(P) & 64u) ? 0u : nsnd;
+            uint64_t my_incl = 0, sib_incl = 0;
+            for (uint32_t s = 0; s < ns; s++) {                      // uniform
+                const uint64_t incl = wave_inclusive_scan_u64(acc && ls == s ? mx : 0ull);
+                if (lane == 63) s_wsum[s][wid] = incl;
+                if (ls == s) my_incl = incl;
+                if ((ls ^ 1u) == s) sib_incl = incl;
+            }
+            __syncthreads();
+            if (tid < (int)ns) {
+                uint64_t t = 0;
+                for (int w = 0; w < NW; w++) t += s_wsum[tid][w];
+                c_tot[tid] = t;
+            }
+            if (acc && ns) {                                         // (acc: ls < nsnd)
+                uint64_t mb = 0, sb = 0;
+                for (int w = 0; w < wid; w++) { mb += s_wsum[ls][w]; sb += s_wsum[ls ^ 1u][w]; }
+                const uint64_t pre = mb + my_incl - mx;
+                my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20;
+                my_trank = my_rank + (uint32_t)((sb + sib_incl) & 1023);
+            }
         }
         if (nz) atomicMax(&c_last[ls], tid << 10 | (int)my_rank);
-        uint32_t my_trank = 0;
-        for (uint32_t t = 0; t < S.ntracks; t++) {
-            const bool mine = acc && track == t;
-            uint32_t tot;
-            const uint32_t pre = block_exclusive_scan<uint32_t, NW>(mine ? 1u : 0u, scan32, tot);
-            if (mine) my_trank = pre;
-            if (tid == 0) c_ttot[t] = tot;
-        }
         uint64_t idx = 0, vb = 0;
         if (acc) {
             idx = s_head[ls] + my_rank;
@@ -639,7 +674,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             s_vcount[tid] += (uint32_t)((t >> 10) & 1023);
             s_vbyte[tid] += t >> 20;
         }
-        if (tid < (int)S.ntracks) s_count[tid] += c_ttot[tid];
+        if (tid < (int)S.ntracks) s_count[tid] += (c_tot[2 * tid] & 1023) + (c_tot[2 * tid + 1] & 1023);
         if (tid < (int)nsnd) c_lastacc[tid] = -1;
         __syncthreads();
     }
