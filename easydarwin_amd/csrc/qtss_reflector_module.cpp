@@ -59,7 +59,7 @@
 // one stripe of the Reflector's push path, and the UDP reader thread takes only `udpMu` -- so a
 // pusher never waits for a tick, and pushers of different sessions rarely share a lock.
 //
-// Scope: RTSP-interleaved pushers (EasyPusher's default transport), UDP
+// Scope (docs/PARITY.md §4.10): RTSP-interleaved pushers (EasyPusher's default transport), UDP
 // pushers and UDP / TCP players.  A UDP push SETUP binds the track's even/odd socket pair as
 // ReflectorStream::BindSockets does (ReflectorStream.cpp:388-500, UDPSocketPool.cpp:81-150) and
 // answers with its port (qtssRTSPReqSetUpServerPort, QTSSReflectorModule.cpp:1686-1688); a

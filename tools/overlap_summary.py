@@ -1,7 +1,7 @@
 """Summarises a rocprofv3 --kernel-trace --memory-copy-trace run of `bench.py --ingest host`:
 for each large host->device copy (an ingest batch's blob), how much of it ran while an engine
 kernel was running (the previous tick's fan-out / ingest), i.e. the PCIe overlap that the
-pinned, double-buffered staging buys.
+pinned, double-buffered staging buys (docs/PARITY.md §4.12).
 Usage: python tools/overlap_summary.py <trace dir> <out.json>"""
 import csv
 import glob
