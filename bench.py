@@ -686,10 +686,10 @@ def main():
     ing_ach = ing_alg / (ing_ms / 1e3) / 1e9
     ingest = {"kernels": "k_ingest + k_tcp_* deframe" if args.ingest == "tcp" else "k_ingest",
               # HIP events on the context stream: with RTSP-interleaved reads the deframe kernels
-              # run on a second stream beside the previous tick's fan-out, so this is the time the
-              # ingest adds to the step (the deframe's exposed part + k_ingest), not a kernel sum
-              "timing": ("exposed: deframe overlapped with the previous tick's fan-out, then k_ingest"
-                         if args.ingest == "tcp" else "k_ingest launch duration"),
+              # run on a second stream beside the previous tick's fan-out (the host reads their
+              # report, then enqueues k_ingest), so this is the time the ingest adds to the step
+              "timing": ("exposed: the deframe runs beside the previous tick's fan-out; the context stream "
+                         "sees k_ingest" if args.ingest == "tcp" else "k_ingest launch duration"),
               "alg_bytes_per_launch": int(ing_alg), "avg_ms": round(ing_ms, 4), "achieved": round(ing_ach, 1),
               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ing_ach / HBM_PEAK_GBS, 4),
               "traffic": ing_traffic, "traffic_source": traffic_source if ing_traffic else None}
