@@ -392,3 +392,13 @@ def test_fanout_sources_point_into_the_last_host_batch():
         ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)  # a new output: the GOP from batch 1 + batch 2
         n = check(b2, 10)                           # 5 new packets x 2 outputs have sources
         assert n == 5 + 12 + 5
+
+
+@pytest.mark.gpu
+def test_device_local_cpus_are_the_gpus_node_within_the_allowed_set():
+    """edgpu_device_local_cpus: the GPU's NUMA node (its PCI function's sysfs local_cpulist), only
+    CPUs this process may run on, and non-empty on an MI355X host."""
+    import os
+    cpus = edgpu.device_local_cpus(0)
+    assert cpus and len(set(cpus)) == len(cpus)
+    assert set(cpus) <= os.sched_getaffinity(0)
