@@ -223,6 +223,7 @@ struct edgpu_ctx {
     int device = 0;
     int num_cus = 256;
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
+    uint64_t joined_rows = 0;       // sub-stream rows of the outputs added since the last tick
     bool deframe_serial = false;    // EDGPU_DEFRAME_SERIAL (measurement): no deframe / fan-out overlap
     uint32_t ablate = 0;
     int timing = EDGPU_TIMING_ALL;  // edgpu_set_timing: which per-launch event pairs are recorded
@@ -1052,6 +1053,7 @@ static uint32_t append_subscriber(edgpu_ctx* x, uint32_t session, int transport,
     SessionHost& sh = x->sessions[session];
     const uint32_t handle = (uint32_t)x->subscribers.size();
     const uint32_t nsub = 2 * sh.ntracks;
+    x->joined_rows += nsub;
     uint32_t first = (uint32_t)x->sub_sender.size(), span = nsub;
     auto fr = x->free_subs.lower_bound(nsub);      // the smallest free range that fits
     while (fr != x->free_subs.end() && fr->second.empty()) ++fr;
@@ -1836,7 +1838,14 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
 // The copy kernel for this tick: EDGPU_FANOUT when set, else the default for whether any active
 // sub-stream needs a per-output patch (TCP channel byte or rewrite).
 static int pick_fanout_variant(const edgpu_ctx* x) {
-    return x->fanout_variant >= 0 ? x->fanout_variant : fanout_default(x->n_rw + x->n_tcp > 0);
+    if (x->fanout_variant >= 0) return x->fanout_variant;
+    // A tick whose new outputs hold a quarter or more of its sub-stream rows, and at least
+    // kBurstRows of them, replays a GOP to each (C4's join burst): long runs per sub-stream, which
+    // the patching kernel's 32-packet chunks move ~3 % faster than the 16-packet ones
+    // (profiles/r05zi_c4_variants/); the steady ticks keep the 16-packet kernel.
+    constexpr uint64_t kBurstRows = 4096;
+    const bool burst = x->joined_rows >= kBurstRows && x->joined_rows * 4 >= x->sub_sender.size();
+    return fanout_default(x->n_rw + x->n_tcp > 0 || burst);
 }
 
 // The plan parameters of the context's current tick (arena / descriptor buffers of x->cur).
@@ -1920,6 +1929,7 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     x->last_now = now_ms;
     queue_source_reports(x, now_ms);
     x->tick_variant = pick_fanout_variant(x);
+    x->joined_rows = 0;
     x->pass_ord = 0;
     x->pass_id = 0;
     const PlanParams p = plan_params(x, now_ms);
@@ -1972,7 +1982,8 @@ int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched
 }
 
 const char* edgpu_fanout_kernel(edgpu_ctx* x) {
-    return x ? fanout_name(pick_fanout_variant(x)) : "";
+    if (!x) return "";
+    return fanout_name(x->fanout_launches ? x->tick_variant : pick_fanout_variant(x));
 }
 
 int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {

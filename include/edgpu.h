@@ -682,9 +682,11 @@ typedef struct edgpu_region {
 int  edgpu_arena_gather(edgpu_ctx* ctx, const edgpu_fanout_result* r, const edgpu_region* regions, uint32_t n,
                         void* dst, uint64_t dst_cap);
 
-/* Name of the fan-out copy kernel this context's next edgpu_fanout launches (for measurement
- * reports): unless EDGPU_FANOUT selects one, it depends on whether any active sub-stream is
- * RTSP-interleaved or rewrites (a per-output patch), see DESIGN.md §3. */
+/* Name of the fan-out copy kernel of this context's last edgpu_fanout (before the first: the one
+ * it would launch), for measurement reports.  Unless EDGPU_FANOUT selects one, a tick takes the
+ * 32-packet-chunk kernel when any active sub-stream is RTSP-interleaved or rewrites (a per-output
+ * patch) or when the outputs added since the last tick hold a quarter or more of its sub-stream
+ * rows and at least 4096 of them (a join burst), else the 16-packet-chunk one; see DESIGN.md §3. */
 const char* edgpu_fanout_kernel(edgpu_ctx* ctx);
 
 /* Cumulative counters since context creation (syncs).  fanout_in_bytes counts the

@@ -245,7 +245,6 @@ def test_fanout_kernel_follows_patching_substreams():
 
         def tick(expect_kernel, expect_relayed):
             nonlocal seq, relayed
-            assert ctx.fanout_kernel().startswith(expect_kernel)
             # one IDR packet (the key pointer) first, then non-key slices
             pk = [(s, 0, 10 * seq + k, _rtp(seq + k, 3000 * seq, payload=(b"\x65" if seq + k == 0 else b"\x41") + b"\x00" * 40))
                   for k in range(5)]
@@ -256,6 +255,7 @@ def test_fanout_kernel_follows_patching_substreams():
             st = ctx.stats()
             assert st.status == 0
             assert st.relayed_packets == expect_relayed
+            assert ctx.fanout_kernel().startswith(expect_kernel)     # the kernel that tick used
 
         tick(plain, 5)                       # the first tick: the UDP output starts at the key packet
         t = ctx.subscriber_add(s, edgpu.TRANSPORT_TCP)
@@ -266,6 +266,12 @@ def test_fanout_kernel_follows_patching_substreams():
         tick(patching, 5)
         ctx.subscriber_rewrite(u, 0)         # identity again
         tick(plain, 5)
+        # a join burst (new outputs: at least 4096 sub-stream rows and a quarter of the tick's)
+        # replays the GOP to each through the 32-packet kernel; the tick after is steady again
+        for _ in range(2100):
+            ctx.subscriber_add(s, edgpu.TRANSPORT_UDP)
+        tick(patching, 5 + 2100 * 30)
+        tick(plain, 5 * 2101)
 
 
 @pytest.mark.gpu
