@@ -642,8 +642,11 @@ def main():
         xdev, hung = run_bounded(lambda: cross_device_check(ctx, args, gids, world, rank, backend, local,
                                                             fleet.sdp(), now_ms), 120.0)
 
+    # a failed or hung check may leave other ranks inside a collective: end without tearing the
+    # process group down (which could wait on them)
+    bail = hung or (xdev is not None and not xdev.get("ok"))
     if rank != 0:
-        if hung:
+        if bail:
             os._exit(0)
         if dist:
             dist.destroy_process_group()
@@ -753,7 +756,7 @@ def main():
     if xdev is not None:
         res["cross_device"] = xdev
     print(json.dumps(res), flush=True)
-    if hung:
+    if bail:
         os._exit(0)
     if dist:
         dist.destroy_process_group()
