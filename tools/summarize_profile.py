@@ -47,7 +47,11 @@ for k in res["kernels"]:
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if r["Kernel_Name"] == k]
     if d:
         res["kernels"][k]["avg_duration_ns_rocprof_timed"] = statistics.mean(d[-bench["steps"]:])
-fan_name = next((k for k in res["kernels"] if k.startswith("k_fanout")), None)
+# the bench line's copy kernel (a run's first tick may take the join-burst kernel: every
+# subscriber joins before it), matched on the truncated name rocprofv3 -T gives
+want = bench["roofline"]["kernel"].split("<")[0]
+fan_name = next((k for k in res["kernels"] if k == want), None) or \
+    next((k for k in res["kernels"] if k.startswith("k_fanout")), None)
 fan = res["kernels"].get(fan_name, {})
 res["fanout_kernel"] = fan_name                              # rocprofv3 -T (truncated) name
 res["bench_fanout_kernel"] = bench["roofline"]["kernel"]     # the engine's variant name (template args)
