@@ -750,8 +750,8 @@ def main():
         # (sendmmsg / writev over PCIe-copied bytes): tools/bench_egress.py, DESIGN.md §5.6
         "wire_note": ("value counts relayed packets made send-ready in HBM (the north_star metric); on sockets "
                       "the engine's egress is host-bound: tools/bench_egress.py, 41 M datagrams/s with UDP GSO "
-                      "and 7.9 M in reference-exact one-datagram-per-send mode vs the reference's sendto() path "
-                      "at 7.9 M on the same box (profiles/r05z_wire/, DESIGN.md 5.6)"),
+                      "and 7.1-7.9 M in reference-exact one-datagram-per-send mode, 0.85-1.00x the reference's "
+                      "sendto() path on the same box (profiles/r05z_wire/, DESIGN.md 5.6)"),
     }
     if xdev is not None:
         res["cross_device"] = xdev
