@@ -749,7 +749,7 @@ def main():
         # the metric counts packets made send-ready in HBM; what reaches sockets is host-bound
         # (sendmmsg / writev over PCIe-copied bytes): tools/bench_egress.py, DESIGN.md §5.6
         "wire_note": ("value counts relayed packets made send-ready in HBM (the north_star metric); on sockets "
-                      "the engine's egress is host-bound: tools/bench_egress.py, 41 M datagrams/s with UDP GSO "
+                      "the engine's egress is host-bound: tools/bench_egress.py, 46 M datagrams/s with UDP GSO "
                       "and 7.1-7.9 M in reference-exact one-datagram-per-send mode, 0.85-1.00x the reference's "
                       "sendto() path on the same box (profiles/r05z_wire/, DESIGN.md 5.6)"),
     }

@@ -530,11 +530,20 @@ static int send_pass(edgpu_egress* e, const edgpu_fanout_result* r, const edgpu_
         w.blocked.clear(); w.why.clear();
         w.udp_datagrams = w.udp_bytes = w.udp_dropped = w.tcp_frames = w.tcp_bytes = w.stale = 0;
     }
+    // Which worker sends a row: a TCP connection's rows, and every row of a paced subscriber, on
+    // the worker of their subscriber (one connection's frames in order, the pacing state without a
+    // lock); plain UDP rows in blocks of consecutive rows -- a subscriber's rows are contiguous and
+    // a session's subscribers mostly so -- so a worker sends whole sessions and reads their shared
+    // regions of the pinned tick from its own caches instead of every worker reading every region.
+    constexpr uint32_t kRowBlock = 64;
+    const bool any_paced = !e->paced.empty();
     auto run = [&](uint32_t k) {
         Worker& w = e->workers[k];
         for (uint32_t q = 0; q < (uint32_t)e->subs.size(); q++) {
             const edgpu_substream_out& s = e->subs[q];
-            if (s.desc_count == 0 || s.subscriber % e->nthreads != k) continue;
+            if (s.desc_count == 0) continue;
+            const bool by_sub = any_paced || s.transport == EDGPU_TRANSPORT_TCP;
+            if ((by_sub ? s.subscriber : q / kRowBlock) % e->nthreads != k) continue;
             auto pc = e->paced.find(s.subscriber);
             if (pc != e->paced.end()) {                  // (one worker owns a subscriber: no lock)
                 if (s.transport == EDGPU_TRANSPORT_TCP) {
