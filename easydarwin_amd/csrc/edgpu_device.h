@@ -84,6 +84,15 @@ struct SenderDev {
     // ring entry, same index), written by k_ingest
     uint64_t batch_lo;
     uint32_t batch_epoch, _pad_b;
+    // ReflectorSocket's receive-time state (reflector_use_in_packet_receive_time, ReflectorStream.h:
+    // 251-254, .cpp:1960-1994): the socket's first trailer-tagged packet of the current SSRC
+    // anchors the arrival clock of every tagged packet after it
+    uint32_t rt_has, rt_ssrc;       // fHasReceiveTime, fCurrentSSRC
+    int64_t  rt_first_arrival;      // fFirstArrivalTime
+    uint64_t rt_first_receive;      // fFirstReceiveTime
+    uint32_t rt_nonmono;            // a tagged packet was enqueued: arrivals along the ring need not
+                                    // be monotone, so arrival searches walk it (first_arrival_at)
+    uint32_t _pad_rt;
 };
 
 // ---- Session images (cross-GPU keyframe fast start) ----
@@ -119,7 +128,8 @@ struct ImgSender {                  // 96 B
     int64_t  last_nonzero;
     uint64_t meta_off, bytes_off;   // from the image start
     uint32_t delta, flags;
-    uint64_t _pad;
+    uint32_t nonmono;               // SenderDev.rt_nonmono: the carried arrivals need not be monotone
+    uint32_t _pad;
 };
 
 struct ImgPlan {                    // one sender of one image (export or import)

@@ -438,6 +438,10 @@ static void fill_defaults(edgpu_config& c) {
     c.ring_growth = (c.ring_growth == EDGPU_FALSE) ? 0 : 1;
     if (!c.max_ring_packets) c.max_ring_packets = 1u << 20;
     if (!c.max_ring_bytes) c.max_ring_bytes = 1ull << 30;
+    c.reflector_use_in_packet_receive_time = (c.reflector_use_in_packet_receive_time &&
+                                              c.reflector_use_in_packet_receive_time != EDGPU_FALSE) ? 1u : 0u;
+    if (!c.reflector_in_packet_max_receive_sec) c.reflector_in_packet_max_receive_sec = 60;
+    else if (c.reflector_in_packet_max_receive_sec == EDGPU_FALSE) c.reflector_in_packet_max_receive_sec = 0;
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -1475,6 +1479,9 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.totals = x->d_totals;
+    p.recv_time = x->cfg.reflector_use_in_packet_receive_time;
+    // sMaxFuturePacketMSec = sMaxFuturePacketSec * 1000 in UInt32 (ReflectorStream.cpp:113)
+    p.max_future_ms = (int64_t)(uint32_t)(x->cfg.reflector_in_packet_max_receive_sec * 1000u);
     p.tcp_groups = tcp ? tcp->groups : nullptr;
     p.tcp_chunkres = tcp ? tcp->chunkres : nullptr;
     p.tcp_offs = tcp ? tcp->offs : nullptr;

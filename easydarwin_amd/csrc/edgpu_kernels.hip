@@ -345,7 +345,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint64_t p_src[THREADS];     // slot / frame start address
     __shared__ uint32_t p_slotb[THREADS];
     __shared__ uint64_t p_vb[THREADS];
+    __shared__ int64_t p_arr[THREADS];      // receive-time trailer: the packet's arrival
     __shared__ uint64_t scan64[NW];
+    // ReflectorSocket receive-time state per socket (reflector_use_in_packet_receive_time)
+    __shared__ uint32_t s_rth[kMaxSendersPerSession], s_rts[kMaxSendersPerSession];
+    __shared__ int64_t s_rta[kMaxSendersPerSession];
+    __shared__ uint64_t s_rtr[kMaxSendersPerSession];
+    __shared__ uint32_t s_rtn;
     // interleaved ingest: the session's chunk table (frame end of each chunk, the recorded
     // candidate or kTcpNone) and its reads, for every lane's frame lookup
     constexpr uint32_t kLdsChunks = 256, kLdsReads = 64;
@@ -372,7 +378,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         s_valid[tid] = D.valid_ssrc; s_lastv[tid] = D.last_valid_s; s_lastnz[tid] = D.last_nonzero;
         s_flags[tid] = D.flags; s_pkmask[tid] = D.pk_mask; s_wmask[tid] = D.word_mask;
         s_meta[tid] = D.meta; s_ring[tid] = D.ring;
+        if (P.recv_time) { s_rth[tid] = D.rt_has; s_rts[tid] = D.rt_ssrc; s_rta[tid] = D.rt_first_arrival; s_rtr[tid] = D.rt_first_receive; }
     }
+    if (tid == 0) s_rtn = 0;
     if (tid < (int)S.ntracks) s_count[tid] = P.streams[S.first_stream + tid].packet_count;
     if (tid < (int)nsnd) c_lastacc[tid] = -1;
 #ifdef EDGPU_AB_VARIANTS
@@ -386,7 +394,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         const uint32_t i = base + tid;
         const bool valid = (uint32_t)tid < n;
         if (tid < (int)nsnd) c_last[tid] = -1;
-        uint32_t len = 0, track = 0, ls = 0, fl = 0, slot = 0;
+        uint32_t len = 0, track = 0, ls = 0, fl = 0, slot = 0, remote_odd = 0;
         uint64_t src = 0;
         int64_t arrival = 0;
         bool acc = false;
@@ -472,6 +480,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             ls = 2 * track + (d.channel & 1);
             arrival = d.arrival_ms;
             slot = d.slot;
+            remote_odd = d.flags & EDGPU_PKT_REMOTE_ODD;
             acc = track < S.ntracks && len > 0;       // ProcessRTPData: inIndex < numStreams
             const uint8_t* sp = P.src_addr ? reinterpret_cast<const uint8_t*>(P.src_addr[i])
                                            : P.blob + (uint64_t)slot * 16;
@@ -528,6 +537,49 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             __syncthreads();
             len = p_len[tid];
         }
+        // ---- receive-time trailer (ReflectorSocket::ProcessPacket, ReflectorStream.cpp:1960-1994):
+        // after the SSRC filter, a packet longer than 12 bytes whose last 12 are "aktt" + BE64
+        // receive time loses them, and its arrival becomes the socket's anchor arrival plus its
+        // receive time's offset from the anchor's -- the anchor being the socket's first tagged
+        // packet since its SSRC (GetSSRC by the REMOTE port's parity: 0 for a push over RTSP)
+        // last changed -- clamped to now + sMaxFuturePacketMSec.  Sequential per socket, so one
+        // lane walks a chunk that holds a tagged packet.  The key-frame test saw the whole packet
+        // (it ran first, :1876-1909) ----
+        const uint32_t len0 = len;
+        if (P.recv_time) {                                        // uniform
+            bool tag = false;
+            if (acc && len > 12) {
+                const uint8_t* t = pk + len - 12;
+                tag = t[0] == 'a' && t[1] == 'k' && t[2] == 't' && t[3] == 't';
+                if (tag) {
+                    uint64_t rt = 0;
+                    for (int k = 4; k < 12; k++) rt = rt << 8 | t[k];
+                    p_ts[tid] = (int64_t)rt;                      // (the SSRC filter is done with p_ts / p_ssrc)
+                    p_ssrc[tid] = remote_odd ? hbe32(hdr, 4) : hbe32(hdr, 8);
+                }
+            }
+            p_arr[tid] = arrival;
+            p_acc[tid] = tag ? 2u : 0u;
+            if (__syncthreads_or(tag ? 1 : 0)) {
+                if (tid == 0) {
+                    s_rtn = 1u;
+                    for (uint32_t p = 0; p < n; p++) {
+                        if (!(p_acc[p] & 2u)) continue;
+                        const uint32_t s = p_snd[p];
+                        const uint64_t rt = (uint64_t)p_ts[p];
+                        const int64_t now_p = p_arr[p];
+                        if (!s_rth[s] || s_rts[s] != p_ssrc[p]) {
+                            s_rts[s] = p_ssrc[p]; s_rta[s] = now_p; s_rtr[s] = rt; s_rth[s] = 1u;
+                        }
+                        int64_t a = s_rta[s] + (int64_t)(rt - s_rtr[s]);
+                        if (a - now_p > P.max_future_ms) a = now_p + P.max_future_ms;
+                        p_arr[p] = a;
+                    }
+                }
+                __syncthreads();
+                if (tag) { arrival = p_arr[tid]; len -= 12; p_len[tid] = (uint16_t)len; }   // (the copy's header / bound)
+            }
+        }
         const bool nz = acc && len > 0;
         const uint32_t slotb = nz ? ((len + 4 + 15) & ~15u) : 0;
         // ---- per-sender queue index / slot offset / non-empty count ----
@@ -578,9 +630,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             if (P.host_epoch)                            // its blob slot, for edgpu_fanout_sources
                 reinterpret_cast<uint32_t*>(s_meta[ls] + ((uint64_t)s_pkmask[ls] + 1) * sizeof(PktMeta))[idx & s_pkmask[ls]] = slot;
             const bool by_port_rtp = !(fl & kSndRtcpPort);
-            const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len >= 20 &&
-                             ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len)
-                                                          : key_frame_first_packet(pk, len));
+            const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len0 >= 20 &&
+                             ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len0)
+                                                          : key_frame_first_packet(pk, len0));
             const bool aud = by_port_rtp && (fl & kSndAudio);
             P.pflags[i] = 1u | (key ? 2u : 0u) | (aud ? 4u : 0u) | ls << 8;
             P.pidx[i] = idx;
@@ -684,6 +736,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (P.host_epoch) { D.batch_lo = D.head; D.batch_epoch = P.host_epoch; }   // (the head before the batch)
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
+        if (P.recv_time) {
+            D.rt_has = s_rth[tid]; D.rt_ssrc = s_rts[tid]; D.rt_first_arrival = s_rta[tid]; D.rt_first_receive = s_rtr[tid];
+            if (s_rtn) D.rt_nonmono = 1u;
+        }
         // tick pipelining, or a copy pass the last tick still owes (edgpu_fanout_next): this batch
         // must not lap what that tick's fan-out (possibly still running on the other stream) reads
         const bool guard = P.overlap || P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
@@ -837,6 +893,30 @@ __device__ uint64_t wave_lower_bound_meta(const PktMeta* meta, uint32_t mask, ui
     return hi;
 }
 
+// The first packet in [lo, hi) whose arrival is at least `cut`: GetClientBufferStartPacketOffset's
+// walk from the oldest packet (ReflectorStream.cpp:1209-1227) and RemoveOldPackets' first young
+// packet (:1245-1285).  Push times are monotone along a ring, so a binary search finds it -- until
+// receive-time trailers rewrote arrivals on the sender (rt_nonmono, :1960-1994): then the walk
+// itself, in arrival order as the reference walks its queue.  The wave form: every lane of the
+// wave calls it with the same arguments and gets the result.
+__device__ uint64_t first_arrival_at(const SenderDev& D, const PktMeta* meta, uint64_t lo, uint64_t hi, int64_t cut) {
+    if (!D.rt_nonmono) return lower_bound_meta(meta, D.pk_mask, lo, hi, [&](const PktMeta& m) { return m.arrival >= cut; });
+    for (; lo < hi; lo++)
+        if (meta[lo & D.pk_mask].arrival >= cut) break;
+    return lo;
+}
+__device__ uint64_t wave_first_arrival_at(const SenderDev& D, const PktMeta* meta, uint64_t lo, uint64_t hi, int64_t cut) {
+    if (!D.rt_nonmono)
+        return wave_lower_bound_meta(meta, D.pk_mask, lo, hi, [&](const PktMeta& m) { return m.arrival >= cut; });
+    const uint64_t lane = threadIdx.x & 63;
+    for (uint64_t b = lo; b < hi; b += 64) {
+        const uint64_t i = b + lane;
+        const unsigned long long t = __ballot(i < hi && meta[i & D.pk_mask].arrival >= cut ? 1 : 0);
+        if (t) return b + (uint64_t)(__ffsll(t) - 1);
+    }
+    return hi;
+}
+
 // K1: per sender, one wave each -- ring tail, fFirstPacketInQueueForNewOutput
 // (ReflectorStream.cpp:1058-1069).
 __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
@@ -886,8 +966,7 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
         if ((uint64_t)ns < tail) ns = -2;                      // key packet overwritten
     } else if (head > tail) {
         const int64_t cutoff = P.T.now - P.T.over_buffer_ms;  // now - arrival <= over buffer
-        const uint64_t f = wave_lower_bound_meta(meta, D.pk_mask, tail, head,
-                                                 [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        const uint64_t f = wave_first_arrival_at(D, meta, tail, head, cutoff);
         if (f < head) ns = (f == tail && tail > D.floor) ? -2 : (int64_t)f;   // -2: window exceeds ring
     }
     // Ring growth: the span the reference would still hold in its unbounded queue -- every packet
@@ -900,8 +979,7 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
         const uint64_t held_b = vend - meta[tail & D.pk_mask].vbyte;
         if (2 * (head - tail) > pk_cap || 2 * held_b > byte_cap) {
             const int64_t age_cut = P.T.now - 10 * P.T.over_buffer_ms;
-            uint64_t r = wave_lower_bound_meta(meta, D.pk_mask, tail, head,
-                                               [&](const PktMeta& m) { return m.arrival >= age_cut; });
+            uint64_t r = wave_first_arrival_at(D, meta, tail, head, age_cut);
             if (D.key >= 0 && (uint64_t)D.key >= tail) r = min(r, (uint64_t)D.key);
             if (D.umin >= tail) r = min(r, D.umin);              // last tick's reads (before the reset below)
             const uint64_t need_pk = head - r;
@@ -2316,8 +2394,7 @@ __global__ void k_first_packet_info(const FirstInfoQuery* Q, FirstInfoResult* R,
     const bool has_rtp = D.head > 0 || (q.rtcp_sender != 0xFFFFFFFFu && senders[q.rtcp_sender].head > 0);
     if (has_rtp) {
         const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
-        const uint64_t f = lower_bound_meta(meta, D.pk_mask, sender_tail(D), D.head,
-                                            [&](const PktMeta& m) { return m.arrival >= q.cutoff; });
+        const uint64_t f = first_arrival_at(D, meta, sender_tail(D), D.head, q.cutoff);
         r.found = 2;
         if (f < D.head) {
             const PktMeta m = meta[f & D.pk_mask];
@@ -2353,14 +2430,14 @@ __global__ void k_image_plan(ImageParams P) {
         if (floor < tail) { set_status(P.status, EDGPU_RING_OVERFLOW); floor = tail; }
     } else if (head > tail) {
         const int64_t cutoff = P.now - P.over_buffer_ms;
-        floor = lower_bound_meta(meta, D.pk_mask, tail, head, [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        floor = first_arrival_at(D, meta, tail, head, cutoff);
         if (floor < head && floor == tail && tail > D.floor) set_status(P.status, EDGPU_RING_OVERFLOW);
     }
     if (E.from == kImageFull && head > tail && floor > tail) {
         // an RTP-Info PLAY on the replica reads the first packet of the over-buffer window
         // (GetFirstPacketInfo, ReflectorStream.cpp:728-753), which may precede the key pointer
         const int64_t cutoff = P.now - P.over_buffer_ms;
-        const uint64_t w = lower_bound_meta(meta, D.pk_mask, tail, head, [&](const PktMeta& m) { return m.arrival >= cutoff; });
+        const uint64_t w = first_arrival_at(D, meta, tail, head, cutoff);
         if (w < floor) floor = w;
     }
     E.floor = floor;
@@ -2388,7 +2465,7 @@ __global__ __launch_bounds__(256) void k_image_pack(ImageParams P) {
         r.vcount_end = D.vcount_end; r.valid_ssrc = D.valid_ssrc; r.last_valid_s = D.last_valid_s;
         r.key = D.key; r.last_nonzero = D.last_nonzero;
         r.meta_off = E.meta_off; r.bytes_off = E.bytes_off;
-        r.delta = E.from != kImageFull; r.flags = D.flags; r._pad = 0;
+        r.delta = E.from != kImageFull; r.flags = D.flags; r.nonmono = D.rt_nonmono; r._pad = 0;
         reinterpret_cast<ImgSender*>(img + sizeof(ImgHeader) + S.ntracks * sizeof(ImgStream))[E.ls] = r;
         if (E.first) {
             ImgHeader h;
@@ -2436,6 +2513,7 @@ __global__ __launch_bounds__(256) void k_image_apply(ImageParams P) {
         D.head = r.head; D.vbyte_end = r.vbyte_end; D.vcount_end = r.vcount_end;
         D.valid_ssrc = r.valid_ssrc; D.last_valid_s = r.last_valid_s;
         D.key = r.key; D.last_nonzero = r.last_nonzero;
+        D.rt_nonmono |= r.nonmono;               // arrivals the owner rewrote travel with its packets
         if (E.first) {
             const ImgStream* st = reinterpret_cast<const ImgStream*>(img + sizeof(ImgHeader));
             for (uint32_t t = 0; t < S.ntracks; t++) P.streams[S.first_stream + t].packet_count = st[t].packet_count;

@@ -57,6 +57,11 @@ struct IngestParams {
     uint32_t host_epoch;    // != 0: the blob is a host batch the host keeps for the tick; record each
                             // packet's slot and the batch (edgpu_fanout_sources)
     TickTotals* totals;
+    // reflector_use_in_packet_receive_time / reflector_in_packet_max_receive_sec
+    // (ReflectorStream.cpp:103-107, 113): strip a 12-byte "aktt" BE64 receive-time trailer and
+    // rebase the packet's arrival on it (:1960-1994)
+    uint32_t recv_time;
+    int64_t max_future_ms;  // sMaxFuturePacketMSec
     // Interleaved ingest (null otherwise): segment g is deframe group g, and k_ingest finds each
     // frame itself -- its chunk from the per-chunk results, its start from the walk's recorded
     // starts, its length and channel from its own '$' header, its arrival from the reads --

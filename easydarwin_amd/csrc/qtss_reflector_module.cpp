@@ -766,6 +766,10 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     GetPref<uint32_t>(M->modPrefs, "reflector_buffer_size_sec", qtssAttrDataTypeUInt32, &bufSec, 1u);
     GetPref<uint32_t>(M->modPrefs, "rtp_reflector_threshold_msec", qtssAttrDataTypeUInt32, &relocate, 2000u);
     GetPref<uint32_t>(M->modPrefs, "reflector_rtp_info_offset_msec", qtssAttrDataTypeUInt32, &rtpInfoOffset, 500u);
+    bool useReceiveTime = false;
+    uint32_t maxFutureSec = 60;
+    GetPref<bool>(M->modPrefs, "reflector_use_in_packet_receive_time", qtssAttrDataTypeBool16, &useReceiveTime, false);
+    GetPref<uint32_t>(M->modPrefs, "reflector_in_packet_max_receive_sec", qtssAttrDataTypeUInt32, &maxFutureSec, 60u);
     M->bucketDelayMs = bucket;
     M->overBufferMs = (int64_t)bufSec * 1000;
     ReadModulePrefsLocked();
@@ -779,6 +783,8 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     cfg.reflector_rtp_info_offset_msec = rtpInfoOffset ? rtpInfoOffset : EDGPU_FALSE;
     cfg.timeout_stream_SSRC_secs = M->timeoutSSRC ? M->timeoutSSRC : 30;
     cfg.use_one_SSRC_per_stream = M->oneSSRC ? 1u : EDGPU_FALSE;
+    cfg.reflector_use_in_packet_receive_time = useReceiveTime ? 1u : 0u;
+    cfg.reflector_in_packet_max_receive_sec = maxFutureSec ? maxFutureSec : EDGPU_FALSE;
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
     // capacities for large fleets (edgpu_config; 0 / unset: the engine defaults): the fan-out
     // arena and descriptors of one tick, the ingest batch of one tick

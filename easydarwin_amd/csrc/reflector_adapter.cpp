@@ -272,7 +272,9 @@ void Reflector::Append(uint32_t session, uint32_t track, const char* packet, uin
             pend = &b.slabPend[st.slab / kSlab].n;
             pend->fetch_add(1, std::memory_order_relaxed);
         }
-        st.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), nowMs, st.slab + st.used, packetLen});
+        // a datagram from an odd source port: GetSSRC(theRemotePort & 1) of the receive-time trailer
+        const uint8_t fl = (src && (src->port & 1)) ? (uint8_t)EDGPU_PKT_REMOTE_ODD : (uint8_t)0;
+        st.pushed.push_back(Pushed{session, (uint8_t)(2 * track + (isRTCP ? 1 : 0)), fl, nowMs, st.slab + st.used, packetLen});
         if (src) st.sources.push_back(*src);
         st.used += slot;
         st.copying.fetch_add(1, std::memory_order_relaxed);
@@ -386,7 +388,7 @@ int Reflector::FlushIngest() {
             b.desc[k].slot = (uint32_t)(p.slot / 16);
             b.desc[k].len = (uint16_t)p.len;
             b.desc[k].channel = p.channel;
-            b.desc[k].flags = 0;
+            b.desc[k].flags = p.flags;
             b.desc[k].arrival_ms = p.t;
             fTick.ingested_bytes += p.len;
         }

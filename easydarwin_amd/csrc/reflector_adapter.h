@@ -201,7 +201,7 @@ private:
     void WaitIdle(std::unique_lock<std::mutex>& lk) { fIdleCv.wait(lk, [&] { return !fDelivering; }); }
     int  ReflectPacketsLocked(int64_t nowMs, OutputSink* sink);
     // one pushed packet: its slot (16-B aligned, the packet 4 bytes in) in the batch's pinned blob
-    struct Pushed { uint32_t session; uint8_t channel; int64_t t; uint64_t slot; uint32_t len; };
+    struct Pushed { uint32_t session; uint8_t channel, flags; int64_t t; uint64_t slot; uint32_t len; };   // flags: EDGPU_PKT_*
     // The push path is striped by session (session % kStripes): a pusher takes only its stripe's
     // lock, and a stripe carves its slots out of 64-KiB slabs of the batch's pinned blob, so
     // pushers of different sessions share no lock and no counter per packet.

@@ -45,6 +45,7 @@ EXPORTED = [
     "edgpu_subscriber_set_slot", "edgpu_device_local_cpus",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
+PKT_REMOTE_ODD = 1          # edgpu_pkt_desc.flags: a UDP datagram from an odd source port
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
 NO_SOURCE = 0xFFFFFFFF
 
@@ -69,6 +70,8 @@ class Config(C.Structure):
         ("ring_growth", C.c_uint32),
         ("max_ring_packets", C.c_uint32),
         ("max_ring_bytes", C.c_uint64),
+        ("reflector_use_in_packet_receive_time", C.c_uint32),
+        ("reflector_in_packet_max_receive_sec", C.c_uint32),
     ]
 
 
@@ -788,8 +791,8 @@ class DeviceBuffer:
 
 
 def build_batch(pkts):
-    """Host-side batch builder: ``pkts`` is a list of (session, channel, arrival_ms, bytes) in
-    arrival order.  Groups them by session (stable) into the edgpu_ingest layout: 16-B
+    """Host-side batch builder: ``pkts`` is a list of (session, channel, arrival_ms, bytes) or
+    (session, channel, arrival_ms, bytes, flags) in arrival order (flags: PKT_REMOTE_ODD).  Groups them by session (stable) into the edgpu_ingest layout: 16-B
     slots with the packet 4 bytes in, a descriptor per packet, per-session segments."""
     order = sorted(range(len(pkts)), key=lambda i: (pkts[i][0], i))
     n = len(pkts)
@@ -801,14 +804,15 @@ def build_batch(pkts):
     off = 0
     last = None
     for k, i in enumerate(order):
-        s, ch, t, data = pkts[i]
+        s, ch, t, data = pkts[i][:4]
+        fl = pkts[i][4] if len(pkts[i]) > 4 else 0
         data = data[:65535]
         if s != last:
             if last is not None:
                 seg_off.append(k)
             seg_sess.append(s)
             last = s
-        desc[k] = (off // 16, len(data), ch, 0, t)
+        desc[k] = (off // 16, len(data), ch, fl, t)
         blob[off + 4:off + 4 + len(data)] = np.frombuffer(data, dtype=np.uint8)
         off += sizes[k]
     seg_off.append(n)

@@ -225,6 +225,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
     cfg.setdefault("reflector_buffer_size_sec", int(pv["reflector_buffer_size_sec"]))
     cfg.setdefault("rtp_reflector_threshold_msec", max(1000, int(pv["rtp_reflector_threshold_msec"])))   # :101-102
     cfg.setdefault("reflector_rtp_info_offset_msec", int(pv["reflector_rtp_info_offset_msec"]) or edgpu.FALSE)
+    cfg.setdefault("reflector_use_in_packet_receive_time", int(pref_bool(pv["reflector_use_in_packet_receive_time"])))
+    cfg.setdefault("reflector_in_packet_max_receive_sec", int(pv["reflector_in_packet_max_receive_sec"]) or edgpu.FALSE)
     mod = {"prefs": dict(trace.prefs)}      # the module prefs (RereadPrefs at PREFS events)
     own = ctx is None
     if own:
@@ -342,7 +344,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                 else:
                     batch = pending
                 if batch:
-                    desc, seg_off, seg_sess, blob = edgpu.build_batch([(gen[p[0]],) + p[1:4] for p in batch])
+                    desc, seg_off, seg_sess, blob = edgpu.build_batch([(gen[p[0]],) + p[1:4] + (p[5],) for p in batch])
                     if pinned:
                         pin_ingest(desc, seg_off, seg_sess, blob)
                     else:
@@ -427,11 +429,11 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             if ev[0] == PKT:
                 _, t, s, ch, data = ev
                 if published[s]:
-                    pending.append((s, ch, t, data, False))
+                    pending.append((s, ch, t, data, False, 0))
             elif ev[0] == UPKT:
                 _, t, s, ch, addr, port, data = ev
                 if published[s]:
-                    pending.append((s, ch, t, data, True))
+                    pending.append((s, ch, t, data, True, edgpu.PKT_REMOTE_ODD if port & 1 else 0))
                     sources.append((gen[s], ch, addr, port, data))
             elif ev[0] == JOIN:
                 # an RTP-Info PLAY reads the queues as they are at the JOIN (HaveStreamBuffers):

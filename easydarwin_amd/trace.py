@@ -105,6 +105,8 @@ PREF_DEFAULTS = {
     "enable_broadcast_push": "true",
     "allow_duplicate_broadcasts": "false",
     "timeout_broadcaster_session_secs": "30",
+    "reflector_use_in_packet_receive_time": "false",
+    "reflector_in_packet_max_receive_sec": "60",
 }
 USER_AGENTS = ("EasyPlayer/1.0", "vlc/3.0.8 LibVLC/3.0.8")    # by JOIN ua_flags bit 0
 

@@ -123,6 +123,16 @@ typedef struct edgpu_config {
     uint32_t ring_growth;
     uint32_t max_ring_packets;              /* per sender bound of growth (1 Mi), power of two */
     uint64_t max_ring_bytes;                /* per sender bound of growth (1 GiB), power of two */
+    /* reflector_use_in_packet_receive_time (default false; read once, ReflectorStream.cpp:103-104):
+     * a packet longer than 12 bytes whose last 12 are "aktt" + a BE64 receive time (ms) loses
+     * them, and its arrival (fTimeArrived: the new-output window, retention, relocation, transmit
+     * times) becomes the socket's anchor arrival plus the receive time's offset from the anchor's
+     * receive time; the anchor is the socket's first tagged packet since its SSRC -- by the
+     * remote port's parity, EDGPU_PKT_REMOTE_ODD -- last changed (ReflectorSocket::ProcessPacket,
+     * :1960-1994).  Arrivals further than reflector_in_packet_max_receive_sec (default 60,
+     * EDGPU_FALSE for 0; :106-107, 113) ahead of the push time are clamped there. */
+    uint32_t reflector_use_in_packet_receive_time;
+    uint32_t reflector_in_packet_max_receive_sec;
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu   /* a flag off / a value of 0 where 0 would select the default */
 
@@ -137,9 +147,13 @@ typedef struct edgpu_pkt_desc {
     uint32_t slot;          /* blob byte offset / 16 */
     uint16_t len;           /* packet length as received (clamped to 2060 at ingest, Q11) */
     uint8_t  channel;       /* interleaved channel: 2*track + is_rtcp */
-    uint8_t  flags;         /* reserved, 0 */
+    uint8_t  flags;         /* EDGPU_PKT_REMOTE_ODD or 0 */
     int64_t  arrival_ms;    /* OS::Milliseconds() when the packet was pushed */
 } edgpu_pkt_desc;
+/* A UDP push datagram from an odd source port: ProcessPacket's GetSSRC(theRemotePort & 1) reads
+ * the RTCP SSRC word for it (ReflectorStream.cpp:1969; only the receive-time trailer reads it).
+ * An RTSP-interleaved push has remote port 0 (PushPacket, :548, :572). */
+#define EDGPU_PKT_REMOTE_ODD 1u
 
 /* One send-ready output packet (16 bytes).  `offset` is the byte offset in the output
  * arena of the bytes to put on the wire: the UDP datagram, or the '$' ch BE16(len) frame

@@ -222,6 +222,7 @@ static const char* const kPrefDefaults[][2] = {            // easydarwin_amd/tra
     {"player_requires_rtp_header_info", "Android,vlc"},
     {"enable_broadcast_announce", "true"}, {"enable_broadcast_push", "true"},
     {"allow_duplicate_broadcasts", "false"}, {"timeout_broadcaster_session_secs", "30"},
+        {"reflector_use_in_packet_receive_time", "false"}, {"reflector_in_packet_max_receive_sec", "60"},
 };
 static FakeObj* g_mod_prefs = nullptr;      // QTSSReflectorModule's prefs object
 static FakeObj* g_srv_prefs = nullptr;      // the server's prefs object

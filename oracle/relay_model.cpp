@@ -78,6 +78,8 @@ struct Prefs {                                   // ReflectorStream::Initialize 
     int64_t max_packet_age_ms = 10000;           // 10 x over buffer
     int64_t relocate_age_ms = 2000;              // rtp_reflector_threshold_msec
     int64_t first_packet_offset_ms = 500;        // ReflectorStream::sFirstPacketOffsetMsec (:70)
+    bool use_receive_time = false;               // reflector_use_in_packet_receive_time (:103-104)
+    int64_t max_future_ms = 60000;               // reflector_in_packet_max_receive_sec x 1000 (:106-107, 113)
     // module prefs (RereadPrefs): new sessions take the SSRC ones
     uint32_t ssrc_timeout_s = 30;                // timeout_stream_SSRC_secs
     bool filter_ssrcs = true;                    // use_one_SSRC_per_stream
@@ -97,6 +99,8 @@ struct Prefs {                                   // ReflectorStream::Initialize 
             max_packet_age_ms = over_buffer_ms != 0 ? over_buffer_ms * 10 : 10000;
             relocate_age_ms = std::max<int64_t>(u32("rtp_reflector_threshold_msec", "2000"), 1000);
             first_packet_offset_ms = u32("reflector_rtp_info_offset_msec", "500");
+            use_receive_time = flag("reflector_use_in_packet_receive_time", "false");
+            max_future_ms = (int64_t)(uint32_t)(u32("reflector_in_packet_max_receive_sec", "60") * 1000u);
         }
         ssrc_timeout_s = u32("timeout_stream_SSRC_secs", "30");
         filter_ssrcs = flag("use_one_SSRC_per_stream", "true");
@@ -211,6 +215,11 @@ struct Sender {
     // per-socket SSRC filter state
     uint32_t valid_ssrc = 0;
     int64_t last_valid_s = 0;
+    // per-socket receive-time state (ReflectorStream.h:251-254)
+    bool has_receive_time = false;
+    uint32_t current_ssrc = 0;
+    int64_t first_arrival = 0;
+    uint64_t first_receive = 0;
 };
 
 struct Stream {
@@ -414,6 +423,26 @@ struct Model {
             it->needed = true;
             snd.key = it; snd.has_key = true;
             se.video_key_flag = false;
+        }
+        // the "aktt" receive-time trailer (:1960-1994), after the key-frame test saw the whole
+        // packet: strip it and rebase the arrival on the socket's anchor; the anchor's SSRC is read
+        // by the REMOTE port's parity (0 for an interleaved push)
+        if (prefs.use_receive_time && it->len > 12) {
+            const uint8_t* t = it->data.data() + it->len - 12;
+            if (memcmp(t, "aktt", 4) == 0) {
+                uint64_t rt = 0;
+                for (int k = 4; k < 12; k++) rt = rt << 8 | t[k];
+                const uint32_t ssrc = (port & 1) ? be32(&it->data[4]) : be32(&it->data[8]);
+                if (!snd.has_receive_time || snd.current_ssrc != ssrc) {
+                    snd.current_ssrc = ssrc;
+                    snd.first_arrival = it->arrival;
+                    snd.first_receive = rt;
+                    snd.has_receive_time = true;
+                }
+                it->arrival = snd.first_arrival + (int64_t)(rt - snd.first_receive);
+                it->len -= 12;
+                if (it->arrival - now > prefs.max_future_ms) it->arrival = now + prefs.max_future_ms;
+            }
         }
     }
 

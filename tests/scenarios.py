@@ -758,6 +758,81 @@ def prefs_push() -> Trace:
     return _assemble(tr, [pk0, pk1], 100, dur, joins, pubs=pubs, prefs=prefs)
 
 
+def _aktt_tag(data: bytes, receive_ms: int) -> bytes:
+    """A pusher's receive-time trailer: "aktt" + BE64 receive time (ms), appended to the packet
+    (ReflectorStream.cpp:1960-1994 reads the packet's last 12 bytes)."""
+    return data + b"aktt" + struct.pack(">Q", receive_ms & 0xFFFFFFFFFFFFFFFF)
+
+
+def aktt() -> Trace:
+    """reflector_use_in_packet_receive_time on (ReflectorStream.cpp:103-107), with
+    reflector_in_packet_max_receive_sec 3 and a 2-s SSRC timeout: pushers append a 12-byte "aktt"
+    BE64 receive-time trailer to most packets (ReflectorSocket::ProcessPacket, :1960-1994).  A
+    tagged packet loses the trailer (every subscriber gets it 12 bytes shorter) and its arrival
+    becomes the socket's anchor arrival plus its receive time's offset from the anchor's -- the
+    anchor being the socket's first tagged packet since its SSRC changed -- clamped to now + 3 s.
+    The rewritten arrivals drive the new-output window, retention, relocation and transmit times.
+
+    * session 0, RTSP-interleaved H.264 + PCMA: receive clock 5e9 ms + t + jitter of +-40 ms (so
+      arrivals are not monotone along a queue), 1 packet in 6 untagged; crafted packets: a
+      13-byte SPS + trailer (the key-frame test sees 25 bytes, the queue keeps 13), a 24-byte one
+      (an RTP header left), a packet shorter than 12 bytes ending in "aktt", a tagged packet whose
+      receive time jumps 100 s ahead (clamped) and one 20 s back; the pusher's SSRC changes at
+      3.5 s (zero-length for 2 s, then latched: the anchor restarts) and it leaves at 6 s and
+      returns at 6.4 s with the same SSRC and a clock 40 s ahead (same session: the old anchor
+      holds, arrivals clamp);
+    * session 1, a UDP push of MPEG-4 video (no key frames: new outputs start in the 1-s window
+      of the rewritten arrivals) with SRs from the odd port, which anchor on the RTCP SSRC word
+      (GetSSRC by the remote port's parity);
+    * UDP, TCP and RTP-Info players joining throughout; a TCP player blocked for 2.5 s (Q9
+      relocation compares arrivals)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 150))
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=30, idr_bytes=5_000, rtcp_every_ms=900,
+                   ssrc=0x0AC7AA01),
+         TrackSpec("audio", "PCMA/8000", 8, ssrc=0x0AC7AA02)]
+    vb = [TrackSpec("video", "H264/90000", 96, bitrate=400_000, gop=30, idr_bytes=5_000, ssrc=0x0AC7AB0B),
+          TrackSpec("audio", "PCMA/8000", 8, ssrc=0x0AC7AB0C)]
+    u = [TrackSpec("video", "MP4V-ES/90000", 96, bitrate=300_000, rtcp_every_ms=700)]
+    tr = Trace()
+    tr.prefs = {"reflector_use_in_packet_receive_time": "true", "reflector_in_packet_max_receive_sec": "3",
+                "timeout_stream_SSRC_secs": "2"}
+    tr.add_session(make_sdp(v))
+    tr.add_session(make_sdp(u), udp_push=True)
+    dur = 9_000
+
+    def tag(lst, base, skip_every=6):
+        out = []
+        for k, p in enumerate(lst):
+            t, ch, d = p[:3]
+            if k % skip_every != skip_every - 1:
+                d = _aktt_tag(d, base + t + int(rng.integers(-40, 41)))
+            out.append((t, ch, d) + tuple(p[3:]))
+        return out
+
+    pk0 = tag(session_packets(v, 3500, SEED_BASE + 151), 5_000_000_000)
+    pk0 += tag(session_packets(vb, 2500, SEED_BASE + 152, t0=3500), 5_000_000_000)
+    pk0 += tag(session_packets(vb, dur - 6400, SEED_BASE + 153, t0=6400), 5_000_040_000)
+    ssrc0 = 0x0AC7AA01
+    crafted = [
+        (1210, 0, _aktt_tag(rtp_header(7, 90, ssrc0, 96, False) + bytes([0x67]), 5_000_001_210)),
+        (1220, 0, _aktt_tag(rtp_header(8, 90, ssrc0, 96, False), 5_000_001_220)),
+        (1230, 0, rtp_header(9, 90, ssrc0, 96, False)[:7] + b"aktt"),
+        (2210, 0, _aktt_tag(rtp_header(10, 180, ssrc0, 96, False) + bytes(40), 5_000_102_210)),
+        (2720, 0, _aktt_tag(rtp_header(11, 270, ssrc0, 96, False) + bytes(30), 4_999_982_720)),
+    ]
+    pk0 = sorted(pk0 + crafted, key=lambda p: p[0])
+    src = _ip(10, 5, 0, 7)
+    pk1 = [(t, ch, d, src, 7200 + (ch & 1)) for t, ch, d in
+           tag(session_packets(u, dur, SEED_BASE + 154), 900_000, skip_every=5)]
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (1500, 0, 3, UDP), (2300, 0, 4, TCP, VLC), (3000, 0, 5, UDP, VLC),
+             (4200, 0, 6, UDP), (6600, 0, 7, TCP), (8000, 0, 8, UDP, VLC),
+             (0, 1, 10, UDP), (1200, 1, 11, TCP), (2500, 1, 12, UDP, VLC), (5000, 1, 13, UDP), (7700, 1, 14, TCP)]
+    ticks = list(range(0, dur + 1, 100))
+    blocks = {t: [(2, 0, 0, 0)] for t in ticks if 4000 <= t < 6500}
+    pubs = [(6000, "unpublish", 0, 0), (6400, "publish", 0)]
+    return _assemble(tr, [pk0, pk1], 100, dur, joins, tick_times=ticks, blocks=blocks, pubs=pubs)
+
+
 # Scenarios for the QTSS module alone: fixtures from the reference module in tools/qtss_replay
 MODULE_SCENARIOS = {"prefs_push": prefs_push}
 
@@ -767,7 +842,7 @@ SCENARIOS = {
     "nokey": nokey, "stall": stall, "anchor": anchor, "rtpinfo": rtpinfo,
     "backpressure": backpressure, "udppush": udppush, "leave": leave, "repush": repush,
     "threaded": threaded, "prefs_buffer": prefs_buffer, "prefs_reread": prefs_reread,
-    "keepalive": keepalive, "highrate": highrate, "longbuffer": longbuffer,
+    "keepalive": keepalive, "highrate": highrate, "longbuffer": longbuffer, "aktt": aktt,
 }
 
 

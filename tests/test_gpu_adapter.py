@@ -21,7 +21,7 @@ TOOL = os.path.join(ROOT, "tools", "adapter_replay")
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["tiny", "mixed", "nal", "ssrc", "anchor", "c1", "rtpinfo", "backpressure", "leave",
                                   "udppush", "repush", "prefs_buffer", "prefs_reread", "keepalive", "highrate",
-                                  "longbuffer"])
+                                  "longbuffer", "aktt"])
 def test_adapter_replay_matches_reference(name, tmp_path):
     fix = json.load(open(os.path.join(GOLD, name + ".json")))
     t, c = tmp_path / "t.edtr", tmp_path / "c.edcp"

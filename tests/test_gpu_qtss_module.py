@@ -38,11 +38,12 @@ UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones
 PREFS = ["prefs_buffer", "prefs_reread", "prefs_push"]   # the server's prefs objects, RereadPrefs
 KEEPALIVE = ["keepalive"]                     # 70 s: the pushers' timeouts and the module's refreshes
 RETENTION = ["highrate", "longbuffer"]        # retention past the default ring capacities (ring growth)
+RECEIVE_TIME = ["aktt"]                       # reflector_use_in_packet_receive_time: the "aktt" trailer
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["whole", "parts"])
-@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE + RETENTION)
+@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE + RETENTION + RECEIVE_TIME)
 def test_module_matches_reference(name, gather, tmp_path):
     """`parts`: every tick's readback gathered in parts, overlapped with the write threads
     (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split).  The
@@ -87,7 +88,7 @@ REF_MODULE = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["repush", "rtpinfo", "leave", "threaded", "udppush", "prefs_reread", "backpressure",
-                                  "keepalive", "prefs_push"])
+                                  "keepalive", "prefs_push", "aktt"])
 @pytest.mark.parametrize("refresh", ["on", "off"])
 def test_module_equals_reference_module(name, refresh, tmp_path):
     """The drop-in and the REFERENCE QTSSReflectorModule (compiled from its own sources,

@@ -95,6 +95,9 @@ int main(int argc, char** argv) {
     cfg.rtp_reflector_threshold_msec = std::max<uint32_t>(1000, prefs.u32("rtp_reflector_threshold_msec"));   // :101-102
     cfg.reflector_rtp_info_offset_msec = prefs.u32("reflector_rtp_info_offset_msec") ? prefs.u32("reflector_rtp_info_offset_msec")
                                                                                      : EDGPU_FALSE;
+    cfg.reflector_use_in_packet_receive_time = prefs.flag("reflector_use_in_packet_receive_time") ? 1u : 0u;
+    cfg.reflector_in_packet_max_receive_sec = prefs.u32("reflector_in_packet_max_receive_sec") ? prefs.u32("reflector_in_packet_max_receive_sec")
+                                                                                               : EDGPU_FALSE;
     if (const char* v = getenv("EDGPU_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)strtoul(v, nullptr, 0);
     Reflector R(&cfg);

@@ -23,6 +23,7 @@ inline const std::vector<std::pair<std::string, std::string>>& defaults() {
         {"player_requires_rtp_header_info", "Android,vlc"},
         {"enable_broadcast_announce", "true"}, {"enable_broadcast_push", "true"},
         {"allow_duplicate_broadcasts", "false"}, {"timeout_broadcaster_session_secs", "30"},
+        {"reflector_use_in_packet_receive_time", "false"}, {"reflector_in_packet_max_receive_sec", "60"},
     };
     return d;
 }
