@@ -159,6 +159,54 @@ void GetPref(QTSS_Object prefs, const char* name, uint32_t type, T* out, T def) 
     (void)cb(kAddInstanceAttributeCallback, prefs, name, (void*)nullptr, type);
     if (PrefID(prefs, name, type, &id)) (void)SetValue(prefs, id, 0, &def, sizeof(T));
 }
+// A value as a string (QTSS_GetValueAsString: the server new[]s it, the caller deletes it); false
+// when the object holds no value there (an empty one included, QTSSDictionary.cpp:144-146).
+bool ValueString(QTSS_Object o, QTSS_AttributeID id, uint32_t idx, std::string* out) {
+    char* c = nullptr;
+    if (!o || cb(kGetValueAsStringCallback, o, id, idx, &c) != QTSS_NoErr || !c) return false;
+    out->assign(c);
+    delete[] c;
+    return true;
+}
+// A char-array pref (QTSSModuleUtils::GetStringAttribute, QTSSModuleUtils.cpp:723-768): its value,
+// else the default, which is added to the prefs object.
+std::string GetStringPref(QTSS_Object prefs, const char* name, const char* def) {
+    QTSS_AttributeID id = 0;
+    std::string v;
+    if (PrefID(prefs, name, qtssAttrDataTypeCharArray, &id) && ValueString(prefs, id, 0, &v)) return v;
+    if (prefs) {
+        (void)cb(kAddInstanceAttributeCallback, prefs, name, (void*)nullptr, (uint32_t)qtssAttrDataTypeCharArray);
+        if (PrefID(prefs, name, qtssAttrDataTypeCharArray, &id)) (void)SetValue(prefs, id, 0, def, (uint32_t)strlen(def));
+    }
+    return def;
+}
+// Every value of a list pref, as QTSSModuleUtils::AddressInList walks it (QTSSModuleUtils.cpp:956-981)
+std::vector<std::string> GetStringListPref(QTSS_Object prefs, const char* name, const char* def) {
+    (void)GetStringPref(prefs, name, def);          // created with the default when missing (QRM:537)
+    std::vector<std::string> out;
+    QTSS_AttributeID id = 0;
+    if (!PrefID(prefs, name, qtssAttrDataTypeCharArray, &id)) return {def};
+    uint32_t n = 0;
+    (void)cb(kGetNumValuesCallback, prefs, id, &n);
+    for (uint32_t i = 0; i < n; i++) {
+        std::string v;
+        if (ValueString(prefs, id, i, &v)) out.push_back(v);
+        else out.push_back(std::string());
+    }
+    return out;
+}
+// The error response QTSSModuleUtils::SendErrorResponse(WithMessage) sends (QTSSModuleUtils.cpp:
+// 369-484) with the server's RTSP_error_message pref off, its default (QTSServerPrefs.cpp:149): the
+// status, no keep-alive, the headers, an empty body.
+QTSS_Error SendErrorResponse(QTSS_Object req, uint32_t status) {
+    (void)SetValue(req, qtssRTSPReqStatusCode, 0, &status, sizeof(status));
+    const bool no = false;
+    (void)SetValue(req, qtssRTSPReqRespKeepAlive, 0, &no, sizeof(no));
+    (void)cb(kSendRTSPHeadersCallback, req);
+    (void)cb(kWriteCallback, req, (const void*)"", (uint32_t)0, (uint32_t*)nullptr, (uint32_t)0);
+    (void)SetValue(req, qtssRTSPReqRespMsg, 0, "", (uint32_t)0);
+    return QTSS_RequestFailed;
+}
 
 // ---- module state ---------------------------------------------------------------------------
 // attributes the module adds (the reference's names, QTSSReflectorModule.cpp:313-346)
@@ -279,6 +327,14 @@ struct Module {
     std::atomic<bool> pushEnabled{true};   // enable_broadcast_push (ProcessRTPData, QRM:606; read without mu)
     bool allowDuplicates = false;       // allow_duplicate_broadcasts (DoSetup, QRM:1682)
     uint32_t broadcasterTimeoutMs = 30000;  // max(30, timeout_broadcaster_session_secs) x 1000 (QRM:483-487, 541)
+    // access (RTSPAuthorize, RTSPRoute, AllowBroadcast; QRM:489-538)
+    bool allowBroadcasts = true;        // allow_broadcasts (sReflectBroadcasts)
+    bool authLocal = false;             // authenticate_local_broadcast
+    bool allowNonSDP = true;            // allow_non_sdp_urls: a player's session by its full path
+    std::string broadcasterGroup = "broadcaster";   // BroadcasterGroup
+    std::string redirectKeyword;        // redirect_broadcast_keyword, trimmed (GetTrimmedKeyWord)
+    std::string redirectDir;            // redirect_broadcasts_dir, movie-folder relative (SetMoviesRelativeDir)
+    std::vector<std::string> ipAllowList{"127.0.0.*"};   // ip_allow_list
     QTSS_Object modPrefs = nullptr;     // this module's prefs object
     QTSS_Object serverPrefs = nullptr;  // the server's prefs object (player_requires_rtp_header_info)
     uint64_t rereads = 0;
@@ -357,6 +413,16 @@ uint32_t ChannelOf(const std::string& query) {
 // EasyDarwin's empty root directory, RTSPRequestInterface.cpp:219-224)
 std::string StreamName(QTSS_Object req) {
     return GetString(req, qtssRTSPReqFileName) + "-" + std::to_string(ChannelOf(GetString(req, qtssRTSPReqQueryString)));
+}
+// A player's stream name (DoSessionSetup with allow_non_sdp_urls, QRM:769-793): the full path,
+// QTSSModuleUtils::GetFullPath (QTSSModuleUtils.cpp:228-285) = the request's root directory + its
+// file name -- the file name alone unless an RTSPRoute module set a root (RedirectBroadcast)
+std::string PlayerStreamName(QTSS_Object req, bool allowNonSDP) {
+    if (!allowNonSDP) return StreamName(req);
+    std::string root = GetString(req, qtssRTSPReqRootDir), file = GetString(req, qtssRTSPReqFileName);
+    if (!root.empty() && root.back() == '/')
+        while (!file.empty() && file[0] == '/') file.erase(0, 1);
+    return root + file + "-" + std::to_string(ChannelOf(GetString(req, qtssRTSPReqQueryString)));
 }
 
 // a first SETUP the reflector does not take: an empty file name, or a ".mov" (DoSessionSetup,
@@ -701,8 +767,10 @@ QTSS_Error Tick() {
 
 // ---- roles ----------------------------------------------------------------------------------
 QTSS_Error Register(QTSS_Register_Params* p) {
+    // the reference's roles (QRM:268-276) but Easy_GetDeviceStream, EasyCMS's
     for (QTSS_Role r : {QTSS_Initialize_Role, QTSS_Shutdown_Role, QTSS_RTSPPreProcessor_Role,
-                        QTSS_ClientSessionClosing_Role, QTSS_RTSPIncomingData_Role, QTSS_RereadPrefs_Role})
+                        QTSS_ClientSessionClosing_Role, QTSS_RTSPIncomingData_Role, QTSS_RTSPAuthorize_Role,
+                        QTSS_RereadPrefs_Role, QTSS_RTSPRoute_Role})
         (void)cb(kAddRoleCallback, r);
     struct { QTSS_ObjectType type; const char* name; QTSS_AttrDataType dt; QTSS_AttributeID* id; } attrs[] = {
         {qtssClientSessionObjectType, "QTSSReflectorModuleRTPInfoWaitTime", qtssAttrDataTypeSInt32, &sRTPInfoWaitTimeAttr},
@@ -744,6 +812,26 @@ void ReadModulePrefsLocked() {
     uint32_t bsecs = 30;
     GetPref<uint32_t>(o, "timeout_broadcaster_session_secs", qtssAttrDataTypeUInt32, &bsecs, 30u);
     M->broadcasterTimeoutMs = std::max<uint32_t>(bsecs, 30) * 1000;
+    GetPref<bool>(o, "allow_non_sdp_urls", qtssAttrDataTypeBool16, &M->allowNonSDP, true);
+    GetPref<bool>(o, "authenticate_local_broadcast", qtssAttrDataTypeBool16, &M->authLocal, false);
+    GetPref<bool>(o, "allow_broadcasts", qtssAttrDataTypeBool16, &M->allowBroadcasts, true);
+    M->broadcasterGroup = GetStringPref(o, "BroadcasterGroup", "broadcaster");
+    // GetTrimmedKeyWord (QRM:411-427): leading '/'s dropped, up to the next '/'
+    std::string kw = GetStringPref(o, "redirect_broadcast_keyword", "");
+    size_t k0 = 0;
+    while (k0 < kw.size() && kw[k0] == '/') k0++;
+    const size_t k1 = kw.find('/', k0);
+    M->redirectKeyword = kw.substr(k0, k1 == std::string::npos ? std::string::npos : k1 - k0);
+    // a directory that does not start at '/' (the empty default too) is under the movie folder
+    // (SetMoviesRelativeDir, QRM:429-448, 528-531)
+    M->redirectDir = GetStringPref(o, "redirect_broadcasts_dir", "");
+    if (M->redirectDir.empty() || M->redirectDir[0] != '/') {
+        std::string movies;
+        (void)ValueString(M->serverPrefs, qtssPrefsMovieFolder, 0, &movies);
+        if (!movies.empty() && movies.back() != '/') movies += '/';
+        M->redirectDir = movies + M->redirectDir;
+    }
+    M->ipAllowList = GetStringListPref(o, "ip_allow_list", "127.0.0.*");
 }
 
 QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
@@ -882,12 +970,12 @@ QTSS_Error DoAnnounce(QTSS_StandardRTSP_Params* p) {
     // which never carries the "-<channel>" every session name has, so here it is refused outright
     {   // enable_broadcast_announce (QRM:900: 412 Precondition Failed, nothing cached)
         std::lock_guard<std::mutex> g(M->mu);
-        if (!M->announceEnabled) return QTSS_RequestFailed;
+        if (!M->announceEnabled) return SendErrorResponse(p->inRTSPRequest, qtssPreconditionFailed);
     }
     const std::string name = GetString(p->inRTSPRequest, qtssRTSPReqFileName);
     if (name.size() > 5 && name.compare(name.size() - 5, 5, ".kill") == 0) return QTSS_RequestFailed;
     uint32_t clen = 0;
-    if (!GetPOD(p->inRTSPRequest, qtssRTSPReqContentLen, &clen)) return QTSS_RequestFailed;
+    if (!GetPOD(p->inRTSPRequest, qtssRTSPReqContentLen, &clen)) return SendErrorResponse(p->inRTSPRequest, qtssClientBadRequest);   // QRM:973-978
     std::string* body = nullptr;
     if (!GetPOD(p->inRTSPRequest, sRequestBodyAttr, &body) || !body) {
         body = new std::string();
@@ -947,12 +1035,18 @@ void SetRoute(const Session& s, bool on) {
 // FindOrCreateSession (QRM:1379-1545).  A player only finds a registered session (:1391-1396);
 // a pusher's SETUP registers one from the announced SDP, and its transport decides whether the
 // session is pushed over UDP.  A found session is not set up again (:1521-1531).
-Session* FindOrCreateSession(const std::string& name, bool isPush, bool udpPush = false) {
+Session* FindOrCreateSession(const std::string& name, QTSS_Object req, bool isPush, bool udpPush = false) {
     auto it = M->byName.find(name);
-    if (it != M->byName.end()) return FindSession(it->second);
+    if (it != M->byName.end()) {
+        // AllowBroadcast before anything else (QRM:1489-1495, 2293-2304): with allow_broadcasts off
+        // every pusher and player SETUP of the session is forbidden
+        if (!M->allowBroadcasts) { (void)SendErrorResponse(req, qtssClientForbidden); return nullptr; }
+        return FindSession(it->second);
+    }
     if (!isPush) return nullptr;
     auto a = M->announced.find(name);
     if (a == M->announced.end() || !M->R) return nullptr;
+    if (!M->allowBroadcasts) { (void)SendErrorResponse(req, qtssClientForbidden); return nullptr; }   // QRM:1429-1437
     Session s;
     s.id = M->nextId++;
     s.name = name;
@@ -1033,7 +1127,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         Session* s = nullptr;
         if (GetPOD(p->inClientSession, sClientBroadcastSessionAttr, &held) && held) s = FindSession((uint32_t)held);
         const bool first = s == nullptr;
-        if (first) s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), true, udp);
+        if (first) s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), p->inRTSPRequest, true, udp);
         if (!s) return QTSS_RequestFailed;
         if (first) DisableOverbufferingIfPref(p->inClientSession);
         // the pusher's client session times out after timeout_broadcaster_session_secs (at least
@@ -1043,10 +1137,13 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
         // the reference sets the session up for one transport; a pusher of the other cannot join it
         // (DeleteReflectorPushSession: the reference it took goes back, :1548-1570)
         auto refuse = [&]() { if (first && s->refs == 0) ReleaseLocked(s); return QTSS_RequestFailed; };
-        if (!digitOK || s->udpPush != udp) return refuse();
+        if (s->udpPush != udp) return refuse();
+        // no track digit, a bad track: 400; a track another pusher set up: 412 unless
+        // allow_duplicate_broadcasts (QRM:1656-1686)
+        if (!digitOK) { (void)refuse(); return SendErrorResponse(p->inRTSPRequest, qtssClientBadRequest); }
         const int t = TrackIndex(*s, trackID);
-        // a bad track, or one another pusher set up: refused unless allow_duplicate_broadcasts (QRM:1682)
-        if (t < 0 || (s->setupToReceive[t] && !M->allowDuplicates)) return refuse();
+        if (t < 0) { (void)refuse(); return SendErrorResponse(p->inRTSPRequest, qtssClientBadRequest); }
+        if (s->setupToReceive[t] && !M->allowDuplicates) { (void)refuse(); return SendErrorResponse(p->inRTSPRequest, qtssPreconditionFailed); }
         if (udp) {
             // the track's socket pair (BindSockets) and its port in the SETUP response
             if (s->pair[t] < 0) {
@@ -1086,7 +1183,9 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     // a player: the first SETUP creates its output and takes a reference (QRM:1614-1622)
     Output* o = nullptr;
     if (!GetPOD(p->inClientSession, sOutputAttr, &o) || !o) {
-        Session* s = NotReflected(p->inRTSPRequest) ? nullptr : FindOrCreateSession(StreamName(p->inRTSPRequest), false);
+        Session* s = NotReflected(p->inRTSPRequest) ? nullptr
+                                                    : FindOrCreateSession(PlayerStreamName(p->inRTSPRequest, M->allowNonSDP),
+                                                                          p->inRTSPRequest, false);
         if (!s) return QTSS_RequestFailed;
         DisableOverbufferingIfPref(p->inClientSession);
         M->outputs.emplace_back(new Output());
@@ -1103,7 +1202,7 @@ QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
     Session* s = FindSession(o->session);
     if (!s) return QTSS_RequestFailed;
     const int t = digitOK ? TrackIndex(*s, trackID) : -1;
-    if (t < 0) return QTSS_RequestFailed;
+    if (t < 0) return SendErrorResponse(p->inRTSPRequest, qtssClientBadRequest);   // no digit / bad track (QRM:1659-1663, 1728-1730)
     QTSS_Object stream = nullptr;
     QTSS_Error e = cb(kAddRTPStreamCallback, p->inClientSession, p->inRTSPRequest, &stream, (uint32_t)0);
     if (e != QTSS_NoErr) return e;
@@ -1352,6 +1451,166 @@ QTSS_Error DestroySession(QTSS_ClientSessionClosing_Params* p) {
     return QTSS_NoErr;
 }
 
+// ---- access: RTSPAuthorize and RTSPRoute ------------------------------------------------------
+// IPComponentStr (QTSSModuleUtils.cpp:1074-1135): an address as four '.'-separated components,
+// valid once four non-empty ones are read (anything after the fourth is ignored); a "*" component
+// on either side matches any.
+struct IPComponents {
+    std::string c[4];
+    bool valid = false;
+    explicit IPComponents(const std::string& s) {
+        size_t p = 0;
+        for (int k = 0; p < s.size(); k++) {
+            size_t e = s.find('.', p);
+            if (e == std::string::npos) e = s.size();
+            if (e == p) break;                           // an empty component
+            c[k] = s.substr(p, e - p);
+            p = e + 1;
+            if (k == 3) { valid = true; break; }
+        }
+    }
+    bool Equal(const IPComponents& t) const {
+        if (!valid || !t.valid) return false;
+        for (int k = 0; k < 4; k++)
+            if (t.c[k] != "*" && c[k] != "*" && t.c[k] != c[k]) return false;
+        return true;
+    }
+};
+
+// QTSSModuleUtils::UserInGroup (QTSSModuleUtils.cpp:918-953): a named user one of whose groups is
+// exactly `group`
+bool UserInGroup(QTSS_Object profile, const std::string& group) {
+    if (!profile || group.empty()) return false;
+    if (GetString(profile, qtssUserName).empty()) return false;
+    uint32_t n = 0;
+    (void)cb(kGetNumValuesCallback, profile, (QTSS_AttributeID)qtssUserGroups, &n);
+    for (uint32_t i = 0; i < n; i++) {
+        std::string g;
+        if (ValueString(profile, qtssUserGroups, i, &g) && g == group) return true;
+    }
+    return false;
+}
+
+uint32_t RequestActions(QTSS_Object req) {
+    uint32_t a = qtssActionFlagsNoFlags;
+    (void)GetPOD(req, qtssRTSPReqAction, &a);
+    return a;
+}
+
+// AcceptSession (QRM:2199-2229): a write request (a push) from a user in BroadcasterGroup, from a
+// local address (127.0.0.*) unless authenticate_local_broadcast, or from an address ip_allow_list
+// matches.  Caller holds mu.
+bool AcceptSession(QTSS_StandardRTSP_Params* p) {
+    if (RequestActions(p->inRTSPRequest) != qtssActionFlagsWrite) return false;
+    QTSS_Object profile = nullptr;
+    (void)GetPOD(p->inRTSPRequest, qtssRTSPReqUserProfile, &profile);
+    if (UserInGroup(profile, M->broadcasterGroup)) return true;
+    char addr[20] = {0};
+    uint32_t len = sizeof(addr);
+    if (GetValue(p->inRTSPSession, qtssRTSPSesRemoteAddrStr, 0, addr, &len) != QTSS_NoErr) return false;
+    const IPComponents client(std::string(addr, len));
+    if (client.Equal(IPComponents("127.0.0.*"))) return !M->authLocal;
+    for (const std::string& a : M->ipAllowList)
+        if (IPComponents(a).Equal(client)) return true;
+    return false;
+}
+
+// QTSSModuleUtils::AuthorizeRequest (QTSSModuleUtils.cpp:1049-1068)
+void SetAuthorization(QTSS_Object req, bool allowed, bool found, bool handled) {
+    (void)SetValue(req, qtssRTSPReqUserAllowed, 0, &allowed, sizeof(allowed));
+    (void)SetValue(req, qtssRTSPReqUserFound, 0, &found, sizeof(found));
+    (void)SetValue(req, qtssRTSPReqAuthHandled, 0, &handled, sizeof(handled));
+}
+
+// QTSS_RTSPAuthorize_Role (ReflectorAuthorizeRTSPRequest, QRM:2231-2257).  An accepted push is
+// authorized outright.  Anything else goes to QTAccessFile::AuthorizeRequest (QTAccessFile.cpp:
+// 492-609) for the request's action with every action but a write left alone: a read is not
+// touched.  For a write it needs the request's local path, root directory and user profile (the
+// server sets the root only when a RTSPRoute module does: EasyDarwin's requests carry none, so a
+// write stops there), looks for a "qtaccess" file from the request's directory up to the root,
+// reads it -- through QTSSModuleUtils::ReadEntireFile, which in EasyDarwin serves the announced-SDP
+// cache alone (QTSSModuleUtils.cpp:68-155), so the text is always empty and "require valid-user"
+// stands in -- and that rule, outside any <Limit WRITE> block, never admits a write
+// (QTAccessFile::AccessAllowed, :187-324).  The user profile's realm becomes the request's; a
+// request without a user is marked handled.  The module then refuses the write: not allowed, no
+// user, not handled.  (Where no qtaccess file is found the reference reads the cache with a NULL
+// path, which throws from std::string; the same empty text is taken here.)
+QTSS_Error Authorize(QTSS_StandardRTSP_Params* p) {
+    std::lock_guard<std::mutex> g(M->mu);
+    QTSS_Object req = p->inRTSPRequest;
+    if (AcceptSession(p)) {
+        SetAuthorization(req, true, true, true);
+        return QTSS_NoErr;
+    }
+    const uint32_t action = RequestActions(req);
+    bool authorized = false;
+    do {
+        if (action == qtssActionFlagsNoFlags || (action & ~(uint32_t)qtssActionFlagsWrite)) break;
+        std::string local, root;
+        QTSS_Object profile = nullptr;
+        if (!ValueString(req, qtssRTSPReqLocalPath, 0, &local) || !ValueString(req, qtssRTSPReqRootDir, 0, &root)) break;
+        if (!GetPOD(req, qtssRTSPReqUserProfile, &profile) || !profile) break;
+        // GetAccessFile_Copy (QTAccessFile.cpp:326-379): the directories of the path, deepest first,
+        // no higher than the root directory
+        {
+            const size_t max_len = local.size() + strlen("qtaccess") + 2;
+            std::string dir = local;
+            const size_t slash = dir.rfind('/');
+            if (slash != std::string::npos) dir.resize(slash);
+            while (dir.size() + strlen("qtaccess") + 1 < max_len) {
+                const std::string f = dir + "/qtaccess";
+                QTSS_Object file = nullptr;
+                if (cb(kOpenFileObjectCallback, f.c_str(), (uint32_t)0, &file) == QTSS_NoErr) {
+                    (void)cb(kCloseFileObjectCallback, file);
+                    break;
+                }
+                const size_t s2 = dir.rfind('/');
+                if (s2 == std::string::npos) break;
+                dir.resize(s2);
+                if (s2 < root.size()) break;
+            }
+        }
+        std::string user;
+        (void)ValueString(profile, qtssUserName, 0, &user);
+        const bool allow = false;                        // "require valid-user" for a write: see above
+        uint32_t scheme = qtssAuthNone;
+        uint32_t n = sizeof(scheme);
+        if (GetValue(req, qtssRTSPReqAuthScheme, 0, &scheme, &n) != QTSS_NoErr) break;
+        std::string realm;
+        if (ValueString(profile, qtssUserRealm, 0, &realm))
+            (void)SetValue(req, qtssRTSPReqURLRealm, 0, realm.data(), (uint32_t)realm.size());
+        authorized = allow;
+        if (!allow && user.empty()) SetAuthorization(req, false, false, true);
+    } while (false);
+    if (!authorized && (action & qtssActionFlagsWrite)) SetAuthorization(req, false, false, false);
+    return QTSS_NoErr;
+}
+
+// QTSS_RTSPRoute_Role (RedirectBroadcast, QRM:2259-2291): a request whose path starts with
+// /<redirect_broadcast_keyword>/ (any case) gets the redirect directory as its root and the path
+// without the keyword -- so its file name, the stream's name, is the next path component
+QTSS_Error Route(QTSS_StandardRTSP_Params* p) {
+    std::string kw, dir;
+    {
+        std::lock_guard<std::mutex> g(M->mu);
+        kw = M->redirectKeyword;
+        dir = M->redirectDir;
+    }
+    if (kw.empty() || dir.empty()) return QTSS_NoErr;
+    std::string path;
+    (void)ValueString(p->inRTSPRequest, qtssRTSPReqFilePath, 0, &path);
+    size_t at = (!path.empty() && path[0] == '/') ? 1 : 0;
+    const size_t end = std::min(path.find('/', at), path.size());
+    const std::string first = path.substr(at, end - at);
+    if (first.size() != kw.size()) return QTSS_NoErr;
+    for (size_t i = 0; i < kw.size(); i++)
+        if (tolower((unsigned char)first[i]) != tolower((unsigned char)kw[i])) return QTSS_NoErr;
+    (void)SetValue(p->inRTSPRequest, qtssRTSPReqRootDir, 0, dir.data(), (uint32_t)dir.size());
+    const std::string rest = path.substr(end);
+    (void)SetValue(p->inRTSPRequest, qtssRTSPReqFilePath, 0, rest.data(), (uint32_t)rest.size());
+    return QTSS_NoErr;
+}
+
 QTSS_Error Dispatch(QTSS_Role role, QTSS_RoleParams* p) {
     switch (role) {
     case QTSS_Register_Role: return Register(p ? &p->regParams : nullptr);
@@ -1361,6 +1620,8 @@ QTSS_Error Dispatch(QTSS_Role role, QTSS_RoleParams* p) {
     case QTSS_RTSPPreProcessor_Role: return ProcessRTSPRequest(&p->rtspRequestParams);
     case QTSS_RTSPIncomingData_Role: return ProcessRTPData(&p->rtspIncomingDataParams);
     case QTSS_ClientSessionClosing_Role: return DestroySession(&p->clientSessionClosingParams);
+    case QTSS_RTSPAuthorize_Role: return Authorize(&p->rtspRequestParams);
+    case QTSS_RTSPRoute_Role: return Route(&p->rtspRequestParams);
     default: return QTSS_NoErr;
     }
 }

@@ -37,7 +37,8 @@ Binary layout (little endian)::
                event* u8 0
                (version 1: no flags byte; version 2: flags bit 0 = UDP push;
                 version 3: as 2, with PUBLISH / UNPUBLISH events;
-                version 4: as 3, with the server's preferences and PREFS events)
+                version 4: as 3, with the server's preferences and PREFS events;
+                version 5: as 4, with IDENT events -- read by tools/qtss_replay alone)
     event   := u8 1 i64 t u32 session u8 channel u32 len bytes[len]          (PKT)
              | u8 2 i64 t u32 session u32 sub_id u8 transport u8 ua_flags    (JOIN)
              | u8 3 i64 t                                                    (TICK)
@@ -48,6 +49,8 @@ Binary layout (little endian)::
              | u8 7 i64 t u32 session u8 kill                                (UNPUBLISH, v3)
              | u8 8 i64 t u32 session                                        (PUBLISH, v3)
              | u8 9 i64 t u32 len bytes[len]                                 (PREFS, v4)
+             | u8 10 i64 t u32 session u8 role u32 addr u8 scheme
+               { u16 len bytes[len] } x 4 (path, user, groups, realm)        (IDENT, v5)
     capture := "EDCP" u32 n { u32 sub u32 session u16 track u8 kind u8 tcp
                              u64 n_packets u64 n_bytes bytes[n_bytes] }*
                [ "EDRR" u32 m { i64 t u32 session u16 track u32 addr u16 port u32 len
@@ -84,7 +87,8 @@ import hashlib
 import struct
 from dataclasses import dataclass, field
 
-PKT, JOIN, TICK, BLOCK, UPKT, LEAVE, UNPUBLISH, PUBLISH, PREFS = 1, 2, 3, 4, 5, 6, 7, 8, 9
+PKT, JOIN, TICK, BLOCK, UPKT, LEAVE, UNPUBLISH, PUBLISH, PREFS, IDENT = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
+IDENT_PUSHER, IDENT_PLAYER = 0, 1
 UDP, TCP = 0, 1
 
 # The reference's defaults of the prefs a trace may set (ReflectorStream.cpp:53-59,
@@ -107,6 +111,14 @@ PREF_DEFAULTS = {
     "timeout_broadcaster_session_secs": "30",
     "reflector_use_in_packet_receive_time": "false",
     "reflector_in_packet_max_receive_sec": "60",
+    # the module's access prefs (QTSSReflectorModule.cpp:141-175, 489-538; RTSPAuthorize, RTSPRoute)
+    "allow_broadcasts": "true",
+    "authenticate_local_broadcast": "false",
+    "BroadcasterGroup": "broadcaster",
+    "ip_allow_list": "127.0.0.*",
+    "redirect_broadcast_keyword": "",
+    "redirect_broadcasts_dir": "",
+    "allow_non_sdp_urls": "true",
 }
 USER_AGENTS = ("EasyPlayer/1.0", "vlc/3.0.8 LibVLC/3.0.8")    # by JOIN ua_flags bit 0
 
@@ -171,6 +183,8 @@ class Trace:
 
     @property
     def version(self) -> int:
+        if any(ev[0] == IDENT for ev in self.events):
+            return 5
         if self.prefs or any(ev[0] == PREFS for ev in self.events):
             return 4
         if any(ev[0] in (PUBLISH, UNPUBLISH) for ev in self.events):
@@ -204,6 +218,15 @@ class Trace:
 
     def publish(self, t: int, session: int):
         self.events.append((PUBLISH, int(t), session))
+
+    def ident(self, t: int, session: int, role: int, addr: int, path: str = "", user: str = "",
+              groups: str = "", realm: str = "", scheme: int = 0):
+        """Who opens the session's next RTSP connection of `role` (IDENT_PUSHER: its next
+        PUBLISH; IDENT_PLAYER: its next JOIN) -- for the module's RTSPRoute / RTSPAuthorize roles
+        (tools/qtss_replay): the client's IPv4 address, the request path ("" = the session's
+        own), the user the server authenticated with its groups (comma-separated) and realm, and
+        the request's auth scheme."""
+        self.events.append((IDENT, int(t), session, role, int(addr), path, user, groups, realm, scheme))
 
     def reprefs(self, t: int, prefs: dict):
         """The server rewrites its prefs (these overrides replace the previous ones) and sends
@@ -253,6 +276,12 @@ class Trace:
             elif ev[0] == PREFS:
                 pb = pack_prefs(ev[2])
                 out.append(struct.pack("<BqI", PREFS, ev[1], len(pb)) + pb)
+            elif ev[0] == IDENT:
+                _, t, s, role, addr, path, user, groups, realm, scheme = ev
+                out.append(struct.pack("<BqIBIB", IDENT, t, s, role, addr, scheme))
+                for txt in (path, user, groups, realm):
+                    b = txt.encode()
+                    out.append(struct.pack("<H", len(b)) + b)
             else:
                 out.append(struct.pack("<Bq", TICK, ev[1]))
         out.append(b"\x00")
@@ -266,7 +295,7 @@ class Trace:
     def from_bytes(buf: bytes) -> "Trace":
         assert buf[:4] == b"EDTR"
         ver, n = struct.unpack_from("<II", buf, 4)
-        assert ver in (1, 2, 3, 4)
+        assert ver in (1, 2, 3, 4, 5)
         p = 12
         tr = Trace()
         for _ in range(n):
@@ -320,6 +349,15 @@ class Trace:
                 _, t, ln = struct.unpack_from("<BqI", buf, p)
                 tr.events.append((PREFS, t, unpack_prefs(buf[p + 13:p + 13 + ln])))
                 p += 13 + ln
+            elif typ == IDENT:
+                _, t, s, role, addr, scheme = struct.unpack_from("<BqIBIB", buf, p)
+                p += 19
+                txt = []
+                for _ in range(4):
+                    (ln,) = struct.unpack_from("<H", buf, p)
+                    txt.append(bytes(buf[p + 2:p + 2 + ln]).decode())
+                    p += 2 + ln
+                tr.events.append((IDENT, t, s, role, addr) + tuple(txt) + (scheme,))
             elif typ == UPKT:
                 _, t, s, ch, addr, port, ln = struct.unpack_from("<BqIBIHI", buf, p)
                 p += 24

@@ -106,6 +106,22 @@ enum : uint32_t {
     qtssPrefsObjectType = four_cc('p', 'r', 'f', 'o'),
     qtssModuleObjectType = four_cc('m', 'o', 'd', 'o'),
     qtssAttrInfoObjectType = four_cc('a', 't', 't', 'r'),
+    qtssUserProfileObjectType = four_cc('u', 's', 'p', 'o'),
+};
+
+// request actions (QTSS.h:127-131), auth schemes (:195-197), RTSP status codes
+// (QTSSRTSPProtocol.h:146-186: an index, the wire code in the comment)
+enum : uint32_t {
+    qtssActionFlagsNoFlags = 0, qtssActionFlagsRead = 1, qtssActionFlagsWrite = 2,
+    qtssAuthNone = 0, qtssAuthBasic = 1, qtssAuthDigest = 2,
+};
+enum : uint32_t {
+    qtssSuccessOK = 1,              // 200
+    qtssClientBadRequest = 13,      // 400
+    qtssClientUnAuthorized = 14,    // 401
+    qtssClientForbidden = 16,       // 403
+    qtssClientNotFound = 17,        // 404
+    qtssPreconditionFailed = 25,    // 412
 };
 
 // attribute ids read or written by the reflector module
@@ -126,6 +142,13 @@ enum : uint32_t {
     qtssRTSPReqContentLen = 25, qtssRTSPReqTransportType = 28, qtssRTSPReqTransportMode = 29,
     qtssRTSPReqRootDir = 14,
     qtssRTSPReqSetUpServerPort = 30,                 // UInt16: server_port of a push SETUP's response
+    qtssRTSPReqFilePathTrunc = 4, qtssRTSPReqStatusCode = 10, qtssRTSPReqUserAllowed = 19,
+    qtssRTSPReqURLRealm = 20, qtssRTSPReqLocalPath = 21, qtssRTSPReqRespMsg = 24, qtssRTSPReqAction = 31,
+    qtssRTSPReqUserProfile = 32, qtssRTSPReqAuthScheme = 34, qtssRTSPReqUserFound = 39, qtssRTSPReqAuthHandled = 40,
+    // RTSP session object (QTSS.h:528-546)
+    qtssRTSPSesRemoteAddrStr = 5,
+    // user profile object (QTSS.h:928-935)
+    qtssUserName = 0, qtssUserGroups = 2, qtssUserRealm = 3,
 };
 
 // RTSP header ids (QTSSRTSPProtocol.h:68-100)
@@ -198,6 +221,7 @@ enum : uint32_t {
     kWriteCallback = 10, kAppendRTSPHeadersCallback = 17, kSendStandardRTSPCallback = 18,
     kAddRTPStreamCallback = 19, kPlayCallback = 20, kPauseCallback = 21, kTeardownCallback = 22,
     kRequestEventCallback = 23, kSetIdleTimerCallback = 24, kReadCallback = 27,
+    kSendRTSPHeadersCallback = 16, kOpenFileObjectCallback = 25, kCloseFileObjectCallback = 26,
     kGetNumValuesCallback = 30, kAddStaticAttributeCallback = 35, kAddInstanceAttributeCallback = 36,
     kGetAttrInfoByNameCallback = 39, kGetValueAsStringCallback = 41, kValueToStringCallback = 45,
     kRemoveValueCallback = 46, kRefreshTimeOutCallback = 52, kLockObjectCallback = 55, kUnlockObjectCallback = 56,

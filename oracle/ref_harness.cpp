@@ -223,6 +223,9 @@ static const char* const kPrefDefaults[][2] = {            // easydarwin_amd/tra
     {"enable_broadcast_announce", "true"}, {"enable_broadcast_push", "true"},
     {"allow_duplicate_broadcasts", "false"}, {"timeout_broadcaster_session_secs", "30"},
         {"reflector_use_in_packet_receive_time", "false"}, {"reflector_in_packet_max_receive_sec", "60"},
+        {"allow_broadcasts", "true"}, {"authenticate_local_broadcast", "false"}, {"BroadcasterGroup", "broadcaster"},
+        {"ip_allow_list", "127.0.0.*"}, {"redirect_broadcast_keyword", ""}, {"redirect_broadcasts_dir", ""},
+        {"allow_non_sdp_urls", "true"},
 };
 static FakeObj* g_mod_prefs = nullptr;      // QTSSReflectorModule's prefs object
 static FakeObj* g_srv_prefs = nullptr;      // the server's prefs object

@@ -54,6 +54,15 @@ SAME(kAddRTPStreamCallback); SAME(kPlayCallback); SAME(kPauseCallback); SAME(kTe
 SAME(kRequestEventCallback); SAME(kSetIdleTimerCallback); SAME(kReadCallback); SAME(kGetNumValuesCallback);
 SAME(kAddStaticAttributeCallback); SAME(kRemoveValueCallback); SAME(kLastCallback);
 SAME(kValueToStringCallback); SAME(kRefreshTimeOutCallback); SAME(kLockObjectCallback); SAME(kUnlockObjectCallback);
+SAME(kSendRTSPHeadersCallback); SAME(kOpenFileObjectCallback); SAME(kCloseFileObjectCallback);
+SAME(qtssUserProfileObjectType); SAME(qtssActionFlagsNoFlags); SAME(qtssActionFlagsRead); SAME(qtssActionFlagsWrite);
+SAME(qtssAuthNone); SAME(qtssAuthBasic); SAME(qtssAuthDigest);
+SAME(qtssSuccessOK); SAME(qtssClientBadRequest); SAME(qtssClientUnAuthorized); SAME(qtssClientForbidden);
+SAME(qtssClientNotFound); SAME(qtssPreconditionFailed);
+SAME(qtssRTSPReqFilePathTrunc); SAME(qtssRTSPReqStatusCode); SAME(qtssRTSPReqUserAllowed); SAME(qtssRTSPReqURLRealm);
+SAME(qtssRTSPReqLocalPath); SAME(qtssRTSPReqRespMsg); SAME(qtssRTSPReqAction); SAME(qtssRTSPReqUserProfile);
+SAME(qtssRTSPReqAuthScheme); SAME(qtssRTSPReqUserFound); SAME(qtssRTSPReqAuthHandled); SAME(qtssRTSPSesRemoteAddrStr);
+SAME(qtssUserName); SAME(qtssUserGroups); SAME(qtssUserRealm);
 
 static_assert(sizeof(E::QTSS_Error) == sizeof(::QTSS_Error), "QTSS_Error");
 static_assert(sizeof(E::QTSS_Role) == sizeof(::QTSS_Role), "QTSS_Role");

@@ -11,7 +11,8 @@ For every scenario in tests/scenarios.py:
      (EDGPU_TT_OUT, pinned for the QTSS module drop-in), the pushers' keep-alive log (the module's
      qtssCliSesTimeoutMsec settings, QTSS_RefreshTimeOut calls and the server's timeouts,
      EDGPU_KEEPALIVE_LOG) and, for ``keepalive``, the same replay with the refreshes ignored
-     (EDGPU_REPLAY_NO_REFRESH: the UDP pusher times out)} and, for the small scenarios, the
+     (EDGPU_REPLAY_NO_REFRESH: the UDP pusher times out); for the module scenarios also every RTSP
+     request's route, authorization and response (EDGPU_REQ_LOG)} and, for the small scenarios, the
      trace and the reference capture themselves (<name>.edtr/.edcp).
 
 Run here (needs /root/reference):  python tests/golden/make_golden.py
@@ -102,9 +103,9 @@ def main():
             tpath = os.path.join(td, name + ".edtr")
             with open(tpath, "wb") as f:
                 f.write(trace)
-            rc, tt, ka = tpath + ".ref", tpath + ".edtt", tpath + ".ka"
+            rc, tt, ka, rq = tpath + ".ref", tpath + ".edtt", tpath + ".ka", tpath + ".req"
             subprocess.run([replay, refmod, tpath, rc], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           env=dict(os.environ, EDGPU_TT_OUT=tt, EDGPU_KEEPALIVE_LOG=ka))
+                           env=dict(os.environ, EDGPU_TT_OUT=tt, EDGPU_KEEPALIVE_LOG=ka, EDGPU_REQ_LOG=rq))
             rb = open(rc, "rb").read()
             cap = read_capture(rb)
             fix = {
@@ -119,6 +120,9 @@ def main():
                 "transmit_sha256": hashlib.sha256(open(tt, "rb").read()).hexdigest(),
                 "keepalive_log_sha256": hashlib.sha256(open(ka, "rb").read()).hexdigest(),
                 "keepalive_log": open(ka).read().splitlines(),
+                # every RTSP request: route, authorization, response (tools/qtss_replay EDGPU_REQ_LOG)
+                "request_log_sha256": hashlib.sha256(open(rq, "rb").read()).hexdigest(),
+                "request_log": open(rq).read().splitlines(),
             }
             with open(os.path.join(HERE, name + ".json"), "w") as f:
                 json.dump(fix, f, indent=1, sort_keys=True)

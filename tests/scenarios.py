@@ -59,11 +59,11 @@ import numpy as np
 
 from easydarwin_amd.synth import (SEED_BASE, TrackSpec, make_sdp, rtp_header, rtcp_sr,
                                   session_packets)
-from easydarwin_amd.trace import TCP, UDP, Trace
+from easydarwin_amd.trace import IDENT_PLAYER, IDENT_PUSHER, TCP, UDP, Trace
 
 
 def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
-              joins: list[tuple], tick_times=None, blocks=None, leaves=None, pubs=None, prefs=None):
+              joins: list[tuple], tick_times=None, blocks=None, leaves=None, pubs=None, prefs=None, idents=None):
     # joins: (t, session, sub, transport) or (t, session, sub, transport, ua_flags)
     # blocks: {tick time: [(sub, track, kind, budget)]}
     # leaves: [(t, sub)]
@@ -87,6 +87,9 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
             pkts.append((p[0], 1 << 30, 0, "U", p[2], p[3]))
     for k, (t, pr) in enumerate(prefs or []):
         pkts.append((t, -2, k, "R", pr))
+    # idents: (t, session, role, addr, path, user, groups, realm) -- before a PUBLISH / JOIN of its time
+    for k, idt in enumerate(idents or []):
+        pkts.append((idt[0], -3, k, "I", idt[1:]))
     pkts.sort(key=lambda x: (x[0], x[1], x[2]))
     joins = sorted([(j[0], 0) + tuple(j[1:]) for j in joins] + [(t, 1, sub) for t, sub in (leaves or [])])
     ticks = tick_times if tick_times is not None else list(range(0, end_ms + 1, tick_ms))
@@ -96,6 +99,8 @@ def _assemble(tr: Trace, per_session: list[list], tick_ms: int, end_ms: int,
             t, s, _, ch, data = pkts[i][:5]
             if ch == "R":
                 tr.reprefs(t, data)
+            elif ch == "I":
+                tr.ident(t, *data)
             elif ch == "P":
                 tr.publish(t, data)
             elif ch == "U":
@@ -833,8 +838,63 @@ def aktt() -> Trace:
     return _assemble(tr, [pk0, pk1], 100, dur, joins, tick_times=ticks, blocks=blocks, pubs=pubs)
 
 
+def access() -> Trace:
+    """The module's access roles (QTSSReflectorModule.cpp:2199-2304), for the QTSS module only: its
+    fixture comes from the REFERENCE module in tools/qtss_replay, which now runs the RTSPRoute and
+    RTSPAuthorize roles before the preprocessor (a request left not allowed is answered 403 by the
+    server) and logs every request's route, authorization and response (EDGPU_REQ_LOG).  Prefs:
+    ip_allow_list "10.7.*.*,192.168.1.20", redirect_broadcast_keyword "/live/" (trimmed to "live"),
+    the redirect directory under the movie folder.  Session 0 (RTSP-interleaved) changes pushers:
+
+    * 1.1 s a pusher from 10.9.0.1, no user: not accepted (not local, not listed), and QTAccessFile
+      stops at the request's missing root directory -> 403;
+    * 1.3 s one from 10.7.3.4 (the allow list's wildcard) -> pushes;
+    * 2.6 s 203.0.113.5, user "alice" in groups editors,broadcaster (BroadcasterGroup) -> pushes;
+    * 3.6 s 203.0.113.6, user "bob" (editors, realm "EasyRealm") -> 403;
+    * 3.7 s bob again at /live/stream0.sdp: routed (root ./Movies/, path /stream0.sdp), so QTAccessFile
+      reaches the movie folder's qtaccess, takes bob's realm, and still refuses the write -> 403;
+    * 3.8 s a local pusher at /LIVE/stream0.sdp: routed (any case) to the same stream -> pushes;
+    * 4.0 s a player at /live/stream0.sdp: routed, its lookup path (root + file name) names no
+      session -> refused; players at /stream0.sdp keep playing;
+    * 4.2 s authenticate_local_broadcast on: session 2's local pusher leaves and returns -> 403;
+    * 5.0 s allow_broadcasts off: a player's SETUP and session 1's returning UDP pusher are answered
+      403 "Broadcast is not allowed." (AllowBroadcast); 6.0 s on again: a player joins."""
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=30, idr_bytes=4_000, rtcp_every_ms=700),
+         TrackSpec("audio", "PCMA/8000", 8)]
+    u = [TrackSpec("video", "H264/90000", 96, bitrate=200_000, gop=30, idr_bytes=3_000, rtcp_every_ms=900)]
+    w = [TrackSpec("video", "H264/90000", 96, bitrate=150_000, gop=20, idr_bytes=2_000)]
+    tr = Trace()
+    base = {"ip_allow_list": "10.7.*.*,192.168.1.20", "redirect_broadcast_keyword": "/live/"}
+    tr.prefs = dict(base)
+    tr.add_session(make_sdp(v))
+    tr.add_session(make_sdp(u), udp_push=True)
+    tr.add_session(make_sdp(w))
+    dur = 7_000
+    pk0 = session_packets(v, dur, SEED_BASE + 160)
+    src = _ip(10, 6, 0, 3)
+    pk1 = [(t, ch, d, src, 6300 + (ch & 1)) for t, ch, d in session_packets(u, dur, SEED_BASE + 161)]
+    pk2 = session_packets(w, dur, SEED_BASE + 162)
+    P, L = IDENT_PUSHER, IDENT_PLAYER
+    idents = [(1100, 0, P, _ip(10, 9, 0, 1), "", "", "", ""),
+              (1300, 0, P, _ip(10, 7, 3, 4), "", "", "", ""),
+              (2600, 0, P, _ip(203, 0, 113, 5), "", "alice", "editors,broadcaster", ""),
+              (3600, 0, P, _ip(203, 0, 113, 6), "", "bob", "editors", "EasyRealm"),
+              (3700, 0, P, _ip(203, 0, 113, 6), "/live/stream0.sdp", "bob", "editors", "EasyRealm"),
+              (3800, 0, P, _ip(127, 0, 0, 1), "/LIVE/stream0.sdp", "", "", ""),
+              (4000, 0, L, _ip(127, 0, 0, 1), "/live/stream0.sdp", "", "", "")]
+    pubs = [(1000, "unpublish", 0, 0), (1100, "publish", 0), (1300, "publish", 0),
+            (2500, "unpublish", 0, 0), (2600, "publish", 0), (3500, "unpublish", 0, 0), (3600, "publish", 0),
+            (3700, "publish", 0), (3800, "publish", 0),
+            (4300, "unpublish", 2, 0), (4400, "publish", 2), (5200, "unpublish", 1, 0), (5300, "publish", 1)]
+    prefs = [(4200, dict(base, authenticate_local_broadcast="true")),
+             (5000, dict(base, allow_broadcasts="false")), (6000, dict(base))]
+    joins = [(0, 0, 1, UDP), (0, 0, 2, TCP), (0, 1, 10, UDP), (0, 2, 20, UDP), (1500, 0, 3, UDP),
+             (4000, 0, 4, UDP), (4100, 0, 5, TCP), (5100, 0, 6, UDP), (6100, 0, 7, UDP), (6200, 1, 11, TCP)]
+    return _assemble(tr, [pk0, pk1, pk2], 100, dur, joins, pubs=pubs, prefs=prefs, idents=idents)
+
+
 # Scenarios for the QTSS module alone: fixtures from the reference module in tools/qtss_replay
-MODULE_SCENARIOS = {"prefs_push": prefs_push}
+MODULE_SCENARIOS = {"prefs_push": prefs_push, "access": access}
 
 
 SCENARIOS = {

@@ -36,6 +36,7 @@ REPLAY = os.path.join(ROOT, "tools", "qtss_replay")
 TCP_PUSH = ["tiny", "c1", "mixed", "clamp", "ssrc", "nal", "nokey", "stall", "anchor", "rtpinfo", "backpressure"]
 UDP_PUSH = ["udppush", "leave", "repush"]   # UDP pushers (with interleaved ones beside them)
 PREFS = ["prefs_buffer", "prefs_reread", "prefs_push"]   # the server's prefs objects, RereadPrefs
+ACCESS = ["access"]                           # RTSPAuthorize / RTSPRoute / allow_broadcasts (module-only fixture)
 KEEPALIVE = ["keepalive"]                     # 70 s: the pushers' timeouts and the module's refreshes
 RETENTION = ["highrate", "longbuffer"]        # retention past the default ring capacities (ring growth)
 RECEIVE_TIME = ["aktt"]                       # reflector_use_in_packet_receive_time: the "aktt" trailer
@@ -43,16 +44,17 @@ RECEIVE_TIME = ["aktt"]                       # reflector_use_in_packet_receive_
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["whole", "parts"])
-@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE + RETENTION + RECEIVE_TIME)
+@pytest.mark.parametrize("name", TCP_PUSH + UDP_PUSH + PREFS + KEEPALIVE + RETENTION + RECEIVE_TIME + ACCESS)
 def test_module_matches_reference(name, gather, tmp_path):
     """`parts`: every tick's readback gathered in parts, overlapped with the write threads
     (EDGPU_GATHER_SPLIT_BYTES=0; by default only ticks of 8 MiB and more are split).  The
     keep-alive log -- the timeout set at every push SETUP, every QTSS_RefreshTimeOut, the server's
     timeouts -- is the reference's too (QTSSReflectorModule.cpp:1644, ReflectorStream.cpp:
     1779-1786).  `prefs_push`'s fixture is the reference module's own output."""
-    t, c, tt, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log"
+    t, c, tt, ka, rq = (tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log",
+                        tmp_path / "rq.log")
     t.write_bytes(_trace(name).to_bytes())
-    env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka))
+    env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka), EDGPU_REQ_LOG=str(rq))
     if gather == "parts":
         env["EDGPU_GATHER_SPLIT_BYTES"] = "0"
     r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
@@ -66,6 +68,8 @@ def test_module_matches_reference(name, gather, tmp_path):
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fixture(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fixture(name)["transmit_sha256"]
     assert hashlib.sha256(ka.read_bytes()).hexdigest() == _fixture(name)["keepalive_log_sha256"]
+    if "request_log" in _fixture(name):   # the reference module's own routes, authorizations, responses
+        assert rq.read_text().splitlines() == _fixture(name)["request_log"]
 
 
 @pytest.mark.gpu
@@ -88,7 +92,7 @@ REF_MODULE = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["repush", "rtpinfo", "leave", "threaded", "udppush", "prefs_reread", "backpressure",
-                                  "keepalive", "prefs_push", "aktt"])
+                                  "keepalive", "prefs_push", "aktt", "access", "c1", "mixed", "nokey", "ssrc"])
 @pytest.mark.parametrize("refresh", ["on", "off"])
 def test_module_equals_reference_module(name, refresh, tmp_path):
     """The drop-in and the REFERENCE QTSSReflectorModule (compiled from its own sources,
@@ -103,14 +107,15 @@ def test_module_equals_reference_module(name, refresh, tmp_path):
     t.write_bytes(_trace(name).to_bytes())
     out = {}
     for tag, so in (("gpu", MODULE), ("ref", REF_MODULE)):
-        c, tt, ka = tmp_path / f"{tag}.edcp", tmp_path / f"{tag}.edtt", tmp_path / f"{tag}.ka"
-        env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka))
+        c, tt, ka, rq = tmp_path / f"{tag}.edcp", tmp_path / f"{tag}.edtt", tmp_path / f"{tag}.ka", tmp_path / f"{tag}.rq"
+        env = dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka), EDGPU_REQ_LOG=str(rq))
         if refresh == "off":
             env["EDGPU_REPLAY_NO_REFRESH"] = "1"
         r = subprocess.run([REPLAY, so, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
         assert r.returncode == 0, (tag, r.stderr[-2000:])
-        out[tag] = (c.read_bytes(), tt.read_bytes(), ka.read_text())
+        out[tag] = (c.read_bytes(), tt.read_bytes(), ka.read_text(), rq.read_text())
     assert out["gpu"][2] == out["ref"][2], "keep-alive logs differ"
+    assert out["gpu"][3].splitlines() == out["ref"][3].splitlines(), "request logs (routes, authorizations, responses) differ"
     assert out["gpu"][0] == out["ref"][0]
     assert out["gpu"][1] == out["ref"][1]
 

@@ -45,4 +45,5 @@ def test_module_registers_through_the_plugin_abi():
     assert r.returncode == 0, r.stderr
     info = json.loads(r.stdout)
     assert info["module"] == "QTSSReflectorModule"
-    assert info["roles"] == 6 and info["attributes"] == 8
+    # the reference's roles (QTSSReflectorModule.cpp:268-276) but EasyCMS's Easy_GetDeviceStream
+    assert info["roles"] == 8 and info["attributes"] == 8

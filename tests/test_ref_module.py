@@ -49,17 +49,20 @@ def test_reference_module_reproduces_fixture(name, refmod, tmp_path):
     its QTSS_RefreshTimeOut calls, the server's timeouts: ReflectorStream.cpp:1779-1786,
     QTSSReflectorModule.cpp:1644) as the harness restated them -- or, for the module-only
     scenarios, as this same module produced them when the fixture was made."""
-    t, c, tt, ka = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log"
+    t, c, tt, ka, rq = (tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "t.edtt", tmp_path / "ka.log",
+                        tmp_path / "rq.log")
     fn = SCENARIOS.get(name) or MODULE_SCENARIOS[name]
     t.write_bytes(fn().to_bytes())
     from conftest import udp_port_lock
     with udp_port_lock():                # UDP pushers bind fixed loopback source ports
         r = subprocess.run([REPLAY, refmod, str(t), str(c)], capture_output=True, text=True, timeout=300,
-                           env=dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka)))
+                           env=dict(os.environ, EDGPU_TT_OUT=str(tt), EDGPU_KEEPALIVE_LOG=str(ka), EDGPU_REQ_LOG=str(rq)))
     assert r.returncode == 0, r.stderr[-3000:]
     assert hashlib.sha256(c.read_bytes()).hexdigest() == _fix(name)["capture_sha256"]
     assert hashlib.sha256(tt.read_bytes()).hexdigest() == _fix(name)["transmit_sha256"]
     assert hashlib.sha256(ka.read_bytes()).hexdigest() == _fix(name)["keepalive_log_sha256"]
+    if "request_log" in _fix(name):        # module scenarios: every request's route, authorization, response
+        assert rq.read_text().splitlines() == _fix(name)["request_log"]
 
 
 def test_reference_module_udp_pusher_times_out_without_refresh(refmod, tmp_path):

@@ -123,6 +123,13 @@ struct Obj {
     Obj* owner = nullptr;                                 // RTP stream objects: their client session
     // dictionaries with named (instance) attributes: the prefs objects
     std::map<std::string, std::pair<uint32_t, uint32_t>> named;   // name -> (id, data type)
+    // RTSP sessions: the connection's user profile and auth scheme (trace IDENT); RTSP requests:
+    // what the module answered (QTSS_SendStandardRTSPResponse / QTSS_SendRTSPHeaders, the bytes it
+    // wrote to the request stream)
+    Obj* profile = nullptr;
+    uint32_t scheme = 0;
+    bool sent_std = false, sent_headers = false;
+    size_t written = 0;
 };
 static std::vector<std::unique_ptr<Obj>> g_objs;
 static std::mutex g_objs_mu;                          // --bench realtime: the churn thread creates objects
@@ -206,18 +213,61 @@ static QTSS_Error cb_id_for_tag(uint32_t type, const char* name, uint32_t* out, 
     *out = it->second;
     return QTSS_NoErr;
 }
+// A request's attributes the server computes from its file path and root directory whenever they
+// are read (param retrieval functions, RTSPRequestInterface.cpp:661-711, 753-802): the file name
+// (the path's first component), the truncated path and the local path (root + path, or + the
+// truncated path for a SETUP), so a module's RTSPRoute rewrite of the path or root shows in them.
+static std::string attr_str(const Obj* o, uint32_t id) {
+    auto it = o->attrs.find(id);
+    return it == o->attrs.end() || it->second.empty() ? std::string() : it->second[0];
+}
+static void materialize(Obj* o, uint32_t id) {
+    if (o->type != qtssRTSPRequestObjectType) return;
+    if (id != qtssRTSPReqFileName && id != qtssRTSPReqFilePathTrunc && id != qtssRTSPReqLocalPath) return;
+    const std::string path = attr_str(o, qtssRTSPReqFilePath);
+    auto trunc = [&]() {                       // GetTruncatedPath: without the last element
+        size_t n = path.size();
+        if (n > 0) { n--; while (n != 0 && path[n] != '/') n--; }
+        return path.substr(0, n);
+    };
+    std::string v;
+    if (id == qtssRTSPReqFileName) {
+        v = path;
+        if (!v.empty() && v[0] == '/') v.erase(0, 1);
+        if (v.find('/') != std::string::npos) v.resize(v.find('/'));
+    } else if (id == qtssRTSPReqFilePathTrunc) {
+        v = trunc();
+    } else {
+        uint32_t m = 0;
+        auto mt = o->attrs.find(qtssRTSPReqMethod);
+        if (mt != o->attrs.end() && !mt->second.empty()) memcpy(&m, mt->second[0].data(), 4);
+        std::string fp = m == qtssSetupMethod ? trunc() : path;
+        const std::string root = attr_str(o, qtssRTSPReqRootDir);
+        if (!root.empty() && root.back() == '/' && !fp.empty() && fp[0] == '/') {
+            size_t k = 0;
+            while (k < fp.size() && fp[k] == '/') k++;
+            fp.erase(0, k);
+        }
+        v = root + fp;
+    }
+    auto& a = o->attrs[id];
+    a.assign(1, v);
+}
 static QTSS_Error cb_get_value_ptr(Obj* o, uint32_t id, uint32_t idx, void** out, uint32_t* len, ...) {
     if (!o) return QTSS_BadArgument;
+    materialize(o, id);
     auto it = o->attrs.find(id);
-    if (it == o->attrs.end() || idx >= it->second.size()) { *len = 0; return QTSS_ValueNotFound; }
+    // a value of length 0 is no value (QTSSDictionary::GetValuePtr, QTSSDictionary.cpp:144-146)
+    if (it == o->attrs.end() || idx >= it->second.size() || it->second[idx].empty()) { *len = 0; return QTSS_ValueNotFound; }
     *out = (void*)it->second[idx].data();
     *len = (uint32_t)it->second[idx].size();
     return QTSS_NoErr;
 }
 static QTSS_Error cb_get_value(Obj* o, uint32_t id, uint32_t idx, void* buf, uint32_t* len, ...) {
     if (!o) return QTSS_BadArgument;
+    materialize(o, id);
     auto it = o->attrs.find(id);
-    if (it == o->attrs.end() || idx >= it->second.size()) return QTSS_ValueNotFound;
+    if (it == o->attrs.end() || idx >= it->second.size() || it->second[idx].empty()) return QTSS_ValueNotFound;
     const std::string& v = it->second[idx];
     if (*len < v.size()) { *len = (uint32_t)v.size(); return QTSS_NotEnoughSpace; }
     memcpy(buf, v.data(), v.size());
@@ -251,9 +301,9 @@ static QTSS_Error cb_num_values(Obj* o, uint32_t id, uint32_t* n, ...) {
 }
 static QTSS_Error cb_value_as_string(Obj* o, uint32_t id, uint32_t idx, char** out, ...) {
     if (!o || !out) return QTSS_BadArgument;
-    *out = nullptr;
+    materialize(o, id);
     auto it = o->attrs.find(id);
-    if (it == o->attrs.end() || idx >= it->second.size()) return QTSS_ValueNotFound;
+    if (it == o->attrs.end() || idx >= it->second.size() || it->second[idx].empty()) return QTSS_ValueNotFound;
     const std::string& v = it->second[idx];
     char* c = new char[v.size() + 1];          // QTSS_GetValueAsString: the caller delete[]s it
     memcpy(c, v.data(), v.size());
@@ -284,8 +334,15 @@ static void load_prefs(const trace_prefs::Prefs& p) {
     g_mod_prefs->named.clear();
     for (const auto& kv : p.over) {
         if (kv.first == "player_requires_rtp_header_info") continue;
-        const bool isBool = kv.second == "true" || kv.second == "false";
         const uint32_t id = g_next_named++;
+        if (trace_prefs::is_string(kv.first)) {             // char array prefs; a LIST-PREF takes a value per entry
+            g_mod_prefs->named[kv.first] = std::make_pair(id, (uint32_t)qtssAttrDataTypeCharArray);
+            const std::vector<std::string> vals = trace_prefs::is_list(kv.first) ? p.list(kv.first)
+                                                                                  : std::vector<std::string>{kv.second};
+            for (size_t i = 0; i < vals.size(); i++) set_attr(g_mod_prefs, id, (uint32_t)i, vals[i].data(), (uint32_t)vals[i].size());
+            continue;
+        }
+        const bool isBool = kv.second == "true" || kv.second == "false";
         g_mod_prefs->named[kv.first] = std::make_pair(id, (uint32_t)(isBool ? qtssAttrDataTypeBool16 : qtssAttrDataTypeUInt32));
         if (isBool) set_pod<bool>(g_mod_prefs, id, kv.second == "true");
         else set_pod<uint32_t>(g_mod_prefs, id, (uint32_t)strtoul(kv.second.c_str(), nullptr, 10));
@@ -339,6 +396,7 @@ static LatHist* lat_hist() {
     return h;
 }
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
+    if (o && o->type == qtssRTSPRequestObjectType) { o->written += len; if (outLen) *outLen = len; return QTSS_NoErr; }
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
     const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (g_count_only) {
@@ -426,6 +484,18 @@ static Obj* g_current_client = nullptr;
 static QTSS_Error cb_set_idle_timer(int64_t, ...) { if (g_current_client) g_current_client->idle_timer = true; return QTSS_NoErr; }
 static QTSS_Error cb_ok(...) { return QTSS_NoErr; }
 static QTSS_Error cb_unimplemented(...) { return QTSS_Unimplemented; }
+// QTSS_SendStandardRTSPResponse / QTSS_SendRTSPHeaders: the response went out (its status is the
+// request's qtssRTSPReqStatusCode, 200 for the standard response)
+static QTSS_Error cb_send_standard(Obj* req, ...) { if (req) req->sent_std = true; return QTSS_NoErr; }
+static QTSS_Error cb_send_headers(Obj* req, ...) { if (req) req->sent_headers = true; return QTSS_NoErr; }
+// QTSS_OpenFileObject / QTSS_CloseFileObject (QTAccessFile::GetAccessFile_Copy walks the request's
+// directories for a "qtaccess" file): the movie folder holds one, nothing else exists
+static QTSS_Error cb_open_file(const char* path, uint32_t, Obj** out, ...) {
+    if (!path || !out) return QTSS_BadArgument;
+    if (strcmp(path, "./Movies/qtaccess") != 0) return QTSS_FileNotFound;
+    *out = new_obj(0);
+    return QTSS_NoErr;
+}
 
 // ---- trace ----------------------------------------------------------------------------------
 struct Reader {
@@ -494,6 +564,62 @@ static void read_reports() {
     g_reports.insert(g_reports.end(), got.begin(), got.end());
 }
 
+// ---- RTSP connections: who opens them (trace v5 IDENT events) -------------------------------
+struct Ident {
+    uint32_t addr = 0x7F000001u;                   // 127.0.0.1: the pushers and players of older traces
+    std::string path, user, groups, realm;         // path "": the session's own
+    uint32_t scheme = 0;                           // qtssAuthNone
+    bool set = false;                              // from an IDENT event
+};
+static std::string dotted(uint32_t a) {
+    return std::to_string(a >> 24) + "." + std::to_string((a >> 16) & 255) + "." + std::to_string((a >> 8) & 255) + "." +
+           std::to_string(a & 255);
+}
+// An RTSP connection from `id`: its remote address (qtssRTSPSesRemoteAddrStr) and the user profile
+// the server's authentication left on it -- the user's name, groups and realm (QTSSUserProfile)
+static Obj* new_rtsp(const Ident& id = Ident()) {
+    Obj* r = new_obj(qtssRTSPSessionObjectType);
+    const std::string a = dotted(id.addr);
+    set_attr(r, qtssRTSPSesRemoteAddrStr, 0, a.data(), (uint32_t)a.size());
+    Obj* u = new_obj(qtssUserProfileObjectType);
+    set_attr(u, qtssUserName, 0, id.user.data(), (uint32_t)id.user.size());
+    uint32_t g = 0;
+    for (size_t p = 0; p < id.groups.size();) {
+        size_t e = id.groups.find(',', p);
+        if (e == std::string::npos) e = id.groups.size();
+        set_attr(u, qtssUserGroups, g++, id.groups.data() + p, (uint32_t)(e - p));
+        p = e + 1;
+    }
+    if (!id.realm.empty()) set_attr(u, qtssUserRealm, 0, id.realm.data(), (uint32_t)id.realm.size());
+    r->profile = u;
+    r->scheme = id.scheme;
+    return r;
+}
+// EDGPU_REQ_LOG=<path>: every RTSP request -- who sent it, the method and path, the file path and
+// root directory after the module's RTSPRoute role, the request's authorization after its
+// RTSPAuthorize role (qtssRTSPReqUserAllowed / UserFound / AuthHandled, qtssRTSPReqURLRealm), and
+// the response: the server's 401 / 403 for a request the authorization refused, else the status
+// the module left (qtssRTSPReqStatusCode) with how it answered (the standard response, its own
+// headers + bytes written, or nothing) and the keep-alive flag
+static FILE* g_req_log = nullptr;
+static std::string status_str(uint32_t s) {
+    switch (s) {
+        case qtssSuccessOK: return "200";
+        case qtssClientBadRequest: return "400";
+        case qtssClientUnAuthorized: return "401";
+        case qtssClientForbidden: return "403";
+        case qtssClientNotFound: return "404";
+        case qtssPreconditionFailed: return "412";
+        default: return "s" + std::to_string(s);
+    }
+}
+template <typename T> static T pod_attr(const Obj* o, uint32_t id, T def) {
+    auto it = o->attrs.find(id);
+    if (it == o->attrs.end() || it->second.empty() || it->second[0].size() != sizeof(T)) return def;
+    T v;
+    memcpy(&v, it->second[0].data(), sizeof(T));
+    return v;
+}
 static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::string& path, const std::string& digit,
                           uint32_t mode, uint32_t transport, const std::string& body = std::string(),
                           Obj** outReq = nullptr) {
@@ -513,6 +639,25 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     set_pod<uint32_t>(req, qtssRTSPReqTransportMode, mode);
     set_pod<uint32_t>(req, qtssRTSPReqTransportType, transport);
     if (!body.empty()) { req->body = body; set_pod<uint32_t>(req, qtssRTSPReqContentLen, (uint32_t)body.size()); }
+    // the server's defaults (RTSPRequestInterface.cpp:200-240): status 200, keep-alive; the action
+    // it sets before the authorization roles (RTSPSession.cpp:604-623): a write for ANNOUNCE, a
+    // record-mode SETUP and any request of a client session the reflector holds as a broadcaster
+    set_pod<uint32_t>(req, qtssRTSPReqStatusCode, qtssSuccessOK);
+    set_pod<bool>(req, qtssRTSPReqRespKeepAlive, true);
+    static uint32_t bcast_attr = 0;
+    if (!bcast_attr) {
+        auto it = g_attr_ids.find(std::to_string(qtssClientSessionObjectType) + ":QTSSReflectorModuleBroadcasterSession");
+        if (it != g_attr_ids.end()) bcast_attr = it->second;
+    }
+    const bool broadcaster = bcast_attr && client && client->attrs.count(bcast_attr) && !client->attrs[bcast_attr].empty();
+    const uint32_t action = (method == qtssAnnounceMethod || (method == qtssSetupMethod && mode == qtssRTPTransportModeRecord) ||
+                             broadcaster) ? qtssActionFlagsWrite : qtssActionFlagsRead;
+    set_pod<uint32_t>(req, qtssRTSPReqAction, action);
+    if (!rtsp->profile) rtsp->profile = new_obj(qtssUserProfileObjectType);
+    set_pod<Obj*>(req, qtssRTSPReqUserProfile, rtsp->profile);
+    set_pod<uint32_t>(req, qtssRTSPReqAuthScheme, rtsp->scheme);
+    const std::string server_realm = "Streaming Server";   // the server's authorization_realm pref
+    set_attr(req, qtssRTSPReqURLRealm, 0, server_realm.data(), (uint32_t)server_realm.size());
     QTSS_RoleParams p;
     memset(&p, 0, sizeof(p));
     p.rtspRequestParams.inRTSPSession = rtsp;
@@ -520,9 +665,32 @@ static QTSS_Error request(Obj* rtsp, Obj* client, uint32_t method, const std::st
     p.rtspRequestParams.inClientSession = client;
     refresh(client);                                   // RTSPSession.cpp:1669
     g_current_client = client;
-    const QTSS_Error e = g_dispatch(QTSS_RTSPPreProcessor_Role, &p);
+    // the routing state, then the authorization state with its defaults (allowed, no user, not
+    // handled): a request left not allowed is answered 401 (Basic / Digest challenge) or 403 by
+    // the server and never reaches the preprocessor (RTSPSession.cpp:725-845)
+    if (g_roles.count(QTSS_RTSPRoute_Role)) (void)g_dispatch(QTSS_RTSPRoute_Role, &p);
+    set_pod<bool>(req, qtssRTSPReqUserAllowed, true);
+    set_pod<bool>(req, qtssRTSPReqUserFound, false);
+    set_pod<bool>(req, qtssRTSPReqAuthHandled, false);
+    if (g_roles.count(QTSS_RTSPAuthorize_Role)) (void)g_dispatch(QTSS_RTSPAuthorize_Role, &p);
+    const bool allowed = pod_attr<bool>(req, qtssRTSPReqUserAllowed, true);
+    QTSS_Error e = QTSS_RequestFailed;
+    if (allowed) e = g_dispatch(QTSS_RTSPPreProcessor_Role, &p);
     g_current_client = nullptr;
-    return e;
+    if (g_req_log) {
+        std::string resp;
+        if (!allowed) resp = rtsp->scheme != qtssAuthNone ? "401 server" : "403 server";
+        else
+            resp = status_str(pod_attr<uint32_t>(req, qtssRTSPReqStatusCode, 0)) +
+                   (req->sent_std ? " std" : req->sent_headers ? " hdr+" + std::to_string(req->written) : " none") +
+                   (pod_attr<bool>(req, qtssRTSPReqRespKeepAlive, true) ? "" : " close");
+        fprintf(g_req_log, "Q %lld %s m%u %s file=%s root=%s auth=%d%d%d realm=%s -> %s\n", (long long)g_now.load(),
+                who(client).c_str(), method, path.c_str(), attr_str(req, qtssRTSPReqFilePath).c_str(),
+                attr_str(req, qtssRTSPReqRootDir).c_str(), (int)allowed, (int)pod_attr<bool>(req, qtssRTSPReqUserFound, false),
+                (int)pod_attr<bool>(req, qtssRTSPReqAuthHandled, false), attr_str(req, qtssRTSPReqURLRealm).c_str(),
+                resp.c_str());
+    }
+    return allowed ? e : QTSS_RequestFailed;
 }
 
 static void* g_so = nullptr;
@@ -556,7 +724,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
     const auto s0 = std::chrono::steady_clock::now();
     for (uint32_t s = 0; s < nsess; s++) {
         const std::string path = "/bench" + std::to_string(s) + ".sdp";      // one component: the stream name
-        rtsp[s] = new_obj(qtssRTSPSessionObjectType);
+        rtsp[s] = new_rtsp();
         client[s] = new_client();
         g_rtsp_of_client[client[s]] = rtsp[s];
         if (request(rtsp[s], client[s], qtssAnnounceMethod, path, "", 0, qtssRTPTransportTypeTCP, sdp) ||
@@ -565,7 +733,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
             request(rtsp[s], client[s], qtssRecordMethod, path, "", qtssRTPTransportModeRecord, qtssRTPTransportTypeTCP))
             { fprintf(stderr, "bench: push setup failed\n"); return 3; }
         for (uint32_t k = 0; k < nsub; k++) {
-            Obj* pr = new_obj(qtssRTSPSessionObjectType);
+            Obj* pr = new_rtsp();
             Obj* pc = new_client();
             g_rtsp_of_client[pc] = pr;
             if (request(pr, pc, qtssSetupMethod, path + "/trackID=1", "1", qtssRTPTransportModePlay, qtssRTPTransportTypeUDP) ||
@@ -683,7 +851,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                     rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
                     const uint32_t s = (uint32_t)(rng % nsess);
                     const std::string path = "/bench" + std::to_string(s) + ".sdp";
-                    Obj* pr = new_obj(qtssRTSPSessionObjectType);
+                    Obj* pr = new_rtsp();
                     Obj* pc = new_client();
                     pc->churn = true;
                     {
@@ -895,7 +1063,10 @@ int main(int argc, char** argv) {
     cbs.addr[kPauseCallback] = (QTSS_CallbackProcPtr)cb_pause;
     cbs.addr[kTeardownCallback] = (QTSS_CallbackProcPtr)cb_teardown;
     cbs.addr[kSetIdleTimerCallback] = (QTSS_CallbackProcPtr)cb_set_idle_timer;
-    cbs.addr[kSendStandardRTSPCallback] = (QTSS_CallbackProcPtr)cb_ok;
+    cbs.addr[kSendStandardRTSPCallback] = (QTSS_CallbackProcPtr)cb_send_standard;
+    cbs.addr[kSendRTSPHeadersCallback] = (QTSS_CallbackProcPtr)cb_send_headers;
+    cbs.addr[kOpenFileObjectCallback] = (QTSS_CallbackProcPtr)cb_open_file;
+    cbs.addr[kCloseFileObjectCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kAppendRTSPHeadersCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kRequestEventCallback] = (QTSS_CallbackProcPtr)cb_ok;
     cbs.addr[kGetAttrInfoByNameCallback] = (QTSS_CallbackProcPtr)cb_attr_info_by_name;
@@ -977,6 +1148,10 @@ int main(int argc, char** argv) {
         g_ka_log = fopen(lp, "w");
         if (!g_ka_log) { perror(lp); return 2; }
     }
+    if (const char* lp = getenv("EDGPU_REQ_LOG")) {
+        g_req_log = fopen(lp, "w");
+        if (!g_req_log) { perror(lp); return 2; }
+    }
     r.p = 4;
     const uint32_t ver = r.get<uint32_t>();
     const uint32_t nsess = r.get<uint32_t>();
@@ -998,20 +1173,25 @@ int main(int argc, char** argv) {
     // leaves (DestroySession, QTSSReflectorModule.cpp:2089-2096)
     std::vector<bool> receiving(nsess, false);
     trace_prefs::Prefs cur = prefs;                            // the prefs of now (PREFS events)
+    // who opens each session's next pusher / player connection (IDENT events; consumed by it)
+    std::vector<Ident> next_pusher(nsess), next_player(nsess);
     // a pusher connection: ANNOUNCE, a record-mode SETUP per track, RECORD (false: refused)
     auto publish = [&](uint32_t s) -> bool {
         const uint32_t tt = (flags[s] & 1) ? qtssRTPTransportTypeUDP : qtssRTPTransportTypeTCP;
-        Obj* rtsp = new_obj(qtssRTSPSessionObjectType);
+        const Ident id = next_pusher[s];
+        next_pusher[s] = Ident();
+        Obj* rtsp = new_rtsp(id);
+        const std::string& path = id.path.empty() ? paths[s] : id.path;
         Obj* client = new_client();
         client->push_s = (int)s;
         client->push_k = (int)pub_count[s]++;
         g_rtsp_of_client[client] = rtsp;
         // refused with enable_broadcast_announce off (QRM:900): the pusher gives up, no SETUP
-        if (request(rtsp, client, qtssAnnounceMethod, paths[s], "", 0, tt, sdps[s])) { client->closed = true; return false; }
+        if (request(rtsp, client, qtssAnnounceMethod, path, "", 0, tt, sdps[s])) { client->closed = true; return false; }
         std::vector<uint16_t> ports;
         for (uint32_t t = 0; t < ntracks[s]; t++) {
             Obj* req = nullptr;
-            if (request(rtsp, client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(t + 1),
+            if (request(rtsp, client, qtssSetupMethod, path + "/trackID=" + std::to_string(t + 1),
                         std::to_string(t + 1), qtssRTPTransportModeRecord, tt, std::string(), &req)) {
                 QTSS_RoleParams p;                         // refused: the connection closes
                 memset(&p, 0, sizeof(p));
@@ -1029,7 +1209,7 @@ int main(int argc, char** argv) {
                 g_rtcp_owner[(uint16_t)(port + 1)] = std::make_pair(s, (uint16_t)t);
             }
         }
-        if (request(rtsp, client, qtssRecordMethod, paths[s], "", qtssRTPTransportModeRecord, tt))
+        if (request(rtsp, client, qtssRecordMethod, path, "", qtssRTPTransportModeRecord, tt))
             { fprintf(stderr, "RECORD failed\n"); exit(3); }
         pushers[s].push_back(PushConn{rtsp, client});
         server_port[s] = ports;
@@ -1127,7 +1307,10 @@ int main(int argc, char** argv) {
         } else if (type == 2) {                                  // JOIN -> SETUP x tracks + PLAY
             const uint32_t s = r.get<uint32_t>(), sub = r.get<uint32_t>();
             const uint8_t tr = r.get<uint8_t>(), ua = r.get<uint8_t>();
-            Player pl{sub, s, new_obj(qtssRTSPSessionObjectType), new_client(), {}};
+            const Ident id = next_player[s];
+            next_player[s] = Ident();
+            const std::string& ppath = id.path.empty() ? paths[s] : id.path;
+            Player pl{sub, s, new_rtsp(id), new_client(), {}};
             pl.client->player_sub = (int)sub;
             g_rtsp_of_client[pl.client] = pl.rtsp;
             const std::string agent = (ua & 1) ? "vlc/3.0.8 LibVLC/3.0.8" : "EasyPlayer/1.0";   // case-sensitive match
@@ -1136,9 +1319,12 @@ int main(int argc, char** argv) {
             const size_t before = g_streams.size();
             bool setup_ok = true;
             for (uint32_t x = 0; x < ntracks[s] && setup_ok; x++)
-                setup_ok = request(pl.rtsp, pl.client, qtssSetupMethod, paths[s] + "/trackID=" + std::to_string(x + 1),
+                setup_ok = request(pl.rtsp, pl.client, qtssSetupMethod, ppath + "/trackID=" + std::to_string(x + 1),
                                    std::to_string(x + 1), qtssRTPTransportModePlay, tt) == QTSS_NoErr;
-            if (setup_ok != alive[s]) {
+            // a player from an IDENT (another path, another client) or with broadcasts disallowed may
+            // be refused on a live session: the request log carries the module's answer
+            const bool may_refuse = id.set || !cur.flag("allow_broadcasts");
+            if (setup_ok != alive[s] && !(may_refuse && alive[s])) {
                 fprintf(stderr, "player SETUP %s on a session that %s\n", setup_ok ? "succeeded" : "failed",
                         alive[s] ? "exists" : "has ended");
                 return 3;
@@ -1148,7 +1334,7 @@ int main(int argc, char** argv) {
                 g_streams[k]->sub = sub; g_streams[k]->session = s; g_streams[k]->track = (uint32_t)(k - before);
                 pl.streams.push_back(g_streams[k]);
             }
-            (void)request(pl.rtsp, pl.client, qtssPlayMethod, paths[s], "", qtssRTPTransportModePlay, tt);
+            (void)request(pl.rtsp, pl.client, qtssPlayMethod, ppath, "", qtssRTPTransportModePlay, tt);
             if (!pl.client->played) {                           // deferred RTP-Info PLAY: dropped
                 close_client(pl.client);
                 continue;
@@ -1214,15 +1400,32 @@ int main(int argc, char** argv) {
             QTSS_RoleParams p;
             memset(&p, 0, sizeof(p));
             if (g_dispatch(QTSS_RereadPrefs_Role, &p) != QTSS_NoErr) { fprintf(stderr, "RereadPrefs failed\n"); return 3; }
+        } else if (type == 10) {                                 // IDENT: who opens the next connection
+            const uint32_t s = r.get<uint32_t>();
+            const uint8_t role = r.get<uint8_t>();
+            Ident id;
+            id.addr = r.get<uint32_t>();
+            id.scheme = r.get<uint8_t>();
+            std::string* txt[4] = {&id.path, &id.user, &id.groups, &id.realm};
+            for (std::string* x : txt) {
+                const uint16_t n = r.get<uint16_t>();
+                x->assign((const char*)&r.d[r.p], n);
+                r.p += n;
+            }
+            id.set = true;
+            (role == 0 ? next_pusher : next_player)[s] = id;
         } else if (type == 8) {                                  // PUBLISH -> a new pusher connection
             const uint32_t s = r.get<uint32_t>();
             // refused when ANNOUNCE is disabled, and on tracks another pusher set up unless
             // allow_duplicate_broadcasts (QRM:900, 1682); the module must agree
             const bool want = cur.flag("enable_broadcast_announce") && (!receiving[s] || cur.flag("allow_duplicate_broadcasts"));
+            // an IDENT's pusher, or any with broadcasts disallowed, is the RTSPAuthorize / AllowBroadcast
+            // decision's to take: the request log carries it
+            const bool decided = next_pusher[s].set || !cur.flag("allow_broadcasts") || cur.flag("authenticate_local_broadcast");
             const std::vector<uint16_t> keep = server_port[s];
             const bool got = publish(s);
             if (!got) server_port[s] = keep;
-            if (got != want) { fprintf(stderr, "PUBLISH of session %u %s\n", s, got ? "accepted" : "refused"); return 3; }
+            if (got != want && !(decided && !got)) { fprintf(stderr, "PUBLISH of session %u %s\n", s, got ? "accepted" : "refused"); return 3; }
         } else {
             fprintf(stderr, "bad event %u\n", type);
             return 3;

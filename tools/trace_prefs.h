@@ -24,8 +24,18 @@ inline const std::vector<std::pair<std::string, std::string>>& defaults() {
         {"enable_broadcast_announce", "true"}, {"enable_broadcast_push", "true"},
         {"allow_duplicate_broadcasts", "false"}, {"timeout_broadcaster_session_secs", "30"},
         {"reflector_use_in_packet_receive_time", "false"}, {"reflector_in_packet_max_receive_sec", "60"},
+        {"allow_broadcasts", "true"}, {"authenticate_local_broadcast", "false"}, {"BroadcasterGroup", "broadcaster"},
+        {"ip_allow_list", "127.0.0.*"}, {"redirect_broadcast_keyword", ""}, {"redirect_broadcasts_dir", ""},
+        {"allow_non_sdp_urls", "true"},
     };
     return d;
+}
+
+// the module prefs whose values are strings (easydarwin.xml CharArray prefs); ip_allow_list is a
+// LIST-PREF: its comma-separated entries are its values
+inline bool is_list(const std::string& k) { return k == "ip_allow_list"; }
+inline bool is_string(const std::string& k) {
+    return is_list(k) || k == "BroadcasterGroup" || k == "redirect_broadcast_keyword" || k == "redirect_broadcasts_dir";
 }
 
 // the user agent of a JOIN's player (trace.py USER_AGENTS, by ua_flags bit 0)
