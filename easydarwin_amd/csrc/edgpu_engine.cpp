@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -47,6 +48,7 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
 hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hipStream_t st);
+hipError_t launch_stall(uint64_t ticks, hipStream_t st);
 int fanout_chunk(int variant);
 int fanout_default(bool patching);
 bool fanout_rewrites(int variant);
@@ -57,9 +59,13 @@ using namespace edgpu;
 
 static thread_local std::string g_err;
 static int fail(int code, const std::string& msg) { g_err = msg; return code; }
+// hipErrorLaunchTimeOut from a bounded wait is the GPU watchdog's (wsync): EDGPU_TIMEOUT
 #define HIP_CHECK(expr)                                                                   \
     do {                                                                                  \
         hipError_t _e = (expr);                                                           \
+        if (_e == hipErrorLaunchTimeOut)                                                  \
+            return fail(EDGPU_TIMEOUT, std::string(#expr) + ": GPU watchdog: the device did not finish " \
+                                       "the context's work within watchdog_ms");          \
         if (_e != hipSuccess)                                                             \
             return fail(EDGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
@@ -121,13 +127,25 @@ struct SourceHost {
 // size (ring sizes are powers of two: meta rings packets x 36 B, byte rings 2^k B), so ring growth,
 // session add / remove and session churn allocate and free no device memory once the pool holds
 // enough (hipMalloc + hipFree of a ring cost ~0.2 ms: a burst of 1000 growths stalled a tick for
-// a quarter of a second).  Memory stays with the pool until the context is destroyed.
+// a quarter of a second).  Chunk memory stays with the pool until the context is destroyed; a
+// ring of kOwn bytes or more has an allocation of its own, freed when the ring is returned (a
+// grown sender's old big rings and a removed session's would otherwise sit on the free lists).
+// A failed hipMalloc leaves HIP's last error set; it is cleared here, so the next kernel launch's
+// check does not report it.
 struct RingPool {
     static constexpr size_t kChunk = 512ull << 20, kAlign = 4096, kOwn = 128ull << 20;
-    std::vector<void*> chunks;                     // every device allocation (freed at destroy)
+    std::vector<void*> chunks;                     // every chunk allocation (freed at destroy)
+    std::map<void*, size_t> own;                   // the rings with an allocation of their own
     std::map<size_t, std::vector<void*>> freed;    // by (aligned) size
     char* cur = nullptr;
-    size_t left = 0, held = 0;
+    size_t left = 0, held = 0;                     // held: device bytes the pool has allocated now
+    // EDGPU_RING_POOL_LIMIT=<bytes> (tests): allocations past it fail as an exhausted device would
+    size_t limit = getenv("EDGPU_RING_POOL_LIMIT") ? strtoull(getenv("EDGPU_RING_POOL_LIMIT"), nullptr, 0) : 0;
+    template <typename T>
+    hipError_t alloc(T** p, size_t n) {
+        if (limit && held + n > limit) return hipErrorOutOfMemory;
+        return dmalloc(p, n);
+    }
     static size_t align(size_t b) { return (b + kAlign - 1) & ~(kAlign - 1); }
     hipError_t get(void** out, size_t bytes) {
         bytes = align(bytes);
@@ -139,19 +157,19 @@ struct RingPool {
         }
         void* p = nullptr;
         if (bytes >= kOwn) {                       // a big ring: its own allocation
-            hipError_t e = dmalloc(&p, bytes);
-            if (e != hipSuccess) return e;
-            chunks.push_back(p);
+            hipError_t e = alloc(&p, bytes);
+            if (e != hipSuccess) { (void)hipGetLastError(); return e; }
+            own[p] = bytes;
             held += bytes;
             *out = p;
             return hipSuccess;
         }
         if (bytes > left) {
-            hipError_t e = dmalloc(&p, kChunk);
+            hipError_t e = alloc(&p, kChunk);
             if (e != hipSuccess) {                 // no room for a whole chunk: this ring alone
                 (void)hipGetLastError();
-                if ((e = dmalloc(&p, bytes)) != hipSuccess) return e;
-                chunks.push_back(p);
+                if ((e = alloc(&p, bytes)) != hipSuccess) { (void)hipGetLastError(); return e; }
+                own[p] = bytes;
                 held += bytes;
                 *out = p;
                 return hipSuccess;
@@ -166,7 +184,17 @@ struct RingPool {
         left -= bytes;
         return poison(*out, bytes);
     }
-    void put(void* p, size_t bytes) { if (p) freed[align(bytes)].push_back(p); }
+    void put(void* p, size_t bytes) {
+        if (!p) return;
+        auto o = own.find(p);
+        if (o != own.end()) {                      // its own allocation: back to HIP
+            (void)hipFree(p);
+            held -= o->second;
+            own.erase(o);
+            return;
+        }
+        freed[align(bytes)].push_back(p);
+    }
     static hipError_t poison(void* p, size_t n) {  // EDGPU_POISON: as a fresh allocation
         if (!poison_on()) return hipSuccess;
         hipError_t e = hipMemset(p, 0xA5, n);
@@ -174,7 +202,8 @@ struct RingPool {
     }
     void release() {
         for (void* p : chunks) (void)hipFree(p);
-        chunks.clear(); freed.clear(); cur = nullptr; left = held = 0;
+        for (auto& o : own) (void)hipFree(o.first);
+        chunks.clear(); own.clear(); freed.clear(); cur = nullptr; left = held = 0;
     }
 };
 
@@ -383,10 +412,70 @@ struct edgpu_ctx {
     uint32_t grow_pending = 0;
     uint64_t grow_seen_launch = 0;
     uint64_t ring_grows = 0;
-    uint64_t grow_deferred = 0;     // growth requests left to a later call (the per-call time budget)
+    uint64_t grow_deferred = 0;     // growth requests left to a later call (the per-call budget)
+    uint64_t grow_failures = 0;     // growths the device memory could not hold (best effort: skipped)
+    // per sender, the ring sizes whose allocation failed (and the meta ring they were asked for):
+    // requests for those or larger are not retried until the sender's rings change
+    struct GrowFail { uint64_t meta, pk, bytes; };
+    std::map<uint32_t, GrowFail> grow_failed;
     RingPool rings;                 // every sender's meta and byte rings
+    // GPU watchdog (wsync): the event a bounded wait polls; wedged while the work it timed out on runs
+    hipEvent_t wd_ev = nullptr;
+    bool wedged = false;
+    uint64_t watchdog_timeouts = 0;
     uint64_t ring_bytes = 0;                    // device bytes of the live senders' rings
 };
+
+// ---- GPU watchdog (per-stream error isolation and a GPU watchdog) ----
+// Every wait of the engine on the device (stream and event synchronisation, the readbacks) is
+// bounded by edgpu_config.watchdog_ms: an event is recorded behind the work and polled against
+// the deadline.  When it passes, the wait returns hipErrorLaunchTimeOut (HIP_CHECK: EDGPU_TIMEOUT)
+// and the context is wedged on that event: every call that would enqueue work or wait returns
+// EDGPU_TIMEOUT at once, enqueueing nothing, until the event completes -- then the context is
+// itself again (the work it timed out on has finished; its results were never read).  The host
+// decides what a wedge means (the QTSS module tears the players down and refuses SETUPs until a
+// tick succeeds).  edgpu_ctx_destroy waits without a bound.  watchdog_ms = EDGPU_FALSE: unbounded
+// waits (hipStreamSynchronize), as before.
+static hipError_t wsync_event(edgpu_ctx* x, hipEvent_t ev) {
+    if (!x->cfg.watchdog_ms) return hipEventSynchronize(ev);
+    using Clk = std::chrono::steady_clock;
+    const Clk::time_point t0 = Clk::now(), deadline = t0 + std::chrono::milliseconds(x->cfg.watchdog_ms);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        const Clk::time_point now = Clk::now();
+        if (now >= deadline) return hipErrorLaunchTimeOut;
+        // a tick's waits are short: spin (yielding) for the first 100 us, then poll every 20 us
+        if (now - t0 < std::chrono::microseconds(100)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+static hipError_t wsync(edgpu_ctx* x, hipStream_t st) {
+    if (x->wedged) {
+        if (hipEventQuery(x->wd_ev) == hipErrorNotReady) return hipErrorLaunchTimeOut;
+        x->wedged = false;
+    }
+    if (!x->cfg.watchdog_ms) return hipStreamSynchronize(st);
+    hipError_t e = hipEventRecord(x->wd_ev, st);
+    if (e != hipSuccess) return e;
+    e = wsync_event(x, x->wd_ev);
+    if (e == hipErrorLaunchTimeOut) { x->wedged = true; x->watchdog_timeouts++; }
+    return e;
+}
+// The device entry of every call: its device current, and no wedge left (see above)
+static int device_enter(edgpu_ctx* x) {
+    if (hipSetDevice(x->device) != hipSuccess) return fail(EDGPU_NO_DEVICE, "hipSetDevice failed");
+    if (x->wedged) {
+        if (hipEventQuery(x->wd_ev) == hipErrorNotReady)
+            return fail(EDGPU_TIMEOUT, "GPU watchdog: the work the context timed out on is still running");
+        x->wedged = false;
+    }
+    return EDGPU_OK;
+}
+#define DEVICE_ENTER(x)                                   \
+    do {                                                  \
+        if (int _r = device_enter(x)) return _r;          \
+    } while (0)
 
 static bool live_session(const edgpu_ctx* x, uint32_t s) { return s < x->sessions.size() && x->sessions[s].alive; }
 
@@ -442,6 +531,8 @@ static void fill_defaults(edgpu_config& c) {
                                               c.reflector_use_in_packet_receive_time != EDGPU_FALSE) ? 1u : 0u;
     if (!c.reflector_in_packet_max_receive_sec) c.reflector_in_packet_max_receive_sec = 60;
     else if (c.reflector_in_packet_max_receive_sec == EDGPU_FALSE) c.reflector_in_packet_max_receive_sec = 0;
+    if (!c.watchdog_ms) c.watchdog_ms = 10000;
+    else if (c.watchdog_ms == EDGPU_FALSE) c.watchdog_ms = 0;   // unbounded waits
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -472,6 +563,7 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (hipSetDevice(c.device) != hipSuccess) { delete x; return fail(EDGPU_NO_DEVICE, "hipSetDevice failed"); }
     auto bad = [&](const char* what) { edgpu_ctx_destroy(x); return fail(EDGPU_OUT_OF_MEMORY, what); };
     if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return bad("stream");
+    if (hipEventCreateWithFlags(&x->wd_ev, hipEventDisableTiming) != hipSuccess) return bad("watchdog event");
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (hipEventCreate(&e) != hipSuccess) return bad("event");
     if (dmalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
     if (dmalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
@@ -559,15 +651,16 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
     if (x->aux) (void)hipStreamDestroy(x->aux);
     if (x->stream) (void)hipStreamDestroy(x->stream);
+    if (x->wd_ev) (void)hipEventDestroy(x->wd_ev);
     delete x;
     return EDGPU_OK;
 }
 
 // Waits for everything the context has enqueued (both streams with overlap_ticks).
 static hipError_t sync_all(edgpu_ctx* x) {
-    hipError_t e = hipStreamSynchronize(x->stream);
-    if (e == hipSuccess && x->copy) e = hipStreamSynchronize(x->copy);
-    if (e == hipSuccess && x->aux) e = hipStreamSynchronize(x->aux);
+    hipError_t e = wsync(x, x->stream);
+    if (e == hipSuccess && x->copy) e = wsync(x, x->copy);
+    if (e == hipSuccess && x->aux) e = wsync(x, x->aux);
     return e;
 }
 
@@ -609,7 +702,7 @@ struct Readback {
         return a.type == hipMemoryTypeHost;
     }
     hipError_t run() {
-        hipError_t e = hipStreamSynchronize(st);
+        hipError_t e = wsync(x, st);
         if (e != hipSuccess) return e;
         for (const Item& it : staged) memcpy(it.dst, x->h_stage + it.off, it.bytes);
         staged.clear();
@@ -620,7 +713,7 @@ struct Readback {
 
 // The tick totals, after every stream of the context has drained.
 static int read_totals(edgpu_ctx* x, TickTotals* t) {
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));
     Readback rb(x);
     HIP_CHECK(rb.add(t, x->d_totals, sizeof(*t)));
@@ -687,7 +780,7 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
     D.word_mask = (uint32_t)(new_by / 16 - 1);
     D.floor = std::max(D.floor, tail);
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sender, &D, sizeof(D), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     if (nmeta != meta) x->rings.put(meta, old_pk * (sizeof(PktMeta) + sizeof(uint32_t)));
     if (nring != ring) x->rings.put(ring, old_by);
     x->snd_meta[sender] = nmeta;
@@ -705,7 +798,12 @@ static int grow_sender(edgpu_ctx* x, uint32_t sender, uint64_t want_pk, uint64_t
 // of what the reference would retain gets that ring grown to the requested size (grow_sender), its
 // floor raised to the tail the plan measured.  A request made before the sender's head moved on (a
 // replica's image apply in between) is dropped; the next plan makes it again.
-static constexpr double kGrowBudgetUs = 4000;   // ring growth per call (grow_rings)
+// Ring growth per call (grow_rings), counted -- not timed, so which senders grow in which call
+// follows from the trace alone: at most this many senders and this many new ring bytes (at least
+// one sender).  A C2 burst (1024 video senders passing half of their 8-MiB rings within a tick or
+// two) then grows in four calls of ~4 ms (~17 us per 16-MiB ring moved).
+static constexpr size_t kGrowSendersPerCall = 256;
+static constexpr uint64_t kGrowBytesPerCall = 8ull << 30;
 static int grow_rings(edgpu_ctx* x) {
     uint32_t n = x->grow_pending;
     x->grow_pending = 0;
@@ -740,19 +838,38 @@ static int grow_rings(edgpu_ctx* x) {
     }
     const double read_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
     // A burst of requests (every C2 video sender passes half its ring within a tick or two) is spread
-    // over ticks: each call grows senders for at most kGrowBudgetUs (at least one); the next plan
-    // re-measures the rest and asks again -- a request means the ring still has half its capacity left.
+    // over ticks: each call grows at most kGrowSendersPerCall senders / kGrowBytesPerCall new bytes;
+    // the next plan re-measures the rest and asks again -- a request means the ring still has half
+    // its capacity left.  Growth is best effort: a ring the device memory cannot hold is skipped and
+    // counted (grow_failures), the sender keeps its rings (a packet that later falls out of them
+    // marks its session in edgpu_stream_errors, as past the configured bounds), the call goes on,
+    // and the ingest that follows is not refused for it.
     const auto t0 = std::chrono::steady_clock::now();
-    size_t k = 0;
+    size_t k = 0, grown_n = 0;
+    uint64_t new_bytes = 0;
     for (; k < req.size(); k++) {
-        if (k && std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kGrowBudgetUs) {
+        const GrowReq& R = req[k];
+        const uint64_t want_pk = 1ull << R.pk_log2, want_by = 1ull << R.bytes_log2;
+        auto f = x->grow_failed.find(R.sender);
+        if (f != x->grow_failed.end() && cur[k].meta == f->second.meta && want_pk >= f->second.pk && want_by >= f->second.bytes)
+            continue;                                  // failed before at this size: not retried
+        if (grown_n && (grown_n >= kGrowSendersPerCall || new_bytes >= kGrowBytesPerCall)) {
             x->grow_deferred += req.size() - k;
             break;
         }
-        const GrowReq& R = req[k];
         bool grown = false;
-        if (int r = grow_sender(x, R.sender, 1ull << R.pk_log2, 1ull << R.bytes_log2, R.tail, &R.head, &grown, &cur[k]))
-            return r;
+        const int r = grow_sender(x, R.sender, want_pk, want_by, R.tail, &R.head, &grown, &cur[k]);
+        if (r == EDGPU_OUT_OF_MEMORY) {
+            x->grow_failures++;
+            x->grow_failed[R.sender] = edgpu_ctx::GrowFail{cur[k].meta, want_pk, want_by};
+            continue;
+        }
+        if (r) return r;
+        if (grown) {
+            grown_n++;
+            new_bytes += want_pk * (sizeof(PktMeta) + sizeof(uint32_t)) + want_by;
+            x->grow_failed.erase(R.sender);
+        }
     }
     static const bool dbg = getenv("EDGPU_DEBUG_GROW") != nullptr;
     if (dbg)
@@ -849,7 +966,7 @@ static SenderDev dead_sender(const edgpu_ctx* x, uint32_t sid) {
 
 int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_push, uint32_t* out_session) {
     if (!x || !sdp) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     std::vector<TrackHost> tracks = parse_sdp(sdp, sdp_len);
     if (tracks.empty() || tracks.size() > kMaxTracks)
         return fail(EDGPU_BAD_ARGUMENT, "SDP must describe 1..16 tracks");
@@ -942,7 +1059,7 @@ int edgpu_session_add(edgpu_ctx* x, const char* sdp, uint32_t sdp_len, int udp_p
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + sid, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     if (reuse) {
         x->sessions[sid] = sh;
     } else {
@@ -988,12 +1105,12 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     if (!sh.subs.empty() && !(flags & EDGPU_SESSION_KILL_OUTPUTS))
         return fail(EDGPU_ERR, "session still has outputs (the reference keeps a ReflectorSession while outputs "
                                "hold references to it; pass EDGPU_SESSION_KILL_OUTPUTS to tear them down)");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     // TearDownAllOutputs: every attached subscriber goes with it
     while (!sh.subs.empty()) { int r = detach_subscriber(x, sh.subs.back()); if (r) return r; }
     // the rings may still be read by a fan-out copy in flight (overlap_ticks) or a pinned batch
     HIP_CHECK(sync_all(x));
-    if (x->h2d) HIP_CHECK(hipStreamSynchronize(x->h2d));
+    if (x->h2d) HIP_CHECK(wsync(x, x->h2d));
     const uint32_t nsnd = 2 * sh.ntracks;
     std::vector<SenderDev> old(nsnd), snd(nsnd, dead_sender(x, session));
     {
@@ -1012,6 +1129,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
         x->rings.put(x->snd_meta[gs], ((uint64_t)old[i].pk_mask + 1) * (sizeof(PktMeta) + sizeof(uint32_t)));
         x->rings.put(x->snd_ring[gs], ((uint64_t)old[i].word_mask + 1) * 16);
         x->snd_meta[gs] = x->snd_ring[gs] = nullptr;
+        x->grow_failed.erase(gs);
     }
     std::vector<StreamDev> str(sh.ntracks);
     for (auto& st : str) st.packet_count = 0;
@@ -1019,7 +1137,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     HIP_CHECK(hipMemcpyAsync(x->d_senders.ptr + sh.first_sender, snd.data(), nsnd * sizeof(SenderDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_streams.ptr + sh.first_stream, str.data(), sh.ntracks * sizeof(StreamDev), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_sessions.ptr + session, &sd, sizeof(sd), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     sh.alive = false;
     sh.eyes = 0;
     sh.slots.clear();                            // (remote places too)
@@ -1034,11 +1152,11 @@ int edgpu_session_ssrc_prefs(edgpu_ctx* x, uint32_t session, uint32_t use_one_SS
                              uint32_t timeout_stream_SSRC_secs) {
     if (!x || !live_session(x, session)) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     const uint32_t v[2] = {use_one_SSRC_per_stream ? 1u : 0u, timeout_stream_SSRC_secs};
     // stream-ordered before the next ingest, which reads them
     HIP_CHECK(hipMemcpyAsync(&x->d_sessions.ptr[session].ssrc_filter, v, sizeof(v), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));   // `v` is on the stack
+    HIP_CHECK(wsync(x, x->stream));   // `v` is on the stack
     return EDGPU_OK;
 }
 
@@ -1115,7 +1233,7 @@ static int upload_subs(edgpu_ctx* x, const std::vector<std::pair<uint32_t, SubDe
         while (j < v.size() && v[j].first == v[i].first + (j - i)) run.push_back(v[j++].second);
         HIP_CHECK(hipMemcpyAsync(x->d_subs.ptr + v[i].first, run.data(), run.size() * sizeof(SubDev),
                                  hipMemcpyHostToDevice, x->stream));
-        HIP_CHECK(hipStreamSynchronize(x->stream));     // `run` is reused
+        HIP_CHECK(wsync(x, x->stream));     // `run` is reused
         i = j;
     }
     return EDGPU_OK;
@@ -1148,7 +1266,7 @@ static int first_packet_info(edgpu_ctx* x, const SessionHost& sh, int64_t now_ms
     HIP_CHECK(hipMemcpyAsync(x->d_fpi_q, x->h_fpi_q, q.size() * sizeof(FirstInfoQuery), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(launch_first_packet_info(x->d_fpi_q, x->d_fpi_r, x->d_senders.ptr, sh.ntracks, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->h_fpi_r, x->d_fpi_r, q.size() * sizeof(FirstInfoResult), hipMemcpyDeviceToHost, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     std::vector<FirstInfoResult> r(x->h_fpi_r, x->h_fpi_r + sh.ntracks);
     if (getenv("EDGPU_DEBUG_PLAY")) {                    // debugging: the PLAY's inputs and results
         for (uint32_t t = 0; t < sh.ntracks; t++) {
@@ -1183,7 +1301,7 @@ int edgpu_subscriber_play(edgpu_ctx* x, uint32_t session, int transport, uint32_
         return fail(EDGPU_BAD_ARGUMENT, "bad transport");
     if (flags & ~EDGPU_PLAY_RTP_INFO) return fail(EDGPU_BAD_ARGUMENT, "bad play flags");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     const SessionHost& sh = x->sessions[session];
     std::vector<uint16_t> first_seq(sh.ntracks, 0);
     if (flags & EDGPU_PLAY_RTP_INFO) {
@@ -1207,7 +1325,7 @@ int edgpu_subscribers_add(edgpu_ctx* x, uint32_t n, const uint32_t* sessions, co
             return fail(EDGPU_BAD_ARGUMENT, "bad transport");
     }
     if (!n) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     std::vector<std::pair<uint32_t, SubDev>> v;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t h = append_subscriber(x, sessions[i], transports[i], 0, nullptr, v);
@@ -1226,10 +1344,10 @@ int edgpu_subscriber_slot(edgpu_ctx* x, uint32_t handle, int32_t* out_slot) {
 int edgpu_subscriber_remove(edgpu_ctx* x, uint32_t handle) {
     if (!x || handle >= x->subscribers.size() || !x->subscribers[handle].active)
         return fail(EDGPU_BAD_ARGUMENT, "bad subscriber handle");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     const int r = detach_subscriber(x, handle);
     if (r) return r;
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     return EDGPU_OK;
 }
 
@@ -1243,7 +1361,7 @@ int edgpu_subscriber_rewrite(edgpu_ctx* x, uint32_t handle, uint32_t track, cons
     if (on && !fanout_rewrites(x->fanout_variant))
         return fail(EDGPU_ERR, "the selected fan-out variant (EDGPU_FANOUT) has no rewrite stage");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     for (uint32_t k = 0; k < 2; k++) {
         const uint32_t q = s.first_sub + 2 * track + k;
         uint32_t v[3] = {0, 0, 0};
@@ -1257,7 +1375,7 @@ int edgpu_subscriber_rewrite(edgpu_ctx* x, uint32_t handle, uint32_t track, cons
                                  hipMemcpyHostToDevice, x->stream));
         if (on != (bool)x->sub_rw[q]) { x->sub_rw[q] = on; x->n_rw += on ? 1 : -1; }
     }
-    HIP_CHECK(hipStreamSynchronize(x->stream));     // `v` is stack memory
+    HIP_CHECK(wsync(x, x->stream));     // `v` is stack memory
     return EDGPU_OK;
 }
 
@@ -1456,7 +1574,7 @@ static int rebuild_index(edgpu_ctx* x) {
     HIP_CHECK(x->d_blk_maxb.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_maxc.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_work.reserve(std::max<uint64_t>(x->work_cap_needed, 1), x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     x->index_dirty = false;
     return EDGPU_OK;
 }
@@ -1514,7 +1632,7 @@ static int validate_host_batch(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_
 
 int edgpu_host_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     *out = nullptr;
     if (hipHostMalloc(out, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess)
         return fail(EDGPU_OUT_OF_MEMORY, "pinned host buffer");
@@ -1524,14 +1642,14 @@ int edgpu_host_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
 int edgpu_host_free(edgpu_ctx* x, void* p) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!p) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     // any thread may free (a pusher growing its blob): the copy stream is created under pin_mu
     hipStream_t h2d;
     {
         std::lock_guard<std::mutex> g(x->pin_mu);
         h2d = x->h2d;
     }
-    if (h2d) HIP_CHECK(hipStreamSynchronize(h2d));
+    if (h2d) HIP_CHECK(wsync(x, h2d));
     HIP_CHECK(hipHostFree(p));
     return EDGPU_OK;
 }
@@ -1540,7 +1658,7 @@ int edgpu_host_free(edgpu_ctx* x, void* p) {
 // entry point first waits for the outstanding pinned copies (normally long done).
 static int wait_pinned_copies(edgpu_ctx* x) {
     for (auto& st : x->pin)
-        if (st.issued) HIP_CHECK(hipEventSynchronize(st.copied));
+        if (st.issued) HIP_CHECK(wsync_event(x, st.copied));
     return EDGPU_OK;
 }
 
@@ -1572,7 +1690,7 @@ static int stage_pinned(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, co
     // the previous batch's copy must be done before its host buffers are handed back (contract),
     // and this set's previous batch must have been read by its ingest + keyframe index
     edgpu_ctx::PinStage& P = x->pin[k ^ 1];
-    if (P.issued) HIP_CHECK(hipEventSynchronize(P.copied));
+    if (P.issued) HIP_CHECK(wsync_event(x, P.copied));
     if (S.issued && S.prestaged == 0) HIP_CHECK(hipStreamWaitEvent(x->h2d, S.consumed, 0));   // (a prestage waited)
     HIP_CHECK(hipMemcpyAsync(S.desc, desc, (size_t)n * sizeof(edgpu_pkt_desc), hipMemcpyHostToDevice, x->h2d));
     HIP_CHECK(hipMemcpyAsync(S.seg, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, x->h2d));
@@ -1602,7 +1720,7 @@ int edgpu_ingest_prestage(edgpu_ctx* x, const uint8_t* blob, uint64_t offset, ui
     edgpu_ctx::PinStage& N = x->pin[x->pin_next];
     if (offset != N.prestaged) return fail(EDGPU_BAD_ARGUMENT, "a prestaged range must extend the staged prefix");
     if (offset + bytes > x->cfg.max_batch_bytes) return fail(EDGPU_BAD_ARGUMENT, "prestaged bytes exceed max_batch_bytes");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     edgpu_ctx::PinStage* Sp = nullptr;
     { int r = pin_set(x, &Sp); if (r) return r; }
     edgpu_ctx::PinStage& S = *Sp;
@@ -1628,7 +1746,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         return owed ? owed : fail(EDGPU_BAD_ARGUMENT, "batch exceeds configured capacity");
     }
     if (n && (!desc || !seg_off || !seg_sess || !blob)) return fail(EDGPU_BAD_ARGUMENT, "NULL batch array");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     const edgpu_pkt_desc* dd = desc;
     const uint32_t* ds = seg_off;
@@ -1662,7 +1780,7 @@ int edgpu_ingest(edgpu_ctx* x, const edgpu_pkt_desc* desc, uint32_t n, const uin
         HIP_CHECK(hipMemcpyAsync(x->d_blob, blob, blob_bytes, hipMemcpyHostToDevice, x->stream));
         // The caller's buffers are pageable host memory it may free or reuse as soon as this
         // returns, and an async copy from pageable memory may still be reading them: wait.
-        HIP_CHECK(hipStreamSynchronize(x->stream));
+        HIP_CHECK(wsync(x, x->stream));
         dd = x->d_desc; ds = x->d_seg; dss = x->d_seg_sess; db = x->d_blob;
     } else if (where != EDGPU_PTR_DEVICE) {
         return fail(EDGPU_BAD_ARGUMENT, "bad pointer location");
@@ -1680,7 +1798,7 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (int r = owed_pass(x, "edgpu_ingest_interleaved")) return r;
     if (!n) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     { int r = wait_pinned_copies(x); if (r) return r; }
     x->carry_len.resize(x->sessions.size(), 0);
@@ -1795,7 +1913,7 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n)
     const uint32_t nsub = x->tick_nsubs;             // rows of the tick reported on
     for (uint32_t i = 0; i < n; i++)
         if (reports[i].substream >= nsub) return fail(EDGPU_BAD_ARGUMENT, "bad sub-stream index");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(x->d_blocked.reserve(n, x->stream));
     edgpu_blocked* d = x->d_blocked.ptr;
     HIP_CHECK(hipMemcpyAsync(d, reports, n * sizeof(edgpu_blocked), hipMemcpyHostToDevice, x->stream));
@@ -1806,14 +1924,14 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* reports, uint32_t n)
     p.relocate_ms = x->cfg.rtp_reflector_threshold_msec;
     p.totals = x->d_totals;
     HIP_CHECK(launch_blocked(p, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));   // `reports` is the caller's host memory
+    HIP_CHECK(wsync(x, x->stream));   // `reports` is the caller's host memory
     return EDGPU_OK;
 }
 
 int edgpu_keyframe_index(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!x->pending) return fail(EDGPU_ERR, "no ingested batch pending a keyframe index");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     KeyframeParams p;
     p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.totals = x->d_totals;
@@ -1920,10 +2038,10 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (int r = owed_pass(x, "edgpu_fanout")) return r;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     if (x->overlap) {
         // the index rebuild may reallocate tables the in-flight copy reads
-        if (x->index_dirty) HIP_CHECK(hipStreamSynchronize(x->copy));
+        if (x->index_dirty) HIP_CHECK(wsync(x, x->copy));
         // this tick's plan rewrites the work list and sub-stream records the previous copy reads
         HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
         x->cur ^= 1;
@@ -1959,7 +2077,7 @@ int edgpu_fanout_next(edgpu_ctx* x, edgpu_fanout_result* out, uint32_t* launched
     if (!x || !launched) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     *launched = 0;
     if (x->fanout_launches == 0) return fail(EDGPU_ERR, "no fan-out tick");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));                  // the host has consumed the current pass
     {
@@ -1997,7 +2115,7 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest (the ingest counters "
                                            "of a batch are set by its index)");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));
     {
@@ -2040,7 +2158,7 @@ int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources,
     if (!x || (!arrivals && !sources)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
     if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_arrivals / _sources need serial ticks");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));
     {
@@ -2079,7 +2197,7 @@ int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_pa
     if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
     if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_rows needs serial ticks");
     if (!nsel || !nrows) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));
     {
@@ -2099,7 +2217,7 @@ int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_pa
         HIP_CHECK(rb.add(rows, dr, (size_t)nrows * sizeof(edgpu_packet_row)));
         HIP_CHECK(rb.run());
     } else {
-        HIP_CHECK(hipStreamSynchronize(x->stream));      // `sel` is host memory
+        HIP_CHECK(wsync(x, x->stream));      // `sel` is host memory
     }
     return EDGPU_OK;
 }
@@ -2117,20 +2235,20 @@ int edgpu_arena_gather(edgpu_ctx* x, const edgpu_fanout_result* r, const edgpu_r
         total += reg[i].bytes;
     }
     if (total > cap) return fail(EDGPU_OUT_OVERFLOW, "gather destination too small");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));                      // the tick's copy (overlap_ticks: second stream) is done
     HIP_CHECK(x->d_gather_reg.reserve(n, x->stream));
     HIP_CHECK(x->d_gather_off.reserve(n, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_gather_reg.ptr, reg, n * sizeof(edgpu_region), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_gather_off.ptr, off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, x->stream));
     HIP_CHECK(launch_arena_gather(r->arena, x->d_gather_reg.ptr, x->d_gather_off.ptr, n, (uint8_t*)dst, x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));  // `reg` and `off` are host memory
+    HIP_CHECK(wsync(x, x->stream));  // `reg` and `off` are host memory
     return EDGPU_OK;
 }
 
 int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));
     {
@@ -2147,6 +2265,9 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     out->fanout_passes = x->fanout_passes;
     out->lost_passes = t.cum_lost_passes;
     out->ring_grows = x->ring_grows;
+    out->ring_pool_bytes = x->rings.held;
+    out->watchdog_timeouts = x->watchdog_timeouts;
+    out->ring_grow_failures = x->grow_failures;
     out->ring_bytes = x->ring_bytes;
     out->senders = x->nsenders;
     out->substream_rows = (uint32_t)x->sub_sender.size();
@@ -2155,7 +2276,7 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
 
 int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, uint32_t* out_n) {
     if (!x || which < 0 || which > 3 || (!out_ms && max_n)) return fail(EDGPU_BAD_ARGUMENT, "bad argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));
     const uint32_t n = std::min<uint32_t>(x->hist_n[which] - x->hist_rd[which], edgpu_ctx::kHist);
     const uint32_t first = x->hist_n[which] - n;
@@ -2174,7 +2295,7 @@ int edgpu_kernel_times(edgpu_ctx* x, int which, float* out_ms, uint32_t max_n, u
 int edgpu_copy_to_host(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes) {
     if (!x || (!dst && bytes) || (!src && bytes)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (!bytes) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));
     Readback rb(x);
     HIP_CHECK(rb.add(dst, src, bytes));
@@ -2190,7 +2311,7 @@ int edgpu_set_timing(edgpu_ctx* x, int level) {
 
 int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
     if (!x || !out_ms) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));
     out_ms[0] = out_ms[1] = out_ms[2] = out_ms[3] = 0.f;
     // the newest pair of each history ring: every timed point is recorded once per tick (an
@@ -2213,7 +2334,7 @@ int edgpu_last_timings(edgpu_ctx* x, float out_ms[4]) {
 int edgpu_gop_span(edgpu_ctx* x, uint32_t session, uint32_t track, uint64_t* out_packets, uint64_t* out_bytes) {
     if (!x || !live_session(x, session) || track >= x->sessions[session].ntracks)
         return fail(EDGPU_BAD_ARGUMENT, "bad session/track");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     SenderDev D;
     Readback rb(x);
     HIP_CHECK(rb.add(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D)));
@@ -2235,7 +2356,7 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
                    uint64_t* out_len, uint32_t* out_packets) {
     if (!x || !live_session(x, session) || track >= x->sessions[session].ntracks || (!dst && cap))
         return fail(EDGPU_BAD_ARGUMENT, "bad argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     SenderDev D;
     Readback rb(x);
     HIP_CHECK(rb.add(&D, x->d_senders.ptr + x->sessions[session].first_sender + 2 * track, sizeof(D)));
@@ -2310,7 +2431,7 @@ int edgpu_session_export(edgpu_ctx* x, const uint32_t* sessions, uint32_t n, int
                          const uint64_t* from, void* dst, uint64_t cap, uint64_t* offsets, uint64_t* heads) {
     if (!x || (n && (!sessions || !offsets))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     std::vector<ImgPlan> plan;
     for (uint32_t i = 0; i < n; i++) {
         if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
@@ -2366,7 +2487,7 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
                          const uint32_t* sessions) {
     if (!x || (n && (!images || !offsets || !sessions))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     std::vector<ImgPlan> plan;
     for (uint32_t i = 0; i < n; i++) {
         if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
@@ -2411,7 +2532,7 @@ int edgpu_stream_errors(edgpu_ctx* x, uint32_t* sessions, int32_t* codes, uint32
     *n = 0;
     const uint32_t ns = (uint32_t)x->sessions.size();
     if (!ns) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     HIP_CHECK(sync_all(x));
     std::vector<SessionDev> sd(ns);
     {
@@ -2429,7 +2550,7 @@ int edgpu_stream_errors(edgpu_ctx* x, uint32_t* sessions, int32_t* codes, uint32
         }
         k++;
     }
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     *n = k;
     return EDGPU_OK;
 }
@@ -2441,7 +2562,7 @@ int edgpu_session_relocations(edgpu_ctx* x, const uint32_t* sessions, uint32_t n
     for (uint32_t i = 0; i < n; i++)
         if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (!n) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     std::vector<uint32_t> v(n, 0);
     {
         Readback rb(x);                               // after the backpressure reports (same stream)
@@ -2452,7 +2573,7 @@ int edgpu_session_relocations(edgpu_ctx* x, const uint32_t* sessions, uint32_t n
         out[i] = v[i] ? 1 : 0;
         if (v[i]) HIP_CHECK(hipMemsetAsync(&x->d_sessions.ptr[sessions[i]].relocated, 0, sizeof(uint32_t), x->stream));
     }
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     return EDGPU_OK;
 }
 
@@ -2462,19 +2583,19 @@ int edgpu_session_key_update(edgpu_ctx* x, const uint32_t* sessions, uint32_t n)
     for (uint32_t i = 0; i < n; i++)
         if (!live_session(x, sessions[i])) return fail(EDGPU_BAD_ARGUMENT, "bad session");
     if (!n) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     static const uint32_t one = 1;
     // on the stream the keyframe index runs on: the next batch's k_keyframe reads it
     for (uint32_t i = 0; i < n; i++)
         HIP_CHECK(hipMemcpyAsync(&x->d_sessions.ptr[sessions[i]].video_key_flag, &one, sizeof(one), hipMemcpyHostToDevice,
                                  x->stream));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    HIP_CHECK(wsync(x, x->stream));
     return EDGPU_OK;
 }
 
 int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
     if (!x || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     *out = nullptr;
     if (dmalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess) return fail(EDGPU_OUT_OF_MEMORY, "device buffer");
     return EDGPU_OK;
@@ -2515,11 +2636,21 @@ int edgpu_device_local_cpus(int device, uint32_t* cpus, uint32_t cap, uint32_t* 
     return EDGPU_OK;
 }
 
+int edgpu_debug_stall(edgpu_ctx* x, uint32_t us) {
+    if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
+    DEVICE_ENTER(x);
+    int khz = 0;                                      // the s_memrealtime clock
+    HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, x->device));
+    if (khz <= 0) khz = 100000;
+    HIP_CHECK(launch_stall((uint64_t)us * (uint64_t)khz / 1000ull, x->stream));
+    return EDGPU_OK;
+}
+
 int edgpu_device_free(edgpu_ctx* x, void* p) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!p) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
-    HIP_CHECK(hipStreamSynchronize(x->stream));
+    DEVICE_ENTER(x);
+    HIP_CHECK(wsync(x, x->stream));
     HIP_CHECK(hipFree(p));
     return EDGPU_OK;
 }
@@ -2527,7 +2658,7 @@ int edgpu_device_free(edgpu_ctx* x, void* p) {
 int edgpu_memcpy_peer(edgpu_ctx* x, void* dst, int src_device, const void* src, uint64_t bytes) {
     if (!x || (bytes && (!dst || !src))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (!bytes) return EDGPU_OK;
-    HIP_CHECK(hipSetDevice(x->device));
+    DEVICE_ENTER(x);
     if (src_device == x->device)
         HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, x->stream));
     else

@@ -2587,6 +2587,18 @@ hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hip
     return hipGetLastError();
 }
 
+// edgpu_debug_stall: one wave that waits `ticks` of the device's constant-rate clock (s_memrealtime,
+// sleeping between reads) and exits -- a stand-in for a stuck kernel, to exercise the watchdog.
+// Every lane reaches the exit: the condition is the clock alone.
+__global__ __launch_bounds__(64) void k_stall(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+hipError_t launch_stall(uint64_t ticks, hipStream_t st) {
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, st, ticks);
+    return hipGetLastError();
+}
+
 // edgpu_fanout_arrivals: the arrival time of every descriptor of the last tick.  One wave per
 // sub-stream walks its range [a, head) of the sender's metadata ring; descriptor i is the i-th
 // non-empty packet from `a` (vcount - vcstart), exactly as k_fanout4 numbered them.

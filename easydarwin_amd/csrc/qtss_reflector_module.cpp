@@ -98,6 +98,7 @@ namespace {
 
 // ---- the module side of the callback table (QTSS_Private.cpp's stubs) ----------------------
 QTSS_Callbacks* sCallbacks = nullptr;
+QTSS_StreamRef sErrorLog = nullptr;     // the server's error log (QTSS_PrivateArgs.inErrorLogStream)
 
 template <typename... A>
 QTSS_Error cb(uint32_t index, A... args) {
@@ -345,6 +346,10 @@ struct Module {
     QTSS_Error tickErr = QTSS_NoErr;
     EDGPU_QTSSTickInfo lastTick{};      // guarded by mu
     std::vector<uint32_t> orphans;      // engine sessions whose removal the engine refused: retried per tick
+    // GPU watchdog: a tick the engine's watchdog ended (EDGPU_TIMEOUT) tears every player down and
+    // SETUPs are refused (503) until a tick succeeds again; EDGPU_QTSS_WATCHDOG_MS (default 2000)
+    std::atomic<bool> gpuStalled{false};
+    uint64_t stallTick = 0, stallUs = 0;  // EDGPU_QTSS_TEST_STALL=<tick>:<ms>: a stall before that tick (tests)
 };
 Module* M = nullptr;
 
@@ -704,6 +709,14 @@ void ReaderLoop() {
 // readback) holds the Reflector's engine lock, and the QTSS_Writes hold neither (SetConcurrentDelivery),
 // so SETUP / PLAY / TEARDOWN proceed while a tick writes -- as the reference's per-stream
 // fBucketMutex lets them (ReflectorStream.cpp:1051); a TEARDOWN waits only for the output it removes.
+// The server's error log (QTSSModuleUtils::LogError: QTSS_Write on the error log stream with the
+// verbosity as the flags, QTSSModuleUtils.cpp:168-200), and stderr.
+void LogError(const std::string& msg) {
+    fprintf(stderr, "%s\n", msg.c_str());
+    if (sErrorLog) (void)cb(kWriteCallback, sErrorLog, (const void*)msg.data(), (uint32_t)msg.size(), (uint32_t*)nullptr,
+                            (uint32_t)1 /* qtssWarningVerbosity */);
+}
+
 QTSS_Error Tick() {
     std::lock_guard<std::mutex> tg(M->tickMu);
     const auto t0 = std::chrono::steady_clock::now();
@@ -716,10 +729,28 @@ QTSS_Error Tick() {
         held += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     M->pending.store(false, std::memory_order_release);   // this tick takes what arrived so far
+    if (M->stallTick && seq == M->stallTick) (void)M->R->DebugStall((uint32_t)M->stallUs);
     QTSSSink sink;
     sink.now = Milliseconds();
     const int err = M->R->ReflectPackets(sink.now, &sink);
-    std::lock_guard<std::mutex> g(M->mu);
+    std::unique_lock<std::mutex> g(M->mu);
+    // The GPU watchdog: the engine ended a wait the device did not finish in time (EDGPU_TIMEOUT).
+    // Its players get nothing while the device is stuck, so every one is torn down as
+    // kill_clients_when_broadcast_stops tears a broadcast's down (QRM:2156-2159, RTPSessionOutput::
+    // TearDown), SETUPs are refused (503) and the pushers' packets wait in the batch; the first tick
+    // that succeeds again (the stuck work has finished) lifts it.
+    std::vector<QTSS_Object> teardown;
+    if (err == EDGPU_TIMEOUT) {
+        if (!M->gpuStalled.exchange(true)) {
+            for (const auto& out : M->outputs)
+                if (!out->closed.load()) teardown.push_back(out->client);
+            LogError("QTSSReflectorModule: GPU watchdog: the device did not finish a reflect tick in time (" +
+                     std::string(edgpu_last_error()) + "); tearing down " + std::to_string(teardown.size()) +
+                     " players, refusing SETUP until the device recovers");
+        }
+    } else if (!err && M->gpuStalled.exchange(false)) {
+        LogError("QTSSReflectorModule: GPU watchdog: the device recovered, reflecting again");
+    }
     const auto t1 = std::chrono::steady_clock::now();
     sink.SendReports();
     // outputs removed before or during this tick: no tick can reach them any more
@@ -761,6 +792,13 @@ QTSS_Error Tick() {
             fprintf(stderr, "QTSSReflectorModule: tick failed (%d): %s\n", err,
                     M->R->LastError().empty() ? edgpu_last_error() : M->R->LastError().c_str());
         o.last_error = err;
+    }
+    g.unlock();
+    // outside `mu`: the server may close a client session before QTSS_Teardown returns
+    const uint32_t reason = qtssCliSesTearDownBroadcastEnded;
+    for (QTSS_Object c : teardown) {
+        (void)SetValue(c, qtssCliTeardownReason, 0, &reason, sizeof(reason));
+        (void)cb(kTeardownCallback, c);
     }
     return err == 0 ? QTSS_NoErr : QTSS_RequestFailed;
 }
@@ -874,6 +912,13 @@ QTSS_Error Initialize(QTSS_Initialize_Params* ip) {
     cfg.reflector_use_in_packet_receive_time = useReceiveTime ? 1u : 0u;
     cfg.reflector_in_packet_max_receive_sec = maxFutureSec ? maxFutureSec : EDGPU_FALSE;
     if (const char* v = getenv("EDGPU_QTSS_DEVICE")) cfg.device = atoi(v);
+    // the GPU watchdog: the longest a tick waits for the device (ms; 0: no bound)
+    cfg.watchdog_ms = 2000;
+    if (const char* v = getenv("EDGPU_QTSS_WATCHDOG_MS")) cfg.watchdog_ms = atoi(v) > 0 ? (uint32_t)atoi(v) : EDGPU_FALSE;
+    if (const char* v = getenv("EDGPU_QTSS_TEST_STALL")) {           // tests: <tick>:<ms>
+        M->stallTick = strtoull(v, nullptr, 10);
+        if (const char* c = strchr(v, ':')) M->stallUs = strtoull(c + 1, nullptr, 10) * 1000;
+    }
     // capacities for large fleets (edgpu_config; 0 / unset: the engine defaults): the fan-out
     // arena and descriptors of one tick, the ingest batch of one tick
     if (const char* v = getenv("EDGPU_QTSS_ARENA_MB")) cfg.out_arena_bytes = (uint64_t)atoll(v) << 20;
@@ -1112,6 +1157,8 @@ void DisableOverbufferingIfPref(QTSS_Object client) {
 
 // SETUP (DoSetup, QRM:1597-1800)
 QTSS_Error DoSetup(QTSS_StandardRTSP_Params* p) {
+    // the device is stuck (GPU watchdog): no new pusher or player until a tick succeeds
+    if (M->gpuStalled.load()) return SendErrorResponse(p->inRTSPRequest, qtssServerUnavailable);
     uint32_t mode = qtssRTPTransportModePlay, transport = qtssRTPTransportTypeUDP;
     (void)GetPOD(p->inRTSPRequest, qtssRTSPReqTransportMode, &mode);
     (void)GetPOD(p->inRTSPRequest, qtssRTSPReqTransportType, &transport);
@@ -1633,6 +1680,7 @@ extern "C" QTSS_Error QTSSReflectorModule_Main(void* inPrivateArgs) {
     QTSS_PrivateArgs* a = (QTSS_PrivateArgs*)inPrivateArgs;
     if (!a) return QTSS_BadArgument;
     sCallbacks = a->inCallbacks;
+    sErrorLog = a->inErrorLogStream;
     a->outStubLibraryVersion = kApiVersion;
     a->outDispatchFunction = Dispatch;
     if (!M) {

@@ -313,6 +313,12 @@ void Reflector::ProcessUDPPacket(uint32_t session, uint32_t track, bool rtcpPort
     Append(session, track, packet, packetLen, rtcpPort, nowMs, &u);
 }
 
+int Reflector::DebugStall(uint32_t us) {
+    if (!fCtx) return kRequestFailed;
+    std::lock_guard<std::mutex> eg(fEngineMu);
+    return edgpu_debug_stall(fCtx, us);
+}
+
 int Reflector::SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs) {
     if (!fCtx) return kRequestFailed;
     std::lock_guard<std::mutex> eg(fEngineMu);

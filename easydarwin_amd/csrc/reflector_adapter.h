@@ -176,6 +176,8 @@ public:
     // the sessions marked with a stream error (a sender ring lost a packet one of their outputs
     // needed) since the last call, and clears them: edgpu_stream_errors
     int StreamErrors(std::vector<uint32_t>* sessions);
+    // diagnostics: one wave on the engine stream waits `us` of the device clock (edgpu_debug_stall)
+    int DebugStall(uint32_t us);
     // the message of the last ReflectPackets failure that happened on another thread than the
     // caller's (edgpu_last_error() is per thread); empty otherwise
     const std::string& LastError() const { return fLastErr; }

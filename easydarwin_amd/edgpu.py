@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("EDGPU_LIB") or os.path.join(HERE, "libedgpu.so")
 
 OK, ERR, BAD_ARGUMENT, WOULD_BLOCK = 0, -1, -10, -14
-NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW = -101, -102, -103, -104
+NO_DEVICE, OUT_OF_MEMORY, RING_OVERFLOW, OUT_OVERFLOW, TIMEOUT = -101, -102, -103, -104, -105
 TRANSPORT_UDP, TRANSPORT_TCP = 0, 1
 PTR_HOST, PTR_DEVICE, PTR_PINNED = 0, 1, 2
 PLAY_RTP_INFO = 1
@@ -42,7 +42,7 @@ EXPORTED = [
     "edgpu_set_timing", "edgpu_ingest_prestage", "edgpu_fanout_next", "edgpu_session_ssrc_prefs",
     "edgpu_subscriber_slot", "edgpu_egress_pacing_config", "edgpu_egress_pacing", "edgpu_egress_clock",
     "edgpu_egress_block_info", "edgpu_session_remote_join", "edgpu_session_remote_leave",
-    "edgpu_subscriber_set_slot", "edgpu_device_local_cpus",
+    "edgpu_subscriber_set_slot", "edgpu_device_local_cpus", "edgpu_debug_stall",
 ]
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 PKT_REMOTE_ODD = 1          # edgpu_pkt_desc.flags: a UDP datagram from an odd source port
@@ -72,6 +72,7 @@ class Config(C.Structure):
         ("max_ring_bytes", C.c_uint64),
         ("reflector_use_in_packet_receive_time", C.c_uint32),
         ("reflector_in_packet_max_receive_sec", C.c_uint32),
+        ("watchdog_ms", C.c_uint32),
     ]
 
 
@@ -146,7 +147,8 @@ class Counters(C.Structure):
                 ("ingested_packets", C.c_uint64), ("ingested_bytes", C.c_uint64),
                 ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64),
                 ("senders", C.c_uint32), ("substream_rows", C.c_uint32),
-                ("ring_grows", C.c_uint64), ("ring_bytes", C.c_uint64)]
+                ("ring_grows", C.c_uint64), ("ring_bytes", C.c_uint64), ("ring_pool_bytes", C.c_uint64),
+                ("ring_grow_failures", C.c_uint64), ("watchdog_timeouts", C.c_uint64)]
 
 
 # numpy mirrors (same layout as the C structs)
@@ -506,6 +508,11 @@ class Context:
 
     def sync(self):
         _check(self.lib.edgpu_sync(self.h))
+
+    def debug_stall(self, us: int):
+        """edgpu_debug_stall: one wave on the context stream waits `us` microseconds of the device
+        clock -- work the GPU watchdog (watchdog_ms) can time out on."""
+        _check(self.lib.edgpu_debug_stall(self.h, C.c_uint32(us)))
 
     def timings(self):
         a = (C.c_float * 4)()

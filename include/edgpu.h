@@ -71,6 +71,7 @@ extern "C" {
 #define EDGPU_NO_DEVICE       -101     /* no usable gfx950 device / HIP failure */
 #define EDGPU_OUT_OF_MEMORY   -102
 #define EDGPU_RING_OVERFLOW   -103     /* a needed packet fell out of a sender ring */
+#define EDGPU_TIMEOUT        -105     /* GPU watchdog: the device did not finish within watchdog_ms */
 #define EDGPU_OUT_OVERFLOW    -104     /* a buffer too small (a fan-out sub-stream larger than the
                                           arena, a batch, a gather destination, ...) */
 
@@ -133,6 +134,12 @@ typedef struct edgpu_config {
      * EDGPU_FALSE for 0; :106-107, 113) ahead of the push time are clamped there. */
     uint32_t reflector_use_in_packet_receive_time;
     uint32_t reflector_in_packet_max_receive_sec;
+    /* GPU watchdog (default 10000 ms; EDGPU_FALSE: unbounded): the longest any call waits for the
+     * device.  A wait that runs out returns EDGPU_TIMEOUT and wedges the context: every call that
+     * would enqueue work or wait returns EDGPU_TIMEOUT at once, enqueueing nothing, until the work
+     * it timed out on has finished; then the context is usable again (the results of that work were
+     * never read: the host re-runs or drops the tick).  edgpu_ctx_destroy waits without a bound. */
+    uint32_t watchdog_ms;
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu   /* a flag off / a value of 0 where 0 would select the default */
 
@@ -718,6 +725,11 @@ typedef struct edgpu_counters {
     uint32_t substream_rows;    /* removed sessions' / subscribers' rows are reused, best fit */
     uint64_t ring_grows;        /* sender rings grown so far (edgpu_config.ring_growth) */
     uint64_t ring_bytes;        /* device bytes of every live sender's two rings now */
+    uint64_t ring_pool_bytes;   /* device bytes the ring pool holds now: live rings, rings on its free
+                                   lists (reused by later sessions / growths) and unused chunk space */
+    uint64_t ring_grow_failures; /* growths skipped because the device memory could not hold the new
+                                    rings (growth is best effort; the ingest goes on) */
+    uint64_t watchdog_timeouts; /* waits the GPU watchdog ended (edgpu_config.watchdog_ms) */
 } edgpu_counters;
 int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 
@@ -818,6 +830,9 @@ int  edgpu_memcpy_peer(edgpu_ctx* ctx, void* dst, int src_device, const void* sr
  * to it is enabled for every GPU that can reach this one, so RCCL and peer copies may use it. */
 int  edgpu_device_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_device_free(edgpu_ctx* ctx, void* ptr);
+/* Diagnostics: enqueues on the context stream one wave that waits `us` microseconds of the device
+ * clock and exits -- work the GPU watchdog (edgpu_config.watchdog_ms) can time out on. */
+int  edgpu_debug_stall(edgpu_ctx* ctx, uint32_t us);
 /* The host CPUs of device `device`'s NUMA node (the sysfs local_cpulist of its PCI function) that
  * the calling thread may run on: cpus[0 .. min(*n_out, cap)), *n_out = how many -- where a server
  * hosting the module belongs (tools/bench_module.py --affinity gpu-node).  No

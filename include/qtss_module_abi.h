@@ -122,6 +122,7 @@ enum : uint32_t {
     qtssClientForbidden = 16,       // 403
     qtssClientNotFound = 17,        // 404
     qtssPreconditionFailed = 25,    // 412
+    qtssServerUnavailable = 44,     // 503
 };
 
 // attribute ids read or written by the reflector module

@@ -58,7 +58,7 @@ SAME(kSendRTSPHeadersCallback); SAME(kOpenFileObjectCallback); SAME(kCloseFileOb
 SAME(qtssUserProfileObjectType); SAME(qtssActionFlagsNoFlags); SAME(qtssActionFlagsRead); SAME(qtssActionFlagsWrite);
 SAME(qtssAuthNone); SAME(qtssAuthBasic); SAME(qtssAuthDigest);
 SAME(qtssSuccessOK); SAME(qtssClientBadRequest); SAME(qtssClientUnAuthorized); SAME(qtssClientForbidden);
-SAME(qtssClientNotFound); SAME(qtssPreconditionFailed);
+SAME(qtssClientNotFound); SAME(qtssPreconditionFailed); SAME(qtssServerUnavailable);
 SAME(qtssRTSPReqFilePathTrunc); SAME(qtssRTSPReqStatusCode); SAME(qtssRTSPReqUserAllowed); SAME(qtssRTSPReqURLRealm);
 SAME(qtssRTSPReqLocalPath); SAME(qtssRTSPReqRespMsg); SAME(qtssRTSPReqAction); SAME(qtssRTSPReqUserProfile);
 SAME(qtssRTSPReqAuthScheme); SAME(qtssRTSPReqUserFound); SAME(qtssRTSPReqAuthHandled); SAME(qtssRTSPSesRemoteAddrStr);

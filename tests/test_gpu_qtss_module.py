@@ -141,3 +141,47 @@ def test_module_threaded_default_mode_matches_reference(tmp_path, arrival):
         assert got.keys() == want.keys()
         bad = {k: (got[k][:2], want[k][:2]) for k in want if got[k] != want[k]}
         assert not bad, f"run {attempt}: {len(bad)} sub-streams differ: {dict(list(bad.items())[:6])}"
+
+
+def _watchdog_trace():
+    """One RTSP-interleaved H.264 push for 4 s, ticks every 100 ms; player 1 from the start, player 2
+    joining at 2.5 s (after the stall below is over)."""
+    from easydarwin_amd.trace import UDP, Trace
+    from scenarios import SEED_BASE, TrackSpec, _assemble, make_sdp, session_packets
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=300_000, gop=30, idr_bytes=4_000)]
+    tr = Trace()
+    tr.add_session(make_sdp(v))
+    pk = session_packets(v, 4000, SEED_BASE + 170)
+    return _assemble(tr, [pk], 100, 4000, [(0, 0, 1, UDP), (2500, 0, 2, UDP)])
+
+
+@pytest.mark.gpu
+def test_module_gpu_watchdog(tmp_path):
+    """SURVEY §5's GPU watchdog through the module (VERDICT r5 missing #2): before its 10th tick the
+    engine stream gets a wave that waits 0.9 s (EDGPU_QTSS_TEST_STALL), the watchdog is 0.3 s.  The
+    tick returns the timeout; the module logs it through the server's error log, tears every player
+    down (QTSS_Teardown, as kill_clients does) and answers a SETUP made meanwhile at once with 503;
+    the fake server retries the tick every 50 ms; once the wave has exited the tick succeeds, the
+    module logs the recovery, and a player joining later gets exactly the reference's bytes."""
+    from easydarwin_amd.trace import capture_summary, read_capture
+    tr = _watchdog_trace()
+    t, c, el, rq = tmp_path / "t.edtr", tmp_path / "c.edcp", tmp_path / "err.log", tmp_path / "rq.log"
+    t.write_bytes(tr.to_bytes())
+    env = dict(os.environ, EDGPU_QTSS_WATCHDOG_MS="300", EDGPU_QTSS_TEST_STALL="10:900", EDGPU_REPLAY_TICK_RETRY="1",
+               EDGPU_ERROR_LOG=str(el), EDGPU_REQ_LOG=str(rq))
+    r = subprocess.run([REPLAY, MODULE, str(t), str(c)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    log = el.read_text()
+    assert "GPU watchdog: the device did not finish a reflect tick in time" in log, log
+    assert "tearing down 1 players" in log and "the device recovered" in log, log
+    assert "T 900 tick failed" in log and "P probe SETUP refused in <50 ms" in log, log
+    assert any(" player 999999 " in l and l.endswith("-> 503 hdr+0 close") for l in rq.read_text().splitlines())
+    got = capture_summary(read_capture(c.read_bytes()))
+    # the reference (the port oracle of the same trace): player 2's bytes equal; player 1 stopped at the stall
+    port = os.path.join(ROOT, "oracle", "relay_model")
+    ref_t, ref_c = tmp_path / "r.edtr", tmp_path / "r.edcp"
+    ref_t.write_bytes(tr.to_bytes())
+    subprocess.run([port, str(ref_t), str(ref_c)], check=True)
+    want = capture_summary(read_capture(ref_c.read_bytes()))
+    assert got["2/0/0"] == want["2/0/0"] and got["2/0/0"][0] > 0
+    assert 0 < got["1/0/0"][0] < want["1/0/0"][0]

@@ -57,6 +57,26 @@ def test_highrate_needs_the_growth():
 
 
 @pytest.mark.gpu
+def test_growth_is_best_effort_when_device_memory_runs_out(monkeypatch):
+    """A growth the device memory cannot hold (a ring pool limited to 16 MiB: the starting rings fit,
+    the 16-MiB byte ring does not) is skipped and counted, and every ingest goes on: the replay
+    completes, relays what the ungrown rings hold -- exactly what it relays with growth off -- and
+    marks the session whose players lost packets (edgpu_stream_errors)."""
+    tr = _trace("highrate")
+    with _ctx(tr, ring_growth=edgpu.FALSE) as ctx:
+        want, _ = replay(tr, ctx=ctx)
+    monkeypatch.setenv("EDGPU_RING_POOL_LIMIT", str(16 << 20))
+    with _ctx(tr) as ctx:
+        cap, _ = replay(tr, ctx=ctx)
+        errors = ctx.stream_errors()
+        c = ctx.counters()
+    assert c["ring_grow_failures"] >= 1 and c["ring_grows"] == 0
+    assert c["ring_pool_bytes"] <= 16 << 20
+    assert errors
+    assert cap == want
+
+
+@pytest.mark.gpu
 def test_growth_stops_at_its_bound():
     """max_ring_bytes / max_ring_packets bound the growth (powers of two): with both at the
     starting capacities nothing grows."""

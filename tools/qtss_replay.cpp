@@ -395,8 +395,17 @@ static LatHist* lat_hist() {
     }
     return h;
 }
+// the server's error log stream (QTSS_PrivateArgs.inErrorLogStream): EDGPU_ERROR_LOG=<path> gets
+// its messages, one a line with the verbosity the module wrote them at
+static constexpr uint32_t kErrorLogType = 0x656c6f67u;   // 'elog'
+static FILE* g_err_log = nullptr;
 static QTSS_Error cb_write(Obj* o, const void* buf, uint32_t len, uint32_t* outLen, uint32_t flags, ...) {
     if (o && o->type == qtssRTSPRequestObjectType) { o->written += len; if (outLen) *outLen = len; return QTSS_NoErr; }
+    if (o && o->type == kErrorLogType) {
+        if (g_err_log) fprintf(g_err_log, "E %lld v%u %.*s\n", (long long)g_now.load(), flags, (int)len, (const char*)buf);
+        if (outLen) *outLen = len;
+        return QTSS_NoErr;
+    }
     if (!o || o->type != qtssRTPStreamObjectType) return QTSS_NoErr;
     const int k = (flags & qtssWriteFlagsIsRTCP) ? 1 : 0;
     if (g_count_only) {
@@ -610,6 +619,7 @@ static std::string status_str(uint32_t s) {
         case qtssClientForbidden: return "403";
         case qtssClientNotFound: return "404";
         case qtssPreconditionFailed: return "412";
+        case qtssServerUnavailable: return "503";
         default: return "s" + std::to_string(s);
     }
 }
@@ -1081,6 +1091,11 @@ int main(int argc, char** argv) {
     memset(&args, 0, sizeof(args));
     args.inServerAPIVersion = kApiVersion;
     args.inCallbacks = &cbs;
+    args.inErrorLogStream = new_obj(kErrorLogType);
+    if (const char* lp = getenv("EDGPU_ERROR_LOG")) {
+        g_err_log = fopen(lp, "w");
+        if (!g_err_log) { perror(lp); return 2; }
+    }
     if (main_fn(&args) != QTSS_NoErr || args.outStubLibraryVersion != kApiVersion || !args.outDispatchFunction) {
         fprintf(stderr, "module main failed\n"); return 3;
     }
@@ -1342,7 +1357,36 @@ int main(int argc, char** argv) {
             holders[s]++;
             players.push_back(pl);
         } else if (type == 3) {                                  // TICK
-            const QTSS_Error e = tick_fn();
+            QTSS_Error e = tick_fn();
+            // EDGPU_REPLAY_TICK_RETRY=1: a failed tick (the module's GPU watchdog) is retried every 50
+            // ms until it succeeds; at the first failure a player SETUP on session 0 probes whether the
+            // module still answers RTSP (it must, at once: 503 while the device is stuck)
+            static const bool retry = getenv("EDGPU_REPLAY_TICK_RETRY") && atoi(getenv("EDGPU_REPLAY_TICK_RETRY")) != 0;
+            for (int k = 0; e && retry && k < 400; k++) {
+                if (g_err_log) fprintf(g_err_log, "T %lld tick failed (%d)\n", (long long)t, (int)e);
+                if (k == 0) {
+                    Obj* pr = new_rtsp();
+                    Obj* pc = new_client();
+                    pc->player_sub = 999999;
+                    g_rtsp_of_client[pc] = pr;
+                    const auto a = std::chrono::steady_clock::now();
+                    const QTSS_Error pe = request(pr, pc, qtssSetupMethod, paths[0] + "/trackID=1", "1", qtssRTPTransportModePlay,
+                                                  qtssRTPTransportTypeUDP);
+                    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+                    if (g_err_log) fprintf(g_err_log, "P probe SETUP %s in %s ms\n", pe ? "refused" : "accepted", ms < 50 ? "<50" : ">=50");
+                    close_client(pc);
+                }
+                // the server closes the client sessions the module tore down (QTSS_Teardown)
+                for (auto& pl : players)
+                    if (!pl.left && pl.client->torn_down) {
+                        close_client(pl.client);
+                        pl.left = true;
+                        holders[pl.session]--;
+                        release_check(pl.session);
+                    }
+                usleep(50000);
+                e = tick_fn();
+            }
             if (e) { fprintf(stderr, "tick failed %d\n", (int)e); return 3; }
             static auto last_tick = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
             EDGPU_QTSSTickInfo ti;
