@@ -318,6 +318,7 @@ int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* r, uint32_t n) {
     }
     return EDGPU_OK;
 }
+int edgpu_debug_stall(edgpu_ctx* x, uint32_t) { touch(x); return EDGPU_OK; }   // no device to stall
 int edgpu_device_local_cpus(int, uint32_t*, uint32_t, uint32_t* n) {   // no GPU: no placement
     if (n) *n = 0;
     return EDGPU_ERR;
