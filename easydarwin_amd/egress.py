@@ -19,10 +19,35 @@ applies the gate itself (EDTR_SERVER_GATE=1).
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
 import socket
 import struct
 
 from . import edgpu
+
+_DRAIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libudp_drain.so")
+_drain_lib = None
+
+
+def _drain():
+    """tools/libudp_drain.so: a thread per UDP receiver that takes datagrams (recvmmsg) while the
+    egress sends -- a tick replaying a whole GOP to a new player outruns any receive buffer
+    net.core.rmem_max allows, and loopback UDP drops what does not fit."""
+    global _drain_lib
+    if _drain_lib is None:
+        lib = C.CDLL(_DRAIN)
+        lib.udpd_start.restype = C.c_void_p
+        lib.udpd_start.argtypes = [C.POINTER(C.c_int), C.c_int]
+        lib.udpd_stop.argtypes = [C.c_void_p]
+        lib.udpd_size.restype = C.c_size_t
+        lib.udpd_size.argtypes = [C.c_void_p, C.c_int]
+        lib.udpd_count.restype = C.c_size_t
+        lib.udpd_count.argtypes = [C.c_void_p, C.c_int]
+        lib.udpd_take.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        lib.udpd_free.argtypes = [C.c_void_p]
+        _drain_lib = lib
+    return _drain_lib
 
 
 class SocketSink:
@@ -37,6 +62,7 @@ class SocketSink:
         self.udp = {}           # (handle, track, kind) -> receiver socket
         self.tcp = {}           # handle -> [sender end, reader end, bytearray]
         self.parts = {}         # (handle, track, kind) -> wire image parts (UDP)
+        self.npk = {}           # (handle, track, kind) -> datagrams received (UDP)
         self.q_of = []          # sub-stream index -> (handle, track, kind)
         self.sub_id = {}        # handle -> subscriber id
         self.blocked = []       # (tick time, sub_id, track, kind, sent)
@@ -48,6 +74,7 @@ class SocketSink:
             for k in (0, 1):
                 self.q_of.append((handle, t, k))
                 self.parts[(handle, t, k)] = []
+                self.npk[(handle, t, k)] = 0
         if tcp:
             a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
             if self.tcp_sndbuf:
@@ -74,7 +101,24 @@ class SocketSink:
     def tick(self, result, t: int):
         if self.pacing is not None:
             self.eg.clock(t)
-        st = self.eg.send(result)
+        # the UDP receivers drain on their own threads while the egress sends (tools/udp_drain.c)
+        keys = list(self.udp)
+        lib = _drain()
+        fds = (C.c_int * max(1, len(keys)))(*[self.udp[k].fileno() for k in keys])
+        h = lib.udpd_start(fds, len(keys)) if keys else None
+        try:
+            st = self.eg.send(result)
+        finally:
+            if h:
+                lib.udpd_stop(h)
+                for i, k in enumerate(keys):
+                    n = lib.udpd_size(h, i)
+                    if n:
+                        b = C.create_string_buffer(n)
+                        lib.udpd_take(h, i, b)
+                        self.parts[k].append(b.raw)
+                        self.npk[k] += lib.udpd_count(h, i)
+                lib.udpd_free(h)
         self.stats.append(st)
         for q, _sent, written, cause in self.eg.block_info():
             if cause != 0:                          # the write gate held it, not the socket
@@ -93,6 +137,7 @@ class SocketSink:
                 except BlockingIOError:
                     break
                 self.parts[key].append(struct.pack(">H", len(d)) + d)
+                self.npk[key] += 1
         for h, (_a, b, buf) in self.tcp.items():
             if h in skip:
                 continue
@@ -113,7 +158,7 @@ class SocketSink:
             if self.eg.flush() == 0:
                 break
         self.drain()
-        images = {k: (len(v), b"".join(v)) for k, v in self.parts.items()}
+        images = {k: (self.npk[k], b"".join(v)) for k, v in self.parts.items()}
         for h, (_a, _b, buf) in self.tcp.items():
             per = {}
             p = 0

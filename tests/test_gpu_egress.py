@@ -30,11 +30,11 @@ def _fixture(name):
 
 
 @pytest.mark.gpu
-# `highrate` replays a 13.5-MB GOP to two UDP players in one tick: past what a loopback receiver
-# holds (net.core.rmem_max) before this test reads it, so the kernel drops datagrams as UDP does;
-# its bytes are pinned through the C ABI, the adapter and the module instead
+# `highrate` replays a 13.5-MB GOP to two UDP players in one tick -- past what a loopback receive
+# buffer holds (net.core.rmem_max): the receivers drain on their own threads while the egress sends
+# (SocketSink, tools/udp_drain.c), so every datagram arrives
 @pytest.mark.parametrize("name", [n for n in SCENARIOS                     # not the scripted BLOCKs
-                                  if not any(ev[0] == BLOCK for ev in SCENARIOS[n]().events) and n != "highrate"])
+                                  if not any(ev[0] == BLOCK for ev in SCENARIOS[n]().events)])
 def test_socket_egress_matches_reference(name):
     cap, _ = replay(SCENARIOS[name](), sockets={"threads": 3})
     fix = _fixture(name)
@@ -201,7 +201,7 @@ def _gate_reference(tr: Trace, report, exe, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", [n for n in SCENARIOS
-                                  if not any(ev[0] == BLOCK for ev in SCENARIOS[n]().events) and n != "highrate"])
+                                  if not any(ev[0] == BLOCK for ev in SCENARIOS[n]().events)])
 def test_paced_egress_matches_the_reference_server_gate(name, oracle_bins, tmp_path):
     """Q20: with pacing on (edgpu_egress_pacing) the egress applies the server's RTPStream::Write
     gate -- the over-buffer window holds a new output's first packets until their transmit time
