@@ -474,9 +474,6 @@ def main():
     ap.add_argument("--subs", type=int, default=16, help="UDP subscribers per session")
     ap.add_argument("--tick-ms", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--overlap", action="store_true",
-                    help="tick pipelining: ingest(t+1) beside the fan-out copy of t on a second stream "
-                         "(measured slower on C2: both phases are HBM-bound and contend)")
     ap.add_argument("--ingest", choices=["desc", "tcp", "host"], default="desc",
                     help="desc: packets handed over as descriptors + slots in HBM (edgpu_ingest, the "
                          "reflector's per-packet PushPacket boundary); tcp: the pushers' RTSP-interleaved TCP "
@@ -568,8 +565,7 @@ def main():
                         out_arena_bytes=max_arena, max_out_packets=max_out,
                         max_batch_packets=max_pk + 1,
                         max_batch_bytes=(max(b["bytes"] for b in batches) + (1 << 20)) if args.ingest in ("tcp", "host")
-                        else 1 << 20,
-                        overlap_ticks=1 if args.overlap else 0)
+                        else 1 << 20)
     if args.ingest == "host":
         for bt in batches:
             bt["pinned"] = make_pinned(ctx, bt)

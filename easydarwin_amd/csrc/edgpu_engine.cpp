@@ -261,11 +261,6 @@ struct edgpu_ctx {
                                     // frames per wave round; 2 the same with per-lane frame state;
                                     // 1 one frame per round; 0 two loads per word
     hipStream_t stream = nullptr;
-    // tick pipelining (edgpu_config.overlap_ticks): the fan-out copy kernel runs on `copy`,
-    // ordered after its plan by ev_plan; the next plan waits for ev_copy
-    bool overlap = false;
-    hipStream_t copy = nullptr;
-    hipEvent_t ev_plan = nullptr, ev_copy = nullptr;
     // the RTSP-interleaved deframe (k_tcp_*) runs on `aux`: it reads only the call's TCP bytes
     // and writes deframe scratch, so it overlaps the previous tick's fan-out still on `stream`;
     // the host reads its report, then enqueues k_ingest (no cross-stream wait left on `stream`)
@@ -274,7 +269,6 @@ struct edgpu_ctx {
     // the last keyframe index (it reads the segment tables the next deframe rewrites)
     hipEvent_t ev_kf = nullptr;
     bool kf_recorded = false;
-    int cur = 0;                    // output buffer of the current tick (0 / 1)
     // per-launch timing history: [which][slot][start,end]
     static const int kHist = 256;
     hipEvent_t hist[4][kHist][2] = {};
@@ -367,9 +361,8 @@ struct edgpu_ctx {
     uint32_t pend_nseg = 0;
     bool pending = false;
 
-    uint8_t* d_arena_buf[2] = {nullptr, nullptr};
-    edgpu_out_desc* d_out_desc_buf[2] = {nullptr, nullptr};
-    DevVec<edgpu_substream_out> d_sub_out_buf2;   // second sub-stream table (overlap)
+    uint8_t* d_arena = nullptr;                 // the tick's (pass's) send-ready bytes
+    edgpu_out_desc* d_out_desc = nullptr;       // and descriptors
     // RTSP-interleaved ingest: per-session carried partial frame (device) and its length
     // (host mirror, read back with every call's results), per-call walk tables
     std::vector<uint32_t> carry_len;
@@ -571,16 +564,8 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (dmalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
     if (dmalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
     if (dmalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
-    x->overlap = c.overlap_ticks != 0;
-    for (int k = 0; k < (x->overlap ? 2 : 1); k++) {
-        if (dmalloc(&x->d_arena_buf[k], c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
-        if (dmalloc(&x->d_out_desc_buf[k], sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
-    }
-    if (x->overlap) {
-        if (hipStreamCreateWithFlags(&x->copy, hipStreamNonBlocking) != hipSuccess) return bad("copy stream");
-        if (hipEventCreateWithFlags(&x->ev_plan, hipEventDisableTiming) != hipSuccess) return bad("event");
-        if (hipEventCreateWithFlags(&x->ev_copy, hipEventDisableTiming) != hipSuccess) return bad("event");
-    }
+    if (dmalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
+    if (dmalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
     if (dmalloc(&x->d_totals, sizeof(TickTotals)) != hipSuccess) return bad("totals");
     if (dmalloc(&x->d_grow, sizeof(GrowReq) * kMaxGrow) != hipSuccess) return bad("ring growth requests");
     if (hipHostMalloc((void**)&x->h_grow_flag, 64, hipHostMallocMapped) != hipSuccess ||
@@ -610,13 +595,12 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (!x) return EDGPU_OK;
     (void)hipSetDevice(x->device);
     if (x->stream) (void)hipStreamSynchronize(x->stream);
-    if (x->copy) (void)hipStreamSynchronize(x->copy);
     x->rings.release();                          // (every sender's rings)
     if (x->d_null) (void)hipFree(x->d_null);
     x->d_sessions.release(); x->d_senders.release(); x->d_streams.release(); x->d_subs.release();
     x->d_sub_index.release(); x->d_sub_range.release(); x->d_sub_pos.release(); x->d_fansub.release(); x->d_sub_out.release(); x->d_work.release();
     x->d_blk_bytes.release(); x->d_blk_count.release(); x->d_blk_maxb.release(); x->d_blk_maxc.release();
-    x->d_img_plan.release(); x->d_sub_out_buf2.release();
+    x->d_img_plan.release();
     x->d_carry.release(); x->d_tcp_groups.release(); x->d_tcp_reads.release(); x->d_tcp_chunk_group.release();
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
@@ -632,8 +616,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
     if (x->d_img_status) (void)hipFree(x->d_img_status);
     for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
-                    (void*)x->d_blob, (void*)x->d_arena_buf[0], (void*)x->d_out_desc_buf[0],
-                    (void*)x->d_arena_buf[1], (void*)x->d_out_desc_buf[1], (void*)x->d_totals, (void*)x->d_grow})
+                    (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals, (void*)x->d_grow})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
     if (x->h2d) (void)hipStreamSynchronize(x->h2d);
@@ -643,9 +626,6 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
         if (st.consumed) (void)hipEventDestroy(st.consumed);
     }
     if (x->h2d) (void)hipStreamDestroy(x->h2d);
-    if (x->ev_plan) (void)hipEventDestroy(x->ev_plan);
-    if (x->ev_copy) (void)hipEventDestroy(x->ev_copy);
-    if (x->copy) (void)hipStreamDestroy(x->copy);
     if (x->aux) (void)hipStreamSynchronize(x->aux);
     if (x->ev_serial) (void)hipEventDestroy(x->ev_serial);
     if (x->ev_kf) (void)hipEventDestroy(x->ev_kf);
@@ -656,10 +636,9 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     return EDGPU_OK;
 }
 
-// Waits for everything the context has enqueued (both streams with overlap_ticks).
+// Waits for everything the context has enqueued (the context stream and the deframe's).
 static hipError_t sync_all(edgpu_ctx* x) {
     hipError_t e = wsync(x, x->stream);
-    if (e == hipSuccess && x->copy) e = wsync(x, x->copy);
     if (e == hipSuccess && x->aux) e = wsync(x, x->aux);
     return e;
 }
@@ -1108,7 +1087,7 @@ int edgpu_session_remove(edgpu_ctx* x, uint32_t session, uint32_t flags) {
     DEVICE_ENTER(x);
     // TearDownAllOutputs: every attached subscriber goes with it
     while (!sh.subs.empty()) { int r = detach_subscriber(x, sh.subs.back()); if (r) return r; }
-    // the rings may still be read by a fan-out copy in flight (overlap_ticks) or a pinned batch
+    // the rings may still be read by a fan-out copy in flight or a pinned batch
     HIP_CHECK(sync_all(x));
     if (x->h2d) HIP_CHECK(wsync(x, x->h2d));
     const uint32_t nsnd = 2 * sh.ntracks;
@@ -1568,7 +1547,6 @@ static int rebuild_index(edgpu_ctx* x) {
     if (!range.empty()) HIP_CHECK(hipMemcpyAsync(x->d_sub_range.ptr, range.data(), range.size() * 4, hipMemcpyHostToDevice, x->stream));
     const uint32_t nblk = (nsub + 255) / 256;
     HIP_CHECK(x->d_sub_out.reserve(std::max<uint32_t>(nsub, 1), x->stream));
-    if (x->overlap) HIP_CHECK(x->d_sub_out_buf2.reserve(std::max<uint32_t>(nsub, 1), x->stream));
     HIP_CHECK(x->d_blk_bytes.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_count.reserve(std::max<uint32_t>(nblk, 1), x->stream));
     HIP_CHECK(x->d_blk_maxb.reserve(std::max<uint32_t>(nblk, 1), x->stream));
@@ -1595,7 +1573,6 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
     p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
-    p.overlap = (x->overlap && x->fanout_launches > 0) ? 1u : 0u;   // a copy may be in flight
     p.totals = x->d_totals;
     p.recv_time = x->cfg.reflector_use_in_packet_receive_time;
     // sMaxFuturePacketMSec = sMaxFuturePacketSec * 1000 in UInt32 (ReflectorStream.cpp:113)
@@ -1973,13 +1950,13 @@ static int pick_fanout_variant(const edgpu_ctx* x) {
     return fanout_default(x->n_rw + x->n_tcp > 0 || burst);
 }
 
-// The plan parameters of the context's current tick (arena / descriptor buffers of x->cur).
+// The plan parameters of the context's current tick.
 static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     const uint32_t nsub = x->tick_nsubs;            // rows added since are not the tick's
     PlanParams p;
     p.senders = x->d_senders.ptr; p.subs = x->d_subs.ptr; p.sub_index = x->d_sub_index.ptr;
     p.sub_pos = x->d_sub_pos.ptr; p.sub_range = x->d_sub_range.ptr; p.fansub = x->d_fansub.ptr;
-    p.sub_out = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
+    p.sub_out = x->d_sub_out.ptr;
     p.work = x->d_work.ptr;
     p.blk_bytes = x->d_blk_bytes.ptr; p.blk_count = x->d_blk_count.ptr;
     p.blk_maxb = x->d_blk_maxb.ptr; p.blk_maxc = x->d_blk_maxc.ptr;
@@ -2003,32 +1980,26 @@ static PlanParams plan_params(edgpu_ctx* x, int64_t now_ms) {
     return p;
 }
 
-// The copy kernel of the current pass (on the copy stream with overlap_ticks, after the plan).
+// The copy kernel of the current pass (after the plan, on the context stream).
 static int launch_copy_pass(edgpu_ctx* x, edgpu_fanout_result* out) {
     FanoutParams f;
     f.senders = x->d_senders.ptr; f.sub_range = x->d_sub_range.ptr; f.subs = x->d_subs.ptr;
     f.sub_index = x->d_sub_index.ptr; f.work = x->d_work.ptr; f.fansub = x->d_fansub.ptr;
-    f.arena = x->d_arena_buf[x->cur]; f.desc = x->d_out_desc_buf[x->cur];
+    f.arena = x->d_arena; f.desc = x->d_out_desc;
     f.arena_words = x->cfg.out_arena_bytes / 16;
     f.max_desc = x->cfg.max_out_packets;
     f.totals = x->d_totals;
     f.ablate = x->ablate;
     hipStream_t cs = x->stream;
-    if (x->overlap) {
-        HIP_CHECK(hipEventRecord(x->ev_plan, x->stream));
-        HIP_CHECK(hipStreamWaitEvent(x->copy, x->ev_plan, 0));
-        cs = x->copy;
-    }
     HIP_CHECK(hist_mark(x, 0, 0, cs));
     HIP_CHECK(launch_fanout(f, x->tick_variant, x->num_cus, cs));
     HIP_CHECK(hist_mark(x, 0, 1, cs));
-    if (x->overlap) HIP_CHECK(hipEventRecord(x->ev_copy, x->copy));
     x->fanout_passes++;
     x->passes_more = -1;
     if (out) {
         out->arena = f.arena;
         out->desc = f.desc;
-        out->substreams = (x->overlap && x->cur) ? x->d_sub_out_buf2.ptr : x->d_sub_out.ptr;
+        out->substreams = x->d_sub_out.ptr;
         out->n_substreams = x->tick_nsubs;
     }
     return EDGPU_OK;
@@ -2039,13 +2010,6 @@ int edgpu_fanout(edgpu_ctx* x, int64_t now_ms, edgpu_fanout_result* out) {
     if (x->pending) return fail(EDGPU_ERR, "edgpu_keyframe_index must run after edgpu_ingest");
     if (int r = owed_pass(x, "edgpu_fanout")) return r;
     DEVICE_ENTER(x);
-    if (x->overlap) {
-        // the index rebuild may reallocate tables the in-flight copy reads
-        if (x->index_dirty) HIP_CHECK(wsync(x, x->copy));
-        // this tick's plan rewrites the work list and sub-stream records the previous copy reads
-        HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));
-        x->cur ^= 1;
-    }
     // rows freed during the last tick may be reused from now on (its passes are delivered)
     for (const auto& f : x->free_pending) x->free_subs[f.first].push_back(f.second);
     x->free_pending.clear();
@@ -2157,7 +2121,6 @@ int edgpu_fanout_arrivals(edgpu_ctx* x, int64_t* out, uint32_t n, int kind) {
 int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources, uint32_t n, int kind) {
     if (!x || (!arrivals && !sources)) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
-    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_arrivals / _sources need serial ticks");
     DEVICE_ENTER(x);
     TickTotals t;
     HIP_CHECK(sync_all(x));
@@ -2195,7 +2158,6 @@ int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources,
 int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_packet_row* rows, uint64_t nrows, int kind) {
     if (!x || (nsel && (!sel || !rows))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
     if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
-    if (x->overlap) return fail(EDGPU_BAD_ARGUMENT, "edgpu_fanout_rows needs serial ticks");
     if (!nsel || !nrows) return EDGPU_OK;
     DEVICE_ENTER(x);
     TickTotals t;
@@ -2210,7 +2172,7 @@ int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_pa
     if (kind == EDGPU_PTR_HOST) { HIP_CHECK(x->d_rows.reserve(nrows, x->stream)); dr = x->d_rows.ptr; }
     HIP_CHECK(x->d_row_sel.reserve(2 * (uint64_t)nsel, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_row_sel.ptr, sel, 2 * (size_t)nsel * sizeof(uint32_t), hipMemcpyHostToDevice, x->stream));
-    HIP_CHECK(launch_sub_rows(x->d_subs.ptr, x->d_senders.ptr, x->d_out_desc_buf[x->cur], x->d_row_sel.ptr, nsel,
+    HIP_CHECK(launch_sub_rows(x->d_subs.ptr, x->d_senders.ptr, x->d_out_desc, x->d_row_sel.ptr, nsel,
                               x->tick_nsubs, x->pass_id, x->host_epoch_last, dr, nrows, x->stream));
     if (kind == EDGPU_PTR_HOST) {
         Readback rb(x);
@@ -2236,7 +2198,7 @@ int edgpu_arena_gather(edgpu_ctx* x, const edgpu_fanout_result* r, const edgpu_r
     }
     if (total > cap) return fail(EDGPU_OUT_OVERFLOW, "gather destination too small");
     DEVICE_ENTER(x);
-    HIP_CHECK(sync_all(x));                      // the tick's copy (overlap_ticks: second stream) is done
+    HIP_CHECK(sync_all(x));                      // the tick's copy is done
     HIP_CHECK(x->d_gather_reg.reserve(n, x->stream));
     HIP_CHECK(x->d_gather_off.reserve(n, x->stream));
     HIP_CHECK(hipMemcpyAsync(x->d_gather_reg.ptr, reg, n * sizeof(edgpu_region), hipMemcpyHostToDevice, x->stream));
@@ -2503,7 +2465,6 @@ int edgpu_session_import(edgpu_ctx* x, const void* images, const uint64_t* offse
         }
     }
     if (plan.empty()) return EDGPU_OK;
-    if (x->overlap) HIP_CHECK(hipStreamWaitEvent(x->stream, x->ev_copy, 0));   // rings the copy reads
     if (x->grow_pending || __atomic_load_n(x->h_grow_flag, __ATOMIC_ACQUIRE)) { int r = grow_rings(x); if (r) return r; }
     if (x->cfg.ring_growth) {
         // a replica's rings must hold what its owner's image carries (a full image: the key packet's

@@ -740,9 +740,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             D.rt_has = s_rth[tid]; D.rt_ssrc = s_rts[tid]; D.rt_first_arrival = s_rta[tid]; D.rt_first_receive = s_rtr[tid];
             if (s_rtn) D.rt_nonmono = 1u;
         }
-        // tick pipelining, or a copy pass the last tick still owes (edgpu_fanout_next): this batch
-        // must not lap what that tick's fan-out (possibly still running on the other stream) reads
-        const bool guard = P.overlap || P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
+        // a copy pass the last tick still owes (edgpu_fanout_next): this batch must not lap what
+        // that tick's remaining passes read
+        const bool guard = P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
         if (guard && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
                       s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
             atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);

@@ -53,7 +53,6 @@ struct IngestParams {
                             // (default); 0 two aligned loads per word (EDGPU_INGEST_TCP)
     uint32_t ablate;        // timing experiments only (EDGPU_ABLATE bits 4-7: 16 no totals, 32 no slot
                             // copy, 64 no per-sender scans)
-    uint32_t overlap;       // check the ring against the in-flight fan-out window (fan_lo/fan_vlo)
     uint32_t host_epoch;    // != 0: the blob is a host batch the host keeps for the tick; record each
                             // packet's slot and the batch (edgpu_fanout_sources)
     TickTotals* totals;

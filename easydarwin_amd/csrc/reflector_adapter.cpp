@@ -31,8 +31,6 @@ Reflector::Reflector(const edgpu_config* cfg) {
     edgpu_config c;
     if (cfg) c = *cfg; else edgpu_config_default(&c);
     if (!c.max_batch_bytes) c.max_batch_bytes = 1ull << 30;      // 0: the engine's default (edgpu_ctx_create)
-    fOverlap = c.overlap_ticks != 0;
-    if (c.overlap_ticks) fBatchSources = false;                   // (per-descriptor sources need serial ticks)
     for (Batch& b : fBatch) {
         b.nslabs = c.max_batch_bytes / kSlab + 1;
         b.slabPend.reset(new Batch::Pend[b.nslabs]);
@@ -58,7 +56,7 @@ Reflector::~Reflector() {
         for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
             if (p) (void)edgpu_host_free(fCtx, p);
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
-    for (PinBuf* pb : {&fPinSubs, &fPinDesc, &fPinRows})
+    for (PinBuf* pb : {&fPinSubs, &fPinRows})
         if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
     edgpu_ctx_destroy(fCtx);
 }
@@ -534,71 +532,56 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     // descriptor of a sub-stream that is not an identity one, one per packet of each sender's
     // identity sub-streams (its longest one's rows serve the others, edgpu_fanout_rows)
     const uint32_t nq = res.n_substreams;
-    const uint64_t nd = st.pass_packets;
     if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
     const edgpu_substream_out* subs = (const edgpu_substream_out*)fPinSubs.p;
     if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
     fRowOf.assign(nq, 0);
     fRowDelta.assign(nq, 0);
     uint64_t nrows = 0;
-    if (fOverlap) {
-        // tick pipelining: the descriptors themselves (no arrivals, no batch sources)
-        if (sink->WantsArrivals()) return fail_with(kBadArgument, "packet arrivals need serial ticks");
-        if ((err = EnsurePinned(fPinDesc, nd * sizeof(edgpu_out_desc))) ||
-            (err = EnsurePinned(fPinRows, nd * sizeof(edgpu_packet_row))))
-            return err;
-        if ((err = edgpu_copy_to_host(fCtx, fPinDesc.p, res.desc, nd * sizeof(edgpu_out_desc)))) return err;
-        const edgpu_out_desc* d = (const edgpu_out_desc*)fPinDesc.p;
-        edgpu_packet_row* rw = (edgpu_packet_row*)fPinRows.p;
-        for (uint64_t i = 0; i < nd; i++) rw[i] = edgpu_packet_row{d[i].offset, d[i].len, d[i].packet_id, -1, EDGPU_NO_SOURCE, 0};
-        for (uint32_t q = 0; q < nq; q++) { fRowOf[q] = subs[q].desc_base; fRowDelta[q] = -(int64_t)subs[q].out_base; }
-        nrows = nd;
-    } else {
-        // the representative tick_regions gathers (the longest by bytes): its rows serve the
-        // sender's other identity sub-streams, each a suffix of it in bytes and in packets
-        fRowRep = edgpu_host::identity_reps(subs, nq);
-        fRowSel.clear();
-        for (uint32_t q = 0; q < nq; q++) {
-            const edgpu_substream_out& s = subs[q];
-            if (!s.desc_count || ((s.flags & EDGPU_SUB_IDENTITY) && fRowRep[s.sender] != q)) continue;
-            fRowSel.push_back(q);
-            fRowSel.push_back((uint32_t)nrows);
-            fRowOf[q] = (uint32_t)nrows;
-            fRowDelta[q] = -(int64_t)s.out_base;
-            nrows += s.desc_count;
-        }
-        for (uint32_t q = 0; q < nq; q++) {             // the others of a sender: a suffix of its rows
-            const edgpu_substream_out& s = subs[q];
-            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
-            const edgpu_substream_out& R = subs[fRowRep[s.sender]];
-            fRowOf[q] = fRowOf[fRowRep[s.sender]] + (R.desc_count - s.desc_count);
-            fRowDelta[q] = -(int64_t)R.out_base - (int64_t)(R.out_bytes - s.out_bytes);
-        }
-        if (nrows > 0xFFFFFFFFull) return fail_with(kRequestFailed, "tick rows exceed 2^32");
-        if ((err = EnsurePinned(fPinRows, nrows * sizeof(edgpu_packet_row)))) return err;
-        if ((err = edgpu_fanout_rows(fCtx, fRowSel.data(), (uint32_t)(fRowSel.size() / 2), (edgpu_packet_row*)fPinRows.p,
-                                     nrows, EDGPU_PTR_HOST)))
-            return err;
-        // the suffix sharing holds only if every sub-stream's first row is where its bytes start in
-        // the representative's region (a UDP datagram 4 bytes into its slot, after the interleave
-        // header room); a plan that broke it would write wrong bytes silently
-        const edgpu_packet_row* rw = (const edgpu_packet_row*)fPinRows.p;
-        for (uint32_t q = 0; q < nq; q++) {
-            const edgpu_substream_out& s = subs[q];
-            if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
-            const edgpu_substream_out& R = subs[fRowRep[s.sender]];
-            if (R.desc_count < s.desc_count || R.out_bytes < s.out_bytes ||
-                rw[fRowOf[q]].offset != R.out_base + (R.out_bytes - s.out_bytes) +
-                                            (s.transport == EDGPU_TRANSPORT_TCP ? 0u : 4u))
-                return fail_with(kRequestFailed, "identity sub-stream is not a suffix of its sender's longest");
-        }
+    // the representative tick_regions gathers (the longest by bytes): its rows serve the
+    // sender's other identity sub-streams, each a suffix of it in bytes and in packets
+    fRowRep = edgpu_host::identity_reps(subs, nq);
+    fRowSel.clear();
+    for (uint32_t q = 0; q < nq; q++) {
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count || ((s.flags & EDGPU_SUB_IDENTITY) && fRowRep[s.sender] != q)) continue;
+        fRowSel.push_back(q);
+        fRowSel.push_back((uint32_t)nrows);
+        fRowOf[q] = (uint32_t)nrows;
+        fRowDelta[q] = -(int64_t)s.out_base;
+        nrows += s.desc_count;
+    }
+    for (uint32_t q = 0; q < nq; q++) {             // the others of a sender: a suffix of its rows
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
+        const edgpu_substream_out& R = subs[fRowRep[s.sender]];
+        fRowOf[q] = fRowOf[fRowRep[s.sender]] + (R.desc_count - s.desc_count);
+        fRowDelta[q] = -(int64_t)R.out_base - (int64_t)(R.out_bytes - s.out_bytes);
+    }
+    if (nrows > 0xFFFFFFFFull) return fail_with(kRequestFailed, "tick rows exceed 2^32");
+    if ((err = EnsurePinned(fPinRows, nrows * sizeof(edgpu_packet_row)))) return err;
+    if ((err = edgpu_fanout_rows(fCtx, fRowSel.data(), (uint32_t)(fRowSel.size() / 2), (edgpu_packet_row*)fPinRows.p,
+                                 nrows, EDGPU_PTR_HOST)))
+        return err;
+    // the suffix sharing holds only if every sub-stream's first row is where its bytes start in
+    // the representative's region (a UDP datagram 4 bytes into its slot, after the interleave
+    // header room); a plan that broke it would write wrong bytes silently
+    const edgpu_packet_row* rw = (const edgpu_packet_row*)fPinRows.p;
+    for (uint32_t q = 0; q < nq; q++) {
+        const edgpu_substream_out& s = subs[q];
+        if (!s.desc_count || !(s.flags & EDGPU_SUB_IDENTITY) || fRowRep[s.sender] == q) continue;
+        const edgpu_substream_out& R = subs[fRowRep[s.sender]];
+        if (R.desc_count < s.desc_count || R.out_bytes < s.out_bytes ||
+            rw[fRowOf[q]].offset != R.out_base + (R.out_bytes - s.out_bytes) +
+                                        (s.transport == EDGPU_TRANSPORT_TCP ? 0u : 4u))
+            return fail_with(kRequestFailed, "identity sub-stream is not a suffix of its sender's longest");
     }
     const edgpu_packet_row* rows = (const edgpu_packet_row*)fPinRows.p;
     // Packets that came with the batch this tick ingested are still in its pinned blob: an identity
     // UDP sub-stream made only of them is written from there (its wire bytes are the packets') and
     // needs no readback.  The rest -- GOP replays of new outputs, earlier batches, interleaved or
     // rewritten sub-streams -- is gathered.
-    const bool useSrc = fBatchSources && fIngestedBlob != nullptr && !fOverlap;
+    const bool useSrc = fBatchSources && fIngestedBlob != nullptr;
     fSkip.assign(useSrc ? nq : 0, 0);
     if (useSrc)
         for (uint32_t q = 0; q < nq; q++) {
@@ -620,7 +603,7 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         fHostOutCap = cap;
     }
     fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) +
-                            (fOverlap ? nd * sizeof(edgpu_out_desc) : nrows * sizeof(edgpu_packet_row));
+                            nrows * sizeof(edgpu_packet_row);
     // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
     // PCIe, one pass) in up to TickParts::kMax parts of the sub-stream table, each part's regions after the
     // previous part's: with several write threads a gather thread brings part k + 1 over while the

@@ -150,8 +150,7 @@ public:
     // the receiver-report SSRC / CNAME time a track's ReflectorStream would have drawn
     int  SetSourceIdentity(uint32_t session, uint32_t track, uint32_t ssrc, int64_t cnameSecs);
     // ingest everything pushed since the last call, update the keyframe index, fan out at
-    // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order).  A sink
-    // that WantsArrivals() needs serial ticks (no edgpu_config.overlap_ticks): kBadArgument.
+    // `nowMs` and deliver every send-ready packet to `sink` (per sub-stream, in order).
     int  ReflectPackets(int64_t nowMs, OutputSink* sink);
     // threads that deliver a tick's writes (default 1; at most 64); call between ticks
     void SetWriteThreads(uint32_t n);
@@ -289,10 +288,9 @@ private:
     // readback buffers
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
-    PinBuf fPinSubs, fPinDesc, fPinRows;                    // sub-stream table, descriptors (overlap_ticks), rows
+    PinBuf fPinSubs, fPinRows;                              // sub-stream table, rows
     std::vector<uint32_t> fRowSel, fRowOf, fRowRep;         // edgpu_fanout_rows' selection, per sub-stream row start
     std::vector<int64_t> fRowDelta;
-    bool fOverlap = false;                                  // edgpu_config.overlap_ticks: no edgpu_fanout_rows
     const uint8_t* fIngestedBlob = nullptr;                 // the blob the last FlushIngest ingested (intact
                                                             // until the next one swaps it back in)
     bool fBatchSources = true;                              // EDGPU_BATCH_SOURCES=0: read every byte back

@@ -65,7 +65,6 @@ class Config(C.Structure):
         ("max_out_packets", C.c_uint32),
         ("max_batch_packets", C.c_uint32),
         ("max_batch_bytes", C.c_uint64),
-        ("overlap_ticks", C.c_uint32),
         ("reflector_rtp_info_offset_msec", C.c_uint32),
         ("ring_growth", C.c_uint32),
         ("max_ring_packets", C.c_uint32),

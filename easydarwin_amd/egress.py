@@ -38,7 +38,7 @@ def _drain():
     if _drain_lib is None:
         lib = C.CDLL(_DRAIN)
         lib.udpd_start.restype = C.c_void_p
-        lib.udpd_start.argtypes = [C.POINTER(C.c_int), C.c_int]
+        lib.udpd_start.argtypes = [C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
         lib.udpd_stop.argtypes = [C.c_void_p]
         lib.udpd_size.restype = C.c_size_t
         lib.udpd_size.argtypes = [C.c_void_p, C.c_int]
@@ -80,6 +80,8 @@ class SocketSink:
             if self.tcp_sndbuf:
                 a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, self.tcp_sndbuf)
                 b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, self.tcp_sndbuf)
+            else:           # (clamped to net.core.wmem_max) a GOP replay should not block the egress
+                a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 32 << 20)
             a.setblocking(False)
             b.setblocking(False)
             self.eg.tcp(handle, a.fileno())
@@ -101,23 +103,37 @@ class SocketSink:
     def tick(self, result, t: int):
         if self.pacing is not None:
             self.eg.clock(t)
-        # the UDP receivers drain on their own threads while the egress sends (tools/udp_drain.c)
+        # the receivers drain on their own threads while the egress sends (tools/udp_drain.c):
+        # every UDP socket, and the TCP players this tick does not hold
+        held = self.hold.get(t, set())
         keys = list(self.udp)
+        tcp = [h for h in self.tcp if self.sub_id[h] not in held]
         lib = _drain()
-        fds = (C.c_int * max(1, len(keys)))(*[self.udp[k].fileno() for k in keys])
-        h = lib.udpd_start(fds, len(keys)) if keys else None
+        n_rx = len(keys) + len(tcp)
+        fds = (C.c_int * max(1, n_rx))(*([self.udp[k].fileno() for k in keys] + [self.tcp[h][1].fileno() for h in tcp]))
+        stream = (C.c_int * max(1, n_rx))(*([0] * len(keys) + [1] * len(tcp)))
+        h = lib.udpd_start(fds, stream, n_rx) if n_rx else None
         try:
             st = self.eg.send(result)
         finally:
             if h:
                 lib.udpd_stop(h)
-                for i, k in enumerate(keys):
+                for i in range(n_rx):
                     n = lib.udpd_size(h, i)
-                    if n:
-                        b = C.create_string_buffer(n)
-                        lib.udpd_take(h, i, b)
-                        self.parts[k].append(b.raw)
-                        self.npk[k] += lib.udpd_count(h, i)
+                    if not n:
+                        continue
+                    b = C.create_string_buffer(n)
+                    lib.udpd_take(h, i, b)
+                    raw = b.raw
+                    if i >= len(keys):
+                        self.tcp[tcp[i - len(keys)]][2] += raw
+                        continue
+                    k, o = keys[i], 0
+                    while o < n:                    # one part per datagram, as drain() keeps them
+                        ln = (raw[o] << 8) | raw[o + 1]
+                        self.parts[k].append(raw[o:o + 2 + ln])
+                        o += 2 + ln
+                    self.npk[k] += lib.udpd_count(h, i)
                 lib.udpd_free(h)
         self.stats.append(st)
         for q, _sent, written, cause in self.eg.block_info():
@@ -125,7 +141,6 @@ class SocketSink:
                 continue
             h, trk, kind = self.q_of[q]
             self.blocked.append((t, self.sub_id[h], trk, kind, written))
-        held = self.hold.get(t, set())
         self.drain(skip={h for h, sid in self.sub_id.items() if sid in held})
         return st
 

@@ -191,10 +191,6 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
            pinned: bool = False, tick_info: list | None = None, slots: dict | None = None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
-    With overlap_ticks=1 in cfg, each tick's result is read only after the next tick's batch
-    has been ingested and indexed, so that ingest runs while the previous fan-out copy may
-    still be in flight (the pipelined mode's contract: results stay valid one extra tick).
-
     replica=None: subscribers join the context that ingests (the owner).
     replica="all" / "late" / "split": subscribers join a replica session on a second context,
     kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
@@ -276,7 +272,6 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         images = {}
         pending, joins, stats = [], [], []
         tick_info = tick_info if tick_info is not None else []
-        lag = bool(cfg.get("overlap_ticks")) and replica is None
         unread = []                         # (ctx, tag, result, t, budgets) of ticks not read back yet
 
         def drain():
@@ -359,8 +354,8 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
         sink = None
         if sockets is not None:
             from .egress import SocketSink
-            if any(ev[0] == BLOCK for ev in trace.events) or lag:
-                raise ValueError("socket egress replays take neither BLOCK events nor overlap_ticks")
+            if any(ev[0] == BLOCK for ev in trace.events):
+                raise ValueError("socket egress replays take no BLOCK events")
             kw = {k: v for k, v in sockets.items() if k not in ("report", "stats")}
             if kw.get("pacing") is not None:        # the gate's reflector prefs are the trace's
                 kw["pacing"] = dict({"bucket_delay_ms": int(pv["reflector_bucket_offset_delay_msec"]),
@@ -401,15 +396,13 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             for tr in range(sess_tracks[s]):
                 for k in (0, 1):
                     images[(tag, h, tr, k)] = []
-        if lag and any(ev[0] == BLOCK for ev in trace.events):
-            raise ValueError("backpressure reports need each tick read before the next ingest")
 
         def outputs_of(s):
             return [th for th, meta in subs_meta.items() if meta[1] == s and th not in gone]
 
         def end_session(s, kill=False):
             """The owner session ends; its replicas with it (their subscribers too with a kill)."""
-            drain()                         # (overlap_ticks: a session goes only after its last tick is read)
+            drain()                         # (a session goes only after its last tick is read)
             if link is not None:
                 link.remove(gen[s], kill_outputs=kill)
                 rsess.pop(s, None)
@@ -525,8 +518,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
                     if replica != "split":
                         unread.pop()                 # (no subscribers on the owner)
                     unread.append((rep, 1, rep.fanout(t), t, by_handle))
-                if not lag:
-                    drain()
+                drain()
         drain()
         wire = None
         if sink is not None:

@@ -104,12 +104,6 @@ typedef struct edgpu_config {
     uint32_t max_out_packets;               /* descriptor capacity per tick (1 Mi)       */
     uint32_t max_batch_packets;             /* ingest batch capacity (1 Mi)              */
     uint64_t max_batch_bytes;               /* ingest blob capacity (1 GiB)              */
-    /* 1: tick pipelining.  The fan-out copy of tick t runs on a second HIP stream, so the
-     * next edgpu_ingest / edgpu_keyframe_index overlap it; arena, descriptors and the
-     * sub-stream table are double-buffered (a tick's result stays valid until the second
-     * edgpu_fanout after it).  Each sender ring must then hold the in-flight fan-out window
-     * plus one ingest batch, else EDGPU_RING_OVERFLOW.  0 (default): one stream. */
-    uint32_t overlap_ticks;
     uint32_t reflector_rtp_info_offset_msec; /* RTP-Info first packet: within over-buffer minus
                                                this (ReflectorStream.cpp:109-110); default 500,
                                                EDGPU_FALSE for an offset of 0 */
@@ -197,8 +191,11 @@ typedef struct edgpu_substream_out {
 #define EDGPU_SUB_IDENTITY 1u
 #define EDGPU_SUB_NEW      2u
 
-/* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout (the second
- * next one with overlap_ticks). */
+/* Result of edgpu_fanout.  Device pointers, valid until the next edgpu_fanout.  Ticks run in
+ * order on one stream: a tick's fan-out reads the rings after its own ingest and before the
+ * next one (the engine had a pipelined mode that overlapped the next ingest with the fan-out;
+ * it was dropped because backpressure reports and arrivals of the overlapped batch arrived a
+ * tick late -- the pushers' H2D copies still overlap through edgpu_ingest_host). */
 typedef struct edgpu_fanout_result {
     const uint8_t*              arena;          /* device */
     const edgpu_out_desc*       desc;           /* device */
@@ -443,8 +440,7 @@ int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
  * those fail with EDGPU_ERR while a pass is owed (session removal reads that from the device when
  * the host has not read the tick's stats; edgpu_counters.lost_passes counts passes a tick still
  * owed when the next tick was planned).  edgpu_ingest / edgpu_ingest_interleaved fail the same
- * way while the host knows of an owed pass; before it has read the stats an ingest may run (the
- * overlap_ticks pattern), and a batch that would lap the tick's window in a ring while a pass is
+ * way while the host knows of an owed pass; before it has read the stats an ingest may run, and a batch that would lap the tick's window in a ring while a pass is
  * owed fails the ring (EDGPU_RING_OVERFLOW) instead of corrupting the pass.  Subscribers may come and go between passes: the passes keep the tick's table (rows
  * added since are not in it, rows of removed subscribers still deliver the tick, and their rows
  * are reused only from the next tick).  Backpressure reports (edgpu_fanout_blocked) take

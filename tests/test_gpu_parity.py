@@ -7,7 +7,7 @@ import os
 import pytest
 
 from easydarwin_amd.replay import replay
-from easydarwin_amd.trace import BLOCK, Trace, capture_summary, read_capture
+from easydarwin_amd.trace import Trace, capture_summary, read_capture
 from scenarios import MODULE_SCENARIOS, SCENARIOS
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -30,15 +30,10 @@ def _trace(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [0, 1], ids=["serial", "overlap"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
-def test_engine_matches_reference(name, overlap):
-    """overlap=1: tick pipelining (edgpu_config.overlap_ticks) with each tick read back only
-    after the next batch was ingested, so ingest runs beside the in-flight fan-out copy."""
+def test_engine_matches_reference(name):
     tr = _trace(name)
-    if overlap and any(ev[0] == BLOCK for ev in tr.events):
-        pytest.skip("backpressure reports need each tick read back before the next ingest")
-    cap, stats = replay(tr, overlap_ticks=overlap)
+    cap, stats = replay(tr)
     fix = _fixture(name)
     got = capture_summary(read_capture(cap))
     want = fix["substreams"]

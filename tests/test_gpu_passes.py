@@ -17,7 +17,7 @@ import pytest
 
 from easydarwin_amd import edgpu
 from easydarwin_amd.replay import replay
-from easydarwin_amd.trace import BLOCK, PKT, capture_summary, read_capture
+from easydarwin_amd.trace import PKT, capture_summary, read_capture
 from scenarios import SCENARIOS, random_scenario
 from test_gpu_parity import _fixture, _trace
 
@@ -48,12 +48,9 @@ def _check_split(info, arena, desc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [0, 1], ids=["serial", "overlap"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
-def test_split_ticks_match_reference(name, overlap):
+def test_split_ticks_match_reference(name):
     tr = _trace(name)
-    if overlap and any(ev[0] == BLOCK for ev in tr.events):
-        pytest.skip("backpressure reports need each tick read back before the next ingest")
     info = []
     cap, _ = replay(tr, tick_info=info)
     want = _fixture(name)["capture_sha256"]
@@ -61,7 +58,7 @@ def test_split_ticks_match_reference(name, overlap):
     arena, desc = _small(info)
     for a, d in ((arena, desc), (2 * arena, 2 * desc), (arena, 1 << 20), (1 << 28, desc)):
         got_info = []
-        got, _ = replay(tr, tick_info=got_info, overlap_ticks=overlap, out_arena_bytes=a, max_out_packets=d)
+        got, _ = replay(tr, tick_info=got_info, out_arena_bytes=a, max_out_packets=d)
         if got != cap:
             g, w = capture_summary(read_capture(got)), capture_summary(read_capture(cap))
             bad = [k for k in w if g.get(k) != w[k]]

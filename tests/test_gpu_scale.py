@@ -48,8 +48,7 @@ def _run_slice(n_sess, subs, ticks, seed=7):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [0, 1], ids=["serial", "overlap"])
-def test_workload_slice_matches_oracle(oracle_bins, overlap):
+def test_workload_slice_matches_oracle(oracle_bins):
     n_sess, subs, ticks = 8, 3, 4
     fleet, batches, mats = _run_slice(n_sess, subs, ticks)
     # trace for the oracle
@@ -75,13 +74,12 @@ def test_workload_slice_matches_oracle(oracle_bins, overlap):
         subprocess.run([oracle_bins["port"], p, c], check=True)
         want = open(c, "rb").read()
     from easydarwin_amd.replay import replay
-    got, _ = replay(tr, overlap_ticks=overlap)
+    got, _ = replay(tr)
     assert got == want
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [0, 1], ids=["serial", "overlap"])
-def test_c2_full_size_properties(overlap):
+def test_c2_full_size_properties():
     n_sess, subs, ticks = 1024, 16, 3
     fleet, batches, mats = _run_slice(n_sess, subs, ticks, seed=11)
     max_pk = max(b["n"] for b in batches)
@@ -89,7 +87,7 @@ def test_c2_full_size_properties(overlap):
     with edgpu.Context(video_ring_packets=8192, video_ring_bytes=16 << 20, other_ring_packets=256,
                        other_ring_bytes=64 << 10, out_arena_bytes=int(max_bytes * subs * 1.05) // 16 * 16,
                        max_out_packets=int(max_pk * subs * 1.05), max_batch_packets=max_pk + 1,
-                       max_batch_bytes=max_bytes + 16, overlap_ticks=overlap) as ctx:
+                       max_batch_bytes=max_bytes + 16) as ctx:
         for _ in range(n_sess):
             s = ctx.session_add(fleet.sdp())
             for _k in range(subs):

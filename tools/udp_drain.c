@@ -4,8 +4,10 @@
  * buffer net.core.rmem_max allows, and loopback UDP drops what does not fit, as UDP does; so each
  * receiver socket gets a thread that takes datagrams (recvmmsg) as they arrive, from before the
  * egress starts sending until after it returns.  Each socket's datagrams are kept in arrival
- * order as BE16(len) + bytes, the capture's UDP wire image (easydarwin_amd/trace.py).
- *   udpd_start(fds, n) -> handle;  udpd_stop(handle) (joins, then drains what is left);
+ * order as BE16(len) + bytes, the capture's UDP wire image (easydarwin_amd/trace.py).  A TCP
+ * player's socket (stream[i] != 0: the reader end of its socketpair) is drained the same way, its
+ * bytes kept as they come: a GOP replay past the socket buffer would otherwise block the egress.
+ *   udpd_start(fds, stream, n) -> handle;  udpd_stop(handle) (joins, then drains what is left);
  *   udpd_size(handle, i) / udpd_count(handle, i) / udpd_take(handle, i, out): the image of fds[i],
  *   its datagram count;  udpd_free(handle). */
 #define _GNU_SOURCE
@@ -16,11 +18,12 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <time.h>
 
 enum { kBatch = 64, kMax = 65536 };
 
 typedef struct {
-    int fd;
+    int fd, stream;
     uint8_t* slots;                 /* kBatch receive buffers of kMax bytes */
     uint8_t* buf;
     size_t len, cap, count;
@@ -44,9 +47,29 @@ static void put(Rx* r, const uint8_t* d, size_t n) {
     r->count++;
 }
 
-/* every datagram waiting now; returns how many were taken */
+static void put_raw(Rx* r, const uint8_t* d, size_t n) {
+    if (r->len + n > r->cap) {
+        size_t c = r->cap ? r->cap * 2 : (1 << 20);
+        while (c < r->len + n) c *= 2;
+        r->buf = (uint8_t*)realloc(r->buf, c);
+        r->cap = c;
+    }
+    memcpy(r->buf + r->len, d, n);
+    r->len += n;
+}
+
+/* every datagram (stream: every byte) waiting now; returns how many reads took something */
 static int take(Rx* r) {
     uint8_t* bufs = r->slots;
+    if (r->stream) {
+        int total = 0;
+        for (;;) {
+            const ssize_t n = recv(r->fd, bufs, (size_t)kBatch * kMax, MSG_DONTWAIT);
+            if (n <= 0) return total;
+            put_raw(r, bufs, (size_t)n);
+            total++;
+        }
+    }
     struct mmsghdr m[kBatch];
     struct iovec io[kBatch];
     int total = 0;
@@ -65,21 +88,31 @@ static int take(Rx* r) {
     }
 }
 
+/* Spins while datagrams keep coming and for 20 ms after the last one: a sleeping (or yielding)
+ * receiver gets the CPU back later than the sender needs to fill a receive buffer clamped to
+ * net.core.rmem_max (a sched_yield measured 1.6 ms beside a sending thread); then waits in poll.
+ * Needs a core per receiver beside the sender's (the GPU box's CPU share has them). */
 static void* loop(void* arg) {
     Rx* r = (Rx*)arg;
     struct pollfd p = {r->fd, POLLIN, 0};
+    struct timespec last, now;
+    clock_gettime(CLOCK_MONOTONIC, &last);
     while (!r->stop) {
-        if (take(r) == 0) (void)poll(&p, 1, 1);
+        if (take(r) > 0) { clock_gettime(CLOCK_MONOTONIC, &last); continue; }
+        clock_gettime(CLOCK_MONOTONIC, &now);
+        const long idle_us = (now.tv_sec - last.tv_sec) * 1000000L + (now.tv_nsec - last.tv_nsec) / 1000;
+        if (idle_us >= 20000) (void)poll(&p, 1, 1);
     }
     return NULL;
 }
 
-void* udpd_start(const int* fds, int n) {
+void* udpd_start(const int* fds, const int* stream, int n) {
     Drain* d = (Drain*)calloc(1, sizeof(Drain));
     d->rx = (Rx*)calloc((size_t)n, sizeof(Rx));
     d->n = n;
     for (int i = 0; i < n; i++) {
         d->rx[i].fd = fds[i];
+        d->rx[i].stream = stream ? stream[i] : 0;
         d->rx[i].slots = (uint8_t*)malloc((size_t)kBatch * kMax);
         pthread_create(&d->rx[i].th, NULL, loop, &d->rx[i]);
     }
@@ -96,7 +129,7 @@ void udpd_stop(void* h) {
 }
 
 size_t udpd_size(void* h, int i) { return ((Drain*)h)->rx[i].len; }
-size_t udpd_count(void* h, int i) { return ((Drain*)h)->rx[i].count; }
+size_t udpd_count(void* h, int i) { return ((Drain*)h)->rx[i].count; }   /* datagrams */
 
 void udpd_take(void* h, int i, uint8_t* out) {
     Rx* r = &((Drain*)h)->rx[i];
