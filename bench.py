@@ -627,6 +627,9 @@ def main():
     in_bytes = c1["fanout_in_bytes"] - c0["fanout_in_bytes"]
     launches = c1["fanout_launches"] - c0["fanout_launches"]
     alg_bytes = out_bytes + in_bytes + 16 * relayed      # SURVEY.md §8.d per-launch definition
+    per_step = {"kernel_launches": round((c1["kernel_launches"] - c0["kernel_launches"]) / steps, 2),
+                "host_syncs": round((c1["host_syncs"] - c0["host_syncs"]) / steps, 2),
+                "timing_events": 2 if not args.all_timing_events else None}
 
     dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None,
                                           force=force_pg)
@@ -737,6 +740,7 @@ def main():
         # which times the reference's ReflectPackets apart from its PushPacket
         "reflect_loop": ({"relayed_per_s": round(relayed / max(launches, 1) / (float(np.mean(k_tick)) / 1e3), 1),
                           "timing": "tick_plan_plus_fanout kernel time per step"} if k_tick else None),
+        "per_step": per_step,
         "timing_events": ("every kernel's, inside the timed steps" if args.all_timing_events else
                           f"the fan-out copy kernel's pair inside the timed steps; ingest, keyframe and plan "
                           f"from {extra} steps after them"),

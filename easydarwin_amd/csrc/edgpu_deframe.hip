@@ -733,11 +733,11 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
 
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
     if (p.nchunks)
-        hipLaunchKernelGGL(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
+        EDGPU_LAUNCH(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
                            dim3(64 * kWalkWaves), 0, st, p);
-    hipLaunchKernelGGL(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
-    hipLaunchKernelGGL(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
-    hipLaunchKernelGGL(k_tcp_finish, dim3(p.ngroups), dim3(64), 0, st, p);
+    EDGPU_LAUNCH(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
+    EDGPU_LAUNCH(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
+    EDGPU_LAUNCH(k_tcp_finish, dim3(p.ngroups), dim3(64), 0, st, p);
     return hipGetLastError();
 }
 

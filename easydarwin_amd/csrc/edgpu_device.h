@@ -268,8 +268,10 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long relayed_packets;
     unsigned long long relayed_bytes;
     unsigned long long arena_bytes;
-    unsigned long long ingested_packets;
-    unsigned long long ingested_bytes;
+    // the last batch's ingest counters, by ingest parity: k_ingest adds into slot seq & 1 and its
+    // workgroup 0 zeroes the other slot for the next ingest (no reset launch, no "last workgroup"
+    // round trip)
+    unsigned long long ing_pk[2], ing_b[2];
     int status;
     unsigned int nwork;
     // cumulative (never reset)
@@ -281,9 +283,6 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     int ingest_status;              // sticky: an ingest lapped data an in-flight fan-out reads
     unsigned int fan_next;          // dynamic fan-out variants: next work item to claim (per tick)
     unsigned int _pad;
-    // the cumulative ingest counters at the last index update: ingested_* = cum - mark, set by
-    // the keyframe index after every ingest (no reset launch before the ingest)
-    unsigned long long ingest_mark_packets, ingest_mark_bytes;
     // measurement builds: the copy kernel's workgroups' first start / first and last exit
     // (s_memrealtime, 100 MHz) -- the tail of the dynamic schedule (EDGPU_FAN_TAIL=1 prints it)
     unsigned long long fan_t0_min, fan_done_min, fan_done_max;

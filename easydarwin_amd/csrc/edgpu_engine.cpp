@@ -27,7 +27,6 @@
 
 namespace edgpu {
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st);
-hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st);
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st);
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
                                     uint32_t n, hipStream_t st);
@@ -335,8 +334,6 @@ struct edgpu_ctx {
     uint32_t* d_seg = nullptr;
     uint32_t* d_seg_sess = nullptr;
     uint8_t* d_blob = nullptr;
-    uint32_t* d_pflags = nullptr;
-    uint64_t* d_pidx = nullptr;
     CopyJob* d_jobs = nullptr;
     // pinned-host ingest (EDGPU_PTR_PINNED): two device staging sets filled on `h2d`
     struct PinStage {
@@ -416,6 +413,9 @@ struct edgpu_ctx {
     hipEvent_t wd_ev = nullptr;
     bool wedged = false;
     uint64_t watchdog_timeouts = 0;
+    uint32_t ing_slot = 0;          // the last ingest's counter slot (TickTotals.ing_pk)
+    uint64_t kernel_launches = 0;   // edgpu_counters (LaunchScope)
+    uint64_t host_syncs = 0;        // host waits on the GPU (wsync / wsync_event)
     uint64_t ring_bytes = 0;                    // device bytes of the live senders' rings
 };
 
@@ -430,6 +430,7 @@ struct edgpu_ctx {
 // tick succeeds).  edgpu_ctx_destroy waits without a bound.  watchdog_ms = EDGPU_FALSE: unbounded
 // waits (hipStreamSynchronize), as before.
 static hipError_t wsync_event(edgpu_ctx* x, hipEvent_t ev) {
+    x->host_syncs++;
     if (!x->cfg.watchdog_ms) return hipEventSynchronize(ev);
     using Clk = std::chrono::steady_clock;
     const Clk::time_point t0 = Clk::now(), deadline = t0 + std::chrono::milliseconds(x->cfg.watchdog_ms);
@@ -448,7 +449,7 @@ static hipError_t wsync(edgpu_ctx* x, hipStream_t st) {
         if (hipEventQuery(x->wd_ev) == hipErrorNotReady) return hipErrorLaunchTimeOut;
         x->wedged = false;
     }
-    if (!x->cfg.watchdog_ms) return hipStreamSynchronize(st);
+    if (!x->cfg.watchdog_ms) { x->host_syncs++; return hipStreamSynchronize(st); }
     hipError_t e = hipEventRecord(x->wd_ev, st);
     if (e != hipSuccess) return e;
     e = wsync_event(x, x->wd_ev);
@@ -465,7 +466,20 @@ static int device_enter(edgpu_ctx* x) {
     }
     return EDGPU_OK;
 }
+// Adds the kernels an API call launched (on this thread, EDGPU_LAUNCH) to the context's count;
+// only the outermost call of the thread counts (API functions call each other)
+struct LaunchScope {
+    static thread_local int depth;
+    edgpu_ctx* x;
+    uint64_t start;
+    explicit LaunchScope(edgpu_ctx* c) : x(c), start(tl_launches) { depth++; }
+    ~LaunchScope() {
+        if (--depth == 0) x->kernel_launches += tl_launches - start;
+    }
+};
+thread_local int LaunchScope::depth = 0;
 #define DEVICE_ENTER(x)                                   \
+    LaunchScope _edgpu_launch_scope(x);                   \
     do {                                                  \
         if (int _r = device_enter(x)) return _r;          \
     } while (0)
@@ -561,8 +575,6 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     if (dmalloc(&x->d_desc, sizeof(edgpu_pkt_desc) * (size_t)c.max_batch_packets) != hipSuccess) return bad("desc staging");
     if (dmalloc(&x->d_seg, sizeof(uint32_t) * ((size_t)c.max_batch_packets + 1)) != hipSuccess) return bad("seg staging");
     if (dmalloc(&x->d_seg_sess, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("seg staging");
-    if (dmalloc(&x->d_pflags, sizeof(uint32_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pflags");
-    if (dmalloc(&x->d_pidx, sizeof(uint64_t) * (size_t)c.max_batch_packets) != hipSuccess) return bad("pidx");
     if (dmalloc(&x->d_jobs, sizeof(CopyJob) * (size_t)c.max_batch_packets) != hipSuccess) return bad("jobs");
     if (dmalloc(&x->d_arena, c.out_arena_bytes) != hipSuccess) return bad("fan-out arena");
     if (dmalloc(&x->d_out_desc, sizeof(edgpu_out_desc) * (size_t)c.max_out_packets) != hipSuccess) return bad("descriptors");
@@ -615,7 +627,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     if (x->d_tcp_tot) (void)hipFree(x->d_tcp_tot);
     if (x->d_tcp_raw) (void)hipFree(x->d_tcp_raw);
     if (x->d_img_status) (void)hipFree(x->d_img_status);
-    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_pflags, (void*)x->d_pidx, (void*)x->d_jobs,
+    for (void* p : {(void*)x->d_desc, (void*)x->d_seg, (void*)x->d_seg_sess, (void*)x->d_jobs,
                     (void*)x->d_blob, (void*)x->d_arena, (void*)x->d_out_desc, (void*)x->d_totals, (void*)x->d_grow})
         if (p) (void)hipFree(p);
     for (auto& w : x->hist) for (auto& s : w) for (auto& e : s) if (e) (void)hipEventDestroy(e);
@@ -1523,21 +1535,30 @@ static bool hist_pair(const edgpu_ctx* x, int w, uint32_t seq, hipEvent_t* a, hi
     return true;
 }
 
+// The active sub-stream rows grouped by sender, each sender's in row order (sub_index), every
+// sender's [begin, end) into it (sub_range) and each row's position (sub_pos): a counting sort by
+// sender, linear in rows + senders (a subscriber joining or leaving rebuilds it before the next
+// fan-out: at 2-ms ticks with players coming and going that is most ticks).
 static int rebuild_index(edgpu_ctx* x) {
     const uint32_t nsub = (uint32_t)x->sub_sender.size();
-    std::vector<uint32_t> idx;
-    idx.reserve(nsub);
-    for (uint32_t i = 0; i < nsub; i++) if (x->sub_active[i]) idx.push_back(i);
-    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return x->sub_sender[a] < x->sub_sender[b]; });
     std::vector<uint32_t> range(2 * (size_t)x->nsenders, 0);
-    for (uint32_t k = 0; k < idx.size();) {
-        uint32_t s = x->sub_sender[idx[k]], e = k;
-        while (e < idx.size() && x->sub_sender[idx[e]] == s) e++;
-        range[2 * s] = k; range[2 * s + 1] = e;
-        k = e;
+    for (uint32_t i = 0; i < nsub; i++)                     // rows per sender (in range[2s + 1])
+        if (x->sub_active[i]) range[2 * (size_t)x->sub_sender[i] + 1]++;
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < x->nsenders; s++) {
+        const uint32_t c = range[2 * (size_t)s + 1];
+        range[2 * (size_t)s] = total;
+        range[2 * (size_t)s + 1] = total;                   // the fill cursor; ends at begin + count
+        total += c;
     }
+    std::vector<uint32_t> idx(total);
     std::vector<uint32_t> pos(nsub, 0xFFFFFFFFu);
-    for (uint32_t k = 0; k < idx.size(); k++) pos[idx[k]] = k;
+    for (uint32_t i = 0; i < nsub; i++)
+        if (x->sub_active[i]) {
+            const uint32_t k = range[2 * (size_t)x->sub_sender[i] + 1]++;
+            idx[k] = i;
+            pos[i] = k;
+        }
     HIP_CHECK(x->d_sub_index.reserve(std::max<size_t>(idx.size(), 1), x->stream));
     HIP_CHECK(x->d_fansub.reserve(std::max<size_t>(idx.size(), 1), x->stream));
     HIP_CHECK(x->d_sub_pos.reserve(std::max<size_t>(nsub, 1), x->stream));
@@ -1571,9 +1592,10 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
-    p.pflags = x->d_pflags; p.pidx = x->d_pidx;
     p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.totals = x->d_totals;
+    x->ing_slot ^= 1u;
+    p.ing_slot = x->ing_slot;
     p.recv_time = x->cfg.reflector_use_in_packet_receive_time;
     // sMaxFuturePacketMSec = sMaxFuturePacketSec * 1000 in UInt32 (ReflectorStream.cpp:113)
     p.max_future_ms = (int64_t)(uint32_t)(x->cfg.reflector_in_packet_max_receive_sec * 1000u);
@@ -1909,21 +1931,10 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
     if (!x) return fail(EDGPU_BAD_ARGUMENT, "ctx is NULL");
     if (!x->pending) return fail(EDGPU_ERR, "no ingested batch pending a keyframe index");
     DEVICE_ENTER(x);
-    KeyframeParams p;
-    p.seg_off = x->pend_seg; p.seg_sess = x->pend_seg_sess; p.pflags = x->d_pflags; p.pidx = x->d_pidx;
-    p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.totals = x->d_totals;
-    // the index starts where the ingest it indexes ended when the host did nothing in between
-    // (that point is already recorded: an event record costs the GPU ~5 us of idle), else here
-    const uint32_t kslot = x->hist_n[3] % edgpu_ctx::kHist;
-    if (x->kf_share && x->last_seq[2] + 1 == x->hist_n[2]) {
-        x->kf_from[kslot] = x->last_seq[2];
-    } else {
-        x->kf_from[kslot] = edgpu_ctx::kOwnStart;
-        HIP_CHECK(hist_mark(x, 3, 0));
-    }
+    // The index itself ran inside k_ingest (each workgroup walks its segment's packets through it
+    // in arrival order once they are enqueued): this call only closes the batch -- one kernel
+    // launch and its ~5 us of dependent-launch gap less per tick than a separate k_keyframe.
     x->kf_share = false;
-    HIP_CHECK(launch_keyframe(p, x->pend_nseg, x->stream));
-    HIP_CHECK(hist_mark(x, 3, 1));
     if (x->aux) {       // the next deframe (on aux) rewrites the segment tables this index reads
         HIP_CHECK(hipEventRecord(x->ev_kf, x->stream));
         x->kf_recorded = true;
@@ -1932,7 +1943,6 @@ int edgpu_keyframe_index(edgpu_ctx* x) {
         HIP_CHECK(hipEventRecord(x->pin[x->pend_stage].consumed, x->stream));
         x->pend_stage = -1;
     }
-    x->timed_keyframe = true;
     x->pending = false;
     return EDGPU_OK;
 }
@@ -2091,8 +2101,8 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
     out->relayed_packets = t.relayed_packets;
     out->relayed_bytes = t.relayed_bytes;
     out->arena_bytes = t.arena_bytes;
-    out->ingested_packets = t.ingested_packets;
-    out->ingested_bytes = t.ingested_bytes;
+    out->ingested_packets = t.ing_pk[x->ing_slot];
+    out->ingested_bytes = t.ing_b[x->ing_slot];
     out->status = t.status ? t.status : t.ingest_status;
     out->_pad = t.nwork;
     const uint32_t slot = x->pass_ord & 1u;
@@ -2229,6 +2239,8 @@ int edgpu_counters_get(edgpu_ctx* x, edgpu_counters* out) {
     out->ring_grows = x->ring_grows;
     out->ring_pool_bytes = x->rings.held;
     out->watchdog_timeouts = x->watchdog_timeouts;
+    out->kernel_launches = x->kernel_launches;
+    out->host_syncs = x->host_syncs;
     out->ring_grow_failures = x->grow_failures;
     out->ring_bytes = x->ring_bytes;
     out->senders = x->nsenders;
@@ -2546,7 +2558,7 @@ int edgpu_session_key_update(edgpu_ctx* x, const uint32_t* sessions, uint32_t n)
     if (!n) return EDGPU_OK;
     DEVICE_ENTER(x);
     static const uint32_t one = 1;
-    // on the stream the keyframe index runs on: the next batch's k_keyframe reads it
+    // on the context stream: the next batch's k_ingest reads it
     for (uint32_t i = 0; i < n; i++)
         HIP_CHECK(hipMemcpyAsync(&x->d_sessions.ptr[sessions[i]].video_key_flag, &one, sizeof(one), hipMemcpyHostToDevice,
                                  x->stream));

@@ -4,11 +4,12 @@
 //                   (ReflectorStream.cpp:529-576, 1769-2010): clamp (Q11), UDP-RTCP SR gate
 //                   (Q14), SSRC latch filter (Q13, ReflectorStream.cpp:1732-1767), per-stream
 //                   packet ids, enqueue into the sender's HBM rings, key-frame candidate parse
-//                   (IsKeyFrameFirstPacket, ReflectorStream.cpp:1403-1513).
+//                   (IsKeyFrameFirstPacket, ReflectorStream.cpp:1403-1513), and the key
+//                   pointer update + session-wide audio anchor (ReflectorStream.cpp:1876-1934:
+//                   wave 0 of the workgroup, 64 packets per step, ballot + last-set-bit instead
+//                   of the reference's per-packet branch chain; it was a kernel of its own,
+//                   k_keyframe, until round 6).
 //                   One 256-thread workgroup per session segment, one packet per lane.
-//   k_keyframe      key pointer update and session-wide audio anchor (ReflectorStream.cpp:
-//                   1876-1934): one wave per session, 64 packets per step, ballot +
-//                   last-set-bit instead of the reference's per-packet branch chain.
 //   k_plan_*        ReflectPackets' per-tick decisions (ReflectorStream.cpp:1024-1136):
 //                   new-output start (key pointer, else GetClientBufferStartPacketOffset),
 //                   per-sub-stream range, bookmark and last-id commit, output offsets.
@@ -315,6 +316,7 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
 // EDGPU_INGEST_DEPTH=2 for A/B runs
 // THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
 // for A/B: one round for a C2 session's ~375 packets per tick)
+
 template <uint32_t DEPTH, int THREADS = kIngestThreads>
 // waves_per_eu(4): the kernel needs 4 waves per SIMD (4 resident 256-thread sessions per CU), and
 // the interleaved copy's four frames in flight fit 128 VGPRs that way
@@ -352,6 +354,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ int64_t s_rta[kMaxSendersPerSession];
     __shared__ uint64_t s_rtr[kMaxSendersPerSession];
     __shared__ uint32_t s_rtn;
+    // the keyframe index (ReflectorSocket::ProcessPacket's key and audio-anchor steps,
+    // ReflectorStream.cpp:1876-1934), folded in: each sender's key pointer; per chunk each wave's
+    // last key / audio event (bit0 any, bit1 it was a key) and, per sender, the newest packet that
+    // sets its key pointer as (lane + 1) << 52 | queue index (0: none)
+    __shared__ int64_t s_key[kMaxSendersPerSession];
+    __shared__ uint32_t s_wev[NW];
+    __shared__ unsigned long long s_klast[kMaxSendersPerSession];
     // interleaved ingest: the session's chunk table (frame end of each chunk, the recorded
     // candidate or kTcpNone) and its reads, for every lane's frame lookup
     constexpr uint32_t kLdsChunks = 256, kLdsReads = 64;
@@ -378,6 +387,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         s_valid[tid] = D.valid_ssrc; s_lastv[tid] = D.last_valid_s; s_lastnz[tid] = D.last_nonzero;
         s_flags[tid] = D.flags; s_pkmask[tid] = D.pk_mask; s_wmask[tid] = D.word_mask;
         s_meta[tid] = D.meta; s_ring[tid] = D.ring;
+        s_key[tid] = D.key;
+        s_klast[tid] = 0ull;
         if (P.recv_time) { s_rth[tid] = D.rt_has; s_rts[tid] = D.rt_ssrc; s_rta[tid] = D.rt_first_arrival; s_rtr[tid] = D.rt_first_receive; }
     }
     if (tid == 0) s_rtn = 0;
@@ -389,7 +400,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __syncthreads();
 
     uint64_t in_pk = 0, in_bytes = 0;
+    // ReflectorSession::fHasVideoKeyFrameUpdate before the chunk (every thread keeps the same)
+    bool kflag = S.video_key_flag != 0;
+    constexpr unsigned long long kQiMask = (1ull << 52) - 1;
     for (uint32_t base = b; base < e; base += THREADS) {
+        // the last chunk's newest key-pointer packets (its atomics are behind the last barrier)
+        if (tid < (int)nsnd && s_klast[tid]) { s_key[tid] = (int64_t)(s_klast[tid] & kQiMask); s_klast[tid] = 0ull; }
         const uint32_t n = min((uint32_t)THREADS, e - base);
         const uint32_t i = base + tid;
         const bool valid = (uint32_t)tid < n;
@@ -616,6 +632,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         if (nz) atomicMax(&c_last[ls], tid << 10 | (int)my_rank);
         uint64_t idx = 0, vb = 0;
+        bool kev_key = false, kev_aud = false;
         if (acc) {
             idx = s_head[ls] + my_rank;
             vb = s_vbyte[ls] + my_slotpre;
@@ -633,16 +650,32 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len0 >= 20 &&
                              ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len0)
                                                           : key_frame_first_packet(pk, len0));
-            const bool aud = by_port_rtp && (fl & kSndAudio);
-            P.pflags[i] = 1u | (key ? 2u : 0u) | (aud ? 4u : 0u) | ls << 8;
-            P.pidx[i] = idx;
-        } else if (valid) {
-            P.pflags[i] = 0;
-            P.pidx[i] = 0;
+            kev_key = key;
+            kev_aud = by_port_rtp && (fl & kSndAudio);
         }
+        // ---- keyframe index, part 1: each wave's key / audio events in arrival order (ballots) ----
+        const uint64_t kK = __ballot(kev_key), kE = kK | __ballot(kev_aud);
+        if ((tid & 63) == 0)
+            s_wev[tid >> 6] = kE ? 1u | (uint32_t)((kK >> (63 - __clzll((long long)kE))) & 1ull) << 1 : 0u;
         p_slotb[tid] = slotb;
         p_vb[tid] = vb;
         __syncthreads();
+        // ---- keyframe index, part 2: a video key packet moves its sender's key pointer; an audio
+        // packet anchors its sender's when the last key / audio event before it was a key packet
+        // (none in the chunk before it: the session's flag); the newest such packet per sender wins
+        // (Q5).  A lane's previous event: its wave's lower lanes, else the earlier waves' last ----
+        {
+            const int lane = tid & 63, wid = tid >> 6;
+            bool fin = kflag;
+            for (int w = 0; w < wid; w++)
+                if (s_wev[w] & 1u) fin = (s_wev[w] >> 1) & 1u;
+            const uint64_t below = lane ? (kE & ((1ull << lane) - 1)) : 0ull;
+            const bool anchor = kev_aud && (below ? ((kK >> (63 - __clzll((long long)below))) & 1ull) != 0 : fin);
+            if (kev_key || anchor)
+                atomicMax(&s_klast[ls], (unsigned long long)(tid + 1) << 52 | (idx & kQiMask));
+            for (int w = 0; w < NW; w++)                              // the flag after the chunk
+                if (s_wev[w] & 1u) kflag = (s_wev[w] >> 1) & 1u;
+        }
         // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
         if (EDGPU_ABL(P) & 32u) {
@@ -735,6 +768,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         SenderDev& D = P.senders[S.first_sender + tid];
         if (P.host_epoch) { D.batch_lo = D.head; D.batch_epoch = P.host_epoch; }   // (the head before the batch)
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
+        D.key = s_klast[tid] ? (int64_t)(s_klast[tid] & kQiMask) : s_key[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
         if (P.recv_time) {
             D.rt_has = s_rth[tid]; D.rt_ssrc = s_rts[tid]; D.rt_first_arrival = s_rta[tid]; D.rt_first_receive = s_rtr[tid];
@@ -748,6 +782,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);
     }
     if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];
+    if (tid == 0) P.sessions[P.seg_sess[seg]].video_key_flag = kflag ? 1u : 0u;
     // block totals
     uint64_t t1, t2;
     const uint64_t a1 = block_exclusive_scan<uint64_t, NW>(in_pk, scan64, t1);
@@ -756,7 +791,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid == 0 && !(EDGPU_ABL(P) & 16u)) {
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
+        atomicAdd(&P.totals->ing_pk[P.ing_slot], (unsigned long long)t1);
+        atomicAdd(&P.totals->ing_b[P.ing_slot], (unsigned long long)t2);
     }
+    if (seg == 0 && tid == 0) { P.totals->ing_pk[P.ing_slot ^ 1u] = 0; P.totals->ing_b[P.ing_slot ^ 1u] = 0; }
 #ifdef EDGPU_AB_VARIANTS
     if (tid == 0) {
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -798,66 +836,6 @@ __global__ __launch_bounds__(kCopyThreads) void k_ingest_copy(IngestParams P) {
 // =========================================================================================
 // Keyframe index + audio anchor: one wave per session segment.
 // =========================================================================================
-
-// The last ingest's counters from the cumulative ones (run once the ingest has finished).
-__device__ __forceinline__ void mark_ingest_totals(TickTotals* t) {
-    const unsigned long long p = t->cum_ingested_packets, b = t->cum_ingested_bytes;
-    t->ingested_packets = p - t->ingest_mark_packets; t->ingested_bytes = b - t->ingest_mark_bytes;
-    t->ingest_mark_packets = p; t->ingest_mark_bytes = b;
-#ifdef EDGPU_AB_VARIANTS
-    // measurement builds: the finished ingest's span and first workgroup exit, then a reset
-    t->ing_last_span = t->ing_done_max - t->ing_t0_min; t->ing_last_first = t->ing_done_min - t->ing_t0_min;
-    t->ing_t0_min = ~0ull; t->ing_done_min = ~0ull; t->ing_done_max = 0;
-#endif
-}
-
-__global__ __launch_bounds__(64) void k_keyframe(KeyframeParams P) {
-    const uint32_t seg = blockIdx.x;
-    if (seg == 0 && threadIdx.x == 0) mark_ingest_totals(P.totals);   // the ingest has finished
-    const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
-    const uint32_t sess = P.seg_sess[seg];
-    const SessionDev S = P.sessions[sess];
-    const int lane = threadIdx.x;
-    bool flag = S.video_key_flag != 0;
-    __shared__ int64_t s_key[kMaxSendersPerSession];
-    const uint32_t nsnd = 2 * S.ntracks;
-    if (lane < (int)nsnd) s_key[lane] = P.senders[S.first_sender + lane].key;
-    __syncthreads();
-    for (uint32_t base = b; base < e; base += 64) {
-        const uint32_t i = base + lane;
-        const uint32_t f = i < e ? P.pflags[i] : 0u;
-        const uint64_t idx = i < e ? P.pidx[i] : 0ull;
-        const uint64_t K = __ballot((f & 2u) != 0);
-        const uint64_t A = __ballot((f & 4u) != 0);
-        const uint64_t E = K | A;
-        const uint64_t below = (lane == 0) ? 0ull : (E & ((1ull << lane) - 1));
-        bool anchor = false;
-        if (f & 4u) {
-            if (below) {
-                const int j = 63 - __clzll((long long)below);
-                anchor = (K >> j) & 1ull;
-            } else {
-                anchor = flag;
-            }
-        }
-        uint64_t C = __ballot((f & 2u) != 0 || anchor);
-        // apply in arrival order: the latest match wins (Q5)
-        while (C) {
-            const int j = __ffsll((unsigned long long)C) - 1;
-            C &= C - 1;
-            const uint32_t fj = __shfl(f, j, 64);
-            const uint64_t ij = __shfl(idx, j, 64);
-            if (lane == 0) s_key[(fj >> 8) & 0xFF] = (int64_t)ij;
-        }
-        if (E) {
-            const int top = 63 - __clzll((long long)E);
-            flag = (K >> top) & 1ull;
-        }
-        __syncthreads();
-    }
-    if (lane < (int)nsnd) P.senders[S.first_sender + lane].key = s_key[lane];
-    if (lane == 0) P.sessions[sess].video_key_flag = flag ? 1u : 0u;
-}
 
 // =========================================================================================
 // Fan-out planning
@@ -923,6 +901,11 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     t->relayed_packets = 0; t->relayed_bytes = 0; t->arena_bytes = 0;   // the ingest counters stay
     t->status = 0; t->nwork = 0; t->fan_next = 0; t->stream_errors = 0;
     t->fan_t0_min = ~0ull; t->fan_done_min = ~0ull; t->fan_done_max = 0;
+#ifdef EDGPU_AB_VARIANTS
+    // measurement builds: the last ingest's span and first workgroup exit, then a reset
+    t->ing_last_span = t->ing_done_max - t->ing_t0_min; t->ing_last_first = t->ing_done_min - t->ing_t0_min;
+    t->ing_t0_min = ~0ull; t->ing_done_min = ~0ull; t->ing_done_max = 0;
+#endif
     // a pass the previous tick still owed is lost now (its host never called edgpu_fanout_next)
     if (t->pass_next[t->pass_slot & 1u] != kNoPass) t->cum_lost_passes++;
     t->pass_slot = 0;
@@ -932,11 +915,11 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
 
 // Per-tick counter updates as one tiny launch (a hipMemsetAsync of a few bytes costs two fill
 // kernels): which = 0 fan-out totals reset (when k_plan_senders, which does it itself, does not
-// run), 1 the ingest counters of an empty batch (when k_keyframe, which does it itself, does not).
+// run), 1 the ingest counters of an empty batch (when k_ingest, which does it itself, does not run).
 __global__ void k_totals_reset(TickTotals* t, int which) {
     if (threadIdx.x != 0) return;
     if (which == 0) reset_tick_totals(t);
-    else mark_ingest_totals(t);
+    else for (int k = 0; k < 2; k++) { t->ing_pk[k] = 0; t->ing_b[k] = 0; }
 }
 
 // A sender ring lost a packet an output of its session needed (per-stream isolation: the
@@ -2553,6 +2536,7 @@ __global__ void k_image_fit(ImageParams P) {
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (internal C++ API used by edgpu_engine.cpp)
 namespace edgpu {
+thread_local uint64_t tl_launches = 0;
 
 // edgpu_arena_gather: one workgroup per region, 16-B words (offsets / lengths are slot-aligned)
 __global__ __launch_bounds__(256) void k_arena_gather(const u32x4* arena, const edgpu_region* reg, const uint64_t* dst_off,
@@ -2564,7 +2548,7 @@ __global__ __launch_bounds__(256) void k_arena_gather(const u32x4* arena, const 
 }
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st) {
-    if (n) hipLaunchKernelGGL(k_arena_gather, dim3(n), dim3(256), 0, st, reinterpret_cast<const u32x4*>(arena), reg,
+    if (n) EDGPU_LAUNCH(k_arena_gather, dim3(n), dim3(256), 0, st, reinterpret_cast<const u32x4*>(arena), reg,
                               dst_off, reinterpret_cast<u32x4*>(dst));
     return hipGetLastError();
 }
@@ -2582,7 +2566,7 @@ __global__ __launch_bounds__(256) void k_copy_to_pinned(const u32x4* __restrict_
             reinterpret_cast<uint8_t*>(dst)[b] = reinterpret_cast<const uint8_t*>(src)[b];
 }
 hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hipStream_t st) {
-    if (bytes) hipLaunchKernelGGL(k_copy_to_pinned, dim3(1024), dim3(256), 0, st, reinterpret_cast<const u32x4*>(src),
+    if (bytes) EDGPU_LAUNCH(k_copy_to_pinned, dim3(1024), dim3(256), 0, st, reinterpret_cast<const u32x4*>(src),
                                   reinterpret_cast<u32x4*>(dst), bytes);
     return hipGetLastError();
 }
@@ -2595,7 +2579,7 @@ __global__ __launch_bounds__(64) void k_stall(uint64_t ticks) {
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 hipError_t launch_stall(uint64_t ticks, hipStream_t st) {
-    hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, st, ticks);
+    EDGPU_LAUNCH(k_stall, dim3(1), dim3(64), 0, st, ticks);
     return hipGetLastError();
 }
 
@@ -2619,7 +2603,7 @@ __global__ __launch_bounds__(256) void k_desc_arrival(const SubDev* subs, const 
 }
 hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                                int64_t* out, hipStream_t st) {
-    if (nsubs) hipLaunchKernelGGL(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass, out);
+    if (nsubs) EDGPU_LAUNCH(k_desc_arrival, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass, out);
     return hipGetLastError();
 }
 
@@ -2645,7 +2629,7 @@ __global__ __launch_bounds__(256) void k_desc_source(const SubDev* subs, const S
 }
 hipError_t launch_desc_source(const SubDev* subs, const SenderDev* senders, uint32_t nsubs, uint32_t pass,
                               uint32_t epoch, uint32_t* out, hipStream_t st) {
-    if (nsubs) hipLaunchKernelGGL(k_desc_source, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass,
+    if (nsubs) EDGPU_LAUNCH(k_desc_source, dim3((nsubs + 3) / 4), dim3(256), 0, st, subs, senders, nsubs, pass,
                                   epoch, out);
     return hipGetLastError();
 }
@@ -2686,63 +2670,58 @@ __global__ __launch_bounds__(256) void k_sub_rows(const SubDev* subs, const Send
 hipError_t launch_sub_rows(const SubDev* subs, const SenderDev* senders, const edgpu_out_desc* desc, const uint32_t* sel,
                            uint32_t nsel, uint32_t nsubs, uint32_t pass, uint32_t epoch, edgpu_packet_row* rows,
                            uint64_t nrows, hipStream_t st) {
-    if (nsel) hipLaunchKernelGGL(k_sub_rows, dim3((nsel + 3) / 4), dim3(256), 0, st, subs, senders, desc, sel, nsel,
+    if (nsel) EDGPU_LAUNCH(k_sub_rows, dim3((nsel + 3) / 4), dim3(256), 0, st, subs, senders, desc, sel, nsel,
                                  nsubs, pass, epoch, rows, nrows);
     return hipGetLastError();
 }
 
 
 hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
-    if (nseg == 0) return hipSuccess;
+    if (nseg == 0) {                         // still the (empty) ingest's counters
+        EDGPU_LAUNCH(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 1);
+        return hipGetLastError();
+    }
 #ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
     static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();
-    if (threads == 512) hipLaunchKernelGGL((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
-    else if (depth == 2) hipLaunchKernelGGL(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
-    else hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    if (threads == 512) EDGPU_LAUNCH((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
+    else if (depth == 2) EDGPU_LAUNCH(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    else EDGPU_LAUNCH(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     if (p.npk && EDGPU_COPY_MODE(p) == 1) {
         const uint32_t per = kCopyThreads / kCopyLanes;
-        hipLaunchKernelGGL(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
+        EDGPU_LAUNCH(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
 #else
-    hipLaunchKernelGGL(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    EDGPU_LAUNCH(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
 #endif
     return hipGetLastError();
 }
 hipError_t launch_image(const ImageParams& p, int phase, hipStream_t st) {
     if (p.nplan == 0) return hipSuccess;
-    if (phase == 0) hipLaunchKernelGGL(k_image_plan, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
-    else if (phase == 1) hipLaunchKernelGGL(k_image_pack, dim3(p.nplan), dim3(256), 0, st, p);
-    else if (phase == 2) hipLaunchKernelGGL(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL(k_image_fit, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
+    if (phase == 0) EDGPU_LAUNCH(k_image_plan, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
+    else if (phase == 1) EDGPU_LAUNCH(k_image_pack, dim3(p.nplan), dim3(256), 0, st, p);
+    else if (phase == 2) EDGPU_LAUNCH(k_image_apply, dim3(p.nplan), dim3(256), 0, st, p);
+    else EDGPU_LAUNCH(k_image_fit, dim3((p.nplan + 255) / 256), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 hipError_t launch_first_packet_info(const FirstInfoQuery* q, FirstInfoResult* r, const SenderDev* senders,
                                     uint32_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_first_packet_info, dim3((n + 63) / 64), dim3(64), 0, st, q, r, senders, n);
+    EDGPU_LAUNCH(k_first_packet_info, dim3((n + 63) / 64), dim3(64), 0, st, q, r, senders, n);
     return hipGetLastError();
 }
 hipError_t launch_blocked(const BlockedParams& p, hipStream_t st) {
-    if (p.n) hipLaunchKernelGGL(k_blocked, dim3((p.n + 63) / 64), dim3(64), 0, st, p);
+    if (p.n) EDGPU_LAUNCH(k_blocked, dim3((p.n + 63) / 64), dim3(64), 0, st, p);
     return hipGetLastError();
 }
 
-hipError_t launch_keyframe(const KeyframeParams& p, uint32_t nseg, hipStream_t st) {
-    if (nseg == 0) {                         // still the (empty) ingest's counters
-        hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 1);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(k_keyframe, dim3(nseg), dim3(64), 0, st, p);
-    return hipGetLastError();
-}
 hipError_t launch_plan(const PlanParams& p, hipStream_t st) {
     const uint32_t nsb = p.T.nsenders ? (p.T.nsenders + 255) / 256 : 0;
-    if (nsb) hipLaunchKernelGGL(k_plan_senders, dim3((p.T.nsenders + 3) / 4), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 0);
-    if (p.T.nsub_blocks) hipLaunchKernelGGL(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
+    if (nsb) EDGPU_LAUNCH(k_plan_senders, dim3((p.T.nsenders + 3) / 4), dim3(256), 0, st, p);
+    else EDGPU_LAUNCH(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 0);
+    if (p.T.nsub_blocks) EDGPU_LAUNCH(k_plan_subs, dim3(p.T.nsub_blocks), dim3(256), 0, st, p);
     const uint32_t nfb = max(p.T.nsub_blocks, nsb);
-    if (nfb) hipLaunchKernelGGL(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
+    if (nfb) EDGPU_LAUNCH(k_plan_final, dim3(nfb), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 // A sender ring moved into a larger one (ring growth): kind 0 the PktMeta ring, 1 its blob-slot
@@ -2753,15 +2732,15 @@ hipError_t launch_ring_move(int kind, const void* src, uint64_t smask, void* dst
     const uint64_t nb = (n + 255) / 256;
     const uint32_t blocks = (uint32_t)(nb < 4096 ? nb : 4096);
     if (kind == 0)
-        hipLaunchKernelGGL(k_ring_move<PktMeta>, dim3(blocks), dim3(256), 0, st, (const PktMeta*)src, smask, (PktMeta*)dst, dmask, lo, n);
+        EDGPU_LAUNCH(k_ring_move<PktMeta>, dim3(blocks), dim3(256), 0, st, (const PktMeta*)src, smask, (PktMeta*)dst, dmask, lo, n);
     else if (kind == 1)
-        hipLaunchKernelGGL(k_ring_move<uint32_t>, dim3(blocks), dim3(256), 0, st, (const uint32_t*)src, smask, (uint32_t*)dst, dmask, lo, n);
+        EDGPU_LAUNCH(k_ring_move<uint32_t>, dim3(blocks), dim3(256), 0, st, (const uint32_t*)src, smask, (uint32_t*)dst, dmask, lo, n);
     else
-        hipLaunchKernelGGL(k_ring_move<u32x4>, dim3(blocks), dim3(256), 0, st, (const u32x4*)src, smask, (u32x4*)dst, dmask, lo, n);
+        EDGPU_LAUNCH(k_ring_move<u32x4>, dim3(blocks), dim3(256), 0, st, (const u32x4*)src, smask, (u32x4*)dst, dmask, lo, n);
     return hipGetLastError();
 }
 hipError_t launch_plan_pass(const PlanParams& p, hipStream_t st) {
-    hipLaunchKernelGGL(k_plan_pass, dim3(max(p.T.nsub_blocks, 1u)), dim3(256), 0, st, p);
+    EDGPU_LAUNCH(k_plan_pass, dim3(max(p.T.nsub_blocks, 1u)), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 // Fan-out variants (EDGPU_FANOUT env var, for A/B measurement).  Each entry: kernel,
@@ -2917,6 +2896,7 @@ hipError_t launch_fanout(const FanoutParams& p, int variant, int num_cus, hipStr
         if (v.max_wg_per_cu && occ[variant] > v.max_wg_per_cu) occ[variant] = v.max_wg_per_cu;
     }
     void* args[] = {(void*)&p};
+    ++tl_launches;
     return hipLaunchKernel(v.fn, dim3(num_cus * occ[variant]), dim3(v.threads), args, v.lds, st);
 }
 }  // namespace edgpu

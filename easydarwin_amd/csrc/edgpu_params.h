@@ -21,6 +21,15 @@
 
 namespace edgpu {
 
+// Kernel launches made on this thread (edgpu_counters.kernel_launches: the engine adds what each
+// API call launched).  Every launch goes through EDGPU_LAUNCH.
+extern thread_local uint64_t tl_launches;
+#define EDGPU_LAUNCH(...)                          \
+    do {                                           \
+        ++::edgpu::tl_launches;                    \
+        hipLaunchKernelGGL(__VA_ARGS__);           \
+    } while (0)
+
 // Interleaved frames a k_ingest wave copies per round (all their loads before the first
 // store): 4 since the copy is specialised on the frame's word offset (128 VGPRs, 4 waves per
 // SIMD); it was 2 (tools/build_ingest_ab.sh builds others)
@@ -43,8 +52,6 @@ struct IngestParams {
     SessionDev* sessions;
     SenderDev* senders;
     StreamDev* streams;
-    uint32_t* pflags;       // per desc: bit0 enqueued, bit1 video key, bit2 audio event, bits 8-15 local sender
-    uint64_t* pidx;         // per desc: sender queue index
     CopyJob* jobs;          // per desc: slot copy for k_ingest_copy
     uint32_t npk;           // descriptors in the batch
     uint32_t copy_mode;     // 0: copy inside k_ingest, 1: k_ingest_copy (EDGPU_INGEST)
@@ -56,6 +63,7 @@ struct IngestParams {
     uint32_t host_epoch;    // != 0: the blob is a host batch the host keeps for the tick; record each
                             // packet's slot and the batch (edgpu_fanout_sources)
     TickTotals* totals;
+    uint32_t ing_slot;      // this batch's ingest counters: TickTotals.ing_pk / ing_b [ing_slot]
     // reflector_use_in_packet_receive_time / reflector_in_packet_max_receive_sec
     // (ReflectorStream.cpp:103-107, 113): strip a 12-byte "aktt" BE64 receive-time trailer and
     // rebase the packet's arrival on it (:1960-1994)
@@ -72,16 +80,6 @@ struct IngestParams {
     const TcpRead* tcp_reads;
     const uint8_t* tcp_raw;
     const uint8_t* tcp_stage;
-};
-
-struct KeyframeParams {
-    const uint32_t* seg_off;
-    const uint32_t* seg_sess;
-    const uint32_t* pflags;
-    const uint64_t* pidx;
-    SessionDev* sessions;
-    SenderDev* senders;
-    TickTotals* totals;
 };
 
 struct PlanParams {

@@ -785,6 +785,9 @@ QTSS_Error Tick() {
     o.hold_ms = held + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     o.hold_max_ms = std::max(o.hold_max_ms, o.hold_ms);
     o.hold_sum_ms += o.hold_ms;
+    o.wall_sum_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    o.ingest_sum_ms += t.ingest_ms; o.fanout_sum_ms += t.fanout_ms;
+    o.readback_sum_ms += t.readback_ms; o.write_sum_ms += t.write_ms;
     o.ticks++;
     if (err) {
         // the first failure is logged with the engine's message; later ones are counted

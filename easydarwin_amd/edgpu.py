@@ -147,7 +147,8 @@ class Counters(C.Structure):
                 ("fanout_passes", C.c_uint64), ("lost_passes", C.c_uint64),
                 ("senders", C.c_uint32), ("substream_rows", C.c_uint32),
                 ("ring_grows", C.c_uint64), ("ring_bytes", C.c_uint64), ("ring_pool_bytes", C.c_uint64),
-                ("ring_grow_failures", C.c_uint64), ("watchdog_timeouts", C.c_uint64)]
+                ("ring_grow_failures", C.c_uint64), ("watchdog_timeouts", C.c_uint64),
+                ("kernel_launches", C.c_uint64), ("host_syncs", C.c_uint64)]
 
 
 # numpy mirrors (same layout as the C structs)

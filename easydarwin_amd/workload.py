@@ -2,9 +2,11 @@
 
 C2: ``n_sessions`` pushed H.264/90000 1080p30 streams at 4 Mb/s, 2 s GOP (IDR ~120 KB,
 SPS 36-B and PPS 20-B packets before it), FU-A at 1400-byte RTP packets, marker on each
-frame's last packet, 90 kHz timestamps (+3000 per frame), random initial seq / ts / SSRC
-and a random GOP phase per session; ``subs_per_session`` UDP subscribers each.  Packets
-arrive at their frame time; one batch = one tick interval (default 1 s).
+frame's last packet, 90 kHz timestamps (+3000 per frame), random initial seq / ts / SSRC,
+a random GOP phase and a random capture offset (0-33 ms: pushers are not frame-synchronous) per
+session; ``subs_per_session`` UDP subscribers each.  Packets arrive at their frame time; one
+batch = the packets that arrived in one tick interval (default 1 s; at 20-ms ticks about 60 % of
+the sessions have a frame in each batch).
 
 Only the RTP/FU headers are synthesised on the host; payload bytes are filled on the GPU
 (they are never inspected by the relay, only moved).  Session ids are global so that a
@@ -67,12 +69,13 @@ class H264Fleet:
         self.ts0 = np.array([r.integers(0, 1 << 32) for r in rngs], dtype=np.int64)
         self.ssrc = np.array([r.integers(1, 1 << 32) for r in rngs], dtype=np.int64)
         self.phase = np.array([r.integers(0, GOP) for r in rngs], dtype=np.int64)
+        self.offset = np.array([r.integers(0, 1000 // FPS + 1) for r in rngs], dtype=np.int64)   # ms
+        self.fdone = np.zeros(n, dtype=np.int64)     # frames of each session batched so far
         self.rng = np.random.Generator(np.random.PCG64(SEED_BASE + config_index))
         self.idr_bytes = idr_bytes
         gop_bytes = bitrate // 8 * GOP // FPS
         self.p_mean = (gop_bytes - idr_bytes - 40) // (GOP - 1)
         self.tick_ms = tick_ms
-        self.frame = 0            # next frame index (global clock, all sessions share fps)
         self.tracks = [TrackSpec("video", "H264/90000", 96, bitrate=bitrate, gop=GOP, idr_bytes=idr_bytes)]
 
     def sdp(self) -> str:
@@ -85,19 +88,25 @@ class H264Fleet:
         ``hdr`` (n x 16 bytes: the slot's first 16 bytes = 4-B reserved + 12-B RTP header),
         ``fu`` (n x 2: bytes 16-17 of the slot = FU indicator/header or NAL header + 1 byte),
         ``slot_bytes`` (n), ``t_end`` (tick time)."""
-        f0 = self.frame
-        # the frames due by the end of this tick (a tick shorter than a frame interval may carry none)
+        # frame f of session s arrives at f * 1000 // FPS + offset[s]; this tick takes the frames
+        # that arrived before its end (a tick shorter than a frame interval may carry none of a
+        # session's)
         self.t_ms = getattr(self, "t_ms", 0) + self.tick_ms
-        nf = self.t_ms * FPS // 1000 - f0
-        self.frame += nf
+        span = self.t_ms - self.offset
+        due = np.where(span > 0, (span * FPS + 999) // 1000, 0)        # frames arrived before t_ms
+        f0s = self.fdone
+        nfs = due - f0s
+        self.fdone = due
         n = self.n
-        fidx = f0 + np.arange(nf)                                    # frames of this tick
-        gop_pos = (fidx[None, :] + self.phase[:, None]) % GOP          # (n, nf)
+        nf = int(nfs.max()) if n else 0                                # frame columns (ragged: masked)
+        fidx = f0s[:, None] + np.arange(nf)[None, :]                   # (n, nf)
+        valid = np.arange(nf)[None, :] < nfs[:, None]
+        gop_pos = (fidx + self.phase[:, None]) % GOP
         is_idr = gop_pos == 0
         psize = (self.p_mean * self.rng.uniform(0.8, 1.2, size=(n, nf))).astype(np.int64)
         size = np.where(is_idr, self.idr_bytes, psize)                 # NAL bytes incl. header
         nfrag = (size - 1 + FRAG - 1) // FRAG                          # FU-A fragments
-        npk = nfrag + np.where(is_idr, 2, 0)                           # + SPS + PPS
+        npk = np.where(valid, nfrag + np.where(is_idr, 2, 0), 0)       # + SPS + PPS
         # per-packet expansion (session-major, frame order, packet order)
         tot = int(npk.sum())
         sess_of_frame = np.repeat(np.arange(n), nf)
@@ -118,8 +127,9 @@ class H264Fleet:
         sess_first = np.concatenate([[0], np.cumsum(pk_per_sess)[:-1]])
         seq = (self.seq[sess] + (np.arange(tot) - sess_first[sess])) & 0xFFFF
         self.seq = (self.seq + pk_per_sess) & 0xFFFF
-        ts = (self.ts0[sess] + 3000 * (f0 + fl)) & 0xFFFFFFFF
-        arrival = (f0 + fl) * 1000 // FPS
+        fr = f0s[sess] + fl
+        ts = (self.ts0[sess] + 3000 * fr) & 0xFFFFFFFF
+        arrival = fr * 1000 // FPS + self.offset[sess]
         marker = last
         hdr = np.zeros((tot, 16), dtype=np.uint8)
         hdr[:, 4] = 0x80
@@ -141,5 +151,5 @@ class H264Fleet:
             "n": tot, "len": plen.astype(np.uint16), "channel": np.zeros(tot, np.uint8),
             "arrival": arrival.astype(np.int64), "hdr": hdr, "fu": fu,
             "slot_bytes": slot_bytes.astype(np.int64), "seg_off": seg_off,
-            "t_end": int((f0 + nf) * 1000 // FPS),
+            "t_end": int(self.t_ms),
         }

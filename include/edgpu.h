@@ -424,6 +424,8 @@ int  edgpu_ingest_interleaved(edgpu_ctx* ctx, const edgpu_tcp_read* reads, uint3
                               const uint8_t* bytes, uint64_t n_bytes, int ptr_location,
                               edgpu_tcp_result* results);
 
+/* Closes the ingested batch (the keyframe index itself runs inside the ingest kernel, after each
+ * segment's packets are enqueued); required between an ingest and the next call. */
 int  edgpu_keyframe_index(edgpu_ctx* ctx);
 int  edgpu_fanout(edgpu_ctx* ctx, int64_t now_ms, edgpu_fanout_result* out);
 
@@ -726,16 +728,16 @@ typedef struct edgpu_counters {
     uint64_t ring_grow_failures; /* growths skipped because the device memory could not hold the new
                                     rings (growth is best effort; the ingest goes on) */
     uint64_t watchdog_timeouts; /* waits the GPU watchdog ended (edgpu_config.watchdog_ms) */
+    uint64_t kernel_launches;   /* kernels the context's calls launched */
+    uint64_t host_syncs;        /* times a call waited for the GPU (stream / event synchronize) */
 } edgpu_counters;
 int  edgpu_counters_get(edgpu_ctx* ctx, edgpu_counters* out);
 
 /* Per-launch device durations (ms, HIP events on the ctx stream) recorded since the last
  * call, oldest first, for `which` = 0 fan-out copy kernel, 1 whole fan-out tick (plan +
- * copy), 2 ingest, 3 keyframe index.  Up to 256 launches are kept; the history is cleared
- * after reading.  [3] runs from the end of the ingest it indexes when that ingest was
- * enqueued without a host round trip (edgpu_ingest: it then includes the launch gap between
- * the two calls), else from its own start event (edgpu_ingest_interleaved, which syncs and
- * reads results back in between).  Syncs. */
+ * copy), 2 ingest (with the keyframe index it carries), 3 keyframe index (no entries since the
+ * index runs inside the ingest kernel).  Up to 256 launches are kept; the history is cleared
+ * after reading.  Syncs. */
 int  edgpu_kernel_times(edgpu_ctx* ctx, int which, float* out_ms, uint32_t max_n, uint32_t* out_n);
 
 /* Which per-launch timing events the context records from now on (default EDGPU_TIMING_ALL).
@@ -755,7 +757,7 @@ int  edgpu_copy_to_host(edgpu_ctx* ctx, void* dst, const void* device_src, uint6
 
 /* Device-side timing of the last edgpu_fanout's kernels (HIP events on the ctx stream),
  * in milliseconds: [0] fan-out copy kernel, [1] whole fan-out (plan + copy),
- * [2] ingest, [3] keyframe index. */
+ * [2] ingest (with the keyframe index), [3] 0 (the index runs inside the ingest). */
 int  edgpu_last_timings(edgpu_ctx* ctx, float out_ms[4]);
 
 /* Keyframe fast start: bytes a joining subscriber of `session`/`track` would receive now

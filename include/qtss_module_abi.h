@@ -278,6 +278,9 @@ typedef struct EDGPU_QTSSTickInfo {
     uint64_t stream_errors;             /* sessions a tick marked since Initialize: a sender ring lost
                                            a packet one of their outputs needed (logged by name;
                                            the ticks went on for every other session) */
+    /* sums over every tick since Initialize (a host takes differences over a window): wall time
+       (start to the last write), then its ingest / fan-out / readback / write parts */
+    double   wall_sum_ms, ingest_sum_ms, fanout_sum_ms, readback_sum_ms, write_sum_ms;
 } EDGPU_QTSSTickInfo;
 edqtss::QTSS_Error EDGPU_QTSSReflectorModule_LastTick(EDGPU_QTSSTickInfo* out);
 }

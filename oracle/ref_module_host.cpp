@@ -19,6 +19,13 @@
 //                                            session (RTP then RTCP, track order), as
 //                                            ReflectorSocket::Run does (ReflectorStream.cpp:
 //                                            1709-1714) and oracle/ref_harness.cpp's TICK does;
+//       EDGPU_REFHOST_Ticker(on)          -- (--bench real time) the server's task threads: a
+//                                            ReflectorSocket task runs ReflectPackets as soon as a
+//                                            pushed packet signals it (ReflectorStream.cpp:573,
+//                                            1676-1714); here EDGPU_REF_TICK_THREADS threads sweep
+//                                            their share of the sessions' senders every
+//                                            EDGPU_REF_REFLECT_MSEC (default 1) ms, without the
+//                                            session map's mutex (a task holds its session);
 //       EDGPU_QTSSReflectorModule_PollUDP -- the datagrams waiting on the UDP-push sockets the
 //                                            module bound (UDPSocketPool, BindSockets :388-506),
 //                                            each clamped to the 2060-byte packet buffer and
@@ -33,6 +40,7 @@
 #include <sys/socket.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 #include <cstdio>
@@ -140,11 +148,64 @@ struct TickInfo {
     uint64_t prestaged_bytes, passes, rereads;
     double hold_max_ms, hold_sum_ms;
     uint64_t stream_errors;
+    double wall_sum_ms, ingest_sum_ms, fanout_sum_ms, readback_sum_ms, write_sum_ms;
 };
 static TickInfo g_tick;
 extern "C" QTSS_Error EDGPU_QTSSReflectorModule_LastTick(TickInfo* out) {
     *out = g_tick;
     return QTSS_NoErr;
+}
+
+// ReflectPackets on a session's senders, RTP then RTCP per track, each under its socket's demuxer
+// mutex with its free queue (ReflectorStream.cpp:1676-1714)
+static void reflect_session(ReflectorSession* sess) {
+    for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
+        ReflectorStream* st = sess->GetStreamByIndex(x);
+        if (st == NULL || st->GetSocketPair() == NULL) continue;
+        ReflectorSocket* a = (ReflectorSocket*)st->GetSocketPair()->GetSocketA();
+        ReflectorSocket* b = (ReflectorSocket*)st->GetSocketPair()->GetSocketB();
+        SInt64 wake = 0;
+        {
+            OSMutexLocker l(a->GetDemuxer()->GetMutex());
+            st->GetRTPSender()->ReflectPackets(&wake, &(a->*get(FreeQueueMember())));
+        }
+        wake = 0;
+        {
+            OSMutexLocker l(b->GetDemuxer()->GetMutex());
+            st->GetRTCPSender()->ReflectPackets(&wake, &(b->*get(FreeQueueMember())));
+        }
+    }
+}
+
+static std::atomic<bool> g_rt_stop{false};
+static std::vector<std::thread> g_rt_threads;
+extern "C" void EDGPU_REFHOST_Ticker(int on) {
+    if (!on) {
+        g_rt_stop = true;
+        for (std::thread& t : g_rt_threads) t.join();
+        g_rt_threads.clear();
+        return;
+    }
+    const unsigned nthreads = getenv("EDGPU_REF_TICK_THREADS") ? std::max(1, atoi(getenv("EDGPU_REF_TICK_THREADS"))) : 1;
+    const int every = getenv("EDGPU_REF_REFLECT_MSEC") ? std::max(0, atoi(getenv("EDGPU_REF_REFLECT_MSEC"))) : 1;
+    g_rt_stop = false;
+    for (unsigned w = 0; w < nthreads; w++)
+        g_rt_threads.emplace_back([w, nthreads, every]() {
+            while (!g_rt_stop.load()) {
+                std::vector<ReflectorSession*> sessions;
+                {
+                    OSMutexLocker locker(session_map()->GetMutex());
+                    sessions = live_sessions();     // (the bench's sessions live until its end)
+                }
+                const auto a = std::chrono::steady_clock::now();
+                for (size_t k = w; k < sessions.size(); k += nthreads) reflect_session(sessions[k]);
+                if (w == 0) {
+                    g_tick.ticks++;
+                    g_tick.wall_sum_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(every));
+            }
+        });
 }
 
 extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
@@ -158,6 +219,7 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             g_tick.hold_max_ms = std::max(g_tick.hold_max_ms, g_tick.hold_ms);
             g_tick.hold_sum_ms += g_tick.hold_ms;
+            g_tick.wall_sum_ms += g_tick.hold_ms;
         }
     } done{t0};
     OSMutexLocker locker(session_map()->GetMutex());
@@ -167,25 +229,7 @@ extern "C" QTSS_Error EDGPU_QTSSReflectorModule_Tick(void) {
     static const unsigned nthreads = getenv("EDGPU_REF_TICK_THREADS") ? (unsigned)atoi(getenv("EDGPU_REF_TICK_THREADS")) : 1;
     const std::vector<ReflectorSession*> sessions = live_sessions();
     auto reflect = [&](unsigned w, unsigned nw) {
-        for (size_t k = w; k < sessions.size(); k += nw) {
-            ReflectorSession* sess = sessions[k];
-            for (UInt32 x = 0; x < sess->GetNumStreams(); x++) {
-                ReflectorStream* st = sess->GetStreamByIndex(x);
-                if (st == NULL || st->GetSocketPair() == NULL) continue;
-                ReflectorSocket* a = (ReflectorSocket*)st->GetSocketPair()->GetSocketA();
-                ReflectorSocket* b = (ReflectorSocket*)st->GetSocketPair()->GetSocketB();
-                SInt64 wake = 0;
-                {
-                    OSMutexLocker l(a->GetDemuxer()->GetMutex());
-                    st->GetRTPSender()->ReflectPackets(&wake, &(a->*get(FreeQueueMember())));
-                }
-                wake = 0;
-                {
-                    OSMutexLocker l(b->GetDemuxer()->GetMutex());
-                    st->GetRTCPSender()->ReflectPackets(&wake, &(b->*get(FreeQueueMember())));
-                }
-            }
-        }
+        for (size_t k = w; k < sessions.size(); k += nw) reflect_session(sessions[k]);
     };
     if (nthreads <= 1) {
         reflect(0, 1);

@@ -36,6 +36,9 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# RTP packets per second one --bench pusher sends (tools/qtss_replay.cpp run_bench): a 2-s GOP of a
+# 120-KB IDR (87 FU-A fragments + SPS + PPS) and 59 P frames of 14,915 B (11 fragments each)
+PKT_PER_SESSION_S = (87 + 2 + 59 * 11) / 2.0
 
 
 def gpu_node_cpus() -> list:
@@ -96,6 +99,51 @@ def realtime_runs(args) -> list:
             raise SystemExit(f"qtss_replay --bench realtime failed ({r.returncode}): {r.stderr.strip()[-400:]}")
         out.append(json.loads([ln for ln in r.stdout.splitlines() if '"mode": "realtime"' in ln][-1]))
     return out
+
+
+def realtime_one(module: str, sessions: int, args, env_extra: dict) -> dict:
+    env = dict(os.environ, EDGPU_BENCH_REALTIME="1", **env_extra)
+    env.setdefault("EDGPU_QTSS_ARENA_MB", str(args.arena_mb))
+    env.setdefault("EDGPU_QTSS_MAX_OUT_PACKETS", str(args.max_out_packets))
+    env.setdefault("EDGPU_QTSS_WRITE_THREADS", str(args.write_threads))
+    cmd = [os.path.join(ROOT, "tools", "qtss_replay"), module,
+           "--bench", str(sessions), str(args.subs), str(args.seconds), str(args.tick_ms), str(args.threads)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=args.timeout)
+    if r.returncode:
+        raise SystemExit(f"qtss_replay --bench realtime ({module}, {sessions}) failed ({r.returncode}): "
+                         f"{r.stderr.strip()[-400:]}")
+    return json.loads([ln for ln in r.stdout.splitlines() if '"mode": "realtime"' in ln][-1])
+
+
+def realtime_sweep(args) -> dict:
+    """Sessions 1024 -> 8192 at their real rate, the drop-in on its default ticker (reflect on
+    arrival, at most every 2 ms) beside the reference module on the server's task threads (its
+    senders swept every EDGPU_REF_REFLECT_MSEC = 1 ms by as many threads as the drop-in has write
+    threads, oracle/ref_module_host.cpp EDGPU_REFHOST_Ticker).  A fleet is held when the RTP write
+    latency's p99 is <= the bound and at least 98 % of the offered packets are written."""
+    rows = {"drop-in": [], "reference": []}
+    refmod = os.path.join(ROOT, "oracle", "_ref", "libQTSSReflectorModule_ref.so")
+    for n in args.sweep:
+        d = realtime_one(args.module, n, args, {"EDGPU_QTSS_REFLECT_ON_ARRIVAL": "2"})
+        rows["drop-in"].append(d)
+        print(json.dumps({"progress": "drop-in", "sessions": n, "p99": d["latency_ms"]["p99"],
+                          "relayed_per_s": d["relayed_per_s"]}), file=sys.stderr, flush=True)
+        if not args.no_reference and os.path.exists(refmod):
+            r = realtime_one(refmod, n, args, {"EDGPU_REF_TICK_THREADS": str(args.write_threads)})
+            rows["reference"].append(r)
+            print(json.dumps({"progress": "reference", "sessions": n, "p99": r["latency_ms"]["p99"],
+                              "relayed_per_s": r["relayed_per_s"]}), file=sys.stderr, flush=True)
+
+    def held(rs):
+        best = None
+        for d in rs:
+            # the offered write rate: every RTP packet to every player (the drop-in's first run sets it)
+            want = d["sessions"] * d["subs"] * PKT_PER_SESSION_S
+            if d["latency_ms"]["p99"] <= args.p99_ms and d["relayed_per_s"] >= 0.98 * want:
+                best = d["sessions"]
+        return best
+    return {"p99_bound_ms": args.p99_ms, "runs": rows,
+            "capacity_sessions": {k: held(v) for k, v in rows.items()}}
 
 
 def reference_module_run(args, threads: int | None = None) -> dict | None:
@@ -161,6 +209,12 @@ def main():
     # the module on its own ticker at the streams' real rate: throughput = the offered load,
     # plus the latency it adds (fixed tick vs reflect-on-arrival)
     ap.add_argument("--realtime", action="store_true")
+    # --realtime-sweep: sessions 1024 -> 8192 (or --sweep) at their real rate, the drop-in on its
+    # default ticker and the reference module on the server's task threads; the largest fleet each
+    # holds at p99 write latency <= --p99-ms
+    ap.add_argument("--realtime-sweep", action="store_true")
+    ap.add_argument("--sweep", type=lambda s: [int(x) for x in s.split(",")], default=[1024, 2048, 4096, 8192])
+    ap.add_argument("--p99-ms", type=float, default=10.0)
     # gpu-node: every run (the fake server with its pusher threads and either module, and the
     # reference reflector's processes) on the CPUs of the GPU's NUMA node, as a server is deployed
     # next to its GPU; none: wherever the scheduler puts them (the box allows both sockets)
@@ -171,6 +225,12 @@ def main():
         cpus = gpu_node_cpus()
         os.sched_setaffinity(0, cpus)                  # inherited by every run started below
         affinity.update(cpus=cpu_ranges(cpus), n_cpus=len(cpus))
+    if args.realtime_sweep:
+        print(json.dumps({"workload": f"C2-shaped fleets at their real rate through the QTSS module: RTSP-interleaved "
+                                      f"H.264 30-fps 4 Mb/s pushers x {args.subs} UDP players, {args.threads} pusher "
+                                      f"threads, {args.seconds} s timed after 1 s", "affinity": affinity,
+                          **realtime_sweep(args)}))
+        return
     if args.realtime:
         print(json.dumps({"workload": f"C2 at its real rate through the QTSS module: {args.sessions} RTSP-interleaved "
                                       f"H.264 30-fps pushers x {args.subs} UDP players, {args.threads} pusher threads, "

@@ -717,6 +717,8 @@ struct Pusher {                                        // one synthetic H.264 pu
 };
 static const bool g_bench_trace = getenv("EDGPU_BENCH_TRACE") && atoi(getenv("EDGPU_BENCH_TRACE")) != 0;
 static std::atomic<uint64_t> g_pushed{0};             // --bench: RTSPIncomingData calls made (per dispatch phase)
+// the reference module's host (oracle/ref_module_host.cpp): its task threads for a real-time bench
+static void (*g_ref_ticker)(int) = nullptr;
 static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Error (*tick_fn)(void),
                      QTSS_Error (*last_fn)(EDGPU_QTSSTickInfo*)) {
     (void)poll_fn;
@@ -819,11 +821,12 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         P.ts += 90000 / fps;
     };
     if (g_realtime) {
-        // Real time: the pushers push each frame at its time (1024 x 30 fps sessions, as a server's
-        // RTSP threads receive them); the module reflects on its own ticker (EDGPU_QTSS_TICK_MSEC,
+        // Real time: the pushers push each frame at its time (1024 x 30 fps sessions, their capture
+        // times spread over the frame interval, as a server's RTSP threads receive them); the module reflects on its own ticker (EDGPU_QTSS_TICK_MSEC,
         // EDGPU_QTSS_REFLECT_ON_ARRIVAL).  Measured after a 1-s warm-up: relayed packets/s and the
         // latency from RTSPIncomingData to QTSS_Write of every RTP packet.
         using Clk = std::chrono::steady_clock;
+        if (g_ref_ticker) g_ref_ticker(1);
         const auto t0 = Clk::now();
         std::atomic<bool> done{false};
         std::vector<std::thread> th;
@@ -833,8 +836,11 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
                 while (!done.load()) {
                     const int64_t el = std::chrono::duration_cast<std::chrono::milliseconds>(Clk::now() - t0).count();
                     advance_clock(el);
+                    // independent pushers are not frame-synchronous: session s captures its frames
+                    // s / nsess of a frame interval after session 0
                     for (uint32_t s = w; s < nsess; s += nthreads)
-                        while ((int64_t)ps[s].frame * 1000 / fps <= el) push_frame(s, fr, el);
+                        while ((int64_t)ps[s].frame * 1000 / fps + (int64_t)s * (1000 / fps) / nsess <= el)
+                            push_frame(s, fr, el);
                     std::this_thread::sleep_for(std::chrono::microseconds(500));
                 }
             });
@@ -886,6 +892,8 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         std::this_thread::sleep_for(std::chrono::milliseconds(1000));
         g_lat_on = true;
         const uint64_t w0 = stream_writes();
+        EDGPU_QTSSTickInfo tA;
+        if (last_fn(&tA)) return 3;
         const auto m0 = Clk::now();
         std::this_thread::sleep_for(std::chrono::milliseconds((int64_t)(seconds * 1000)));
         const uint64_t w1 = stream_writes();
@@ -894,6 +902,7 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         done = true;
         for (auto& t : th) t.join();
         if (churner.joinable()) churner.join();
+        if (g_ref_ticker) g_ref_ticker(0);
         auto stats = [](std::vector<double> v) {
             std::sort(v.begin(), v.end());
             char b[160];
@@ -926,17 +935,25 @@ static int run_bench(int argc, char** argv, uint32_t (*poll_fn)(void), QTSS_Erro
         };
         EDGPU_QTSSTickInfo ti;
         if (last_fn(&ti)) return 3;
+        // the ticks of the timed window: count and mean wall time with its parts
+        const double nt = (double)std::max<uint64_t>(1, ti.ticks - tA.ticks);
+        char tw[320];
+        snprintf(tw, sizeof(tw), "{\"ticks\": %llu, \"wall_ms\": %.3f, \"ingest_ms\": %.3f, \"fanout_ms\": %.3f, "
+                 "\"readback_ms\": %.3f, \"write_ms\": %.3f}", (unsigned long long)(ti.ticks - tA.ticks),
+                 (ti.wall_sum_ms - tA.wall_sum_ms) / nt, (ti.ingest_sum_ms - tA.ingest_sum_ms) / nt,
+                 (ti.fanout_sum_ms - tA.fanout_sum_ms) / nt, (ti.readback_sum_ms - tA.readback_sum_ms) / nt,
+                 (ti.write_sum_ms - tA.write_sum_ms) / nt);
         const char* tm = getenv("EDGPU_QTSS_TICK_MSEC");
         const char* ar = getenv("EDGPU_QTSS_REFLECT_ON_ARRIVAL");
-        printf("{\"mode\": \"realtime\", \"sessions\": %u, \"subs\": %u, \"pusher_threads\": %u, \"tick_ms\": %s, "
+        printf("{\"mode\": \"realtime\", \"module\": \"%s\", \"sessions\": %u, \"subs\": %u, \"pusher_threads\": %u, \"tick_ms\": %s, "
                "\"reflect_on_arrival_ms\": %s, \"seconds\": %.3f, \"relayed_per_s\": %.1f, \"ticks\": %llu, "
                "\"failed_ticks\": %llu, \"lock_hold_ms\": {\"mean\": %.3f, \"max\": %.3f}, "
                "\"latency_ms\": {\"packets\": %llu, \"mean\": %.3f, \"p50\": %.2f, "
-               "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}, \"rtsp_ms\": %s}\n",
-               nsess, nsub, nthreads, tm ? tm : "20", ar ? ar : "0", secs, (double)(w1 - w0) / secs,
+               "\"p99\": %.2f, \"p999\": %.2f, \"max_bin\": %.2f}, \"rtsp_ms\": %s, \"window_ticks\": %s}\n",
+               g_ref_ticker ? "reference" : "drop-in", nsess, nsub, nthreads, tm ? tm : "20", ar ? ar : "0", secs, (double)(w1 - w0) / secs,
                (unsigned long long)ti.ticks, (unsigned long long)ti.failed_ticks,
                ti.ticks ? ti.hold_sum_ms / (double)ti.ticks : 0.0, ti.hold_max_ms, (unsigned long long)all.n,
-               all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12), rtsp.c_str());
+               all.n ? all.sum_us / all.n / 1000.0 : 0.0, pct(0.5), pct(0.99), pct(0.999), pct(1.0 - 1e-12), rtsp.c_str(), tw);
         return 0;
     }
     const uint32_t nticks = (uint32_t)(seconds * 1000 / tick_ms + 0.5);
@@ -1151,6 +1168,7 @@ int main(int argc, char** argv) {
     if (bench) {
         auto last_fn = (QTSS_Error (*)(EDGPU_QTSSTickInfo*))dlsym(so, "EDGPU_QTSSReflectorModule_LastTick");
         if (!last_fn) { fprintf(stderr, "module entry points missing\n"); return 3; }
+        g_ref_ticker = (void (*)(int))dlsym(so, "EDGPU_REFHOST_Ticker");
         const int rc = run_bench(argc, argv, poll_fn, tick_fn, last_fn);
         memset(&rp, 0, sizeof(rp));
         (void)g_dispatch(QTSS_Shutdown_Role, &rp);
