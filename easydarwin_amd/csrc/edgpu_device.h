@@ -288,6 +288,7 @@ struct TickTotals {                 // device-side, mirrors edgpu_tick_stats
     unsigned long long fan_t0_min, fan_done_min, fan_done_max;
     unsigned long long ing_t0_min, ing_done_min, ing_done_max;    // the same for k_ingest
     unsigned long long ing_last_span, ing_last_first;             // ... of the last finished ingest
+    unsigned long long ing_ph[8], ing_last_ph[8];                 // k_ingest phase sums ([0]: segments)
     // Copy passes of an over-capacity tick (edgpu_fanout_next).  Slot k & 1 belongs to the k-th
     // launched pass: the arena bytes and descriptors its sub-streams span, and the id of the next
     // pass (kNoPass: none).  A pass's plan resets the other slot for the pass after it.

@@ -2117,6 +2117,11 @@ int edgpu_tick_stats_get(edgpu_ctx* x, edgpu_tick_stats* out) {
         fprintf(stderr, "fan tail: span %.1f us, first exit at %.1f us, items %u; ingest span %.1f us, first exit at %.1f us\n",
                 (t.fan_done_max - t.fan_t0_min) / 100.0, (t.fan_done_min - t.fan_t0_min) / 100.0, t.nwork,
                 t.ing_last_span / 100.0, t.ing_last_first / 100.0);
+    if (getenv("EDGPU_FAN_TAIL") && t.ing_last_ph[0]) {
+        fprintf(stderr, "ingest phases (us per segment, %llu segments):", (unsigned long long)t.ing_last_ph[0]);
+        for (int k = 1; k < 7; k++) fprintf(stderr, " %.2f", t.ing_last_ph[k] / 100.0 / t.ing_last_ph[0]);
+        fprintf(stderr, "\n");
+    }
 #endif
     return EDGPU_OK;
 }

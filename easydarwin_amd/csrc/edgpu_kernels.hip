@@ -323,10 +323,12 @@ template <uint32_t DEPTH, int THREADS = kIngestThreads>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_ingest(IngestParams P) {
     constexpr int NW = THREADS / 64;
     const uint32_t seg = blockIdx.x;
+    const int tid = threadIdx.x;
     const uint32_t b = P.seg_off[seg], e = P.seg_off[seg + 1];
     const SessionDev S = P.sessions[P.seg_sess[seg]];
     const uint32_t nsnd = 2 * S.ntracks;
-    const int tid = threadIdx.x;
+    // a copy pass the last tick still owes (edgpu_fanout_next): read now, checked at the end
+    const bool pass_owed = P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
 
     __shared__ uint64_t s_head[kMaxSendersPerSession], s_vbyte[kMaxSendersPerSession];
     __shared__ uint32_t s_vcount[kMaxSendersPerSession], s_valid[kMaxSendersPerSession];
@@ -396,8 +398,24 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid < (int)nsnd) c_lastacc[tid] = -1;
 #ifdef EDGPU_AB_VARIANTS
     if (tid == 0) atomicMin(&P.totals->ing_t0_min, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    // measurement builds: thread 0's time per phase (s_memrealtime, 100 MHz), summed over the
+    // non-empty segments (EDGPU_FAN_TAIL prints the means): 1 session / sender state, 2 descriptor
+    // + header + SSRC filter, 3 rank scans, 4 meta stores + keyframe ballots, 5 slot copy, 6 tail
+    unsigned long long ph_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_last = __builtin_amdgcn_s_memrealtime();
+#define EDGPU_ING_T(k)                                                                   \
+    do {                                                                                 \
+        if (tid == 0) {                                                                  \
+            const unsigned long long ph_now = __builtin_amdgcn_s_memrealtime();          \
+            ph_t[k] += ph_now - ph_last;                                                 \
+            ph_last = ph_now;                                                            \
+        }                                                                                \
+    } while (0)
+#else
+#define EDGPU_ING_T(k) do {} while (0)
 #endif
     __syncthreads();
+    EDGPU_ING_T(1);
 
     uint64_t in_pk = 0, in_bytes = 0;
     // ReflectorSession::fHasVideoKeyFrameUpdate before the chunk (every thread keeps the same)
@@ -551,6 +569,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 }
             }
             __syncthreads();
+            EDGPU_ING_T(2);
             len = p_len[tid];
         }
         // ---- receive-time trailer (ReflectorSocket::ProcessPacket, ReflectorStream.cpp:1960-1994):
@@ -617,6 +636,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 if ((ls ^ 1u) == s) sib_incl = incl;
             }
             __syncthreads();
+            EDGPU_ING_T(3);
             if (tid < (int)ns) {
                 uint64_t t = 0;
                 for (int w = 0; w < NW; w++) t += s_wsum[tid][w];
@@ -660,6 +680,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         p_slotb[tid] = slotb;
         p_vb[tid] = vb;
         __syncthreads();
+        EDGPU_ING_T(4);
         // ---- keyframe index, part 2: a video key packet moves its sender's key pointer; an audio
         // packet anchors its sender's when the last key / audio event before it was a key packet
         // (none in the chunk before it: the session's flag); the newest such packet per sender wins
@@ -762,6 +783,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (tid < (int)S.ntracks) s_count[tid] += (c_tot[2 * tid] & 1023) + (c_tot[2 * tid + 1] & 1023);
         if (tid < (int)nsnd) c_lastacc[tid] = -1;
         __syncthreads();
+        EDGPU_ING_T(5);
     }
 
     if (tid < (int)nsnd) {
@@ -776,18 +798,21 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         // a copy pass the last tick still owes (edgpu_fanout_next): this batch must not lap what
         // that tick's remaining passes read
-        const bool guard = P.totals->pass_next[P.totals->pass_slot & 1u] != kNoPass;
-        if (guard && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
+        if (pass_owed && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
                       s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
             atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);
     }
     if (tid < (int)S.ntracks) P.streams[S.first_stream + tid].packet_count = s_count[tid];
     if (tid == 0) P.sessions[P.seg_sess[seg]].video_key_flag = kflag ? 1u : 0u;
-    // block totals
-    uint64_t t1, t2;
-    const uint64_t a1 = block_exclusive_scan<uint64_t, NW>(in_pk, scan64, t1);
-    const uint64_t a2 = block_exclusive_scan<uint64_t, NW>(in_bytes, scan64, t2);
-    (void)a1; (void)a2;
+    // block totals: packets (< 2^21) and bytes (< 2^32) of the segment packed in one word, one
+    // DPP scan per wave and one barrier
+    const uint64_t wt = wave_inclusive_scan_u64(in_bytes << 21 | in_pk);
+    if ((tid & 63) == 63) scan64[tid >> 6] = wt;
+    __syncthreads();
+    uint64_t t1 = 0, t2 = 0;
+    if (tid == 0) {
+        for (int w = 0; w < NW; w++) { t1 += scan64[w] & ((1ull << 21) - 1); t2 += scan64[w] >> 21; }
+    }
     if (tid == 0 && !(EDGPU_ABL(P) & 16u)) {
         atomicAdd(&P.totals->cum_ingested_packets, (unsigned long long)t1);
         atomicAdd(&P.totals->cum_ingested_bytes, (unsigned long long)t2);
@@ -796,6 +821,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     if (seg == 0 && tid == 0) { P.totals->ing_pk[P.ing_slot ^ 1u] = 0; P.totals->ing_b[P.ing_slot ^ 1u] = 0; }
 #ifdef EDGPU_AB_VARIANTS
+    EDGPU_ING_T(6);
+    if (tid == 0 && e > b) {
+        for (int k = 1; k < 7; k++) atomicAdd(&P.totals->ing_ph[k], ph_t[k]);
+        atomicAdd(&P.totals->ing_ph[0], 1ull);
+    }
     if (tid == 0) {
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
         atomicMin(&P.totals->ing_done_min, t);
@@ -905,6 +935,7 @@ __device__ __forceinline__ void reset_tick_totals(TickTotals* t) {
     // measurement builds: the last ingest's span and first workgroup exit, then a reset
     t->ing_last_span = t->ing_done_max - t->ing_t0_min; t->ing_last_first = t->ing_done_min - t->ing_t0_min;
     t->ing_t0_min = ~0ull; t->ing_done_min = ~0ull; t->ing_done_max = 0;
+    for (int k = 0; k < 8; k++) { t->ing_last_ph[k] = t->ing_ph[k]; t->ing_ph[k] = 0; }
 #endif
     // a pass the previous tick still owed is lost now (its host never called edgpu_fanout_next)
     if (t->pass_next[t->pass_slot & 1u] != kNoPass) t->cum_lost_passes++;
