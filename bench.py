@@ -116,7 +116,7 @@ def make_pinned(ctx: edgpu.Context, bt: dict):
     return parts
 
 
-def run_step(ctx: edgpu.Context, bt: dict):
+def run_step(ctx: edgpu.Context, bt: dict, link=None):
     if "pinned" in bt:
         p = bt["pinned"]
         ctx.ingest_pinned(p["desc"].ptr, bt["n"], p["seg"].ptr, p["sess"].ptr, bt["nseg"], p["blob"].ptr, bt["bytes"])
@@ -126,46 +126,65 @@ def run_step(ctx: edgpu.Context, bt: dict):
         ctx.ingest_device(bt["desc"].data_ptr(), bt["n"], bt["seg"].data_ptr(), bt["sess"].data_ptr(),
                           bt["nseg"], bt["blob"].data_ptr(), bt["bytes"])
     ctx.keyframe_index()
+    if link is not None:                # N > 1: this rank's images to its replicas' ranks, and back
+        link.sync(bt["t"])
     ctx.fanout(bt["t"])
 
 
-def cross_device_check(ctx, args, gids, world: int, rank: int, backend: str, local: int, sdp: str, now_ms: int,
-                       k: int = 16) -> dict:
-    """N > 1, after the timed steps (untimed): BASELINE C4's cross-GPU exchange on the node's own
-    devices.  Every rank takes replicas of the first k sessions of the next rank and brings their
-    session images over with dist.exchange_images (DistReplicaLink.sync: RCCL batch_isend_irecv
-    between the GPUs' device buffers under nccl, host buffers under gloo); then each replica's GOP
-    (the CKeyFrameCache image, key packet -> newest) must equal its owner's byte for byte."""
+def replica_preflight(ctx, world: int, rank: int) -> dict:
+    """N > 1, before the steady state: can this node's processes map each other's HBM (IPC handles,
+    HSA dmabuf)?  Every rank exports a small buffer, opens the next rank's and writes / reads a word
+    there; failures are caught locally so every rank reaches every collective.  All ranks get the
+    same verdict (the replicas run only if every rank passed)."""
+    import numpy as np
+    import torch.distributed as tdist
+    mine, err, buf = None, None, None
+    try:
+        buf = ctx.device_alloc(4096)
+        ctx.copy_to_device(buf.ptr, np.zeros(16, np.uint8))
+        mine = ctx.ipc_export(buf.ptr)
+    except Exception as e:                            # noqa: BLE001 -- reported in the line
+        err = f"export: {type(e).__name__}: {e}"
+    hs = [None] * world
+    tdist.all_gather_object(hs, mine)
+    nxt = hs[(rank + 1) % world]
+    if err is None and nxt is not None:
+        try:
+            p = ctx.ipc_open(nxt)
+            ctx.copy_to_device(p + 8 * rank % 4096, np.array([rank + 1], np.uint64))
+            ok = int(ctx.copy_to_host(p + 8 * rank % 4096, 8).view(np.uint64)[0]) == rank + 1
+            ctx.ipc_close(p)
+            if not ok:
+                err = "peer word read back wrong"
+        except Exception as e:                        # noqa: BLE001
+            err = f"open: {type(e).__name__}: {e}"
+    elif err is None:
+        err = "next rank exported no handle"
+    res = [None] * world
+    tdist.all_gather_object(res, err)
+    tdist.barrier()
+    if buf is not None:
+        buf.free()
+    errs = [e for e in res if e]
+    return {"ok": not errs, "error": errs[0] if errs else None}
+
+
+def replica_check(ctx, link, gids, world: int) -> dict:
+    """After the timing: every replica's GOP (the CKeyFrameCache image, key packet -> newest) equals
+    its owner's byte for byte (sha256, gathered)."""
     import hashlib
     import torch.distributed as tdist
-    from easydarwin_amd.replica import DistReplicaLink
-    torch.cuda.set_device(local)                      # (a thread of its own: HIP's device is per thread)
-    link = DistReplicaLink(ctx, world, rank, comm="cuda" if backend == "nccl" else "cpu")
-    for si, g in enumerate(gids):
-        link.own(int(g), si)
-    want = [int(g) for g in owned_sessions(args.sessions, (rank + 1) % world, world)[:k]]
-    for g in want:
-        link.want(g, sdp)
-    tdist.barrier()
-    t0 = time.perf_counter()
-    sent, recv = link.sync(now_ms)
-    ms = (time.perf_counter() - t0) * 1e3
 
     def digest(s):
         return hashlib.sha256(ctx.gop_copy(s, 0)[0]).hexdigest()
-    mine = {int(g): digest(si) for si, g in enumerate(gids[:k])}
+    mine = {int(g): digest(si) for si, g in enumerate(gids) if int(g) in link.wanted_by_others}
     every = [None] * world
     tdist.all_gather_object(every, mine)
     owners = {g: d for m in every for g, d in m.items()}
-    ok = all(digest(link.replica_of[g]) == owners[g] for g in want)
+    ok = all(digest(s) == owners[g] for g, s in link.replica_of.items())
     res = [None] * world
-    tdist.all_gather_object(res, (ok, int(sent), int(recv), ms))
-    return {"ok": all(r[0] for r in res), "ranks": world, "sessions_per_rank": k,
-            "image_bytes": sum(r[1] for r in res), "received_bytes": sum(r[2] for r in res),
-            "ms_max": round(max(r[3] for r in res), 3),
-            "transport": ("RCCL batch_isend_irecv, device buffers on distinct GPUs" if backend == "nccl"
-                          else "gloo, host buffers (ranks may share a GPU)"),
-            "check": "each replica's GOP image (key packet -> newest) equals its owner's (sha256)"}
+    tdist.all_gather_object(res, ok)
+    return {"ok": all(res), "check": "each replica's GOP image (key packet -> newest) equals its owner's (sha256)"}
 
 
 def run_bounded(fn, seconds: float):
@@ -492,6 +511,11 @@ def main():
     ap.add_argument("--all-timing-events", action="store_true",
                     help="record every timing event inside the timed steps too (the ingest / keyframe / "
                          "plan durations then come from them; each event costs the step 4-8 us)")
+    ap.add_argument("--replicas", type=int, default=64,
+                    help="N > 1: sessions of the next rank each rank replicates in the steady state (BASELINE "
+                         "C4: subscribers whose egress GPU is not the stream's owner), fed every step through "
+                         "peer mailboxes (xGMI, no collective); 0: none")
+    ap.add_argument("--replica-subs", type=int, default=1, help="UDP subscribers per replica session")
     ap.add_argument("--ablation-study", action="store_true",
                     help="allow EDGPU_ABLATE (timing experiments that skip work): the line is then not a "
                          "valid measurement and says so")
@@ -579,9 +603,26 @@ def main():
                 ctx.subscriber_rewrite(h, 0, ssrc=int(fleet.ssrc[si]))
             elif args.rewrite:
                 ctx.subscriber_rewrite(h, 0, seq_delta=h * 7919 + 1, ts_delta=h * 0x9E3779B1, ssrc=0x5EED0000 + h)
+    # N > 1: BASELINE C4's steady state inside the timed steps -- each rank replicates the first
+    # --replicas sessions of the next rank (subscribers whose egress GPU is not the owner's), joined
+    # here (the collective: mailbox handles) and fed every step through peer mailboxes (no collective)
+    link, rep = None, None
+    if dist and world > 1 and args.replicas > 0:
+        pre = replica_preflight(ctx, world, rank)
+        rep = {"preflight": pre}
+        if pre["ok"]:
+            from easydarwin_amd.replica import DistReplicaLink
+            link = DistReplicaLink(ctx, world, rank, lockstep=False)
+            for si, g in enumerate(gids):
+                link.own(int(g), si)
+            for g in owned_sessions(args.sessions, (rank + 1) % world, world)[:args.replicas]:
+                rs = link.want(int(g), fleet.sdp())
+                for _k in range(args.replica_subs):
+                    ctx.subscriber_add(rs, edgpu.TRANSPORT_UDP)
+            link.connect()
 
     for i in range(warm):
-        run_step(ctx, batches[i])
+        run_step(ctx, batches[i], link)
     ctx.sync()
     st = ctx.stats()
     if st.status != 0:
@@ -597,14 +638,18 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    x0 = (link.sync_s, link.bytes_sent, sum(mb.wait_s for mb, _ in list(link.out.values()) + list(link.inbox.values()))) \
+        if link else None
     t0 = time.perf_counter()
     for i in range(warm, warm + steps):
-        run_step(ctx, batches[i])
+        run_step(ctx, batches[i], link)
     ctx.sync()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    x1 = (link.sync_s, link.bytes_sent, sum(mb.wait_s for mb, _ in list(link.out.values()) + list(link.inbox.values()))) \
+        if link else None
 
     c1 = ctx.counters()
     st = ctx.stats()
@@ -614,7 +659,7 @@ def main():
     if extra:
         ctx.set_timing(ctx.TIMING_ALL)
         for i in range(warm + steps, warm + steps + extra):
-            run_step(ctx, batches[i])
+            run_step(ctx, batches[i], link)
         ctx.sync()
         if ctx.stats().status != 0:
             raise SystemExit("engine status after the timing steps")
@@ -633,13 +678,28 @@ def main():
 
     dt, (relayed_all, out_all) = reduce_run(dt, [relayed, out_bytes], device=dev if backend == "nccl" else None,
                                           force=force_pg)
-    # N > 1: the C4 session-image exchange across the devices, checked (after the timing; bounded:
-    # a hung exchange is reported and the process ends without waiting for it)
+    # N > 1: the replicas' GOPs against their owners' (after the timing; bounded: a hung check is
+    # reported and the process ends without waiting for it), and the steady-state exchange's cost
     xdev, hung = None, False
-    if dist and world > 1:
-        now_ms = int(batches[warm + steps + extra - 1]["t"])
-        xdev, hung = run_bounded(lambda: cross_device_check(ctx, args, gids, world, rank, backend, local,
-                                                            fleet.sdp(), now_ms), 120.0)
+    if dist and world > 1 and rep is not None:
+        if link is not None:
+            def check():
+                torch.cuda.set_device(local)          # (a thread of its own: HIP's device is per thread)
+                return replica_check(ctx, link, gids, world)
+            xdev, hung = run_bounded(check, 120.0)
+            if not hung:
+                per = [None] * world
+                dist.all_gather_object(per, ((x1[0] - x0[0]) / steps, (x1[1] - x0[1]) / steps, (x1[2] - x0[2]) / steps))
+                rep.update({
+                    "sessions_per_rank": args.replicas, "subs_each": args.replica_subs,
+                    "exchange_ms_per_step": round(1e3 * max(p[0] for p in per), 4),
+                    "peer_wait_ms_per_step": round(1e3 * max(p[2] for p in per), 4),
+                    "image_bytes_per_step": int(sum(p[1] for p in per)),
+                    "transport": "peer mailboxes in the owners' HBM (IPC handles at the join); the replica's GPU "
+                                 "imports over xGMI; no collective inside the timed steps",
+                    "check": xdev})
+        else:
+            xdev = {"ok": False, "error": rep["preflight"]["error"], "replicas": "skipped: IPC preflight failed"}
 
     # a failed or hung check may leave other ranks inside a collective: end without tearing the
     # process group down (which could wait on them)
@@ -723,6 +783,8 @@ def main():
                    "rewrite": rewrite_desc,
                    "engine_env": knobs,
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"
+                                  + (f"; C4 replicas: {args.replicas} sessions/rank fed through peer mailboxes"
+                                     if link is not None else "")
                                   + ("" if backend == "nccl" or world == 1 else f" ({backend} rehearsal, ranks sharing GPUs)"),
                    "process_group": (backend if dist else None)},
         "relayed_GBps": round(out_all / dt / 1e9, 2),
@@ -753,7 +815,9 @@ def main():
                       "and 7.1-7.9 M in reference-exact one-datagram-per-send mode, 0.85-1.00x the reference's "
                       "sendto() path on the same box (profiles/r05z_wire/, DESIGN.md 5.6)"),
     }
-    if xdev is not None:
+    if rep is not None:
+        res["replicas"] = rep
+    elif xdev is not None:
         res["cross_device"] = xdev
     print(json.dumps(res), flush=True)
     if bail:

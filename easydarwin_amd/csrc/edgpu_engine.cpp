@@ -2579,6 +2579,43 @@ int edgpu_device_alloc(edgpu_ctx* x, uint64_t bytes, void** out) {
     return EDGPU_OK;
 }
 
+int edgpu_ipc_export(edgpu_ctx* x, const void* p, uint8_t handle[EDGPU_IPC_HANDLE_BYTES]) {
+    if (!x || !p || !handle) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    static_assert(sizeof(hipIpcMemHandle_t) == EDGPU_IPC_HANDLE_BYTES, "IPC handle size");
+    DEVICE_ENTER(x);
+    hipIpcMemHandle_t h;
+    HIP_CHECK(hipIpcGetMemHandle(&h, const_cast<void*>(p)));
+    memcpy(handle, &h, sizeof(h));
+    return EDGPU_OK;
+}
+
+int edgpu_ipc_open(edgpu_ctx* x, const uint8_t handle[EDGPU_IPC_HANDLE_BYTES], void** out) {
+    if (!x || !handle || !out) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    DEVICE_ENTER(x);
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    *out = nullptr;
+    HIP_CHECK(hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess));
+    return EDGPU_OK;
+}
+
+int edgpu_ipc_close(edgpu_ctx* x, void* p) {
+    if (!x || !p) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    DEVICE_ENTER(x);
+    HIP_CHECK(sync_all(x));                     // nothing enqueued may still read it
+    HIP_CHECK(hipIpcCloseMemHandle(p));
+    return EDGPU_OK;
+}
+
+int edgpu_copy_to_device(edgpu_ctx* x, void* dst, const void* src, uint64_t bytes) {
+    if (!x || (bytes && (!dst || !src))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (!bytes) return EDGPU_OK;
+    DEVICE_ENTER(x);
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, x->stream));
+    HIP_CHECK(wsync(x, x->stream));            // `src` is the caller's
+    return EDGPU_OK;
+}
+
 // The host CPUs of the device's NUMA node (its PCI function's sysfs local_cpulist) that the
 // calling thread may run on: where a server's host threads belong next to this GPU.
 int edgpu_device_local_cpus(int device, uint32_t* cpus, uint32_t cap, uint32_t* n_out) {

@@ -43,7 +43,9 @@ EXPORTED = [
     "edgpu_subscriber_slot", "edgpu_egress_pacing_config", "edgpu_egress_pacing", "edgpu_egress_clock",
     "edgpu_egress_block_info", "edgpu_session_remote_join", "edgpu_session_remote_leave",
     "edgpu_subscriber_set_slot", "edgpu_device_local_cpus", "edgpu_debug_stall",
+    "edgpu_ipc_export", "edgpu_ipc_open", "edgpu_ipc_close", "edgpu_copy_to_device",
 ]
+IPC_HANDLE_BYTES = 64
 TCP_MESSAGE, TCP_DROPPED = 1, 2
 PKT_REMOTE_ODD = 1          # edgpu_pkt_desc.flags: a UDP datagram from an odd source port
 IMAGE_FULL = 0xFFFFFFFFFFFFFFFF
@@ -229,6 +231,10 @@ def load(path: str = LIB_PATH):
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
+        "edgpu_ipc_export": (I32, [P, P, P]),
+        "edgpu_ipc_open": (I32, [P, P, C.POINTER(P)]),
+        "edgpu_ipc_close": (I32, [P, P]),
+        "edgpu_copy_to_device": (I32, [P, P, P, U64]),
         "edgpu_fanout_kernel": (C.c_char_p, [P]),
         "edgpu_subscriber_play": (I32, [P, U32, I32, U32, I64, C.POINTER(U32), P]),
         "edgpu_subscribers_add": (I32, [P, U32, P, P, P]),
@@ -610,6 +616,27 @@ class Context:
 
     def device_alloc(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
+
+    def ipc_export(self, dev_ptr: int) -> bytes:
+        """The inter-process handle of a buffer from device_alloc (edgpu_ipc_export)."""
+        h = (C.c_uint8 * IPC_HANDLE_BYTES)()
+        _check(self.lib.edgpu_ipc_export(self.h, C.c_void_p(dev_ptr), h))
+        return bytes(h)
+
+    def ipc_open(self, handle: bytes) -> int:
+        """Maps another process's buffer (edgpu_ipc_open); returns the pointer this GPU uses."""
+        h = (C.c_uint8 * IPC_HANDLE_BYTES).from_buffer_copy(handle)
+        out = C.c_void_p()
+        _check(self.lib.edgpu_ipc_open(self.h, h, C.byref(out)))
+        return int(out.value)
+
+    def ipc_close(self, ptr: int):
+        _check(self.lib.edgpu_ipc_close(self.h, C.c_void_p(ptr)))
+
+    def copy_to_device(self, dev_ptr: int, data):
+        a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data)
+        if a.nbytes:
+            _check(self.lib.edgpu_copy_to_device(self.h, C.c_void_p(dev_ptr), _ptr(a), int(a.nbytes)))
 
     def copy_to_host(self, dev_ptr, nbytes: int) -> np.ndarray:
         out = np.empty(int(nbytes), dtype=np.uint8)

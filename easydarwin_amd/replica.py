@@ -14,8 +14,10 @@ Transport:
 
 * in one process (two contexts, possibly on two GPUs): ``ReplicaLink`` exports into a buffer
   on the owner's GPU and pulls it with ``edgpu_memcpy_peer`` (hipMemcpyPeerAsync);
-* one process per GPU: ``dist.exchange_images`` moves images with RCCL point-to-point
-  send/recv, batched the way ``ncclGroupStart``/``ncclSend``/``ncclRecv`` batch them.
+* one process per GPU: ``DistReplicaLink`` -- at the join each owner hands every replica rank
+  the IPC handle of a mailbox in its HBM (easydarwin_amd/mailbox.py); after that the owner
+  exports into it and the replica's GPU imports straight out of it over xGMI, with no
+  collective on the steady-state path.
 """
 from __future__ import annotations
 
@@ -127,80 +129,178 @@ class ReplicaLink:
 
 
 class DistReplicaLink:
-    """The one-process-per-GPU form of ReplicaLink: the owner of global session g is rank
-    ``dist.owner(g, world)``; a rank that serves subscribers of a session it does not own keeps
-    a replica of it, and every ``sync`` round moves full images (first time) or deltas from the
-    owners with ``dist.exchange_images`` (RCCL point-to-point under the nccl backend, device
-    buffers; gloo in CPU-side tests, host buffers).  Every rank calls ``sync`` at the same
-    points (it is collective)."""
+    """The one-process-per-GPU form of ReplicaLink.  The owner of global session g is rank
+    ``dist.owner(g, world)``; a rank that serves subscribers of a session it does not own keeps a
+    replica of it.
 
-    def __init__(self, ctx: edgpu.Context, world: int, rank: int, comm: str = "cuda"):
-        import torch
-        self.torch = torch
+    Joins are the control plane, and the only collective: ``connect`` gathers every rank's
+    replicated sessions, each owner sizes one peer mailbox per replica rank in its own HBM
+    (``mailbox.Mailbox``: double-buffered image slots + header words) and hands its IPC handle
+    over, and the replica maps it (``edgpu_ipc_open``); ``places`` numbers the joiners in their
+    owners' bucket arrays (``dist.route_places``).  The steady state has no collective: ``sync``
+    exports each owned session's images (full the first time per replica rank, deltas after)
+    straight into the mailboxes and imports this rank's replicas straight from the owners'
+    mailboxes -- the replica's GPU reads the owner's HBM over xGMI -- and ``feedback`` carries the
+    replicas' relocations back through the same mailboxes.  Every rank calls ``connect`` /
+    ``places`` at the same (join) ticks and ``sync`` / ``feedback`` at every tick.
+
+    lockstep: ``feedback`` waits for every replica's relocations of the tick (exact one-process
+    semantics, the parity tests); without it a relocation may reach its owner a tick late.
+    session_bytes: mailbox slot room per replicated session (full images are key -> newest:
+    about 2 s of stream; default EDGPU_MAILBOX_SESSION_MB or 4 MiB)."""
+
+    def __init__(self, ctx: edgpu.Context, world: int, rank: int, lockstep: bool = True,
+                 session_bytes: int | None = None, timeout_s: float = 60.0, region_cls=None):
+        import os
+
+        from .mailbox import DeviceRegion
+        self.region_cls = region_cls or DeviceRegion     # mailbox.HostRegion: the CPU rehearsal
         self.ctx, self.world, self.rank = ctx, world, rank
-        self.comm = comm                              # "cuda": RCCL device buffers; "cpu": gloo
+        self.lockstep = lockstep
+        self.session_bytes = session_bytes or int(float(os.environ.get("EDGPU_MAILBOX_SESSION_MB", "4")) * (1 << 20))
+        self.timeout_s = timeout_s
         self.local_of: dict[int, int] = {}            # owned global session -> engine session
         self.replica_of: dict[int, int] = {}          # replicated global session -> engine session
         self.heads: dict[tuple[int, int], np.ndarray] = {}   # (global session, dst rank) -> heads
+        self.out: dict[int, tuple] = {}               # dst rank -> (Mailbox, [global sessions])
+        self.inbox: dict[int, tuple] = {}             # src rank -> (Mailbox, [global sessions])
+        self._retired: list = []                      # replaced mailboxes, freed at the next connect
         self.bytes_sent = self.bytes_received = 0
+        self.sync_s = 0.0                             # host time inside sync()
 
     def own(self, g: int, local: int):
         self.local_of[int(g)] = int(local)
 
     def want(self, g: int, sdp: str, udp_push: bool = False) -> int:
-        """Creates the replica of global session g here; its first sync brings the full image."""
+        """Creates the replica of global session g here; the next connect() brings it into its
+        owner's mailbox and the sync after that its full image."""
         rs = self.ctx.session_add(sdp, udp_push)
         self.replica_of[int(g)] = rs
         return rs
 
     def places(self, events):
-        """dist.route_places over this context: the owners here take / free the places of every
-        rank's replica joins / leaves (events as route_places takes them); returns {key: place}
-        for this rank's joins, each to be given to its subscriber with subscriber_set_slot."""
+        """dist.route_places over this context (collective, at joins): the owners here take / free
+        the places of every rank's replica joins / leaves; returns {key: place} for this rank's
+        joins, each to be given to its subscriber with subscriber_set_slot."""
         from .dist import route_places
         return route_places(events, lambda g: self.ctx.session_remote_join(self.local_of[g]),
                             lambda g, p: self.ctx.session_remote_leave(self.local_of[g], p),
                             self.world, self.rank)
 
-    def _export(self, sessions, dst_rank, now_ms):
+    def connect(self):
+        """The join round (collective): every rank's replicated sessions reach their owners, which
+        (re)create the mailboxes whose session lists grew past their room and hand the new
+        handles over.  A mailbox keeps its sequence when only its list changes."""
+        import torch.distributed as dist
+
+        from .dist import owner
+        from .mailbox import Mailbox
+        for mb in self._retired:
+            mb.close()
+        self._retired = []
+        wants = [None] * self.world
+        dist.all_gather_object(wants, sorted(self.replica_of))
+        made = {}
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            mine = [g for g in wants[r] if owner(g, self.world) == self.rank]
+            cur = self.out.get(r)
+            if not mine:
+                if cur:
+                    self._retired.append(cur[0])
+                    self.out.pop(r)
+                continue
+            if cur is None or len(mine) > cur[0].max_sessions:
+                room = max(len(mine), 2 * (cur[0].max_sessions if cur else 0), 8)
+                mb = Mailbox(self.region_cls, self.ctx, room, room * self.session_bytes, timeout_s=self.timeout_s)
+                if cur:
+                    self._retired.append(cur[0])
+                self.out[r] = (mb, mine)
+                made[r] = (mb.handle, room, room * self.session_bytes)
+            else:
+                self.out[r] = (cur[0], mine)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, made)
+        for src in range(self.world):
+            if src == self.rank:
+                continue
+            mine = [g for g in sorted(self.replica_of) if owner(g, self.world) == src]
+            if self.rank in handles[src]:
+                h, room, slot_bytes = handles[src][self.rank]
+                if src in self.inbox:
+                    self._retired.append(self.inbox[src][0])
+                self.inbox[src] = (Mailbox(self.region_cls, self.ctx, room, slot_bytes, handle=h,
+                                           timeout_s=self.timeout_s), mine)
+            elif src in self.inbox:
+                if mine:
+                    self.inbox[src] = (self.inbox[src][0], mine)
+                else:
+                    self._retired.append(self.inbox.pop(src)[0])
+
+    def _export_fn(self, sessions, dst_rank, now_ms):
         local = [self.local_of[g] for g in sessions]
         nsnd = [self.ctx.senders_of([s]) for s in local]
         since = np.concatenate([self.heads.get((g, dst_rank), np.full(n, edgpu.IMAGE_FULL, dtype=np.uint64))
                                 for g, n in zip(sessions, nsnd)])
-        offsets, _ = self.ctx.session_export(local, now_ms, since=since)              # size query
-        total = int(offsets[-1])
-        dev = self.torch.empty(max(total, 16), dtype=self.torch.uint8, device="cuda")
-        self.torch.cuda.synchronize()
-        offsets, heads = self.ctx.session_export(local, now_ms, dev.data_ptr(), dev.numel(), since=since)
-        k = 0
-        for g, n in zip(sessions, nsnd):
-            self.heads[(g, dst_rank)] = heads[k:k + n].copy()
-            k += n
-        return (dev if self.comm == "cuda" else dev.cpu()), offsets
 
-    def _import(self, buf, offsets, sessions, src_rank):
-        dev = buf if buf.is_cuda else buf.cuda()
-        self.torch.cuda.synchronize()
-        self.ctx.session_import(dev.data_ptr(), offsets, [self.replica_of[g] for g in sessions])
+        def fn(dst, cap):
+            offsets, heads = self.ctx.session_export(local, now_ms, dst, cap, since=since)
+            k = 0
+            for g, n in zip(sessions, nsnd):
+                self.heads[(g, dst_rank)] = heads[k:k + n].copy()
+                k += n
+            return offsets
+        return fn
 
     def sync(self, now_ms: int):
-        from .dist import exchange_images
-        sent, recv = exchange_images(
-            sorted(self.replica_of), lambda s, r: self._export(s, r, now_ms), self._import,
-            lambda n: self.torch.empty(n, dtype=self.torch.uint8, device="cuda" if self.comm == "cuda" else "cpu"),
-            self.world, self.rank)
+        """Publishes this rank's images to every replica rank, then imports this rank's replicas
+        from every owner (no collective).  Returns (bytes sent, bytes received)."""
+        import time as _time
+        t0 = _time.perf_counter()
+        sent = recv = 0
+        for r, (mb, sessions) in sorted(self.out.items()):
+            sent += mb.publish(self._export_fn(sessions, r, now_ms), len(sessions))
+        for src, (mb, sessions) in sorted(self.inbox.items()):
+            local = [self.replica_of[g] for g in sessions]
+            recv += mb.consume(lambda ptr, offs: self.ctx.session_import(ptr, offs, local), len(sessions))
         self.bytes_sent += sent
         self.bytes_received += recv
+        self.sync_s += _time.perf_counter() - t0
         return sent, recv
 
     def feedback(self) -> list:
-        """ReplicaLink.feedback across ranks (dist.route_relocations): this rank's replicas'
-        relocations go to the owners, and the owned sessions other ranks relocated get their
-        flag set here.  Collective; call it after the replicas' backpressure reports and before
-        the owners' next keyframe index.  Returns the owned global sessions updated."""
-        from .dist import route_relocations
+        """The replicas' relocations to their owners (ReplicaLink.feedback across ranks, through
+        the mailboxes): call it after this rank's backpressure reports and before its next ingest.
+        Returns the owned global sessions whose key-update flag was set here."""
         g_of = {v: g for g, v in self.replica_of.items()}
-        hit = self.ctx.session_relocations(sorted(g_of)) if g_of else []
-        return route_relocations([g_of[s] for s in hit],
-                                 lambda gs: self.ctx.session_key_update([self.local_of[g] for g in gs]),
-                                 self.world, self.rank)
+        hit = set(g_of[s] for s in self.ctx.session_relocations(sorted(g_of))) if g_of else set()
+        for _src, (mb, sessions) in sorted(self.inbox.items()):
+            mb.feedback([g for g in sessions if g in hit])
+        mine = set()
+        for _r, (mb, _sessions) in sorted(self.out.items()):
+            mine.update(mb.collect(self.lockstep))
+        upd = sorted(g for g in mine if g in self.local_of)
+        if upd:
+            self.ctx.session_key_update([self.local_of[g] for g in upd])
+        return upd
+
+    @property
+    def wanted_by_others(self) -> set:
+        """Owned global sessions some other rank replicates (as of the last connect)."""
+        return {g for _mb, ss in self.out.values() for g in ss}
+
+    def stats(self) -> dict:
+        boxes = [mb for mb, _ in self.out.values()] + [mb for mb, _ in self.inbox.values()]
+        return {"bytes_sent": self.bytes_sent, "bytes_received": self.bytes_received,
+                "sync_s": round(self.sync_s, 6), "peer_wait_s": round(sum(mb.wait_s for mb in boxes), 6),
+                "mailboxes_out": len(self.out), "mailboxes_in": len(self.inbox)}
+
+    def close(self):
+        for mb in self._retired:
+            mb.close()
+        for mb, _ in list(self.inbox.values()):
+            mb.close()
+        for mb, _ in list(self.out.values()):
+            mb.close()
+        self._retired, self.inbox, self.out = [], {}, {}

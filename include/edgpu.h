@@ -828,6 +828,20 @@ int  edgpu_memcpy_peer(edgpu_ctx* ctx, void* dst, int src_device, const void* sr
  * to it is enabled for every GPU that can reach this one, so RCCL and peer copies may use it. */
 int  edgpu_device_alloc(edgpu_ctx* ctx, uint64_t bytes, void** out);
 int  edgpu_device_free(edgpu_ctx* ctx, void* ptr);
+
+/* Peer mailboxes between processes (one process per GPU): the steady-state replica feed without a
+ * collective (easydarwin_amd/replica.py PeerMailbox).  edgpu_ipc_export gives the
+ * handle of a buffer from edgpu_device_alloc (hipIpcGetMemHandle, HSA dmabuf IPC); another process
+ * opens it with edgpu_ipc_open and gets a pointer its own GPU reads and writes over xGMI (peer
+ * access enabled lazily) -- edgpu_session_import can read images straight from it, and
+ * edgpu_copy_to_host / edgpu_copy_to_device move its header words.  edgpu_ipc_close unmaps it. */
+#define EDGPU_IPC_HANDLE_BYTES 64
+int  edgpu_ipc_export(edgpu_ctx* ctx, const void* device_ptr, uint8_t handle[EDGPU_IPC_HANDLE_BYTES]);
+int  edgpu_ipc_open(edgpu_ctx* ctx, const uint8_t handle[EDGPU_IPC_HANDLE_BYTES], void** out);
+int  edgpu_ipc_close(edgpu_ctx* ctx, void* ptr);
+/* Copies host memory into device memory this context's GPU can write (its own, or a peer buffer
+ * from edgpu_ipc_open); complete when the call returns. */
+int  edgpu_copy_to_device(edgpu_ctx* ctx, void* device_dst, const void* src, uint64_t bytes);
 /* Diagnostics: enqueues on the context stream one wave that waits `us` microseconds of the device
  * clock and exits -- work the GPU watchdog (edgpu_config.watchdog_ms) can time out on. */
 int  edgpu_debug_stall(edgpu_ctx* ctx, uint32_t us);

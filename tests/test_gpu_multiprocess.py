@@ -6,11 +6,13 @@ multi-GPU path of SURVEY.md §8.e executed by libedgpu in separate processes, as
   (dist.owner), replays its shard of a multi-session trace through the engine, and the union of
   the two captures is the reference capture (relay_model, pinned to the reference).
 * Exchange: one process owns every session (ingest + owner ticks), the other serves every
-  subscriber from replica sessions kept in step by session images that dist.exchange_images
-  moves between the processes each tick (DistReplicaLink: full image first, deltas after); the
-  subscribers' bytes equal the reference reflector's capture.  With two or more GPUs visible
-  the processes take GPUs 0 and 1 and the images cross devices over RCCL (nccl backend, device
-  buffers); on a one-GPU box both share GPU 0 and the images go over gloo through host memory.
+  subscriber from replica sessions kept in step by session images (DistReplicaLink: full image
+  first, deltas after) that the owner exports into peer mailboxes in its HBM and the replica's
+  GPU imports straight out of them through IPC mappings -- the only collectives are the join
+  rounds (mailbox handles, bucket places); the subscribers' bytes equal the reference
+  reflector's capture.  With two or more GPUs visible the processes take GPUs 0 and 1 (the
+  images cross over xGMI, the control plane over RCCL); on a one-GPU box both share GPU 0 (the
+  same IPC mappings within one device, the control plane over gloo).
 """
 import hashlib
 import json
@@ -114,7 +116,7 @@ def _exchange_worker(rank, world, port, name, out_q):
         # global ids whose FNV-1a owner is rank 0, one per trace session
         gid = [g for g in range(10_000) if owner(g, world) == 0][:len(tr.sdps)]
         with edgpu.Context(device=rank if cross else 0) as ctx:
-            link = DistReplicaLink(ctx, world, rank, comm="cuda" if cross else "cpu")
+            link = DistReplicaLink(ctx, world, rank)
             local = {}
             if rank == 0:
                 for s, sdp in enumerate(tr.sdps):
@@ -126,8 +128,8 @@ def _exchange_worker(rank, world, port, name, out_q):
             for ev in tr.events:
                 if ev[0] == PKT and rank == 0:
                     pending.append((local[ev[2]], ev[3], ev[1], ev[4]))
-                elif ev[0] == JOIN and rank == 1:
-                    joins.append(ev)
+                elif ev[0] == JOIN:
+                    joins.append(ev)                         # (both ranks see the trace's joins)
                 elif ev[0] == TICK:
                     t = ev[1]
                     if rank == 0:
@@ -137,14 +139,19 @@ def _exchange_worker(rank, world, port, name, out_q):
                             ctx.keyframe_index()
                             pending = []
                         ctx.fanout(t)                        # the owner ticks (no subscribers)
-                    else:
+                    elif joins:
                         for j in joins:                      # a replica before the sync that fills it
                             if gid[j[2]] not in link.replica_of:
                                 local[j[2]] = link.want(gid[j[2]], tr.sdps[j[2]])
-                    link.sync(t)                             # collective: images owner -> replica
-                    # collective: the joiners' bucket places, taken in the owner's arrays
-                    given = link.places([("join", j[1], gid[j[2]], int(j[3])) for j in joins] if rank == 1 else [])
-                    if rank == 1:
+                    if joins:
+                        link.connect()                       # join round (collective): mailbox handles
+                    link.sync(t)                             # no collective: images owner -> replica
+                    if joins:
+                        # join round (collective): the joiners' bucket places, taken in the owner's arrays
+                        given = link.places([("join", j[1], gid[j[2]], int(j[3])) for j in joins] if rank == 1 else [])
+                    if rank == 0:
+                        joins = []
+                    else:
                         for j in joins:
                             h = ctx.subscriber_add(local[j[2]], edgpu.TRANSPORT_TCP if j[4] else edgpu.TRANSPORT_UDP)
                             ctx.subscriber_set_slot(h, given[int(j[3])])
@@ -170,6 +177,7 @@ def _exchange_worker(rank, world, port, name, out_q):
                 result = link.bytes_sent
             got = [None] * world
             dist.all_gather_object(got, (result, cross))
+            link.close()                             # (after the gather: the replica is done reading)
             if rank == 0:
                 out_q.put(got)
         dist.destroy_process_group()
