@@ -321,6 +321,7 @@ class Context:
         _check(lib.edgpu_ctx_create(C.byref(c), C.byref(h)))
         self.h = h
         self.lib = lib
+        self.device = int(device)
         self._ntracks = {}          # session -> tracks (senders_of without a C call per session)
 
     def close(self):

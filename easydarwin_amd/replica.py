@@ -146,15 +146,23 @@ class DistReplicaLink:
 
     lockstep: ``feedback`` waits for every replica's relocations of the tick (exact one-process
     semantics, the parity tests); without it a relocation may reach its owner a tick late.
+    pull: "copy" (default) brings each publication into a local staging buffer with one peer DMA
+    copy (hipMemcpyPeerAsync over xGMI) and imports from there; "direct" lets the import kernel read
+    the owner's mapped HBM itself (one HBM write + read less per image byte).
     session_bytes: mailbox slot room per replicated session (full images are key -> newest:
     about 2 s of stream; default EDGPU_MAILBOX_SESSION_MB or 4 MiB)."""
 
     def __init__(self, ctx: edgpu.Context, world: int, rank: int, lockstep: bool = True,
-                 session_bytes: int | None = None, timeout_s: float = 60.0, region_cls=None):
+                 session_bytes: int | None = None, timeout_s: float = 60.0, region_cls=None,
+                 pull: str = "copy"):
         import os
 
         from .mailbox import DeviceRegion
         self.region_cls = region_cls or DeviceRegion     # mailbox.HostRegion: the CPU rehearsal
+        if pull not in ("copy", "direct"):
+            raise ValueError("pull: 'copy' or 'direct'")
+        self.pull = pull if region_cls is None else "direct"   # (host regions: the stand-in reads them)
+        self._stage = None                                # local staging buffer (pull="copy")
         self.ctx, self.world, self.rank = ctx, world, rank
         self.lockstep = lockstep
         self.session_bytes = session_bytes or int(float(os.environ.get("EDGPU_MAILBOX_SESSION_MB", "4")) * (1 << 20))
@@ -217,7 +225,7 @@ class DistReplicaLink:
                 if cur:
                     self._retired.append(cur[0])
                 self.out[r] = (mb, mine)
-                made[r] = (mb.handle, room, room * self.session_bytes)
+                made[r] = (mb.handle, room, room * self.session_bytes, getattr(self.ctx, "device", 0))
             else:
                 self.out[r] = (cur[0], mine)
         handles = [None] * self.world
@@ -227,11 +235,12 @@ class DistReplicaLink:
                 continue
             mine = [g for g in sorted(self.replica_of) if owner(g, self.world) == src]
             if self.rank in handles[src]:
-                h, room, slot_bytes = handles[src][self.rank]
+                h, room, slot_bytes, dev = handles[src][self.rank]
                 if src in self.inbox:
                     self._retired.append(self.inbox[src][0])
-                self.inbox[src] = (Mailbox(self.region_cls, self.ctx, room, slot_bytes, handle=h,
-                                           timeout_s=self.timeout_s), mine)
+                mb = Mailbox(self.region_cls, self.ctx, room, slot_bytes, handle=h, timeout_s=self.timeout_s)
+                mb.src_device = dev
+                self.inbox[src] = (mb, mine)
             elif src in self.inbox:
                 if mine:
                     self.inbox[src] = (self.inbox[src][0], mine)
@@ -263,11 +272,24 @@ class DistReplicaLink:
             sent += mb.publish(self._export_fn(sessions, r, now_ms), len(sessions))
         for src, (mb, sessions) in sorted(self.inbox.items()):
             local = [self.replica_of[g] for g in sessions]
-            recv += mb.consume(lambda ptr, offs: self.ctx.session_import(ptr, offs, local), len(sessions))
+            recv += mb.consume(lambda ptr, offs, mb=mb: self._import(mb, ptr, offs, local), len(sessions))
         self.bytes_sent += sent
         self.bytes_received += recv
         self.sync_s += _time.perf_counter() - t0
         return sent, recv
+
+    def _import(self, mb, ptr, offsets, local):
+        if self.pull == "direct":
+            self.ctx.session_import(ptr, offsets, local)
+            return
+        nbytes = int(offsets[-1])
+        if self._stage is None or self._stage.nbytes < nbytes:
+            if self._stage is not None:
+                self._stage.free()
+            self._stage = self.ctx.device_alloc(max(nbytes * 5 // 4, 1 << 20))
+        # one peer DMA copy over xGMI, then the import from local HBM (stream-ordered after it)
+        self.ctx.memcpy_peer(self._stage.ptr, mb.src_device, ptr, nbytes)
+        self.ctx.session_import(self._stage.ptr, offsets, local)
 
     def feedback(self) -> list:
         """The replicas' relocations to their owners (ReplicaLink.feedback across ranks, through
@@ -304,3 +326,6 @@ class DistReplicaLink:
         for mb, _ in list(self.out.values()):
             mb.close()
         self._retired, self.inbox, self.out = [], {}, {}
+        if self._stage is not None:
+            self._stage.free()
+            self._stage = None

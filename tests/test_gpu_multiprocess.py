@@ -99,7 +99,7 @@ def test_two_engine_processes_shard_sessions(oracle_bins):
     assert merged == _capture(list(range(N_SESS)), oracle_bins["port"])
 
 
-def _exchange_worker(rank, world, port, name, out_q):
+def _exchange_worker(rank, world, port, name, pull, out_q):
     """rank 0: owner of every session of the scenario; rank 1: every subscriber, on replicas.
     Two GPUs: rank r on GPU r, images over RCCL; one GPU: both on GPU 0, images over gloo."""
     try:
@@ -116,7 +116,7 @@ def _exchange_worker(rank, world, port, name, out_q):
         # global ids whose FNV-1a owner is rank 0, one per trace session
         gid = [g for g in range(10_000) if owner(g, world) == 0][:len(tr.sdps)]
         with edgpu.Context(device=rank if cross else 0) as ctx:
-            link = DistReplicaLink(ctx, world, rank)
+            link = DistReplicaLink(ctx, world, rank, pull=pull)
             local = {}
             if rank == 0:
                 for s, sdp in enumerate(tr.sdps):
@@ -187,14 +187,17 @@ def _exchange_worker(rank, world, port, name, out_q):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pull", ["copy", "direct"])
 @pytest.mark.parametrize("name", ["c1", "mixed"])
-def test_session_images_move_between_engine_processes(name):
+def test_session_images_move_between_engine_processes(name, pull):
+    """pull="copy": the replica brings each publication over with one peer DMA copy, then imports;
+    "direct": its import kernel reads the owner's mapped HBM."""
     with open(os.path.join(GOLD, name + ".json")) as f:
         fix = json.load(f)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, name, pull, q)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)
