@@ -133,16 +133,18 @@ def run_step(ctx: edgpu.Context, bt: dict, link=None):
 
 def replica_preflight(ctx, world: int, rank: int) -> dict:
     """N > 1, before the steady state: can this node's processes map each other's HBM (IPC handles,
-    HSA dmabuf)?  Every rank exports a small buffer, opens the next rank's and writes / reads a word
-    there; failures are caught locally so every rank reaches every collective.  All ranks get the
+    HSA dmabuf)?  Every rank exports a small buffer, opens the next rank's, writes / reads a word
+    there and pulls it with a peer DMA copy (the mailboxes' exact mechanisms); failures are caught
+    locally so every rank reaches every collective.  All ranks get the
     same verdict (the replicas run only if every rank passed)."""
     import numpy as np
     import torch.distributed as tdist
-    mine, err, buf = None, None, None
+    mine, err, buf, loc = None, None, None, None
     try:
         buf = ctx.device_alloc(4096)
+        loc = ctx.device_alloc(4096)
         ctx.copy_to_device(buf.ptr, np.zeros(16, np.uint8))
-        mine = ctx.ipc_export(buf.ptr)
+        mine = (ctx.ipc_export(buf.ptr), ctx.device)
     except Exception as e:                            # noqa: BLE001 -- reported in the line
         err = f"export: {type(e).__name__}: {e}"
     hs = [None] * world
@@ -150,9 +152,12 @@ def replica_preflight(ctx, world: int, rank: int) -> dict:
     nxt = hs[(rank + 1) % world]
     if err is None and nxt is not None:
         try:
-            p = ctx.ipc_open(nxt)
-            ctx.copy_to_device(p + 8 * rank % 4096, np.array([rank + 1], np.uint64))
-            ok = int(ctx.copy_to_host(p + 8 * rank % 4096, 8).view(np.uint64)[0]) == rank + 1
+            p = ctx.ipc_open(nxt[0])
+            off = 8 * rank % 4096
+            ctx.copy_to_device(p + off, np.array([rank + 1], np.uint64))
+            ok = int(ctx.copy_to_host(p + off, 8).view(np.uint64)[0]) == rank + 1
+            ctx.memcpy_peer(loc.ptr, nxt[1], p + off, 8)          # a peer DMA pull, as the replicas do
+            ok = ok and int(ctx.copy_to_host(loc.ptr, 8).view(np.uint64)[0]) == rank + 1
             ctx.ipc_close(p)
             if not ok:
                 err = "peer word read back wrong"
@@ -163,8 +168,9 @@ def replica_preflight(ctx, world: int, rank: int) -> dict:
     res = [None] * world
     tdist.all_gather_object(res, err)
     tdist.barrier()
-    if buf is not None:
-        buf.free()
+    for b in (buf, loc):
+        if b is not None:
+            b.free()
     errs = [e for e in res if e]
     return {"ok": not errs, "error": errs[0] if errs else None}
 
