@@ -278,3 +278,67 @@ def test_failed_pass_leaves_the_context_usable(name, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     failed, after = map(int, re.search(r"(\d+) failed ticks, (\d+) good ticks after", r.stderr).groups())
     assert failed == 1 and after > 0, r.stderr[-2000:]
+
+
+def _tick_bytes(ctx, r, out):
+    """Appends each sub-stream's packets of one pass to out[(subscriber, track, kind)]."""
+    _st, subs, desc, arena = ctx.read_tick(r)
+    for q in subs:
+        n = int(q["desc_count"])
+        if not n:
+            continue
+        d = desc[int(q["desc_base"]):int(q["desc_base"]) + n]
+        out.setdefault((int(q["subscriber"]), int(q["track"]), int(q["kind"])), []).extend(
+            arena[o:o + ln].tobytes() for o, ln in zip(d["offset"], d["len"]))
+
+
+@pytest.mark.gpu
+def test_subscribers_change_between_passes():
+    """include/edgpu.h edgpu_fanout_next: subscribers may come and go between the copy passes of a
+    tick.  The passes keep the tick's table -- a subscriber added between passes gets nothing from
+    this tick (its new-output start comes with the next one), a removed subscriber's rows still
+    deliver the rest of the tick -- so a tick split into passes with a join and a leave landing
+    between them delivers what the same tick in one pass delivers with the join and the leave
+    after it, in this tick and the next (the module's concurrent delivery can land AddOutput /
+    RemoveOutput there, reflector_adapter.cpp SetConcurrentDelivery)."""
+    tr = _tiny_ctx_trace()
+    info = []
+    replay(tr, tick_info=info)
+    arena, desc = _small(info)
+    pk = [ev for ev in tr.events if ev[0] == PKT]
+    batches = [[(e[2], e[3], e[1], e[4]) for e in pk[a:b]] for a, b in ((0, 400), (400, 800))]
+    times = [pk[399][1], pk[799][1]]
+    got = {}
+    for mode, cfg in (("split", dict(out_arena_bytes=arena, max_out_packets=desc)), ("one", {})):
+        ticks = []
+        with edgpu.Context(**cfg) as ctx:
+            sessions = [ctx.session_add(sdp) for sdp in tr.sdps]
+            handles = {s: [ctx.subscriber_add(s, edgpu.TRANSPORT_UDP) for _ in range(3)] for s in sessions}
+            leaving = handles[sessions[-1]][0]
+            passes = 0
+            for k, (batch, t) in enumerate(zip(batches, times)):
+                out = {}
+                d, seg, sess, blob = edgpu.build_batch(batch)
+                ctx.ingest_host(d, seg, sess, blob)
+                ctx.keyframe_index()
+                r = ctx.fanout(t)
+                _tick_bytes(ctx, r, out)
+                passes += 1
+                if k == 0 and mode == "split":
+                    assert ctx.stats().more_passes == 1, "the tick should be split"
+                    joined = ctx.subscriber_add(sessions[0], edgpu.TRANSPORT_UDP)   # between passes
+                    ctx.subscriber_remove(leaving)
+                while (r := ctx.fanout_next()) is not None:
+                    _tick_bytes(ctx, r, out)
+                    passes += 1
+                if k == 0 and mode == "one":
+                    joined = ctx.subscriber_add(sessions[0], edgpu.TRANSPORT_UDP)   # after the tick
+                    ctx.subscriber_remove(leaving)
+                assert ctx.stats().status == 0
+                ticks.append(out)
+            got[mode] = (ticks, joined, leaving, passes)
+    (split, j1, l1, np1), (one, j2, l2, np2) = got["split"], got["one"]
+    assert (j1, l1) == (j2, l2) and np1 > np2
+    assert split == one
+    assert any(key[0] == l1 for key in split[0]) and not any(key[0] == l1 for key in split[1])
+    assert not any(key[0] == j1 for key in split[0]) and any(key[0] == j1 for key in split[1])
