@@ -47,6 +47,8 @@ hipError_t launch_desc_arrival(const SubDev* subs, const SenderDev* senders, uin
 hipError_t launch_arena_gather(const uint8_t* arena, const edgpu_region* reg, const uint64_t* dst_off, uint32_t n,
                                uint8_t* dst, hipStream_t st);
 hipError_t launch_copy_to_pinned(void* dst, const void* src, uint64_t bytes, hipStream_t st);
+hipError_t launch_sub_active(const edgpu_substream_out* sub, uint32_t n, uint32_t* blk, edgpu_substream_out* rows,
+                             uint32_t* q, uint32_t cap, uint32_t* total, hipStream_t st);
 hipError_t launch_stall(uint64_t ticks, hipStream_t st);
 int fanout_chunk(int variant);
 int fanout_default(bool patching);
@@ -387,6 +389,8 @@ struct edgpu_ctx {
     DevVec<uint32_t> d_sources;                 // edgpu_fanout_packet_info
     DevVec<uint32_t> d_row_sel;                 // edgpu_fanout_rows
     DevVec<edgpu_packet_row> d_rows;
+    DevVec<uint32_t> d_act_blk, d_act_q;        // edgpu_fanout_active: per-workgroup counts, staging
+    DevVec<edgpu_substream_out> d_act_rows;
     uint32_t ingest_epoch = 0;                  // ingests so far
     uint32_t host_epoch_last = 0;               // the last ingest's epoch if it was a host batch, else 0
     DevVec<uint64_t> d_gather_off;
@@ -617,6 +621,7 @@ int edgpu_ctx_destroy(edgpu_ctx* x) {
     x->d_tcp_ncand.release(); x->d_tcp_cands.release(); x->d_tcp_links.release(); x->d_tcp_chunkres.release();
     x->d_tcp_results.release(); x->d_tcp_offs.release(); x->d_tcp_stage.release(); x->d_blocked.release();
     x->d_gather_reg.release(); x->d_gather_off.release(); x->d_arrivals.release(); x->d_sources.release(); x->d_row_sel.release(); x->d_rows.release();
+    x->d_act_blk.release(); x->d_act_q.release(); x->d_act_rows.release();
     if (x->d_fpi_q) (void)hipFree(x->d_fpi_q);
     if (x->d_fpi_r) (void)hipFree(x->d_fpi_r);
     if (x->h_fpi_q) (void)hipHostFree(x->h_fpi_q);
@@ -2167,6 +2172,44 @@ int edgpu_fanout_packet_info(edgpu_ctx* x, int64_t* arrivals, uint32_t* sources,
         if (sources) HIP_CHECK(rb.add(sources, dsrc, (size_t)npass * sizeof(uint32_t)));
     }
     HIP_CHECK(rb.run());
+    return EDGPU_OK;
+}
+
+int edgpu_fanout_active(edgpu_ctx* x, edgpu_substream_out* rows, uint32_t* q, uint32_t cap, uint32_t* n_out, int kind) {
+    if (!x || !n_out || (cap && (!rows || !q))) return fail(EDGPU_BAD_ARGUMENT, "NULL argument");
+    if (kind != EDGPU_PTR_HOST && kind != EDGPU_PTR_DEVICE) return fail(EDGPU_BAD_ARGUMENT, "bad ptr_kind");
+    *n_out = 0;
+    if (x->fanout_launches == 0) return fail(EDGPU_ERR, "no fan-out tick");
+    DEVICE_ENTER(x);
+    const uint32_t n = x->tick_nsubs;
+    if (!n) return EDGPU_OK;
+    const uint32_t nb = (n + 255) / 256;
+    HIP_CHECK(x->d_act_blk.reserve((size_t)nb + 1, x->stream));
+    uint32_t* total = x->d_act_blk.ptr + nb;
+    // pinned host destinations are stored into by the kernel over PCIe; others through a staging copy
+    const bool direct = kind == EDGPU_PTR_DEVICE || (!cap || (Readback::is_pinned(rows) && Readback::is_pinned(q)));
+    edgpu_substream_out* dr = rows;
+    uint32_t* dq = q;
+    if (!direct) {
+        HIP_CHECK(x->d_act_rows.reserve(std::max<uint32_t>(cap, 1), x->stream));
+        HIP_CHECK(x->d_act_q.reserve(std::max<uint32_t>(cap, 1), x->stream));
+        dr = x->d_act_rows.ptr; dq = x->d_act_q.ptr;
+    }
+    HIP_CHECK(launch_sub_active(x->d_sub_out.ptr, n, x->d_act_blk.ptr, dr, dq, cap, total, x->stream));
+    uint32_t tot = 0;
+    {
+        Readback rb(x);
+        HIP_CHECK(rb.add(&tot, total, sizeof(tot)));
+        HIP_CHECK(rb.run());
+    }
+    if (!direct && tot && cap) {
+        const uint32_t k = std::min(tot, cap);
+        Readback rb(x);
+        HIP_CHECK(rb.add(rows, dr, (size_t)k * sizeof(edgpu_substream_out)));
+        HIP_CHECK(rb.add(q, dq, (size_t)k * sizeof(uint32_t)));
+        HIP_CHECK(rb.run());
+    }
+    *n_out = tot;
     return EDGPU_OK;
 }
 

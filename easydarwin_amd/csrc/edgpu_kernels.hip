@@ -2698,6 +2698,56 @@ __global__ __launch_bounds__(256) void k_sub_rows(const SubDev* subs, const Send
         rows[base + i] = r;
     }
 }
+// edgpu_fanout_active: the sub-stream rows of the current pass that carry descriptors or are new,
+// in table order.  k_sub_active_count: per workgroup of 256 rows its count; k_sub_active_write: its base
+// (the counts of the workgroups before it, reduced in LDS), each active row's rank (wave ballots
+// + the waves' counts), the row and its index stored at base + rank (straight into pinned host
+// memory when the caller gave it); the last workgroup stores the total.
+__global__ __launch_bounds__(256) void k_sub_active_count(const edgpu_substream_out* sub, uint32_t n, uint32_t* blk) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const int act = i < n && (sub[i].desc_count != 0 || (sub[i].flags & EDGPU_SUB_NEW));
+    const int c = __syncthreads_count(act);
+    if (threadIdx.x == 0) blk[blockIdx.x] = (uint32_t)c;
+}
+
+__global__ __launch_bounds__(256) void k_sub_active_write(const edgpu_substream_out* sub, uint32_t n, const uint32_t* blk,
+                                                          edgpu_substream_out* rows, uint32_t* q, uint32_t cap,
+                                                          uint32_t* total) {
+    __shared__ uint32_t s_part[256];
+    __shared__ uint32_t s_wave[4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t part = 0;
+    for (uint32_t b = tid; b < blockIdx.x; b += 256) part += blk[b];
+    s_part[tid] = part;
+    const uint32_t i = blockIdx.x * 256 + tid;
+    const bool act = i < n && (sub[i].desc_count != 0 || (sub[i].flags & EDGPU_SUB_NEW));
+    const uint64_t m = __ballot(act);
+    if (lane == 0) s_wave[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) s_part[tid] += s_part[tid + s];
+        __syncthreads();
+    }
+    uint32_t pos = s_part[0];
+    for (int w = 0; w < wid; w++) pos += s_wave[w];
+    pos += (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (act && pos < cap) {
+        rows[pos] = sub[i];
+        q[pos] = i;
+    }
+    if (blockIdx.x == gridDim.x - 1 && tid == 0)
+        *total = s_part[0] + s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+}
+
+hipError_t launch_sub_active(const edgpu_substream_out* sub, uint32_t n, uint32_t* blk, edgpu_substream_out* rows,
+                             uint32_t* q, uint32_t cap, uint32_t* total, hipStream_t st) {
+    const uint32_t nb = (n + 255) / 256;
+    if (!nb) return hipSuccess;
+    EDGPU_LAUNCH(k_sub_active_count, dim3(nb), dim3(256), 0, st, sub, n, blk);
+    EDGPU_LAUNCH(k_sub_active_write, dim3(nb), dim3(256), 0, st, sub, n, blk, rows, q, cap, total);
+    return hipGetLastError();
+}
+
 hipError_t launch_sub_rows(const SubDev* subs, const SenderDev* senders, const edgpu_out_desc* desc, const uint32_t* sel,
                            uint32_t nsel, uint32_t nsubs, uint32_t pass, uint32_t epoch, edgpu_packet_row* rows,
                            uint64_t nrows, hipStream_t st) {

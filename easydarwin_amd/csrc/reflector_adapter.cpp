@@ -56,7 +56,7 @@ Reflector::~Reflector() {
         for (void* p : {(void*)b.blob, (void*)b.desc, (void*)b.seg, (void*)b.segSess})
             if (p) (void)edgpu_host_free(fCtx, p);
     if (fHostOut) (void)edgpu_host_free(fCtx, fHostOut);
-    for (PinBuf* pb : {&fPinSubs, &fPinRows})
+    for (PinBuf* pb : {&fPinSubs, &fPinQ, &fPinRows})
         if (pb->p) (void)edgpu_host_free(fCtx, pb->p);
     edgpu_ctx_destroy(fCtx);
 }
@@ -528,13 +528,22 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
                            bool firstPass, std::vector<edgpu_blocked>* blockedOut) {
     int err;
     auto t0 = Clock::now();
-    // the sub-stream table lands in a pinned buffer, then the rows of the writes: one per
+    // the pass's sub-streams with packets (and the new outputs), compacted in table order into
+    // pinned buffers (edgpu_fanout_active: at 2-ms ticks a few % of the table -- every host loop
+    // below and every write thread walks only them), then the rows of the writes: one per
     // descriptor of a sub-stream that is not an identity one, one per packet of each sender's
-    // identity sub-streams (its longest one's rows serve the others, edgpu_fanout_rows)
-    const uint32_t nq = res.n_substreams;
-    if ((err = EnsurePinned(fPinSubs, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
+    // identity sub-streams (its longest one's rows serve the others, edgpu_fanout_rows).  Below,
+    // a sub-stream is its compact index; fActiveQ maps it to its table row.
+    const uint32_t ntab = res.n_substreams;
+    if ((err = EnsurePinned(fPinSubs, (uint64_t)std::max<uint32_t>(ntab, 1) * sizeof(edgpu_substream_out))) ||
+        (err = EnsurePinned(fPinQ, (uint64_t)std::max<uint32_t>(ntab, 1) * sizeof(uint32_t))))
+        return err;
     const edgpu_substream_out* subs = (const edgpu_substream_out*)fPinSubs.p;
-    if ((err = edgpu_copy_to_host(fCtx, fPinSubs.p, res.substreams, (uint64_t)nq * sizeof(edgpu_substream_out)))) return err;
+    const uint32_t* tabq = (const uint32_t*)fPinQ.p;
+    uint32_t nq = 0;
+    if ((err = edgpu_fanout_active(fCtx, (edgpu_substream_out*)fPinSubs.p, (uint32_t*)fPinQ.p, ntab, &nq, EDGPU_PTR_HOST)))
+        return err;
+    if (nq > ntab) return fail_with(kRequestFailed, "active sub-streams exceed the table");
     fRowOf.assign(nq, 0);
     fRowDelta.assign(nq, 0);
     uint64_t nrows = 0;
@@ -545,7 +554,7 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     for (uint32_t q = 0; q < nq; q++) {
         const edgpu_substream_out& s = subs[q];
         if (!s.desc_count || ((s.flags & EDGPU_SUB_IDENTITY) && fRowRep[s.sender] != q)) continue;
-        fRowSel.push_back(q);
+        fRowSel.push_back(tabq[q]);
         fRowSel.push_back((uint32_t)nrows);
         fRowOf[q] = (uint32_t)nrows;
         fRowDelta[q] = -(int64_t)s.out_base;
@@ -602,7 +611,7 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
         fHostOut = (uint8_t*)h;
         fHostOutCap = cap;
     }
-    fTick.readback_bytes += tr.bytes + (uint64_t)nq * sizeof(edgpu_substream_out) +
+    fTick.readback_bytes += tr.bytes + (uint64_t)nq * (sizeof(edgpu_substream_out) + sizeof(uint32_t)) +
                             nrows * sizeof(edgpu_packet_row);
     // The distinct bytes are gathered straight into the pinned buffer (the kernel's stores cross
     // PCIe, one pass) in up to TickParts::kMax parts of the sub-stream table, each part's regions after the
@@ -652,7 +661,7 @@ int Reflector::DeliverPass(const edgpu_fanout_result& res, const edgpu_tick_stat
     } relock{release ? fTickLock : nullptr};
     if (firstPass) sink->BeginTick(subs, nq);               // every row carries its flags in every pass
     WriteJob job;
-    job.subs = subs; job.nsubs = nq;
+    job.subs = subs; job.nsubs = nq; job.tabq = tabq;
     job.rows = rows; job.row_of = fRowOf.data(); job.delta = fRowDelta.data();
     job.arrivals = sink->WantsArrivals();
     job.batch = useSrc ? fIngestedBlob : nullptr;
@@ -742,7 +751,7 @@ void Reflector::WriteSubscribers(WriteJob& j, uint32_t worker, uint32_t nworkers
             w.worker = worker;
             writes++;
             const int err = j.sink->Write(w);
-            if (err == kWouldBlock) { r.blocked.push_back(edgpu_blocked{s, i}); break; }
+            if (err == kWouldBlock) { r.blocked.push_back(edgpu_blocked{j.tabq[s], i}); break; }
             if (err) { r.err = err; r.writes = writes; return; }
         }
     }

@@ -92,9 +92,10 @@ public:
     virtual int WritePacket(uint32_t subscriber, uint16_t track, bool isRTCP, bool interleaved,
                             const uint8_t* wire, uint32_t wireLen, uint32_t packetID) = 0;
     // Sinks that model the transmit time override these three: ReflectPackets then reads the
-    // tick's arrival times (edgpu_fanout_arrivals), shows the sink the whole sub-stream table
-    // first (the reference walks each sender's outputs in bucket order, so whether an earlier
-    // output was new decides `firstPacket` for the later ones, ReflectorStream.cpp:1086-1108),
+    // tick's arrival times (edgpu_fanout_arrivals), shows the sink the first pass's sub-streams
+    // that carry packets or are new outputs first, in table order (the reference walks each
+    // sender's outputs in bucket order, so whether an earlier output was new decides
+    // `firstPacket` for the later ones, ReflectorStream.cpp:1086-1108),
     // and calls Write for every packet.  Write / WritePacket are called concurrently for
     // different subscribers when the Reflector has more than one write thread (w.worker tells
     // them apart); BeginTick runs before, on the ticking thread.
@@ -241,7 +242,8 @@ private:
                 int64_t nowMs, const edgpu_udp_source* src);
     // the write phase of a tick, for the subscribers of one worker
     struct WriteJob {
-        const edgpu_substream_out* subs; uint32_t nsubs;
+        const edgpu_substream_out* subs; uint32_t nsubs;   // the pass's active sub-streams (compact)
+        const uint32_t* tabq = nullptr;                     // compact index -> sub-stream table row
         // sub-stream s's i-th write is rows[row_of[s] + i] (edgpu_fanout_rows: identity sub-streams
         // of one sender share their longest one's rows); its bytes are at regions->at(host, s) +
         // row.offset + delta[s]
@@ -288,7 +290,7 @@ private:
     // readback buffers
     struct PinBuf { void* p = nullptr; uint64_t cap = 0; };  // pinned, grown on demand
     int  EnsurePinned(PinBuf& b, uint64_t bytes);
-    PinBuf fPinSubs, fPinRows;                              // sub-stream table, rows
+    PinBuf fPinSubs, fPinQ, fPinRows;                       // active sub-streams, their table rows, rows
     std::vector<uint32_t> fRowSel, fRowOf, fRowRep;         // edgpu_fanout_rows' selection, per sub-stream row start
     std::vector<int64_t> fRowDelta;
     const uint8_t* fIngestedBlob = nullptr;                 // the blob the last FlushIngest ingested (intact

@@ -30,7 +30,7 @@ EXPORTED = [
     "edgpu_fanout", "edgpu_tick_stats_get", "edgpu_copy_to_host", "edgpu_last_timings",
     "edgpu_gop_span", "edgpu_counters_get", "edgpu_kernel_times", "edgpu_gop_copy",
     "edgpu_session_export", "edgpu_session_import", "edgpu_session_relocations", "edgpu_session_key_update",
-    "edgpu_stream_errors", "edgpu_fanout_packet_info", "edgpu_fanout_rows",
+    "edgpu_stream_errors", "edgpu_fanout_packet_info", "edgpu_fanout_rows", "edgpu_fanout_active",
     "edgpu_memcpy_peer", "edgpu_device_alloc",
     "edgpu_device_free", "edgpu_fanout_kernel", "edgpu_subscriber_play",
     "edgpu_subscribers_add", "edgpu_ingest_interleaved", "edgpu_fanout_blocked",
@@ -228,6 +228,7 @@ def load(path: str = LIB_PATH):
         "edgpu_stream_errors": (I32, [P, P, P, U32, P]),
         "edgpu_fanout_packet_info": (I32, [P, P, P, U32, I32]),
         "edgpu_fanout_rows": (I32, [P, P, U32, P, U64, I32]),
+        "edgpu_fanout_active": (I32, [P, P, P, U32, C.POINTER(U32), I32]),
         "edgpu_memcpy_peer": (I32, [P, P, I32, P, U64]),
         "edgpu_device_alloc": (I32, [P, U64, C.POINTER(P)]),
         "edgpu_device_free": (I32, [P, P]),
@@ -676,6 +677,16 @@ class Context:
         out = np.zeros(max(nrows, 1), dtype=self.ROW_DTYPE)
         _check(self.lib.edgpu_fanout_rows(self.h, _ptr(sel), len(sel), _ptr(out), nrows, PTR_HOST))
         return out[:nrows]
+
+    def fanout_active(self, cap: int):
+        """The current pass's sub-streams with descriptors, compacted in table order
+        (edgpu_fanout_active): (rows as SUB_DTYPE, their table indices, total count)."""
+        rows = np.zeros(max(int(cap), 1), dtype=SUB_DTYPE)
+        q = np.zeros(max(int(cap), 1), dtype=np.uint32)
+        n = C.c_uint32()
+        _check(self.lib.edgpu_fanout_active(self.h, _ptr(rows), _ptr(q), int(cap), C.byref(n), PTR_HOST))
+        k = min(n.value, int(cap))
+        return rows[:k], q[:k], n.value
 
     def read_tick(self, r: FanoutResult):
         """(stats, substream table, descriptors, arena) of the current copy pass of the last

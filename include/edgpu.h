@@ -678,6 +678,16 @@ typedef struct edgpu_packet_row {
     uint32_t source;        /* blob slot in the last host batch, or EDGPU_NO_SOURCE */
     uint32_t _pad;
 } edgpu_packet_row;
+/* The sub-streams of the current copy pass that carry descriptors or are new outputs
+ * (EDGPU_SUB_NEW: a host deriving per-tick state from new outputs sees every one), compacted and
+ * in table order:
+ * rows[i] is row q[i] of the pass's sub-stream table (edgpu_fanout_result.substreams), i <
+ * min(*n_out, cap); *n_out counts all of them.  A host delivering a tick reads back only what it
+ * writes -- at 2-ms ticks a few % of a 32k-row table.  `rows` / `q`: device memory
+ * (EDGPU_PTR_DEVICE) or host memory (EDGPU_PTR_HOST; pinned buffers from edgpu_host_alloc are
+ * stored into by the kernel over PCIe, others through a device copy).  Syncs. */
+int  edgpu_fanout_active(edgpu_ctx* ctx, edgpu_substream_out* rows, uint32_t* q, uint32_t cap, uint32_t* n_out,
+                         int kind);
 /* The rows of SELECTED sub-streams of the current copy pass only: sel[2k] is a row of the
  * sub-stream table, sel[2k + 1] where its rows start in `rows`: rows[sel[2k + 1] + i] for its
  * descriptor desc_base + i, i < desc_count (rows at or past `nrows` are not written).  Two

@@ -342,3 +342,38 @@ def test_subscribers_change_between_passes():
     assert split == one
     assert any(key[0] == l1 for key in split[0]) and not any(key[0] == l1 for key in split[1])
     assert not any(key[0] == j1 for key in split[0]) and any(key[0] == j1 for key in split[1])
+
+
+@pytest.mark.gpu
+def test_fanout_active_compacts_each_pass():
+    """edgpu_fanout_active: each pass's sub-streams with descriptors (or new), compacted in table order --
+    the rows and indices a full read of the table (read_tick) filtered on the host gives; a
+    capacity below the count truncates the rows and still reports the count."""
+    tr = _tiny_ctx_trace()
+    info = []
+    replay(tr, tick_info=info)
+    arena, desc = _small(info)
+    pk = [ev for ev in tr.events if ev[0] == PKT]
+    with edgpu.Context(out_arena_bytes=arena, max_out_packets=desc) as ctx:
+        sessions = [ctx.session_add(sdp) for sdp in tr.sdps]
+        for s in sessions:
+            for k in range(5):
+                ctx.subscriber_add(s, edgpu.TRANSPORT_TCP if k % 2 else edgpu.TRANSPORT_UDP)
+        seen = 0
+        for a, b in ((0, 300), (300, 700)):
+            d, seg, sess, blob = edgpu.build_batch([(e[2], e[3], e[1], e[4]) for e in pk[a:b]])
+            ctx.ingest_host(d, seg, sess, blob)
+            ctx.keyframe_index()
+            r = ctx.fanout(pk[b - 1][1])
+            while r is not None:
+                subs = ctx.read_tick(r)[1]
+                idx = [i for i in range(len(subs)) if subs[i]["desc_count"] or subs[i]["flags"] & edgpu.SUB_NEW]
+                rows, q, n = ctx.fanout_active(len(subs) + 3)
+                assert n == len(idx) and q.tolist() == idx
+                assert rows.tobytes() == subs[idx].tobytes()
+                if n > 1:
+                    rows2, q2, n2 = ctx.fanout_active(1)
+                    assert n2 == n and q2.tolist() == idx[:1] and rows2.tobytes() == subs[idx[:1]].tobytes()
+                seen += n
+                r = ctx.fanout_next()
+        assert seen > 0

@@ -309,6 +309,18 @@ int edgpu_fanout_rows(edgpu_ctx* x, const uint32_t* sel, uint32_t nsel, edgpu_pa
     }
     return EDGPU_OK;
 }
+int edgpu_fanout_active(edgpu_ctx* x, edgpu_substream_out* rows, uint32_t* q, uint32_t cap, uint32_t* n_out, int) {
+    touch(x);
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < x->table.size(); i++) {
+        const edgpu_substream_out& o = x->table[i];
+        if (!o.desc_count && !(o.flags & EDGPU_SUB_NEW)) continue;
+        if (n < cap) { rows[n] = o; q[n] = i; }
+        n++;
+    }
+    *n_out = n;
+    return EDGPU_OK;
+}
 int edgpu_fanout_blocked(edgpu_ctx* x, const edgpu_blocked* r, uint32_t n) {
     touch(x);
     for (uint32_t i = 0; i < n; i++) {
