@@ -20,10 +20,10 @@
 #include <sys/socket.h>
 #include <time.h>
 
-enum { kBatch = 64, kMax = 65536 };
+enum { kBatch = 64, kMax = 65536, kSpinMax = 16 };
 
 typedef struct {
-    int fd, stream;
+    int fd, stream, spin;
     uint8_t* slots;                 /* kBatch receive buffers of kMax bytes */
     uint8_t* buf;
     size_t len, cap, count;
@@ -91,7 +91,9 @@ static int take(Rx* r) {
 /* Spins while datagrams keep coming and for 20 ms after the last one: a sleeping (or yielding)
  * receiver gets the CPU back later than the sender needs to fill a receive buffer clamped to
  * net.core.rmem_max (a sched_yield measured 1.6 ms beside a sending thread); then waits in poll.
- * Needs a core per receiver beside the sender's (the GPU box's CPU share has them). */
+ * Needs a core per receiver beside the sender's (the GPU box's CPU share has them): with more than
+ * kSpinMax receivers (a fleet of slow players, e.g. the `udppush` golden's 520 sockets) every one
+ * waits in poll instead. */
 static void* loop(void* arg) {
     Rx* r = (Rx*)arg;
     struct pollfd p = {r->fd, POLLIN, 0};
@@ -99,6 +101,7 @@ static void* loop(void* arg) {
     clock_gettime(CLOCK_MONOTONIC, &last);
     while (!r->stop) {
         if (take(r) > 0) { clock_gettime(CLOCK_MONOTONIC, &last); continue; }
+        if (!r->spin) { (void)poll(&p, 1, 1); continue; }
         clock_gettime(CLOCK_MONOTONIC, &now);
         const long idle_us = (now.tv_sec - last.tv_sec) * 1000000L + (now.tv_nsec - last.tv_nsec) / 1000;
         if (idle_us >= 20000) (void)poll(&p, 1, 1);
@@ -113,6 +116,7 @@ void* udpd_start(const int* fds, const int* stream, int n) {
     for (int i = 0; i < n; i++) {
         d->rx[i].fd = fds[i];
         d->rx[i].stream = stream ? stream[i] : 0;
+        d->rx[i].spin = n <= kSpinMax;
         d->rx[i].slots = (uint8_t*)malloc((size_t)kBatch * kMax);
         pthread_create(&d->rx[i].th, NULL, loop, &d->rx[i]);
     }
