@@ -522,6 +522,9 @@ def main():
                          "C4: subscribers whose egress GPU is not the stream's owner), fed every step through "
                          "peer mailboxes (xGMI, no collective); 0: none")
     ap.add_argument("--replica-subs", type=int, default=1, help="UDP subscribers per replica session")
+    ap.add_argument("--ring-mb", type=int, default=16,
+                    help="diagnostic: initial video ring MiB per sender (default 16; recorded in the line)")
+    ap.add_argument("--no-ring-growth", action="store_true", help="diagnostic: rings keep their initial sizes")
     ap.add_argument("--ablation-study", action="store_true",
                     help="allow EDGPU_ABLATE (timing experiments that skip work): the line is then not a "
                          "valid measurement and says so")
@@ -590,7 +593,8 @@ def main():
     max_pk = max(b["n"] for b in batches)
     max_out = int(max(b["n"] for b in batches) * args.subs * 1.05) + 1024
     max_arena = int(max(b["bytes"] for b in batches) * args.subs * 1.05) // 16 * 16 + (1 << 20)
-    ctx = edgpu.Context(device=local, video_ring_packets=8192, video_ring_bytes=16 << 20,
+    ring_cfg = {"ring_growth": edgpu.FALSE} if args.no_ring_growth else {}
+    ctx = edgpu.Context(device=local, video_ring_packets=8192, video_ring_bytes=args.ring_mb << 20, **ring_cfg,
                         other_ring_packets=256, other_ring_bytes=64 << 10,
                         out_arena_bytes=max_arena, max_out_packets=max_out,
                         max_batch_packets=max_pk + 1,
@@ -788,6 +792,8 @@ def main():
                    "tick_ms": args.tick_ms,
                    "rewrite": rewrite_desc,
                    "engine_env": knobs,
+                   **({"diagnostic_rings": {"video_ring_mb": args.ring_mb, "growth": not args.no_ring_growth}}
+                      if args.ring_mb != 16 or args.no_ring_growth else {}),
                    "parallelism": f"stream-hash shards x{world}, no data-path collective"
                                   + (f"; C4 replicas: {args.replicas} sessions/rank fed through peer mailboxes"
                                      if link is not None else "")
