@@ -8,8 +8,8 @@ HBM over xGMI (edgpu_session_import takes the mapped pointer) and the two proces
 the mailbox's header words.  The CPU rehearsal (gloo tests, no GPU) uses POSIX shared memory the
 same way.  Layout (bytes):
 
-  [0, 64)      owner writes:   seq u64 (the last publication), slot u32, n u32, bytes u64,
-               collected u64 (the feedback round it took last)
+  [0, 64)      owner writes:   collected u64 at 24 (the feedback round it took last); the
+               publications' own headers are the slots'
   [64, 128)    replica writes: ack u64 (the last publication imported), nfb u32, fb_seq u64
                (the publication whose feedback follows)
   [128, FB)    replica writes: feedback -- global ids of sessions one of its outputs relocated
@@ -155,8 +155,7 @@ class Mailbox:
         h = self.region.read(0, HDR_BYTES)
         u64 = h[0:32].view(np.uint64)
         r64 = h[64:96].view(np.uint64)
-        return {"seq": int(u64[0]), "slot": int(h[8:12].view(np.uint32)[0]), "n": int(h[12:16].view(np.uint32)[0]),
-                "bytes": int(u64[2]), "collected": int(u64[3]), "ack": int(r64[0]),
+        return {"collected": int(u64[3]), "ack": int(r64[0]),
                 "nfb": int(h[72:76].view(np.uint32)[0]), "fb_seq": int(r64[2])}
 
     def _wait(self, pred, what: str) -> dict:
@@ -197,7 +196,6 @@ class Mailbox:
         hdr[8:16] = np.array([k, n], np.uint32).view(np.uint8)
         hdr[16:24] = np.array([total], np.uint64).view(np.uint8)
         self.region.write(base, hdr)       # the slot's seq: its bytes and offsets are complete already
-        self.region.write(0, hdr)          # (the mailbox header: the latest, for inspection)
         self.bytes_moved += total
         return total
 
