@@ -11,7 +11,9 @@ same way.  Layout (bytes):
   [0, 64)      owner writes:   collected u64 at 24 (the feedback round it took last); the
                publications' own headers are the slots'
   [64, 128)    replica writes: ack u64 (the last publication imported), nfb u32, fb_seq u64
-               (the publication whose feedback follows)
+               (the last publication imported when the feedback was written), fb_round u64
+               (the feedback round: one per feedback call, so a replica that reports twice
+               between two publications loses neither report)
   [128, FB)    replica writes: feedback -- global ids of sessions one of its outputs relocated
                (ReflectorSender::NeedRelocateBookMark -> SetHasVideoKeyFrameUpdate, ReflectorStream.cpp:
                1311-1317), at most `max_sessions`
@@ -27,7 +29,8 @@ Protocol -- every rank calls the steps at the same points of its ticks:
                      header with the new seq (the image bytes are complete before it changes)
   consume   replica  waits until the slot of the publication it expects holds it, reads the
                      offsets, imports from the mapped slot and writes ack = seq
-  feedback  replica  (after its tick's backpressure reports) the relocations it saw, fb_seq = seq
+  feedback  replica  (after its tick's backpressure reports) the relocations it saw, fb_seq = seq,
+                     fb_round + 1
   collect   owner    takes the feedback -- in lockstep mode waiting for fb_seq == seq, so a
                      relocation reaches the owner before its next ingest as in the one-process
                      reference.  Without lockstep a round the owner has not taken yet is carried
@@ -77,6 +80,18 @@ class DeviceRegion:
             self.buf = None
         elif self.base:
             self.ctx.ipc_close(self.base)
+        self.base = 0
+
+
+class SameProcessRegion(DeviceRegion):
+    """The replica end of a mailbox whose owner lives in this process (replica.MailboxReplicaLink):
+    the owner's device pointer itself stands for the handle."""
+
+    def __init__(self, ctx, nbytes: int = 0, handle: int | None = None):
+        self.ctx, self.buf = ctx, None
+        self.base, self.nbytes, self.handle = int(handle), nbytes, handle
+
+    def close(self):
         self.base = 0
 
 
@@ -146,6 +161,7 @@ class Mailbox:
         self.handle = self.region.handle
         self.seq = 0                      # owner: last published; replica: last imported
         self.collected = 0                # owner: the feedback round it took last
+        self.fb_round = 0                 # replica: its last feedback round
         self.fb_last: list = []           # replica: its last feedback round's ids
         self.timeout_s = timeout_s
         self.bytes_moved = 0
@@ -156,7 +172,7 @@ class Mailbox:
         u64 = h[0:32].view(np.uint64)
         r64 = h[64:96].view(np.uint64)
         return {"collected": int(u64[3]), "ack": int(r64[0]),
-                "nfb": int(h[72:76].view(np.uint32)[0]), "fb_seq": int(r64[2])}
+                "nfb": int(h[72:76].view(np.uint32)[0]), "fb_seq": int(r64[2]), "fb_round": int(r64[3])}
 
     def _wait(self, pred, what: str) -> dict:
         t0 = time.perf_counter()
@@ -206,10 +222,10 @@ class Mailbox:
             h = self._wait(lambda h: h["fb_seq"] >= self.seq, f"feedback of publication {self.seq}")
         else:
             h = self._hdr()
-        if h["fb_seq"] <= self.collected:
+        if h["fb_round"] <= self.collected:
             return []
         ids = self.region.read(HDR_BYTES, 4 * h["nfb"]).view(np.uint32).tolist() if h["nfb"] else []
-        self.collected = h["fb_seq"]
+        self.collected = h["fb_round"]
         self.region.write(24, np.array([self.collected], np.uint64))
         return ids
 
@@ -248,9 +264,9 @@ class Mailbox:
         return nbytes
 
     def feedback(self, relocated=()) -> None:
-        """This tick's relocations (global ids), as the feedback round of the last publication."""
+        """This tick's relocations (global ids), as a feedback round after the last publication."""
         fb = set(int(g) for g in relocated)
-        if self.fb_last and self._hdr()["collected"] < self.seq - 1:    # the last round not taken yet
+        if self.fb_last and self._hdr()["collected"] < self.fb_round:   # the last round not taken yet
             fb |= set(self.fb_last)
         ids = np.asarray(sorted(fb), dtype=np.uint32)
         if len(ids) > self.max_sessions:
@@ -258,10 +274,11 @@ class Mailbox:
         self.fb_last = ids.tolist()
         if len(ids):
             self.region.write(HDR_BYTES, ids)
-        w = np.zeros(16, np.uint8)
+        self.fb_round += 1
+        w = np.zeros(24, np.uint8)
         w[0:4] = np.array([len(ids)], np.uint32).view(np.uint8)
-        w[8:16] = np.array([self.seq], np.uint64).view(np.uint8)
-        self.region.write(72, w)           # nfb with fb_seq: the ids are written already
+        w[8:24] = np.array([self.seq, self.fb_round], np.uint64).view(np.uint8)
+        self.region.write(72, w)           # nfb, fb_seq, fb_round: the ids are written already
 
     def close(self):
         self.region.close()

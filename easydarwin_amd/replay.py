@@ -188,12 +188,13 @@ def _batches(trace: Trace, flush_on_rtpinfo: bool):
 
 def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None = None,
            interleaved: int | None = None, sockets: dict | None = None, rewrite: dict | None = None,
-           pinned: bool = False, tick_info: list | None = None, slots: dict | None = None, **cfg):
+           pinned: bool = False, tick_info: list | None = None, slots: dict | None = None, link_cls=None, **cfg):
     """Returns (capture_bytes, per-tick stats list).
 
     replica=None: subscribers join the context that ingests (the owner).
     replica="all" / "late" / "split": subscribers join a replica session on a second context,
-    kept in step with the owner by session images (easydarwin_amd/replica.py); "all" creates
+    kept in step with the owner by session images (easydarwin_amd/replica.py; `link_cls`: the
+    link class, ReplicaLink by default, replica.MailboxReplicaLink through a peer mailbox); "all" creates
     every replica before the first packet; "late" creates a fresh replica for every joining
     subscriber at its join tick, from a full image taken mid-stream (the C4 fast-start
     path); "split" sends the odd subscriber ids to one replica per session and keeps the even
@@ -235,7 +236,7 @@ def replay(trace: Trace, ctx: edgpu.Context | None = None, replica: str | None =
             raise ValueError("socket egress replays serve one context")
         dev = int(cfg.get("device", 0))
         rep = edgpu.Context(**cfg)
-        link = ReplicaLink(ctx, dev, rep, dev)
+        link = (link_cls or ReplicaLink)(ctx, dev, rep, dev)
     try:
         sess_tracks = []
         rsess = {}

@@ -128,6 +128,78 @@ class ReplicaLink:
         return upd
 
 
+class MailboxReplicaLink(ReplicaLink):
+    """ReplicaLink whose images and relocations travel through a peer mailbox in the owner's HBM
+    (easydarwin_amd/mailbox.py), as DistReplicaLink's do between processes -- both ends in one
+    process: the replica end reads the owner's buffer directly instead of through an IPC mapping
+    (a process cannot open an IPC handle of its own memory).  So every golden pins the mailbox
+    protocol, the import straight from the mailbox slot and the lockstep relocation feedback on
+    the GPU (tests/test_gpu_replica.py, mode "mailbox")."""
+
+    def __init__(self, owner: edgpu.Context, owner_device: int, replica: edgpu.Context,
+                 replica_device: int, session_bytes: int = 4 << 20):
+        super().__init__(owner, owner_device, replica, replica_device)
+        self.session_bytes = session_bytes
+        self.out_mb = self.in_mb = None
+        self._retired = []
+
+    def _boxes(self, n: int, nbytes: int):
+        from .mailbox import DeviceRegion, Mailbox, SameProcessRegion
+        mb = self.out_mb
+        if mb is not None and n <= mb.max_sessions and nbytes <= mb.slot_size - mb.meta:
+            return
+        room = max(n, 2 * (mb.max_sessions if mb else 0), 8)
+        slot = max(room * self.session_bytes, 2 * nbytes)
+        if mb is not None:
+            self._retired += [self.in_mb, mb]
+        self.out_mb = Mailbox(DeviceRegion, self.owner, room, slot)
+        self.in_mb = Mailbox(SameProcessRegion, self.replica, room, slot, handle=self.out_mb.region.base)
+
+    def sync(self, now_ms: int) -> int:
+        if not self.pairs:
+            return 0
+        osess = [o for o, _ in self.pairs]
+        nsnd = [self.owner.senders_of([o]) for o in osess]
+        since = np.concatenate([self.heads[pr] if pr in self.heads
+                                else np.full(n, edgpu.IMAGE_FULL, dtype=np.uint64)
+                                for pr, n in zip(self.pairs, nsnd)])
+        offsets, _ = self.owner.session_export(osess, now_ms, since=since)     # size query
+        self._boxes(len(self.pairs), int(offsets[-1]))
+        pairs = list(self.pairs)
+
+        def export_fn(dst, cap):
+            offsets, heads = self.owner.session_export(osess, now_ms, dst, cap, since=since)
+            k = 0
+            for pr, n in zip(pairs, nsnd):
+                self.heads[pr] = heads[k:k + n].copy()
+                k += n
+            return offsets
+        self.out_mb.publish(export_fn, len(pairs))
+        total = self.in_mb.consume(lambda ptr, offs: self.replica.session_import(ptr, offs, [r for _, r in pairs]),
+                                   len(pairs))
+        self.bytes_shipped += total
+        return total
+
+    def feedback(self) -> list:
+        if self.in_mb is None:              # nothing published yet: nothing to relocate either
+            return super().feedback()
+        if not self.pairs:
+            return []
+        hit = set(self.replica.session_relocations([r for _, r in self.pairs]))
+        self.in_mb.feedback([o for o, r in self.pairs if r in hit])
+        upd = sorted(set(self.out_mb.collect(lockstep=True)))
+        if upd:
+            self.owner.session_key_update(upd)
+        return upd
+
+    def close(self):
+        for mb in self._retired + [self.in_mb, self.out_mb]:
+            if mb is not None:
+                mb.close()
+        self._retired, self.in_mb, self.out_mb = [], None, None
+        super().close()
+
+
 class DistReplicaLink:
     """The one-process-per-GPU form of ReplicaLink.  The owner of global session g is rank
     ``dist.owner(g, world)``; a rank that serves subscribers of a session it does not own keeps a

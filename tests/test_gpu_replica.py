@@ -14,6 +14,9 @@ or without its outputs, a fresh re-push, RereadPrefs): the lifecycle reaches the
 ids from a replica and the even ones from the owner, and the bucket places of all of them are
 the ones a single context gives -- the reference's one array (ReflectorStream::AddOutput,
 ReflectorStream.cpp:281-334) -- so the transmit times' bucket lateness is the reference's too.
+Each mode runs a second time with the images and relocations going through a peer mailbox in
+the owner's memory (replica.MailboxReplicaLink), so every golden pins the mailbox protocol the
+one-process-per-GPU link uses, the import straight from the mailbox slot included.
 """
 import hashlib
 
@@ -22,16 +25,21 @@ import pytest
 
 from easydarwin_amd import edgpu
 from easydarwin_amd.replay import replay
+from easydarwin_amd.replica import MailboxReplicaLink
 from scenarios import SCENARIOS
 from test_gpu_parity import _fixture, _trace
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["all", "late", "split"])
+@pytest.mark.parametrize("mode", ["all", "late", "split",
+                                  "all+mailbox", "late+mailbox", "split+mailbox"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
 def test_replica_matches_reference(name, mode):
+    """"+mailbox": the images and the relocation feedback travel through a peer mailbox
+    (MailboxReplicaLink: the protocol DistReplicaLink runs between processes, both ends here)."""
     tr = _trace(name)
-    cap, _ = replay(tr, replica=mode)
+    mode, _, via = mode.partition("+")
+    cap, _ = replay(tr, replica=mode, link_cls=MailboxReplicaLink if via else None)
     if hashlib.sha256(cap).hexdigest() != _fixture(name)["capture_sha256"]:
         from easydarwin_amd.trace import capture_summary, read_capture
         g, w = capture_summary(read_capture(cap)), _fixture(name)["substreams"]
