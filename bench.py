@@ -532,7 +532,7 @@ def main():
 
     # Engine switches that change what is measured are recorded in the line; EDGPU_ABLATE skips
     # work inside the timed region, so a bench under it is refused unless it is an ablation study.
-    knobs = {k: os.environ[k] for k in ("EDGPU_FANOUT", "EDGPU_INGEST_DEPTH", "EDGPU_INGEST", "EDGPU_INGEST_TCP", "EDGPU_INGEST_THREADS", "EDGPU_ABLATE",
+    knobs = {k: os.environ[k] for k in ("EDGPU_TCP_WALK", "EDGPU_TCP_SEG", "EDGPU_FANOUT", "EDGPU_INGEST_DEPTH", "EDGPU_INGEST", "EDGPU_INGEST_TCP", "EDGPU_INGEST_THREADS", "EDGPU_ABLATE",
                                         "EDGPU_POISON", "EDGPU_LIB") if k in os.environ}
     if "EDGPU_ABLATE" in knobs and not args.ablation_study:
         raise SystemExit("EDGPU_ABLATE is set: ablations skip work in the timed region (use --ablation-study)")
@@ -730,6 +730,14 @@ def main():
                     if args.rewrite_same_ssrc else
                     "per-subscriber seq/ts/SSRC" if args.rewrite else "identity (reference parity mode)")
     ing_traffic = None
+    # the deframe walk's shape (edgpu_engine.cpp: EDGPU_TCP_WALK / EDGPU_TCP_SEG, segments of 4 by
+    # default): part of the workload a traffic profile was taken on
+    deframe_walk = None
+    if args.ingest == "tcp":
+        w = {"0": "parallel", "1": "serial", "2": "seg"}.get(os.environ.get("EDGPU_TCP_WALK", "seg"),
+                                                             os.environ.get("EDGPU_TCP_WALK", "seg"))
+        deframe_walk = f"seg{max(int(os.environ.get('EDGPU_TCP_SEG', '4')), 1)}" if w == "seg" else \
+            ("serial" if w == "serial" else "parallel")
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_fanout_c2*.json"))):
         if world != 1:
             break
@@ -738,7 +746,7 @@ def main():
             wl = pj.get("workload", {})
             if (pj.get("bench_fanout_kernel") == ctx.fanout_kernel() and wl.get("sessions_per_gpu") == args.sessions
                     and wl.get("subs_per_session") == args.subs and wl.get("ingest") == args.ingest
-                    and wl.get("tick_ms", 1000) == args.tick_ms
+                    and wl.get("tick_ms", 1000) == args.tick_ms and wl.get("deframe_walk") == deframe_walk
                     and wl.get("rewrite", "identity (reference parity mode)") == rewrite_desc):
                 traffic = pj.get("hbm_bytes_per_launch")
                 ing_traffic = pj.get("ingest_hbm_bytes_per_launch")
@@ -788,6 +796,7 @@ def main():
                                + (", RTSP-interleaved TCP push reads deframed on the GPU" if args.ingest == "tcp" else "")
                                + (", batches in pinned host memory (PCIe H2D overlapped)" if args.ingest == "host" else ""),
                    "ingest": args.ingest,
+                   **({"deframe_walk": deframe_walk} if deframe_walk else {}),
                    "sessions_per_gpu": args.sessions, "subs_per_session": args.subs,
                    "tick_ms": args.tick_ms,
                    "rewrite": rewrite_desc,

@@ -501,6 +501,121 @@ __global__ __launch_bounds__(256) void k_tcp_resolve(TcpParams P) {
     }
 }
 
+// ---- k_tcp_walk_seg: the walk in segments of P.seg chunks, one wave per segment ----
+// A candidate walk covers its whole segment: chunk after chunk it records the frames in that
+// chunk's row of the same candidate index and links the row to itself in the next chunk, and at
+// the segment's end it links to the next segment's candidate as k_tcp_walk does at a chunk's.  So
+// k_tcp_resolve follows the links unchanged, and only a segment's first chunk has a candidate
+// window: P.seg x fewer windows (2 KiB per 32-KiB chunk, 0.03 GB at C2) and false candidates
+// than k_tcp_walk, for walks P.seg x longer -- still beside the fan-out.  The
+// other chunks of a segment report more candidates than kept, so a search that lands there (only
+// after a sequential fallback) walks sequentially.
+__global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu(EDGPU_TCP_WALK_WPE)))
+void k_tcp_walk_seg(TcpParams P) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ uint16_t s_own[kWalkWaves][kTcpCands], s_next[kWalkWaves][kTcpCands];
+    const uint32_t c = blockIdx.x * kWalkWaves + wid;
+    if (c >= P.nchunks) return;                                   // (per wave: no block barrier below)
+    const TcpGroup G = P.groups[P.chunk_group[c]];
+    const uint32_t k = c - G.first_chunk;
+    if (k % P.seg) {
+        if (lane == 0) P.ncand[c] = kTcpCands + 1;
+        return;
+    }
+    const TcpView v = tcp_view(P, G);
+    const uint32_t kend = min(k + P.seg, G.nchunks);              // the segment: chunks [k, kend)
+    const uint64_t start = (uint64_t)k * kTcpChunk, send = min((uint64_t)kend * kTcpChunk, v.len);
+    const uint32_t n = tcp_candidates(v, start, s_own[wid], lane);
+    const uint32_t nn = send < v.len ? tcp_candidates(v, send, s_next[wid], lane) : 0u;
+    if (lane == 0) P.ncand[c] = n;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");        // the lists, written lane by lane
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (n > kTcpCands) return;                                     // (uniform)
+    for (uint32_t j = (uint32_t)lane; j < n; j += 64) {
+        uint64_t pos = start + s_own[wid][j];
+        for (uint32_t kk = k; kk < kend; kk++) {
+            const uint64_t cs = (uint64_t)kk * kTcpChunk, ce = min(cs + kTcpChunk, v.len);
+            const size_t ci = (size_t)(G.first_chunk + kk) * kTcpCands + j;
+            const uint64_t entry = pos;
+            uint32_t nf;
+            const uint32_t code = tcp_walk(v, pos, cs, ce, nf, P.offs + ci * kTcpFrames);
+            uint8_t link = 0xFE;
+            bool more = false;
+            if (code == kWalkRun && pos < v.len) {
+                if (kk + 1 < kend) {                              // the same walk, the next chunk
+                    link = (uint8_t)j;
+                    more = true;
+                } else {                                          // the next segment's candidate
+                    link = 0xFF;
+                    if (nn <= kTcpCands) {
+                        const uint32_t q = (uint32_t)(pos - send);
+                        for (uint32_t i = 0; i < nn; i++)
+                            if (s_next[wid][i] == q) { link = (uint8_t)i; break; }
+                    }
+                }
+            }
+            TcpCand r;
+            r.q = (uint32_t)(entry - cs);
+            r.exit = (uint32_t)(pos - cs);
+            r.nframes = nf;
+            r.code = code;
+            P.cands[ci] = r;
+            P.links[ci] = link;
+            if (!more) break;
+        }
+    }
+}
+
+// ---- k_tcp_chain: k_tcp_walk + k_tcp_resolve in one, each stream walked in order ----
+// One lane per session: its walk enters each chunk where the previous chunk's ended, so it reads
+// only the true chain's headers -- no candidate windows, no false candidates (the parallel walk's
+// ~0.05 GB of the two, r06 C2: DESIGN §5.4).  The hops are one dependent load each; the lanes of a
+// wave hop side by side, so 1024 sessions are 16 waves, which keep ~1024 header loads in flight
+// beside the previous tick's fan-out.  It writes what k_tcp_resolve writes (chunk results with the
+// walk's records as candidate row 0, the group's frames / stop code / stop position), so
+// k_tcp_scan, k_tcp_finish and k_ingest run unchanged.
+__global__ __launch_bounds__(64) void k_tcp_chain(TcpParams P) {
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    if (g >= P.ngroups) return;
+    const TcpGroup G = P.groups[g];
+    const TcpView v = tcp_view(P, G);
+    uint64_t pos = 0, stop = v.len;
+    uint32_t fb = 0, stop_code = kWalkRun;
+    bool stopped = false;
+    for (uint32_t k = 0; k < G.nchunks; k++) {
+        const uint32_t c = G.first_chunk + k;
+        TcpChunkRes R;
+        R.fbase = fb;
+        if (stopped) {
+            R.entry = kTcpNone; R.nframes = 0; R.cand = kTcpNone;
+            P.chunkres[c] = R;
+            continue;
+        }
+        const uint64_t start = (uint64_t)k * kTcpChunk, end = min(start + kTcpChunk, v.len);
+        const uint64_t entry = pos;
+        uint32_t nf = 0;
+        const uint32_t code = tcp_walk(v, pos, start, end, nf, P.offs + (size_t)c * kTcpCands * kTcpFrames);
+        TcpCand r;
+        r.q = (uint32_t)(entry - start);
+        r.exit = (uint32_t)(pos - start);
+        r.nframes = nf;
+        r.code = code;
+        P.cands[(size_t)c * kTcpCands] = r;
+        R.entry = nf ? r.q : kTcpNone;
+        R.nframes = nf;
+        R.cand = 0;
+        P.chunkres[c] = R;
+        fb += nf;
+        if (code != kWalkRun || pos >= v.len) { stopped = true; stop_code = code; stop = pos; }
+    }
+    TcpGroup& W = P.groups[g];
+    W.nframes = fb;
+    // a walk that ran off the end of the stream stops there: everything framed
+    W.code = (stop_code == kWalkPartial && stop >= v.len) ? kWalkRun : stop_code;
+    W.stop = stop;
+}
+
 // ---- k_tcp_scan: one 1024-thread workgroup; sessions -> ingest segments ----
 // Each thread takes a run of consecutive sessions (one for up to 1024 sessions): all frame
 // counts are loaded at once, one block scan places them.
@@ -732,10 +847,16 @@ __global__ __launch_bounds__(64) void k_tcp_finish(TcpParams P) {
 }
 
 hipError_t launch_deframe(const TcpParams& p, hipStream_t st) {
-    if (p.nchunks)
-        EDGPU_LAUNCH(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
-                           dim3(64 * kWalkWaves), 0, st, p);
-    EDGPU_LAUNCH(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
+    if (p.walk == 1) {
+        if (p.ngroups) EDGPU_LAUNCH(k_tcp_chain, dim3((p.ngroups + 63) / 64), dim3(64), 0, st, p);
+    } else {
+        if (p.nchunks && p.walk == 2)
+            EDGPU_LAUNCH(k_tcp_walk_seg, dim3((p.nchunks + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, st, p);
+        else if (p.nchunks)
+            EDGPU_LAUNCH(k_tcp_walk<kTcpWalkCpw>, dim3((p.nchunks + kWalkWaves * kTcpWalkCpw - 1) / (kWalkWaves * kTcpWalkCpw)),
+                         dim3(64 * kWalkWaves), 0, st, p);
+        EDGPU_LAUNCH(k_tcp_resolve, dim3(p.ngroups), dim3(256), 0, st, p);
+    }
     EDGPU_LAUNCH(k_tcp_scan, dim3(1), dim3(kScanThreads), 0, st, p);
     EDGPU_LAUNCH(k_tcp_finish, dim3(p.ngroups), dim3(64), 0, st, p);
     return hipGetLastError();

@@ -255,6 +255,9 @@ struct edgpu_ctx {
     int fanout_variant = -1;        // EDGPU_FANOUT (A/B measurement); -1 = default kernel
     uint64_t joined_rows = 0;       // sub-stream rows of the outputs added since the last tick
     bool deframe_serial = false;    // EDGPU_DEFRAME_SERIAL (measurement): no deframe / fan-out overlap
+    uint32_t tcp_walk = 2;          // EDGPU_TCP_WALK: 0 parallel chunk walk + resolve, 1 serial chain,
+                                    // 2 segments of tcp_seg chunks (TcpParams.walk)
+    uint32_t tcp_seg = 4;           // EDGPU_TCP_SEG
     uint32_t ablate = 0;
     int timing = EDGPU_TIMING_ALL;  // edgpu_set_timing: which per-launch event pairs are recorded
     uint32_t ingest_mode = 0;       // EDGPU_INGEST: 0 copy in k_ingest, 1 separate copy kernel
@@ -603,6 +606,10 @@ int edgpu_ctx_create(const edgpu_config* cfg_in, edgpu_ctx** out) {
     // measurement: the deframe waits for everything enqueued before it (no overlap with the last fan-out)
     if (const char* v = getenv("EDGPU_DEFRAME_SERIAL")) x->deframe_serial = atoi(v) != 0;
 #endif
+    // the deframe walk (TcpParams.walk): "serial" / "parallel"
+    if (const char* v = getenv("EDGPU_TCP_WALK"))
+        x->tcp_walk = !strcmp(v, "serial") || !strcmp(v, "1") ? 1u : !strcmp(v, "seg") || !strcmp(v, "2") ? 2u : 0u;
+    if (const char* v = getenv("EDGPU_TCP_SEG")) x->tcp_seg = (uint32_t)std::max(atoi(v), 1);
     *out = x;
     return EDGPU_OK;
 }
@@ -1891,6 +1898,8 @@ int edgpu_ingest_interleaved(edgpu_ctx* x, const edgpu_tcp_read* reads, uint32_t
     p.desc = x->d_desc; p.src_addr = x->d_tcp_src; p.max_desc = x->cfg.max_batch_packets;
     p.seg_off = x->d_seg; p.seg_sess = x->d_seg_sess;
     p.results = x->d_tcp_results.ptr; p.tot = x->d_tcp_tot;
+    p.walk = x->tcp_walk;
+    p.seg = x->tcp_seg;
     HIP_CHECK(launch_deframe(p, x->aux));
     // The report is the deframe's alone (k_tcp_finish counts the frames too): read on aux, it
     // waits for the deframe only, which runs beside the previous tick's fan-out.  k_ingest is

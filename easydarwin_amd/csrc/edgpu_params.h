@@ -196,6 +196,10 @@ struct TcpParams {
     uint32_t* seg_sess;
     edgpu_tcp_result* results;
     TcpTotals* tot;
+    uint32_t walk;          // 0: k_tcp_walk + k_tcp_resolve (candidate windows, every chunk at once);
+                            // 1: k_tcp_chain (each stream walked in order, one lane per session);
+                            // 2: k_tcp_walk_seg + k_tcp_resolve (candidate windows every `seg` chunks)
+    uint32_t seg;           // walk 2: chunks per segment
 };
 
 struct BlockedParams {

@@ -103,6 +103,38 @@ def test_report_matches_restatement_split_calls(name):
 def test_many_sessions_device_reads():
     """64 sessions in one call, each a different seeded connection shape, reads resident in
     HBM (EDGPU_PTR_DEVICE); then a second call continuing every session's carry."""
+    _many_sessions()
+
+
+# The deframe walk's three shapes (EDGPU_TCP_WALK, read at context creation; TcpParams.walk):
+# every chunk from candidate windows at once, one serial chain per session, and segments of
+# EDGPU_TCP_SEG chunks (the default, 4) -- seg 1 is the per-chunk walk, seg 3 ends segments
+# mid-stream at odd chunk counts.  Each must give the restatement's reports and the reference's
+# frames.
+WALKS = [("parallel", 4), ("serial", 4), ("seg", 1), ("seg", 2), ("seg", 3), ("seg", 8)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("walk,seg", WALKS, ids=[f"{w}{s if w == 'seg' else ''}" for w, s in WALKS])
+def test_walk_shapes_match_restatement(walk, seg, monkeypatch):
+    monkeypatch.setenv("EDGPU_TCP_WALK", walk)
+    monkeypatch.setenv("EDGPU_TCP_SEG", str(seg))
+    for name in CASES:
+        reads = case(name)
+        rows, blob = _rows([(0, reads)])
+        want, frames = ingest_reads({}, rows, blob)
+        with edgpu.Context(**CFG) as ctx:
+            ctx.session_add(SDP)
+            assert _as_list(_call(ctx, rows, blob)) == want, name
+            assert ctx.stats().ingested_packets == len(frames), name
+    _many_sessions()
+    for name in ("anchor", "prefs_buffer"):
+        cap, _ = replay(_trace(name), interleaved=1)
+        with open(os.path.join(GOLD, name + ".json")) as f:
+            assert hashlib.sha256(cap).hexdigest() == json.load(f)["capture_sha256"], name
+
+
+def _many_sessions():
     rng = random.Random(5)
     conns = []
     for s in range(64):

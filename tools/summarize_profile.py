@@ -56,6 +56,8 @@ fan = res["kernels"].get(fan_name, {})
 res["fanout_kernel"] = fan_name                              # rocprofv3 -T (truncated) name
 res["bench_fanout_kernel"] = bench["roofline"]["kernel"]     # the engine's variant name (template args)
 res["workload"] = {k: bench["config"].get(k) for k in ("sessions_per_gpu", "subs_per_session", "ingest", "tick_ms", "rewrite")}
+if bench["config"].get("deframe_walk"):
+    res["workload"]["deframe_walk"] = bench["config"]["deframe_walk"]
 res["hbm_bytes_per_launch"] = fan.get("hbm_bytes_per_launch")
 # the ingest side of a step: k_ingest (+ the RTSP-interleaved deframe kernels k_tcp_*)
 ing = [k for k in res["kernels"] if k.startswith("k_ingest") or k.startswith("k_tcp")]
