@@ -125,7 +125,9 @@ def test_walk_shapes_match_restatement(walk, seg, monkeypatch):
         want, frames = ingest_reads({}, rows, blob)
         with edgpu.Context(**CFG) as ctx:
             ctx.session_add(SDP)
-            assert _as_list(_call(ctx, rows, blob)) == want, name
+            got = _call(ctx, rows, blob)
+            ctx.keyframe_index()
+            assert _as_list(got) == want, name
             assert ctx.stats().ingested_packets == len(frames), name
     _many_sessions()
     for name in ("anchor", "prefs_buffer"):
