@@ -1146,6 +1146,19 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     __shared__ uint64_t sb[4];
     __shared__ uint32_t sc[4];
+    // loads that do not wait for the K2 partials, issued first so that their latency overlaps the
+    // partials' reduction: this row's size, and the work-item counts of the senders this lane
+    // reserves for (below)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    auto chunks_of = [&](const SenderDev& D) {
+        return (uint32_t)(((D.head > D.umin ? D.head - D.umin : 0) + P.T.chunk - 1) / P.T.chunk);
+    };
+    uint64_t bytes = 0; uint32_t count = 0;
+    if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
+    uint32_t res_nch = 0, res_base = 0;
+    if (gw + lane * nwaves < P.T.nsenders) res_nch = chunks_of(P.senders[gw + lane * nwaves]);
     // Every block adds up all the K2 partials (a few hundred at most): the tick's totals, the
     // part before this block, and the largest sub-stream.
     uint64_t base_b, tb_all, mb;
@@ -1186,8 +1199,6 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
         if (!fits && impossible) atomicExch(&P.totals->status, EDGPU_OUT_OVERFLOW);
         if (fits) { P.totals->pass_bytes[0] = tb_all; P.totals->pass_desc[0] = tc_all; }
     }
-    uint64_t bytes = 0; uint32_t count = 0;
-    if (q < P.T.nsubs) { bytes = P.subs[q].bytes; count = P.subs[q].count; }
     uint64_t tb; uint32_t tc;
     const uint64_t pb = block_exclusive_scan<uint64_t>(bytes, sb, tb);
     const uint32_t pc = block_exclusive_scan<uint32_t>(count, sc, tc);
@@ -1249,18 +1260,17 @@ __global__ __launch_bounds__(256) void k_plan_final(PlanParams P) {
     // work items: one wave per sender (waves stride over senders), one lane per chunk.  Chunk
     // k covers packets [umin + k * chunk, min(umin + (k + 1) * chunk, head)), so every lane
     // loads its two boundary records at once instead of walking the chunks one by one.
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    auto chunks_of = [&](const SenderDev& D) {
-        return (uint32_t)(((D.head > D.umin ? D.head - D.umin : 0) + P.T.chunk - 1) / P.T.chunk);
-    };
-    // the wave's senders are gw, gw + nwaves, ...: lane j reserves the items of the j-th, so its
-    // first 64 senders cost one round of atomics in flight together, not one round trip each
-    uint32_t res_nch = 0, res_base = 0;
-    if (gw + lane * nwaves < P.T.nsenders) {
-        res_nch = chunks_of(P.senders[gw + lane * nwaves]);
-        if (res_nch) res_base = atomicAdd(&P.totals->nwork, res_nch);
+    // the wave's senders are gw, gw + nwaves, ...: lane j reserves the items of the j-th.  The
+    // block's reservations are one atomicAdd on the tick's item count, its lanes' bases a block
+    // scan: one same-address atomic per block instead of one per sender (4096 serialised at one
+    // L2 channel, each lane waiting for its return, were most of this kernel's fixed ~14 us)
+    {
+        __shared__ uint32_t s_wbase;
+        uint32_t tot;
+        const uint32_t pre = block_exclusive_scan<uint32_t>(res_nch, sc, tot);
+        if (threadIdx.x == 0) s_wbase = tot ? atomicAdd(&P.totals->nwork, tot) : 0u;
+        __syncthreads();
+        res_base = s_wbase + pre;
     }
     uint32_t j = 0;
     for (uint32_t s = gw; s < P.T.nsenders; s += nwaves, j++) {
