@@ -705,9 +705,12 @@ def main():
                     "exchange_ms_per_step": round(1e3 * max(p[0] for p in per), 4),
                     "peer_wait_ms_per_step": round(1e3 * max(p[2] for p in per), 4),
                     "image_bytes_per_step": int(sum(p[1] for p in per)),
-                    "transport": "peer mailboxes in the owners' HBM (IPC handles at the join); the replica's GPU "
-                                 "imports over xGMI; no collective inside the timed steps",
+                    "transport": "peer mailboxes: images in the owners' HBM (IPC handles at the join), header "
+                                 "words in shared memory; the replica's GPU imports over xGMI; no collective "
+                                 "inside the timed steps",
                     "check": xdev})
+                dist.barrier()                        # every rank is done with every mailbox
+                link.close()
         else:
             xdev = {"ok": False, "error": rep["preflight"]["error"], "replicas": "skipped: IPC preflight failed"}
 

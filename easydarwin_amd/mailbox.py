@@ -1,15 +1,18 @@
 """Peer mailboxes: the steady-state replica feed between processes, without a collective
 ("xGMI peer copies (RCCL only for the cross-GPU subscriber join)").
 
-One mailbox carries one owner rank's session images to one replica rank.  It lives in the
-owner's device memory (edgpu_device_alloc) and the replica maps it once, at the join
-(edgpu_ipc_open): from then on the replica's GPU reads the images straight out of the owner's
-HBM over xGMI (edgpu_session_import takes the mapped pointer) and the two processes meet only in
-the mailbox's header words.  The CPU rehearsal (gloo tests, no GPU) uses POSIX shared memory the
-same way.  Layout (bytes):
+One mailbox carries one owner rank's session images to one replica rank, in two regions the
+owner creates and hands over at the join:
+  * data: the image slots, in the owner's device memory (edgpu_device_alloc); the replica maps
+    it once (edgpu_ipc_open) and its GPU reads the images straight out of the owner's HBM over
+    xGMI (edgpu_session_import takes the mapped pointer, or a peer copy of it);
+  * control: the header words, the feedback ids and each slot's header and offsets, in POSIX
+    shared memory (the ranks of a node share its host memory) -- polled and written by the two
+    processes directly, so a step's handshake costs no device transfers.  The CPU rehearsal
+    (gloo tests, no GPU) keeps the images in shared memory as well.
 
-  [0, 64)      owner writes:   collected u64 at 24 (the feedback round it took last); the
-               publications' own headers are the slots'
+Control layout (bytes):
+  [0, 64)      owner writes:   collected u64 at 24 (the feedback round it took last)
   [64, 128)    replica writes: ack u64 (the last publication imported), nfb u32, fb_seq u64
                (the last publication imported when the feedback was written), fb_round u64
                (the feedback round: one per feedback call, so a replica that reports twice
@@ -17,18 +20,19 @@ same way.  Layout (bytes):
   [128, FB)    replica writes: feedback -- global ids of sessions one of its outputs relocated
                (ReflectorSender::NeedRelocateBookMark -> SetHasVideoKeyFrameUpdate, ReflectorStream.cpp:
                1311-1317), at most `max_sessions`
-  slot k (k = 0, 1) at slot_base(k): its own header (seq u64 of the publication it holds, n u32,
-               bytes u64), offsets u64[n + 1], then the images (16-B aligned); publication p
-               goes to slot p & 1, so a replica one publication behind still finds its own
+  slot k meta  the header of the publication in data slot k (seq u64, slot/n u32, bytes u64),
+               then its offsets u64[n + 1]; publication p goes to slot p & 1, so a replica one
+               publication behind still finds its own
 
 Protocol -- every rank calls the steps at the same points of its ticks:
 
   publish   owner    waits until ack >= seq - 1 (the slot it is about to reuse was imported),
                      exports the images (full the first time a session is sent to this replica,
-                     deltas after) into slot (seq + 1) & 1, writes their offsets, then the slot's
-                     header with the new seq (the image bytes are complete before it changes)
+                     deltas after) into data slot (seq + 1) & 1 (the export is complete when it
+                     returns), writes their offsets, then the slot's header with the new seq
   consume   replica  waits until the slot of the publication it expects holds it, reads the
-                     offsets, imports from the mapped slot and writes ack = seq
+                     offsets, imports from the mapped slot (complete when it returns) and writes
+                     ack = seq
   feedback  replica  (after its tick's backpressure reports) the relocations it saw, fb_seq = seq,
                      fb_round + 1
   collect   owner    takes the feedback -- in lockstep mode waiting for fb_seq == seq, so a
@@ -60,7 +64,6 @@ class DeviceRegion:
             self.buf = ctx.device_alloc(nbytes)
             self.base, self.nbytes = self.buf.ptr, nbytes
             self.handle = ctx.ipc_export(self.base)
-            ctx.copy_to_device(self.base, np.zeros(HDR_BYTES, np.uint8))
         else:
             self.buf = None
             self.base, self.nbytes, self.handle = ctx.ipc_open(handle), nbytes, handle
@@ -95,6 +98,9 @@ class SameProcessRegion(DeviceRegion):
         self.base = 0
 
 
+_created_here: set = set()           # shared-memory names this process created
+
+
 class HostRegion:
     """The CPU rehearsal's mailbox: POSIX shared memory (the handle is its name)."""
 
@@ -104,10 +110,19 @@ class HostRegion:
             self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, HDR_BYTES))
             self.owner = True
             self.handle = self.shm.name.encode()
+            _created_here.add(self.shm.name)
         else:
             self.shm = shared_memory.SharedMemory(name=handle.decode())
             self.owner = False
             self.handle = handle
+            # the creating rank owns the segment's lifetime: this process's resource tracker must
+            # not unlink it at exit (Python < 3.13 registers every attach)
+            if self.shm.name not in _created_here:
+                from multiprocessing import resource_tracker
+                try:
+                    resource_tracker.unregister(self.shm._name, "shared_memory")
+                except Exception:
+                    pass
         self.nbytes = self.shm.size
         self.view = np.ndarray((self.nbytes,), dtype=np.uint8, buffer=self.shm.buf)
         if self.owner:
@@ -129,36 +144,44 @@ class HostRegion:
             del self.view
             self.shm.close()
             if self.owner:
+                _created_here.discard(self.shm.name)
                 self.shm.unlink()
             self.shm = None
 
 
 def slot_meta(max_sessions: int) -> int:
-    """A slot's header (64 B) + offsets, rounded so its images start SLOT_ALIGN-aligned."""
-    return -(-(64 + 8 * (max_sessions + 1)) // SLOT_ALIGN) * SLOT_ALIGN
+    """A slot's header (64 B) + offsets in the control region, 64-B aligned."""
+    return -(-(64 + 8 * (max_sessions + 1)) // 64) * 64
 
 
-def slot_layout(max_sessions: int, slot_bytes: int):
-    """(feedback region end, slot 0 base, slot 1 base, slot size) for a mailbox of `max_sessions`
-    sessions whose publications hold at most `slot_bytes` of images."""
+def ctl_layout(max_sessions: int):
+    """(feedback region end, slot 0 meta, slot 1 meta, control bytes)."""
     fb_end = HDR_BYTES + 4 * max_sessions
-    size = slot_meta(max_sessions) + -(-slot_bytes // SLOT_ALIGN) * SLOT_ALIGN
-    s0 = -(-fb_end // SLOT_ALIGN) * SLOT_ALIGN
-    return fb_end, s0, s0 + size, size
+    m0 = -(-fb_end // 64) * 64
+    sm = slot_meta(max_sessions)
+    return fb_end, m0, m0 + sm, m0 + 2 * sm
 
 
 class Mailbox:
     """One direction owner -> replica.  The owner creates it (handle=None) and hands `handle`
-    over at the join; the replica opens it with the same sizes."""
+    (the data region's handle, the control region's name) over at the join; the replica opens it
+    with the same sizes.  `region_cls` holds the image slots (DeviceRegion, or HostRegion in the
+    rehearsal); the control words are always a HostRegion."""
 
-    def __init__(self, region_cls, ctx, max_sessions: int, slot_bytes: int, handle: bytes | None = None,
+    def __init__(self, region_cls, ctx, max_sessions: int, slot_bytes: int, handle=None,
                  timeout_s: float = 60.0):
         self.max_sessions, self.slot_bytes = int(max_sessions), int(slot_bytes)
-        self.fb_end, s0, s1, self.slot_size = slot_layout(self.max_sessions, self.slot_bytes)
-        self.slot_base = (s0, s1)
-        self.meta = slot_meta(self.max_sessions)            # slot header + offsets
-        self.region = region_cls(ctx, s1 + self.slot_size, handle)
-        self.handle = self.region.handle
+        self.fb_end, m0, m1, ctl_bytes = ctl_layout(self.max_sessions)
+        self.slot_meta_at = (m0, m1)
+        self.slot_room = -(-self.slot_bytes // SLOT_ALIGN) * SLOT_ALIGN
+        h_data, h_ctl = handle if handle is not None else (None, None)
+        self.ctl = HostRegion(None, ctl_bytes, h_ctl)
+        try:
+            self.data = region_cls(ctx, 2 * self.slot_room, h_data)
+        except Exception:
+            self.ctl.close()
+            raise
+        self.handle = (self.data.handle, self.ctl.handle)
         self.seq = 0                      # owner: last published; replica: last imported
         self.collected = 0                # owner: the feedback round it took last
         self.fb_round = 0                 # replica: its last feedback round
@@ -168,7 +191,7 @@ class Mailbox:
         self.wait_s = 0.0                 # time spent waiting for the peer
 
     def _hdr(self) -> dict:
-        h = self.region.read(0, HDR_BYTES)
+        h = self.ctl.read(0, HDR_BYTES)
         u64 = h[0:32].view(np.uint64)
         r64 = h[64:96].view(np.uint64)
         return {"collected": int(u64[3]), "ack": int(r64[0]),
@@ -186,32 +209,33 @@ class Mailbox:
                 raise TimeoutError(f"peer mailbox: {what} not seen in {self.timeout_s:.0f} s (peer rank gone?)")
             if delay:
                 time.sleep(delay)
-            delay = min(max(delay * 2, 20e-6), 1e-3)
+            delay = min(max(delay * 2, 5e-6), 1e-3)
 
     # ---- owner side ----
     def publish(self, export_fn, n: int) -> int:
         """export_fn(dst, cap) -> offsets[n + 1] writes n sessions' images at dst (a device
-        pointer; a host view in the rehearsal).  Returns the bytes published."""
+        pointer; a host view in the rehearsal), complete when it returns.  Returns the bytes
+        published."""
         if n > self.max_sessions:
             raise ValueError(f"mailbox holds {self.max_sessions} sessions, {n} published")
         if self.seq >= 2:
             want = self.seq - 1
             self._wait(lambda h: h["ack"] >= want, f"import of publication {want}")
         k = (self.seq + 1) & 1
-        base = self.slot_base[k]
-        offsets = np.asarray(export_fn(self.region.addr(base + self.meta), self.slot_size - self.meta), dtype=np.uint64)
+        offsets = np.asarray(export_fn(self.data.addr(k * self.slot_room), self.slot_room), dtype=np.uint64)
         if len(offsets) != n + 1:
             raise ValueError("export_fn must return n + 1 offsets")
         total = int(offsets[-1])
-        if total > self.slot_size - self.meta:
-            raise ValueError(f"publication of {total} bytes exceeds the mailbox slot ({self.slot_size - self.meta})")
-        self.region.write(base + 64, offsets)
+        if total > self.slot_room:
+            raise ValueError(f"publication of {total} bytes exceeds the mailbox slot ({self.slot_room})")
+        meta = self.slot_meta_at[k]
+        self.ctl.write(meta + 64, offsets)
         self.seq += 1
         hdr = np.zeros(24, np.uint8)
         hdr[0:8] = np.array([self.seq], np.uint64).view(np.uint8)
         hdr[8:16] = np.array([k, n], np.uint32).view(np.uint8)
         hdr[16:24] = np.array([total], np.uint64).view(np.uint8)
-        self.region.write(base, hdr)       # the slot's seq: its bytes and offsets are complete already
+        self.ctl.write(meta, hdr)          # the slot's seq: its images and offsets are complete already
         self.bytes_moved += total
         return total
 
@@ -224,21 +248,22 @@ class Mailbox:
             h = self._hdr()
         if h["fb_round"] <= self.collected:
             return []
-        ids = self.region.read(HDR_BYTES, 4 * h["nfb"]).view(np.uint32).tolist() if h["nfb"] else []
+        ids = self.ctl.read(HDR_BYTES, 4 * h["nfb"]).view(np.uint32).tolist() if h["nfb"] else []
         self.collected = h["fb_round"]
-        self.region.write(24, np.array([self.collected], np.uint64))
+        self.ctl.write(24, np.array([self.collected], np.uint64))
         return ids
 
     # ---- replica side ----
     def consume(self, import_fn, n: int) -> int:
         """Waits for the next publication, applies it (import_fn(src, offsets), src the mapped
-        slot's images) and acks it.  Returns the bytes imported."""
+        slot's images, complete when it returns) and acks it.  Returns the bytes imported."""
         want = self.seq + 1
-        base = self.slot_base[want & 1]
+        k = want & 1
+        meta = self.slot_meta_at[k]
         t0 = time.perf_counter()
         delay = 0.0
         while True:                                    # the slot's own header
-            sh = self.region.read(base, 64 + 8 * (n + 1))
+            sh = self.ctl.read(meta, 64 + 8 * (n + 1))
             seq = int(sh[0:8].view(np.uint64)[0])
             if seq >= want:
                 break
@@ -247,19 +272,19 @@ class Mailbox:
                                    f"(peer rank gone?)")
             if delay:
                 time.sleep(delay)
-            delay = min(max(delay * 2, 20e-6), 1e-3)
+            delay = min(max(delay * 2, 5e-6), 1e-3)
         self.wait_s += time.perf_counter() - t0
         if seq != want:
             raise RuntimeError(f"peer mailbox: slot holds publication {seq} while {want} was expected")
-        k, nn = sh[8:16].view(np.uint32)
+        kk, nn = sh[8:16].view(np.uint32)
         nbytes = int(sh[16:24].view(np.uint64)[0])
         if int(nn) != n:
             raise RuntimeError(f"peer mailbox: publication of {int(nn)} sessions, {n} replicated")
         offsets = sh[64:64 + 8 * (n + 1)].view(np.uint64)
         if nbytes:
-            import_fn(self.region.addr(base + self.meta), offsets)
+            import_fn(self.data.addr(k * self.slot_room), offsets)
         self.seq = want
-        self.region.write(64, np.array([self.seq], np.uint64))
+        self.ctl.write(64, np.array([self.seq], np.uint64))
         self.bytes_moved += nbytes
         return nbytes
 
@@ -273,12 +298,13 @@ class Mailbox:
             raise ValueError("more relocations than replicated sessions")
         self.fb_last = ids.tolist()
         if len(ids):
-            self.region.write(HDR_BYTES, ids)
+            self.ctl.write(HDR_BYTES, ids)
         self.fb_round += 1
         w = np.zeros(24, np.uint8)
         w[0:4] = np.array([len(ids)], np.uint32).view(np.uint8)
         w[8:24] = np.array([self.seq, self.fb_round], np.uint64).view(np.uint8)
-        self.region.write(72, w)           # nfb, fb_seq, fb_round: the ids are written already
+        self.ctl.write(72, w)              # nfb, fb_seq, fb_round: the ids are written already
 
     def close(self):
-        self.region.close()
+        self.data.close()
+        self.ctl.close()

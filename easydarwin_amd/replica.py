@@ -132,7 +132,8 @@ class MailboxReplicaLink(ReplicaLink):
     """ReplicaLink whose images and relocations travel through a peer mailbox in the owner's HBM
     (easydarwin_amd/mailbox.py), as DistReplicaLink's do between processes -- both ends in one
     process: the replica end reads the owner's buffer directly instead of through an IPC mapping
-    (a process cannot open an IPC handle of its own memory).  So every golden pins the mailbox
+    (a process cannot open an IPC handle of its own memory); the control words are the same
+    shared-memory region.  So every golden pins the mailbox
     protocol, the import straight from the mailbox slot and the lockstep relocation feedback on
     the GPU (tests/test_gpu_replica.py, mode "mailbox")."""
 
@@ -146,14 +147,15 @@ class MailboxReplicaLink(ReplicaLink):
     def _boxes(self, n: int, nbytes: int):
         from .mailbox import DeviceRegion, Mailbox, SameProcessRegion
         mb = self.out_mb
-        if mb is not None and n <= mb.max_sessions and nbytes <= mb.slot_size - mb.meta:
+        if mb is not None and n <= mb.max_sessions and nbytes <= mb.slot_room:
             return
         room = max(n, 2 * (mb.max_sessions if mb else 0), 8)
         slot = max(room * self.session_bytes, 2 * nbytes)
         if mb is not None:
             self._retired += [self.in_mb, mb]
         self.out_mb = Mailbox(DeviceRegion, self.owner, room, slot)
-        self.in_mb = Mailbox(SameProcessRegion, self.replica, room, slot, handle=self.out_mb.region.base)
+        self.in_mb = Mailbox(SameProcessRegion, self.replica, room, slot,
+                             handle=(self.out_mb.data.base, self.out_mb.ctl.handle))
 
     def sync(self, now_ms: int) -> int:
         if not self.pairs:
@@ -206,9 +208,9 @@ class DistReplicaLink:
     replica of it.
 
     Joins are the control plane, and the only collective: ``connect`` gathers every rank's
-    replicated sessions, each owner sizes one peer mailbox per replica rank in its own HBM
-    (``mailbox.Mailbox``: double-buffered image slots + header words) and hands its IPC handle
-    over, and the replica maps it (``edgpu_ipc_open``); ``places`` numbers the joiners in their
+    replicated sessions, each owner sizes one peer mailbox per replica rank (``mailbox.Mailbox``:
+    double-buffered image slots in its own HBM, the header words in POSIX shared memory) and hands
+    the IPC handle and the shared-memory name over, and the replica maps them (``edgpu_ipc_open``); ``places`` numbers the joiners in their
     owners' bucket arrays (``dist.route_places``).  The steady state has no collective: ``sync``
     exports each owned session's images (full the first time per replica rank, deltas after)
     straight into the mailboxes and imports this rank's replicas straight from the owners'
