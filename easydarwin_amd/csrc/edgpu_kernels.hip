@@ -30,6 +30,21 @@ namespace edgpu {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// k_ingest's slot-copy policy: bit 0 the copy's source loads non-temporal, bit 1 its ring stores
+// (so the copy's stream is the XCD L2's first victim and each packet's first line, read by the
+// header phase with the default policy, can still be there when the copy reads it again).
+#ifndef EDGPU_INGEST_NT
+#define EDGPU_INGEST_NT 0
+#endif
+__device__ __forceinline__ u32x4 ing_ld(const u32x4* p) {
+    if constexpr ((EDGPU_INGEST_NT & 1) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ void ing_st(u32x4* p, u32x4 v) {
+    if constexpr ((EDGPU_INGEST_NT & 2) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __device__ __forceinline__ uint32_t be16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
 __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
     return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
@@ -245,15 +260,15 @@ __device__ __forceinline__ void tcp_frame_store(const u32x4 (&b)[3], u32x4 b3, u
     u32x4 v0 = funnel_next<Q>(b[0], lane0(b[1]), r);
     if (lane == 0) v0.x = slot_header(fl - 4u);
     if (lastk == 0) v0 = keep16(v0, rem);
-    if ((uint32_t)lane < nw) ring[base & wm] = v0;
+    if ((uint32_t)lane < nw) ing_st(ring + (base & wm), v0);
     if (lastk >= 1) {
         u32x4 v1 = funnel_next<Q>(b[1], lane0(b[2]), r);
         if (lastk == 1) v1 = keep16(v1, rem - 1024);
-        if ((uint32_t)lane + 64 < nw) ring[(base + 64) & wm] = v1;
+        if ((uint32_t)lane + 64 < nw) ing_st(ring + ((base + 64) & wm), v1);
     }
     if (lastk >= 2) {
         const u32x4 v2 = keep16(funnel_next<Q>(b[2], b3, r), rem - 2048);
-        if ((uint32_t)lane + 128 < nw) ring[(base + 128) & wm] = v2;
+        if ((uint32_t)lane + 128 < nw) ing_st(ring + ((base + 128) & wm), v2);
     }
 }
 
@@ -288,9 +303,9 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
             const uint32_t nblk = sb[d] ? (uint32_t)((sp + fl[d] - 1 - a0) >> 4) + 1 : 0u;
             const u32x4* ab = reinterpret_cast<const u32x4*>(a0);
             const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-            b[d][0] = (uint32_t)lane < nblk ? ab[lane] : z;
-            b[d][1] = (uint32_t)lane + 64 < nblk ? ab[lane + 64] : z;
-            b[d][2] = (uint32_t)lane + 128 < nblk ? ab[lane + 128] : z;
+            b[d][0] = (uint32_t)lane < nblk ? ing_ld(ab + lane) : z;
+            b[d][1] = (uint32_t)lane + 64 < nblk ? ing_ld(ab + lane + 64) : z;
+            b[d][2] = (uint32_t)lane + 128 < nblk ? ing_ld(ab + lane + 128) : z;
             b3[d] = 192u < nblk ? *(cu32x4*)(ab + 192) : z;              // scalar
         }
 #pragma unroll
@@ -317,7 +332,15 @@ __device__ __forceinline__ void tcp_slot_copy_s(uint32_t n, const uint32_t* p_sl
 // THREADS: workgroup size, one packet per lane per round (256 by default; EDGPU_INGEST_THREADS=512
 // for A/B: one round for a C2 session's ~375 packets per tick)
 
-template <uint32_t DEPTH, int THREADS = kIngestThreads>
+// SPEC (descriptor batches in the blob): the slot copy runs FIRST, at each packet's speculative
+// ring place -- every packet that passes the track / length test is taken to be enqueued with its
+// full length -- and the header words the reflector reads (packet bytes 0..27) are taken from the
+// copy's own registers, so each packet's first line is fetched once and one dependent load per
+// round is gone.  What the header then decides changes no byte offset: a packet the RTCP-port or
+// SSRC test refuses keeps its bytes as a hole in the ring (nothing points into it), a stripped
+// receive-time trailer stays as slack at its slot's end and its slot header is rewritten.  Ranks and
+// non-empty counts are scanned again only in a round where a decision differed from the guess.
+template <uint32_t DEPTH, int THREADS = kIngestThreads, bool SPEC = false>
 // waves_per_eu(4): the kernel needs 4 waves per SIMD (4 resident 256-thread sessions per CU), and
 // the interleaved copy's four frames in flight fit 128 VGPRs that way
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_ingest(IngestParams P) {
@@ -350,6 +373,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ uint32_t p_slotb[THREADS];
     __shared__ uint64_t p_vb[THREADS];
     __shared__ int64_t p_arr[THREADS];      // receive-time trailer: the packet's arrival
+    __shared__ u32x4 p_hdr[SPEC ? THREADS : 1][2];   // SPEC: slot words 0 and 1, from the copy
     __shared__ uint64_t scan64[NW];
     // ReflectorSocket receive-time state per socket (reflector_use_in_packet_receive_time)
     __shared__ uint32_t s_rth[kMaxSendersPerSession], s_rts[kMaxSendersPerSession];
@@ -432,7 +456,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         uint64_t src = 0;
         int64_t arrival = 0;
         bool acc = false;
-        const uint8_t* pk = nullptr;
         uint32_t hdr[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};   // packet bytes 0..27, little-endian words
         bool direct = false;            // an interleaved frame found here
         if (valid && P.tcp_groups) {
@@ -492,7 +515,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 slot = 0;
                 acc = track < S.ntracks && len > 0;
                 src = (uint64_t)(uintptr_t)sp;
-                pk = sp + 4;
                 // as load16_unaligned(sp, lim) / (sp + 16, lim) with lim = sp + 4 + len: a block
                 // past lim is not read (the word keeps the previous block's bytes)
                 const uintptr_t lim = (uintptr_t)sp + 4 + len;
@@ -519,7 +541,104 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             const uint8_t* sp = P.src_addr ? reinterpret_cast<const uint8_t*>(P.src_addr[i])
                                            : P.blob + (uint64_t)slot * 16;
             src = (uint64_t)(uintptr_t)sp;
-            pk = sp + 4;
+            in_pk += 1;
+            in_bytes += len;
+        }
+        // ---- SPEC: the speculative ranks / ring places, the slot copy, then the header words ----
+        uint32_t my_rank = 0, my_nzpre = 0, my_trank = 0;
+        uint64_t my_slotpre = 0;
+        // every sender of the session in one pass: each wave scans (count | non-empty << 10 | slot
+        // bytes << 20) per sender in registers (wave_inclusive_scan_u64), the wave totals meet in
+        // LDS across one barrier.  A packet keeps the prefixes of its own sender and of its track's
+        // other one (RTP / RTCP, ls ^ 1): its rank in the track (fStreamCountID order) is their sum.
+        // (a packet refused after SPEC's guess, !a with sbytes > 0, still counts its hole's bytes)
+        auto rank_scan = [&](bool a, bool z, uint32_t sbytes) {
+            const int lane = tid & 63, wid = tid >> 6;
+            const uint64_t mx = (a ? 1ull | (uint64_t)(z ? 1 : 0) << 10 : 0ull) | (uint64_t)sbytes << 20;
+            const uint32_t ns = (EDGPU_ABL(P) & 64u) ? 0u : nsnd;
+            uint64_t my_incl = 0, sib_incl = 0;
+            for (uint32_t s = 0; s < ns; s++) {                      // uniform
+                const uint64_t incl = wave_inclusive_scan_u64((a || sbytes) && ls == s ? mx : 0ull);
+                if (lane == 63) s_wsum[s][wid] = incl;
+                if (ls == s) my_incl = incl;
+                if ((ls ^ 1u) == s) sib_incl = incl;
+            }
+            __syncthreads();
+            EDGPU_ING_T(3);
+            if (tid < (int)ns) {
+                uint64_t t = 0;
+                for (int w = 0; w < NW; w++) t += s_wsum[tid][w];
+                c_tot[tid] = t;
+            }
+            if ((a || sbytes) && ns) {                               // (then ls < nsnd)
+                uint64_t mb = 0, sb = 0;
+                for (int w = 0; w < wid; w++) { mb += s_wsum[ls][w]; sb += s_wsum[ls ^ 1u][w]; }
+                const uint64_t pre = mb + my_incl - mx;
+                my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20;
+                my_trank = my_rank + (uint32_t)((sb + sib_incl) & 1023);
+            }
+        };
+        const bool acc0 = acc;                 // SPEC's guess: enqueued, non-empty, full length
+        const uint32_t len_d = len;
+        const uint32_t slotb_s = SPEC && acc ? ((len + 4 + 15) & ~15u) : 0u;
+        if constexpr (SPEC) {
+            rank_scan(acc0, acc0, slotb_s);
+            p_snd[tid] = (uint8_t)ls;
+            p_len[tid] = (uint16_t)len;
+            p_src[tid] = src;
+            p_slotb[tid] = slotb_s;
+            p_vb[tid] = acc0 ? s_vbyte[ls] + my_slotpre : 0ull;
+            p_arr[tid] = arrival;                     // (kept in LDS across the copy)
+            __syncthreads();
+            // the copy (as copy_mode 0 below); lanes 0 and 1 keep slot words 0 and 1 for the header
+            constexpr uint32_t kDepth = DEPTH, kW = THREADS / 64;
+            const uint32_t lane = tid & 63, wid = tid >> 6;
+            for (uint32_t p = wid; p < n; p += kDepth * kW) {
+                uint32_t nw[kDepth];
+                u32x4 v[kDepth][3];
+#pragma unroll
+                for (uint32_t d = 0; d < kDepth; d++) {
+                    const uint32_t pd = p + d * kW;
+                    nw[d] = pd < n ? p_slotb[pd] / 16 : 0u;
+                    const u32x4* sp = reinterpret_cast<const u32x4*>(pd < n ? p_src[pd] : 0ull);
+#pragma unroll
+                    for (uint32_t k = 0; k < 3; k++) {
+                        v[d][k] = u32x4{0u, 0u, 0u, 0u};
+                        if (lane + 64 * k < nw[d]) v[d][k] = ing_ld(sp + lane + 64 * k);
+                    }
+                }
+#pragma unroll
+                for (uint32_t d = 0; d < kDepth; d++) {
+                    if (nw[d] == 0) continue;
+                    const uint32_t pd = p + d * kW;
+                    if (lane < 2) p_hdr[pd][lane] = v[d][0];
+                    u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[pd]]);
+                    const uint64_t w0 = p_vb[pd] >> 4;
+                    const uint32_t wm = s_wmask[p_snd[pd]];
+                    if (lane == 0) v[d][0].x = slot_header(p_len[pd]);
+#pragma unroll
+                    for (uint32_t k = 0; k < 3; k++)
+                        if (lane + 64 * k < nw[d]) ing_st(ring + ((w0 + lane + 64 * k) & wm), v[d][k]);
+                }
+            }
+            __syncthreads();
+            arrival = p_arr[tid];                     // (and these, rather than held across it)
+            src = p_src[tid];
+            len = p_len[tid];
+            track = ls >> 1;
+            if (acc0) {
+                const u32x4 w0 = p_hdr[tid][0];
+                const u32x4 w1 = len > 12 ? p_hdr[tid][1] : u32x4{0u, 0u, 0u, 0u};
+                hdr[0] = w0.y; hdr[1] = w0.z; hdr[2] = w0.w; hdr[3] = w1.x;
+                hdr[4] = w1.y; hdr[5] = w1.z; hdr[6] = w1.w;
+                fl = s_flags[ls];
+                // UDP push: socket B is the odd port, so only SRs survive (Q14)
+                if (fl & kSndRtcpPort)
+                    acc = len >= 8 && len >= 4 * hbe16(hdr, 2) + 4 && (hbyte(hdr, 0) >> 6) == 2 && hbyte(hdr, 1) == 200;
+            }
+        }
+        if (valid && !direct && !SPEC) {
+            const uint8_t* sp = reinterpret_cast<const uint8_t*>(src);
             // the slot's first 32 bytes (packet bytes 0..27) in two 16-B loads: every header
             // field the reflector reads for a CSRC-free packet comes from these registers
             u32x4 w0 = u32x4{0u, 0u, 0u, 0u}, w1 = w0;
@@ -538,8 +657,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             // UDP push: socket B is the odd port, so only SRs survive (Q14)
             if (acc && (fl & kSndRtcpPort))
                 acc = len >= 8 && len >= 4 * hbe16(hdr, 2) + 4 && (hbyte(hdr, 0) >> 6) == 2 && hbyte(hdr, 1) == 200;
-            in_pk += 1;
-            in_bytes += len;
         }
         p_snd[tid] = (uint8_t)ls;
         p_acc[tid] = acc;
@@ -584,7 +701,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (P.recv_time) {                                        // uniform
             bool tag = false;
             if (acc && len > 12) {
-                const uint8_t* t = pk + len - 12;
+                const uint8_t* t = reinterpret_cast<const uint8_t*>(src) + 4 + len - 12;
                 tag = t[0] == 'a' && t[1] == 'k' && t[2] == 't' && t[3] == 't';
                 if (tag) {
                     uint64_t rt = 0;
@@ -617,38 +734,35 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         const bool nz = acc && len > 0;
         const uint32_t slotb = nz ? ((len + 4 + 15) & ~15u) : 0;
-        // ---- per-sender queue index / slot offset / non-empty count ----
-        // Every sender of the session in one pass: each wave scans (count | non-empty << 10 | slot
-        // bytes << 20) per sender in registers (wave_inclusive_scan_u64), the wave totals meet in
-        // LDS across one barrier.  A packet keeps the prefixes of its own sender and of its track's
-        // other one (RTP / RTCP, ls ^ 1): its rank in the track (fStreamCountID order) is their sum.
-        uint32_t my_rank = 0, my_nzpre = 0, my_trank = 0;
-        uint64_t my_slotpre = 0;
-        {
-            const int lane = tid & 63, wid = tid >> 6;
-            const uint64_t mx = 1ull | (uint64_t)(nz ? 1 : 0) << 10 | (uint64_t)slotb << 20;
-            const uint32_t ns = (EDGPU_ABL(P) & 64u) ? 0u : nsnd;
-            uint64_t my_incl = 0, sib_incl = 0;
-            for (uint32_t s = 0; s < ns; s++) {                      // uniform
-                const uint64_t incl = wave_inclusive_scan_u64(acc && ls == s ? mx : 0ull);
-                if (lane == 63) s_wsum[s][wid] = incl;
-                if (ls == s) my_incl = incl;
-                if ((ls ^ 1u) == s) sib_incl = incl;
+        // ---- per-sender queue index / slot offset / non-empty count (rank_scan above).  SPEC:
+        // the slot bytes stay the guessed ones (a refused packet's bytes become a hole), and the
+        // ranks are scanned again only if a packet's enqueue / non-empty state differs from the guess
+        uint64_t vb_empty = 0;
+        if constexpr (SPEC) {
+            if (__syncthreads_or(acc != acc0 || nz != acc0 ? 1 : 0)) {
+                rank_scan(acc, nz, slotb_s);
+                // a packet the SSRC filter emptied takes the place of its sender's next non-empty
+                // packet (this round's, else the round's end): the holes before it belong to the
+                // non-empty packet before them, and a range starting at it starts where its first
+                // bytes do.  One lane per sender walks the round backwards (rounds with a refusal only)
+                p_slotb[tid] = nz ? 1u : 0u;
+                __syncthreads();
+                if (tid < (int)nsnd) {
+                    uint64_t nxt = s_vbyte[tid] + (c_tot[tid] >> 20);
+                    for (int p = (int)n - 1; p >= 0; p--) {
+                        if (p_snd[p] != tid) continue;
+                        if (p_slotb[p]) nxt = p_vb[p];
+                        else p_vb[p] = nxt;
+                    }
+                }
+                __syncthreads();
+                vb_empty = p_vb[tid];
             }
-            __syncthreads();
-            EDGPU_ING_T(3);
-            if (tid < (int)ns) {
-                uint64_t t = 0;
-                for (int w = 0; w < NW; w++) t += s_wsum[tid][w];
-                c_tot[tid] = t;
-            }
-            if (acc && ns) {                                         // (acc: ls < nsnd)
-                uint64_t mb = 0, sb = 0;
-                for (int w = 0; w < wid; w++) { mb += s_wsum[ls][w]; sb += s_wsum[ls ^ 1u][w]; }
-                const uint64_t pre = mb + my_incl - mx;
-                my_rank = pre & 1023; my_nzpre = (pre >> 10) & 1023; my_slotpre = pre >> 20;
-                my_trank = my_rank + (uint32_t)((sb + sib_incl) & 1023);
-            }
+            if (nz && len != len_d)                      // a stripped trailer: the slot header's length
+                reinterpret_cast<uint32_t*>(s_ring[ls])[(((s_vbyte[ls] + my_slotpre) >> 4) & s_wmask[ls]) * 4] =
+                    slot_header(len);
+        } else {
+            rank_scan(acc, nz, slotb);
         }
         if (nz) atomicMax(&c_last[ls], tid << 10 | (int)my_rank);
         uint64_t idx = 0, vb = 0;
@@ -656,6 +770,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (acc) {
             idx = s_head[ls] + my_rank;
             vb = s_vbyte[ls] + my_slotpre;
+            if (SPEC && !nz) vb = vb_empty;              // (SPEC: see the walk above)
             PktMeta m;
             m.vbyte = vb;
             m.id = s_count[track] + my_trank + 1;        // fStreamCountID = ++fPacketCount
@@ -669,7 +784,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             const bool by_port_rtp = !(fl & kSndRtcpPort);
             const bool key = by_port_rtp && (fl & kSndVideo) && (fl & kSndH264) && len0 >= 20 &&
                              ((hbyte(hdr, 0) & 0x0F) == 0 ? key_frame_first_packet_cc0(hdr, len0)
-                                                          : key_frame_first_packet(pk, len0));
+                                                          : key_frame_first_packet(reinterpret_cast<const uint8_t*>(src) + 4, len0));
             kev_key = key;
             kev_aud = by_port_rtp && (fl & kSndAudio);
         }
@@ -677,8 +792,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         const uint64_t kK = __ballot(kev_key), kE = kK | __ballot(kev_aud);
         if ((tid & 63) == 0)
             s_wev[tid >> 6] = kE ? 1u | (uint32_t)((kK >> (63 - __clzll((long long)kE))) & 1ull) << 1 : 0u;
-        p_slotb[tid] = slotb;
-        p_vb[tid] = vb;
+        if constexpr (!SPEC) {
+            p_slotb[tid] = slotb;
+            p_vb[tid] = vb;
+        }
         __syncthreads();
         EDGPU_ING_T(4);
         // ---- keyframe index, part 2: a video key packet moves its sender's key pointer; an audio
@@ -699,8 +816,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         // ---- slot copy: here, one wave per packet (copy_mode 0), or as a job for
         // k_ingest_copy's flat grid over packets (copy_mode 1) ----
-        if (EDGPU_ABL(P) & 32u) {
-            // timing ablation only: no slot copy
+        if (SPEC || (EDGPU_ABL(P) & 32u)) {
+            // SPEC: copied above; or a timing ablation: no slot copy
         } else if (EDGPU_COPY_MODE(P) == 0 && P.src_addr && EDGPU_TCP_COPY(P) >= 1) {   // frames inside the TCP byte stream
             if (EDGPU_TCP_COPY(P) == 3) tcp_slot_copy_s<kTcpFramesPerRound, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
             else if (EDGPU_TCP_COPY(P) >= 2) tcp_slot_copy<2, THREADS>(n, p_slotb, p_src, p_len, p_snd, p_vb, s_ring, s_wmask);
@@ -745,7 +862,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
                     for (uint32_t k = 0; k < 3; k++) {
                         v[d][k] = u32x4{0u, 0u, 0u, 0u};
-                        if (lane + 64 * k < nw[d]) v[d][k] = sp[lane + 64 * k];
+                        if (lane + 64 * k < nw[d]) v[d][k] = ing_ld(sp + lane + 64 * k);
                     }
                 }
 #pragma unroll
@@ -758,7 +875,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                     if (lane == 0) v[d][0].x = slot_header(p_len[pd]);
 #pragma unroll
                     for (uint32_t k = 0; k < 3; k++)
-                        if (lane + 64 * k < nw[d]) ring[(w0 + lane + 64 * k) & wm] = v[d][k];
+                        if (lane + 64 * k < nw[d]) ing_st(ring + ((w0 + lane + 64 * k) & wm), v[d][k]);
                 }
             }
         } else if (valid) {
@@ -2772,18 +2889,23 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
         EDGPU_LAUNCH(k_totals_reset, dim3(1), dim3(64), 0, st, p.totals, 1);
         return hipGetLastError();
     }
+    // descriptor batches in the blob take the speculative copy (k_ingest SPEC); frames inside a
+    // TCP byte stream find their lengths in their own first bytes and keep the header-first order
+    const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0;
 #ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
     static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();
     if (threads == 512) EDGPU_LAUNCH((k_ingest<4, 512>), dim3(nseg), dim3(512), 0, st, p);
     else if (depth == 2) EDGPU_LAUNCH(k_ingest<2>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    else if (spec && !getenv("EDGPU_INGEST_NOSPEC")) EDGPU_LAUNCH((k_ingest<4, kIngestThreads, true>), dim3(nseg), dim3(kIngestThreads), 0, st, p);
     else EDGPU_LAUNCH(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
     if (p.npk && EDGPU_COPY_MODE(p) == 1) {
         const uint32_t per = kCopyThreads / kCopyLanes;
         EDGPU_LAUNCH(k_ingest_copy, dim3((p.npk + per - 1) / per), dim3(kCopyThreads), 0, st, p);
     }
 #else
-    EDGPU_LAUNCH(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    if (spec) EDGPU_LAUNCH((k_ingest<4, kIngestThreads, true>), dim3(nseg), dim3(kIngestThreads), 0, st, p);
+    else EDGPU_LAUNCH(k_ingest<4>, dim3(nseg), dim3(kIngestThreads), 0, st, p);
 #endif
     return hipGetLastError();
 }
