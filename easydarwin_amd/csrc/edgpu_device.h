@@ -77,7 +77,9 @@ struct SenderDev {
     int64_t  new_start;             // fFirstPacketInQueueForNewOutput, -1 = NULL
     uint64_t tail;                  // oldest index still intact in both rings
     uint64_t umin;                  // min range start over this sender's sub-streams
-    uint32_t _pad_items[2];
+    uint64_t vclob;                 // bytes of the ring's virtual stream written so far (>= vbyte_end:
+                                    // k_ingest's speculative copy may reach past it); slots older than
+                                    // vclob - ring bytes are overwritten
     uint64_t fan_lo, fan_vlo;       // oldest packet index / vbyte the last fan-out reads
     // the last host batch (edgpu_fanout_sources): packets [batch_lo, head) came from the blob of
     // the ingest whose epoch is batch_epoch; their blob slots follow the meta ring (uint32 per

@@ -2407,7 +2407,7 @@ int edgpu_gop_copy(edgpu_ctx* x, uint32_t session, uint32_t track, uint8_t* dst,
     }
     HIP_CHECK(rb.run());
     const uint64_t vb0 = meta[0].vbyte, span = D.vbyte_end - vb0;
-    if (span > bcap) return fail(EDGPU_RING_OVERFLOW, "GOP no longer in the byte ring");
+    if (std::max(D.vbyte_end, D.vclob) - vb0 > bcap) return fail(EDGPU_RING_OVERFLOW, "GOP no longer in the byte ring");
     std::vector<uint8_t> bytes(span);
     const uint8_t* ring = reinterpret_cast<const uint8_t*>(D.ring);
     for (uint64_t i = 0; i < span;) {

@@ -358,6 +358,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ int64_t s_lastv[kMaxSendersPerSession], s_lastnz[kMaxSendersPerSession];
     __shared__ uint32_t s_flags[kMaxSendersPerSession], s_pkmask[kMaxSendersPerSession], s_wmask[kMaxSendersPerSession];
     __shared__ uint64_t s_meta[kMaxSendersPerSession], s_ring[kMaxSendersPerSession];
+    __shared__ uint64_t s_vclob[kMaxSendersPerSession];     // SPEC: the ring's write high-water mark
     __shared__ uint64_t s_count[kMaxTracks];
     __shared__ uint64_t c_tot[kMaxSendersPerSession];
     __shared__ uint64_t s_wsum[kMaxSendersPerSession][NW];    // per sender, each wave's total
@@ -414,6 +415,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         s_flags[tid] = D.flags; s_pkmask[tid] = D.pk_mask; s_wmask[tid] = D.word_mask;
         s_meta[tid] = D.meta; s_ring[tid] = D.ring;
         s_key[tid] = D.key;
+        s_vclob[tid] = D.vclob;
         s_klast[tid] = 0ull;
         if (P.recv_time) { s_rth[tid] = D.rt_has; s_rts[tid] = D.rt_ssrc; s_rta[tid] = D.rt_first_arrival; s_rtr[tid] = D.rt_first_receive; }
     }
@@ -578,19 +580,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 my_trank = my_rank + (uint32_t)((sb + sib_incl) & 1023);
             }
         };
-        const bool acc0 = acc;                 // SPEC's guess: enqueued, non-empty, full length
-        const uint32_t len_d = len;
-        const uint32_t slotb_s = SPEC && acc ? ((len + 4 + 15) & ~15u) : 0u;
-        if constexpr (SPEC) {
-            rank_scan(acc0, acc0, slotb_s);
-            p_snd[tid] = (uint8_t)ls;
-            p_len[tid] = (uint16_t)len;
-            p_src[tid] = src;
-            p_slotb[tid] = slotb_s;
-            p_vb[tid] = acc0 ? s_vbyte[ls] + my_slotpre : 0ull;
-            p_arr[tid] = arrival;                     // (kept in LDS across the copy)
-            __syncthreads();
-            // the copy (as copy_mode 0 below); lanes 0 and 1 keep slot words 0 and 1 for the header
+        // the slot copy of the round's packets with p_slotb > 0 from p_src to ring place p_vb (as
+        // copy_mode 0 below); with `capture`, lanes 0 and 1 leave slot words 0 and 1 for the header
+        auto slot_copy = [&](bool capture) {
             constexpr uint32_t kDepth = DEPTH, kW = THREADS / 64;
             const uint32_t lane = tid & 63, wid = tid >> 6;
             for (uint32_t p = wid; p < n; p += kDepth * kW) {
@@ -611,7 +603,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (uint32_t d = 0; d < kDepth; d++) {
                     if (nw[d] == 0) continue;
                     const uint32_t pd = p + d * kW;
-                    if (lane < 2) p_hdr[pd][lane] = v[d][0];
+                    if (capture && lane < 2) p_hdr[pd][lane] = v[d][0];
                     u32x4* ring = reinterpret_cast<u32x4*>(s_ring[p_snd[pd]]);
                     const uint64_t w0 = p_vb[pd] >> 4;
                     const uint32_t wm = s_wmask[p_snd[pd]];
@@ -621,6 +613,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                         if (lane + 64 * k < nw[d]) ing_st(ring + ((w0 + lane + 64 * k) & wm), v[d][k]);
                 }
             }
+        };
+        const bool acc0 = acc;                 // SPEC's guess: enqueued, non-empty, full length
+        const uint32_t len_d = len;
+        const uint32_t slotb_s = SPEC && acc ? ((len + 4 + 15) & ~15u) : 0u;
+        if constexpr (SPEC) {
+            rank_scan(acc0, acc0, slotb_s);
+            p_snd[tid] = (uint8_t)ls;
+            p_len[tid] = (uint16_t)len;
+            p_src[tid] = src;
+            p_slotb[tid] = slotb_s;
+            p_vb[tid] = acc0 ? s_vbyte[ls] + my_slotpre : 0ull;
+            p_arr[tid] = arrival;                     // (kept in LDS across the copy)
+            __syncthreads();
+            slot_copy(true);
             __syncthreads();
             arrival = p_arr[tid];                     // (and these, rather than held across it)
             src = p_src[tid];
@@ -737,28 +743,24 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         // ---- per-sender queue index / slot offset / non-empty count (rank_scan above).  SPEC:
         // the slot bytes stay the guessed ones (a refused packet's bytes become a hole), and the
         // ranks are scanned again only if a packet's enqueue / non-empty state differs from the guess
-        uint64_t vb_empty = 0;
+        bool recopied = false;
         if constexpr (SPEC) {
             if (__syncthreads_or(acc != acc0 || nz != acc0 ? 1 : 0)) {
-                rank_scan(acc, nz, slotb_s);
-                // a packet the SSRC filter emptied takes the place of its sender's next non-empty
-                // packet (this round's, else the round's end): the holes before it belong to the
-                // non-empty packet before them, and a range starting at it starts where its first
-                // bytes do.  One lane per sender walks the round backwards (rounds with a refusal only)
-                p_slotb[tid] = nz ? 1u : 0u;
+                // a refusal: the round is laid out again without the refused packets' bytes and its
+                // enqueued packets copied again to their final places (from the batch, so the two
+                // copies never read each other).  The guessed layout's end stays as the sender's
+                // write high-water mark (vclob): ring slots it reached are no longer intact.
+                if (tid < (int)nsnd) s_vclob[tid] = max(s_vclob[tid], s_vbyte[tid] + (c_tot[tid] >> 20));
+                const uint32_t fb = nz ? slotb_s : 0u;
+                rank_scan(acc, nz, fb);
+                p_slotb[tid] = fb;
+                p_vb[tid] = nz ? s_vbyte[ls] + my_slotpre : 0ull;
+                p_len[tid] = (uint16_t)len;
                 __syncthreads();
-                if (tid < (int)nsnd) {
-                    uint64_t nxt = s_vbyte[tid] + (c_tot[tid] >> 20);
-                    for (int p = (int)n - 1; p >= 0; p--) {
-                        if (p_snd[p] != tid) continue;
-                        if (p_slotb[p]) nxt = p_vb[p];
-                        else p_vb[p] = nxt;
-                    }
-                }
-                __syncthreads();
-                vb_empty = p_vb[tid];
+                slot_copy(false);
+                recopied = true;
             }
-            if (nz && len != len_d)                      // a stripped trailer: the slot header's length
+            if (!recopied && nz && len != len_d)         // a stripped trailer: the slot header's length
                 reinterpret_cast<uint32_t*>(s_ring[ls])[(((s_vbyte[ls] + my_slotpre) >> 4) & s_wmask[ls]) * 4] =
                     slot_header(len);
         } else {
@@ -770,7 +772,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (acc) {
             idx = s_head[ls] + my_rank;
             vb = s_vbyte[ls] + my_slotpre;
-            if (SPEC && !nz) vb = vb_empty;              // (SPEC: see the walk above)
             PktMeta m;
             m.vbyte = vb;
             m.id = s_count[track] + my_trank + 1;        // fStreamCountID = ++fPacketCount
@@ -907,6 +908,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         SenderDev& D = P.senders[S.first_sender + tid];
         if (P.host_epoch) { D.batch_lo = D.head; D.batch_epoch = P.host_epoch; }   // (the head before the batch)
         D.head = s_head[tid]; D.vbyte_end = s_vbyte[tid]; D.vcount_end = s_vcount[tid];
+        D.vclob = s_vclob[tid];
         D.key = s_klast[tid] ? (int64_t)(s_klast[tid] & kQiMask) : s_key[tid];
         D.valid_ssrc = s_valid[tid]; D.last_valid_s = s_lastv[tid]; D.last_nonzero = s_lastnz[tid];
         if (P.recv_time) {
@@ -915,7 +917,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         // a copy pass the last tick still owes (edgpu_fanout_next): this batch must not lap what
         // that tick's remaining passes read
-        if (pass_owed && (s_vbyte[tid] > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
+        if (pass_owed && (max(s_vbyte[tid], s_vclob[tid]) > D.fan_vlo + ((uint64_t)s_wmask[tid] + 1) * 16 ||
                       s_head[tid] > D.fan_lo + (uint64_t)s_pkmask[tid] + 1))
             atomicCAS(&P.totals->ingest_status, 0, EDGPU_RING_OVERFLOW);
     }
@@ -1087,10 +1089,11 @@ __global__ __launch_bounds__(256) void k_plan_senders(PlanParams P) {
     const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16;
     uint64_t lo = head > pk_cap ? head - pk_cap : 0;
     lo = max(lo, D.floor);                                    // a replica holds nothing older
-    const uint64_t vend = D.vbyte_end;
-    // oldest packet whose slot is still intact in the byte ring
+    const uint64_t vend = D.vbyte_end, vhigh = max(vend, D.vclob);
+    // oldest packet whose slot is still intact in the byte ring (no write since reached it: the
+    // ingest's speculative copy may have written past vbyte_end, up to vclob)
     const uint64_t tail = wave_lower_bound_meta(meta, D.pk_mask, lo, head,
-                                                [&](const PktMeta& m) { return vend - m.vbyte <= byte_cap; });
+                                                [&](const PktMeta& m) { return vhigh - m.vbyte <= byte_cap; });
     int64_t ns = -1;
     if (D.key >= 0) {
         ns = D.key;
@@ -2515,7 +2518,7 @@ void k_fanout5(FanoutParams P) {
 __device__ uint64_t sender_tail(const SenderDev& D) {
     const PktMeta* meta = reinterpret_cast<const PktMeta*>(D.meta);
     const uint64_t head = D.head, pk_cap = (uint64_t)D.pk_mask + 1;
-    const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16, vend = D.vbyte_end;
+    const uint64_t byte_cap = ((uint64_t)D.word_mask + 1) * 16, vend = max(D.vbyte_end, D.vclob);
     uint64_t lo = head > pk_cap ? head - pk_cap : 0;
     lo = max(lo, D.floor);
     return lower_bound_meta(meta, D.pk_mask, lo, head,

@@ -1013,3 +1013,62 @@ def _random_prefs(rng, stream: bool) -> dict:
     keys = sorted(choices)
     pick = [k for k in keys if rng.random() < 0.4]
     return {k: choices[k]() for k in pick}
+
+
+def spec_stress(tick_ms: int = 1000) -> Trace:
+    """Refusals inside large ingest rounds, for k_ingest's speculative copy: the copy
+    runs at each packet's guessed ring place before the header decides, so every refusal leaves
+    a hole.  Not a golden: the oracle is pinned to the compiled reference on it (CPU test).
+
+    * session 0, an 8 Mb/s H.264 push (~700 packets per 1-s tick, several 256-packet rounds):
+      from 1.5 s a second pusher SSRC interleaves runs of 1 to 300 packets (zero-length after
+      the SSRC filter, runs crossing round and tick boundaries), players joining inside runs;
+    * session 1, a UDP push whose odd port also carries bursts of receiver reports and truncated
+      SRs (refused by the SR gate, Q14: holes with no queue entry) between its SRs;
+    * session 2, an audio-only push with the receive-time trailer on its odd packets.
+    UDP and TCP players join throughout."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 170))
+    dur = 6_000
+    v = [TrackSpec("video", "H264/90000", 96, bitrate=8_000_000, gop=30, idr_bytes=60_000, ssrc=0x5BEC0001),
+         TrackSpec("audio", "MPEG4-GENERIC/48000/2", 97, ssrc=0x5BEC0002)]
+    u = [TrackSpec("video", "H264/90000", 96, bitrate=2_000_000, gop=30, idr_bytes=20_000, rtcp_every_ms=300)]
+    a = [TrackSpec("audio", "PCMA/8000", 8, ssrc=0x5BEC0A0A)]
+    tr = Trace()
+    tr.prefs = {"reflector_use_in_packet_receive_time": "true"}
+    tr.add_session(make_sdp(v))
+    tr.add_session(make_sdp(u), udp_push=True)
+    tr.add_session(make_sdp(a))
+    pk0 = []
+    seq_b = 0
+    for t, ch, data in session_packets(v, dur, SEED_BASE + 171):
+        pk0.append((t, ch, data))
+        if ch == 0 and t >= 1500 and rng.random() < 0.01:       # a run of the foreign SSRC
+            for _ in range(int(rng.integers(1, 301))):
+                seq_b += 1
+                nal = 0x65 if rng.random() < 0.05 else 0x41
+                pay = bytes([nal]) + rng.integers(0, 256, size=int(rng.integers(20, 1400)), dtype=np.uint8).tobytes()
+                pk0.append((t, 0, rtp_header(seq_b, t * 90, 0x0BADBEEF, 96, False) + pay))
+    src = _ip(10, 0, 7, 7)
+    pk1 = []
+    for t, ch, data in session_packets(u, dur, SEED_BASE + 172):
+        pk1.append((t, ch, data, src, 6000 + (ch & 1)))
+        if ch == 0 and rng.random() < 0.03:                       # refused on the odd port
+            for _ in range(int(rng.integers(1, 40))):
+                if rng.random() < 0.5:
+                    rr = struct.pack(">BBHI", 0x81, 201, 7, 0x1234) + bytes(24)
+                else:
+                    rr = rtcp_sr(0x5BEC00FF, t, 0, 1, 1)[:int(rng.integers(8, 24))]
+                pk1.append((t, 1, rr, src, 6001))
+    pk2 = []
+    for k, (t, ch, data) in enumerate(session_packets(a, dur, SEED_BASE + 173)):
+        if k % 2:
+            data = data + b"aktt" + struct.pack(">Q", 7_000_000_000 + t + int(rng.integers(0, 30)))
+        pk2.append((t, ch, data))
+    joins, sub = [], 1
+    for t in sorted(int(x) for x in rng.integers(0, dur - 300, size=14)):
+        joins.append((t, int(rng.integers(0, 3)), sub, TCP if rng.random() < 0.4 else UDP))
+        sub += 1
+    for s in range(3):
+        joins.append((0, s, sub, UDP))
+        sub += 1
+    return _assemble(tr, [pk0, pk1, pk2], tick_ms, dur, joins)
