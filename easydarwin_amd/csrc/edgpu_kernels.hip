@@ -443,7 +443,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     __syncthreads();
     EDGPU_ING_T(1);
 
-    uint64_t in_pk = 0, in_bytes = 0;
+    uint32_t in_pk = 0, in_bytes = 0;          // (a segment: < 2^21 packets, < 2^32 bytes)
     // ReflectorSession::fHasVideoKeyFrameUpdate before the chunk (every thread keeps the same)
     bool kflag = S.video_key_flag != 0;
     constexpr unsigned long long kQiMask = (1ull << 52) - 1;
@@ -759,6 +759,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                 __syncthreads();
                 slot_copy(false);
                 recopied = true;
+                // (the header words and the arrival from LDS again, rather than held across the copy)
+                const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
+                const u32x4 w0 = acc0 ? p_hdr[tid][0] : z4, w1 = acc0 && len_d > 12 ? p_hdr[tid][1] : z4;
+                hdr[0] = w0.y; hdr[1] = w0.z; hdr[2] = w0.w; hdr[3] = w1.x;
+                hdr[4] = w1.y; hdr[5] = w1.z; hdr[6] = w1.w;
+                arrival = p_arr[tid];
             }
             if (!recopied && nz && len != len_d)         // a stripped trailer: the slot header's length
                 reinterpret_cast<uint32_t*>(s_ring[ls])[(((s_vbyte[ls] + my_slotpre) >> 4) & s_wmask[ls]) * 4] =
@@ -925,7 +931,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (tid == 0) P.sessions[P.seg_sess[seg]].video_key_flag = kflag ? 1u : 0u;
     // block totals: packets (< 2^21) and bytes (< 2^32) of the segment packed in one word, one
     // DPP scan per wave and one barrier
-    const uint64_t wt = wave_inclusive_scan_u64(in_bytes << 21 | in_pk);
+    const uint64_t wt = wave_inclusive_scan_u64((uint64_t)in_bytes << 21 | in_pk);
     if ((tid & 63) == 63) scan64[tid >> 6] = wt;
     __syncthreads();
     uint64_t t1 = 0, t2 = 0;
@@ -2894,7 +2900,10 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     }
     // descriptor batches in the blob take the speculative copy (k_ingest SPEC); frames inside a
     // TCP byte stream find their lengths in their own first bytes and keep the header-first order
-    const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0;
+#ifndef EDGPU_SPEC_MIN
+#define EDGPU_SPEC_MIN 0      // (measurement builds: the speculative copy only from this many packets per segment)
+#endif
+    const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0 && p.npk >= (uint64_t)EDGPU_SPEC_MIN * nseg;
 #ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
     static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();
