@@ -2901,7 +2901,8 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     // descriptor batches in the blob take the speculative copy (k_ingest SPEC); frames inside a
     // TCP byte stream find their lengths in their own first bytes and keep the header-first order
 #ifndef EDGPU_SPEC_MIN
-#define EDGPU_SPEC_MIN 0      // (measurement builds: the speculative copy only from this many packets per segment)
+#define EDGPU_SPEC_MIN 128    // the speculative copy from this many packets per segment on (a 1-s C2 tick: ~375; at
+                              // 100-ms ticks, one round per session, the header-first order is 0.8 % faster per step)
 #endif
     const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0 && p.npk >= (uint64_t)EDGPU_SPEC_MIN * nseg;
 #ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
