@@ -545,6 +545,8 @@ static void fill_defaults(edgpu_config& c) {
                                               c.reflector_use_in_packet_receive_time != EDGPU_FALSE) ? 1u : 0u;
     if (!c.reflector_in_packet_max_receive_sec) c.reflector_in_packet_max_receive_sec = 60;
     else if (c.reflector_in_packet_max_receive_sec == EDGPU_FALSE) c.reflector_in_packet_max_receive_sec = 0;
+    if (!c.ingest_spec_min) c.ingest_spec_min = 128;
+    else if (c.ingest_spec_min == EDGPU_FALSE) c.ingest_spec_min = 0;   // never
     if (!c.watchdog_ms) c.watchdog_ms = 10000;
     else if (c.watchdog_ms == EDGPU_FALSE) c.watchdog_ms = 0;   // unbounded waits
 }
@@ -1604,7 +1606,7 @@ static int enqueue_ingest(edgpu_ctx* x, const edgpu_pkt_desc* dd, uint32_t n, co
     p.desc = dd; p.seg_off = ds; p.seg_sess = dss; p.blob = db;
     p.src_addr = tcp ? tcp->src_addr : nullptr;
     p.sessions = x->d_sessions.ptr; p.senders = x->d_senders.ptr; p.streams = x->d_streams.ptr;
-    p.jobs = x->d_jobs; p.npk = n; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
+    p.jobs = x->d_jobs; p.npk = n; p.spec_min = x->cfg.ingest_spec_min; p.ablate = x->ablate; p.copy_mode = copy_mode; p.tcp_copy = x->tcp_copy;
     p.totals = x->d_totals;
     x->ing_slot ^= 1u;
     p.ing_slot = x->ing_slot;

@@ -2900,11 +2900,7 @@ hipError_t launch_ingest(const IngestParams& p, uint32_t nseg, hipStream_t st) {
     }
     // descriptor batches in the blob take the speculative copy (k_ingest SPEC); frames inside a
     // TCP byte stream find their lengths in their own first bytes and keep the header-first order
-#ifndef EDGPU_SPEC_MIN
-#define EDGPU_SPEC_MIN 128    // the speculative copy from this many packets per segment on (a 1-s C2 tick: ~375; at
-                              // 100-ms ticks, one round per session, the header-first order is 0.8 % faster per step)
-#endif
-    const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0 && p.npk >= (uint64_t)EDGPU_SPEC_MIN * nseg;
+    const bool spec = !p.tcp_groups && !p.src_addr && EDGPU_COPY_MODE(p) == 0 && p.spec_min && p.npk >= (uint64_t)p.spec_min * nseg;
 #ifdef EDGPU_AB_VARIANTS   // measurement builds: the ingest shapes of Appendix A.2
     static const int depth = [] { const char* v = getenv("EDGPU_INGEST_DEPTH"); return v ? atoi(v) : 4; }();
     static const int threads = [] { const char* v = getenv("EDGPU_INGEST_THREADS"); return v && atoi(v) == 512 ? 512 : 256; }();

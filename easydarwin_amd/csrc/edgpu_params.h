@@ -54,6 +54,7 @@ struct IngestParams {
     StreamDev* streams;
     CopyJob* jobs;          // per desc: slot copy for k_ingest_copy
     uint32_t npk;           // descriptors in the batch
+    uint32_t spec_min;      // the speculative copy from this many packets per segment on (0: never)
     uint32_t copy_mode;     // 0: copy inside k_ingest, 1: k_ingest_copy (EDGPU_INGEST)
     uint32_t tcp_copy;      // frames in the TCP byte stream: 1 one aligned load per word + the
                             // neighbour word by DPP, 2 the same with two frames per wave round

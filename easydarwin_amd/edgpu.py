@@ -74,6 +74,7 @@ class Config(C.Structure):
         ("reflector_use_in_packet_receive_time", C.c_uint32),
         ("reflector_in_packet_max_receive_sec", C.c_uint32),
         ("watchdog_ms", C.c_uint32),
+        ("ingest_spec_min", C.c_uint32),
     ]
 
 

@@ -134,6 +134,11 @@ typedef struct edgpu_config {
      * it timed out on has finished; then the context is usable again (the results of that work were
      * never read: the host re-runs or drops the tick).  edgpu_ctx_destroy waits without a bound. */
     uint32_t watchdog_ms;
+    /* k_ingest's speculative copy (no reference counterpart; output bytes are the same either
+     * way): a descriptor batch whose segments average at least this many packets is copied first
+     * and its header words read from the copy (default 128, a 1-s C2 tick; 1: always; EDGPU_FALSE:
+     * never, the header-first order).  DESIGN.md §3. */
+    uint32_t ingest_spec_min;
 } edgpu_config;
 #define EDGPU_FALSE 0xFFFFFFFFu   /* a flag off / a value of 0 where 0 would select the default */
 

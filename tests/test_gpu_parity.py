@@ -54,3 +54,13 @@ def test_pinned_host_ingest_matches_reference(name):
     ingested asynchronously (EDGPU_PTR_PINNED: copy stream + event) give the reference bytes."""
     cap, _ = replay(_trace(name), pinned=True)
     assert hashlib.sha256(cap).hexdigest() == _fixture(name)["capture_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SCENARIOS))
+def test_speculative_ingest_matches_reference(name):
+    """Every golden with k_ingest's speculative copy forced on every descriptor batch
+    (edgpu_config.ingest_spec_min = 1; by default only 1-s-sized batches take it):
+    refused, emptied and trailer-stripped packets change no output byte."""
+    cap, _ = replay(_trace(name), ingest_spec_min=1)
+    assert hashlib.sha256(cap).hexdigest() == _fixture(name)["capture_sha256"]

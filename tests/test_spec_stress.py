@@ -42,12 +42,18 @@ def test_engine_matches_oracle_on_spec_stress(tick, oracle_bins, tmp_path):
     tr = spec_stress(tick)
     tb = tr.to_bytes()
     want = _run(oracle_bins["port"], tb, tmp_path, "port")
-    cap, _ = replay(tr)
-    same = cap == want                   # (a bool: pytest would diff megabytes of bytes)
-    assert same, "C ABI replay (speculative copy)"
+    for spec_min in (1, 0xFFFFFFFF):     # the speculative copy on every batch / never
+        cap, _ = replay(tr, ingest_spec_min=spec_min)
+        same = cap == want               # (a bool: pytest would diff megabytes of bytes)
+        assert same, f"C ABI replay (ingest_spec_min {spec_min:#x})"
     assert all(len(ev[4]) <= 2043 for ev in tr.events if ev[0] == PKT)
     cap, _ = replay(tr, interleaved=1)
     same = cap == want
     assert same, "interleaved push (header-first copy)"
-    same = _run(ADAPTER, tb, tmp_path, "adapter") == want
-    assert same, "C++ adapter"
+    for spec_min in ("1", "0xFFFFFFFF"):
+        t, c = tmp_path / "a.edtr", tmp_path / "a.edcp"
+        t.write_bytes(tb)
+        subprocess.run([ADAPTER, str(t), str(c)], check=True, stderr=subprocess.DEVNULL, timeout=300,
+                       env=dict(os.environ, EDGPU_INGEST_SPEC_MIN=spec_min))
+        same = c.read_bytes() == want
+        assert same, f"C++ adapter (ingest_spec_min {spec_min})"

@@ -99,6 +99,7 @@ int main(int argc, char** argv) {
     cfg.reflector_in_packet_max_receive_sec = prefs.u32("reflector_in_packet_max_receive_sec") ? prefs.u32("reflector_in_packet_max_receive_sec")
                                                                                                : EDGPU_FALSE;
     if (const char* v = getenv("EDGPU_ARENA_BYTES")) cfg.out_arena_bytes = strtoull(v, nullptr, 0);
+    if (const char* v = getenv("EDGPU_INGEST_SPEC_MIN")) cfg.ingest_spec_min = (uint32_t)strtoul(v, nullptr, 0);
     if (const char* v = getenv("EDGPU_MAX_OUT_PACKETS")) cfg.max_out_packets = (uint32_t)strtoul(v, nullptr, 0);
     Reflector R(&cfg);
     uint64_t ticks = 0, passes = 0, stream_errors = 0;
